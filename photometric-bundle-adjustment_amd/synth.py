@@ -1,0 +1,337 @@
+"""Synthetic photometric / geometric BA problems (SURVEY.md §8d generator).
+
+The reference has no synthetic generator of its own (its inputs come from the OpenCV frontend,
+src/sfm.cpp:1117-1167, which cannot run here).  This module builds problems with the reference's data
+model restated as SoA arrays:
+
+* keyframes  ``T_w_k`` as Sophus ``[qx qy qz qw tx ty tz]`` (common_types.h:174-179, se3.hpp:70)
+* points     anchored in a host keyframe with inverse *distance* ρ along the unit bearing of
+             ``u_ref`` (common_types.h:188-217, reprojection.h:105-108)
+* blocks     one per (point, later observing keyframe), the anchor itself excluded
+             (map_utils.h:347-375)
+
+Trajectory ``T_w_k = (exp([0, 0.002k, 0]), [0.05k, 0, 0])``; every point is observed by the K keyframes
+after its host, so ``n_blocks = K·n_points``.
+
+Two image sources:
+* ``texture="render"`` ray-casts every keyframe onto a textured plane, so the photometric residual of the
+  unperturbed state is ~0 (for solver / convergence tests);
+* ``texture="noise"`` gives each keyframe an independent smooth random texture (for throughput, where
+  image content is irrelevant).  ``bench.py`` builds those on the GPU with torch.
+"""
+from __future__ import annotations
+
+import dataclasses
+import math
+from typing import Optional
+
+import numpy as np
+
+PHOTOMETRIC, GEOMETRIC = 0, 1
+PINHOLE, DOUBLE_SPHERE, EUCM = 0, 1, 2
+MODEL_IDS = {"pinhole": PINHOLE, "ds": DOUBLE_SPHERE, "eucm": EUCM}
+KIND_IDS = {"photometric": PHOTOMETRIC, "geometric": GEOMETRIC}
+
+# EuRoC-like 752×480 intrinsics per model, vector layout of camera_models.h ([fx fy cx cy p1 p2 0 0]).
+DEFAULT_INTRINSICS = {
+    PINHOLE: [458.654, 457.296, 367.215, 248.375, 0, 0, 0, 0],
+    DOUBLE_SPHERE: [349.7, 349.9, 365.9, 249.0, -0.28, 0.57, 0, 0],
+    EUCM: [460.0, 459.0, 365.5, 249.5, 0.59, 1.1, 0, 0],
+}
+
+# DSO-style 8-pixel residual pattern (du, dv) — SURVEY.md §8d.
+PATTERN8 = np.array([(0, -2), (-1, -1), (1, -1), (-2, 0), (0, 0), (2, 0), (-1, 1), (0, 2)], np.float32)
+
+
+@dataclasses.dataclass
+class Problem:
+    kind: int
+    model: int
+    width: int
+    height: int
+    intrinsics: np.ndarray          # (n_cams, 8) float64
+    frame_cam: np.ndarray           # (n_frames,) int32
+    images: Optional[np.ndarray]    # (n_frames, H, W) uint8, photometric only
+    pattern: np.ndarray             # (P, 2) float32
+    point_host: np.ndarray          # (n_points,) int32
+    u_ref: np.ndarray               # (n_points, 2) float64
+    host_intensity: Optional[np.ndarray]  # (n_points, P) float32
+    block_point: np.ndarray         # (n_blocks,) int32
+    block_target: np.ndarray        # (n_blocks,) int32
+    u_obs: Optional[np.ndarray]     # (n_blocks, 2) float64, geometric only
+    poses: np.ndarray               # (n_frames, 7) float64 — current state
+    rho: np.ndarray                 # (n_points,) float64 — current state
+    poses_gt: Optional[np.ndarray] = None
+    rho_gt: Optional[np.ndarray] = None
+
+    @property
+    def n_frames(self) -> int:
+        return int(self.frame_cam.shape[0])
+
+    @property
+    def n_points(self) -> int:
+        return int(self.point_host.shape[0])
+
+    @property
+    def n_blocks(self) -> int:
+        return int(self.block_point.shape[0])
+
+    @property
+    def P(self) -> int:
+        return int(self.pattern.shape[0]) if self.kind == PHOTOMETRIC else 2
+
+    @property
+    def R(self) -> int:
+        """Residuals per block."""
+        return self.P if self.kind == PHOTOMETRIC else 2
+
+    @property
+    def record(self) -> int:
+        """Floats per block record [r | J_host | J_target | J_rho]."""
+        return 14 * self.R
+
+
+# ------------------------------------------------------------------------------------------------
+# SE3 / camera helpers (numpy, vectorised, double).  Same conventions as Sophus.
+# ------------------------------------------------------------------------------------------------
+def quat_to_rot(q: np.ndarray) -> np.ndarray:
+    x, y, z, w = q[..., 0], q[..., 1], q[..., 2], q[..., 3]
+    R = np.empty(q.shape[:-1] + (3, 3))
+    R[..., 0, 0] = 1 - 2 * (y * y + z * z)
+    R[..., 0, 1] = 2 * (x * y - w * z)
+    R[..., 0, 2] = 2 * (x * z + w * y)
+    R[..., 1, 0] = 2 * (x * y + w * z)
+    R[..., 1, 1] = 1 - 2 * (x * x + z * z)
+    R[..., 1, 2] = 2 * (y * z - w * x)
+    R[..., 2, 0] = 2 * (x * z - w * y)
+    R[..., 2, 1] = 2 * (y * z + w * x)
+    R[..., 2, 2] = 1 - 2 * (x * x + y * y)
+    return R
+
+
+def quat_mul(a: np.ndarray, b: np.ndarray) -> np.ndarray:
+    ax, ay, az, aw = np.moveaxis(a, -1, 0)
+    bx, by, bz, bw = np.moveaxis(b, -1, 0)
+    return np.stack([aw * bx + ax * bw + ay * bz - az * by,
+                     aw * by + ay * bw + az * bx - ax * bz,
+                     aw * bz + az * bw + ax * by - ay * bx,
+                     aw * bw - ax * bx - ay * by - az * bz], -1)
+
+
+def so3_exp(w: np.ndarray) -> np.ndarray:
+    th = np.linalg.norm(w, axis=-1, keepdims=True)
+    small = th < 1e-10
+    th_s = np.where(small, 1.0, th)
+    imag = np.where(small, 0.5 - th * th / 48.0, np.sin(0.5 * th_s) / th_s)
+    real = np.where(small, 1.0 - th * th / 8.0, np.cos(0.5 * th_s))
+    return np.concatenate([imag * w, real], -1)
+
+
+def se3_exp(d: np.ndarray) -> np.ndarray:
+    """Sophus SE3::exp for tangent [υ, ω] (se3.hpp:763-784), vectorised."""
+    d = np.asarray(d, np.float64)
+    v, w = d[..., :3], d[..., 3:]
+    q = so3_exp(w)
+    th = np.linalg.norm(w, axis=-1)[..., None, None]
+    Om = np.zeros(d.shape[:-1] + (3, 3))
+    Om[..., 0, 1], Om[..., 0, 2], Om[..., 1, 2] = -w[..., 2], w[..., 1], -w[..., 0]
+    Om[..., 1, 0], Om[..., 2, 0], Om[..., 2, 1] = w[..., 2], -w[..., 1], w[..., 0]
+    Om2 = Om @ Om
+    ths = np.where(th < 1e-10, 1.0, th)
+    a = np.where(th < 1e-10, 0.5, (1 - np.cos(ths)) / ths ** 2)
+    b = np.where(th < 1e-10, 1.0 / 6.0, (ths - np.sin(ths)) / ths ** 3)
+    V = np.eye(3) + a * Om + b * Om2
+    t = (V @ v[..., None])[..., 0]
+    return np.concatenate([q, t], -1)
+
+
+def se3_mul(a: np.ndarray, b: np.ndarray) -> np.ndarray:
+    q = quat_mul(a[..., :4], b[..., :4])
+    q = q / np.linalg.norm(q, axis=-1, keepdims=True)
+    t = a[..., 4:] + (quat_to_rot(a[..., :4]) @ b[..., 4:, None])[..., 0]
+    return np.concatenate([q, t], -1)
+
+
+def se3_plus(T: np.ndarray, d: np.ndarray) -> np.ndarray:
+    """LocalParameterizationSE3::Plus — T · exp(δ) (local_parameterization_se3.hpp:43-50)."""
+    return se3_mul(T, se3_exp(d))
+
+
+def unproject(model: int, k: np.ndarray, uv: np.ndarray) -> np.ndarray:
+    """Unit bearings (camera_models.h unproject + normalize), vectorised over uv (..., 2)."""
+    k = np.asarray(k, np.float64)
+    mx = (uv[..., 0] - k[..., 2]) / k[..., 0]
+    my = (uv[..., 1] - k[..., 3]) / k[..., 1]
+    r2 = mx * mx + my * my
+    if model == PINHOLE:
+        b = np.stack([mx, my, np.ones_like(mx)], -1)
+    elif model == DOUBLE_SPHERE:
+        xi, al = k[..., 4], k[..., 5]
+        mz = (1 - al * al * r2) / (al * np.sqrt(1 - (2 * al - 1) * r2) + 1 - al)
+        fac = (mz * xi + np.sqrt(mz * mz + (1 - xi * xi) * r2)) / (mz * mz + r2)
+        b = np.stack([fac * mx, fac * my, fac * mz - xi], -1)
+    else:
+        al, be = k[..., 4], k[..., 5]
+        mz = (1 - be * al * al * r2) / (al * np.sqrt(1 - (2 * al - 1) * be * r2) + (1 - al))
+        b = np.stack([mx, my, mz], -1)
+    return b / np.linalg.norm(b, axis=-1, keepdims=True)
+
+
+def project(model: int, k: np.ndarray, p: np.ndarray) -> np.ndarray:
+    k = np.asarray(k, np.float64)
+    x, y, z = p[..., 0], p[..., 1], p[..., 2]
+    if model == PINHOLE:
+        den = z
+    elif model == DOUBLE_SPHERE:
+        xi, al = k[..., 4], k[..., 5]
+        d1 = np.sqrt(x * x + y * y + z * z)
+        xz = xi * d1 + z
+        d2 = np.sqrt(x * x + y * y + xz * xz)
+        den = al * d2 + (1 - al) * xz
+    else:
+        al, be = k[..., 4], k[..., 5]
+        d = np.sqrt(be * (x * x + y * y) + z * z)
+        den = al * d + (1 - al) * z
+    return np.stack([k[..., 0] * x / den + k[..., 2], k[..., 1] * y / den + k[..., 3]], -1)
+
+
+def bilinear(img: np.ndarray, u: np.ndarray, v: np.ndarray) -> np.ndarray:
+    """Bilinear + edge clamp (the oracle's interpolator), vectorised over one image."""
+    H, W = img.shape
+    u = np.clip(u, -2, W + 1)
+    v = np.clip(v, -2, H + 1)
+    x0 = np.floor(u)
+    y0 = np.floor(v)
+    a, b = u - x0, v - y0
+    x0 = x0.astype(np.int64)
+    y0 = y0.astype(np.int64)
+    xa, xb = np.clip(x0, 0, W - 1), np.clip(x0 + 1, 0, W - 1)
+    ya, yb = np.clip(y0, 0, H - 1), np.clip(y0 + 1, 0, H - 1)
+    I = img.astype(np.float64)
+    return ((1 - b) * ((1 - a) * I[ya, xa] + a * I[ya, xb]) + b * ((1 - a) * I[yb, xa] + a * I[yb, xb]))
+
+
+# ------------------------------------------------------------------------------------------------
+# Scene
+# ------------------------------------------------------------------------------------------------
+def trajectory(n_frames: int, step: float = 0.05, yaw: float = 0.002) -> np.ndarray:
+    k = np.arange(n_frames, dtype=np.float64)
+    w = np.stack([np.zeros_like(k), yaw * k, np.zeros_like(k)], -1)
+    q = so3_exp(w)
+    t = np.stack([step * k, np.zeros_like(k), np.zeros_like(k)], -1)
+    return np.concatenate([q, t], -1)
+
+
+class PlaneTexture:
+    """Smooth intensity field on the world plane Z = z0 (sum of random sinusoids), range ~[20, 235]."""
+
+    def __init__(self, rng: np.random.Generator, z0: float = 6.0, n_waves: int = 12):
+        self.z0 = z0
+        ang = rng.uniform(0, np.pi, n_waves)
+        freq = rng.uniform(0.8, 7.0, n_waves) * 2 * np.pi  # rad / m
+        self.kx, self.ky = freq * np.cos(ang), freq * np.sin(ang)
+        self.phase = rng.uniform(0, 2 * np.pi, n_waves)
+        self.amp = rng.uniform(0.5, 1.0, n_waves)
+        self.amp /= self.amp.sum()
+
+    def __call__(self, X: np.ndarray, Y: np.ndarray) -> np.ndarray:
+        s = np.zeros_like(X)
+        for i in range(len(self.kx)):
+            s += self.amp[i] * np.sin(self.kx[i] * X + self.ky[i] * Y + self.phase[i])
+        return 127.5 + 107.5 * s
+
+    def render(self, model: int, k: np.ndarray, pose: np.ndarray, W: int, H: int) -> np.ndarray:
+        uu, vv = np.meshgrid(np.arange(W, dtype=np.float64), np.arange(H, dtype=np.float64))
+        b = unproject(model, k, np.stack([uu, vv], -1))
+        R = quat_to_rot(pose[:4])
+        d = b @ R.T
+        lam = (self.z0 - pose[6]) / d[..., 2]
+        X = pose[4] + lam * d[..., 0]
+        Y = pose[5] + lam * d[..., 1]
+        return np.clip(np.rint(self(X, Y)), 0, 255).astype(np.uint8)
+
+    def depth(self, pose: np.ndarray, b: np.ndarray) -> np.ndarray:
+        """Distance along bearings b (camera frame) to the plane."""
+        d = (quat_to_rot(pose[..., :4]) @ b[..., None])[..., 0]
+        return (self.z0 - pose[..., 6]) / d[..., 2]
+
+
+def noise_images(rng: np.random.Generator, n: int, W: int, H: int, cell: int = 8) -> np.ndarray:
+    """Independent smooth random textures (bilinear upsample of a coarse random grid)."""
+    gh, gw = H // cell + 2, W // cell + 2
+    g = rng.uniform(20, 235, (n, gh, gw))
+    ys = np.arange(H) / cell
+    xs = np.arange(W) / cell
+    y0 = np.floor(ys).astype(int)
+    x0 = np.floor(xs).astype(int)
+    fy = (ys - y0)[None, :, None]
+    fx = (xs - x0)[None, None, :]
+    a = g[:, y0][:, :, x0]
+    b = g[:, y0][:, :, x0 + 1]
+    c = g[:, y0 + 1][:, :, x0]
+    d = g[:, y0 + 1][:, :, x0 + 1]
+    img = (1 - fy) * ((1 - fx) * a + fx * b) + fy * ((1 - fx) * c + fx * d)
+    img += rng.normal(0, 2.0, img.shape)
+    return np.clip(np.rint(img), 0, 255).astype(np.uint8)
+
+
+def make_problem(n_frames: int = 8, n_points: int = 64, K: int = 4, width: int = 752, height: int = 480,
+                 model: int | str = PINHOLE, kind: int | str = PHOTOMETRIC, pattern: Optional[np.ndarray] = None,
+                 seed: int = 42, texture: str = "render", perturb: bool = True, pose_sigma: float = 0.003,
+                 rho_sigma: float = 0.02, border: int = 24, obs_sigma: float = 0.5,
+                 with_images: bool = True) -> Problem:
+    """Build a synthetic problem.  ``poses``/``rho`` hold the perturbed state."""
+    model = MODEL_IDS.get(model, model) if isinstance(model, str) else model
+    kind = KIND_IDS.get(kind, kind) if isinstance(kind, str) else kind
+    if n_frames < K + 1:
+        raise ValueError("need at least K+1 keyframes")
+    rng = np.random.default_rng(seed)
+    intr = np.array([DEFAULT_INTRINSICS[model]], np.float64)
+    intr[0, :4] *= width / 752.0  # intrinsics are quoted for 752×480; rescale for other sizes
+    frame_cam = np.zeros(n_frames, np.int32)
+    poses_gt = trajectory(n_frames)
+    pat = PATTERN8 if pattern is None else np.asarray(pattern, np.float32)
+
+    point_host = rng.integers(0, n_frames - K, n_points).astype(np.int32)
+    u_ref = np.stack([rng.integers(border, width - border, n_points),
+                      rng.integers(border, height - border, n_points)], -1).astype(np.float64)
+    b = unproject(model, intr[0], u_ref)
+
+    tex = None
+    if texture == "render":
+        tex = PlaneTexture(rng)
+        dist = tex.depth(poses_gt[point_host], b)
+    else:
+        dist = np.clip(6.0 + rng.normal(0, 1.0, n_points), 3.0, 12.0)
+    rho_gt = 1.0 / dist
+
+    block_point = np.repeat(np.arange(n_points, dtype=np.int32), K)
+    block_target = (np.repeat(point_host, K) + np.tile(np.arange(1, K + 1, dtype=np.int32), n_points)).astype(np.int32)
+
+    images = host_int = u_obs = None
+    if kind == PHOTOMETRIC and with_images:
+        if texture == "render":
+            images = np.stack([tex.render(model, intr[0], poses_gt[f], width, height) for f in range(n_frames)])
+        else:
+            images = noise_images(rng, n_frames, width, height)
+        host_int = np.empty((n_points, len(pat)), np.float32)
+        for f in np.unique(point_host):
+            sel = np.nonzero(point_host == f)[0]
+            uu = u_ref[sel, None, 0] + pat[None, :, 0]
+            vv = u_ref[sel, None, 1] + pat[None, :, 1]
+            host_int[sel] = bilinear(images[f], uu, vv).astype(np.float32)
+    if kind == GEOMETRIC:
+        ph = b / rho_gt[:, None]
+        Th, Tt = poses_gt[point_host[block_point]], poses_gt[block_target]
+        pw = (quat_to_rot(Th[:, :4]) @ ph[block_point, :, None])[..., 0] + Th[:, 4:]
+        pt = (np.swapaxes(quat_to_rot(Tt[:, :4]), -1, -2) @ (pw - Tt[:, 4:])[..., None])[..., 0]
+        u_obs = project(model, intr[0], pt) + rng.normal(0, obs_sigma, (len(block_point), 2))
+
+    poses, rho = poses_gt.copy(), rho_gt.copy()
+    if perturb:
+        poses = se3_plus(poses_gt, pose_sigma * rng.normal(0, 1, (n_frames, 6)))
+        rho = rho_gt * (1 + rho_sigma * rng.normal(0, 1, n_points))
+    return Problem(kind=kind, model=model, width=width, height=height, intrinsics=intr, frame_cam=frame_cam,
+                   images=images, pattern=pat, point_host=point_host, u_ref=u_ref, host_intensity=host_int,
+                   block_point=block_point, block_target=block_target, u_obs=u_obs, poses=poses, rho=rho,
+                   poses_gt=poses_gt, rho_gt=rho_gt)

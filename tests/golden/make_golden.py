@@ -1,0 +1,157 @@
+#!/usr/bin/env python3
+"""Regenerate the golden fixtures in tests/golden/ from the reference's own vendored Sophus/Eigen.
+
+Runs in the build container only (needs /root/reference): builds oracle/_ref/ref_harness from
+oracle/ref_harness.cpp against /root/reference/thirdparty/{Sophus,eigen}, feeds it seeded synthetic
+problems (photometric-bundle-adjustment_amd/synth.py) and stores inputs + outputs as compressed .npz.
+The GPU box only ever sees the .npz files.
+
+Harness input layout ("block" mode), little-endian:
+  int32 kind, model, n_frames, n_points, n_blocks, n_cams, W, H, P
+  f64 intrinsics[8·n_cams]; i32 frame_cam[n_frames]; u8 images[n_frames·H·W] (photometric)
+  f32 pattern[2P] (photometric); i32 point_host[n_points]; f64 u_ref[2·n_points]
+  f32 host_intensity[P·n_points] (photometric); i32 block_point[n_blocks]; i32 block_target[n_blocks]
+  f64 u_obs[2·n_blocks] (geometric); f64 poses[7·n_frames]; f64 rho[n_points]
+Output: f64 record[n_blocks·14R]; u8 valid[n_blocks]; u8 fd_ok[n_blocks]
+"""
+from __future__ import annotations
+
+import importlib
+import json
+import os
+import subprocess
+import sys
+import tempfile
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, ROOT)
+synth = importlib.import_module("photometric-bundle-adjustment_amd.synth")
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+HARNESS = os.path.join(ROOT, "oracle", "_ref", "ref_harness")
+
+
+def build_harness():
+    subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle"), "ref"], check=True)
+    if not os.path.exists(HARNESS):
+        raise SystemExit("reference not present; cannot regenerate golden vectors")
+
+
+def write_problem(f, pb):
+    ph = pb.kind == synth.PHOTOMETRIC
+    P = pb.pattern.shape[0] if ph else 0
+    np.array([pb.kind, pb.model, pb.n_frames, pb.n_points, pb.n_blocks, pb.intrinsics.shape[0],
+              pb.width, pb.height, P], np.int32).tofile(f)
+    pb.intrinsics.astype(np.float64).tofile(f)
+    pb.frame_cam.astype(np.int32).tofile(f)
+    if ph:
+        pb.images.astype(np.uint8).tofile(f)
+        pb.pattern.astype(np.float32).tofile(f)
+    pb.point_host.astype(np.int32).tofile(f)
+    pb.u_ref.astype(np.float64).tofile(f)
+    if ph:
+        pb.host_intensity.astype(np.float32).tofile(f)
+    pb.block_point.astype(np.int32).tofile(f)
+    pb.block_target.astype(np.int32).tofile(f)
+    if not ph:
+        pb.u_obs.astype(np.float64).tofile(f)
+    pb.poses.astype(np.float64).tofile(f)
+    pb.rho.astype(np.float64).tofile(f)
+
+
+def run_block(pb):
+    with tempfile.TemporaryDirectory() as td:
+        fin, fout = os.path.join(td, "in.bin"), os.path.join(td, "out.bin")
+        with open(fin, "wb") as f:
+            write_problem(f, pb)
+        subprocess.run([HARNESS, "block", fin, fout], check=True)
+        raw = np.fromfile(fout, np.uint8)
+    R = pb.pattern.shape[0] if pb.kind == synth.PHOTOMETRIC else 2
+    nrec = 14 * R * pb.n_blocks * 8
+    rec = raw[:nrec].view(np.float64).reshape(pb.n_blocks, 14 * R)
+    valid = raw[nrec:nrec + pb.n_blocks]
+    fdok = raw[nrec + pb.n_blocks:nrec + 2 * pb.n_blocks]
+    return rec, valid, fdok
+
+
+def save_block_fixture(name, pb, note):
+    rec, valid, fdok = run_block(pb)
+    arrays = dict(kind=pb.kind, model=pb.model, width=pb.width, height=pb.height, intrinsics=pb.intrinsics,
+                  frame_cam=pb.frame_cam, pattern=pb.pattern, point_host=pb.point_host, u_ref=pb.u_ref,
+                  block_point=pb.block_point, block_target=pb.block_target, poses=pb.poses, rho=pb.rho,
+                  expect_record=rec, expect_valid=valid, expect_fd_ok=fdok)
+    if pb.images is not None:
+        arrays["images"] = pb.images
+        arrays["host_intensity"] = pb.host_intensity
+    if pb.u_obs is not None:
+        arrays["u_obs"] = pb.u_obs
+    np.savez_compressed(os.path.join(GOLDEN, name + ".npz"), **arrays)
+    return dict(file=name + ".npz", blocks=int(pb.n_blocks), valid=int(valid.sum()), fd_ok=int(fdok.sum()), note=note)
+
+
+def se3_fixture(n=256, seed=7):
+    rng = np.random.default_rng(seed)
+
+    def rand_pose(k):
+        q = rng.normal(size=(k, 4))
+        q /= np.linalg.norm(q, axis=1, keepdims=True)
+        return np.concatenate([q, rng.normal(0, 3, (k, 3))], 1)
+
+    poses, poses2 = rand_pose(n), rand_pose(n)
+    deltas = rng.normal(0, 0.5, (n, 6))
+    deltas[: n // 8, 3:] *= 1e-12  # exercise the small-angle branch of SO3::expAndTheta
+    points = rng.normal(0, 5, (n, 3))
+    with tempfile.TemporaryDirectory() as td:
+        fin, fout = os.path.join(td, "in.bin"), os.path.join(td, "out.bin")
+        with open(fin, "wb") as f:
+            np.array([n], np.int32).tofile(f)
+            poses.tofile(f)
+            poses2.tofile(f)
+            deltas.tofile(f)
+            points.tofile(f)
+        subprocess.run([HARNESS, "se3", fin, fout], check=True)
+        out = np.fromfile(fout, np.float64).reshape(n, 7 + 7 + 7 + 3 + 42 + 7)
+    np.savez_compressed(os.path.join(GOLDEN, "sophus_se3.npz"), poses=poses, poses2=poses2, deltas=deltas,
+                        points=points, exp=out[:, 0:7], plus=out[:, 7:14], inverse=out[:, 14:21],
+                        act=out[:, 21:24], plus_jacobian=out[:, 24:66].reshape(n, 7, 6), rel=out[:, 66:73])
+    return dict(file="sophus_se3.npz", n=n, note="Sophus::SE3d exp / T*exp / inverse / T*p / "
+                "Dx_this_mul_exp_x_at_0 / T2^-1*T (se3.hpp:135-211,763-784)")
+
+
+def main():
+    build_harness()
+    manifest = {"generator": "tests/golden/make_golden.py", "harness": "oracle/ref_harness.cpp",
+                "compiled_against": ["/root/reference/thirdparty/Sophus (1.1.0)", "/root/reference/thirdparty/eigen (3.3.8)"],
+                "fixtures": []}
+    manifest["fixtures"].append(se3_fixture())
+    W, H = 320, 200
+    cases = [
+        ("geometric_pinhole", dict(kind="geometric", model="pinhole", n_frames=10, n_points=300, width=752, height=480, seed=11),
+         "reprojection.h:105-108 residual, pinhole; tangent J by long-double central differences through Sophus"),
+        ("geometric_ds", dict(kind="geometric", model="ds", n_frames=10, n_points=300, width=752, height=480, seed=12),
+         "reprojection.h:105-108 residual, double sphere (camera_models.h:226-277)"),
+        ("photometric_pinhole", dict(kind="photometric", model="pinhole", n_frames=7, n_points=128, width=W, height=H, seed=13),
+         "photometric residual (photometric_error.h:151-179 + bilinear), pinhole, 8-px DSO pattern"),
+        ("photometric_ds", dict(kind="photometric", model="ds", n_frames=7, n_points=96, width=W, height=H, seed=14),
+         "photometric residual, double sphere"),
+        ("photometric_eucm", dict(kind="photometric", model="eucm", n_frames=7, n_points=96, width=W, height=H, seed=15),
+         "photometric residual, EUCM (Ceres PhotometricError camera)"),
+    ]
+    for name, kw, note in cases:
+        pb = synth.make_problem(border=12 if kw["width"] < 752 else 24, **kw)
+        manifest["fixtures"].append(save_block_fixture(name, pb, note))
+    # Edge cases: points pushed off-image (edge clamp) and behind the target (invalid blocks).
+    pb = synth.make_problem(kind="photometric", model="pinhole", n_frames=6, n_points=64, width=W, height=H, seed=16, border=2)
+    # keyframe 5 turned around (π about y): every block targeting it leaves the pinhole domain → invalid
+    pb.poses[5] = synth.se3_plus(pb.poses[5], np.array([0, 0, 0, 0, np.pi, 0.0]))
+    pb.u_ref[8:16, 0] = W - 1.0          # right image edge: pattern taps clamp
+    pb.u_ref[16:24, 1] = 0.0             # top edge
+    manifest["fixtures"].append(save_block_fixture("photometric_edges", pb, "edge clamp + invalid (behind camera) blocks"))
+    with open(os.path.join(GOLDEN, "MANIFEST.json"), "w") as f:
+        json.dump(manifest, f, indent=1)
+    print(json.dumps(manifest, indent=1))
+
+
+if __name__ == "__main__":
+    main()
