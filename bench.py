@@ -1,0 +1,225 @@
+#!/usr/bin/env python3
+"""bench.py — photometric residual+Jacobian blocks/s on MI355X (BASELINE.json metric, configs[3] workload).
+
+Workload per GPU (BASELINE.json configs[3] / SURVEY.md §8d C4): a synthetic 1000-keyframe × 100k-point problem,
+8-pixel DSO pattern, every point observed by the 4 keyframes after its host → 400,000 residual blocks
+(3.2 M pixel residuals), 752×480 u8 images (361 MB), pinhole camera.  One step = one full evaluation of
+every block's residuals and tangent Jacobians (Ceres-mode records, include/pba.h) at a new state that is
+already resident in HBM: state copy + pair kernel + block kernel, all on the engine stream.
+
+Multi-GPU (launched by torch.distributed.run): residual blocks shard by host keyframe — each rank owns its
+own 1000-host-keyframe shard (weak scaling) and evaluates it with no data-path collective (the Ceres-mode
+evaluation has no exchange step).  Timing: W warmup steps, then exactly K steps bracketed by
+barrier + synchronize; the MAX over ranks is reported; value = all ranks' blocks ÷ that time.
+
+Also reported: the block kernel's roofline position (algorithmic bytes ÷ HIP-event-timed kernel duration,
+on the engine stream) and a CPU baseline (the oracle's dual-number AutoDiff evaluation — the reference's
+Ceres AutoDiff arithmetic restated — timed on a bounded sample of the same workload on this host).
+"""
+from __future__ import annotations
+
+import argparse
+import importlib
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+synth = importlib.import_module("photometric-bundle-adjustment_amd.synth")
+engine_mod = importlib.import_module("photometric-bundle-adjustment_amd.engine")
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+
+
+def gpu_noise_images(torch, n, H, W, seed, device):
+    """Independent smooth random u8 textures, generated on the GPU (content irrelevant for throughput)."""
+    import torch.nn.functional as F
+    g = torch.Generator(device=device)
+    g.manual_seed(seed)
+    out = torch.empty((n, H, W), dtype=torch.uint8, device=device)
+    chunk = 100
+    for s in range(0, n, chunk):
+        m = min(chunk, n - s)
+        coarse = torch.rand((m, 1, H // 8 + 2, W // 8 + 2), generator=g, device=device) * 215 + 20
+        img = F.interpolate(coarse, size=(H + 16, W + 16), mode="bilinear", align_corners=False)[:, 0, :H, :W]
+        img = img + torch.randn((m, H, W), generator=g, device=device) * 2.0
+        out[s:s + m] = img.round().clamp(0, 255).to(torch.uint8)
+    return out
+
+
+def algorithmic_bytes_per_block(P: int, K: int, n_pairs: int, n_blocks: int) -> float:
+    """SURVEY.md §8d, Ceres mode, fp32 records: inputs + taps + outputs per block (formula in DESIGN.md)."""
+    idx = 8.0                                  # block_point + block_pair (int32)
+    point = (8.0 + 8.0 + 4.0 * P) / K          # u_ref (2×f32) + ρ (f64) + I_h (P×f32), shared by K blocks
+    pair = 64.0 * n_pairs / n_blocks           # fp32 R|t + ids, shared by all blocks of a (host, target) pair
+    taps = 4.0 * P                             # 4 u8 bilinear taps per pixel (gradient from the same taps)
+    out = 4.0 * 14 * P + 4.0 + 1.0             # record [r | J_h | J_t | J_ρ] + cost + valid
+    return idx + point + pair + taps + out
+
+
+def cpu_baseline(pb, images_host, budget_s: float, threads: int):
+    """Oracle (dual-number AutoDiff, as Ceres' AutoDiffCostFunction) on a bounded sample of the workload."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    pbc = synth.Problem(**{**pb.__dict__, "images": images_host})
+
+    def run(n):
+        sub = synth.Problem(**{**pbc.__dict__, "block_point": pbc.block_point[:n], "block_target": pbc.block_target[:n]})
+        t0 = time.perf_counter()
+        O.evaluate(sub, want_jac=True, n_threads=threads)
+        return time.perf_counter() - t0
+
+    n = 4000
+    dt = run(n)
+    rate = n / max(dt, 1e-9)
+    n = int(min(pb.n_blocks, max(4000, rate * budget_s)))
+    dt = run(n)
+    return {"value": n / dt, "unit": "blocks/s", "cores": threads, "kind": "port",
+            "sample": f"first {n} of the {pb.n_blocks} blocks of the same problem (r + tangent J, P=8), "
+                      f"{dt:.1f} s on {threads} host threads; oracle/oracle.cpp Jet<15> AutoDiff"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--frames", type=int, default=1000)
+    ap.add_argument("--points", type=int, default=100000)
+    ap.add_argument("--targets", type=int, default=4)
+    ap.add_argument("--width", type=int, default=752)
+    ap.add_argument("--height", type=int, default=480)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}; launch N>1 with torch.distributed.run")
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    # ---- problem shard of this rank (host keyframes of shard `rank`, seeded per rank) ----------------
+    K, F, Np = args.targets, args.frames, args.points
+    pb = synth.make_problem(n_frames=F, n_points=Np, K=K, width=args.width, height=args.height, kind="photometric",
+                            model="pinhole", texture="noise", with_images=False, seed=42 + rank)
+    images = gpu_noise_images(torch, F, args.height, args.width, 1234 + rank, dev)
+    host = torch.from_numpy(pb.point_host.astype(np.int64)).to(dev)
+    uu = torch.from_numpy(pb.u_ref[:, 0].astype(np.int64)).to(dev)[:, None] + torch.from_numpy(pb.pattern[:, 0].astype(np.int64)).to(dev)
+    vv = torch.from_numpy(pb.u_ref[:, 1].astype(np.int64)).to(dev)[:, None] + torch.from_numpy(pb.pattern[:, 1].astype(np.int64)).to(dev)
+    # integer u_ref and integer pattern → the bilinear host sample is exactly the pixel value
+    pb.host_intensity = images[host[:, None], vv, uu].float().cpu().numpy()
+
+    eng = engine_mod.Engine(synth.PHOTOMETRIC, synth.PINHOLE, device=local_rank, huber_width=9.0)
+    eng.set_problem(pb, images_device_ptr=images.data_ptr())
+    n_blocks = pb.n_blocks
+    rng = np.random.default_rng(7 + rank)
+    states = []
+    for _ in range(2):  # alternate two perturbed states so every step evaluates a new point
+        poses = synth.se3_plus(pb.poses, 1e-3 * rng.normal(0, 1, (F, 6)))
+        rho = pb.rho * (1 + 0.01 * rng.normal(0, 1, Np))
+        states.append((torch.from_numpy(poses).to(dev), torch.from_numpy(rho).to(dev)))
+    eng.set_state_device(states[0][0].data_ptr(), states[0][1].data_ptr())
+    eng.evaluate(True)
+    _, valid = eng.records()
+
+    def step(i):
+        p, r = states[i & 1]
+        eng.set_state_device(p.data_ptr(), r.data_ptr())
+        eng.evaluate(True, sync=False)
+
+    for i in range(args.warmup):
+        step(i)
+    eng.synchronize()
+    eng.enable_kernel_timing(True)
+    eng.kernel_timing()  # reset
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(i)
+    eng.synchronize()
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    if world > 1:
+        dist.barrier()
+    elapsed = t1 - t0
+    kern_ms, launches = eng.kernel_timing()
+    t = torch.tensor([elapsed, kern_ms / max(launches, 1)], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed_max, kern_avg_ms = float(t[0]), float(t[1])
+
+    if rank == 0:
+        ms_per_step = 1e3 * elapsed_max / args.steps
+        total_blocks = n_blocks * world * args.steps
+        value = total_blocks / elapsed_max
+        n_pairs = len(np.unique(pb.point_host[pb.block_point].astype(np.int64) * F + pb.block_target))
+        bpb = algorithmic_bytes_per_block(pb.P, K, n_pairs, n_blocks)
+        achieved = bpb * n_blocks / (kern_avg_ms * 1e-3) / 1e9
+        traffic = None
+        tf = os.path.join(ROOT, "profiles", "traffic_photometric_block_kernel.json")
+        if os.path.exists(tf):
+            try:
+                tj = json.load(open(tf))
+                if tj.get("n_blocks") == n_blocks and tj.get("P") == pb.P:
+                    traffic = tj.get("hbm_bytes_per_launch")
+            except Exception:
+                traffic = None
+        cpu = None
+        if world == 1 and not args.no_cpu_baseline:
+            threads = max(1, min(16, os.cpu_count() or 1))
+            cpu = cpu_baseline(pb, images.cpu().numpy(), args.cpu_seconds, threads)
+        out = {
+            "metric": "photometric residual+jacobian blocks/sec",
+            "value": value,
+            "unit": "blocks/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": ms_per_step,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic",
+            "config": {
+                "workload": f"C4 shard per GPU: synthetic {F} keyframes x {Np} points x {pb.P}-px patch x {K} targets "
+                            f"= {n_blocks} residual blocks, {args.width}x{args.height} u8 images, pinhole; one step = "
+                            f"full r + tangent-J evaluation (Ceres-mode records) at a new HBM-resident state",
+                "keyframes": F, "points": Np, "patch": pb.P, "targets_per_point": K, "blocks_per_gpu": n_blocks,
+                "valid_blocks": int(valid.sum()), "parallelism": f"host-keyframe shards x{world} (no data-path collective)",
+            },
+            "roofline": {
+                "bound": "hbm",
+                "kernel": "photometric_block_kernel<pinhole,8>",
+                "achieved": achieved,
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS,
+                "traffic": traffic,
+                "bytes_per_block_alg": bpb,
+                "kernel_avg_us": kern_avg_ms * 1e3,
+            },
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    eng.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,134 @@
+/* include/pba.h — C ABI of the MI355X photometric bundle-adjustment residual/Jacobian engine.
+ *
+ * This is the drop-in boundary for the reference's hot path.  In the reference every residual block is
+ * a separate Ceres AutoDiffCostFunction evaluated on CPU threads:
+ *
+ *   map_utils.h:347-375      problem build: one AutoDiffCostFunction<Functor,2,7,7,1,8> + HuberLoss per
+ *                            (landmark, non-anchor observation); parameters (T_w_host, T_w_target, ρ, intr)
+ *   reprojection.h:83-112    BundleAdjustmentReprojectionCostFunctor::operator()  (geometric residual)
+ *   photometric_error.h:139-182  PhotometricError<8>::operator()                 (photometric residual)
+ *   program_evaluator.h:139-258  ProgramEvaluator::Evaluate — the per-block ParallelFor this replaces
+ *   residual_block.cc:69-198     ResidualBlock::Evaluate   — J_local = J_global · P(7×6)
+ *   evaluation_callback.h:63-76  EvaluationCallback::PrepareForEvaluation — where pba_evaluate is called
+ *
+ * One engine evaluates ALL blocks of a problem in one launch on one GPU.  Conventions:
+ *   pose        Sophus SE3d storage [qx qy qz qw tx ty tz], camera-to-world T_w_c (common_types.h:174-179)
+ *   tangent     δ = [υ(3), ω(3)], right update T·exp(δ)  (local_parameterization_se3.hpp:43-50)
+ *   point       anchored at its host keyframe; inverse DISTANCE ρ along the unit bearing of u_ref
+ *               (common_types.h:205-217; reprojection.h:105-108)
+ *   intrinsics  8-vector [fx fy cx cy p1 p2 p3 p4] (camera_models.h:50); model shared by all cameras,
+ *               host camera model used for the target too (reprojection.h:99-100)
+ *   block       (point, target keyframe); host = the point's host keyframe
+ *   residuals   geometric: r = u_obs − π_t(T_w_t⁻¹ T_w_h b/ρ)                    (R = 2)
+ *               photometric: r_k = I_t(π_t(R_th b_k + ρ t_th)) − I_h,k, k < P      (R = P)
+ *               bilinear interpolation of the u8 target image, Grid2D-style edge clamp
+ *   record      per block, R×14 floats: [ r(R) | J_host(R×6) | J_target(R×6) | J_rho(R) ], row-major,
+ *               tangent-space (= Ceres' J_global·P of residual_block.cc:136-158), NOT robustified
+ *               (the loss stays with the caller, residual_block.cc:161-196).
+ *   valid       per block 1/0; 0 when a projection leaves the camera's domain or a value is non-finite;
+ *               the record is then all zeros (a Ceres adapter returns false for such a block,
+ *               matching residual_block.cc:113-131).
+ *
+ * Memory: every pointer argument is a HOST pointer unless the function name ends in _device.  The engine
+ * owns its device buffers; the caller owns its host buffers.  One engine per GPU; calls on one engine
+ * must be serialised by the caller (thread-compatible, not thread-safe).  All functions return PBA_OK
+ * (0) or a negative status; pba_last_error() describes the most recent failure of the calling thread.
+ */
+#ifndef PBA_H_
+#define PBA_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PBA_OK 0
+#define PBA_ERR_INVALID_ARGUMENT (-1)
+#define PBA_ERR_DEVICE (-2)          /* HIP runtime error (no device, launch failure, …) */
+#define PBA_ERR_OUT_OF_MEMORY (-3)
+#define PBA_ERR_NOT_READY (-4)       /* a set_* call required by this call has not been made */
+
+#define PBA_RESIDUAL_PHOTOMETRIC 0
+#define PBA_RESIDUAL_GEOMETRIC 1
+
+#define PBA_CAMERA_PINHOLE 0        /* camera_models.h:48-114  */
+#define PBA_CAMERA_DOUBLE_SPHERE 1  /* camera_models.h:198-284 */
+#define PBA_CAMERA_EUCM 2           /* camera_models.h:116-196 */
+
+#define PBA_MAX_PATTERN 32
+
+typedef struct pba_engine pba_engine;
+
+typedef struct pba_options {
+  int32_t device;         /* HIP device ordinal */
+  int32_t residual_kind;  /* PBA_RESIDUAL_* */
+  int32_t camera_model;   /* PBA_CAMERA_* */
+  float huber_width;      /* a of HuberLoss(a) for the per-block cost (loss_function.cc:48-62); <= 0: squared */
+} pba_options;
+
+/* Lifecycle ------------------------------------------------------------------------------------- */
+int pba_create(const pba_options* options, pba_engine** out_engine);
+int pba_destroy(pba_engine* engine);
+const char* pba_status_string(int status);
+const char* pba_last_error(void);
+int pba_version(void);  /* 100·major + minor */
+
+/* Problem description (BundleAdjustment problem build, map_utils.h:322-375) ---------------------- */
+/* intrinsics: 8·n_cams doubles */
+int pba_set_cameras(pba_engine* engine, int32_t n_cams, const double* intrinsics);
+/* frame_cam[n_frames]: camera index of every keyframe; images: n_frames·height·width u8, row-major,
+ * required for photometric engines (may be NULL for geometric ones). */
+int pba_set_frames(pba_engine* engine, int32_t n_frames, const int32_t* frame_cam, int32_t width,
+                   int32_t height, const uint8_t* images);
+/* same, with the images already in device memory (copied device-to-device on the engine stream) */
+int pba_set_frames_device(pba_engine* engine, int32_t n_frames, const int32_t* frame_cam, int32_t width,
+                          int32_t height, const uint8_t* d_images);
+/* residual pattern: P (du, dv) pairs, P <= PBA_MAX_PATTERN (photometric only) */
+int pba_set_pattern(pba_engine* engine, int32_t P, const float* offsets);
+/* points: host keyframe, u_ref (2 doubles, pixel in the host image), host_intensity (P floats,
+ * photometric only — the I_h,k of photometric_error.h:179). */
+int pba_set_points(pba_engine* engine, int32_t n_points, const int32_t* host_frame, const double* u_ref,
+                   const float* host_intensity);
+/* blocks: point index and target keyframe per block; u_obs (2 doubles per block) for geometric engines.
+ * target != host(point) is required. */
+int pba_set_blocks(pba_engine* engine, int32_t n_blocks, const int32_t* block_point,
+                   const int32_t* block_target, const double* u_obs);
+
+/* Evaluation (EvaluationCallback::PrepareForEvaluation → one launch) ----------------------------- */
+/* poses: 7·n_frames doubles; inv_dist: n_points doubles (host memory; copied to the device) */
+int pba_set_state(pba_engine* engine, const double* poses, const double* inv_dist);
+int pba_set_state_device(pba_engine* engine, const double* d_poses, const double* d_inv_dist);
+/* Enqueue the evaluation of every block on the engine's stream.  want_jacobians = 0 writes only the
+ * residual part of each record (Ceres' residual-only evaluation, trust_region_minimizer.cc:761-779). */
+int pba_evaluate(pba_engine* engine, int32_t want_jacobians);
+int pba_synchronize(pba_engine* engine);
+
+/* Results ---------------------------------------------------------------------------------------- */
+int pba_record_floats(const pba_engine* engine);   /* 14·R */
+int pba_residuals_per_block(const pba_engine* engine);
+/* records: n_blocks·record_floats floats; valid: n_blocks bytes (either may be NULL).  Synchronises. */
+int pba_get_records(pba_engine* engine, float* records, uint8_t* valid);
+/* per-block cost ½ρ(‖r‖²) with the engine's Huber width (0 for invalid blocks) */
+int pba_get_block_costs(pba_engine* engine, float* costs);
+/* Σ block costs, summed in double on the host; n_valid may be NULL */
+int pba_get_cost(pba_engine* engine, double* total_cost, int32_t* n_valid);
+
+/* Device-side access for in-process consumers (zero copy) ----------------------------------------- */
+/* hipStream_t the engine enqueues on (may be replaced with pba_set_stream; NULL = engine's own) */
+int pba_set_stream(pba_engine* engine, void* hip_stream);
+int pba_get_stream(pba_engine* engine, void** hip_stream);
+int pba_device_records(pba_engine* engine, float** d_records, uint8_t** d_valid, float** d_costs);
+
+/* Kernel timing: when enabled, every pba_evaluate brackets its residual/Jacobian block kernel with
+ * hipEvents on the engine stream; pba_get_kernel_timing synchronises, returns the summed device time of
+ * the block kernel (ms) and the launch count since the last call, and resets. */
+int pba_enable_kernel_timing(pba_engine* engine, int32_t enable);
+int pba_get_kernel_timing(pba_engine* engine, double* total_ms, int32_t* launches);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* PBA_H_ */

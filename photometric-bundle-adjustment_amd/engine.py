@@ -1,0 +1,220 @@
+"""Python binding of the C ABI in include/pba.h (ctypes over csrc/libpba.so).
+
+This is the host-side mirror used by the tests and bench; the C++ Ceres-style adapter for the reference's
+own code lives in include/pba_ceres.h.  There is no CPU fallback: if libpba.so is
+missing or the device call fails, every method raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import re
+import subprocess
+from typing import Optional
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(HERE, "csrc")
+LIB_PATH = os.path.join(CSRC, "libpba.so")
+HEADER = os.path.join(os.path.dirname(HERE), "include", "pba.h")
+
+PBA_OK = 0
+_LIB = None
+
+
+class Options(C.Structure):
+    _fields_ = [("device", C.c_int32), ("residual_kind", C.c_int32), ("camera_model", C.c_int32),
+                ("huber_width", C.c_float)]
+
+
+def build(force: bool = False) -> str:
+    """Compile csrc/libpba.so for gfx950 with hipcc (in-tree)."""
+    args = ["make", "-s", "-C", CSRC]
+    if force:
+        args.append("-B")
+    subprocess.run(args + ["libpba.so"], check=True)
+    return LIB_PATH
+
+
+def header_functions() -> list[str]:
+    """Every function declared in include/pba.h."""
+    src = open(HEADER).read()
+    return sorted(set(re.findall(r"^\s*(?:int|const char\*|void)\s+(pba_\w+)\s*\(", src, re.M)))
+
+
+def lib():
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(f"HIP engine library missing: {LIB_PATH} (run __graft_entry__.build())")
+    L = C.CDLL(LIB_PATH)
+    vp, i32 = C.c_void_p, C.c_int32
+    sig = {
+        "pba_create": ([C.POINTER(Options), C.POINTER(vp)], C.c_int),
+        "pba_destroy": ([vp], C.c_int),
+        "pba_status_string": ([C.c_int], C.c_char_p),
+        "pba_last_error": ([], C.c_char_p),
+        "pba_version": ([], C.c_int),
+        "pba_set_cameras": ([vp, i32, vp], C.c_int),
+        "pba_set_frames": ([vp, i32, vp, i32, i32, vp], C.c_int),
+        "pba_set_frames_device": ([vp, i32, vp, i32, i32, vp], C.c_int),
+        "pba_set_pattern": ([vp, i32, vp], C.c_int),
+        "pba_set_points": ([vp, i32, vp, vp, vp], C.c_int),
+        "pba_set_blocks": ([vp, i32, vp, vp, vp], C.c_int),
+        "pba_set_state": ([vp, vp, vp], C.c_int),
+        "pba_set_state_device": ([vp, vp, vp], C.c_int),
+        "pba_evaluate": ([vp, i32], C.c_int),
+        "pba_synchronize": ([vp], C.c_int),
+        "pba_record_floats": ([vp], C.c_int),
+        "pba_residuals_per_block": ([vp], C.c_int),
+        "pba_get_records": ([vp, vp, vp], C.c_int),
+        "pba_get_block_costs": ([vp, vp], C.c_int),
+        "pba_get_cost": ([vp, C.POINTER(C.c_double), C.POINTER(i32)], C.c_int),
+        "pba_set_stream": ([vp, vp], C.c_int),
+        "pba_get_stream": ([vp, C.POINTER(vp)], C.c_int),
+        "pba_device_records": ([vp, C.POINTER(vp), C.POINTER(vp), C.POINTER(vp)], C.c_int),
+        "pba_enable_kernel_timing": ([vp, i32], C.c_int),
+        "pba_get_kernel_timing": ([vp, C.POINTER(C.c_double), C.POINTER(i32)], C.c_int),
+    }
+    for name, (argt, rest) in sig.items():
+        f = getattr(L, name)
+        f.argtypes = argt
+        f.restype = rest
+    _LIB = L
+    return L
+
+
+class PbaError(RuntimeError):
+    pass
+
+
+def _check(rc: int, what: str):
+    if rc != PBA_OK:
+        L = lib()
+        raise PbaError(f"{what}: {L.pba_status_string(rc).decode()} — {L.pba_last_error().decode()}")
+
+
+def _p(a: Optional[np.ndarray]):
+    return None if a is None else C.c_void_p(a.ctypes.data)
+
+
+class Engine:
+    """One engine = one problem on one GPU (include/pba.h)."""
+
+    def __init__(self, kind: int, model: int, device: int = 0, huber_width: float = 0.0):
+        L = lib()
+        self._L = L
+        self._h = C.c_void_p()
+        opt = Options(device, kind, model, huber_width)
+        _check(L.pba_create(C.byref(opt), C.byref(self._h)), "pba_create")
+        self.kind, self.model = kind, model
+        self.n_blocks = self.n_points = self.n_frames = 0
+        self._keep = []
+
+    # -- problem -------------------------------------------------------------------------------
+    def set_problem(self, pb, images_device_ptr: Optional[int] = None):
+        L, h = self._L, self._h
+        intr = np.ascontiguousarray(pb.intrinsics, np.float64)
+        _check(L.pba_set_cameras(h, intr.shape[0], _p(intr)), "pba_set_cameras")
+        fc = np.ascontiguousarray(pb.frame_cam, np.int32)
+        if images_device_ptr is not None:
+            _check(L.pba_set_frames_device(h, fc.shape[0], _p(fc), pb.width, pb.height, C.c_void_p(images_device_ptr)),
+                   "pba_set_frames_device")
+        else:
+            imgs = None if pb.images is None else np.ascontiguousarray(pb.images, np.uint8)
+            _check(L.pba_set_frames(h, fc.shape[0], _p(fc), pb.width, pb.height, _p(imgs)), "pba_set_frames")
+        if pb.kind == 0:
+            pat = np.ascontiguousarray(pb.pattern, np.float32)
+            _check(L.pba_set_pattern(h, pat.shape[0], _p(pat)), "pba_set_pattern")
+        ph = np.ascontiguousarray(pb.point_host, np.int32)
+        ur = np.ascontiguousarray(pb.u_ref, np.float64)
+        hi = None if pb.kind != 0 else np.ascontiguousarray(pb.host_intensity, np.float32)
+        _check(L.pba_set_points(h, ph.shape[0], _p(ph), _p(ur), _p(hi)), "pba_set_points")
+        bp = np.ascontiguousarray(pb.block_point, np.int32)
+        bt = np.ascontiguousarray(pb.block_target, np.int32)
+        uo = None if pb.u_obs is None else np.ascontiguousarray(pb.u_obs, np.float64)
+        _check(L.pba_set_blocks(h, bp.shape[0], _p(bp), _p(bt), _p(uo)), "pba_set_blocks")
+        self.n_blocks, self.n_points, self.n_frames = bp.shape[0], ph.shape[0], fc.shape[0]
+        self.R = L.pba_residuals_per_block(h)
+        self.record = L.pba_record_floats(h)
+
+    def set_state(self, poses: np.ndarray, rho: np.ndarray):
+        poses = np.ascontiguousarray(poses, np.float64)
+        rho = np.ascontiguousarray(rho, np.float64)
+        if poses.size != 7 * self.n_frames or rho.size != self.n_points:
+            raise ValueError("state shape mismatch")
+        _check(self._L.pba_set_state(self._h, _p(poses), _p(rho)), "pba_set_state")
+
+    def set_state_device(self, poses_ptr: int, rho_ptr: int):
+        _check(self._L.pba_set_state_device(self._h, C.c_void_p(poses_ptr), C.c_void_p(rho_ptr)), "pba_set_state_device")
+
+    # -- evaluation ------------------------------------------------------------------------------
+    def evaluate(self, want_jacobians: bool = True, sync: bool = True):
+        _check(self._L.pba_evaluate(self._h, int(bool(want_jacobians))), "pba_evaluate")
+        if sync:
+            self.synchronize()
+
+    def synchronize(self):
+        _check(self._L.pba_synchronize(self._h), "pba_synchronize")
+
+    def records(self):
+        rec = np.empty((self.n_blocks, self.record), np.float32)
+        valid = np.empty(self.n_blocks, np.uint8)
+        _check(self._L.pba_get_records(self._h, _p(rec), _p(valid)), "pba_get_records")
+        return rec, valid
+
+    def block_costs(self):
+        c = np.empty(self.n_blocks, np.float32)
+        _check(self._L.pba_get_block_costs(self._h, _p(c)), "pba_get_block_costs")
+        return c
+
+    def cost(self):
+        tot, nv = C.c_double(), C.c_int32()
+        _check(self._L.pba_get_cost(self._h, C.byref(tot), C.byref(nv)), "pba_get_cost")
+        return tot.value, nv.value
+
+    def stream(self) -> int:
+        s = C.c_void_p()
+        _check(self._L.pba_get_stream(self._h, C.byref(s)), "pba_get_stream")
+        return s.value or 0
+
+    def set_stream(self, stream_ptr: int):
+        _check(self._L.pba_set_stream(self._h, C.c_void_p(stream_ptr)), "pba_set_stream")
+
+    def device_records(self):
+        r, v, c = C.c_void_p(), C.c_void_p(), C.c_void_p()
+        _check(self._L.pba_device_records(self._h, C.byref(r), C.byref(v), C.byref(c)), "pba_device_records")
+        return r.value, v.value, c.value
+
+    def enable_kernel_timing(self, on: bool = True):
+        _check(self._L.pba_enable_kernel_timing(self._h, int(on)), "pba_enable_kernel_timing")
+
+    def kernel_timing(self):
+        """(summed block-kernel ms, launches) since the last call (HIP events on the engine stream)."""
+        ms, n = C.c_double(), C.c_int32()
+        _check(self._L.pba_get_kernel_timing(self._h, C.byref(ms), C.byref(n)), "pba_get_kernel_timing")
+        return ms.value, n.value
+
+    def close(self):
+        if self._h:
+            self._L.pba_destroy(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+
+def split_record(rec: np.ndarray, R: int):
+    n = rec.shape[0]
+    return rec[:, :R], rec[:, R:7 * R].reshape(n, R, 6), rec[:, 7 * R:13 * R].reshape(n, R, 6), rec[:, 13 * R:14 * R]
