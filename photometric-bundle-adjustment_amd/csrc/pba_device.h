@@ -1,9 +1,15 @@
-// pba_device.h — per-lane arithmetic of the residual/Jacobian kernels (fp32, gfx950).
+// pba_device.h — per-lane arithmetic of the residual/Jacobian kernels (gfx950).
 //
-// Closed-form tangent Jacobians instead of the reference's dual numbers:
-// the reference differentiates BundleAdjustmentReprojectionCostFunctor (reprojection.h:83-112) with
-// Jet<double,23> and maps through LocalParameterizationSE3 (residual_block.cc:136-158); here the
-// composition d r / d δ with T ⊞ δ = T·exp(δ) is written out directly:
+// Precision split.  The sub-pixel position u = π_t(p) decides which bilinear cell is read and the
+// interpolation weights, so everything from the bearing to (u, v) runs in fp64 (unproject, warp,
+// projection) — an fp32 warp puts ~3e-5 px of rounding into u at 752-px coordinates, which shows up as
+// 1e-4-relative Jacobian noise through the image gradient.  The kernels have ALU to spare (memory-bound),
+// so this costs nothing measurable.  The Jacobian chain (∇I · ∂π/∂p · ∂p/∂δ) and the records are fp32.
+//
+// Closed-form tangent Jacobians instead of the reference's dual numbers: the
+// reference differentiates BundleAdjustmentReprojectionCostFunctor (reprojection.h:83-112) with
+// Jet<double,23> and maps through LocalParameterizationSE3 (residual_block.cc:136-158); here
+// d r / d δ with T ⊞ δ = T·exp(δ) is written out directly:
 //
 //   p_t = R_th p_h + t_th ,  p_h = b / ρ                     (geometric, unscaled)
 //   p̃   = R_th b + ρ t_th = ρ p_t                            (photometric, photometric_error.h:155-159)
@@ -20,74 +26,100 @@ namespace pba {
 
 enum : int { CAM_PINHOLE = 0, CAM_DS = 1, CAM_EUCM = 2 };
 
-struct Vec3 { float x, y, z; };
+template <class S>
+struct V3 { S x, y, z; };
+using Vec3 = V3<float>;
+using Vec3d = V3<double>;
 
-__device__ __forceinline__ Vec3 cross(const Vec3& a, const Vec3& b) {
+template <class S>
+__device__ __forceinline__ V3<S> cross(const V3<S>& a, const V3<S>& b) {
   return {a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x};
 }
-__device__ __forceinline__ float dot(const Vec3& a, const Vec3& b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+template <class S>
+__device__ __forceinline__ S dot(const V3<S>& a, const V3<S>& b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+__device__ __forceinline__ Vec3 to_f(const Vec3d& a) { return {(float)a.x, (float)a.y, (float)a.z}; }
 
 // a (row) · R  (R row-major 3×3)
-__device__ __forceinline__ Vec3 row_mul(const Vec3& a, const float* R) {
-  return {a.x * R[0] + a.y * R[3] + a.z * R[6], a.x * R[1] + a.y * R[4] + a.z * R[7],
-          a.x * R[2] + a.y * R[5] + a.z * R[8]};
+template <class S, class T>
+__device__ __forceinline__ V3<S> row_mul(const V3<S>& a, const T* R) {
+  return {a.x * (S)R[0] + a.y * (S)R[3] + a.z * (S)R[6], a.x * (S)R[1] + a.y * (S)R[4] + a.z * (S)R[7],
+          a.x * (S)R[2] + a.y * (S)R[5] + a.z * (S)R[8]};
 }
-__device__ __forceinline__ Vec3 mat_mul(const float* R, const Vec3& b) {
-  return {R[0] * b.x + R[1] * b.y + R[2] * b.z, R[3] * b.x + R[4] * b.y + R[5] * b.z,
-          R[6] * b.x + R[7] * b.y + R[8] * b.z};
+template <class S, class T>
+__device__ __forceinline__ V3<S> mat_mul(const T* R, const V3<S>& b) {
+  return {(S)R[0] * b.x + (S)R[1] * b.y + (S)R[2] * b.z, (S)R[3] * b.x + (S)R[4] * b.y + (S)R[5] * b.z,
+          (S)R[6] * b.x + (S)R[7] * b.y + (S)R[8] * b.z};
 }
 
 // Unit bearing of pixel (u, v) — camera_models.h unproject (pinhole :93-107, EUCM :162-190,
-// DS :247-277) followed by normalize() (reprojection.h:104).
+// DS :247-277) followed by normalize() (reprojection.h:104).  fp64.
 template <int MODEL>
-__device__ __forceinline__ Vec3 unproject(const float* k, float u, float v) {
-  const float mx = (u - k[2]) / k[0];
-  const float my = (v - k[3]) / k[1];
-  Vec3 b;
+__device__ __forceinline__ Vec3d unproject(const double* k, double u, double v) {
+  const double mx = (u - k[2]) / k[0];
+  const double my = (v - k[3]) / k[1];
+  Vec3d b;
   if (MODEL == CAM_PINHOLE) {
-    b = {mx, my, 1.0f};
+    b = {mx, my, 1.0};
   } else if (MODEL == CAM_DS) {
-    const float xi = k[4], al = k[5];
-    const float r2 = mx * mx + my * my;
-    const float mz = (1.0f - al * al * r2) / (al * sqrtf(1.0f - (2.0f * al - 1.0f) * r2) + 1.0f - al);
-    const float fac = (mz * xi + sqrtf(mz * mz + (1.0f - xi * xi) * r2)) / (mz * mz + r2);
+    const double xi = k[4], al = k[5];
+    const double r2 = mx * mx + my * my;
+    const double mz = (1.0 - al * al * r2) / (al * sqrt(1.0 - (2.0 * al - 1.0) * r2) + 1.0 - al);
+    const double fac = (mz * xi + sqrt(mz * mz + (1.0 - xi * xi) * r2)) / (mz * mz + r2);
     b = {fac * mx, fac * my, fac * mz - xi};
   } else {
-    const float al = k[4], be = k[5];
-    const float r2 = mx * mx + my * my;
-    b = {mx, my, (1.0f - be * al * al * r2) / (al * sqrtf(1.0f - (2.0f * al - 1.0f) * be * r2) + (1.0f - al))};
+    const double al = k[4], be = k[5];
+    const double r2 = mx * mx + my * my;
+    b = {mx, my, (1.0 - be * al * al * r2) / (al * sqrt(1.0 - (2.0 * al - 1.0) * be * r2) + (1.0 - al))};
   }
-  const float inv = rsqrtf(b.x * b.x + b.y * b.y + b.z * b.z);
+  const double inv = 1.0 / sqrt(b.x * b.x + b.y * b.y + b.z * b.z);
   return {b.x * inv, b.y * inv, b.z * inv};
 }
 
 // Projection domain on the (possibly scaled) point — identical rule to oracle/oracle.cpp in_domain().
 template <int MODEL>
-__device__ __forceinline__ bool in_domain(const float* k, const Vec3& p) {
-  if (MODEL == CAM_PINHOLE) return p.z > 1e-6f;
+__device__ __forceinline__ bool in_domain(const double* k, const Vec3d& p) {
+  if (MODEL == CAM_PINHOLE) return p.z > 1e-6;
   if (MODEL == CAM_EUCM) {
-    const float al = k[4], be = k[5];
-    const float rr = sqrtf(be * (p.x * p.x + p.y * p.y) + p.z * p.z);
-    const float w = al > 0.5f ? (1.0f - al) / al : al / (1.0f - al);
-    return p.z > -w * rr + 1e-10f;
+    const double al = k[4], be = k[5];
+    const double rr = sqrt(be * (p.x * p.x + p.y * p.y) + p.z * p.z);
+    const double w = al > 0.5 ? (1.0 - al) / al : al / (1.0 - al);
+    return p.z > -w * rr + 1e-10;
   }
-  const float xi = k[4], al = k[5];
-  const float d1 = sqrtf(p.x * p.x + p.y * p.y + p.z * p.z);
-  const float w1 = al <= 0.5f ? al / (1.0f - al) : (1.0f - al) / al;
-  const float w2 = (w1 + xi) / sqrtf(2.0f * w1 * xi + xi * xi + 1.0f);
-  return p.z > -w2 * d1 + 1e-10f;
+  const double xi = k[4], al = k[5];
+  const double d1 = sqrt(p.x * p.x + p.y * p.y + p.z * p.z);
+  const double w1 = al <= 0.5 ? al / (1.0 - al) : (1.0 - al) / al;
+  const double w2 = (w1 + xi) / sqrt(2.0 * w1 * xi + xi * xi + 1.0);
+  return p.z > -w2 * d1 + 1e-10;
 }
 
-// Projection and its 2×3 Jacobian (rows du/dp, dv/dp) — camera_models.h project (pinhole :75-91,
-// EUCM :140-160, DS :226-245).
+// Projection (fp64) — camera_models.h project (pinhole :75-91, EUCM :140-160, DS :226-245).
 template <int MODEL>
-__device__ __forceinline__ void project_jac(const float* k, const Vec3& p, float& u, float& v, Vec3& du, Vec3& dv) {
-  const float fx = k[0], fy = k[1], cx = k[2], cy = k[3];
+__device__ __forceinline__ void project(const double* k, const Vec3d& p, double& u, double& v) {
+  double den;
+  if (MODEL == CAM_PINHOLE) {
+    den = p.z;
+  } else if (MODEL == CAM_DS) {
+    const double xi = k[4], al = k[5];
+    const double d1 = sqrt(p.x * p.x + p.y * p.y + p.z * p.z);
+    const double kk = xi * d1 + p.z;
+    const double d2 = sqrt(p.x * p.x + p.y * p.y + kk * kk);
+    den = al * d2 + (1.0 - al) * kk;
+  } else {
+    const double al = k[4], be = k[5];
+    den = al * sqrt(be * (p.x * p.x + p.y * p.y) + p.z * p.z) + (1.0 - al) * p.z;
+  }
+  const double iden = 1.0 / den;
+  u = k[0] * (p.x * iden) + k[2];
+  v = k[1] * (p.y * iden) + k[3];
+}
+
+// 2×3 projection Jacobian (rows du/dp, dv/dp), fp32.
+template <int MODEL>
+__device__ __forceinline__ void project_jac(const float* k, const Vec3& p, Vec3& du, Vec3& dv) {
+  const float fx = k[0], fy = k[1];
   if (MODEL == CAM_PINHOLE) {
     const float iz = 1.0f / p.z;
     const float mx = p.x * iz, my = p.y * iz;
-    u = fx * mx + cx;
-    v = fy * my + cy;
     du = {fx * iz, 0.0f, -fx * mx * iz};
     dv = {0.0f, fy * iz, -fy * my * iz};
     return;
@@ -113,20 +145,18 @@ __device__ __forceinline__ void project_jac(const float* k, const Vec3& p, float
   }
   const float iden = 1.0f / den;
   const float mx = p.x * iden, my = p.y * iden;
-  u = fx * mx + cx;
-  v = fy * my + cy;
   du = {fx * iden * (1.0f - mx * dden.x), -fx * iden * mx * dden.y, -fx * iden * mx * dden.z};
   dv = {-fy * iden * my * dden.x, fy * iden * (1.0f - my * dden.y), -fy * iden * my * dden.z};
 }
 
 // Bilinear interpolation of a u8 image with Grid2D-style edge clamp; value and gradient from the same
-// four taps.  u = column, v = row.
-__device__ __forceinline__ void bilinear(const uint8_t* __restrict__ img, int W, int H, float u, float v,
+// four taps.  u = column, v = row, positions in fp64, weights in fp32.
+__device__ __forceinline__ void bilinear(const uint8_t* __restrict__ img, int W, int H, double u, double v,
                                          float& I, float& gx, float& gy) {
-  u = fminf(fmaxf(u, -2.0f), (float)W + 1.0f);
-  v = fminf(fmaxf(v, -2.0f), (float)H + 1.0f);
-  const float xf = floorf(u), yf = floorf(v);
-  const float a = u - xf, b = v - yf;
+  u = fmin(fmax(u, -2.0), (double)W + 1.0);
+  v = fmin(fmax(v, -2.0), (double)H + 1.0);
+  const double xf = floor(u), yf = floor(v);
+  const float a = (float)(u - xf), b = (float)(v - yf);
   const int x0 = (int)xf, y0 = (int)yf;
   const int xa = min(max(x0, 0), W - 1), xb = min(max(x0 + 1, 0), W - 1);
   const int ya = min(max(y0, 0), H - 1), yb = min(max(y0 + 1, 0), H - 1);

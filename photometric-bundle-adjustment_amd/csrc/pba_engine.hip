@@ -31,19 +31,30 @@ using namespace pba;
 namespace {
 
 constexpr int kBlockThreads = 256;
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+// Relative pose of one (host, target) keyframe pair, fp64, 128 B (L2-resident: 4k pairs = 512 KB at C4).
+struct alignas(16) PairRec {
+  double R[9];
+  double t[3];
+  int host_cam, target_cam, target, pad0;
+  int pad1[4];
+};
+static_assert(sizeof(PairRec) == 128, "PairRec layout");
 
 struct KernelArgs {
   const uint8_t* images;
   int width, height;
   long long frame_stride;
-  const float* intr;             // 8 floats per camera
+  const float* intr;             // 8 floats per camera (Jacobian chain)
+  const double* intr_d;          // 8 doubles per camera (warp / projection)
   const int* block_point;
   const int* block_pair;
-  const float4* pair_pose;       // 4 float4 per pair: R(9) t(3) host_cam target_cam target_frame pad
-  const float2* u_ref;           // per point
+  const PairRec* pairs;
+  const double2* u_ref;          // per point
   const float* host_int;         // P per point
   const double* rho;             // per point (state)
-  const float2* u_obs;           // per block (geometric)
+  const double2* u_obs;          // per block (geometric)
   float* out;                    // records
   float* cost;                   // per block
   uint8_t* valid;                // per block
@@ -68,11 +79,11 @@ __device__ __forceinline__ float huber_cost(float s, float a) {
 }
 
 // ------------------------------------------------------------------------------------------------
-// Pair kernel: relative poses in fp64 (avoids fp32 cancellation in t_w_h − t_w_t for long trajectories)
+// Pair kernel: relative poses in fp64 (q_th = q_wt*·q_wh, t_th = q_wt*·(t_wh − t_wt))
 // ------------------------------------------------------------------------------------------------
 __global__ void pair_kernel(const double* __restrict__ poses, const int* __restrict__ pair_host,
                             const int* __restrict__ pair_target, const int* __restrict__ frame_cam,
-                            float4* __restrict__ pair_pose, int n_pairs) {
+                            PairRec* __restrict__ pairs, int n_pairs) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n_pairs) return;
   const int h = pair_host[i], t = pair_target[i];
@@ -89,38 +100,23 @@ __global__ void pair_kernel(const double* __restrict__ poses, const int* __restr
   const double tx = 2 * qx, ty = 2 * qy, tz = 2 * qz;
   const double twx = tx * qw, twy = ty * qw, twz = tz * qw, txx = tx * qx, txy = ty * qx, txz = tz * qx;
   const double tyy = ty * qy, tyz = tz * qy, tzz = tz * qz;
-  const double R[9] = {1 - (tyy + tzz), txy - twz, txz + twy, txy + twz, 1 - (txx + tzz), tyz - twx,
-                       txz - twy, tyz + twx, 1 - (txx + tyy)};
+  PairRec r;
+  r.R[0] = 1 - (tyy + tzz); r.R[1] = txy - twz;       r.R[2] = txz + twy;
+  r.R[3] = txy + twz;       r.R[4] = 1 - (txx + tzz); r.R[5] = tyz - twx;
+  r.R[6] = txz - twy;       r.R[7] = tyz + twx;       r.R[8] = 1 - (txx + tyy);
   // t_th = q_wt* · (t_wh − t_wt) (photometric_error.h:153), rotation as so3.hpp:367-370
   const double d0 = H[4] - T[4], d1 = H[5] - T[5], d2 = H[6] - T[6];
   double u0 = ay * d2 - az * d1, u1 = az * d0 - ax * d2, u2 = ax * d1 - ay * d0;
   u0 += u0; u1 += u1; u2 += u2;
-  const double t0 = d0 + aw * u0 + (ay * u2 - az * u1);
-  const double t1 = d1 + aw * u1 + (az * u0 - ax * u2);
-  const double t2 = d2 + aw * u2 + (ax * u1 - ay * u0);
-  float4* o = pair_pose + 4 * i;
-  o[0] = make_float4((float)R[0], (float)R[1], (float)R[2], (float)R[3]);
-  o[1] = make_float4((float)R[4], (float)R[5], (float)R[6], (float)R[7]);
-  o[2] = make_float4((float)R[8], (float)t0, (float)t1, (float)t2);
-  o[3] = make_float4(__int_as_float(frame_cam[h]), __int_as_float(frame_cam[t]), __int_as_float(t), 0.0f);
-}
-
-struct PairPose {
-  float R[9];
-  Vec3 t;
-  int host_cam, target_cam, target;
-};
-
-__device__ __forceinline__ PairPose load_pair(const float4* __restrict__ pp, int pair) {
-  const float4 a = pp[4 * pair + 0], b = pp[4 * pair + 1], c = pp[4 * pair + 2], d = pp[4 * pair + 3];
-  PairPose r;
-  r.R[0] = a.x; r.R[1] = a.y; r.R[2] = a.z; r.R[3] = a.w;
-  r.R[4] = b.x; r.R[5] = b.y; r.R[6] = b.z; r.R[7] = b.w; r.R[8] = c.x;
-  r.t = {c.y, c.z, c.w};
-  r.host_cam = __float_as_int(d.x);
-  r.target_cam = __float_as_int(d.y);
-  r.target = __float_as_int(d.z);
-  return r;
+  r.t[0] = d0 + aw * u0 + (ay * u2 - az * u1);
+  r.t[1] = d1 + aw * u1 + (az * u0 - ax * u2);
+  r.t[2] = d2 + aw * u2 + (ax * u1 - ay * u0);
+  r.host_cam = frame_cam[h];
+  r.target_cam = frame_cam[t];
+  r.target = t;
+  r.pad0 = 0;
+  r.pad1[0] = r.pad1[1] = r.pad1[2] = r.pad1[3] = 0;
+  pairs[i] = r;
 }
 
 // Sum / AND over the LPB lanes of one block (LPB | 64, groups are aligned lane ranges).
@@ -138,75 +134,99 @@ __device__ __forceinline__ int group_and(int v) {
 }
 
 // ------------------------------------------------------------------------------------------------
-// Photometric block kernel: lane = (block, pixel k)
+// Photometric block kernel: lane = (block, pixel k); a workgroup = 256/LPB consecutive blocks whose
+// records are staged in LDS and leave as one contiguous, 16-B-per-lane, non-temporal store stream.
 // ------------------------------------------------------------------------------------------------
 template <int MODEL, int LPB, bool JAC>
 __global__ __launch_bounds__(kBlockThreads) void photometric_block_kernel(const KernelArgs a) {
-  const int gtid = logical_tile() * kBlockThreads + threadIdx.x;
-  const int blk = gtid / LPB;
-  const int k = gtid % LPB;
-  if (blk >= a.n_blocks) return;  // a block's LPB lanes leave together
+  constexpr int BPW = kBlockThreads / LPB;  // blocks per workgroup
+  __shared__ __attribute__((aligned(16))) float stage[JAC ? BPW * 14 * LPB : 4];
   const int P = a.P;
-  const bool act = k < P;
+  const int rec_f = 14 * P;
+  const int blk0 = logical_tile() * BPW;
+  const int lb = threadIdx.x / LPB;
+  const int k = threadIdx.x % LPB;
+  const int blk = blk0 + lb;
+  const bool live = blk < a.n_blocks;  // a block's LPB lanes agree
+  const bool act = live && k < P;
 
-  const int pt = a.block_point[blk];
-  const PairPose pp = load_pair(a.pair_pose, a.block_pair[blk]);
-  const float* kh = a.intr + 8 * pp.host_cam;
-  const float* kt = a.intr + 8 * pp.target_cam;
-  const float2 ur = a.u_ref[pt];
-  const float rho = (float)a.rho[pt];
-  const int kk = act ? k : 0;
-  const float Ih = a.host_int[(long long)pt * P + kk];
-
-  // warp: p̃ = R_th b_k + ρ t_th  (photometric_error.h:158-159)
-  const Vec3 b = unproject<MODEL>(kh, ur.x + a.pattern[2 * kk], ur.y + a.pattern[2 * kk + 1]);
-  const Vec3 Rb = mat_mul(pp.R, b);
-  const Vec3 p = {Rb.x + rho * pp.t.x, Rb.y + rho * pp.t.y, Rb.z + rho * pp.t.z};
-  const bool dom = in_domain<MODEL>(kt, p);
-  float u, v;
-  Vec3 du, dv;
-  project_jac<MODEL>(kt, p, u, v, du, dv);
-  float I = 0.0f, gx = 0.0f, gy = 0.0f;
-  if (dom) bilinear(a.images + pp.target * a.frame_stride, a.width, a.height, u, v, I, gx, gy);
-  const float r = I - Ih;  // photometric_error.h:179
-
+  float r = 0.0f, jr = 0.0f;
+  Vec3 jh_v = {0, 0, 0}, jh_w = {0, 0, 0}, jt_v = {0, 0, 0}, jt_w = {0, 0, 0};
+  int ok = 1;
+  if (live) {
+    const int pt = a.block_point[blk];
+    const PairRec& pp = a.pairs[a.block_pair[blk]];
+    const double* khd = a.intr_d + 8 * pp.host_cam;
+    const double* ktd = a.intr_d + 8 * pp.target_cam;
+    const double2 ur = a.u_ref[pt];
+    const double rho = a.rho[pt];
+    const int kk = k < P ? k : 0;
+    const float Ih = a.host_int[(long long)pt * P + kk];
+    // warp in fp64: p̃ = R_th b_k + ρ t_th  (photometric_error.h:158-159)
+    const Vec3d b = unproject<MODEL>(khd, ur.x + (double)a.pattern[2 * kk], ur.y + (double)a.pattern[2 * kk + 1]);
+    const Vec3d Rb = mat_mul(pp.R, b);
+    const Vec3d p = {Rb.x + rho * pp.t[0], Rb.y + rho * pp.t[1], Rb.z + rho * pp.t[2]};
+    const bool dom = in_domain<MODEL>(ktd, p);
+    float I = 0.0f, gx = 0.0f, gy = 0.0f;
+    if (dom) {
+      double u, v;
+      project<MODEL>(ktd, p, u, v);
+      bilinear(a.images + pp.target * a.frame_stride, a.width, a.height, u, v, I, gx, gy);
+    }
+    r = I - Ih;  // photometric_error.h:179
+    ok = (dom && isfinite(r)) || !(k < P);
+    if (JAC && dom) {
+      // q = ∇I · ∂π/∂p̃ (1×3), then the chain of the header comment (fp32)
+      const Vec3 pf = to_f(p), bf = to_f(b);
+      Vec3 du, dv;
+      project_jac<MODEL>(a.intr + 8 * pp.target_cam, pf, du, dv);
+      const Vec3 q = {gx * du.x + gy * dv.x, gx * du.y + gy * dv.y, gx * du.z + gy * dv.z};
+      const Vec3 qR = row_mul(q, pp.R);
+      const float rf = (float)rho;
+      jh_v = {rf * qR.x, rf * qR.y, rf * qR.z};
+      jh_w = cross(bf, qR);  // −(qR)×b
+      jt_v = {-rf * q.x, -rf * q.y, -rf * q.z};
+      jt_w = cross(q, pf);   // q·[p̃]×
+      jr = q.x * (float)pp.t[0] + q.y * (float)pp.t[1] + q.z * (float)pp.t[2];
+    }
+  }
   // per-block validity and ‖r‖² (wave shuffles over the block's lanes)
-  const int ok = group_and<LPB>((dom && isfinite(r)) || !act);
+  ok = group_and<LPB>(ok);
   const float s = group_sum<LPB>(act ? r * r : 0.0f);
-  float* rec = a.out + (long long)blk * 14 * P;
-  if (k == 0) {
+  if (live && k == 0) {
     a.valid[blk] = (uint8_t)ok;
     a.cost[blk] = ok ? huber_cost(s, a.huber) : 0.0f;
   }
-  if (!act) return;
   if (!ok) {
-    rec[k] = 0.0f;
-    if (JAC) {
-      float2* jh = reinterpret_cast<float2*>(rec + P + 6 * k);
-      float2* jt = reinterpret_cast<float2*>(rec + 7 * P + 6 * k);
-      jh[0] = jh[1] = jh[2] = make_float2(0.f, 0.f);
-      jt[0] = jt[1] = jt[2] = make_float2(0.f, 0.f);
-      rec[13 * P + k] = 0.0f;
-    }
+    r = jr = 0.0f;
+    jh_v = jh_w = jt_v = jt_w = {0, 0, 0};
+  }
+  if (!JAC) {
+    if (act) a.out[(long long)blk * rec_f + k] = r;
     return;
   }
-  rec[k] = r;
-  if (!JAC) return;
-  // q = ∇I · ∂π/∂p̃  (1×3), then the chain (pba_device.h header)
-  const Vec3 q = {gx * du.x + gy * dv.x, gx * du.y + gy * dv.y, gx * du.z + gy * dv.z};
-  const Vec3 qR = row_mul(q, pp.R);
-  const Vec3 wh = cross(b, qR);   // −(qR)×b
-  const Vec3 wt = cross(q, p);    // q·[p̃]×
-  const float jr = dot(q, pp.t);
-  float2* jh = reinterpret_cast<float2*>(rec + P + 6 * k);
-  float2* jt = reinterpret_cast<float2*>(rec + 7 * P + 6 * k);
-  jh[0] = make_float2(rho * qR.x, rho * qR.y);
-  jh[1] = make_float2(rho * qR.z, wh.x);
-  jh[2] = make_float2(wh.y, wh.z);
-  jt[0] = make_float2(-rho * q.x, -rho * q.y);
-  jt[1] = make_float2(-rho * q.z, wt.x);
-  jt[2] = make_float2(wt.y, wt.z);
-  rec[13 * P + k] = jr;
+  // stage the record row of pixel k: r | J_host row | J_target row | J_rho
+  if (k < P) {
+    float* s_rec = stage + lb * rec_f;
+    s_rec[k] = r;
+    float* h = s_rec + P + 6 * k;
+    h[0] = jh_v.x; h[1] = jh_v.y; h[2] = jh_v.z; h[3] = jh_w.x; h[4] = jh_w.y; h[5] = jh_w.z;
+    float* t = s_rec + 7 * P + 6 * k;
+    t[0] = jt_v.x; t[1] = jt_v.y; t[2] = jt_v.z; t[3] = jt_w.x; t[4] = jt_w.y; t[5] = jt_w.z;
+    s_rec[13 * P + k] = jr;
+  }
+  __syncthreads();
+  const int nblk = min(BPW, a.n_blocks - blk0);
+  if (nblk <= 0) return;
+  const int nf = nblk * rec_f;
+  float* dst = a.out + (long long)blk0 * rec_f;
+  if ((rec_f & 3) == 0) {  // 16-B aligned slab: float4 non-temporal stream
+    const f32x4* src4 = reinterpret_cast<const f32x4*>(stage);
+    f32x4* dst4 = reinterpret_cast<f32x4*>(dst);
+    for (int i = threadIdx.x; i < (nf >> 2); i += kBlockThreads) __builtin_nontemporal_store(src4[i], dst4 + i);
+  } else {
+    for (int i = threadIdx.x; i < nf; i += kBlockThreads) __builtin_nontemporal_store(stage[i], dst + i);
+  }
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -217,40 +237,44 @@ __global__ __launch_bounds__(kBlockThreads) void geometric_block_kernel(const Ke
   const int blk = logical_tile() * kBlockThreads + threadIdx.x;
   if (blk >= a.n_blocks) return;
   const int pt = a.block_point[blk];
-  const PairPose pp = load_pair(a.pair_pose, a.block_pair[blk]);
-  const float* kh = a.intr + 8 * pp.host_cam;
-  const float* kt = a.intr + 8 * pp.target_cam;
-  const float2 ur = a.u_ref[pt];
-  const float2 uo = a.u_obs[blk];
-  const float rho = (float)a.rho[pt];
-  const float irho = 1.0f / rho;
-  const Vec3 b = unproject<MODEL>(kh, ur.x, ur.y);
-  const Vec3 ph = {b.x * irho, b.y * irho, b.z * irho};
-  const Vec3 Rp = mat_mul(pp.R, ph);
-  const Vec3 p = {Rp.x + pp.t.x, Rp.y + pp.t.y, Rp.z + pp.t.z};
-  float u, v;
-  Vec3 du, dv;
-  project_jac<MODEL>(kt, p, u, v, du, dv);
-  const float r0 = uo.x - u, r1 = uo.y - v;
-  float4* rec = reinterpret_cast<float4*>(a.out + (long long)blk * 28);
+  const PairRec& pp = a.pairs[a.block_pair[blk]];
+  const double* khd = a.intr_d + 8 * pp.host_cam;
+  const double* ktd = a.intr_d + 8 * pp.target_cam;
+  const double2 ur = a.u_ref[pt];
+  const double2 uo = a.u_obs[blk];
+  const double rho = a.rho[pt];
+  const double irho = 1.0 / rho;
+  // p = T_w_t⁻¹ · T_w_h · (b / ρ) in fp64
+  const Vec3d b = unproject<MODEL>(khd, ur.x, ur.y);
+  const Vec3d ph = {b.x * irho, b.y * irho, b.z * irho};
+  const Vec3d Rp = mat_mul(pp.R, ph);
+  const Vec3d p = {Rp.x + pp.t[0], Rp.y + pp.t[1], Rp.z + pp.t[2]};
+  double u, v;
+  project<MODEL>(ktd, p, u, v);
+  const float r0 = (float)(uo.x - u), r1 = (float)(uo.y - v);
+  f32x4* rec = reinterpret_cast<f32x4*>(a.out + (long long)blk * 28);
   float J[28];
   J[0] = r0;
   J[1] = r1;
   bool ok = isfinite(r0) && isfinite(r1);
   if (JAC) {
-    const Vec3 Rb = mat_mul(pp.R, b);
+    const Vec3 pf = to_f(p), phf = to_f(ph);
+    const Vec3 Rbf = to_f(mat_mul(pp.R, b));
+    const float irf = (float)irho;
+    Vec3 du, dv;
+    project_jac<MODEL>(a.intr + 8 * pp.target_cam, pf, du, dv);
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const Vec3 d = i == 0 ? du : dv;
       const Vec3 g = {-d.x, -d.y, -d.z};  // ∂r/∂p = −∂π/∂p
       const Vec3 gR = row_mul(g, pp.R);
-      const Vec3 wh = cross(ph, gR);
-      const Vec3 wt = cross(g, p);
+      const Vec3 wh = cross(phf, gR);
+      const Vec3 wt = cross(g, pf);
       float* jh = J + 2 + 6 * i;
       float* jt = J + 14 + 6 * i;
       jh[0] = gR.x; jh[1] = gR.y; jh[2] = gR.z; jh[3] = wh.x; jh[4] = wh.y; jh[5] = wh.z;
       jt[0] = -g.x; jt[1] = -g.y; jt[2] = -g.z; jt[3] = wt.x; jt[4] = wt.y; jt[5] = wt.z;
-      J[26 + i] = -dot(g, Rb) * irho * irho;
+      J[26 + i] = -dot(g, Rbf) * irf * irf;
     }
 #pragma unroll
     for (int i = 2; i < 28; ++i) ok = ok && isfinite(J[i]);
@@ -263,7 +287,8 @@ __global__ __launch_bounds__(kBlockThreads) void geometric_block_kernel(const Ke
   }
   if (JAC) {
 #pragma unroll
-    for (int i = 0; i < 7; ++i) rec[i] = make_float4(J[4 * i], J[4 * i + 1], J[4 * i + 2], J[4 * i + 3]);
+    for (int i = 0; i < 7; ++i)
+      __builtin_nontemporal_store(f32x4{J[4 * i], J[4 * i + 1], J[4 * i + 2], J[4 * i + 3]}, rec + i);
   } else {
     reinterpret_cast<float2*>(rec)[0] = make_float2(J[0], J[1]);
   }
@@ -317,14 +342,15 @@ struct pba_engine {
   std::vector<int> frame_cam_h, point_host_h;
   std::vector<float> pattern_h;
   DevBuf<float> intr;
+  DevBuf<double> intr_d;
   DevBuf<int> frame_cam;
   DevBuf<uint8_t> images;
-  DevBuf<float2> u_ref;
+  DevBuf<double2> u_ref;
   DevBuf<float> host_int;
   DevBuf<int> block_point, block_pair;
-  DevBuf<float2> u_obs;
+  DevBuf<double2> u_obs;
   DevBuf<int> pair_host, pair_target;
-  DevBuf<float4> pair_pose;
+  DevBuf<PairRec> pairs;
   DevBuf<double> poses, rho;
   DevBuf<float> out, cost;
   DevBuf<uint8_t> valid;
@@ -411,9 +437,9 @@ int pba_destroy(pba_engine* e) {
   if (!e) return PBA_OK;
   (void)hipSetDevice(e->opt.device);
   if (e->stream) (void)hipStreamSynchronize(e->stream);
-  e->intr.release(); e->frame_cam.release(); e->images.release(); e->u_ref.release(); e->host_int.release();
+  e->intr.release(); e->intr_d.release(); e->frame_cam.release(); e->images.release(); e->u_ref.release(); e->host_int.release();
   e->block_point.release(); e->block_pair.release(); e->u_obs.release(); e->pair_host.release();
-  e->pair_target.release(); e->pair_pose.release(); e->poses.release(); e->rho.release(); e->out.release();
+  e->pair_target.release(); e->pairs.release(); e->poses.release(); e->rho.release(); e->out.release();
   e->cost.release(); e->valid.release();
   for (hipEvent_t ev : e->ev_pool) (void)hipEventDestroy(ev);
   if (e->own_stream) (void)hipStreamDestroy(e->own_stream);
@@ -441,7 +467,9 @@ int pba_set_cameras(pba_engine* e, int32_t n_cams, const double* intrinsics) {
   for (int c = 0; c < n_cams; ++c)
     if (!(f[8 * c] != 0.0f && f[8 * c + 1] != 0.0f)) return fail(PBA_ERR_INVALID_ARGUMENT, "zero focal length");
   PBA_HIP(e->intr.resize(f.size()));
+  PBA_HIP(e->intr_d.resize(f.size()));
   PBA_HIP(hipMemcpyAsync(e->intr.p, f.data(), f.size() * sizeof(float), hipMemcpyHostToDevice, e->stream));
+  PBA_HIP(hipMemcpyAsync(e->intr_d.p, intrinsics, f.size() * sizeof(double), hipMemcpyHostToDevice, e->stream));
   PBA_HIP(hipStreamSynchronize(e->stream));
   e->n_cams = n_cams;
   return PBA_OK;
@@ -502,10 +530,8 @@ int pba_set_points(pba_engine* e, int32_t n_points, const int32_t* host_frame, c
   for (int i = 0; i < n_points; ++i)
     if (host_frame[i] < 0 || host_frame[i] >= e->n_frames) return fail(PBA_ERR_INVALID_ARGUMENT, "host frame out of range");
   if (int rc = check_device(e)) return rc;
-  std::vector<float2> ur(n_points);
-  for (int i = 0; i < n_points; ++i) ur[i] = make_float2((float)u_ref[2 * i], (float)u_ref[2 * i + 1]);
   PBA_HIP(e->u_ref.resize(n_points));
-  PBA_HIP(hipMemcpyAsync(e->u_ref.p, ur.data(), n_points * sizeof(float2), hipMemcpyHostToDevice, e->stream));
+  PBA_HIP(hipMemcpyAsync(e->u_ref.p, u_ref, n_points * sizeof(double2), hipMemcpyHostToDevice, e->stream));
   if (photometric) {
     PBA_HIP(e->host_int.resize((size_t)n_points * e->P));
     PBA_HIP(hipMemcpyAsync(e->host_int.p, host_intensity, (size_t)n_points * e->P * sizeof(float),
@@ -556,17 +582,14 @@ int pba_set_blocks(pba_engine* e, int32_t n_blocks, const int32_t* block_point, 
   PBA_HIP(e->block_pair.resize(n_blocks));
   PBA_HIP(e->pair_host.resize(np));
   PBA_HIP(e->pair_target.resize(np));
-  PBA_HIP(e->pair_pose.resize(4 * (size_t)np));
+  PBA_HIP(e->pairs.resize((size_t)np));
   PBA_HIP(hipMemcpyAsync(e->block_point.p, block_point, n_blocks * sizeof(int), hipMemcpyHostToDevice, e->stream));
   PBA_HIP(hipMemcpyAsync(e->block_pair.p, pair_of.data(), n_blocks * sizeof(int), hipMemcpyHostToDevice, e->stream));
   PBA_HIP(hipMemcpyAsync(e->pair_host.p, ph.data(), np * sizeof(int), hipMemcpyHostToDevice, e->stream));
   PBA_HIP(hipMemcpyAsync(e->pair_target.p, pt.data(), np * sizeof(int), hipMemcpyHostToDevice, e->stream));
   if (geometric) {
-    std::vector<float2> uo(n_blocks);
-    for (int b = 0; b < n_blocks; ++b) uo[b] = make_float2((float)u_obs[2 * b], (float)u_obs[2 * b + 1]);
     PBA_HIP(e->u_obs.resize(n_blocks));
-    PBA_HIP(hipMemcpyAsync(e->u_obs.p, uo.data(), n_blocks * sizeof(float2), hipMemcpyHostToDevice, e->stream));
-    PBA_HIP(hipStreamSynchronize(e->stream));
+    PBA_HIP(hipMemcpyAsync(e->u_obs.p, u_obs, n_blocks * sizeof(double2), hipMemcpyHostToDevice, e->stream));
   }
   PBA_HIP(e->out.resize((size_t)n_blocks * rec));
   PBA_HIP(e->cost.resize(n_blocks));
@@ -608,16 +631,17 @@ int pba_evaluate(pba_engine* e, int32_t want_jacobians) {
   if (photometric && (!e->have_images || e->P <= 0)) return fail(PBA_ERR_NOT_READY, "images/pattern missing");
   if (int rc = check_device(e)) return rc;
   pair_kernel<<<(e->n_pairs + 255) / 256, 256, 0, e->stream>>>(e->poses.p, e->pair_host.p, e->pair_target.p,
-                                                               e->frame_cam.p, e->pair_pose.p, e->n_pairs);
+                                                               e->frame_cam.p, e->pairs.p, e->n_pairs);
   KernelArgs ka{};
   ka.images = e->images.p;
   ka.width = e->width;
   ka.height = e->height;
   ka.frame_stride = (long long)e->width * e->height;
   ka.intr = e->intr.p;
+  ka.intr_d = e->intr_d.p;
   ka.block_point = e->block_point.p;
   ka.block_pair = e->block_pair.p;
-  ka.pair_pose = e->pair_pose.p;
+  ka.pairs = e->pairs.p;
   ka.u_ref = e->u_ref.p;
   ka.host_int = e->host_int.p;
   ka.rho = e->rho.p;
