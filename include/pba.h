@@ -127,6 +127,50 @@ int pba_device_records(pba_engine* engine, float** d_records, uint8_t** d_valid,
 int pba_enable_kernel_timing(pba_engine* engine, int32_t enable);
 int pba_get_kernel_timing(pba_engine* engine, double* total_ms, int32_t* launches);
 
+/* On-device Gauss-Newton / Levenberg-Marquardt --------------------------------
+ * Replaces the solver side of ceres::Solve for this problem (map_utils.h:378-383: LM, SPARSE_SCHUR): the
+ * normal equations JᵀJ / Jᵀr are accumulated on the device with the Huber corrector of
+ * residual_block.cc:161-196, the inverse distances are eliminated (Schur complement; the <2,1,6>
+ * structure of schur_complement_solver.cc:138-146), and the reduced camera system is factorised on the
+ * device (block-skyline Cholesky, fp64).  Damping follows levenberg_marquardt_strategy.cc: (H + λ·D)δ = −g
+ * with D = diag(JᵀJ) clamped to [1e-6, 1e32], λ = 1/trust-region radius. */
+#define PBA_TERMINATION_CONVERGENCE 0     /* |Δcost| ≤ function_tolerance · cost */
+#define PBA_TERMINATION_MAX_ITERATIONS 1
+#define PBA_TERMINATION_FAILURE 2         /* trust region collapsed */
+
+typedef struct pba_solver_options {
+  int32_t max_iterations;               /* BundleAdjustmentOptions::max_num_iterations (20, map_utils.h:318) */
+  int32_t pad_;
+  double initial_trust_region_radius;   /* Ceres default 1e4 */
+  double function_tolerance;            /* Ceres default 1e-6 */
+  double parameter_tolerance;           /* reserved (Ceres default 1e-8) */
+  double min_relative_decrease;         /* Ceres default 1e-3 */
+} pba_solver_options;
+
+typedef struct pba_solver_summary {
+  int32_t iterations, successful_steps, unsuccessful_steps, termination;
+  double initial_cost, final_cost;      /* Σ ½ρ(‖r‖²) */
+  double total_ms, linearize_ms, solve_ms, cost_ms;  /* host wall-clock */
+} pba_solver_summary;
+
+/* constant parameter blocks (Problem::SetParameterBlockConstant, map_utils.h:334-336) */
+int pba_set_fixed_frames(pba_engine* engine, int32_t n, const int32_t* frames);
+/* Jacobian evaluation at the current state + normal-equation pieces; cost may be NULL */
+int pba_gn_linearize(pba_engine* engine, double* cost);
+/* Schur complement for damping lambda, reduced-system solve, candidate state; solver_status ≠ 0 when the
+ * reduced system was not positive definite (the candidate is then not formed) */
+int pba_gn_step(pba_engine* engine, double lambda, double* model_decrease, int32_t* solver_status);
+int pba_gn_candidate_cost(pba_engine* engine, double* cost);
+int pba_gn_accept(pba_engine* engine);   /* state ← candidate */
+/* full LM loop (trust_region_minimizer.cc semantics); options may be NULL (Ceres defaults, 20 iterations) */
+int pba_solve(pba_engine* engine, const pba_solver_options* options, pba_solver_summary* summary);
+/* read back the state (7·n_frames poses, n_points inverse distances) */
+int pba_get_state(pba_engine* engine, double* poses, double* inv_dist);
+/* testing/inspection: reduced camera system as a dense (6·n_frames)² matrix and its right-hand side g
+ * (the solve is S δ = −g), and the last step (δ poses 6·n_frames, δρ n_points) */
+int pba_gn_get_reduced_system(pba_engine* engine, double* S_dense, double* g);
+int pba_gn_get_step(pba_engine* engine, double* d_poses, double* d_inv_dist);
+
 #ifdef __cplusplus
 }
 #endif

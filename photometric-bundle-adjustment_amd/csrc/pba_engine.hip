@@ -23,60 +23,18 @@
 #include <string>
 #include <vector>
 
-#include "pba.h"
-#include "pba_device.h"
+#include "pba_internal.h"
 
 using namespace pba;
+using namespace pba::detail;
+
+namespace pba {
+namespace detail {
+thread_local std::string g_last_error;
+}  // namespace detail
+}  // namespace pba
 
 namespace {
-
-constexpr int kBlockThreads = 256;
-typedef float f32x4 __attribute__((ext_vector_type(4)));
-
-// Relative pose of one (host, target) keyframe pair, fp64, 128 B (L2-resident: 4k pairs = 512 KB at C4).
-struct alignas(16) PairRec {
-  double R[9];
-  double t[3];
-  int host_cam, target_cam, target, pad0;
-  int pad1[4];
-};
-static_assert(sizeof(PairRec) == 128, "PairRec layout");
-
-struct KernelArgs {
-  const uint8_t* images;
-  int width, height;
-  long long frame_stride;
-  const float* intr;             // 8 floats per camera (Jacobian chain)
-  const double* intr_d;          // 8 doubles per camera (warp / projection)
-  const int* block_point;
-  const int* block_pair;
-  const PairRec* pairs;
-  const double2* u_ref;          // per point
-  const float* host_int;         // P per point
-  const double* rho;             // per point (state)
-  const double2* u_obs;          // per block (geometric)
-  float* out;                    // records
-  float* cost;                   // per block
-  uint8_t* valid;                // per block
-  int n_blocks;
-  int P;
-  float huber;
-  float pattern[2 * PBA_MAX_PATTERN];
-};
-
-// XCD-aware tile order: consecutive logical tiles (→ neighbouring host keyframes → shared target images)
-// land on the same XCD's L2 (blocks are dealt round-robin over the 8 XCDs; speed only, never correctness).
-__device__ __forceinline__ int logical_tile() {
-  const int n = gridDim.x, b = blockIdx.x;
-  const int xcd = b & 7, slot = b >> 3;
-  const int q = n >> 3, rem = n & 7;
-  return xcd * q + min(xcd, rem) + slot;
-}
-
-__device__ __forceinline__ float huber_cost(float s, float a) {
-  if (a <= 0.0f || s <= a * a) return 0.5f * s;  // loss_function.cc:48-62, cost = ½ρ(s)
-  return 0.5f * (2.0f * a * sqrtf(s) - a * a);
-}
 
 // ------------------------------------------------------------------------------------------------
 // Pair kernel: relative poses in fp64 (q_th = q_wt*·q_wh, t_th = q_wt*·(t_wh − t_wt))
@@ -114,32 +72,20 @@ __global__ void pair_kernel(const double* __restrict__ poses, const int* __restr
   r.host_cam = frame_cam[h];
   r.target_cam = frame_cam[t];
   r.target = t;
-  r.pad0 = 0;
+  r.host = h;
   r.pad1[0] = r.pad1[1] = r.pad1[2] = r.pad1[3] = 0;
   pairs[i] = r;
-}
-
-// Sum / AND over the LPB lanes of one block (LPB | 64, groups are aligned lane ranges).
-template <int LPB>
-__device__ __forceinline__ float group_sum(float v) {
-#pragma unroll
-  for (int m = LPB / 2; m >= 1; m >>= 1) v += __shfl_xor(v, m, 64);
-  return v;
-}
-template <int LPB>
-__device__ __forceinline__ int group_and(int v) {
-#pragma unroll
-  for (int m = LPB / 2; m >= 1; m >>= 1) v &= __shfl_xor(v, m, 64);
-  return v;
 }
 
 // ------------------------------------------------------------------------------------------------
 // Photometric block kernel: lane = (block, pixel k); a workgroup = 256/LPB consecutive blocks whose
 // records are staged in LDS and leave as one contiguous, 16-B-per-lane, non-temporal store stream.
+// MODE 0: residual part of the records only; 1: full records; 2: per-block cost/validity only.
 // ------------------------------------------------------------------------------------------------
-template <int MODEL, int LPB, bool JAC>
+template <int MODEL, int LPB, int MODE>
 __global__ __launch_bounds__(kBlockThreads) void photometric_block_kernel(const KernelArgs a) {
   constexpr int BPW = kBlockThreads / LPB;  // blocks per workgroup
+  constexpr bool JAC = MODE == 1;
   __shared__ __attribute__((aligned(16))) float stage[JAC ? BPW * 14 * LPB : 4];
   const int P = a.P;
   const int rec_f = 14 * P;
@@ -150,70 +96,30 @@ __global__ __launch_bounds__(kBlockThreads) void photometric_block_kernel(const 
   const bool live = blk < a.n_blocks;  // a block's LPB lanes agree
   const bool act = live && k < P;
 
-  float r = 0.0f, jr = 0.0f;
-  Vec3 jh_v = {0, 0, 0}, jh_w = {0, 0, 0}, jt_v = {0, 0, 0}, jt_w = {0, 0, 0};
-  int ok = 1;
-  if (live) {
-    const int pt = a.block_point[blk];
-    const PairRec& pp = a.pairs[a.block_pair[blk]];
-    const double* khd = a.intr_d + 8 * pp.host_cam;
-    const double* ktd = a.intr_d + 8 * pp.target_cam;
-    const double2 ur = a.u_ref[pt];
-    const double rho = a.rho[pt];
-    const int kk = k < P ? k : 0;
-    const float Ih = a.host_int[(long long)pt * P + kk];
-    // warp in fp64: p̃ = R_th b_k + ρ t_th  (photometric_error.h:158-159)
-    const Vec3d b = unproject<MODEL>(khd, ur.x + (double)a.pattern[2 * kk], ur.y + (double)a.pattern[2 * kk + 1]);
-    const Vec3d Rb = mat_mul(pp.R, b);
-    const Vec3d p = {Rb.x + rho * pp.t[0], Rb.y + rho * pp.t[1], Rb.z + rho * pp.t[2]};
-    const bool dom = in_domain<MODEL>(ktd, p);
-    float I = 0.0f, gx = 0.0f, gy = 0.0f;
-    if (dom) {
-      double u, v;
-      project<MODEL>(ktd, p, u, v);
-      bilinear(a.images + pp.target * a.frame_stride, a.width, a.height, u, v, I, gx, gy);
-    }
-    r = I - Ih;  // photometric_error.h:179
-    ok = (dom && isfinite(r)) || !(k < P);
-    if (JAC && dom) {
-      // q = ∇I · ∂π/∂p̃ (1×3), then the chain of the header comment (fp32)
-      const Vec3 pf = to_f(p), bf = to_f(b);
-      Vec3 du, dv;
-      project_jac<MODEL>(a.intr + 8 * pp.target_cam, pf, du, dv);
-      const Vec3 q = {gx * du.x + gy * dv.x, gx * du.y + gy * dv.y, gx * du.z + gy * dv.z};
-      const Vec3 qR = row_mul(q, pp.R);
-      const float rf = (float)rho;
-      jh_v = {rf * qR.x, rf * qR.y, rf * qR.z};
-      jh_w = cross(bf, qR);  // −(qR)×b
-      jt_v = {-rf * q.x, -rf * q.y, -rf * q.z};
-      jt_w = cross(q, pf);   // q·[p̃]×
-      jr = q.x * (float)pp.t[0] + q.y * (float)pp.t[1] + q.z * (float)pp.t[2];
-    }
-  }
+  Row row;
+  if (act) row = photometric_row<MODEL, JAC>(a, blk, k);
   // per-block validity and ‖r‖² (wave shuffles over the block's lanes)
-  ok = group_and<LPB>(ok);
-  const float s = group_sum<LPB>(act ? r * r : 0.0f);
+  const int ok = group_and<LPB>(act ? row.ok : 1);
+  const float s = group_sum<LPB>(act ? row.r * row.r : 0.0f);
   if (live && k == 0) {
     a.valid[blk] = (uint8_t)ok;
     a.cost[blk] = ok ? huber_cost(s, a.huber) : 0.0f;
   }
-  if (!ok) {
-    r = jr = 0.0f;
-    jh_v = jh_w = jt_v = jt_w = {0, 0, 0};
-  }
+  if (MODE == 2) return;
+  if (!ok) row = Row();
   if (!JAC) {
-    if (act) a.out[(long long)blk * rec_f + k] = r;
+    if (act) a.out[(long long)blk * rec_f + k] = row.r;
     return;
   }
   // stage the record row of pixel k: r | J_host row | J_target row | J_rho
-  if (k < P) {
+  if (act) {
     float* s_rec = stage + lb * rec_f;
-    s_rec[k] = r;
+    s_rec[k] = row.r;
     float* h = s_rec + P + 6 * k;
-    h[0] = jh_v.x; h[1] = jh_v.y; h[2] = jh_v.z; h[3] = jh_w.x; h[4] = jh_w.y; h[5] = jh_w.z;
+    h[0] = row.hv.x; h[1] = row.hv.y; h[2] = row.hv.z; h[3] = row.hw.x; h[4] = row.hw.y; h[5] = row.hw.z;
     float* t = s_rec + 7 * P + 6 * k;
-    t[0] = jt_v.x; t[1] = jt_v.y; t[2] = jt_v.z; t[3] = jt_w.x; t[4] = jt_w.y; t[5] = jt_w.z;
-    s_rec[13 * P + k] = jr;
+    t[0] = row.tv.x; t[1] = row.tv.y; t[2] = row.tv.z; t[3] = row.tw.x; t[4] = row.tw.y; t[5] = row.tw.z;
+    s_rec[13 * P + k] = row.jr;
   }
   __syncthreads();
   const int nblk = min(BPW, a.n_blocks - blk0);
@@ -294,103 +200,79 @@ __global__ __launch_bounds__(kBlockThreads) void geometric_block_kernel(const Ke
   }
 }
 
-thread_local std::string g_last_error;
-
-int fail(int code, const std::string& msg) {
-  g_last_error = msg;
-  return code;
-}
-
-#define PBA_HIP(expr)                                                                          \
-  do {                                                                                         \
-    hipError_t e_ = (expr);                                                                    \
-    if (e_ != hipSuccess)                                                                      \
-      return fail(e_ == hipErrorOutOfMemory ? PBA_ERR_OUT_OF_MEMORY : PBA_ERR_DEVICE,          \
-                  std::string(#expr) + ": " + hipGetErrorString(e_));                          \
-  } while (0)
-
-template <class T>
-struct DevBuf {
-  T* p = nullptr;
-  size_t n = 0;
-  hipError_t resize(size_t count) {
-    if (count <= n && p) return hipSuccess;
-    if (p) (void)hipFree(p);
-    p = nullptr;
-    n = 0;
-    if (count == 0) return hipSuccess;
-    hipError_t e = hipMalloc(&p, count * sizeof(T));
-    if (e == hipSuccess) n = count;
-    return e;
-  }
-  void release() {
-    if (p) (void)hipFree(p);
-    p = nullptr;
-    n = 0;
-  }
-};
-
-}  // namespace
-
-struct pba_engine {
-  pba_options opt{};
-  hipStream_t own_stream = nullptr;
-  hipStream_t stream = nullptr;
-  int n_cams = 0, n_frames = 0, n_points = 0, n_blocks = 0, n_pairs = 0;
-  int width = 0, height = 0, P = 0;
-  bool have_images = false;
-  std::vector<int> frame_cam_h, point_host_h;
-  std::vector<float> pattern_h;
-  DevBuf<float> intr;
-  DevBuf<double> intr_d;
-  DevBuf<int> frame_cam;
-  DevBuf<uint8_t> images;
-  DevBuf<double2> u_ref;
-  DevBuf<float> host_int;
-  DevBuf<int> block_point, block_pair;
-  DevBuf<double2> u_obs;
-  DevBuf<int> pair_host, pair_target;
-  DevBuf<PairRec> pairs;
-  DevBuf<double> poses, rho;
-  DevBuf<float> out, cost;
-  DevBuf<uint8_t> valid;
-  bool state_set = false;
-  bool evaluated = false;
-  bool timing = false;
-  std::vector<hipEvent_t> ev_pool;   // start/stop pairs, reused
-  size_t ev_used = 0;
-
-  int R() const { return opt.residual_kind == PBA_RESIDUAL_PHOTOMETRIC ? P : 2; }
-};
-
-namespace {
-
-int check_device(pba_engine* e) {
-  PBA_HIP(hipSetDevice(e->opt.device));
-  return PBA_OK;
-}
-
 template <int MODEL>
-void launch_blocks(pba_engine* e, const KernelArgs& ka, bool jac) {
+void launch_blocks(pba_engine* e, const KernelArgs& ka, int mode) {
   if (e->opt.residual_kind == PBA_RESIDUAL_GEOMETRIC) {
     const int grid = (e->n_blocks + kBlockThreads - 1) / kBlockThreads;
-    if (jac) geometric_block_kernel<MODEL, true><<<grid, kBlockThreads, 0, e->stream>>>(ka);
+    if (mode == 1) geometric_block_kernel<MODEL, true><<<grid, kBlockThreads, 0, e->stream>>>(ka);
     else geometric_block_kernel<MODEL, false><<<grid, kBlockThreads, 0, e->stream>>>(ka);
     return;
   }
   const int lpb = e->P <= 8 ? 8 : (e->P <= 16 ? 16 : 32);
   const long long lanes = (long long)e->n_blocks * lpb;
   const int grid = (int)((lanes + kBlockThreads - 1) / kBlockThreads);
-#define PBA_LAUNCH_PH(L)                                                                              \
-  if (jac) photometric_block_kernel<MODEL, L, true><<<grid, kBlockThreads, 0, e->stream>>>(ka);      \
-  else photometric_block_kernel<MODEL, L, false><<<grid, kBlockThreads, 0, e->stream>>>(ka);
+#define PBA_LAUNCH_PH(L)                                                                                \
+  if (mode == 1) photometric_block_kernel<MODEL, L, 1><<<grid, kBlockThreads, 0, e->stream>>>(ka);     \
+  else if (mode == 0) photometric_block_kernel<MODEL, L, 0><<<grid, kBlockThreads, 0, e->stream>>>(ka); \
+  else photometric_block_kernel<MODEL, L, 2><<<grid, kBlockThreads, 0, e->stream>>>(ka);
   if (lpb == 8) { PBA_LAUNCH_PH(8) }
   else if (lpb == 16) { PBA_LAUNCH_PH(16) }
   else { PBA_LAUNCH_PH(32) }
 #undef PBA_LAUNCH_PH
 }
 
+void launch_mode(pba_engine* e, const KernelArgs& ka, int mode) {
+  switch (e->opt.camera_model) {
+    case PBA_CAMERA_PINHOLE: launch_blocks<CAM_PINHOLE>(e, ka, mode); break;
+    case PBA_CAMERA_DOUBLE_SPHERE: launch_blocks<CAM_DS>(e, ka, mode); break;
+    default: launch_blocks<CAM_EUCM>(e, ka, mode); break;
+  }
+}
+
 }  // namespace
+
+namespace pba {
+namespace detail {
+
+KernelArgs make_kernel_args(pba_engine* e, const PairRec* pairs, const double* rho) {
+  KernelArgs ka{};
+  ka.images = e->images.p;
+  ka.width = e->width;
+  ka.height = e->height;
+  ka.frame_stride = (long long)e->width * e->height;
+  ka.intr = e->intr.p;
+  ka.intr_d = e->intr_d.p;
+  ka.block_point = e->block_point.p;
+  ka.block_pair = e->block_pair.p;
+  ka.pairs = pairs;
+  ka.u_ref = e->u_ref.p;
+  ka.host_int = e->host_int.p;
+  ka.rho = rho;
+  ka.u_obs = e->u_obs.p;
+  ka.out = e->out.p;
+  ka.cost = e->cost.p;
+  ka.valid = e->valid.p;
+  ka.n_blocks = e->n_blocks;
+  ka.P = e->opt.residual_kind == PBA_RESIDUAL_PHOTOMETRIC ? e->P : 2;
+  ka.huber = e->opt.huber_width;
+  for (size_t i = 0; i < e->pattern_h.size() && i < 2 * PBA_MAX_PATTERN; ++i) ka.pattern[i] = e->pattern_h[i];
+  return ka;
+}
+
+void launch_pairs(pba_engine* e, const double* poses, PairRec* pairs) {
+  pair_kernel<<<(e->n_pairs + 255) / 256, 256, 0, e->stream>>>(poses, e->pair_host.p, e->pair_target.p,
+                                                               e->frame_cam.p, pairs, e->n_pairs);
+}
+
+int launch_cost_only(pba_engine* e, const PairRec* pairs, const double* rho) {
+  const KernelArgs ka = make_kernel_args(e, pairs, rho);
+  launch_mode(e, ka, 2);
+  PBA_HIP(hipGetLastError());
+  return PBA_OK;
+}
+
+}  // namespace detail
+}  // namespace pba
 
 extern "C" {
 
@@ -598,6 +480,12 @@ int pba_set_blocks(pba_engine* e, int32_t n_blocks, const int32_t* block_point, 
   e->n_blocks = n_blocks;
   e->n_pairs = np;
   e->evaluated = false;
+  e->block_point_h.assign(block_point, block_point + n_blocks);
+  e->block_target_h.assign(block_target, block_target + n_blocks);
+  e->pair_of_h = std::move(pair_of);
+  e->pair_host_h = std::move(ph);
+  e->pair_target_h = std::move(pt);
+  e->gn.prepared = false;
   return PBA_OK;
 }
 
@@ -630,29 +518,8 @@ int pba_evaluate(pba_engine* e, int32_t want_jacobians) {
   const bool photometric = e->opt.residual_kind == PBA_RESIDUAL_PHOTOMETRIC;
   if (photometric && (!e->have_images || e->P <= 0)) return fail(PBA_ERR_NOT_READY, "images/pattern missing");
   if (int rc = check_device(e)) return rc;
-  pair_kernel<<<(e->n_pairs + 255) / 256, 256, 0, e->stream>>>(e->poses.p, e->pair_host.p, e->pair_target.p,
-                                                               e->frame_cam.p, e->pairs.p, e->n_pairs);
-  KernelArgs ka{};
-  ka.images = e->images.p;
-  ka.width = e->width;
-  ka.height = e->height;
-  ka.frame_stride = (long long)e->width * e->height;
-  ka.intr = e->intr.p;
-  ka.intr_d = e->intr_d.p;
-  ka.block_point = e->block_point.p;
-  ka.block_pair = e->block_pair.p;
-  ka.pairs = e->pairs.p;
-  ka.u_ref = e->u_ref.p;
-  ka.host_int = e->host_int.p;
-  ka.rho = e->rho.p;
-  ka.u_obs = e->u_obs.p;
-  ka.out = e->out.p;
-  ka.cost = e->cost.p;
-  ka.valid = e->valid.p;
-  ka.n_blocks = e->n_blocks;
-  ka.P = photometric ? e->P : 2;
-  ka.huber = e->opt.huber_width;
-  for (size_t i = 0; i < e->pattern_h.size() && i < 2 * PBA_MAX_PATTERN; ++i) ka.pattern[i] = e->pattern_h[i];
+  launch_pairs(e, e->poses.p, e->pairs.p);
+  const KernelArgs ka = make_kernel_args(e, e->pairs.p, e->rho.p);
   const bool jac = want_jacobians != 0;
   hipEvent_t ev_stop = nullptr;
   if (e->timing) {
@@ -665,11 +532,7 @@ int pba_evaluate(pba_engine* e, int32_t want_jacobians) {
     ev_stop = e->ev_pool[e->ev_used + 1];
     e->ev_used += 2;
   }
-  switch (e->opt.camera_model) {
-    case PBA_CAMERA_PINHOLE: launch_blocks<CAM_PINHOLE>(e, ka, jac); break;
-    case PBA_CAMERA_DOUBLE_SPHERE: launch_blocks<CAM_DS>(e, ka, jac); break;
-    default: launch_blocks<CAM_EUCM>(e, ka, jac); break;
-  }
+  launch_mode(e, ka, jac ? 1 : 0);
   PBA_HIP(hipGetLastError());
   if (ev_stop) PBA_HIP(hipEventRecord(ev_stop, e->stream));
   e->evaluated = true;

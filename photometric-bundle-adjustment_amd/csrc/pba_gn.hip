@@ -1,0 +1,1141 @@
+// pba_gn.hip — on-device Gauss-Newton / Levenberg-Marquardt for the photometric (and geometric) BA problem.
+//
+// Replaces the reference's per-iteration CPU work after the cost functors: the Jacobian writer and
+// gradient accumulation (program_evaluator.h:233-257), the Schur eliminator + reduced camera system
+// Cholesky of SPARSE_SCHUR (schur_complement_solver.cc:138-146; Schur structure <2,1,6>), and the
+// Levenberg-Marquardt trust-region loop (trust_region_minimizer.cc, levenberg_marquardt_strategy.cc).
+//
+// Pipeline per LM iteration (all on the engine stream):
+//   linearize_kernel   lane = (block, residual row).  Row residual/Jacobian (pba_internal.h), Huber weight
+//                      per block (Ceres Corrector, first-order form), then the 104 normal-equation products
+//                      of the row are reduce-scattered over the block's lanes with wave shuffles, summed over
+//                      the workgroup's blocks in LDS in fixed order, and written as one partial slot set per
+//                      workgroup ("linearise chunk": ≤ 256/LPB blocks of one host keyframe):
+//                        H_hh, g_h, and per distinct target t: H_ht, H_tt, g_t   (fp32)
+//                      plus 16 floats per block for the point elimination: H_ρρ, g_ρ, W_h = J_hᵀJ_ρ, W_t = J_tᵀJ_ρ.
+//   schur_kernel       one workgroup per "Schur chunk" (≤ 64 points of one host): per point
+//                      H'_ρρ = H_ρρ + λ·clamp(H_ρρ), then −Σ_p W_a W_bᵀ / H'_ρρ and −Σ_p W_a g_ρ / H'_ρρ for every
+//                      co-observed pose pair (a, b) of the chunk, fp64, fixed order.
+//   assemble_kernel    one lane per element of the reduced camera system S (skyline storage, lower blocks)
+//                      and of g: fixed-order fp64 sums of the partial slots through precomputed contribution
+//                      lists, + λ·clamp(diag) (Ceres LM diagonal), identity rows for constant frames.
+//   skyline_solve_kernel  one workgroup: right-looking block-skyline Cholesky S = LLᵀ in fp64, then
+//                      forward/back substitution for δ_poses.
+//   pose_update_kernel / point_update_kernel  T ← T·exp(δ) (Sophus SE3::exp, fp64), back-substitution
+//                      δρ = −(g_ρ + Σ W_aᵀ δ_a)/H'_ρρ, and the LM model decrease ½(λ δᵀDδ − gᵀδ).
+//   cost: pair_kernel + photometric/geometric kernel in cost-only mode + fixed-order reduction.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstring>
+#include <map>
+#include <numeric>
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "pba_internal.h"
+
+using namespace pba;
+using namespace pba::detail;
+
+namespace {
+
+constexpr int NV = 104;          // normal-equation products per residual row
+constexpr int SCHUR_PTS = 64;    // points per Schur chunk
+constexpr int SCHUR_W = 1024;    // points × local poses per Schur chunk (LDS budget)
+constexpr int SLOT_LIN_BASE = 42;  // H_hh(36) + g_h(6)
+constexpr int SLOT_LIN_T = 78;     // H_ht(36) + H_tt(36) + g_t(6)
+
+enum : int { C_TRANSPOSE = 1, C_SCHUR = 2 };
+
+// x = [J_h(6) | J_t(6) | J_ρ | r]; product v = x[pa(v)] · x[pb(v)]
+__host__ __device__ constexpr int upper_index(int i, int j) {  // 6×6 upper triangle, i ≤ j
+  return i * 6 - i * (i - 1) / 2 + (j - i);
+}
+__host__ __device__ constexpr int pa(int v) {
+  if (v < 21) { int i = 0; while (upper_index(i, 5) < v) ++i; return i; }
+  if (v < 57) return (v - 21) / 6;
+  if (v < 78) { int i = 0; while (upper_index(i, 5) < v - 57) ++i; return 6 + i; }
+  if (v < 84) return v - 78;
+  if (v < 90) return 6 + (v - 84);
+  if (v < 92) return 12;
+  if (v < 98) return v - 92;
+  if (v < 104) return 6 + (v - 98);
+  return 13;
+}
+__host__ __device__ constexpr int pb(int v) {
+  if (v < 21) { const int i = pa(v); return i + (v - upper_index(i, i)); }
+  if (v < 57) return 6 + (v - 21) % 6;
+  if (v < 78) { const int i = pa(v) - 6; return 6 + i + (v - 57 - upper_index(i, i)); }
+  if (v < 90) return 13;
+  if (v == 90) return 12;
+  if (v == 91) return 13;
+  if (v < 104) return 12;
+  return 13;
+}
+static_assert(pa(0) == 0 && pb(0) == 0 && pa(20) == 5 && pb(20) == 5 && pa(6) == 1 && pb(6) == 1, "table");
+static_assert(pa(57) == 6 && pb(57) == 6 && pa(77) == 11 && pb(77) == 11, "table");
+static_assert(pa(21) == 0 && pb(21) == 6 && pa(56) == 5 && pb(56) == 11, "table");
+
+struct LinArgs {
+  const int* gn_block;
+  const int4* chunk_desc;   // first GN block, count, n_targets, partial offset (floats)
+  const uint8_t* blk_lt;
+  float* blk_schur;
+  float* part_lin;
+  int n_chunks;
+};
+
+// ------------------------------------------------------------------------------------------------
+// linearize_kernel
+// ------------------------------------------------------------------------------------------------
+template <int V>
+__device__ __forceinline__ float nprod(const float* x) {
+  if constexpr (V < NV) {
+    constexpr int A = pa(V), B = pb(V);
+    return x[A] * x[B];
+  } else {
+    return 0.0f;
+  }
+}
+
+template <int RD, int LPB, int... Q>
+__device__ __forceinline__ void fill_round(float* vals, const float* x, std::integer_sequence<int, Q...>) {
+  ((vals[Q] = nprod<RD * LPB + Q>(x)), ...);
+}
+
+// Round RD of the normal-equation products: LPB products per lane, reduce-scattered over the block's lanes
+// (recursive halving: lane k ends with the block sum of product RD·LPB + k).
+template <int RD, int ROUNDS, int LPB>
+__device__ __forceinline__ void lin_rounds(const float* x, int k, float* srow) {
+  if constexpr (RD < ROUNDS) {
+    float vals[LPB];
+    fill_round<RD, LPB>(vals, x, std::make_integer_sequence<int, LPB>{});
+#pragma unroll
+    for (int m = LPB / 2; m >= 1; m >>= 1) {
+      const bool hi = (k & m) != 0;
+#pragma unroll
+      for (int i = 0; i < m; ++i) {
+        const float send = hi ? vals[i] : vals[i + m];
+        const float keep = hi ? vals[i + m] : vals[i];
+        vals[i] = keep + __shfl_xor(send, m, 64);
+      }
+    }
+    if (srow) srow[RD * LPB + k] = vals[0];
+    lin_rounds<RD + 1, ROUNDS, LPB>(x, k, srow);
+  }
+}
+
+template <int KIND, int MODEL, int LPB>
+__global__ __launch_bounds__(kBlockThreads) void linearize_kernel(const KernelArgs a, const LinArgs g) {
+  constexpr int BPW = kBlockThreads / LPB;
+  constexpr int ROUNDS = (NV + LPB - 1) / LPB;
+  constexpr int NVP = ROUNDS * LPB;
+  __shared__ float sblk[BPW][NVP + 1];
+  __shared__ int s_lt[BPW];
+  const int chunk = logical_tile();
+  if (chunk >= g.n_chunks) return;
+  const int4 d = g.chunk_desc[chunk];
+  const int first = d.x, count = d.y, n_t = d.z, poff = d.w;
+  const int lb = threadIdx.x / LPB, k = threadIdx.x % LPB;
+  const bool live = lb < count;
+  const int R = KIND == PBA_RESIDUAL_PHOTOMETRIC ? a.P : 2;
+  const bool act = live && k < R;
+  int blk = 0;
+  Row row;
+  if (live) {
+    blk = g.gn_block[first + lb];
+    if (k == 0) s_lt[lb] = g.blk_lt[first + lb];
+  }
+  if (act) row = eval_row<KIND, MODEL, true>(a, blk, k);
+  const int ok = group_and<LPB>(act ? row.ok : 1);
+  const float s = group_sum<LPB>(act && ok ? row.r * row.r : 0.0f);
+  const float w = ok ? huber_weight(s, a.huber) : 0.0f;
+  if (live && k == 0) {
+    a.valid[blk] = (uint8_t)ok;
+    a.cost[blk] = ok ? huber_cost(s, a.huber) : 0.0f;
+  }
+  // weighted row x̃ = √w · x  → products carry w (Ceres Corrector with ρ'' ≤ 0: J̃ = √ρ' J, r̃ = √ρ' r)
+  const float sw = (act && ok) ? sqrtf(w) : 0.0f;
+  const float x[14] = {sw * row.hv.x, sw * row.hv.y, sw * row.hv.z, sw * row.hw.x, sw * row.hw.y, sw * row.hw.z,
+                       sw * row.tv.x, sw * row.tv.y, sw * row.tv.z, sw * row.tw.x, sw * row.tw.y, sw * row.tw.z,
+                       sw * row.jr,   sw * row.r};
+  lin_rounds<0, ROUNDS, LPB>(x, k, live ? &sblk[lb][0] : nullptr);
+  __syncthreads();
+  // per-block point-elimination data: [H_ρρ, g_ρ, W_h(6), W_t(6), 0, 0]
+  for (int i = threadIdx.x; i < count * 16; i += kBlockThreads) {
+    const int b = i >> 4, q = i & 15;
+    float v = 0.0f;
+    if (q == 0) v = sblk[b][90];
+    else if (q == 1) v = sblk[b][91];
+    else if (q < 8) v = sblk[b][92 + q - 2];
+    else if (q < 14) v = sblk[b][98 + q - 8];
+    g.blk_schur[(long long)(first + b) * 16 + q] = v;
+  }
+  // chunk partial slots (fixed summation order over the chunk's blocks)
+  const int nout = SLOT_LIN_BASE + SLOT_LIN_T * n_t;
+  for (int o = threadIdx.x; o < nout; o += kBlockThreads) {
+    int v, tsel = -1;
+    if (o < 36) {
+      const int r = o / 6, c = o % 6;
+      v = upper_index(min(r, c), max(r, c));
+    } else if (o < 42) {
+      v = 78 + (o - 36);
+    } else {
+      const int j = (o - 42) / SLOT_LIN_T, q = (o - 42) % SLOT_LIN_T;
+      tsel = j;
+      if (q < 36) v = 21 + q;
+      else if (q < 72) { const int r = (q - 36) / 6, c = (q - 36) % 6; v = 57 + upper_index(min(r, c), max(r, c)); }
+      else v = 84 + (q - 72);
+    }
+    float acc = 0.0f;
+    for (int b = 0; b < count; ++b)
+      if (tsel < 0 || s_lt[b] == tsel) acc += sblk[b][v];
+    g.part_lin[(long long)poff + o] = acc;
+  }
+}
+
+struct SchurArgs {
+  const int4* desc;       // first GN point, n points, n local poses, partial offset (doubles)
+  const int2* aux;        // used-pair list offset, n used pairs
+  const uchar2* pairs;    // (a, b) local pose pairs, a ≤ b
+  const int* pt_first;
+  const int* pt_nblk;
+  const uint8_t* blk_lv;
+  const float* blk_schur;
+  double* part_schur;
+  double* pt_data;        // per GN point [H_ρρ, g_ρ, W_h(6)] (undamped)
+  int n_chunks;
+};
+
+// ------------------------------------------------------------------------------------------------
+// schur_kernel: point elimination for damping λ
+// ------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(kBlockThreads) void schur_kernel(const SchurArgs g, double lambda) {
+  __shared__ float W[SCHUR_W][6];
+  __shared__ double s_inv[SCHUR_PTS], s_gl[SCHUR_PTS];
+  const int c = blockIdx.x;
+  if (c >= g.n_chunks) return;
+  const int4 d = g.desc[c];
+  const int first = d.x, npt = d.y, nv = d.z, poff = d.w;
+  const int2 ax = g.aux[c];
+  for (int i = threadIdx.x; i < npt * nv * 6; i += kBlockThreads) (&W[0][0])[i] = 0.0f;
+  __syncthreads();
+  if (threadIdx.x < npt) {
+    const int p = threadIdx.x, gp = first + p;
+    const int fb = g.pt_first[gp], nb = g.pt_nblk[gp];
+    double H = 0.0, gl = 0.0, wh[6] = {0, 0, 0, 0, 0, 0};
+    for (int b = fb; b < fb + nb; ++b) {
+      const float* q = g.blk_schur + (long long)b * 16;
+      H += q[0];
+      gl += q[1];
+      const int lv = g.blk_lv[b];
+      for (int i = 0; i < 6; ++i) {
+        wh[i] += q[2 + i];
+        W[p * nv + lv][i] += q[8 + i];
+      }
+    }
+    for (int i = 0; i < 6; ++i) W[p * nv + 0][i] = (float)wh[i];
+    const double D = fmin(fmax(H, 1e-6), 1e32);
+    const double Hd = H + lambda * D;
+    s_inv[p] = Hd > 0.0 ? 1.0 / Hd : 0.0;
+    s_gl[p] = gl;
+    double* pd = g.pt_data + (long long)gp * 8;
+    pd[0] = H;
+    pd[1] = gl;
+    for (int i = 0; i < 6; ++i) pd[2 + i] = wh[i];
+  }
+  __syncthreads();
+  const int nout = ax.y * 36 + nv * 6;
+  for (int o = threadIdx.x; o < nout; o += kBlockThreads) {
+    double acc = 0.0;
+    if (o < ax.y * 36) {
+      const uchar2 ab = g.pairs[ax.x + o / 36];
+      const int r = (o % 36) / 6, cc = o % 6;
+      for (int p = 0; p < npt; ++p)
+        acc += (double)W[p * nv + ab.x][r] * (double)W[p * nv + ab.y][cc] * s_inv[p];
+    } else {
+      const int q = o - ax.y * 36, a = q / 6, r = q % 6;
+      for (int p = 0; p < npt; ++p) acc += (double)W[p * nv + a][r] * s_gl[p] * s_inv[p];
+    }
+    g.part_schur[(long long)poff + o] = acc;
+  }
+}
+
+struct AsmArgs {
+  const float* part_lin;
+  const double* part_schur;
+  const int* sky_cptr;
+  const int2* sky_contrib;
+  const int* g_cptr;
+  const int2* g_contrib;
+  const int* blk_i;
+  const int* blk_j;
+  const uint8_t* fixed;
+  double* S;
+  double* g;
+  double* g_dir;
+  double* Ddiag;
+  int n_sky;
+  int n_frames;
+};
+
+__device__ __forceinline__ double contrib_value(const AsmArgs& a, int2 c, int r, int cc, bool& schur) {
+  const int off = c.x, fl = c.y;
+  const int e = (fl & C_TRANSPOSE) ? cc * 6 + r : r * 6 + cc;
+  schur = (fl & C_SCHUR) != 0;
+  return schur ? -a.part_schur[(long long)off + e] : (double)a.part_lin[(long long)off + e];
+}
+
+// ------------------------------------------------------------------------------------------------
+// assemble_kernel: S (skyline, lower blocks) and g from the partial slots
+// ------------------------------------------------------------------------------------------------
+__global__ void assemble_kernel(const AsmArgs a, double lambda) {
+  const int tid = blockIdx.x * blockDim.x + threadIdx.x;
+  const int nS = a.n_sky * 36;
+  if (tid < nS) {
+    const int s = tid / 36, e = tid % 36, r = e / 6, cc = e % 6;
+    const int i = a.blk_i[s], j = a.blk_j[s];
+    double sum = 0.0, dsum = 0.0;
+    for (int q = a.sky_cptr[s]; q < a.sky_cptr[s + 1]; ++q) {
+      bool schur;
+      const double v = contrib_value(a, a.sky_contrib[q], r, cc, schur);
+      sum += v;
+      if (!schur) dsum += v;
+    }
+    double val = sum;
+    if (a.fixed[i] || a.fixed[j]) {
+      val = (i == j && r == cc) ? 1.0 : 0.0;
+    } else if (i == j && r == cc) {
+      const double D = fmin(fmax(dsum, 1e-6), 1e32);  // levenberg_marquardt_strategy.cc min/max diagonal
+      a.Ddiag[6 * i + r] = D;
+      val = sum + lambda * D;
+    }
+    a.S[tid] = val;
+    return;
+  }
+  const int t = tid - nS;
+  if (t >= 6 * a.n_frames) return;
+  const int i = t / 6, r = t % 6;
+  double sum = 0.0, dsum = 0.0;
+  for (int q = a.g_cptr[i]; q < a.g_cptr[i + 1]; ++q) {
+    const int2 c = a.g_contrib[q];
+    if (c.y & C_SCHUR) sum -= a.part_schur[(long long)c.x + r];
+    else {
+      const double v = a.part_lin[(long long)c.x + r];
+      sum += v;
+      dsum += v;
+    }
+  }
+  a.g[t] = a.fixed[i] ? 0.0 : sum;
+  a.g_dir[t] = a.fixed[i] ? 0.0 : dsum;
+  if (a.fixed[i]) a.Ddiag[t] = 0.0;
+}
+
+// ------------------------------------------------------------------------------------------------
+// skyline_solve_kernel: S δ = −g, S = LLᵀ in place (block skyline, right-looking), one workgroup
+// ------------------------------------------------------------------------------------------------
+__device__ inline bool chol6(const double* A, double* L) {
+  for (int i = 0; i < 36; ++i) L[i] = 0.0;
+  for (int j = 0; j < 6; ++j) {
+    double s = A[j * 6 + j];
+    for (int k = 0; k < j; ++k) s -= L[j * 6 + k] * L[j * 6 + k];
+    if (!(s > 0.0)) return false;
+    const double ljj = sqrt(s);
+    L[j * 6 + j] = ljj;
+    for (int i = j + 1; i < 6; ++i) {
+      double t = A[i * 6 + j];
+      for (int k = 0; k < j; ++k) t -= L[i * 6 + k] * L[j * 6 + k];
+      L[i * 6 + j] = t / ljj;
+    }
+  }
+  return true;
+}
+__device__ inline void inv_lower6(const double* L, double* Li) {
+  for (int i = 0; i < 36; ++i) Li[i] = 0.0;
+  for (int c = 0; c < 6; ++c) {
+    Li[c * 6 + c] = 1.0 / L[c * 6 + c];
+    for (int r = c + 1; r < 6; ++r) {
+      double s = 0.0;
+      for (int k = c; k < r; ++k) s += L[r * 6 + k] * Li[k * 6 + c];
+      Li[r * 6 + c] = -s / L[r * 6 + r];
+    }
+  }
+}
+
+struct SolveArgs {
+  double* S;
+  const int* first;
+  const int* row;
+  const int* last;
+  const double* g;
+  double* Linv;
+  double* x;
+  int* status;
+  int N;
+};
+
+__device__ __forceinline__ long long sky_off(const SolveArgs& a, int i, int j) {  // block (i, j), j ≥ first(i)
+  return ((long long)a.row[i] + (j - a.first[i])) * 36;
+}
+
+__global__ __launch_bounds__(256) void skyline_solve_kernel(const SolveArgs a) {
+  __shared__ double sA[36], sL[36], sLi[36];
+  __shared__ int s_fail;
+  const int tid = threadIdx.x;
+  if (tid == 0) s_fail = 0;
+  for (int k = 0; k < a.N; ++k) {
+    const long long okk = sky_off(a, k, k);
+    if (tid < 36) sA[tid] = a.S[okk + tid];
+    __syncthreads();
+    if (tid == 0) {
+      if (!chol6(sA, sL)) s_fail = k + 1;
+      else inv_lower6(sL, sLi);
+    }
+    __syncthreads();
+    if (s_fail) {
+      if (tid == 0) *a.status = s_fail;
+      return;
+    }
+    if (tid < 36) {
+      a.S[okk + tid] = sL[tid];
+      a.Linv[(long long)k * 36 + tid] = sLi[tid];
+    }
+    const int lk = a.last[k];
+    // column panel L_ik = A_ik · L_kk⁻ᵀ, 7 blocks per pass (read all, barrier, write)
+    for (int i0 = k + 1; i0 <= lk; i0 += 7) {
+      double val = 0.0;
+      long long dst = -1;
+      const int idx = tid;
+      const int i = i0 + idx / 36;
+      if (idx < 252 && i <= lk && a.first[i] <= k) {
+        const int e = idx % 36, r = e / 6, c = e % 6;
+        const long long o = sky_off(a, i, k);
+        for (int m = 0; m <= c; ++m) val += a.S[o + r * 6 + m] * sLi[c * 6 + m];
+        dst = o + e;
+      }
+      __syncthreads();
+      if (dst >= 0) a.S[dst] = val;
+      __threadfence_block();
+      __syncthreads();
+    }
+    // trailing update A_ij −= L_ik L_jkᵀ for k < j ≤ i ≤ last(k)
+    const int nk = lk - k;
+    const int npairs = nk * (nk + 1) / 2;
+    for (int idx = tid; idx < npairs * 36; idx += 256) {
+      const int pidx = idx / 36, e = idx % 36, r = e / 6, c = e % 6;
+      int ii = 0;  // decode lower-triangular pair index → (ii ≥ jj)
+      while ((ii + 1) * (ii + 2) / 2 <= pidx) ++ii;
+      const int jj = pidx - ii * (ii + 1) / 2;
+      const int i = k + 1 + ii, j = k + 1 + jj;
+      if (a.first[i] > k || a.first[j] > k) continue;
+      const long long oi = sky_off(a, i, k), oj = sky_off(a, j, k);
+      double s = 0.0;
+      for (int m = 0; m < 6; ++m) s += a.S[oi + r * 6 + m] * a.S[oj + c * 6 + m];
+      a.S[sky_off(a, i, j) + e] -= s;
+    }
+    __threadfence_block();
+    __syncthreads();
+  }
+  // forward substitution L y = −g (y in x)
+  for (int t = tid; t < 6 * a.N; t += 256) a.x[t] = -a.g[t];
+  __threadfence_block();
+  __syncthreads();
+  for (int k = 0; k < a.N; ++k) {
+    __shared__ double yk[6];
+    if (tid < 6) {
+      double s = 0.0;
+      for (int m = 0; m <= tid; ++m) s += a.Linv[(long long)k * 36 + tid * 6 + m] * a.x[6 * k + m];
+      yk[tid] = s;
+    }
+    __syncthreads();
+    if (tid < 6) a.x[6 * k + tid] = yk[tid];
+    const int lk = a.last[k];
+    for (int idx = tid; idx < (lk - k) * 6; idx += 256) {
+      const int i = k + 1 + idx / 6, r = idx % 6;
+      if (a.first[i] > k) continue;
+      const long long o = sky_off(a, i, k);
+      double s = 0.0;
+      for (int m = 0; m < 6; ++m) s += a.S[o + r * 6 + m] * yk[m];
+      a.x[6 * i + r] -= s;
+    }
+    __threadfence_block();
+    __syncthreads();
+  }
+  // back substitution Lᵀ x = y
+  for (int k = a.N - 1; k >= 0; --k) {
+    __shared__ double tk[6];
+    if (tid < 6) {
+      double s = a.x[6 * k + tid];
+      for (int i = k + 1; i <= a.last[k]; ++i) {
+        if (a.first[i] > k) continue;
+        const long long o = sky_off(a, i, k);
+        for (int m = 0; m < 6; ++m) s -= a.S[o + m * 6 + tid] * a.x[6 * i + m];
+      }
+      tk[tid] = s;
+    }
+    __syncthreads();
+    if (tid < 6) {
+      double s = 0.0;
+      for (int m = tid; m < 6; ++m) s += a.Linv[(long long)k * 36 + m * 6 + tid] * tk[m];
+      a.x[6 * k + tid] = s;
+    }
+    __threadfence_block();
+    __syncthreads();
+  }
+  if (tid == 0) *a.status = 0;
+}
+
+// ------------------------------------------------------------------------------------------------
+// Updates: poses T·exp(δ) (se3.hpp:763-784) and back-substituted inverse distances
+// ------------------------------------------------------------------------------------------------
+__device__ void se3_exp_mul(const double* T, const double* d, double* out) {
+  const double w0 = d[3], w1 = d[4], w2 = d[5];
+  const double th2 = w0 * w0 + w1 * w1 + w2 * w2, th = sqrt(th2);
+  double imag, real, A, B;
+  if (th < 1e-10) {
+    real = 1.0 - th2 / 8.0 + th2 * th2 / 384.0;
+    imag = 0.5 - th2 / 48.0 + th2 * th2 / 3840.0;
+    A = 0.5;
+    B = 1.0 / 6.0;
+  } else {
+    real = cos(0.5 * th);
+    imag = sin(0.5 * th) / th;
+    A = (1.0 - cos(th)) / th2;
+    B = (th - sin(th)) / (th2 * th);
+  }
+  const double qx = imag * w0, qy = imag * w1, qz = imag * w2, qw = real;
+  // V υ = υ + A ω×υ + B ω×(ω×υ)
+  const double v0 = d[0], v1 = d[1], v2 = d[2];
+  const double c0 = w1 * v2 - w2 * v1, c1 = w2 * v0 - w0 * v2, c2 = w0 * v1 - w1 * v0;
+  const double cc0 = w1 * c2 - w2 * c1, cc1 = w2 * c0 - w0 * c2, cc2 = w0 * c1 - w1 * c0;
+  const double tx = v0 + A * c0 + B * cc0, ty = v1 + A * c1 + B * cc1, tz = v2 + A * c2 + B * cc2;
+  // T · exp(δ): q = q_T ⊗ q_δ (normalised), t = t_T + R_T t_δ
+  const double ax = T[0], ay = T[1], az = T[2], aw = T[3];
+  double rw = aw * qw - ax * qx - ay * qy - az * qz;
+  double rx = aw * qx + ax * qw + ay * qz - az * qy;
+  double ry = aw * qy + ay * qw + az * qx - ax * qz;
+  double rz = aw * qz + az * qw + ax * qy - ay * qx;
+  const double n = 1.0 / sqrt(rw * rw + rx * rx + ry * ry + rz * rz);
+  double u0 = ay * tz - az * ty, u1 = az * tx - ax * tz, u2 = ax * ty - ay * tx;
+  u0 += u0; u1 += u1; u2 += u2;
+  out[0] = rx * n; out[1] = ry * n; out[2] = rz * n; out[3] = rw * n;
+  out[4] = T[4] + tx + aw * u0 + (ay * u2 - az * u1);
+  out[5] = T[5] + ty + aw * u1 + (az * u0 - ax * u2);
+  out[6] = T[6] + tz + aw * u2 + (ax * u1 - ay * u0);
+}
+
+__device__ __forceinline__ void block_reduce2(double a, double b, double* out) {
+  __shared__ double sa[kBlockThreads / 64], sb[kBlockThreads / 64];
+  for (int m = 32; m >= 1; m >>= 1) {
+    a += __shfl_xor(a, m, 64);
+    b += __shfl_xor(b, m, 64);
+  }
+  const int w = threadIdx.x / 64, l = threadIdx.x % 64;
+  if (l == 0) { sa[w] = a; sb[w] = b; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double x = 0, y = 0;
+    for (int i = 0; i < (int)(blockDim.x / 64); ++i) { x += sa[i]; y += sb[i]; }
+    out[0] = x;
+    out[1] = y;
+  }
+}
+
+__global__ __launch_bounds__(kBlockThreads) void pose_update_kernel(const double* poses, const double* x,
+                                                                   const double* g_dir, const double* Ddiag,
+                                                                   const uint8_t* fixed, double* poses_new,
+                                                                   double* red, int n) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  double dg = 0.0, dD = 0.0;
+  if (i < n) {
+    if (fixed[i]) {
+      for (int q = 0; q < 7; ++q) poses_new[7 * i + q] = poses[7 * i + q];
+    } else {
+      se3_exp_mul(poses + 7 * i, x + 6 * i, poses_new + 7 * i);
+      for (int r = 0; r < 6; ++r) {
+        dg += x[6 * i + r] * g_dir[6 * i + r];
+        dD += x[6 * i + r] * x[6 * i + r] * Ddiag[6 * i + r];
+      }
+    }
+  }
+  block_reduce2(dg, dD, red + 2 * blockIdx.x);
+}
+
+struct PointUpdateArgs {
+  const double* pt_data;
+  const int* pt_first;
+  const int* pt_nblk;
+  const int* pt_orig;
+  const int* pt_host;
+  const int* gn_target;
+  const float* blk_schur;
+  const double* x;
+  const uint8_t* fixed;
+  const double* rho;
+  double* rho_new;
+  double* drho;
+  double* red;
+  int n_points;
+};
+
+__global__ __launch_bounds__(kBlockThreads) void point_update_kernel(const PointUpdateArgs a, double lambda) {
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  double dg = 0.0, dD = 0.0;
+  if (p < a.n_points) {
+    const double* pd = a.pt_data + (long long)p * 8;
+    const double H = pd[0], gl = pd[1];
+    const double D = fmin(fmax(H, 1e-6), 1e32);
+    const double Hd = H + lambda * D;
+    const int h = a.pt_host[p];
+    double s = gl;
+    for (int i = 0; i < 6; ++i) s += pd[2 + i] * a.x[6 * h + i];
+    for (int b = a.pt_first[p]; b < a.pt_first[p] + a.pt_nblk[p]; ++b) {
+      const int t = a.gn_target[b];
+      const float* q = a.blk_schur + (long long)b * 16;
+      for (int i = 0; i < 6; ++i) s += (double)q[8 + i] * a.x[6 * t + i];
+    }
+    const double dr = Hd > 0.0 ? -s / Hd : 0.0;
+    const int o = a.pt_orig[p];
+    a.rho_new[o] = a.rho[o] + dr;
+    a.drho[o] = dr;
+    dg = dr * gl;
+    dD = dr * dr * D;
+  }
+  block_reduce2(dg, dD, a.red + 2 * blockIdx.x);
+}
+
+__global__ __launch_bounds__(kBlockThreads) void cost_reduce_kernel(const float* cost, const uint8_t* valid, int n,
+                                                                    double* red) {
+  double c = 0.0, v = 0.0;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    c += cost[i];
+    v += valid[i];
+  }
+  block_reduce2(c, v, red + 2 * blockIdx.x);
+}
+
+// ------------------------------------------------------------------------------------------------
+// host side
+// ------------------------------------------------------------------------------------------------
+int gn_lpb(const pba_engine* e) {
+  if (e->opt.residual_kind == PBA_RESIDUAL_GEOMETRIC) return 4;
+  return e->P <= 8 ? 8 : (e->P <= 16 ? 16 : 32);
+}
+
+// Symbolic analysis: GN block order, chunks, slot layouts, skyline profile and contribution lists.
+int gn_prepare(pba_engine* e) {
+  GnData& G = e->gn;
+  const int nb = e->n_blocks, nf = e->n_frames;
+  if (nb <= 0) return fail(PBA_ERR_NOT_READY, "pba_set_blocks first");
+  G.lpb = gn_lpb(e);
+  G.bpw = kBlockThreads / G.lpb;
+  const std::vector<int>& ph = e->point_host_h;
+  // GN order: (host, point, target)
+  std::vector<int> order(nb);
+  std::iota(order.begin(), order.end(), 0);
+  std::stable_sort(order.begin(), order.end(), [&](int a, int b) {
+    const int pa_ = e->block_point_h[a], pb_ = e->block_point_h[b];
+    if (ph[pa_] != ph[pb_]) return ph[pa_] < ph[pb_];
+    if (pa_ != pb_) return pa_ < pb_;
+    return e->block_target_h[a] < e->block_target_h[b];
+  });
+  std::vector<int> gtgt(nb);
+  for (int i = 0; i < nb; ++i) gtgt[i] = e->block_target_h[order[i]];
+  // linearise chunks
+  std::vector<int4> cdesc;
+  std::vector<uint8_t> blt(nb);
+  std::vector<std::vector<int>> chunk_targets;
+  std::vector<int> chunk_host;
+  size_t off = 0;
+  for (int i = 0; i < nb;) {
+    const int h = ph[e->block_point_h[order[i]]];
+    int j = i;
+    std::vector<int> tg;
+    while (j < nb && j - i < G.bpw && ph[e->block_point_h[order[j]]] == h) {
+      const int t = gtgt[j];
+      auto it = std::find(tg.begin(), tg.end(), t);
+      blt[j] = (uint8_t)(it - tg.begin());
+      if (it == tg.end()) tg.push_back(t);
+      ++j;
+    }
+    cdesc.push_back(make_int4(i, j - i, (int)tg.size(), (int)off));
+    off += SLOT_LIN_BASE + SLOT_LIN_T * tg.size();
+    chunk_targets.push_back(tg);
+    chunk_host.push_back(h);
+    i = j;
+  }
+  G.lin_floats = off;
+  G.n_chunks = (int)cdesc.size();
+  // GN points
+  std::vector<int> pfirst, pnblk, porig, phost;
+  for (int i = 0; i < nb;) {
+    const int p = e->block_point_h[order[i]];
+    int j = i;
+    while (j < nb && e->block_point_h[order[j]] == p) ++j;
+    pfirst.push_back(i);
+    pnblk.push_back(j - i);
+    porig.push_back(p);
+    phost.push_back(ph[p]);
+    i = j;
+  }
+  const int ngp = (int)pfirst.size();
+  G.n_gn_points = ngp;
+  // Schur chunks
+  std::vector<int4> sdesc;
+  std::vector<int2> saux;
+  std::vector<uchar2> spairs;
+  std::vector<uint8_t> blv(nb, 0);
+  std::vector<std::vector<int>> schur_poses;
+  std::vector<std::vector<std::pair<int, int>>> schur_used;
+  size_t soff = 0;
+  for (int p = 0; p < ngp;) {
+    const int h = phost[p];
+    std::vector<int> poses{h};
+    int q = p;
+    while (q < ngp && q - p < SCHUR_PTS && phost[q] == h) {
+      std::vector<int> add;
+      for (int b = pfirst[q]; b < pfirst[q] + pnblk[q]; ++b)
+        if (std::find(poses.begin(), poses.end(), gtgt[b]) == poses.end() &&
+            std::find(add.begin(), add.end(), gtgt[b]) == add.end())
+          add.push_back(gtgt[b]);
+      const int nv = (int)(poses.size() + add.size());
+      if (q > p && ((q - p + 1) * nv > SCHUR_W || nv > 255)) break;
+      if (nv > 255 || nv > SCHUR_W) return fail(PBA_ERR_INVALID_ARGUMENT, "a point observes too many keyframes");
+      poses.insert(poses.end(), add.begin(), add.end());
+      ++q;
+    }
+    const int nv = (int)poses.size();
+    std::vector<char> used(nv * nv, 0);
+    for (int r = p; r < q; ++r) {
+      std::vector<int> lv{0};
+      for (int b = pfirst[r]; b < pfirst[r] + pnblk[r]; ++b) {
+        const int l = (int)(std::find(poses.begin(), poses.end(), gtgt[b]) - poses.begin());
+        blv[b] = (uint8_t)l;
+        lv.push_back(l);
+      }
+      for (int x : lv)
+        for (int y : lv) used[std::min(x, y) * nv + std::max(x, y)] = 1;
+    }
+    std::vector<std::pair<int, int>> up;
+    for (int x = 0; x < nv; ++x)
+      for (int y = x; y < nv; ++y)
+        if (used[x * nv + y]) up.emplace_back(x, y);
+    saux.push_back(make_int2((int)spairs.size(), (int)up.size()));
+    for (auto& pr : up) spairs.push_back(make_uchar2((unsigned char)pr.first, (unsigned char)pr.second));
+    sdesc.push_back(make_int4(p, q - p, nv, (int)soff));
+    soff += 36 * up.size() + 6 * nv;
+    schur_poses.push_back(poses);
+    schur_used.push_back(up);
+    p = q;
+  }
+  G.schur_doubles = soff;
+  G.n_schur = (int)sdesc.size();
+  // reduced camera system structure: lower blocks (i ≥ j)
+  std::map<std::pair<int, int>, std::vector<int2>> contrib;
+  std::vector<std::vector<int2>> gcon(nf);
+  auto add = [&](int fa, int fb, int o, int flags) {  // contribution block in orientation (fa rows, fb cols)
+    if (fa >= fb) contrib[{fa, fb}].push_back(make_int2(o, flags));
+    else contrib[{fb, fa}].push_back(make_int2(o, flags | C_TRANSPOSE));
+  };
+  std::vector<char> observed(nf, 0);
+  for (int c = 0; c < G.n_chunks; ++c) {
+    const int h = chunk_host[c], o = cdesc[c].w;
+    observed[h] = 1;
+    add(h, h, o, 0);
+    gcon[h].push_back(make_int2(o + 36, 0));
+    for (size_t j = 0; j < chunk_targets[c].size(); ++j) {
+      const int t = chunk_targets[c][j], bo = o + SLOT_LIN_BASE + SLOT_LIN_T * (int)j;
+      observed[t] = 1;
+      add(h, t, bo, 0);
+      add(t, t, bo + 36, 0);
+      gcon[t].push_back(make_int2(bo + 72, 0));
+    }
+  }
+  for (int s = 0; s < G.n_schur; ++s) {
+    const auto& poses = schur_poses[s];
+    const int o = sdesc[s].w;
+    for (size_t u = 0; u < schur_used[s].size(); ++u) {
+      const int fa = poses[schur_used[s][u].first], fb = poses[schur_used[s][u].second];
+      add(fa, fb, o + 36 * (int)u, C_SCHUR);
+    }
+    for (size_t a = 0; a < poses.size(); ++a)
+      gcon[poses[a]].push_back(make_int2(o + 36 * (int)schur_used[s].size() + 6 * (int)a, C_SCHUR));
+  }
+  for (int i = 0; i < nf; ++i) contrib[{i, i}];  // every diagonal block exists
+  std::vector<int> first(nf), rowp(nf + 1), last(nf);
+  for (int i = 0; i < nf; ++i) first[i] = i;
+  for (auto& kv : contrib) first[kv.first.first] = std::min(first[kv.first.first], kv.first.second);
+  rowp[0] = 0;
+  for (int i = 0; i < nf; ++i) rowp[i + 1] = rowp[i] + (i - first[i] + 1);
+  G.n_sky = rowp[nf];
+  for (int k = 0; k < nf; ++k) last[k] = k;
+  for (int i = 0; i < nf; ++i)
+    for (int k = first[i]; k < i; ++k) last[k] = std::max(last[k], i);
+  std::vector<int> cptr(G.n_sky + 1, 0), bi(G.n_sky), bj(G.n_sky);
+  std::vector<std::vector<int2>> per(G.n_sky);
+  for (int i = 0; i < nf; ++i)
+    for (int j = first[i]; j <= i; ++j) {
+      const int s = rowp[i] + (j - first[i]);
+      bi[s] = i;
+      bj[s] = j;
+    }
+  for (auto& kv : contrib) {
+    const int s = rowp[kv.first.first] + (kv.first.second - first[kv.first.first]);
+    per[s] = kv.second;
+  }
+  std::vector<int2> flat;
+  for (int s = 0; s < G.n_sky; ++s) {
+    cptr[s] = (int)flat.size();
+    flat.insert(flat.end(), per[s].begin(), per[s].end());
+  }
+  cptr[G.n_sky] = (int)flat.size();
+  std::vector<int> gptr(nf + 1);
+  std::vector<int2> gflat;
+  for (int i = 0; i < nf; ++i) {
+    gptr[i] = (int)gflat.size();
+    gflat.insert(gflat.end(), gcon[i].begin(), gcon[i].end());
+  }
+  gptr[nf] = (int)gflat.size();
+  // constant frames: requested + never observed
+  std::vector<uint8_t> fixed(nf, 0);
+  for (int i = 0; i < nf; ++i) fixed[i] = (i < (int)G.fixed_h.size() && G.fixed_h[i]) || !observed[i];
+  // upload
+  hipStream_t st = e->stream;
+  PBA_HIP(G.gn_block.upload(order, st));
+  PBA_HIP(G.chunk_desc.upload(cdesc, st));
+  PBA_HIP(G.blk_lt.upload(blt, st));
+  PBA_HIP(G.blk_schur.resize((size_t)nb * 16));
+  PBA_HIP(G.part_lin.resize(std::max<size_t>(G.lin_floats, 1)));
+  PBA_HIP(G.pt_first.upload(pfirst, st));
+  PBA_HIP(G.pt_nblk.upload(pnblk, st));
+  PBA_HIP(G.pt_orig.upload(porig, st));
+  PBA_HIP(G.pt_host.upload(phost, st));
+  PBA_HIP(G.gn_target.upload(gtgt, st));
+  PBA_HIP(G.schur_desc.upload(sdesc, st));
+  PBA_HIP(G.schur_aux.upload(saux, st));
+  PBA_HIP(G.schur_pairs.upload(spairs, st));
+  PBA_HIP(G.blk_lv.upload(blv, st));
+  PBA_HIP(G.part_schur.resize(std::max<size_t>(G.schur_doubles, 1)));
+  PBA_HIP(G.pt_data.resize((size_t)ngp * 8));
+  PBA_HIP(G.sky_first.upload(first, st));
+  PBA_HIP(G.sky_row.upload(rowp, st));
+  PBA_HIP(G.sky_last.upload(last, st));
+  PBA_HIP(G.sky_cptr.upload(cptr, st));
+  PBA_HIP(G.sky_contrib.upload(flat.empty() ? std::vector<int2>{make_int2(0, 0)} : flat, st));
+  PBA_HIP(G.g_cptr.upload(gptr, st));
+  PBA_HIP(G.g_contrib.upload(gflat.empty() ? std::vector<int2>{make_int2(0, 0)} : gflat, st));
+  PBA_HIP(G.sky_blk_i.upload(bi, st));
+  PBA_HIP(G.sky_blk_j.upload(bj, st));
+  PBA_HIP(G.fixed.upload(fixed, st));
+  PBA_HIP(G.S.resize((size_t)G.n_sky * 36));
+  PBA_HIP(G.g.resize((size_t)nf * 6));
+  PBA_HIP(G.g_dir.resize((size_t)nf * 6));
+  PBA_HIP(G.Ddiag.resize((size_t)nf * 6));
+  PBA_HIP(G.Linv.resize((size_t)nf * 36));
+  PBA_HIP(G.x.resize((size_t)nf * 6));
+  PBA_HIP(G.poses_new.resize((size_t)nf * 7));
+  PBA_HIP(G.rho_new.resize((size_t)e->n_points));
+  PBA_HIP(G.drho.resize((size_t)e->n_points));
+  PBA_HIP(G.pairs_new.resize((size_t)e->n_pairs));
+  PBA_HIP(G.status.resize(1));
+  const int red_pose = (nf + kBlockThreads - 1) / kBlockThreads;
+  const int red_pt = (ngp + kBlockThreads - 1) / kBlockThreads;
+  G.red_slots = std::max(std::max(red_pose + red_pt, 1024), 1);
+  PBA_HIP(G.red.resize((size_t)2 * G.red_slots));
+  G.red_h.resize(2 * G.red_slots);
+  PBA_HIP(hipMemsetAsync(G.drho.p, 0, sizeof(double) * e->n_points, st));
+  PBA_HIP(hipStreamSynchronize(st));
+  G.prepared = true;
+  G.fixed_eff = fixed;
+  return PBA_OK;
+}
+
+template <int KIND, int MODEL>
+void launch_linearize(pba_engine* e, const KernelArgs& ka, const LinArgs& la) {
+  const int grid = la.n_chunks;
+  switch (e->gn.lpb) {
+    case 4: linearize_kernel<KIND, MODEL, 4><<<grid, kBlockThreads, 0, e->stream>>>(ka, la); break;
+    case 8: linearize_kernel<KIND, MODEL, 8><<<grid, kBlockThreads, 0, e->stream>>>(ka, la); break;
+    case 16: linearize_kernel<KIND, MODEL, 16><<<grid, kBlockThreads, 0, e->stream>>>(ka, la); break;
+    default: linearize_kernel<KIND, MODEL, 32><<<grid, kBlockThreads, 0, e->stream>>>(ka, la); break;
+  }
+}
+
+template <int KIND>
+void launch_linearize_k(pba_engine* e, const KernelArgs& ka, const LinArgs& la) {
+  switch (e->opt.camera_model) {
+    case PBA_CAMERA_PINHOLE: launch_linearize<KIND, CAM_PINHOLE>(e, ka, la); break;
+    case PBA_CAMERA_DOUBLE_SPHERE: launch_linearize<KIND, CAM_DS>(e, ka, la); break;
+    default: launch_linearize<KIND, CAM_EUCM>(e, ka, la); break;
+  }
+}
+
+int ensure_prepared(pba_engine* e) {
+  if (!e) return fail(PBA_ERR_INVALID_ARGUMENT, "null engine");
+  if (e->n_blocks <= 0) return fail(PBA_ERR_NOT_READY, "pba_set_blocks first");
+  if (!e->state_set) return fail(PBA_ERR_NOT_READY, "pba_set_state first");
+  if (e->opt.residual_kind == PBA_RESIDUAL_PHOTOMETRIC && (!e->have_images || e->P <= 0))
+    return fail(PBA_ERR_NOT_READY, "images/pattern missing");
+  if (int rc = check_device(e)) return rc;
+  if (!e->gn.prepared)
+    if (int rc = gn_prepare(e)) return rc;
+  return PBA_OK;
+}
+
+// Σ of 2-vectors over `slots` reduction slots, in fixed order on the host.
+int read_red(pba_engine* e, int slots, double* a, double* b) {
+  GnData& G = e->gn;
+  PBA_HIP(hipMemcpyAsync(G.red_h.data(), G.red.p, sizeof(double) * 2 * slots, hipMemcpyDeviceToHost, e->stream));
+  PBA_HIP(hipStreamSynchronize(e->stream));
+  double x = 0, y = 0;
+  for (int i = 0; i < slots; ++i) {
+    x += G.red_h[2 * i];
+    y += G.red_h[2 * i + 1];
+  }
+  *a = x;
+  if (b) *b = y;
+  return PBA_OK;
+}
+
+int total_cost(pba_engine* e, double* cost, int* n_valid) {
+  const int grid = std::min(1024, (e->n_blocks + kBlockThreads - 1) / kBlockThreads);
+  cost_reduce_kernel<<<grid, kBlockThreads, 0, e->stream>>>(e->cost.p, e->valid.p, e->n_blocks, e->gn.red.p);
+  PBA_HIP(hipGetLastError());
+  double c, v;
+  if (int rc = read_red(e, grid, &c, &v)) return rc;
+  *cost = c;
+  if (n_valid) *n_valid = (int)v;
+  return PBA_OK;
+}
+
+int linearize(pba_engine* e, double* cost) {
+  GnData& G = e->gn;
+  launch_pairs(e, e->poses.p, e->pairs.p);
+  const KernelArgs ka = make_kernel_args(e, e->pairs.p, e->rho.p);
+  LinArgs la{G.gn_block.p, G.chunk_desc.p, G.blk_lt.p, G.blk_schur.p, G.part_lin.p, G.n_chunks};
+  if (e->opt.residual_kind == PBA_RESIDUAL_PHOTOMETRIC) launch_linearize_k<PBA_RESIDUAL_PHOTOMETRIC>(e, ka, la);
+  else launch_linearize_k<PBA_RESIDUAL_GEOMETRIC>(e, ka, la);
+  PBA_HIP(hipGetLastError());
+  e->evaluated = false;  // records are not written in GN mode
+  if (cost) return total_cost(e, cost, nullptr);
+  return PBA_OK;
+}
+
+// Schur complement for λ, assembly, solve and candidate state; returns the LM model decrease.
+int gn_step(pba_engine* e, double lambda, double* model_decrease, int* solver_status) {
+  GnData& G = e->gn;
+  const int nf = e->n_frames;
+  SchurArgs sa{G.schur_desc.p, G.schur_aux.p, G.schur_pairs.p, G.pt_first.p, G.pt_nblk.p, G.blk_lv.p,
+               G.blk_schur.p, G.part_schur.p, G.pt_data.p, G.n_schur};
+  schur_kernel<<<G.n_schur, kBlockThreads, 0, e->stream>>>(sa, lambda);
+  AsmArgs aa{G.part_lin.p, G.part_schur.p, G.sky_cptr.p, G.sky_contrib.p, G.g_cptr.p, G.g_contrib.p,
+             G.sky_blk_i.p, G.sky_blk_j.p, G.fixed.p, G.S.p, G.g.p, G.g_dir.p, G.Ddiag.p, G.n_sky, nf};
+  const int nthreads = G.n_sky * 36 + 6 * nf;
+  assemble_kernel<<<(nthreads + 255) / 256, 256, 0, e->stream>>>(aa, lambda);
+  SolveArgs so{G.S.p, G.sky_first.p, G.sky_row.p, G.sky_last.p, G.g.p, G.Linv.p, G.x.p, G.status.p, nf};
+  skyline_solve_kernel<<<1, 256, 0, e->stream>>>(so);
+  PBA_HIP(hipGetLastError());
+  int status = 0;
+  PBA_HIP(hipMemcpyAsync(&status, G.status.p, sizeof(int), hipMemcpyDeviceToHost, e->stream));
+  PBA_HIP(hipStreamSynchronize(e->stream));
+  if (solver_status) *solver_status = status;
+  if (status != 0) {
+    if (model_decrease) *model_decrease = 0.0;
+    return PBA_OK;
+  }
+  const int gp = (nf + kBlockThreads - 1) / kBlockThreads;
+  const int gq = (G.n_gn_points + kBlockThreads - 1) / kBlockThreads;
+  pose_update_kernel<<<gp, kBlockThreads, 0, e->stream>>>(e->poses.p, G.x.p, G.g_dir.p, G.Ddiag.p, G.fixed.p,
+                                                          G.poses_new.p, G.red.p, nf);
+  PointUpdateArgs pa_{G.pt_data.p, G.pt_first.p, G.pt_nblk.p, G.pt_orig.p, G.pt_host.p, G.gn_target.p,
+                      G.blk_schur.p, G.x.p, G.fixed.p, e->rho.p, G.rho_new.p, G.drho.p, G.red.p + 2 * gp,
+                      G.n_gn_points};
+  point_update_kernel<<<gq, kBlockThreads, 0, e->stream>>>(pa_, lambda);
+  PBA_HIP(hipGetLastError());
+  double dg, dD;
+  if (int rc = read_red(e, gp + gq, &dg, &dD)) return rc;
+  // LM model decrease L(0) − L(δ) = −gᵀδ − ½δᵀHδ = ½(λ δᵀDδ − gᵀδ)   since (H + λD)δ = −g
+  if (model_decrease) *model_decrease = 0.5 * (lambda * dD - dg);
+  return PBA_OK;
+}
+
+int candidate_cost(pba_engine* e, double* cost) {
+  GnData& G = e->gn;
+  launch_pairs(e, G.poses_new.p, G.pairs_new.p);
+  if (int rc = launch_cost_only(e, G.pairs_new.p, G.rho_new.p)) return rc;
+  return total_cost(e, cost, nullptr);
+}
+
+int accept(pba_engine* e) {
+  GnData& G = e->gn;
+  PBA_HIP(hipMemcpyAsync(e->poses.p, G.poses_new.p, sizeof(double) * 7 * e->n_frames, hipMemcpyDeviceToDevice, e->stream));
+  PBA_HIP(hipMemcpyAsync(e->rho.p, G.rho_new.p, sizeof(double) * e->n_points, hipMemcpyDeviceToDevice, e->stream));
+  return PBA_OK;
+}
+
+double now_ms() {
+  return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+}  // namespace
+
+extern "C" {
+
+int pba_set_fixed_frames(pba_engine* e, int32_t n, const int32_t* frames) {
+  if (!e || n < 0 || (n > 0 && !frames)) return fail(PBA_ERR_INVALID_ARGUMENT, "bad fixed-frame arguments");
+  if (e->n_frames <= 0) return fail(PBA_ERR_NOT_READY, "pba_set_frames first");
+  std::vector<uint8_t> f(e->n_frames, 0);
+  for (int i = 0; i < n; ++i) {
+    if (frames[i] < 0 || frames[i] >= e->n_frames) return fail(PBA_ERR_INVALID_ARGUMENT, "fixed frame out of range");
+    f[frames[i]] = 1;
+  }
+  e->gn.fixed_h = f;
+  e->gn.prepared = false;
+  return PBA_OK;
+}
+
+int pba_gn_linearize(pba_engine* e, double* cost) {
+  if (int rc = ensure_prepared(e)) return rc;
+  return linearize(e, cost);
+}
+
+int pba_gn_step(pba_engine* e, double lambda, double* model_decrease, int32_t* solver_status) {
+  if (int rc = ensure_prepared(e)) return rc;
+  if (!(lambda >= 0.0)) return fail(PBA_ERR_INVALID_ARGUMENT, "lambda must be >= 0");
+  int st = 0;
+  const int rc = gn_step(e, lambda, model_decrease, &st);
+  if (solver_status) *solver_status = st;
+  return rc;
+}
+
+int pba_gn_candidate_cost(pba_engine* e, double* cost) {
+  if (int rc = ensure_prepared(e)) return rc;
+  if (!cost) return fail(PBA_ERR_INVALID_ARGUMENT, "null cost");
+  return candidate_cost(e, cost);
+}
+
+int pba_gn_accept(pba_engine* e) {
+  if (int rc = ensure_prepared(e)) return rc;
+  return accept(e);
+}
+
+int pba_get_state(pba_engine* e, double* poses, double* inv_dist) {
+  if (!e) return fail(PBA_ERR_INVALID_ARGUMENT, "null engine");
+  if (!e->state_set) return fail(PBA_ERR_NOT_READY, "pba_set_state first");
+  if (int rc = check_device(e)) return rc;
+  if (poses) PBA_HIP(hipMemcpyAsync(poses, e->poses.p, sizeof(double) * 7 * e->n_frames, hipMemcpyDeviceToHost, e->stream));
+  if (inv_dist) PBA_HIP(hipMemcpyAsync(inv_dist, e->rho.p, sizeof(double) * e->n_points, hipMemcpyDeviceToHost, e->stream));
+  PBA_HIP(hipStreamSynchronize(e->stream));
+  return PBA_OK;
+}
+
+int pba_gn_get_reduced_system(pba_engine* e, double* S_dense, double* g) {
+  if (int rc = ensure_prepared(e)) return rc;
+  GnData& G = e->gn;
+  const int nf = e->n_frames;
+  std::vector<int> first(nf), row(nf + 1);
+  PBA_HIP(hipMemcpy(first.data(), G.sky_first.p, sizeof(int) * nf, hipMemcpyDeviceToHost));
+  PBA_HIP(hipMemcpy(row.data(), G.sky_row.p, sizeof(int) * (nf + 1), hipMemcpyDeviceToHost));
+  if (S_dense) {
+    std::vector<double> sky((size_t)G.n_sky * 36);
+    PBA_HIP(hipMemcpy(sky.data(), G.S.p, sizeof(double) * sky.size(), hipMemcpyDeviceToHost));
+    const size_t n = 6 * (size_t)nf;
+    std::fill(S_dense, S_dense + n * n, 0.0);
+    for (int i = 0; i < nf; ++i)
+      for (int j = first[i]; j <= i; ++j) {
+        const double* B = &sky[((size_t)row[i] + (j - first[i])) * 36];
+        for (int r = 0; r < 6; ++r)
+          for (int c = 0; c < 6; ++c) {
+            S_dense[(6 * i + r) * n + 6 * j + c] = B[r * 6 + c];
+            S_dense[(6 * j + c) * n + 6 * i + r] = B[r * 6 + c];
+          }
+      }
+  }
+  if (g) PBA_HIP(hipMemcpy(g, G.g.p, sizeof(double) * 6 * nf, hipMemcpyDeviceToHost));
+  return PBA_OK;
+}
+
+int pba_gn_get_step(pba_engine* e, double* dposes, double* drho) {
+  if (int rc = ensure_prepared(e)) return rc;
+  GnData& G = e->gn;
+  if (dposes) PBA_HIP(hipMemcpy(dposes, G.x.p, sizeof(double) * 6 * e->n_frames, hipMemcpyDeviceToHost));
+  if (drho) PBA_HIP(hipMemcpy(drho, G.drho.p, sizeof(double) * e->n_points, hipMemcpyDeviceToHost));
+  return PBA_OK;
+}
+
+// Levenberg-Marquardt (trust_region_minimizer.cc + levenberg_marquardt_strategy.cc semantics):
+// μ = 1/radius, step accepted when (cost − cost_new)/model_decrease > min_relative_decrease (1e-3);
+// success: radius /= max(1/3, 1 − (2ρ − 1)³), decrease factor 2; failure: radius /= factor, factor *= 2.
+int pba_solve(pba_engine* e, const pba_solver_options* o, pba_solver_summary* sum) {
+  if (int rc = ensure_prepared(e)) return rc;
+  pba_solver_options opt{};
+  opt.max_iterations = 20;
+  opt.initial_trust_region_radius = 1e4;
+  opt.function_tolerance = 1e-6;
+  opt.parameter_tolerance = 1e-8;
+  opt.min_relative_decrease = 1e-3;
+  if (o) opt = *o;
+  pba_solver_summary s{};
+  const double t0 = now_ms();
+  double cost = 0.0;
+  double t = now_ms();
+  if (int rc = linearize(e, &cost)) return rc;
+  s.linearize_ms += now_ms() - t;
+  s.initial_cost = cost;
+  double radius = opt.initial_trust_region_radius, factor = 2.0;
+  int iter = 0;
+  s.termination = PBA_TERMINATION_MAX_ITERATIONS;
+  for (; iter < opt.max_iterations; ++iter) {
+    const double lambda = 1.0 / radius;
+    double model = 0.0;
+    int st = 0;
+    t = now_ms();
+    if (int rc = gn_step(e, lambda, &model, &st)) return rc;
+    s.solve_ms += now_ms() - t;
+    if (st != 0 || !(model > 0.0)) {  // non-positive-definite or no predicted decrease: shrink the region
+      radius /= factor;
+      factor *= 2.0;
+      ++s.unsuccessful_steps;
+      if (radius < 1e-32) { s.termination = PBA_TERMINATION_FAILURE; break; }
+      continue;
+    }
+    double cost_new = 0.0;
+    t = now_ms();
+    if (int rc = candidate_cost(e, &cost_new)) return rc;
+    s.cost_ms += now_ms() - t;
+    const double rel = (cost - cost_new) / model;
+    if (rel > opt.min_relative_decrease && std::isfinite(cost_new)) {
+      if (int rc = accept(e)) return rc;
+      const double decrease = cost - cost_new;
+      ++s.successful_steps;
+      radius = radius / std::max(1.0 / 3.0, 1.0 - std::pow(2.0 * rel - 1.0, 3));
+      factor = 2.0;
+      cost = cost_new;
+      if (decrease <= opt.function_tolerance * cost) {  // Ceres: |Δcost| ≤ function_tolerance · cost
+        s.termination = PBA_TERMINATION_CONVERGENCE;
+        ++iter;
+        break;
+      }
+      t = now_ms();
+      if (int rc = linearize(e, nullptr)) return rc;
+      PBA_HIP(hipStreamSynchronize(e->stream));
+      s.linearize_ms += now_ms() - t;
+    } else {
+      ++s.unsuccessful_steps;
+      radius /= factor;
+      factor *= 2.0;
+      if (radius < 1e-32) { s.termination = PBA_TERMINATION_FAILURE; break; }
+    }
+  }
+  s.iterations = iter;
+  s.final_cost = cost;
+  s.total_ms = now_ms() - t0;
+  if (sum) *sum = s;
+  return PBA_OK;
+}
+
+}  // extern "C"

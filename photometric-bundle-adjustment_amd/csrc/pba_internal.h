@@ -1,0 +1,310 @@
+// pba_internal.h — engine state, kernel argument blocks and the per-row residual/Jacobian arithmetic
+// shared by the Ceres-mode kernels (pba_engine.hip) and the Gauss-Newton kernels (pba_gn.hip).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "pba.h"
+#include "pba_device.h"
+
+namespace pba {
+namespace detail {
+
+constexpr int kBlockThreads = 256;
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+// Relative pose of one (host, target) keyframe pair, fp64, 128 B (L2-resident: 4k pairs = 512 KB at C4).
+struct alignas(16) PairRec {
+  double R[9];
+  double t[3];
+  int host_cam, target_cam, target, host;
+  int pad1[4];
+};
+static_assert(sizeof(PairRec) == 128, "PairRec layout");
+
+struct KernelArgs {
+  const uint8_t* images;
+  int width, height;
+  long long frame_stride;
+  const float* intr;             // 8 floats per camera (Jacobian chain)
+  const double* intr_d;          // 8 doubles per camera (warp / projection)
+  const int* block_point;
+  const int* block_pair;
+  const PairRec* pairs;
+  const double2* u_ref;          // per point
+  const float* host_int;         // P per point
+  const double* rho;             // per point (state)
+  const double2* u_obs;          // per block (geometric)
+  float* out;                    // records
+  float* cost;                   // per block
+  uint8_t* valid;                // per block
+  int n_blocks;
+  int P;
+  float huber;
+  float pattern[2 * PBA_MAX_PATTERN];
+};
+
+// XCD-aware tile order: consecutive logical tiles (→ neighbouring host keyframes → shared target images)
+// land on the same XCD's L2 (blocks are dealt round-robin over the 8 XCDs; speed only, never correctness).
+__device__ __forceinline__ int logical_tile() {
+  const int n = gridDim.x, b = blockIdx.x;
+  const int xcd = b & 7, slot = b >> 3;
+  const int q = n >> 3, rem = n & 7;
+  return xcd * q + min(xcd, rem) + slot;
+}
+
+// Huber loss (loss_function.cc:48-62): cost = ½ρ(s); Corrector weight ρ'(s) (corrector.cc:42-110 — ρ'' ≤ 0
+// for Huber, so Ceres scales r and J by √ρ' and the normal equations by ρ').
+__device__ __forceinline__ float huber_cost(float s, float a) {
+  if (a <= 0.0f || s <= a * a) return 0.5f * s;
+  return 0.5f * (2.0f * a * sqrtf(s) - a * a);
+}
+__device__ __forceinline__ float huber_weight(float s, float a) {
+  if (a <= 0.0f || s <= a * a) return 1.0f;
+  return fmaxf(a * rsqrtf(s), 1.17549435e-38f);
+}
+
+// Sum / AND over the LPB lanes of one block (LPB | 64, groups are aligned lane ranges).
+template <int LPB>
+__device__ __forceinline__ float group_sum(float v) {
+#pragma unroll
+  for (int m = LPB / 2; m >= 1; m >>= 1) v += __shfl_xor(v, m, 64);
+  return v;
+}
+template <int LPB>
+__device__ __forceinline__ int group_and(int v) {
+#pragma unroll
+  for (int m = LPB / 2; m >= 1; m >>= 1) v &= __shfl_xor(v, m, 64);
+  return v;
+}
+
+// One residual row with its tangent Jacobian: r, ∂r/∂[υ_h ω_h], ∂r/∂[υ_t ω_t], ∂r/∂ρ.
+struct Row {
+  float r = 0.0f, jr = 0.0f;
+  Vec3 hv = {0, 0, 0}, hw = {0, 0, 0}, tv = {0, 0, 0}, tw = {0, 0, 0};
+  int ok = 1;
+};
+
+// Photometric row k of block blk (photometric_error.h:139-182 with the bilinear interpolator; the
+// Jacobian chain of pba_device.h).  Warp and projection in fp64, chain in fp32.
+template <int MODEL, bool JAC>
+__device__ __forceinline__ Row photometric_row(const KernelArgs& a, int blk, int k) {
+  Row o;
+  const int P = a.P;
+  const int pt = a.block_point[blk];
+  const PairRec& pp = a.pairs[a.block_pair[blk]];
+  const double* khd = a.intr_d + 8 * pp.host_cam;
+  const double* ktd = a.intr_d + 8 * pp.target_cam;
+  const double2 ur = a.u_ref[pt];
+  const double rho = a.rho[pt];
+  const float Ih = a.host_int[(long long)pt * P + k];
+  // p̃ = R_th b_k + ρ t_th  (photometric_error.h:158-159)
+  const Vec3d b = unproject<MODEL>(khd, ur.x + (double)a.pattern[2 * k], ur.y + (double)a.pattern[2 * k + 1]);
+  const Vec3d Rb = mat_mul(pp.R, b);
+  const Vec3d p = {Rb.x + rho * pp.t[0], Rb.y + rho * pp.t[1], Rb.z + rho * pp.t[2]};
+  const bool dom = in_domain<MODEL>(ktd, p);
+  float I = 0.0f, gx = 0.0f, gy = 0.0f;
+  if (dom) {
+    double u, v;
+    project<MODEL>(ktd, p, u, v);
+    bilinear(a.images + pp.target * a.frame_stride, a.width, a.height, u, v, I, gx, gy);
+  }
+  o.r = I - Ih;  // photometric_error.h:179
+  o.ok = dom && isfinite(o.r);
+  if (JAC && dom) {
+    // q = ∇I · ∂π/∂p̃ (1×3)
+    const Vec3 pf = to_f(p), bf = to_f(b);
+    Vec3 du, dv;
+    project_jac<MODEL>(a.intr + 8 * pp.target_cam, pf, du, dv);
+    const Vec3 q = {gx * du.x + gy * dv.x, gx * du.y + gy * dv.y, gx * du.z + gy * dv.z};
+    const Vec3 qR = row_mul(q, pp.R);
+    const float rf = (float)rho;
+    o.hv = {rf * qR.x, rf * qR.y, rf * qR.z};
+    o.hw = cross(bf, qR);  // −(qR)×b
+    o.tv = {-rf * q.x, -rf * q.y, -rf * q.z};
+    o.tw = cross(q, pf);   // q·[p̃]×
+    o.jr = q.x * (float)pp.t[0] + q.y * (float)pp.t[1] + q.z * (float)pp.t[2];
+  }
+  return o;
+}
+
+// Geometric row k ∈ {0: u, 1: v} of block blk (reprojection.h:105-108): r = u_obs − π_t(T_th · b/ρ).
+template <int MODEL, bool JAC>
+__device__ __forceinline__ Row geometric_row(const KernelArgs& a, int blk, int k) {
+  Row o;
+  const int pt = a.block_point[blk];
+  const PairRec& pp = a.pairs[a.block_pair[blk]];
+  const double2 ur = a.u_ref[pt];
+  const double2 uo = a.u_obs[blk];
+  const double irho = 1.0 / a.rho[pt];
+  const Vec3d b = unproject<MODEL>(a.intr_d + 8 * pp.host_cam, ur.x, ur.y);
+  const Vec3d ph = {b.x * irho, b.y * irho, b.z * irho};
+  const Vec3d Rp = mat_mul(pp.R, ph);
+  const Vec3d p = {Rp.x + pp.t[0], Rp.y + pp.t[1], Rp.z + pp.t[2]};
+  double u, v;
+  project<MODEL>(a.intr_d + 8 * pp.target_cam, p, u, v);
+  o.r = (float)(k == 0 ? uo.x - u : uo.y - v);
+  o.ok = isfinite(o.r);
+  if (JAC) {
+    const Vec3 pf = to_f(p), phf = to_f(ph), Rbf = to_f(mat_mul(pp.R, b));
+    Vec3 du, dv;
+    project_jac<MODEL>(a.intr + 8 * pp.target_cam, pf, du, dv);
+    const Vec3 d = k == 0 ? du : dv;
+    const Vec3 g = {-d.x, -d.y, -d.z};  // ∂r/∂p = −∂π/∂p
+    const Vec3 gR = row_mul(g, pp.R);
+    o.hv = gR;
+    o.hw = cross(phf, gR);
+    o.tv = d;
+    o.tw = cross(g, pf);
+    const float irf = (float)irho;
+    o.jr = -dot(g, Rbf) * irf * irf;
+    o.ok = o.ok && isfinite(o.hv.x + o.hv.y + o.hv.z + o.hw.x + o.hw.y + o.hw.z) &&
+           isfinite(o.tw.x + o.tw.y + o.tw.z + o.tv.x + o.tv.y + o.tv.z + o.jr);
+  }
+  return o;
+}
+
+template <int KIND, int MODEL, bool JAC>
+__device__ __forceinline__ Row eval_row(const KernelArgs& a, int blk, int k) {
+  if (KIND == PBA_RESIDUAL_PHOTOMETRIC) return photometric_row<MODEL, JAC>(a, blk, k);
+  return geometric_row<MODEL, JAC>(a, blk, k);
+}
+
+// ---------------------------------------------------------------------------------------------------------
+// Host-side helpers
+// ---------------------------------------------------------------------------------------------------------
+extern thread_local std::string g_last_error;
+
+inline int fail(int code, const std::string& msg) {
+  g_last_error = msg;
+  return code;
+}
+
+#define PBA_HIP(expr)                                                                          \
+  do {                                                                                         \
+    hipError_t e_ = (expr);                                                                    \
+    if (e_ != hipSuccess)                                                                      \
+      return ::pba::detail::fail(e_ == hipErrorOutOfMemory ? PBA_ERR_OUT_OF_MEMORY : PBA_ERR_DEVICE, \
+                                 std::string(#expr) + ": " + hipGetErrorString(e_));           \
+  } while (0)
+
+template <class T>
+struct DevBuf {
+  T* p = nullptr;
+  size_t n = 0;
+  hipError_t resize(size_t count) {
+    if (count <= n && p) return hipSuccess;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    n = 0;
+    if (count == 0) return hipSuccess;
+    hipError_t e = hipMalloc(&p, count * sizeof(T));
+    if (e == hipSuccess) n = count;
+    return e;
+  }
+  hipError_t upload(const std::vector<T>& h, hipStream_t s) {
+    hipError_t e = resize(h.size());
+    if (e != hipSuccess || h.empty()) return e;
+    return hipMemcpyAsync(p, h.data(), h.size() * sizeof(T), hipMemcpyHostToDevice, s);
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    n = 0;
+  }
+};
+
+// Gauss-Newton state: the symbolic analysis of the normal equations (built once per problem structure) and
+// the device buffers of one linearisation / Schur complement / solve.  See pba_gn.hip for the layouts.
+struct GnData {
+  bool prepared = false;
+  int lpb = 8, bpw = 32;
+  int n_chunks = 0, n_schur = 0, n_gn_points = 0, n_sky = 0;
+  size_t lin_floats = 0, schur_doubles = 0;
+  DevBuf<int> gn_block;          // GN order → original block
+  DevBuf<int4> chunk_desc;       // linearise chunk: first GN block, count, n_targets, partial offset
+  DevBuf<uint8_t> blk_lt;        // GN block → local target slot in its linearise chunk
+  DevBuf<float> blk_schur;       // GN block → 16 floats [Hll gl Wh(6) Wt(6) 0 0]
+  DevBuf<float> part_lin;        // linearise chunk partials (fp32)
+  DevBuf<int> pt_first, pt_nblk, pt_orig;  // GN point → first GN block, block count, original point
+  DevBuf<int4> schur_desc;       // Schur chunk: first GN point, n points, n local poses, partial offset
+  DevBuf<int2> schur_aux;        // Schur chunk: used-pair list offset, n used pairs
+  DevBuf<uchar2> schur_pairs;    // used local pose pairs (a ≤ b) of every Schur chunk
+  DevBuf<int> pt_host, gn_target;  // GN point → host frame; GN block → target frame
+  DevBuf<double> drho;           // last step's δρ (original point order)
+  std::vector<uint8_t> fixed_eff;  // constant frames actually used (requested + unobserved)
+  DevBuf<uint8_t> blk_lv;        // GN block → local pose index of its target in its Schur chunk
+  DevBuf<double> part_schur;     // Schur chunk partials (fp64)
+  DevBuf<double> pt_data;        // GN point → [H'll, gl, Wh(6)] of the last Schur pass (fp64)
+  DevBuf<int> sky_first, sky_row, sky_last;  // skyline profile of the reduced camera system
+  DevBuf<int> sky_cptr, g_cptr;  // contribution lists (CSR) per skyline block / per pose
+  DevBuf<int2> sky_contrib, g_contrib;
+  DevBuf<int> sky_blk_i, sky_blk_j;  // skyline block → (row pose, column pose)
+  DevBuf<double> S, g, g_dir, Ddiag, Linv, x;  // skyline system, rhs, direct gradient, LM diagonal, L_kk⁻¹, step
+  DevBuf<uint8_t> fixed;
+  std::vector<uint8_t> fixed_h;
+  DevBuf<double> poses_new, rho_new, red;
+  DevBuf<int> status;
+  DevBuf<PairRec> pairs_new;
+  std::vector<double> red_h;
+  int red_slots = 0;
+};
+
+}  // namespace detail
+}  // namespace pba
+
+struct pba_engine {
+  pba_options opt{};
+  hipStream_t own_stream = nullptr;
+  hipStream_t stream = nullptr;
+  int n_cams = 0, n_frames = 0, n_points = 0, n_blocks = 0, n_pairs = 0;
+  int width = 0, height = 0, P = 0;
+  bool have_images = false;
+  std::vector<int> frame_cam_h, point_host_h, block_point_h, block_target_h, pair_of_h, pair_host_h, pair_target_h;
+  std::vector<float> pattern_h;
+  pba::detail::DevBuf<float> intr;
+  pba::detail::DevBuf<double> intr_d;
+  pba::detail::DevBuf<int> frame_cam;
+  pba::detail::DevBuf<uint8_t> images;
+  pba::detail::DevBuf<double2> u_ref;
+  pba::detail::DevBuf<float> host_int;
+  pba::detail::DevBuf<int> block_point, block_pair;
+  pba::detail::DevBuf<double2> u_obs;
+  pba::detail::DevBuf<int> pair_host, pair_target;
+  pba::detail::DevBuf<pba::detail::PairRec> pairs;
+  pba::detail::DevBuf<double> poses, rho;
+  pba::detail::DevBuf<float> out, cost;
+  pba::detail::DevBuf<uint8_t> valid;
+  bool state_set = false;
+  bool evaluated = false;
+  bool timing = false;
+  std::vector<hipEvent_t> ev_pool;   // start/stop pairs, reused
+  size_t ev_used = 0;
+  pba::detail::GnData gn;
+
+  int R() const { return opt.residual_kind == PBA_RESIDUAL_PHOTOMETRIC ? P : 2; }
+};
+
+namespace pba {
+namespace detail {
+
+inline int check_device(pba_engine* e) {
+  PBA_HIP(hipSetDevice(e->opt.device));
+  return PBA_OK;
+}
+
+// Kernel arguments describing the engine's current problem and state.
+KernelArgs make_kernel_args(pba_engine* e, const PairRec* pairs, const double* rho);
+
+// Pair kernel launch (relative poses of every (host, target) pair from an fp64 pose array).
+void launch_pairs(pba_engine* e, const double* poses, PairRec* pairs);
+
+// Residual-only evaluation writing only per-block costs/validity (state given by pairs/rho).
+int launch_cost_only(pba_engine* e, const PairRec* pairs, const double* rho);
+
+}  // namespace detail
+}  // namespace pba

@@ -28,6 +28,22 @@ class Options(C.Structure):
                 ("huber_width", C.c_float)]
 
 
+class SolverOptions(C.Structure):
+    _fields_ = [("max_iterations", C.c_int32), ("pad_", C.c_int32), ("initial_trust_region_radius", C.c_double),
+                ("function_tolerance", C.c_double), ("parameter_tolerance", C.c_double),
+                ("min_relative_decrease", C.c_double)]
+
+
+class SolverSummary(C.Structure):
+    _fields_ = [("iterations", C.c_int32), ("successful_steps", C.c_int32), ("unsuccessful_steps", C.c_int32),
+                ("termination", C.c_int32), ("initial_cost", C.c_double), ("final_cost", C.c_double),
+                ("total_ms", C.c_double), ("linearize_ms", C.c_double), ("solve_ms", C.c_double),
+                ("cost_ms", C.c_double)]
+
+    def as_dict(self):
+        return {f: getattr(self, f) for f, _ in self._fields_}
+
+
 def build(force: bool = False) -> str:
     """Compile csrc/libpba.so for gfx950 with hipcc (in-tree)."""
     args = ["make", "-s", "-C", CSRC]
@@ -77,6 +93,15 @@ def lib():
         "pba_device_records": ([vp, C.POINTER(vp), C.POINTER(vp), C.POINTER(vp)], C.c_int),
         "pba_enable_kernel_timing": ([vp, i32], C.c_int),
         "pba_get_kernel_timing": ([vp, C.POINTER(C.c_double), C.POINTER(i32)], C.c_int),
+        "pba_set_fixed_frames": ([vp, i32, vp], C.c_int),
+        "pba_gn_linearize": ([vp, C.POINTER(C.c_double)], C.c_int),
+        "pba_gn_step": ([vp, C.c_double, C.POINTER(C.c_double), C.POINTER(i32)], C.c_int),
+        "pba_gn_candidate_cost": ([vp, C.POINTER(C.c_double)], C.c_int),
+        "pba_gn_accept": ([vp], C.c_int),
+        "pba_solve": ([vp, C.POINTER(SolverOptions), C.POINTER(SolverSummary)], C.c_int),
+        "pba_get_state": ([vp, vp, vp], C.c_int),
+        "pba_gn_get_reduced_system": ([vp, vp, vp], C.c_int),
+        "pba_gn_get_step": ([vp, vp, vp], C.c_int),
     }
     for name, (argt, rest) in sig.items():
         f = getattr(L, name)
@@ -196,6 +221,56 @@ class Engine:
         ms, n = C.c_double(), C.c_int32()
         _check(self._L.pba_get_kernel_timing(self._h, C.byref(ms), C.byref(n)), "pba_get_kernel_timing")
         return ms.value, n.value
+
+    # -- on-device Gauss-Newton / LM ---------------------------------------------------------------
+    def set_fixed_frames(self, frames):
+        f = np.ascontiguousarray(frames, np.int32)
+        _check(self._L.pba_set_fixed_frames(self._h, f.shape[0], _p(f) if f.size else None), "pba_set_fixed_frames")
+
+    def gn_linearize(self) -> float:
+        c = C.c_double()
+        _check(self._L.pba_gn_linearize(self._h, C.byref(c)), "pba_gn_linearize")
+        return c.value
+
+    def gn_step(self, lam: float):
+        m, st = C.c_double(), C.c_int32()
+        _check(self._L.pba_gn_step(self._h, lam, C.byref(m), C.byref(st)), "pba_gn_step")
+        return m.value, st.value
+
+    def gn_candidate_cost(self) -> float:
+        c = C.c_double()
+        _check(self._L.pba_gn_candidate_cost(self._h, C.byref(c)), "pba_gn_candidate_cost")
+        return c.value
+
+    def gn_accept(self):
+        _check(self._L.pba_gn_accept(self._h), "pba_gn_accept")
+
+    def solve(self, max_iterations=20, initial_trust_region_radius=1e4, function_tolerance=1e-6,
+              min_relative_decrease=1e-3) -> dict:
+        o = SolverOptions(max_iterations, 0, initial_trust_region_radius, function_tolerance, 1e-8,
+                          min_relative_decrease)
+        s = SolverSummary()
+        _check(self._L.pba_solve(self._h, C.byref(o), C.byref(s)), "pba_solve")
+        return s.as_dict()
+
+    def get_state(self):
+        poses = np.empty((self.n_frames, 7), np.float64)
+        rho = np.empty(self.n_points, np.float64)
+        _check(self._L.pba_get_state(self._h, _p(poses), _p(rho)), "pba_get_state")
+        return poses, rho
+
+    def gn_reduced_system(self):
+        n = 6 * self.n_frames
+        S = np.empty((n, n), np.float64)
+        g = np.empty(n, np.float64)
+        _check(self._L.pba_gn_get_reduced_system(self._h, _p(S), _p(g)), "pba_gn_get_reduced_system")
+        return S, g
+
+    def gn_last_step(self):
+        dp = np.empty((self.n_frames, 6), np.float64)
+        dr = np.empty(self.n_points, np.float64)
+        _check(self._L.pba_gn_get_step(self._h, _p(dp), _p(dr)), "pba_gn_get_step")
+        return dp, dr
 
     def close(self):
         if self._h:

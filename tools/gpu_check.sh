@@ -10,7 +10,7 @@ TAG=${TAG:-run}
 ok() { local rc=$1; [ "$rc" -eq 0 ] || [ "$rc" -eq 1 ]; }
 
 if [ "${TESTS:-1}" = "1" ]; then
-  timeout -k 10 900 python -m pytest tests -m gpu -q -rA > gpurun_out/pytest_gpu.log 2>&1; rc=$?
+  timeout -k 10 900 python -m pytest tests -m gpu -q -rA ${PYTEST_ARGS:-} > gpurun_out/pytest_gpu.log 2>&1; rc=$?
   echo "pytest rc=$rc"; grep -E "passed|failed" gpurun_out/pytest_gpu.log | tail -3
   ok $rc || exit $rc
   timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1; rc=$?
