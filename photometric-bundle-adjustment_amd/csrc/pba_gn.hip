@@ -832,6 +832,7 @@ int gn_prepare(pba_engine* e) {
   PBA_HIP(G.sky_blk_j.upload(bj, st));
   PBA_HIP(G.fixed.upload(fixed, st));
   PBA_HIP(G.S.resize((size_t)G.n_sky * 36));
+  PBA_HIP(G.L.resize((size_t)G.n_sky * 36));
   PBA_HIP(G.g.resize((size_t)nf * 6));
   PBA_HIP(G.g_dir.resize((size_t)nf * 6));
   PBA_HIP(G.Ddiag.resize((size_t)nf * 6));
@@ -936,7 +937,8 @@ int gn_step(pba_engine* e, double lambda, double* model_decrease, int* solver_st
              G.sky_blk_i.p, G.sky_blk_j.p, G.fixed.p, G.S.p, G.g.p, G.g_dir.p, G.Ddiag.p, G.n_sky, nf};
   const int nthreads = G.n_sky * 36 + 6 * nf;
   assemble_kernel<<<(nthreads + 255) / 256, 256, 0, e->stream>>>(aa, lambda);
-  SolveArgs so{G.S.p, G.sky_first.p, G.sky_row.p, G.sky_last.p, G.g.p, G.Linv.p, G.x.p, G.status.p, nf};
+  PBA_HIP(hipMemcpyAsync(G.L.p, G.S.p, sizeof(double) * 36 * (size_t)G.n_sky, hipMemcpyDeviceToDevice, e->stream));
+  SolveArgs so{G.L.p, G.sky_first.p, G.sky_row.p, G.sky_last.p, G.g.p, G.Linv.p, G.x.p, G.status.p, nf};
   skyline_solve_kernel<<<1, 256, 0, e->stream>>>(so);
   PBA_HIP(hipGetLastError());
   int status = 0;
