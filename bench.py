@@ -98,6 +98,51 @@ def cpu_baseline(pb, images_host, budget_s: float, threads: int):
                       f"Jet<15> dual-number AutoDiff (the reference's Ceres AutoDiff arithmetic, restated)"}
 
 
+def gn_benchmark(eng, n_frames, iters, torch, dist, dev):
+    """ms per Gauss-Newton iteration (BASELINE.json metric, part 2) on the same shard: one iteration =
+    linearise (r, J, Huber, JᵀJ/Jᵀr partials) + Schur complement + reduced-system assembly + skyline
+    Cholesky solve + pose/point update + candidate cost, with the LM accept/reject decision on the host."""
+    eng.set_fixed_frames(np.array([0, 1], np.int32))
+    lam = 1e-2
+    eng.gn_linearize()
+    eng.gn_step(lam)  # warm-up (symbolic analysis happened at the first call)
+    eng.gn_candidate_cost()
+    parts = {"linearize_ms": 0.0, "step_ms": 0.0, "cost_ms": 0.0}
+    accepted = 0
+    cost = eng.gn_linearize()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        t = time.perf_counter()
+        model, st = eng.gn_step(lam)
+        t1 = time.perf_counter()
+        parts["step_ms"] += 1e3 * (t1 - t)
+        c_new = eng.gn_candidate_cost() if st == 0 else float("inf")
+        t2 = time.perf_counter()
+        parts["cost_ms"] += 1e3 * (t2 - t1)
+        if c_new < cost:
+            eng.gn_accept()
+            accepted += 1
+            lam = max(lam / 3, 1e-8)
+        else:
+            lam *= 4
+        t3 = time.perf_counter()
+        cost = eng.gn_linearize()  # next iteration's linearisation (counted in every iteration)
+        parts["linearize_ms"] += 1e3 * (time.perf_counter() - t3)
+    torch.cuda.synchronize()
+    total = time.perf_counter() - t0
+    t = torch.tensor([total], dtype=torch.float64, device=dev)
+    if dist is not None:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    n = iters
+    return {"ms_per_iteration": 1e3 * float(t[0]) / n, "iterations": n, "accepted": accepted,
+            "breakdown_ms_per_iteration": {k: v / n for k, v in parts.items()},
+            "note": "host wall clock incl. the per-iteration D2H of cost / model decrease / solver status; "
+                    "noise-textured images, so steps are not expected to converge — timing only"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -110,6 +155,7 @@ def main():
     ap.add_argument("--height", type=int, default=480)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--gn-iterations", type=int, default=5)
     args = ap.parse_args()
 
     import torch
@@ -177,6 +223,10 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed_max, kern_avg_ms = float(t[0]), float(t[1])
 
+    gn = None
+    if args.gn_iterations > 0:
+        gn = gn_benchmark(eng, F, args.gn_iterations, torch, dist if world > 1 else None, dev)
+
     if rank == 0:
         ms_per_step = 1e3 * elapsed_max / args.steps
         total_blocks = n_blocks * world * args.steps
@@ -229,6 +279,7 @@ def main():
                 "kernel_avg_us": kern_avg_ms * 1e3,
             },
             "cpu_baseline": cpu,
+            "gn": gn,
         }
         print(json.dumps(out), flush=True)
     eng.close()
