@@ -29,6 +29,7 @@
 #include <algorithm>
 #include <chrono>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <numeric>
@@ -490,6 +491,215 @@ __global__ __launch_bounds__(256) void skyline_solve_kernel(const SolveArgs a) {
 }
 
 // ------------------------------------------------------------------------------------------------
+// band_solve_kernel<B>: the same factorisation when every block row satisfies first(i) ≥ i − B (the
+// structure of windowed/sequential BA — C3/C4 have B = 4).  The active window of the factor (block rows
+// k..k+B, B+1 blocks each) lives in LDS as a ring; block row k+B+2 is prefetched into registers two steps
+// ahead; forward substitution is fused into the factor loop; finished rows of L and L_kk⁻¹ go to a dense
+// band buffer in global memory for the backward pass, which prefetches its column panel one step ahead.
+// ------------------------------------------------------------------------------------------------
+struct BandArgs {
+  const double* S;      // skyline reduced system
+  const int* first;
+  const int* row;
+  const double* g;
+  double* Lband;        // N × (B+1) blocks × 36, block c of row i = column i − B + c
+  double* Linv;         // N × 36
+  double* x;            // y during the forward pass, then the step
+  int* status;
+  int N;
+};
+
+template <int B>
+__global__ __launch_bounds__(256) void band_solve_kernel(const BandArgs a) {
+  constexpr int W = B + 1;
+  constexpr int ROWF = W * 36;
+  constexpr int PF = (ROWF + 255) / 256;
+  constexpr int COLF = B * 36 + 36 + 6;  // backward panel: L_(k+q),k (q = 1..B), L_kk⁻¹, y_k
+  constexpr int PB = (COLF + 255) / 256;
+  __shared__ double win[W * ROWF];
+  __shared__ double sLi[36], sv[6];
+  __shared__ double ring[W * 6];
+  __shared__ int s_fail;
+  const int tid = threadIdx.x, N = a.N;
+
+  auto fetch_row = [&](int i, double* regs) {
+#pragma unroll
+    for (int q = 0; q < PF; ++q) {
+      const int idx = tid + q * 256;
+      double v = 0.0;
+      if (i < N && idx < ROWF) {
+        const int c = idx / 36, e = idx % 36, j = i - B + c;
+        if (j >= a.first[i] && j <= i) v = a.S[((long long)a.row[i] + (j - a.first[i])) * 36 + e];
+      }
+      regs[q] = v;
+    }
+  };
+  auto store_row = [&](int i, const double* regs) {
+    double* r = win + (i % W) * ROWF;
+#pragma unroll
+    for (int q = 0; q < PF; ++q) {
+      const int idx = tid + q * 256;
+      if (idx < ROWF) r[idx] = regs[q];
+    }
+  };
+
+  if (tid == 0) s_fail = 0;
+  for (int i = 0; i < W; ++i) {
+    double r[PF];
+    fetch_row(i, r);
+    store_row(i, r);
+  }
+  if (tid < W * 6) ring[tid] = 0.0;
+  double pre[PF];
+  fetch_row(W, pre);
+  __syncthreads();
+
+  for (int k = 0; k < N; ++k) {
+    double nxt[PF];
+    fetch_row(k + W + 1, nxt);  // in flight during this step
+    double* rk = win + (k % W) * ROWF;
+    if (tid == 0) {
+      double L[36], Li[36];
+      if (!chol6(rk + B * 36, L)) {
+        s_fail = k + 1;
+      } else {
+        inv_lower6(L, Li);
+        for (int e = 0; e < 36; ++e) {
+          rk[B * 36 + e] = L[e];
+          sLi[e] = Li[e];
+        }
+      }
+    }
+    __syncthreads();
+    if (s_fail) {
+      if (tid == 0) *a.status = s_fail;
+      return;
+    }
+    // forward substitution, fused: b_k = −g_k − Σ_j L_kj y_j ; y_k = L_kk⁻¹ b_k
+    if (tid < 6) {
+      double s = -a.g[6 * k + tid];
+#pragma unroll
+      for (int c = 0; c < B; ++c) {
+        const int j = k - B + c;
+        if (j < 0) continue;
+        const double* Lb = rk + c * 36;
+        const double* yj = ring + (j % W) * 6;
+        for (int m = 0; m < 6; ++m) s -= Lb[tid * 6 + m] * yj[m];
+      }
+      sv[tid] = s;
+    }
+    // column panel L_ik = A_ik · L_kk⁻ᵀ for i = k+1..k+B (two phases: read, barrier, write)
+    const int nk = min(B, N - 1 - k);
+    constexpr int PP = (B * 36 + 255) / 256;
+    double pv[PP];
+#pragma unroll
+    for (int q = 0; q < PP; ++q) {
+      const int idx = tid + q * 256;
+      pv[q] = 0.0;
+      if (idx < nk * 36) {
+        const int ii = 1 + idx / 36, e = idx % 36, r = e / 6, c = e % 6;
+        const double* A = win + ((k + ii) % W) * ROWF + (B - ii) * 36;
+        double v = 0.0;
+        for (int m = 0; m <= c; ++m) v += A[r * 6 + m] * sLi[c * 6 + m];
+        pv[q] = v;
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < PP; ++q) {
+      const int idx = tid + q * 256;
+      if (idx < nk * 36) {
+        const int ii = 1 + idx / 36, e = idx % 36;
+        win[((k + ii) % W) * ROWF + (B - ii) * 36 + e] = pv[q];
+      }
+    }
+    if (tid < 6) {
+      double y = 0.0;
+      for (int m = 0; m <= tid; ++m) y += sLi[tid * 6 + m] * sv[m];
+      ring[(k % W) * 6 + tid] = y;
+      a.x[6 * k + tid] = y;
+    }
+    __syncthreads();
+    // trailing update A_ij −= L_ik L_jkᵀ, k < j ≤ i ≤ k+nk
+    const int npairs = nk * (nk + 1) / 2;
+    for (int idx = tid; idx < npairs * 36; idx += 256) {
+      const int pidx = idx / 36, e = idx % 36, r = e / 6, c = e % 6;
+      int ii = 0;
+      while ((ii + 1) * (ii + 2) / 2 <= pidx) ++ii;
+      const int jj = pidx - ii * (ii + 1) / 2;
+      const int i = k + 1 + ii, j = k + 1 + jj;
+      const double* Li_ = win + (i % W) * ROWF + (k - i + B) * 36;
+      const double* Lj_ = win + (j % W) * ROWF + (k - j + B) * 36;
+      double s = 0.0;
+      for (int m = 0; m < 6; ++m) s += Li_[r * 6 + m] * Lj_[c * 6 + m];
+      win[(i % W) * ROWF + (j - i + B) * 36 + e] -= s;
+    }
+    // row k of L and L_kk⁻¹ to global for the backward pass
+    for (int idx = tid; idx < ROWF; idx += 256) a.Lband[(long long)k * ROWF + idx] = rk[idx];
+    if (tid < 36) a.Linv[(long long)k * 36 + tid] = sLi[tid];
+    __syncthreads();
+    store_row(k + W, pre);  // reuses row k's slot
+#pragma unroll
+    for (int q = 0; q < PF; ++q) pre[q] = nxt[q];
+    __syncthreads();
+  }
+  __threadfence();
+  __syncthreads();
+  // backward substitution x_k = L_kk⁻ᵀ (y_k − Σ_q L_(k+q),kᵀ x_(k+q)); column panel prefetched a step ahead
+  __shared__ double col[COLF];
+  auto fetch_col = [&](int k, double* regs) {
+#pragma unroll
+    for (int q = 0; q < PB; ++q) {
+      const int idx = tid + q * 256;
+      double v = 0.0;
+      if (k >= 0 && idx < COLF) {
+        if (idx < B * 36) {
+          const int qq = 1 + idx / 36, e = idx % 36, i = k + qq;
+          if (i < N) v = a.Lband[(long long)i * ROWF + (B - qq) * 36 + e];
+        } else if (idx < B * 36 + 36) {
+          v = a.Linv[(long long)k * 36 + (idx - B * 36)];
+        } else {
+          v = a.x[6 * k + (idx - B * 36 - 36)];
+        }
+      }
+      regs[q] = v;
+    }
+  };
+  if (tid < W * 6) ring[tid] = 0.0;
+  double cpre[PB];
+  fetch_col(N - 1, cpre);
+  __syncthreads();
+  for (int k = N - 1; k >= 0; --k) {
+#pragma unroll
+    for (int q = 0; q < PB; ++q) {
+      const int idx = tid + q * 256;
+      if (idx < COLF) col[idx] = cpre[q];
+    }
+    fetch_col(k - 1, cpre);
+    __syncthreads();
+    if (tid < 6) {
+      double s = col[B * 36 + 36 + tid];
+      for (int q = 1; q <= B; ++q) {
+        if (k + q >= N) break;
+        const double* Lq = col + (q - 1) * 36;
+        const double* xq = ring + ((k + q) % W) * 6;
+        for (int m = 0; m < 6; ++m) s -= Lq[m * 6 + tid] * xq[m];
+      }
+      sv[tid] = s;
+    }
+    __syncthreads();
+    if (tid < 6) {
+      double xk = 0.0;
+      for (int m = tid; m < 6; ++m) xk += col[B * 36 + m * 6 + tid] * sv[m];
+      ring[(k % W) * 6 + tid] = xk;
+      a.x[6 * k + tid] = xk;
+    }
+    __syncthreads();
+  }
+  if (tid == 0) *a.status = 0;
+}
+
+// ------------------------------------------------------------------------------------------------
 // Updates: poses T·exp(δ) (se3.hpp:763-784) and back-substituted inverse distances
 // ------------------------------------------------------------------------------------------------
 __device__ void se3_exp_mul(const double* T, const double* d, double* out) {
@@ -772,6 +982,8 @@ int gn_prepare(pba_engine* e) {
   rowp[0] = 0;
   for (int i = 0; i < nf; ++i) rowp[i + 1] = rowp[i] + (i - first[i] + 1);
   G.n_sky = rowp[nf];
+  G.band = 0;
+  for (int i = 0; i < nf; ++i) G.band = std::max(G.band, i - first[i]);
   for (int k = 0; k < nf; ++k) last[k] = k;
   for (int i = 0; i < nf; ++i)
     for (int k = first[i]; k < i; ++k) last[k] = std::max(last[k], i);
@@ -833,6 +1045,10 @@ int gn_prepare(pba_engine* e) {
   PBA_HIP(G.fixed.upload(fixed, st));
   PBA_HIP(G.S.resize((size_t)G.n_sky * 36));
   PBA_HIP(G.L.resize((size_t)G.n_sky * 36));
+  G.band_kernel = G.band <= 4 ? 4 : (G.band <= 8 ? 8 : (G.band <= 16 ? 16 : 0));
+  if (const char* fs = getenv("PBA_FORCE_SKYLINE"))  // test hook: exercise the general skyline solver
+    if (fs[0] == '1') G.band_kernel = 0;
+  if (G.band_kernel) PBA_HIP(G.Lband.resize((size_t)nf * (G.band_kernel + 1) * 36));
   PBA_HIP(G.g.resize((size_t)nf * 6));
   PBA_HIP(G.g_dir.resize((size_t)nf * 6));
   PBA_HIP(G.Ddiag.resize((size_t)nf * 6));
@@ -937,9 +1153,16 @@ int gn_step(pba_engine* e, double lambda, double* model_decrease, int* solver_st
              G.sky_blk_i.p, G.sky_blk_j.p, G.fixed.p, G.S.p, G.g.p, G.g_dir.p, G.Ddiag.p, G.n_sky, nf};
   const int nthreads = G.n_sky * 36 + 6 * nf;
   assemble_kernel<<<(nthreads + 255) / 256, 256, 0, e->stream>>>(aa, lambda);
-  PBA_HIP(hipMemcpyAsync(G.L.p, G.S.p, sizeof(double) * 36 * (size_t)G.n_sky, hipMemcpyDeviceToDevice, e->stream));
-  SolveArgs so{G.L.p, G.sky_first.p, G.sky_row.p, G.sky_last.p, G.g.p, G.Linv.p, G.x.p, G.status.p, nf};
-  skyline_solve_kernel<<<1, 256, 0, e->stream>>>(so);
+  if (G.band_kernel) {  // banded structure: LDS-window factorisation (the skyline buffer stays untouched)
+    BandArgs ba{G.S.p, G.sky_first.p, G.sky_row.p, G.g.p, G.Lband.p, G.Linv.p, G.x.p, G.status.p, nf};
+    if (G.band_kernel == 4) band_solve_kernel<4><<<1, 256, 0, e->stream>>>(ba);
+    else if (G.band_kernel == 8) band_solve_kernel<8><<<1, 256, 0, e->stream>>>(ba);
+    else band_solve_kernel<16><<<1, 256, 0, e->stream>>>(ba);
+  } else {
+    PBA_HIP(hipMemcpyAsync(G.L.p, G.S.p, sizeof(double) * 36 * (size_t)G.n_sky, hipMemcpyDeviceToDevice, e->stream));
+    SolveArgs so{G.L.p, G.sky_first.p, G.sky_row.p, G.sky_last.p, G.g.p, G.Linv.p, G.x.p, G.status.p, nf};
+    skyline_solve_kernel<<<1, 256, 0, e->stream>>>(so);
+  }
   PBA_HIP(hipGetLastError());
   int status = 0;
   PBA_HIP(hipMemcpyAsync(&status, G.status.p, sizeof(int), hipMemcpyDeviceToHost, e->stream));

@@ -223,7 +223,8 @@ struct DevBuf {
 struct GnData {
   bool prepared = false;
   int lpb = 8, bpw = 32;
-  int n_chunks = 0, n_schur = 0, n_gn_points = 0, n_sky = 0;
+  int n_chunks = 0, n_schur = 0, n_gn_points = 0, n_sky = 0, band = 0, band_kernel = 0;
+  bool force_skyline = false;
   size_t lin_floats = 0, schur_doubles = 0;
   DevBuf<int> gn_block;          // GN order → original block
   DevBuf<int4> chunk_desc;       // linearise chunk: first GN block, count, n_targets, partial offset
@@ -244,7 +245,7 @@ struct GnData {
   DevBuf<int> sky_cptr, g_cptr;  // contribution lists (CSR) per skyline block / per pose
   DevBuf<int2> sky_contrib, g_contrib;
   DevBuf<int> sky_blk_i, sky_blk_j;  // skyline block → (row pose, column pose)
-  DevBuf<double> S, L, g, g_dir, Ddiag, Linv, x;  // skyline system, its factor, rhs, direct gradient, LM diagonal, L_kk⁻¹, step
+  DevBuf<double> S, L, Lband, g, g_dir, Ddiag, Linv, x;  // skyline system, its factor, rhs, direct gradient, LM diagonal, L_kk⁻¹, step
   DevBuf<uint8_t> fixed;
   std::vector<uint8_t> fixed_h;
   DevBuf<double> poses_new, rho_new, red;

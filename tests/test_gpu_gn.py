@@ -112,3 +112,49 @@ def test_c3_sized_gn_iteration_runs():
         dp, dl = eng.gn_last_step()
     assert np.isfinite(dp).all() and np.isfinite(dl).all()
     assert np.isfinite(c_new)
+
+
+@pytest.mark.parametrize("force_skyline", [False, True])
+def test_banded_and_skyline_solvers_agree(force_skyline, monkeypatch):
+    """The banded LDS-window solver (bandwidth ≤ 16 blocks) and the general skyline solver give the
+    reference step; a loop-closure block (host 0 → target n−1) forces the general path."""
+    if force_skyline:
+        monkeypatch.setenv("PBA_FORCE_SKYLINE", "1")
+    pb = synth.make_problem(n_frames=12, n_points=80, width=376, height=240, seed=51, border=12)
+    fixed = (0,)
+    H, g, _ = GR.linearize(pb, pb.poses, pb.rho, 9.0, fixed)
+    _, gS_ref, dp_ref, dl_ref, _ = GR.schur_step(H, g, pb.n_frames, 1e-3, fixed)
+    with make_engine(pb, 9.0, fixed) as eng:
+        eng.gn_linearize()
+        _, st = eng.gn_step(1e-3)
+        dp, dl = eng.gn_last_step()
+    assert st == 0
+    assert np.linalg.norm(dp - dp_ref) <= 1e-3 * np.linalg.norm(dp_ref)
+    assert np.linalg.norm(dl - dl_ref) <= 1e-3 * np.linalg.norm(dl_ref)
+
+
+def test_loop_closure_structure_uses_skyline():
+    pb = synth.make_problem(kind="geometric", n_frames=24, n_points=150, seed=52, obs_sigma=0.2)
+    # add loop-closure observations: points of host 0 seen again by the last keyframe
+    sel = np.nonzero(pb.point_host == 0)[0][:10]
+    extra_t = np.full(len(sel), pb.n_frames - 1, np.int32)
+    Th, Tt = pb.poses_gt[0], pb.poses_gt[pb.n_frames - 1]
+    b = synth.unproject(pb.model, pb.intrinsics[0], pb.u_ref[sel])
+    ph = b / pb.rho_gt[sel, None]
+    pw = (synth.quat_to_rot(Th[:4]) @ ph.T).T + Th[4:]
+    pt = (synth.quat_to_rot(Tt[:4]).T @ (pw - Tt[4:]).T).T
+    uo = synth.project(pb.model, pb.intrinsics[0], pt)
+    ok = pt[:, 2] > 0.5
+    pb = synth.Problem(**{**pb.__dict__, "block_point": np.concatenate([pb.block_point, sel[ok].astype(np.int32)]),
+                          "block_target": np.concatenate([pb.block_target, extra_t[ok]]),
+                          "u_obs": np.concatenate([pb.u_obs, uo[ok]])})
+    fixed = (0,)
+    H, g, _ = GR.linearize(pb, pb.poses, pb.rho, 1.0, fixed)
+    _, _, dp_ref, dl_ref, _ = GR.schur_step(H, g, pb.n_frames, 1e-3, fixed)
+    with make_engine(pb, 1.0, fixed) as eng:
+        eng.gn_linearize()
+        _, st = eng.gn_step(1e-3)
+        dp, dl = eng.gn_last_step()
+    assert st == 0
+    assert np.linalg.norm(dp - dp_ref) <= 1e-3 * np.linalg.norm(dp_ref)
+    assert np.linalg.norm(dl - dl_ref) <= 1e-3 * np.linalg.norm(dl_ref)
