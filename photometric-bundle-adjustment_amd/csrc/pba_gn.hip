@@ -280,6 +280,8 @@ struct AsmArgs {
   double* g;
   double* g_dir;
   double* Ddiag;
+  double* Sband;   // optional dense band copy (block c of row i = column i − B + c), B = band
+  int band;
   int n_sky;
   int n_frames;
 };
@@ -316,6 +318,7 @@ __global__ void assemble_kernel(const AsmArgs a, double lambda) {
       val = sum + lambda * D;
     }
     a.S[tid] = val;
+    if (a.Sband) a.Sband[((long long)i * (a.band + 1) + (j - i + a.band)) * 36 + e] = val;
     return;
   }
   const int t = tid - nS;
@@ -492,33 +495,54 @@ __global__ __launch_bounds__(256) void skyline_solve_kernel(const SolveArgs a) {
 
 // ------------------------------------------------------------------------------------------------
 // band_solve_kernel<B>: the same factorisation when every block row satisfies first(i) ≥ i − B (the
-// structure of windowed/sequential BA — C3/C4 have B = 4).  The active window of the factor (block rows
-// k..k+B, B+1 blocks each) lives in LDS as a ring; block row k+B+2 is prefetched into registers two steps
-// ahead; forward substitution is fused into the factor loop; finished rows of L and L_kk⁻¹ go to a dense
-// band buffer in global memory for the backward pass, which prefetches its column panel one step ahead.
+// structure of windowed/sequential BA — C3/C4 have B = 4).  The assembly also writes S in dense band
+// layout (block c of row i = column i − B + c), so the next block row's address needs no indirection.
+// The active window of the factor (block rows k..k+B) lives in LDS as a ring; block row k+B+2 is
+// prefetched into registers two steps ahead.  Per step: one lane factors the 6×6 diagonal block
+// (reciprocal pivots, no inverse), B·6 lanes solve the column panel L_ik = A_ik L_kk⁻ᵀ row by row, the
+// trailing triangle is updated in parallel, and forward substitution is fused in.  Finished rows of L and
+// the reciprocal pivots go to global memory for the backward pass, which prefetches one step ahead.
 // ------------------------------------------------------------------------------------------------
 struct BandArgs {
-  const double* S;      // skyline reduced system
-  const int* first;
-  const int* row;
+  const double* Sband;  // N × (B+1) blocks × 36
   const double* g;
-  double* Lband;        // N × (B+1) blocks × 36, block c of row i = column i − B + c
-  double* Linv;         // N × 36
+  double* Lband;        // factor, same layout
+  double* invd;         // N × 6 reciprocal pivots
   double* x;            // y during the forward pass, then the step
   int* status;
   int N;
 };
+
+__device__ inline bool chol6_rcp(double* A, double* invd) {  // in place, lower; returns reciprocal pivots
+  for (int j = 0; j < 6; ++j) {
+    double s = A[j * 6 + j];
+    for (int k = 0; k < j; ++k) s -= A[j * 6 + k] * A[j * 6 + k];
+    if (!(s > 0.0)) return false;
+    const double l = sqrt(s), il = 1.0 / l;
+    A[j * 6 + j] = l;
+    invd[j] = il;
+    for (int i = j + 1; i < 6; ++i) {
+      double t = A[i * 6 + j];
+      for (int k = 0; k < j; ++k) t -= A[i * 6 + k] * A[j * 6 + k];
+      A[i * 6 + j] = t * il;
+    }
+  }
+  for (int i = 0; i < 6; ++i)
+    for (int j = i + 1; j < 6; ++j) A[i * 6 + j] = 0.0;
+  return true;
+}
 
 template <int B>
 __global__ __launch_bounds__(256) void band_solve_kernel(const BandArgs a) {
   constexpr int W = B + 1;
   constexpr int ROWF = W * 36;
   constexpr int PF = (ROWF + 255) / 256;
-  constexpr int COLF = B * 36 + 36 + 6;  // backward panel: L_(k+q),k (q = 1..B), L_kk⁻¹, y_k
+  constexpr int COLF = B * 36 + 36 + 6 + 6;  // backward panel: L_(k+q),k (q = 1..B), L_kk, 1/pivots, y_k
   constexpr int PB = (COLF + 255) / 256;
   __shared__ double win[W * ROWF];
-  __shared__ double sLi[36], sv[6];
+  __shared__ double sd[6], sv[6];
   __shared__ double ring[W * 6];
+  __shared__ double col[COLF];
   __shared__ int s_fail;
   const int tid = threadIdx.x, N = a.N;
 
@@ -526,12 +550,7 @@ __global__ __launch_bounds__(256) void band_solve_kernel(const BandArgs a) {
 #pragma unroll
     for (int q = 0; q < PF; ++q) {
       const int idx = tid + q * 256;
-      double v = 0.0;
-      if (i < N && idx < ROWF) {
-        const int c = idx / 36, e = idx % 36, j = i - B + c;
-        if (j >= a.first[i] && j <= i) v = a.S[((long long)a.row[i] + (j - a.first[i])) * 36 + e];
-      }
-      regs[q] = v;
+      regs[q] = (i < N && idx < ROWF) ? a.Sband[(long long)i * ROWF + idx] : 0.0;
     }
   };
   auto store_row = [&](int i, const double* regs) {
@@ -558,69 +577,61 @@ __global__ __launch_bounds__(256) void band_solve_kernel(const BandArgs a) {
     double nxt[PF];
     fetch_row(k + W + 1, nxt);  // in flight during this step
     double* rk = win + (k % W) * ROWF;
+    double* Lkk = rk + B * 36;
     if (tid == 0) {
-      double L[36], Li[36];
-      if (!chol6(rk + B * 36, L)) {
-        s_fail = k + 1;
-      } else {
-        inv_lower6(L, Li);
-        for (int e = 0; e < 36; ++e) {
-          rk[B * 36 + e] = L[e];
-          sLi[e] = Li[e];
-        }
-      }
+      if (!chol6_rcp(Lkk, sd)) s_fail = k + 1;
     }
     __syncthreads();
     if (s_fail) {
       if (tid == 0) *a.status = s_fail;
       return;
     }
-    // forward substitution, fused: b_k = −g_k − Σ_j L_kj y_j ; y_k = L_kk⁻¹ b_k
-    if (tid < 6) {
-      double s = -a.g[6 * k + tid];
-#pragma unroll
-      for (int c = 0; c < B; ++c) {
-        const int j = k - B + c;
-        if (j < 0) continue;
-        const double* Lb = rk + c * 36;
-        const double* yj = ring + (j % W) * 6;
-        for (int m = 0; m < 6; ++m) s -= Lb[tid * 6 + m] * yj[m];
-      }
-      sv[tid] = s;
-    }
-    // column panel L_ik = A_ik · L_kk⁻ᵀ for i = k+1..k+B (two phases: read, barrier, write)
     const int nk = min(B, N - 1 - k);
-    constexpr int PP = (B * 36 + 255) / 256;
-    double pv[PP];
+    if (tid < nk * 6) {
+      // panel row r of L_ik:  X L_kkᵀ = A_ik  →  X[r][c] = (A[r][c] − Σ_{m<c} X[r][m] L_kk[c][m]) / L_kk[c][c]
+      const int ii = 1 + tid / 6, r = tid % 6;
+      double* A = win + ((k + ii) % W) * ROWF + (B - ii) * 36 + r * 6;
+      double X[6];
 #pragma unroll
-    for (int q = 0; q < PP; ++q) {
-      const int idx = tid + q * 256;
-      pv[q] = 0.0;
-      if (idx < nk * 36) {
-        const int ii = 1 + idx / 36, e = idx % 36, r = e / 6, c = e % 6;
-        const double* A = win + ((k + ii) % W) * ROWF + (B - ii) * 36;
-        double v = 0.0;
-        for (int m = 0; m <= c; ++m) v += A[r * 6 + m] * sLi[c * 6 + m];
-        pv[q] = v;
+      for (int c = 0; c < 6; ++c) {
+        double t = A[c];
+#pragma unroll
+        for (int m = 0; m < c; ++m) t -= X[m] * Lkk[c * 6 + m];
+        X[c] = t * sd[c];
+      }
+#pragma unroll
+      for (int c = 0; c < 6; ++c) A[c] = X[c];
+    } else if (tid == 255) {
+      // forward substitution, fused: y_k = L_kk⁻¹ (−g_k − Σ_j L_kj y_j)
+      double b[6];
+#pragma unroll
+      for (int r = 0; r < 6; ++r) {
+        double s = -a.g[6 * k + r];
+#pragma unroll
+        for (int c = 0; c < B; ++c) {
+          const int j = k - B + c;
+          if (j < 0) continue;
+          const double* Lb = rk + c * 36 + r * 6;
+          const double* yj = ring + (j % W) * 6;
+          for (int m = 0; m < 6; ++m) s -= Lb[m] * yj[m];
+        }
+        b[r] = s;
+      }
+#pragma unroll
+      for (int c = 0; c < 6; ++c) {
+        double t = b[c];
+#pragma unroll
+        for (int m = 0; m < c; ++m) t -= Lkk[c * 6 + m] * b[m];
+        b[c] = t * sd[c];
+      }
+#pragma unroll
+      for (int r = 0; r < 6; ++r) {
+        ring[(k % W) * 6 + r] = b[r];
+        a.x[6 * k + r] = b[r];
       }
     }
     __syncthreads();
-#pragma unroll
-    for (int q = 0; q < PP; ++q) {
-      const int idx = tid + q * 256;
-      if (idx < nk * 36) {
-        const int ii = 1 + idx / 36, e = idx % 36;
-        win[((k + ii) % W) * ROWF + (B - ii) * 36 + e] = pv[q];
-      }
-    }
-    if (tid < 6) {
-      double y = 0.0;
-      for (int m = 0; m <= tid; ++m) y += sLi[tid * 6 + m] * sv[m];
-      ring[(k % W) * 6 + tid] = y;
-      a.x[6 * k + tid] = y;
-    }
-    __syncthreads();
-    // trailing update A_ij −= L_ik L_jkᵀ, k < j ≤ i ≤ k+nk
+    // trailing update A_ij −= L_ik L_jkᵀ, k < j ≤ i ≤ k+nk; finished row k to global meanwhile
     const int npairs = nk * (nk + 1) / 2;
     for (int idx = tid; idx < npairs * 36; idx += 256) {
       const int pidx = idx / 36, e = idx % 36, r = e / 6, c = e % 6;
@@ -631,12 +642,12 @@ __global__ __launch_bounds__(256) void band_solve_kernel(const BandArgs a) {
       const double* Li_ = win + (i % W) * ROWF + (k - i + B) * 36;
       const double* Lj_ = win + (j % W) * ROWF + (k - j + B) * 36;
       double s = 0.0;
+#pragma unroll
       for (int m = 0; m < 6; ++m) s += Li_[r * 6 + m] * Lj_[c * 6 + m];
       win[(i % W) * ROWF + (j - i + B) * 36 + e] -= s;
     }
-    // row k of L and L_kk⁻¹ to global for the backward pass
     for (int idx = tid; idx < ROWF; idx += 256) a.Lband[(long long)k * ROWF + idx] = rk[idx];
-    if (tid < 36) a.Linv[(long long)k * 36 + tid] = sLi[tid];
+    if (tid < 6) a.invd[6 * k + tid] = sd[tid];
     __syncthreads();
     store_row(k + W, pre);  // reuses row k's slot
 #pragma unroll
@@ -646,7 +657,6 @@ __global__ __launch_bounds__(256) void band_solve_kernel(const BandArgs a) {
   __threadfence();
   __syncthreads();
   // backward substitution x_k = L_kk⁻ᵀ (y_k − Σ_q L_(k+q),kᵀ x_(k+q)); column panel prefetched a step ahead
-  __shared__ double col[COLF];
   auto fetch_col = [&](int k, double* regs) {
 #pragma unroll
     for (int q = 0; q < PB; ++q) {
@@ -657,9 +667,11 @@ __global__ __launch_bounds__(256) void band_solve_kernel(const BandArgs a) {
           const int qq = 1 + idx / 36, e = idx % 36, i = k + qq;
           if (i < N) v = a.Lband[(long long)i * ROWF + (B - qq) * 36 + e];
         } else if (idx < B * 36 + 36) {
-          v = a.Linv[(long long)k * 36 + (idx - B * 36)];
+          v = a.Lband[(long long)k * ROWF + B * 36 + (idx - B * 36)];
+        } else if (idx < B * 36 + 42) {
+          v = a.invd[6 * k + (idx - B * 36 - 36)];
         } else {
-          v = a.x[6 * k + (idx - B * 36 - 36)];
+          v = a.x[6 * k + (idx - B * 36 - 42)];
         }
       }
       regs[q] = v;
@@ -677,22 +689,33 @@ __global__ __launch_bounds__(256) void band_solve_kernel(const BandArgs a) {
     }
     fetch_col(k - 1, cpre);
     __syncthreads();
-    if (tid < 6) {
-      double s = col[B * 36 + 36 + tid];
-      for (int q = 1; q <= B; ++q) {
-        if (k + q >= N) break;
-        const double* Lq = col + (q - 1) * 36;
-        const double* xq = ring + ((k + q) % W) * 6;
-        for (int m = 0; m < 6; ++m) s -= Lq[m * 6 + tid] * xq[m];
+    if (tid == 0) {
+      double t[6];
+#pragma unroll
+      for (int r = 0; r < 6; ++r) {
+        double s = col[B * 36 + 42 + r];
+        for (int q = 1; q <= B; ++q) {
+          if (k + q >= N) break;
+          const double* Lq = col + (q - 1) * 36;
+          const double* xq = ring + ((k + q) % W) * 6;
+          for (int m = 0; m < 6; ++m) s -= Lq[m * 6 + r] * xq[m];
+        }
+        t[r] = s;
       }
-      sv[tid] = s;
-    }
-    __syncthreads();
-    if (tid < 6) {
-      double xk = 0.0;
-      for (int m = tid; m < 6; ++m) xk += col[B * 36 + m * 6 + tid] * sv[m];
-      ring[(k % W) * 6 + tid] = xk;
-      a.x[6 * k + tid] = xk;
+      const double* L = col + B * 36;
+      const double* id = col + B * 36 + 36;
+#pragma unroll
+      for (int r = 5; r >= 0; --r) {  // L_kkᵀ x = t
+        double s = t[r];
+#pragma unroll
+        for (int m = r + 1; m < 6; ++m) s -= L[m * 6 + r] * t[m];
+        t[r] = s * id[r];
+      }
+#pragma unroll
+      for (int r = 0; r < 6; ++r) {
+        ring[(k % W) * 6 + r] = t[r];
+        a.x[6 * k + r] = t[r];
+      }
     }
     __syncthreads();
   }
@@ -1048,7 +1071,12 @@ int gn_prepare(pba_engine* e) {
   G.band_kernel = G.band <= 4 ? 4 : (G.band <= 8 ? 8 : (G.band <= 16 ? 16 : 0));
   if (const char* fs = getenv("PBA_FORCE_SKYLINE"))  // test hook: exercise the general skyline solver
     if (fs[0] == '1') G.band_kernel = 0;
-  if (G.band_kernel) PBA_HIP(G.Lband.resize((size_t)nf * (G.band_kernel + 1) * 36));
+  if (G.band_kernel) {
+    const size_t nb_ = (size_t)nf * (G.band_kernel + 1) * 36;
+    PBA_HIP(G.Lband.resize(nb_));
+    PBA_HIP(G.Sband.resize(nb_));
+    PBA_HIP(hipMemsetAsync(G.Sband.p, 0, nb_ * sizeof(double), st));  // positions outside the profile stay 0
+  }
   PBA_HIP(G.g.resize((size_t)nf * 6));
   PBA_HIP(G.g_dir.resize((size_t)nf * 6));
   PBA_HIP(G.Ddiag.resize((size_t)nf * 6));
@@ -1150,11 +1178,12 @@ int gn_step(pba_engine* e, double lambda, double* model_decrease, int* solver_st
                G.blk_schur.p, G.part_schur.p, G.pt_data.p, G.n_schur};
   schur_kernel<<<G.n_schur, kBlockThreads, 0, e->stream>>>(sa, lambda);
   AsmArgs aa{G.part_lin.p, G.part_schur.p, G.sky_cptr.p, G.sky_contrib.p, G.g_cptr.p, G.g_contrib.p,
-             G.sky_blk_i.p, G.sky_blk_j.p, G.fixed.p, G.S.p, G.g.p, G.g_dir.p, G.Ddiag.p, G.n_sky, nf};
+             G.sky_blk_i.p, G.sky_blk_j.p, G.fixed.p, G.S.p, G.g.p, G.g_dir.p, G.Ddiag.p,
+             G.band_kernel ? G.Sband.p : nullptr, G.band_kernel, G.n_sky, nf};
   const int nthreads = G.n_sky * 36 + 6 * nf;
   assemble_kernel<<<(nthreads + 255) / 256, 256, 0, e->stream>>>(aa, lambda);
   if (G.band_kernel) {  // banded structure: LDS-window factorisation (the skyline buffer stays untouched)
-    BandArgs ba{G.S.p, G.sky_first.p, G.sky_row.p, G.g.p, G.Lband.p, G.Linv.p, G.x.p, G.status.p, nf};
+    BandArgs ba{G.Sband.p, G.g.p, G.Lband.p, G.Linv.p, G.x.p, G.status.p, nf};
     if (G.band_kernel == 4) band_solve_kernel<4><<<1, 256, 0, e->stream>>>(ba);
     else if (G.band_kernel == 8) band_solve_kernel<8><<<1, 256, 0, e->stream>>>(ba);
     else band_solve_kernel<16><<<1, 256, 0, e->stream>>>(ba);

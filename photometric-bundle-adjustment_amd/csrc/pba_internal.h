@@ -245,7 +245,7 @@ struct GnData {
   DevBuf<int> sky_cptr, g_cptr;  // contribution lists (CSR) per skyline block / per pose
   DevBuf<int2> sky_contrib, g_contrib;
   DevBuf<int> sky_blk_i, sky_blk_j;  // skyline block → (row pose, column pose)
-  DevBuf<double> S, L, Lband, g, g_dir, Ddiag, Linv, x;  // skyline system, its factor, rhs, direct gradient, LM diagonal, L_kk⁻¹, step
+  DevBuf<double> S, L, Sband, Lband, g, g_dir, Ddiag, Linv, x;  // skyline system, its factor, rhs, direct gradient, LM diagonal, L_kk⁻¹, step
   DevBuf<uint8_t> fixed;
   std::vector<uint8_t> fixed_h;
   DevBuf<double> poses_new, rho_new, red;
