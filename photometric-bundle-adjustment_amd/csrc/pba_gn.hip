@@ -579,7 +579,32 @@ __global__ __launch_bounds__(256) void band_solve_kernel(const BandArgs a) {
     double* rk = win + (k % W) * ROWF;
     double* Lkk = rk + B * 36;
     if (tid == 0) {
-      if (!chol6_rcp(Lkk, sd)) s_fail = k + 1;
+      // registers, not LDS, inside the serial factorisation (one LDS round trip per operand otherwise)
+      double A[36], d[6];
+#pragma unroll
+      for (int e = 0; e < 36; ++e) A[e] = Lkk[e];
+      if (!chol6_rcp(A, d)) {
+        s_fail = k + 1;
+      } else {
+#pragma unroll
+        for (int e = 0; e < 36; ++e) Lkk[e] = A[e];
+#pragma unroll
+        for (int e = 0; e < 6; ++e) sd[e] = d[e];
+      }
+    } else if (tid >= 64 && tid < 70) {
+      // right-hand side of the fused forward substitution: b_k = −g_k − Σ_j L_kj y_j (L_kj final by now)
+      const int r = tid - 64;
+      double s = -a.g[6 * k + r];
+#pragma unroll
+      for (int c = 0; c < B; ++c) {
+        const int j = k - B + c;
+        if (j < 0) continue;
+        const double* Lb = rk + c * 36 + r * 6;
+        const double* yj = ring + (j % W) * 6;
+#pragma unroll
+        for (int m = 0; m < 6; ++m) s -= Lb[m] * yj[m];
+      }
+      sv[r] = s;
     }
     __syncthreads();
     if (s_fail) {
@@ -602,27 +627,18 @@ __global__ __launch_bounds__(256) void band_solve_kernel(const BandArgs a) {
 #pragma unroll
       for (int c = 0; c < 6; ++c) A[c] = X[c];
     } else if (tid == 255) {
-      // forward substitution, fused: y_k = L_kk⁻¹ (−g_k − Σ_j L_kj y_j)
-      double b[6];
+      // y_k = L_kk⁻¹ b_k (registers)
+      double L[36], b[6], d[6];
 #pragma unroll
-      for (int r = 0; r < 6; ++r) {
-        double s = -a.g[6 * k + r];
+      for (int e = 0; e < 36; ++e) L[e] = Lkk[e];
 #pragma unroll
-        for (int c = 0; c < B; ++c) {
-          const int j = k - B + c;
-          if (j < 0) continue;
-          const double* Lb = rk + c * 36 + r * 6;
-          const double* yj = ring + (j % W) * 6;
-          for (int m = 0; m < 6; ++m) s -= Lb[m] * yj[m];
-        }
-        b[r] = s;
-      }
+      for (int r = 0; r < 6; ++r) { b[r] = sv[r]; d[r] = sd[r]; }
 #pragma unroll
       for (int c = 0; c < 6; ++c) {
         double t = b[c];
 #pragma unroll
-        for (int m = 0; m < c; ++m) t -= Lkk[c * 6 + m] * b[m];
-        b[c] = t * sd[c];
+        for (int m = 0; m < c; ++m) t -= L[c * 6 + m] * b[m];
+        b[c] = t * d[c];
       }
 #pragma unroll
       for (int r = 0; r < 6; ++r) {
@@ -689,27 +705,32 @@ __global__ __launch_bounds__(256) void band_solve_kernel(const BandArgs a) {
     }
     fetch_col(k - 1, cpre);
     __syncthreads();
-    if (tid == 0) {
-      double t[6];
+    if (tid < 6) {
+      const int r = tid;
+      double s = col[B * 36 + 42 + r];
 #pragma unroll
-      for (int r = 0; r < 6; ++r) {
-        double s = col[B * 36 + 42 + r];
-        for (int q = 1; q <= B; ++q) {
-          if (k + q >= N) break;
-          const double* Lq = col + (q - 1) * 36;
-          const double* xq = ring + ((k + q) % W) * 6;
-          for (int m = 0; m < 6; ++m) s -= Lq[m * 6 + r] * xq[m];
-        }
-        t[r] = s;
+      for (int q = 1; q <= B; ++q) {
+        if (k + q >= N) break;
+        const double* Lq = col + (q - 1) * 36;
+        const double* xq = ring + ((k + q) % W) * 6;
+#pragma unroll
+        for (int m = 0; m < 6; ++m) s -= Lq[m * 6 + r] * xq[m];
       }
-      const double* L = col + B * 36;
-      const double* id = col + B * 36 + 36;
+      sv[r] = s;
+    }
+    __syncthreads();
+    if (tid == 0) {
+      double L[36], t[6], id[6];
+#pragma unroll
+      for (int e = 0; e < 36; ++e) L[e] = col[B * 36 + e];
+#pragma unroll
+      for (int r = 0; r < 6; ++r) { t[r] = sv[r]; id[r] = col[B * 36 + 36 + r]; }
 #pragma unroll
       for (int r = 5; r >= 0; --r) {  // L_kkᵀ x = t
-        double s = t[r];
+        double v = t[r];
 #pragma unroll
-        for (int m = r + 1; m < 6; ++m) s -= L[m * 6 + r] * t[m];
-        t[r] = s * id[r];
+        for (int m = r + 1; m < 6; ++m) v -= L[m * 6 + r] * t[m];
+        t[r] = v * id[r];
       }
 #pragma unroll
       for (int r = 0; r < 6; ++r) {
