@@ -176,10 +176,21 @@ __global__ __launch_bounds__(kBlockThreads) void linearize_kernel(const KernelAr
     else if (q < 14) v = sblk[b][98 + q - 8];
     g.blk_schur[(long long)(first + b) * 16 + q] = v;
   }
-  // chunk partial slots (fixed summation order over the chunk's blocks)
+  // chunk partial slots (fixed summation order over the chunk's blocks): per local target a block mask,
+  // then fully unrolled, predicated sums — independent LDS reads instead of a dependent loop
+  __shared__ unsigned long long s_mask[BPW];
+  if ((int)threadIdx.x < n_t) {
+    unsigned long long msk = 0;
+    for (int b = 0; b < count; ++b)
+      if (s_lt[b] == (int)threadIdx.x) msk |= 1ull << b;
+    s_mask[threadIdx.x] = msk;
+  }
+  __syncthreads();
+  const unsigned long long all = count >= 64 ? ~0ull : ((1ull << count) - 1ull);
   const int nout = SLOT_LIN_BASE + SLOT_LIN_T * n_t;
   for (int o = threadIdx.x; o < nout; o += kBlockThreads) {
-    int v, tsel = -1;
+    int v;
+    unsigned long long msk = all;
     if (o < 36) {
       const int r = o / 6, c = o % 6;
       v = upper_index(min(r, c), max(r, c));
@@ -187,14 +198,14 @@ __global__ __launch_bounds__(kBlockThreads) void linearize_kernel(const KernelAr
       v = 78 + (o - 36);
     } else {
       const int j = (o - 42) / SLOT_LIN_T, q = (o - 42) % SLOT_LIN_T;
-      tsel = j;
+      msk = s_mask[j];
       if (q < 36) v = 21 + q;
       else if (q < 72) { const int r = (q - 36) / 6, c = (q - 36) % 6; v = 57 + upper_index(min(r, c), max(r, c)); }
       else v = 84 + (q - 72);
     }
     float acc = 0.0f;
-    for (int b = 0; b < count; ++b)
-      if (tsel < 0 || s_lt[b] == tsel) acc += sblk[b][v];
+#pragma unroll
+    for (int b = 0; b < BPW; ++b) acc += ((msk >> b) & 1ull) ? sblk[b][v] : 0.0f;
     g.part_lin[(long long)poff + o] = acc;
   }
 }
@@ -513,21 +524,37 @@ struct BandArgs {
   int N;
 };
 
+// 1/√x to full fp64 precision: hardware v_rsq_f64 seed + two Newton steps (the pivot is on the solver's
+// serial critical path; this is ~3x shorter than sqrt() + division).
+__device__ __forceinline__ double rsqrt_nr(double x) {
+  double y = __builtin_amdgcn_rsq(x);
+  double e = fma(-x * y, y, 1.0);
+  y = fma(0.5 * y, e, y);
+  e = fma(-x * y, y, 1.0);
+  return fma(0.5 * y, e, y);
+}
+
 __device__ inline bool chol6_rcp(double* A, double* invd) {  // in place, lower; returns reciprocal pivots
+#pragma unroll
   for (int j = 0; j < 6; ++j) {
     double s = A[j * 6 + j];
+#pragma unroll
     for (int k = 0; k < j; ++k) s -= A[j * 6 + k] * A[j * 6 + k];
     if (!(s > 0.0)) return false;
-    const double l = sqrt(s), il = 1.0 / l;
+    const double il = rsqrt_nr(s), l = s * il;
     A[j * 6 + j] = l;
     invd[j] = il;
+#pragma unroll
     for (int i = j + 1; i < 6; ++i) {
       double t = A[i * 6 + j];
+#pragma unroll
       for (int k = 0; k < j; ++k) t -= A[i * 6 + k] * A[j * 6 + k];
       A[i * 6 + j] = t * il;
     }
   }
+#pragma unroll
   for (int i = 0; i < 6; ++i)
+#pragma unroll
     for (int j = i + 1; j < 6; ++j) A[i * 6 + j] = 0.0;
   return true;
 }
@@ -665,11 +692,12 @@ __global__ __launch_bounds__(256) void band_solve_kernel(const BandArgs a) {
     for (int idx = tid; idx < ROWF; idx += 256) a.Lband[(long long)k * ROWF + idx] = rk[idx];
     if (tid < 6) a.invd[6 * k + tid] = sd[tid];
     __syncthreads();
-    store_row(k + W, pre);  // reuses row k's slot
+    // row k+B+1 into row k's slot; first read by the next step's panel, which is behind its first barrier
+    store_row(k + W, pre);
 #pragma unroll
     for (int q = 0; q < PF; ++q) pre[q] = nxt[q];
-    __syncthreads();
   }
+  __syncthreads();
   __threadfence();
   __syncthreads();
   // backward substitution x_k = L_kk⁻ᵀ (y_k − Σ_q L_(k+q),kᵀ x_(k+q)); column panel prefetched a step ahead
