@@ -103,39 +103,30 @@ __device__ __forceinline__ float nprod(const float* x) {
   }
 }
 
-template <int RD, int LPB, int... Q>
-__device__ __forceinline__ void fill_round(float* vals, const float* x, std::integer_sequence<int, Q...>) {
-  ((vals[Q] = nprod<RD * LPB + Q>(x)), ...);
+// The 104 normal-equation products of one row, all-reduced over the block's LPB lanes (DPP butterflies,
+// no lane-dependent selects), 8 at a time; lane 0 of the block stores each group of block sums as 2 float4s.
+template <int LPB, int G, int... Q>
+__device__ __forceinline__ void product_group(const float* x, float* o, std::integer_sequence<int, Q...>) {
+  ((o[Q] = group_sum<LPB>(nprod<G * 8 + Q>(x))), ...);
 }
-
-// Round RD of the normal-equation products: LPB products per lane, reduce-scattered over the block's lanes
-// (recursive halving: lane k ends with the block sum of product RD·LPB + k).
-template <int RD, int ROUNDS, int LPB>
-__device__ __forceinline__ void lin_rounds(const float* x, int k, float* srow) {
-  if constexpr (RD < ROUNDS) {
-    float vals[LPB];
-    fill_round<RD, LPB>(vals, x, std::make_integer_sequence<int, LPB>{});
-#pragma unroll
-    for (int m = LPB / 2; m >= 1; m >>= 1) {
-      const bool hi = (k & m) != 0;
-#pragma unroll
-      for (int i = 0; i < m; ++i) {
-        const float send = hi ? vals[i] : vals[i + m];
-        const float keep = hi ? vals[i + m] : vals[i];
-        vals[i] = keep + __shfl_xor(send, m, 64);
-      }
+template <int LPB, int G>
+__device__ __forceinline__ void block_products(const float* x, float* srow, bool writer) {
+  if constexpr (G * 8 < NV) {
+    float o[8];
+    product_group<LPB, G>(x, o, std::make_integer_sequence<int, 8>{});
+    if (writer) {
+      *reinterpret_cast<float4*>(srow + G * 8) = make_float4(o[0], o[1], o[2], o[3]);
+      *reinterpret_cast<float4*>(srow + G * 8 + 4) = make_float4(o[4], o[5], o[6], o[7]);
     }
-    if (srow) srow[RD * LPB + k] = vals[0];
-    lin_rounds<RD + 1, ROUNDS, LPB>(x, k, srow);
+    block_products<LPB, G + 1>(x, srow, writer);
   }
 }
 
 template <int KIND, int MODEL, int LPB>
 __global__ __launch_bounds__(kBlockThreads) void linearize_kernel(const KernelArgs a, const LinArgs g) {
   constexpr int BPW = kBlockThreads / LPB;
-  constexpr int ROUNDS = (NV + LPB - 1) / LPB;
-  constexpr int NVP = ROUNDS * LPB;
-  __shared__ float sblk[BPW][NVP + 1];
+  constexpr int NVP = 104;  // multiple of 4
+  __shared__ __attribute__((aligned(16))) float sblk[BPW][NVP + 4];
   __shared__ int s_lt[BPW];
   const int chunk = logical_tile();
   if (chunk >= g.n_chunks) return;
@@ -164,7 +155,7 @@ __global__ __launch_bounds__(kBlockThreads) void linearize_kernel(const KernelAr
   const float x[14] = {sw * row.hv.x, sw * row.hv.y, sw * row.hv.z, sw * row.hw.x, sw * row.hw.y, sw * row.hw.z,
                        sw * row.tv.x, sw * row.tv.y, sw * row.tv.z, sw * row.tw.x, sw * row.tw.y, sw * row.tw.z,
                        sw * row.jr,   sw * row.r};
-  lin_rounds<0, ROUNDS, LPB>(x, k, live ? &sblk[lb][0] : nullptr);
+  block_products<LPB, 0>(x, &sblk[lb < BPW ? lb : 0][0], live && k == 0);
   __syncthreads();
   // per-block point-elimination data: [H_ρρ, g_ρ, W_h(6), W_t(6), 0, 0]
   for (int i = threadIdx.x; i < count * 16; i += kBlockThreads) {
@@ -329,7 +320,7 @@ __global__ void assemble_kernel(const AsmArgs a, double lambda) {
       val = sum + lambda * D;
     }
     a.S[tid] = val;
-    if (a.Sband) a.Sband[((long long)i * (a.band + 1) + (j - i + a.band)) * 36 + e] = val;
+    if (a.Sband) a.Sband[(long long)i * ((a.band + 1) * 36 + 6) + (j - i + a.band) * 36 + e] = val;
     return;
   }
   const int t = tid - nS;
@@ -346,6 +337,7 @@ __global__ void assemble_kernel(const AsmArgs a, double lambda) {
     }
   }
   a.g[t] = a.fixed[i] ? 0.0 : sum;
+  if (a.Sband) a.Sband[(long long)i * ((a.band + 1) * 36 + 6) + (a.band + 1) * 36 + r] = a.fixed[i] ? 0.0 : sum;
   a.g_dir[t] = a.fixed[i] ? 0.0 : dsum;
   if (a.fixed[i]) a.Ddiag[t] = 0.0;
 }
@@ -515,11 +507,9 @@ __global__ __launch_bounds__(256) void skyline_solve_kernel(const SolveArgs a) {
 // the reciprocal pivots go to global memory for the backward pass, which prefetches one step ahead.
 // ------------------------------------------------------------------------------------------------
 struct BandArgs {
-  const double* Sband;  // N × (B+1) blocks × 36
-  const double* g;
-  double* Lband;        // factor, same layout
-  double* invd;         // N × 6 reciprocal pivots
-  double* x;            // y during the forward pass, then the step
+  const double* Sband;  // N rows × ((B+1)·36 + 6): blocks of columns i−B..i, then g_i
+  double* Lcol;         // N column records × (B·36 + 48): L_(k+q),k for q = 1..B | L_kk | 1/pivots | y_k
+  double* x;            // the step δ_poses
   int* status;
   int N;
 };
@@ -563,50 +553,49 @@ template <int B>
 __global__ __launch_bounds__(256) void band_solve_kernel(const BandArgs a) {
   constexpr int W = B + 1;
   constexpr int ROWF = W * 36;
-  constexpr int PF = (ROWF + 255) / 256;
-  constexpr int COLF = B * 36 + 36 + 6 + 6;  // backward panel: L_(k+q),k (q = 1..B), L_kk, 1/pivots, y_k
-  constexpr int PB = (COLF + 255) / 256;
-  __shared__ double win[W * ROWF];
+  constexpr int ROWG = ROWF + 6;
+  constexpr int COLF = B * 36 + 48;
+  constexpr int CH = B <= 8 ? 16 : 4;      // rows / column records per prefetch chunk
+  constexpr int STG = CH * COLF;           // ≥ CH·ROWG
+  constexpr int PCH = (STG + 255) / 256;
+  __shared__ double win[W * ROWG];         // ring of block rows k..k+B (slot i % W)
+  __shared__ double stage[2 * STG];        // double-buffered prefetch chunks
+  __shared__ double ring[W * 6];           // y (forward) / x (backward) of the last B+1 block rows
   __shared__ double sd[6], sv[6];
-  __shared__ double ring[W * 6];
-  __shared__ double col[COLF];
   __shared__ int s_fail;
   const int tid = threadIdx.x, N = a.N;
 
-  auto fetch_row = [&](int i, double* regs) {
+  // ---- forward: factor + fused forward substitution -------------------------------------------------
+  auto load_rows = [&](int r0, double* regs) {  // rows r0 .. r0+CH−1 (zero beyond N)
 #pragma unroll
-    for (int q = 0; q < PF; ++q) {
+    for (int q = 0; q < PCH; ++q) {
       const int idx = tid + q * 256;
-      regs[q] = (i < N && idx < ROWF) ? a.Sband[(long long)i * ROWF + idx] : 0.0;
+      const int i = r0 + idx / ROWG;
+      regs[q] = (idx < CH * ROWG && i < N) ? a.Sband[(long long)r0 * ROWG + idx] : 0.0;
     }
   };
-  auto store_row = [&](int i, const double* regs) {
-    double* r = win + (i % W) * ROWF;
+  auto put_stage = [&](int buf, const double* regs, int n) {
 #pragma unroll
-    for (int q = 0; q < PF; ++q) {
+    for (int q = 0; q < PCH; ++q) {
       const int idx = tid + q * 256;
-      if (idx < ROWF) r[idx] = regs[q];
+      if (idx < n) stage[buf * STG + idx] = regs[q];
     }
   };
-
   if (tid == 0) s_fail = 0;
-  for (int i = 0; i < W; ++i) {
-    double r[PF];
-    fetch_row(i, r);
-    store_row(i, r);
-  }
+  for (int idx = tid; idx < W * ROWG; idx += 256)
+    win[idx] = (idx / ROWG < N) ? a.Sband[idx] : 0.0;  // rows 0..B into slots 0..B
   if (tid < W * 6) ring[tid] = 0.0;
-  double pre[PF];
-  fetch_row(W, pre);
+  double pf[PCH];
+  load_rows(W, pf);
+  put_stage(0, pf, CH * ROWG);
   __syncthreads();
 
   for (int k = 0; k < N; ++k) {
-    double nxt[PF];
-    fetch_row(k + W + 1, nxt);  // in flight during this step
-    double* rk = win + (k % W) * ROWF;
+    const int c = k / CH, o = k % CH;
+    double* rk = win + (k % W) * ROWG;
     double* Lkk = rk + B * 36;
+    if (o == 0) load_rows(W + (c + 1) * CH, pf);  // next chunk, lands during the next CH steps
     if (tid == 0) {
-      // registers, not LDS, inside the serial factorisation (one LDS round trip per operand otherwise)
       double A[36], d[6];
 #pragma unroll
       for (int e = 0; e < 36; ++e) A[e] = Lkk[e];
@@ -618,20 +607,19 @@ __global__ __launch_bounds__(256) void band_solve_kernel(const BandArgs a) {
 #pragma unroll
         for (int e = 0; e < 6; ++e) sd[e] = d[e];
       }
-    } else if (tid >= 64 && tid < 70) {
-      // right-hand side of the fused forward substitution: b_k = −g_k − Σ_j L_kj y_j (L_kj final by now)
+    } else if (tid >= 64 && tid < 70) {  // b_k = −g_k − Σ_j L_kj y_j   (L_kj final, y_j in the ring)
       const int r = tid - 64;
-      double s = -a.g[6 * k + r];
+      double v = -rk[ROWF + r];
 #pragma unroll
-      for (int c = 0; c < B; ++c) {
-        const int j = k - B + c;
+      for (int cc = 0; cc < B; ++cc) {
+        const int j = k - B + cc;
         if (j < 0) continue;
-        const double* Lb = rk + c * 36 + r * 6;
+        const double* Lb = rk + cc * 36 + r * 6;
         const double* yj = ring + (j % W) * 6;
 #pragma unroll
-        for (int m = 0; m < 6; ++m) s -= Lb[m] * yj[m];
+        for (int m = 0; m < 6; ++m) v -= Lb[m] * yj[m];
       }
-      sv[r] = s;
+      sv[r] = v;
     }
     __syncthreads();
     if (s_fail) {
@@ -639,120 +627,111 @@ __global__ __launch_bounds__(256) void band_solve_kernel(const BandArgs a) {
       return;
     }
     const int nk = min(B, N - 1 - k);
-    if (tid < nk * 6) {
-      // panel row r of L_ik:  X L_kkᵀ = A_ik  →  X[r][c] = (A[r][c] − Σ_{m<c} X[r][m] L_kk[c][m]) / L_kk[c][c]
+    double* rec = a.Lcol + (long long)k * COLF;
+    if (tid < nk * 6) {  // panel row r of L_ik = A_ik L_kk⁻ᵀ
       const int ii = 1 + tid / 6, r = tid % 6;
-      double* A = win + ((k + ii) % W) * ROWF + (B - ii) * 36 + r * 6;
+      double* A = win + ((k + ii) % W) * ROWG + (B - ii) * 36 + r * 6;
       double X[6];
 #pragma unroll
-      for (int c = 0; c < 6; ++c) {
-        double t = A[c];
+      for (int cc = 0; cc < 6; ++cc) {
+        double t = A[cc];
 #pragma unroll
-        for (int m = 0; m < c; ++m) t -= X[m] * Lkk[c * 6 + m];
-        X[c] = t * sd[c];
+        for (int m = 0; m < cc; ++m) t -= X[m] * Lkk[cc * 6 + m];
+        X[cc] = t * sd[cc];
       }
 #pragma unroll
-      for (int c = 0; c < 6; ++c) A[c] = X[c];
-    } else if (tid == 255) {
-      // y_k = L_kk⁻¹ b_k (registers)
-      double L[36], b[6], d[6];
+      for (int cc = 0; cc < 6; ++cc) A[cc] = X[cc];
+    } else if (tid >= 192 && tid < 228) {
+      rec[B * 36 + (tid - 192)] = Lkk[tid - 192];
+    } else if (tid >= 228 && tid < 234) {
+      rec[B * 36 + 36 + (tid - 228)] = sd[tid - 228];
+    } else if (tid == 255) {  // y_k = L_kk⁻¹ b_k
+      double L[36], bb[6], d[6];
 #pragma unroll
       for (int e = 0; e < 36; ++e) L[e] = Lkk[e];
 #pragma unroll
-      for (int r = 0; r < 6; ++r) { b[r] = sv[r]; d[r] = sd[r]; }
+      for (int r = 0; r < 6; ++r) { bb[r] = sv[r]; d[r] = sd[r]; }
 #pragma unroll
-      for (int c = 0; c < 6; ++c) {
-        double t = b[c];
+      for (int cc = 0; cc < 6; ++cc) {
+        double t = bb[cc];
 #pragma unroll
-        for (int m = 0; m < c; ++m) t -= L[c * 6 + m] * b[m];
-        b[c] = t * d[c];
+        for (int m = 0; m < cc; ++m) t -= L[cc * 6 + m] * bb[m];
+        bb[cc] = t * d[cc];
       }
 #pragma unroll
       for (int r = 0; r < 6; ++r) {
-        ring[(k % W) * 6 + r] = b[r];
-        a.x[6 * k + r] = b[r];
+        ring[(k % W) * 6 + r] = bb[r];
+        rec[B * 36 + 42 + r] = bb[r];
       }
     }
     __syncthreads();
-    // trailing update A_ij −= L_ik L_jkᵀ, k < j ≤ i ≤ k+nk; finished row k to global meanwhile
+    // trailing update A_ij −= L_ik L_jkᵀ (k < j ≤ i ≤ k+nk); column k of L to the record
     const int npairs = nk * (nk + 1) / 2;
     for (int idx = tid; idx < npairs * 36; idx += 256) {
-      const int pidx = idx / 36, e = idx % 36, r = e / 6, c = e % 6;
+      const int pidx = idx / 36, e = idx % 36, r = e / 6, cc = e % 6;
       int ii = 0;
       while ((ii + 1) * (ii + 2) / 2 <= pidx) ++ii;
       const int jj = pidx - ii * (ii + 1) / 2;
       const int i = k + 1 + ii, j = k + 1 + jj;
-      const double* Li_ = win + (i % W) * ROWF + (k - i + B) * 36;
-      const double* Lj_ = win + (j % W) * ROWF + (k - j + B) * 36;
-      double s = 0.0;
+      const double* Li_ = win + (i % W) * ROWG + (k - i + B) * 36;
+      const double* Lj_ = win + (j % W) * ROWG + (k - j + B) * 36;
+      double sacc = 0.0;
 #pragma unroll
-      for (int m = 0; m < 6; ++m) s += Li_[r * 6 + m] * Lj_[c * 6 + m];
-      win[(i % W) * ROWF + (j - i + B) * 36 + e] -= s;
+      for (int m = 0; m < 6; ++m) sacc += Li_[r * 6 + m] * Lj_[cc * 6 + m];
+      win[(i % W) * ROWG + (j - i + B) * 36 + e] -= sacc;
     }
-    for (int idx = tid; idx < ROWF; idx += 256) a.Lband[(long long)k * ROWF + idx] = rk[idx];
-    if (tid < 6) a.invd[6 * k + tid] = sd[tid];
+    for (int idx = tid; idx < B * 36; idx += 256) {
+      const int q = 1 + idx / 36, e = idx % 36;
+      rec[idx] = (q <= nk) ? win[((k + q) % W) * ROWG + (B - q) * 36 + e] : 0.0;
+    }
+    // row k+B+1 from the staged chunk into row k's slot (first read by the next step's panel)
+    {
+      const double* src = stage + (c & 1) * STG + o * ROWG;
+      for (int idx = tid; idx < ROWG; idx += 256) rk[idx] = src[idx];
+    }
+    if (o == CH - 1) put_stage((c + 1) & 1, pf, CH * ROWG);
     __syncthreads();
-    // row k+B+1 into row k's slot; first read by the next step's panel, which is behind its first barrier
-    store_row(k + W, pre);
-#pragma unroll
-    for (int q = 0; q < PF; ++q) pre[q] = nxt[q];
   }
-  __syncthreads();
   __threadfence();
   __syncthreads();
-  // backward substitution x_k = L_kk⁻ᵀ (y_k − Σ_q L_(k+q),kᵀ x_(k+q)); column panel prefetched a step ahead
-  auto fetch_col = [&](int k, double* regs) {
+
+  // ---- backward: x_k = L_kk⁻ᵀ (y_k − Σ_q L_(k+q),kᵀ x_(k+q)), column records streamed in reverse ---------
+  auto load_cols = [&](int s0, double* regs) {  // records for steps s0..s0+CH−1, k = N−1−s
 #pragma unroll
-    for (int q = 0; q < PB; ++q) {
+    for (int q = 0; q < PCH; ++q) {
       const int idx = tid + q * 256;
-      double v = 0.0;
-      if (k >= 0 && idx < COLF) {
-        if (idx < B * 36) {
-          const int qq = 1 + idx / 36, e = idx % 36, i = k + qq;
-          if (i < N) v = a.Lband[(long long)i * ROWF + (B - qq) * 36 + e];
-        } else if (idx < B * 36 + 36) {
-          v = a.Lband[(long long)k * ROWF + B * 36 + (idx - B * 36)];
-        } else if (idx < B * 36 + 42) {
-          v = a.invd[6 * k + (idx - B * 36 - 36)];
-        } else {
-          v = a.x[6 * k + (idx - B * 36 - 42)];
-        }
-      }
-      regs[q] = v;
+      const int sidx = s0 + idx / COLF;
+      regs[q] = (idx < STG && sidx < N) ? a.Lcol[(long long)(N - 1 - sidx) * COLF + idx % COLF] : 0.0;
     }
   };
   if (tid < W * 6) ring[tid] = 0.0;
-  double cpre[PB];
-  fetch_col(N - 1, cpre);
+  load_cols(0, pf);
+  put_stage(0, pf, STG);
   __syncthreads();
-  for (int k = N - 1; k >= 0; --k) {
-#pragma unroll
-    for (int q = 0; q < PB; ++q) {
-      const int idx = tid + q * 256;
-      if (idx < COLF) col[idx] = cpre[q];
-    }
-    fetch_col(k - 1, cpre);
-    __syncthreads();
+  for (int sstep = 0; sstep < N; ++sstep) {
+    const int k = N - 1 - sstep, c = sstep / CH, o = sstep % CH;
+    if (o == 0) load_cols((c + 1) * CH, pf);
+    const double* rec = stage + (c & 1) * STG + o * COLF;
     if (tid < 6) {
       const int r = tid;
-      double s = col[B * 36 + 42 + r];
+      double v = rec[B * 36 + 42 + r];
 #pragma unroll
       for (int q = 1; q <= B; ++q) {
         if (k + q >= N) break;
-        const double* Lq = col + (q - 1) * 36;
+        const double* Lq = rec + (q - 1) * 36;
         const double* xq = ring + ((k + q) % W) * 6;
 #pragma unroll
-        for (int m = 0; m < 6; ++m) s -= Lq[m * 6 + r] * xq[m];
+        for (int m = 0; m < 6; ++m) v -= Lq[m * 6 + r] * xq[m];
       }
-      sv[r] = s;
+      sv[r] = v;
     }
     __syncthreads();
     if (tid == 0) {
       double L[36], t[6], id[6];
 #pragma unroll
-      for (int e = 0; e < 36; ++e) L[e] = col[B * 36 + e];
+      for (int e = 0; e < 36; ++e) L[e] = rec[B * 36 + e];
 #pragma unroll
-      for (int r = 0; r < 6; ++r) { t[r] = sv[r]; id[r] = col[B * 36 + 36 + r]; }
+      for (int r = 0; r < 6; ++r) { t[r] = sv[r]; id[r] = rec[B * 36 + 36 + r]; }
 #pragma unroll
       for (int r = 5; r >= 0; --r) {  // L_kkᵀ x = t
         double v = t[r];
@@ -766,6 +745,7 @@ __global__ __launch_bounds__(256) void band_solve_kernel(const BandArgs a) {
         a.x[6 * k + r] = t[r];
       }
     }
+    if (o == CH - 1) put_stage((c + 1) & 1, pf, STG);
     __syncthreads();
   }
   if (tid == 0) *a.status = 0;
@@ -1121,8 +1101,8 @@ int gn_prepare(pba_engine* e) {
   if (const char* fs = getenv("PBA_FORCE_SKYLINE"))  // test hook: exercise the general skyline solver
     if (fs[0] == '1') G.band_kernel = 0;
   if (G.band_kernel) {
-    const size_t nb_ = (size_t)nf * (G.band_kernel + 1) * 36;
-    PBA_HIP(G.Lband.resize(nb_));
+    const size_t nb_ = (size_t)nf * ((G.band_kernel + 1) * 36 + 6);
+    PBA_HIP(G.Lband.resize((size_t)nf * (G.band_kernel * 36 + 48)));  // column records
     PBA_HIP(G.Sband.resize(nb_));
     PBA_HIP(hipMemsetAsync(G.Sband.p, 0, nb_ * sizeof(double), st));  // positions outside the profile stay 0
   }
@@ -1232,7 +1212,7 @@ int gn_step(pba_engine* e, double lambda, double* model_decrease, int* solver_st
   const int nthreads = G.n_sky * 36 + 6 * nf;
   assemble_kernel<<<(nthreads + 255) / 256, 256, 0, e->stream>>>(aa, lambda);
   if (G.band_kernel) {  // banded structure: LDS-window factorisation (the skyline buffer stays untouched)
-    BandArgs ba{G.Sband.p, G.g.p, G.Lband.p, G.Linv.p, G.x.p, G.status.p, nf};
+    BandArgs ba{G.Sband.p, G.Lband.p, G.x.p, G.status.p, nf};
     if (G.band_kernel == 4) band_solve_kernel<4><<<1, 256, 0, e->stream>>>(ba);
     else if (G.band_kernel == 8) band_solve_kernel<8><<<1, 256, 0, e->stream>>>(ba);
     else band_solve_kernel<16><<<1, 256, 0, e->stream>>>(ba);

@@ -68,11 +68,21 @@ __device__ __forceinline__ float huber_weight(float s, float a) {
   return fmaxf(a * rsqrtf(s), 1.17549435e-38f);
 }
 
-// Sum / AND over the LPB lanes of one block (LPB | 64, groups are aligned lane ranges).
+// All-reduce over the LPB lanes of one block (LPB | 64, groups are aligned lane ranges) with DPP lane
+// moves fused into the adds: quad_perm [1,0,3,2] and [2,3,0,1] (xor 1, xor 2), row_half_mirror (pairs the two
+// quads of an 8-lane group), row_mirror (the two halves of a 16-lane row), then a swizzle for 32.
+template <int CTRL>
+__device__ __forceinline__ float dpp(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
 template <int LPB>
 __device__ __forceinline__ float group_sum(float v) {
-#pragma unroll
-  for (int m = LPB / 2; m >= 1; m >>= 1) v += __shfl_xor(v, m, 64);
+  if (LPB >= 2) v += dpp<0xB1>(v);
+  if (LPB >= 4) v += dpp<0x4E>(v);
+  if (LPB >= 8) v += dpp<0x141>(v);
+  if (LPB >= 16) v += dpp<0x140>(v);
+  if (LPB >= 32) v += __shfl_xor(v, 16, 64);
+  if (LPB >= 64) v += __shfl_xor(v, 32, 64);
   return v;
 }
 template <int LPB>
