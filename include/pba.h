@@ -107,6 +107,9 @@ int pba_synchronize(pba_engine* engine);
 
 /* Results ---------------------------------------------------------------------------------------- */
 int pba_record_floats(const pba_engine* engine);   /* 14·R */
+int pba_num_blocks(const pba_engine* engine);
+int pba_num_points(const pba_engine* engine);
+int pba_num_frames(const pba_engine* engine);
 int pba_residuals_per_block(const pba_engine* engine);
 /* records: n_blocks·record_floats floats; valid: n_blocks bytes (either may be NULL).  Synchronises. */
 int pba_get_records(pba_engine* engine, float* records, uint8_t* valid);

@@ -570,6 +570,9 @@ int pba_synchronize(pba_engine* e) {
 
 int pba_record_floats(const pba_engine* e) { return e ? 14 * e->R() : 0; }
 int pba_residuals_per_block(const pba_engine* e) { return e ? e->R() : 0; }
+int pba_num_blocks(const pba_engine* e) { return e ? e->n_blocks : 0; }
+int pba_num_points(const pba_engine* e) { return e ? e->n_points : 0; }
+int pba_num_frames(const pba_engine* e) { return e ? e->n_frames : 0; }
 
 int pba_get_records(pba_engine* e, float* records, uint8_t* valid) {
   if (!e) return fail(PBA_ERR_INVALID_ARGUMENT, "null engine");

@@ -85,6 +85,9 @@ def lib():
         "pba_synchronize": ([vp], C.c_int),
         "pba_record_floats": ([vp], C.c_int),
         "pba_residuals_per_block": ([vp], C.c_int),
+        "pba_num_blocks": ([vp], C.c_int),
+        "pba_num_points": ([vp], C.c_int),
+        "pba_num_frames": ([vp], C.c_int),
         "pba_get_records": ([vp, vp, vp], C.c_int),
         "pba_get_block_costs": ([vp, vp], C.c_int),
         "pba_get_cost": ([vp, C.POINTER(C.c_double), C.POINTER(i32)], C.c_int),
