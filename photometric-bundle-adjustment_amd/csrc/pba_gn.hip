@@ -752,6 +752,184 @@ __global__ __launch_bounds__(256) void band_solve_kernel(const BandArgs a) {
 }
 
 // ------------------------------------------------------------------------------------------------
+// Block cyclic reduction (bandwidth B ≤ 8 block rows).  Super-row I = block rows [I·B, (I+1)·B) turns the
+// banded reduced camera system into a block-tridiagonal SPD system with m×m blocks (m = 6B): diagonal D_I,
+// coupling U_I = S(I, I+1).  Each level eliminates the odd super-rows j in parallel (one workgroup each:
+// dense Cholesky of D_j in LDS, X_j = D_j⁻¹ [U_{j−1}ᵀ | U_j | b_j]) and rebuilds the even ones
+// (D'_i = D_i − U_{i−1}ᵀ X_{i−1}^U − U_i X_{i+1}^L, U'_i = −U_i X_{i+1}^U, b'_i likewise).  log2(N/B) levels
+// replace the N-step sequential factorisation; back-substitution runs the levels in reverse
+// (x_j = X_j^b − X_j^L x_{j−1} − X_j^U x_{j+1}).
+// ------------------------------------------------------------------------------------------------
+struct CrLevel {
+  double* D;   // n × m²
+  double* U;   // n × m²   (U of the last row = 0)
+  double* b;   // n × m
+  double* X;   // ⌊n/2⌋ × m × (2m+1)
+  double* x;   // n × m
+  int n;
+};
+
+template <int M>
+__global__ __launch_bounds__(256) void cr_build_kernel(const double* __restrict__ Sband, CrLevel L0, int N, int B) {
+  // one thread per element of D_I, U_I and b_I of level 0 (rows ≥ N are identity padding)
+  const long long tid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long long nD = (long long)L0.n * M * M;
+  const int ROWG = (B + 1) * 36 + 6;
+  auto lower = [&](int i, int j, int r, int c) -> double {  // S[6i+r][6j+c] for i ≥ j within the band
+    if (i >= N || j >= N) return (i == j && r == c) ? 1.0 : 0.0;
+    if (i - j > B) return 0.0;
+    return Sband[(long long)i * ROWG + (j - i + B) * 36 + r * 6 + c];
+  };
+  if (tid < nD) {
+    const int I = (int)(tid / (M * M)), e = (int)(tid % (M * M)), R = e / M, C = e % M;
+    const int i = I * B + R / 6, j = I * B + C / 6, r = R % 6, c = C % 6;
+    L0.D[tid] = i >= j ? lower(i, j, r, c) : lower(j, i, c, r);
+    // U_I: rows of super-row I, columns of super-row I+1 → S[6i+r][6j'+c] with j' > i
+    const int jn = (I + 1) * B + C / 6;
+    L0.U[tid] = (I + 1 < L0.n) ? lower(jn, i, c, r) : 0.0;
+    return;
+  }
+  const long long t = tid - nD;
+  if (t < (long long)L0.n * M) {
+    const int I = (int)(t / M), R = (int)(t % M), i = I * B + R / 6;
+    L0.b[t] = i < N ? -Sband[(long long)i * ROWG + (B + 1) * 36 + R % 6] : 0.0;
+  }
+}
+
+// Eliminate super-row j (odd rows of the level, or the single root row when `root`): X = D⁻¹ [U_{j−1}ᵀ | U_j | b].
+template <int M>
+__global__ __launch_bounds__(256) void cr_odd_kernel(CrLevel L, int root, int* status) {
+  constexpr int NC = 2 * M + 1;
+  __shared__ double A[M][M + 1];
+  __shared__ double Y[M][NC + 1];
+  __shared__ double inv[M];
+  __shared__ int fail;
+  const int tid = threadIdx.x;
+  const int j = root ? 0 : 2 * blockIdx.x + 1;
+  const double* D = L.D + (long long)j * M * M;
+  for (int e = tid; e < M * M; e += 256) A[e / M][e % M] = D[e];
+  for (int e = tid; e < M * NC; e += 256) {
+    const int r = e / NC, c = e % NC;
+    double v;
+    if (c < M) v = root ? 0.0 : L.U[(long long)(j - 1) * M * M + c * M + r];          // U_{j−1}ᵀ
+    else if (c < 2 * M) v = (!root && j + 1 < L.n) ? L.U[(long long)j * M * M + r * M + (c - M)] : 0.0;  // U_j
+    else v = L.b[(long long)j * M + r];
+    Y[r][c] = v;
+  }
+  if (tid == 0) fail = 0;
+  __syncthreads();
+  // dense Cholesky, right-looking, lower triangle in place
+  for (int k = 0; k < M; ++k) {
+    if (tid == 0) {
+      const double p = A[k][k];
+      if (!(p > 0.0)) fail = 1;
+      const double il = p > 0.0 ? rsqrt_nr(p) : 0.0;
+      A[k][k] = p * il;
+      inv[k] = il;
+    }
+    __syncthreads();
+    for (int r = k + 1 + tid; r < M; r += 256) A[r][k] *= inv[k];
+    __syncthreads();
+    const int nt = M - 1 - k;
+    for (int e = tid; e < nt * nt; e += 256) {
+      const int r = k + 1 + e / nt, c = k + 1 + e % nt;
+      if (c <= r) A[r][c] -= A[r][k] * A[c][k];
+    }
+    __syncthreads();
+  }
+  if (fail) {
+    if (tid == 0) atomicOr(status, 1);
+    return;
+  }
+  // L Y = RHS, then Lᵀ X = Y (columns in parallel)
+  for (int k = 0; k < M; ++k) {
+    for (int c = tid; c < NC; c += 256) Y[k][c] *= inv[k];
+    __syncthreads();
+    for (int e = tid; e < (M - 1 - k) * NC; e += 256) {
+      const int r = k + 1 + e / NC, c = e % NC;
+      Y[r][c] -= A[r][k] * Y[k][c];
+    }
+    __syncthreads();
+  }
+  for (int k = M - 1; k >= 0; --k) {
+    for (int c = tid; c < NC; c += 256) Y[k][c] *= inv[k];
+    __syncthreads();
+    for (int e = tid; e < k * NC; e += 256) {
+      const int r = e / NC, c = e % NC;
+      Y[r][c] -= A[k][r] * Y[k][c];
+    }
+    __syncthreads();
+  }
+  if (root) {
+    for (int r = tid; r < M; r += 256) L.x[r] = Y[r][2 * M];
+    return;
+  }
+  double* X = L.X + (long long)(j / 2) * M * NC;
+  for (int e = tid; e < M * NC; e += 256) X[e] = Y[e / NC][e % NC];
+}
+
+// Rebuild even super-row i of level L as row i/2 of level L+1.
+template <int M>
+__global__ __launch_bounds__(256) void cr_even_kernel(CrLevel L, CrLevel Ln) {
+  constexpr int NC = 2 * M + 1;
+  const int i = 2 * blockIdx.x, in = blockIdx.x;
+  const bool left = i - 1 >= 0, right = i + 1 < L.n;
+  const double* Ul = left ? L.U + (long long)(i - 1) * M * M : nullptr;  // U_{i−1}
+  const double* Ui = L.U + (long long)i * M * M;                          // U_i
+  const double* Xl = left ? L.X + (long long)((i - 1) / 2) * M * NC : nullptr;
+  const double* Xr = right ? L.X + (long long)((i + 1) / 2) * M * NC : nullptr;
+  for (int e = threadIdx.x; e < 2 * M * M + M; e += 256) {
+    if (e < M * M) {  // D'
+      const int r = e / M, c = e % M;
+      double v = L.D[(long long)i * M * M + e];
+      if (left)
+        for (int q = 0; q < M; ++q) v -= Ul[q * M + r] * Xl[q * NC + M + c];   // U_{i−1}ᵀ X^U_{i−1}
+      if (right)
+        for (int q = 0; q < M; ++q) v -= Ui[r * M + q] * Xr[q * NC + c];       // U_i X^L_{i+1}
+      Ln.D[(long long)in * M * M + e] = v;
+    } else if (e < 2 * M * M) {  // U' = −U_i X^U_{i+1}
+      const int f = e - M * M, r = f / M, c = f % M;
+      double v = 0.0;
+      if (right)
+        for (int q = 0; q < M; ++q) v -= Ui[r * M + q] * Xr[q * NC + M + c];
+      Ln.U[(long long)in * M * M + f] = v;
+    } else {  // b'
+      const int r = e - 2 * M * M;
+      double v = L.b[(long long)i * M + r];
+      if (left)
+        for (int q = 0; q < M; ++q) v -= Ul[q * M + r] * Xl[q * NC + 2 * M];
+      if (right)
+        for (int q = 0; q < M; ++q) v -= Ui[r * M + q] * Xr[q * NC + 2 * M];
+      Ln.b[(long long)in * M + r] = v;
+    }
+  }
+}
+
+// x of level L from x of level L+1.
+template <int M>
+__global__ void cr_back_kernel(CrLevel L, const double* __restrict__ xn) {
+  constexpr int NC = 2 * M + 1;
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= L.n * M) return;
+  const int row = t / M, r = t % M;
+  if ((row & 1) == 0) {
+    L.x[t] = xn[(row / 2) * M + r];
+    return;
+  }
+  const double* X = L.X + (long long)(row / 2) * M * NC + r * NC;
+  double v = X[2 * M];
+  for (int c = 0; c < M; ++c) v -= X[c] * xn[((row - 1) / 2) * M + c];
+  if (row + 1 < L.n)
+    for (int c = 0; c < M; ++c) v -= X[M + c] * xn[((row + 1) / 2) * M + c];
+  L.x[t] = v;
+}
+
+__global__ void cr_scatter_kernel(const double* __restrict__ x0, double* __restrict__ step, int N) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t < 6 * N) step[t] = x0[t];  // super-row I, element R ↔ block row I·B + R/6, component R%6
+}
+
+// ------------------------------------------------------------------------------------------------
 // Updates: poses T·exp(δ) (se3.hpp:763-784) and back-substituted inverse distances
 // ------------------------------------------------------------------------------------------------
 __device__ void se3_exp_mul(const double* T, const double* d, double* out) {
@@ -1098,13 +1276,41 @@ int gn_prepare(pba_engine* e) {
   PBA_HIP(G.S.resize((size_t)G.n_sky * 36));
   PBA_HIP(G.L.resize((size_t)G.n_sky * 36));
   G.band_kernel = G.band <= 4 ? 4 : (G.band <= 8 ? 8 : (G.band <= 16 ? 16 : 0));
-  if (const char* fs = getenv("PBA_FORCE_SKYLINE"))  // test hook: exercise the general skyline solver
-    if (fs[0] == '1') G.band_kernel = 0;
+  // solver choice: block cyclic reduction (bandwidth ≤ 8), LDS-window band Cholesky (≤ 16), skyline (any).
+  // PBA_SOLVER=cr|band|skyline forces one (test hook; cr/band fall back when the bandwidth does not allow).
+  G.solver = G.band_kernel && G.band_kernel <= 8 ? SOLVER_CR : (G.band_kernel ? SOLVER_BAND : SOLVER_SKYLINE);
+  if (const char* fs = getenv("PBA_SOLVER")) {
+    const std::string f(fs);
+    if (f == "skyline") G.solver = SOLVER_SKYLINE;
+    else if (f == "band" && G.band_kernel) G.solver = SOLVER_BAND;
+    else if (f == "cr" && G.band_kernel && G.band_kernel <= 8) G.solver = SOLVER_CR;
+  }
+  if (G.solver == SOLVER_SKYLINE) G.band_kernel = 0;
   if (G.band_kernel) {
     const size_t nb_ = (size_t)nf * ((G.band_kernel + 1) * 36 + 6);
     PBA_HIP(G.Lband.resize((size_t)nf * (G.band_kernel * 36 + 48)));  // column records
     PBA_HIP(G.Sband.resize(nb_));
     PBA_HIP(hipMemsetAsync(G.Sband.p, 0, nb_ * sizeof(double), st));  // positions outside the profile stay 0
+  }
+  G.cr_levels.clear();
+  if (G.solver == SOLVER_CR) {
+    const int M = 6 * G.band_kernel;
+    std::vector<int> ns{(nf + G.band_kernel - 1) / G.band_kernel};
+    while (ns.back() > 1) ns.push_back((ns.back() + 1) / 2);
+    size_t total = 0;
+    for (int n : ns) total += (size_t)n * M * M * 2 + (size_t)n * M * 2 + (size_t)(n / 2) * M * (2 * M + 1);
+    PBA_HIP(G.cr_buf.resize(total));
+    size_t off = 0;
+    for (int n : ns) {
+      CrLevelHost L;
+      L.n = n;
+      L.D = off; off += (size_t)n * M * M;
+      L.U = off; off += (size_t)n * M * M;
+      L.b = off; off += (size_t)n * M;
+      L.x = off; off += (size_t)n * M;
+      L.X = off; off += (size_t)(n / 2) * M * (2 * M + 1);
+      G.cr_levels.push_back(L);
+    }
   }
   PBA_HIP(G.g.resize((size_t)nf * 6));
   PBA_HIP(G.g_dir.resize((size_t)nf * 6));
@@ -1199,6 +1405,32 @@ int linearize(pba_engine* e, double* cost) {
   return PBA_OK;
 }
 
+CrLevel cr_level(GnData& G, int l) {
+  const CrLevelHost& h = G.cr_levels[l];
+  double* base = G.cr_buf.p;
+  return CrLevel{base + h.D, base + h.U, base + h.b, base + h.X, base + h.x, h.n};
+}
+
+template <int M>
+void cr_solve(pba_engine* e) {
+  GnData& G = e->gn;
+  const int nl = (int)G.cr_levels.size();
+  CrLevel L0 = cr_level(G, 0);
+  const long long nthreads = (long long)L0.n * M * M + (long long)L0.n * M;
+  cr_build_kernel<M><<<(unsigned)((nthreads + 255) / 256), 256, 0, e->stream>>>(G.Sband.p, L0, e->n_frames, G.band_kernel);
+  for (int l = 0; l + 1 < nl; ++l) {
+    CrLevel L = cr_level(G, l), Ln = cr_level(G, l + 1);
+    cr_odd_kernel<M><<<L.n / 2, 256, 0, e->stream>>>(L, 0, G.status.p);
+    cr_even_kernel<M><<<(L.n + 1) / 2, 256, 0, e->stream>>>(L, Ln);
+  }
+  cr_odd_kernel<M><<<1, 256, 0, e->stream>>>(cr_level(G, nl - 1), 1, G.status.p);
+  for (int l = nl - 2; l >= 0; --l) {
+    CrLevel L = cr_level(G, l), Ln = cr_level(G, l + 1);
+    cr_back_kernel<M><<<(L.n * M + 255) / 256, 256, 0, e->stream>>>(L, Ln.x);
+  }
+  cr_scatter_kernel<<<(6 * e->n_frames + 255) / 256, 256, 0, e->stream>>>(L0.x, G.x.p, e->n_frames);
+}
+
 // Schur complement for λ, assembly, solve and candidate state; returns the LM model decrease.
 int gn_step(pba_engine* e, double lambda, double* model_decrease, int* solver_status) {
   GnData& G = e->gn;
@@ -1211,7 +1443,11 @@ int gn_step(pba_engine* e, double lambda, double* model_decrease, int* solver_st
              G.band_kernel ? G.Sband.p : nullptr, G.band_kernel, G.n_sky, nf};
   const int nthreads = G.n_sky * 36 + 6 * nf;
   assemble_kernel<<<(nthreads + 255) / 256, 256, 0, e->stream>>>(aa, lambda);
-  if (G.band_kernel) {  // banded structure: LDS-window factorisation (the skyline buffer stays untouched)
+  if (G.solver == SOLVER_CR) {
+    PBA_HIP(hipMemsetAsync(G.status.p, 0, sizeof(int), e->stream));
+    if (G.band_kernel == 4) cr_solve<24>(e);
+    else cr_solve<48>(e);
+  } else if (G.band_kernel) {  // banded structure: LDS-window factorisation (the skyline buffer stays untouched)
     BandArgs ba{G.Sband.p, G.Lband.p, G.x.p, G.status.p, nf};
     if (G.band_kernel == 4) band_solve_kernel<4><<<1, 256, 0, e->stream>>>(ba);
     else if (G.band_kernel == 8) band_solve_kernel<8><<<1, 256, 0, e->stream>>>(ba);

@@ -228,12 +228,20 @@ struct DevBuf {
   }
 };
 
+enum : int { SOLVER_SKYLINE = 0, SOLVER_BAND = 1, SOLVER_CR = 2 };
+struct CrLevelHost {
+  size_t D = 0, U = 0, b = 0, X = 0, x = 0;
+  int n = 0;
+};
+
 // Gauss-Newton state: the symbolic analysis of the normal equations (built once per problem structure) and
 // the device buffers of one linearisation / Schur complement / solve.  See pba_gn.hip for the layouts.
 struct GnData {
   bool prepared = false;
   int lpb = 8, bpw = 32;
-  int n_chunks = 0, n_schur = 0, n_gn_points = 0, n_sky = 0, band = 0, band_kernel = 0;
+  int n_chunks = 0, n_schur = 0, n_gn_points = 0, n_sky = 0, band = 0, band_kernel = 0, solver = 0;
+  std::vector<CrLevelHost> cr_levels;  // block-cyclic-reduction level layout (offsets into cr_buf)
+  DevBuf<double> cr_buf;
   bool force_skyline = false;
   size_t lin_floats = 0, schur_doubles = 0;
   DevBuf<int> gn_block;          // GN order → original block

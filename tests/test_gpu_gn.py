@@ -114,13 +114,15 @@ def test_c3_sized_gn_iteration_runs():
     assert np.isfinite(c_new)
 
 
-@pytest.mark.parametrize("force_skyline", [False, True])
-def test_banded_and_skyline_solvers_agree(force_skyline, monkeypatch):
-    """The banded LDS-window solver (bandwidth ≤ 16 blocks) and the general skyline solver give the
-    reference step; a loop-closure block (host 0 → target n−1) forces the general path."""
-    if force_skyline:
-        monkeypatch.setenv("PBA_FORCE_SKYLINE", "1")
-    pb = synth.make_problem(n_frames=12, n_points=80, width=376, height=240, seed=51, border=12)
+@pytest.mark.parametrize("solver", ["cr", "band", "skyline"])
+@pytest.mark.parametrize("n_frames", [12, 13, 6, 37])
+def test_reduced_solvers_agree(solver, n_frames, monkeypatch):
+    """Block cyclic reduction (default for bandwidth ≤ 8 block rows), the LDS-window band Cholesky and the
+    general skyline Cholesky all give the reference step (frame counts that are not multiples of the
+    super-row size exercise the identity padding of cyclic reduction)."""
+    monkeypatch.setenv("PBA_SOLVER", solver)
+    pb = synth.make_problem(n_frames=n_frames, n_points=10 * n_frames, width=376, height=240, seed=51 + n_frames,
+                            border=12)
     fixed = (0,)
     H, g, _ = GR.linearize(pb, pb.poses, pb.rho, 9.0, fixed)
     _, gS_ref, dp_ref, dl_ref, _ = GR.schur_step(H, g, pb.n_frames, 1e-3, fixed)
