@@ -17,8 +17,8 @@ import re
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-OURS = re.compile(r"(photometric_block_kernel|geometric_block_kernel|pair_kernel|gn_\w+|schur_\w+|linearize\w*|solve\w*|"
-                  r"reduce\w*|update\w*|__amd_rocclr_copyBuffer)")
+OURS = re.compile(r"(photometric_block_kernel|geometric_block_kernel|pair_kernel|cr_\w+|assemble\w*|band_\w+|"
+                  r"skyline\w*|schur_\w+|linearize\w*|update\w*|reduce\w*|__amd_rocclr_copyBuffer)")
 
 
 def short(name):
