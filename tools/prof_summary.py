@@ -50,7 +50,8 @@ def main(tag, prefix):
             for c, (m, n) in sorted(cs.items()):
                 w.writerow([k, g, c, m, n])
     for (k, g), cs in pmc.items():
-        if "FETCH_SIZE" in cs and "WRITE_SIZE" in cs and "block_kernel" in k:
+        # the timed bench kernel: MODE 1 (full residual + Jacobian records), not the cost-only MODE 2 launch
+        if "FETCH_SIZE" in cs and "WRITE_SIZE" in cs and "block_kernel" in k and k.endswith(", 1>"):
             fetch, write = cs["FETCH_SIZE"][0] * 1024, cs["WRITE_SIZE"][0] * 1024
             out = {"kernel": k, "grid_size": int(g), "fetch_bytes_per_launch": fetch, "write_bytes_per_launch": write,
                    "hbm_bytes_per_launch": fetch + write, "profile": f"profiles/{prefix}_pmc.csv",
