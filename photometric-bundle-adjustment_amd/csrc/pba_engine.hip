@@ -78,6 +78,29 @@ __global__ void pair_kernel(const double* __restrict__ poses, const int* __restr
 }
 
 // ------------------------------------------------------------------------------------------------
+// Image relayout: row-major u8 frames → 16×8 tiles (pba_device.h).  One lane per 16-texel tile row; pad
+// texels (x ≥ W or y ≥ H) are zero and never read (taps are clamped to the image).
+// ------------------------------------------------------------------------------------------------
+__global__ void tile_images_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst, int W, int H,
+                                   int tiles_x, int tiles_y, long long n_rows) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n_rows) return;
+  // i enumerates (frame, tile, row-in-tile) in destination order → 16-B coalesced stores
+  const int r = (int)(i & 7);
+  const long long tile = i >> 3;
+  const long long tiles_per_frame = (long long)tiles_x * tiles_y;
+  const long long f = tile / tiles_per_frame;
+  const int t = (int)(tile - f * tiles_per_frame);
+  const int ty = t / tiles_x, tx = t - ty * tiles_x;
+  const int y = ty * kTileH + r, x0 = tx * kTileW;
+  union { uint8_t b[16]; uint4 v; } row;
+  const uint8_t* s = src + f * W * (long long)H + (long long)y * W;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) row.b[j] = (y < H && x0 + j < W) ? s[x0 + j] : (uint8_t)0;
+  reinterpret_cast<uint4*>(dst)[i] = row.v;
+}
+
+// ------------------------------------------------------------------------------------------------
 // Photometric block kernel: lane = (block, pixel k); a workgroup = 256/LPB consecutive blocks whose
 // records are staged in LDS and leave as one contiguous, 16-B-per-lane, non-temporal store stream.
 // MODE 0: residual part of the records only; 1: full records; 2: per-block cost/validity only.
@@ -239,7 +262,8 @@ KernelArgs make_kernel_args(pba_engine* e, const PairRec* pairs, const double* r
   ka.images = e->images.p;
   ka.width = e->width;
   ka.height = e->height;
-  ka.frame_stride = (long long)e->width * e->height;
+  ka.tiles_x = tiles_x_of(e->width);
+  ka.frame_stride = tiled_frame_bytes(e->width, e->height);
   ka.intr = e->intr.p;
   ka.intr_d = e->intr_d.p;
   ka.block_point = e->block_point.p;
@@ -372,9 +396,24 @@ static int set_frames_impl(pba_engine* e, int32_t n_frames, const int32_t* frame
   PBA_HIP(e->frame_cam.resize(n_frames));
   PBA_HIP(hipMemcpyAsync(e->frame_cam.p, frame_cam, n_frames * sizeof(int), hipMemcpyHostToDevice, e->stream));
   if (images) {
+    // frames arrive row-major (the reference's cv::Mat / pangolin image rows) and are re-tiled once on the
+    // device; host input is staged through a transient device buffer.
     const size_t bytes = (size_t)n_frames * width * height;
-    PBA_HIP(e->images.resize(bytes));
-    PBA_HIP(hipMemcpyAsync(e->images.p, images, bytes, kind, e->stream));
+    const int tx = tiles_x_of(width), ty = (height + kTileH - 1) / kTileH;
+    PBA_HIP(e->images.resize((size_t)n_frames * tiled_frame_bytes(width, height)));
+    const uint8_t* src = images;
+    DevBuf<uint8_t> staging;
+    if (kind == hipMemcpyHostToDevice) {
+      PBA_HIP(staging.resize(bytes));
+      PBA_HIP(hipMemcpyAsync(staging.p, images, bytes, kind, e->stream));
+      src = staging.p;
+    }
+    const long long n_rows = (long long)n_frames * tx * ty * kTileH;
+    tile_images_kernel<<<(unsigned)((n_rows + 255) / 256), 256, 0, e->stream>>>(src, e->images.p, width, height,
+                                                                               tx, ty, n_rows);
+    PBA_HIP(hipGetLastError());
+    PBA_HIP(hipStreamSynchronize(e->stream));
+    staging.release();
     e->have_images = true;
   }
   PBA_HIP(hipStreamSynchronize(e->stream));

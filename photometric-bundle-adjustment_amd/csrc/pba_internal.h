@@ -28,8 +28,8 @@ static_assert(sizeof(PairRec) == 128, "PairRec layout");
 
 struct KernelArgs {
   const uint8_t* images;
-  int width, height;
-  long long frame_stride;
+  int width, height, tiles_x;
+  long long frame_stride;        // bytes per tiled frame
   const float* intr;             // 8 floats per camera (Jacobian chain)
   const double* intr_d;          // 8 doubles per camera (warp / projection)
   const int* block_point;
@@ -121,7 +121,7 @@ __device__ __forceinline__ Row photometric_row(const KernelArgs& a, int blk, int
   if (dom) {
     double u, v;
     project<MODEL>(ktd, p, u, v);
-    bilinear(a.images + pp.target * a.frame_stride, a.width, a.height, u, v, I, gx, gy);
+    bilinear(a.images + pp.target * a.frame_stride, a.width, a.height, a.tiles_x, u, v, I, gx, gy);
   }
   o.r = I - Ih;  // photometric_error.h:179
   o.ok = dom && isfinite(o.r);
@@ -206,6 +206,10 @@ template <class T>
 struct DevBuf {
   T* p = nullptr;
   size_t n = 0;
+  DevBuf() = default;
+  DevBuf(const DevBuf&) = delete;
+  DevBuf& operator=(const DevBuf&) = delete;
+  ~DevBuf() { release(); }
   hipError_t resize(size_t count) {
     if (count <= n && p) return hipSuccess;
     if (p) (void)hipFree(p);
