@@ -98,49 +98,47 @@ def cpu_baseline(pb, images_host, budget_s: float, threads: int):
                       f"Jet<15> dual-number AutoDiff (the reference's Ceres AutoDiff arithmetic, restated)"}
 
 
-def gn_benchmark(eng, n_frames, iters, torch, dist, dev):
-    """ms per Gauss-Newton iteration (BASELINE.json metric, part 2) on the same shard: one iteration =
-    linearise (r, J, Huber, JᵀJ/Jᵀr partials) + Schur complement + reduced-system assembly + skyline
-    Cholesky solve + pose/point update + candidate cost, with the LM accept/reject decision on the host."""
-    eng.set_fixed_frames(np.array([0, 1], np.int32))
-    lam = 1e-2
-    eng.gn_linearize()
-    eng.gn_step(lam)  # warm-up (symbolic analysis happened at the first call)
-    eng.gn_candidate_cost()
-    parts = {"linearize_ms": 0.0, "step_ms": 0.0, "cost_ms": 0.0}
-    accepted = 0
-    cost = eng.gn_linearize()
-    if dist is not None:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(iters):
-        t = time.perf_counter()
-        model, st = eng.gn_step(lam)
-        t1 = time.perf_counter()
-        parts["step_ms"] += 1e3 * (t1 - t)
-        c_new = eng.gn_candidate_cost() if st == 0 else float("inf")
-        t2 = time.perf_counter()
-        parts["cost_ms"] += 1e3 * (t2 - t1)
-        if c_new < cost:
-            eng.gn_accept()
-            accepted += 1
-            lam = max(lam / 3, 1e-8)
-        else:
-            lam *= 4
-        t3 = time.perf_counter()
-        cost = eng.gn_linearize()  # next iteration's linearisation (counted in every iteration)
-        parts["linearize_ms"] += 1e3 * (time.perf_counter() - t3)
-    torch.cuda.synchronize()
-    total = time.perf_counter() - t0
-    t = torch.tensor([total], dtype=torch.float64, device=dev)
+def all_reduce_max(torch, dist, values, dev):
+    """MAX over ranks of a few host scalars (on the device for RCCL, through the host for gloo)."""
+    on_dev = dist is not None and dist.get_backend() == "nccl"
+    t = torch.tensor(values, dtype=torch.float64, device=dev if on_dev else "cpu")
     if dist is not None:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    n = iters
-    return {"ms_per_iteration": 1e3 * float(t[0]) / n, "iterations": n, "accepted": accepted,
-            "breakdown_ms_per_iteration": {k: v / n for k, v in parts.items()},
-            "note": "host wall clock incl. the per-iteration D2H of cost / model decrease / solver status; "
-                    "noise-textured images, so steps are not expected to converge — timing only"}
+    return t.cpu()
+
+
+def gn_benchmark(eng, iters, torch, dist, dev, world):
+    """ms per Levenberg-Marquardt iteration (BASELINE.json metric, part 2) on the same problem, through the
+    engine's own LM loop (pba_solve; pba_solve_distributed with an RCCL all-reduce of the banded reduced
+    system for N>1).  An iteration = Schur complement + reduced-system solve + candidate cost, plus the
+    next linearisation (r, J, Huber, JᵀJ/Jᵀr partials) after an accepted step; function_tolerance = 0 so
+    exactly `iters` iterations run.  Two keyframes are held constant (the reference's fixed cameras)."""
+    D = importlib.import_module("photometric-bundle-adjustment_amd.distributed")
+    eng.set_fixed_frames(np.array([0, 1], np.int32))
+    eng.gn_linearize()  # symbolic analysis (once per problem structure), outside the timed region
+    opts = dict(max_iterations=iters, function_tolerance=0.0)
+    if world > 1:
+        band = D.global_band(eng, None, dev)
+        ar = D.TorchAllReduce(eng.gn_exchange_size(band), dev)
+        eng.solve_distributed(band, ar.ptr, ar, max_iterations=1)  # warm-up
+        dist.barrier()
+        torch.cuda.synchronize()
+        s = eng.solve_distributed(band, ar.ptr, ar, **opts)
+        exchange_mb = 8.0 * eng.gn_exchange_size(band) / 1e6
+    else:
+        eng.solve(max_iterations=1)  # warm-up
+        torch.cuda.synchronize()
+        s = eng.solve(**opts)
+        exchange_mb = None
+    t = all_reduce_max(torch, dist, [s["total_ms"], s["linearize_ms"], s["solve_ms"], s["cost_ms"]], dev)
+    n = max(s["iterations"], 1)
+    return {"ms_per_iteration": float(t[0]) / n, "iterations": s["iterations"], "accepted": s["successful_steps"],
+            "breakdown_ms_per_iteration": {"linearize_ms": float(t[1]) / n, "step_ms": float(t[2]) / n,
+                                           "cost_ms": float(t[3]) / n},
+            "exchange_mb_per_iteration": exchange_mb,
+            "note": "host wall clock of the engine's LM loop (pba_solve" + (f"_distributed, {dist.get_backend()} all-reduce "
+                    "(nccl = RCCL) of the banded reduced camera system + 3 scalars per iteration" if world > 1 else "") +
+                    "); noise-textured images, so the steps are not expected to converge — timing only"}
 
 
 def main():
@@ -155,7 +153,7 @@ def main():
     ap.add_argument("--height", type=int, default=480)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--gn-iterations", type=int, default=5)
+    ap.add_argument("--gn-iterations", type=int, default=10)
     args = ap.parse_args()
 
     import torch
@@ -166,29 +164,47 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}; launch N>1 with torch.distributed.run")
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
+    # PBA_BENCH_BACKEND=gloo rehearses the N>1 path with several ranks on fewer GPUs (ranks share devices)
+    backend = os.environ.get("PBA_BENCH_BACKEND", "nccl")
+    dev_index = local_rank % max(torch.cuda.device_count(), 1) if backend != "nccl" else local_rank
+    torch.cuda.set_device(dev_index)
+    dev = torch.device("cuda", dev_index)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
 
-    # ---- problem shard of this rank (host keyframes of shard `rank`, seeded per rank) ----------------
+    # ---- problem shard of this rank --------------------------------------------------------------------
+    # Global keyframe indexing: rank r hosts keyframes [r·F, (r+1)·F); its points are observed by the K
+    # keyframes after their host, so the last K hosts of a shard reach into the next shard (coupled
+    # reduced system for the multi-GPU Gauss-Newton).  Every rank holds all NF = world·F + K poses.
     K, F, Np = args.targets, args.frames, args.points
-    pb = synth.make_problem(n_frames=F, n_points=Np, K=K, width=args.width, height=args.height, kind="photometric",
+    NF = world * F + K
+    pb = synth.make_problem(n_frames=F + K, n_points=Np, K=K, width=args.width, height=args.height, kind="photometric",
                             model="pinhole", texture="noise", with_images=False, seed=42 + rank)
-    images = gpu_noise_images(torch, F, args.height, args.width, 1234 + rank, dev)
+    off = rank * F
+    pb.point_host = (pb.point_host + off).astype(np.int32)
+    pb.block_target = (pb.block_target + off).astype(np.int32)
+    pb.frame_cam = np.zeros(NF, np.int32)
+    prng = np.random.default_rng(99)  # same global poses on every rank
+    pb.poses_gt = synth.trajectory(NF)
+    pb.poses = synth.se3_plus(pb.poses_gt, 3e-3 * prng.normal(0, 1, (NF, 6)))
+    images = torch.zeros((NF, args.height, args.width), dtype=torch.uint8, device=dev)
+    images[off:off + F + K] = gpu_noise_images(torch, F + K, args.height, args.width, 1234 + rank, dev)
     host = torch.from_numpy(pb.point_host.astype(np.int64)).to(dev)
     uu = torch.from_numpy(pb.u_ref[:, 0].astype(np.int64)).to(dev)[:, None] + torch.from_numpy(pb.pattern[:, 0].astype(np.int64)).to(dev)
     vv = torch.from_numpy(pb.u_ref[:, 1].astype(np.int64)).to(dev)[:, None] + torch.from_numpy(pb.pattern[:, 1].astype(np.int64)).to(dev)
     # integer u_ref and integer pattern → the bilinear host sample is exactly the pixel value
     pb.host_intensity = images[host[:, None], vv, uu].float().cpu().numpy()
 
-    eng = engine_mod.Engine(synth.PHOTOMETRIC, synth.PINHOLE, device=local_rank, huber_width=9.0)
+    eng = engine_mod.Engine(synth.PHOTOMETRIC, synth.PINHOLE, device=dev_index, huber_width=9.0)
     eng.set_problem(pb, images_device_ptr=images.data_ptr())
     n_blocks = pb.n_blocks
     rng = np.random.default_rng(7 + rank)
     states = []
     for _ in range(2):  # alternate two perturbed states so every step evaluates a new point
-        poses = synth.se3_plus(pb.poses, 1e-3 * rng.normal(0, 1, (F, 6)))
+        poses = synth.se3_plus(pb.poses, 1e-3 * rng.normal(0, 1, (NF, 6)))
         rho = pb.rho * (1 + 0.01 * rng.normal(0, 1, Np))
         states.append((torch.from_numpy(poses).to(dev), torch.from_numpy(rho).to(dev)))
     eng.set_state_device(states[0][0].data_ptr(), states[0][1].data_ptr())
@@ -218,20 +234,19 @@ def main():
         dist.barrier()
     elapsed = t1 - t0
     kern_ms, launches = eng.kernel_timing()
-    t = torch.tensor([elapsed, kern_ms / max(launches, 1)], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    t = all_reduce_max(torch, dist if world > 1 else None, [elapsed, kern_ms / max(launches, 1)], dev)
     elapsed_max, kern_avg_ms = float(t[0]), float(t[1])
 
     gn = None
     if args.gn_iterations > 0:
-        gn = gn_benchmark(eng, F, args.gn_iterations, torch, dist if world > 1 else None, dev)
+        eng.set_state(pb.poses, pb.rho)
+        gn = gn_benchmark(eng, args.gn_iterations, torch, dist if world > 1 else None, dev, world)
 
     if rank == 0:
         ms_per_step = 1e3 * elapsed_max / args.steps
         total_blocks = n_blocks * world * args.steps
         value = total_blocks / elapsed_max
-        n_pairs = len(np.unique(pb.point_host[pb.block_point].astype(np.int64) * F + pb.block_target))
+        n_pairs = len(np.unique(pb.point_host[pb.block_point].astype(np.int64) * NF + pb.block_target))
         bpb = algorithmic_bytes_per_block(pb.P, K, n_pairs, n_blocks)
         achieved = bpb * n_blocks / (kern_avg_ms * 1e-3) / 1e9
         traffic = None
@@ -246,7 +261,7 @@ def main():
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             threads = max(1, min(16, os.cpu_count() or 1))
-            cpu = cpu_baseline(pb, images.cpu().numpy(), args.cpu_seconds, threads)
+            cpu = cpu_baseline(pb, images.cpu().numpy(), args.cpu_seconds, threads)  # N=1: all NF frames local
         out = {
             "metric": "photometric residual+jacobian blocks/sec",
             "value": value,
@@ -261,11 +276,12 @@ def main():
             "dtype": "f32",
             "data": "synthetic",
             "config": {
-                "workload": f"C4 shard per GPU: synthetic {F} keyframes x {Np} points x {pb.P}-px patch x {K} targets "
+                "workload": f"C4 shard per GPU: synthetic {F} host keyframes x {Np} points x {pb.P}-px patch x {K} targets "
                             f"= {n_blocks} residual blocks, {args.width}x{args.height} u8 images, pinhole; one step = "
                             f"full r + tangent-J evaluation (Ceres-mode records) at a new HBM-resident state",
-                "keyframes": F, "points": Np, "patch": pb.P, "targets_per_point": K, "blocks_per_gpu": n_blocks,
-                "valid_blocks": int(valid.sum()), "parallelism": f"host-keyframe shards x{world} (no data-path collective)",
+                "keyframes": F, "keyframes_global": NF, "points": Np, "patch": pb.P, "targets_per_point": K, "blocks_per_gpu": n_blocks,
+                "valid_blocks": int(valid.sum()), "parallelism": f"host-keyframe shards x{world} (evaluation: no data-path collective; "
+                                               f"GN: RCCL all-reduce of the reduced camera system)",
             },
             "roofline": {
                 "bound": "hbm",

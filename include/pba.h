@@ -174,6 +174,33 @@ int pba_get_state(pba_engine* engine, double* poses, double* inv_dist);
 int pba_gn_get_reduced_system(pba_engine* engine, double* S_dense, double* g);
 int pba_gn_get_step(pba_engine* engine, double* d_poses, double* d_inv_dist);
 
+/* Multi-GPU Gauss-Newton ------------------------------------------------------------
+ * One engine per GPU.  Every engine holds ALL keyframes (global frame indices, identical poses) and the
+ * points hosted by its shard of keyframes with all their blocks, so the inverse distances are eliminated
+ * locally (a point's blocks never leave its host's rank).  The only exchange is the sum of the per-rank
+ * reduced camera systems: rank r contributes S_r = A_r − B_r (C_r + λD_C)⁻¹ B_rᵀ, its gradients and the
+ * undamped pose diagonal; after the all-reduce every rank adds λ·clamp(diag), applies the constant frames
+ * and solves the same system (block cyclic reduction / band Cholesky), then back-substitutes its own points.
+ *
+ * The exchange buffer is a DEVICE array of pba_gn_exchange_size doubles, banded with K ∈ {4, 8, 16} block
+ * rows, K ≥ max over ranks of pba_gn_band: per frame i, (K+1) 6×6 blocks (block c = column i−K+c, row
+ * major) followed by 24 doubles [g(6) | g_direct(6) | diag(A)(6) | observed | 0…]; then 8 scalar slots. */
+int pba_gn_band(pba_engine* engine, int32_t* band);   /* local reduced-system bandwidth (block rows) */
+int pba_gn_exchange_size(pba_engine* engine, int32_t band, int64_t* count);
+/* after pba_gn_linearize: point elimination for lambda + this rank's partial system into d_exchange */
+int pba_gn_step_export(pba_engine* engine, double lambda, int32_t band, double* d_exchange);
+/* d_exchange holds the sum over ranks: damping, constant frames, solve, candidate state.  model_pose is the
+ * pose part of the LM model decrease (identical on every rank), model_points this rank's point part. */
+int pba_gn_step_import(pba_engine* engine, double lambda, int32_t band, const double* d_exchange,
+                       double* model_pose, double* model_points, int32_t* solver_status);
+/* In-place sum over all ranks of count doubles at d_buf (device memory of this engine's GPU), complete when
+ * it returns; e.g. ncclAllReduce(d_buf, d_buf, count, ncclDouble, ncclSum, comm, stream) + stream sync. */
+typedef int (*pba_allreduce_fn)(void* user, double* d_buf, int64_t count);
+/* pba_solve over all ranks: the same LM decisions everywhere (costs, model decreases and the reduced
+ * system are all-reduced through `allreduce`, which every rank must call collectively). */
+int pba_solve_distributed(pba_engine* engine, const pba_solver_options* options, int32_t band, double* d_exchange,
+                          pba_allreduce_fn allreduce, void* user, pba_solver_summary* summary);
+
 #ifdef __cplusplus
 }
 #endif

@@ -343,6 +343,98 @@ __global__ void assemble_kernel(const AsmArgs a, double lambda) {
 }
 
 // ------------------------------------------------------------------------------------------------
+// Multi-GPU exchange (include/pba.h): this rank's partial reduced system in the banded exchange layout,
+// and the finalisation of the summed system into the band solvers' input.
+// ------------------------------------------------------------------------------------------------
+constexpr int EX_TAIL = 24;  // g(6) | g_direct(6) | diag(A)(6) | observed | pad
+__host__ __device__ constexpr long long ex_row(int K) { return (long long)(K + 1) * 36 + EX_TAIL; }
+
+// One lane per element of the local skyline (same contribution lists as assemble_kernel, nothing damped or
+// fixed) and per pose-gradient element.  Positions outside the local profile stay zero (memset).
+__global__ void export_kernel(const AsmArgs a, const uint8_t* __restrict__ observed, double* __restrict__ X, int K) {
+  const int tid = blockIdx.x * blockDim.x + threadIdx.x;
+  const int nS = a.n_sky * 36;
+  const long long RS = ex_row(K);
+  if (tid < nS) {
+    const int s = tid / 36, e = tid % 36, r = e / 6, cc = e % 6;
+    const int i = a.blk_i[s], j = a.blk_j[s];
+    double sum = 0.0, dsum = 0.0;
+    for (int q = a.sky_cptr[s]; q < a.sky_cptr[s + 1]; ++q) {
+      bool schur;
+      const double v = contrib_value(a, a.sky_contrib[q], r, cc, schur);
+      sum += v;
+      if (!schur) dsum += v;
+    }
+    X[(long long)i * RS + (j - i + K) * 36 + e] = sum;
+    if (i == j && r == cc) X[(long long)i * RS + (K + 1) * 36 + 12 + r] = dsum;
+    return;
+  }
+  const int t = tid - nS;
+  if (t >= 6 * a.n_frames) return;
+  const int i = t / 6, r = t % 6;
+  double sum = 0.0, dsum = 0.0;
+  for (int q = a.g_cptr[i]; q < a.g_cptr[i + 1]; ++q) {
+    const int2 c = a.g_contrib[q];
+    if (c.y & C_SCHUR) sum -= a.part_schur[(long long)c.x + r];
+    else {
+      const double v = a.part_lin[(long long)c.x + r];
+      sum += v;
+      dsum += v;
+    }
+  }
+  double* tail = X + (long long)i * RS + (K + 1) * 36;
+  tail[r] = sum;
+  tail[6 + r] = dsum;
+  if (r == 0) tail[18] = observed[i] ? 1.0 : 0.0;
+}
+
+struct ImportArgs {
+  const double* X;         // summed exchange buffer
+  const uint8_t* fixed_req;
+  double* Sband;           // band solver input, row stride (K+1)·36 + 6
+  double* g;
+  double* g_dir;
+  double* Ddiag;
+  uint8_t* fixed;          // effective constant frames: requested, or observed by no rank
+  int n_frames;
+  int K;
+};
+
+// One lane per element of the band solver input: + λ·clamp(diag(A)) (levenberg_marquardt_strategy.cc),
+// identity rows/columns for constant frames — the same arithmetic as assemble_kernel on the summed system.
+__global__ void import_kernel(const ImportArgs a, double lambda) {
+  const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const int K = a.K;
+  const long long SR = (long long)(K + 1) * 36 + 6, RS = ex_row(K);
+  if (t >= SR * a.n_frames) return;
+  const int i = (int)(t / SR), q = (int)(t - (long long)i * SR);
+  const double* row = a.X + (long long)i * RS;
+  const double* tail = row + (K + 1) * 36;
+  const bool fi = a.fixed_req[i] || tail[18] == 0.0;
+  if (q < (K + 1) * 36) {
+    const int c = q / 36, e = q % 36, r = e / 6, cc = e % 6, j = i - K + c;
+    double val = 0.0;
+    if (j >= 0) {
+      const bool fj = a.fixed_req[j] || a.X[(long long)j * RS + (K + 1) * 36 + 18] == 0.0;
+      val = row[q];
+      if (fi || fj) {
+        val = (i == j && r == cc) ? 1.0 : 0.0;
+      } else if (i == j && r == cc) {
+        val += lambda * fmin(fmax(tail[12 + r], 1e-6), 1e32);
+      }
+    }
+    a.Sband[t] = val;
+    return;
+  }
+  const int r = q - (K + 1) * 36;
+  a.Sband[t] = fi ? 0.0 : tail[r];
+  a.g[6 * i + r] = fi ? 0.0 : tail[r];
+  a.g_dir[6 * i + r] = fi ? 0.0 : tail[6 + r];
+  a.Ddiag[6 * i + r] = fi ? 0.0 : fmin(fmax(tail[12 + r], 1e-6), 1e32);
+  if (r == 0) a.fixed[i] = fi ? 1 : 0;
+}
+
+// ------------------------------------------------------------------------------------------------
 // skyline_solve_kernel: S δ = −g, S = LLᵀ in place (block skyline, right-looking), one workgroup
 // ------------------------------------------------------------------------------------------------
 __device__ inline bool chol6(const double* A, double* L) {
@@ -1066,6 +1158,46 @@ int gn_lpb(const pba_engine* e) {
   return e->P <= 8 ? 8 : (e->P <= 16 ? 16 : 32);
 }
 
+int band_kernel_for(int band) { return band <= 4 ? 4 : (band <= 8 ? 8 : (band <= 16 ? 16 : 0)); }
+
+// Reduced-system solver buffers for band K (0: skyline only): band input Sband (row stride (K+1)·36 + 6,
+// zero outside the profile), band-Cholesky column records, cyclic-reduction levels.
+int configure_solver(pba_engine* e, int K, int solver) {
+  GnData& G = e->gn;
+  const int nf = e->n_frames;
+  hipStream_t st = e->stream;
+  G.band_kernel = K;
+  G.solver = solver;
+  G.sband_dirty = false;
+  if (K) {
+    const size_t nb_ = (size_t)nf * ((K + 1) * 36 + 6);
+    PBA_HIP(G.Lband.resize((size_t)nf * (K * 36 + 48)));  // column records
+    PBA_HIP(G.Sband.resize(nb_));
+    PBA_HIP(hipMemsetAsync(G.Sband.p, 0, nb_ * sizeof(double), st));  // positions outside the profile stay 0
+  }
+  G.cr_levels.clear();
+  if (solver == SOLVER_CR) {
+    const int M = 6 * K;
+    std::vector<int> ns{(nf + K - 1) / K};
+    while (ns.back() > 1) ns.push_back((ns.back() + 1) / 2);
+    size_t total = 0;
+    for (int n : ns) total += (size_t)n * M * M * 2 + (size_t)n * M * 2 + (size_t)(n / 2) * M * (2 * M + 1);
+    PBA_HIP(G.cr_buf.resize(total));
+    size_t off = 0;
+    for (int n : ns) {
+      CrLevelHost L;
+      L.n = n;
+      L.D = off; off += (size_t)n * M * M;
+      L.U = off; off += (size_t)n * M * M;
+      L.b = off; off += (size_t)n * M;
+      L.x = off; off += (size_t)n * M;
+      L.X = off; off += (size_t)(n / 2) * M * (2 * M + 1);
+      G.cr_levels.push_back(L);
+    }
+  }
+  return PBA_OK;
+}
+
 // Symbolic analysis: GN block order, chunks, slot layouts, skyline profile and contribution lists.
 int gn_prepare(pba_engine* e) {
   GnData& G = e->gn;
@@ -1275,43 +1407,22 @@ int gn_prepare(pba_engine* e) {
   PBA_HIP(G.fixed.upload(fixed, st));
   PBA_HIP(G.S.resize((size_t)G.n_sky * 36));
   PBA_HIP(G.L.resize((size_t)G.n_sky * 36));
-  G.band_kernel = G.band <= 4 ? 4 : (G.band <= 8 ? 8 : (G.band <= 16 ? 16 : 0));
   // solver choice: block cyclic reduction (bandwidth ≤ 8), LDS-window band Cholesky (≤ 16), skyline (any).
   // PBA_SOLVER=cr|band|skyline forces one (test hook; cr/band fall back when the bandwidth does not allow).
-  G.solver = G.band_kernel && G.band_kernel <= 8 ? SOLVER_CR : (G.band_kernel ? SOLVER_BAND : SOLVER_SKYLINE);
+  const int K = band_kernel_for(G.band);
+  int solver = K && K <= 8 ? SOLVER_CR : (K ? SOLVER_BAND : SOLVER_SKYLINE);
   if (const char* fs = getenv("PBA_SOLVER")) {
     const std::string f(fs);
-    if (f == "skyline") G.solver = SOLVER_SKYLINE;
-    else if (f == "band" && G.band_kernel) G.solver = SOLVER_BAND;
-    else if (f == "cr" && G.band_kernel && G.band_kernel <= 8) G.solver = SOLVER_CR;
+    if (f == "skyline") solver = SOLVER_SKYLINE;
+    else if (f == "band" && K) solver = SOLVER_BAND;
+    else if (f == "cr" && K && K <= 8) solver = SOLVER_CR;
   }
-  if (G.solver == SOLVER_SKYLINE) G.band_kernel = 0;
-  if (G.band_kernel) {
-    const size_t nb_ = (size_t)nf * ((G.band_kernel + 1) * 36 + 6);
-    PBA_HIP(G.Lband.resize((size_t)nf * (G.band_kernel * 36 + 48)));  // column records
-    PBA_HIP(G.Sband.resize(nb_));
-    PBA_HIP(hipMemsetAsync(G.Sband.p, 0, nb_ * sizeof(double), st));  // positions outside the profile stay 0
-  }
-  G.cr_levels.clear();
-  if (G.solver == SOLVER_CR) {
-    const int M = 6 * G.band_kernel;
-    std::vector<int> ns{(nf + G.band_kernel - 1) / G.band_kernel};
-    while (ns.back() > 1) ns.push_back((ns.back() + 1) / 2);
-    size_t total = 0;
-    for (int n : ns) total += (size_t)n * M * M * 2 + (size_t)n * M * 2 + (size_t)(n / 2) * M * (2 * M + 1);
-    PBA_HIP(G.cr_buf.resize(total));
-    size_t off = 0;
-    for (int n : ns) {
-      CrLevelHost L;
-      L.n = n;
-      L.D = off; off += (size_t)n * M * M;
-      L.U = off; off += (size_t)n * M * M;
-      L.b = off; off += (size_t)n * M;
-      L.x = off; off += (size_t)n * M;
-      L.X = off; off += (size_t)(n / 2) * M * (2 * M + 1);
-      G.cr_levels.push_back(L);
-    }
-  }
+  if (int rc = configure_solver(e, solver == SOLVER_SKYLINE ? 0 : K, solver)) return rc;
+  PBA_HIP(G.observed.upload(std::vector<uint8_t>(observed.begin(), observed.end()), st));
+  std::vector<uint8_t> req(nf, 0);
+  for (int i = 0; i < nf && i < (int)G.fixed_h.size(); ++i) req[i] = G.fixed_h[i];
+  PBA_HIP(G.fixed_req.upload(req, st));
+  PBA_HIP(G.fixed_dist.resize(nf));
   PBA_HIP(G.g.resize((size_t)nf * 6));
   PBA_HIP(G.g_dir.resize((size_t)nf * 6));
   PBA_HIP(G.Ddiag.resize((size_t)nf * 6));
@@ -1431,6 +1542,55 @@ void cr_solve(pba_engine* e) {
   cr_scatter_kernel<<<(6 * e->n_frames + 255) / 256, 256, 0, e->stream>>>(L0.x, G.x.p, e->n_frames);
 }
 
+// After a solve into G.x: solver status, candidate poses/points, and the two parts of the LM model decrease
+// L(0) − L(δ) = −gᵀδ − ½δᵀHδ = ½(λ δᵀDδ − gᵀδ)  (since (H + λD)δ = −g): pose part and point part.
+int finish_step(pba_engine* e, double lambda, const uint8_t* fixed, double* model_pose, double* model_points,
+                int* solver_status) {
+  GnData& G = e->gn;
+  const int nf = e->n_frames;
+  int status = 0;
+  PBA_HIP(hipMemcpyAsync(&status, G.status.p, sizeof(int), hipMemcpyDeviceToHost, e->stream));
+  PBA_HIP(hipStreamSynchronize(e->stream));
+  if (solver_status) *solver_status = status;
+  *model_pose = *model_points = 0.0;
+  if (status != 0) return PBA_OK;
+  const int gp = (nf + kBlockThreads - 1) / kBlockThreads;
+  const int gq = (G.n_gn_points + kBlockThreads - 1) / kBlockThreads;
+  pose_update_kernel<<<gp, kBlockThreads, 0, e->stream>>>(e->poses.p, G.x.p, G.g_dir.p, G.Ddiag.p, fixed,
+                                                          G.poses_new.p, G.red.p, nf);
+  PointUpdateArgs pa_{G.pt_data.p, G.pt_first.p, G.pt_nblk.p, G.pt_orig.p, G.pt_host.p, G.gn_target.p,
+                      G.blk_schur.p, G.x.p, fixed, e->rho.p, G.rho_new.p, G.drho.p, G.red.p + 2 * gp,
+                      G.n_gn_points};
+  if (gq > 0) point_update_kernel<<<gq, kBlockThreads, 0, e->stream>>>(pa_, lambda);
+  PBA_HIP(hipGetLastError());
+  PBA_HIP(hipMemcpyAsync(G.red_h.data(), G.red.p, sizeof(double) * 2 * (gp + gq), hipMemcpyDeviceToHost, e->stream));
+  PBA_HIP(hipStreamSynchronize(e->stream));
+  double dg = 0, dD = 0, qg = 0, qD = 0;
+  for (int i = 0; i < gp; ++i) { dg += G.red_h[2 * i]; dD += G.red_h[2 * i + 1]; }
+  for (int i = gp; i < gp + gq; ++i) { qg += G.red_h[2 * i]; qD += G.red_h[2 * i + 1]; }
+  *model_pose = 0.5 * (lambda * dD - dg);
+  *model_points = 0.5 * (lambda * qD - qg);
+  return PBA_OK;
+}
+
+// Band solvers on G.Sband (block cyclic reduction for K ≤ 8, LDS-window band Cholesky for K = 16).
+int band_solve(pba_engine* e) {
+  GnData& G = e->gn;
+  const int nf = e->n_frames;
+  if (G.solver == SOLVER_CR) {
+    PBA_HIP(hipMemsetAsync(G.status.p, 0, sizeof(int), e->stream));
+    if (G.band_kernel == 4) cr_solve<24>(e);
+    else cr_solve<48>(e);
+  } else {
+    BandArgs ba{G.Sband.p, G.Lband.p, G.x.p, G.status.p, nf};
+    if (G.band_kernel == 4) band_solve_kernel<4><<<1, 256, 0, e->stream>>>(ba);
+    else if (G.band_kernel == 8) band_solve_kernel<8><<<1, 256, 0, e->stream>>>(ba);
+    else band_solve_kernel<16><<<1, 256, 0, e->stream>>>(ba);
+  }
+  PBA_HIP(hipGetLastError());
+  return PBA_OK;
+}
+
 // Schur complement for λ, assembly, solve and candidate state; returns the LM model decrease.
 int gn_step(pba_engine* e, double lambda, double* model_decrease, int* solver_status) {
   GnData& G = e->gn;
@@ -1441,44 +1601,23 @@ int gn_step(pba_engine* e, double lambda, double* model_decrease, int* solver_st
   AsmArgs aa{G.part_lin.p, G.part_schur.p, G.sky_cptr.p, G.sky_contrib.p, G.g_cptr.p, G.g_contrib.p,
              G.sky_blk_i.p, G.sky_blk_j.p, G.fixed.p, G.S.p, G.g.p, G.g_dir.p, G.Ddiag.p,
              G.band_kernel ? G.Sband.p : nullptr, G.band_kernel, G.n_sky, nf};
+  if (G.sband_dirty && G.band_kernel) {  // a distributed import filled the whole band: clear the off-profile part
+    PBA_HIP(hipMemsetAsync(G.Sband.p, 0, sizeof(double) * (size_t)nf * ((G.band_kernel + 1) * 36 + 6), e->stream));
+    G.sband_dirty = false;
+  }
   const int nthreads = G.n_sky * 36 + 6 * nf;
   assemble_kernel<<<(nthreads + 255) / 256, 256, 0, e->stream>>>(aa, lambda);
-  if (G.solver == SOLVER_CR) {
-    PBA_HIP(hipMemsetAsync(G.status.p, 0, sizeof(int), e->stream));
-    if (G.band_kernel == 4) cr_solve<24>(e);
-    else cr_solve<48>(e);
-  } else if (G.band_kernel) {  // banded structure: LDS-window factorisation (the skyline buffer stays untouched)
-    BandArgs ba{G.Sband.p, G.Lband.p, G.x.p, G.status.p, nf};
-    if (G.band_kernel == 4) band_solve_kernel<4><<<1, 256, 0, e->stream>>>(ba);
-    else if (G.band_kernel == 8) band_solve_kernel<8><<<1, 256, 0, e->stream>>>(ba);
-    else band_solve_kernel<16><<<1, 256, 0, e->stream>>>(ba);
+  if (G.band_kernel) {
+    if (int rc = band_solve(e)) return rc;
   } else {
     PBA_HIP(hipMemcpyAsync(G.L.p, G.S.p, sizeof(double) * 36 * (size_t)G.n_sky, hipMemcpyDeviceToDevice, e->stream));
     SolveArgs so{G.L.p, G.sky_first.p, G.sky_row.p, G.sky_last.p, G.g.p, G.Linv.p, G.x.p, G.status.p, nf};
     skyline_solve_kernel<<<1, 256, 0, e->stream>>>(so);
   }
   PBA_HIP(hipGetLastError());
-  int status = 0;
-  PBA_HIP(hipMemcpyAsync(&status, G.status.p, sizeof(int), hipMemcpyDeviceToHost, e->stream));
-  PBA_HIP(hipStreamSynchronize(e->stream));
-  if (solver_status) *solver_status = status;
-  if (status != 0) {
-    if (model_decrease) *model_decrease = 0.0;
-    return PBA_OK;
-  }
-  const int gp = (nf + kBlockThreads - 1) / kBlockThreads;
-  const int gq = (G.n_gn_points + kBlockThreads - 1) / kBlockThreads;
-  pose_update_kernel<<<gp, kBlockThreads, 0, e->stream>>>(e->poses.p, G.x.p, G.g_dir.p, G.Ddiag.p, G.fixed.p,
-                                                          G.poses_new.p, G.red.p, nf);
-  PointUpdateArgs pa_{G.pt_data.p, G.pt_first.p, G.pt_nblk.p, G.pt_orig.p, G.pt_host.p, G.gn_target.p,
-                      G.blk_schur.p, G.x.p, G.fixed.p, e->rho.p, G.rho_new.p, G.drho.p, G.red.p + 2 * gp,
-                      G.n_gn_points};
-  point_update_kernel<<<gq, kBlockThreads, 0, e->stream>>>(pa_, lambda);
-  PBA_HIP(hipGetLastError());
-  double dg, dD;
-  if (int rc = read_red(e, gp + gq, &dg, &dD)) return rc;
-  // LM model decrease L(0) − L(δ) = −gᵀδ − ½δᵀHδ = ½(λ δᵀDδ − gᵀδ)   since (H + λD)δ = −g
-  if (model_decrease) *model_decrease = 0.5 * (lambda * dD - dg);
+  double mp = 0.0, mq = 0.0;
+  if (int rc = finish_step(e, lambda, G.fixed.p, &mp, &mq, solver_status)) return rc;
+  if (model_decrease) *model_decrease = mp + mq;
   return PBA_OK;
 }
 
@@ -1493,6 +1632,64 @@ int accept(pba_engine* e) {
   GnData& G = e->gn;
   PBA_HIP(hipMemcpyAsync(e->poses.p, G.poses_new.p, sizeof(double) * 7 * e->n_frames, hipMemcpyDeviceToDevice, e->stream));
   PBA_HIP(hipMemcpyAsync(e->rho.p, G.rho_new.p, sizeof(double) * e->n_points, hipMemcpyDeviceToDevice, e->stream));
+  return PBA_OK;
+}
+
+// ---- multi-GPU step (include/pba.h) ------------------------------------------------------------
+int exchange_K(pba_engine* e, int band, int* K) {
+  *K = band_kernel_for(std::max(band, e->gn.band));
+  if (band < e->gn.band) return fail(PBA_ERR_INVALID_ARGUMENT, "band below this rank's reduced-system bandwidth");
+  if (*K == 0) return fail(PBA_ERR_INVALID_ARGUMENT, "distributed solve needs a reduced-system bandwidth <= 16");
+  return PBA_OK;
+}
+
+long long exchange_count(pba_engine* e, int K) { return (long long)e->n_frames * ex_row(K) + 8; }
+
+int step_export(pba_engine* e, double lambda, int band, double* X) {
+  GnData& G = e->gn;
+  int K;
+  if (int rc = exchange_K(e, band, &K)) return rc;
+  const int nf = e->n_frames;
+  SchurArgs sa{G.schur_desc.p, G.schur_aux.p, G.schur_pairs.p, G.pt_first.p, G.pt_nblk.p, G.blk_lv.p,
+               G.blk_schur.p, G.part_schur.p, G.pt_data.p, G.n_schur};
+  if (G.n_schur > 0) schur_kernel<<<G.n_schur, kBlockThreads, 0, e->stream>>>(sa, lambda);
+  PBA_HIP(hipMemsetAsync(X, 0, sizeof(double) * (size_t)nf * ex_row(K), e->stream));
+  AsmArgs aa{G.part_lin.p, G.part_schur.p, G.sky_cptr.p, G.sky_contrib.p, G.g_cptr.p, G.g_contrib.p,
+             G.sky_blk_i.p, G.sky_blk_j.p, G.fixed.p, G.S.p, G.g.p, G.g_dir.p, G.Ddiag.p, nullptr, K, G.n_sky, nf};
+  const int nthreads = G.n_sky * 36 + 6 * nf;
+  export_kernel<<<(nthreads + 255) / 256, 256, 0, e->stream>>>(aa, G.observed.p, X, K);
+  PBA_HIP(hipGetLastError());
+  return PBA_OK;
+}
+
+int step_import(pba_engine* e, double lambda, int band, const double* X, double* model_pose, double* model_points,
+                int* solver_status) {
+  GnData& G = e->gn;
+  int K;
+  if (int rc = exchange_K(e, band, &K)) return rc;
+  if (G.band_kernel != K || G.solver == SOLVER_SKYLINE) {
+    const char* fs = getenv("PBA_SOLVER");
+    const int solver = (K <= 8 && !(fs && std::string(fs) == "band")) ? SOLVER_CR : SOLVER_BAND;
+    if (int rc = configure_solver(e, K, solver)) return rc;
+  }
+  const int nf = e->n_frames;
+  ImportArgs ia{X, G.fixed_req.p, G.Sband.p, G.g.p, G.g_dir.p, G.Ddiag.p, G.fixed_dist.p, nf, K};
+  const long long n = (long long)nf * ((K + 1) * 36 + 6);
+  import_kernel<<<(unsigned)((n + 255) / 256), 256, 0, e->stream>>>(ia, lambda);
+  PBA_HIP(hipGetLastError());
+  G.sband_dirty = true;
+  if (int rc = band_solve(e)) return rc;
+  return finish_step(e, lambda, G.fixed_dist.p, model_pose, model_points, solver_status);
+}
+
+// Collective helper: Σ over ranks of n ≤ 8 host scalars through the scalar slots of the exchange buffer.
+int allreduce_scalars(pba_engine* e, double* X, int K, pba_allreduce_fn fn, void* user, double* v, int n) {
+  double* slot = X + (long long)e->n_frames * ex_row(K);
+  PBA_HIP(hipMemcpyAsync(slot, v, sizeof(double) * n, hipMemcpyHostToDevice, e->stream));
+  PBA_HIP(hipStreamSynchronize(e->stream));
+  if (int rc = fn(user, slot, n)) return fail(PBA_ERR_DEVICE, "allreduce callback failed (" + std::to_string(rc) + ")");
+  PBA_HIP(hipMemcpyAsync(v, slot, sizeof(double) * n, hipMemcpyDeviceToHost, e->stream));
+  PBA_HIP(hipStreamSynchronize(e->stream));
   return PBA_OK;
 }
 
@@ -1586,11 +1783,62 @@ int pba_gn_get_step(pba_engine* e, double* dposes, double* drho) {
   return PBA_OK;
 }
 
+int pba_gn_band(pba_engine* e, int32_t* band) {
+  if (int rc = ensure_prepared(e)) return rc;
+  if (!band) return fail(PBA_ERR_INVALID_ARGUMENT, "null band");
+  *band = e->gn.band;
+  return PBA_OK;
+}
+
+int pba_gn_exchange_size(pba_engine* e, int32_t band, int64_t* count) {
+  if (int rc = ensure_prepared(e)) return rc;
+  if (!count) return fail(PBA_ERR_INVALID_ARGUMENT, "null count");
+  int K;
+  if (int rc = exchange_K(e, band, &K)) return rc;
+  *count = exchange_count(e, K);
+  return PBA_OK;
+}
+
+int pba_gn_step_export(pba_engine* e, double lambda, int32_t band, double* d_exchange) {
+  if (int rc = ensure_prepared(e)) return rc;
+  if (!d_exchange) return fail(PBA_ERR_INVALID_ARGUMENT, "null exchange buffer");
+  if (!(lambda >= 0.0)) return fail(PBA_ERR_INVALID_ARGUMENT, "lambda must be >= 0");
+  if (int rc = step_export(e, lambda, band, d_exchange)) return rc;
+  PBA_HIP(hipStreamSynchronize(e->stream));
+  return PBA_OK;
+}
+
+int pba_gn_step_import(pba_engine* e, double lambda, int32_t band, const double* d_exchange, double* model_pose,
+                       double* model_points, int32_t* solver_status) {
+  if (int rc = ensure_prepared(e)) return rc;
+  if (!d_exchange) return fail(PBA_ERR_INVALID_ARGUMENT, "null exchange buffer");
+  if (!(lambda >= 0.0)) return fail(PBA_ERR_INVALID_ARGUMENT, "lambda must be >= 0");
+  double mp = 0.0, mq = 0.0;
+  int st = 0;
+  if (int rc = step_import(e, lambda, band, d_exchange, &mp, &mq, &st)) return rc;
+  if (model_pose) *model_pose = mp;
+  if (model_points) *model_points = mq;
+  if (solver_status) *solver_status = st;
+  return PBA_OK;
+}
+
+}  // extern "C"
+
+namespace {
+
+struct Reducer {  // multi-GPU collective context of pba_solve_distributed (null: single GPU)
+  pba_allreduce_fn fn;
+  void* user;
+  double* X;
+  int band, K;
+};
+
 // Levenberg-Marquardt (trust_region_minimizer.cc + levenberg_marquardt_strategy.cc semantics):
 // μ = 1/radius, step accepted when (cost − cost_new)/model_decrease > min_relative_decrease (1e-3);
 // success: radius /= max(1/3, 1 − (2ρ − 1)³), decrease factor 2; failure: radius /= factor, factor *= 2.
-int pba_solve(pba_engine* e, const pba_solver_options* o, pba_solver_summary* sum) {
-  if (int rc = ensure_prepared(e)) return rc;
+// With a Reducer every cost, model decrease and the reduced system are sums over ranks, so all ranks take
+// the same decisions and the same pose steps.
+int lm_loop(pba_engine* e, const pba_solver_options* o, const Reducer* red, pba_solver_summary* sum) {
   pba_solver_options opt{};
   opt.max_iterations = 20;
   opt.initial_trust_region_radius = 1e4;
@@ -1603,6 +1851,8 @@ int pba_solve(pba_engine* e, const pba_solver_options* o, pba_solver_summary* su
   double cost = 0.0;
   double t = now_ms();
   if (int rc = linearize(e, &cost)) return rc;
+  if (red)
+    if (int rc = allreduce_scalars(e, red->X, red->K, red->fn, red->user, &cost, 1)) return rc;
   s.linearize_ms += now_ms() - t;
   s.initial_cost = cost;
   double radius = opt.initial_trust_region_radius, factor = 2.0;
@@ -1610,11 +1860,34 @@ int pba_solve(pba_engine* e, const pba_solver_options* o, pba_solver_summary* su
   s.termination = PBA_TERMINATION_MAX_ITERATIONS;
   for (; iter < opt.max_iterations; ++iter) {
     const double lambda = 1.0 / radius;
-    double model = 0.0;
+    double model = 0.0, cost_new = 0.0;
     int st = 0;
     t = now_ms();
-    if (int rc = gn_step(e, lambda, &model, &st)) return rc;
-    s.solve_ms += now_ms() - t;
+    if (!red) {
+      if (int rc = gn_step(e, lambda, &model, &st)) return rc;
+      s.solve_ms += now_ms() - t;
+      if (st == 0 && model > 0.0) {
+        t = now_ms();
+        if (int rc = candidate_cost(e, &cost_new)) return rc;
+        s.cost_ms += now_ms() - t;
+      }
+    } else {
+      if (int rc = step_export(e, lambda, red->band, red->X)) return rc;
+      PBA_HIP(hipStreamSynchronize(e->stream));
+      if (int rc = red->fn(red->user, red->X, (long long)e->n_frames * ex_row(red->K)))
+        return fail(PBA_ERR_DEVICE, "allreduce callback failed (" + std::to_string(rc) + ")");
+      double mp = 0.0, mq = 0.0;
+      if (int rc = step_import(e, lambda, red->band, red->X, &mp, &mq, &st)) return rc;
+      s.solve_ms += now_ms() - t;
+      double v[2] = {mq, 0.0};
+      t = now_ms();
+      if (st == 0)  // st is identical on every rank (same summed system)
+        if (int rc = candidate_cost(e, &v[1])) return rc;
+      if (int rc = allreduce_scalars(e, red->X, red->K, red->fn, red->user, v, 2)) return rc;
+      s.cost_ms += now_ms() - t;
+      model = mp + v[0];
+      cost_new = v[1];
+    }
     if (st != 0 || !(model > 0.0)) {  // non-positive-definite or no predicted decrease: shrink the region
       radius /= factor;
       factor *= 2.0;
@@ -1622,10 +1895,6 @@ int pba_solve(pba_engine* e, const pba_solver_options* o, pba_solver_summary* su
       if (radius < 1e-32) { s.termination = PBA_TERMINATION_FAILURE; break; }
       continue;
     }
-    double cost_new = 0.0;
-    t = now_ms();
-    if (int rc = candidate_cost(e, &cost_new)) return rc;
-    s.cost_ms += now_ms() - t;
     const double rel = (cost - cost_new) / model;
     if (rel > opt.min_relative_decrease && std::isfinite(cost_new)) {
       if (int rc = accept(e)) return rc;
@@ -1655,6 +1924,24 @@ int pba_solve(pba_engine* e, const pba_solver_options* o, pba_solver_summary* su
   s.total_ms = now_ms() - t0;
   if (sum) *sum = s;
   return PBA_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int pba_solve(pba_engine* e, const pba_solver_options* o, pba_solver_summary* sum) {
+  if (int rc = ensure_prepared(e)) return rc;
+  return lm_loop(e, o, nullptr, sum);
+}
+
+int pba_solve_distributed(pba_engine* e, const pba_solver_options* o, int32_t band, double* d_exchange,
+                          pba_allreduce_fn allreduce, void* user, pba_solver_summary* sum) {
+  if (int rc = ensure_prepared(e)) return rc;
+  if (!d_exchange || !allreduce) return fail(PBA_ERR_INVALID_ARGUMENT, "null exchange buffer or allreduce");
+  Reducer r{allreduce, user, d_exchange, band, 0};
+  if (int rc = exchange_K(e, band, &r.K)) return rc;
+  return lm_loop(e, o, &r, sum);
 }
 
 }  // extern "C"

@@ -269,6 +269,8 @@ struct GnData {
   DevBuf<int> sky_blk_i, sky_blk_j;  // skyline block → (row pose, column pose)
   DevBuf<double> S, L, Sband, Lband, g, g_dir, Ddiag, Linv, x;  // skyline system, its factor, rhs, direct gradient, LM diagonal, L_kk⁻¹, step
   DevBuf<uint8_t> fixed;
+  DevBuf<uint8_t> observed, fixed_req, fixed_dist;  // multi-GPU: local observation flags, requested / effective constants
+  bool sband_dirty = false;                         // Sband fully written by a distributed import
   std::vector<uint8_t> fixed_h;
   DevBuf<double> poses_new, rho_new, red;
   DevBuf<int> status;

@@ -44,6 +44,10 @@ class SolverSummary(C.Structure):
         return {f: getattr(self, f) for f, _ in self._fields_}
 
 
+# int (*pba_allreduce_fn)(void* user, double* d_buf, int64_t count)
+ALLREDUCE_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_int64)
+
+
 def build(force: bool = False) -> str:
     """Compile csrc/libpba.so for gfx950 with hipcc (in-tree)."""
     args = ["make", "-s", "-C", CSRC]
@@ -105,6 +109,13 @@ def lib():
         "pba_get_state": ([vp, vp, vp], C.c_int),
         "pba_gn_get_reduced_system": ([vp, vp, vp], C.c_int),
         "pba_gn_get_step": ([vp, vp, vp], C.c_int),
+        "pba_gn_band": ([vp, C.POINTER(i32)], C.c_int),
+        "pba_gn_exchange_size": ([vp, i32, C.POINTER(C.c_int64)], C.c_int),
+        "pba_gn_step_export": ([vp, C.c_double, i32, vp], C.c_int),
+        "pba_gn_step_import": ([vp, C.c_double, i32, vp, C.POINTER(C.c_double), C.POINTER(C.c_double),
+                                C.POINTER(i32)], C.c_int),
+        "pba_solve_distributed": ([vp, C.POINTER(SolverOptions), i32, vp, ALLREDUCE_FN, vp,
+                                   C.POINTER(SolverSummary)], C.c_int),
     }
     for name, (argt, rest) in sig.items():
         f = getattr(L, name)
@@ -254,6 +265,51 @@ class Engine:
                           min_relative_decrease)
         s = SolverSummary()
         _check(self._L.pba_solve(self._h, C.byref(o), C.byref(s)), "pba_solve")
+        return s.as_dict()
+
+    # -- multi-GPU Gauss-Newton (include/pba.h §8e; host driver in distributed.py) ------------------
+    def gn_band(self) -> int:
+        b = C.c_int32()
+        _check(self._L.pba_gn_band(self._h, C.byref(b)), "pba_gn_band")
+        return b.value
+
+    def gn_exchange_size(self, band: int) -> int:
+        n = C.c_int64()
+        _check(self._L.pba_gn_exchange_size(self._h, band, C.byref(n)), "pba_gn_exchange_size")
+        return n.value
+
+    def gn_step_export(self, lam: float, band: int, exchange_ptr: int):
+        _check(self._L.pba_gn_step_export(self._h, lam, band, C.c_void_p(exchange_ptr)), "pba_gn_step_export")
+
+    def gn_step_import(self, lam: float, band: int, exchange_ptr: int):
+        """(model decrease pose part, this rank's point part, solver status)"""
+        mp, mq, st = C.c_double(), C.c_double(), C.c_int32()
+        _check(self._L.pba_gn_step_import(self._h, lam, band, C.c_void_p(exchange_ptr), C.byref(mp), C.byref(mq),
+                                          C.byref(st)), "pba_gn_step_import")
+        return mp.value, mq.value, st.value
+
+    def solve_distributed(self, band: int, exchange_ptr: int, allreduce, max_iterations=20,
+                          initial_trust_region_radius=1e4, function_tolerance=1e-6, min_relative_decrease=1e-3) -> dict:
+        """pba_solve_distributed; `allreduce(ptr, count) -> None` sums `count` doubles at device address `ptr`
+        over all ranks in place (collective, complete on return)."""
+        err = []
+
+        def cb(_user, ptr, count):
+            try:
+                allreduce(ptr, count)
+                return 0
+            except BaseException as ex:  # surfaced after the C call returns
+                err.append(ex)
+                return 1
+
+        fn = ALLREDUCE_FN(cb)
+        o = SolverOptions(max_iterations, 0, initial_trust_region_radius, function_tolerance, 1e-8,
+                          min_relative_decrease)
+        s = SolverSummary()
+        rc = self._L.pba_solve_distributed(self._h, C.byref(o), band, C.c_void_p(exchange_ptr), fn, None, C.byref(s))
+        if err:
+            raise err[0]
+        _check(rc, "pba_solve_distributed")
         return s.as_dict()
 
     def get_state(self):

@@ -128,3 +128,35 @@ def lm(pb, a, fixed=(), max_iterations=20, radius=1e4, function_tolerance=1e-6, 
             radius /= factor
             factor *= 2
     return poses, rho, cost0, cost, it
+
+
+def partial_system(pb, poses, rho, a, lam):
+    """One rank's contribution to the multi-GPU exchange (include/pba.h): nothing damped or fixed on the
+    pose side, the rank's own points eliminated with their damping.  Returns (S_r, g_r, g_direct_r,
+    diag(A_r), observed_r) with S_r = A_r − B_r (C_r + λ·clamp(C_r))⁻¹ B_rᵀ, g_r = g_p − B_r (C_r + λD_C)⁻¹ g_l."""
+    H, g, _ = linearize(pb, poses, rho, a, ())
+    P = 6 * pb.n_frames
+    A, B = H[:P, :P], H[:P, P:]
+    C = np.diag(H[P:, P:])
+    Cd = C + lam * np.clip(C, 1e-6, 1e32)
+    Ci = np.where(Cd > 0, 1.0 / np.where(Cd > 0, Cd, 1.0), 0.0)
+    S = A - (B * Ci) @ B.T
+    gS = g[:P] - B @ (Ci * g[P:])
+    obs = np.array([np.any(H[6 * i:6 * i + 6, :]) for i in range(pb.n_frames)], np.float64)
+    return S, gS, g[:P].copy(), np.diag(A).copy(), obs
+
+
+def finalize_system(S, gS, dA, obs, lam, fixed=()):
+    """The import side: + λ·clamp(diag(A)) and constant frames (requested or observed by no rank)."""
+    n = len(obs)
+    fx = np.zeros(6 * n, bool)
+    for i in range(n):
+        if i in set(int(f) for f in fixed) or obs[i] == 0:
+            fx[6 * i:6 * i + 6] = True
+    S = S + lam * np.diag(np.clip(dA, 1e-6, 1e32))
+    gS = gS.copy()
+    S[fx, :] = 0
+    S[:, fx] = 0
+    S[fx, fx] = 1.0
+    gS[fx] = 0
+    return S, gS
