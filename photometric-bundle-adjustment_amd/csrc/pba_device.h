@@ -113,40 +113,44 @@ __device__ __forceinline__ void project(const double* k, const Vec3d& p, double&
   v = k[1] * (p.y * iden) + k[3];
 }
 
-// 2×3 projection Jacobian (rows du/dp, dv/dp), fp32.
-template <int MODEL>
-__device__ __forceinline__ void project_jac(const float* k, const Vec3& p, Vec3& du, Vec3& dv) {
-  const float fx = k[0], fy = k[1];
+__device__ __forceinline__ float sqrt_s(float x) { return sqrtf(x); }
+__device__ __forceinline__ double sqrt_s(double x) { return sqrt(x); }
+
+// 2×3 projection Jacobian (rows du/dp, dv/dp); fp32 in the Jacobian chain, fp64 where a product with it
+// cancels (the geometric ∂r/∂ρ).
+template <int MODEL, class S>
+__device__ __forceinline__ void project_jac(const S* k, const V3<S>& p, V3<S>& du, V3<S>& dv) {
+  const S fx = k[0], fy = k[1], one = S(1), zero = S(0);
   if (MODEL == CAM_PINHOLE) {
-    const float iz = 1.0f / p.z;
-    const float mx = p.x * iz, my = p.y * iz;
-    du = {fx * iz, 0.0f, -fx * mx * iz};
-    dv = {0.0f, fy * iz, -fy * my * iz};
+    const S iz = one / p.z;
+    const S mx = p.x * iz, my = p.y * iz;
+    du = {fx * iz, zero, -fx * mx * iz};
+    dv = {zero, fy * iz, -fy * my * iz};
     return;
   }
-  float den;
-  Vec3 dden;
+  S den;
+  V3<S> dden;
   if (MODEL == CAM_DS) {
-    const float xi = k[4], al = k[5];
-    const float d1 = sqrtf(p.x * p.x + p.y * p.y + p.z * p.z);
-    const float kk = xi * d1 + p.z;
-    const float d2 = sqrtf(p.x * p.x + p.y * p.y + kk * kk);
-    den = al * d2 + (1.0f - al) * kk;
-    const float id1 = 1.0f / d1, id2 = 1.0f / d2;
-    const Vec3 dk = {xi * p.x * id1, xi * p.y * id1, xi * p.z * id1 + 1.0f};
-    const Vec3 dd2 = {(p.x + kk * dk.x) * id2, (p.y + kk * dk.y) * id2, kk * dk.z * id2};
-    dden = {al * dd2.x + (1.0f - al) * dk.x, al * dd2.y + (1.0f - al) * dk.y, al * dd2.z + (1.0f - al) * dk.z};
+    const S xi = k[4], al = k[5];
+    const S d1 = sqrt_s(p.x * p.x + p.y * p.y + p.z * p.z);
+    const S kk = xi * d1 + p.z;
+    const S d2 = sqrt_s(p.x * p.x + p.y * p.y + kk * kk);
+    den = al * d2 + (one - al) * kk;
+    const S id1 = one / d1, id2 = one / d2;
+    const V3<S> dk = {xi * p.x * id1, xi * p.y * id1, xi * p.z * id1 + one};
+    const V3<S> dd2 = {(p.x + kk * dk.x) * id2, (p.y + kk * dk.y) * id2, kk * dk.z * id2};
+    dden = {al * dd2.x + (one - al) * dk.x, al * dd2.y + (one - al) * dk.y, al * dd2.z + (one - al) * dk.z};
   } else {
-    const float al = k[4], be = k[5];
-    const float d = sqrtf(be * (p.x * p.x + p.y * p.y) + p.z * p.z);
-    den = al * d + (1.0f - al) * p.z;
-    const float id = 1.0f / d;
-    dden = {al * be * p.x * id, al * be * p.y * id, al * p.z * id + (1.0f - al)};
+    const S al = k[4], be = k[5];
+    const S d = sqrt_s(be * (p.x * p.x + p.y * p.y) + p.z * p.z);
+    den = al * d + (one - al) * p.z;
+    const S id = one / d;
+    dden = {al * be * p.x * id, al * be * p.y * id, al * p.z * id + (one - al)};
   }
-  const float iden = 1.0f / den;
-  const float mx = p.x * iden, my = p.y * iden;
-  du = {fx * iden * (1.0f - mx * dden.x), -fx * iden * mx * dden.y, -fx * iden * mx * dden.z};
-  dv = {-fy * iden * my * dden.x, fy * iden * (1.0f - my * dden.y), -fy * iden * my * dden.z};
+  const S iden = one / den;
+  const S mx = p.x * iden, my = p.y * iden;
+  du = {fx * iden * (one - mx * dden.x), -fx * iden * mx * dden.y, -fx * iden * mx * dden.z};
+  dv = {-fy * iden * my * dden.x, fy * iden * (one - my * dden.y), -fy * iden * my * dden.z};
 }
 
 // Keyframe images live in HBM as 16×8-texel tiles of 128 B (one L2 line): tile (x>>4, y>>3) at

@@ -188,7 +188,7 @@ __global__ __launch_bounds__(kBlockThreads) void geometric_block_kernel(const Ke
   bool ok = isfinite(r0) && isfinite(r1);
   if (JAC) {
     const Vec3 pf = to_f(p), phf = to_f(ph);
-    const Vec3 Rbf = to_f(mat_mul(pp.R, b));
+    const Vec3 tf = {(float)pp.t[0], (float)pp.t[1], (float)pp.t[2]};
     const float irf = (float)irho;
     Vec3 du, dv;
     project_jac<MODEL>(a.intr + 8 * pp.target_cam, pf, du, dv);
@@ -203,7 +203,7 @@ __global__ __launch_bounds__(kBlockThreads) void geometric_block_kernel(const Ke
       float* jt = J + 14 + 6 * i;
       jh[0] = gR.x; jh[1] = gR.y; jh[2] = gR.z; jh[3] = wh.x; jh[4] = wh.y; jh[5] = wh.z;
       jt[0] = -g.x; jt[1] = -g.y; jt[2] = -g.z; jt[3] = wt.x; jt[4] = wt.y; jt[5] = wt.z;
-      J[26 + i] = -dot(g, Rbf) * irf * irf;
+      J[26 + i] = dot(g, tf) * irf;  // = ∂π/∂p·R b/ρ² without the cancellation (∂π/∂p·p = 0), pba_internal.h
     }
 #pragma unroll
     for (int i = 2; i < 28; ++i) ok = ok && isfinite(J[i]);

@@ -288,11 +288,35 @@ struct AsmArgs {
   int n_frames;
 };
 
-__device__ __forceinline__ double contrib_value(const AsmArgs& a, int2 c, int r, int cc, bool& schur) {
-  const int off = c.x, fl = c.y;
-  const int e = (fl & C_TRANSPOSE) ? cc * 6 + r : r * 6 + cc;
-  schur = (fl & C_SCHUR) != 0;
-  return schur ? -a.part_schur[(long long)off + e] : (double)a.part_lin[(long long)off + e];
+// Fixed-order sums over a contribution list (total, and the part that is not a Schur term — the undamped
+// JᵀJ diagonal / direct gradient).  The list entries and their values are gathered 8 at a time so eight
+// independent loads are in flight per lane instead of one dependent index → value chain per term.
+constexpr int GATHER = 8;
+__device__ __forceinline__ void contrib_sums(const AsmArgs& a, const int2* __restrict__ list, int beg, int end, int e,
+                                             int et, double& sum, double& dsum) {
+  sum = dsum = 0.0;
+  for (int q0 = beg; q0 < end; q0 += GATHER) {
+    int2 c[GATHER];
+    double v[GATHER];
+#pragma unroll
+    for (int u = 0; u < GATHER; ++u) c[u] = list[min(q0 + u, end - 1)];
+#pragma unroll
+    for (int u = 0; u < GATHER; ++u) {
+      // both loads unconditional (the other one at a valid dummy offset): no divergent branch, no wait
+      const int off = c[u].x + ((c[u].y & C_TRANSPOSE) ? et : e);
+      const bool sc = (c[u].y & C_SCHUR) != 0;
+      const double vs = a.part_schur[sc ? off : 0];
+      const float vl = a.part_lin[sc ? 0 : off];
+      v[u] = sc ? -vs : (double)vl;
+    }
+#pragma unroll
+    for (int u = 0; u < GATHER; ++u) {
+      if (q0 + u < end) {
+        sum += v[u];
+        if (!(c[u].y & C_SCHUR)) dsum += v[u];
+      }
+    }
+  }
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -304,13 +328,8 @@ __global__ void assemble_kernel(const AsmArgs a, double lambda) {
   if (tid < nS) {
     const int s = tid / 36, e = tid % 36, r = e / 6, cc = e % 6;
     const int i = a.blk_i[s], j = a.blk_j[s];
-    double sum = 0.0, dsum = 0.0;
-    for (int q = a.sky_cptr[s]; q < a.sky_cptr[s + 1]; ++q) {
-      bool schur;
-      const double v = contrib_value(a, a.sky_contrib[q], r, cc, schur);
-      sum += v;
-      if (!schur) dsum += v;
-    }
+    double sum, dsum;
+    contrib_sums(a, a.sky_contrib, a.sky_cptr[s], a.sky_cptr[s + 1], r * 6 + cc, cc * 6 + r, sum, dsum);
     double val = sum;
     if (a.fixed[i] || a.fixed[j]) {
       val = (i == j && r == cc) ? 1.0 : 0.0;
@@ -326,16 +345,8 @@ __global__ void assemble_kernel(const AsmArgs a, double lambda) {
   const int t = tid - nS;
   if (t >= 6 * a.n_frames) return;
   const int i = t / 6, r = t % 6;
-  double sum = 0.0, dsum = 0.0;
-  for (int q = a.g_cptr[i]; q < a.g_cptr[i + 1]; ++q) {
-    const int2 c = a.g_contrib[q];
-    if (c.y & C_SCHUR) sum -= a.part_schur[(long long)c.x + r];
-    else {
-      const double v = a.part_lin[(long long)c.x + r];
-      sum += v;
-      dsum += v;
-    }
-  }
+  double sum, dsum;
+  contrib_sums(a, a.g_contrib, a.g_cptr[i], a.g_cptr[i + 1], r, r, sum, dsum);
   a.g[t] = a.fixed[i] ? 0.0 : sum;
   if (a.Sband) a.Sband[(long long)i * ((a.band + 1) * 36 + 6) + (a.band + 1) * 36 + r] = a.fixed[i] ? 0.0 : sum;
   a.g_dir[t] = a.fixed[i] ? 0.0 : dsum;
@@ -358,13 +369,8 @@ __global__ void export_kernel(const AsmArgs a, const uint8_t* __restrict__ obser
   if (tid < nS) {
     const int s = tid / 36, e = tid % 36, r = e / 6, cc = e % 6;
     const int i = a.blk_i[s], j = a.blk_j[s];
-    double sum = 0.0, dsum = 0.0;
-    for (int q = a.sky_cptr[s]; q < a.sky_cptr[s + 1]; ++q) {
-      bool schur;
-      const double v = contrib_value(a, a.sky_contrib[q], r, cc, schur);
-      sum += v;
-      if (!schur) dsum += v;
-    }
+    double sum, dsum;
+    contrib_sums(a, a.sky_contrib, a.sky_cptr[s], a.sky_cptr[s + 1], r * 6 + cc, cc * 6 + r, sum, dsum);
     X[(long long)i * RS + (j - i + K) * 36 + e] = sum;
     if (i == j && r == cc) X[(long long)i * RS + (K + 1) * 36 + 12 + r] = dsum;
     return;
@@ -372,16 +378,8 @@ __global__ void export_kernel(const AsmArgs a, const uint8_t* __restrict__ obser
   const int t = tid - nS;
   if (t >= 6 * a.n_frames) return;
   const int i = t / 6, r = t % 6;
-  double sum = 0.0, dsum = 0.0;
-  for (int q = a.g_cptr[i]; q < a.g_cptr[i + 1]; ++q) {
-    const int2 c = a.g_contrib[q];
-    if (c.y & C_SCHUR) sum -= a.part_schur[(long long)c.x + r];
-    else {
-      const double v = a.part_lin[(long long)c.x + r];
-      sum += v;
-      dsum += v;
-    }
-  }
+  double sum, dsum;
+  contrib_sums(a, a.g_contrib, a.g_cptr[i], a.g_cptr[i + 1], r, r, sum, dsum);
   double* tail = X + (long long)i * RS + (K + 1) * 36;
   tail[r] = sum;
   tail[6 + r] = dsum;
@@ -888,110 +886,134 @@ __global__ __launch_bounds__(256) void cr_build_kernel(const double* __restrict_
   }
 }
 
-// Eliminate super-row j (odd rows of the level, or the single root row when `root`): X = D⁻¹ [U_{j−1}ᵀ | U_j | b].
+// Eliminate super-row j (odd rows of the level, or the single root row when `root`): X = D⁻¹ [U_{j−1}ᵀ | U_j | b]
+// by Gauss-Jordan on the augmented M × (3M+1) matrix [D | RHS] (no pivoting: D is SPD, its pivots are
+// positive).  Lane c owns column c in registers (steps fully unrolled, so every register index is static).
+// Step k: the pivot column's owner publishes its M values to LDS (double-buffered: one barrier per step),
+// every lane reads them as broadcasts and updates its own column.  Measured on MI355X
+// (tools/micro/cr_odd_timing.hip, M = 24): 12 µs per launch against 29 µs for an element-owner
+// formulation whose per-step publish/read traffic was LDS-bound.  A non-positive pivot flags the status.
 template <int M>
 __global__ __launch_bounds__(256) void cr_odd_kernel(CrLevel L, int root, int* status) {
-  constexpr int NC = 2 * M + 1;
-  __shared__ double A[M][M + 1];
-  __shared__ double Y[M][NC + 1];
-  __shared__ double inv[M];
-  __shared__ int fail;
+  constexpr int NC = 2 * M + 1, W = M + NC;
+  static_assert(W <= 256, "one lane per column");
+  __shared__ __attribute__((aligned(16))) double colk[2][M];
   const int tid = threadIdx.x;
   const int j = root ? 0 : 2 * blockIdx.x + 1;
+  const int c = min(tid, W - 1);
   const double* D = L.D + (long long)j * M * M;
-  for (int e = tid; e < M * M; e += 256) A[e / M][e % M] = D[e];
-  for (int e = tid; e < M * NC; e += 256) {
-    const int r = e / NC, c = e % NC;
-    double v;
-    if (c < M) v = root ? 0.0 : L.U[(long long)(j - 1) * M * M + c * M + r];          // U_{j−1}ᵀ
-    else if (c < 2 * M) v = (!root && j + 1 < L.n) ? L.U[(long long)j * M * M + r * M + (c - M)] : 0.0;  // U_j
-    else v = L.b[(long long)j * M + r];
-    Y[r][c] = v;
+  double a[M];
+#pragma unroll
+  for (int r = 0; r < M; ++r) {  // all of a lane's loads in flight at once
+    const double* src;
+    if (c < M) src = D + r * M + c;
+    else if (c < 2 * M) src = root ? nullptr : L.U + (long long)(j - 1) * M * M + (c - M) * M + r;  // U_{j−1}ᵀ
+    else if (c < 3 * M) src = (!root && j + 1 < L.n) ? L.U + (long long)j * M * M + r * M + (c - 2 * M) : nullptr;  // U_j
+    else src = L.b + (long long)j * M + r;
+    a[r] = src ? *src : 0.0;
   }
-  if (tid == 0) fail = 0;
-  __syncthreads();
-  // dense Cholesky, right-looking, lower triangle in place
-  for (int k = 0; k < M; ++k) {
-    if (tid == 0) {
-      const double p = A[k][k];
-      if (!(p > 0.0)) fail = 1;
-      const double il = p > 0.0 ? rsqrt_nr(p) : 0.0;
-      A[k][k] = p * il;
-      inv[k] = il;
+  bool bad = false;
+  auto step = [&](int k) {
+    const int buf = k & 1;
+    if (tid == k) {
+#pragma unroll
+      for (int r = 0; r < M; ++r) colk[buf][r] = a[r];
     }
     __syncthreads();
-    for (int r = k + 1 + tid; r < M; r += 256) A[r][k] *= inv[k];
-    __syncthreads();
-    const int nt = M - 1 - k;
-    for (int e = tid; e < nt * nt; e += 256) {
-      const int r = k + 1 + e / nt, c = k + 1 + e % nt;
-      if (c <= r) A[r][c] -= A[r][k] * A[c][k];
-    }
-    __syncthreads();
+    const double p = colk[buf][k];
+    bad |= !(p > 0.0);
+    double ak = a[0];
+#pragma unroll
+    for (int r = 1; r < M; ++r) ak = r == k ? a[r] : ak;  // static register indices even when k is not
+    const double t = ak / p;  // this column's entry of the normalised pivot row
+#pragma unroll
+    for (int r = 0; r < M; ++r) a[r] = r == k ? t : a[r] - colk[buf][r] * t;
+  };
+  if constexpr (M <= 24) {
+#pragma unroll
+    for (int k = 0; k < M; ++k) step(k);
+  } else {
+#pragma unroll 1
+    for (int k = 0; k < M; ++k) step(k);
   }
-  if (fail) {
+  if (bad) {  // uniform: every lane saw the same pivots
     if (tid == 0) atomicOr(status, 1);
     return;
   }
-  // L Y = RHS, then Lᵀ X = Y (columns in parallel)
-  for (int k = 0; k < M; ++k) {
-    for (int c = tid; c < NC; c += 256) Y[k][c] *= inv[k];
-    __syncthreads();
-    for (int e = tid; e < (M - 1 - k) * NC; e += 256) {
-      const int r = k + 1 + e / NC, c = e % NC;
-      Y[r][c] -= A[r][k] * Y[k][c];
-    }
-    __syncthreads();
-  }
-  for (int k = M - 1; k >= 0; --k) {
-    for (int c = tid; c < NC; c += 256) Y[k][c] *= inv[k];
-    __syncthreads();
-    for (int e = tid; e < k * NC; e += 256) {
-      const int r = e / NC, c = e % NC;
-      Y[r][c] -= A[k][r] * Y[k][c];
-    }
-    __syncthreads();
-  }
   if (root) {
-    for (int r = tid; r < M; r += 256) L.x[r] = Y[r][2 * M];
+    if (tid == W - 1)
+#pragma unroll
+      for (int r = 0; r < M; ++r) L.x[r] = a[r];
     return;
   }
-  double* X = L.X + (long long)(j / 2) * M * NC;
-  for (int e = tid; e < M * NC; e += 256) X[e] = Y[e / NC][e % NC];
+  if (tid >= M && tid < W) {
+    double* X = L.X + (long long)(j / 2) * M * NC + (c - M);
+#pragma unroll
+    for (int r = 0; r < M; ++r) X[r * NC] = a[r];
+  }
 }
 
-// Rebuild even super-row i of level L as row i/2 of level L+1.
+// Rebuild even super-row i of level L as row i/2 of level L+1; both neighbours' X and the couplings are
+// staged in LDS first (the products are M-long dot products over them).
 template <int M>
 __global__ __launch_bounds__(256) void cr_even_kernel(CrLevel L, CrLevel Ln) {
   constexpr int NC = 2 * M + 1;
+  extern __shared__ double smem[];
+  double* sUl = smem;               // U_{i−1}   M×M
+  double* sUi = sUl + M * M;        // U_i       M×M
+  double* sXl = sUi + M * M;        // X_{i−1}   M×NC
+  double* sXr = sXl + M * NC;       // X_{i+1}   M×NC
   const int i = 2 * blockIdx.x, in = blockIdx.x;
   const bool left = i - 1 >= 0, right = i + 1 < L.n;
-  const double* Ul = left ? L.U + (long long)(i - 1) * M * M : nullptr;  // U_{i−1}
-  const double* Ui = L.U + (long long)i * M * M;                          // U_i
+  const double* Ul = left ? L.U + (long long)(i - 1) * M * M : nullptr;
+  const double* Ui = L.U + (long long)i * M * M;
   const double* Xl = left ? L.X + (long long)((i - 1) / 2) * M * NC : nullptr;
   const double* Xr = right ? L.X + (long long)((i + 1) / 2) * M * NC : nullptr;
+  {
+    constexpr int NU = (M * M + 255) / 256, NX = (M * NC + 255) / 256;
+    double a0[NU], a1[NU], x0[NX], x1[NX];
+#pragma unroll
+    for (int u = 0; u < NU; ++u) {
+      const int e = min((int)threadIdx.x + 256 * u, M * M - 1);
+      a0[u] = left ? Ul[e] : 0.0;
+      a1[u] = Ui[e];
+    }
+#pragma unroll
+    for (int u = 0; u < NX; ++u) {
+      const int e = min((int)threadIdx.x + 256 * u, M * NC - 1);
+      x0[u] = left ? Xl[e] : 0.0;
+      x1[u] = right ? Xr[e] : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < NU; ++u) {
+      const int e = threadIdx.x + 256 * u;
+      if (e < M * M) { sUl[e] = a0[u]; sUi[e] = a1[u]; }
+    }
+#pragma unroll
+    for (int u = 0; u < NX; ++u) {
+      const int e = threadIdx.x + 256 * u;
+      if (e < M * NC) { sXl[e] = x0[u]; sXr[e] = x1[u]; }
+    }
+  }
+  __syncthreads();
   for (int e = threadIdx.x; e < 2 * M * M + M; e += 256) {
-    if (e < M * M) {  // D'
+    if (e < M * M) {  // D' = D − U_{i−1}ᵀ X^U_{i−1} − U_i X^L_{i+1}
       const int r = e / M, c = e % M;
       double v = L.D[(long long)i * M * M + e];
-      if (left)
-        for (int q = 0; q < M; ++q) v -= Ul[q * M + r] * Xl[q * NC + M + c];   // U_{i−1}ᵀ X^U_{i−1}
-      if (right)
-        for (int q = 0; q < M; ++q) v -= Ui[r * M + q] * Xr[q * NC + c];       // U_i X^L_{i+1}
+#pragma unroll 8
+      for (int q = 0; q < M; ++q) v -= sUl[q * M + r] * sXl[q * NC + M + c] + sUi[r * M + q] * sXr[q * NC + c];
       Ln.D[(long long)in * M * M + e] = v;
     } else if (e < 2 * M * M) {  // U' = −U_i X^U_{i+1}
       const int f = e - M * M, r = f / M, c = f % M;
       double v = 0.0;
-      if (right)
-        for (int q = 0; q < M; ++q) v -= Ui[r * M + q] * Xr[q * NC + M + c];
+#pragma unroll 8
+      for (int q = 0; q < M; ++q) v -= sUi[r * M + q] * sXr[q * NC + M + c];
       Ln.U[(long long)in * M * M + f] = v;
     } else {  // b'
       const int r = e - 2 * M * M;
       double v = L.b[(long long)i * M + r];
-      if (left)
-        for (int q = 0; q < M; ++q) v -= Ul[q * M + r] * Xl[q * NC + 2 * M];
-      if (right)
-        for (int q = 0; q < M; ++q) v -= Ui[r * M + q] * Xr[q * NC + 2 * M];
+#pragma unroll 8
+      for (int q = 0; q < M; ++q) v -= sUl[q * M + r] * sXl[q * NC + 2 * M] + sUi[r * M + q] * sXr[q * NC + 2 * M];
       Ln.b[(long long)in * M + r] = v;
     }
   }
@@ -1523,8 +1545,19 @@ CrLevel cr_level(GnData& G, int l) {
 }
 
 template <int M>
+constexpr size_t cr_even_lds() { return sizeof(double) * (2 * M * M + 2 * M * (2 * M + 1)); }
+
+template <int M>
 void cr_solve(pba_engine* e) {
   GnData& G = e->gn;
+  if (cr_even_lds<M>() > 65536) {  // above the default dynamic-LDS limit (gfx950 has 160 KiB per CU)
+    static bool raised = false;
+    if (!raised) {
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&cr_even_kernel<M>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)cr_even_lds<M>());
+      raised = true;
+    }
+  }
   const int nl = (int)G.cr_levels.size();
   CrLevel L0 = cr_level(G, 0);
   const long long nthreads = (long long)L0.n * M * M + (long long)L0.n * M;
@@ -1532,7 +1565,7 @@ void cr_solve(pba_engine* e) {
   for (int l = 0; l + 1 < nl; ++l) {
     CrLevel L = cr_level(G, l), Ln = cr_level(G, l + 1);
     cr_odd_kernel<M><<<L.n / 2, 256, 0, e->stream>>>(L, 0, G.status.p);
-    cr_even_kernel<M><<<(L.n + 1) / 2, 256, 0, e->stream>>>(L, Ln);
+    cr_even_kernel<M><<<(L.n + 1) / 2, 256, cr_even_lds<M>(), e->stream>>>(L, Ln);
   }
   cr_odd_kernel<M><<<1, 256, 0, e->stream>>>(cr_level(G, nl - 1), 1, G.status.p);
   for (int l = nl - 2; l >= 0; --l) {

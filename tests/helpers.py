@@ -56,7 +56,7 @@ def near_cell_boundary(uv: np.ndarray, eps: float = 2e-3) -> np.ndarray:
 
 
 def compare_records(kind: int, R: int, got: np.ndarray, ref: np.ndarray, valid_got, valid_ref, uv=None,
-                    r_atol: float | None = None, j_rtol: float = 1e-4):
+                    r_atol: float | None = None, j_rtol: float = 1e-5):
     """fp32 engine vs double oracle.  Returns a dict of error statistics and asserts the bounds.
 
     Residuals:  photometric |Δr| ≤ r_atol (intensity units, default 2.55e-3 = 1e-5 × 255);

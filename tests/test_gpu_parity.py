@@ -3,7 +3,7 @@
 Tolerances (fp32 device vs double oracle; rationale in tests/helpers.compare_records and DESIGN.md §Parity):
   photometric residual |Δr| ≤ 2.55e-3 intensity units (1e-5 × the 255 range)
   geometric residual   |Δr| ≤ 1e-3 px
-  Jacobians            per block and parameter block, max|ΔJ| ≤ 1e-4 × max|J_ref|
+  Jacobians            per block and parameter block, max|ΔJ| ≤ 1e-5 × max|J_ref| (BASELINE north star: 1e-5 relative)
                        (photometric pixels within 2e-3 px of a bilinear cell edge excluded)
   validity flags       identical
 """
