@@ -51,27 +51,52 @@ __device__ __forceinline__ V3<S> mat_mul(const T* R, const V3<S>& b) {
           (S)R[6] * b.x + (S)R[7] * b.y + (S)R[8] * b.z};
 }
 
+// Reciprocal / reciprocal square root to ~1 ulp in fp64: hardware v_rcp_f64 / v_rsq_f64 seed + two Newton
+// steps.  The IEEE division and sqrt() sequences the compiler emits otherwise (div_scale / div_fmas /
+// div_fixup, ldexp range scaling) were ~15% of the block kernel's VALU instructions.  Arguments here are
+// finite and far from the denormal range (focal lengths, depths inside the projection domain, |b|² ≈ 1).
+__device__ __forceinline__ double rcp_nr(double x) {
+  double y = __builtin_amdgcn_rcp(x);
+  double e = fma(-x, y, 1.0);
+  y = fma(y, e, y);
+  e = fma(-x, y, 1.0);
+  return fma(y, e, y);
+}
+__device__ __forceinline__ double rsqrt_nr(double x) {
+  double y = __builtin_amdgcn_rsq(x);
+  double e = fma(-x * y, y, 1.0);
+  y = fma(0.5 * y, e, y);
+  e = fma(-x * y, y, 1.0);
+  return fma(0.5 * y, e, y);
+}
+__device__ __forceinline__ float rcp_s(float x) { return __builtin_amdgcn_rcpf(x); }  // 1 ulp (fp32 chain)
+__device__ __forceinline__ double rcp_s(double x) { return rcp_nr(x); }
+
+// Camera record in device memory: kCamD doubles per camera — the 8 intrinsics [fx fy cx cy p1..p4]
+// (camera_models.h:50) followed by 1/fx, 1/fy (precomputed on the host), zero padded.
+constexpr int kCamD = 16;
+
 // Unit bearing of pixel (u, v) — camera_models.h unproject (pinhole :93-107, EUCM :162-190,
-// DS :247-277) followed by normalize() (reprojection.h:104).  fp64.
+// DS :247-277) followed by normalize() (reprojection.h:104).  fp64; k is a kCamD camera record.
 template <int MODEL>
 __device__ __forceinline__ Vec3d unproject(const double* k, double u, double v) {
-  const double mx = (u - k[2]) / k[0];
-  const double my = (v - k[3]) / k[1];
+  const double mx = (u - k[2]) * k[8];
+  const double my = (v - k[3]) * k[9];
   Vec3d b;
   if (MODEL == CAM_PINHOLE) {
     b = {mx, my, 1.0};
   } else if (MODEL == CAM_DS) {
     const double xi = k[4], al = k[5];
     const double r2 = mx * mx + my * my;
-    const double mz = (1.0 - al * al * r2) / (al * sqrt(1.0 - (2.0 * al - 1.0) * r2) + 1.0 - al);
-    const double fac = (mz * xi + sqrt(mz * mz + (1.0 - xi * xi) * r2)) / (mz * mz + r2);
+    const double mz = (1.0 - al * al * r2) * rcp_nr(al * sqrt(1.0 - (2.0 * al - 1.0) * r2) + 1.0 - al);
+    const double fac = (mz * xi + sqrt(mz * mz + (1.0 - xi * xi) * r2)) * rcp_nr(mz * mz + r2);
     b = {fac * mx, fac * my, fac * mz - xi};
   } else {
     const double al = k[4], be = k[5];
     const double r2 = mx * mx + my * my;
-    b = {mx, my, (1.0 - be * al * al * r2) / (al * sqrt(1.0 - (2.0 * al - 1.0) * be * r2) + (1.0 - al))};
+    b = {mx, my, (1.0 - be * al * al * r2) * rcp_nr(al * sqrt(1.0 - (2.0 * al - 1.0) * be * r2) + (1.0 - al))};
   }
-  const double inv = 1.0 / sqrt(b.x * b.x + b.y * b.y + b.z * b.z);
+  const double inv = rsqrt_nr(b.x * b.x + b.y * b.y + b.z * b.z);
   return {b.x * inv, b.y * inv, b.z * inv};
 }
 
@@ -92,9 +117,10 @@ __device__ __forceinline__ bool in_domain(const double* k, const Vec3d& p) {
   return p.z > -w2 * d1 + 1e-10;
 }
 
-// Projection (fp64) — camera_models.h project (pinhole :75-91, EUCM :140-160, DS :226-245).
+// Projection (fp64) — camera_models.h project (pinhole :75-91, EUCM :140-160, DS :226-245).  Returns
+// 1/den (pinhole: 1/z), which project_jac reuses.
 template <int MODEL>
-__device__ __forceinline__ void project(const double* k, const Vec3d& p, double& u, double& v) {
+__device__ __forceinline__ double project(const double* k, const Vec3d& p, double& u, double& v) {
   double den;
   if (MODEL == CAM_PINHOLE) {
     den = p.z;
@@ -108,46 +134,42 @@ __device__ __forceinline__ void project(const double* k, const Vec3d& p, double&
     const double al = k[4], be = k[5];
     den = al * sqrt(be * (p.x * p.x + p.y * p.y) + p.z * p.z) + (1.0 - al) * p.z;
   }
-  const double iden = 1.0 / den;
+  const double iden = rcp_nr(den);
   u = k[0] * (p.x * iden) + k[2];
   v = k[1] * (p.y * iden) + k[3];
+  return iden;
 }
 
 __device__ __forceinline__ float sqrt_s(float x) { return sqrtf(x); }
 __device__ __forceinline__ double sqrt_s(double x) { return sqrt(x); }
 
-// 2×3 projection Jacobian (rows du/dp, dv/dp); fp32 in the Jacobian chain, fp64 where a product with it
-// cancels (the geometric ∂r/∂ρ).
+// 2×3 projection Jacobian (rows du/dp, dv/dp) given iden = 1/den from project(); fp32 in the Jacobian chain,
+// fp64 where a product with it cancels (∂r/∂ρ).  k: the first 8 intrinsics, in S.
 template <int MODEL, class S>
-__device__ __forceinline__ void project_jac(const S* k, const V3<S>& p, V3<S>& du, V3<S>& dv) {
+__device__ __forceinline__ void project_jac(const S* k, const V3<S>& p, S iden, V3<S>& du, V3<S>& dv) {
   const S fx = k[0], fy = k[1], one = S(1), zero = S(0);
   if (MODEL == CAM_PINHOLE) {
-    const S iz = one / p.z;
-    const S mx = p.x * iz, my = p.y * iz;
-    du = {fx * iz, zero, -fx * mx * iz};
-    dv = {zero, fy * iz, -fy * my * iz};
+    const S mx = p.x * iden, my = p.y * iden;
+    du = {fx * iden, zero, -fx * mx * iden};
+    dv = {zero, fy * iden, -fy * my * iden};
     return;
   }
-  S den;
   V3<S> dden;
   if (MODEL == CAM_DS) {
     const S xi = k[4], al = k[5];
     const S d1 = sqrt_s(p.x * p.x + p.y * p.y + p.z * p.z);
     const S kk = xi * d1 + p.z;
     const S d2 = sqrt_s(p.x * p.x + p.y * p.y + kk * kk);
-    den = al * d2 + (one - al) * kk;
-    const S id1 = one / d1, id2 = one / d2;
+    const S id1 = rcp_s(d1), id2 = rcp_s(d2);
     const V3<S> dk = {xi * p.x * id1, xi * p.y * id1, xi * p.z * id1 + one};
     const V3<S> dd2 = {(p.x + kk * dk.x) * id2, (p.y + kk * dk.y) * id2, kk * dk.z * id2};
     dden = {al * dd2.x + (one - al) * dk.x, al * dd2.y + (one - al) * dk.y, al * dd2.z + (one - al) * dk.z};
   } else {
     const S al = k[4], be = k[5];
     const S d = sqrt_s(be * (p.x * p.x + p.y * p.y) + p.z * p.z);
-    den = al * d + (one - al) * p.z;
-    const S id = one / d;
+    const S id = rcp_s(d);
     dden = {al * be * p.x * id, al * be * p.y * id, al * p.z * id + (one - al)};
   }
-  const S iden = one / den;
   const S mx = p.x * iden, my = p.y * iden;
   du = {fx * iden * (one - mx * dden.x), -fx * iden * mx * dden.y, -fx * iden * mx * dden.z};
   dv = {-fy * iden * my * dden.x, fy * iden * (one - my * dden.y), -fy * iden * my * dden.z};
@@ -182,8 +204,11 @@ __device__ __forceinline__ void bilinear(const uint8_t* __restrict__ img, int W,
   const float top = I00 + a * (I10 - I00);
   const float bot = I01 + a * (I11 - I01);
   I = top + b * (bot - top);
-  gx = (I10 - I00) + b * ((I11 - I01) - (I10 - I00));
-  gy = bot - top;
+  // ∂I/∂u, ∂I/∂v from exact integer tap differences with fp64 cell fractions: a gradient component near
+  // zero is the difference of two O(255) terms, and an fp32 fraction leaves ~1.5e-5 absolute error there
+  // (3e-5 relative on J_ρ at P = 1).  Dead code for residual-only callers.
+  gx = (float)fma(v - yf, (double)((I11 - I01) - (I10 - I00)), (double)(I10 - I00));
+  gy = (float)fma(u - xf, (double)((I11 - I10) - (I01 - I00)), (double)(I01 - I00));
 }
 
 }  // namespace pba

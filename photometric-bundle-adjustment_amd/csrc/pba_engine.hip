@@ -39,11 +39,9 @@ namespace {
 // ------------------------------------------------------------------------------------------------
 // Pair kernel: relative poses in fp64 (q_th = q_wt*·q_wh, t_th = q_wt*·(t_wh − t_wt))
 // ------------------------------------------------------------------------------------------------
-__global__ void pair_kernel(const double* __restrict__ poses, const int* __restrict__ pair_host,
-                            const int* __restrict__ pair_target, const int* __restrict__ frame_cam,
-                            PairRec* __restrict__ pairs, int n_pairs) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n_pairs) return;
+__device__ __forceinline__ void make_pair(const double* __restrict__ poses, const int* __restrict__ pair_host,
+                                          const int* __restrict__ pair_target, const int* __restrict__ frame_cam,
+                                          PairRec* __restrict__ pairs, int i) {
   const int h = pair_host[i], t = pair_target[i];
   const double* H = poses + 7 * h;
   const double* T = poses + 7 * t;
@@ -75,6 +73,32 @@ __global__ void pair_kernel(const double* __restrict__ poses, const int* __restr
   r.host = h;
   r.pad1[0] = r.pad1[1] = r.pad1[2] = r.pad1[3] = 0;
   pairs[i] = r;
+}
+
+__global__ void pair_kernel(const double* __restrict__ poses, const int* __restrict__ pair_host,
+                            const int* __restrict__ pair_target, const int* __restrict__ frame_cam,
+                            PairRec* __restrict__ pairs, int n_pairs) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n_pairs) make_pair(poses, pair_host, pair_target, frame_cam, pairs, i);
+}
+
+// State upload fused with the pair kernel (one launch instead of two copies + pair_kernel): workgroups
+// [0, pair_wgs) form the relative poses straight from the caller's pose array, the rest copy the poses and
+// inverse distances into the engine's state buffers (16 B per lane, grid-stride).
+__global__ void state_kernel(const double* __restrict__ src_poses, const double* __restrict__ src_rho,
+                             double* __restrict__ poses, double* __restrict__ rho, int n_pose_d, int n_points,
+                             const int* __restrict__ pair_host, const int* __restrict__ pair_target,
+                             const int* __restrict__ frame_cam, PairRec* __restrict__ pairs, int n_pairs,
+                             int pair_wgs) {
+  if ((int)blockIdx.x < pair_wgs) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n_pairs) make_pair(src_poses, pair_host, pair_target, frame_cam, pairs, i);
+    return;
+  }
+  const long long stride = (long long)(gridDim.x - pair_wgs) * blockDim.x;
+  const long long i0 = (long long)(blockIdx.x - pair_wgs) * blockDim.x + threadIdx.x;
+  for (long long i = i0; i < n_pose_d; i += stride) poses[i] = src_poses[i];
+  for (long long i = i0; i < n_points; i += stride) rho[i] = src_rho[i];
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -167,19 +191,19 @@ __global__ __launch_bounds__(kBlockThreads) void geometric_block_kernel(const Ke
   if (blk >= a.n_blocks) return;
   const int pt = a.block_point[blk];
   const PairRec& pp = a.pairs[a.block_pair[blk]];
-  const double* khd = a.intr_d + 8 * pp.host_cam;
-  const double* ktd = a.intr_d + 8 * pp.target_cam;
+  const double* khd = a.intr_d + kCamD * pp.host_cam;
+  const double* ktd = a.intr_d + kCamD * pp.target_cam;
   const double2 ur = a.u_ref[pt];
   const double2 uo = a.u_obs[blk];
   const double rho = a.rho[pt];
-  const double irho = 1.0 / rho;
+  const double irho = rcp_nr(rho);
   // p = T_w_t⁻¹ · T_w_h · (b / ρ) in fp64
   const Vec3d b = unproject<MODEL>(khd, ur.x, ur.y);
   const Vec3d ph = {b.x * irho, b.y * irho, b.z * irho};
   const Vec3d Rp = mat_mul(pp.R, ph);
   const Vec3d p = {Rp.x + pp.t[0], Rp.y + pp.t[1], Rp.z + pp.t[2]};
   double u, v;
-  project<MODEL>(ktd, p, u, v);
+  const double iden = project<MODEL>(ktd, p, u, v);
   const float r0 = (float)(uo.x - u), r1 = (float)(uo.y - v);
   f32x4* rec = reinterpret_cast<f32x4*>(a.out + (long long)blk * 28);
   float J[28];
@@ -191,7 +215,7 @@ __global__ __launch_bounds__(kBlockThreads) void geometric_block_kernel(const Ke
     const Vec3 tf = {(float)pp.t[0], (float)pp.t[1], (float)pp.t[2]};
     const float irf = (float)irho;
     Vec3 du, dv;
-    project_jac<MODEL>(a.intr + 8 * pp.target_cam, pf, du, dv);
+    project_jac<MODEL>(a.intr + 8 * pp.target_cam, pf, (float)iden, du, dv);
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const Vec3 d = i == 0 ? du : dv;
@@ -372,10 +396,17 @@ int pba_set_cameras(pba_engine* e, int32_t n_cams, const double* intrinsics) {
   for (size_t i = 0; i < f.size(); ++i) f[i] = (float)intrinsics[i];
   for (int c = 0; c < n_cams; ++c)
     if (!(f[8 * c] != 0.0f && f[8 * c + 1] != 0.0f)) return fail(PBA_ERR_INVALID_ARGUMENT, "zero focal length");
+  // fp64 camera records: the 8 intrinsics, then 1/fx, 1/fy (kCamD doubles each, pba_device.h)
+  std::vector<double> d((size_t)kCamD * n_cams, 0.0);
+  for (int c = 0; c < n_cams; ++c) {
+    for (int j = 0; j < 8; ++j) d[(size_t)kCamD * c + j] = intrinsics[8 * c + j];
+    d[(size_t)kCamD * c + 8] = 1.0 / intrinsics[8 * c];
+    d[(size_t)kCamD * c + 9] = 1.0 / intrinsics[8 * c + 1];
+  }
   PBA_HIP(e->intr.resize(f.size()));
-  PBA_HIP(e->intr_d.resize(f.size()));
+  PBA_HIP(e->intr_d.resize(d.size()));
   PBA_HIP(hipMemcpyAsync(e->intr.p, f.data(), f.size() * sizeof(float), hipMemcpyHostToDevice, e->stream));
-  PBA_HIP(hipMemcpyAsync(e->intr_d.p, intrinsics, f.size() * sizeof(double), hipMemcpyHostToDevice, e->stream));
+  PBA_HIP(hipMemcpyAsync(e->intr_d.p, d.data(), d.size() * sizeof(double), hipMemcpyHostToDevice, e->stream));
   PBA_HIP(hipStreamSynchronize(e->stream));
   e->n_cams = n_cams;
   return PBA_OK;
@@ -418,6 +449,7 @@ static int set_frames_impl(pba_engine* e, int32_t n_frames, const int32_t* frame
   }
   PBA_HIP(hipStreamSynchronize(e->stream));
   e->frame_cam_h.assign(frame_cam, frame_cam + n_frames);
+  e->pairs_fresh = false;
   e->n_frames = n_frames;
   e->width = width;
   e->height = height;
@@ -519,6 +551,7 @@ int pba_set_blocks(pba_engine* e, int32_t n_blocks, const int32_t* block_point, 
   e->n_blocks = n_blocks;
   e->n_pairs = np;
   e->evaluated = false;
+  e->pairs_fresh = false;
   e->block_point_h.assign(block_point, block_point + n_blocks);
   e->block_target_h.assign(block_target, block_target + n_blocks);
   e->pair_of_h = std::move(pair_of);
@@ -536,6 +569,7 @@ int pba_set_state(pba_engine* e, const double* poses, const double* inv_dist) {
   PBA_HIP(hipMemcpyAsync(e->poses.p, poses, 7 * (size_t)e->n_frames * sizeof(double), hipMemcpyHostToDevice, e->stream));
   PBA_HIP(hipMemcpyAsync(e->rho.p, inv_dist, (size_t)e->n_points * sizeof(double), hipMemcpyHostToDevice, e->stream));
   e->state_set = true;
+  e->pairs_fresh = false;
   return PBA_OK;
 }
 
@@ -544,9 +578,15 @@ int pba_set_state_device(pba_engine* e, const double* d_poses, const double* d_i
   if (e->n_points <= 0 || e->n_frames <= 0) return fail(PBA_ERR_NOT_READY, "problem not set");
   if (int rc = check_device(e)) return rc;
   PBA_HIP(e->poses.resize(7 * (size_t)e->n_frames));
-  PBA_HIP(hipMemcpyAsync(e->poses.p, d_poses, 7 * (size_t)e->n_frames * sizeof(double), hipMemcpyDeviceToDevice, e->stream));
-  PBA_HIP(hipMemcpyAsync(e->rho.p, d_inv_dist, (size_t)e->n_points * sizeof(double), hipMemcpyDeviceToDevice, e->stream));
+  const int n_pose_d = 7 * e->n_frames;
+  const int pair_wgs = e->n_blocks > 0 ? (e->n_pairs + 255) / 256 : 0;
+  const int copy_wgs = std::min(1024, (std::max(n_pose_d, e->n_points) + 255) / 256);
+  state_kernel<<<pair_wgs + copy_wgs, 256, 0, e->stream>>>(d_poses, d_inv_dist, e->poses.p, e->rho.p, n_pose_d,
+                                                           e->n_points, e->pair_host.p, e->pair_target.p,
+                                                           e->frame_cam.p, e->pairs.p, e->n_pairs, pair_wgs);
+  PBA_HIP(hipGetLastError());
   e->state_set = true;
+  e->pairs_fresh = pair_wgs > 0;
   return PBA_OK;
 }
 
@@ -557,14 +597,16 @@ int pba_evaluate(pba_engine* e, int32_t want_jacobians) {
   const bool photometric = e->opt.residual_kind == PBA_RESIDUAL_PHOTOMETRIC;
   if (photometric && (!e->have_images || e->P <= 0)) return fail(PBA_ERR_NOT_READY, "images/pattern missing");
   if (int rc = check_device(e)) return rc;
-  launch_pairs(e, e->poses.p, e->pairs.p);
+  if (!e->pairs_fresh) launch_pairs(e, e->poses.p, e->pairs.p);  // else formed by pba_set_state_device
+  e->pairs_fresh = true;
   const KernelArgs ka = make_kernel_args(e, e->pairs.p, e->rho.p);
   const bool jac = want_jacobians != 0;
   hipEvent_t ev_stop = nullptr;
   if (e->timing) {
     while (e->ev_pool.size() < e->ev_used + 2) {
       hipEvent_t ev;
-      PBA_HIP(hipEventCreate(&ev));
+      // timing-only events: no system-scope fence (no L2 writeback of the records inside the bracket)
+      PBA_HIP(hipEventCreateWithFlags(&ev, hipEventDisableSystemFence));
       e->ev_pool.push_back(ev);
     }
     PBA_HIP(hipEventRecord(e->ev_pool[e->ev_used], e->stream));

@@ -604,16 +604,8 @@ struct BandArgs {
   int N;
 };
 
-// 1/√x to full fp64 precision: hardware v_rsq_f64 seed + two Newton steps (the pivot is on the solver's
-// serial critical path; this is ~3x shorter than sqrt() + division).
-__device__ __forceinline__ double rsqrt_nr(double x) {
-  double y = __builtin_amdgcn_rsq(x);
-  double e = fma(-x * y, y, 1.0);
-  y = fma(0.5 * y, e, y);
-  e = fma(-x * y, y, 1.0);
-  return fma(0.5 * y, e, y);
-}
-
+// rsqrt_nr (pba_device.h): hardware v_rsq_f64 seed + two Newton steps — the pivot is on the solver's
+// serial critical path; this is ~3x shorter than sqrt() + division.
 __device__ inline bool chol6_rcp(double* A, double* invd) {  // in place, lower; returns reciprocal pivots
 #pragma unroll
   for (int j = 0; j < 6; ++j) {
@@ -1665,6 +1657,7 @@ int accept(pba_engine* e) {
   GnData& G = e->gn;
   PBA_HIP(hipMemcpyAsync(e->poses.p, G.poses_new.p, sizeof(double) * 7 * e->n_frames, hipMemcpyDeviceToDevice, e->stream));
   PBA_HIP(hipMemcpyAsync(e->rho.p, G.rho_new.p, sizeof(double) * e->n_points, hipMemcpyDeviceToDevice, e->stream));
+  e->pairs_fresh = false;
   return PBA_OK;
 }
 

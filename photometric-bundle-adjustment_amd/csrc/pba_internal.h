@@ -31,7 +31,7 @@ struct KernelArgs {
   int width, height, tiles_x;
   long long frame_stride;        // bytes per tiled frame
   const float* intr;             // 8 floats per camera (Jacobian chain)
-  const double* intr_d;          // 8 doubles per camera (warp / projection)
+  const double* intr_d;          // kCamD doubles per camera (warp / projection; pba_device.h)
   const int* block_point;
   const int* block_pair;
   const PairRec* pairs;
@@ -107,8 +107,8 @@ __device__ __forceinline__ Row photometric_row(const KernelArgs& a, int blk, int
   const int P = a.P;
   const int pt = a.block_point[blk];
   const PairRec& pp = a.pairs[a.block_pair[blk]];
-  const double* khd = a.intr_d + 8 * pp.host_cam;
-  const double* ktd = a.intr_d + 8 * pp.target_cam;
+  const double* khd = a.intr_d + kCamD * pp.host_cam;
+  const double* ktd = a.intr_d + kCamD * pp.target_cam;
   const double2 ur = a.u_ref[pt];
   const double rho = a.rho[pt];
   const float Ih = a.host_int[(long long)pt * P + k];
@@ -118,9 +118,10 @@ __device__ __forceinline__ Row photometric_row(const KernelArgs& a, int blk, int
   const Vec3d p = {Rb.x + rho * pp.t[0], Rb.y + rho * pp.t[1], Rb.z + rho * pp.t[2]};
   const bool dom = in_domain<MODEL>(ktd, p);
   float I = 0.0f, gx = 0.0f, gy = 0.0f;
+  double iden = 0.0;
   if (dom) {
     double u, v;
-    project<MODEL>(ktd, p, u, v);
+    iden = project<MODEL>(ktd, p, u, v);
     bilinear(a.images + pp.target * a.frame_stride, a.width, a.height, a.tiles_x, u, v, I, gx, gy);
   }
   o.r = I - Ih;  // photometric_error.h:179
@@ -129,7 +130,7 @@ __device__ __forceinline__ Row photometric_row(const KernelArgs& a, int blk, int
     // q = ∇I · ∂π/∂p̃ (1×3)
     const Vec3 pf = to_f(p), bf = to_f(b);
     Vec3 du, dv;
-    project_jac<MODEL>(a.intr + 8 * pp.target_cam, pf, du, dv);
+    project_jac<MODEL>(a.intr + 8 * pp.target_cam, pf, (float)iden, du, dv);
     const Vec3 q = {gx * du.x + gy * dv.x, gx * du.y + gy * dv.y, gx * du.z + gy * dv.z};
     const Vec3 qR = row_mul(q, pp.R);
     const float rf = (float)rho;
@@ -140,7 +141,7 @@ __device__ __forceinline__ Row photometric_row(const KernelArgs& a, int blk, int
     // ∂r/∂ρ = ∇I·∂π/∂p̃·t: ∂π/∂p̃·t cancels when t points along the ray (the epipolar motion is small),
     // so those two dot products run in fp64 (fp32 left ~3e-5 relative error on J_ρ at short baselines)
     Vec3d dud, dvd;
-    project_jac<MODEL>(ktd, p, dud, dvd);
+    project_jac<MODEL>(ktd, p, iden, dud, dvd);
     const Vec3d td = {pp.t[0], pp.t[1], pp.t[2]};
     o.jr = (float)((double)gx * dot(dud, td) + (double)gy * dot(dvd, td));
   }
@@ -155,19 +156,19 @@ __device__ __forceinline__ Row geometric_row(const KernelArgs& a, int blk, int k
   const PairRec& pp = a.pairs[a.block_pair[blk]];
   const double2 ur = a.u_ref[pt];
   const double2 uo = a.u_obs[blk];
-  const double irho = 1.0 / a.rho[pt];
-  const Vec3d b = unproject<MODEL>(a.intr_d + 8 * pp.host_cam, ur.x, ur.y);
+  const double irho = rcp_nr(a.rho[pt]);
+  const Vec3d b = unproject<MODEL>(a.intr_d + kCamD * pp.host_cam, ur.x, ur.y);
   const Vec3d ph = {b.x * irho, b.y * irho, b.z * irho};
   const Vec3d Rp = mat_mul(pp.R, ph);
   const Vec3d p = {Rp.x + pp.t[0], Rp.y + pp.t[1], Rp.z + pp.t[2]};
   double u, v;
-  project<MODEL>(a.intr_d + 8 * pp.target_cam, p, u, v);
+  const double iden = project<MODEL>(a.intr_d + kCamD * pp.target_cam, p, u, v);
   o.r = (float)(k == 0 ? uo.x - u : uo.y - v);
   o.ok = isfinite(o.r);
   if (JAC) {
     const Vec3 pf = to_f(p), phf = to_f(ph);
     Vec3 du, dv;
-    project_jac<MODEL>(a.intr + 8 * pp.target_cam, pf, du, dv);
+    project_jac<MODEL>(a.intr + 8 * pp.target_cam, pf, (float)iden, du, dv);
     const Vec3 d = k == 0 ? du : dv;
     const Vec3 g = {-d.x, -d.y, -d.z};  // ∂r/∂p = −∂π/∂p
     const Vec3 gR = row_mul(g, pp.R);
@@ -312,6 +313,7 @@ struct pba_engine {
   pba::detail::DevBuf<float> out, cost;
   pba::detail::DevBuf<uint8_t> valid;
   bool state_set = false;
+  bool pairs_fresh = false;          // pairs hold T_th of the current poses (pba_set_state_device forms them)
   bool evaluated = false;
   bool timing = false;
   std::vector<hipEvent_t> ev_pool;   // start/stop pairs, reused
