@@ -72,27 +72,30 @@ __device__ __forceinline__ double rsqrt_nr(double x) {
 __device__ __forceinline__ float rcp_s(float x) { return __builtin_amdgcn_rcpf(x); }  // 1 ulp (fp32 chain)
 __device__ __forceinline__ double rcp_s(double x) { return rcp_nr(x); }
 
-// Camera record in device memory: kCamD doubles per camera — the 8 intrinsics [fx fy cx cy p1..p4]
-// (camera_models.h:50) followed by 1/fx, 1/fy (precomputed on the host), zero padded.
-constexpr int kCamD = 16;
+// Camera record in device memory: kCamD doubles per camera, laid out for the two uses —
+//   [0..5]   projection   "tk": fx fy cx cy p1 p2      (camera_models.h:50, p1/p2 = ξ,α (DS) or α,β (EUCM))
+//   [6..11]  unprojection "hk": cx cy 1/fx 1/fy p1 p2   (reciprocals precomputed on the host)
+//   [12..15] p3 p4 0 0
+// The pair kernel copies the host camera's hk and the target camera's tk into every PairRec.
+constexpr int kCamD = 16, kCamHk = 6;
 
 // Unit bearing of pixel (u, v) — camera_models.h unproject (pinhole :93-107, EUCM :162-190,
-// DS :247-277) followed by normalize() (reprojection.h:104).  fp64; k is a kCamD camera record.
+// DS :247-277) followed by normalize() (reprojection.h:104).  fp64; hk = [cx cy 1/fx 1/fy p1 p2].
 template <int MODEL>
-__device__ __forceinline__ Vec3d unproject(const double* k, double u, double v) {
-  const double mx = (u - k[2]) * k[8];
-  const double my = (v - k[3]) * k[9];
+__device__ __forceinline__ Vec3d unproject(const double* hk, double u, double v) {
+  const double mx = (u - hk[0]) * hk[2];
+  const double my = (v - hk[1]) * hk[3];
   Vec3d b;
   if (MODEL == CAM_PINHOLE) {
     b = {mx, my, 1.0};
   } else if (MODEL == CAM_DS) {
-    const double xi = k[4], al = k[5];
+    const double xi = hk[4], al = hk[5];
     const double r2 = mx * mx + my * my;
     const double mz = (1.0 - al * al * r2) * rcp_nr(al * sqrt(1.0 - (2.0 * al - 1.0) * r2) + 1.0 - al);
     const double fac = (mz * xi + sqrt(mz * mz + (1.0 - xi * xi) * r2)) * rcp_nr(mz * mz + r2);
     b = {fac * mx, fac * my, fac * mz - xi};
   } else {
-    const double al = k[4], be = k[5];
+    const double al = hk[4], be = hk[5];
     const double r2 = mx * mx + my * my;
     b = {mx, my, (1.0 - be * al * al * r2) * rcp_nr(al * sqrt(1.0 - (2.0 * al - 1.0) * be * r2) + (1.0 - al))};
   }
@@ -100,7 +103,8 @@ __device__ __forceinline__ Vec3d unproject(const double* k, double u, double v) 
   return {b.x * inv, b.y * inv, b.z * inv};
 }
 
-// Projection domain on the (possibly scaled) point — identical rule to oracle/oracle.cpp in_domain().
+// Projection domain on the (possibly scaled) point — identical rule to oracle/oracle.cpp in_domain();
+// k = tk layout [fx fy cx cy p1 p2].
 template <int MODEL>
 __device__ __forceinline__ bool in_domain(const double* k, const Vec3d& p) {
   if (MODEL == CAM_PINHOLE) return p.z > 1e-6;
@@ -117,8 +121,8 @@ __device__ __forceinline__ bool in_domain(const double* k, const Vec3d& p) {
   return p.z > -w2 * d1 + 1e-10;
 }
 
-// Projection (fp64) — camera_models.h project (pinhole :75-91, EUCM :140-160, DS :226-245).  Returns
-// 1/den (pinhole: 1/z), which project_jac reuses.
+// Projection (fp64) — camera_models.h project (pinhole :75-91, EUCM :140-160, DS :226-245); k = tk layout
+// [fx fy cx cy p1 p2].  Returns 1/den (pinhole: 1/z), which project_jac reuses.
 template <int MODEL>
 __device__ __forceinline__ double project(const double* k, const Vec3d& p, double& u, double& v) {
   double den;

@@ -41,7 +41,7 @@ namespace {
 // ------------------------------------------------------------------------------------------------
 __device__ __forceinline__ void make_pair(const double* __restrict__ poses, const int* __restrict__ pair_host,
                                           const int* __restrict__ pair_target, const int* __restrict__ frame_cam,
-                                          PairRec* __restrict__ pairs, int i) {
+                                          const double* __restrict__ cams, PairRec* __restrict__ pairs, int i) {
   const int h = pair_host[i], t = pair_target[i];
   const double* H = poses + 7 * h;
   const double* T = poses + 7 * t;
@@ -71,15 +71,22 @@ __device__ __forceinline__ void make_pair(const double* __restrict__ poses, cons
   r.target_cam = frame_cam[t];
   r.target = t;
   r.host = h;
-  r.pad1[0] = r.pad1[1] = r.pad1[2] = r.pad1[3] = 0;
+  const double* hc = cams + kCamD * r.host_cam + kCamHk;
+  const double* tc = cams + kCamD * r.target_cam;
+  for (int j = 0; j < kCamHk; ++j) {
+    r.hk[j] = hc[j];
+    r.tk[j] = tc[j];
+  }
+  for (int j = 0; j < 9; ++j) r.Rf[j] = (float)r.R[j];
+  for (int j = 0; j < 3; ++j) r.tf[j] = (float)r.t[j];
   pairs[i] = r;
 }
 
 __global__ void pair_kernel(const double* __restrict__ poses, const int* __restrict__ pair_host,
                             const int* __restrict__ pair_target, const int* __restrict__ frame_cam,
-                            PairRec* __restrict__ pairs, int n_pairs) {
+                            const double* __restrict__ cams, PairRec* __restrict__ pairs, int n_pairs) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n_pairs) make_pair(poses, pair_host, pair_target, frame_cam, pairs, i);
+  if (i < n_pairs) make_pair(poses, pair_host, pair_target, frame_cam, cams, pairs, i);
 }
 
 // State upload fused with the pair kernel (one launch instead of two copies + pair_kernel): workgroups
@@ -88,11 +95,11 @@ __global__ void pair_kernel(const double* __restrict__ poses, const int* __restr
 __global__ void state_kernel(const double* __restrict__ src_poses, const double* __restrict__ src_rho,
                              double* __restrict__ poses, double* __restrict__ rho, int n_pose_d, int n_points,
                              const int* __restrict__ pair_host, const int* __restrict__ pair_target,
-                             const int* __restrict__ frame_cam, PairRec* __restrict__ pairs, int n_pairs,
-                             int pair_wgs) {
+                             const int* __restrict__ frame_cam, const double* __restrict__ cams,
+                             PairRec* __restrict__ pairs, int n_pairs, int pair_wgs) {
   if ((int)blockIdx.x < pair_wgs) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n_pairs) make_pair(src_poses, pair_host, pair_target, frame_cam, pairs, i);
+    if (i < n_pairs) make_pair(src_poses, pair_host, pair_target, frame_cam, cams, pairs, i);
     return;
   }
   const long long stride = (long long)(gridDim.x - pair_wgs) * blockDim.x;
@@ -125,15 +132,22 @@ __global__ void tile_images_kernel(const uint8_t* __restrict__ src, uint8_t* __r
 }
 
 // ------------------------------------------------------------------------------------------------
-// Photometric block kernel: lane = (block, pixel k); a workgroup = 256/LPB consecutive blocks whose
-// records are staged in LDS and leave as one contiguous, 16-B-per-lane, non-temporal store stream.
+// Photometric block kernel: lane = (block, pixel k); a workgroup = a tile of 256/LPB consecutive blocks.
+//   prologue   the tile's pair records + points are staged in LDS (stage_tile), the pattern too;
+//   rows       every lane evaluates its row from LDS (broadcast reads) + its four image taps;
+//   records    staged in LDS (aliasing the tile, after a barrier) and stored as one contiguous,
+//              16-B-per-lane, non-temporal stream.
 // MODE 0: residual part of the records only; 1: full records; 2: per-block cost/validity only.
 // ------------------------------------------------------------------------------------------------
 template <int MODEL, int LPB, int MODE>
 __global__ __launch_bounds__(kBlockThreads) void photometric_block_kernel(const KernelArgs a) {
   constexpr int BPW = kBlockThreads / LPB;  // blocks per workgroup
   constexpr bool JAC = MODE == 1;
-  __shared__ __attribute__((aligned(16))) float stage[JAC ? BPW * 14 * LPB : 4];
+  constexpr int kStageBytes = JAC ? BPW * 14 * LPB * 4 : 0;
+  constexpr int kTileBytes = BPW * (int)sizeof(TileBlock);
+  __shared__ __attribute__((aligned(16))) unsigned char lds[kStageBytes > kTileBytes ? kStageBytes : kTileBytes];
+  __shared__ float2 s_pat[LPB];
+  TileBlock* s_tb = reinterpret_cast<TileBlock*>(lds);
   const int P = a.P;
   const int rec_f = 14 * P;
   const int blk0 = logical_tile() * BPW;
@@ -143,30 +157,41 @@ __global__ __launch_bounds__(kBlockThreads) void photometric_block_kernel(const 
   const bool live = blk < a.n_blocks;  // a block's LPB lanes agree
   const bool act = live && k < P;
 
+  if ((int)threadIdx.x < P) s_pat[threadIdx.x] = make_float2(a.pattern[2 * threadIdx.x], a.pattern[2 * threadIdx.x + 1]);
+  const int pt = stage_tile<LPB>(a, s_tb, lb, k, blk, live);
+  const float Ih = act ? a.host_int[(long long)pt * P + k] : 0.0f;
+  __syncthreads();
   Row row;
-  if (act) row = photometric_row<MODEL, JAC>(a, blk, k);
-  // per-block validity and ‖r‖² (wave shuffles over the block's lanes)
-  const int ok = group_and<LPB>(act ? row.ok : 1);
+  if (act) row = photometric_row<MODEL, JAC>(a, s_tb[lb], s_pat[k], Ih);
+  // per-block validity (ballot over the wave: the block's LPB lanes are an aligned bit field) and ‖r‖²
+  const int ok = group_all<LPB>(act ? row.ok : 1);
   const float s = group_sum<LPB>(act ? row.r * row.r : 0.0f);
   if (live && k == 0) {
     a.valid[blk] = (uint8_t)ok;
     a.cost[blk] = ok ? huber_cost(s, a.huber) : 0.0f;
   }
   if (MODE == 2) return;
-  if (!ok) row = Row();
   if (!JAC) {
-    if (act) a.out[(long long)blk * rec_f + k] = row.r;
+    if (act) a.out[(long long)blk * rec_f + k] = ok ? row.r : 0.0f;
     return;
   }
-  // stage the record row of pixel k: r | J_host row | J_target row | J_rho
+  __syncthreads();  // every lane has read its tile block: the record stage may overwrite it
+  float* stage = reinterpret_cast<float*>(lds);
+  // stage the record row of pixel k: r | J_host row | J_target row | J_rho  (zeros for invalid blocks)
   if (act) {
     float* s_rec = stage + lb * rec_f;
-    s_rec[k] = row.r;
     float* h = s_rec + P + 6 * k;
-    h[0] = row.hv.x; h[1] = row.hv.y; h[2] = row.hv.z; h[3] = row.hw.x; h[4] = row.hw.y; h[5] = row.hw.z;
     float* t = s_rec + 7 * P + 6 * k;
-    t[0] = row.tv.x; t[1] = row.tv.y; t[2] = row.tv.z; t[3] = row.tw.x; t[4] = row.tw.y; t[5] = row.tw.z;
-    s_rec[13 * P + k] = row.jr;
+    if (ok) {
+      s_rec[k] = row.r;
+      h[0] = row.hv.x; h[1] = row.hv.y; h[2] = row.hv.z; h[3] = row.hw.x; h[4] = row.hw.y; h[5] = row.hw.z;
+      t[0] = row.tv.x; t[1] = row.tv.y; t[2] = row.tv.z; t[3] = row.tw.x; t[4] = row.tw.y; t[5] = row.tw.z;
+      s_rec[13 * P + k] = row.jr;
+    } else {
+      s_rec[k] = 0.0f;
+      for (int j = 0; j < 6; ++j) h[j] = t[j] = 0.0f;
+      s_rec[13 * P + k] = 0.0f;
+    }
   }
   __syncthreads();
   const int nblk = min(BPW, a.n_blocks - blk0);
@@ -198,7 +223,7 @@ __global__ __launch_bounds__(kBlockThreads) void geometric_block_kernel(const Ke
   const double rho = a.rho[pt];
   const double irho = rcp_nr(rho);
   // p = T_w_t⁻¹ · T_w_h · (b / ρ) in fp64
-  const Vec3d b = unproject<MODEL>(khd, ur.x, ur.y);
+  const Vec3d b = unproject<MODEL>(khd + kCamHk, ur.x, ur.y);
   const Vec3d ph = {b.x * irho, b.y * irho, b.z * irho};
   const Vec3d Rp = mat_mul(pp.R, ph);
   const Vec3d p = {Rp.x + pp.t[0], Rp.y + pp.t[1], Rp.z + pp.t[2]};
@@ -292,6 +317,7 @@ KernelArgs make_kernel_args(pba_engine* e, const PairRec* pairs, const double* r
   ka.intr_d = e->intr_d.p;
   ka.block_point = e->block_point.p;
   ka.block_pair = e->block_pair.p;
+  ka.block_pp = e->block_pp.p;
   ka.pairs = pairs;
   ka.u_ref = e->u_ref.p;
   ka.host_int = e->host_int.p;
@@ -309,7 +335,7 @@ KernelArgs make_kernel_args(pba_engine* e, const PairRec* pairs, const double* r
 
 void launch_pairs(pba_engine* e, const double* poses, PairRec* pairs) {
   pair_kernel<<<(e->n_pairs + 255) / 256, 256, 0, e->stream>>>(poses, e->pair_host.p, e->pair_target.p,
-                                                               e->frame_cam.p, pairs, e->n_pairs);
+                                                               e->frame_cam.p, e->intr_d.p, pairs, e->n_pairs);
 }
 
 int launch_cost_only(pba_engine* e, const PairRec* pairs, const double* rho) {
@@ -368,7 +394,7 @@ int pba_destroy(pba_engine* e) {
   (void)hipSetDevice(e->opt.device);
   if (e->stream) (void)hipStreamSynchronize(e->stream);
   e->intr.release(); e->intr_d.release(); e->frame_cam.release(); e->images.release(); e->u_ref.release(); e->host_int.release();
-  e->block_point.release(); e->block_pair.release(); e->u_obs.release(); e->pair_host.release();
+  e->block_point.release(); e->block_pair.release(); e->block_pp.release(); e->u_obs.release(); e->pair_host.release();
   e->pair_target.release(); e->pairs.release(); e->poses.release(); e->rho.release(); e->out.release();
   e->cost.release(); e->valid.release();
   for (hipEvent_t ev : e->ev_pool) (void)hipEventDestroy(ev);
@@ -396,12 +422,14 @@ int pba_set_cameras(pba_engine* e, int32_t n_cams, const double* intrinsics) {
   for (size_t i = 0; i < f.size(); ++i) f[i] = (float)intrinsics[i];
   for (int c = 0; c < n_cams; ++c)
     if (!(f[8 * c] != 0.0f && f[8 * c + 1] != 0.0f)) return fail(PBA_ERR_INVALID_ARGUMENT, "zero focal length");
-  // fp64 camera records: the 8 intrinsics, then 1/fx, 1/fy (kCamD doubles each, pba_device.h)
+  // fp64 camera records (kCamD doubles each, pba_device.h): [fx fy cx cy p1 p2 | cx cy 1/fx 1/fy p1 p2 | p3 p4]
   std::vector<double> d((size_t)kCamD * n_cams, 0.0);
   for (int c = 0; c < n_cams; ++c) {
-    for (int j = 0; j < 8; ++j) d[(size_t)kCamD * c + j] = intrinsics[8 * c + j];
-    d[(size_t)kCamD * c + 8] = 1.0 / intrinsics[8 * c];
-    d[(size_t)kCamD * c + 9] = 1.0 / intrinsics[8 * c + 1];
+    const double* k = intrinsics + 8 * c;
+    double* r = d.data() + (size_t)kCamD * c;
+    for (int j = 0; j < 6; ++j) r[j] = k[j];
+    r[6] = k[2]; r[7] = k[3]; r[8] = 1.0 / k[0]; r[9] = 1.0 / k[1]; r[10] = k[4]; r[11] = k[5];
+    r[12] = k[6]; r[13] = k[7];
   }
   PBA_HIP(e->intr.resize(f.size()));
   PBA_HIP(e->intr_d.resize(d.size()));
@@ -538,6 +566,9 @@ int pba_set_blocks(pba_engine* e, int32_t n_blocks, const int32_t* block_point, 
   PBA_HIP(e->pairs.resize((size_t)np));
   PBA_HIP(hipMemcpyAsync(e->block_point.p, block_point, n_blocks * sizeof(int), hipMemcpyHostToDevice, e->stream));
   PBA_HIP(hipMemcpyAsync(e->block_pair.p, pair_of.data(), n_blocks * sizeof(int), hipMemcpyHostToDevice, e->stream));
+  std::vector<int2> pp(n_blocks);
+  for (int b = 0; b < n_blocks; ++b) pp[b] = make_int2(block_point[b], pair_of[b]);
+  PBA_HIP(e->block_pp.upload(pp, e->stream));
   PBA_HIP(hipMemcpyAsync(e->pair_host.p, ph.data(), np * sizeof(int), hipMemcpyHostToDevice, e->stream));
   PBA_HIP(hipMemcpyAsync(e->pair_target.p, pt.data(), np * sizeof(int), hipMemcpyHostToDevice, e->stream));
   if (geometric) {
@@ -583,7 +614,8 @@ int pba_set_state_device(pba_engine* e, const double* d_poses, const double* d_i
   const int copy_wgs = std::min(1024, (std::max(n_pose_d, e->n_points) + 255) / 256);
   state_kernel<<<pair_wgs + copy_wgs, 256, 0, e->stream>>>(d_poses, d_inv_dist, e->poses.p, e->rho.p, n_pose_d,
                                                            e->n_points, e->pair_host.p, e->pair_target.p,
-                                                           e->frame_cam.p, e->pairs.p, e->n_pairs, pair_wgs);
+                                                           e->frame_cam.p, e->intr_d.p, e->pairs.p, e->n_pairs,
+                                                           pair_wgs);
   PBA_HIP(hipGetLastError());
   e->state_set = true;
   e->pairs_fresh = pair_wgs > 0;

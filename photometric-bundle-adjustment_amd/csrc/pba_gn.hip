@@ -142,8 +142,18 @@ __global__ __launch_bounds__(kBlockThreads) void linearize_kernel(const KernelAr
     blk = g.gn_block[first + lb];
     if (k == 0) s_lt[lb] = g.blk_lt[first + lb];
   }
-  if (act) row = eval_row<KIND, MODEL, true>(a, blk, k);
-  const int ok = group_and<LPB>(act ? row.ok : 1);
+  if constexpr (KIND == PBA_RESIDUAL_PHOTOMETRIC) {
+    __shared__ TileBlock s_tb[BPW];
+    __shared__ float2 s_pat[LPB];
+    if ((int)threadIdx.x < R) s_pat[threadIdx.x] = make_float2(a.pattern[2 * threadIdx.x], a.pattern[2 * threadIdx.x + 1]);
+    const int pt = stage_tile<LPB>(a, s_tb, lb, k, blk, live);
+    const float Ih = act ? a.host_int[(long long)pt * R + k] : 0.0f;
+    __syncthreads();
+    if (act) row = photometric_row<MODEL, true>(a, s_tb[lb], s_pat[k], Ih);
+  } else {
+    if (act) row = geometric_row<MODEL, true>(a, blk, k);
+  }
+  const int ok = group_all<LPB>(act ? row.ok : 1);
   const float s = group_sum<LPB>(act && ok ? row.r * row.r : 0.0f);
   const float w = ok ? huber_weight(s, a.huber) : 0.0f;
   if (live && k == 0) {

@@ -17,14 +17,27 @@ namespace detail {
 constexpr int kBlockThreads = 256;
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-// Relative pose of one (host, target) keyframe pair, fp64, 128 B (L2-resident: 4k pairs = 512 KB at C4).
+// Relative pose of one (host, target) keyframe pair with the camera constants its residual rows need, 256 B
+// (L2-resident: 4k pairs = 1 MB at C4).  Formed by pair_kernel / state_kernel (pba_engine.hip).
 struct alignas(16) PairRec {
-  double R[9];
-  double t[3];
+  double R[9];                 // R_th, fp64 (warp)
+  double t[3];                 // t_th
   int host_cam, target_cam, target, host;
-  int pad1[4];
+  double hk[kCamHk];           // host camera, unprojection layout [cx cy 1/fx 1/fy p1 p2]
+  double tk[kCamHk];           // target camera, projection layout [fx fy cx cy p1 p2]
+  float Rf[9], tf[3];          // fp32 R_th, t_th (Jacobian chain)
 };
-static_assert(sizeof(PairRec) == 128, "PairRec layout");
+static_assert(sizeof(PairRec) == 256, "PairRec layout");
+
+// One block of a workgroup's tile, staged in LDS by stage_tile(): its pair record and its point.
+struct alignas(16) TileBlock {
+  PairRec pr;
+  double2 ur;                  // u_ref (host pixel)
+  double rho;                  // inverse distance (state)
+  int point, pad;
+};
+static_assert(sizeof(TileBlock) == 288, "TileBlock layout");
+constexpr int kTileParts = sizeof(TileBlock) / 16;  // 18 × 16 B
 
 struct KernelArgs {
   const uint8_t* images;
@@ -34,6 +47,7 @@ struct KernelArgs {
   const double* intr_d;          // kCamD doubles per camera (warp / projection; pba_device.h)
   const int* block_point;
   const int* block_pair;
+  const int2* block_pp;          // per block {point, pair}
   const PairRec* pairs;
   const double2* u_ref;          // per point
   const float* host_int;         // P per point
@@ -92,6 +106,16 @@ __device__ __forceinline__ int group_and(int v) {
   return v;
 }
 
+// AND over the LPB lanes of one block from a wave ballot (the block's lanes are an aligned bit field).
+// Every lane of the wave must be active.
+template <int LPB>
+__device__ __forceinline__ int group_all(int v) {
+  const unsigned long long m = __ballot(v != 0);
+  const unsigned long long grp = LPB >= 64 ? ~0ull : ((1ull << LPB) - 1ull);
+  const int sh = (int)(__lane_id() & (64 - LPB));
+  return ((m >> sh) & grp) == grp;
+}
+
 // One residual row with its tangent Jacobian: r, ∂r/∂[υ_h ω_h], ∂r/∂[υ_t ω_t], ∂r/∂ρ.
 struct Row {
   float r = 0.0f, jr = 0.0f;
@@ -99,40 +123,61 @@ struct Row {
   int ok = 1;
 };
 
-// Photometric row k of block blk (photometric_error.h:139-182 with the bilinear interpolator; the
-// Jacobian chain of pba_device.h).  Warp and projection in fp64, chain in fp32.
+// Cooperative tile prologue: the LPB lanes of block lb copy its pair record, u_ref and ρ into LDS as
+// 18 16-B parts (lane k takes parts k, k+LPB, …) — one broadcast copy per block instead of every lane
+// loading the 256-B record and the point data itself.  Returns the block's point.  The caller barriers.
+template <int LPB>
+__device__ __forceinline__ int stage_tile(const KernelArgs& a, TileBlock* s_tb, int lb, int k, int blk, bool live) {
+  if (!live) return 0;
+  const int2 pp = a.block_pp[blk];
+  const uint4* src = reinterpret_cast<const uint4*>(a.pairs + pp.y);
+  uint4* dst = reinterpret_cast<uint4*>(s_tb + lb);
+#pragma unroll
+  for (int part = k; part < kTileParts; part += LPB) {
+    uint4 v;
+    if (part < 16) {
+      v = src[part];
+    } else if (part == 16) {
+      v = reinterpret_cast<const uint4*>(a.u_ref)[pp.x];
+    } else {
+      const double r = a.rho[pp.x];
+      v = make_uint4(__double2loint(r), __double2hiint(r), (unsigned)pp.x, 0u);
+    }
+    dst[part] = v;
+  }
+  return pp.x;
+}
+
+// Photometric row k of a staged block (photometric_error.h:139-182 with the bilinear interpolator; the
+// Jacobian chain of pba_device.h).  Warp and projection in fp64, chain in fp32.  off = pattern offset k,
+// Ih = host intensity I_h,k.
 template <int MODEL, bool JAC>
-__device__ __forceinline__ Row photometric_row(const KernelArgs& a, int blk, int k) {
+__device__ __forceinline__ Row photometric_row(const KernelArgs& a, const TileBlock& tb, float2 off, float Ih) {
   Row o;
-  const int P = a.P;
-  const int pt = a.block_point[blk];
-  const PairRec& pp = a.pairs[a.block_pair[blk]];
-  const double* khd = a.intr_d + kCamD * pp.host_cam;
-  const double* ktd = a.intr_d + kCamD * pp.target_cam;
-  const double2 ur = a.u_ref[pt];
-  const double rho = a.rho[pt];
-  const float Ih = a.host_int[(long long)pt * P + k];
+  const PairRec& pp = tb.pr;
+  const double rho = tb.rho;
   // p̃ = R_th b_k + ρ t_th  (photometric_error.h:158-159)
-  const Vec3d b = unproject<MODEL>(khd, ur.x + (double)a.pattern[2 * k], ur.y + (double)a.pattern[2 * k + 1]);
+  const Vec3d b = unproject<MODEL>(pp.hk, tb.ur.x + (double)off.x, tb.ur.y + (double)off.y);
   const Vec3d Rb = mat_mul(pp.R, b);
   const Vec3d p = {Rb.x + rho * pp.t[0], Rb.y + rho * pp.t[1], Rb.z + rho * pp.t[2]};
-  const bool dom = in_domain<MODEL>(ktd, p);
+  const bool dom = in_domain<MODEL>(pp.tk, p);
   float I = 0.0f, gx = 0.0f, gy = 0.0f;
   double iden = 0.0;
   if (dom) {
     double u, v;
-    iden = project<MODEL>(ktd, p, u, v);
-    bilinear(a.images + pp.target * a.frame_stride, a.width, a.height, a.tiles_x, u, v, I, gx, gy);
+    iden = project<MODEL>(pp.tk, p, u, v);
+    bilinear(a.images + (long long)pp.target * a.frame_stride, a.width, a.height, a.tiles_x, u, v, I, gx, gy);
   }
   o.r = I - Ih;  // photometric_error.h:179
   o.ok = dom && isfinite(o.r);
   if (JAC && dom) {
     // q = ∇I · ∂π/∂p̃ (1×3)
     const Vec3 pf = to_f(p), bf = to_f(b);
+    const float kf[6] = {(float)pp.tk[0], (float)pp.tk[1], 0.0f, 0.0f, (float)pp.tk[4], (float)pp.tk[5]};
     Vec3 du, dv;
-    project_jac<MODEL>(a.intr + 8 * pp.target_cam, pf, (float)iden, du, dv);
+    project_jac<MODEL>(kf, pf, (float)iden, du, dv);
     const Vec3 q = {gx * du.x + gy * dv.x, gx * du.y + gy * dv.y, gx * du.z + gy * dv.z};
-    const Vec3 qR = row_mul(q, pp.R);
+    const Vec3 qR = row_mul(q, pp.Rf);
     const float rf = (float)rho;
     o.hv = {rf * qR.x, rf * qR.y, rf * qR.z};
     o.hw = cross(bf, qR);  // −(qR)×b
@@ -141,7 +186,7 @@ __device__ __forceinline__ Row photometric_row(const KernelArgs& a, int blk, int
     // ∂r/∂ρ = ∇I·∂π/∂p̃·t: ∂π/∂p̃·t cancels when t points along the ray (the epipolar motion is small),
     // so those two dot products run in fp64 (fp32 left ~3e-5 relative error on J_ρ at short baselines)
     Vec3d dud, dvd;
-    project_jac<MODEL>(ktd, p, iden, dud, dvd);
+    project_jac<MODEL>(pp.tk, p, iden, dud, dvd);
     const Vec3d td = {pp.t[0], pp.t[1], pp.t[2]};
     o.jr = (float)((double)gx * dot(dud, td) + (double)gy * dot(dvd, td));
   }
@@ -157,7 +202,7 @@ __device__ __forceinline__ Row geometric_row(const KernelArgs& a, int blk, int k
   const double2 ur = a.u_ref[pt];
   const double2 uo = a.u_obs[blk];
   const double irho = rcp_nr(a.rho[pt]);
-  const Vec3d b = unproject<MODEL>(a.intr_d + kCamD * pp.host_cam, ur.x, ur.y);
+  const Vec3d b = unproject<MODEL>(a.intr_d + kCamD * pp.host_cam + kCamHk, ur.x, ur.y);
   const Vec3d ph = {b.x * irho, b.y * irho, b.z * irho};
   const Vec3d Rp = mat_mul(pp.R, ph);
   const Vec3d p = {Rp.x + pp.t[0], Rp.y + pp.t[1], Rp.z + pp.t[2]};
@@ -184,12 +229,6 @@ __device__ __forceinline__ Row geometric_row(const KernelArgs& a, int blk, int k
            isfinite(o.tw.x + o.tw.y + o.tw.z + o.tv.x + o.tv.y + o.tv.z + o.jr);
   }
   return o;
-}
-
-template <int KIND, int MODEL, bool JAC>
-__device__ __forceinline__ Row eval_row(const KernelArgs& a, int blk, int k) {
-  if (KIND == PBA_RESIDUAL_PHOTOMETRIC) return photometric_row<MODEL, JAC>(a, blk, k);
-  return geometric_row<MODEL, JAC>(a, blk, k);
 }
 
 // ---------------------------------------------------------------------------------------------------------
@@ -306,6 +345,7 @@ struct pba_engine {
   pba::detail::DevBuf<double2> u_ref;
   pba::detail::DevBuf<float> host_int;
   pba::detail::DevBuf<int> block_point, block_pair;
+  pba::detail::DevBuf<int2> block_pp;
   pba::detail::DevBuf<double2> u_obs;
   pba::detail::DevBuf<int> pair_host, pair_target;
   pba::detail::DevBuf<pba::detail::PairRec> pairs;
