@@ -122,17 +122,52 @@ __device__ __forceinline__ void block_products(const float* x, float* srow, bool
   }
 }
 
+// Slot of the product x[r]·x[c] (r ≤ c) in the 104-product layout, or 255 when not needed (x13·x13, pad columns).
+__host__ __device__ constexpr int slot_of(int r, int c) {
+  for (int v = 0; v < NV; ++v)
+    if (pa(v) == r && pb(v) == c) return v;
+  return 255;
+}
+// MFMA 16×16 output held by lane l: C[4(l/16) + m][l%16], m = 0..3 → the four slots of lane l (upper triangle
+// only, so each product is written once), packed as bytes.
+__host__ __device__ constexpr unsigned slot_word(int lane) {
+  unsigned w = 0;
+  for (int m = 0; m < 4; ++m) {
+    const int r = 4 * (lane >> 4) + m, c = lane & 15;
+    w |= (unsigned)(r <= c ? slot_of(r, c) : 255) << (8 * m);
+  }
+  return w;
+}
+template <int... L>
+constexpr auto make_slot_table(std::integer_sequence<int, L...>) {
+  struct T { unsigned w[64]; };
+  return T{{slot_word(L)...}};
+}
+__constant__ const auto kSlotTable = make_slot_table(std::make_integer_sequence<int, 64>{});
+
+// Block normal-equation products by matrix cores: the block's weighted rows X (R × 14, padded to LPB × 16) give
+// XᵀX = Σ_k x_kᵀx_k as LPB/4 v_mfma_f32_16x16x4f32 steps (operand A = Xᵀ and B = X are the same register:
+// lane l holds X[4s + l/16][l%16]).  Replaces 104 products + a 3-step DPP all-reduce per row (~416 VALU per
+// lane) with 16 MFMAs per wave.
 template <int KIND, int MODEL, int LPB>
 __global__ __launch_bounds__(kBlockThreads) void linearize_kernel(const KernelArgs a, const LinArgs g) {
-  constexpr int BPW = kBlockThreads / LPB;
-  constexpr int NVP = 104;  // multiple of 4
-  __shared__ __attribute__((aligned(16))) float sblk[BPW][NVP + 4];
+  constexpr int BPW = kBlockThreads / LPB;  // blocks per workgroup
+  constexpr int BW = 64 / LPB;              // blocks per wave
+  constexpr int NVP = 108;                  // 104 products, padded
+  constexpr int kTileW = KIND == PBA_RESIDUAL_PHOTOMETRIC ? BW * (int)sizeof(TileBlock) : 0;
+  constexpr int kRowsW = 64 * 16 * 4, kProdW = BW * NVP * 4;
+  constexpr int kArena = (kTileW > kRowsW ? (kTileW > kProdW ? kTileW : kProdW) : (kRowsW > kProdW ? kRowsW : kProdW));
+  // per-wave arena, used in turn by the wave's tile blocks, its weighted rows and its blocks' products
+  // (each phase only touches the wave's own blocks; LDS is in order within a wave)
+  __shared__ __attribute__((aligned(16))) unsigned char arena[4][kArena];
   __shared__ int s_lt[BPW];
+  __shared__ float2 s_pat[LPB];
   const int chunk = logical_tile();
   if (chunk >= g.n_chunks) return;
   const int4 d = g.chunk_desc[chunk];
   const int first = d.x, count = d.y, n_t = d.z, poff = d.w;
-  const int lb = threadIdx.x / LPB, k = threadIdx.x % LPB;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int lb = threadIdx.x / LPB, k = threadIdx.x % LPB, wb = lb % BW;
   const bool live = lb < count;
   const int R = KIND == PBA_RESIDUAL_PHOTOMETRIC ? a.P : 2;
   const bool act = live && k < R;
@@ -143,13 +178,12 @@ __global__ __launch_bounds__(kBlockThreads) void linearize_kernel(const KernelAr
     if (k == 0) s_lt[lb] = g.blk_lt[first + lb];
   }
   if constexpr (KIND == PBA_RESIDUAL_PHOTOMETRIC) {
-    __shared__ TileBlock s_tb[BPW];
-    __shared__ float2 s_pat[LPB];
+    TileBlock* s_tb = reinterpret_cast<TileBlock*>(arena[wave]);
     if ((int)threadIdx.x < R) s_pat[threadIdx.x] = make_float2(a.pattern[2 * threadIdx.x], a.pattern[2 * threadIdx.x + 1]);
-    const int pt = stage_tile<LPB>(a, s_tb, lb, k, blk, live);
+    const int pt = stage_tile<LPB>(a, s_tb, wb, k, blk, live);
     const float Ih = act ? a.host_int[(long long)pt * R + k] : 0.0f;
     __syncthreads();
-    if (act) row = photometric_row<MODEL, true>(a, s_tb[lb], s_pat[k], Ih);
+    if (act) row = photometric_row<MODEL, true>(a, s_tb[wb], s_pat[k], Ih);
   } else {
     if (act) row = geometric_row<MODEL, true>(a, blk, k);
   }
@@ -162,19 +196,55 @@ __global__ __launch_bounds__(kBlockThreads) void linearize_kernel(const KernelAr
   }
   // weighted row x̃ = √w · x  → products carry w (Ceres Corrector with ρ'' ≤ 0: J̃ = √ρ' J, r̃ = √ρ' r)
   const float sw = (act && ok) ? sqrtf(w) : 0.0f;
-  const float x[14] = {sw * row.hv.x, sw * row.hv.y, sw * row.hv.z, sw * row.hw.x, sw * row.hw.y, sw * row.hw.z,
-                       sw * row.tv.x, sw * row.tv.y, sw * row.tv.z, sw * row.tw.x, sw * row.tw.y, sw * row.tw.z,
-                       sw * row.jr,   sw * row.r};
-  block_products<LPB, 0>(x, &sblk[lb < BPW ? lb : 0][0], live && k == 0);
+  float* sX = reinterpret_cast<float*>(arena[wave]);  // the wave's 64 rows × 16 floats (overwrites its tile blocks)
+  {
+    float4* xr = reinterpret_cast<float4*>(sX + lane * 16);
+    xr[0] = make_float4(sw * row.hv.x, sw * row.hv.y, sw * row.hv.z, sw * row.hw.x);
+    xr[1] = make_float4(sw * row.hw.y, sw * row.hw.z, sw * row.tv.x, sw * row.tv.y);
+    xr[2] = make_float4(sw * row.tv.z, sw * row.tw.x, sw * row.tw.y, sw * row.tw.z);
+    xr[3] = make_float4(sw * row.jr, sw * row.r, 0.0f, 0.0f);
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  {
+    const int ci = lane & 15, kq = lane >> 4;
+    float op[BW][LPB / 4];
+#pragma unroll
+    for (int b = 0; b < BW; ++b)
+#pragma unroll
+      for (int st = 0; st < LPB / 4; ++st) op[b][st] = sX[(b * LPB + 4 * st + kq) * 16 + ci];
+    f32x4 acc[BW];
+#pragma unroll
+    for (int b = 0; b < BW; ++b) {
+      acc[b] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+      for (int st = 0; st < LPB / 4; ++st) acc[b] = __builtin_amdgcn_mfma_f32_16x16x4f32(op[b][st], op[b][st], acc[b], 0, 0, 0);
+    }
+    // the products of the wave's blocks, 104 slots each (overwrites the rows: every operand read above precedes
+    // these stores in the wave's LDS order)
+    float* sP = reinterpret_cast<float*>(arena[wave]);
+    const unsigned slots = kSlotTable.w[lane];
+#pragma unroll
+    for (int b = 0; b < BW; ++b)
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+        const unsigned v = (slots >> (8 * m)) & 255u;
+        if (v < (unsigned)NV) sP[b * NVP + v] = acc[b][m];
+      }
+  }
   __syncthreads();
+  auto sblk = [&](int b, int v) -> float {  // product v of workgroup block b
+    return reinterpret_cast<const float*>(arena[b / BW])[(b % BW) * NVP + v];
+  };
   // per-block point-elimination data: [H_ρρ, g_ρ, W_h(6), W_t(6), 0, 0]
   for (int i = threadIdx.x; i < count * 16; i += kBlockThreads) {
     const int b = i >> 4, q = i & 15;
     float v = 0.0f;
-    if (q == 0) v = sblk[b][90];
-    else if (q == 1) v = sblk[b][91];
-    else if (q < 8) v = sblk[b][92 + q - 2];
-    else if (q < 14) v = sblk[b][98 + q - 8];
+    if (q == 0) v = sblk(b, 90);
+    else if (q == 1) v = sblk(b, 91);
+    else if (q < 8) v = sblk(b, 92 + q - 2);
+    else if (q < 14) v = sblk(b, 98 + q - 8);
     g.blk_schur[(long long)(first + b) * 16 + q] = v;
   }
   // chunk partial slots (fixed summation order over the chunk's blocks): per local target a block mask,
@@ -206,7 +276,7 @@ __global__ __launch_bounds__(kBlockThreads) void linearize_kernel(const KernelAr
     }
     float acc = 0.0f;
 #pragma unroll
-    for (int b = 0; b < BPW; ++b) acc += ((msk >> b) & 1ull) ? sblk[b][v] : 0.0f;
+    for (int b = 0; b < BPW; ++b) acc += ((msk >> b) & 1ull) ? sblk(b, v) : 0.0f;
     g.part_lin[(long long)poff + o] = acc;
   }
 }
@@ -889,17 +959,20 @@ __global__ __launch_bounds__(256) void cr_build_kernel(const double* __restrict_
 }
 
 // Eliminate super-row j (odd rows of the level, or the single root row when `root`): X = D⁻¹ [U_{j−1}ᵀ | U_j | b]
-// by Gauss-Jordan on the augmented M × (3M+1) matrix [D | RHS] (no pivoting: D is SPD, its pivots are
-// positive).  Lane c owns column c in registers (steps fully unrolled, so every register index is static).
-// Step k: the pivot column's owner publishes its M values to LDS (double-buffered: one barrier per step),
-// every lane reads them as broadcasts and updates its own column.  Measured on MI355X
-// (tools/micro/cr_odd_timing.hip, M = 24): 12 µs per launch against 29 µs for an element-owner
+// by 2×2-block Gauss-Jordan on the augmented M × (3M+1) matrix [D | RHS] (no pivoting: D is SPD, so are its
+// 2×2 pivot blocks).  Lane c owns column c in registers (steps fully unrolled, so every register index is
+// static).  Step k: the pivot columns' owners publish their 2M values to LDS (double-buffered: one barrier per
+// step), every lane reads them as broadcasts and updates its own column.  Measured on MI355X
+// (tools/micro/cr_odd_timing.hip, M = 24): 12 µs per launch for 1×1 pivots against 29 µs for an element-owner
 // formulation whose per-step publish/read traffic was LDS-bound.  A non-positive pivot flags the status.
 template <int M>
-__global__ __launch_bounds__(256) void cr_odd_kernel(CrLevel L, int root, int* status) {
+constexpr int kCrOddThreads = ((3 * M + 1) + 63) / 64 * 64;  // one lane per column of [D | RHS], whole waves
+
+template <int M>
+__global__ __launch_bounds__(kCrOddThreads<M>) void cr_odd_kernel(CrLevel L, int root, int* status) {
   constexpr int NC = 2 * M + 1, W = M + NC;
   static_assert(W <= 256, "one lane per column");
-  __shared__ __attribute__((aligned(16))) double colk[2][M];
+  __shared__ __attribute__((aligned(16))) double colk[2][2][M];
   const int tid = threadIdx.x;
   const int j = root ? 0 : 2 * blockIdx.x + 1;
   const int c = min(tid, W - 1);
@@ -915,28 +988,39 @@ __global__ __launch_bounds__(256) void cr_odd_kernel(CrLevel L, int root, int* s
     a[r] = src ? *src : 0.0;
   }
   bool bad = false;
+  // Step k eliminates the pivot pair (k, k+1): its two owner lanes publish their columns, every lane forms the
+  // 2×2 pivot block P (SPD: P00 > 0, det P > 0), its entries of the normalised pivot rows [t0 t1]ᵀ = P⁻¹[a_k a_k+1]ᵀ
+  // and the rank-2 update — M/2 barriers instead of M.
   auto step = [&](int k) {
-    const int buf = k & 1;
-    if (tid == k) {
+    const int buf = (k >> 1) & 1;
+    if (tid == k || tid == k + 1) {
+      double* dst = colk[buf][tid - k];
 #pragma unroll
-      for (int r = 0; r < M; ++r) colk[buf][r] = a[r];
+      for (int r = 0; r < M; ++r) dst[r] = a[r];
     }
     __syncthreads();
-    const double p = colk[buf][k];
-    bad |= !(p > 0.0);
-    double ak = a[0];
+    const double* c0 = colk[buf][0];
+    const double* c1 = colk[buf][1];
+    const double p00 = c0[k], p10 = c0[k + 1], p01 = c1[k], p11 = c1[k + 1];
+    const double det = p00 * p11 - p01 * p10;
+    bad |= !(p00 > 0.0 && det > 0.0);
+    const double rd = rcp_nr(det);  // same value in every lane
+    double ak = a[0], ak1 = a[1];
 #pragma unroll
     for (int r = 1; r < M; ++r) ak = r == k ? a[r] : ak;  // static register indices even when k is not
-    const double t = ak / p;  // this column's entry of the normalised pivot row
 #pragma unroll
-    for (int r = 0; r < M; ++r) a[r] = r == k ? t : a[r] - colk[buf][r] * t;
+    for (int r = 2; r < M; ++r) ak1 = r == k + 1 ? a[r] : ak1;
+    const double t0 = (p11 * ak - p01 * ak1) * rd;
+    const double t1 = (p00 * ak1 - p10 * ak) * rd;
+#pragma unroll
+    for (int r = 0; r < M; ++r) a[r] = r == k ? t0 : (r == k + 1 ? t1 : a[r] - c0[r] * t0 - c1[r] * t1);
   };
   if constexpr (M <= 24) {
 #pragma unroll
-    for (int k = 0; k < M; ++k) step(k);
+    for (int k = 0; k < M; k += 2) step(k);
   } else {
 #pragma unroll 1
-    for (int k = 0; k < M; ++k) step(k);
+    for (int k = 0; k < M; k += 2) step(k);
   }
   if (bad) {  // uniform: every lane saw the same pivots
     if (tid == 0) atomicOr(status, 1);
@@ -1021,28 +1105,57 @@ __global__ __launch_bounds__(256) void cr_even_kernel(CrLevel L, CrLevel Ln) {
   }
 }
 
-// x of level L from x of level L+1.
+// Back-substitution, level L from level L+1: x_j = X_j^b − X_j^L x_{j−1} − X_j^U x_{j+1} for the odd rows, x of the
+// even rows from the next level.  Level 0's x is the step δ itself (super-row I, element R ↔ block row
+// I·B + R/6, component R%6), so it is written straight into the step vector.  The small levels at the bottom
+// (n ≤ kCrTailRows) run in ONE workgroup with barriers between levels — one launch instead of one per level.
+constexpr int kMaxCrLevels = 26;
+constexpr int kCrTailRows = 32;
+struct CrLevels {
+  CrLevel lv[kMaxCrLevels];
+  int nl;
+};
+
 template <int M>
-__global__ void cr_back_kernel(CrLevel L, const double* __restrict__ xn) {
+__device__ __forceinline__ void cr_back_row(const CrLevel& L, const double* __restrict__ xn, double* out, int t) {
   constexpr int NC = 2 * M + 1;
-  const int t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= L.n * M) return;
   const int row = t / M, r = t % M;
+  double v;
   if ((row & 1) == 0) {
-    L.x[t] = xn[(row / 2) * M + r];
-    return;
+    v = xn[(row / 2) * M + r];
+  } else {
+    const double* X = L.X + (long long)(row / 2) * M * NC + r * NC;
+    v = X[2 * M];
+    const double* xl = xn + ((row - 1) / 2) * M;
+#pragma unroll 8
+    for (int c = 0; c < M; ++c) v -= X[c] * xl[c];
+    if (row + 1 < L.n) {
+      const double* xr = xn + ((row + 1) / 2) * M;
+#pragma unroll 8
+      for (int c = 0; c < M; ++c) v -= X[M + c] * xr[c];
+    }
   }
-  const double* X = L.X + (long long)(row / 2) * M * NC + r * NC;
-  double v = X[2 * M];
-  for (int c = 0; c < M; ++c) v -= X[c] * xn[((row - 1) / 2) * M + c];
-  if (row + 1 < L.n)
-    for (int c = 0; c < M; ++c) v -= X[M + c] * xn[((row + 1) / 2) * M + c];
-  L.x[t] = v;
+  out[t] = v;
 }
 
-__global__ void cr_scatter_kernel(const double* __restrict__ x0, double* __restrict__ step, int N) {
+// one (large) level, one lane per output
+template <int M>
+__global__ void cr_back_kernel(CrLevel L, const double* __restrict__ xn, double* __restrict__ out, int lim) {
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t < 6 * N) step[t] = x0[t];  // super-row I, element R ↔ block row I·B + R/6, component R%6
+  if (t < lim) cr_back_row<M>(L, xn, out, t);
+}
+
+// levels hi … lo (all small) in one workgroup
+template <int M>
+__global__ __launch_bounds__(1024) void cr_back_tail_kernel(const CrLevels C, int hi, int lo, double* __restrict__ step,
+                                                            int N) {
+  for (int l = hi; l >= lo; --l) {
+    const CrLevel& L = C.lv[l];
+    double* out = l == 0 ? step : L.x;
+    const int lim = l == 0 ? 6 * N : L.n * M;
+    for (int t = threadIdx.x; t < lim; t += blockDim.x) cr_back_row<M>(L, C.lv[l + 1].x, out, t);
+    __syncthreads();  // this level's x is read by the next (lower) level
+  }
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1566,15 +1679,24 @@ void cr_solve(pba_engine* e) {
   cr_build_kernel<M><<<(unsigned)((nthreads + 255) / 256), 256, 0, e->stream>>>(G.Sband.p, L0, e->n_frames, G.band_kernel);
   for (int l = 0; l + 1 < nl; ++l) {
     CrLevel L = cr_level(G, l), Ln = cr_level(G, l + 1);
-    cr_odd_kernel<M><<<L.n / 2, 256, 0, e->stream>>>(L, 0, G.status.p);
+    cr_odd_kernel<M><<<L.n / 2, kCrOddThreads<M>, 0, e->stream>>>(L, 0, G.status.p);
     cr_even_kernel<M><<<(L.n + 1) / 2, 256, cr_even_lds<M>(), e->stream>>>(L, Ln);
   }
-  cr_odd_kernel<M><<<1, 256, 0, e->stream>>>(cr_level(G, nl - 1), 1, G.status.p);
-  for (int l = nl - 2; l >= 0; --l) {
-    CrLevel L = cr_level(G, l), Ln = cr_level(G, l + 1);
-    cr_back_kernel<M><<<(L.n * M + 255) / 256, 256, 0, e->stream>>>(L, Ln.x);
+  cr_odd_kernel<M><<<1, kCrOddThreads<M>, 0, e->stream>>>(cr_level(G, nl - 1), 1, G.status.p);
+  if (nl == 1) {  // a single super-row: the root's x is the step
+    (void)hipMemcpyAsync(G.x.p, L0.x, sizeof(double) * 6 * e->n_frames, hipMemcpyDeviceToDevice, e->stream);
+    return;
   }
-  cr_scatter_kernel<<<(6 * e->n_frames + 255) / 256, 256, 0, e->stream>>>(L0.x, G.x.p, e->n_frames);
+  CrLevels C{};
+  C.nl = nl;
+  for (int l = 0; l < nl; ++l) C.lv[l] = cr_level(G, l);
+  int lo = nl - 2;  // the tail: levels with at most kCrTailRows super-rows
+  while (lo > 0 && C.lv[lo - 1].n <= kCrTailRows) --lo;
+  cr_back_tail_kernel<M><<<1, 1024, 0, e->stream>>>(C, nl - 2, lo, G.x.p, e->n_frames);
+  for (int l = lo - 1; l >= 0; --l) {
+    const int lim = l == 0 ? 6 * e->n_frames : C.lv[l].n * M;
+    cr_back_kernel<M><<<(lim + 255) / 256, 256, 0, e->stream>>>(C.lv[l], C.lv[l + 1].x, l == 0 ? G.x.p : C.lv[l].x, lim);
+  }
 }
 
 // After a solve into G.x: solver status, candidate poses/points, and the two parts of the LM model decrease

@@ -135,6 +135,24 @@ def test_reduced_solvers_agree(solver, n_frames, monkeypatch):
     assert np.linalg.norm(dl - dl_ref) <= 1e-3 * np.linalg.norm(dl_ref)
 
 
+@pytest.mark.parametrize("n_frames", [150, 300])
+def test_cyclic_reduction_large_levels(n_frames, monkeypatch):
+    """Problems whose top cyclic-reduction levels exceed the single-workgroup tail (> 32 super-rows) take the
+    per-level back-substitution launches; the step must equal the band Cholesky's."""
+    pb = synth.make_problem(n_frames=n_frames, n_points=20 * n_frames, width=376, height=240, seed=7 + n_frames,
+                            border=12)
+    steps = {}
+    for solver in ("cr", "band"):
+        monkeypatch.setenv("PBA_SOLVER", solver)
+        with make_engine(pb, 9.0, (0,)) as eng:
+            eng.gn_linearize()
+            _, st = eng.gn_step(1e-3)
+            assert st == 0
+            steps[solver] = eng.gn_last_step()
+    for a, b in zip(steps["cr"], steps["band"]):
+        assert np.linalg.norm(a - b) <= 1e-7 * np.linalg.norm(b)
+
+
 def test_loop_closure_structure_uses_skyline():
     pb = synth.make_problem(kind="geometric", n_frames=24, n_points=150, seed=52, obs_sigma=0.2)
     # add loop-closure observations: points of host 0 seen again by the last keyframe
