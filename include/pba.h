@@ -201,6 +201,65 @@ typedef int (*pba_allreduce_fn)(void* user, double* d_buf, int64_t count);
 int pba_solve_distributed(pba_engine* engine, const pba_solver_options* options, int32_t band, double* d_exchange,
                           pba_allreduce_fn allreduce, void* user, pba_solver_summary* summary);
 
+/* Reprojections and outlier flags after a bundle-adjustment pass -------------------
+ * pba_compute_projections replaces compute_projections() + set_outlier_flags() of src/sfm.cpp:1928-2008 for
+ * any list of observations (inlier and outlier obs; the anchor's own observation included, as the reference
+ * does): with the engine's current state, per observation i of point p in frame f
+ *   p_c = T_w_f⁻¹ · T_w_host(p) · (normalize(π_host⁻¹(u_ref(p))) / ρ_p)   (Landmark::get_p, common_types.h:205-217)
+ *   reprojected = π_f(p_c), error = ‖obs_uv − reprojected‖, and for inlier observations the flags below
+ *   (thresholds: sfm.cpp:254-261 defaults 3 px, 40 px, 0.1 m, 0.05 m when th == NULL).
+ * fp64 throughout.  All pointers are host pointers; obs_is_outlier, reprojected, point_c, error, flags may be NULL. */
+#define PBA_OUTLIER_NONE 0u
+#define PBA_OUTLIER_REPROJECTION_HUGE 1u     /* error > huge threshold       (common_types.h:279) */
+#define PBA_OUTLIER_REPROJECTION_NORMAL 2u   /* error > normal threshold     (common_types.h:281) */
+#define PBA_OUTLIER_CAMERA_DISTANCE 4u       /* ‖p_c‖ < distance threshold    (common_types.h:283) */
+#define PBA_OUTLIER_Z_COORDINATE 8u          /* p_c.z < z threshold           (common_types.h:285) */
+
+typedef struct pba_outlier_thresholds {
+  double reprojection_error_normal_px;  /* reprojection_error_outlier_threshold_normal_pixel (3.0)  */
+  double reprojection_error_huge_px;    /* reprojection_error_outlier_threshold_huge_pixel (40.0)   */
+  double camera_center_distance_m;      /* camera_center_distance_outlier_threshold_meter (0.1)     */
+  double z_coordinate_m;                /* z_coordinate_outlier_threshold_meter (0.05)              */
+} pba_outlier_thresholds;
+
+int pba_compute_projections(pba_engine* engine, int32_t n_obs, const int32_t* obs_point, const int32_t* obs_frame,
+                            const double* obs_uv, const uint8_t* obs_is_outlier, const pba_outlier_thresholds* th,
+                            double* reprojected, double* point_c, double* error, uint32_t* flags);
+/* remove_outlier_landmarks (sfm.cpp:2028-2114): remove[p] = 1 for points to drop.  Each point's inlier
+ * observations are visited in frame-index order (= FrameCamId order when frames are indexed that way, as
+ * pba_map_load does) and the first decisive flag wins; the normal-error flag removes a point only when no
+ * observation anywhere carries another flag.  counts (may be NULL): [huge, normal, camera distance, z,
+ * any_severe].  Host-only (no device needed). */
+int pba_outlier_landmarks(int32_t n_points, int32_t n_obs, const int32_t* obs_point, const int32_t* obs_frame,
+                          const uint32_t* flags, const uint8_t* obs_is_outlier, uint8_t* remove, int32_t* counts);
+
+/* Problem loader from the reference's files ----------------------------------------
+ * map.cereal (save_map_file, map_utils.h:58-86: cereal binary archive of corners, matches, tracks, outlier
+ * tracks, cameras, landmarks; serializers serialization.h:155-205) + opt_calib.json (cereal JSON of the
+ * Calibration, serialization.h:115-143; the DoubleSphere LoadCalibration form is accepted too), turned into
+ * the arrays of pba_set_cameras/frames/points/blocks exactly as bundle_adjustment builds its problem
+ * (map_utils.h:322-375): frames = map cameras in FrameCamId order (frame_cam = cam_id), points = landmarks in
+ * TrackId order anchored at their smallest observing FrameCamId (u_ref = that corner, ρ = inv_depth),
+ * blocks = the other observations (u_obs = their corners).  Host-only; the getters copy into caller arrays
+ * sized from pba_map_info (any pointer may be NULL). */
+typedef struct pba_map pba_map;
+typedef struct pba_map_info {
+  int32_t n_frames, n_points, n_blocks, n_cams;
+  int32_t camera_model;      /* PBA_CAMERA_* shared by all cameras */
+  int32_t n_outlier_obs;     /* Landmark::outlier_obs entries */
+  int32_t width, height;     /* from the calibration (0 when absent) */
+} pba_map_info;
+int pba_map_load(const char* map_path, const char* calib_path, pba_map** out_map);
+int pba_map_destroy(pba_map* map);
+int pba_map_get_info(const pba_map* map, pba_map_info* info);
+/* intrinsics 8·n_cams [fx fy cx cy p1 p2 p3 p4]; T_i_c 7·n_cams (Sophus storage) */
+int pba_map_get_cameras(const pba_map* map, double* intrinsics, double* T_i_c);
+/* FrameCamId.frame_id, cam_id (= camera index) and T_w_c per frame */
+int pba_map_get_frames(const pba_map* map, int64_t* frame_id, int32_t* frame_cam, double* poses);
+int pba_map_get_points(const pba_map* map, int64_t* track_id, int32_t* host_frame, double* u_ref, double* inv_dist);
+int pba_map_get_blocks(const pba_map* map, int32_t* block_point, int32_t* block_target, double* u_obs);
+int pba_map_get_outlier_obs(const pba_map* map, int32_t* point, int32_t* frame, double* uv);
+
 #ifdef __cplusplus
 }
 #endif

@@ -39,6 +39,7 @@
 #include <cstdint>
 #include <cstring>
 #include <thread>
+#include <map>
 #include <vector>
 #include <algorithm>
 #include <type_traits>
@@ -510,6 +511,77 @@ void orc_unproject(int model, const double* k8, const double* uv2, double* b3) {
 int orc_in_domain(int model, const double* k8, const double* p3) { return in_domain(model, k8, p3) ? 1 : 0; }
 void orc_bilinear(const uint8_t* img, int W, int H, double u, double v, double* f3) {
   bilinear(img, W, H, u, v, f3, f3 + 1, f3 + 2);
+}
+
+// compute_projections + set_outlier_flags (src/sfm.cpp:1928-2008), per observation.  th = [normal px, huge px,
+// camera distance m, z m].  Landmark::get_p (common_types.h:205-217) then T_w_c.inverse() * p_w with Sophus
+// (se3.hpp:208-211 inverse, so3.hpp:362-370 action).
+int orc_compute_projections(int model, const double* intr8, const int* frame_cam, const double* poses,
+                            const int* point_host, const double* u_ref, const double* rho, int n_obs,
+                            const int* obs_point, const int* obs_frame, const double* obs_uv,
+                            const uint8_t* obs_outlier, const double* th, double* reproj, double* pc, double* err,
+                            uint32_t* flags) {
+  for (int i = 0; i < n_obs; ++i) {
+    const int pt = obs_point[i], f = obs_frame[i], h = point_host[pt];
+    double b[3];
+    unproject(model, intr8 + 8 * frame_cam[h], u_ref + 2 * pt, b);
+    const double ph[3] = {b[0] / rho[pt], b[1] / rho[pt], b[2] / rho[pt]};
+    double pw[3];
+    orc_se3_act(poses + 7 * h, ph, pw);
+    double Ti[7], p[3];
+    orc_se3_inverse(poses + 7 * f, Ti);
+    orc_se3_act(Ti, pw, p);
+    double uv[2];
+    project<double>(model, intr8 + 8 * frame_cam[f], p, uv);
+    const double e = std::sqrt((obs_uv[2 * i] - uv[0]) * (obs_uv[2 * i] - uv[0]) +
+                               (obs_uv[2 * i + 1] - uv[1]) * (obs_uv[2 * i + 1] - uv[1]));
+    uint32_t fl = 0;
+    if (!(obs_outlier && obs_outlier[i])) {
+      if (e > th[1]) fl |= 1u;                                                    // OutlierReprojectionErrorHuge
+      if (e > th[0]) fl |= 2u;                                                    // OutlierReprojectionErrorNormal
+      if (std::sqrt(p[0] * p[0] + p[1] * p[1] + p[2] * p[2]) < th[2]) fl |= 4u;   // OutlierCameraDistance
+      if (p[2] < th[3]) fl |= 8u;                                                 // OutlierZCoordinate
+    }
+    reproj[2 * i] = uv[0];
+    reproj[2 * i + 1] = uv[1];
+    for (int j = 0; j < 3; ++j) pc[3 * i + j] = p[j];
+    err[i] = e;
+    flags[i] = fl;
+  }
+  return 0;
+}
+
+// remove_outlier_landmarks (src/sfm.cpp:2028-2114): track_projections as map<track, map<frame, flags>> (the
+// reference's std::map<FrameCamId, …> iteration order), then the same per-track loop.  counts = [huge,
+// normal, camera distance, z, any_severe].
+int orc_outlier_landmarks(int n_points, int n_obs, const int* obs_point, const int* obs_frame, const uint32_t* flags,
+                          const uint8_t* obs_outlier, uint8_t* remove, int* counts) {
+  std::map<int, std::map<int, uint32_t>> tracks;
+  for (int i = 0; i < n_obs; ++i)
+    if (!(obs_outlier && obs_outlier[i])) tracks[obs_point[i]][obs_frame[i]] = flags[i];
+  bool any_severe = false;
+  for (const auto& kv : tracks) {
+    for (const auto& o : kv.second)
+      if (o.second & ~2u) { any_severe = true; break; }
+    if (any_severe) break;
+  }
+  int huge = 0, normal = 0, dist = 0, z = 0;
+  for (int p = 0; p < n_points; ++p) remove[p] = 0;
+  for (const auto& kv : tracks) {
+    bool rm = false, normal_counted = false;
+    for (const auto& o : kv.second) {
+      if (o.second & 1u) { ++huge; rm = true; break; }
+      if (o.second & 2u) {
+        if (!normal_counted) { ++normal; normal_counted = true; }
+        if (!any_severe) { rm = true; break; }
+      }
+      if (o.second & 4u) { rm = true; ++dist; break; }
+      if (o.second & 8u) { rm = true; ++z; break; }
+    }
+    remove[kv.first] = rm;
+  }
+  counts[0] = huge; counts[1] = normal; counts[2] = dist; counts[3] = z; counts[4] = any_severe;
+  return 0;
 }
 
 }  // extern "C"

@@ -51,6 +51,11 @@ def lib():
         L.orc_in_domain.argtypes = [C.c_int, C.c_void_p, C.c_void_p]
         L.orc_in_domain.restype = C.c_int
         L.orc_bilinear.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_double, C.c_double, C.c_void_p]
+        L.orc_compute_projections.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                              C.c_void_p, C.c_int] + [C.c_void_p] * 9
+        L.orc_compute_projections.restype = C.c_int
+        L.orc_outlier_landmarks.argtypes = [C.c_int, C.c_int] + [C.c_void_p] * 6
+        L.orc_outlier_landmarks.restype = C.c_int
         _LIB = L
     return _LIB
 
@@ -164,3 +169,38 @@ def se3_act(T, p):
 
 def se3_inverse(T):
     return _call("orc_se3_inverse", 7, T)
+
+
+def compute_projections(pb, poses, rho, obs_point, obs_frame, obs_uv, obs_is_outlier=None,
+                        thresholds=(3.0, 40.0, 0.1, 0.05)) -> dict:
+    """compute_projections + set_outlier_flags (src/sfm.cpp:1928-2008) in double, per observation."""
+    k = np.ascontiguousarray(pb.intrinsics, np.float64)
+    fc = np.ascontiguousarray(pb.frame_cam, np.int32)
+    P = np.ascontiguousarray(poses, np.float64)
+    ph = np.ascontiguousarray(pb.point_host, np.int32)
+    ur = np.ascontiguousarray(pb.u_ref, np.float64)
+    rh = np.ascontiguousarray(rho, np.float64)
+    op = np.ascontiguousarray(obs_point, np.int32)
+    of = np.ascontiguousarray(obs_frame, np.int32)
+    uv = np.ascontiguousarray(obs_uv, np.float64)
+    oo = None if obs_is_outlier is None else np.ascontiguousarray(obs_is_outlier, np.uint8)
+    th = np.ascontiguousarray(thresholds, np.float64)
+    n = op.shape[0]
+    out = {"reprojected": np.zeros((n, 2)), "point_c": np.zeros((n, 3)), "error": np.zeros(n),
+           "flags": np.zeros(n, np.uint32)}
+    lib().orc_compute_projections(pb.model, _ptr(k), _ptr(fc), _ptr(P), _ptr(ph), _ptr(ur), _ptr(rh), n, _ptr(op),
+                                  _ptr(of), _ptr(uv), _ptr(oo), _ptr(th), _ptr(out["reprojected"]),
+                                  _ptr(out["point_c"]), _ptr(out["error"]), _ptr(out["flags"]))
+    return out
+
+
+def outlier_landmarks(n_points, obs_point, obs_frame, flags, obs_is_outlier=None):
+    """remove_outlier_landmarks (src/sfm.cpp:2028-2114) over map<track, map<frame, flags>>."""
+    op = np.ascontiguousarray(obs_point, np.int32)
+    of = np.ascontiguousarray(obs_frame, np.int32)
+    fl = np.ascontiguousarray(flags, np.uint32)
+    oo = None if obs_is_outlier is None else np.ascontiguousarray(obs_is_outlier, np.uint8)
+    rm = np.zeros(n_points, np.uint8)
+    counts = np.zeros(5, np.int32)
+    lib().orc_outlier_landmarks(n_points, op.shape[0], _ptr(op), _ptr(of), _ptr(fl), _ptr(oo), _ptr(rm), _ptr(counts))
+    return rm.astype(bool), dict(zip(("huge", "normal", "camera_distance", "z", "any_severe"), counts.tolist()))

@@ -393,7 +393,7 @@ int pba_destroy(pba_engine* e) {
   if (!e) return PBA_OK;
   (void)hipSetDevice(e->opt.device);
   if (e->stream) (void)hipStreamSynchronize(e->stream);
-  e->intr.release(); e->intr_d.release(); e->frame_cam.release(); e->images.release(); e->u_ref.release(); e->host_int.release();
+  e->intr.release(); e->intr_d.release(); e->frame_cam.release(); e->images.release(); e->u_ref.release(); e->host_int.release(); e->point_host_d.release();
   e->block_point.release(); e->block_pair.release(); e->block_pp.release(); e->u_obs.release(); e->pair_host.release();
   e->pair_target.release(); e->pairs.release(); e->poses.release(); e->rho.release(); e->out.release();
   e->cost.release(); e->valid.release();
@@ -513,6 +513,8 @@ int pba_set_points(pba_engine* e, int32_t n_points, const int32_t* host_frame, c
   if (int rc = check_device(e)) return rc;
   PBA_HIP(e->u_ref.resize(n_points));
   PBA_HIP(hipMemcpyAsync(e->u_ref.p, u_ref, n_points * sizeof(double2), hipMemcpyHostToDevice, e->stream));
+  PBA_HIP(e->point_host_d.resize(n_points));
+  PBA_HIP(hipMemcpyAsync(e->point_host_d.p, host_frame, n_points * sizeof(int), hipMemcpyHostToDevice, e->stream));
   if (photometric) {
     PBA_HIP(e->host_int.resize((size_t)n_points * e->P));
     PBA_HIP(hipMemcpyAsync(e->host_int.p, host_intensity, (size_t)n_points * e->P * sizeof(float),

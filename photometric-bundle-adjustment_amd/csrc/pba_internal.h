@@ -343,6 +343,7 @@ struct pba_engine {
   pba::detail::DevBuf<int> frame_cam;
   pba::detail::DevBuf<uint8_t> images;
   pba::detail::DevBuf<double2> u_ref;
+  pba::detail::DevBuf<int> point_host_d;   // host keyframe per point
   pba::detail::DevBuf<float> host_int;
   pba::detail::DevBuf<int> block_point, block_pair;
   pba::detail::DevBuf<int2> block_pp;

@@ -28,6 +28,20 @@ class Options(C.Structure):
                 ("huber_width", C.c_float)]
 
 
+class OutlierThresholds(C.Structure):
+    """pba_outlier_thresholds (defaults: src/sfm.cpp:254-261)."""
+    _fields_ = [("reprojection_error_normal_px", C.c_double), ("reprojection_error_huge_px", C.c_double),
+                ("camera_center_distance_m", C.c_double), ("z_coordinate_m", C.c_double)]
+
+
+OUTLIER_HUGE, OUTLIER_NORMAL, OUTLIER_DISTANCE, OUTLIER_Z = 1, 2, 4, 8
+
+
+class MapInfo(C.Structure):
+    _fields_ = [("n_frames", C.c_int32), ("n_points", C.c_int32), ("n_blocks", C.c_int32), ("n_cams", C.c_int32),
+                ("camera_model", C.c_int32), ("n_outlier_obs", C.c_int32), ("width", C.c_int32), ("height", C.c_int32)]
+
+
 class SolverOptions(C.Structure):
     _fields_ = [("max_iterations", C.c_int32), ("pad_", C.c_int32), ("initial_trust_region_radius", C.c_double),
                 ("function_tolerance", C.c_double), ("parameter_tolerance", C.c_double),
@@ -116,6 +130,16 @@ def lib():
                                 C.POINTER(i32)], C.c_int),
         "pba_solve_distributed": ([vp, C.POINTER(SolverOptions), i32, vp, ALLREDUCE_FN, vp,
                                    C.POINTER(SolverSummary)], C.c_int),
+        "pba_compute_projections": ([vp, i32, vp, vp, vp, vp, C.POINTER(OutlierThresholds), vp, vp, vp, vp], C.c_int),
+        "pba_outlier_landmarks": ([i32, i32, vp, vp, vp, vp, vp, vp], C.c_int),
+        "pba_map_load": ([C.c_char_p, C.c_char_p, C.POINTER(vp)], C.c_int),
+        "pba_map_destroy": ([vp], C.c_int),
+        "pba_map_get_info": ([vp, C.POINTER(MapInfo)], C.c_int),
+        "pba_map_get_cameras": ([vp, vp, vp], C.c_int),
+        "pba_map_get_frames": ([vp, vp, vp, vp], C.c_int),
+        "pba_map_get_points": ([vp, vp, vp, vp, vp], C.c_int),
+        "pba_map_get_blocks": ([vp, vp, vp, vp], C.c_int),
+        "pba_map_get_outlier_obs": ([vp, vp, vp, vp], C.c_int),
     }
     for name, (argt, rest) in sig.items():
         f = getattr(L, name)
@@ -197,6 +221,23 @@ class Engine:
 
     def synchronize(self):
         _check(self._L.pba_synchronize(self._h), "pba_synchronize")
+
+    # -- reprojections / outliers (src/sfm.cpp:1928-2008) --------------------------------------------
+    def compute_projections(self, obs_point, obs_frame, obs_uv, obs_is_outlier=None, thresholds=None) -> dict:
+        """Reprojection of every observation at the current state: dict(reprojected (n,2), point_c (n,3),
+        error (n,), flags (n,) uint32)."""
+        op = np.ascontiguousarray(obs_point, np.int32)
+        of = np.ascontiguousarray(obs_frame, np.int32)
+        uv = np.ascontiguousarray(obs_uv, np.float64).reshape(-1, 2)
+        n = op.shape[0]
+        oo = None if obs_is_outlier is None else np.ascontiguousarray(obs_is_outlier, np.uint8)
+        th = None if thresholds is None else C.byref(OutlierThresholds(*thresholds))
+        out = {"reprojected": np.zeros((n, 2)), "point_c": np.zeros((n, 3)), "error": np.zeros(n),
+               "flags": np.zeros(n, np.uint32)}
+        _check(self._L.pba_compute_projections(self._h, n, _p(op), _p(of), _p(uv), _p(oo), th, _p(out["reprojected"]),
+                                               _p(out["point_c"]), _p(out["error"]), _p(out["flags"])),
+               "pba_compute_projections")
+        return out
 
     def records(self):
         rec = np.empty((self.n_blocks, self.record), np.float32)
@@ -347,6 +388,51 @@ class Engine:
 
     def __exit__(self, *exc):
         self.close()
+
+
+def load_map(map_path: str, calib_path: str):
+    """map.cereal + opt_calib.json → (synth.Problem (geometric), extras dict) through pba_map_load (host-only C++)."""
+    import importlib
+    synth = importlib.import_module(__package__ + ".synth")
+    L = lib()
+    h = C.c_void_p()
+    _check(L.pba_map_load(map_path.encode(), calib_path.encode(), C.byref(h)), "pba_map_load")
+    try:
+        info = MapInfo()
+        _check(L.pba_map_get_info(h, C.byref(info)), "pba_map_get_info")
+        nf, npt, nb, nc, no = info.n_frames, info.n_points, info.n_blocks, info.n_cams, info.n_outlier_obs
+        intr, tic = np.zeros((nc, 8)), np.zeros((nc, 7))
+        fid, fcam, poses = np.zeros(nf, np.int64), np.zeros(nf, np.int32), np.zeros((nf, 7))
+        tid, host, uref, rho = np.zeros(npt, np.int64), np.zeros(npt, np.int32), np.zeros((npt, 2)), np.zeros(npt)
+        bp, bt, uobs = np.zeros(nb, np.int32), np.zeros(nb, np.int32), np.zeros((nb, 2))
+        op, of, ouv = np.zeros(no, np.int32), np.zeros(no, np.int32), np.zeros((no, 2))
+        _check(L.pba_map_get_cameras(h, _p(intr), _p(tic)), "pba_map_get_cameras")
+        _check(L.pba_map_get_frames(h, _p(fid), _p(fcam), _p(poses)), "pba_map_get_frames")
+        _check(L.pba_map_get_points(h, _p(tid), _p(host), _p(uref), _p(rho)), "pba_map_get_points")
+        _check(L.pba_map_get_blocks(h, _p(bp), _p(bt), _p(uobs)), "pba_map_get_blocks")
+        _check(L.pba_map_get_outlier_obs(h, _p(op), _p(of), _p(ouv)), "pba_map_get_outlier_obs")
+    finally:
+        L.pba_map_destroy(h)
+    pb = synth.Problem(kind=synth.GEOMETRIC, model=info.camera_model, width=info.width, height=info.height,
+                       intrinsics=intr, frame_cam=fcam, images=None, pattern=np.zeros((0, 2), np.float32),
+                       point_host=host, u_ref=uref, host_intensity=None, block_point=bp, block_target=bt, u_obs=uobs,
+                       poses=poses, rho=rho)
+    extras = {"T_i_c": tic, "frame_id": fid, "track_id": tid, "outlier_point": op, "outlier_frame": of,
+              "outlier_uv": ouv}
+    return pb, extras
+
+
+def outlier_landmarks(n_points: int, obs_point, obs_frame, flags, obs_is_outlier=None):
+    """remove_outlier_landmarks (src/sfm.cpp:2028-2114): (remove (n_points,) bool, counts dict)."""
+    op = np.ascontiguousarray(obs_point, np.int32)
+    of = np.ascontiguousarray(obs_frame, np.int32)
+    fl = np.ascontiguousarray(flags, np.uint32)
+    oo = None if obs_is_outlier is None else np.ascontiguousarray(obs_is_outlier, np.uint8)
+    rm = np.zeros(n_points, np.uint8)
+    counts = np.zeros(5, np.int32)
+    _check(lib().pba_outlier_landmarks(n_points, op.shape[0], _p(op), _p(of), _p(fl), _p(oo), _p(rm), _p(counts)),
+           "pba_outlier_landmarks")
+    return rm.astype(bool), dict(zip(("huge", "normal", "camera_distance", "z", "any_severe"), counts.tolist()))
 
 
 def split_record(rec: np.ndarray, R: int):
