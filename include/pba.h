@@ -56,6 +56,7 @@ extern "C" {
 #define PBA_CAMERA_PINHOLE 0        /* camera_models.h:48-114  */
 #define PBA_CAMERA_DOUBLE_SPHERE 1  /* camera_models.h:198-284 */
 #define PBA_CAMERA_EUCM 2           /* camera_models.h:116-196 */
+#define PBA_CAMERA_KB4 3            /* camera_models.h:286-421 (Kannala-Brandt, 4 distortion terms) */
 
 #define PBA_MAX_PATTERN 32
 

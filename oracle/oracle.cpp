@@ -18,7 +18,7 @@
 //   * Huber + Corrector .............. ceres-solver/internal/ceres/loss_function.cc:48-62,
 //                                      corrector.cc:42-110, residual_block.cc:161-196
 //   * Camera models .................. include/visnav/camera_models.h:75-107 (pinhole),
-//                                      :140-190 (EUCM), :226-277 (double sphere)
+//                                      :140-190 (EUCM), :226-277 (double sphere), :316-420 (Kannala-Brandt 4)
 //   * Geometric residual ............. include/visnav/reprojection.h:83-112
 //                                      r = u_obs − π_t(T_w_t⁻¹ · T_w_h · (normalize(π_h⁻¹(u_ref)) / ρ))
 //   * Photometric residual ........... ceres-solver/internal/ceres/autodiff_benchmarks/photometric_error.h:139-182
@@ -75,6 +75,15 @@ template <int N> inline Jet<N> operator*(const Jet<N>& f, double s) { Jet<N> h; 
 template <int N> inline Jet<N> operator*(double s, const Jet<N>& f) { return f * s; }
 template <int N> inline Jet<N> operator/(const Jet<N>& f, double s) { return f * (1.0 / s); }
 template <int N> inline Jet<N> operator/(double s, const Jet<N>& g) { Jet<N> h; const double ib = 1.0 / g.a; h.a = s * ib; const double c = -h.a * ib; for (int i = 0; i < N; ++i) h.v[i] = c * g.v[i]; return h; }
+// atan2(y, x): ∂/∂y = x/(x²+y²), ∂/∂x = −y/(x²+y²) (ceres/jet.h atan2)
+template <int N> inline Jet<N> atan2(const Jet<N>& y, const Jet<N>& x) {
+  Jet<N> h;
+  h.a = std::atan2(y.a, x.a);
+  const double t = 1.0 / (x.a * x.a + y.a * y.a);
+  for (int i = 0; i < N; ++i) h.v[i] = t * (x.a * y.v[i] - y.a * x.v[i]);
+  return h;
+}
+inline double atan2(double y, double x) { return std::atan2(y, x); }
 template <int N> inline Jet<N> sqrt(const Jet<N>& f) { Jet<N> h; h.a = std::sqrt(f.a); const double c = 0.5 / h.a; for (int i = 0; i < N; ++i) h.v[i] = f.v[i] * c; return h; }
 
 inline double val(double x) { return x; }
@@ -188,7 +197,7 @@ inline void se3_mul(const double* a, const double* b, double* out) {
 // ----------------------------------------------------------------------------------------------
 // Camera models (include/visnav/camera_models.h).  Intrinsics vector [fx fy cx cy p1 p2 p3 p4].
 // ----------------------------------------------------------------------------------------------
-enum { CAM_PINHOLE = 0, CAM_DS = 1, CAM_EUCM = 2 };
+enum { CAM_PINHOLE = 0, CAM_DS = 1, CAM_EUCM = 2, CAM_KB4 = 3 };
 
 template <class T>
 inline void project(int model, const double* k, const T p[3], T uv[2]) {
@@ -204,11 +213,24 @@ inline void project(int model, const double* k, const T p[3], T uv[2]) {
     const T denom = alpha * d2 + (1.0 - alpha) * (xi * d1 + p[2]);
     uv[0] = fx * p[0] / denom + cx;
     uv[1] = fy * p[1] / denom + cy;
-  } else {  // EUCM, camera_models.h:140-160
+  } else if (model == CAM_EUCM) {  // camera_models.h:140-160
     const double alpha = k[4], beta = k[5];
     const T d = sqrt(beta * (p[0] * p[0] + p[1] * p[1]) + p[2] * p[2]);
     uv[0] = fx * p[0] / (alpha * d + (1.0 - alpha) * p[2]) + cx;
     uv[1] = fy * p[1] / (alpha * d + (1.0 - alpha) * p[2]) + cy;
+  } else {  // Kannala-Brandt 4, camera_models.h:316-348
+    const double k1 = k[4], k2 = k[5], k3 = k[6], k4 = k[7];
+    const T r = sqrt(p[0] * p[0] + p[1] * p[1]);
+    if (val(r) == 0.0) {
+      uv[0] = T(cx);
+      uv[1] = T(cy);
+      return;
+    }
+    const T theta = atan2(r, p[2]);
+    const T t2 = theta * theta, t3 = t2 * theta;
+    const T d = theta + t3 * (k1 + t2 * (k2 + t2 * (k3 + t2 * k4)));
+    uv[0] = fx * d * p[0] / r + cx;
+    uv[1] = fy * d * p[1] / r + cy;
   }
 }
 
@@ -216,6 +238,7 @@ inline void project(int model, const double* k, const T p[3], T uv[2]) {
 // check; Ceres' PhotometricError::Project has the EUCM one (photometric_error.h:114-121).  Pinhole: z > eps.
 inline bool in_domain(int model, const double* k, const double p[3]) {
   if (model == CAM_PINHOLE) return p[2] > 1e-6;
+  if (model == CAM_KB4) return p[2] > 0.0 || p[0] * p[0] + p[1] * p[1] > 0.0;  // all but the backward axis
   if (model == CAM_EUCM) {
     const double alpha = k[4], beta = k[5];
     const double rho = std::sqrt(beta * (p[0] * p[0] + p[1] * p[1]) + p[2] * p[2]);
@@ -242,12 +265,27 @@ inline void unproject(int model, const double* k, const double uv[2], double b[3
                       (alpha * std::sqrt(1.0 - (2.0 * alpha - 1.0) * r2) + 1.0 - alpha);
     const double factor = (mz * xi + std::sqrt(mz * mz + (1.0 - xi * xi) * r2)) / (mz * mz + r2);
     b[0] = factor * mx; b[1] = factor * my; b[2] = factor * mz - xi;
-  } else {  // EUCM, camera_models.h:162-190
+  } else if (model == CAM_EUCM) {  // camera_models.h:162-190
     const double alpha = k[4], beta = k[5];
     const double r2 = mx * mx + my * my;
     b[0] = mx; b[1] = my;
     b[2] = (1.0 - beta * alpha * alpha * r2) /
            (alpha * std::sqrt(1.0 - (2.0 * alpha - 1.0) * beta * r2) + (1.0 - alpha));
+  } else {  // Kannala-Brandt 4, camera_models.h:352-380 (5 Newton steps from θ = 0)
+    const double ru = std::sqrt(mx * mx + my * my);
+    if (ru == 0.0) {
+      b[0] = 0.0; b[1] = 0.0; b[2] = 1.0;
+    } else {
+      const double k1 = k[4], k2 = k[5], k3 = k[6], k4 = k[7];
+      double th = 0.0;
+      for (int i = 0; i < 5; ++i) {
+        const double t2 = th * th;
+        const double f = th + t2 * th * (k1 + t2 * (k2 + t2 * (k3 + t2 * k4))) - ru;
+        const double df = 1.0 + t2 * (3.0 * k1 + t2 * (5.0 * k2 + t2 * (7.0 * k3 + t2 * 9.0 * k4)));
+        th = th - f / df;
+      }
+      b[0] = std::sin(th) * mx / ru; b[1] = std::sin(th) * my / ru; b[2] = std::cos(th);
+    }
   }
   const double n = std::sqrt(b[0] * b[0] + b[1] * b[1] + b[2] * b[2]);  // res /= res.norm()
   b[0] /= n; b[1] /= n; b[2] /= n;

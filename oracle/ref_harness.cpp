@@ -51,7 +51,7 @@ SE3L pose_from(const double* p) {
 }
 
 // Camera arithmetic, restated from include/visnav/camera_models.h (pinhole :75-107, EUCM :140-190,
-// double sphere :226-277) in long double.
+// double sphere :226-277, Kannala-Brandt 4 :316-420) in long double.
 void project(int model, const double* k, const V3& p, LD uv[2]) {
   const LD fx = k[0], fy = k[1], cx = k[2], cy = k[3];
   if (model == 0) {
@@ -65,12 +65,19 @@ void project(int model, const double* k, const V3& p, LD uv[2]) {
     const LD den = alpha * d2 + (1 - alpha) * xz;
     uv[0] = fx * p[0] / den + cx;
     uv[1] = fy * p[1] / den + cy;
-  } else {
+  } else if (model == 2) {
     const LD alpha = k[4], beta = k[5];
     const LD d = std::sqrt(beta * (p[0] * p[0] + p[1] * p[1]) + p[2] * p[2]);
     const LD den = alpha * d + (1 - alpha) * p[2];
     uv[0] = fx * p[0] / den + cx;
     uv[1] = fy * p[1] / den + cy;
+  } else {  // Kannala-Brandt 4 (camera_models.h:316-348)
+    const LD r = std::sqrt(p[0] * p[0] + p[1] * p[1]);
+    if (r == 0) { uv[0] = cx; uv[1] = cy; return; }
+    const LD th = std::atan2(r, p[2]), t2 = th * th;
+    const LD d = th + t2 * th * ((LD)k[4] + t2 * ((LD)k[5] + t2 * ((LD)k[6] + t2 * (LD)k[7])));
+    uv[0] = fx * d * p[0] / r + cx;
+    uv[1] = fy * d * p[1] / r + cy;
   }
 }
 
@@ -86,10 +93,21 @@ V3 unproject(int model, const double* k, LD u, LD v) {
     const LD mz = (1 - alpha * alpha * r2) / (alpha * std::sqrt(1 - (2 * alpha - 1) * r2) + 1 - alpha);
     const LD fac = (mz * xi + std::sqrt(mz * mz + (1 - xi * xi) * r2)) / (mz * mz + r2);
     b << fac * mx, fac * my, fac * mz - xi;
-  } else {
+  } else if (model == 2) {
     const LD alpha = k[4], beta = k[5];
     const LD r2 = mx * mx + my * my;
     b << mx, my, (1 - beta * alpha * alpha * r2) / (alpha * std::sqrt(1 - (2 * alpha - 1) * beta * r2) + (1 - alpha));
+  } else {  // Kannala-Brandt 4 (camera_models.h:352-380): 5 Newton steps from θ = 0
+    const LD ru = std::sqrt(mx * mx + my * my);
+    if (ru == 0) return V3(0, 0, 1);
+    LD th = 0;
+    for (int i = 0; i < 5; ++i) {
+      const LD t2 = th * th;
+      const LD f = th + t2 * th * ((LD)k[4] + t2 * ((LD)k[5] + t2 * ((LD)k[6] + t2 * (LD)k[7]))) - ru;
+      const LD df = 1 + t2 * (3 * (LD)k[4] + t2 * (5 * (LD)k[5] + t2 * (7 * (LD)k[6] + t2 * 9 * (LD)k[7])));
+      th -= f / df;
+    }
+    b << std::sin(th) * mx / ru, std::sin(th) * my / ru, std::cos(th);
   }
   return b.normalized();
 }
@@ -148,6 +166,7 @@ bool residual(const Problem& pb, int b, const SE3L& Th, const SE3L& Tt, LD rho, 
       const LD w2 = (w1 + xi) / std::sqrt(2 * w1 * xi + xi * xi + 1);
       if (!(p[2] > -w2 * d1 + 1e-10L)) return false;
     }
+    if (pb.model == 3 && !(p[2] > 0 || p[0] * p[0] + p[1] * p[1] > 0)) return false;  // KB4: all but the backward axis
     if (pb.model == 2) {  // EUCM domain, photometric_error.h:114-121
       const LD al = kt[4], be = kt[5];
       const LD rr = std::sqrt(be * (p[0] * p[0] + p[1] * p[1]) + p[2] * p[2]);

@@ -24,7 +24,7 @@
 
 namespace pba {
 
-enum : int { CAM_PINHOLE = 0, CAM_DS = 1, CAM_EUCM = 2 };
+enum : int { CAM_PINHOLE = 0, CAM_DS = 1, CAM_EUCM = 2, CAM_KB4 = 3 };
 
 template <class S>
 struct V3 { S x, y, z; };
@@ -73,11 +73,26 @@ __device__ __forceinline__ float rcp_s(float x) { return __builtin_amdgcn_rcpf(x
 __device__ __forceinline__ double rcp_s(double x) { return rcp_nr(x); }
 
 // Camera record in device memory: kCamD doubles per camera, laid out for the two uses —
-//   [0..5]   projection   "tk": fx fy cx cy p1 p2      (camera_models.h:50, p1/p2 = ξ,α (DS) or α,β (EUCM))
-//   [6..11]  unprojection "hk": cx cy 1/fx 1/fy p1 p2   (reciprocals precomputed on the host)
-//   [12..15] p3 p4 0 0
+//   [0..7]   projection   "tk": fx fy cx cy p1 p2 p3 p4      (camera_models.h:50; p1,p2 = ξ,α (DS) or α,β (EUCM),
+//                                                         p1..p4 = k1..k4 (KB4))
+//   [8..15]  unprojection "hk": cx cy 1/fx 1/fy p1 p2 p3 p4   (reciprocals precomputed on the host)
 // The pair kernel copies the host camera's hk and the target camera's tk into every PairRec.
-constexpr int kCamD = 16, kCamHk = 6;
+constexpr int kCamK = 8, kCamD = 2 * kCamK, kCamHk = kCamK;
+
+__device__ __forceinline__ float atan2_s(float y, float x) { return atan2f(y, x); }
+__device__ __forceinline__ double atan2_s(double y, double x) { return atan2(y, x); }
+
+// Kannala-Brandt d(θ) = θ + θ³(k1 + θ²(k2 + θ²(k3 + θ²k4))) and d'(θ) (camera_models.h:338-343, :406-420)
+template <class S, class K>
+__device__ __forceinline__ S kb4_d(const K* k, S th) {
+  const S t2 = th * th;
+  return th + t2 * th * ((S)k[0] + t2 * ((S)k[1] + t2 * ((S)k[2] + t2 * (S)k[3])));
+}
+template <class S, class K>
+__device__ __forceinline__ S kb4_dd(const K* k, S th) {
+  const S t2 = th * th;
+  return S(1) + t2 * (S(3) * (S)k[0] + t2 * (S(5) * (S)k[1] + t2 * (S(7) * (S)k[2] + t2 * S(9) * (S)k[3])));
+}
 
 // Unit bearing of pixel (u, v) — camera_models.h unproject (pinhole :93-107, EUCM :162-190,
 // DS :247-277) followed by normalize() (reprojection.h:104).  fp64; hk = [cx cy 1/fx 1/fy p1 p2].
@@ -94,10 +109,19 @@ __device__ __forceinline__ Vec3d unproject(const double* hk, double u, double v)
     const double mz = (1.0 - al * al * r2) * rcp_nr(al * sqrt(1.0 - (2.0 * al - 1.0) * r2) + 1.0 - al);
     const double fac = (mz * xi + sqrt(mz * mz + (1.0 - xi * xi) * r2)) * rcp_nr(mz * mz + r2);
     b = {fac * mx, fac * my, fac * mz - xi};
-  } else {
+  } else if (MODEL == CAM_EUCM) {
     const double al = hk[4], be = hk[5];
     const double r2 = mx * mx + my * my;
     b = {mx, my, (1.0 - be * al * al * r2) * rcp_nr(al * sqrt(1.0 - (2.0 * al - 1.0) * be * r2) + (1.0 - al))};
+  } else {  // KB4, camera_models.h:352-380: 5 Newton steps on d(θ) = r_u from θ = 0
+    const double ru = sqrt(mx * mx + my * my);
+    if (ru == 0.0) return {0.0, 0.0, 1.0};
+    double th = 0.0;
+#pragma unroll
+    for (int i = 0; i < 5; ++i) th -= (kb4_d(hk + 4, th) - ru) / kb4_dd(hk + 4, th);
+    double sn, cs;
+    sincos(th, &sn, &cs);
+    b = {sn * mx / ru, sn * my / ru, cs};
   }
   const double inv = rsqrt_nr(b.x * b.x + b.y * b.y + b.z * b.z);
   return {b.x * inv, b.y * inv, b.z * inv};
@@ -108,6 +132,7 @@ __device__ __forceinline__ Vec3d unproject(const double* hk, double u, double v)
 template <int MODEL>
 __device__ __forceinline__ bool in_domain(const double* k, const Vec3d& p) {
   if (MODEL == CAM_PINHOLE) return p.z > 1e-6;
+  if (MODEL == CAM_KB4) return p.z > 0.0 || p.x * p.x + p.y * p.y > 0.0;  // all but the backward axis
   if (MODEL == CAM_EUCM) {
     const double al = k[4], be = k[5];
     const double rr = sqrt(be * (p.x * p.x + p.y * p.y) + p.z * p.z);
@@ -125,6 +150,18 @@ __device__ __forceinline__ bool in_domain(const double* k, const Vec3d& p) {
 // [fx fy cx cy p1 p2].  Returns 1/den (pinhole: 1/z), which project_jac reuses.
 template <int MODEL>
 __device__ __forceinline__ double project(const double* k, const Vec3d& p, double& u, double& v) {
+  if (MODEL == CAM_KB4) {  // camera_models.h:316-348; returns the scale d(θ)/r (1/z at r = 0, its limit)
+    const double r = sqrt(p.x * p.x + p.y * p.y);
+    if (r == 0.0) {
+      u = k[2];
+      v = k[3];
+      return rcp_nr(p.z);
+    }
+    const double d = kb4_d(k + 4, atan2(r, p.z));
+    u = k[0] * d * p.x / r + k[2];
+    v = k[1] * d * p.y / r + k[3];
+    return d / r;
+  }
   double den;
   if (MODEL == CAM_PINHOLE) {
     den = p.z;
@@ -152,6 +189,18 @@ __device__ __forceinline__ double sqrt_s(double x) { return sqrt(x); }
 template <int MODEL, class S>
 __device__ __forceinline__ void project_jac(const S* k, const V3<S>& p, S iden, V3<S>& du, V3<S>& dv) {
   const S fx = k[0], fy = k[1], one = S(1), zero = S(0);
+  if (MODEL == CAM_KB4) {
+    // u = fx·d(θ)·c + cx with (c, s) = (x, y)/r:  ∂u/∂p = fx·(d'(θ)·c·∇θ + (d/r)·(s², −cs, 0)), no cancellation
+    // as r → 0 (iden = d/r from project(); at r = 0 take c = 1, s = 0, the limit)
+    const S r = sqrt_s(p.x * p.x + p.y * p.y);
+    const S c = r > zero ? p.x / r : one, sn = r > zero ? p.y / r : zero;
+    const S ir2 = one / (r * r + p.z * p.z);
+    const V3<S> gt = {p.z * c * ir2, p.z * sn * ir2, -r * ir2};
+    const S dd = kb4_dd(k + 4, atan2_s(r, p.z));
+    du = {fx * (dd * c * gt.x + iden * sn * sn), fx * (dd * c * gt.y - iden * c * sn), fx * dd * c * gt.z};
+    dv = {fy * (dd * sn * gt.x - iden * c * sn), fy * (dd * sn * gt.y + iden * c * c), fy * dd * sn * gt.z};
+    return;
+  }
   if (MODEL == CAM_PINHOLE) {
     const S mx = p.x * iden, my = p.y * iden;
     du = {fx * iden, zero, -fx * mx * iden};

@@ -73,10 +73,11 @@ __device__ __forceinline__ void make_pair(const double* __restrict__ poses, cons
   r.host = h;
   const double* hc = cams + kCamD * r.host_cam + kCamHk;
   const double* tc = cams + kCamD * r.target_cam;
-  for (int j = 0; j < kCamHk; ++j) {
+  for (int j = 0; j < kCamK; ++j) {
     r.hk[j] = hc[j];
     r.tk[j] = tc[j];
   }
+  for (int j = 0; j < 8; ++j) r.pad[j] = 0.0f;
   for (int j = 0; j < 9; ++j) r.Rf[j] = (float)r.R[j];
   for (int j = 0; j < 3; ++j) r.tf[j] = (float)r.t[j];
   pairs[i] = r;
@@ -297,7 +298,8 @@ void launch_mode(pba_engine* e, const KernelArgs& ka, int mode) {
   switch (e->opt.camera_model) {
     case PBA_CAMERA_PINHOLE: launch_blocks<CAM_PINHOLE>(e, ka, mode); break;
     case PBA_CAMERA_DOUBLE_SPHERE: launch_blocks<CAM_DS>(e, ka, mode); break;
-    default: launch_blocks<CAM_EUCM>(e, ka, mode); break;
+    case PBA_CAMERA_EUCM: launch_blocks<CAM_EUCM>(e, ka, mode); break;
+    default: launch_blocks<CAM_KB4>(e, ka, mode); break;
   }
 }
 
@@ -370,7 +372,7 @@ int pba_create(const pba_options* o, pba_engine** out) {
   *out = nullptr;
   if (o->residual_kind != PBA_RESIDUAL_PHOTOMETRIC && o->residual_kind != PBA_RESIDUAL_GEOMETRIC)
     return fail(PBA_ERR_INVALID_ARGUMENT, "unknown residual kind");
-  if (o->camera_model < PBA_CAMERA_PINHOLE || o->camera_model > PBA_CAMERA_EUCM)
+  if (o->camera_model < PBA_CAMERA_PINHOLE || o->camera_model > PBA_CAMERA_KB4)
     return fail(PBA_ERR_INVALID_ARGUMENT, "unknown camera model");
   int n = 0;
   hipError_t err = hipGetDeviceCount(&n);
@@ -422,14 +424,14 @@ int pba_set_cameras(pba_engine* e, int32_t n_cams, const double* intrinsics) {
   for (size_t i = 0; i < f.size(); ++i) f[i] = (float)intrinsics[i];
   for (int c = 0; c < n_cams; ++c)
     if (!(f[8 * c] != 0.0f && f[8 * c + 1] != 0.0f)) return fail(PBA_ERR_INVALID_ARGUMENT, "zero focal length");
-  // fp64 camera records (kCamD doubles each, pba_device.h): [fx fy cx cy p1 p2 | cx cy 1/fx 1/fy p1 p2 | p3 p4]
+  // fp64 camera records (kCamD doubles each, pba_device.h): [fx fy cx cy p1..p4 | cx cy 1/fx 1/fy p1..p4]
   std::vector<double> d((size_t)kCamD * n_cams, 0.0);
   for (int c = 0; c < n_cams; ++c) {
     const double* k = intrinsics + 8 * c;
     double* r = d.data() + (size_t)kCamD * c;
-    for (int j = 0; j < 6; ++j) r[j] = k[j];
-    r[6] = k[2]; r[7] = k[3]; r[8] = 1.0 / k[0]; r[9] = 1.0 / k[1]; r[10] = k[4]; r[11] = k[5];
-    r[12] = k[6]; r[13] = k[7];
+    for (int j = 0; j < 8; ++j) r[j] = k[j];
+    r[8] = k[2]; r[9] = k[3]; r[10] = 1.0 / k[0]; r[11] = 1.0 / k[1];
+    for (int j = 4; j < 8; ++j) r[8 + j] = k[j];
   }
   PBA_HIP(e->intr.resize(f.size()));
   PBA_HIP(e->intr_d.resize(d.size()));

@@ -1598,7 +1598,8 @@ void launch_linearize_k(pba_engine* e, const KernelArgs& ka, const LinArgs& la) 
   switch (e->opt.camera_model) {
     case PBA_CAMERA_PINHOLE: launch_linearize<KIND, CAM_PINHOLE>(e, ka, la); break;
     case PBA_CAMERA_DOUBLE_SPHERE: launch_linearize<KIND, CAM_DS>(e, ka, la); break;
-    default: launch_linearize<KIND, CAM_EUCM>(e, ka, la); break;
+    case PBA_CAMERA_EUCM: launch_linearize<KIND, CAM_EUCM>(e, ka, la); break;
+    default: launch_linearize<KIND, CAM_KB4>(e, ka, la); break;
   }
 }
 

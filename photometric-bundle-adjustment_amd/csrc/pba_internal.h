@@ -23,11 +23,12 @@ struct alignas(16) PairRec {
   double R[9];                 // R_th, fp64 (warp)
   double t[3];                 // t_th
   int host_cam, target_cam, target, host;
-  double hk[kCamHk];           // host camera, unprojection layout [cx cy 1/fx 1/fy p1 p2]
-  double tk[kCamHk];           // target camera, projection layout [fx fy cx cy p1 p2]
+  double hk[kCamK];            // host camera, unprojection layout [cx cy 1/fx 1/fy p1 p2 p3 p4]
+  double tk[kCamK];            // target camera, projection layout [fx fy cx cy p1 p2 p3 p4]
   float Rf[9], tf[3];          // fp32 R_th, t_th (Jacobian chain)
+  float pad[8];
 };
-static_assert(sizeof(PairRec) == 256, "PairRec layout");
+static_assert(sizeof(PairRec) == 320, "PairRec layout");
 
 // One block of a workgroup's tile, staged in LDS by stage_tile(): its pair record and its point.
 struct alignas(16) TileBlock {
@@ -36,8 +37,9 @@ struct alignas(16) TileBlock {
   double rho;                  // inverse distance (state)
   int point, pad;
 };
-static_assert(sizeof(TileBlock) == 288, "TileBlock layout");
-constexpr int kTileParts = sizeof(TileBlock) / 16;  // 18 × 16 B
+static_assert(sizeof(TileBlock) == 352, "TileBlock layout");
+constexpr int kPairParts = sizeof(PairRec) / 16;     // 20 × 16 B
+constexpr int kTileParts = sizeof(TileBlock) / 16;   // 22 × 16 B
 
 struct KernelArgs {
   const uint8_t* images;
@@ -124,7 +126,7 @@ struct Row {
 };
 
 // Cooperative tile prologue: the LPB lanes of block lb copy its pair record, u_ref and ρ into LDS as
-// 18 16-B parts (lane k takes parts k, k+LPB, …) — one broadcast copy per block instead of every lane
+// kTileParts 16-B parts (lane k takes parts k, k+LPB, …) — one broadcast copy per block instead of every lane
 // loading the 256-B record and the point data itself.  Returns the block's point.  The caller barriers.
 template <int LPB>
 __device__ __forceinline__ int stage_tile(const KernelArgs& a, TileBlock* s_tb, int lb, int k, int blk, bool live) {
@@ -135,9 +137,9 @@ __device__ __forceinline__ int stage_tile(const KernelArgs& a, TileBlock* s_tb, 
 #pragma unroll
   for (int part = k; part < kTileParts; part += LPB) {
     uint4 v;
-    if (part < 16) {
+    if (part < kPairParts) {
       v = src[part];
-    } else if (part == 16) {
+    } else if (part == kPairParts) {
       v = reinterpret_cast<const uint4*>(a.u_ref)[pp.x];
     } else {
       const double r = a.rho[pp.x];
@@ -173,7 +175,8 @@ __device__ __forceinline__ Row photometric_row(const KernelArgs& a, const TileBl
   if (JAC && dom) {
     // q = ∇I · ∂π/∂p̃ (1×3)
     const Vec3 pf = to_f(p), bf = to_f(b);
-    const float kf[6] = {(float)pp.tk[0], (float)pp.tk[1], 0.0f, 0.0f, (float)pp.tk[4], (float)pp.tk[5]};
+    const float kf[8] = {(float)pp.tk[0], (float)pp.tk[1], 0.0f, 0.0f,
+                         (float)pp.tk[4], (float)pp.tk[5], (float)pp.tk[6], (float)pp.tk[7]};
     Vec3 du, dv;
     project_jac<MODEL>(kf, pf, (float)iden, du, dv);
     const Vec3 q = {gx * du.x + gy * dv.x, gx * du.y + gy * dv.y, gx * du.z + gy * dv.z};

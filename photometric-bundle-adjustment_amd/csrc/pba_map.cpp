@@ -191,10 +191,11 @@ bool read_file(const char* path, std::string& out) {
   return true;
 }
 
-int model_of(const std::string& name) {  // camera_models.h getName(): "pinhole", "ds", "eucm" ("kb4" unsupported)
+int model_of(const std::string& name) {  // camera_models.h getName(): "pinhole", "ds", "eucm", "kb4"
   if (name == "pinhole") return PBA_CAMERA_PINHOLE;
   if (name == "ds") return PBA_CAMERA_DOUBLE_SPHERE;
   if (name == "eucm") return PBA_CAMERA_EUCM;
+  if (name == "kb4") return PBA_CAMERA_KB4;
   return -1;
 }
 

@@ -134,7 +134,8 @@ int pba_compute_projections(pba_engine* e, int32_t n_obs, const int32_t* obs_poi
   switch (e->opt.camera_model) {
     case PBA_CAMERA_PINHOLE: projections_kernel<CAM_PINHOLE><<<grid, 256, 0, e->stream>>>(a); break;
     case PBA_CAMERA_DOUBLE_SPHERE: projections_kernel<CAM_DS><<<grid, 256, 0, e->stream>>>(a); break;
-    default: projections_kernel<CAM_EUCM><<<grid, 256, 0, e->stream>>>(a); break;
+    case PBA_CAMERA_EUCM: projections_kernel<CAM_EUCM><<<grid, 256, 0, e->stream>>>(a); break;
+    default: projections_kernel<CAM_KB4><<<grid, 256, 0, e->stream>>>(a); break;
   }
   PBA_HIP(hipGetLastError());
   if (reprojected) PBA_HIP(hipMemcpyAsync(reprojected, d_rep.p, sizeof(double2) * n_obs, hipMemcpyDeviceToHost, e->stream));

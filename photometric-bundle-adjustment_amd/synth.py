@@ -28,8 +28,8 @@ from typing import Optional
 import numpy as np
 
 PHOTOMETRIC, GEOMETRIC = 0, 1
-PINHOLE, DOUBLE_SPHERE, EUCM = 0, 1, 2
-MODEL_IDS = {"pinhole": PINHOLE, "ds": DOUBLE_SPHERE, "eucm": EUCM}
+PINHOLE, DOUBLE_SPHERE, EUCM, KB4 = 0, 1, 2, 3
+MODEL_IDS = {"pinhole": PINHOLE, "ds": DOUBLE_SPHERE, "eucm": EUCM, "kb4": KB4}
 KIND_IDS = {"photometric": PHOTOMETRIC, "geometric": GEOMETRIC}
 
 # EuRoC-like 752×480 intrinsics per model, vector layout of camera_models.h ([fx fy cx cy p1 p2 0 0]).
@@ -37,6 +37,8 @@ DEFAULT_INTRINSICS = {
     PINHOLE: [458.654, 457.296, 367.215, 248.375, 0, 0, 0, 0],
     DOUBLE_SPHERE: [349.7, 349.9, 365.9, 249.0, -0.28, 0.57, 0, 0],
     EUCM: [460.0, 459.0, 365.5, 249.5, 0.59, 1.1, 0, 0],
+    # Kannala-Brandt 4: the distortion of camera_models.h getTestProjections (:302-306) with a 752×480 camera
+    KB4: [379.045, 379.008, 375.5, 239.5, 0.00693023, -0.0013828, -0.000272596, -0.000452646],
 }
 
 # DSO-style 8-pixel residual pattern (du, dv) — SURVEY.md §8d.
@@ -170,10 +172,21 @@ def unproject(model: int, k: np.ndarray, uv: np.ndarray) -> np.ndarray:
         mz = (1 - al * al * r2) / (al * np.sqrt(1 - (2 * al - 1) * r2) + 1 - al)
         fac = (mz * xi + np.sqrt(mz * mz + (1 - xi * xi) * r2)) / (mz * mz + r2)
         b = np.stack([fac * mx, fac * my, fac * mz - xi], -1)
-    else:
+    elif model == EUCM:
         al, be = k[..., 4], k[..., 5]
         mz = (1 - be * al * al * r2) / (al * np.sqrt(1 - (2 * al - 1) * be * r2) + (1 - al))
         b = np.stack([mx, my, mz], -1)
+    else:  # KB4: 5 Newton steps on d(θ) = r_u from θ = 0 (camera_models.h:352-380)
+        k1, k2, k3, k4 = k[..., 4], k[..., 5], k[..., 6], k[..., 7]
+        ru = np.sqrt(r2)
+        th = np.zeros_like(ru)
+        for _ in range(5):
+            t2 = th * th
+            f = th + t2 * th * (k1 + t2 * (k2 + t2 * (k3 + t2 * k4))) - ru
+            df = 1 + t2 * (3 * k1 + t2 * (5 * k2 + t2 * (7 * k3 + t2 * 9 * k4)))
+            th = th - f / df
+        safe = np.where(ru > 0, ru, 1.0)
+        b = np.stack([np.sin(th) * mx / safe, np.sin(th) * my / safe, np.cos(th)], -1)
     return b / np.linalg.norm(b, axis=-1, keepdims=True)
 
 
@@ -188,10 +201,17 @@ def project(model: int, k: np.ndarray, p: np.ndarray) -> np.ndarray:
         xz = xi * d1 + z
         d2 = np.sqrt(x * x + y * y + xz * xz)
         den = al * d2 + (1 - al) * xz
-    else:
+    elif model == EUCM:
         al, be = k[..., 4], k[..., 5]
         d = np.sqrt(be * (x * x + y * y) + z * z)
         den = al * d + (1 - al) * z
+    else:  # KB4 (camera_models.h:316-348): u = fx·d(θ)·x/r + cx, θ = atan2(r, z)
+        k1, k2, k3, k4 = k[..., 4], k[..., 5], k[..., 6], k[..., 7]
+        r = np.sqrt(x * x + y * y)
+        th = np.arctan2(r, z)
+        t2 = th * th
+        d = th + t2 * th * (k1 + t2 * (k2 + t2 * (k3 + t2 * k4)))
+        den = np.where(r > 0, r / np.where(d != 0, d, 1.0), z)
     return np.stack([k[..., 0] * x / den + k[..., 2], k[..., 1] * y / den + k[..., 3]], -1)
 
 

@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Regenerate the golden fixtures in tests/golden/ from the reference's own vendored Sophus/Eigen.
 
-Runs in the build container only (needs /root/reference): builds oracle/_ref/ref_harness from
+Runs in the build container only (needs /root/reference; `make_golden.py name …` regenerates only the named
+fixtures): builds oracle/_ref/ref_harness from
 oracle/ref_harness.cpp against /root/reference/thirdparty/{Sophus,eigen}, feeds it seeded synthetic
 problems (photometric-bundle-adjustment_amd/synth.py) and stores inputs + outputs as compressed .npz.
 The GPU box only ever sees the .npz files.
@@ -119,12 +120,13 @@ def se3_fixture(n=256, seed=7):
                 "Dx_this_mul_exp_x_at_0 / T2^-1*T (se3.hpp:135-211,763-784)")
 
 
-def main():
+def main(only=()):
     build_harness()
     manifest = {"generator": "tests/golden/make_golden.py", "harness": "oracle/ref_harness.cpp",
                 "compiled_against": ["/root/reference/thirdparty/Sophus (1.1.0)", "/root/reference/thirdparty/eigen (3.3.8)"],
                 "fixtures": []}
-    manifest["fixtures"].append(se3_fixture())
+    if not only:
+        manifest["fixtures"].append(se3_fixture())
     W, H = 320, 200
     cases = [
         ("geometric_pinhole", dict(kind="geometric", model="pinhole", n_frames=10, n_points=300, width=752, height=480, seed=11),
@@ -137,21 +139,31 @@ def main():
          "photometric residual, double sphere"),
         ("photometric_eucm", dict(kind="photometric", model="eucm", n_frames=7, n_points=96, width=W, height=H, seed=15),
          "photometric residual, EUCM (Ceres PhotometricError camera)"),
+        ("geometric_kb4", dict(kind="geometric", model="kb4", n_frames=10, n_points=300, width=752, height=480, seed=17),
+         "reprojection.h:105-108 residual, Kannala-Brandt 4 (camera_models.h:316-420)"),
+        ("photometric_kb4", dict(kind="photometric", model="kb4", n_frames=7, n_points=96, width=W, height=H, seed=18),
+         "photometric residual, Kannala-Brandt 4"),
     ]
+    if only:  # regenerate just these fixtures, keep the others (and their manifest entries) as they are
+        old = json.load(open(os.path.join(GOLDEN, "MANIFEST.json")))
+        manifest["fixtures"] = [f for f in old["fixtures"] if f["file"][:-4] not in only]
+        cases = [c for c in cases if c[0] in only]
     for name, kw, note in cases:
         pb = synth.make_problem(border=12 if kw["width"] < 752 else 24, **kw)
         manifest["fixtures"].append(save_block_fixture(name, pb, note))
-    # Edge cases: points pushed off-image (edge clamp) and behind the target (invalid blocks).
-    pb = synth.make_problem(kind="photometric", model="pinhole", n_frames=6, n_points=64, width=W, height=H, seed=16, border=2)
-    # keyframe 5 turned around (π about y): every block targeting it leaves the pinhole domain → invalid
-    pb.poses[5] = synth.se3_plus(pb.poses[5], np.array([0, 0, 0, 0, np.pi, 0.0]))
-    pb.u_ref[8:16, 0] = W - 1.0          # right image edge: pattern taps clamp
-    pb.u_ref[16:24, 1] = 0.0             # top edge
-    manifest["fixtures"].append(save_block_fixture("photometric_edges", pb, "edge clamp + invalid (behind camera) blocks"))
+    if not only or "photometric_edges" in only:
+        # Edge cases: points pushed off-image (edge clamp) and behind the target (invalid blocks).
+        pb = synth.make_problem(kind="photometric", model="pinhole", n_frames=6, n_points=64, width=W, height=H, seed=16,
+                                border=2)
+        # keyframe 5 turned around (π about y): every block targeting it leaves the pinhole domain → invalid
+        pb.poses[5] = synth.se3_plus(pb.poses[5], np.array([0, 0, 0, 0, np.pi, 0.0]))
+        pb.u_ref[8:16, 0] = W - 1.0          # right image edge: pattern taps clamp
+        pb.u_ref[16:24, 1] = 0.0             # top edge
+        manifest["fixtures"].append(save_block_fixture("photometric_edges", pb, "edge clamp + invalid (behind camera) blocks"))
     with open(os.path.join(GOLDEN, "MANIFEST.json"), "w") as f:
         json.dump(manifest, f, indent=1)
     print(json.dumps(manifest, indent=1))
 
 
 if __name__ == "__main__":
-    main()
+    main(tuple(sys.argv[1:]))  # optional fixture names: regenerate only those

@@ -24,7 +24,7 @@ def make_engine(pb, huber, fixed):
     return eng
 
 
-CASES = [(0, 0, 9.0), (0, 1, 9.0), (0, 2, 0.0), (1, 0, 1.0), (1, 1, 1.0)]
+CASES = [(0, 0, 9.0), (0, 1, 9.0), (0, 2, 0.0), (0, 3, 9.0), (1, 0, 1.0), (1, 1, 1.0), (1, 3, 1.0)]
 
 
 @pytest.mark.parametrize("kind,model,huber", CASES)

@@ -39,7 +39,7 @@ def test_golden_fixture_parity(name):
     print(name, st)
 
 
-CASES = [(k, m, s) for k in (0, 1) for m in (0, 1, 2) for s in (1, 2)]
+CASES = [(k, m, s) for k in (0, 1) for m in (0, 1, 2, 3) for s in (1, 2)]
 
 
 @pytest.mark.parametrize("kind,model,seed", CASES)

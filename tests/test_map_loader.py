@@ -74,7 +74,7 @@ def test_map_loader_rejects_bad_input(tmp_path):
     with pytest.raises(E.PbaError):
         E.load_map(str(tmp_path / "missing.cereal"), CALIB)
     js = tmp_path / "calib.json"
-    js.write_text(open(CALIB).read().replace('"ds"', '"kb4"'))
+    js.write_text(open(CALIB).read().replace('"ds"', '"fov"'))
     with pytest.raises(E.PbaError):
         E.load_map(MAP, str(js))
     js.write_text("{ not json")

@@ -43,7 +43,7 @@ def test_oracle_matches_reference_harness(name):
     assert np.all(out[ev == 0] == 0)
 
 
-@pytest.mark.parametrize("kind,model", [(0, 0), (0, 1), (0, 2), (1, 0), (1, 1), (1, 2)])
+@pytest.mark.parametrize("kind,model", [(0, 0), (0, 1), (0, 2), (0, 3), (1, 0), (1, 1), (1, 2), (1, 3)])
 def test_oracle_jacobians_vs_finite_differences(kind, model):
     pb = synth.make_problem(n_frames=6, n_points=12, width=320, height=200, kind=kind, model=model, seed=3 + model,
                             border=12)

@@ -76,7 +76,7 @@ def observations(pb, rng):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("model", ["pinhole", "ds", "eucm"])
+@pytest.mark.parametrize("model", ["pinhole", "ds", "eucm", "kb4"])
 def test_compute_projections_match_reference(model):
     rng = np.random.default_rng(11)
     pb = synth.make_problem(kind="geometric", model=model, n_frames=20, n_points=800, seed=21, obs_sigma=0.3)
