@@ -89,7 +89,8 @@ int pba_set_frames_device(pba_engine* engine, int32_t n_frames, const int32_t* f
 /* residual pattern: P (du, dv) pairs, P <= PBA_MAX_PATTERN (photometric only) */
 int pba_set_pattern(pba_engine* engine, int32_t P, const float* offsets);
 /* points: host keyframe, u_ref (2 doubles, pixel in the host image), host_intensity (P floats,
- * photometric only — the I_h,k of photometric_error.h:179). */
+ * photometric only — the I_h,k of photometric_error.h:179; NULL: sampled on the device from the host keyframe's
+ * image at u_ref + pattern offset, bilinear). */
 int pba_set_points(pba_engine* engine, int32_t n_points, const int32_t* host_frame, const double* u_ref,
                    const float* host_intensity);
 /* blocks: point index and target keyframe per block; u_obs (2 doubles per block) for geometric engines.
@@ -107,7 +108,15 @@ int pba_evaluate(pba_engine* engine, int32_t want_jacobians);
 int pba_synchronize(pba_engine* engine);
 
 /* Results ---------------------------------------------------------------------------------------- */
-int pba_record_floats(const pba_engine* engine);   /* 14·R */
+int pba_record_floats(const pba_engine* engine);   /* 14·R (values per record, in the record format) */
+/* Record storage format (photometric engines): PBA_RECORD_F32 (default) or PBA_RECORD_F16 — IEEE half records,
+ * half the HBM write traffic (config C5's "fp16 residuals"; evaluation stays fp64 warp + fp32 chain, rounding
+ * only at the store: ≤ 2⁻¹¹ relative per value).  pba_get_records returns floats either way;
+ * pba_device_records' pointer then addresses 14·R halves per block. */
+#define PBA_RECORD_F32 0
+#define PBA_RECORD_F16 1
+int pba_set_record_format(pba_engine* engine, int32_t format);
+int pba_record_format(const pba_engine* engine);
 int pba_num_blocks(const pba_engine* engine);
 int pba_num_points(const pba_engine* engine);
 int pba_num_frames(const pba_engine* engine);
@@ -202,6 +211,24 @@ typedef int (*pba_allreduce_fn)(void* user, double* d_buf, int64_t count);
 int pba_solve_distributed(pba_engine* engine, const pba_solver_options* options, int32_t band, double* d_exchange,
                           pba_allreduce_fn allreduce, void* user, pba_solver_summary* summary);
 
+/* Image pyramid / coarse-to-fine ------------------------------------------
+ * pba_build_pyramid builds levels 1 … n−1 on the device from the current frames, cameras and points (DSO
+ * convention): level l+1 pixel = round(mean of a 2×2 level-l block), W_{l+1} = ⌊W_l/2⌋; camera fx_l = fx/2^l,
+ * c_l = (c + 0.5)/2^l − 0.5 (distortion unchanged); u_ref_l likewise; the same pattern offsets; I_h,k re-sampled
+ * from the host's level-l image.  pba_set_level selects the level every evaluation / Gauss-Newton entry point
+ * runs on (state and problem structure are shared by all levels).  Any pba_set_cameras/frames/pattern/points
+ * call returns to level 0 and drops the pyramid.  Photometric engines only. */
+#define PBA_MAX_LEVELS 8
+int pba_build_pyramid(pba_engine* engine, int32_t n_levels);
+int pba_num_levels(const pba_engine* engine);
+int pba_set_level(pba_engine* engine, int32_t level);
+int pba_get_level(const pba_engine* engine, int32_t* level, int32_t* width, int32_t* height);
+/* the active level's I_h,k (n_points·P floats) */
+int pba_get_host_intensities(pba_engine* engine, float* host_intensity);
+/* pba_solve on levels n−1 … 0 (coarse to fine); the summary sums iterations/timings, initial cost of the
+ * coarsest level, final cost at level 0 */
+int pba_solve_pyramid(pba_engine* engine, const pba_solver_options* options, pba_solver_summary* summary);
+
 /* Reprojections and outlier flags after a bundle-adjustment pass -------------------
  * pba_compute_projections replaces compute_projections() + set_outlier_flags() of src/sfm.cpp:1928-2008 for
  * any list of observations (inlier and outlier obs; the anchor's own observation included, as the reference
@@ -209,7 +236,8 @@ int pba_solve_distributed(pba_engine* engine, const pba_solver_options* options,
  *   p_c = T_w_f⁻¹ · T_w_host(p) · (normalize(π_host⁻¹(u_ref(p))) / ρ_p)   (Landmark::get_p, common_types.h:205-217)
  *   reprojected = π_f(p_c), error = ‖obs_uv − reprojected‖, and for inlier observations the flags below
  *   (thresholds: sfm.cpp:254-261 defaults 3 px, 40 px, 0.1 m, 0.05 m when th == NULL).
- * fp64 throughout.  All pointers are host pointers; obs_is_outlier, reprojected, point_c, error, flags may be NULL. */
+ * fp64 throughout, at pyramid level 0.  All pointers are host pointers; obs_is_outlier, reprojected, point_c,
+ * error, flags may be NULL. */
 #define PBA_OUTLIER_NONE 0u
 #define PBA_OUTLIER_REPROJECTION_HUGE 1u     /* error > huge threshold       (common_types.h:279) */
 #define PBA_OUTLIER_REPROJECTION_NORMAL 2u   /* error > normal threshold     (common_types.h:281) */

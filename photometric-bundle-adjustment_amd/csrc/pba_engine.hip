@@ -140,11 +140,29 @@ __global__ void tile_images_kernel(const uint8_t* __restrict__ src, uint8_t* __r
 //              16-B-per-lane, non-temporal stream.
 // MODE 0: residual part of the records only; 1: full records; 2: per-block cost/validity only.
 // ------------------------------------------------------------------------------------------------
-template <int MODEL, int LPB, int MODE>
+// Store a workgroup's contiguous record slab (LDS → global): 16-B non-temporal stores when the slab is 16-B
+// aligned, 4-B or 2-B stores otherwise (odd patterns in fp16).
+__device__ __forceinline__ void store_slab(const unsigned char* src, unsigned char* dst, int bytes) {
+  if ((((uintptr_t)dst | (unsigned)bytes) & 15) == 0) {
+    const f32x4* s4 = reinterpret_cast<const f32x4*>(src);
+    f32x4* d4 = reinterpret_cast<f32x4*>(dst);
+    for (int i = threadIdx.x; i < (bytes >> 4); i += kBlockThreads) __builtin_nontemporal_store(s4[i], d4 + i);
+  } else if ((((uintptr_t)dst | (unsigned)bytes) & 3) == 0) {
+    const float* s1 = reinterpret_cast<const float*>(src);
+    float* d1 = reinterpret_cast<float*>(dst);
+    for (int i = threadIdx.x; i < (bytes >> 2); i += kBlockThreads) __builtin_nontemporal_store(s1[i], d1 + i);
+  } else {
+    const _Float16* s1 = reinterpret_cast<const _Float16*>(src);
+    _Float16* d1 = reinterpret_cast<_Float16*>(dst);
+    for (int i = threadIdx.x; i < (bytes >> 1); i += kBlockThreads) d1[i] = s1[i];
+  }
+}
+
+template <int MODEL, int LPB, int MODE, class T>
 __global__ __launch_bounds__(kBlockThreads) void photometric_block_kernel(const KernelArgs a) {
   constexpr int BPW = kBlockThreads / LPB;  // blocks per workgroup
   constexpr bool JAC = MODE == 1;
-  constexpr int kStageBytes = JAC ? BPW * 14 * LPB * 4 : 0;
+  constexpr int kStageBytes = JAC ? BPW * 14 * LPB * (int)sizeof(T) : 0;
   constexpr int kTileBytes = BPW * (int)sizeof(TileBlock);
   __shared__ __attribute__((aligned(16))) unsigned char lds[kStageBytes > kTileBytes ? kStageBytes : kTileBytes];
   __shared__ float2 s_pat[LPB];
@@ -157,6 +175,7 @@ __global__ __launch_bounds__(kBlockThreads) void photometric_block_kernel(const 
   const int blk = blk0 + lb;
   const bool live = blk < a.n_blocks;  // a block's LPB lanes agree
   const bool act = live && k < P;
+  T* out = reinterpret_cast<T*>(a.out);  // records in the engine's format (fp32, or fp16 for PBA_RECORD_F16)
 
   if ((int)threadIdx.x < P) s_pat[threadIdx.x] = make_float2(a.pattern[2 * threadIdx.x], a.pattern[2 * threadIdx.x + 1]);
   const int pt = stage_tile<LPB>(a, s_tb, lb, k, blk, live);
@@ -173,39 +192,31 @@ __global__ __launch_bounds__(kBlockThreads) void photometric_block_kernel(const 
   }
   if (MODE == 2) return;
   if (!JAC) {
-    if (act) a.out[(long long)blk * rec_f + k] = ok ? row.r : 0.0f;
+    if (act) out[(long long)blk * rec_f + k] = (T)(ok ? row.r : 0.0f);
     return;
   }
   __syncthreads();  // every lane has read its tile block: the record stage may overwrite it
-  float* stage = reinterpret_cast<float*>(lds);
+  T* stage = reinterpret_cast<T*>(lds);
   // stage the record row of pixel k: r | J_host row | J_target row | J_rho  (zeros for invalid blocks)
   if (act) {
-    float* s_rec = stage + lb * rec_f;
-    float* h = s_rec + P + 6 * k;
-    float* t = s_rec + 7 * P + 6 * k;
+    T* s_rec = stage + lb * rec_f;
+    T* h = s_rec + P + 6 * k;
+    T* t = s_rec + 7 * P + 6 * k;
     if (ok) {
-      s_rec[k] = row.r;
-      h[0] = row.hv.x; h[1] = row.hv.y; h[2] = row.hv.z; h[3] = row.hw.x; h[4] = row.hw.y; h[5] = row.hw.z;
-      t[0] = row.tv.x; t[1] = row.tv.y; t[2] = row.tv.z; t[3] = row.tw.x; t[4] = row.tw.y; t[5] = row.tw.z;
-      s_rec[13 * P + k] = row.jr;
+      s_rec[k] = (T)row.r;
+      h[0] = (T)row.hv.x; h[1] = (T)row.hv.y; h[2] = (T)row.hv.z; h[3] = (T)row.hw.x; h[4] = (T)row.hw.y; h[5] = (T)row.hw.z;
+      t[0] = (T)row.tv.x; t[1] = (T)row.tv.y; t[2] = (T)row.tv.z; t[3] = (T)row.tw.x; t[4] = (T)row.tw.y; t[5] = (T)row.tw.z;
+      s_rec[13 * P + k] = (T)row.jr;
     } else {
-      s_rec[k] = 0.0f;
-      for (int j = 0; j < 6; ++j) h[j] = t[j] = 0.0f;
-      s_rec[13 * P + k] = 0.0f;
+      s_rec[k] = (T)0.0f;
+      for (int j = 0; j < 6; ++j) h[j] = t[j] = (T)0.0f;
+      s_rec[13 * P + k] = (T)0.0f;
     }
   }
   __syncthreads();
   const int nblk = min(BPW, a.n_blocks - blk0);
   if (nblk <= 0) return;
-  const int nf = nblk * rec_f;
-  float* dst = a.out + (long long)blk0 * rec_f;
-  if ((rec_f & 3) == 0) {  // 16-B aligned slab: float4 non-temporal stream
-    const f32x4* src4 = reinterpret_cast<const f32x4*>(stage);
-    f32x4* dst4 = reinterpret_cast<f32x4*>(dst);
-    for (int i = threadIdx.x; i < (nf >> 2); i += kBlockThreads) __builtin_nontemporal_store(src4[i], dst4 + i);
-  } else {
-    for (int i = threadIdx.x; i < nf; i += kBlockThreads) __builtin_nontemporal_store(stage[i], dst + i);
-  }
+  store_slab(lds, reinterpret_cast<unsigned char*>(out + (long long)blk0 * rec_f), nblk * rec_f * (int)sizeof(T));
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -284,10 +295,13 @@ void launch_blocks(pba_engine* e, const KernelArgs& ka, int mode) {
   const int lpb = e->P <= 8 ? 8 : (e->P <= 16 ? 16 : 32);
   const long long lanes = (long long)e->n_blocks * lpb;
   const int grid = (int)((lanes + kBlockThreads - 1) / kBlockThreads);
-#define PBA_LAUNCH_PH(L)                                                                                \
-  if (mode == 1) photometric_block_kernel<MODEL, L, 1><<<grid, kBlockThreads, 0, e->stream>>>(ka);     \
-  else if (mode == 0) photometric_block_kernel<MODEL, L, 0><<<grid, kBlockThreads, 0, e->stream>>>(ka); \
-  else photometric_block_kernel<MODEL, L, 2><<<grid, kBlockThreads, 0, e->stream>>>(ka);
+  const bool h = e->record_format == PBA_RECORD_F16;
+#define PBA_LAUNCH_PH(L)                                                                                             \
+  if (mode == 1 && h) photometric_block_kernel<MODEL, L, 1, _Float16><<<grid, kBlockThreads, 0, e->stream>>>(ka);  \
+  else if (mode == 1) photometric_block_kernel<MODEL, L, 1, float><<<grid, kBlockThreads, 0, e->stream>>>(ka);     \
+  else if (mode == 0 && h) photometric_block_kernel<MODEL, L, 0, _Float16><<<grid, kBlockThreads, 0, e->stream>>>(ka); \
+  else if (mode == 0) photometric_block_kernel<MODEL, L, 0, float><<<grid, kBlockThreads, 0, e->stream>>>(ka);     \
+  else photometric_block_kernel<MODEL, L, 2, float><<<grid, kBlockThreads, 0, e->stream>>>(ka);
   if (lpb == 8) { PBA_LAUNCH_PH(8) }
   else if (lpb == 16) { PBA_LAUNCH_PH(16) }
   else { PBA_LAUNCH_PH(32) }
@@ -420,6 +434,7 @@ int pba_get_stream(pba_engine* e, void** s) {
 int pba_set_cameras(pba_engine* e, int32_t n_cams, const double* intrinsics) {
   if (!e || n_cams <= 0 || !intrinsics) return fail(PBA_ERR_INVALID_ARGUMENT, "bad camera arguments");
   if (int rc = check_device(e)) return rc;
+  reset_pyramid(e);
   std::vector<float> f(8 * (size_t)n_cams);
   for (size_t i = 0; i < f.size(); ++i) f[i] = (float)intrinsics[i];
   for (int c = 0; c < n_cams; ++c)
@@ -454,6 +469,7 @@ static int set_frames_impl(pba_engine* e, int32_t n_frames, const int32_t* frame
   if (photometric && (long long)width * height > (1LL << 31))
     return fail(PBA_ERR_INVALID_ARGUMENT, "image too large");
   if (int rc = check_device(e)) return rc;
+  reset_pyramid(e);
   PBA_HIP(e->frame_cam.resize(n_frames));
   PBA_HIP(hipMemcpyAsync(e->frame_cam.p, frame_cam, n_frames * sizeof(int), hipMemcpyHostToDevice, e->stream));
   if (images) {
@@ -498,6 +514,7 @@ int pba_set_frames_device(pba_engine* e, int32_t n_frames, const int32_t* frame_
 
 int pba_set_pattern(pba_engine* e, int32_t P, const float* offsets) {
   if (!e || P <= 0 || P > PBA_MAX_PATTERN || !offsets) return fail(PBA_ERR_INVALID_ARGUMENT, "bad pattern");
+  reset_pyramid(e);
   e->pattern_h.assign(offsets, offsets + 2 * P);
   e->P = P;
   return PBA_OK;
@@ -508,24 +525,30 @@ int pba_set_points(pba_engine* e, int32_t n_points, const int32_t* host_frame, c
   if (!e || n_points <= 0 || !host_frame || !u_ref) return fail(PBA_ERR_INVALID_ARGUMENT, "bad point arguments");
   if (e->n_frames <= 0) return fail(PBA_ERR_NOT_READY, "pba_set_frames first");
   const bool photometric = e->opt.residual_kind == PBA_RESIDUAL_PHOTOMETRIC;
-  if (photometric && (e->P <= 0 || !host_intensity))
-    return fail(PBA_ERR_INVALID_ARGUMENT, "photometric points need pba_set_pattern and host intensities");
+  if (photometric && e->P <= 0) return fail(PBA_ERR_NOT_READY, "photometric points need pba_set_pattern first");
+  if (photometric && !host_intensity && !e->have_images)
+    return fail(PBA_ERR_NOT_READY, "sampling host intensities needs the frames' images");
   for (int i = 0; i < n_points; ++i)
     if (host_frame[i] < 0 || host_frame[i] >= e->n_frames) return fail(PBA_ERR_INVALID_ARGUMENT, "host frame out of range");
   if (int rc = check_device(e)) return rc;
+  reset_pyramid(e);
   PBA_HIP(e->u_ref.resize(n_points));
   PBA_HIP(hipMemcpyAsync(e->u_ref.p, u_ref, n_points * sizeof(double2), hipMemcpyHostToDevice, e->stream));
   PBA_HIP(e->point_host_d.resize(n_points));
   PBA_HIP(hipMemcpyAsync(e->point_host_d.p, host_frame, n_points * sizeof(int), hipMemcpyHostToDevice, e->stream));
+  PBA_HIP(e->rho.resize(n_points));
+  e->n_points = n_points;
   if (photometric) {
     PBA_HIP(e->host_int.resize((size_t)n_points * e->P));
-    PBA_HIP(hipMemcpyAsync(e->host_int.p, host_intensity, (size_t)n_points * e->P * sizeof(float),
-                           hipMemcpyHostToDevice, e->stream));
+    if (host_intensity) {
+      PBA_HIP(hipMemcpyAsync(e->host_int.p, host_intensity, (size_t)n_points * e->P * sizeof(float),
+                             hipMemcpyHostToDevice, e->stream));
+    } else if (int rc = sample_host_intensities(e, e->u_ref.p, e->host_int.p)) {  // I_h,k from the host image
+      return rc;
+    }
   }
-  PBA_HIP(e->rho.resize(n_points));
   PBA_HIP(hipStreamSynchronize(e->stream));
   e->point_host_h.assign(host_frame, host_frame + n_points);
-  e->n_points = n_points;
   e->state_set = false;
   return PBA_OK;
 }
@@ -686,6 +709,18 @@ int pba_synchronize(pba_engine* e) {
 }
 
 int pba_record_floats(const pba_engine* e) { return e ? 14 * e->R() : 0; }
+
+int pba_set_record_format(pba_engine* e, int32_t format) {
+  if (!e) return fail(PBA_ERR_INVALID_ARGUMENT, "null engine");
+  if (format != PBA_RECORD_F32 && format != PBA_RECORD_F16) return fail(PBA_ERR_INVALID_ARGUMENT, "unknown record format");
+  if (format == PBA_RECORD_F16 && e->opt.residual_kind != PBA_RESIDUAL_PHOTOMETRIC)
+    return fail(PBA_ERR_INVALID_ARGUMENT, "fp16 records are photometric only");
+  e->record_format = format;
+  e->evaluated = false;
+  return PBA_OK;
+}
+
+int pba_record_format(const pba_engine* e) { return e ? e->record_format : PBA_RECORD_F32; }
 int pba_residuals_per_block(const pba_engine* e) { return e ? e->R() : 0; }
 int pba_num_blocks(const pba_engine* e) { return e ? e->n_blocks : 0; }
 int pba_num_points(const pba_engine* e) { return e ? e->n_points : 0; }
@@ -695,10 +730,17 @@ int pba_get_records(pba_engine* e, float* records, uint8_t* valid) {
   if (!e) return fail(PBA_ERR_INVALID_ARGUMENT, "null engine");
   if (!e->evaluated) return fail(PBA_ERR_NOT_READY, "pba_evaluate first");
   if (int rc = check_device(e)) return rc;
-  if (records)
-    PBA_HIP(hipMemcpyAsync(records, e->out.p, (size_t)e->n_blocks * 14 * e->R() * sizeof(float), hipMemcpyDeviceToHost, e->stream));
+  const size_t n = (size_t)e->n_blocks * 14 * e->R();
+  std::vector<_Float16> half;
+  if (records && e->record_format == PBA_RECORD_F16) {
+    half.resize(n);
+    PBA_HIP(hipMemcpyAsync(half.data(), e->out.p, n * sizeof(_Float16), hipMemcpyDeviceToHost, e->stream));
+  } else if (records) {
+    PBA_HIP(hipMemcpyAsync(records, e->out.p, n * sizeof(float), hipMemcpyDeviceToHost, e->stream));
+  }
   if (valid) PBA_HIP(hipMemcpyAsync(valid, e->valid.p, e->n_blocks, hipMemcpyDeviceToHost, e->stream));
   PBA_HIP(hipStreamSynchronize(e->stream));
+  for (size_t i = 0; i < half.size(); ++i) records[i] = (float)half[i];
   return PBA_OK;
 }
 

@@ -329,8 +329,20 @@ struct GnData {
   int red_slots = 0;
 };
 
+// One pyramid level's images, cameras and points (pba_pyramid.hip); level 0 lives in the engine's own fields.
+struct LevelData {
+  DevBuf<uint8_t> images;
+  int width = 0, height = 0;
+  DevBuf<float> intr;
+  DevBuf<double> intr_d;
+  DevBuf<double2> u_ref;
+  DevBuf<float> host_int;
+};
+
 }  // namespace detail
 }  // namespace pba
+
+#include <memory>
 
 struct pba_engine {
   pba_options opt{};
@@ -356,11 +368,14 @@ struct pba_engine {
   pba::detail::DevBuf<double> poses, rho;
   pba::detail::DevBuf<float> out, cost;
   pba::detail::DevBuf<uint8_t> valid;
+  int record_format = PBA_RECORD_F32;
   bool state_set = false;
   bool pairs_fresh = false;          // pairs hold T_th of the current poses (pba_set_state_device forms them)
   bool evaluated = false;
   bool timing = false;
   std::vector<hipEvent_t> ev_pool;   // start/stop pairs, reused
+  int level = 0;                     // active pyramid level (its buffers are swapped into the fields above)
+  std::vector<std::unique_ptr<pba::detail::LevelData>> pyr;  // [1, n_levels); [0] unused
   size_t ev_used = 0;
   pba::detail::GnData gn;
 
@@ -383,6 +398,10 @@ void launch_pairs(pba_engine* e, const double* poses, PairRec* pairs);
 
 // Residual-only evaluation writing only per-block costs/validity (state given by pairs/rho).
 int launch_cost_only(pba_engine* e, const PairRec* pairs, const double* rho);
+
+// Pyramid (pba_pyramid.hip): back to level 0 and drop the levels; I_h,k sampled from the active level's host images.
+void reset_pyramid(pba_engine* e);
+int sample_host_intensities(pba_engine* e, const double2* u_ref, float* out);
 
 }  // namespace detail
 }  // namespace pba

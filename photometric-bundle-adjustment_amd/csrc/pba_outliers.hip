@@ -100,6 +100,7 @@ int pba_compute_projections(pba_engine* e, int32_t n_obs, const int32_t* obs_poi
   if (!e || n_obs < 0 || (n_obs > 0 && (!obs_point || !obs_frame || !obs_uv)))
     return fail(PBA_ERR_INVALID_ARGUMENT, "bad observation arguments");
   if (!e->state_set || e->n_points <= 0 || e->n_frames <= 0) return fail(PBA_ERR_NOT_READY, "problem/state not set");
+  if (e->level != 0) return fail(PBA_ERR_NOT_READY, "projections are computed at pyramid level 0 (pba_set_level)");
   if (n_obs == 0) return PBA_OK;
   for (int i = 0; i < n_obs; ++i)
     if (obs_point[i] < 0 || obs_point[i] >= e->n_points || obs_frame[i] < 0 || obs_frame[i] >= e->n_frames)

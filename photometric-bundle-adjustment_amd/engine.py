@@ -35,6 +35,7 @@ class OutlierThresholds(C.Structure):
 
 
 OUTLIER_HUGE, OUTLIER_NORMAL, OUTLIER_DISTANCE, OUTLIER_Z = 1, 2, 4, 8
+RECORD_F32, RECORD_F16 = 0, 1
 
 
 class MapInfo(C.Structure):
@@ -132,6 +133,14 @@ def lib():
                                    C.POINTER(SolverSummary)], C.c_int),
         "pba_compute_projections": ([vp, i32, vp, vp, vp, vp, C.POINTER(OutlierThresholds), vp, vp, vp, vp], C.c_int),
         "pba_outlier_landmarks": ([i32, i32, vp, vp, vp, vp, vp, vp], C.c_int),
+        "pba_set_record_format": ([vp, i32], C.c_int),
+        "pba_record_format": ([vp], C.c_int),
+        "pba_build_pyramid": ([vp, i32], C.c_int),
+        "pba_num_levels": ([vp], C.c_int),
+        "pba_set_level": ([vp, i32], C.c_int),
+        "pba_get_level": ([vp, C.POINTER(i32), C.POINTER(i32), C.POINTER(i32)], C.c_int),
+        "pba_get_host_intensities": ([vp, vp], C.c_int),
+        "pba_solve_pyramid": ([vp, C.POINTER(SolverOptions), C.POINTER(SolverSummary)], C.c_int),
         "pba_map_load": ([C.c_char_p, C.c_char_p, C.POINTER(vp)], C.c_int),
         "pba_map_destroy": ([vp], C.c_int),
         "pba_map_get_info": ([vp, C.POINTER(MapInfo)], C.c_int),
@@ -193,7 +202,7 @@ class Engine:
             _check(L.pba_set_pattern(h, pat.shape[0], _p(pat)), "pba_set_pattern")
         ph = np.ascontiguousarray(pb.point_host, np.int32)
         ur = np.ascontiguousarray(pb.u_ref, np.float64)
-        hi = None if pb.kind != 0 else np.ascontiguousarray(pb.host_intensity, np.float32)
+        hi = None if (pb.kind != 0 or pb.host_intensity is None) else np.ascontiguousarray(pb.host_intensity, np.float32)
         _check(L.pba_set_points(h, ph.shape[0], _p(ph), _p(ur), _p(hi)), "pba_set_points")
         bp = np.ascontiguousarray(pb.block_point, np.int32)
         bt = np.ascontiguousarray(pb.block_target, np.int32)
@@ -238,6 +247,10 @@ class Engine:
                                                _p(out["point_c"]), _p(out["error"]), _p(out["flags"])),
                "pba_compute_projections")
         return out
+
+    def set_record_format(self, fmt: int):
+        """RECORD_F32 (default) or RECORD_F16 (records stored as IEEE halves; records() still returns floats)."""
+        _check(self._L.pba_set_record_format(self._h, fmt), "pba_set_record_format")
 
     def records(self):
         rec = np.empty((self.n_blocks, self.record), np.float32)
@@ -306,6 +319,32 @@ class Engine:
                           min_relative_decrease)
         s = SolverSummary()
         _check(self._L.pba_solve(self._h, C.byref(o), C.byref(s)), "pba_solve")
+        return s.as_dict()
+
+    # -- image pyramid / coarse-to-fine (pba_pyramid.hip) ---------------------------------------------
+    def build_pyramid(self, n_levels: int):
+        _check(self._L.pba_build_pyramid(self._h, n_levels), "pba_build_pyramid")
+
+    def set_level(self, level: int):
+        _check(self._L.pba_set_level(self._h, level), "pba_set_level")
+
+    def level(self):
+        """(active level, its width, its height)"""
+        l, w, h = C.c_int32(), C.c_int32(), C.c_int32()
+        _check(self._L.pba_get_level(self._h, C.byref(l), C.byref(w), C.byref(h)), "pba_get_level")
+        return l.value, w.value, h.value
+
+    def host_intensities(self) -> np.ndarray:
+        out = np.zeros((self.n_points, self._L.pba_residuals_per_block(self._h)), np.float32)
+        _check(self._L.pba_get_host_intensities(self._h, _p(out)), "pba_get_host_intensities")
+        return out
+
+    def solve_pyramid(self, max_iterations=20, initial_trust_region_radius=1e4, function_tolerance=1e-6,
+                      min_relative_decrease=1e-3) -> dict:
+        o = SolverOptions(max_iterations, 0, initial_trust_region_radius, function_tolerance, 1e-8,
+                          min_relative_decrease)
+        s = SolverSummary()
+        _check(self._L.pba_solve_pyramid(self._h, C.byref(o), C.byref(s)), "pba_solve_pyramid")
         return s.as_dict()
 
     # -- multi-GPU Gauss-Newton (include/pba.h §8e; host driver in distributed.py) ------------------

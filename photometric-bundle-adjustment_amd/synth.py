@@ -355,3 +355,37 @@ def make_problem(n_frames: int = 8, n_points: int = 64, K: int = 4, width: int =
                    images=images, pattern=pat, point_host=point_host, u_ref=u_ref, host_intensity=host_int,
                    block_point=block_point, block_target=block_target, u_obs=u_obs, poses=poses, rho=rho,
                    poses_gt=poses_gt, rho_gt=rho_gt)
+
+
+# ------------------------------------------------------------------------------------------------
+# Image pyramid (DSO convention, csrc/pba_pyramid.hip) — numpy restatement for tests.
+# ------------------------------------------------------------------------------------------------
+def downsample(images: np.ndarray) -> np.ndarray:
+    """u8 (n, H, W) → (n, ⌊H/2⌋, ⌊W/2⌋), round(mean of each 2×2 block)."""
+    n, H, W = images.shape
+    h, w = H // 2, W // 2
+    a = images[:, :2 * h, :2 * w].astype(np.uint32).reshape(n, h, 2, w, 2)
+    return ((a.sum(axis=(2, 4)) + 2) >> 2).astype(np.uint8)
+
+
+def level_problem(pb: "Problem", level: int, host_intensity: Optional[np.ndarray] = None) -> "Problem":
+    """The problem the engine solves at pyramid `level`: images downsampled `level` times, cameras and u_ref
+    scaled (c_l = (c + 0.5)/2^l − 0.5), I_h,k re-sampled (double bilinear) unless given."""
+    s = 0.5 ** level
+    imgs = pb.images
+    for _ in range(level):
+        imgs = downsample(imgs)
+    k = pb.intrinsics.copy()
+    k[:, 0] *= s
+    k[:, 1] *= s
+    k[:, 2] = (k[:, 2] + 0.5) * s - 0.5
+    k[:, 3] = (k[:, 3] + 0.5) * s - 0.5
+    ur = (pb.u_ref + 0.5) * s - 0.5
+    if host_intensity is None:
+        host_intensity = np.empty((pb.n_points, pb.pattern.shape[0]), np.float32)
+        for f in np.unique(pb.point_host):
+            sel = np.nonzero(pb.point_host == f)[0]
+            host_intensity[sel] = bilinear(imgs[f], ur[sel, None, 0] + pb.pattern[None, :, 0],
+                                           ur[sel, None, 1] + pb.pattern[None, :, 1]).astype(np.float32)
+    return dataclasses.replace(pb, width=imgs.shape[2], height=imgs.shape[1], images=imgs, intrinsics=k, u_ref=ur,
+                               host_intensity=host_intensity)
