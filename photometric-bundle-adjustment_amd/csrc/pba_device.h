@@ -231,29 +231,36 @@ __device__ __forceinline__ void project_jac(const S* k, const V3<S>& p, S iden, 
 // Keyframe images live in HBM as 16×8-texel tiles of 128 B (one L2 line): tile (x>>4, y>>3) at
 // ((y>>3)·tiles_x + (x>>4))·128, texel (x&15) + 16·(y&7) inside.  A warped 8-pixel pattern plus its bilinear
 // taps covers ≈6×6 texels, which touches ≈2.1 tiles against ≈6.3 lines in row-major order (DESIGN.md
-// has the measured FETCH_SIZE per block before and after).
-constexpr int kTileW = 16, kTileH = 8, kTileBytes = kTileW * kTileH;
-__host__ __device__ __forceinline__ int tiles_x_of(int W) { return (W + kTileW - 1) / kTileW; }
+// has the measured FETCH_SIZE per block before and after).  Every frame carries a kImgPad-texel apron that
+// replicates its edge pixels (Grid2D's clamp, cubic_interpolation.h:403-414), so the four taps of any position
+// inside the interpolation clamp [−2, W+1] are plain in-bounds reads: no per-tap clamping.
+constexpr int kTileW = 16, kTileH = 8, kTileBytes = kTileW * kTileH, kImgPad = 4;
+__host__ __device__ __forceinline__ int tiles_x_of(int W) { return (W + 2 * kImgPad + kTileW - 1) / kTileW; }
 __host__ __device__ __forceinline__ long long tiled_frame_bytes(int W, int H) {
-  return (long long)tiles_x_of(W) * ((H + kTileH - 1) / kTileH) * kTileBytes;
+  return (long long)tiles_x_of(W) * ((H + 2 * kImgPad + kTileH - 1) / kTileH) * kTileBytes;
 }
-__device__ __forceinline__ int texel_index(int x, int y, int tiles_x) {
-  return ((((y >> 3) * tiles_x + (x >> 4)) << 7) | ((y & 7) << 4) | (x & 15));
+// byte offset of padded texel (xp, yp) = image pixel (xp − kImgPad, yp − kImgPad)
+__host__ __device__ __forceinline__ unsigned texel_index(int xp, int yp, int tiles_x) {
+  return (((unsigned)((yp >> 3) * tiles_x + (xp >> 4))) << 7) | ((unsigned)(yp & 7) << 4) | (unsigned)(xp & 15);
+}
+__host__ __device__ __forceinline__ unsigned texel_index_img(int x, int y, int tiles_x) {
+  return texel_index(x + kImgPad, y + kImgPad, tiles_x);
 }
 
-// Bilinear interpolation of a tiled u8 image with Grid2D-style edge clamp; value and gradient from the same
-// four taps.  u = column, v = row, positions in fp64, weights in fp32.
+// Bilinear interpolation of a tiled u8 image with Grid2D-style edge clamp (the apron); value and gradient from
+// the same four taps.  u = column, v = row, positions in fp64, value weights in fp32.
 __device__ __forceinline__ void bilinear(const uint8_t* __restrict__ img, int W, int H, int tiles_x, double u,
                                          double v, float& I, float& gx, float& gy) {
   u = fmin(fmax(u, -2.0), (double)W + 1.0);
   v = fmin(fmax(v, -2.0), (double)H + 1.0);
   const double xf = floor(u), yf = floor(v);
   const float a = (float)(u - xf), b = (float)(v - yf);
-  const int x0 = (int)xf, y0 = (int)yf;
-  const int xa = min(max(x0, 0), W - 1), xb = min(max(x0 + 1, 0), W - 1);
-  const int ya = min(max(y0, 0), H - 1), yb = min(max(y0 + 1, 0), H - 1);
-  const float I00 = img[texel_index(xa, ya, tiles_x)], I10 = img[texel_index(xb, ya, tiles_x)];
-  const float I01 = img[texel_index(xa, yb, tiles_x)], I11 = img[texel_index(xb, yb, tiles_x)];
+  const int xp = (int)xf + kImgPad, yp = (int)yf + kImgPad;  // ∈ [2, W+5] × [2, H+5]
+  const unsigned i00 = texel_index(xp, yp, tiles_x);
+  const unsigned dx = (xp & 15) == 15 ? (unsigned)(kTileBytes - 15) : 1u;                 // next column
+  const unsigned dy = (yp & 7) == 7 ? (unsigned)(tiles_x * kTileBytes - 7 * kTileW) : 16u;  // next row
+  const float I00 = img[i00], I10 = img[i00 + dx];
+  const float I01 = img[i00 + dy], I11 = img[i00 + dy + dx];
   const float top = I00 + a * (I10 - I00);
   const float bot = I01 + a * (I11 - I01);
   I = top + b * (bot - top);

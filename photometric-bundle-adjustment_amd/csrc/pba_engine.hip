@@ -110,8 +110,8 @@ __global__ void state_kernel(const double* __restrict__ src_poses, const double*
 }
 
 // ------------------------------------------------------------------------------------------------
-// Image relayout: row-major u8 frames → 16×8 tiles (pba_device.h).  One lane per 16-texel tile row; pad
-// texels (x ≥ W or y ≥ H) are zero and never read (taps are clamped to the image).
+// Image relayout: row-major u8 frames → 16×8 tiles with the edge-replicating apron (pba_device.h).  One lane per
+// 16-texel tile row of the padded frame; texels beyond the padded frame are zero and never read.
 // ------------------------------------------------------------------------------------------------
 __global__ void tile_images_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst, int W, int H,
                                    int tiles_x, int tiles_y, long long n_rows) {
@@ -124,36 +124,36 @@ __global__ void tile_images_kernel(const uint8_t* __restrict__ src, uint8_t* __r
   const long long f = tile / tiles_per_frame;
   const int t = (int)(tile - f * tiles_per_frame);
   const int ty = t / tiles_x, tx = t - ty * tiles_x;
-  const int y = ty * kTileH + r, x0 = tx * kTileW;
+  const int yp = ty * kTileH + r, xp0 = tx * kTileW;
+  const int y = min(max(yp - kImgPad, 0), H - 1);
   union { uint8_t b[16]; uint4 v; } row;
   const uint8_t* s = src + f * W * (long long)H + (long long)y * W;
+  const bool yin = yp < H + 2 * kImgPad;
 #pragma unroll
-  for (int j = 0; j < 16; ++j) row.b[j] = (y < H && x0 + j < W) ? s[x0 + j] : (uint8_t)0;
+  for (int j = 0; j < 16; ++j) {
+    const int xp = xp0 + j;
+    row.b[j] = (yin && xp < W + 2 * kImgPad) ? s[min(max(xp - kImgPad, 0), W - 1)] : (uint8_t)0;
+  }
   reinterpret_cast<uint4*>(dst)[i] = row.v;
 }
 
-// ------------------------------------------------------------------------------------------------
-// Photometric block kernel: lane = (block, pixel k); a workgroup = a tile of 256/LPB consecutive blocks.
-//   prologue   the tile's pair records + points are staged in LDS (stage_tile), the pattern too;
-//   rows       every lane evaluates its row from LDS (broadcast reads) + its four image taps;
-//   records    staged in LDS (aliasing the tile, after a barrier) and stored as one contiguous,
-//              16-B-per-lane, non-temporal stream.
-// MODE 0: residual part of the records only; 1: full records; 2: per-block cost/validity only.
-// ------------------------------------------------------------------------------------------------
 // Store a workgroup's contiguous record slab (LDS → global): 16-B non-temporal stores when the slab is 16-B
 // aligned, 4-B or 2-B stores otherwise (odd patterns in fp16).
+template <class T>
 __device__ __forceinline__ void store_slab(const unsigned char* src, unsigned char* dst, int bytes) {
   if ((((uintptr_t)dst | (unsigned)bytes) & 15) == 0) {
     const f32x4* s4 = reinterpret_cast<const f32x4*>(src);
     f32x4* d4 = reinterpret_cast<f32x4*>(dst);
     for (int i = threadIdx.x; i < (bytes >> 4); i += kBlockThreads) __builtin_nontemporal_store(s4[i], d4 + i);
-  } else if ((((uintptr_t)dst | (unsigned)bytes) & 3) == 0) {
+  } else if (sizeof(T) == 4 || (((uintptr_t)dst | (unsigned)bytes) & 3) == 0) {
     const float* s1 = reinterpret_cast<const float*>(src);
     float* d1 = reinterpret_cast<float*>(dst);
+#pragma unroll 1
     for (int i = threadIdx.x; i < (bytes >> 2); i += kBlockThreads) __builtin_nontemporal_store(s1[i], d1 + i);
   } else {
     const _Float16* s1 = reinterpret_cast<const _Float16*>(src);
     _Float16* d1 = reinterpret_cast<_Float16*>(dst);
+#pragma unroll 1
     for (int i = threadIdx.x; i < (bytes >> 1); i += kBlockThreads) d1[i] = s1[i];
   }
 }
@@ -216,7 +216,7 @@ __global__ __launch_bounds__(kBlockThreads) void photometric_block_kernel(const 
   __syncthreads();
   const int nblk = min(BPW, a.n_blocks - blk0);
   if (nblk <= 0) return;
-  store_slab(lds, reinterpret_cast<unsigned char*>(out + (long long)blk0 * rec_f), nblk * rec_f * (int)sizeof(T));
+  store_slab<T>(lds, reinterpret_cast<unsigned char*>(out + (long long)blk0 * rec_f), nblk * rec_f * (int)sizeof(T));
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -476,7 +476,7 @@ static int set_frames_impl(pba_engine* e, int32_t n_frames, const int32_t* frame
     // frames arrive row-major (the reference's cv::Mat / pangolin image rows) and are re-tiled once on the
     // device; host input is staged through a transient device buffer.
     const size_t bytes = (size_t)n_frames * width * height;
-    const int tx = tiles_x_of(width), ty = (height + kTileH - 1) / kTileH;
+    const int tx = tiles_x_of(width), ty = (height + 2 * kImgPad + kTileH - 1) / kTileH;
     PBA_HIP(e->images.resize((size_t)n_frames * tiled_frame_bytes(width, height)));
     const uint8_t* src = images;
     DevBuf<uint8_t> staging;

@@ -195,43 +195,50 @@ __global__ __launch_bounds__(kBlockThreads) void linearize_kernel(const KernelAr
     a.cost[blk] = ok ? huber_cost(s, a.huber) : 0.0f;
   }
   // weighted row x̃ = √w · x  → products carry w (Ceres Corrector with ρ'' ≤ 0: J̃ = √ρ' J, r̃ = √ρ' r)
-  const float sw = (act && ok) ? sqrtf(w) : 0.0f;
+  const float sw = (act && ok) ? sqrtf(w) : 0.0f;  // rows outside the domain / of dead lanes are all zero
+  auto wx = [&](float x) { return sw * x; };
   float* sX = reinterpret_cast<float*>(arena[wave]);  // the wave's 64 rows × 16 floats (overwrites its tile blocks)
   {
     float4* xr = reinterpret_cast<float4*>(sX + lane * 16);
-    xr[0] = make_float4(sw * row.hv.x, sw * row.hv.y, sw * row.hv.z, sw * row.hw.x);
-    xr[1] = make_float4(sw * row.hw.y, sw * row.hw.z, sw * row.tv.x, sw * row.tv.y);
-    xr[2] = make_float4(sw * row.tv.z, sw * row.tw.x, sw * row.tw.y, sw * row.tw.z);
-    xr[3] = make_float4(sw * row.jr, sw * row.r, 0.0f, 0.0f);
+    xr[0] = make_float4(wx(row.hv.x), wx(row.hv.y), wx(row.hv.z), wx(row.hw.x));
+    xr[1] = make_float4(wx(row.hw.y), wx(row.hw.z), wx(row.tv.x), wx(row.tv.y));
+    xr[2] = make_float4(wx(row.tv.z), wx(row.tw.x), wx(row.tw.y), wx(row.tw.z));
+    xr[3] = make_float4(wx(row.jr), wx(row.r), 0.0f, 0.0f);
   }
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   {
+    // block by block: LPB/4 MFMAs, then the scatter of the 104 products (one accumulator at a time keeps the
+    // MFMA registers, and their occupancy cost, at four).  With NVP ≤ 16·LPB floats a block's products land below
+    // the rows of every later block, so each block's operands are read just before its MFMAs; otherwise (LPB = 4)
+    // every operand is read first.
+    constexpr bool kInterleave = NVP <= 16 * LPB;
     const int ci = lane & 15, kq = lane >> 4;
-    float op[BW][LPB / 4];
-#pragma unroll
-    for (int b = 0; b < BW; ++b)
-#pragma unroll
-      for (int st = 0; st < LPB / 4; ++st) op[b][st] = sX[(b * LPB + 4 * st + kq) * 16 + ci];
-    f32x4 acc[BW];
-#pragma unroll
-    for (int b = 0; b < BW; ++b) {
-      acc[b] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-#pragma unroll
-      for (int st = 0; st < LPB / 4; ++st) acc[b] = __builtin_amdgcn_mfma_f32_16x16x4f32(op[b][st], op[b][st], acc[b], 0, 0, 0);
-    }
-    // the products of the wave's blocks, 104 slots each (overwrites the rows: every operand read above precedes
-    // these stores in the wave's LDS order)
     float* sP = reinterpret_cast<float*>(arena[wave]);
     const unsigned slots = kSlotTable.w[lane];
+    float opa[kInterleave ? 1 : BW][LPB / 4];
+    if constexpr (!kInterleave) {
 #pragma unroll
-    for (int b = 0; b < BW; ++b)
+      for (int b = 0; b < BW; ++b)
+#pragma unroll
+        for (int st = 0; st < LPB / 4; ++st) opa[b][st] = sX[(b * LPB + 4 * st + kq) * 16 + ci];
+    }
+#pragma unroll
+    for (int b = 0; b < BW; ++b) {
+      float op[LPB / 4];
+#pragma unroll
+      for (int st = 0; st < LPB / 4; ++st)
+        op[st] = kInterleave ? sX[(b * LPB + 4 * st + kq) * 16 + ci] : opa[kInterleave ? 0 : b][st];
+      f32x4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+      for (int st = 0; st < LPB / 4; ++st) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(op[st], op[st], acc, 0, 0, 0);
 #pragma unroll
       for (int m = 0; m < 4; ++m) {
         const unsigned v = (slots >> (8 * m)) & 255u;
-        if (v < (unsigned)NV) sP[b * NVP + v] = acc[b][m];
+        if (v < (unsigned)NV) sP[b * NVP + v] = acc[m];
       }
+    }
   }
   __syncthreads();
   auto sblk = [&](int b, int v) -> float {  // product v of workgroup block b

@@ -77,7 +77,7 @@ __device__ __forceinline__ int logical_tile() {
 // for Huber, so Ceres scales r and J by √ρ' and the normal equations by ρ').
 __device__ __forceinline__ float huber_cost(float s, float a) {
   if (a <= 0.0f || s <= a * a) return 0.5f * s;
-  return 0.5f * (2.0f * a * sqrtf(s) - a * a);
+  return 0.5f * (2.0f * a * __builtin_amdgcn_sqrtf(s) - a * a);  // v_sqrt_f32 (1 ulp)
 }
 __device__ __forceinline__ float huber_weight(float s, float a) {
   if (a <= 0.0f || s <= a * a) return 1.0f;
@@ -130,8 +130,8 @@ struct Row {
 // loading the 256-B record and the point data itself.  Returns the block's point.  The caller barriers.
 template <int LPB>
 __device__ __forceinline__ int stage_tile(const KernelArgs& a, TileBlock* s_tb, int lb, int k, int blk, bool live) {
-  if (!live) return 0;
-  const int2 pp = a.block_pp[blk];
+  // a dead block (past the end of the problem) stages the last block, so every lane evaluates valid data
+  const int2 pp = a.block_pp[live ? blk : a.n_blocks - 1];
   const uint4* src = reinterpret_cast<const uint4*>(a.pairs + pp.y);
   uint4* dst = reinterpret_cast<uint4*>(s_tb + lb);
 #pragma unroll

@@ -22,7 +22,7 @@ using namespace pba::detail;
 
 namespace {
 
-// One lane per byte of the level-(l+1) tiled frames (pad texels zero).
+// One lane per byte of the level-(l+1) tiled frames, apron included (edge replicated); pad texels zero.
 __global__ void downsample_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst, int Ws, int Hs, int W,
                                   int H, long long frame_in, long long frame_out, long long n) {
   const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -32,13 +32,14 @@ __global__ void downsample_kernel(const uint8_t* __restrict__ src, uint8_t* __re
   const int tiles_x = tiles_x_of(W), tiles_xs = tiles_x_of(Ws);
   const int tile = o >> 7, in = o & 127;
   const int ty = tile / tiles_x, tx = tile - ty * tiles_x;
-  const int x = tx * kTileW + (in & 15), y = ty * kTileH + (in >> 4);
+  const int xp = tx * kTileW + (in & 15), yp = ty * kTileH + (in >> 4);
   uint8_t v = 0;
-  if (x < W && y < H) {
+  if (xp < W + 2 * kImgPad && yp < H + 2 * kImgPad) {
+    const int x = min(max(xp - kImgPad, 0), W - 1), y = min(max(yp - kImgPad, 0), H - 1);
     const uint8_t* s = src + f * frame_in;
     const int x0 = 2 * x, y0 = 2 * y;  // 2x+1 ≤ Ws−1 and 2y+1 ≤ Hs−1 because W = ⌊Ws/2⌋, H = ⌊Hs/2⌋
-    const unsigned sum = (unsigned)s[texel_index(x0, y0, tiles_xs)] + s[texel_index(x0 + 1, y0, tiles_xs)] +
-                         s[texel_index(x0, y0 + 1, tiles_xs)] + s[texel_index(x0 + 1, y0 + 1, tiles_xs)];
+    const unsigned sum = (unsigned)s[texel_index_img(x0, y0, tiles_xs)] + s[texel_index_img(x0 + 1, y0, tiles_xs)] +
+                         s[texel_index_img(x0, y0 + 1, tiles_xs)] + s[texel_index_img(x0 + 1, y0 + 1, tiles_xs)];
     v = (uint8_t)((sum + 2u) >> 2);
   }
   dst[i] = v;
