@@ -975,16 +975,14 @@ __global__ __launch_bounds__(256) void cr_build_kernel(const double* __restrict_
 template <int M>
 constexpr int kCrOddThreads = ((3 * M + 1) + 63) / 64 * 64;  // one lane per column of [D | RHS], whole waves
 
+// The elimination of one super-row by kCrOddThreads<M> lanes (tid = lane index within that group, c = its
+// column); colk = the group's own publish buffers.  Every lane of the workgroup must call it (barriers).
+// Returns false when a pivot block was not positive definite; a[] = column c of [D⁻¹ | D⁻¹RHS].
 template <int M>
-__global__ __launch_bounds__(kCrOddThreads<M>) void cr_odd_kernel(CrLevel L, int root, int* status) {
+__device__ __forceinline__ bool gj_row(const CrLevel& L, int j, bool root, int tid, double (*colk)[2][M], double* a) {
   constexpr int NC = 2 * M + 1, W = M + NC;
-  static_assert(W <= 256, "one lane per column");
-  __shared__ __attribute__((aligned(16))) double colk[2][2][M];
-  const int tid = threadIdx.x;
-  const int j = root ? 0 : 2 * blockIdx.x + 1;
   const int c = min(tid, W - 1);
   const double* D = L.D + (long long)j * M * M;
-  double a[M];
 #pragma unroll
   for (int r = 0; r < M; ++r) {  // all of a lane's loads in flight at once
     const double* src;
@@ -995,9 +993,6 @@ __global__ __launch_bounds__(kCrOddThreads<M>) void cr_odd_kernel(CrLevel L, int
     a[r] = src ? *src : 0.0;
   }
   bool bad = false;
-  // Step k eliminates the pivot pair (k, k+1): its two owner lanes publish their columns, every lane forms the
-  // 2×2 pivot block P (SPD: P00 > 0, det P > 0), its entries of the normalised pivot rows [t0 t1]ᵀ = P⁻¹[a_k a_k+1]ᵀ
-  // and the rank-2 update — M/2 barriers instead of M.
   auto step = [&](int k) {
     const int buf = (k >> 1) & 1;
     if (tid == k || tid == k + 1) {
@@ -1011,10 +1006,10 @@ __global__ __launch_bounds__(kCrOddThreads<M>) void cr_odd_kernel(CrLevel L, int
     const double p00 = c0[k], p10 = c0[k + 1], p01 = c1[k], p11 = c1[k + 1];
     const double det = p00 * p11 - p01 * p10;
     bad |= !(p00 > 0.0 && det > 0.0);
-    const double rd = rcp_nr(det);  // same value in every lane
+    const double rd = rcp_nr(det);
     double ak = a[0], ak1 = a[1];
 #pragma unroll
-    for (int r = 1; r < M; ++r) ak = r == k ? a[r] : ak;  // static register indices even when k is not
+    for (int r = 1; r < M; ++r) ak = r == k ? a[r] : ak;
 #pragma unroll
     for (int r = 2; r < M; ++r) ak1 = r == k + 1 ? a[r] : ak1;
     const double t0 = (p11 * ak - p01 * ak1) * rd;
@@ -1029,67 +1024,51 @@ __global__ __launch_bounds__(kCrOddThreads<M>) void cr_odd_kernel(CrLevel L, int
 #pragma unroll 1
     for (int k = 0; k < M; k += 2) step(k);
   }
-  if (bad) {  // uniform: every lane saw the same pivots
-    if (tid == 0) atomicOr(status, 1);
-    return;
-  }
-  if (root) {
-    if (tid == W - 1)
-#pragma unroll
-      for (int r = 0; r < M; ++r) L.x[r] = a[r];
-    return;
-  }
-  if (tid >= M && tid < W) {
-    double* X = L.X + (long long)(j / 2) * M * NC + (c - M);
-#pragma unroll
-    for (int r = 0; r < M; ++r) X[r * NC] = a[r];
-  }
+  return !bad;
 }
 
-// Rebuild even super-row i of level L as row i/2 of level L+1; both neighbours' X and the couplings are
-// staged in LDS first (the products are M-long dot products over them).
+// One level of cyclic reduction in ONE launch: workgroup i/2 rebuilds even super-row i.  Its two halves
+// eliminate the neighbouring odd rows i−1 and i+1 side by side (gj_row, redundantly with the neighbouring
+// workgroups — each odd row is done twice, saving a launch and an HBM round trip of X per level), keep both X in
+// LDS, store X_{i+1} for the back-substitution (every odd row is the right neighbour of exactly one even row),
+// then form D'_i = D_i − U_{i−1}ᵀX^U_{i−1} − U_i X^L_{i+1}, U'_i = −U_i X^U_{i+1} and b'_i likewise.
 template <int M>
-__global__ __launch_bounds__(256) void cr_even_kernel(CrLevel L, CrLevel Ln) {
-  constexpr int NC = 2 * M + 1;
+constexpr size_t cr_level_lds() { return sizeof(double) * (2 * M * M + 2 * M * (2 * M + 1)); }
+
+template <int M>
+__global__ __launch_bounds__(2 * kCrOddThreads<M>) void cr_level_kernel(CrLevel L, CrLevel Ln, int* status) {
+  constexpr int NC = 2 * M + 1, W = M + NC, T = kCrOddThreads<M>;
+  __shared__ __attribute__((aligned(16))) double colk[2][2][2][M];
   extern __shared__ double smem[];
   double* sUl = smem;               // U_{i−1}   M×M
   double* sUi = sUl + M * M;        // U_i       M×M
-  double* sXl = sUi + M * M;        // X_{i−1}   M×NC
-  double* sXr = sXl + M * NC;       // X_{i+1}   M×NC
+  double* sX[2] = {sUi + M * M, sUi + M * M + M * NC};  // X_{i−1}, X_{i+1}   M×NC each
   const int i = 2 * blockIdx.x, in = blockIdx.x;
-  const bool left = i - 1 >= 0, right = i + 1 < L.n;
-  const double* Ul = left ? L.U + (long long)(i - 1) * M * M : nullptr;
-  const double* Ui = L.U + (long long)i * M * M;
-  const double* Xl = left ? L.X + (long long)((i - 1) / 2) * M * NC : nullptr;
-  const double* Xr = right ? L.X + (long long)((i + 1) / 2) * M * NC : nullptr;
-  {
-    constexpr int NU = (M * M + 255) / 256, NX = (M * NC + 255) / 256;
-    double a0[NU], a1[NU], x0[NX], x1[NX];
+  const int half = threadIdx.x >= T ? 1 : 0, tl = threadIdx.x - half * T;
+  const int j = half ? i + 1 : i - 1;
+  const bool has = j >= 0 && j < L.n;
+  double a[M];
+  const bool ok = gj_row<M>(L, has ? j : 1, false, tl, colk[half], a);
+  if (!ok && has && tl == 0) atomicOr(status, 1);
+  if (tl >= M && tl < W) {
+    double* x = sX[half] + (tl - M);
 #pragma unroll
-    for (int u = 0; u < NU; ++u) {
-      const int e = min((int)threadIdx.x + 256 * u, M * M - 1);
-      a0[u] = left ? Ul[e] : 0.0;
-      a1[u] = Ui[e];
-    }
+    for (int r = 0; r < M; ++r) x[r * NC] = has ? a[r] : 0.0;
+    if (half && has) {
+      double* X = L.X + (long long)(j / 2) * M * NC + (tl - M);
 #pragma unroll
-    for (int u = 0; u < NX; ++u) {
-      const int e = min((int)threadIdx.x + 256 * u, M * NC - 1);
-      x0[u] = left ? Xl[e] : 0.0;
-      x1[u] = right ? Xr[e] : 0.0;
-    }
-#pragma unroll
-    for (int u = 0; u < NU; ++u) {
-      const int e = threadIdx.x + 256 * u;
-      if (e < M * M) { sUl[e] = a0[u]; sUi[e] = a1[u]; }
-    }
-#pragma unroll
-    for (int u = 0; u < NX; ++u) {
-      const int e = threadIdx.x + 256 * u;
-      if (e < M * NC) { sXl[e] = x0[u]; sXr[e] = x1[u]; }
+      for (int r = 0; r < M; ++r) X[r * NC] = a[r];
     }
   }
+  const bool left = i - 1 >= 0, right = i + 1 < L.n;
+  for (int e = threadIdx.x; e < M * M; e += 2 * T) {
+    sUl[e] = left ? L.U[(long long)(i - 1) * M * M + e] : 0.0;
+    sUi[e] = L.U[(long long)i * M * M + e];
+  }
   __syncthreads();
-  for (int e = threadIdx.x; e < 2 * M * M + M; e += 256) {
+  const double* sXl = sX[0];
+  const double* sXr = sX[1];
+  for (int e = threadIdx.x; e < 2 * M * M + M; e += 2 * T) {
     if (e < M * M) {  // D' = D − U_{i−1}ᵀ X^U_{i−1} − U_i X^L_{i+1}
       const int r = e / M, c = e % M;
       double v = L.D[(long long)i * M * M + e];
@@ -1101,7 +1080,7 @@ __global__ __launch_bounds__(256) void cr_even_kernel(CrLevel L, CrLevel Ln) {
       double v = 0.0;
 #pragma unroll 8
       for (int q = 0; q < M; ++q) v -= sUi[r * M + q] * sXr[q * NC + M + c];
-      Ln.U[(long long)in * M * M + f] = v;
+      Ln.U[(long long)in * M * M + f] = right ? v : 0.0;
     } else {  // b'
       const int r = e - 2 * M * M;
       double v = L.b[(long long)i * M + r];
@@ -1110,6 +1089,22 @@ __global__ __launch_bounds__(256) void cr_even_kernel(CrLevel L, CrLevel Ln) {
       Ln.b[(long long)in * M + r] = v;
     }
   }
+}
+
+// The root super-row (the last level): x = D⁻¹ b.
+template <int M>
+__global__ __launch_bounds__(kCrOddThreads<M>) void cr_root_kernel(CrLevel L, int* status) {
+  constexpr int W = 3 * M + 1;
+  __shared__ __attribute__((aligned(16))) double colk[2][2][M];
+  double a[M];
+  const bool ok = gj_row<M>(L, 0, true, threadIdx.x, colk, a);
+  if (!ok) {  // uniform: every lane saw the same pivots
+    if (threadIdx.x == 0) atomicOr(status, 1);
+    return;
+  }
+  if ((int)threadIdx.x == W - 1)
+#pragma unroll
+    for (int r = 0; r < M; ++r) L.x[r] = a[r];
 }
 
 // Back-substitution, level L from level L+1: x_j = X_j^b − X_j^L x_{j−1} − X_j^U x_{j+1} for the odd rows, x of the
@@ -1668,16 +1663,13 @@ CrLevel cr_level(GnData& G, int l) {
 }
 
 template <int M>
-constexpr size_t cr_even_lds() { return sizeof(double) * (2 * M * M + 2 * M * (2 * M + 1)); }
-
-template <int M>
 void cr_solve(pba_engine* e) {
   GnData& G = e->gn;
-  if (cr_even_lds<M>() > 65536) {  // above the default dynamic-LDS limit (gfx950 has 160 KiB per CU)
+  if (cr_level_lds<M>() > 65536) {  // above the default dynamic-LDS limit (gfx950 has 160 KiB per CU)
     static bool raised = false;
     if (!raised) {
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&cr_even_kernel<M>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)cr_even_lds<M>());
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&cr_level_kernel<M>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)cr_level_lds<M>());
       raised = true;
     }
   }
@@ -1685,12 +1677,11 @@ void cr_solve(pba_engine* e) {
   CrLevel L0 = cr_level(G, 0);
   const long long nthreads = (long long)L0.n * M * M + (long long)L0.n * M;
   cr_build_kernel<M><<<(unsigned)((nthreads + 255) / 256), 256, 0, e->stream>>>(G.Sband.p, L0, e->n_frames, G.band_kernel);
-  for (int l = 0; l + 1 < nl; ++l) {
+  for (int l = 0; l + 1 < nl; ++l) {  // one fused launch per level (odd eliminations + even rebuild)
     CrLevel L = cr_level(G, l), Ln = cr_level(G, l + 1);
-    cr_odd_kernel<M><<<L.n / 2, kCrOddThreads<M>, 0, e->stream>>>(L, 0, G.status.p);
-    cr_even_kernel<M><<<(L.n + 1) / 2, 256, cr_even_lds<M>(), e->stream>>>(L, Ln);
+    cr_level_kernel<M><<<(L.n + 1) / 2, 2 * kCrOddThreads<M>, cr_level_lds<M>(), e->stream>>>(L, Ln, G.status.p);
   }
-  cr_odd_kernel<M><<<1, kCrOddThreads<M>, 0, e->stream>>>(cr_level(G, nl - 1), 1, G.status.p);
+  cr_root_kernel<M><<<1, kCrOddThreads<M>, 0, e->stream>>>(cr_level(G, nl - 1), G.status.p);
   if (nl == 1) {  // a single super-row: the root's x is the step
     (void)hipMemcpyAsync(G.x.p, L0.x, sizeof(double) * 6 * e->n_frames, hipMemcpyDeviceToDevice, e->stream);
     return;
