@@ -105,6 +105,13 @@ int pba_set_state_device(pba_engine* engine, const double* d_poses, const double
 /* Enqueue the evaluation of every block on the engine's stream.  want_jacobians = 0 writes only the
  * residual part of each record (Ceres' residual-only evaluation, trust_region_minimizer.cc:761-779). */
 int pba_evaluate(pba_engine* engine, int32_t want_jacobians);
+/* Evaluate at a device-resident state and adopt it (afterwards it is the engine's state, as after
+ * pba_set_state_device): Ceres' Evaluator::Evaluate(state, …) (program_evaluator.h:139-258), which reads the
+ * parameter state straight from the caller's array.  Photometric engines do it in ONE launch — each block forms
+ * its relative pose from the poses in its prologue and the launch copies the state — so no pair-table or copy
+ * launch precedes the evaluation.  d_poses / d_inv_dist must stay valid until the launch has run. */
+int pba_evaluate_state_device(pba_engine* engine, const double* d_poses, const double* d_inv_dist,
+                              int32_t want_jacobians);
 int pba_synchronize(pba_engine* engine);
 
 /* Results ---------------------------------------------------------------------------------------- */

@@ -37,49 +37,13 @@ thread_local std::string g_last_error;
 namespace {
 
 // ------------------------------------------------------------------------------------------------
-// Pair kernel: relative poses in fp64 (q_th = q_wt*·q_wh, t_th = q_wt*·(t_wh − t_wt))
+// Pair table: relative poses in fp64 (form_pair, pba_internal.h)
 // ------------------------------------------------------------------------------------------------
 __device__ __forceinline__ void make_pair(const double* __restrict__ poses, const int* __restrict__ pair_host,
                                           const int* __restrict__ pair_target, const int* __restrict__ frame_cam,
                                           const double* __restrict__ cams, PairRec* __restrict__ pairs, int i) {
-  const int h = pair_host[i], t = pair_target[i];
-  const double* H = poses + 7 * h;
-  const double* T = poses + 7 * t;
-  // q_th = q_wt* ⊗ q_wh (photometric_error.h:151, Hamilton product as so3.hpp:338-345)
-  const double ax = -T[0], ay = -T[1], az = -T[2], aw = T[3];
-  const double bx = H[0], by = H[1], bz = H[2], bw = H[3];
-  const double qw = aw * bw - ax * bx - ay * by - az * bz;
-  const double qx = aw * bx + ax * bw + ay * bz - az * by;
-  const double qy = aw * by + ay * bw + az * bx - ax * bz;
-  const double qz = aw * bz + az * bw + ax * by - ay * bx;
-  // toRotationMatrix (photometric_error.h:152)
-  const double tx = 2 * qx, ty = 2 * qy, tz = 2 * qz;
-  const double twx = tx * qw, twy = ty * qw, twz = tz * qw, txx = tx * qx, txy = ty * qx, txz = tz * qx;
-  const double tyy = ty * qy, tyz = tz * qy, tzz = tz * qz;
   PairRec r;
-  r.R[0] = 1 - (tyy + tzz); r.R[1] = txy - twz;       r.R[2] = txz + twy;
-  r.R[3] = txy + twz;       r.R[4] = 1 - (txx + tzz); r.R[5] = tyz - twx;
-  r.R[6] = txz - twy;       r.R[7] = tyz + twx;       r.R[8] = 1 - (txx + tyy);
-  // t_th = q_wt* · (t_wh − t_wt) (photometric_error.h:153), rotation as so3.hpp:367-370
-  const double d0 = H[4] - T[4], d1 = H[5] - T[5], d2 = H[6] - T[6];
-  double u0 = ay * d2 - az * d1, u1 = az * d0 - ax * d2, u2 = ax * d1 - ay * d0;
-  u0 += u0; u1 += u1; u2 += u2;
-  r.t[0] = d0 + aw * u0 + (ay * u2 - az * u1);
-  r.t[1] = d1 + aw * u1 + (az * u0 - ax * u2);
-  r.t[2] = d2 + aw * u2 + (ax * u1 - ay * u0);
-  r.host_cam = frame_cam[h];
-  r.target_cam = frame_cam[t];
-  r.target = t;
-  r.host = h;
-  const double* hc = cams + kCamD * r.host_cam + kCamHk;
-  const double* tc = cams + kCamD * r.target_cam;
-  for (int j = 0; j < kCamK; ++j) {
-    r.hk[j] = hc[j];
-    r.tk[j] = tc[j];
-  }
-  for (int j = 0; j < 8; ++j) r.pad[j] = 0.0f;
-  for (int j = 0; j < 9; ++j) r.Rf[j] = (float)r.R[j];
-  for (int j = 0; j < 3; ++j) r.tf[j] = (float)r.t[j];
+  form_pair(poses, frame_cam, cams, pair_host[i], pair_target[i], r);
   pairs[i] = r;
 }
 
@@ -142,6 +106,7 @@ __global__ void tile_images_kernel(const uint8_t* __restrict__ src, uint8_t* __r
 template <class T>
 __device__ __forceinline__ void store_slab(const unsigned char* src, unsigned char* dst, int bytes) {
   if ((((uintptr_t)dst | (unsigned)bytes) & 15) == 0) {
+    // non-temporal 16-B stores (sc1 write-through stores measured 49 → 71 µs for this kernel, profiles/r1_c4_v26)
     const f32x4* s4 = reinterpret_cast<const f32x4*>(src);
     f32x4* d4 = reinterpret_cast<f32x4*>(dst);
     for (int i = threadIdx.x; i < (bytes >> 4); i += kBlockThreads) __builtin_nontemporal_store(s4[i], d4 + i);
@@ -178,6 +143,7 @@ __global__ __launch_bounds__(kBlockThreads) void photometric_block_kernel(const 
   T* out = reinterpret_cast<T*>(a.out);  // records in the engine's format (fp32, or fp16 for PBA_RECORD_F16)
 
   if ((int)threadIdx.x < P) s_pat[threadIdx.x] = make_float2(a.pattern[2 * threadIdx.x], a.pattern[2 * threadIdx.x + 1]);
+  adopt_state(a);
   const int pt = stage_tile<LPB>(a, s_tb, lb, k, blk, live);
   const float Ih = act ? a.host_int[(long long)pt * P + k] : 0.0f;
   __syncthreads();
@@ -335,6 +301,9 @@ KernelArgs make_kernel_args(pba_engine* e, const PairRec* pairs, const double* r
   ka.block_pair = e->block_pair.p;
   ka.block_pp = e->block_pp.p;
   ka.pairs = pairs;
+  ka.block_rec = e->block_rec.p;
+  ka.n_pose_d = 7 * e->n_frames;
+  ka.n_points = e->n_points;
   ka.u_ref = e->u_ref.p;
   ka.host_int = e->host_int.p;
   ka.rho = rho;
@@ -411,7 +380,7 @@ int pba_destroy(pba_engine* e) {
   if (e->stream) (void)hipStreamSynchronize(e->stream);
   e->intr.release(); e->intr_d.release(); e->frame_cam.release(); e->images.release(); e->u_ref.release(); e->host_int.release(); e->point_host_d.release();
   e->block_point.release(); e->block_pair.release(); e->block_pp.release(); e->u_obs.release(); e->pair_host.release();
-  e->pair_target.release(); e->pairs.release(); e->poses.release(); e->rho.release(); e->out.release();
+  e->pair_target.release(); e->block_rec.release(); e->pairs.release(); e->poses.release(); e->rho.release(); e->out.release();
   e->cost.release(); e->valid.release();
   for (hipEvent_t ev : e->ev_pool) (void)hipEventDestroy(ev);
   if (e->own_stream) (void)hipStreamDestroy(e->own_stream);
@@ -432,7 +401,7 @@ int pba_get_stream(pba_engine* e, void** s) {
 }
 
 int pba_set_cameras(pba_engine* e, int32_t n_cams, const double* intrinsics) {
-  if (!e || n_cams <= 0 || !intrinsics) return fail(PBA_ERR_INVALID_ARGUMENT, "bad camera arguments");
+  if (!e || n_cams <= 0 || n_cams > 32767 || !intrinsics) return fail(PBA_ERR_INVALID_ARGUMENT, "bad camera arguments");
   if (int rc = check_device(e)) return rc;
   reset_pyramid(e);
   std::vector<float> f(8 * (size_t)n_cams);
@@ -454,6 +423,30 @@ int pba_set_cameras(pba_engine* e, int32_t n_cams, const double* intrinsics) {
   PBA_HIP(hipMemcpyAsync(e->intr_d.p, d.data(), d.size() * sizeof(double), hipMemcpyHostToDevice, e->stream));
   PBA_HIP(hipStreamSynchronize(e->stream));
   e->n_cams = n_cams;
+  return PBA_OK;
+}
+
+// Per-block {point, host, target, host_cam << 16 | target_cam} for the fused-state prologue (pba_internal.h
+// stage_tile); rebuilt whenever blocks or frame cameras change.  Blocks that no longer fit the frames/points
+// are dropped (pba_set_blocks again).
+static int upload_block_records(pba_engine* e) {
+  const size_t nb = e->block_point_h.size();
+  if (nb == 0 || e->n_blocks <= 0) return PBA_OK;
+  std::vector<int4> rec(nb);
+  const int nf = (int)e->frame_cam_h.size(), np = (int)e->point_host_h.size();
+  for (size_t b = 0; b < nb; ++b) {
+    const int p = e->block_point_h[b], t = e->block_target_h[b];
+    const int h = p < np ? e->point_host_h[p] : nf;
+    if (h >= nf || t >= nf) {
+      e->n_blocks = 0;
+      e->block_point_h.clear();
+      e->block_target_h.clear();
+      return PBA_OK;
+    }
+    rec[b] = make_int4(p, h, t, (e->frame_cam_h[h] << 16) | e->frame_cam_h[t]);
+  }
+  PBA_HIP(e->block_rec.upload(rec, e->stream));
+  PBA_HIP(hipStreamSynchronize(e->stream));
   return PBA_OK;
 }
 
@@ -499,7 +492,7 @@ static int set_frames_impl(pba_engine* e, int32_t n_frames, const int32_t* frame
   e->n_frames = n_frames;
   e->width = width;
   e->height = height;
-  return PBA_OK;
+  return upload_block_records(e);
 }
 
 int pba_set_frames(pba_engine* e, int32_t n_frames, const int32_t* frame_cam, int32_t width, int32_t height,
@@ -616,7 +609,7 @@ int pba_set_blocks(pba_engine* e, int32_t n_blocks, const int32_t* block_point, 
   e->pair_host_h = std::move(ph);
   e->pair_target_h = std::move(pt);
   e->gn.prepared = false;
-  return PBA_OK;
+  return upload_block_records(e);
 }
 
 int pba_set_state(pba_engine* e, const double* poses, const double* inv_dist) {
@@ -637,7 +630,9 @@ int pba_set_state_device(pba_engine* e, const double* d_poses, const double* d_i
   if (int rc = check_device(e)) return rc;
   PBA_HIP(e->poses.resize(7 * (size_t)e->n_frames));
   const int n_pose_d = 7 * e->n_frames;
-  const int pair_wgs = e->n_blocks > 0 ? (e->n_pairs + 255) / 256 : 0;
+  // the photometric evaluation forms its pairs itself (fused state); the table serves the geometric kernels
+  const bool table = e->n_blocks > 0 && e->opt.residual_kind == PBA_RESIDUAL_GEOMETRIC;
+  const int pair_wgs = table ? (e->n_pairs + 255) / 256 : 0;
   const int copy_wgs = std::min(1024, (std::max(n_pose_d, e->n_points) + 255) / 256);
   state_kernel<<<pair_wgs + copy_wgs, 256, 0, e->stream>>>(d_poses, d_inv_dist, e->poses.p, e->rho.p, n_pose_d,
                                                            e->n_points, e->pair_host.p, e->pair_target.p,
@@ -645,21 +640,46 @@ int pba_set_state_device(pba_engine* e, const double* d_poses, const double* d_i
                                                            pair_wgs);
   PBA_HIP(hipGetLastError());
   e->state_set = true;
-  e->pairs_fresh = pair_wgs > 0;
+  e->pairs_fresh = table;
   return PBA_OK;
 }
 
-int pba_evaluate(pba_engine* e, int32_t want_jacobians) {
-  if (!e) return fail(PBA_ERR_INVALID_ARGUMENT, "null engine");
-  if (e->n_blocks <= 0) return fail(PBA_ERR_NOT_READY, "pba_set_blocks first");
-  if (!e->state_set) return fail(PBA_ERR_NOT_READY, "pba_set_state first");
+namespace {
+
+// One evaluation launch at state (poses, rho); with `adopt`, the same launch copies that state into the engine's
+// buffers (it then is the engine's state, as after pba_set_state_device).
+int evaluate_at(pba_engine* e, const double* poses, const double* rho, bool adopt, bool jac) {
   const bool photometric = e->opt.residual_kind == PBA_RESIDUAL_PHOTOMETRIC;
   if (photometric && (!e->have_images || e->P <= 0)) return fail(PBA_ERR_NOT_READY, "images/pattern missing");
   if (int rc = check_device(e)) return rc;
-  if (!e->pairs_fresh) launch_pairs(e, e->poses.p, e->pairs.p);  // else formed by pba_set_state_device
-  e->pairs_fresh = true;
-  const KernelArgs ka = make_kernel_args(e, e->pairs.p, e->rho.p);
-  const bool jac = want_jacobians != 0;
+  KernelArgs ka;
+  if (photometric) {
+    const int lpb = e->P <= 8 ? 8 : (e->P <= 16 ? 16 : 32);
+    const long long lanes = (long long)e->n_blocks * lpb;  // the launch's lanes (whole workgroups)
+    if (adopt && lanes < std::max<long long>(7LL * e->n_frames, e->n_points)) {
+      if (int rc = pba_set_state_device(e, poses, rho)) return rc;  // more state than lanes: copy first
+      poses = e->poses.p;
+      rho = e->rho.p;
+      adopt = false;
+    }
+    ka = make_kernel_args(e, nullptr, rho);
+    ka.poses = poses;
+    if (adopt) {
+      PBA_HIP(e->poses.resize(7 * (size_t)e->n_frames));
+      ka.adopt_poses = e->poses.p;
+      ka.adopt_rho = e->rho.p;
+      e->state_set = true;
+      e->pairs_fresh = false;
+    }
+  } else {
+    if (adopt) {
+      if (int rc = pba_set_state_device(e, poses, rho)) return rc;
+    } else if (!e->pairs_fresh) {
+      launch_pairs(e, e->poses.p, e->pairs.p);
+    }
+    e->pairs_fresh = true;
+    ka = make_kernel_args(e, e->pairs.p, e->rho.p);
+  }
   hipEvent_t ev_stop = nullptr;
   if (e->timing) {
     while (e->ev_pool.size() < e->ev_used + 2) {
@@ -677,6 +697,21 @@ int pba_evaluate(pba_engine* e, int32_t want_jacobians) {
   if (ev_stop) PBA_HIP(hipEventRecord(ev_stop, e->stream));
   e->evaluated = true;
   return PBA_OK;
+}
+
+}  // namespace
+
+int pba_evaluate(pba_engine* e, int32_t want_jacobians) {
+  if (!e) return fail(PBA_ERR_INVALID_ARGUMENT, "null engine");
+  if (e->n_blocks <= 0) return fail(PBA_ERR_NOT_READY, "pba_set_blocks first");
+  if (!e->state_set) return fail(PBA_ERR_NOT_READY, "pba_set_state first");
+  return evaluate_at(e, e->poses.p, e->rho.p, false, want_jacobians != 0);
+}
+
+int pba_evaluate_state_device(pba_engine* e, const double* d_poses, const double* d_inv_dist, int32_t want_jacobians) {
+  if (!e || !d_poses || !d_inv_dist) return fail(PBA_ERR_INVALID_ARGUMENT, "null state");
+  if (e->n_blocks <= 0) return fail(PBA_ERR_NOT_READY, "pba_set_blocks first");
+  return evaluate_at(e, d_poses, d_inv_dist, true, want_jacobians != 0);
 }
 
 int pba_enable_kernel_timing(pba_engine* e, int32_t enable) {

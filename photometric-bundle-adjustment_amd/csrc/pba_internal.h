@@ -17,8 +17,9 @@ namespace detail {
 constexpr int kBlockThreads = 256;
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-// Relative pose of one (host, target) keyframe pair with the camera constants its residual rows need, 256 B
-// (L2-resident: 4k pairs = 1 MB at C4).  Formed by pair_kernel / state_kernel (pba_engine.hip).
+// Relative pose of one (host, target) keyframe pair with the camera constants its residual rows need, 320 B
+// (L2-resident: 4k pairs = 1.3 MB at C4).  Formed by form_pair: in the pair table (pair_kernel, state_kernel) or
+// in a block kernel's LDS tile (fused state).
 struct alignas(16) PairRec {
   double R[9];                 // R_th, fp64 (warp)
   double t[3];                 // t_th
@@ -29,6 +30,72 @@ struct alignas(16) PairRec {
   float pad[8];
 };
 static_assert(sizeof(PairRec) == 320, "PairRec layout");
+static_assert(offsetof(PairRec, hk) % 16 == 0 && offsetof(PairRec, tk) == offsetof(PairRec, hk) + 8 * kCamK,
+              "camera constants: 8 contiguous 16-B parts (fused-state prologue)");
+
+// Relative pose of pair (h, t) into r: q_th = q_wt*·q_wh, t_th = q_wt*·(t_wh − t_wt) in fp64 (photometric_error.h:
+// 151-153; Hamilton product as so3.hpp:338-345, rotation as so3.hpp:367-370), with the camera constants.  The
+// three parts write their fields in place, so r may live in LDS (tile prologue: one lane per part, which keeps
+// the prologue's register peak below the row evaluation's) or in the pair table (pair_kernel: all three).
+__device__ __forceinline__ void pair_rotation(const double* __restrict__ H, const double* __restrict__ T, PairRec& r) {
+  const double ax = -T[0], ay = -T[1], az = -T[2], aw = T[3];
+  const double bx = H[0], by = H[1], bz = H[2], bw = H[3];
+  const double qw = aw * bw - ax * bx - ay * by - az * bz;
+  const double qx = aw * bx + ax * bw + ay * bz - az * by;
+  const double qy = aw * by + ay * bw + az * bx - ax * bz;
+  const double qz = aw * bz + az * bw + ax * by - ay * bx;
+  // toRotationMatrix (photometric_error.h:152)
+  const double tx = 2 * qx, ty = 2 * qy, tz = 2 * qz;
+  const double twx = tx * qw, twy = ty * qw, twz = tz * qw, txx = tx * qx, txy = ty * qx, txz = tz * qx;
+  const double tyy = ty * qy, tyz = tz * qy, tzz = tz * qz;
+  double R[9];
+  R[0] = 1 - (tyy + tzz); R[1] = txy - twz;       R[2] = txz + twy;
+  R[3] = txy + twz;       R[4] = 1 - (txx + tzz); R[5] = tyz - twx;
+  R[6] = txz - twy;       R[7] = tyz + twx;       R[8] = 1 - (txx + tyy);
+#pragma unroll
+  for (int j = 0; j < 9; ++j) {
+    r.R[j] = R[j];
+    r.Rf[j] = (float)R[j];
+  }
+}
+__device__ __forceinline__ void pair_translation(const double* __restrict__ H, const double* __restrict__ T,
+                                                 PairRec& r) {
+  const double ax = -T[0], ay = -T[1], az = -T[2], aw = T[3];
+  const double d0 = H[4] - T[4], d1 = H[5] - T[5], d2 = H[6] - T[6];
+  double u0 = ay * d2 - az * d1, u1 = az * d0 - ax * d2, u2 = ax * d1 - ay * d0;
+  u0 += u0; u1 += u1; u2 += u2;
+  double tt[3];
+  tt[0] = d0 + aw * u0 + (ay * u2 - az * u1);
+  tt[1] = d1 + aw * u1 + (az * u0 - ax * u2);
+  tt[2] = d2 + aw * u2 + (ax * u1 - ay * u0);
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    r.t[j] = tt[j];
+    r.tf[j] = (float)tt[j];
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) r.pad[j] = 0.0f;
+}
+__device__ __forceinline__ void pair_cameras(const double* __restrict__ cams, int h, int t, int hc, int tc,
+                                             PairRec& r) {
+  r.host_cam = hc;
+  r.target_cam = tc;
+  r.target = t;
+  r.host = h;
+  const double* hk = cams + kCamD * hc + kCamHk;
+  const double* tk = cams + kCamD * tc;
+#pragma unroll
+  for (int j = 0; j < kCamK; ++j) {
+    r.hk[j] = hk[j];
+    r.tk[j] = tk[j];
+  }
+}
+__device__ __forceinline__ void form_pair(const double* __restrict__ poses, const int* __restrict__ frame_cam,
+                                          const double* __restrict__ cams, int h, int t, PairRec& r) {
+  pair_rotation(poses + 7 * h, poses + 7 * t, r);
+  pair_translation(poses + 7 * h, poses + 7 * t, r);
+  pair_cameras(cams, h, t, frame_cam[h], frame_cam[t], r);
+}
 
 // One block of a workgroup's tile, staged in LDS by stage_tile(): its pair record and its point.
 struct alignas(16) TileBlock {
@@ -50,7 +117,13 @@ struct KernelArgs {
   const int* block_point;
   const int* block_pair;
   const int2* block_pp;          // per block {point, pair}
-  const PairRec* pairs;
+  const PairRec* pairs;          // pair table (used when poses == nullptr)
+  const double* poses;           // state poses: when set, every block forms its pair record in the tile prologue
+  const int4* block_rec;         // per block {point, host, target, host_cam << 16 | target_cam} (with poses)
+  double* adopt_poses;           // when set, the launch also copies poses/rho (the state it evaluates at) here
+  double* adopt_rho;
+  int n_pose_d;                  // 7 × frames
+  int n_points;
   const double2* u_ref;          // per point
   const float* host_int;         // P per point
   const double* rho;             // per point (state)
@@ -127,13 +200,56 @@ struct Row {
 
 // Cooperative tile prologue: the LPB lanes of block lb copy its pair record, u_ref and ρ into LDS as
 // kTileParts 16-B parts (lane k takes parts k, k+LPB, …) — one broadcast copy per block instead of every lane
-// loading the 256-B record and the point data itself.  Returns the block's point.  The caller barriers.
+// loading the record and the point data itself — or, with a.poses set, form the pair record from the state
+// (no pair-table launch before the evaluation).  Returns the block's point.  The caller barriers.
 template <int LPB>
 __device__ __forceinline__ int stage_tile(const KernelArgs& a, TileBlock* s_tb, int lb, int k, int blk, bool live) {
   // a dead block (past the end of the problem) stages the last block, so every lane evaluates valid data
+  uint4* dst = reinterpret_cast<uint4*>(s_tb + lb);
+  if (LPB >= 8 && a.poses) {  // (LPB < 8: linearize of geometric rows, always on the table path)
+    // Fused state: the block's lanes issue every load first, with lane-dependent addresses and no branches (one
+    // memory round trip, as on the table path), then lane 0 forms R_th, lane 1 t_th and the ids, lane k copies
+    // camera part k (hk: parts 0-3, tk: 4-7), lanes 2-3 the point.  The block record carries host, target and
+    // cameras, so this is as many dependent loads as the table path.
+    static_assert(kCamK == 8, "fused prologue: 8 camera parts");
+    const int4 br = a.block_rec[live ? blk : a.n_blocks - 1];
+    const double* H = a.poses + 7 * br.y;
+    const double* T = a.poses + 7 * br.z;
+    double h[7], t[7];
+#pragma unroll
+    for (int j = 0; j < 7; ++j) {
+      h[j] = H[j];
+      t[j] = T[j];
+    }
+    const int hc = br.w >> 16, tc = br.w & 0xffff, kc = k & 7;
+    const uint4 cam = reinterpret_cast<const uint4*>(a.intr_d + (kc < 4 ? kCamD * hc + kCamHk : kCamD * tc))[kc & 3];
+    const uint4 ur = reinterpret_cast<const uint4*>(a.u_ref)[br.x];
+    const double rho = a.rho[br.x];
+    // every load above completes here, before the lanes diverge (otherwise the compiler sinks each load into the
+    // one branch that uses it and the branches pay a memory round trip each, serially)
+    asm volatile("" ::"v"(cam.x), "v"(cam.y), "v"(cam.z), "v"(cam.w), "v"(ur.x), "v"(ur.y), "v"(ur.z), "v"(ur.w),
+                 "v"(rho));
+#pragma unroll
+    for (int j = 0; j < 7; ++j) asm volatile("" ::"v"(h[j]), "v"(t[j]));
+    PairRec& pr = s_tb[lb].pr;
+    if (k < 8) dst[(int)(offsetof(PairRec, hk) / 16) + k] = cam;
+    if (k == 0) {
+      pair_rotation(h, t, pr);
+    } else if (k == 1) {
+      pair_translation(h, t, pr);
+      pr.host_cam = hc;
+      pr.target_cam = tc;
+      pr.target = br.z;
+      pr.host = br.y;
+    } else if (k == 2) {
+      dst[kPairParts] = ur;
+    } else if (k == 3) {
+      dst[kPairParts + 1] = make_uint4(__double2loint(rho), __double2hiint(rho), (unsigned)br.x, 0u);
+    }
+    return br.x;
+  }
   const int2 pp = a.block_pp[live ? blk : a.n_blocks - 1];
   const uint4* src = reinterpret_cast<const uint4*>(a.pairs + pp.y);
-  uint4* dst = reinterpret_cast<uint4*>(s_tb + lb);
 #pragma unroll
   for (int part = k; part < kTileParts; part += LPB) {
     uint4 v;
@@ -148,6 +264,17 @@ __device__ __forceinline__ int stage_tile(const KernelArgs& a, TileBlock* s_tb, 
     dst[part] = v;
   }
   return pp.x;
+}
+
+// The launch that evaluates at a caller's state also adopts it: one element per lane (grid ≥ frames·7, points).
+__device__ __forceinline__ void adopt_state(const KernelArgs& a) {
+  if (!a.adopt_rho) return;
+  const long long g = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= a.n_points && g >= a.n_pose_d) return;
+  const double r = a.rho[g < a.n_points ? g : 0], p = a.poses[g < a.n_pose_d ? g : 0];
+  asm volatile("" ::"v"(r), "v"(p));  // both loads in flight together (see stage_tile)
+  if (g < a.n_points) a.adopt_rho[g] = r;
+  if (g < a.n_pose_d) a.adopt_poses[g] = p;
 }
 
 // Photometric row k of a staged block (photometric_error.h:139-182 with the bilinear interpolator; the
@@ -364,6 +491,7 @@ struct pba_engine {
   pba::detail::DevBuf<int2> block_pp;
   pba::detail::DevBuf<double2> u_obs;
   pba::detail::DevBuf<int> pair_host, pair_target;
+  pba::detail::DevBuf<int4> block_rec;  // {point, host, target, cams} per block (fused-state prologue)
   pba::detail::DevBuf<pba::detail::PairRec> pairs;
   pba::detail::DevBuf<double> poses, rho;
   pba::detail::DevBuf<float> out, cost;

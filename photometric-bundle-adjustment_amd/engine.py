@@ -101,6 +101,7 @@ def lib():
         "pba_set_state": ([vp, vp, vp], C.c_int),
         "pba_set_state_device": ([vp, vp, vp], C.c_int),
         "pba_evaluate": ([vp, i32], C.c_int),
+        "pba_evaluate_state_device": ([vp, vp, vp, i32], C.c_int),
         "pba_synchronize": ([vp], C.c_int),
         "pba_record_floats": ([vp], C.c_int),
         "pba_residuals_per_block": ([vp], C.c_int),
@@ -225,6 +226,14 @@ class Engine:
     # -- evaluation ------------------------------------------------------------------------------
     def evaluate(self, want_jacobians: bool = True, sync: bool = True):
         _check(self._L.pba_evaluate(self._h, int(bool(want_jacobians))), "pba_evaluate")
+        if sync:
+            self.synchronize()
+
+    def evaluate_state_device(self, poses_ptr: int, rho_ptr: int, want_jacobians: bool = True, sync: bool = True):
+        """Evaluate at a device-resident state and adopt it (Ceres Evaluator::Evaluate(state, …),
+        program_evaluator.h:139-258): one launch for photometric engines."""
+        _check(self._L.pba_evaluate_state_device(self._h, C.c_void_p(poses_ptr), C.c_void_p(rho_ptr),
+                                                 int(bool(want_jacobians))), "pba_evaluate_state_device")
         if sync:
             self.synchronize()
 

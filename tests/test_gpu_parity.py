@@ -97,6 +97,51 @@ def test_deterministic_and_state_update():
     compare_records(0, pb.R, c, ref, vc, vref, projected_uv(pb_gt))
 
 
+@pytest.mark.parametrize("kind,model,extra_points", [(0, 0, 0), (0, 3, 0), (1, 0, 0), (0, 0, 40000)])
+def test_evaluate_state_device_adopts(kind, model, extra_points):
+    """pba_evaluate_state_device (one launch for photometric engines: pairs formed in the block prologue, state
+    copied by the same launch) equals set_state + evaluate, matches the oracle at that state, and leaves the state
+    adopted.  extra_points > 0 appends points without blocks (more state than lanes: the copy-first path)."""
+    import torch
+
+    pb = synth.make_problem(kind=kind, model=model, n_frames=8, n_points=300, width=376, height=240, seed=41,
+                            border=10)
+    if extra_points:
+        rng = np.random.default_rng(3)
+        n = extra_points
+        pb = synth.Problem(**{**pb.__dict__,
+                              "u_ref": np.concatenate([pb.u_ref, pb.u_ref[rng.integers(0, pb.n_points, n)]]),
+                              "point_host": np.concatenate([pb.point_host, np.zeros(n, pb.point_host.dtype)]),
+                              "rho": np.concatenate([pb.rho, np.full(n, 0.5)]),
+                              "rho_gt": np.concatenate([pb.rho_gt, np.full(n, 0.6)]),
+                              "host_intensity": (np.concatenate([pb.host_intensity, np.zeros((n, pb.P), np.float32)])
+                                                 if pb.host_intensity is not None else None)})
+    dev = torch.device("cuda", 0)
+    poses_d = torch.from_numpy(np.ascontiguousarray(pb.poses_gt)).to(dev)
+    rho_d = torch.from_numpy(np.ascontiguousarray(pb.rho_gt)).to(dev)
+    with E.Engine(kind, model) as eng:
+        eng.set_problem(pb)
+        eng.set_state(pb.poses, pb.rho)
+        eng.evaluate_state_device(poses_d.data_ptr(), rho_d.data_ptr(), True)
+        a, va = eng.records()
+        ca = eng.block_costs()
+        poses, rho = eng.get_state()
+        np.testing.assert_array_equal(poses, pb.poses_gt)
+        np.testing.assert_array_equal(rho, pb.rho_gt)
+        eng.evaluate(True)  # at the adopted state
+        b, vb = eng.records()
+        np.testing.assert_array_equal(a, b)
+        np.testing.assert_array_equal(va, vb)
+        eng.set_state(pb.poses_gt, pb.rho_gt)
+        eng.evaluate(True)
+        c, _ = eng.records()
+        np.testing.assert_array_equal(a, c)
+        np.testing.assert_array_equal(ca, eng.block_costs())
+    ref, vref = O.evaluate(pb, poses=pb.poses_gt, rho=pb.rho_gt)
+    pb_gt = synth.Problem(**{**pb.__dict__, "poses": pb.poses_gt, "rho": pb.rho_gt})
+    compare_records(kind, pb.R, a, ref, va, vref, projected_uv(pb_gt))
+
+
 def test_invalid_inputs_raise():
     pb = synth.make_problem(n_frames=6, n_points=20, width=64, height=48, seed=1, border=6)
     with E.Engine(0, 0) as eng:
