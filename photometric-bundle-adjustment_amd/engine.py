@@ -16,7 +16,7 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
-LIB_PATH = os.path.join(CSRC, "libpba.so")
+LIB_PATH = os.environ.get("PBA_LIBRARY") or os.path.join(CSRC, "libpba.so")  # override: A/B builds (tools/)
 HEADER = os.path.join(os.path.dirname(HERE), "include", "pba.h")
 
 PBA_OK = 0
