@@ -142,6 +142,37 @@ def gn_benchmark(eng, iters, torch, dist, dev, world):
                     "); noise-textured images, so the steps are not expected to converge — timing only"}
 
 
+def gn_c3(iters, torch, dev_index, dev):
+    """BASELINE.json configs[2] (C3): synthetic 200 keyframes × 20k points × 8-px patch (80k blocks) with
+    rendered (smooth, textured) images, so LM actually converges; on-device JᵀJ/Jᵀr + Schur GN through the
+    engine's LM loop (pba_solve).  One GPU (rank 0 at N = 1 only)."""
+    t0 = time.perf_counter()
+    pb = synth.make_problem(n_frames=200, n_points=20000, K=4, kind="photometric", model="pinhole", seed=42)
+    gen_s = time.perf_counter() - t0
+    eng = engine_mod.Engine(synth.PHOTOMETRIC, synth.PINHOLE, device=dev_index, huber_width=9.0)
+    try:
+        images = torch.from_numpy(pb.images).to(dev)
+        eng.set_problem(pb, images_device_ptr=images.data_ptr())
+        eng.set_fixed_frames(np.array([0, 1], np.int32))
+        eng.set_state(pb.poses, pb.rho)
+        eng.gn_linearize()  # symbolic analysis, outside the timed region
+        eng.solve(max_iterations=1)  # warm-up
+        eng.set_state(pb.poses, pb.rho)
+        torch.cuda.synchronize()
+        s = eng.solve(max_iterations=iters, function_tolerance=0.0)
+    finally:
+        eng.close()
+    n = max(s["iterations"], 1)
+    return {"config": "C3: synthetic 200 keyframes x 20000 points x 8-px patch x 4 targets = 80000 blocks, 752x480 "
+                      "rendered images, pinhole, 2 fixed keyframes",
+            "ms_per_iteration": s["total_ms"] / n, "iterations": s["iterations"], "accepted": s["successful_steps"],
+            "initial_cost": s["initial_cost"], "final_cost": s["final_cost"],
+            "breakdown_ms_per_iteration": {"linearize_ms": s["linearize_ms"] / n, "step_ms": s["solve_ms"] / n,
+                                           "cost_ms": s["cost_ms"] / n},
+            "problem_generation_s": gen_s,
+            "note": "host wall clock of pba_solve (Ceres LM logic on the host, every kernel on the device)"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -156,6 +187,7 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--gn-iterations", type=int, default=10)
+    ap.add_argument("--no-c3", action="store_true", help="skip the C3 Gauss-Newton measurement (configs[2])")
     args = ap.parse_args()
 
     import torch
@@ -260,6 +292,9 @@ def main():
     if args.gn_iterations > 0:
         eng.set_state(pb.poses, pb.rho)
         gn = gn_benchmark(eng, args.gn_iterations, torch, dist if world > 1 else None, dev, world)
+    c3 = None
+    if world == 1 and not args.no_c3 and args.gn_iterations > 0:
+        c3 = gn_c3(args.gn_iterations, torch, dev_index, dev)
 
     if rank == 0:
         ms_per_step = 1e3 * elapsed_max / args.steps
@@ -314,6 +349,7 @@ def main():
             },
             "cpu_baseline": cpu,
             "gn": gn,
+            "gn_c3": c3,
             "host": {k: round(v, 2) for k, v in host_diag.items()},
         }
         print(json.dumps(out), flush=True)
