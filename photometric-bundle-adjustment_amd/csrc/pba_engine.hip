@@ -5,15 +5,12 @@
 //   ResidualBlock::Evaluate (residual_block.cc:69-158) → AutoDiffCostFunction<Functor,…> →
 //   BundleAdjustmentReprojectionCostFunctor (reprojection.h:83-112) / PhotometricError (photometric_error.h:139-182)
 //
-// Two launches per evaluation, on one stream:
-//   1. pair_kernel      one lane per distinct (host, target) keyframe pair: T_th = T_w_t⁻¹ T_w_h in fp64
-//                       from the fp64 state, stored as fp32 R_th|t_th (+camera ids, target frame) — 64 B/pair.
-//   2. *_block_kernel   photometric: one lane per (block, pattern pixel), a wave = 64/LPB blocks;
-//                       geometric:   one lane per block.
-//                       SoA inputs (block_point, block_pair, u_ref, host_intensity, ρ) read coalesced,
-//                       pair poses from L2, image taps gathered from the target keyframe's u8 image,
-//                       Jacobian chain in registers, per-block ‖r‖² + validity by wave shuffles,
-//                       records stored as one contiguous 14R-float slab per block.
+// Photometric evaluation is ONE launch (photometric_block_kernel): one lane per (block, pattern pixel), a wave =
+// 64/LPB blocks.  Each block's lanes form its relative pose T_th = T_w_t⁻¹ T_w_h in fp64 from the state poses in
+// the tile prologue (fused state, pba_internal.h:stage_tile) — or copy it from the pair table (pair_kernel /
+// state_kernel: the geometric kernels and the Gauss-Newton path) — with u_ref and ρ into LDS; image taps are
+// gathered from the target keyframe's tiled u8 image, the Jacobian chain stays in registers, per-block ‖r‖² and
+// validity come from wave shuffles, and the workgroup's records leave as one contiguous slab.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -106,7 +103,8 @@ __global__ void tile_images_kernel(const uint8_t* __restrict__ src, uint8_t* __r
 template <class T>
 __device__ __forceinline__ void store_slab(const unsigned char* src, unsigned char* dst, int bytes) {
   if ((((uintptr_t)dst | (unsigned)bytes) & 15) == 0) {
-    // non-temporal 16-B stores (sc1 write-through stores measured 49 → 71 µs for this kernel, profiles/r1_c4_v26)
+    // non-temporal 16-B stores (write-through sc1 stores measured 49 → 71 µs for this kernel; per-lane stores
+    // straight from registers, without the LDS slab, 49 → 104 µs: DESIGN.md §3)
     const f32x4* s4 = reinterpret_cast<const f32x4*>(src);
     f32x4* d4 = reinterpret_cast<f32x4*>(dst);
     for (int i = threadIdx.x; i < (bytes >> 4); i += kBlockThreads) __builtin_nontemporal_store(s4[i], d4 + i);

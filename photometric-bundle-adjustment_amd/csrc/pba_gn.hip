@@ -1091,6 +1091,147 @@ __global__ __launch_bounds__(2 * kCrOddThreads<M>) void cr_level_kernel(CrLevel 
   }
 }
 
+// Wave-level variant for super-rows of ≤ 31 unknowns (B ≤ 5 keyframes), where [D | one coupling block | b] fits one
+// wave: lane c < M holds column c of D, lanes M…2M−1 the coupling block's columns, lane 2M b.  The pivot columns are
+// then always in the elimination's own wave: lanes k, k+1 publish them to a per-wave LDS buffer and every lane reads
+// them back with no s_barrier (LDS operations of one wave are processed in order), all 24 reads in flight at once.
+// Same arithmetic, same order as gj_row (bit-identical X).  Measured (tools/micro/cr_level_timing.hip, M = 24):
+// 17.0 → 14.5 µs per level launch.
+template <int M>
+__device__ __forceinline__ bool gj_wave(const double* __restrict__ D, const double* __restrict__ R1, bool r1_trans,
+                                        const double* __restrict__ b, int ncol, int c, double2* piv, double* a) {
+#pragma unroll
+  for (int r = 0; r < M; ++r) {
+    const double* src = nullptr;
+    if (c < M) src = D + r * M + c;
+    else if (c < 2 * M) src = R1 ? (r1_trans ? R1 + (c - M) * M + r : R1 + r * M + (c - M)) : nullptr;
+    else if (c < M + ncol) src = b ? b + r : nullptr;
+    a[r] = src ? *src : 0.0;
+  }
+  bool bad = false;
+#pragma unroll
+  for (int k = 0; k < M; k += 2) {
+    if (c == k || c == k + 1) {
+      double* dst = reinterpret_cast<double*>(piv) + (c - k);
+#pragma unroll
+      for (int r = 0; r < M; ++r) dst[2 * r] = a[r];
+    }
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
+    double2 cr[M];
+#pragma unroll
+    for (int r = 0; r < M; ++r) cr[r] = piv[r];
+    const double p00 = cr[k].x, p10 = cr[k + 1].x, p01 = cr[k].y, p11 = cr[k + 1].y;
+    const double det = p00 * p11 - p01 * p10;
+    bad |= !(p00 > 0.0 && det > 0.0);
+    const double rd = rcp_nr(det);
+    const double ak = a[k], ak1 = a[k + 1];
+    const double t0 = (p11 * ak - p01 * ak1) * rd;
+    const double t1 = (p00 * ak1 - p10 * ak) * rd;
+#pragma unroll
+    for (int r = 0; r < M; ++r) a[r] = r == k ? t0 : (r == k + 1 ? t1 : a[r] - cr[r].x * t0 - cr[r].y * t1);
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
+  }
+  return !bad;
+}
+
+template <int M>
+constexpr size_t cr_level_wave_lds() { return sizeof(double) * (3 * M * M + M + 2 * M * (2 * M + 1)); }
+
+// One level, 4 waves per even super-row i: wave 0 eliminates row i−1 on [D | U_{i−1} | b] (X^U, X^b), waves 1 and 2
+// row i+1 on [D | U_iᵀ | b] (X^L, X^b) and [D | U_{i+1}] (X^U) — D's columns replicated per wave — while wave 3
+// parks U_{i−1}, U_i, D_i and b_i in LDS for the rebuild of row i.
+template <int M>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void cr_level_wave_kernel(
+    CrLevel L, CrLevel Ln, int* status) {
+  static_assert(2 * M + 1 <= 64, "one wave per elimination");
+  constexpr int NC = 2 * M + 1;
+  __shared__ __attribute__((aligned(16))) double2 piv[3][M];
+  extern __shared__ double smem[];
+  double* sUl = smem;
+  double* sUi = sUl + M * M;
+  double* sD = sUi + M * M;
+  double* sb = sD + M * M;
+  double* sX[2] = {sb + M, sb + M + M * NC};
+  const int i = 2 * blockIdx.x, in = blockIdx.x;
+  const bool left = i - 1 >= 0, right = i + 1 < L.n;
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  if (w == 3) {
+    for (int e = lane; e < 3 * M * M + M; e += 64) {
+      const double* src = nullptr;
+      if (e < M * M) src = left ? L.U + (long long)(i - 1) * M * M + e : nullptr;
+      else if (e < 2 * M * M) src = L.U + (long long)i * M * M + (e - M * M);
+      else if (e < 3 * M * M) src = L.D + (long long)i * M * M + (e - 2 * M * M);
+      else src = L.b + (long long)i * M + (e - 3 * M * M);
+      smem[e] = src ? *src : 0.0;
+    }
+  } else {
+    const int j = w == 0 ? i - 1 : i + 1;
+    const bool has = j >= 0 && j < L.n;
+    const int jj = has ? j : 1;  // a missing neighbour eliminates a real row and contributes zeros
+    const double* D = L.D + (long long)jj * M * M;
+    const double* bj = L.b + (long long)jj * M;
+    double a[M];
+    bool ok;
+    if (w == 0) ok = gj_wave<M>(D, L.U + (long long)jj * M * M, false, bj, M + 1, lane, piv[0], a);
+    else if (w == 1) ok = gj_wave<M>(D, L.U + (long long)(jj - 1) * M * M, true, bj, M + 1, lane, piv[1], a);
+    else ok = gj_wave<M>(D, jj + 1 < L.n ? L.U + (long long)jj * M * M : nullptr, false, nullptr, M, lane, piv[2], a);
+    if (!ok && has && lane == 0) atomicOr(status, 1);
+    if (lane >= M && lane < 2 * M + (w == 2 ? 0 : 1)) {
+      const int col = lane < 2 * M ? (w == 1 ? lane - M : lane) : 2 * M;
+      double* x = sX[w == 0 ? 0 : 1] + col;
+#pragma unroll
+      for (int r = 0; r < M; ++r) x[r * NC] = has ? a[r] : 0.0;
+      if (w != 0 && has) {  // X_{i+1} for the back-substitution
+        double* X = L.X + (long long)(j / 2) * M * NC + col;
+#pragma unroll
+        for (int r = 0; r < M; ++r) X[r * NC] = a[r];
+      }
+    }
+  }
+  __syncthreads();
+  const double* sXl = sX[0];
+  const double* sXr = sX[1];
+  for (int e = threadIdx.x; e < 2 * M * M + M; e += 256) {
+    if (e < M * M) {  // D' = D − U_{i−1}ᵀ X^U_{i−1} − U_i X^L_{i+1}
+      const int r = e / M, c = e % M;
+      double v = sD[e];
+#pragma unroll 8
+      for (int q = 0; q < M; ++q) v -= sUl[q * M + r] * sXl[q * NC + M + c] + sUi[r * M + q] * sXr[q * NC + c];
+      Ln.D[(long long)in * M * M + e] = v;
+    } else if (e < 2 * M * M) {  // U' = −U_i X^U_{i+1}
+      const int f = e - M * M, r = f / M, c = f % M;
+      double v = 0.0;
+#pragma unroll 8
+      for (int q = 0; q < M; ++q) v -= sUi[r * M + q] * sXr[q * NC + M + c];
+      Ln.U[(long long)in * M * M + f] = right ? v : 0.0;
+    } else {  // b'
+      const int r = e - 2 * M * M;
+      double v = sb[r];
+#pragma unroll 8
+      for (int q = 0; q < M; ++q) v -= sUl[q * M + r] * sXl[q * NC + 2 * M] + sUi[r * M + q] * sXr[q * NC + 2 * M];
+      Ln.b[(long long)in * M + r] = v;
+    }
+  }
+}
+
+// The root super-row on one wave (lane 2M carries b; the coupling lanes are empty).
+template <int M>
+__global__ __launch_bounds__(64) void cr_root_wave_kernel(CrLevel L, int* status) {
+  __shared__ __attribute__((aligned(16))) double2 piv[M];
+  double a[M];
+  const int lane = threadIdx.x;
+  const bool ok = gj_wave<M>(L.D, nullptr, false, L.b, M + 1, lane, piv, a);
+  if (!ok) {
+    if (lane == 0) atomicOr(status, 1);
+    return;
+  }
+  if (lane == 2 * M)
+#pragma unroll
+    for (int r = 0; r < M; ++r) L.x[r] = a[r];
+}
+
 // The root super-row (the last level): x = D⁻¹ b.
 template <int M>
 __global__ __launch_bounds__(kCrOddThreads<M>) void cr_root_kernel(CrLevel L, int* status) {
@@ -1679,9 +1820,13 @@ void cr_solve(pba_engine* e) {
   cr_build_kernel<M><<<(unsigned)((nthreads + 255) / 256), 256, 0, e->stream>>>(G.Sband.p, L0, e->n_frames, G.band_kernel);
   for (int l = 0; l + 1 < nl; ++l) {  // one fused launch per level (odd eliminations + even rebuild)
     CrLevel L = cr_level(G, l), Ln = cr_level(G, l + 1);
-    cr_level_kernel<M><<<(L.n + 1) / 2, 2 * kCrOddThreads<M>, cr_level_lds<M>(), e->stream>>>(L, Ln, G.status.p);
+    if constexpr (2 * M + 1 <= 64)
+      cr_level_wave_kernel<M><<<(L.n + 1) / 2, 256, cr_level_wave_lds<M>(), e->stream>>>(L, Ln, G.status.p);
+    else
+      cr_level_kernel<M><<<(L.n + 1) / 2, 2 * kCrOddThreads<M>, cr_level_lds<M>(), e->stream>>>(L, Ln, G.status.p);
   }
-  cr_root_kernel<M><<<1, kCrOddThreads<M>, 0, e->stream>>>(cr_level(G, nl - 1), G.status.p);
+  if constexpr (2 * M + 1 <= 64) cr_root_wave_kernel<M><<<1, 64, 0, e->stream>>>(cr_level(G, nl - 1), G.status.p);
+  else cr_root_kernel<M><<<1, kCrOddThreads<M>, 0, e->stream>>>(cr_level(G, nl - 1), G.status.p);
   if (nl == 1) {  // a single super-row: the root's x is the step
     (void)hipMemcpyAsync(G.x.p, L0.x, sizeof(double) * 6 * e->n_frames, hipMemcpyDeviceToDevice, e->stream);
     return;
