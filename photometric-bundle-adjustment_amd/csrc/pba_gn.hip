@@ -1096,7 +1096,7 @@ __global__ __launch_bounds__(2 * kCrOddThreads<M>) void cr_level_kernel(CrLevel 
 // then always in the elimination's own wave: lanes k, k+1 publish them to a per-wave LDS buffer and every lane reads
 // them back with no s_barrier (LDS operations of one wave are processed in order), all 24 reads in flight at once.
 // Same arithmetic, same order as gj_row (bit-identical X).  Measured (tools/micro/cr_level_timing.hip, M = 24):
-// 17.0 → 14.5 µs per level launch.
+// 17.0 → 14.5 µs per level launch (13.0 with the rebuild on the matrix cores, below).
 template <int M>
 __device__ __forceinline__ bool gj_wave(const double* __restrict__ D, const double* __restrict__ R1, bool r1_trans,
                                         const double* __restrict__ b, int ncol, int c, double2* piv, double* a) {
@@ -1135,6 +1135,8 @@ __device__ __forceinline__ bool gj_wave(const double* __restrict__ D, const doub
   }
   return !bad;
 }
+
+typedef double v4f64 __attribute__((ext_vector_type(4)));
 
 template <int M>
 constexpr size_t cr_level_wave_lds() { return sizeof(double) * (3 * M * M + M + 2 * M * (2 * M + 1)); }
@@ -1191,29 +1193,53 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     }
   }
   __syncthreads();
+  // Rebuild of row i on the matrix cores: [D' | U' | b'] = [D | 0 | b] − U_{i−1}ᵀ·[X^U_{i−1} | 0 | X^b_{i−1}]
+  // − U_i·X_{i+1}, as 2 × 4 output tiles of v_mfma_f64_16x16x4f64 (rows padded to 32, columns to 64).  Wave w takes
+  // row tile w & 1 and column tiles 2(w >> 1) + {0, 1}: the two tiles share the A operands and run as two
+  // independent accumulator chains.  Layouts (tools/micro/mfma_f64_layout.hip): A lane l = (row l%16, k l/16),
+  // B lane l = (k l/16, column l%16), accumulator entry v of lane l = (row l/16 + 4v, column l%16).
+  // 3.9 → 2.7 µs per level against the scalar LDS products (tools/micro/cr_level_timing.hip, V5).
+  static_assert(M % 4 == 0 && M <= 32, "K steps of 4, two row tiles");
   const double* sXl = sX[0];
   const double* sXr = sX[1];
-  for (int e = threadIdx.x; e < 2 * M * M + M; e += 256) {
-    if (e < M * M) {  // D' = D − U_{i−1}ᵀ X^U_{i−1} − U_i X^L_{i+1}
-      const int r = e / M, c = e % M;
-      double v = sD[e];
-#pragma unroll 8
-      for (int q = 0; q < M; ++q) v -= sUl[q * M + r] * sXl[q * NC + M + c] + sUi[r * M + q] * sXr[q * NC + c];
-      Ln.D[(long long)in * M * M + e] = v;
-    } else if (e < 2 * M * M) {  // U' = −U_i X^U_{i+1}
-      const int f = e - M * M, r = f / M, c = f % M;
-      double v = 0.0;
-#pragma unroll 8
-      for (int q = 0; q < M; ++q) v -= sUi[r * M + q] * sXr[q * NC + M + c];
-      Ln.U[(long long)in * M * M + f] = right ? v : 0.0;
-    } else {  // b'
-      const int r = e - 2 * M * M;
-      double v = sb[r];
-#pragma unroll 8
-      for (int q = 0; q < M; ++q) v -= sUl[q * M + r] * sXl[q * NC + 2 * M] + sUi[r * M + q] * sXr[q * NC + 2 * M];
-      Ln.b[(long long)in * M + r] = v;
+  const int rt = w & 1;
+  const int arow = 16 * rt + (lane & 15), kq = lane >> 4;
+  int bcol[2];
+  v4f64 acc[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    bcol[h] = 16 * ((w >> 1) * 2 + h) + (lane & 15);
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      const int r = 16 * rt + (lane >> 4) + 4 * v, c = bcol[h];
+      acc[h][v] = (r < M) ? (c < M ? sD[r * M + c] : (c == 2 * M ? sb[r] : 0.0)) : 0.0;
     }
   }
+#pragma unroll
+  for (int s4 = 0; s4 < M / 4; ++s4) {
+    const int q = 4 * s4 + kq;
+    const double a2 = arow < M ? -sUi[arow * M + q] : 0.0;
+    const double a1 = arow < M ? -sUl[q * M + arow] : 0.0;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int c = bcol[h];
+      const double b2 = c < NC ? sXr[q * NC + c] : 0.0;
+      const double b1 = c < M ? sXl[q * NC + M + c] : (c == 2 * M ? sXl[q * NC + 2 * M] : 0.0);
+      acc[h] = __builtin_amdgcn_mfma_f64_16x16x4f64(a2, b2, acc[h], 0, 0, 0);
+      acc[h] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1, acc[h], 0, 0, 0);
+    }
+  }
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      const int r = 16 * rt + (lane >> 4) + 4 * v, c = bcol[h];
+      if (r < M) {
+        if (c < M) Ln.D[(long long)in * M * M + r * M + c] = acc[h][v];
+        else if (c < 2 * M) Ln.U[(long long)in * M * M + r * M + (c - M)] = right ? acc[h][v] : 0.0;
+        else if (c == 2 * M) Ln.b[(long long)in * M + r] = acc[h][v];
+      }
+    }
 }
 
 // The root super-row on one wave (lane 2M carries b; the coupling lanes are empty).

@@ -659,6 +659,111 @@ __global__ __launch_bounds__(256) void level4(CrLevel L, CrLevel Ln, int* status
   }
 }
 
+// V5: V2 + the row rebuild on the matrix cores: O = [D | 0 | b] − U_{i−1}ᵀ·B1 − U_i·X_{i+1} as 2 × 4 output tiles
+// of v_mfma_f64_16x16x4f64 (rows padded 24 → 32, columns 49 → 64), two tiles per wave, K = 24 in 6 steps.
+typedef double v4d __attribute__((ext_vector_type(4)));
+template <int M, bool ST>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void level5(CrLevel L, CrLevel Ln, int* status, long long* stamps) {
+  constexpr int NC = 2 * M + 1;
+  __shared__ __attribute__((aligned(16))) double2 piv[3][M];
+  extern __shared__ double smem[];
+  double* sUl = smem;
+  double* sUi = sUl + M * M;
+  double* sD = sUi + M * M;
+  double* sb = sD + M * M;
+  double* sX[2] = {sb + M, sb + M + M * NC};
+  long long st[5];
+  st[0] = wall_clock64();
+  const int i = 2 * blockIdx.x, in = blockIdx.x;
+  const bool left = i - 1 >= 0, right = i + 1 < L.n;
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  double a[M];
+  if (w == 3) {
+    for (int e = lane; e < 3 * M * M + M; e += 64) {
+      const double* src = nullptr;
+      if (e < M * M) src = left ? L.U + (long long)(i - 1) * M * M + e : nullptr;
+      else if (e < 2 * M * M) src = L.U + (long long)i * M * M + (e - M * M);
+      else if (e < 3 * M * M) src = L.D + (long long)i * M * M + (e - 2 * M * M);
+      else src = L.b + (long long)i * M + (e - 3 * M * M);
+      smem[e] = src ? *src : 0.0;
+    }
+    if (ST) st[1] = wall_clock64();
+  } else {
+    const int j = w == 0 ? i - 1 : i + 1;
+    const bool has = j >= 0 && j < L.n;
+    const int jj = has ? j : 1;
+    const double* D = L.D + (long long)jj * M * M;
+    const double* bj = L.b + (long long)jj * M;
+    bool ok;
+    if (w == 0) ok = gj_wave<M, ST>(D, L.U + (long long)jj * M * M, false, bj, M + 1, lane, piv[0], a, st);
+    else if (w == 1) ok = gj_wave<M, ST>(D, L.U + (long long)(jj - 1) * M * M, true, bj, M + 1, lane, piv[1], a, st);
+    else ok = gj_wave<M, ST>(D, jj + 1 < L.n ? L.U + (long long)jj * M * M : nullptr, false, nullptr, M, lane, piv[2], a, st);
+    if (!ok && has && lane == 0) atomicOr(status, 1);
+    if (lane >= M && lane < 2 * M + (w == 2 ? 0 : 1)) {
+      const int col = lane < 2 * M ? (w == 1 ? lane - M : lane) : 2 * M;
+      double* x = sX[w == 0 ? 0 : 1] + col;
+#pragma unroll
+      for (int r = 0; r < M; ++r) x[r * NC] = has ? a[r] : 0.0;
+      if (w != 0 && has) {
+        double* X = L.X + (long long)(j / 2) * M * NC + col;
+#pragma unroll
+        for (int r = 0; r < M; ++r) X[r * NC] = a[r];
+      }
+    }
+  }
+  if (ST) st[2] = wall_clock64();
+  __syncthreads();
+  if (ST) st[3] = wall_clock64();
+  const double* sXl = sX[0];
+  const double* sXr = sX[1];
+  // wave w: row tile rt = w & 1, column tiles ct = (w >> 1) * 2 + {0, 1}: the two tiles share the A operands and
+  // run as two independent accumulator chains
+  const int rt = w & 1;
+  const int arow = 16 * rt + (lane & 15), kq = lane >> 4;  // operand A: row, k within the step
+  int bcol[2];
+  v4d acc[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    bcol[h] = 16 * ((w >> 1) * 2 + h) + (lane & 15);
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {  // C = [D | 0 | b]; accumulator entry v of lane l: row l/16 + 4v, column l%16
+      const int r = 16 * rt + (lane >> 4) + 4 * v, c = bcol[h];
+      acc[h][v] = (r < M) ? (c < M ? sD[r * M + c] : (c == 2 * M ? sb[r] : 0.0)) : 0.0;
+    }
+  }
+#pragma unroll
+  for (int s4 = 0; s4 < M / 4; ++s4) {
+    const int q = 4 * s4 + kq;
+    const double a2 = arow < M ? -sUi[arow * M + q] : 0.0;
+    const double a1 = arow < M ? -sUl[q * M + arow] : 0.0;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int c = bcol[h];
+      const double b2 = c < NC ? sXr[q * NC + c] : 0.0;
+      const double b1 = c < M ? sXl[q * NC + M + c] : (c == 2 * M ? sXl[q * NC + 2 * M] : 0.0);
+      acc[h] = __builtin_amdgcn_mfma_f64_16x16x4f64(a2, b2, acc[h], 0, 0, 0);
+      acc[h] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1, acc[h], 0, 0, 0);
+    }
+  }
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      const int r = 16 * rt + (lane >> 4) + 4 * v, c = bcol[h];
+      if (r < M) {
+        if (c < M) Ln.D[(long long)in * M * M + r * M + c] = acc[h][v];
+        else if (c < 2 * M) Ln.U[(long long)in * M * M + r * M + (c - M)] = right ? acc[h][v] : 0.0;
+        else if (c == 2 * M) Ln.b[(long long)in * M + r] = acc[h][v];
+      }
+    }
+  if (ST) {
+    __syncthreads();
+    st[4] = wall_clock64();
+    if (threadIdx.x == 0)
+      for (int q = 0; q < 5; ++q) stamps[blockIdx.x * 5 + q] = st[q];
+  }
+}
+
 template <class K0, class K1>
 void run(const char* name, K0 kfast, K1 kstamp, int grid, int threads, size_t lds, CrLevel L, CrLevel Ln, int* status,
          long long* stamps) {
@@ -722,6 +827,7 @@ int main(int argc, char** argv) {
   run("V2", &level2<M, false>, &level2<M, true>, grid, 256, lds1, L, Ln, status, stamps);
   run("V3", &level3<M, false>, &level3<M, true>, grid, 384, lds1, L, Ln, status, stamps);
   run("V4", &level4<M, false>, &level4<M, true>, grid, 256, lds1, L, Ln, status, stamps);
+  run("V5", &level5<M, false>, &level5<M, true>, grid, 256, lds1, L, Ln, status, stamps);
   {
     std::vector<double> a0((size_t)Ln.n * M * M), a2(a0.size()), u0(a0.size()), u2(a0.size());
     std::vector<double> x0((size_t)(n / 2 + 1) * M * NC), x2(x0.size());
@@ -729,7 +835,8 @@ int main(int argc, char** argv) {
     CK(hipMemcpy(a0.data(), Ln.D, a0.size() * 8, hipMemcpyDeviceToHost));
     CK(hipMemcpy(u0.data(), Ln.U, u0.size() * 8, hipMemcpyDeviceToHost));
     CK(hipMemcpy(x0.data(), L.X, (size_t)(n / 2) * M * NC * 8, hipMemcpyDeviceToHost));
-    if (getenv("CMP4")) level4<M, false><<<grid, 256, lds1>>>(L, Ln, status, stamps);
+    if (getenv("CMP5")) level5<M, false><<<grid, 256, lds1>>>(L, Ln, status, stamps);
+    else if (getenv("CMP4")) level4<M, false><<<grid, 256, lds1>>>(L, Ln, status, stamps);
     else if (getenv("CMP3")) level3<M, false><<<grid, 384, lds1>>>(L, Ln, status, stamps);
     else level2<M, false><<<grid, 256, lds1>>>(L, Ln, status, stamps);
     CK(hipMemcpy(a2.data(), Ln.D, a2.size() * 8, hipMemcpyDeviceToHost));
@@ -739,8 +846,17 @@ int main(int argc, char** argv) {
     for (size_t q = 0; q < a0.size(); ++q) { d = std::max(d, std::abs(a0[q] - a2[q])); du = std::max(du, std::abs(u0[q] - u2[q])); }
     for (size_t q = 0; q < (size_t)(n / 2) * M * NC; ++q) dx = std::max(dx, std::abs(x0[q] - x2[q]));
     double sd = 0; for (size_t q = 0; q < a0.size(); ++q) sd = std::max(sd, std::abs(a0[q]));
+    {
+      std::vector<double> bb0((size_t)Ln.n * M), bb2(bb0.size());
+      level<M, false><<<grid, 2 * kT<M>, lds0>>>(L, Ln, status, stamps);
+      CK(hipMemcpy(bb0.data(), Ln.b, bb0.size() * 8, hipMemcpyDeviceToHost));
+      if (getenv("CMP5")) level5<M, false><<<grid, 256, lds1>>>(L, Ln, status, stamps);
+      CK(hipMemcpy(bb2.data(), Ln.b, bb2.size() * 8, hipMemcpyDeviceToHost));
+      double db = 0; for (size_t q = 0; q < bb0.size(); ++q) db = std::max(db, std::abs(bb0[q] - bb2[q]));
+      printf("  max |db'| = %g\n", db);
+    }
     std::vector<double> b0((size_t)Ln.n * M), b2(b0.size());
-    printf("%s vs V0 max |dD'| = %g (max |D'| %g) |dU'| = %g |dX| = %g\n", getenv("CMP4") ? "V4" : getenv("CMP3") ? "V3" : "V2", d, sd, du, dx);
+    printf("%s vs V0 max |dD'| = %g (max |D'| %g) |dU'| = %g |dX| = %g\n", getenv("CMP5") ? "V5" : getenv("CMP4") ? "V4" : getenv("CMP3") ? "V3" : "V2", d, sd, du, dx);
   }
   {  // V1 must reproduce V0 exactly
     std::vector<double> a0((size_t)Ln.n * M * M), a1(a0.size());
