@@ -170,7 +170,10 @@ typedef struct pba_solver_options {
 typedef struct pba_solver_summary {
   int32_t iterations, successful_steps, unsuccessful_steps, termination;
   double initial_cost, final_cost;      /* Σ ½ρ(‖r‖²) */
-  double total_ms, linearize_ms, solve_ms, cost_ms;  /* host wall-clock */
+  /* total_ms: host wall clock of the whole solve.  The parts: pba_solve — device time between stream events (one
+   * host synchronisation per LM trial, so the parts do not add up to total_ms); pba_solve_distributed — host wall
+   * clock of each phase, collectives included. */
+  double total_ms, linearize_ms, solve_ms, cost_ms;
 } pba_solver_summary;
 
 /* constant parameter blocks (Problem::SetParameterBlockConstant, map_utils.h:334-336) */

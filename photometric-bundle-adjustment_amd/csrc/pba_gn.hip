@@ -1741,7 +1741,7 @@ int gn_prepare(pba_engine* e) {
   PBA_HIP(G.status.resize(1));
   const int red_pose = (nf + kBlockThreads - 1) / kBlockThreads;
   const int red_pt = (ngp + kBlockThreads - 1) / kBlockThreads;
-  G.red_slots = std::max(std::max(red_pose + red_pt, 1024), 1);
+  G.red_slots = red_pose + red_pt + 1024;  // update partials, then (step_and_candidate_cost) the cost partials
   PBA_HIP(G.red.resize((size_t)2 * G.red_slots));
   G.red_h.resize(2 * G.red_slots);
   PBA_HIP(hipMemsetAsync(G.drho.p, 0, sizeof(double) * e->n_points, st));
@@ -1871,16 +1871,10 @@ void cr_solve(pba_engine* e) {
 
 // After a solve into G.x: solver status, candidate poses/points, and the two parts of the LM model decrease
 // L(0) − L(δ) = −gᵀδ − ½δᵀHδ = ½(λ δᵀDδ − gᵀδ)  (since (H + λD)δ = −g): pose part and point part.
-int finish_step(pba_engine* e, double lambda, const uint8_t* fixed, double* model_pose, double* model_points,
-                int* solver_status) {
+// Candidate poses/points and the model-decrease partials into reduction slots [0, gp + gq) of G.red.
+void enqueue_updates(pba_engine* e, double lambda, const uint8_t* fixed, int* gp_out, int* gq_out) {
   GnData& G = e->gn;
   const int nf = e->n_frames;
-  int status = 0;
-  PBA_HIP(hipMemcpyAsync(&status, G.status.p, sizeof(int), hipMemcpyDeviceToHost, e->stream));
-  PBA_HIP(hipStreamSynchronize(e->stream));
-  if (solver_status) *solver_status = status;
-  *model_pose = *model_points = 0.0;
-  if (status != 0) return PBA_OK;
   const int gp = (nf + kBlockThreads - 1) / kBlockThreads;
   const int gq = (G.n_gn_points + kBlockThreads - 1) / kBlockThreads;
   pose_update_kernel<<<gp, kBlockThreads, 0, e->stream>>>(e->poses.p, G.x.p, G.g_dir.p, G.Ddiag.p, fixed,
@@ -1889,14 +1883,33 @@ int finish_step(pba_engine* e, double lambda, const uint8_t* fixed, double* mode
                       G.blk_schur.p, G.x.p, fixed, e->rho.p, G.rho_new.p, G.drho.p, G.red.p + 2 * gp,
                       G.n_gn_points};
   if (gq > 0) point_update_kernel<<<gq, kBlockThreads, 0, e->stream>>>(pa_, lambda);
-  PBA_HIP(hipGetLastError());
-  PBA_HIP(hipMemcpyAsync(G.red_h.data(), G.red.p, sizeof(double) * 2 * (gp + gq), hipMemcpyDeviceToHost, e->stream));
-  PBA_HIP(hipStreamSynchronize(e->stream));
+  *gp_out = gp;
+  *gq_out = gq;
+}
+
+void model_from_slots(const GnData& G, double lambda, int gp, int gq, double* model_pose, double* model_points) {
   double dg = 0, dD = 0, qg = 0, qD = 0;
   for (int i = 0; i < gp; ++i) { dg += G.red_h[2 * i]; dD += G.red_h[2 * i + 1]; }
   for (int i = gp; i < gp + gq; ++i) { qg += G.red_h[2 * i]; qD += G.red_h[2 * i + 1]; }
   *model_pose = 0.5 * (lambda * dD - dg);
   *model_points = 0.5 * (lambda * qD - qg);
+}
+
+int finish_step(pba_engine* e, double lambda, const uint8_t* fixed, double* model_pose, double* model_points,
+                int* solver_status) {
+  GnData& G = e->gn;
+  int status = 0;
+  PBA_HIP(hipMemcpyAsync(&status, G.status.p, sizeof(int), hipMemcpyDeviceToHost, e->stream));
+  PBA_HIP(hipStreamSynchronize(e->stream));
+  if (solver_status) *solver_status = status;
+  *model_pose = *model_points = 0.0;
+  if (status != 0) return PBA_OK;
+  int gp = 0, gq = 0;
+  enqueue_updates(e, lambda, fixed, &gp, &gq);
+  PBA_HIP(hipGetLastError());
+  PBA_HIP(hipMemcpyAsync(G.red_h.data(), G.red.p, sizeof(double) * 2 * (gp + gq), hipMemcpyDeviceToHost, e->stream));
+  PBA_HIP(hipStreamSynchronize(e->stream));
+  model_from_slots(G, lambda, gp, gq, model_pose, model_points);
   return PBA_OK;
 }
 
@@ -1918,8 +1931,8 @@ int band_solve(pba_engine* e) {
   return PBA_OK;
 }
 
-// Schur complement for λ, assembly, solve and candidate state; returns the LM model decrease.
-int gn_step(pba_engine* e, double lambda, double* model_decrease, int* solver_status) {
+// Schur complement for λ, assembly and reduced-system solve into G.x (enqueued only).
+int enqueue_solve(pba_engine* e, double lambda) {
   GnData& G = e->gn;
   const int nf = e->n_frames;
   SchurArgs sa{G.schur_desc.p, G.schur_aux.p, G.schur_pairs.p, G.pt_first.p, G.pt_nblk.p, G.blk_lv.p,
@@ -1942,9 +1955,51 @@ int gn_step(pba_engine* e, double lambda, double* model_decrease, int* solver_st
     skyline_solve_kernel<<<1, 256, 0, e->stream>>>(so);
   }
   PBA_HIP(hipGetLastError());
+  return PBA_OK;
+}
+
+// Schur complement for λ, assembly, solve and candidate state; returns the LM model decrease.
+int gn_step(pba_engine* e, double lambda, double* model_decrease, int* solver_status) {
+  if (int rc = enqueue_solve(e, lambda)) return rc;
   double mp = 0.0, mq = 0.0;
-  if (int rc = finish_step(e, lambda, G.fixed.p, &mp, &mq, solver_status)) return rc;
+  if (int rc = finish_step(e, lambda, e->gn.fixed.p, &mp, &mq, solver_status)) return rc;
   if (model_decrease) *model_decrease = mp + mq;
+  return PBA_OK;
+}
+
+// One LM trial with ONE host synchronisation (single GPU): solve, candidate state, model-decrease partials and the
+// candidate's cost are all enqueued back to back and read with one D2H, instead of three round trips (status,
+// model decrease, cost) — each host round trip left the GPU idle ~30 µs (profiles/r1_c4_v31 kernel trace).  The
+// candidate is evaluated even when the solve failed (its numbers are then discarded): a garbage state is
+// memory-safe in every evaluation kernel (non-finite or out-of-image projections are clamped / out of domain).
+// ev (optional): events recorded at the start, between the candidate state and its cost, and at the end.
+int step_and_candidate_cost(pba_engine* e, double lambda, double* model_decrease, int* solver_status, double* cost,
+                            hipEvent_t* ev) {
+  GnData& G = e->gn;
+  if (ev) PBA_HIP(hipEventRecord(ev[0], e->stream));
+  if (int rc = enqueue_solve(e, lambda)) return rc;
+  int gp = 0, gq = 0;
+  enqueue_updates(e, lambda, G.fixed.p, &gp, &gq);
+  if (ev) PBA_HIP(hipEventRecord(ev[1], e->stream));
+  launch_pairs(e, G.poses_new.p, G.pairs_new.p);
+  if (int rc = launch_cost_only(e, G.pairs_new.p, G.rho_new.p)) return rc;
+  const int gc = std::min(1024, (e->n_blocks + kBlockThreads - 1) / kBlockThreads);
+  cost_reduce_kernel<<<gc, kBlockThreads, 0, e->stream>>>(e->cost.p, e->valid.p, e->n_blocks, G.red.p + 2 * (gp + gq));
+  PBA_HIP(hipGetLastError());
+  if (ev) PBA_HIP(hipEventRecord(ev[2], e->stream));
+  int status = 0;
+  PBA_HIP(hipMemcpyAsync(&status, G.status.p, sizeof(int), hipMemcpyDeviceToHost, e->stream));
+  PBA_HIP(hipMemcpyAsync(G.red_h.data(), G.red.p, sizeof(double) * 2 * (gp + gq + gc), hipMemcpyDeviceToHost,
+                         e->stream));
+  PBA_HIP(hipStreamSynchronize(e->stream));
+  *solver_status = status;
+  double mp = 0.0, mq = 0.0, c = 0.0;
+  if (status == 0) {
+    model_from_slots(G, lambda, gp, gq, &mp, &mq);
+    for (int i = gp + gq; i < gp + gq + gc; ++i) c += G.red_h[2 * i];
+  }
+  *model_decrease = mp + mq;
+  *cost = c;
   return PBA_OK;
 }
 
@@ -2175,6 +2230,17 @@ int lm_loop(pba_engine* e, const pba_solver_options* o, const Reducer* red, pba_
   opt.min_relative_decrease = 1e-3;
   if (o) opt = *o;
   pba_solver_summary s{};
+  struct Events {  // single GPU: step | candidate cost | end, linearisation begin | end
+    hipEvent_t ev[5] = {};
+    ~Events() {
+      for (hipEvent_t x : ev)
+        if (x) (void)hipEventDestroy(x);
+    }
+  } events;
+  hipEvent_t* ev = events.ev;
+  if (!red)
+    for (int i = 0; i < 5; ++i) PBA_HIP(hipEventCreate(&ev[i]));
+  bool lin_pending = false;
   const double t0 = now_ms();
   double cost = 0.0;
   double t = now_ms();
@@ -2192,12 +2258,17 @@ int lm_loop(pba_engine* e, const pba_solver_options* o, const Reducer* red, pba_
     int st = 0;
     t = now_ms();
     if (!red) {
-      if (int rc = gn_step(e, lambda, &model, &st)) return rc;
-      s.solve_ms += now_ms() - t;
-      if (st == 0 && model > 0.0) {
-        t = now_ms();
-        if (int rc = candidate_cost(e, &cost_new)) return rc;
-        s.cost_ms += now_ms() - t;
+      // one synchronisation per trial; the breakdown is device time between events (no extra syncs)
+      if (int rc = step_and_candidate_cost(e, lambda, &model, &st, &cost_new, ev)) return rc;
+      float ms = 0.0f;
+      PBA_HIP(hipEventElapsedTime(&ms, ev[0], ev[1]));
+      s.solve_ms += ms;
+      PBA_HIP(hipEventElapsedTime(&ms, ev[1], ev[2]));
+      s.cost_ms += ms;
+      if (lin_pending) {  // the linearisation enqueued after the previous accepted step ran before ev[0]
+        PBA_HIP(hipEventElapsedTime(&ms, ev[3], ev[4]));
+        s.linearize_ms += ms;
+        lin_pending = false;
       }
     } else {
       if (int rc = step_export(e, lambda, red->band, red->X)) return rc;
@@ -2236,16 +2307,29 @@ int lm_loop(pba_engine* e, const pba_solver_options* o, const Reducer* red, pba_
         ++iter;
         break;
       }
-      t = now_ms();
-      if (int rc = linearize(e, nullptr)) return rc;
-      PBA_HIP(hipStreamSynchronize(e->stream));
-      s.linearize_ms += now_ms() - t;
+      if (!red) {  // enqueued behind the accept; the next trial's synchronisation covers it
+        PBA_HIP(hipEventRecord(ev[3], e->stream));
+        if (int rc = linearize(e, nullptr)) return rc;
+        PBA_HIP(hipEventRecord(ev[4], e->stream));
+        lin_pending = true;
+      } else {
+        t = now_ms();
+        if (int rc = linearize(e, nullptr)) return rc;
+        PBA_HIP(hipStreamSynchronize(e->stream));
+        s.linearize_ms += now_ms() - t;
+      }
     } else {
       ++s.unsuccessful_steps;
       radius /= factor;
       factor *= 2.0;
       if (radius < 1e-32) { s.termination = PBA_TERMINATION_FAILURE; break; }
     }
+  }
+  if (lin_pending) {  // the last accepted step's linearisation (the engine state stays linearised)
+    PBA_HIP(hipStreamSynchronize(e->stream));
+    float ms = 0.0f;
+    PBA_HIP(hipEventElapsedTime(&ms, ev[3], ev[4]));
+    s.linearize_ms += ms;
   }
   s.iterations = iter;
   s.final_cost = cost;
