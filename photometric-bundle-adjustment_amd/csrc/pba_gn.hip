@@ -1743,7 +1743,8 @@ int gn_prepare(pba_engine* e) {
   const int red_pt = (ngp + kBlockThreads - 1) / kBlockThreads;
   G.red_slots = red_pose + red_pt + 1024;  // update partials, then (step_and_candidate_cost) the cost partials
   PBA_HIP(G.red.resize((size_t)2 * G.red_slots));
-  G.red_h.resize(2 * G.red_slots);
+  PBA_HIP(G.red_h.resize(2 * G.red_slots));
+  PBA_HIP(G.status_h.resize(1));
   PBA_HIP(hipMemsetAsync(G.drho.p, 0, sizeof(double) * e->n_points, st));
   PBA_HIP(hipStreamSynchronize(st));
   G.prepared = true;
@@ -1987,11 +1988,11 @@ int step_and_candidate_cost(pba_engine* e, double lambda, double* model_decrease
   cost_reduce_kernel<<<gc, kBlockThreads, 0, e->stream>>>(e->cost.p, e->valid.p, e->n_blocks, G.red.p + 2 * (gp + gq));
   PBA_HIP(hipGetLastError());
   if (ev) PBA_HIP(hipEventRecord(ev[2], e->stream));
-  int status = 0;
-  PBA_HIP(hipMemcpyAsync(&status, G.status.p, sizeof(int), hipMemcpyDeviceToHost, e->stream));
+  PBA_HIP(hipMemcpyAsync(G.status_h.data(), G.status.p, sizeof(int), hipMemcpyDeviceToHost, e->stream));
   PBA_HIP(hipMemcpyAsync(G.red_h.data(), G.red.p, sizeof(double) * 2 * (gp + gq + gc), hipMemcpyDeviceToHost,
                          e->stream));
   PBA_HIP(hipStreamSynchronize(e->stream));
+  const int status = G.status_h[0];
   *solver_status = status;
   double mp = 0.0, mq = 0.0, c = 0.0;
   if (status == 0) {
