@@ -100,8 +100,9 @@ __global__ void tile_images_kernel(const uint8_t* __restrict__ src, uint8_t* __r
 
 // Store a workgroup's contiguous record slab (LDS → global): 16-B non-temporal stores when the slab is 16-B
 // aligned, 4-B or 2-B stores otherwise (odd patterns in fp16).
-template <class T>
+template <class T, int NTH = kBlockThreads>
 __device__ __forceinline__ void store_slab(const unsigned char* src, unsigned char* dst, int bytes) {
+  constexpr int kBlockThreads = NTH;  // the workgroup's threads share the slab
   if ((((uintptr_t)dst | (unsigned)bytes) & 15) == 0) {
     // non-temporal 16-B stores (write-through sc1 stores measured 49 → 71 µs for this kernel; per-lane stores
     // straight from registers, without the LDS slab, 49 → 104 µs: DESIGN.md §3)
@@ -183,6 +184,98 @@ __global__ __launch_bounds__(kBlockThreads) void photometric_block_kernel(const 
   store_slab<T>(lds, reinterpret_cast<unsigned char*>(out + (long long)blk0 * rec_f), nblk * rec_f * (int)sizeof(T));
 }
 
+// Patterns of 9…32 pixels (the 21-px pattern of config C5): still 8 lanes per block, each lane evaluating pixels
+// k, k+8, … (PPL of them), so a wave carries 8 blocks and the per-block prologue (pair record, point) is paid once
+// per 8 blocks — one lane per pixel (32 lanes per block) ran the 21-px C4 shard at 181 µs per launch with a third
+// of its lanes idle and the prologue amortised over 2 blocks per wave.  Rows go to the record stage as they are
+// produced (stage and tile in separate LDS regions); an invalid block's record is zeroed once its validity is known
+// (the same lanes rewrite their own rows: LDS operations of one wave stay in order).  256 threads per workgroup,
+// 128 when the fp32 stage of 32 blocks would not fit the 64 KiB of static LDS.
+template <int PPL, class T>
+constexpr int kMultiThreads = 32 * 14 * 8 * PPL * (int)sizeof(T) + 32 * (int)sizeof(TileBlock) > 60 * 1024 ? 128 : 256;
+
+template <int MODEL, int MODE, class T, int PPL>
+__global__ __launch_bounds__((kMultiThreads<PPL, T>)) void photometric_block_kernel_multi(const KernelArgs a) {
+  constexpr int LPB = 8, NTH = kMultiThreads<PPL, T>, BPW = NTH / LPB;
+  constexpr bool JAC = MODE == 1;
+  constexpr int kStageBytes = JAC ? BPW * 14 * LPB * PPL * (int)sizeof(T) : 0;
+  constexpr int kTileBytes = BPW * (int)sizeof(TileBlock);
+  __shared__ __attribute__((aligned(16))) unsigned char lds[kStageBytes + kTileBytes];
+  __shared__ float2 s_pat[LPB * PPL];
+  T* stage = reinterpret_cast<T*>(lds);
+  TileBlock* s_tb = reinterpret_cast<TileBlock*>(lds + kStageBytes);
+  const int P = a.P;
+  const int rec_f = 14 * P;
+  const int blk0 = logical_tile() * BPW;
+  const int lb = threadIdx.x / LPB;
+  const int k = threadIdx.x % LPB;
+  const int blk = blk0 + lb;
+  const bool live = blk < a.n_blocks;  // a block's LPB lanes agree
+  T* out = reinterpret_cast<T*>(a.out);
+
+  if ((int)threadIdx.x < P) s_pat[threadIdx.x] = make_float2(a.pattern[2 * threadIdx.x], a.pattern[2 * threadIdx.x + 1]);
+  adopt_state(a);
+  const int pt = stage_tile<LPB>(a, s_tb, lb, k, blk, live);
+  float Ih[PPL];
+#pragma unroll
+  for (int j = 0; j < PPL; ++j) {
+    const int px = k + LPB * j;
+    Ih[j] = live && px < P ? a.host_int[(long long)pt * P + px] : 0.0f;
+  }
+  __syncthreads();
+  T* s_rec = stage + lb * rec_f;
+  int okl = 1;
+  float s = 0.0f, rr[PPL];
+#pragma unroll
+  for (int j = 0; j < PPL; ++j) {
+    const int px = k + LPB * j;
+    const bool act = live && px < P;
+    Row row;
+    if (act) row = photometric_row<MODEL, JAC>(a, s_tb[lb], s_pat[px], Ih[j]);
+    okl &= act ? row.ok : 1;
+    s += act ? row.r * row.r : 0.0f;
+    rr[j] = row.r;
+    if (JAC && act) {  // record row px: r | J_host row | J_target row | J_rho
+      T* h = s_rec + P + 6 * px;
+      T* t = s_rec + 7 * P + 6 * px;
+      s_rec[px] = (T)row.r;
+      h[0] = (T)row.hv.x; h[1] = (T)row.hv.y; h[2] = (T)row.hv.z; h[3] = (T)row.hw.x; h[4] = (T)row.hw.y; h[5] = (T)row.hw.z;
+      t[0] = (T)row.tv.x; t[1] = (T)row.tv.y; t[2] = (T)row.tv.z; t[3] = (T)row.tw.x; t[4] = (T)row.tw.y; t[5] = (T)row.tw.z;
+      s_rec[13 * P + px] = (T)row.jr;
+    }
+  }
+  // per-block validity (ballot over the wave: the block's LPB lanes are an aligned bit field) and ‖r‖²
+  const int ok = group_all<LPB>(okl);
+  s = group_sum<LPB>(s);
+  if (live && k == 0) {
+    a.valid[blk] = (uint8_t)ok;
+    a.cost[blk] = ok ? huber_cost(s, a.huber) : 0.0f;
+  }
+  if (MODE == 2) return;
+  if (!JAC) {
+#pragma unroll
+    for (int j = 0; j < PPL; ++j) {
+      const int px = k + LPB * j;
+      if (live && px < P) out[(long long)blk * rec_f + px] = (T)(ok ? rr[j] : 0.0f);
+    }
+    return;
+  }
+  if (live && !ok) {  // an invalid block leaves a zero record (Ceres' Evaluate returning false)
+#pragma unroll
+    for (int j = 0; j < PPL; ++j) {
+      const int px = k + LPB * j;
+      if (px >= P) continue;
+      s_rec[px] = (T)0.0f;
+      s_rec[13 * P + px] = (T)0.0f;
+      for (int q = 0; q < 6; ++q) s_rec[P + 6 * px + q] = s_rec[7 * P + 6 * px + q] = (T)0.0f;
+    }
+  }
+  __syncthreads();
+  const int nblk = min(BPW, a.n_blocks - blk0);
+  if (nblk <= 0) return;
+  store_slab<T, NTH>(lds, reinterpret_cast<unsigned char*>(out + (long long)blk0 * rec_f), nblk * rec_f * (int)sizeof(T));
+}
+
 // ------------------------------------------------------------------------------------------------
 // Geometric block kernel (reprojection.h:105-108): lane = block, record 28 floats = 7 float4 stores
 // ------------------------------------------------------------------------------------------------
@@ -256,20 +349,35 @@ void launch_blocks(pba_engine* e, const KernelArgs& ka, int mode) {
     else geometric_block_kernel<MODEL, false><<<grid, kBlockThreads, 0, e->stream>>>(ka);
     return;
   }
-  const int lpb = e->P <= 8 ? 8 : (e->P <= 16 ? 16 : 32);
-  const long long lanes = (long long)e->n_blocks * lpb;
-  const int grid = (int)((lanes + kBlockThreads - 1) / kBlockThreads);
   const bool h = e->record_format == PBA_RECORD_F16;
-#define PBA_LAUNCH_PH(L)                                                                                             \
-  if (mode == 1 && h) photometric_block_kernel<MODEL, L, 1, _Float16><<<grid, kBlockThreads, 0, e->stream>>>(ka);  \
-  else if (mode == 1) photometric_block_kernel<MODEL, L, 1, float><<<grid, kBlockThreads, 0, e->stream>>>(ka);     \
-  else if (mode == 0 && h) photometric_block_kernel<MODEL, L, 0, _Float16><<<grid, kBlockThreads, 0, e->stream>>>(ka); \
-  else if (mode == 0) photometric_block_kernel<MODEL, L, 0, float><<<grid, kBlockThreads, 0, e->stream>>>(ka);     \
-  else photometric_block_kernel<MODEL, L, 2, float><<<grid, kBlockThreads, 0, e->stream>>>(ka);
-  if (lpb == 8) { PBA_LAUNCH_PH(8) }
-  else if (lpb == 16) { PBA_LAUNCH_PH(16) }
-  else { PBA_LAUNCH_PH(32) }
-#undef PBA_LAUNCH_PH
+  if (e->P <= 8) {
+    const int grid = (int)(((long long)e->n_blocks * 8 + kBlockThreads - 1) / kBlockThreads);
+    if (mode == 1 && h) photometric_block_kernel<MODEL, 8, 1, _Float16><<<grid, kBlockThreads, 0, e->stream>>>(ka);
+    else if (mode == 1) photometric_block_kernel<MODEL, 8, 1, float><<<grid, kBlockThreads, 0, e->stream>>>(ka);
+    else if (mode == 0 && h) photometric_block_kernel<MODEL, 8, 0, _Float16><<<grid, kBlockThreads, 0, e->stream>>>(ka);
+    else if (mode == 0) photometric_block_kernel<MODEL, 8, 0, float><<<grid, kBlockThreads, 0, e->stream>>>(ka);
+    else photometric_block_kernel<MODEL, 8, 2, float><<<grid, kBlockThreads, 0, e->stream>>>(ka);
+    return;
+  }
+  // 9…32 pixels: 8 lanes per block, ⌈P/8⌉ pixels per lane
+#define PBA_LAUNCH_ONE(PPL, M, TT)                                                                      \
+  {                                                                                                     \
+    constexpr int nth = kMultiThreads<PPL, TT>;                                                         \
+    const int grid = (int)(((long long)e->n_blocks * 8 + nth - 1) / nth);                              \
+    photometric_block_kernel_multi<MODEL, M, TT, PPL><<<grid, nth, 0, e->stream>>>(ka);                 \
+  }
+#define PBA_LAUNCH_PPL(PPL)                                        \
+  if (mode == 1 && h) PBA_LAUNCH_ONE(PPL, 1, _Float16)             \
+  else if (mode == 1) PBA_LAUNCH_ONE(PPL, 1, float)                \
+  else if (mode == 0 && h) PBA_LAUNCH_ONE(PPL, 0, _Float16)        \
+  else if (mode == 0) PBA_LAUNCH_ONE(PPL, 0, float)                \
+  else PBA_LAUNCH_ONE(PPL, 2, float)
+  const int ppl = (e->P + 7) / 8;
+  if (ppl == 2) { PBA_LAUNCH_PPL(2) }
+  else if (ppl == 3) { PBA_LAUNCH_PPL(3) }
+  else { PBA_LAUNCH_PPL(4) }
+#undef PBA_LAUNCH_PPL
+#undef PBA_LAUNCH_ONE
 }
 
 void launch_mode(pba_engine* e, const KernelArgs& ka, int mode) {
