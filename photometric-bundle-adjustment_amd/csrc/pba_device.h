@@ -3,8 +3,9 @@
 // Precision split.  The sub-pixel position u = π_t(p) decides which bilinear cell is read and the
 // interpolation weights, so everything from the bearing to (u, v) runs in fp64 (unproject, warp,
 // projection) — an fp32 warp puts ~3e-5 px of rounding into u at 752-px coordinates, which shows up as
-// 1e-4-relative Jacobian noise through the image gradient.  The kernels have ALU to spare (memory-bound),
-// so this costs nothing measurable.  The Jacobian chain (∇I · ∂π/∂p · ∂p/∂δ) and the records are fp32.
+// 1e-4-relative Jacobian noise through the image gradient.  The block kernel is bound by memory latency at
+// full occupancy with its SIMDs ~55–60 % VALU-busy (profiles/r1_c4_v13_sq_counters.json), so the fp64 part is
+// mostly hidden.  The Jacobian chain (∇I · ∂π/∂p · ∂p/∂δ) and the records are fp32.
 //
 // Closed-form tangent Jacobians instead of the reference's dual numbers: the
 // reference differentiates BundleAdjustmentReprojectionCostFunctor (reprojection.h:83-112) with
