@@ -149,8 +149,15 @@ __constant__ const auto kSlotTable = make_slot_table(std::make_integer_sequence<
 // XᵀX = Σ_k x_kᵀx_k as LPB/4 v_mfma_f32_16x16x4f32 steps (operand A = Xᵀ and B = X are the same register:
 // lane l holds X[4s + l/16][l%16]).  Replaces 104 products + a 3-step DPP all-reduce per row (~416 VALU per
 // lane) with 16 MFMAs per wave.
+// The photometric pinhole 8-lane instantiation requests 8 waves per SIMD: the compiler then keeps the accumulator in
+// VGPRs (56, no AGPRs, no spills) instead of 62 VGPRs + 4 AGPRs at 7 waves (linearise 0.101 -> 0.098 ms per LM
+// iteration at C4, tools/ab_bench.sh); the other instantiations would spill under that request.
 template <int KIND, int MODEL, int LPB>
-__global__ __launch_bounds__(kBlockThreads) void linearize_kernel(const KernelArgs a, const LinArgs g) {
+constexpr int kLinWaves = KIND == PBA_RESIDUAL_PHOTOMETRIC && MODEL == CAM_PINHOLE && LPB == 8 ? 8 : 1;
+
+template <int KIND, int MODEL, int LPB>
+__global__ __launch_bounds__(kBlockThreads) __attribute__((amdgpu_waves_per_eu(kLinWaves<KIND, MODEL, LPB>, 8)))
+void linearize_kernel(const KernelArgs a, const LinArgs g) {
   constexpr int BPW = kBlockThreads / LPB;  // blocks per workgroup
   constexpr int BW = 64 / LPB;              // blocks per wave
   constexpr int NVP = 108;                  // 104 products, padded
