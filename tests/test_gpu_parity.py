@@ -171,11 +171,20 @@ def test_large_problem_sampled_parity():
 
 
 def test_pattern_sizes():
-    """Patterns of 1…21 pixels (C5's 21-px pattern) go through the 8/16/32-lane kernel variants."""
+    """Patterns of 1…32 pixels (C5's 21-px pattern; PBA_MAX_PATTERN = 32): one pixel per lane up to 8, then the
+    multi-pixel kernel with ⌈P/8⌉ = 2, 3, 4 pixels per lane (P = 32 in fp32 runs 128-thread workgroups), records,
+    residual-only records and block costs against the oracle."""
     rng = np.random.default_rng(5)
-    for P in (1, 5, 8, 12, 21):
+    for P in (1, 5, 8, 9, 12, 16, 17, 21, 24, 27, 32):
         pat = rng.integers(-3, 4, (P, 2)).astype(np.float32)
         pb = synth.make_problem(n_frames=7, n_points=100, width=376, height=240, pattern=pat, seed=P, border=12)
-        rec, valid, _ = run_engine(pb)
+        rec, valid, costs = run_engine(pb, huber=9.0)
         ref, vref = O.evaluate(pb)
         compare_records(0, P, rec, ref, valid, vref, projected_uv(pb))
+        res_only, valid_r, _ = run_engine(pb, jac=False)
+        assert np.array_equal(valid_r, valid)
+        np.testing.assert_allclose(res_only[:, :P], rec[:, :P], atol=2.55e-3)  # separate instantiations
+        for b in np.flatnonzero(vref):
+            c_ref, _ = O.huber_block(ref[b, :P], 9.0)
+            tol = 2.55e-3 * np.abs(ref[b, :P]).sum() + 1e-5 * abs(c_ref) + 1e-5
+            assert abs(costs[b] - c_ref) <= tol, (P, b, costs[b], c_ref)

@@ -102,7 +102,7 @@ def test_coarse_to_fine_widens_the_basin():
     assert res["single"][0] > 2.0 * res["pyramid"][0], res
 
 
-@pytest.mark.parametrize("P", [8, 21, 5])
+@pytest.mark.parametrize("P", [8, 21, 5, 30])
 def test_fp16_records(P):
     rng = np.random.default_rng(P)
     pat = synth.PATTERN8 if P == 8 else rng.integers(-3, 4, (P, 2)).astype(np.float32)
