@@ -50,6 +50,33 @@ def test_reduced_system_and_step(kind, model, huber, lam):
     assert abs(model_dec - model_ref) <= 1e-3 * abs(model_ref) + 1e-9
 
 
+@pytest.mark.parametrize("P", [12, 21, 32])
+def test_reduced_system_large_patterns(P):
+    """Patterns beyond 8 px (the 16/32-lane linearisation and the multi-pixel candidate-cost kernel): reduced
+    system, step and candidate cost against the dense reference, same tolerances as above."""
+    pat = np.random.default_rng(P).integers(-3, 4, (P, 2)).astype(np.float32)
+    pb = synth.make_problem(n_frames=8, n_points=60, width=376, height=240, pattern=pat, seed=40 + P, border=12)
+    fixed = (0,)
+    lam = 1e-3
+    H, g, cost = GR.linearize(pb, pb.poses, pb.rho, 9.0, fixed)
+    S_ref, gS_ref, dp_ref, dl_ref, model_ref = GR.schur_step(H, g, pb.n_frames, lam, fixed)
+    with make_engine(pb, 9.0, fixed) as eng:
+        c = eng.gn_linearize()
+        model_dec, st = eng.gn_step(lam)
+        assert st == 0
+        S, gS = eng.gn_reduced_system()
+        dp, dl = eng.gn_last_step()
+        c_new = eng.gn_candidate_cost()
+    assert abs(c - cost) <= 1e-5 * cost + 1e-6
+    assert np.abs(S - S_ref).max() <= 1e-4 * np.abs(S_ref).max()
+    assert np.abs(gS - gS_ref).max() <= 1e-4 * np.abs(gS_ref).max() + 1e-9
+    assert np.linalg.norm(dp - dp_ref) <= 1e-3 * np.linalg.norm(dp_ref) + 1e-12
+    assert abs(model_dec - model_ref) <= 1e-3 * abs(model_ref) + 1e-9
+    np_, nr = GR.apply_step(pb.poses, pb.rho, dp, dl)
+    _, _, cost_new_ref = GR.linearize(pb, np_, nr, 9.0, fixed)
+    assert abs(c_new - cost_new_ref) <= 1e-5 * cost_new_ref + 1e-6
+
+
 def test_candidate_cost_and_accept():
     pb = synth.make_problem(n_frames=8, n_points=80, width=376, height=240, seed=21, border=12)
     with make_engine(pb, 9.0, (0,)) as eng:
