@@ -81,6 +81,9 @@ static_assert(pa(0) == 0 && pb(0) == 0 && pa(20) == 5 && pb(20) == 5 && pa(6) ==
 static_assert(pa(57) == 6 && pb(57) == 6 && pa(77) == 11 && pb(77) == 11, "table");
 static_assert(pa(21) == 0 && pb(21) == 6 && pa(56) == 5 && pb(56) == 11, "table");
 
+// LM decision record kept on the device by the single-GPU loop (lm_decide_kernel).
+enum : int { kLmCost = 0, kLmCostNew = 1, kLmModel = 2, kLmRel = 3, kLmAccept = 4, kLmStatus = 5, kLmFields = 6 };
+
 struct LinArgs {
   const int* gn_block;
   const int4* chunk_desc;   // first GN block, count, n_targets, partial offset (floats)
@@ -88,6 +91,7 @@ struct LinArgs {
   float* blk_schur;
   float* part_lin;
   int n_chunks;
+  const double* gate;       // LM decision record (lm_decide_kernel): run only if it accepted; nullptr = always
 };
 
 // ------------------------------------------------------------------------------------------------
@@ -171,6 +175,7 @@ void linearize_kernel(const KernelArgs a, const LinArgs g) {
   __shared__ float2 s_pat[LPB];
   const int chunk = logical_tile();
   if (chunk >= g.n_chunks) return;
+  if (g.gate && g.gate[kLmAccept] == 0.0) return;  // speculative linearisation of a rejected step: nothing to do
   const int4 d = g.chunk_desc[chunk];
   const int first = d.x, count = d.y, n_t = d.z, poff = d.w;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -1463,6 +1468,59 @@ __global__ __launch_bounds__(kBlockThreads) void cost_reduce_kernel(const float*
   block_reduce2(c, v, red + 2 * blockIdx.x);
 }
 
+// The LM trial's decision on the device (trust_region_minimizer.cc semantics, the same sums and order as the host
+// code of the distributed loop): model decrease from the update partials (slots [0, gp + gq)), candidate cost from
+// the cost partials (slots [gp + gq, gp + gq + gc)), accepted when the solve succeeded, the model predicts a
+// decrease and (cost − cost_new) / model > min_relative_decrease.  On acceptance the record's current cost becomes
+// the candidate's.  One workgroup: strided per-thread sums, then a fixed-order tree in LDS (deterministic).
+__global__ __launch_bounds__(256) void lm_decide_kernel(const double* __restrict__ red, int gp, int gq, int gc,
+                                                        const int* __restrict__ status, double lambda, double min_rel,
+                                                        double* __restrict__ lm) {
+  __shared__ double part[5][256];
+  double v[5] = {0, 0, 0, 0, 0};  // dg, dD, qg, qD, c
+  for (int i = threadIdx.x; i < gp + gq + gc; i += 256) {
+    const double a = red[2 * i], b = red[2 * i + 1];
+    if (i < gp) { v[0] += a; v[1] += b; }
+    else if (i < gp + gq) { v[2] += a; v[3] += b; }
+    else v[4] += a;
+  }
+#pragma unroll
+  for (int q = 0; q < 5; ++q) part[q][threadIdx.x] = v[q];
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w)
+#pragma unroll
+      for (int q = 0; q < 5; ++q) part[q][threadIdx.x] += part[q][threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x != 0) return;
+  const double dg = part[0][0], dD = part[1][0], qg = part[2][0], qD = part[3][0], c = part[4][0];
+  const int st = *status;
+  const double model = __dadd_rn(__dmul_rn(0.5, __dsub_rn(__dmul_rn(lambda, dD), dg)),
+                                 __dmul_rn(0.5, __dsub_rn(__dmul_rn(lambda, qD), qg)));
+  const double cost = lm[kLmCost];
+  const double rel = (cost - c) / model;
+  const bool accept = st == 0 && model > 0.0 && rel > min_rel && isfinite(c);
+  lm[kLmCostNew] = c;
+  lm[kLmModel] = model;
+  lm[kLmRel] = rel;
+  lm[kLmAccept] = accept ? 1.0 : 0.0;
+  lm[kLmStatus] = (double)st;
+  if (accept) lm[kLmCost] = c;
+}
+
+// The accepted candidate becomes the state (device-side accept, gated by the decision record).
+__global__ void lm_accept_kernel(const double* __restrict__ lm, const double* __restrict__ poses_new,
+                                 const double* __restrict__ rho_new, double* __restrict__ poses, double* __restrict__ rho,
+                                 int n_pose_d, int n_points) {
+  if (lm[kLmAccept] == 0.0) return;
+  const int n = max(n_pose_d, n_points);
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    if (i < n_pose_d) poses[i] = poses_new[i];
+    if (i < n_points) rho[i] = rho_new[i];
+  }
+}
+
 // ------------------------------------------------------------------------------------------------
 // host side
 // ------------------------------------------------------------------------------------------------
@@ -1751,7 +1809,8 @@ int gn_prepare(pba_engine* e) {
   G.red_slots = red_pose + red_pt + 1024;  // update partials, then (step_and_candidate_cost) the cost partials
   PBA_HIP(G.red.resize((size_t)2 * G.red_slots));
   PBA_HIP(G.red_h.resize(2 * G.red_slots));
-  PBA_HIP(G.status_h.resize(1));
+  PBA_HIP(G.lm.resize(kLmFields));
+  PBA_HIP(G.lm_h.resize(kLmFields));
   PBA_HIP(hipMemsetAsync(G.drho.p, 0, sizeof(double) * e->n_points, st));
   PBA_HIP(hipStreamSynchronize(st));
   G.prepared = true;
@@ -1818,11 +1877,12 @@ int total_cost(pba_engine* e, double* cost, int* n_valid) {
   return PBA_OK;
 }
 
-int linearize(pba_engine* e, double* cost) {
+// gate: the device LM decision record — the kernels then run only if it accepted (speculatively enqueued).
+int linearize(pba_engine* e, double* cost, const double* gate = nullptr) {
   GnData& G = e->gn;
   launch_pairs(e, e->poses.p, e->pairs.p);
   const KernelArgs ka = make_kernel_args(e, e->pairs.p, e->rho.p);
-  LinArgs la{G.gn_block.p, G.chunk_desc.p, G.blk_lt.p, G.blk_schur.p, G.part_lin.p, G.n_chunks};
+  LinArgs la{G.gn_block.p, G.chunk_desc.p, G.blk_lt.p, G.blk_schur.p, G.part_lin.p, G.n_chunks, gate};
   if (e->opt.residual_kind == PBA_RESIDUAL_PHOTOMETRIC) launch_linearize_k<PBA_RESIDUAL_PHOTOMETRIC>(e, ka, la);
   else launch_linearize_k<PBA_RESIDUAL_GEOMETRIC>(e, ka, la);
   PBA_HIP(hipGetLastError());
@@ -1975,39 +2035,41 @@ int gn_step(pba_engine* e, double lambda, double* model_decrease, int* solver_st
   return PBA_OK;
 }
 
-// One LM trial with ONE host synchronisation (single GPU): solve, candidate state, model-decrease partials and the
-// candidate's cost are all enqueued back to back and read with one D2H, instead of three round trips (status,
-// model decrease, cost) — each host round trip left the GPU idle ~30 µs (profiles/r1_c4_v31 kernel trace).  The
-// candidate is evaluated even when the solve failed (its numbers are then discarded): a garbage state is
-// memory-safe in every evaluation kernel (non-finite or out-of-image projections are clamped / out of domain).
-// ev (optional): events recorded at the start, between the candidate state and its cost, and at the end.
-int step_and_candidate_cost(pba_engine* e, double lambda, double* model_decrease, int* solver_status, double* cost,
-                            hipEvent_t* ev) {
+// One LM trial on a single GPU, enqueued whole: solve → candidate state and model-decrease partials → candidate cost
+// → the accept/reject decision on the device (lm_decide_kernel) → read-back of the decision record → gated accept
+// → gated (speculative) linearisation at the new state.  The host waits only for the read-back, so an accepted
+// step's linearisation runs while the host computes the next λ: no host round trip leaves the GPU idle on the
+// accept path (each one cost ~30 µs: profiles/r1_c4_v31 kernel trace).  The candidate is evaluated even when the
+// solve failed (its numbers are then discarded): a garbage state is memory-safe in every evaluation kernel
+// (non-finite or out-of-image projections are clamped / out of domain).  ev: step | candidate cost | decision,
+// then the linearisation's begin | end; ev_read: the read-back.  d receives the decision record (kLm*).
+int lm_trial(pba_engine* e, double lambda, double min_rel, const hipEvent_t* ev, const hipEvent_t* ev_lin,
+             hipEvent_t ev_read, double* d) {
   GnData& G = e->gn;
-  if (ev) PBA_HIP(hipEventRecord(ev[0], e->stream));
+  PBA_HIP(hipEventRecord(ev[0], e->stream));
   if (int rc = enqueue_solve(e, lambda)) return rc;
   int gp = 0, gq = 0;
   enqueue_updates(e, lambda, G.fixed.p, &gp, &gq);
-  if (ev) PBA_HIP(hipEventRecord(ev[1], e->stream));
+  PBA_HIP(hipEventRecord(ev[1], e->stream));
   launch_pairs(e, G.poses_new.p, G.pairs_new.p);
   if (int rc = launch_cost_only(e, G.pairs_new.p, G.rho_new.p)) return rc;
   const int gc = std::min(1024, (e->n_blocks + kBlockThreads - 1) / kBlockThreads);
   cost_reduce_kernel<<<gc, kBlockThreads, 0, e->stream>>>(e->cost.p, e->valid.p, e->n_blocks, G.red.p + 2 * (gp + gq));
+  lm_decide_kernel<<<1, 256, 0, e->stream>>>(G.red.p, gp, gq, gc, G.status.p, lambda, min_rel, G.lm.p);
   PBA_HIP(hipGetLastError());
-  if (ev) PBA_HIP(hipEventRecord(ev[2], e->stream));
-  PBA_HIP(hipMemcpyAsync(G.status_h.data(), G.status.p, sizeof(int), hipMemcpyDeviceToHost, e->stream));
-  PBA_HIP(hipMemcpyAsync(G.red_h.data(), G.red.p, sizeof(double) * 2 * (gp + gq + gc), hipMemcpyDeviceToHost,
-                         e->stream));
-  PBA_HIP(hipStreamSynchronize(e->stream));
-  const int status = G.status_h[0];
-  *solver_status = status;
-  double mp = 0.0, mq = 0.0, c = 0.0;
-  if (status == 0) {
-    model_from_slots(G, lambda, gp, gq, &mp, &mq);
-    for (int i = gp + gq; i < gp + gq + gc; ++i) c += G.red_h[2 * i];
-  }
-  *model_decrease = mp + mq;
-  *cost = c;
+  PBA_HIP(hipEventRecord(ev[2], e->stream));
+  PBA_HIP(hipMemcpyAsync(G.lm_h.data(), G.lm.p, sizeof(double) * kLmFields, hipMemcpyDeviceToHost, e->stream));
+  PBA_HIP(hipEventRecord(ev_read, e->stream));
+  const int npd = 7 * e->n_frames;
+  const int na = std::max(npd, e->n_points);
+  lm_accept_kernel<<<std::min(1024, (na + 255) / 256), 256, 0, e->stream>>>(G.lm.p, G.poses_new.p, G.rho_new.p,
+                                                                             e->poses.p, e->rho.p, npd, e->n_points);
+  e->pairs_fresh = false;
+  PBA_HIP(hipEventRecord(ev_lin[0], e->stream));
+  if (int rc = linearize(e, nullptr, G.lm.p)) return rc;
+  PBA_HIP(hipEventRecord(ev_lin[1], e->stream));
+  PBA_HIP(hipEventSynchronize(ev_read));
+  for (int i = 0; i < kLmFields; ++i) d[i] = G.lm_h[i];
   return PBA_OK;
 }
 
@@ -2229,7 +2291,7 @@ struct Reducer {  // multi-GPU collective context of pba_solve_distributed (null
 // success: radius /= max(1/3, 1 − (2ρ − 1)³), decrease factor 2; failure: radius /= factor, factor *= 2.
 // With a Reducer every cost, model decrease and the reduced system are sums over ranks, so all ranks take
 // the same decisions and the same pose steps.
-int lm_loop(pba_engine* e, const pba_solver_options* o, const Reducer* red, pba_solver_summary* sum) {
+pba_solver_options lm_options(const pba_solver_options* o) {
   pba_solver_options opt{};
   opt.max_iterations = 20;
   opt.initial_trust_region_radius = 1e4;
@@ -2237,24 +2299,93 @@ int lm_loop(pba_engine* e, const pba_solver_options* o, const Reducer* red, pba_
   opt.parameter_tolerance = 1e-8;
   opt.min_relative_decrease = 1e-3;
   if (o) opt = *o;
+  return opt;
+}
+
+// Single GPU: every trial is enqueued whole (lm_trial) and the accept/reject decision is taken on the device, so
+// the host only reads the decision record back; the breakdown is device time between stream events.
+int lm_loop_single(pba_engine* e, const pba_solver_options* o, pba_solver_summary* sum) {
+  GnData& G = e->gn;
+  const pba_solver_options opt = lm_options(o);
   pba_solver_summary s{};
-  struct Events {  // single GPU: step | candidate cost | end, linearisation begin | end
-    hipEvent_t ev[5] = {};
+  struct Events {  // step | candidate cost | decision; read-back; two linearisation (begin, end) pairs
+    hipEvent_t ev[8] = {};
     ~Events() {
       for (hipEvent_t x : ev)
         if (x) (void)hipEventDestroy(x);
     }
   } events;
   hipEvent_t* ev = events.ev;
-  if (!red)
-    for (int i = 0; i < 5; ++i) PBA_HIP(hipEventCreate(&ev[i]));
-  bool lin_pending = false;
+  for (int i = 0; i < 8; ++i) PBA_HIP(hipEventCreate(&ev[i]));
+  const double t0 = now_ms();
+  double cost = 0.0;
+  if (int rc = linearize(e, &cost)) return rc;
+  s.linearize_ms += now_ms() - t0;
+  s.initial_cost = cost;
+  G.lm_h[kLmCost] = cost;  // the device's current cost
+  PBA_HIP(hipMemcpyAsync(G.lm.p, G.lm_h.data(), sizeof(double), hipMemcpyHostToDevice, e->stream));
+  double radius = opt.initial_trust_region_radius, factor = 2.0;
+  int iter = 0, pending = -1;  // pending: event pair of an accepted step's linearisation not yet timed
+  s.termination = PBA_TERMINATION_MAX_ITERATIONS;
+  for (; iter < opt.max_iterations; ++iter) {
+    const double lambda = 1.0 / radius;
+    const hipEvent_t* lin = ev + 4 + 2 * (iter & 1);
+    double d[kLmFields];
+    if (int rc = lm_trial(e, lambda, opt.min_relative_decrease, ev, lin, ev[3], d)) return rc;
+    float ms = 0.0f;
+    PBA_HIP(hipEventElapsedTime(&ms, ev[0], ev[1]));
+    s.solve_ms += ms;
+    PBA_HIP(hipEventElapsedTime(&ms, ev[1], ev[2]));
+    s.cost_ms += ms;
+    if (pending >= 0) {  // the previous accepted step's linearisation ran before this trial's events
+      PBA_HIP(hipEventElapsedTime(&ms, ev[pending], ev[pending + 1]));
+      s.linearize_ms += ms;
+      pending = -1;
+    }
+    if (d[kLmAccept] == 0.0) {  // failed solve, no predicted decrease, or too little actual decrease
+      ++s.unsuccessful_steps;
+      radius /= factor;
+      factor *= 2.0;
+      if (radius < 1e-32) { s.termination = PBA_TERMINATION_FAILURE; break; }
+      continue;
+    }
+    const double cost_new = d[kLmCostNew], rel = d[kLmRel];
+    const double decrease = cost - cost_new;
+    ++s.successful_steps;
+    radius = radius / std::max(1.0 / 3.0, 1.0 - std::pow(2.0 * rel - 1.0, 3));
+    factor = 2.0;
+    cost = cost_new;
+    pending = 4 + 2 * (iter & 1);
+    if (decrease <= opt.function_tolerance * cost) {  // Ceres: |Δcost| ≤ function_tolerance · cost
+      s.termination = PBA_TERMINATION_CONVERGENCE;
+      ++iter;
+      break;
+    }
+  }
+  PBA_HIP(hipStreamSynchronize(e->stream));  // the last trial's accept / linearisation
+  if (pending >= 0) {
+    float ms = 0.0f;
+    PBA_HIP(hipEventElapsedTime(&ms, ev[pending], ev[pending + 1]));
+    s.linearize_ms += ms;
+  }
+  s.iterations = iter;
+  s.final_cost = cost;
+  s.total_ms = now_ms() - t0;
+  if (sum) *sum = s;
+  return PBA_OK;
+}
+
+// Multi-GPU: the reduced system and the costs are all-reduced through the caller's collective between the steps
+// (host-synchronised), so every rank takes the same decisions and the same pose steps.
+int lm_loop(pba_engine* e, const pba_solver_options* o, const Reducer* red, pba_solver_summary* sum) {
+  if (!red) return lm_loop_single(e, o, sum);
+  const pba_solver_options opt = lm_options(o);
+  pba_solver_summary s{};
   const double t0 = now_ms();
   double cost = 0.0;
   double t = now_ms();
   if (int rc = linearize(e, &cost)) return rc;
-  if (red)
-    if (int rc = allreduce_scalars(e, red->X, red->K, red->fn, red->user, &cost, 1)) return rc;
+  if (int rc = allreduce_scalars(e, red->X, red->K, red->fn, red->user, &cost, 1)) return rc;
   s.linearize_ms += now_ms() - t;
   s.initial_cost = cost;
   double radius = opt.initial_trust_region_radius, factor = 2.0;
@@ -2265,36 +2396,21 @@ int lm_loop(pba_engine* e, const pba_solver_options* o, const Reducer* red, pba_
     double model = 0.0, cost_new = 0.0;
     int st = 0;
     t = now_ms();
-    if (!red) {
-      // one synchronisation per trial; the breakdown is device time between events (no extra syncs)
-      if (int rc = step_and_candidate_cost(e, lambda, &model, &st, &cost_new, ev)) return rc;
-      float ms = 0.0f;
-      PBA_HIP(hipEventElapsedTime(&ms, ev[0], ev[1]));
-      s.solve_ms += ms;
-      PBA_HIP(hipEventElapsedTime(&ms, ev[1], ev[2]));
-      s.cost_ms += ms;
-      if (lin_pending) {  // the linearisation enqueued after the previous accepted step ran before ev[0]
-        PBA_HIP(hipEventElapsedTime(&ms, ev[3], ev[4]));
-        s.linearize_ms += ms;
-        lin_pending = false;
-      }
-    } else {
-      if (int rc = step_export(e, lambda, red->band, red->X)) return rc;
-      PBA_HIP(hipStreamSynchronize(e->stream));
-      if (int rc = red->fn(red->user, red->X, (long long)e->n_frames * ex_row(red->K)))
-        return fail(PBA_ERR_DEVICE, "allreduce callback failed (" + std::to_string(rc) + ")");
-      double mp = 0.0, mq = 0.0;
-      if (int rc = step_import(e, lambda, red->band, red->X, &mp, &mq, &st)) return rc;
-      s.solve_ms += now_ms() - t;
-      double v[2] = {mq, 0.0};
-      t = now_ms();
-      if (st == 0)  // st is identical on every rank (same summed system)
-        if (int rc = candidate_cost(e, &v[1])) return rc;
-      if (int rc = allreduce_scalars(e, red->X, red->K, red->fn, red->user, v, 2)) return rc;
-      s.cost_ms += now_ms() - t;
-      model = mp + v[0];
-      cost_new = v[1];
-    }
+    if (int rc = step_export(e, lambda, red->band, red->X)) return rc;
+    PBA_HIP(hipStreamSynchronize(e->stream));
+    if (int rc = red->fn(red->user, red->X, (long long)e->n_frames * ex_row(red->K)))
+      return fail(PBA_ERR_DEVICE, "allreduce callback failed (" + std::to_string(rc) + ")");
+    double mp = 0.0, mq = 0.0;
+    if (int rc = step_import(e, lambda, red->band, red->X, &mp, &mq, &st)) return rc;
+    s.solve_ms += now_ms() - t;
+    double v[2] = {mq, 0.0};
+    t = now_ms();
+    if (st == 0)  // st is identical on every rank (same summed system)
+      if (int rc = candidate_cost(e, &v[1])) return rc;
+    if (int rc = allreduce_scalars(e, red->X, red->K, red->fn, red->user, v, 2)) return rc;
+    s.cost_ms += now_ms() - t;
+    model = mp + v[0];
+    cost_new = v[1];
     if (st != 0 || !(model > 0.0)) {  // non-positive-definite or no predicted decrease: shrink the region
       radius /= factor;
       factor *= 2.0;
@@ -2315,29 +2431,16 @@ int lm_loop(pba_engine* e, const pba_solver_options* o, const Reducer* red, pba_
         ++iter;
         break;
       }
-      if (!red) {  // enqueued behind the accept; the next trial's synchronisation covers it
-        PBA_HIP(hipEventRecord(ev[3], e->stream));
-        if (int rc = linearize(e, nullptr)) return rc;
-        PBA_HIP(hipEventRecord(ev[4], e->stream));
-        lin_pending = true;
-      } else {
-        t = now_ms();
-        if (int rc = linearize(e, nullptr)) return rc;
-        PBA_HIP(hipStreamSynchronize(e->stream));
-        s.linearize_ms += now_ms() - t;
-      }
+      t = now_ms();
+      if (int rc = linearize(e, nullptr)) return rc;
+      PBA_HIP(hipStreamSynchronize(e->stream));
+      s.linearize_ms += now_ms() - t;
     } else {
       ++s.unsuccessful_steps;
       radius /= factor;
       factor *= 2.0;
       if (radius < 1e-32) { s.termination = PBA_TERMINATION_FAILURE; break; }
     }
-  }
-  if (lin_pending) {  // the last accepted step's linearisation (the engine state stays linearised)
-    PBA_HIP(hipStreamSynchronize(e->stream));
-    float ms = 0.0f;
-    PBA_HIP(hipEventElapsedTime(&ms, ev[3], ev[4]));
-    s.linearize_ms += ms;
   }
   s.iterations = iter;
   s.final_cost = cost;

@@ -479,7 +479,8 @@ struct GnData {
   DevBuf<int> status;
   DevBuf<PairRec> pairs_new;
   PinnedBuf<double> red_h;
-  PinnedBuf<int> status_h;
+  DevBuf<double> lm;         // LM decision record of the single-GPU loop (pba_gn.hip: kLm*)
+  PinnedBuf<double> lm_h;
   int red_slots = 0;
 };
 
