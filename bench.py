@@ -237,6 +237,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--gn-iterations", type=int, default=10)
     ap.add_argument("--no-c3", action="store_true", help="skip the C3 Gauss-Newton measurement (configs[2])")
+    ap.add_argument("--no-c5", action="store_true", help="skip the C5-style 21-px / fp16 / pyramid measurement")
     args = ap.parse_args()
 
     import torch
@@ -345,7 +346,7 @@ def main():
     if world == 1 and not args.no_c3 and args.gn_iterations > 0:
         c3 = gn_c3(args.gn_iterations, torch, dev_index, dev)
     c5 = None
-    if world == 1 and not args.no_c3:
+    if world == 1 and not args.no_c5:
         eng.close()  # the headline engine's buffers are not needed any more
         c5 = c5_eval(pb, images, states, args.steps, torch, dev_index, dev)
 

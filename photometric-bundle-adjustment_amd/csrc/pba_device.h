@@ -250,26 +250,44 @@ __host__ __device__ __forceinline__ unsigned texel_index_img(int x, int y, int t
 
 // Bilinear interpolation of a tiled u8 image with Grid2D-style edge clamp (the apron); value and gradient from
 // the same four taps.  u = column, v = row, positions in fp64, value weights in fp32.
-__device__ __forceinline__ void bilinear(const uint8_t* __restrict__ img, int W, int H, int tiles_x, double u,
-                                         double v, float& I, float& gx, float& gy) {
-  u = fmin(fmax(u, -2.0), (double)W + 1.0);
+// Split in two (bilinear_taps → bilinear_eval) for callers that issue several positions' taps before using any;
+// bilinear() is the two back to back.
+struct Taps {
+  double fu, fv;       // cell fractions u − ⌊u⌋, v − ⌊v⌋ (fp64: the gradient needs them exactly)
+  float I00, I10, I01, I11;
+};
+__device__ __forceinline__ Taps bilinear_taps(const uint8_t* __restrict__ img, int W, int H, int tiles_x, double u,
+                                              double v) {
+  u = fmin(fmax(u, -2.0), (double)W + 1.0);  // NaN positions clamp to −2 (maxNum): always an in-bounds read
   v = fmin(fmax(v, -2.0), (double)H + 1.0);
   const double xf = floor(u), yf = floor(v);
-  const float a = (float)(u - xf), b = (float)(v - yf);
   const int xp = (int)xf + kImgPad, yp = (int)yf + kImgPad;  // ∈ [2, W+5] × [2, H+5]
   const unsigned i00 = texel_index(xp, yp, tiles_x);
   const unsigned dx = (xp & 15) == 15 ? (unsigned)(kTileBytes - 15) : 1u;                 // next column
   const unsigned dy = (yp & 7) == 7 ? (unsigned)(tiles_x * kTileBytes - 7 * kTileW) : 16u;  // next row
-  const float I00 = img[i00], I10 = img[i00 + dx];
-  const float I01 = img[i00 + dy], I11 = img[i00 + dy + dx];
-  const float top = I00 + a * (I10 - I00);
-  const float bot = I01 + a * (I11 - I01);
+  Taps t;
+  t.fu = u - xf;
+  t.fv = v - yf;
+  t.I00 = img[i00];
+  t.I10 = img[i00 + dx];
+  t.I01 = img[i00 + dy];
+  t.I11 = img[i00 + dy + dx];
+  return t;
+}
+__device__ __forceinline__ void bilinear_eval(const Taps& t, float& I, float& gx, float& gy) {
+  const float a = (float)t.fu, b = (float)t.fv;
+  const float top = t.I00 + a * (t.I10 - t.I00);
+  const float bot = t.I01 + a * (t.I11 - t.I01);
   I = top + b * (bot - top);
   // ∂I/∂u, ∂I/∂v from exact integer tap differences with fp64 cell fractions: a gradient component near
   // zero is the difference of two O(255) terms, and an fp32 fraction leaves ~1.5e-5 absolute error there
   // (3e-5 relative on J_ρ at P = 1).  Dead code for residual-only callers.
-  gx = (float)fma(v - yf, (double)((I11 - I01) - (I10 - I00)), (double)(I10 - I00));
-  gy = (float)fma(u - xf, (double)((I11 - I10) - (I01 - I00)), (double)(I01 - I00));
+  gx = (float)fma(t.fv, (double)((t.I11 - t.I01) - (t.I10 - t.I00)), (double)(t.I10 - t.I00));
+  gy = (float)fma(t.fu, (double)((t.I11 - t.I10) - (t.I01 - t.I00)), (double)(t.I01 - t.I00));
+}
+__device__ __forceinline__ void bilinear(const uint8_t* __restrict__ img, int W, int H, int tiles_x, double u,
+                                         double v, float& I, float& gx, float& gy) {
+  bilinear_eval(bilinear_taps(img, W, H, tiles_x, u, v), I, gx, gy);
 }
 
 }  // namespace pba

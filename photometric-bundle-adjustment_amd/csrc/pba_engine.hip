@@ -191,6 +191,8 @@ __global__ __launch_bounds__(kBlockThreads) void photometric_block_kernel(const 
 // produced (stage and tile in separate LDS regions); an invalid block's record is zeroed once its validity is known
 // (the same lanes rewrite their own rows: LDS operations of one wave stay in order).  256 threads per workgroup,
 // 128 when the fp32 stage of 32 blocks would not fit the 64 KiB of static LDS.
+__host__ __device__ constexpr int multi_stage_bytes(int bpw, int P, int tsize) { return (bpw * 14 * P * tsize + 15) & ~15; }
+
 template <int PPL, class T>
 constexpr int kMultiThreads = 32 * 14 * 8 * PPL * (int)sizeof(T) + 32 * (int)sizeof(TileBlock) > 60 * 1024 ? 128 : 256;
 
@@ -198,13 +200,13 @@ template <int MODEL, int MODE, class T, int PPL>
 __global__ __launch_bounds__((kMultiThreads<PPL, T>)) void photometric_block_kernel_multi(const KernelArgs a) {
   constexpr int LPB = 8, NTH = kMultiThreads<PPL, T>, BPW = NTH / LPB;
   constexpr bool JAC = MODE == 1;
-  constexpr int kStageBytes = JAC ? BPW * 14 * LPB * PPL * (int)sizeof(T) : 0;
-  constexpr int kTileBytes = BPW * (int)sizeof(TileBlock);
-  __shared__ __attribute__((aligned(16))) unsigned char lds[kStageBytes + kTileBytes];
+  // dynamic LDS sized for the actual P (multi_stage_bytes): the 21-px fp16 stage is 18.4 KB instead of 21 KB for
+  // 24 px, which lets a fifth workgroup onto the CU (LDS is what bounds this kernel's occupancy)
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   __shared__ float2 s_pat[LPB * PPL];
-  T* stage = reinterpret_cast<T*>(lds);
-  TileBlock* s_tb = reinterpret_cast<TileBlock*>(lds + kStageBytes);
   const int P = a.P;
+  T* stage = reinterpret_cast<T*>(lds);
+  TileBlock* s_tb = reinterpret_cast<TileBlock*>(lds + (JAC ? multi_stage_bytes(BPW, P, (int)sizeof(T)) : 0));
   const int rec_f = 14 * P;
   const int blk0 = logical_tile() * BPW;
   const int lb = threadIdx.x / LPB;
@@ -364,7 +366,9 @@ void launch_blocks(pba_engine* e, const KernelArgs& ka, int mode) {
   {                                                                                                     \
     constexpr int nth = kMultiThreads<PPL, TT>;                                                         \
     const int grid = (int)(((long long)e->n_blocks * 8 + nth - 1) / nth);                              \
-    photometric_block_kernel_multi<MODEL, M, TT, PPL><<<grid, nth, 0, e->stream>>>(ka);                 \
+    const size_t lds = (M == 1 ? multi_stage_bytes(nth / 8, e->P, (int)sizeof(TT)) : 0) +              \
+                       (size_t)(nth / 8) * sizeof(TileBlock);                                           \
+    photometric_block_kernel_multi<MODEL, M, TT, PPL><<<grid, nth, lds, e->stream>>>(ka);               \
   }
 #define PBA_LAUNCH_PPL(PPL)                                        \
   if (mode == 1 && h) PBA_LAUNCH_ONE(PPL, 1, _Float16)             \

@@ -84,6 +84,12 @@ def lib():
         return _LIB
     if not os.path.exists(LIB_PATH):
         raise RuntimeError(f"HIP engine library missing: {LIB_PATH} (run __graft_entry__.build())")
+    # torch bundles its own HIP runtime under the same soname: load it first so the engine binds to that one.
+    # Loaded the other way round (engine first), torch's runtime later finds no devices in this process.
+    try:
+        import torch  # noqa: F401  (loads libraries only; no GPU initialisation)
+    except ImportError:
+        pass
     L = C.CDLL(LIB_PATH)
     vp, i32 = C.c_void_p, C.c_int32
     sig = {

@@ -31,7 +31,7 @@ if [ "${PROFILE:-1}" = "1" ]; then
   echo "rocprof kt rc=$rc"; [ $rc -eq 0 ] || exit $rc
   for C in FETCH_SIZE WRITE_SIZE; do
     timeout -k 10 600 rocprofv3 --pmc $C --output-format csv -d gpurun_out/prof_${TAG}_$C -o run -- \
-        python bench.py --steps 5 --warmup 2 --clock-warmup-s 0 --gn-iterations 2 --no-c3 --no-cpu-baseline > gpurun_out/prof_${TAG}_$C.log 2>&1; rc=$?
+        python bench.py --steps 5 --warmup 2 --clock-warmup-s 0 --gn-iterations 2 --no-c3 --no-c5 --no-cpu-baseline > gpurun_out/prof_${TAG}_$C.log 2>&1; rc=$?
     echo "rocprof $C rc=$rc"; [ $rc -eq 0 ] || exit $rc
   done
 fi
