@@ -1,20 +1,24 @@
 #!/usr/bin/env python3
-"""bench.py — photometric residual+Jacobian blocks/s on MI355X (BASELINE.json metric, configs[3] workload).
+"""bench.py — photometric residual+Jacobian blocks/s on MI355X (BASELINE.json metric; configs[3] workload).
 
-Workload per GPU (BASELINE.json configs[3] / SURVEY.md §8d C4): a synthetic 1000-keyframe × 100k-point problem,
-8-pixel DSO pattern, every point observed by the 4 keyframes after its host → 400,000 residual blocks
-(3.2 M pixel residuals), 752×480 u8 images (361 MB), pinhole camera.  One step = one full evaluation of
-every block's residuals and tangent Jacobians (Ceres-mode records, include/pba.h) at a new state that is
-already resident in HBM: state copy + pair kernel + block kernel, all on the engine stream.
+Workload (BASELINE.json configs[3] / SURVEY.md §8d C4): ONE synthetic problem of 1000 host keyframes × 100k points,
+8-pixel DSO pattern, every point observed by the 4 keyframes after its host → 400,000 residual blocks (3.2 M pixel
+residuals), 1004 keyframes of 752×480 u8 images (361 MB), pinhole camera.  One step = one full evaluation of every
+block's residuals and tangent Jacobians (Ceres-mode records, include/pba.h) at a new state already resident in HBM:
+ONE launch (pba_evaluate_state_device — the blocks form their relative poses in the prologue and the launch adopts
+the state).
 
-Multi-GPU (launched by torch.distributed.run): residual blocks shard by host keyframe — each rank owns its
-own 1000-host-keyframe shard (weak scaling) and evaluates it with no data-path collective (the Ceres-mode
-evaluation has no exchange step).  Timing: W warmup steps, then exactly K steps bracketed by
-barrier + synchronize; the MAX over ranks is reported; value = all ranks' blocks ÷ that time.
+Multi-GPU (torch.distributed.run, one rank per GPU): the one problem's residual blocks are sharded by host keyframe
+(distributed.shard_problem: contiguous host ranges balanced by block count); every rank evaluates its shard with no
+data-path collective (the evaluation has no exchange step) → `scaling: "strong"`, value = 400k blocks
+÷ the max-over-ranks time.  The weak-scaling figure (every rank its own full 1000-keyframe problem) is reported under
+"weak" when N > 1.  Timing: a clock warm-up, W warmup steps, then exactly K steps bracketed by barrier + synchronize.
 
-Also reported: the block kernel's roofline position (algorithmic bytes ÷ HIP-event-timed kernel duration,
-on the engine stream) and a CPU baseline (the oracle's dual-number AutoDiff evaluation — the reference's
-Ceres AutoDiff arithmetic restated — timed on a bounded sample of the same workload on this host).
+Also reported: the block kernel's roofline position (algorithmic bytes ÷ HIP-event-timed kernel duration on the engine
+stream); the CPU baseline — the reference's CPU path, real Ceres 2.0.0 (built from the reference's vendored sources
+by oracle/ceres.mk) evaluating AutoDiff cost functions with its ProgramEvaluator on this host's cores, timed by its
+own "Jacobian & residual evaluation" timer on a bounded sample of the same workload; ms per LM iteration of the
+on-device Gauss-Newton (C4 here, C3 = configs[2] in "gn_c3"); and the C5-style 21-px / fp16 / pyramid leg.
 """
 from __future__ import annotations
 
@@ -31,24 +35,9 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 synth = importlib.import_module("photometric-bundle-adjustment_amd.synth")
 engine_mod = importlib.import_module("photometric-bundle-adjustment_amd.engine")
+D = importlib.import_module("photometric-bundle-adjustment_amd.distributed")
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
-
-
-def gpu_noise_images(torch, n, H, W, seed, device):
-    """Independent smooth random u8 textures, generated on the GPU (content irrelevant for throughput)."""
-    import torch.nn.functional as F
-    g = torch.Generator(device=device)
-    g.manual_seed(seed)
-    out = torch.empty((n, H, W), dtype=torch.uint8, device=device)
-    chunk = 100
-    for s in range(0, n, chunk):
-        m = min(chunk, n - s)
-        coarse = torch.rand((m, 1, H // 8 + 2, W // 8 + 2), generator=g, device=device) * 215 + 20
-        img = F.interpolate(coarse, size=(H + 16, W + 16), mode="bilinear", align_corners=False)[:, 0, :H, :W]
-        img = img + torch.randn((m, H, W), generator=g, device=device) * 2.0
-        out[s:s + m] = img.round().clamp(0, 255).to(torch.uint8)
-    return out
 
 
 def algorithmic_bytes_per_block(P: int, K: int, n_frames: int, n_points: int, n_blocks: int) -> float:
@@ -62,41 +51,72 @@ def algorithmic_bytes_per_block(P: int, K: int, n_frames: int, n_points: int, n_
     return idx + point + state + taps + out
 
 
-def cpu_baseline(pb, images_host, budget_s: float, threads: int):
-    """Oracle (dual-number AutoDiff, as Ceres' AutoDiffCostFunction) on a bounded sample of the workload:
-    repeated passes over a block sample until ~budget_s of CPU work has been timed."""
+def host_cores():
+    """Cores this process may use (affinity ∩ cgroup CPU quota), the machine's count and the CPU model."""
+    n_all = os.cpu_count() or 1
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:
+        aff = n_all
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = float(q) / float(per)
+    except (OSError, ValueError):
+        pass
+    usable = max(1, min(aff, int(quota + 0.5) if quota else aff))
+    model = ""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {"usable": usable, "nproc": n_all, "affinity": aff, "cgroup_quota_cpus": quota, "cpu_model": model}
+
+
+def cpu_baseline(pb, images_host, budget_s: float):
+    """The reference's CPU path on a bounded sample of the same workload: real Ceres 2.0.0 (oracle/_ref, built from
+    the reference's vendored sources) — ceres::Solve, LEVENBERG_MARQUARDT + SPARSE_SCHUR, one AutoDiffCostFunction per
+    residual block over the restated PhotometricError functor (bilinear, pinhole), HuberLoss, the reference's
+    LocalParameterizationSE3, num_threads = the usable host cores (map_utils.h:376-381) — timed by Ceres' own
+    "Jacobian & residual evaluation" timer (Solver::Summary).  Sample: the points hosted by the first keyframes."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    import ctypes
-    import oracle as O
-    pbc = synth.Problem(**{**pb.__dict__, "images": images_host})
-    L = O.lib()
-    keep = O._Keep()
-    s = O.make_problem_struct(pbc, keep)
-    poses = keep(pbc.poses, np.float64)
-    rho = keep(pbc.rho, np.float64)
-    out = np.zeros((pbc.n_blocks, 14 * pbc.P), np.float64)
-    valid = np.zeros(pbc.n_blocks, np.uint8)
-
-    def run(n):
-        s.n_blocks = n
-        t0 = time.perf_counter()
-        rc = L.orc_evaluate(ctypes.byref(s), poses.ctypes.data, rho.ctypes.data, 1, out.ctypes.data,
-                            valid.ctypes.data, threads)
-        assert rc == 0
-        return time.perf_counter() - t0
-
-    n = min(pbc.n_blocks, 20000)
-    rate = n / max(run(n), 1e-9)
-    n = int(min(pbc.n_blocks, max(20000, rate * budget_s)))
-    passes, total, done = 0, 0.0, 0
-    while total < budget_s and passes < 1000:
-        total += run(n)
-        done += n
-        passes += 1
-    return {"value": done / total, "unit": "blocks/s", "cores": threads, "kind": "port",
-            "sample": f"{passes} pass(es) over the first {n} of the {pbc.n_blocks} blocks of the same problem "
-                      f"(r + tangent J, P={pbc.P}), {total:.1f} s on {threads} host threads; oracle/oracle.cpp "
-                      f"Jet<15> dual-number AutoDiff (the reference's Ceres AutoDiff arithmetic, restated)"}
+    import ceres_runner as CR
+    cores = host_cores()
+    if not CR.available():
+        return None
+    hosts = 250
+    sel_pts = np.nonzero(pb.point_host < hosts)[0]
+    remap = np.full(pb.n_points, -1, np.int64)
+    remap[sel_pts] = np.arange(len(sel_pts))
+    sel_blk = np.nonzero(remap[pb.block_point] >= 0)[0]
+    nfs = hosts + 4
+    sample = synth.Problem(kind=pb.kind, model=pb.model, width=pb.width, height=pb.height, intrinsics=pb.intrinsics,
+                           frame_cam=pb.frame_cam[:nfs], images=images_host[:nfs], pattern=pb.pattern,
+                           point_host=pb.point_host[sel_pts], u_ref=pb.u_ref[sel_pts],
+                           host_intensity=pb.host_intensity[sel_pts], block_point=remap[pb.block_point[sel_blk]].astype(np.int32),
+                           block_target=pb.block_target[sel_blk], u_obs=None, poses=pb.poses[:nfs], rho=pb.rho[sel_pts])
+    t0 = time.perf_counter()
+    r = CR.run("cpu", sample, iters=2, huber=9.0, threads=cores["usable"], fixed=(0, 1), ftol=0.0)
+    per_eval = r["jacobian_evaluation_s"] / max(r["jacobian_evaluations"], 1)
+    iters = int(min(60, max(2, budget_s / max(per_eval, 1e-3))))
+    if iters > 2:
+        r = CR.run("cpu", sample, iters=iters, huber=9.0, threads=cores["usable"], fixed=(0, 1), ftol=0.0)
+    n_eval = r["jacobian_evaluations"]
+    rate = sample.n_blocks * n_eval / r["jacobian_evaluation_s"]
+    return {"value": rate, "unit": "blocks/s", "cores": r["threads"], "kind": "reference",
+            "per_core": rate / max(r["threads"], 1), "host": cores,
+            "sample": f"{sample.n_blocks} blocks (the points hosted by keyframes 0-{hosts - 1} of the same problem, "
+                      f"{nfs} frames), {n_eval} Jacobian+residual evaluations timed by Ceres' Solver::Summary "
+                      f"({r['jacobian_evaluation_s']:.1f} s of {time.perf_counter() - t0:.1f} s wall) in ceres::Solve "
+                      f"(LM, SPARSE_SCHUR, {r['threads']} threads); real Ceres 2.0.0 ProgramEvaluator + AutoDiff over "
+                      f"the restated photometric functor (the reference's own photometric functor is on its absent "
+                      f"pba2 branch)",
+            "residual_only_blocks_per_s": sample.n_blocks * r["residual_evaluations"] / max(r["residual_evaluation_s"], 1e-9),
+            "linear_solver_s_per_iteration": r["linear_solver_s"] / max(len(r["costs"]) - 1, 1)}
 
 
 def all_reduce_max(torch, dist, values, dev):
@@ -108,13 +128,69 @@ def all_reduce_max(torch, dist, values, dev):
     return t.cpu()
 
 
+def make_states(pb, torch, dev, seed):
+    rng = np.random.default_rng(seed)
+    states = []
+    for _ in range(2):  # alternate two perturbed states so every step evaluates a new point
+        poses = synth.se3_plus(pb.poses, 1e-3 * rng.normal(0, 1, (pb.n_frames, 6)))
+        rho = pb.rho * (1 + 0.01 * rng.normal(0, 1, pb.n_points))
+        states.append((torch.from_numpy(poses).to(dev), torch.from_numpy(rho).to(dev)))
+    return states
+
+
+def time_evaluation(eng, states, steps, warmup, clock_warmup_s, torch, dist, dev):
+    """W warmup steps (after a clock warm-up), then K timed steps bracketed by barrier + synchronize; returns
+    (max-over-ranks elapsed s, max-over-ranks average block-kernel µs, host diagnostics)."""
+    def step(i):  # one launch: pairs formed in the block prologue, state adopted by the same launch
+        p, r = states[i & 1]
+        eng.evaluate_state_device(p.data_ptr(), r.data_ptr(), True, sync=False)
+
+    # clock warm-up (untimed, on top of the W warmup steps): the GPU's clocks take ~0.1 s of load to ramp, and a short
+    # run measured 70 µs per step cold against 54 µs warm (profiles/r1_bench_c4_v27.json)
+    t_w = time.perf_counter()
+    i = 0
+    while time.perf_counter() - t_w < clock_warmup_s:
+        for _ in range(20):
+            step(i)
+            i += 1
+        eng.synchronize()
+    for i in range(warmup):
+        step(i)
+    eng.synchronize()
+    # diagnostic (not the metric): the same steps without the per-launch timing events, and the host's enqueue rate
+    t0 = time.perf_counter()
+    for i in range(steps):
+        step(i)
+    t_enq = time.perf_counter()
+    eng.synchronize()
+    host_diag = {"us_per_step_without_events": 1e6 * (time.perf_counter() - t0) / steps,
+                 "enqueue_us_per_step_without_events": 1e6 * (t_enq - t0) / steps}
+    eng.enable_kernel_timing(True)
+    eng.kernel_timing()  # reset
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        step(i)
+    host_diag["enqueue_us_per_step"] = 1e6 * (time.perf_counter() - t0) / steps
+    eng.synchronize()
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    if dist is not None:
+        dist.barrier()
+    kern_ms, launches = eng.kernel_timing()
+    eng.enable_kernel_timing(False)
+    t = all_reduce_max(torch, dist, [t1 - t0, 1e3 * kern_ms / max(launches, 1)], dev)
+    return float(t[0]), float(t[1]), host_diag
+
+
 def gn_benchmark(eng, iters, torch, dist, dev, world):
     """ms per Levenberg-Marquardt iteration (BASELINE.json metric, part 2) on the same problem, through the
     engine's own LM loop (pba_solve; pba_solve_distributed with an RCCL all-reduce of the banded reduced
     system for N>1).  An iteration = Schur complement + reduced-system solve + candidate cost, plus the
     next linearisation (r, J, Huber, JᵀJ/Jᵀr partials) after an accepted step; function_tolerance = 0 so
     exactly `iters` iterations run.  Two keyframes are held constant (the reference's fixed cameras)."""
-    D = importlib.import_module("photometric-bundle-adjustment_amd.distributed")
     eng.set_fixed_frames(np.array([0, 1], np.int32))
     eng.gn_linearize()  # symbolic analysis (once per problem structure), outside the timed region
     opts = dict(max_iterations=iters, function_tolerance=0.0)
@@ -176,11 +252,11 @@ def gn_c3(iters, torch, dev_index, dev):
 DISK21 = np.array([(dx, dy) for dy in range(-2, 3) for dx in range(-2, 3) if dx * dx + dy * dy <= 5], np.float32)
 
 
-def c5_eval(pb, images, states, steps, torch, dev_index, dev):
-    """BASELINE.json configs[4] (C5) on this GPU's synthetic C4 shard: 21-pixel pattern (the radius-√5 disk), records
-    stored as fp16 (PBA_RECORD_F16), and a 3-level image pyramid built on the device.  Same one-launch step as the
-    headline (evaluate at a new HBM-resident state); the full EuRoC sequence is not in the container, so the
-    images are the shard's synthetic ones."""
+def c5_eval(pb, images, states, steps, warmup, clock_warmup_s, torch, dev_index, dev):
+    """BASELINE.json configs[4] (C5) on the C4 problem: 21-pixel pattern (the radius-√5 disk), records stored as
+    fp16 (PBA_RECORD_F16), and a 3-level image pyramid built on the device.  Same one-launch step and the same clock
+    warm-up / warmup count as the headline; the full EuRoC sequence is not in the container, so the images are the
+    synthetic ones."""
     import copy
     pb5 = copy.copy(pb)
     pb5.pattern = DISK21
@@ -197,29 +273,14 @@ def c5_eval(pb, images, states, steps, torch, dev_index, dev):
         eng.build_pyramid(3)
         eng.synchronize()
         pyr_ms = 1e3 * (time.perf_counter() - t0)
-
-        def step(i):
-            p, r = states[i & 1]
-            eng.evaluate_state_device(p.data_ptr(), r.data_ptr(), True, sync=False)
-
-        for i in range(max(steps // 4, 5)):
-            step(i)
-        eng.synchronize()
-        eng.enable_kernel_timing(True)
-        eng.kernel_timing()
-        t0 = time.perf_counter()
-        for i in range(steps):
-            step(i)
-        eng.synchronize()
-        el = time.perf_counter() - t0
-        kern_ms, launches = eng.kernel_timing()
+        el, kern_us, _ = time_evaluation(eng, states, steps, warmup, clock_warmup_s, torch, None, dev)
     finally:
         eng.close()
     P = DISK21.shape[0]
-    return {"config": f"C5-style: the C4 shard with a {P}-px pattern, fp16 records, 3-level pyramid (synthetic images)",
-            "blocks_per_s": pb.n_blocks * steps / el, "ms_per_step": 1e3 * el / steps,
-            "kernel_avg_us": 1e3 * kern_ms / max(launches, 1), "record_format": "f16", "P": P,
-            "record_bytes_per_block": 2 * 14 * P, "pyramid_levels": 3, "pyramid_build_ms": pyr_ms}
+    return {"config": f"C5-style: the C4 problem with a {P}-px pattern, fp16 records, 3-level pyramid (synthetic images)",
+            "blocks_per_s": pb.n_blocks * steps / el, "ms_per_step": 1e3 * el / steps, "kernel_avg_us": kern_us,
+            "record_format": "f16", "P": P, "record_bytes_per_block": 2 * 14 * P, "pyramid_levels": 3,
+            "pyramid_build_ms": pyr_ms}
 
 
 def main():
@@ -231,13 +292,12 @@ def main():
     ap.add_argument("--frames", type=int, default=1000)
     ap.add_argument("--points", type=int, default=100000)
     ap.add_argument("--targets", type=int, default=4)
-    ap.add_argument("--width", type=int, default=752)
-    ap.add_argument("--height", type=int, default=480)
-    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--cpu-seconds", type=float, default=8.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--gn-iterations", type=int, default=10)
     ap.add_argument("--no-c3", action="store_true", help="skip the C3 Gauss-Newton measurement (configs[2])")
     ap.add_argument("--no-c5", action="store_true", help="skip the C5-style 21-px / fp16 / pyramid measurement")
+    ap.add_argument("--no-weak", action="store_true", help="N > 1: skip the weak-scaling leg")
     args = ap.parse_args()
 
     import torch
@@ -253,122 +313,74 @@ def main():
     dev_index = local_rank % max(torch.cuda.device_count(), 1) if backend != "nccl" else local_rank
     torch.cuda.set_device(dev_index)
     dev = torch.device("cuda", dev_index)
+    dd = None
     if world > 1:
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
         else:
             dist.init_process_group(backend)
+        dd = dist
 
-    # ---- problem shard of this rank --------------------------------------------------------------------
-    # Global keyframe indexing: rank r hosts keyframes [r·F, (r+1)·F); its points are observed by the K
-    # keyframes after their host, so the last K hosts of a shard reach into the next shard (coupled
-    # reduced system for the multi-GPU Gauss-Newton).  Every rank holds all NF = world·F + K poses.
+    # ---- the one C4 problem, sharded by host keyframe (strong scaling) ----------------------------------------
     K, F, Np = args.targets, args.frames, args.points
-    NF = world * F + K
-    pb = synth.make_problem(n_frames=F + K, n_points=Np, K=K, width=args.width, height=args.height, kind="photometric",
-                            model="pinhole", texture="noise", with_images=False, seed=42 + rank)
-    off = rank * F
-    pb.point_host = (pb.point_host + off).astype(np.int32)
-    pb.block_target = (pb.block_target + off).astype(np.int32)
-    pb.frame_cam = np.zeros(NF, np.int32)
-    prng = np.random.default_rng(99)  # same global poses on every rank
-    pb.poses_gt = synth.trajectory(NF)
-    pb.poses = synth.se3_plus(pb.poses_gt, 3e-3 * prng.normal(0, 1, (NF, 6)))
-    images = torch.zeros((NF, args.height, args.width), dtype=torch.uint8, device=dev)
-    images[off:off + F + K] = gpu_noise_images(torch, F + K, args.height, args.width, 1234 + rank, dev)
-    host = torch.from_numpy(pb.point_host.astype(np.int64)).to(dev)
-    uu = torch.from_numpy(pb.u_ref[:, 0].astype(np.int64)).to(dev)[:, None] + torch.from_numpy(pb.pattern[:, 0].astype(np.int64)).to(dev)
-    vv = torch.from_numpy(pb.u_ref[:, 1].astype(np.int64)).to(dev)[:, None] + torch.from_numpy(pb.pattern[:, 1].astype(np.int64)).to(dev)
-    # integer u_ref and integer pattern → the bilinear host sample is exactly the pixel value
-    pb.host_intensity = images[host[:, None], vv, uu].float().cpu().numpy()
-
+    full, images = synth.c4_shard(dev, n_frames=F, n_points=Np, K=K)  # identical on every rank (same seeds)
+    if world > 1:
+        pb, _, _ = D.shard_problem(full, world, rank)
+    else:
+        pb = full
     eng = engine_mod.Engine(synth.PHOTOMETRIC, synth.PINHOLE, device=dev_index, huber_width=9.0)
     eng.set_problem(pb, images_device_ptr=images.data_ptr())
-    n_blocks = pb.n_blocks
-    rng = np.random.default_rng(7 + rank)
-    states = []
-    for _ in range(2):  # alternate two perturbed states so every step evaluates a new point
-        poses = synth.se3_plus(pb.poses, 1e-3 * rng.normal(0, 1, (NF, 6)))
-        rho = pb.rho * (1 + 0.01 * rng.normal(0, 1, Np))
-        states.append((torch.from_numpy(poses).to(dev), torch.from_numpy(rho).to(dev)))
+    states = make_states(pb, torch, dev, 7)
     eng.set_state_device(states[0][0].data_ptr(), states[0][1].data_ptr())
     eng.evaluate(True)
     _, valid = eng.records()
-
-    def step(i):  # one launch: pairs formed in the block prologue, state adopted by the same launch
-        p, r = states[i & 1]
-        eng.evaluate_state_device(p.data_ptr(), r.data_ptr(), True, sync=False)
-
-    # clock warm-up (untimed, on top of the W warmup steps): the GPU's clocks take ~0.1 s of load to ramp, and
-    # a short run measured 70 µs per step cold against 54 µs warm (profiles/r1_bench_c4_v27.json)
-    t_w = time.perf_counter()
-    i = 0
-    while time.perf_counter() - t_w < args.clock_warmup_s:
-        for _ in range(20):
-            step(i)
-            i += 1
-        eng.synchronize()
-    for i in range(args.warmup):
-        step(i)
-    eng.synchronize()
-    # diagnostic (not the metric): the same steps without the per-launch timing events, and the host's enqueue rate
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        step(i)
-    t_enq = time.perf_counter()
-    eng.synchronize()
-    host_diag = {"us_per_step_without_events": 1e6 * (time.perf_counter() - t0) / args.steps,
-                 "enqueue_us_per_step_without_events": 1e6 * (t_enq - t0) / args.steps}
-    eng.enable_kernel_timing(True)
-    eng.kernel_timing()  # reset
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        step(i)
-    host_diag["enqueue_us_per_step"] = 1e6 * (time.perf_counter() - t0) / args.steps
-    eng.synchronize()
-    torch.cuda.synchronize()
-    t1 = time.perf_counter()
-    if world > 1:
-        dist.barrier()
-    elapsed = t1 - t0
-    kern_ms, launches = eng.kernel_timing()
-    t = all_reduce_max(torch, dist if world > 1 else None, [elapsed, kern_ms / max(launches, 1)], dev)
-    elapsed_max, kern_avg_ms = float(t[0]), float(t[1])
+    elapsed, kern_us, host_diag = time_evaluation(eng, states, args.steps, args.warmup, args.clock_warmup_s, torch, dd, dev)
+    kern_us_local = kern_us
 
     gn = None
     if args.gn_iterations > 0:
         eng.set_state(pb.poses, pb.rho)
-        gn = gn_benchmark(eng, args.gn_iterations, torch, dist if world > 1 else None, dev, world)
+        gn = gn_benchmark(eng, args.gn_iterations, torch, dd, dev, world)
+    eng.close()
+
+    weak = None
+    if world > 1 and not args.no_weak:  # every rank its own full-size problem (global keyframe indices)
+        pbw, imw = synth.c4_shard(dev, rank=rank, world=world, n_frames=F, n_points=Np, K=K)
+        engw = engine_mod.Engine(synth.PHOTOMETRIC, synth.PINHOLE, device=dev_index, huber_width=9.0)
+        engw.set_problem(pbw, images_device_ptr=imw.data_ptr())
+        stw = make_states(pbw, torch, dev, 7 + rank)
+        el_w, kern_w, _ = time_evaluation(engw, stw, args.steps, args.warmup, args.clock_warmup_s, torch, dd, dev)
+        engw.close()
+        del imw
+        weak = {"value": pbw.n_blocks * world * args.steps / el_w, "unit": "blocks/s", "ms_per_step": 1e3 * el_w / args.steps,
+                "blocks_per_gpu": pbw.n_blocks, "kernel_avg_us": kern_w,
+                "note": "every rank evaluates its own 1000-host-keyframe x 100k-point problem (per-GPU work fixed)"}
+
     c3 = None
     if world == 1 and not args.no_c3 and args.gn_iterations > 0:
         c3 = gn_c3(args.gn_iterations, torch, dev_index, dev)
     c5 = None
     if world == 1 and not args.no_c5:
-        eng.close()  # the headline engine's buffers are not needed any more
-        c5 = c5_eval(pb, images, states, args.steps, torch, dev_index, dev)
+        c5 = c5_eval(full, images, states, args.steps, args.warmup, args.clock_warmup_s, torch, dev_index, dev)
 
     if rank == 0:
-        ms_per_step = 1e3 * elapsed_max / args.steps
-        total_blocks = n_blocks * world * args.steps
-        value = total_blocks / elapsed_max
-        bpb = algorithmic_bytes_per_block(pb.P, K, NF, Np, n_blocks)
-        achieved = bpb * n_blocks / (kern_avg_ms * 1e-3) / 1e9
+        total_blocks = full.n_blocks
+        ms_per_step = 1e3 * elapsed / args.steps
+        value = total_blocks * args.steps / elapsed
+        bpb = algorithmic_bytes_per_block(pb.P, K, pb.n_frames, pb.n_points, pb.n_blocks)
+        achieved = bpb * pb.n_blocks / (kern_us_local * 1e-6) / 1e9
         traffic = None
         tf = os.path.join(ROOT, "profiles", "traffic_photometric_block_kernel.json")
         if os.path.exists(tf):
             try:
                 tj = json.load(open(tf))
-                if tj.get("n_blocks") == n_blocks and tj.get("P") == pb.P:
+                if tj.get("n_blocks") == pb.n_blocks and tj.get("P") == pb.P:
                     traffic = tj.get("hbm_bytes_per_launch")
             except Exception:
                 traffic = None
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
-            threads = max(1, min(16, os.cpu_count() or 1))
-            cpu = cpu_baseline(pb, images.cpu().numpy(), args.cpu_seconds, threads)  # N=1: all NF frames local
+            cpu = cpu_baseline(full, images.cpu().numpy(), args.cpu_seconds)
         out = {
             "metric": "photometric residual+jacobian blocks/sec",
             "value": value,
@@ -378,17 +390,19 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": ms_per_step,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong",
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic",
             "config": {
-                "workload": f"C4 shard per GPU: synthetic {F} host keyframes x {Np} points x {pb.P}-px patch x {K} targets "
-                            f"= {n_blocks} residual blocks, {args.width}x{args.height} u8 images, pinhole; one step = "
-                            f"full r + tangent-J evaluation (Ceres-mode records) at a new HBM-resident state",
-                "keyframes": F, "keyframes_global": NF, "points": Np, "patch": pb.P, "targets_per_point": K, "blocks_per_gpu": n_blocks,
-                "valid_blocks": int(valid.sum()), "parallelism": f"host-keyframe shards x{world} (evaluation: no data-path collective; "
-                                               f"GN: RCCL all-reduce of the reduced camera system)",
+                "workload": f"C4: one synthetic problem of {F} host keyframes x {Np} points x {pb.P}-px patch x {K} "
+                            f"targets = {total_blocks} residual blocks, {full.width}x{full.height} u8 images, pinhole; one "
+                            f"step = full r + tangent-J evaluation (Ceres-mode records) at a new HBM-resident state"
+                            + (f", sharded by host keyframe over {world} GPUs" if world > 1 else ""),
+                "keyframes": F, "keyframes_global": full.n_frames, "points": Np, "patch": pb.P, "targets_per_point": K,
+                "blocks_total": total_blocks, "blocks_rank0": pb.n_blocks, "valid_blocks_rank0": int(valid.sum()),
+                "parallelism": f"host-keyframe shards x{world} (evaluation: no data-path collective; "
+                               f"GN: RCCL all-reduce of the reduced camera system)",
             },
             "roofline": {
                 "bound": "hbm",
@@ -399,16 +413,16 @@ def main():
                 "frac": achieved / HBM_PEAK_GBS,
                 "traffic": traffic,
                 "bytes_per_block_alg": bpb,
-                "kernel_avg_us": kern_avg_ms * 1e3,
+                "kernel_avg_us": kern_us_local,
             },
             "cpu_baseline": cpu,
             "gn": gn,
             "gn_c3": c3,
             "c5": c5,
+            "weak": weak,
             "host": {k: round(v, 2) for k, v in host_diag.items()},
         }
         print(json.dumps(out), flush=True)
-    eng.close()
     if world > 1:
         dist.destroy_process_group()
 

@@ -130,6 +130,14 @@ int pba_num_frames(const pba_engine* engine);
 int pba_residuals_per_block(const pba_engine* engine);
 /* records: n_blocks·record_floats floats; valid: n_blocks bytes (either may be NULL).  Synchronises. */
 int pba_get_records(pba_engine* engine, float* records, uint8_t* valid);
+/* residuals only: n_blocks·R floats (the first R values of every record, one strided DMA copy instead of the
+ * whole record — what a residual-only evaluation needs, trust_region_minimizer.cc:761-779); valid may be NULL.
+ * Synchronises. */
+int pba_get_residuals(pba_engine* engine, float* residuals, uint8_t* valid);
+/* page-locked host memory for the read-back buffers of an adapter (records / residuals then arrive by DMA at
+ * full PCIe rate instead of being staged through a driver buffer) */
+int pba_host_alloc(size_t bytes, void** ptr);
+int pba_host_free(void* ptr);
 /* per-block cost ½ρ(‖r‖²) with the engine's Huber width (0 for invalid blocks) */
 int pba_get_block_costs(pba_engine* engine, float* costs);
 /* Σ block costs, summed in double on the host; n_valid may be NULL */
@@ -154,7 +162,9 @@ int pba_get_kernel_timing(pba_engine* engine, double* total_ms, int32_t* launche
  * structure of schur_complement_solver.cc:138-146), and the reduced camera system is factorised on the
  * device (block-skyline Cholesky, fp64).  Damping follows levenberg_marquardt_strategy.cc: (H + λ·D)δ = −g
  * with D = diag(JᵀJ) clamped to [1e-6, 1e32], λ = 1/trust-region radius. */
-#define PBA_TERMINATION_CONVERGENCE 0     /* |Δcost| ≤ function_tolerance · cost */
+#define PBA_TERMINATION_CONVERGENCE 0     /* a valid step with |cost − candidate cost| ≤ function_tolerance · cost
+                                           * (trust_region_minimizer.cc:115-117, :729-750); that step is NOT applied.
+                                           * Ceres' parameter/gradient tolerances are not evaluated. */
 #define PBA_TERMINATION_MAX_ITERATIONS 1
 #define PBA_TERMINATION_FAILURE 2         /* trust region collapsed */
 

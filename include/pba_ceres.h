@@ -7,7 +7,8 @@
 //                          Problem::Options::evaluation_callback (problem.h:185).  On the solver thread,
 //                          after Ceres copied the state into the user's T_w_c / inv_depth memory
 //                          (program_evaluator.h:157-162), it gathers poses and inverse distances, uploads
-//                          them and evaluates all blocks (pba_evaluate), then copies the records back.
+//                          them and evaluates all blocks (pba_evaluate), then copies the records (or, for a
+//                          residual-only evaluation, just the residuals) back into page-locked memory.
 //   * GpuBlockCost<R,…>  : ceres::SizedCostFunction per block.  Evaluate() is a re-entrant copy out of the
 //                          evaluator's record buffer (Ceres calls it from num_threads workers,
 //                          program_evaluator.h:187-229); returns false for invalid blocks like a functor
@@ -85,6 +86,33 @@ class SE3TangentParameterization : public ceres::LocalParameterization {
   int LocalSize() const override { return 6; }
 };
 
+// Page-locked host array from the engine library (pba_host_alloc): the per-evaluation read-backs are DMA copies.
+template <class T>
+class PinnedArray {
+ public:
+  PinnedArray() = default;
+  PinnedArray(const PinnedArray&) = delete;
+  PinnedArray& operator=(const PinnedArray&) = delete;
+  ~PinnedArray() { pba_host_free(p_); }
+  void resize(size_t n) {
+    if (n <= n_ && p_) return;
+    pba_host_free(p_);
+    p_ = nullptr;
+    n_ = 0;
+    void* q = nullptr;
+    check(pba_host_alloc(n * sizeof(T), &q), "pba_host_alloc");
+    p_ = static_cast<T*>(q);
+    n_ = n;
+  }
+  T* data() { return p_; }
+  const T* data() const { return p_; }
+  const T& operator[](size_t i) const { return p_[i]; }
+
+ private:
+  T* p_ = nullptr;
+  size_t n_ = 0;
+};
+
 class GpuEvaluator : public ceres::EvaluationCallback {
  public:
   // poses[f] = T_w_c.data() of keyframe f (7 doubles, user memory Ceres optimises in place);
@@ -95,6 +123,11 @@ class GpuEvaluator : public ceres::EvaluationCallback {
     rec_ = pba_record_floats(engine_);
   }
 
+  // Called on the solver thread after Ceres has written the evaluation point into the user's parameter memory
+  // (program_evaluator.h:157-162).  A Jacobian evaluation reads back the whole records; a residual-only one (the
+  // LM candidate, trust_region_minimizer.cc:761-779) only the residuals, R of every 14R record values.  The
+  // evaluation after an accepted step comes with new_evaluation_point = false (trust_region_minimizer.cc:805-822):
+  // when the point was already evaluated with Jacobians nothing is recomputed.
   void PrepareForEvaluation(bool evaluate_jacobians, bool new_evaluation_point) override {
     if (!new_evaluation_point && have_point_ && (have_jac_ || !evaluate_jacobians)) return;
     state_p_.resize(7 * poses_.size());
@@ -104,15 +137,25 @@ class GpuEvaluator : public ceres::EvaluationCallback {
     check(pba_set_state(engine_, state_p_.data(), state_r_.data()), "pba_set_state");
     check(pba_evaluate(engine_, evaluate_jacobians ? 1 : 0), "pba_evaluate");
     const size_t nb = (size_t)pba_num_blocks(engine_);
-    records_.resize(nb * rec_);
     valid_.resize(nb);
-    check(pba_get_records(engine_, records_.data(), valid_.data()), "pba_get_records");
+    if (evaluate_jacobians) {
+      records_.resize(nb * rec_);
+      check(pba_get_records(engine_, records_.data(), valid_.data()), "pba_get_records");
+      res_ = records_.data();
+      res_stride_ = rec_;
+    } else {
+      residuals_.resize(nb * R_);
+      check(pba_get_residuals(engine_, residuals_.data(), valid_.data()), "pba_get_residuals");
+      res_ = residuals_.data();
+      res_stride_ = R_;
+    }
     have_point_ = true;
     have_jac_ = evaluate_jacobians;
   }
 
   int residuals_per_block() const { return R_; }
-  const float* record(int block) const { return &records_[(size_t)block * rec_]; }
+  const float* record(int block) const { return records_.data() + (size_t)block * rec_; }  // with has_jacobians()
+  const float* residuals(int block) const { return res_ + (size_t)block * res_stride_; }
   bool valid(int block) const { return valid_[block] != 0; }
   bool has_jacobians() const { return have_jac_; }
 
@@ -120,8 +163,10 @@ class GpuEvaluator : public ceres::EvaluationCallback {
   pba_engine* engine_;
   std::vector<double*> poses_, rho_;
   std::vector<double> state_p_, state_r_;
-  std::vector<float> records_;
-  std::vector<uint8_t> valid_;
+  PinnedArray<float> records_, residuals_;
+  PinnedArray<uint8_t> valid_;
+  const float* res_ = nullptr;
+  int res_stride_ = 0;
   int R_ = 0, rec_ = 0;
   bool have_point_ = false, have_jac_ = false;
 };
@@ -131,10 +176,11 @@ class GpuEvaluator : public ceres::EvaluationCallback {
 // reference, map_utils.h:340-345; its Jacobian is reported as zero).
 inline bool copy_block(const GpuEvaluator& ev, int block, int R, double* residuals, double** jacobians, int n_intr) {
   if (!ev.valid(block)) return false;
-  const float* rec = ev.record(block);
-  for (int k = 0; k < R; ++k) residuals[k] = rec[k];
+  const float* res = ev.residuals(block);
+  for (int k = 0; k < R; ++k) residuals[k] = res[k];
   if (!jacobians) return true;
   if (!ev.has_jacobians()) return false;  // Ceres asked for J at a point evaluated residual-only
+  const float* rec = ev.record(block);
   for (int k = 0; k < R; ++k) {
     if (jacobians[0]) {
       for (int c = 0; c < 6; ++c) jacobians[0][k * 7 + c] = rec[R + 6 * k + c];

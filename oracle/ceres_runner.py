@@ -1,0 +1,43 @@
+"""TEST-ONLY: runs tests/cpp/ceres_lm_driver (the real Ceres 2.0.0 LM solve of map_utils.h:322-383, built by
+oracle/ceres.mk into oracle/_ref/) on a synthetic problem, in its CPU (the reference's AutoDiff path) or GPU
+(include/pba_ceres.h over the engine) mode, and returns the parsed JSON summary.  Used by tests/ and by bench.py's
+cpu_baseline leg (Ceres' own "Jacobian & residual evaluation" timer)."""
+from __future__ import annotations
+
+import json
+import os
+import subprocess
+import sys
+import tempfile
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+DRIVER = os.path.join(ROOT, "oracle", "_ref", "ceres_lm_driver")
+ADAPTER_DRIVER = os.path.join(ROOT, "oracle", "_ref", "adapter_driver")
+sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
+
+
+def available() -> bool:
+    return os.path.exists(DRIVER)
+
+
+def run(mode: str, pb, iters: int = 20, huber: float = 1.0, threads: int = 8, fixed=(0, 1), ftol: float = 1e-6,
+        timeout: float = 600.0) -> dict:
+    from make_golden import write_problem
+    with tempfile.TemporaryDirectory() as td:
+        fin, fout = os.path.join(td, "in.bin"), os.path.join(td, "out.json")
+        with open(fin, "wb") as f:
+            write_problem(f, pb)
+        fx = ",".join(str(int(i)) for i in fixed) if len(fixed) else "-"
+        subprocess.run([DRIVER, mode, fin, fout, str(iters), repr(float(huber)), str(threads), fx, repr(float(ftol))],
+                       check=True, timeout=timeout)
+        with open(fout) as f:
+            out = json.load(f)
+    out["poses"] = np.asarray(out["poses"]).reshape(-1, 7)
+    out["rho"] = np.asarray(out["rho"])
+    it = np.asarray(out["iterations"], np.float64).reshape(-1, 5)
+    out["costs"] = it[:, 1]
+    out["step_ok"] = it[:, 2].astype(bool)
+    out["relative_decrease"] = it[:, 3]
+    return out

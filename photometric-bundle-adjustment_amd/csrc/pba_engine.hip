@@ -764,8 +764,8 @@ int evaluate_at(pba_engine* e, const double* poses, const double* rho, bool adop
   if (int rc = check_device(e)) return rc;
   KernelArgs ka;
   if (photometric) {
-    const int lpb = e->P <= 8 ? 8 : (e->P <= 16 ? 16 : 32);
-    const long long lanes = (long long)e->n_blocks * lpb;  // the launch's lanes (whole workgroups)
+    // every photometric launch runs 8 lanes per block (photometric_block_kernel / _multi, launch_blocks)
+    const long long lanes = (long long)e->n_blocks * 8;
     if (adopt && lanes < std::max<long long>(7LL * e->n_frames, e->n_points)) {
       if (int rc = pba_set_state_device(e, poses, rho)) return rc;  // more state than lanes: copy first
       poses = e->poses.p;
@@ -886,6 +886,41 @@ int pba_get_records(pba_engine* e, float* records, uint8_t* valid) {
   if (valid) PBA_HIP(hipMemcpyAsync(valid, e->valid.p, e->n_blocks, hipMemcpyDeviceToHost, e->stream));
   PBA_HIP(hipStreamSynchronize(e->stream));
   for (size_t i = 0; i < half.size(); ++i) records[i] = (float)half[i];
+  return PBA_OK;
+}
+
+int pba_get_residuals(pba_engine* e, float* residuals, uint8_t* valid) {
+  if (!e) return fail(PBA_ERR_INVALID_ARGUMENT, "null engine");
+  if (!e->evaluated) return fail(PBA_ERR_NOT_READY, "pba_evaluate first");
+  if (int rc = check_device(e)) return rc;
+  const size_t R = (size_t)e->R(), nb = (size_t)e->n_blocks;
+  std::vector<_Float16> half;
+  if (residuals && nb) {
+    // the first R values of every 14R-value record: one pitched device-to-host copy
+    if (e->record_format == PBA_RECORD_F16) {
+      half.resize(nb * R);
+      PBA_HIP(hipMemcpy2DAsync(half.data(), R * sizeof(_Float16), e->out.p, 14 * R * sizeof(_Float16),
+                               R * sizeof(_Float16), nb, hipMemcpyDeviceToHost, e->stream));
+    } else {
+      PBA_HIP(hipMemcpy2DAsync(residuals, R * sizeof(float), e->out.p, 14 * R * sizeof(float), R * sizeof(float), nb,
+                               hipMemcpyDeviceToHost, e->stream));
+    }
+  }
+  if (valid) PBA_HIP(hipMemcpyAsync(valid, e->valid.p, nb, hipMemcpyDeviceToHost, e->stream));
+  PBA_HIP(hipStreamSynchronize(e->stream));
+  for (size_t i = 0; i < half.size(); ++i) residuals[i] = (float)half[i];
+  return PBA_OK;
+}
+
+int pba_host_alloc(size_t bytes, void** ptr) {
+  if (!ptr) return fail(PBA_ERR_INVALID_ARGUMENT, "null argument");
+  *ptr = nullptr;
+  PBA_HIP(hipHostMalloc(ptr, bytes ? bytes : 1, hipHostMallocDefault));
+  return PBA_OK;
+}
+
+int pba_host_free(void* ptr) {
+  if (ptr) PBA_HIP(hipHostFree(ptr));
   return PBA_OK;
 }
 

@@ -82,7 +82,7 @@ static_assert(pa(57) == 6 && pb(57) == 6 && pa(77) == 11 && pb(77) == 11, "table
 static_assert(pa(21) == 0 && pb(21) == 6 && pa(56) == 5 && pb(56) == 11, "table");
 
 // LM decision record kept on the device by the single-GPU loop (lm_decide_kernel).
-enum : int { kLmCost = 0, kLmCostNew = 1, kLmModel = 2, kLmRel = 3, kLmAccept = 4, kLmStatus = 5, kLmFields = 6 };
+enum : int { kLmCost = 0, kLmCostNew = 1, kLmModel = 2, kLmRel = 3, kLmAccept = 4, kLmStatus = 5, kLmConverged = 6, kLmFields = 7 };
 
 struct LinArgs {
   const int* gn_block;
@@ -1475,7 +1475,7 @@ __global__ __launch_bounds__(kBlockThreads) void cost_reduce_kernel(const float*
 // the candidate's.  One workgroup: strided per-thread sums, then a fixed-order tree in LDS (deterministic).
 __global__ __launch_bounds__(256) void lm_decide_kernel(const double* __restrict__ red, int gp, int gq, int gc,
                                                         const int* __restrict__ status, double lambda, double min_rel,
-                                                        double* __restrict__ lm) {
+                                                        double ftol, double* __restrict__ lm) {
   __shared__ double part[5][256];
   double v[5] = {0, 0, 0, 0, 0};  // dg, dD, qg, qD, c
   for (int i = threadIdx.x; i < gp + gq + gc; i += 256) {
@@ -1500,7 +1500,11 @@ __global__ __launch_bounds__(256) void lm_decide_kernel(const double* __restrict
                                  __dmul_rn(0.5, __dsub_rn(__dmul_rn(lambda, qD), qg)));
   const double cost = lm[kLmCost];
   const double rel = (cost - c) / model;
-  const bool accept = st == 0 && model > 0.0 && rel > min_rel && isfinite(c);
+  // a valid step whose cost change is within the function tolerance ends the solve WITHOUT being applied
+  // (trust_region_minimizer.cc:115-117, FunctionToleranceReached :729-750, checked before IsStepSuccessful)
+  const bool converged = st == 0 && model > 0.0 && fabs(cost - c) <= ftol * cost;
+  const bool accept = st == 0 && model > 0.0 && rel > min_rel && isfinite(c) && !converged;
+  lm[kLmConverged] = converged ? 1.0 : 0.0;
   lm[kLmCostNew] = c;
   lm[kLmModel] = model;
   lm[kLmRel] = rel;
@@ -1509,15 +1513,20 @@ __global__ __launch_bounds__(256) void lm_decide_kernel(const double* __restrict
   if (accept) lm[kLmCost] = c;
 }
 
-// The accepted candidate becomes the state (device-side accept, gated by the decision record).
+// The accepted candidate becomes the state (device-side accept, gated by the decision record; lm == nullptr: always).
+// Only the points of the Gauss-Newton problem are copied (through pt_orig): rho_new holds nothing for a point with
+// no residual block, and such a point keeps its state, as a parameter Ceres never sees would.
 __global__ void lm_accept_kernel(const double* __restrict__ lm, const double* __restrict__ poses_new,
-                                 const double* __restrict__ rho_new, double* __restrict__ poses, double* __restrict__ rho,
-                                 int n_pose_d, int n_points) {
-  if (lm[kLmAccept] == 0.0) return;
-  const int n = max(n_pose_d, n_points);
+                                 const double* __restrict__ rho_new, const int* __restrict__ pt_orig,
+                                 double* __restrict__ poses, double* __restrict__ rho, int n_pose_d, int n_gn_points) {
+  if (lm && lm[kLmAccept] == 0.0) return;
+  const int n = max(n_pose_d, n_gn_points);
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
     if (i < n_pose_d) poses[i] = poses_new[i];
-    if (i < n_points) rho[i] = rho_new[i];
+    if (i < n_gn_points) {
+      const int o = pt_orig[i];
+      rho[o] = rho_new[o];
+    }
   }
 }
 
@@ -1901,12 +1910,9 @@ template <int M>
 void cr_solve(pba_engine* e) {
   GnData& G = e->gn;
   if (cr_level_lds<M>() > 65536) {  // above the default dynamic-LDS limit (gfx950 has 160 KiB per CU)
-    static bool raised = false;
-    if (!raised) {
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&cr_level_kernel<M>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)cr_level_lds<M>());
-      raised = true;
-    }
+    // the attribute is per device: set it on every solve (cheap) rather than once per process
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&cr_level_kernel<M>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)cr_level_lds<M>());
   }
   const int nl = (int)G.cr_levels.size();
   CrLevel L0 = cr_level(G, 0);
@@ -2035,6 +2041,16 @@ int gn_step(pba_engine* e, double lambda, double* model_decrease, int* solver_st
   return PBA_OK;
 }
 
+// state ← candidate (poses, and the inverse distances of the Gauss-Newton points), gated by lm when given
+void launch_accept(pba_engine* e, const double* lm) {
+  GnData& G = e->gn;
+  const int npd = 7 * e->n_frames;
+  const int na = std::max(npd, G.n_gn_points);
+  lm_accept_kernel<<<std::min(1024, (na + 255) / 256), 256, 0, e->stream>>>(lm, G.poses_new.p, G.rho_new.p, G.pt_orig.p,
+                                                                             e->poses.p, e->rho.p, npd, G.n_gn_points);
+  e->pairs_fresh = false;
+}
+
 // One LM trial on a single GPU, enqueued whole: solve → candidate state and model-decrease partials → candidate cost
 // → the accept/reject decision on the device (lm_decide_kernel) → read-back of the decision record → gated accept
 // → gated (speculative) linearisation at the new state.  The host waits only for the read-back, so an accepted
@@ -2043,7 +2059,7 @@ int gn_step(pba_engine* e, double lambda, double* model_decrease, int* solver_st
 // solve failed (its numbers are then discarded): a garbage state is memory-safe in every evaluation kernel
 // (non-finite or out-of-image projections are clamped / out of domain).  ev: step | candidate cost | decision,
 // then the linearisation's begin | end; ev_read: the read-back.  d receives the decision record (kLm*).
-int lm_trial(pba_engine* e, double lambda, double min_rel, const hipEvent_t* ev, const hipEvent_t* ev_lin,
+int lm_trial(pba_engine* e, double lambda, double min_rel, double ftol, const hipEvent_t* ev, const hipEvent_t* ev_lin,
              hipEvent_t ev_read, double* d) {
   GnData& G = e->gn;
   PBA_HIP(hipEventRecord(ev[0], e->stream));
@@ -2055,16 +2071,12 @@ int lm_trial(pba_engine* e, double lambda, double min_rel, const hipEvent_t* ev,
   if (int rc = launch_cost_only(e, G.pairs_new.p, G.rho_new.p)) return rc;
   const int gc = std::min(1024, (e->n_blocks + kBlockThreads - 1) / kBlockThreads);
   cost_reduce_kernel<<<gc, kBlockThreads, 0, e->stream>>>(e->cost.p, e->valid.p, e->n_blocks, G.red.p + 2 * (gp + gq));
-  lm_decide_kernel<<<1, 256, 0, e->stream>>>(G.red.p, gp, gq, gc, G.status.p, lambda, min_rel, G.lm.p);
+  lm_decide_kernel<<<1, 256, 0, e->stream>>>(G.red.p, gp, gq, gc, G.status.p, lambda, min_rel, ftol, G.lm.p);
   PBA_HIP(hipGetLastError());
   PBA_HIP(hipEventRecord(ev[2], e->stream));
   PBA_HIP(hipMemcpyAsync(G.lm_h.data(), G.lm.p, sizeof(double) * kLmFields, hipMemcpyDeviceToHost, e->stream));
   PBA_HIP(hipEventRecord(ev_read, e->stream));
-  const int npd = 7 * e->n_frames;
-  const int na = std::max(npd, e->n_points);
-  lm_accept_kernel<<<std::min(1024, (na + 255) / 256), 256, 0, e->stream>>>(G.lm.p, G.poses_new.p, G.rho_new.p,
-                                                                             e->poses.p, e->rho.p, npd, e->n_points);
-  e->pairs_fresh = false;
+  launch_accept(e, G.lm.p);
   PBA_HIP(hipEventRecord(ev_lin[0], e->stream));
   if (int rc = linearize(e, nullptr, G.lm.p)) return rc;
   PBA_HIP(hipEventRecord(ev_lin[1], e->stream));
@@ -2081,10 +2093,8 @@ int candidate_cost(pba_engine* e, double* cost) {
 }
 
 int accept(pba_engine* e) {
-  GnData& G = e->gn;
-  PBA_HIP(hipMemcpyAsync(e->poses.p, G.poses_new.p, sizeof(double) * 7 * e->n_frames, hipMemcpyDeviceToDevice, e->stream));
-  PBA_HIP(hipMemcpyAsync(e->rho.p, G.rho_new.p, sizeof(double) * e->n_points, hipMemcpyDeviceToDevice, e->stream));
-  e->pairs_fresh = false;
+  launch_accept(e, nullptr);
+  PBA_HIP(hipGetLastError());
   return PBA_OK;
 }
 
@@ -2331,7 +2341,7 @@ int lm_loop_single(pba_engine* e, const pba_solver_options* o, pba_solver_summar
     const double lambda = 1.0 / radius;
     const hipEvent_t* lin = ev + 4 + 2 * (iter & 1);
     double d[kLmFields];
-    if (int rc = lm_trial(e, lambda, opt.min_relative_decrease, ev, lin, ev[3], d)) return rc;
+    if (int rc = lm_trial(e, lambda, opt.min_relative_decrease, opt.function_tolerance, ev, lin, ev[3], d)) return rc;
     float ms = 0.0f;
     PBA_HIP(hipEventElapsedTime(&ms, ev[0], ev[1]));
     s.solve_ms += ms;
@@ -2342,6 +2352,11 @@ int lm_loop_single(pba_engine* e, const pba_solver_options* o, pba_solver_summar
       s.linearize_ms += ms;
       pending = -1;
     }
+    if (d[kLmConverged] != 0.0) {  // |Δcost| ≤ function_tolerance · cost: stop at the current state
+      s.termination = PBA_TERMINATION_CONVERGENCE;
+      ++iter;
+      break;
+    }
     if (d[kLmAccept] == 0.0) {  // failed solve, no predicted decrease, or too little actual decrease
       ++s.unsuccessful_steps;
       radius /= factor;
@@ -2349,18 +2364,12 @@ int lm_loop_single(pba_engine* e, const pba_solver_options* o, pba_solver_summar
       if (radius < 1e-32) { s.termination = PBA_TERMINATION_FAILURE; break; }
       continue;
     }
-    const double cost_new = d[kLmCostNew], rel = d[kLmRel];
-    const double decrease = cost - cost_new;
+    const double rel = d[kLmRel];
     ++s.successful_steps;
     radius = radius / std::max(1.0 / 3.0, 1.0 - std::pow(2.0 * rel - 1.0, 3));
     factor = 2.0;
-    cost = cost_new;
+    cost = d[kLmCostNew];
     pending = 4 + 2 * (iter & 1);
-    if (decrease <= opt.function_tolerance * cost) {  // Ceres: |Δcost| ≤ function_tolerance · cost
-      s.termination = PBA_TERMINATION_CONVERGENCE;
-      ++iter;
-      break;
-    }
   }
   PBA_HIP(hipStreamSynchronize(e->stream));  // the last trial's accept / linearisation
   if (pending >= 0) {
@@ -2418,19 +2427,18 @@ int lm_loop(pba_engine* e, const pba_solver_options* o, const Reducer* red, pba_
       if (radius < 1e-32) { s.termination = PBA_TERMINATION_FAILURE; break; }
       continue;
     }
+    if (std::fabs(cost - cost_new) <= opt.function_tolerance * cost) {  // trust_region_minimizer.cc:115-117, :729
+      s.termination = PBA_TERMINATION_CONVERGENCE;                       // (the step is not applied)
+      ++iter;
+      break;
+    }
     const double rel = (cost - cost_new) / model;
     if (rel > opt.min_relative_decrease && std::isfinite(cost_new)) {
       if (int rc = accept(e)) return rc;
-      const double decrease = cost - cost_new;
       ++s.successful_steps;
       radius = radius / std::max(1.0 / 3.0, 1.0 - std::pow(2.0 * rel - 1.0, 3));
       factor = 2.0;
       cost = cost_new;
-      if (decrease <= opt.function_tolerance * cost) {  // Ceres: |Δcost| ≤ function_tolerance · cost
-        s.termination = PBA_TERMINATION_CONVERGENCE;
-        ++iter;
-        break;
-      }
       t = now_ms();
       if (int rc = linearize(e, nullptr)) return rc;
       PBA_HIP(hipStreamSynchronize(e->stream));

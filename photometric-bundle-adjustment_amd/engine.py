@@ -116,6 +116,9 @@ def lib():
         "pba_num_frames": ([vp], C.c_int),
         "pba_get_records": ([vp, vp, vp], C.c_int),
         "pba_get_block_costs": ([vp, vp], C.c_int),
+        "pba_get_residuals": ([vp, vp, vp], C.c_int),
+        "pba_host_alloc": ([C.c_size_t, C.POINTER(vp)], C.c_int),
+        "pba_host_free": ([vp], C.c_int),
         "pba_get_cost": ([vp, C.POINTER(C.c_double), C.POINTER(i32)], C.c_int),
         "pba_set_stream": ([vp, vp], C.c_int),
         "pba_get_stream": ([vp, C.POINTER(vp)], C.c_int),
@@ -272,6 +275,13 @@ class Engine:
         valid = np.empty(self.n_blocks, np.uint8)
         _check(self._L.pba_get_records(self._h, _p(rec), _p(valid)), "pba_get_records")
         return rec, valid
+
+    def residuals(self):
+        """Residuals only (the first R values of every record, one pitched copy) and the validity flags."""
+        r = np.empty((self.n_blocks, self.R), np.float32)
+        valid = np.empty(self.n_blocks, np.uint8)
+        _check(self._L.pba_get_residuals(self._h, _p(r), _p(valid)), "pba_get_residuals")
+        return r, valid
 
     def block_costs(self):
         c = np.empty(self.n_blocks, np.float32)

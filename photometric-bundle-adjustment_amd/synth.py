@@ -13,9 +13,12 @@ model restated as SoA arrays:
 Trajectory ``T_w_k = (exp([0, 0.002k, 0]), [0.05k, 0, 0])``; every point is observed by the K keyframes
 after its host, so ``n_blocks = K·n_points``.
 
-Two image sources:
+Three image sources:
 * ``texture="render"`` ray-casts every keyframe onto a textured plane, so the photometric residual of the
   unperturbed state is ~0 (for solver / convergence tests);
+* ``texture="euroc"`` does the same with real image content: the plane carries a 2×2 mosaic of the reference's own
+  EuRoC V1 cam0 frames (tests/golden/euroc_texture.npz, made by tests/golden/make_euroc_texture.py), and points
+  are placed on high-gradient host pixels (as a direct-method front end selects them);
 * ``texture="noise"`` gives each keyframe an independent smooth random texture (for throughput, where
   image content is irrelevant).  ``bench.py`` builds those on the GPU with torch.
 """
@@ -276,6 +279,37 @@ class PlaneTexture:
         return (self.z0 - pose[..., 6]) / d[..., 2]
 
 
+class ImageTexture(PlaneTexture):
+    """A u8 image on the world plane Z = z0 (texel `texel` metres, centred on (x0, y0), mirrored beyond its edges),
+    bilinearly sampled — real image content for rendered keyframes."""
+
+    def __init__(self, image: np.ndarray, z0: float = 6.0, texel: float = 0.017, x0: float = 1.0, y0: float = 0.0):
+        self.z0, self.img, self.texel = z0, image.astype(np.float64), texel
+        self.x0 = x0 - 0.5 * texel * image.shape[1]
+        self.y0 = y0 - 0.5 * texel * image.shape[0]
+
+    def __call__(self, X: np.ndarray, Y: np.ndarray) -> np.ndarray:
+        H, W = self.img.shape
+        u = (X - self.x0) / self.texel
+        v = (Y - self.y0) / self.texel
+        u = _mirror(u, W)
+        v = _mirror(v, H)
+        return bilinear(self.img, u, v)
+
+
+def _mirror(x: np.ndarray, n: int) -> np.ndarray:
+    """Mirrored repeat of coordinates into [0, n−1]."""
+    p = 2.0 * (n - 1)
+    y = np.mod(x, p)
+    return np.where(y > n - 1, p - y, y)
+
+
+def euroc_texture_image() -> np.ndarray:
+    import os
+    here = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    return np.load(os.path.join(here, "tests", "golden", "euroc_texture.npz"))["texture"]
+
+
 def noise_images(rng: np.random.Generator, n: int, W: int, H: int, cell: int = 8) -> np.ndarray:
     """Independent smooth random textures (bilinear upsample of a coarse random grid)."""
     gh, gw = H // cell + 2, W // cell + 2
@@ -299,27 +333,50 @@ def make_problem(n_frames: int = 8, n_points: int = 64, K: int = 4, width: int =
                  model: int | str = PINHOLE, kind: int | str = PHOTOMETRIC, pattern: Optional[np.ndarray] = None,
                  seed: int = 42, texture: str = "render", perturb: bool = True, pose_sigma: float = 0.003,
                  rho_sigma: float = 0.02, border: int = 24, obs_sigma: float = 0.5,
-                 with_images: bool = True) -> Problem:
-    """Build a synthetic problem.  ``poses``/``rho`` hold the perturbed state."""
+                 with_images: bool = True, intrinsics: Optional[np.ndarray] = None,
+                 frame_cam: Optional[np.ndarray] = None, poses_gt: Optional[np.ndarray] = None) -> Problem:
+    """Build a synthetic problem.  ``poses``/``rho`` hold the perturbed state.  ``intrinsics``
+    ((n_cams, 8), quoted for width × height) overrides the model's default camera, ``frame_cam`` assigns cameras to
+    keyframes (a stereo rig: alternating 0/1) and ``poses_gt`` replaces the default trajectory."""
     model = MODEL_IDS.get(model, model) if isinstance(model, str) else model
     kind = KIND_IDS.get(kind, kind) if isinstance(kind, str) else kind
     if n_frames < K + 1:
         raise ValueError("need at least K+1 keyframes")
     rng = np.random.default_rng(seed)
-    intr = np.array([DEFAULT_INTRINSICS[model]], np.float64)
-    intr[0, :4] *= width / 752.0  # intrinsics are quoted for 752×480; rescale for other sizes
-    frame_cam = np.zeros(n_frames, np.int32)
-    poses_gt = trajectory(n_frames)
+    if intrinsics is not None:
+        intr = np.asarray(intrinsics, np.float64).reshape(-1, 8).copy()
+    else:
+        intr = np.array([DEFAULT_INTRINSICS[model]], np.float64)
+        intr[0, :4] *= width / 752.0  # intrinsics are quoted for 752×480; rescale for other sizes
+    frame_cam = np.zeros(n_frames, np.int32) if frame_cam is None else np.asarray(frame_cam, np.int32)
+    poses_gt = trajectory(n_frames) if poses_gt is None else np.asarray(poses_gt, np.float64)
+    kf = intr[frame_cam]  # per-keyframe intrinsics
     pat = PATTERN8 if pattern is None else np.asarray(pattern, np.float32)
 
     point_host = rng.integers(0, n_frames - K, n_points).astype(np.int32)
     u_ref = np.stack([rng.integers(border, width - border, n_points),
                       rng.integers(border, height - border, n_points)], -1).astype(np.float64)
-    b = unproject(model, intr[0], u_ref)
 
     tex = None
-    if texture == "render":
-        tex = PlaneTexture(rng)
+    rendered = None
+    if texture == "euroc":
+        tex = ImageTexture(euroc_texture_image())
+        rendered = np.stack([tex.render(model, kf[f], poses_gt[f], width, height) for f in range(n_frames)])
+        # high-gradient host pixels: of 6 candidates per point keep the one with the largest |∇I|
+        cand = 6
+        ch = rng.integers(0, n_frames - K, n_points * cand).astype(np.int32)
+        cu = rng.integers(border, width - border, n_points * cand)
+        cv = rng.integers(border, height - border, n_points * cand)
+        img = rendered.astype(np.float64)
+        g = np.abs(img[ch, cv, cu + 1] - img[ch, cv, cu - 1]) + np.abs(img[ch, cv + 1, cu] - img[ch, cv - 1, cu])
+        best = np.argmax(g.reshape(n_points, cand), 1) + cand * np.arange(n_points)
+        point_host = ch[best]
+        u_ref = np.stack([cu[best], cv[best]], -1).astype(np.float64)
+    b = unproject(model, kf[point_host], u_ref)
+
+    if texture in ("render", "euroc"):
+        if tex is None:
+            tex = PlaneTexture(rng)
         dist = tex.depth(poses_gt[point_host], b)
     else:
         dist = np.clip(6.0 + rng.normal(0, 1.0, n_points), 3.0, 12.0)
@@ -330,8 +387,10 @@ def make_problem(n_frames: int = 8, n_points: int = 64, K: int = 4, width: int =
 
     images = host_int = u_obs = None
     if kind == PHOTOMETRIC and with_images:
-        if texture == "render":
-            images = np.stack([tex.render(model, intr[0], poses_gt[f], width, height) for f in range(n_frames)])
+        if rendered is not None:
+            images = rendered
+        elif texture == "render":
+            images = np.stack([tex.render(model, kf[f], poses_gt[f], width, height) for f in range(n_frames)])
         else:
             images = noise_images(rng, n_frames, width, height)
         host_int = np.empty((n_points, len(pat)), np.float32)
@@ -345,7 +404,7 @@ def make_problem(n_frames: int = 8, n_points: int = 64, K: int = 4, width: int =
         Th, Tt = poses_gt[point_host[block_point]], poses_gt[block_target]
         pw = (quat_to_rot(Th[:, :4]) @ ph[block_point, :, None])[..., 0] + Th[:, 4:]
         pt = (np.swapaxes(quat_to_rot(Tt[:, :4]), -1, -2) @ (pw - Tt[:, 4:])[..., None])[..., 0]
-        u_obs = project(model, intr[0], pt) + rng.normal(0, obs_sigma, (len(block_point), 2))
+        u_obs = project(model, kf[block_target], pt) + rng.normal(0, obs_sigma, (len(block_point), 2))
 
     poses, rho = poses_gt.copy(), rho_gt.copy()
     if perturb:
@@ -389,3 +448,120 @@ def level_problem(pb: "Problem", level: int, host_intensity: Optional[np.ndarray
                                            ur[sel, None, 1] + pb.pattern[None, :, 1]).astype(np.float32)
     return dataclasses.replace(pb, width=imgs.shape[2], height=imgs.shape[1], images=imgs, intrinsics=k, u_ref=ur,
                                host_intensity=host_intensity)
+
+
+# ------------------------------------------------------------------------------------------------
+# BASELINE.json configurations that the tests and the bench build
+# ------------------------------------------------------------------------------------------------
+def euroc_ds_intrinsics() -> np.ndarray:
+    """(2, 8) double-sphere intrinsics of the EuRoC stereo pair from the reference's own calibration data file
+    (data/euroc_calib/calibration-double-sphere.json, copied to tests/golden/map_small/)."""
+    import json
+    import os
+    here = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    with open(os.path.join(here, "tests", "golden", "map_small", "euroc_calibration-double-sphere.json")) as f:
+        cams = json.load(f)["value0"]["cam.intrinsics"]
+    return np.array([[c["fx"], c["fy"], c["cx"], c["cy"], c["xi"], c["alpha"], 0.0, 0.0] for c in cams], np.float64)
+
+
+def stereo_trajectory(n_keyframes: int, baseline: float = 0.11) -> np.ndarray:
+    """Keyframe i → frames 2i (cam0) and 2i+1 (cam1): T_w_c = T_w_i · T_i_c with T_i_c0 = I and T_i_c1 a
+    `baseline` shift along x (EuRoC's stereo rig; the sfm map's FrameCamId order, common_types.h:87-90)."""
+    T_w_i = trajectory(n_keyframes, step=0.15)
+    out = np.empty((2 * n_keyframes, 7))
+    out[0::2] = T_w_i
+    out[1::2] = se3_mul(T_w_i, np.array([0, 0, 0, 1, baseline, 0, 0], np.float64)[None].repeat(n_keyframes, 0))
+    return out
+
+
+def c1_problem(seed: int = 42, n_keyframes: int = 20, n_points: int = 2000, K: int = 4, **kw) -> Problem:
+    """configs[0] (C1): EuRoC-sized geometric BA — 20 stereo keyframes (40 frames, double-sphere cameras with the
+    reference's EuRoC calibration), ~2k landmarks each seen by the K frames after its anchor (stereo partner
+    included), 752×480; as bundle_adjustment() builds it (map_utils.h:322-375).  Fixed frames {0, 1} = the
+    reference's fixed cameras {(0,0), (0,1)} (sfm.cpp:1903)."""
+    nf = 2 * n_keyframes
+    return make_problem(n_frames=nf, n_points=n_points, K=K, kind=GEOMETRIC, model=DOUBLE_SPHERE, seed=seed,
+                        intrinsics=euroc_ds_intrinsics(), frame_cam=np.arange(nf, dtype=np.int32) % 2,
+                        poses_gt=stereo_trajectory(n_keyframes), **kw)
+
+
+def c2_problem(seed: int = 42, n_frames: int = 50, n_points: int = 5000, K: int = 4, **kw) -> Problem:
+    """configs[1] (C2): EuRoC-sized photometric BA — 50 keyframes of real EuRoC V1 image content (texture="euroc"),
+    cam0's double-sphere calibration, 8-px pattern, ~5k points on high-gradient pixels × K = 4 targets."""
+    return make_problem(n_frames=n_frames, n_points=n_points, K=K, kind=PHOTOMETRIC, model=DOUBLE_SPHERE, seed=seed,
+                        texture="euroc", intrinsics=euroc_ds_intrinsics()[:1], **kw)
+
+
+def render_torch(tex: PlaneTexture, K: np.ndarray, poses: np.ndarray, W: int, H: int, device, chunk: int = 64):
+    """PlaneTexture.render for a pinhole camera on the GPU (torch, fp64 rays): (n, H, W) u8 tensor."""
+    import torch
+    n = poses.shape[0]
+    out = torch.empty((n, H, W), dtype=torch.uint8, device=device)
+    v, u = torch.meshgrid(torch.arange(H, dtype=torch.float64, device=device),
+                          torch.arange(W, dtype=torch.float64, device=device), indexing="ij")
+    b = torch.stack([(u - K[2]) / K[0], (v - K[3]) / K[1], torch.ones_like(u)], -1)
+    b = b / torch.linalg.norm(b, dim=-1, keepdim=True)
+    kx = torch.tensor(tex.kx, device=device)
+    ky = torch.tensor(tex.ky, device=device)
+    ph = torch.tensor(tex.phase, device=device)
+    amp = torch.tensor(tex.amp, device=device)
+    for s in range(0, n, chunk):
+        P = torch.tensor(poses[s:s + chunk], dtype=torch.float64, device=device)
+        R = torch.tensor(quat_to_rot(poses[s:s + chunk, :4]), device=device)
+        d = torch.einsum("hwj,nij->nhwi", b, R)
+        lam = (tex.z0 - P[:, 6, None, None]) / d[..., 2]
+        X = P[:, 4, None, None] + lam * d[..., 0]
+        Y = P[:, 5, None, None] + lam * d[..., 1]
+        acc = torch.zeros_like(X)
+        for i in range(kx.shape[0]):
+            acc += amp[i] * torch.sin(kx[i] * X + ky[i] * Y + ph[i])
+        out[s:s + chunk] = torch.clamp(torch.round(127.5 + 107.5 * acc), 0, 255).to(torch.uint8)
+    return out
+
+
+def c4_shard(device, rank: int = 0, world: int = 1, n_frames: int = 1000, n_points: int = 100000, K: int = 4,
+             width: int = 752, height: int = 480, texture: str = "noise", seed: int = 42):
+    """configs[3] (C4) shard of `rank`: hosts [rank·F, (rank+1)·F) of a world·F + K keyframe trajectory, n_points
+    points each seen by the K keyframes after its host (n_blocks = K·n_points), pinhole 752×480, 8-px pattern.
+    Images are built on the GPU (torch): "noise" (independent smooth textures; throughput) or "render" (one
+    textured plane seen by every keyframe, so the residual at the true state is ~0 and LM converges).  Returns
+    (problem with images=None and host intensities filled, images as a device tensor of all world·F + K frames)."""
+    import torch
+    import torch.nn.functional as F_
+    F = n_frames
+    NF = world * F + K
+    off = rank * F
+    pb = make_problem(n_frames=F + K, n_points=n_points, K=K, width=width, height=height, kind=PHOTOMETRIC,
+                      model=PINHOLE, texture="noise", with_images=False, seed=seed + rank)
+    pb.point_host = (pb.point_host + off).astype(np.int32)
+    pb.block_target = (pb.block_target + off).astype(np.int32)
+    pb.frame_cam = np.zeros(NF, np.int32)
+    prng = np.random.default_rng(99)  # the same global poses on every rank
+    pb.poses_gt = trajectory(NF)
+    images = torch.zeros((NF, height, width), dtype=torch.uint8, device=device)
+    if texture == "render":
+        tex = PlaneTexture(np.random.default_rng(seed))
+        b = unproject(PINHOLE, pb.intrinsics[0], pb.u_ref)
+        pb.rho_gt = 1.0 / tex.depth(pb.poses_gt[pb.point_host], b)
+        pb.rho = pb.rho_gt * (1 + 0.02 * np.random.default_rng(seed + 1).normal(0, 1, n_points))
+        images[off:off + F + K] = render_torch(tex, pb.intrinsics[0], pb.poses_gt[off:off + F + K], width, height,
+                                               device)
+    else:
+        g = torch.Generator(device=device)
+        g.manual_seed(1234 + rank)
+        for s in range(0, F + K, 100):
+            m = min(100, F + K - s)
+            coarse = torch.rand((m, 1, height // 8 + 2, width // 8 + 2), generator=g, device=device) * 215 + 20
+            img = F_.interpolate(coarse, size=(height + 16, width + 16), mode="bilinear",
+                                 align_corners=False)[:, 0, :height, :width]
+            img = img + torch.randn((m, height, width), generator=g, device=device) * 2.0
+            images[off + s:off + s + m] = img.round().clamp(0, 255).to(torch.uint8)
+    pb.poses = se3_plus(pb.poses_gt, 3e-3 * prng.normal(0, 1, (NF, 6)))
+    host = torch.from_numpy(pb.point_host.astype(np.int64)).to(device)
+    uu = torch.from_numpy(pb.u_ref[:, 0].astype(np.int64)).to(device)[:, None] + \
+        torch.from_numpy(pb.pattern[:, 0].astype(np.int64)).to(device)
+    vv = torch.from_numpy(pb.u_ref[:, 1].astype(np.int64)).to(device)[:, None] + \
+        torch.from_numpy(pb.pattern[:, 1].astype(np.int64)).to(device)
+    # integer u_ref and integer pattern → the bilinear host sample is exactly the pixel value
+    pb.host_intensity = images[host[:, None], vv, uu].float().cpu().numpy()
+    return pb, images

@@ -1,0 +1,289 @@
+// tests/cpp/ceres_lm_driver.cpp — TEST-ONLY: the reference's bundle_adjustment() solve (map_utils.h:322-383) run by
+// the real Ceres Solver 2.0.0 (vendored in the reference, built by oracle/ceres.mk) in one of two modes:
+//
+//   cpu  the reference's CPU path: one ceres::AutoDiffCostFunction per residual block over the restated functor
+//        (tests/cpp/ceres_functors.h), the reference's own LocalParameterizationSE3 (local_parameterization_se3.hpp).
+//   gpu  the drop-in: the same Problem with include/pba_ceres.h — GpuEvaluator as Problem::Options::
+//        evaluation_callback, GpuPhotometricCost / GpuReprojectionCost per block, SE3TangentParameterization —
+//        evaluated by the MI355X engine (libpba.so).  The evaluation-callback protocol of
+//        evaluation_callback_test.cc:79-160 is checked on every call (Prepare/Evaluate pairing, new_evaluation_point
+//        semantics, Jacobians requested iff prepared with Jacobians, parameters equal to the prepared state).
+//
+// Both modes: HuberLoss(a) per block (map_utils.h:370-371), two constant keyframes (SetParameterBlockConstant,
+// :334-336), constant intrinsics blocks for the geometric functor (:340-345), LEVENBERG_MARQUARDT + SPARSE_SCHUR
+// (:378-381).  Writes a JSON summary: per-iteration cost / success / relative decrease, termination, final state,
+// Ceres' evaluation timers and the protocol counters.
+//
+//   usage: ceres_lm_driver <cpu|gpu> <problem.bin> <out.json> [iters] [huber] [threads] [fixed,frames] [ftol]
+//          (problem layout: tests/golden/make_golden.py write_problem)
+#include <atomic>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <memory>
+#include <sstream>
+#include <string>
+#include <vector>
+
+#include "ceres_functors.h"
+#include "local_parameterization_se3.hpp"  // the reference's (include/visnav/), compiled where it lies
+#include "pba_ceres.h"
+
+namespace {
+
+template <class T>
+std::vector<T> rd(FILE* f, size_t n) {
+  std::vector<T> v(n);
+  if (n && fread(v.data(), sizeof(T), n, f) != n) {
+    fprintf(stderr, "short read\n");
+    exit(2);
+  }
+  return v;
+}
+
+uint64_t djb2(const double* p, size_t n, uint64_t h = 5381) {  // evaluation_callback_test.cc:45-56
+  const unsigned char* c = reinterpret_cast<const unsigned char*>(p);
+  for (size_t i = 0; i < n * sizeof(double); ++i) h = h * 33 + c[i];
+  return h;
+}
+
+struct Protocol {
+  std::atomic<long> violations{0}, evaluate_calls{0};
+  long prepare_calls = 0, evaluate_calls_at_prepare = 0;
+  bool requested_jacobians = false, new_point = false;
+  uint64_t hash = 0;
+  std::vector<double> state;  // user state snapshot at the last Prepare
+  std::string log;            // "J"/"r" + "n"/"s" per Prepare (jacobians?, new point?)
+};
+
+// GpuEvaluator with the checks of evaluation_callback_test.cc:79-112 (Prepare side).
+class CheckedEvaluator : public pba_ceres::GpuEvaluator {
+ public:
+  CheckedEvaluator(pba_engine* e, std::vector<double*> poses, std::vector<double*> rho, int n_blocks, Protocol* pr)
+      : GpuEvaluator(e, poses, rho), poses_(poses), rho_(rho), nb_(n_blocks), pr_(pr) {}
+  void PrepareForEvaluation(bool evaluate_jacobians, bool new_evaluation_point) override {
+    Protocol& p = *pr_;
+    std::vector<double> st;
+    st.reserve(7 * poses_.size() + rho_.size());
+    for (double* q : poses_) st.insert(st.end(), q, q + 7);
+    for (double* r : rho_) st.push_back(*r);
+    const uint64_t h = djb2(st.data(), st.size());
+    // Prepare() and a full pass of Evaluate() calls alternate
+    if (p.prepare_calls > 0 && p.evaluate_calls.load() - p.evaluate_calls_at_prepare != nb_) ++p.violations;
+    if (p.prepare_calls > 0) {
+      if (new_evaluation_point && h == p.hash) ++p.violations;   // a new point has new parameters
+      if (!new_evaluation_point && h != p.hash) ++p.violations;  // the same point has the same parameters
+    }
+    p.prepare_calls++;
+    p.evaluate_calls_at_prepare = p.evaluate_calls.load();
+    p.requested_jacobians = evaluate_jacobians;
+    p.new_point = new_evaluation_point;
+    p.hash = h;
+    p.state = std::move(st);
+    p.log += evaluate_jacobians ? 'J' : 'r';
+    p.log += new_evaluation_point ? 'n' : 's';
+    GpuEvaluator::PrepareForEvaluation(evaluate_jacobians, new_evaluation_point);
+  }
+
+ private:
+  std::vector<double*> poses_, rho_;
+  long nb_;
+  Protocol* pr_;
+};
+
+// The per-block side of evaluation_callback_test.cc:113-160 around the adapter's CostFunction.
+class CheckedCost : public ceres::CostFunction {
+ public:
+  CheckedCost(ceres::CostFunction* inner, Protocol* pr, int host, int target, int point, int nf)
+      : inner_(inner), pr_(pr), host_(host), target_(target), point_(point), nf_(nf) {
+    set_num_residuals(inner->num_residuals());
+    *mutable_parameter_block_sizes() = inner->parameter_block_sizes();
+  }
+  bool Evaluate(double const* const* parameters, double* residuals, double** jacobians) const override {
+    Protocol& p = *pr_;
+    p.evaluate_calls++;
+    bool ok = p.requested_jacobians == (jacobians != nullptr);
+    ok = ok && std::memcmp(parameters[0], &p.state[7 * host_], 7 * sizeof(double)) == 0;
+    ok = ok && std::memcmp(parameters[1], &p.state[7 * target_], 7 * sizeof(double)) == 0;
+    ok = ok && parameters[2][0] == p.state[7 * (size_t)nf_ + point_];
+    if (!ok) ++p.violations;
+    return inner_->Evaluate(parameters, residuals, jacobians);
+  }
+
+ private:
+  std::unique_ptr<ceres::CostFunction> inner_;
+  Protocol* pr_;
+  int host_, target_, point_, nf_;
+};
+
+void json_array(std::ostringstream& o, const double* v, size_t n) {
+  o << "[";
+  char buf[40];
+  for (size_t i = 0; i < n; ++i) {
+    snprintf(buf, sizeof buf, "%.17g", v[i]);
+    o << (i ? "," : "") << buf;
+  }
+  o << "]";
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  if (argc < 4) {
+    fprintf(stderr, "usage: %s <cpu|gpu> <problem.bin> <out.json> [iters] [huber] [threads] [fixed] [ftol]\n", argv[0]);
+    return 1;
+  }
+  const bool gpu = std::string(argv[1]) == "gpu";
+  const int iters = argc > 4 ? atoi(argv[4]) : 20;
+  const double huber = argc > 5 ? atof(argv[5]) : 1.0;
+  const int threads = argc > 6 ? atoi(argv[6]) : 8;
+  std::vector<int> fixed;
+  if (argc > 7 && argv[7][0] != '-') {
+    std::stringstream ss(argv[7]);
+    std::string tok;
+    while (std::getline(ss, tok, ',')) fixed.push_back(atoi(tok.c_str()));
+  }
+  const double ftol = argc > 8 ? atof(argv[8]) : 1e-6;
+
+  FILE* f = fopen(argv[2], "rb");
+  if (!f) return 2;
+  const auto hdr = rd<int32_t>(f, 9);
+  const int kind = hdr[0], model = hdr[1], nf = hdr[2], np = hdr[3], nb = hdr[4], nc = hdr[5], W = hdr[6], H = hdr[7];
+  const int P = hdr[8];
+  auto intr = rd<double>(f, 8 * nc);
+  const auto frame_cam = rd<int32_t>(f, nf);
+  const auto images = rd<uint8_t>(f, kind == 0 ? (size_t)nf * W * H : 0);
+  const auto pattern = rd<float>(f, kind == 0 ? 2 * P : 0);
+  const auto point_host = rd<int32_t>(f, np);
+  const auto u_ref = rd<double>(f, 2 * np);
+  const auto host_int = rd<float>(f, kind == 0 ? (size_t)P * np : 0);
+  const auto block_point = rd<int32_t>(f, nb);
+  const auto block_target = rd<int32_t>(f, nb);
+  const auto u_obs = rd<double>(f, kind == 1 ? 2 * nb : 0);
+  const auto poses_in = rd<double>(f, 7 * nf);
+  std::vector<double> rho = rd<double>(f, np);
+  fclose(f);
+  if (kind == 0 && P != 8) {
+    fprintf(stderr, "driver is built for P = 8\n");
+    return 3;
+  }
+
+  // user memory, as the reference keeps it (Camera::T_w_c, Landmark::inv_depth, calib intrinsics)
+  std::vector<Sophus::SE3d> T(nf);
+  for (int i = 0; i < nf; ++i) std::memcpy(T[i].data(), &poses_in[7 * i], 7 * sizeof(double));
+  std::vector<double*> pose_ptr(nf), rho_ptr(np);
+  for (int i = 0; i < nf; ++i) pose_ptr[i] = T[i].data();
+  for (int p = 0; p < np; ++p) rho_ptr[p] = &rho[p];
+
+  Protocol protocol;
+  pba_engine* e = nullptr;
+  std::unique_ptr<CheckedEvaluator> ev;
+  ceres::Problem::Options popt;
+  if (gpu) {
+    pba_options opt{0, kind, model, 0.0f};
+    pba_ceres::check(pba_create(&opt, &e), "pba_create");
+    pba_ceres::check(pba_set_cameras(e, nc, intr.data()), "cameras");
+    pba_ceres::check(pba_set_frames(e, nf, frame_cam.data(), W, H, kind == 0 ? images.data() : nullptr), "frames");
+    if (kind == 0) pba_ceres::check(pba_set_pattern(e, P, pattern.data()), "pattern");
+    pba_ceres::check(pba_set_points(e, np, point_host.data(), u_ref.data(), kind == 0 ? host_int.data() : nullptr),
+                     "points");
+    pba_ceres::check(pba_set_blocks(e, nb, block_point.data(), block_target.data(), kind == 1 ? u_obs.data() : nullptr),
+                     "blocks");
+    ev.reset(new CheckedEvaluator(e, pose_ptr, rho_ptr, nb, &protocol));
+    popt.evaluation_callback = ev.get();  // problem.h:185 (not owned)
+  }
+  ceres::Problem problem(popt);
+  for (int i = 0; i < nf; ++i) {  // map_utils.h:330-337
+    ceres::LocalParameterization* lp = gpu ? static_cast<ceres::LocalParameterization*>(new pba_ceres::SE3TangentParameterization)
+                                           : new Sophus::test::LocalParameterizationSE3;
+    problem.AddParameterBlock(T[i].data(), 7, lp);
+  }
+  for (int i : fixed) problem.SetParameterBlockConstant(T[i].data());
+  if (kind == 1)
+    for (int c = 0; c < nc; ++c) {  // :340-345
+      problem.AddParameterBlock(&intr[8 * c], 8);
+      problem.SetParameterBlockConstant(&intr[8 * c]);
+    }
+  // CPU photometric: one interpolator per keyframe image, host bearings per point
+  std::vector<std::unique_ptr<pba_test::BilinearInterpolator>> interp;
+  std::vector<Eigen::Matrix<double, 3, 8>> bearings;
+  std::vector<double> host_int_d;
+  if (!gpu && kind == 0) {
+    for (int i = 0; i < nf; ++i) interp.emplace_back(new pba_test::BilinearInterpolator(&images[(size_t)i * W * H], H, W));
+    bearings.resize(np);
+    host_int_d.assign(host_int.begin(), host_int.end());
+    for (int p = 0; p < np; ++p)
+      for (int k = 0; k < 8; ++k)
+        bearings[p].col(k) = pba_test::Unproject(model, &intr[8 * frame_cam[point_host[p]]],
+                                                 Eigen::Vector2d(u_ref[2 * p] + pattern[2 * k], u_ref[2 * p + 1] + pattern[2 * k + 1]));
+  }
+  for (int b = 0; b < nb; ++b) {  // :347-375
+    const int p = block_point[b], h = point_host[p], t = block_target[b];
+    ceres::LossFunction* loss = huber > 0 ? new ceres::HuberLoss(huber) : nullptr;
+    ceres::CostFunction* cf;
+    if (gpu) {
+      ceres::CostFunction* inner = kind == 0 ? static_cast<ceres::CostFunction*>(new pba_ceres::GpuPhotometricCost<8>(ev.get(), b))
+                                             : new pba_ceres::GpuReprojectionCost(ev.get(), b);
+      cf = new CheckedCost(inner, &protocol, h, t, p, nf);
+    } else if (kind == 1) {
+      cf = new ceres::AutoDiffCostFunction<pba_test::GeometricFunctor, 2, 7, 7, 1, 8>(new pba_test::GeometricFunctor(
+          Eigen::Vector2d(u_obs[2 * b], u_obs[2 * b + 1]), Eigen::Vector2d(u_ref[2 * p], u_ref[2 * p + 1]),
+          &intr[8 * frame_cam[h]], model));
+    } else {
+      using F = pba_test::PhotometricFunctor<8, pba_test::BilinearInterpolator>;
+      cf = new ceres::AutoDiffCostFunction<F, 8, 7, 7, 1>(
+          new F(&host_int_d[(size_t)8 * p], bearings[p], *interp[t], &intr[8 * frame_cam[t]], model));
+    }
+    if (kind == 1)
+      problem.AddResidualBlock(cf, loss, T[h].data(), T[t].data(), &rho[p], &intr[8 * frame_cam[t]]);
+    else
+      problem.AddResidualBlock(cf, loss, T[h].data(), T[t].data(), &rho[p]);
+  }
+
+  ceres::Solver::Options so;  // map_utils.h:376-381
+  so.max_num_iterations = iters;
+  so.linear_solver_type = ceres::SPARSE_SCHUR;
+  so.num_threads = threads;
+  so.function_tolerance = ftol;
+  ceres::Solver::Summary sum;
+  ceres::Solve(so, &problem, &sum);
+
+  std::ostringstream o;
+  o << "{\"mode\":\"" << (gpu ? "gpu" : "cpu") << "\",\"termination\":" << (int)sum.termination_type
+    << ",\"message\":\"" << sum.message << "\",\"successful_steps\":" << sum.num_successful_steps
+    << ",\"unsuccessful_steps\":" << sum.num_unsuccessful_steps << ",\"iterations\":[";
+  for (size_t i = 0; i < sum.iterations.size(); ++i) {
+    const auto& it = sum.iterations[i];
+    char buf[200];
+    snprintf(buf, sizeof buf, "%s[%d,%.17g,%d,%.17g,%.17g]", i ? "," : "", it.iteration, it.cost,
+             it.step_is_successful ? 1 : 0, it.relative_decrease, it.trust_region_radius);
+    o << buf;
+  }
+  char buf[400];
+  snprintf(buf, sizeof buf, "],\"initial_cost\":%.17g,\"final_cost\":%.17g", sum.initial_cost, sum.final_cost);
+  o << buf;
+  snprintf(buf, sizeof buf,
+           ",\"jacobian_evaluation_s\":%.6g,\"jacobian_evaluations\":%d,\"residual_evaluation_s\":%.6g,"
+           "\"residual_evaluations\":%d,\"linear_solver_s\":%.6g,\"minimizer_s\":%.6g,\"total_s\":%.6g,\"threads\":%d",
+           sum.jacobian_evaluation_time_in_seconds, sum.num_jacobian_evaluations, sum.residual_evaluation_time_in_seconds,
+           sum.num_residual_evaluations, sum.linear_solver_time_in_seconds, sum.minimizer_time_in_seconds,
+           sum.total_time_in_seconds, sum.num_threads_used);
+  o << buf;
+  o << ",\"protocol\":{\"prepare_calls\":" << protocol.prepare_calls << ",\"evaluate_calls\":" << protocol.evaluate_calls.load()
+    << ",\"violations\":" << protocol.violations.load() << ",\"log\":\"" << protocol.log << "\"}";
+  std::vector<double> pf(7 * (size_t)nf);
+  for (int i = 0; i < nf; ++i) std::memcpy(&pf[7 * i], T[i].data(), 7 * sizeof(double));
+  o << ",\"poses\":";
+  json_array(o, pf.data(), pf.size());
+  o << ",\"rho\":";
+  json_array(o, rho.data(), rho.size());
+  o << "}\n";
+  FILE* g = fopen(argv[3], "w");
+  if (!g) return 4;
+  fputs(o.str().c_str(), g);
+  fclose(g);
+  ev.reset();
+  if (e) pba_destroy(e);
+  return 0;
+}

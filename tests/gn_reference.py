@@ -100,33 +100,44 @@ def apply_step(poses, rho, dp, dl):
     return synth.se3_plus(poses, dp), rho + dl
 
 
-def lm(pb, a, fixed=(), max_iterations=20, radius=1e4, function_tolerance=1e-6, min_relative_decrease=1e-3):
+def lm(pb, a, fixed=(), max_iterations=20, radius=1e4, function_tolerance=1e-6, min_relative_decrease=1e-3,
+       summary=False):
+    """Ceres' trust-region loop (trust_region_minimizer.cc:67-136): an invalid step (no predicted decrease) and a
+    rejected one shrink the radius; a valid step whose |cost change| ≤ function_tolerance · cost ends the solve
+    WITHOUT being applied (FunctionToleranceReached, :115-117, checked before IsStepSuccessful)."""
     poses, rho = pb.poses.copy(), pb.rho.copy()
     H, g, cost = linearize(pb, poses, rho, a, fixed)
     cost0 = cost
     factor = 2.0
     it = 0
+    ok = bad = 0
+    converged = False
     for it in range(1, max_iterations + 1):
         lam = 1.0 / radius
         _, _, dp, dl, model = schur_step(H, g, pb.n_frames, lam, fixed)
         if not model > 0:
             radius /= factor
             factor *= 2
+            bad += 1
             continue
         np_, nr = apply_step(poses, rho, dp, dl)
         _, _, cost_new = linearize(pb, np_, nr, a, fixed)
+        if abs(cost - cost_new) <= function_tolerance * cost:
+            converged = True
+            break
         rel = (cost - cost_new) / model
         if rel > min_relative_decrease:
-            dec = cost - cost_new
             poses, rho, cost = np_, nr, cost_new
             radius = radius / max(1.0 / 3.0, 1.0 - (2.0 * rel - 1.0) ** 3)
             factor = 2.0
-            if dec <= function_tolerance * cost:
-                break
+            ok += 1
             H, g, cost = linearize(pb, poses, rho, a, fixed)
         else:
             radius /= factor
             factor *= 2
+            bad += 1
+    if summary:
+        return poses, rho, cost0, cost, it, {"successful_steps": ok, "unsuccessful_steps": bad, "converged": converged}
     return poses, rho, cost0, cost, it
 
 

@@ -13,7 +13,7 @@ import numpy as np
 import pytest
 
 import oracle as O
-from helpers import ROOT, compare_records, engine_module, projected_uv, synth
+from helpers import R_ATOL_GEOMETRIC, R_ATOL_PHOTOMETRIC, ROOT, compare_records, engine_module, projected_uv, synth
 
 E = engine_module()
 DRIVER_SRC = os.path.join(ROOT, "tests", "cpp", "adapter_driver.cpp")
@@ -59,6 +59,6 @@ def test_adapter_records_match_oracle(kind, model):
     ref, vref = O.evaluate(pb)
     compare_records(kind, R, rec.astype(np.float32), ref, valid, vref, projected_uv(pb) if kind == 0 else None)
     assert np.array_equal(valid_r, vref)
-    np.testing.assert_allclose(ronly[vref == 1], ref[vref == 1, :R], atol=2.55e-3 if kind == 0 else 1e-3)
+    np.testing.assert_allclose(ronly[vref == 1], ref[vref == 1, :R], atol=R_ATOL_PHOTOMETRIC if kind == 0 else R_ATOL_GEOMETRIC)
     delta = np.array([0.01, -0.02, 0.03, 0.004, -0.005, 0.006])
     np.testing.assert_allclose(plus, O.se3_plus(pb.poses[0], delta), atol=1e-14)

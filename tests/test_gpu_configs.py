@@ -1,0 +1,219 @@
+"""GPU tests at the sizes of BASELINE.json's configurations:
+
+* C1 (configs[0]) — 20 EuRoC stereo keyframes × 2k landmarks, geometric, double-sphere cameras with the reference's
+  EuRoC calibration: records against the oracle; the engine's LM (pba_solve) and the Ceres drop-in (real Ceres 2.0.0
+  LM with include/pba_ceres.h over the engine) against the reference's CPU path (real Ceres with AutoDiff).
+* C2 (configs[1]) — 50 keyframes of real EuRoC V1 image content, 8-px pattern, 20k blocks, double sphere: the Ceres
+  drop-in against real Ceres on the CPU, iteration by iteration, with the evaluation-callback protocol checked on
+  every call (evaluation_callback_test.cc:79-160).
+* C4 (configs[3]) — the headline problem, 1000 keyframes × 100k points × 8 px (400k blocks): sampled oracle parity
+  over all hosts, full-size properties (validity, finiteness, cost = Σ½ρ(‖r‖²), the state-adopting launch
+  bit-identical to set_state + evaluate, fp16 records within 2⁻¹¹), and one Gauss-Newton / LM iteration on rendered
+  images (cost decreases; the cyclic-reduction step equals the band-Cholesky step to 1e-7).
+
+Tolerances: records as tests/helpers.compare_records (north star 1e-5 relative).  LM trajectories: the GPU path
+computes in fp32 (records) where the CPU path computes in fp64, so per-iteration costs agree to 1e-5 relative while
+the accept/reject sequence must be identical.  Final states: the Ceres drop-in (fp32 records, Ceres' fp64 normal
+equations) to 1e-5 m in the poses and 1e-4 of the inverse-distance scale; the engine's own solver (fp32 JᵀJ block
+products, fp64 sums) to 1e-4 m and 1e-3 relative — it stops, like Ceres, at the first step whose cost change is
+within the function tolerance, so the stopping state carries the step-size differences of fp32 normal equations.
+"""
+import importlib
+import os
+
+import numpy as np
+import pytest
+
+import ceres_runner as CR
+import gn_reference as GR
+import oracle as O
+from helpers import compare_records, engine_module, projected_uv, synth
+
+pytestmark = pytest.mark.gpu
+E = engine_module()
+THREADS = int(os.environ.get("OMP_NUM_THREADS", "8"))
+needs_ceres = pytest.mark.skipif(not CR.available(), reason="oracle/_ref/ceres_lm_driver not built (oracle/ceres.mk)")
+
+
+def make_engine(pb, huber, fixed=(0, 1)):
+    eng = E.Engine(pb.kind, pb.model, huber_width=huber)
+    eng.set_problem(pb)
+    eng.set_fixed_frames(np.array(fixed, np.int32))
+    eng.set_state(pb.poses, pb.rho)
+    return eng
+
+
+def assert_same_trajectory(a, b, cost_rtol=1e-5):
+    """Two Ceres runs (real Ceres' Solver::Summary): the same accept/reject sequence and per-iteration costs."""
+    assert len(a["costs"]) == len(b["costs"]), (a["message"], b["message"])
+    assert np.array_equal(a["step_ok"], b["step_ok"])
+    np.testing.assert_allclose(a["costs"], b["costs"], rtol=cost_rtol)
+    assert a["termination"] == b["termination"]
+
+
+# ---------------------------------------------------------------------------------------------------- C1
+@pytest.fixture(scope="module")
+def c1():
+    pb = synth.c1_problem()
+    pb.poses[:2] = pb.poses_gt[:2]
+    return pb
+
+
+def test_c1_records_match_oracle(c1):
+    with make_engine(c1, 1.0) as eng:
+        eng.evaluate(True)
+        rec, valid = eng.records()
+    ref, vref = O.evaluate(c1)
+    st = compare_records(1, 2, rec, ref, valid, vref)
+    assert valid.all(), st
+
+
+@needs_ceres
+def test_c1_engine_lm_matches_ceres_cpu(c1):
+    """pba_solve (on-device Schur GN / LM) against the reference path: real Ceres LM (SPARSE_SCHUR) with AutoDiff."""
+    ref = CR.run("cpu", c1, iters=20, huber=1.0, threads=THREADS)
+    with make_engine(c1, 1.0) as eng:
+        s = eng.solve(max_iterations=20)
+        poses, rho = eng.get_state()
+    # Ceres counts iteration 0 (the initial evaluation) as a successful step
+    assert s["successful_steps"] == ref["successful_steps"] - 1, (s, ref["message"])
+    assert s["unsuccessful_steps"] == ref["unsuccessful_steps"]
+    assert abs(s["initial_cost"] - ref["costs"][0]) <= 1e-6 * ref["costs"][0]
+    assert abs(s["final_cost"] - ref["final_cost"]) <= 1e-5 * ref["final_cost"], (s, ref["final_cost"])
+    np.testing.assert_allclose(poses[:, 4:], ref["poses"][:, 4:], atol=1e-4)
+    np.testing.assert_allclose(rho, ref["rho"], rtol=1e-3)
+
+
+@needs_ceres
+def test_c1_ceres_dropin_matches_ceres_cpu(c1):
+    """The north star's drop-in: the same ceres::Solve with the GPU EvaluationCallback + per-block CostFunctions."""
+    ref = CR.run("cpu", c1, iters=20, huber=1.0, threads=THREADS)
+    got = CR.run("gpu", c1, iters=20, huber=1.0, threads=THREADS)
+    assert got["protocol"]["violations"] == 0, got["protocol"]
+    assert_same_trajectory(got, ref)
+    np.testing.assert_allclose(got["poses"][:, 4:], ref["poses"][:, 4:], atol=1e-5)
+    np.testing.assert_allclose(got["rho"], ref["rho"], rtol=1e-4, atol=1e-4 * np.abs(ref["rho"]).max())
+
+
+# ---------------------------------------------------------------------------------------------------- C2
+@pytest.fixture(scope="module")
+def c2():
+    pb = synth.c2_problem()
+    pb.poses[:2] = pb.poses_gt[:2]
+    return pb
+
+
+def test_c2_records_match_oracle(c2):
+    with make_engine(c2, 9.0) as eng:
+        eng.evaluate(True)
+        rec, valid = eng.records()
+    ref, vref = O.evaluate(c2)
+    compare_records(0, 8, rec, ref, valid, vref, projected_uv(c2))
+
+
+@needs_ceres
+def test_c2_ceres_dropin_matches_ceres_cpu(c2):
+    """C2 = "Ceres LM + GPU EvaluationCallback": real Ceres' LM over the engine against real Ceres' LM over AutoDiff
+    of the restated functor, on real EuRoC image content.  The callback protocol holds on every call, and the
+    trust-region sequence has residual-only candidates ("rn") followed, after an accepted step, by a Jacobian
+    evaluation at the same point ("Js")."""
+    ref = CR.run("cpu", c2, iters=12, huber=9.0, threads=THREADS)
+    got = CR.run("gpu", c2, iters=12, huber=9.0, threads=THREADS)
+    p = got["protocol"]
+    assert p["violations"] == 0, p
+    log = [p["log"][i:i + 2] for i in range(0, len(p["log"]), 2)]
+    assert log[0] == "Jn" and "rn" in log and "Js" in log, log
+    for a, b in zip(log, log[1:]):
+        if b == "Js":
+            assert a == "rn", log  # an accepted candidate is re-evaluated with Jacobians at the same point
+    assert_same_trajectory(got, ref)
+    assert got["costs"][-1] < 0.2 * got["costs"][0]
+    np.testing.assert_allclose(got["poses"][:, 4:], ref["poses"][:, 4:], atol=1e-5)
+    np.testing.assert_allclose(got["rho"], ref["rho"], rtol=1e-4, atol=1e-4 * np.abs(ref["rho"]).max())
+    # the end-to-end rate of the drop-in (Ceres' own timers), for the record
+    print(f"\nC2 Ceres drop-in: {got['jacobian_evaluations']} J evaluations in {got['jacobian_evaluation_s']:.3f} s "
+          f"(CPU AutoDiff {ref['jacobian_evaluation_s']:.3f} s on {ref['threads']} threads)")
+
+
+# ---------------------------------------------------------------------------------------------------- C4
+@pytest.fixture(scope="module")
+def c4():
+    import torch
+    pb, images = synth.c4_shard(torch.device("cuda", 0))
+    return pb, images
+
+
+def test_c4_full_size_parity_and_properties(c4):
+    import torch
+    pb, images = c4
+    assert pb.n_blocks == 400000 and pb.n_frames == 1004
+    rng = np.random.default_rng(3)
+    states = []
+    for _ in range(2):
+        poses = synth.se3_plus(pb.poses, 1e-3 * rng.normal(0, 1, (pb.n_frames, 6)))
+        rho = pb.rho * (1 + 0.01 * rng.normal(0, 1, pb.n_points))
+        states.append((torch.from_numpy(poses).cuda(), torch.from_numpy(rho).cuda(), poses, rho))
+    with E.Engine(0, 0, huber_width=9.0) as eng:
+        eng.set_problem(pb, images_device_ptr=images.data_ptr())
+        # (1) the one-launch state-adopting evaluation …
+        eng.evaluate_state_device(states[1][0].data_ptr(), states[1][1].data_ptr(), True)
+        rec_a, valid_a = eng.records()
+        cost_a = eng.block_costs()
+        # … is bit-identical to set_state_device + evaluate
+        eng.set_state_device(states[0][0].data_ptr(), states[0][1].data_ptr())
+        eng.evaluate(True)
+        eng.set_state_device(states[1][0].data_ptr(), states[1][1].data_ptr())
+        eng.evaluate(True)
+        rec_b, valid_b = eng.records()
+        assert np.array_equal(valid_a, valid_b) and np.array_equal(rec_a.view(np.uint32), rec_b.view(np.uint32))
+        # fp16 records: every value within 2⁻¹¹ relative + 2⁻¹⁴ absolute of the fp32 record
+        eng.set_record_format(E.RECORD_F16)
+        eng.evaluate(True)
+        rec_h, valid_h = eng.records()
+    assert np.array_equal(valid_h, valid_a)
+    bad = ~(np.abs(rec_h - rec_a) <= 2.0 ** -11 * np.abs(rec_a) + 2.0 ** -14)
+    if bad.any():
+        i, j = np.argwhere(bad)[0]
+        pytest.fail(f"fp16 records: {bad.sum()} values out of bound, max|fp32| {np.abs(rec_a).max():.4g}, "
+                    f"columns {np.unique(np.nonzero(bad)[1])[:20]}, e.g. [{i},{j}] {rec_a[i, j]!r} -> {rec_h[i, j]!r}")
+    # full size: every block valid (targets are 1-4 keyframes ahead, points well inside), all finite
+    assert valid_a.all() and np.isfinite(rec_a).all()
+    # per-block cost = ½ρ(Σr²) from the record's residuals (Huber 9, loss_function.cc:48-62)
+    r = rec_a[:, :8].astype(np.float64)
+    s = (r * r).sum(1)
+    c_ref = np.where(s <= 81.0, 0.5 * s, 0.5 * (2 * 9.0 * np.sqrt(s) - 81.0))
+    np.testing.assert_allclose(cost_a, c_ref, rtol=2e-6, atol=1e-4)
+    # sampled oracle parity: 4096 blocks spread over all 1000 hosts
+    sel = np.linspace(0, pb.n_blocks - 1, 4096).astype(np.int64)
+    assert len(np.unique(pb.point_host[pb.block_point[sel]])) >= 900
+    sub = synth.Problem(**{**pb.__dict__, "images": images.cpu().numpy(), "block_point": pb.block_point[sel],
+                           "block_target": pb.block_target[sel], "poses": states[1][2], "rho": states[1][3]})
+    ref, vref = O.evaluate(sub)
+    compare_records(0, 8, rec_a[sel], ref, valid_a[sel], vref, projected_uv(sub))
+
+
+def test_c4_gauss_newton_iteration_on_rendered_images(monkeypatch):
+    """One LM iteration of the on-device Schur GN at full C4 size on rendered images: the block-cyclic-reduction
+    step equals the band-Cholesky step to 1e-7, the reduced system is finite, and the accepted step lowers the cost."""
+    import torch
+    pb, images = synth.c4_shard(torch.device("cuda", 0), texture="render")
+    steps = {}
+    for solver in ("cr", "band"):
+        monkeypatch.setenv("PBA_SOLVER", solver)
+        with E.Engine(0, 0, huber_width=9.0) as eng:
+            eng.set_problem(pb, images_device_ptr=images.data_ptr())
+            eng.set_fixed_frames(np.array([0, 1], np.int32))
+            eng.set_state(pb.poses, pb.rho)
+            c0 = eng.gn_linearize()
+            m, st = eng.gn_step(1e-4)
+            assert st == 0 and m > 0
+            steps[solver] = eng.gn_last_step()
+            c1 = eng.gn_candidate_cost()
+            if solver == "cr":
+                eng.set_state(pb.poses, pb.rho)
+                s = eng.solve(max_iterations=1)
+                assert s["successful_steps"] == 1 and s["final_cost"] < s["initial_cost"], s
+        assert np.isfinite(steps[solver][0]).all() and np.isfinite(steps[solver][1]).all()
+        assert c1 < c0, (solver, c0, c1)
+    for a, b in zip(steps["cr"], steps["band"]):
+        assert np.linalg.norm(a - b) <= 1e-7 * np.linalg.norm(b)

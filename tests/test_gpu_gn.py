@@ -93,21 +93,58 @@ def test_candidate_cost_and_accept():
     assert abs(c_new - c_ref) <= 1e-5 * c_ref + 1e-6
 
 
-@pytest.mark.parametrize("kind,model,huber", [(0, 0, 9.0), (1, 0, 1.0), (1, 1, 1.0)])
-def test_lm_matches_reference_lm(kind, model, huber):
+LM_CASES = [
+    # kind, model, huber, pose σ, ρ σ, min_relative_decrease, iterations
+    (0, 0, 9.0, 0.003, 0.02, 1e-3, 15),
+    (1, 0, 1.0, 0.003, 0.02, 1e-3, 15),
+    (1, 1, 1.0, 0.003, 0.02, 1e-3, 15),
+    (1, 0, 1.0, 0.05, 0.3, 1e-3, 15),  # converges (function tolerance) after 9 trials
+    # a strict acceptance threshold forces rejected steps: the reference's relative decreases are 1.77 1.92 2.07
+    # 1.89 1.23, then 0.896 0.896 0.896 0.897 0.905 0.902 0.919 (all rejected: margin ≥ 0.03), then ≈ 1.0
+    (0, 0, 9.0, 0.003, 0.02, 0.95, 15),
+]
+
+
+@pytest.mark.parametrize("kind,model,huber,ps,rs,min_rel,iters", LM_CASES)
+def test_lm_matches_reference_lm(kind, model, huber, ps, rs, min_rel, iters):
+    """The device LM loop (lm_decide_kernel + gated accept / speculative linearisation) takes the same trust-region
+    decisions as the host reference of trust_region_minimizer.cc: same iterations, successful and unsuccessful
+    step counts, termination, final cost, poses and inverse distances."""
     pb = synth.make_problem(kind=kind, model=model, n_frames=8, n_points=120, width=376, height=240, seed=31,
-                            border=12, obs_sigma=0.3)
+                            border=12, obs_sigma=0.3, pose_sigma=ps, rho_sigma=rs)
     pb.poses[:2] = pb.poses_gt[:2]
     fixed = (0, 1)
-    p_ref, r_ref, c0_ref, c1_ref, it_ref = GR.lm(pb, huber, fixed, max_iterations=15)
+    p_ref, r_ref, c0_ref, c1_ref, it_ref, info = GR.lm(pb, huber, fixed, max_iterations=iters,
+                                                        min_relative_decrease=min_rel, summary=True)
     with make_engine(pb, huber, fixed) as eng:
-        summ = eng.solve(max_iterations=15)
+        summ = eng.solve(max_iterations=iters, min_relative_decrease=min_rel)
         poses, rho = eng.get_state()
     assert abs(summ["initial_cost"] - c0_ref) <= 1e-5 * c0_ref
     assert summ["final_cost"] < summ["initial_cost"]
     assert abs(summ["final_cost"] - c1_ref) <= 1e-3 * c1_ref + 1e-6, (summ, c1_ref)
+    assert summ["iterations"] == it_ref, (summ, it_ref, info)
+    assert summ["successful_steps"] == info["successful_steps"], (summ, info)
+    assert summ["unsuccessful_steps"] == info["unsuccessful_steps"], (summ, info)
+    assert (summ["termination"] == 0) == info["converged"], (summ, info)
     np.testing.assert_allclose(poses[:, 4:], p_ref[:, 4:], atol=1e-5)
     np.testing.assert_allclose(poses[:, :4] * np.sign(poses[:, 3:4]), p_ref[:, :4] * np.sign(p_ref[:, 3:4]), atol=1e-5)
+    np.testing.assert_allclose(rho, r_ref, rtol=1e-4)
+
+
+def test_point_without_blocks_keeps_its_state():
+    """A landmark observed only by its host has no residual block (map_utils.h:347-375 adds none; pba_map_load
+    keeps it as a point).  Ceres never sees its inverse distance, so solve() must leave it bit-identical."""
+    pb = synth.make_problem(kind="geometric", n_frames=8, n_points=100, width=376, height=240, seed=33, border=12)
+    keep = pb.block_point != 7
+    pb = synth.Problem(**{**pb.__dict__, "block_point": pb.block_point[keep], "block_target": pb.block_target[keep],
+                          "u_obs": pb.u_obs[keep]})
+    rho0 = pb.rho.copy()
+    with make_engine(pb, 1.0, (0,)) as eng:
+        summ = eng.solve(max_iterations=5)
+        _, rho = eng.get_state()
+    assert summ["successful_steps"] > 0
+    assert rho[7] == rho0[7]
+    assert np.abs(rho - rho0).max() > 0
 
 
 def test_photometric_lm_converges_towards_ground_truth():
