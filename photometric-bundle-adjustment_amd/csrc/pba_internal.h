@@ -10,6 +10,7 @@
 
 #include "pba.h"
 #include "pba_device.h"
+#include "pba_host.h"
 
 namespace pba {
 namespace detail {
@@ -314,11 +315,18 @@ __device__ __forceinline__ Row photometric_row(const KernelArgs& a, const TileBl
     o.tv = {-rf * q.x, -rf * q.y, -rf * q.z};
     o.tw = cross(q, pf);   // q·[p̃]×
     // ∂r/∂ρ = ∇I·∂π/∂p̃·t: ∂π/∂p̃·t cancels when t points along the ray (the epipolar motion is small),
-    // so those two dot products run in fp64 (fp32 left ~3e-5 relative error on J_ρ at short baselines)
-    Vec3d dud, dvd;
-    project_jac<MODEL>(pp.tk, p, iden, dud, dvd);
-    const Vec3d td = {pp.t[0], pp.t[1], pp.t[2]};
-    o.jr = (float)((double)gx * dot(dud, td) + (double)gy * dot(dvd, td));
+    // so the cancelling part runs in fp64 (fp32 left ~3e-5 relative error on J_ρ at short baselines)
+    if (MODEL == CAM_PINHOLE) {
+      // ∂u/∂p̃·t = fx/z (t_x − m_x t_z), ∂v/∂p̃·t = fy/z (t_y − m_y t_z), m = p̃_xy / z (the projection's own
+      // quotients): 7 fp64 operations instead of the general 2×3 Jacobian and two dot products
+      const double ex = fma(-(p.x * iden), pp.t[2], pp.t[0]), ey = fma(-(p.y * iden), pp.t[2], pp.t[1]);
+      o.jr = (float)(iden * fma((double)gx * pp.tk[0], ex, (double)gy * pp.tk[1] * ey));
+    } else {
+      Vec3d dud, dvd;
+      project_jac<MODEL>(pp.tk, p, iden, dud, dvd);
+      const Vec3d td = {pp.t[0], pp.t[1], pp.t[2]};
+      o.jr = (float)((double)gx * dot(dud, td) + (double)gy * dot(dvd, td));
+    }
   }
   return o;
 }
@@ -364,13 +372,6 @@ __device__ __forceinline__ Row geometric_row(const KernelArgs& a, int blk, int k
 // ---------------------------------------------------------------------------------------------------------
 // Host-side helpers
 // ---------------------------------------------------------------------------------------------------------
-extern thread_local std::string g_last_error;
-
-inline int fail(int code, const std::string& msg) {
-  g_last_error = msg;
-  return code;
-}
-
 #define PBA_HIP(expr)                                                                          \
   do {                                                                                         \
     hipError_t e_ = (expr);                                                                    \

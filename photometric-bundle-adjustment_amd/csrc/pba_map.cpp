@@ -27,7 +27,8 @@
 #include <unordered_map>
 #include <vector>
 
-#include "pba_internal.h"
+#include "pba.h"
+#include "pba_host.h"
 
 using pba::detail::fail;
 

@@ -27,7 +27,7 @@ import pytest
 import ceres_runner as CR
 import gn_reference as GR
 import oracle as O
-from helpers import compare_records, engine_module, projected_uv, synth
+from helpers import compare_records, engine_module, near_cell_boundary, projected_uv, synth
 
 pytestmark = pytest.mark.gpu
 E = engine_module()
@@ -171,7 +171,12 @@ def test_c4_full_size_parity_and_properties(c4):
         eng.evaluate(True)
         rec_h, valid_h = eng.records()
     assert np.array_equal(valid_h, valid_a)
-    bad = ~(np.abs(rec_h - rec_a) <= 2.0 ** -11 * np.abs(rec_a) + 2.0 ** -14)
+    # (the fp16 and fp32 launches are separate instantiations: at a pixel within 2e-3 px of a bilinear cell edge the
+    # last-ulp difference of the warp may pick the neighbouring cell, whose gradient differs — as in compare_records)
+    at1 = synth.Problem(**{**pb.__dict__, "poses": states[1][2], "rho": states[1][3]})
+    edge = near_cell_boundary(projected_uv(at1))                              # (n_blocks, 8)
+    col_edge = np.concatenate([np.zeros_like(edge), np.repeat(edge, 6, 1), np.repeat(edge, 6, 1), edge], 1)
+    bad = ~(np.abs(rec_h - rec_a) <= 2.0 ** -11 * np.abs(rec_a) + 2.0 ** -14) & ~col_edge
     if bad.any():
         i, j = np.argwhere(bad)[0]
         pytest.fail(f"fp16 records: {bad.sum()} values out of bound, max|fp32| {np.abs(rec_a).max():.4g}, "
