@@ -21,7 +21,8 @@
  *   block       (point, target keyframe); host = the point's host keyframe
  *   residuals   geometric: r = u_obs − π_t(T_w_t⁻¹ T_w_h b/ρ)                    (R = 2)
  *               photometric: r_k = I_t(π_t(R_th b_k + ρ t_th)) − I_h,k, k < P      (R = P)
- *               bilinear interpolation of the u8 target image, Grid2D-style edge clamp
+ *               bilinear (default) or Ceres' bicubic interpolation of the u8 target image (pba_set_interpolator),
+ *               Grid2D edge clamp
  *   record      per block, R×14 floats: [ r(R) | J_host(R×6) | J_target(R×6) | J_rho(R) ], row-major,
  *               tangent-space (= Ceres' J_global·P of residual_block.cc:136-158), NOT robustified
  *               (the loss stays with the caller, residual_block.cc:161-196).
@@ -90,7 +91,7 @@ int pba_set_frames_device(pba_engine* engine, int32_t n_frames, const int32_t* f
 int pba_set_pattern(pba_engine* engine, int32_t P, const float* offsets);
 /* points: host keyframe, u_ref (2 doubles, pixel in the host image), host_intensity (P floats,
  * photometric only — the I_h,k of photometric_error.h:179; NULL: sampled on the device from the host keyframe's
- * image at u_ref + pattern offset, bilinear). */
+ * image at u_ref + pattern offset, with the engine's interpolator: call pba_set_interpolator first). */
 int pba_set_points(pba_engine* engine, int32_t n_points, const int32_t* host_frame, const double* u_ref,
                    const float* host_intensity);
 /* blocks: point index and target keyframe per block; u_obs (2 doubles per block) for geometric engines.
@@ -124,6 +125,19 @@ int pba_record_floats(const pba_engine* engine);   /* 14·R (values per record, 
 #define PBA_RECORD_F16 1
 int pba_set_record_format(pba_engine* engine, int32_t format);
 int pba_record_format(const pba_engine* engine);
+/* Image interpolator of the photometric residual (and of the device-sampled I_h,k): PBA_INTERP_BILINEAR (default,
+ * the north star's) or PBA_INTERP_BICUBIC — Ceres' BiCubicInterpolator over Grid2D<uint8_t, 1>
+ * (cubic_interpolation.h:252-344, edge clamp :403-414), the interpolator of PhotometricError<8>
+ * (photometric_error.h:84): with PBA_CAMERA_EUCM the engine then evaluates that functor's residual exactly.
+ * Applies to every evaluation and Gauss-Newton entry point. */
+#define PBA_INTERP_BILINEAR 0
+#define PBA_INTERP_BICUBIC 1
+int pba_set_interpolator(pba_engine* engine, int32_t interpolator);
+int pba_interpolator(const pba_engine* engine);
+/* The interpolator at n positions uv (2 doubles each, (column, row) pixels, any value: outside the image the edge is
+ * clamped as Grid2D does) of one frame of the active level: out = 3 floats per position [I, ∂I/∂u, ∂I/∂v]
+ * (BiCubicInterpolator::Evaluate(r = v, c = u) returns f, dfdr = ∂I/∂v, dfdc = ∂I/∂u).  Synchronises. */
+int pba_sample_image(pba_engine* engine, int32_t frame, int32_t n, const double* uv, float* out);
 int pba_num_blocks(const pba_engine* engine);
 int pba_num_points(const pba_engine* engine);
 int pba_num_frames(const pba_engine* engine);

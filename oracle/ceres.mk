@@ -61,15 +61,19 @@ DRV_FLAGS := -std=c++17 -O2 -DNDEBUG -w -pthread $(CERES_DEFS) $(CERES_INC) -I$(
              -I$(REF)/include/visnav -I$(ROOT)/include -I$(ROOT)/tests/cpp
 DRV_LIBS := _ref/libceres.a -L$(PBA_LIB) -lpba -Wl,-rpath,'$$ORIGIN/../../photometric-bundle-adjustment_amd/csrc' -pthread
 
-drivers: _ref/ceres_lm_driver _ref/adapter_driver
+drivers: _ref/ceres_lm_driver _ref/adapter_driver _ref/golden_ceres
 
 _ref/ceres_lm_driver: $(ROOT)/tests/cpp/ceres_lm_driver.cpp $(ROOT)/tests/cpp/ceres_functors.h $(ROOT)/include/pba_ceres.h \
                       $(ROOT)/include/pba.h _ref/libceres.a $(PBA_LIB)/libpba.so
-	$(CXX) $(DRV_FLAGS) -o $@ $< $(DRV_LIBS)
+	$(CXX) $(DRV_FLAGS) -I$(CERES)/internal/ceres/autodiff_benchmarks -o $@ $< $(DRV_LIBS)
 
 # the adapter driver of tests/test_ceres_adapter.py, against the REAL ceres/ceres.h instead of the test double
 _ref/adapter_driver: $(ROOT)/tests/cpp/adapter_driver.cpp $(ROOT)/include/pba_ceres.h $(ROOT)/include/pba.h _ref/libceres.a $(PBA_LIB)/libpba.so
 	$(CXX) $(DRV_FLAGS) -o $@ $< $(DRV_LIBS)
+
+# golden vectors from Ceres' own BiCubicInterpolator and PhotometricError<8> (tests/golden/make_ceres_golden.py)
+_ref/golden_ceres: golden_ceres.cpp $(ROOT)/tests/cpp/ceres_functors.h _ref/libceres.a
+	$(CXX) $(DRV_FLAGS) -I$(CERES)/internal/ceres/autodiff_benchmarks -o $@ $< _ref/libceres.a -pthread
 
 .PHONY: drivers
 

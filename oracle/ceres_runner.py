@@ -30,8 +30,8 @@ def run(mode: str, pb, iters: int = 20, huber: float = 1.0, threads: int = 8, fi
         with open(fin, "wb") as f:
             write_problem(f, pb)
         fx = ",".join(str(int(i)) for i in fixed) if len(fixed) else "-"
-        subprocess.run([DRIVER, mode, fin, fout, str(iters), repr(float(huber)), str(threads), fx, repr(float(ftol))],
-                       check=True, timeout=timeout)
+        subprocess.run([DRIVER, mode, fin, fout, str(iters), repr(float(huber)), str(threads), fx, repr(float(ftol)),
+                        str(int(getattr(pb, "interp", 0)))], check=True, timeout=timeout)
         with open(fout) as f:
             out = json.load(f)
     out["poses"] = np.asarray(out["poses"]).reshape(-1, 7)

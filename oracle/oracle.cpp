@@ -309,17 +309,47 @@ inline void bilinear(const uint8_t* img, int W, int H, double u, double v, doubl
   *dfdu = (1.0 - b) * (I10 - I00) + b * (I11 - I01);
   *dfdv = (1.0 - a) * (I01 - I00) + a * (I11 - I10);
 }
+// Ceres' BiCubicInterpolator over Grid2D<uint8_t, 1> (cubic_interpolation.h:252-344): CubicHermiteSpline (:64-90)
+// along the four rows of the 4×4 neighbourhood, then along the column; Grid2D::GetValue clamps indices (:403-414).
+inline void hermite(double p0, double p1, double p2, double p3, double x, double* f, double* dfdx) {
+  const double a = 0.5 * (-p0 + 3.0 * p1 - 3.0 * p2 + p3);
+  const double b = 0.5 * (2.0 * p0 - 5.0 * p1 + 4.0 * p2 - p3);
+  const double c = 0.5 * (-p0 + p2);
+  const double d = p1;
+  if (f) *f = d + x * (c + x * (b + x * a));
+  if (dfdx) *dfdx = c + x * (2.0 * b + 3.0 * a * x);
+}
+inline void bicubic(const uint8_t* img, int W, int H, double u, double v, double* f, double* dfdu, double* dfdv) {
+  const double r = v, c = u;  // Evaluate(r, c): row = v, column = u (photometric_error.h:175-177)
+  const int row = (int)std::floor(r), col = (int)std::floor(c);
+  auto get = [&](int rr, int cc) {
+    rr = std::min(std::max(rr, 0), H - 1);
+    cc = std::min(std::max(cc, 0), W - 1);
+    return (double)img[(size_t)rr * W + cc];
+  };
+  double fr[4], dfr[4];
+  for (int i = 0; i < 4; ++i)
+    hermite(get(row - 1 + i, col - 1), get(row - 1 + i, col), get(row - 1 + i, col + 1), get(row - 1 + i, col + 2),
+            c - col, &fr[i], &dfr[i]);
+  hermite(fr[0], fr[1], fr[2], fr[3], r - row, f, dfdv);
+  hermite(dfr[0], dfr[1], dfr[2], dfr[3], r - row, dfdu, nullptr);
+}
+inline void sample(int interp_kind, const uint8_t* img, int W, int H, double u, double v, double* f, double* du,
+                   double* dv) {
+  if (interp_kind == 1) bicubic(img, W, H, u, v, f, du, dv);
+  else bilinear(img, W, H, u, v, f, du, dv);
+}
 template <int N>
-inline Jet<N> interp(const uint8_t* img, int W, int H, const Jet<N>& u, const Jet<N>& v) {
+inline Jet<N> interp(int ik, const uint8_t* img, int W, int H, const Jet<N>& u, const Jet<N>& v) {
   double f, du, dv;
-  bilinear(img, W, H, u.a, v.a, &f, &du, &dv);
+  sample(ik, img, W, H, u.a, v.a, &f, &du, &dv);
   Jet<N> r(f);
   for (int i = 0; i < N; ++i) r.v[i] = du * u.v[i] + dv * v.v[i];
   return r;
 }
-inline double interp(const uint8_t* img, int W, int H, double u, double v) {
+inline double interp(int ik, const uint8_t* img, int W, int H, double u, double v) {
   double f, du, dv;
-  bilinear(img, W, H, u, v, &f, &du, &dv);
+  sample(ik, img, W, H, u, v, &f, &du, &dv);
   return f;
 }
 
@@ -336,7 +366,7 @@ typedef struct {
   int32_t n_frames, n_points, n_blocks, n_cams;
   int32_t width, height;
   int32_t P;           // patch size (photometric)
-  int32_t pad_;
+  int32_t interp;      // 0 bilinear, 1 Ceres' bicubic (photometric)
   const double* intrinsics;     // 8 × n_cams
   const int32_t* frame_cam;     // n_frames
   const uint8_t* images;        // n_frames × height × width (photometric)
@@ -393,7 +423,7 @@ bool geometric_block(const orc_problem& pb, const double* poses, const double* r
   return std::isfinite(val(res[0])) && std::isfinite(val(res[1]));
 }
 
-// Photometric functor (photometric_error.h:139-182, bilinear interpolator, camera per frame).
+// Photometric functor (photometric_error.h:139-182, bilinear or bicubic interpolator, camera per frame).
 template <class T>
 bool photometric_block(const orc_problem& pb, const double* poses, const double* rho, int b, T* res) {
   const int pt = pb.block_point[b], tgt = pb.block_target[b], host = pb.point_host[pt];
@@ -422,7 +452,7 @@ bool photometric_block(const orc_problem& pb, const double* poses, const double*
     if (!in_domain(pb.model, kt, pv)) return false;
     T uv[2];
     project(pb.model, kt, p, uv);
-    const T I = interp(img, pb.width, pb.height, uv[0], uv[1]);
+    const T I = interp(pb.interp, img, pb.width, pb.height, uv[0], uv[1]);
     res[k] = I - (double)pb.host_intensity[(size_t)pb.P * pt + k];
     if (!std::isfinite(val(res[k]))) return false;
   }
@@ -547,6 +577,9 @@ void orc_se3_inverse(const double* T7, double* out7) {  // se3.hpp:208-211
 void orc_project(int model, const double* k8, const double* p3, double* uv2) { project<double>(model, k8, p3, uv2); }
 void orc_unproject(int model, const double* k8, const double* uv2, double* b3) { unproject(model, k8, uv2, b3); }
 int orc_in_domain(int model, const double* k8, const double* p3) { return in_domain(model, k8, p3) ? 1 : 0; }
+void orc_sample(int interp_kind, const uint8_t* img, int W, int H, double u, double v, double* f3) {
+  sample(interp_kind, img, W, H, u, v, &f3[0], &f3[1], &f3[2]);
+}
 void orc_bilinear(const uint8_t* img, int W, int H, double u, double v, double* f3) {
   bilinear(img, W, H, u, v, f3, f3 + 1, f3 + 2);
 }

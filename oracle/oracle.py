@@ -18,7 +18,7 @@ _LIB = None
 class OrcProblem(C.Structure):
     _fields_ = [("kind", C.c_int32), ("model", C.c_int32), ("n_frames", C.c_int32), ("n_points", C.c_int32),
                 ("n_blocks", C.c_int32), ("n_cams", C.c_int32), ("width", C.c_int32), ("height", C.c_int32),
-                ("P", C.c_int32), ("pad_", C.c_int32),
+                ("P", C.c_int32), ("interp", C.c_int32),
                 ("intrinsics", C.c_void_p), ("frame_cam", C.c_void_p), ("images", C.c_void_p),
                 ("pattern", C.c_void_p), ("point_host", C.c_void_p), ("u_ref", C.c_void_p),
                 ("host_intensity", C.c_void_p), ("block_point", C.c_void_p), ("block_target", C.c_void_p),
@@ -51,6 +51,7 @@ def lib():
         L.orc_in_domain.argtypes = [C.c_int, C.c_void_p, C.c_void_p]
         L.orc_in_domain.restype = C.c_int
         L.orc_bilinear.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_double, C.c_double, C.c_void_p]
+        L.orc_sample.argtypes = [C.c_int, C.c_void_p, C.c_int, C.c_int, C.c_double, C.c_double, C.c_void_p]
         L.orc_compute_projections.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
                                               C.c_void_p, C.c_int] + [C.c_void_p] * 9
         L.orc_compute_projections.restype = C.c_int
@@ -85,6 +86,7 @@ def make_problem_struct(pb, keep: _Keep) -> OrcProblem:
     s.n_cams = pb.intrinsics.shape[0]
     s.width, s.height = pb.width, pb.height
     s.P = pb.pattern.shape[0] if pb.kind == 0 else 2
+    s.interp = int(getattr(pb, "interp", 0))
     s.intrinsics = _ptr(keep(pb.intrinsics, np.float64))
     s.frame_cam = _ptr(keep(pb.frame_cam, np.int32))
     s.images = _ptr(keep(pb.images, np.uint8))
@@ -119,6 +121,20 @@ def evaluate(pb, poses=None, rho=None, want_jac: bool = True, n_threads: int = 1
     if rc != 0:
         raise RuntimeError(f"orc_evaluate failed ({rc})")
     return out, valid
+
+
+def sample(img: np.ndarray, uv: np.ndarray, interp: int = 0) -> np.ndarray:
+    """The oracle's interpolator (0 bilinear, 1 Ceres' bicubic) of a u8 image at (column, row) positions:
+    (n, 3) float64 [I, ∂I/∂u, ∂I/∂v]."""
+    L = lib()
+    img = np.ascontiguousarray(img, np.uint8)
+    uv = np.asarray(uv, np.float64).reshape(-1, 2)
+    out = np.zeros((uv.shape[0], 3))
+    f3 = np.zeros(3)
+    for i, (u, v) in enumerate(uv):
+        L.orc_sample(int(interp), _ptr(img), img.shape[1], img.shape[0], float(u), float(v), _ptr(f3))
+        out[i] = f3
+    return out
 
 
 def split_record(out: np.ndarray, R: int):

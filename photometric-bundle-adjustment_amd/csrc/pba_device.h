@@ -290,4 +290,54 @@ __device__ __forceinline__ void bilinear(const uint8_t* __restrict__ img, int W,
   bilinear_eval(bilinear_taps(img, W, H, tiles_x, u, v), I, gx, gy);
 }
 
+// Ceres' BiCubicInterpolator over Grid2D<uint8_t, 1> (cubic_interpolation.h:252-344, the interpolator of
+// PhotometricError, photometric_error.h:84): four horizontal cubic Hermite (Catmull-Rom) splines through the 4×4 taps
+// around (⌊v⌋, ⌊u⌋), value and ∂/∂u per row, then one vertical spline of the values (→ I, ∂I/∂v) and one of the
+// row derivatives (→ ∂I/∂u).  fp64 as Ceres (CubicHermiteSpline :64-90, same operation order).  The 4-texel apron is
+// Grid2D's edge clamp (:403-414) for every tap of a position inside [−2, W+1] × [−2, H+1]; beyond that all 16 taps
+// of Ceres' unclamped evaluation are the same edge texel, which the clamped position reproduces (constant spline).
+__device__ __forceinline__ void hermite(double p0, double p1, double p2, double p3, double x, double& f, double& df) {
+  const double a = 0.5 * (-p0 + 3.0 * p1 - 3.0 * p2 + p3);
+  const double b = 0.5 * (2.0 * p0 - 5.0 * p1 + 4.0 * p2 - p3);
+  const double c = 0.5 * (-p0 + p2);
+  const double d = p1;
+  f = d + x * (c + x * (b + x * a));
+  df = c + x * (2.0 * b + 3.0 * a * x);
+}
+__device__ __forceinline__ void bicubic(const uint8_t* __restrict__ img, int W, int H, int tiles_x, double u, double v,
+                                        float& I, float& gx, float& gy) {
+  u = fmin(fmax(u, -2.0), (double)W + 1.0);
+  v = fmin(fmax(v, -2.0), (double)H + 1.0);
+  const double xf = floor(u), yf = floor(v);
+  const int xp = (int)xf + kImgPad, yp = (int)yf + kImgPad;  // taps xp−1 … xp+2 ∈ [1, W+7]: inside the apron
+  const double x = u - xf, y = v - yf;
+  double f[4], dfdc[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    double p[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) p[c] = (double)img[texel_index(xp - 1 + c, yp - 1 + r, tiles_x)];
+    hermite(p[0], p[1], p[2], p[3], x, f[r], dfdc[r]);
+  }
+  double val, dfdr, dfdu, unused;
+  hermite(f[0], f[1], f[2], f[3], y, val, dfdr);
+  hermite(dfdc[0], dfdc[1], dfdc[2], dfdc[3], y, dfdu, unused);
+  I = (float)val;
+  gx = (float)dfdu;
+  gy = (float)dfdr;
+}
+
+enum : int { INTERP_BILINEAR = 0, INTERP_BICUBIC = 1 };
+
+// The kernels' photometric template parameter carries the camera model and the interpolator: PM = model + 4·interp.
+__host__ __device__ constexpr int cam_of(int pm) { return pm & 3; }
+__host__ __device__ constexpr int interp_of(int pm) { return pm >> 2; }
+
+template <int INTERP>
+__device__ __forceinline__ void interpolate(const uint8_t* __restrict__ img, int W, int H, int tiles_x, double u, double v,
+                                            float& I, float& gx, float& gy) {
+  if (INTERP == INTERP_BICUBIC) bicubic(img, W, H, tiles_x, u, v, I, gx, gy);
+  else bilinear(img, W, H, tiles_x, u, v, I, gx, gy);
+}
+
 }  // namespace pba

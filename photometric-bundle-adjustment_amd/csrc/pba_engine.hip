@@ -122,7 +122,7 @@ __device__ __forceinline__ void store_slab(const unsigned char* src, unsigned ch
   }
 }
 
-template <int MODEL, int LPB, int MODE, class T>
+template <int PM, int LPB, int MODE, class T>  // PM = camera model + 4 · interpolator
 __global__ __launch_bounds__(kBlockThreads) void photometric_block_kernel(const KernelArgs a) {
   constexpr int BPW = kBlockThreads / LPB;  // blocks per workgroup
   constexpr bool JAC = MODE == 1;
@@ -147,7 +147,7 @@ __global__ __launch_bounds__(kBlockThreads) void photometric_block_kernel(const 
   const float Ih = act ? a.host_int[(long long)pt * P + k] : 0.0f;
   __syncthreads();
   Row row;
-  if (act) row = photometric_row<MODEL, JAC>(a, s_tb[lb], s_pat[k], Ih);
+  if (act) row = photometric_row<PM, JAC>(a, s_tb[lb], s_pat[k], Ih);
   // per-block validity (ballot over the wave: the block's LPB lanes are an aligned bit field) and ‖r‖²
   const int ok = group_all<LPB>(act ? row.ok : 1);
   const float s = group_sum<LPB>(act ? row.r * row.r : 0.0f);
@@ -196,7 +196,7 @@ __host__ __device__ constexpr int multi_stage_bytes(int bpw, int P, int tsize) {
 template <int PPL, class T>
 constexpr int kMultiThreads = 32 * 14 * 8 * PPL * (int)sizeof(T) + 32 * (int)sizeof(TileBlock) > 60 * 1024 ? 128 : 256;
 
-template <int MODEL, int MODE, class T, int PPL>
+template <int PM, int MODE, class T, int PPL>
 __global__ __launch_bounds__((kMultiThreads<PPL, T>)) void photometric_block_kernel_multi(const KernelArgs a) {
   constexpr int LPB = 8, NTH = kMultiThreads<PPL, T>, BPW = NTH / LPB;
   constexpr bool JAC = MODE == 1;
@@ -233,7 +233,7 @@ __global__ __launch_bounds__((kMultiThreads<PPL, T>)) void photometric_block_ker
     const int px = k + LPB * j;
     const bool act = live && px < P;
     Row row;
-    if (act) row = photometric_row<MODEL, JAC>(a, s_tb[lb], s_pat[px], Ih[j]);
+    if (act) row = photometric_row<PM, JAC>(a, s_tb[lb], s_pat[px], Ih[j]);
     okl &= act ? row.ok : 1;
     s += act ? row.r * row.r : 0.0f;
     rr[j] = row.r;
@@ -344,21 +344,23 @@ __global__ __launch_bounds__(kBlockThreads) void geometric_block_kernel(const Ke
 }
 
 template <int MODEL>
-void launch_blocks(pba_engine* e, const KernelArgs& ka, int mode) {
-  if (e->opt.residual_kind == PBA_RESIDUAL_GEOMETRIC) {
-    const int grid = (e->n_blocks + kBlockThreads - 1) / kBlockThreads;
-    if (mode == 1) geometric_block_kernel<MODEL, true><<<grid, kBlockThreads, 0, e->stream>>>(ka);
-    else geometric_block_kernel<MODEL, false><<<grid, kBlockThreads, 0, e->stream>>>(ka);
-    return;
-  }
+void launch_geometric(pba_engine* e, const KernelArgs& ka, int mode) {
+  const int grid = (e->n_blocks + kBlockThreads - 1) / kBlockThreads;
+  if (mode == 1) geometric_block_kernel<MODEL, true><<<grid, kBlockThreads, 0, e->stream>>>(ka);
+  else geometric_block_kernel<MODEL, false><<<grid, kBlockThreads, 0, e->stream>>>(ka);
+}
+
+// PM = camera model + 4 · interpolator (pba_device.h)
+template <int PM>
+void launch_photometric(pba_engine* e, const KernelArgs& ka, int mode) {
   const bool h = e->record_format == PBA_RECORD_F16;
   if (e->P <= 8) {
     const int grid = (int)(((long long)e->n_blocks * 8 + kBlockThreads - 1) / kBlockThreads);
-    if (mode == 1 && h) photometric_block_kernel<MODEL, 8, 1, _Float16><<<grid, kBlockThreads, 0, e->stream>>>(ka);
-    else if (mode == 1) photometric_block_kernel<MODEL, 8, 1, float><<<grid, kBlockThreads, 0, e->stream>>>(ka);
-    else if (mode == 0 && h) photometric_block_kernel<MODEL, 8, 0, _Float16><<<grid, kBlockThreads, 0, e->stream>>>(ka);
-    else if (mode == 0) photometric_block_kernel<MODEL, 8, 0, float><<<grid, kBlockThreads, 0, e->stream>>>(ka);
-    else photometric_block_kernel<MODEL, 8, 2, float><<<grid, kBlockThreads, 0, e->stream>>>(ka);
+    if (mode == 1 && h) photometric_block_kernel<PM, 8, 1, _Float16><<<grid, kBlockThreads, 0, e->stream>>>(ka);
+    else if (mode == 1) photometric_block_kernel<PM, 8, 1, float><<<grid, kBlockThreads, 0, e->stream>>>(ka);
+    else if (mode == 0 && h) photometric_block_kernel<PM, 8, 0, _Float16><<<grid, kBlockThreads, 0, e->stream>>>(ka);
+    else if (mode == 0) photometric_block_kernel<PM, 8, 0, float><<<grid, kBlockThreads, 0, e->stream>>>(ka);
+    else photometric_block_kernel<PM, 8, 2, float><<<grid, kBlockThreads, 0, e->stream>>>(ka);
     return;
   }
   // 9…32 pixels: 8 lanes per block, ⌈P/8⌉ pixels per lane
@@ -368,7 +370,7 @@ void launch_blocks(pba_engine* e, const KernelArgs& ka, int mode) {
     const int grid = (int)(((long long)e->n_blocks * 8 + nth - 1) / nth);                              \
     const size_t lds = (M == 1 ? multi_stage_bytes(nth / 8, e->P, (int)sizeof(TT)) : 0) +              \
                        (size_t)(nth / 8) * sizeof(TileBlock);                                           \
-    photometric_block_kernel_multi<MODEL, M, TT, PPL><<<grid, nth, lds, e->stream>>>(ka);               \
+    photometric_block_kernel_multi<PM, M, TT, PPL><<<grid, nth, lds, e->stream>>>(ka);                  \
   }
 #define PBA_LAUNCH_PPL(PPL)                                        \
   if (mode == 1 && h) PBA_LAUNCH_ONE(PPL, 1, _Float16)             \
@@ -385,11 +387,24 @@ void launch_blocks(pba_engine* e, const KernelArgs& ka, int mode) {
 }
 
 void launch_mode(pba_engine* e, const KernelArgs& ka, int mode) {
-  switch (e->opt.camera_model) {
-    case PBA_CAMERA_PINHOLE: launch_blocks<CAM_PINHOLE>(e, ka, mode); break;
-    case PBA_CAMERA_DOUBLE_SPHERE: launch_blocks<CAM_DS>(e, ka, mode); break;
-    case PBA_CAMERA_EUCM: launch_blocks<CAM_EUCM>(e, ka, mode); break;
-    default: launch_blocks<CAM_KB4>(e, ka, mode); break;
+  if (e->opt.residual_kind == PBA_RESIDUAL_GEOMETRIC) {
+    switch (e->opt.camera_model) {
+      case PBA_CAMERA_PINHOLE: launch_geometric<CAM_PINHOLE>(e, ka, mode); break;
+      case PBA_CAMERA_DOUBLE_SPHERE: launch_geometric<CAM_DS>(e, ka, mode); break;
+      case PBA_CAMERA_EUCM: launch_geometric<CAM_EUCM>(e, ka, mode); break;
+      default: launch_geometric<CAM_KB4>(e, ka, mode); break;
+    }
+    return;
+  }
+  switch (e->opt.camera_model + 4 * e->interp) {
+    case 0: launch_photometric<0>(e, ka, mode); break;
+    case 1: launch_photometric<1>(e, ka, mode); break;
+    case 2: launch_photometric<2>(e, ka, mode); break;
+    case 3: launch_photometric<3>(e, ka, mode); break;
+    case 4: launch_photometric<4>(e, ka, mode); break;
+    case 5: launch_photometric<5>(e, ka, mode); break;
+    case 6: launch_photometric<6>(e, ka, mode); break;
+    default: launch_photometric<7>(e, ka, mode); break;
   }
 }
 

@@ -157,7 +157,7 @@ __constant__ const auto kSlotTable = make_slot_table(std::make_integer_sequence<
 // VGPRs (56, no AGPRs, no spills) instead of 62 VGPRs + 4 AGPRs at 7 waves (linearise 0.101 -> 0.098 ms per LM
 // iteration at C4, tools/ab_bench.sh); the other instantiations would spill under that request.
 template <int KIND, int MODEL, int LPB>
-constexpr int kLinWaves = KIND == PBA_RESIDUAL_PHOTOMETRIC && MODEL == CAM_PINHOLE && LPB == 8 ? 8 : 1;
+constexpr int kLinWaves = KIND == PBA_RESIDUAL_PHOTOMETRIC && MODEL == CAM_PINHOLE + 4 * INTERP_BILINEAR && LPB == 8 ? 8 : 1;
 
 template <int KIND, int MODEL, int LPB>
 __global__ __launch_bounds__(kBlockThreads) __attribute__((amdgpu_waves_per_eu(kLinWaves<KIND, MODEL, LPB>, 8)))
@@ -1827,7 +1827,7 @@ int gn_prepare(pba_engine* e) {
   return PBA_OK;
 }
 
-template <int KIND, int MODEL>
+template <int KIND, int MODEL>  // photometric: MODEL = camera model + 4 · interpolator
 void launch_linearize(pba_engine* e, const KernelArgs& ka, const LinArgs& la) {
   const int grid = la.n_chunks;
   switch (e->gn.lpb) {
@@ -1838,13 +1838,25 @@ void launch_linearize(pba_engine* e, const KernelArgs& ka, const LinArgs& la) {
   }
 }
 
-template <int KIND>
-void launch_linearize_k(pba_engine* e, const KernelArgs& ka, const LinArgs& la) {
+void launch_linearize_photometric(pba_engine* e, const KernelArgs& ka, const LinArgs& la) {
+  switch (e->opt.camera_model + 4 * e->interp) {
+    case 0: launch_linearize<PBA_RESIDUAL_PHOTOMETRIC, 0>(e, ka, la); break;
+    case 1: launch_linearize<PBA_RESIDUAL_PHOTOMETRIC, 1>(e, ka, la); break;
+    case 2: launch_linearize<PBA_RESIDUAL_PHOTOMETRIC, 2>(e, ka, la); break;
+    case 3: launch_linearize<PBA_RESIDUAL_PHOTOMETRIC, 3>(e, ka, la); break;
+    case 4: launch_linearize<PBA_RESIDUAL_PHOTOMETRIC, 4>(e, ka, la); break;
+    case 5: launch_linearize<PBA_RESIDUAL_PHOTOMETRIC, 5>(e, ka, la); break;
+    case 6: launch_linearize<PBA_RESIDUAL_PHOTOMETRIC, 6>(e, ka, la); break;
+    default: launch_linearize<PBA_RESIDUAL_PHOTOMETRIC, 7>(e, ka, la); break;
+  }
+}
+
+void launch_linearize_geometric(pba_engine* e, const KernelArgs& ka, const LinArgs& la) {
   switch (e->opt.camera_model) {
-    case PBA_CAMERA_PINHOLE: launch_linearize<KIND, CAM_PINHOLE>(e, ka, la); break;
-    case PBA_CAMERA_DOUBLE_SPHERE: launch_linearize<KIND, CAM_DS>(e, ka, la); break;
-    case PBA_CAMERA_EUCM: launch_linearize<KIND, CAM_EUCM>(e, ka, la); break;
-    default: launch_linearize<KIND, CAM_KB4>(e, ka, la); break;
+    case PBA_CAMERA_PINHOLE: launch_linearize<PBA_RESIDUAL_GEOMETRIC, CAM_PINHOLE>(e, ka, la); break;
+    case PBA_CAMERA_DOUBLE_SPHERE: launch_linearize<PBA_RESIDUAL_GEOMETRIC, CAM_DS>(e, ka, la); break;
+    case PBA_CAMERA_EUCM: launch_linearize<PBA_RESIDUAL_GEOMETRIC, CAM_EUCM>(e, ka, la); break;
+    default: launch_linearize<PBA_RESIDUAL_GEOMETRIC, CAM_KB4>(e, ka, la); break;
   }
 }
 
@@ -1892,8 +1904,8 @@ int linearize(pba_engine* e, double* cost, const double* gate = nullptr) {
   launch_pairs(e, e->poses.p, e->pairs.p);
   const KernelArgs ka = make_kernel_args(e, e->pairs.p, e->rho.p);
   LinArgs la{G.gn_block.p, G.chunk_desc.p, G.blk_lt.p, G.blk_schur.p, G.part_lin.p, G.n_chunks, gate};
-  if (e->opt.residual_kind == PBA_RESIDUAL_PHOTOMETRIC) launch_linearize_k<PBA_RESIDUAL_PHOTOMETRIC>(e, ka, la);
-  else launch_linearize_k<PBA_RESIDUAL_GEOMETRIC>(e, ka, la);
+  if (e->opt.residual_kind == PBA_RESIDUAL_PHOTOMETRIC) launch_linearize_photometric(e, ka, la);
+  else launch_linearize_geometric(e, ka, la);
   PBA_HIP(hipGetLastError());
   e->evaluated = false;  // records are not written in GN mode
   if (cost) return total_cost(e, cost, nullptr);

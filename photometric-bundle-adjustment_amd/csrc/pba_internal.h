@@ -278,11 +278,13 @@ __device__ __forceinline__ void adopt_state(const KernelArgs& a) {
   if (g < a.n_pose_d) a.adopt_poses[g] = p;
 }
 
-// Photometric row k of a staged block (photometric_error.h:139-182 with the bilinear interpolator; the
+// Photometric row k of a staged block (photometric_error.h:139-182 with the bilinear or Ceres' bicubic interpolator; the
 // Jacobian chain of pba_device.h).  Warp and projection in fp64, chain in fp32.  off = pattern offset k,
 // Ih = host intensity I_h,k.
-template <int MODEL, bool JAC>
+// PM = camera model + 4 · interpolator (pba_device.h cam_of / interp_of).
+template <int PM, bool JAC>
 __device__ __forceinline__ Row photometric_row(const KernelArgs& a, const TileBlock& tb, float2 off, float Ih) {
+  constexpr int MODEL = cam_of(PM);
   Row o;
   const PairRec& pp = tb.pr;
   const double rho = tb.rho;
@@ -296,7 +298,8 @@ __device__ __forceinline__ Row photometric_row(const KernelArgs& a, const TileBl
   if (dom) {
     double u, v;
     iden = project<MODEL>(pp.tk, p, u, v);
-    bilinear(a.images + (long long)pp.target * a.frame_stride, a.width, a.height, a.tiles_x, u, v, I, gx, gy);
+    interpolate<interp_of(PM)>(a.images + (long long)pp.target * a.frame_stride, a.width, a.height, a.tiles_x, u, v,
+                               I, gx, gy);
   }
   o.r = I - Ih;  // photometric_error.h:179
   o.ok = dom && isfinite(o.r);
@@ -526,6 +529,7 @@ struct pba_engine {
   pba::detail::DevBuf<float> out, cost;
   pba::detail::DevBuf<uint8_t> valid;
   int record_format = PBA_RECORD_F32;
+  int interp = PBA_INTERP_BILINEAR;  // pba_set_interpolator
   bool state_set = false;
   bool pairs_fresh = false;          // pairs hold T_th of the current poses (pba_set_state_device forms them)
   bool evaluated = false;

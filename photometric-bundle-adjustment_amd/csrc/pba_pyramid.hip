@@ -50,7 +50,8 @@ __global__ void scale_points_kernel(const double2* __restrict__ u0, double2* __r
   if (i < n) ul[i] = make_double2((u0[i].x + 0.5) * s - 0.5, (u0[i].y + 0.5) * s - 0.5);
 }
 
-// I_h,k = bilinear(host image, u_ref + offset_k), one lane per (point, k)
+// I_h,k = interpolated host image at u_ref + offset_k (the engine's interpolator), one lane per (point, k)
+template <int INTERP>
 __global__ void host_intensity_kernel(const uint8_t* __restrict__ images, long long frame_stride, int W, int H,
                                       const double2* __restrict__ u_ref, const int* __restrict__ host,
                                       const float* __restrict__ pattern, int P, float* __restrict__ out, long long n) {
@@ -59,9 +60,22 @@ __global__ void host_intensity_kernel(const uint8_t* __restrict__ images, long l
   const int pt = (int)(i / P), k = (int)(i - (long long)pt * P);
   const double2 u = u_ref[pt];
   float I, gx, gy;
-  bilinear(images + (long long)host[pt] * frame_stride, W, H, tiles_x_of(W), u.x + (double)pattern[2 * k],
-           u.y + (double)pattern[2 * k + 1], I, gx, gy);
+  interpolate<INTERP>(images + (long long)host[pt] * frame_stride, W, H, tiles_x_of(W), u.x + (double)pattern[2 * k],
+                      u.y + (double)pattern[2 * k + 1], I, gx, gy);
   out[i] = I;
+}
+
+// pba_sample_image: the engine's interpolator at caller positions of one frame (value and gradient)
+template <int INTERP>
+__global__ void sample_image_kernel(const uint8_t* __restrict__ img, int W, int H, const double2* __restrict__ uv,
+                                    float* __restrict__ out, int n) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  float I, gx, gy;
+  interpolate<INTERP>(img, W, H, tiles_x_of(W), uv[i].x, uv[i].y, I, gx, gy);
+  out[3 * i] = I;
+  out[3 * i + 1] = gx;
+  out[3 * i + 2] = gy;
 }
 
 void swap_buf(DevBuf<uint8_t>& a, DevBuf<uint8_t>& b) { std::swap(a.p, b.p); std::swap(a.n, b.n); }
@@ -96,9 +110,14 @@ int sample_host_intensities(pba_engine* e, const double2* u_ref, float* out) {
   if (n == 0) return PBA_OK;
   DevBuf<float> pat;
   PBA_HIP(pat.upload(e->pattern_h, e->stream));
-  host_intensity_kernel<<<(unsigned)((n + 255) / 256), 256, 0, e->stream>>>(
-      e->images.p, tiled_frame_bytes(e->width, e->height), e->width, e->height, u_ref, e->point_host_d.p, pat.p, e->P,
-      out, n);
+  const unsigned grid = (unsigned)((n + 255) / 256);
+  const long long fs = tiled_frame_bytes(e->width, e->height);
+  if (e->interp == INTERP_BICUBIC)
+    host_intensity_kernel<INTERP_BICUBIC><<<grid, 256, 0, e->stream>>>(e->images.p, fs, e->width, e->height, u_ref,
+                                                                         e->point_host_d.p, pat.p, e->P, out, n);
+  else
+    host_intensity_kernel<INTERP_BILINEAR><<<grid, 256, 0, e->stream>>>(e->images.p, fs, e->width, e->height, u_ref,
+                                                                          e->point_host_d.p, pat.p, e->P, out, n);
   PBA_HIP(hipGetLastError());
   PBA_HIP(hipStreamSynchronize(e->stream));
   return PBA_OK;
@@ -108,6 +127,40 @@ int sample_host_intensities(pba_engine* e, const double2* u_ref, float* out) {
 }  // namespace pba
 
 extern "C" {
+
+int pba_set_interpolator(pba_engine* e, int32_t interpolator) {
+  if (!e) return fail(PBA_ERR_INVALID_ARGUMENT, "null engine");
+  if (interpolator != PBA_INTERP_BILINEAR && interpolator != PBA_INTERP_BICUBIC)
+    return fail(PBA_ERR_INVALID_ARGUMENT, "unknown interpolator");
+  e->interp = interpolator;
+  e->evaluated = false;
+  return PBA_OK;
+}
+
+int pba_interpolator(const pba_engine* e) { return e ? e->interp : PBA_INTERP_BILINEAR; }
+
+int pba_sample_image(pba_engine* e, int32_t frame, int32_t n, const double* uv, float* out) {
+  if (!e || (n > 0 && (!uv || !out)) || n < 0) return fail(PBA_ERR_INVALID_ARGUMENT, "bad sample arguments");
+  if (!e->have_images) return fail(PBA_ERR_NOT_READY, "no images");
+  if (frame < 0 || frame >= e->n_frames) return fail(PBA_ERR_INVALID_ARGUMENT, "frame out of range");
+  if (n == 0) return PBA_OK;
+  if (int rc = check_device(e)) return rc;
+  DevBuf<double2> d_uv;
+  DevBuf<float> d_out;
+  PBA_HIP(d_uv.resize(n));
+  PBA_HIP(d_out.resize(3 * (size_t)n));
+  PBA_HIP(hipMemcpyAsync(d_uv.p, uv, sizeof(double2) * n, hipMemcpyHostToDevice, e->stream));
+  const uint8_t* img = e->images.p + (long long)frame * tiled_frame_bytes(e->width, e->height);
+  const unsigned grid = (unsigned)((n + 255) / 256);
+  if (e->interp == INTERP_BICUBIC)
+    sample_image_kernel<INTERP_BICUBIC><<<grid, 256, 0, e->stream>>>(img, e->width, e->height, d_uv.p, d_out.p, n);
+  else
+    sample_image_kernel<INTERP_BILINEAR><<<grid, 256, 0, e->stream>>>(img, e->width, e->height, d_uv.p, d_out.p, n);
+  PBA_HIP(hipGetLastError());
+  PBA_HIP(hipMemcpyAsync(out, d_out.p, sizeof(float) * 3 * n, hipMemcpyDeviceToHost, e->stream));
+  PBA_HIP(hipStreamSynchronize(e->stream));
+  return PBA_OK;
+}
 
 int pba_build_pyramid(pba_engine* e, int32_t n_levels) {
   if (!e || n_levels < 1 || n_levels > PBA_MAX_LEVELS) return fail(PBA_ERR_INVALID_ARGUMENT, "bad level count");

@@ -36,6 +36,7 @@ class OutlierThresholds(C.Structure):
 
 OUTLIER_HUGE, OUTLIER_NORMAL, OUTLIER_DISTANCE, OUTLIER_Z = 1, 2, 4, 8
 RECORD_F32, RECORD_F16 = 0, 1
+INTERP_BILINEAR, INTERP_BICUBIC = 0, 1  # pba_set_interpolator
 
 
 class MapInfo(C.Structure):
@@ -119,6 +120,9 @@ def lib():
         "pba_get_residuals": ([vp, vp, vp], C.c_int),
         "pba_host_alloc": ([C.c_size_t, C.POINTER(vp)], C.c_int),
         "pba_host_free": ([vp], C.c_int),
+        "pba_set_interpolator": ([vp, i32], C.c_int),
+        "pba_interpolator": ([vp], C.c_int),
+        "pba_sample_image": ([vp, i32, i32, vp, vp], C.c_int),
         "pba_get_cost": ([vp, C.POINTER(C.c_double), C.POINTER(i32)], C.c_int),
         "pba_set_stream": ([vp, vp], C.c_int),
         "pba_get_stream": ([vp, C.POINTER(vp)], C.c_int),
@@ -210,6 +214,7 @@ class Engine:
         if pb.kind == 0:
             pat = np.ascontiguousarray(pb.pattern, np.float32)
             _check(L.pba_set_pattern(h, pat.shape[0], _p(pat)), "pba_set_pattern")
+            _check(L.pba_set_interpolator(h, int(getattr(pb, "interp", 0))), "pba_set_interpolator")
         ph = np.ascontiguousarray(pb.point_host, np.int32)
         ur = np.ascontiguousarray(pb.u_ref, np.float64)
         hi = None if (pb.kind != 0 or pb.host_intensity is None) else np.ascontiguousarray(pb.host_intensity, np.float32)
@@ -275,6 +280,13 @@ class Engine:
         valid = np.empty(self.n_blocks, np.uint8)
         _check(self._L.pba_get_records(self._h, _p(rec), _p(valid)), "pba_get_records")
         return rec, valid
+
+    def sample_image(self, frame: int, uv: np.ndarray) -> np.ndarray:
+        """The engine's interpolator at (column, row) positions of one frame: (n, 3) float32 [I, ∂I/∂u, ∂I/∂v]."""
+        uv = np.ascontiguousarray(uv, np.float64).reshape(-1, 2)
+        out = np.empty((uv.shape[0], 3), np.float32)
+        _check(self._L.pba_sample_image(self._h, frame, uv.shape[0], _p(uv), _p(out)), "pba_sample_image")
+        return out
 
     def residuals(self):
         """Residuals only (the first R values of every record, one pitched copy) and the validity flags."""

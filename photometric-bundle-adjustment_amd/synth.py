@@ -68,6 +68,7 @@ class Problem:
     rho: np.ndarray                 # (n_points,) float64 — current state
     poses_gt: Optional[np.ndarray] = None
     rho_gt: Optional[np.ndarray] = None
+    interp: int = 0                 # image interpolator: 0 bilinear, 1 Ceres' bicubic (pba_set_interpolator)
 
     @property
     def n_frames(self) -> int:

@@ -14,7 +14,11 @@
 // (:378-381).  Writes a JSON summary: per-iteration cost / success / relative decrease, termination, final state,
 // Ceres' evaluation timers and the protocol counters.
 //
-//   usage: ceres_lm_driver <cpu|gpu> <problem.bin> <out.json> [iters] [huber] [threads] [fixed,frames] [ftol]
+// With interp = 1 (bicubic) the GPU engine uses Ceres' BiCubicInterpolator arithmetic (pba_set_interpolator) and the
+// CPU mode, for an EUCM camera, runs the vendored ceres::PhotometricError<8> itself (photometric_error.h:79-189) —
+// the whole CPU side is then reference-held code.
+//
+//   usage: ceres_lm_driver <cpu|gpu> <problem.bin> <out.json> [iters] [huber] [threads] [fixed,frames] [ftol] [interp]
 //          (problem layout: tests/golden/make_golden.py write_problem)
 #include <atomic>
 #include <cstdint>
@@ -29,6 +33,7 @@
 #include "ceres_functors.h"
 #include "local_parameterization_se3.hpp"  // the reference's (include/visnav/), compiled where it lies
 #include "pba_ceres.h"
+#include "photometric_error.h"              // ceres-solver/internal/ceres/autodiff_benchmarks/
 
 namespace {
 
@@ -117,6 +122,21 @@ class CheckedCost : public ceres::CostFunction {
   int host_, target_, point_, nf_;
 };
 
+// ceres::PhotometricError<8> throws outside the EUCM domain (photometric_error.h:165-171); inside a solve that is an
+// invalid evaluation (residual_block.cc:113-131): return false instead.
+struct CeresPhotometric {
+  explicit CeresPhotometric(ceres::PhotometricError<8>* f) : f_(f) {}
+  template <class T>
+  bool operator()(const T* const h, const T* const t, const T* const r, T* res) const {
+    try {
+      return (*f_)(h, t, r, res);
+    } catch (const std::runtime_error&) {
+      return false;
+    }
+  }
+  std::unique_ptr<ceres::PhotometricError<8>> f_;
+};
+
 void json_array(std::ostringstream& o, const double* v, size_t n) {
   o << "[";
   char buf[40];
@@ -145,6 +165,7 @@ int main(int argc, char** argv) {
     while (std::getline(ss, tok, ',')) fixed.push_back(atoi(tok.c_str()));
   }
   const double ftol = argc > 8 ? atof(argv[8]) : 1e-6;
+  const int interp = argc > 9 ? atoi(argv[9]) : 0;
 
   FILE* f = fopen(argv[2], "rb");
   if (!f) return 2;
@@ -186,6 +207,7 @@ int main(int argc, char** argv) {
     pba_ceres::check(pba_set_cameras(e, nc, intr.data()), "cameras");
     pba_ceres::check(pba_set_frames(e, nf, frame_cam.data(), W, H, kind == 0 ? images.data() : nullptr), "frames");
     if (kind == 0) pba_ceres::check(pba_set_pattern(e, P, pattern.data()), "pattern");
+    if (kind == 0) pba_ceres::check(pba_set_interpolator(e, interp), "interpolator");
     pba_ceres::check(pba_set_points(e, np, point_host.data(), u_ref.data(), kind == 0 ? host_int.data() : nullptr),
                      "points");
     pba_ceres::check(pba_set_blocks(e, nb, block_point.data(), block_target.data(), kind == 1 ? u_obs.data() : nullptr),
@@ -206,17 +228,35 @@ int main(int argc, char** argv) {
       problem.SetParameterBlockConstant(&intr[8 * c]);
     }
   // CPU photometric: one interpolator per keyframe image, host bearings per point
-  std::vector<std::unique_ptr<pba_test::BilinearInterpolator>> interp;
-  std::vector<Eigen::Matrix<double, 3, 8>> bearings;
+  using PE = ceres::PhotometricError<8>;
+  const bool ceres_pe = !gpu && kind == 0 && interp == 1 && model == pba_test::CAM_EUCM;
+  if (!gpu && kind == 0 && interp == 1 && !ceres_pe) {
+    fprintf(stderr, "cpu mode: bicubic is the vendored PhotometricError<8>, EUCM cameras only\n");
+    return 3;
+  }
+  std::vector<std::unique_ptr<pba_test::BilinearInterpolator>> bilin;
+  std::vector<std::unique_ptr<pba_test::Grid>> grids;
+  std::vector<std::unique_ptr<pba_test::BicubicInterpolator>> bicub;
+  std::vector<Eigen::Matrix<double, 3, 8>, Eigen::aligned_allocator<Eigen::Matrix<double, 3, 8>>> bearings;
+  std::vector<PE::Patch<double>, Eigen::aligned_allocator<PE::Patch<double>>> patches;
+  std::vector<PE::Intrinsics, Eigen::aligned_allocator<PE::Intrinsics>> K6(nc);
+  for (int c = 0; c < nc; ++c) K6[c] << intr[8 * c], intr[8 * c + 1], intr[8 * c + 2], intr[8 * c + 3], intr[8 * c + 4], intr[8 * c + 5];
   std::vector<double> host_int_d;
   if (!gpu && kind == 0) {
-    for (int i = 0; i < nf; ++i) interp.emplace_back(new pba_test::BilinearInterpolator(&images[(size_t)i * W * H], H, W));
+    for (int i = 0; i < nf; ++i) {
+      bilin.emplace_back(new pba_test::BilinearInterpolator(&images[(size_t)i * W * H], H, W));
+      grids.emplace_back(new pba_test::Grid(&images[(size_t)i * W * H], 0, H, 0, W));
+      bicub.emplace_back(new pba_test::BicubicInterpolator(*grids.back()));
+    }
     bearings.resize(np);
+    patches.resize(np);
     host_int_d.assign(host_int.begin(), host_int.end());
     for (int p = 0; p < np; ++p)
-      for (int k = 0; k < 8; ++k)
+      for (int k = 0; k < 8; ++k) {
         bearings[p].col(k) = pba_test::Unproject(model, &intr[8 * frame_cam[point_host[p]]],
                                                  Eigen::Vector2d(u_ref[2 * p] + pattern[2 * k], u_ref[2 * p + 1] + pattern[2 * k + 1]));
+        patches[p][k] = host_int[(size_t)8 * p + k];
+      }
   }
   for (int b = 0; b < nb; ++b) {  // :347-375
     const int p = block_point[b], h = point_host[p], t = block_target[b];
@@ -230,10 +270,13 @@ int main(int argc, char** argv) {
       cf = new ceres::AutoDiffCostFunction<pba_test::GeometricFunctor, 2, 7, 7, 1, 8>(new pba_test::GeometricFunctor(
           Eigen::Vector2d(u_obs[2 * b], u_obs[2 * b + 1]), Eigen::Vector2d(u_ref[2 * p], u_ref[2 * p + 1]),
           &intr[8 * frame_cam[h]], model));
+    } else if (ceres_pe) {  // the vendored functor itself (it keeps references to the patch, bearings, image, K)
+      cf = new ceres::AutoDiffCostFunction<CeresPhotometric, 8, 7, 7, 1>(
+          new CeresPhotometric(new PE(patches[p], bearings[p], *bicub[t], K6[frame_cam[t]])));
     } else {
       using F = pba_test::PhotometricFunctor<8, pba_test::BilinearInterpolator>;
       cf = new ceres::AutoDiffCostFunction<F, 8, 7, 7, 1>(
-          new F(&host_int_d[(size_t)8 * p], bearings[p], *interp[t], &intr[8 * frame_cam[t]], model));
+          new F(&host_int_d[(size_t)8 * p], bearings[p], *bilin[t], &intr[8 * frame_cam[t]], model));
     }
     if (kind == 1)
       problem.AddResidualBlock(cf, loss, T[h].data(), T[t].data(), &rho[p], &intr[8 * frame_cam[t]]);

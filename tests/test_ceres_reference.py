@@ -31,6 +31,7 @@ def test_adapter_compiles_against_real_ceres():
                "-Wno-deprecated-declarations", "-Wno-sign-compare", "-Wno-ignored-qualifiers", "-Wno-misleading-indentation",
                *[f for f in flags if f.startswith(("-D", "-I"))],
                "-I", os.path.join(REF, "thirdparty", "Sophus"), "-I", os.path.join(REF, "include", "visnav"),
+               "-I", os.path.join(REF, "thirdparty", "ceres-solver", "internal", "ceres", "autodiff_benchmarks"),
                "-I", os.path.join(ROOT, "include"), "-I", os.path.join(ROOT, "tests", "cpp"),
                os.path.join(ROOT, "tests", "cpp", src)]
         r = subprocess.run(cmd, capture_output=True, text=True)
@@ -53,6 +54,23 @@ def test_real_ceres_lm_equals_python_reference(kind, model, huber):
     assert (got["termination"] == 0) == info["converged"]  # ceres::CONVERGENCE == 0
     np.testing.assert_allclose(got["poses"], p_ref, atol=1e-12)
     np.testing.assert_allclose(got["rho"], r_ref, rtol=1e-10)
+
+
+@needs_driver
+def test_real_photometric_error_lm_equals_python_reference():
+    """EUCM + bicubic: real Ceres LM over the vendored ceres::PhotometricError<8> (reference-held functor) takes the
+    trajectory of tests/gn_reference.lm over the oracle — pins the oracle's bicubic functor inside a whole solve."""
+    from test_ceres_golden import load_ceres_photometric
+    pb, _, _ = load_ceres_photometric()
+    pb.poses[:2] = synth.se3_plus(pb.poses[:2], np.zeros((2, 6)))
+    got = CR.run("cpu", pb, iters=10, huber=9.0, threads=4)
+    p_ref, r_ref, c0, c1, it, info = GR.lm(pb, 9.0, (0, 1), max_iterations=10, summary=True)
+    assert abs(got["costs"][0] - c0) <= 1e-10 * c0
+    assert abs(got["final_cost"] - c1) <= 1e-8 * c1, (got["final_cost"], c1)
+    assert got["successful_steps"] == info["successful_steps"] + 1
+    assert got["unsuccessful_steps"] == info["unsuccessful_steps"]
+    np.testing.assert_allclose(got["poses"], p_ref, atol=1e-10)
+    np.testing.assert_allclose(got["rho"], r_ref, rtol=1e-8)
 
 
 @needs_driver

@@ -171,12 +171,18 @@ def test_c4_full_size_parity_and_properties(c4):
         eng.evaluate(True)
         rec_h, valid_h = eng.records()
     assert np.array_equal(valid_h, valid_a)
-    # (the fp16 and fp32 launches are separate instantiations: at a pixel within 2e-3 px of a bilinear cell edge the
-    # last-ulp difference of the warp may pick the neighbouring cell, whose gradient differs — as in compare_records)
+    # The fp16 and fp32 launches are separate instantiations whose fp32 arithmetic may contract differently: a
+    # Jacobian entry formed by cancellation (e.g. the ω columns, b × (qR) with |qR| ~ 1e4) carries ~1e-7 of the
+    # block's Jacobian scale of evaluation noise either way.  Bound: fp16 rounding (2⁻¹¹ relative, 2⁻¹⁴ absolute) plus
+    # 1e-6 of the block's largest |J| (the north star's parity bound is 1e-5); pixels within 2e-3 px of a bilinear
+    # cell edge, where the last-ulp warp difference may pick the neighbouring cell, are excluded as in compare_records.
     at1 = synth.Problem(**{**pb.__dict__, "poses": states[1][2], "rho": states[1][3]})
     edge = near_cell_boundary(projected_uv(at1))                              # (n_blocks, 8)
     col_edge = np.concatenate([np.zeros_like(edge), np.repeat(edge, 6, 1), np.repeat(edge, 6, 1), edge], 1)
-    bad = ~(np.abs(rec_h - rec_a) <= 2.0 ** -11 * np.abs(rec_a) + 2.0 ** -14) & ~col_edge
+    jscale = np.abs(rec_a[:, 8:]).max(1, keepdims=True)
+    bound = 2.0 ** -11 * np.abs(rec_a) + 2.0 ** -14 + np.concatenate([np.zeros((pb.n_blocks, 8)),
+                                                                      np.repeat(1e-6 * jscale, 104, 1)], 1)
+    bad = ~(np.abs(rec_h - rec_a) <= bound) & ~col_edge
     if bad.any():
         i, j = np.argwhere(bad)[0]
         pytest.fail(f"fp16 records: {bad.sum()} values out of bound, max|fp32| {np.abs(rec_a).max():.4g}, "

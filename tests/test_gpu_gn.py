@@ -24,14 +24,17 @@ def make_engine(pb, huber, fixed):
     return eng
 
 
-CASES = [(0, 0, 9.0), (0, 1, 9.0), (0, 2, 0.0), (0, 3, 9.0), (1, 0, 1.0), (1, 1, 1.0), (1, 3, 1.0)]
+CASES = [(0, 0, 9.0), (0, 1, 9.0), (0, 2, 0.0), (0, 3, 9.0), (1, 0, 1.0), (1, 1, 1.0), (1, 3, 1.0),
+         (0, 6, 9.0)]  # 6 = EUCM (2) + 4 · bicubic: PhotometricError<8>'s residual in the Gauss-Newton path
 
 
 @pytest.mark.parametrize("kind,model,huber", CASES)
 @pytest.mark.parametrize("lam", [1e-4, 1e-1])
 def test_reduced_system_and_step(kind, model, huber, lam):
+    interp, model = model >> 2, model & 3
     pb = synth.make_problem(kind=kind, model=model, n_frames=8, n_points=60, width=376, height=240, seed=11 + model,
                             border=12)
+    pb.interp = interp
     fixed = (0,)
     H, g, cost = GR.linearize(pb, pb.poses, pb.rho, huber, fixed)
     S_ref, gS_ref, dp_ref, dl_ref, model_ref = GR.schur_step(H, g, pb.n_frames, lam, fixed)
