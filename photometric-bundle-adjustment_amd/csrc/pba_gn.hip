@@ -21,7 +21,7 @@
 //                      lists, + λ·clamp(diag) (Ceres LM diagonal), identity rows for constant frames.
 //   skyline_solve_kernel  one workgroup: right-looking block-skyline Cholesky S = LLᵀ in fp64, then
 //                      forward/back substitution for δ_poses.
-//   pose_update_kernel / point_update_kernel  T ← T·exp(δ) (Sophus SE3::exp, fp64), back-substitution
+//   update_kernel      T ← T·exp(δ) (Sophus SE3::exp, fp64), back-substitution
 //                      δρ = −(g_ρ + Σ W_aᵀ δ_a)/H'_ρρ, and the LM model decrease ½(λ δᵀDδ − gᵀδ).
 //   cost: pair_kernel + photometric/geometric kernel in cost-only mode + fixed-order reduction.
 #include <hip/hip_runtime.h>
@@ -1105,13 +1105,26 @@ __global__ __launch_bounds__(2 * kCrOddThreads<M>) void cr_level_kernel(CrLevel 
 
 // Wave-level variant for super-rows of ≤ 31 unknowns (B ≤ 5 keyframes), where [D | one coupling block | b] fits one
 // wave: lane c < M holds column c of D, lanes M…2M−1 the coupling block's columns, lane 2M b.  The pivot columns are
-// then always in the elimination's own wave: lanes k, k+1 publish them to a per-wave LDS buffer and every lane reads
-// them back with no s_barrier (LDS operations of one wave are processed in order), all 24 reads in flight at once.
-// Same arithmetic, same order as gj_row (bit-identical X).  Measured (tools/micro/cr_level_timing.hip, M = 24):
-// 17.0 → 14.5 µs per level launch (13.0 with the rebuild on the matrix cores, below).
-template <int M>
+// then always in the elimination's own wave: the pivot lanes publish them to a per-wave LDS buffer and every lane
+// reads them back with no s_barrier (LDS operations of one wave are processed in order).  Measured
+// (tools/micro/cr_level_timing.hip, M = 24): 17.0 → 14.5 µs per level launch with 2-column pivots (13.0 with the
+// rebuild on the matrix cores, below); 4-column pivot blocks (6 publish/read round trips instead of 12): C4 step
+// 0.228 → 0.216 ms per LM iteration (8-column blocks: 0.216-0.220, their per-lane 8×8 solve costs what the saved
+// round trips gain).
+#ifndef PBA_CR_PIVOT
+#define PBA_CR_PIVOT 4
+#endif
+constexpr int kCrPivot = PBA_CR_PIVOT;  // columns per Gauss-Jordan step of gj_wave (1, 2, 4 or 8; divides M)
+
+// Pivot blocks of PB columns: lanes k … k+PB−1 publish their columns to the wave's LDS buffer (row r: PB doubles),
+// every lane reads the PB×PB pivot block P and solves P t = a[k … k+PB−1] in registers (unpivoted Gauss-Jordan:
+// D is SPD, so is every pivot block; all of P's pivots must be positive), then updates its other rows
+// a[r] −= Σ_j piv[r][j] t_j.  The publish / read round trip is paid M/PB times instead of M/2 times; the updates are
+// the same FMAs.
+template <int M, int PB = kCrPivot>
 __device__ __forceinline__ bool gj_wave(const double* __restrict__ D, const double* __restrict__ R1, bool r1_trans,
-                                        const double* __restrict__ b, int ncol, int c, double2* piv, double* a) {
+                                        const double* __restrict__ b, int ncol, int c, double* piv, double* a) {
+  static_assert(M % PB == 0, "pivot blocks tile the system");
 #pragma unroll
   for (int r = 0; r < M; ++r) {
     const double* src = nullptr;
@@ -1122,26 +1135,48 @@ __device__ __forceinline__ bool gj_wave(const double* __restrict__ D, const doub
   }
   bool bad = false;
 #pragma unroll
-  for (int k = 0; k < M; k += 2) {
-    if (c == k || c == k + 1) {
-      double* dst = reinterpret_cast<double*>(piv) + (c - k);
+  for (int k = 0; k < M; k += PB) {
+    if (c >= k && c < k + PB) {
+      double* dst = piv + (c - k);
 #pragma unroll
-      for (int r = 0; r < M; ++r) dst[2 * r] = a[r];
+      for (int r = 0; r < M; ++r) dst[PB * r] = a[r];
     }
     __builtin_amdgcn_wave_barrier();
     asm volatile("" ::: "memory");
-    double2 cr[M];
+    double P[PB][PB], t[PB];
 #pragma unroll
-    for (int r = 0; r < M; ++r) cr[r] = piv[r];
-    const double p00 = cr[k].x, p10 = cr[k + 1].x, p01 = cr[k].y, p11 = cr[k + 1].y;
-    const double det = p00 * p11 - p01 * p10;
-    bad |= !(p00 > 0.0 && det > 0.0);
-    const double rd = rcp_nr(det);
-    const double ak = a[k], ak1 = a[k + 1];
-    const double t0 = (p11 * ak - p01 * ak1) * rd;
-    const double t1 = (p00 * ak1 - p10 * ak) * rd;
+    for (int i = 0; i < PB; ++i) {
 #pragma unroll
-    for (int r = 0; r < M; ++r) a[r] = r == k ? t0 : (r == k + 1 ? t1 : a[r] - cr[r].x * t0 - cr[r].y * t1);
+      for (int j = 0; j < PB; ++j) P[i][j] = piv[PB * (k + i) + j];
+      t[i] = a[k + i];
+    }
+#pragma unroll
+    for (int i = 0; i < PB; ++i) {  // t ← P⁻¹ t
+      bad |= !(P[i][i] > 0.0);
+      const double inv = rcp_nr(P[i][i]);
+#pragma unroll
+      for (int j = i + 1; j < PB; ++j) P[i][j] *= inv;
+      t[i] *= inv;
+#pragma unroll
+      for (int q = 0; q < PB; ++q) {
+        if (q == i) continue;
+        const double f = P[q][i];
+#pragma unroll
+        for (int j = i + 1; j < PB; ++j) P[q][j] -= f * P[i][j];
+        t[q] -= f * t[i];
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < M; ++r) {
+      if (r >= k && r < k + PB) {
+        a[r] = t[r - k];
+      } else {
+        double v = a[r];
+#pragma unroll
+        for (int j = 0; j < PB; ++j) v -= piv[PB * r + j] * t[j];
+        a[r] = v;
+      }
+    }
     __builtin_amdgcn_wave_barrier();
     asm volatile("" ::: "memory");
   }
@@ -1161,7 +1196,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     CrLevel L, CrLevel Ln, int* status) {
   static_assert(2 * M + 1 <= 64, "one wave per elimination");
   constexpr int NC = 2 * M + 1;
-  __shared__ __attribute__((aligned(16))) double2 piv[3][M];
+  __shared__ __attribute__((aligned(16))) double piv[3][M * kCrPivot];
   extern __shared__ double smem[];
   double* sUl = smem;
   double* sUi = sUl + M * M;
@@ -1257,7 +1292,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 // The root super-row on one wave (lane 2M carries b; the coupling lanes are empty).
 template <int M>
 __global__ __launch_bounds__(64) void cr_root_wave_kernel(CrLevel L, int* status) {
-  __shared__ __attribute__((aligned(16))) double2 piv[M];
+  __shared__ __attribute__((aligned(16))) double piv[M * kCrPivot];
   double a[M];
   const int lane = threadIdx.x;
   const bool ok = gj_wave<M>(L.D, nullptr, false, L.b, M + 1, lane, piv, a);
@@ -1395,24 +1430,39 @@ __device__ __forceinline__ void block_reduce2(double a, double b, double* out) {
   }
 }
 
-__global__ __launch_bounds__(kBlockThreads) void pose_update_kernel(const double* poses, const double* x,
-                                                                   const double* g_dir, const double* Ddiag,
-                                                                   const uint8_t* fixed, double* poses_new,
-                                                                   double* red, int n) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+struct PoseUpdateArgs {
+  const double* poses;
+  const double* x;
+  const double* g_dir;
+  const double* Ddiag;
+  const uint8_t* fixed;
+  double* poses_new;
+  double* red;
+  int n;
+};
+
+// candidate pose of frame i: T·exp(δ_i), or T for a constant frame
+__device__ __forceinline__ void candidate_pose(const PoseUpdateArgs& a, int i, double* out) {
+  if (a.fixed[i]) {
+    for (int q = 0; q < 7; ++q) out[q] = a.poses[7 * i + q];
+  } else {
+    se3_exp_mul(a.poses + 7 * i, a.x + 6 * i, out);
+  }
+}
+
+__device__ __forceinline__ void pose_update_block(const PoseUpdateArgs& a, int blk) {
+  const int i = blk * blockDim.x + threadIdx.x;
   double dg = 0.0, dD = 0.0;
-  if (i < n) {
-    if (fixed[i]) {
-      for (int q = 0; q < 7; ++q) poses_new[7 * i + q] = poses[7 * i + q];
-    } else {
-      se3_exp_mul(poses + 7 * i, x + 6 * i, poses_new + 7 * i);
+  if (i < a.n) {
+    candidate_pose(a, i, a.poses_new + 7 * i);
+    if (!a.fixed[i]) {
       for (int r = 0; r < 6; ++r) {
-        dg += x[6 * i + r] * g_dir[6 * i + r];
-        dD += x[6 * i + r] * x[6 * i + r] * Ddiag[6 * i + r];
+        dg += a.x[6 * i + r] * a.g_dir[6 * i + r];
+        dD += a.x[6 * i + r] * a.x[6 * i + r] * a.Ddiag[6 * i + r];
       }
     }
   }
-  block_reduce2(dg, dD, red + 2 * blockIdx.x);
+  block_reduce2(dg, dD, a.red + 2 * blk);
 }
 
 struct PointUpdateArgs {
@@ -1432,8 +1482,9 @@ struct PointUpdateArgs {
   int n_points;
 };
 
-__global__ __launch_bounds__(kBlockThreads) void point_update_kernel(const PointUpdateArgs a, double lambda) {
-  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+// blk: the point workgroup's index among the point workgroups; slot: its reduction slot
+__device__ __forceinline__ void point_update_block(const PointUpdateArgs& a, double lambda, int blk, int slot) {
+  const int p = blk * blockDim.x + threadIdx.x;
   double dg = 0.0, dD = 0.0;
   if (p < a.n_points) {
     const double* pd = a.pt_data + (long long)p * 8;
@@ -1455,7 +1506,43 @@ __global__ __launch_bounds__(kBlockThreads) void point_update_kernel(const Point
     dg = dr * gl;
     dD = dr * dr * D;
   }
-  block_reduce2(dg, dD, a.red + 2 * blockIdx.x);
+  block_reduce2(dg, dD, a.red + 2 * slot);
+}
+
+struct PairUpdateArgs {
+  const int* pair_host;
+  const int* pair_target;
+  const int* frame_cam;
+  const double* cams;
+  PairRec* pairs_new;  // nullptr: no candidate pair table (geometric engines form theirs in the cost path too)
+  int n_pairs;
+};
+
+// The step's candidate state in ONE launch: workgroups [0, gp) update the poses (T·exp(δ)) and reduce the pose part
+// of the model decrease, [gp, gp + gq) back-substitute the inverse distances and reduce the point part (partial slots
+// in the same fixed order as two separate launches), and the rest form the candidate pair table straight from
+// T_h·exp(δ_h), T_t·exp(δ_t) — candidate_pose, the same arithmetic as the pose workgroups, so the pairs equal
+// form_pair(poses_new) bit for bit — which saves the separate pair launch before the candidate cost.
+__global__ __launch_bounds__(kBlockThreads) void update_kernel(const PoseUpdateArgs pa, const PointUpdateArgs qa,
+                                                               const PairUpdateArgs ra, int gp, int gq, double lambda) {
+  const int b = blockIdx.x;
+  if (b < gp) {
+    pose_update_block(pa, b);
+  } else if (b < gp + gq) {
+    point_update_block(qa, lambda, b - gp, b);
+  } else {
+    const int i = (b - gp - gq) * blockDim.x + threadIdx.x;
+    if (i >= ra.n_pairs) return;
+    const int h = ra.pair_host[i], t = ra.pair_target[i];
+    double H[7], T[7];
+    candidate_pose(pa, h, H);
+    candidate_pose(pa, t, T);
+    PairRec r;
+    pair_rotation(H, T, r);
+    pair_translation(H, T, r);
+    pair_cameras(ra.cams, h, t, ra.frame_cam[h], ra.frame_cam[t], r);
+    ra.pairs_new[i] = r;
+  }
 }
 
 __global__ __launch_bounds__(kBlockThreads) void cost_reduce_kernel(const float* cost, const uint8_t* valid, int n,
@@ -1823,6 +1910,7 @@ int gn_prepare(pba_engine* e) {
   PBA_HIP(hipMemsetAsync(G.drho.p, 0, sizeof(double) * e->n_points, st));
   PBA_HIP(hipStreamSynchronize(st));
   G.prepared = true;
+  G.pairs_new_fresh = false;
   G.fixed_eff = fixed;
   return PBA_OK;
 }
@@ -1963,12 +2051,14 @@ void enqueue_updates(pba_engine* e, double lambda, const uint8_t* fixed, int* gp
   const int nf = e->n_frames;
   const int gp = (nf + kBlockThreads - 1) / kBlockThreads;
   const int gq = (G.n_gn_points + kBlockThreads - 1) / kBlockThreads;
-  pose_update_kernel<<<gp, kBlockThreads, 0, e->stream>>>(e->poses.p, G.x.p, G.g_dir.p, G.Ddiag.p, fixed,
-                                                          G.poses_new.p, G.red.p, nf);
-  PointUpdateArgs pa_{G.pt_data.p, G.pt_first.p, G.pt_nblk.p, G.pt_orig.p, G.pt_host.p, G.gn_target.p,
-                      G.blk_schur.p, G.x.p, fixed, e->rho.p, G.rho_new.p, G.drho.p, G.red.p + 2 * gp,
-                      G.n_gn_points};
-  if (gq > 0) point_update_kernel<<<gq, kBlockThreads, 0, e->stream>>>(pa_, lambda);
+  const int gr = (e->n_pairs + kBlockThreads - 1) / kBlockThreads;
+  PoseUpdateArgs pa{e->poses.p, G.x.p, G.g_dir.p, G.Ddiag.p, fixed, G.poses_new.p, G.red.p, nf};
+  // point workgroup q writes reduction slot gp + q, as the separate launches did
+  PointUpdateArgs qa{G.pt_data.p, G.pt_first.p, G.pt_nblk.p, G.pt_orig.p, G.pt_host.p, G.gn_target.p,
+                     G.blk_schur.p, G.x.p, fixed, e->rho.p, G.rho_new.p, G.drho.p, G.red.p, G.n_gn_points};
+  PairUpdateArgs ra{e->pair_host.p, e->pair_target.p, e->frame_cam.p, e->intr_d.p, G.pairs_new.p, e->n_pairs};
+  update_kernel<<<gp + gq + gr, kBlockThreads, 0, e->stream>>>(pa, qa, ra, gp, gq, lambda);
+  G.pairs_new_fresh = true;
   *gp_out = gp;
   *gq_out = gq;
 }
@@ -2079,8 +2169,7 @@ int lm_trial(pba_engine* e, double lambda, double min_rel, double ftol, const hi
   int gp = 0, gq = 0;
   enqueue_updates(e, lambda, G.fixed.p, &gp, &gq);
   PBA_HIP(hipEventRecord(ev[1], e->stream));
-  launch_pairs(e, G.poses_new.p, G.pairs_new.p);
-  if (int rc = launch_cost_only(e, G.pairs_new.p, G.rho_new.p)) return rc;
+  if (int rc = launch_cost_only(e, G.pairs_new.p, G.rho_new.p)) return rc;  // pairs_new from update_kernel
   const int gc = std::min(1024, (e->n_blocks + kBlockThreads - 1) / kBlockThreads);
   cost_reduce_kernel<<<gc, kBlockThreads, 0, e->stream>>>(e->cost.p, e->valid.p, e->n_blocks, G.red.p + 2 * (gp + gq));
   lm_decide_kernel<<<1, 256, 0, e->stream>>>(G.red.p, gp, gq, gc, G.status.p, lambda, min_rel, ftol, G.lm.p);
@@ -2099,7 +2188,7 @@ int lm_trial(pba_engine* e, double lambda, double min_rel, double ftol, const hi
 
 int candidate_cost(pba_engine* e, double* cost) {
   GnData& G = e->gn;
-  launch_pairs(e, G.poses_new.p, G.pairs_new.p);
+  if (!G.pairs_new_fresh) launch_pairs(e, G.poses_new.p, G.pairs_new.p);
   if (int rc = launch_cost_only(e, G.pairs_new.p, G.rho_new.p)) return rc;
   return total_cost(e, cost, nullptr);
 }

@@ -482,6 +482,7 @@ struct GnData {
   DevBuf<double> poses_new, rho_new, red;
   DevBuf<int> status;
   DevBuf<PairRec> pairs_new;
+  bool pairs_new_fresh = false;  // pairs_new formed by the last update_kernel (its candidate state)
   PinnedBuf<double> red_h;
   DevBuf<double> lm;         // LM decision record of the single-GPU loop (pba_gn.hip: kLm*)
   PinnedBuf<double> lm_h;
