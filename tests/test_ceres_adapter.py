@@ -1,8 +1,10 @@
 """The Ceres adapter (include/pba_ceres.h) driven like Ceres' evaluator (tests/cpp/adapter_driver.cpp).
 
-CPU: the adapter compiles against the Ceres 2.0 interface (test double tests/cpp/mock_ceres).
+CPU: the adapter compiles against the Ceres 2.0 interface (test double tests/cpp/mock_ceres; against the real
+vendored Ceres in tests/test_ceres_reference.py).
 GPU: per-block Evaluate through the adapter reproduces the oracle's tangent records after Ceres'
-J_global·P step; residual-only evaluations and LocalParameterization::Plus agree too.
+J_global·P step; residual-only evaluations and LocalParameterization::Plus agree too.  The driver is the one linked
+against real Ceres 2.0.0 (oracle/_ref/adapter_driver, oracle/ceres.mk) when it was built, else the test-double build.
 """
 import os
 import subprocess
@@ -17,6 +19,7 @@ from helpers import R_ATOL_GEOMETRIC, R_ATOL_PHOTOMETRIC, ROOT, compare_records,
 
 E = engine_module()
 DRIVER_SRC = os.path.join(ROOT, "tests", "cpp", "adapter_driver.cpp")
+REAL_CERES_DRIVER = os.path.join(ROOT, "oracle", "_ref", "adapter_driver")
 
 
 def build_driver(out_dir):
@@ -43,7 +46,7 @@ def test_adapter_records_match_oracle(kind, model):
     pb = synth.make_problem(kind=kind, model=model, n_frames=8, n_points=100, width=376, height=240, seed=61,
                             border=10)
     with tempfile.TemporaryDirectory() as td:
-        exe = build_driver(td)
+        exe = REAL_CERES_DRIVER if os.access(REAL_CERES_DRIVER, os.X_OK) else build_driver(td)
         fin, fout = os.path.join(td, "in.bin"), os.path.join(td, "out.bin")
         with open(fin, "wb") as f:
             write_problem(f, pb)
