@@ -194,11 +194,13 @@ typedef struct pba_solver_options {
 typedef struct pba_solver_summary {
   int32_t iterations, successful_steps, unsuccessful_steps, termination;
   double initial_cost, final_cost;      /* Σ ½ρ(‖r‖²) */
-  /* total_ms: host wall clock of the whole solve.  The parts: pba_solve — device time between stream events (one
-   * host synchronisation per LM trial, so the parts do not add up to total_ms); pba_solve_distributed — host wall
-   * clock of each phase, collectives included. */
+  /* total_ms: host wall clock of the whole solve.  The parts: pba_solve — device time between stream events, only
+   * with pba_set_solver_timing(engine, 1) (the events cost the GPU a few µs of idle time each, so they are off by
+   * default and the parts are then 0); pba_solve_distributed — host wall clock of each phase, collectives included. */
   double total_ms, linearize_ms, solve_ms, cost_ms;
 } pba_solver_summary;
+/* per-phase device timing of pba_solve (linearize_ms / solve_ms / cost_ms of the summary); default off */
+int pba_set_solver_timing(pba_engine* engine, int32_t enable);
 
 /* constant parameter blocks (Problem::SetParameterBlockConstant, map_utils.h:334-336) */
 int pba_set_fixed_frames(pba_engine* engine, int32_t n, const int32_t* frames);

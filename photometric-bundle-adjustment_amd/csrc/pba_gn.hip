@@ -27,6 +27,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cmath>
 #include <cstdlib>
@@ -85,9 +86,10 @@ static_assert(pa(21) == 0 && pb(21) == 6 && pa(56) == 5 && pb(56) == 11, "table"
 enum : int { kLmCost = 0, kLmCostNew = 1, kLmModel = 2, kLmRel = 3, kLmAccept = 4, kLmStatus = 5, kLmConverged = 6, kLmFields = 7 };
 
 struct LinArgs {
-  const int* gn_block;
-  const int4* chunk_desc;   // first GN block, count, n_targets, partial offset (floats)
-  const uint8_t* blk_lt;
+  const int* lin_block;     // linearise order → block (GN order regrouped by target within each host)
+  const int* lin_gpos;      // linearise order → GN position (blk_schur index)
+  const int4* chunk_desc;   // first linearise position, count, n_targets, partial offset (floats)
+  const uint8_t* blk_lt;    // linearise order → local target slot in its chunk
   float* blk_schur;
   float* part_lin;
   int n_chunks;
@@ -97,35 +99,6 @@ struct LinArgs {
 // ------------------------------------------------------------------------------------------------
 // linearize_kernel
 // ------------------------------------------------------------------------------------------------
-template <int V>
-__device__ __forceinline__ float nprod(const float* x) {
-  if constexpr (V < NV) {
-    constexpr int A = pa(V), B = pb(V);
-    return x[A] * x[B];
-  } else {
-    return 0.0f;
-  }
-}
-
-// The 104 normal-equation products of one row, all-reduced over the block's LPB lanes (DPP butterflies,
-// no lane-dependent selects), 8 at a time; lane 0 of the block stores each group of block sums as 2 float4s.
-template <int LPB, int G, int... Q>
-__device__ __forceinline__ void product_group(const float* x, float* o, std::integer_sequence<int, Q...>) {
-  ((o[Q] = group_sum<LPB>(nprod<G * 8 + Q>(x))), ...);
-}
-template <int LPB, int G>
-__device__ __forceinline__ void block_products(const float* x, float* srow, bool writer) {
-  if constexpr (G * 8 < NV) {
-    float o[8];
-    product_group<LPB, G>(x, o, std::make_integer_sequence<int, 8>{});
-    if (writer) {
-      *reinterpret_cast<float4*>(srow + G * 8) = make_float4(o[0], o[1], o[2], o[3]);
-      *reinterpret_cast<float4*>(srow + G * 8 + 4) = make_float4(o[4], o[5], o[6], o[7]);
-    }
-    block_products<LPB, G + 1>(x, srow, writer);
-  }
-}
-
 // Slot of the product x[r]·x[c] (r ≤ c) in the 104-product layout, or 255 when not needed (x13·x13, pad columns).
 __host__ __device__ constexpr int slot_of(int r, int c) {
   for (int v = 0; v < NV; ++v)
@@ -149,30 +122,29 @@ constexpr auto make_slot_table(std::integer_sequence<int, L...>) {
 }
 __constant__ const auto kSlotTable = make_slot_table(std::make_integer_sequence<int, 64>{});
 
-// Block normal-equation products by matrix cores: the block's weighted rows X (R × 14, padded to LPB × 16) give
-// XᵀX = Σ_k x_kᵀx_k as LPB/4 v_mfma_f32_16x16x4f32 steps (operand A = Xᵀ and B = X are the same register:
-// lane l holds X[4s + l/16][l%16]).  Replaces 104 products + a 3-step DPP all-reduce per row (~416 VALU per
-// lane) with 16 MFMAs per wave.
-// The photometric pinhole 8-lane instantiation requests 8 waves per SIMD: the compiler then keeps the accumulator in
-// VGPRs (56, no AGPRs, no spills) instead of 62 VGPRs + 4 AGPRs at 7 waves (linearise 0.101 -> 0.098 ms per LM
-// iteration at C4, tools/ab_bench.sh); the other instantiations would spill under that request.
+// Normal-equation products by matrix cores: weighted rows X (R × 14, padded to LPB × 16 per block) give
+// XᵀX = Σ_k x_kᵀx_k as v_mfma_f32_16x16x4f32 steps (operand A = Xᵀ and B = X are the same register: lane l holds
+// X[4s + l/16][l%16]).  A chunk's blocks are ordered by target (gn_prepare), so the blocks of one target are
+// consecutive in a wave and their rows form ONE accumulation chain: a wave issues 16 MFMAs whatever its targets, and
+// stores one product set per distinct target instead of one per block.
 template <int KIND, int MODEL, int LPB>
 constexpr int kLinWaves = KIND == PBA_RESIDUAL_PHOTOMETRIC && MODEL == CAM_PINHOLE + 4 * INTERP_BILINEAR && LPB == 8 ? 8 : 1;
 
 template <int KIND, int MODEL, int LPB>
 __global__ __launch_bounds__(kBlockThreads) __attribute__((amdgpu_waves_per_eu(kLinWaves<KIND, MODEL, LPB>, 8)))
 void linearize_kernel(const KernelArgs a, const LinArgs g) {
-  constexpr int BPW = kBlockThreads / LPB;  // blocks per workgroup
   constexpr int BW = 64 / LPB;              // blocks per wave
+  constexpr int NW = kBlockThreads / 64;    // waves per workgroup
+  constexpr int SPB = LPB / 4;              // MFMA steps per block
   constexpr int NVP = 108;                  // 104 products, padded
   constexpr int kTileW = KIND == PBA_RESIDUAL_PHOTOMETRIC ? BW * (int)sizeof(TileBlock) : 0;
   constexpr int kRowsW = 64 * 16 * 4, kProdW = BW * NVP * 4;
   constexpr int kArena = (kTileW > kRowsW ? (kTileW > kProdW ? kTileW : kProdW) : (kRowsW > kProdW ? kRowsW : kProdW));
-  // per-wave arena, used in turn by the wave's tile blocks, its weighted rows and its blocks' products
+  // per-wave arena, used in turn by the wave's tile blocks, its weighted rows and its per-target products
   // (each phase only touches the wave's own blocks; LDS is in order within a wave)
-  __shared__ __attribute__((aligned(16))) unsigned char arena[4][kArena];
-  __shared__ int s_lt[BPW];
+  __shared__ __attribute__((aligned(16))) unsigned char arena[NW][kArena];
   __shared__ float2 s_pat[LPB];
+  __shared__ int s_wlo[NW], s_wn[NW];
   const int chunk = logical_tile();
   if (chunk >= g.n_chunks) return;
   if (g.gate && g.gate[kLmAccept] == 0.0) return;  // speculative linearisation of a rejected step: nothing to do
@@ -183,11 +155,12 @@ void linearize_kernel(const KernelArgs a, const LinArgs g) {
   const bool live = lb < count;
   const int R = KIND == PBA_RESIDUAL_PHOTOMETRIC ? a.P : 2;
   const bool act = live && k < R;
-  int blk = 0;
+  int blk = 0, gpos = 0, lt = 0;
   Row row;
   if (live) {
-    blk = g.gn_block[first + lb];
-    if (k == 0) s_lt[lb] = g.blk_lt[first + lb];
+    blk = g.lin_block[first + lb];
+    gpos = g.lin_gpos[first + lb];
+    lt = g.blk_lt[first + lb];
   }
   if constexpr (KIND == PBA_RESIDUAL_PHOTOMETRIC) {
     TileBlock* s_tb = reinterpret_cast<TileBlock*>(arena[wave]);
@@ -208,94 +181,97 @@ void linearize_kernel(const KernelArgs a, const LinArgs g) {
   }
   // weighted row x̃ = √w · x  → products carry w (Ceres Corrector with ρ'' ≤ 0: J̃ = √ρ' J, r̃ = √ρ' r)
   const float sw = (act && ok) ? sqrtf(w) : 0.0f;  // rows outside the domain / of dead lanes are all zero
-  auto wx = [&](float x) { return sw * x; };
+  const float x[14] = {sw * row.hv.x, sw * row.hv.y, sw * row.hv.z, sw * row.hw.x, sw * row.hw.y, sw * row.hw.z,
+                       sw * row.tv.x, sw * row.tv.y, sw * row.tv.z, sw * row.tw.x, sw * row.tw.y, sw * row.tw.z,
+                       sw * row.jr, sw * row.r};
   float* sX = reinterpret_cast<float*>(arena[wave]);  // the wave's 64 rows × 16 floats (overwrites its tile blocks)
   {
     float4* xr = reinterpret_cast<float4*>(sX + lane * 16);
-    xr[0] = make_float4(wx(row.hv.x), wx(row.hv.y), wx(row.hv.z), wx(row.hw.x));
-    xr[1] = make_float4(wx(row.hw.y), wx(row.hw.z), wx(row.tv.x), wx(row.tv.y));
-    xr[2] = make_float4(wx(row.tv.z), wx(row.tw.x), wx(row.tw.y), wx(row.tw.z));
-    xr[3] = make_float4(wx(row.jr), wx(row.r), 0.0f, 0.0f);
+    xr[0] = make_float4(x[0], x[1], x[2], x[3]);
+    xr[1] = make_float4(x[4], x[5], x[6], x[7]);
+    xr[2] = make_float4(x[8], x[9], x[10], x[11]);
+    xr[3] = make_float4(x[12], x[13], 0.0f, 0.0f);
   }
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   {
-    // block by block: LPB/4 MFMAs, then the scatter of the 104 products (one accumulator at a time keeps the
-    // MFMA registers, and their occupancy cost, at four).  With NVP ≤ 16·LPB floats a block's products land below
-    // the rows of every later block, so each block's operands are read just before its MFMAs; otherwise (LPB = 4)
-    // every operand is read first.
-    constexpr bool kInterleave = NVP <= 16 * LPB;
+    // every operand first (the product sets below overwrite the rows), then the wave's blocks in order; each run of
+    // equal local target is summed in registers and its 16×16 result scattered as the 104 products of that slot
     const int ci = lane & 15, kq = lane >> 4;
+    float op[BW * SPB];
+#pragma unroll
+    for (int st = 0; st < BW * SPB; ++st) op[st] = sX[(4 * st + kq) * 16 + ci];
     float* sP = reinterpret_cast<float*>(arena[wave]);
     const unsigned slots = kSlotTable.w[lane];
-    float opa[kInterleave ? 1 : BW][LPB / 4];
-    if constexpr (!kInterleave) {
-#pragma unroll
-      for (int b = 0; b < BW; ++b)
-#pragma unroll
-        for (int st = 0; st < LPB / 4; ++st) opa[b][st] = sX[(b * LPB + 4 * st + kq) * 16 + ci];
-    }
-#pragma unroll
-    for (int b = 0; b < BW; ++b) {
-      float op[LPB / 4];
-#pragma unroll
-      for (int st = 0; st < LPB / 4; ++st)
-        op[st] = kInterleave ? sX[(b * LPB + 4 * st + kq) * 16 + ci] : opa[kInterleave ? 0 : b][st];
-      f32x4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
-#pragma unroll
-      for (int st = 0; st < LPB / 4; ++st) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(op[st], op[st], acc, 0, 0, 0);
+    const int nbw = min(max(count - wave * BW, 0), BW);  // live blocks of this wave (wave-uniform)
+    const int lo = __builtin_amdgcn_readfirstlane(lt);     // lane 0 holds the wave's first block
+    auto flush = [&](const f32x4& acc, int slot) {
 #pragma unroll
       for (int m = 0; m < 4; ++m) {
         const unsigned v = (slots >> (8 * m)) & 255u;
-        if (v < (unsigned)NV) sP[b * NVP + v] = acc[m];
+        if (v < (unsigned)NV) sP[slot * NVP + v] = acc[m];
       }
+    };
+    // per block: its own chain (SPB steps); row 12 of the result, C[12][c] on lanes 48 + c, is the block's
+    // point-elimination data x̃_ρ·x̃_c → [H_ρρ, g_ρ, W_h(6), W_t(6), 0, 0] at its GN position (schur_kernel walks
+    // them point by point); the block's products are then added to its target run's sum
+    const int pc = lane - 48, pq = pc < 12 ? pc + 2 : (pc < 14 ? pc - 12 : pc);
+    f32x4 tacc = {0.0f, 0.0f, 0.0f, 0.0f};
+    int cur = lo;
+#pragma unroll
+    for (int b = 0; b < BW; ++b) {
+      if (b < nbw) {
+        f32x4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+        for (int st = 0; st < SPB; ++st)
+          acc = __builtin_amdgcn_mfma_f32_16x16x4f32(op[b * SPB + st], op[b * SPB + st], acc, 0, 0, 0);
+        const int gpb = __builtin_amdgcn_readlane(gpos, b * LPB);
+        if (pc >= 0) g.blk_schur[(long long)gpb * 16 + pq] = acc[0];
+        const int ltb = __builtin_amdgcn_readlane(lt, b * LPB);
+        if (ltb != cur) {
+          flush(tacc, cur - lo);
+          tacc = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+          cur = ltb;
+        }
+        tacc += acc;
+      }
+    }
+    if (nbw > 0) flush(tacc, cur - lo);
+    if (lane == 0) {
+      s_wlo[wave] = lo;
+      s_wn[wave] = nbw > 0 ? cur - lo + 1 : 0;
     }
   }
   __syncthreads();
-  auto sblk = [&](int b, int v) -> float {  // product v of workgroup block b
-    return reinterpret_cast<const float*>(arena[b / BW])[(b % BW) * NVP + v];
-  };
-  // per-block point-elimination data: [H_ρρ, g_ρ, W_h(6), W_t(6), 0, 0]
-  for (int i = threadIdx.x; i < count * 16; i += kBlockThreads) {
-    const int b = i >> 4, q = i & 15;
-    float v = 0.0f;
-    if (q == 0) v = sblk(b, 90);
-    else if (q == 1) v = sblk(b, 91);
-    else if (q < 8) v = sblk(b, 92 + q - 2);
-    else if (q < 14) v = sblk(b, 98 + q - 8);
-    g.blk_schur[(long long)(first + b) * 16 + q] = v;
-  }
-  // chunk partial slots (fixed summation order over the chunk's blocks): per local target a block mask,
-  // then fully unrolled, predicated sums — independent LDS reads instead of a dependent loop
-  __shared__ unsigned long long s_mask[BPW];
-  if ((int)threadIdx.x < n_t) {
-    unsigned long long msk = 0;
-    for (int b = 0; b < count; ++b)
-      if (s_lt[b] == (int)threadIdx.x) msk |= 1ull << b;
-    s_mask[threadIdx.x] = msk;
-  }
-  __syncthreads();
-  const unsigned long long all = count >= 64 ? ~0ull : ((1ull << count) - 1ull);
+  // chunk partial slots, fixed summation order (wave, then slot): H_hh / g_h over every product set of the chunk,
+  // H_ht / H_tt / g_t of local target j from the ≤ NW sets of j (one per wave that holds j's blocks)
+  auto sset = [&](int w, int i, int v) -> float { return reinterpret_cast<const float*>(arena[w])[i * NVP + v]; };
   const int nout = SLOT_LIN_BASE + SLOT_LIN_T * n_t;
   for (int o = threadIdx.x; o < nout; o += kBlockThreads) {
-    int v;
-    unsigned long long msk = all;
+    int v, j = -1;
     if (o < 36) {
       const int r = o / 6, c = o % 6;
       v = upper_index(min(r, c), max(r, c));
     } else if (o < 42) {
       v = 78 + (o - 36);
     } else {
-      const int j = (o - 42) / SLOT_LIN_T, q = (o - 42) % SLOT_LIN_T;
-      msk = s_mask[j];
+      j = (o - 42) / SLOT_LIN_T;
+      const int q = (o - 42) % SLOT_LIN_T;
       if (q < 36) v = 21 + q;
       else if (q < 72) { const int r = (q - 36) / 6, c = (q - 36) % 6; v = 57 + upper_index(min(r, c), max(r, c)); }
       else v = 84 + (q - 72);
     }
     float acc = 0.0f;
 #pragma unroll
-    for (int b = 0; b < BPW; ++b) acc += ((msk >> b) & 1ull) ? sblk(b, v) : 0.0f;
+    for (int w = 0; w < NW; ++w) {
+      const int wl = s_wlo[w], wn = s_wn[w];
+      if (j < 0) {
+        for (int i = 0; i < wn; ++i) acc += sset(w, i, v);
+      } else if (j >= wl && j < wl + wn) {
+        acc += sset(w, j - wl, v);
+      }
+    }
     g.part_lin[(long long)poff + o] = acc;
   }
 }
@@ -951,9 +927,12 @@ struct CrLevel {
 };
 
 template <int M>
-__global__ __launch_bounds__(256) void cr_build_kernel(const double* __restrict__ Sband, CrLevel L0, int N, int B) {
-  // one thread per element of D_I, U_I and b_I of level 0 (rows ≥ N are identity padding)
+__global__ __launch_bounds__(256) void cr_build_kernel(const double* __restrict__ Sband, CrLevel L0, int N, int B,
+                                                       int* __restrict__ status) {
+  // one thread per element of D_I, U_I and b_I of level 0 (rows ≥ N are identity padding); the solve's failure flag
+  // is cleared here (the levels only ever set it), which saves a memset launch per solve
   const long long tid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (tid == 0) *status = 0;
   const long long nD = (long long)L0.n * M * M;
   const int ROWG = (B + 1) * 36 + 6;
   auto lower = [&](int i, int j, int r, int c) -> double {  // S[6i+r][6j+c] for i ≥ j within the band
@@ -1560,9 +1539,13 @@ __global__ __launch_bounds__(kBlockThreads) void cost_reduce_kernel(const float*
 // the cost partials (slots [gp + gq, gp + gq + gc)), accepted when the solve succeeded, the model predicts a
 // decrease and (cost − cost_new) / model > min_relative_decrease.  On acceptance the record's current cost becomes
 // the candidate's.  One workgroup: strided per-thread sums, then a fixed-order tree in LDS (deterministic).
+// The record is also published to page-locked, host-coherent memory (host_rec: the kLmFields values, then the trial's
+// sequence number after a system-scope fence), so the host learns the decision by polling instead of through a copy
+// and a stream event (each of which left the GPU idle ~6 µs).
 __global__ __launch_bounds__(256) void lm_decide_kernel(const double* __restrict__ red, int gp, int gq, int gc,
                                                         const int* __restrict__ status, double lambda, double min_rel,
-                                                        double ftol, double* __restrict__ lm) {
+                                                        double ftol, double* __restrict__ lm,
+                                                        volatile double* __restrict__ host_rec, double seq) {
   __shared__ double part[5][256];
   double v[5] = {0, 0, 0, 0, 0};  // dg, dD, qg, qD, c
   for (int i = threadIdx.x; i < gp + gq + gc; i += 256) {
@@ -1598,6 +1581,17 @@ __global__ __launch_bounds__(256) void lm_decide_kernel(const double* __restrict
   lm[kLmAccept] = accept ? 1.0 : 0.0;
   lm[kLmStatus] = (double)st;
   if (accept) lm[kLmCost] = c;
+  if (host_rec) {
+    host_rec[kLmCost] = accept ? c : cost;
+    host_rec[kLmCostNew] = c;
+    host_rec[kLmModel] = model;
+    host_rec[kLmRel] = rel;
+    host_rec[kLmAccept] = accept ? 1.0 : 0.0;
+    host_rec[kLmStatus] = (double)st;
+    host_rec[kLmConverged] = converged ? 1.0 : 0.0;
+    __threadfence_system();
+    host_rec[kLmFields] = seq;
+  }
 }
 
 // The accepted candidate becomes the state (device-side accept, gated by the decision record; lm == nullptr: always).
@@ -1684,6 +1678,17 @@ int gn_prepare(pba_engine* e) {
   });
   std::vector<int> gtgt(nb);
   for (int i = 0; i < nb; ++i) gtgt[i] = e->block_target_h[order[i]];
+  // linearise order: each host's GN range regrouped by target (stable), so a chunk's blocks of one target are
+  // consecutive (one matrix-core chain per target run in linearize_kernel)
+  std::vector<int> lpos(nb);
+  std::iota(lpos.begin(), lpos.end(), 0);
+  for (int i = 0; i < nb;) {
+    const int h = ph[e->block_point_h[order[i]]];
+    int j = i;
+    while (j < nb && ph[e->block_point_h[order[j]]] == h) ++j;
+    std::stable_sort(lpos.begin() + i, lpos.begin() + j, [&](int x, int y) { return gtgt[x] < gtgt[y]; });
+    i = j;
+  }
   // linearise chunks
   std::vector<int4> cdesc;
   std::vector<uint8_t> blt(nb);
@@ -1691,11 +1696,11 @@ int gn_prepare(pba_engine* e) {
   std::vector<int> chunk_host;
   size_t off = 0;
   for (int i = 0; i < nb;) {
-    const int h = ph[e->block_point_h[order[i]]];
+    const int h = ph[e->block_point_h[order[lpos[i]]]];
     int j = i;
     std::vector<int> tg;
-    while (j < nb && j - i < G.bpw && ph[e->block_point_h[order[j]]] == h) {
-      const int t = gtgt[j];
+    while (j < nb && j - i < G.bpw && ph[e->block_point_h[order[lpos[j]]]] == h) {
+      const int t = gtgt[lpos[j]];
       auto it = std::find(tg.begin(), tg.end(), t);
       blt[j] = (uint8_t)(it - tg.begin());
       if (it == tg.end()) tg.push_back(t);
@@ -1846,7 +1851,10 @@ int gn_prepare(pba_engine* e) {
   for (int i = 0; i < nf; ++i) fixed[i] = (i < (int)G.fixed_h.size() && G.fixed_h[i]) || !observed[i];
   // upload
   hipStream_t st = e->stream;
-  PBA_HIP(G.gn_block.upload(order, st));
+  std::vector<int> lblk(nb);
+  for (int i = 0; i < nb; ++i) lblk[i] = order[lpos[i]];
+  PBA_HIP(G.lin_block.upload(lblk, st));
+  PBA_HIP(G.lin_gpos.upload(lpos, st));
   PBA_HIP(G.chunk_desc.upload(cdesc, st));
   PBA_HIP(G.blk_lt.upload(blt, st));
   PBA_HIP(G.blk_schur.resize((size_t)nb * 16));
@@ -1906,7 +1914,9 @@ int gn_prepare(pba_engine* e) {
   PBA_HIP(G.red.resize((size_t)2 * G.red_slots));
   PBA_HIP(G.red_h.resize(2 * G.red_slots));
   PBA_HIP(G.lm.resize(kLmFields));
-  PBA_HIP(G.lm_h.resize(kLmFields));
+  // decision record + sequence number, written by lm_decide_kernel over the bus (fine-grained host memory)
+  PBA_HIP(G.lm_h.resize(kLmFields + 1, hipHostMallocCoherent | hipHostMallocMapped));
+  PBA_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&G.lm_host_d), G.lm_h.p, 0));
   PBA_HIP(hipMemsetAsync(G.drho.p, 0, sizeof(double) * e->n_points, st));
   PBA_HIP(hipStreamSynchronize(st));
   G.prepared = true;
@@ -1987,11 +1997,15 @@ int total_cost(pba_engine* e, double* cost, int* n_valid) {
 }
 
 // gate: the device LM decision record — the kernels then run only if it accepted (speculatively enqueued).
-int linearize(pba_engine* e, double* cost, const double* gate = nullptr) {
+// pairs: the relative poses of the state to linearise at (nullptr: formed here from the engine's poses).
+int linearize(pba_engine* e, double* cost, const double* gate = nullptr, const PairRec* pairs = nullptr) {
   GnData& G = e->gn;
-  launch_pairs(e, e->poses.p, e->pairs.p);
-  const KernelArgs ka = make_kernel_args(e, e->pairs.p, e->rho.p);
-  LinArgs la{G.gn_block.p, G.chunk_desc.p, G.blk_lt.p, G.blk_schur.p, G.part_lin.p, G.n_chunks, gate};
+  if (!pairs) {
+    launch_pairs(e, e->poses.p, e->pairs.p);
+    pairs = e->pairs.p;
+  }
+  const KernelArgs ka = make_kernel_args(e, pairs, e->rho.p);
+  LinArgs la{G.lin_block.p, G.lin_gpos.p, G.chunk_desc.p, G.blk_lt.p, G.blk_schur.p, G.part_lin.p, G.n_chunks, gate};
   if (e->opt.residual_kind == PBA_RESIDUAL_PHOTOMETRIC) launch_linearize_photometric(e, ka, la);
   else launch_linearize_geometric(e, ka, la);
   PBA_HIP(hipGetLastError());
@@ -2017,7 +2031,8 @@ void cr_solve(pba_engine* e) {
   const int nl = (int)G.cr_levels.size();
   CrLevel L0 = cr_level(G, 0);
   const long long nthreads = (long long)L0.n * M * M + (long long)L0.n * M;
-  cr_build_kernel<M><<<(unsigned)((nthreads + 255) / 256), 256, 0, e->stream>>>(G.Sband.p, L0, e->n_frames, G.band_kernel);
+  cr_build_kernel<M><<<(unsigned)((nthreads + 255) / 256), 256, 0, e->stream>>>(G.Sband.p, L0, e->n_frames, G.band_kernel,
+                                                                                G.status.p);
   for (int l = 0; l + 1 < nl; ++l) {  // one fused launch per level (odd eliminations + even rebuild)
     CrLevel L = cr_level(G, l), Ln = cr_level(G, l + 1);
     if constexpr (2 * M + 1 <= 64)
@@ -2094,7 +2109,6 @@ int band_solve(pba_engine* e) {
   GnData& G = e->gn;
   const int nf = e->n_frames;
   if (G.solver == SOLVER_CR) {
-    PBA_HIP(hipMemsetAsync(G.status.p, 0, sizeof(int), e->stream));
     if (G.band_kernel == 4) cr_solve<24>(e);
     else cr_solve<48>(e);
   } else {
@@ -2153,37 +2167,52 @@ void launch_accept(pba_engine* e, const double* lm) {
   e->pairs_fresh = false;
 }
 
-// One LM trial on a single GPU, enqueued whole: solve → candidate state and model-decrease partials → candidate cost
-// → the accept/reject decision on the device (lm_decide_kernel) → read-back of the decision record → gated accept
-// → gated (speculative) linearisation at the new state.  The host waits only for the read-back, so an accepted
-// step's linearisation runs while the host computes the next λ: no host round trip leaves the GPU idle on the
-// accept path (each one cost ~30 µs: profiles/r1_c4_v31 kernel trace).  The candidate is evaluated even when the
-// solve failed (its numbers are then discarded): a garbage state is memory-safe in every evaluation kernel
-// (non-finite or out-of-image projections are clamped / out of domain).  ev: step | candidate cost | decision,
-// then the linearisation's begin | end; ev_read: the read-back.  d receives the decision record (kLm*).
-int lm_trial(pba_engine* e, double lambda, double min_rel, double ftol, const hipEvent_t* ev, const hipEvent_t* ev_lin,
-             hipEvent_t ev_read, double* d) {
+// Wait for trial `seq`'s decision record, published by lm_decide_kernel into host-coherent memory: a poll, not a
+// stream event (an event left the GPU idle ~6 µs each) — while the host polls, the GPU runs on into the gated accept
+// and linearisation.  The stream is queried now and then so a device error or a record that never comes ends the wait.
+int wait_decision(pba_engine* e, double seq, double* d) {
+  volatile double* r = e->gn.lm_h.p;
+  for (unsigned spins = 1;; ++spins) {
+    if (r[kLmFields] == seq) break;
+    if ((spins & 255u) == 0u) {
+      const hipError_t q = hipStreamQuery(e->stream);
+      if (q == hipSuccess && r[kLmFields] != seq) return fail(PBA_ERR_DEVICE, "LM decision record was not published");
+      if (q != hipSuccess && q != hipErrorNotReady) return fail(PBA_ERR_DEVICE, std::string("HIP: ") + hipGetErrorString(q));
+    }
+  }
+  std::atomic_thread_fence(std::memory_order_acquire);
+  for (int i = 0; i < kLmFields; ++i) d[i] = r[i];
+  return PBA_OK;
+}
+
+// One LM trial on a single GPU, enqueued whole: solve → candidate state, candidate pairs and model-decrease partials →
+// candidate cost → the accept/reject decision on the device (lm_decide_kernel, which also publishes it to the host)
+// → gated accept → gated (speculative) linearisation at the new state, on the candidate's pair table.  The host waits
+// only for the published decision, so an accepted step's linearisation runs while the host computes the next λ.  The
+// candidate is evaluated even when the solve failed (its numbers are then discarded): a garbage state is memory-safe in
+// every evaluation kernel (non-finite or out-of-image projections are clamped / out of domain).  ev (phase timing
+// only, else nullptr): step begin | candidate cost begin | decision end | linearisation begin | end.  d receives the
+// decision record (kLm*).
+int lm_trial(pba_engine* e, double lambda, double min_rel, double ftol, double seq, const hipEvent_t* ev, double* d) {
   GnData& G = e->gn;
-  PBA_HIP(hipEventRecord(ev[0], e->stream));
+  if (ev) PBA_HIP(hipEventRecord(ev[0], e->stream));
   if (int rc = enqueue_solve(e, lambda)) return rc;
   int gp = 0, gq = 0;
   enqueue_updates(e, lambda, G.fixed.p, &gp, &gq);
-  PBA_HIP(hipEventRecord(ev[1], e->stream));
+  if (ev) PBA_HIP(hipEventRecord(ev[1], e->stream));
   if (int rc = launch_cost_only(e, G.pairs_new.p, G.rho_new.p)) return rc;  // pairs_new from update_kernel
   const int gc = std::min(1024, (e->n_blocks + kBlockThreads - 1) / kBlockThreads);
   cost_reduce_kernel<<<gc, kBlockThreads, 0, e->stream>>>(e->cost.p, e->valid.p, e->n_blocks, G.red.p + 2 * (gp + gq));
-  lm_decide_kernel<<<1, 256, 0, e->stream>>>(G.red.p, gp, gq, gc, G.status.p, lambda, min_rel, ftol, G.lm.p);
+  lm_decide_kernel<<<1, 256, 0, e->stream>>>(G.red.p, gp, gq, gc, G.status.p, lambda, min_rel, ftol, G.lm.p,
+                                             G.lm_host_d, seq);
   PBA_HIP(hipGetLastError());
-  PBA_HIP(hipEventRecord(ev[2], e->stream));
-  PBA_HIP(hipMemcpyAsync(G.lm_h.data(), G.lm.p, sizeof(double) * kLmFields, hipMemcpyDeviceToHost, e->stream));
-  PBA_HIP(hipEventRecord(ev_read, e->stream));
+  if (ev) PBA_HIP(hipEventRecord(ev[2], e->stream));
   launch_accept(e, G.lm.p);
-  PBA_HIP(hipEventRecord(ev_lin[0], e->stream));
-  if (int rc = linearize(e, nullptr, G.lm.p)) return rc;
-  PBA_HIP(hipEventRecord(ev_lin[1], e->stream));
-  PBA_HIP(hipEventSynchronize(ev_read));
-  for (int i = 0; i < kLmFields; ++i) d[i] = G.lm_h[i];
-  return PBA_OK;
+  if (ev) PBA_HIP(hipEventRecord(ev[3], e->stream));
+  // an accepted candidate's relative poses are pairs_new (update_kernel): no pair launch at the new state
+  if (int rc = linearize(e, nullptr, G.lm.p, G.pairs_new.p)) return rc;
+  if (ev) PBA_HIP(hipEventRecord(ev[4], e->stream));
+  return wait_decision(e, seq, d);
 }
 
 int candidate_cost(pba_engine* e, double* cost) {
@@ -2419,39 +2448,48 @@ int lm_loop_single(pba_engine* e, const pba_solver_options* o, pba_solver_summar
   GnData& G = e->gn;
   const pba_solver_options opt = lm_options(o);
   pba_solver_summary s{};
-  struct Events {  // step | candidate cost | decision; read-back; two linearisation (begin, end) pairs
-    hipEvent_t ev[8] = {};
+  struct Events {  // phase timing (pba_set_solver_timing): step | candidate cost | decision; two linearisation pairs
+    hipEvent_t ev[7] = {};
     ~Events() {
       for (hipEvent_t x : ev)
         if (x) (void)hipEventDestroy(x);
     }
   } events;
+  const bool timed = G.phase_timing;
   hipEvent_t* ev = events.ev;
-  for (int i = 0; i < 8; ++i) PBA_HIP(hipEventCreate(&ev[i]));
+  if (timed)
+    for (int i = 0; i < 7; ++i) PBA_HIP(hipEventCreate(&ev[i]));
   const double t0 = now_ms();
   double cost = 0.0;
   if (int rc = linearize(e, &cost)) return rc;
   s.linearize_ms += now_ms() - t0;
   s.initial_cost = cost;
   G.lm_h[kLmCost] = cost;  // the device's current cost
+  G.lm_h[kLmFields] = 0.0;  // no trial published yet
   PBA_HIP(hipMemcpyAsync(G.lm.p, G.lm_h.data(), sizeof(double), hipMemcpyHostToDevice, e->stream));
   double radius = opt.initial_trust_region_radius, factor = 2.0;
   int iter = 0, pending = -1;  // pending: event pair of an accepted step's linearisation not yet timed
   s.termination = PBA_TERMINATION_MAX_ITERATIONS;
+  hipEvent_t tev[5] = {};
   for (; iter < opt.max_iterations; ++iter) {
     const double lambda = 1.0 / radius;
-    const hipEvent_t* lin = ev + 4 + 2 * (iter & 1);
+    const int lin = 3 + 2 * (iter & 1);
+    if (timed) tev[0] = ev[0], tev[1] = ev[1], tev[2] = ev[2], tev[3] = ev[lin], tev[4] = ev[lin + 1];
     double d[kLmFields];
-    if (int rc = lm_trial(e, lambda, opt.min_relative_decrease, opt.function_tolerance, ev, lin, ev[3], d)) return rc;
-    float ms = 0.0f;
-    PBA_HIP(hipEventElapsedTime(&ms, ev[0], ev[1]));
-    s.solve_ms += ms;
-    PBA_HIP(hipEventElapsedTime(&ms, ev[1], ev[2]));
-    s.cost_ms += ms;
-    if (pending >= 0) {  // the previous accepted step's linearisation ran before this trial's events
-      PBA_HIP(hipEventElapsedTime(&ms, ev[pending], ev[pending + 1]));
-      s.linearize_ms += ms;
-      pending = -1;
+    if (int rc = lm_trial(e, lambda, opt.min_relative_decrease, opt.function_tolerance, (double)(iter + 1),
+                          timed ? tev : nullptr, d)) return rc;
+    if (timed) {
+      float ms = 0.0f;
+      PBA_HIP(hipEventSynchronize(ev[2]));
+      PBA_HIP(hipEventElapsedTime(&ms, ev[0], ev[1]));
+      s.solve_ms += ms;
+      PBA_HIP(hipEventElapsedTime(&ms, ev[1], ev[2]));
+      s.cost_ms += ms;
+      if (pending >= 0) {  // the previous accepted step's linearisation ran before this trial's events
+        PBA_HIP(hipEventElapsedTime(&ms, ev[pending], ev[pending + 1]));
+        s.linearize_ms += ms;
+        pending = -1;
+      }
     }
     if (d[kLmConverged] != 0.0) {  // |Δcost| ≤ function_tolerance · cost: stop at the current state
       s.termination = PBA_TERMINATION_CONVERGENCE;
@@ -2470,10 +2508,10 @@ int lm_loop_single(pba_engine* e, const pba_solver_options* o, pba_solver_summar
     radius = radius / std::max(1.0 / 3.0, 1.0 - std::pow(2.0 * rel - 1.0, 3));
     factor = 2.0;
     cost = d[kLmCostNew];
-    pending = 4 + 2 * (iter & 1);
+    pending = lin;
   }
   PBA_HIP(hipStreamSynchronize(e->stream));  // the last trial's accept / linearisation
-  if (pending >= 0) {
+  if (timed && pending >= 0) {
     float ms = 0.0f;
     PBA_HIP(hipEventElapsedTime(&ms, ev[pending], ev[pending + 1]));
     s.linearize_ms += ms;
@@ -2565,6 +2603,12 @@ extern "C" {
 int pba_solve(pba_engine* e, const pba_solver_options* o, pba_solver_summary* sum) {
   if (int rc = ensure_prepared(e)) return rc;
   return lm_loop(e, o, nullptr, sum);
+}
+
+int pba_set_solver_timing(pba_engine* e, int32_t enable) {
+  if (!e) return fail(PBA_ERR_INVALID_ARGUMENT, "null engine");
+  e->gn.phase_timing = enable != 0;
+  return PBA_OK;
 }
 
 int pba_solve_distributed(pba_engine* e, const pba_solver_options* o, int32_t band, double* d_exchange,

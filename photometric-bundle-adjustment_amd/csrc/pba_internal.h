@@ -425,12 +425,12 @@ struct PinnedBuf {
   ~PinnedBuf() {
     if (p) (void)hipHostFree(p);
   }
-  hipError_t resize(size_t count) {
+  hipError_t resize(size_t count, unsigned flags = hipHostMallocDefault) {
     if (count <= n && p) return hipSuccess;
     if (p) (void)hipHostFree(p);
     p = nullptr;
     n = 0;
-    hipError_t e = hipHostMalloc(reinterpret_cast<void**>(&p), (count ? count : 1) * sizeof(T), hipHostMallocDefault);
+    hipError_t e = hipHostMalloc(reinterpret_cast<void**>(&p), (count ? count : 1) * sizeof(T), flags);
     if (e == hipSuccess) n = count;
     return e;
   }
@@ -455,9 +455,10 @@ struct GnData {
   DevBuf<double> cr_buf;
   bool force_skyline = false;
   size_t lin_floats = 0, schur_doubles = 0;
-  DevBuf<int> gn_block;          // GN order → original block
-  DevBuf<int4> chunk_desc;       // linearise chunk: first GN block, count, n_targets, partial offset
-  DevBuf<uint8_t> blk_lt;        // GN block → local target slot in its linearise chunk
+  DevBuf<int> lin_block;         // linearise order (GN order regrouped by target within each host) → block
+  DevBuf<int> lin_gpos;          // linearise order → GN position
+  DevBuf<int4> chunk_desc;       // linearise chunk: first linearise position, count, n_targets, partial offset
+  DevBuf<uint8_t> blk_lt;        // linearise position → local target slot in its chunk
   DevBuf<float> blk_schur;       // GN block → 16 floats [Hll gl Wh(6) Wt(6) 0 0]
   DevBuf<float> part_lin;        // linearise chunk partials (fp32)
   DevBuf<int> pt_first, pt_nblk, pt_orig;  // GN point → first GN block, block count, original point
@@ -485,7 +486,9 @@ struct GnData {
   bool pairs_new_fresh = false;  // pairs_new formed by the last update_kernel (its candidate state)
   PinnedBuf<double> red_h;
   DevBuf<double> lm;         // LM decision record of the single-GPU loop (pba_gn.hip: kLm*)
-  PinnedBuf<double> lm_h;
+  PinnedBuf<double> lm_h;    // its host copy (+ sequence number), host-coherent, written by lm_decide_kernel
+  double* lm_host_d = nullptr;  // lm_h's device address
+  bool phase_timing = false;    // pba_set_solver_timing: stream events around the LM phases
   int red_slots = 0;
 };
 

@@ -121,6 +121,7 @@ def lib():
         "pba_host_alloc": ([C.c_size_t, C.POINTER(vp)], C.c_int),
         "pba_host_free": ([vp], C.c_int),
         "pba_set_interpolator": ([vp, i32], C.c_int),
+        "pba_set_solver_timing": ([vp, i32], C.c_int),
         "pba_interpolator": ([vp], C.c_int),
         "pba_sample_image": ([vp, i32, i32, vp, vp], C.c_int),
         "pba_get_cost": ([vp, C.POINTER(C.c_double), C.POINTER(i32)], C.c_int),
@@ -349,6 +350,10 @@ class Engine:
 
     def gn_accept(self):
         _check(self._L.pba_gn_accept(self._h), "pba_gn_accept")
+
+    def set_solver_timing(self, enable: bool):
+        """per-phase device timing of solve() (linearize_ms / solve_ms / cost_ms); off by default"""
+        _check(self._L.pba_set_solver_timing(self._h, 1 if enable else 0), "pba_set_solver_timing")
 
     def solve(self, max_iterations=20, initial_trust_region_radius=1e4, function_tolerance=1e-6,
               min_relative_decrease=1e-3) -> dict:

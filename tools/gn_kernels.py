@@ -1,0 +1,45 @@
+#!/usr/bin/env python3
+"""Diagnostic: the GN kernels of one LM iteration at C4, run unconditionally (linearise, step, candidate cost) N
+times at a fixed state, for `rocprofv3 --kernel-trace --stats` per-kernel averages of a library variant
+(PBA_LIBRARY=…).  Not a parity check and not the bench: variants under study may compute garbage.
+
+    rocprofv3 --kernel-trace --stats -d gpurun_out/gnk -o run -- python tools/gn_kernels.py [--iters 20]
+"""
+import argparse
+import importlib
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+synth = importlib.import_module("photometric-bundle-adjustment_amd.synth")
+E = importlib.import_module("photometric-bundle-adjustment_amd.engine")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--texture", default="noise")
+    args = ap.parse_args()
+    import numpy as np
+    import torch
+    dev = torch.device("cuda", 0)
+    pb, images = synth.c4_shard(dev, texture=args.texture)
+    eng = E.Engine(synth.PHOTOMETRIC, synth.PINHOLE, device=0, huber_width=9.0)
+    eng.set_problem(pb, images_device_ptr=images.data_ptr())
+    eng.set_fixed_frames(np.array([0, 1], np.int32))
+    eng.set_state(pb.poses, pb.rho)
+    eng.gn_linearize()
+    t0 = time.perf_counter()
+    for _ in range(args.iters):
+        eng.gn_linearize()
+        eng.gn_step(1e-4)
+        eng.gn_candidate_cost()
+    eng.synchronize()
+    print(f"{1e3 * (time.perf_counter() - t0) / args.iters:.3f} ms per (linearise + step + candidate cost), host-synchronous")
+    eng.close()
+
+
+if __name__ == "__main__":
+    main()
