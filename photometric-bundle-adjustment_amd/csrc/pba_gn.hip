@@ -45,9 +45,11 @@ using namespace pba::detail;
 
 namespace {
 
+typedef double v4f64 __attribute__((ext_vector_type(4)));
+
 constexpr int NV = 104;          // normal-equation products per residual row
-constexpr int SCHUR_PTS = 64;    // points per Schur chunk
-constexpr int SCHUR_W = 1024;    // points × local poses per Schur chunk (LDS budget)
+constexpr int SCHUR_PTS = 128;   // points per Schur chunk
+constexpr int SCHUR_W = 2048;    // points × local poses per Schur chunk (LDS budget: dynamic, 24 B each)
 constexpr int SLOT_LIN_BASE = 42;  // H_hh(36) + g_h(6)
 constexpr int SLOT_LIN_T = 78;     // H_ht(36) + H_tt(36) + g_t(6)
 
@@ -278,7 +280,7 @@ void linearize_kernel(const KernelArgs a, const LinArgs g) {
 
 struct SchurArgs {
   const int4* desc;       // first GN point, n points, n local poses, partial offset (doubles)
-  const int2* aux;        // used-pair list offset, n used pairs
+  const int4* aux;        // pair list offset, n pairs, first GN block, n blocks (the last two: diagnostics)
   const uchar2* pairs;    // (a, b) local pose pairs, a ≤ b
   const int* pt_first;
   const int* pt_nblk;
@@ -293,40 +295,97 @@ struct SchurArgs {
 // schur_kernel: point elimination for damping λ
 // ------------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(kBlockThreads) void schur_kernel(const SchurArgs g, double lambda) {
-  __shared__ float W[SCHUR_W][6];
+  extern __shared__ __attribute__((aligned(16))) float W_dyn[];  // W [points × local poses][6] (gn_prepare: schur_lds)
   __shared__ double s_inv[SCHUR_PTS], s_gl[SCHUR_PTS];
   const int c = blockIdx.x;
   if (c >= g.n_chunks) return;
   const int4 d = g.desc[c];
   const int first = d.x, npt = d.y, nv = d.z, poff = d.w;
-  const int2 ax = g.aux[c];
+  const int4 ax = g.aux[c];
+  float (*W)[6] = reinterpret_cast<float (*)[6]>(W_dyn);
   for (int i = threadIdx.x; i < npt * nv * 6; i += kBlockThreads) (&W[0][0])[i] = 0.0f;
   __syncthreads();
-  if (threadIdx.x < npt) {
-    const int p = threadIdx.x, gp = first + p;
-    const int fb = g.pt_first[gp], nb = g.pt_nblk[gp];
-    double H = 0.0, gl = 0.0, wh[6] = {0, 0, 0, 0, 0, 0};
-    for (int b = fb; b < fb + nb; ++b) {
-      const float* q = g.blk_schur + (long long)b * 16;
-      H += q[0];
-      gl += q[1];
-      const int lv = g.blk_lv[b];
-      for (int i = 0; i < 6; ++i) {
-        wh[i] += q[2 + i];
-        W[p * nv + lv][i] += q[8 + i];
+  // four lanes per point, each summing one float4 of the point's blocks' 16-float records in block order:
+  // q = 0: H_ρρ, g_ρ, W_h[0..1]   q = 1: W_h[2..5]   q = 2: W_t[0..3] → W[p][lv]   q = 3: W_t[4..5] → W[p][lv]
+  // (staging the chunk's records in LDS block-parallel instead measured slower: 23 → 35 µs at C4, its LDS halves the
+  // resident workgroups)
+  for (int p0 = 0; p0 < npt; p0 += kBlockThreads / 4) {
+    const int p = p0 + (threadIdx.x >> 2), q = threadIdx.x & 3, gp = first + p;
+    if (p < npt) {
+      const int fb = g.pt_first[gp], nb = g.pt_nblk[gp];
+      double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
+      constexpr int kBatch = 8;  // every load of a batch issued before the first use: one memory round trip per batch
+      for (int b0 = fb; b0 < fb + nb; b0 += kBatch) {
+        float4 v[kBatch];
+        int lv[kBatch];
+#pragma unroll
+        for (int u = 0; u < kBatch; ++u) {
+          const int b = min(b0 + u, fb + nb - 1);
+          v[u] = reinterpret_cast<const float4*>(g.blk_schur + (long long)b * 16)[q];
+          lv[u] = q < 2 ? 0 : g.blk_lv[b];
+        }
+#pragma unroll
+        for (int u = 0; u < kBatch; ++u) {
+          if (b0 + u >= fb + nb) break;
+          if (q < 2) {
+            s0 += v[u].x; s1 += v[u].y; s2 += v[u].z; s3 += v[u].w;
+          } else {
+            float* wt = W[p * nv + lv[u]];
+            if (q == 2) { wt[0] += v[u].x; wt[1] += v[u].y; wt[2] += v[u].z; wt[3] += v[u].w; }
+            else { wt[4] += v[u].x; wt[5] += v[u].y; }
+          }
+        }
+      }
+      double* pd = g.pt_data + (long long)gp * 8;
+      if (q == 0) {
+        W[p * nv][0] = (float)s2;
+        W[p * nv][1] = (float)s3;
+        const double D = fmin(fmax(s0, 1e-6), 1e32);
+        const double Hd = s0 + lambda * D;
+        s_inv[p] = Hd > 0.0 ? 1.0 / Hd : 0.0;
+        s_gl[p] = s1;
+        pd[0] = s0; pd[1] = s1; pd[2] = s2; pd[3] = s3;
+      } else if (q == 1) {
+        W[p * nv][2] = (float)s0; W[p * nv][3] = (float)s1; W[p * nv][4] = (float)s2; W[p * nv][5] = (float)s3;
+        pd[4] = s0; pd[5] = s1; pd[6] = s2; pd[7] = s3;
       }
     }
-    for (int i = 0; i < 6; ++i) W[p * nv + 0][i] = (float)wh[i];
-    const double D = fmin(fmax(H, 1e-6), 1e32);
-    const double Hd = H + lambda * D;
-    s_inv[p] = Hd > 0.0 ? 1.0 / Hd : 0.0;
-    s_gl[p] = gl;
-    double* pd = g.pt_data + (long long)gp * 8;
-    pd[0] = H;
-    pd[1] = gl;
-    for (int i = 0; i < 6; ++i) pd[2 + i] = wh[i];
   }
   __syncthreads();
+  if (nv * 6 + 1 <= 32) {
+    // ≤ 5 local poses (a temporal window): the chunk's sums are one small GEMM on the matrix cores,
+    // C = (W·diag(1/H'_ρρ))ᵀ [W | g_ρ] over its points (K = points, 4 per v_mfma_f64_16x16x4f64 step), 32 × 32 in
+    // four 16 × 16 tiles, one per wave; C's 6 × 6 blocks (a, b) of the used pose pairs and its column nv·6 (the
+    // gradient terms) are the partial slots.  Layouts as in cr_level_wave_kernel: A lane l = (row l%16, k l/16),
+    // B lane l = (k l/16, column l%16), accumulator entry v of lane l = (row l/16 + 4v, column l%16).
+    const int nv6 = nv * 6;
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int ti = wv & 1, tj = wv >> 1;
+    const int ca = 16 * ti + (lane & 15), cb = 16 * tj + (lane & 15), kq = lane >> 4;
+    const float* Wf = &W[0][0];
+    v4f64 acc = {0.0, 0.0, 0.0, 0.0};
+    for (int p0 = 0; p0 < npt; p0 += 4) {
+      const int p = p0 + kq;
+      const bool pin = p < npt;
+      const double av = (pin && ca < nv6) ? (double)Wf[p * nv6 + ca] * s_inv[p] : 0.0;
+      const double bv = !pin ? 0.0 : (cb < nv6 ? (double)Wf[p * nv6 + cb] : (cb == nv6 ? s_gl[p] : 0.0));
+      acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
+    }
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      const int r = 16 * ti + (lane >> 4) + 4 * v;
+      if (r >= nv6) continue;
+      if (cb < nv6) {
+        // canonical pair order (gn_prepare): (0,0) (0,1) … (0,nv−1) (1,1) …; blocks of unused pairs are zero
+        const int pa_ = r / 6, pb_ = cb / 6;
+        const int u = pa_ * nv - pa_ * (pa_ - 1) / 2 + (pb_ - pa_);
+        if (pa_ <= pb_) g.part_schur[(long long)poff + u * 36 + (r % 6) * 6 + cb % 6] = acc[v];
+      } else if (cb == nv6) {
+        g.part_schur[(long long)poff + ax.y * 36 + r] = acc[v];
+      }
+    }
+    return;
+  }
   const int nout = ax.y * 36 + nv * 6;
   for (int o = threadIdx.x; o < nout; o += kBlockThreads) {
     double acc = 0.0;
@@ -1162,7 +1221,6 @@ __device__ __forceinline__ bool gj_wave(const double* __restrict__ D, const doub
   return !bad;
 }
 
-typedef double v4f64 __attribute__((ext_vector_type(4)));
 
 template <int M>
 constexpr size_t cr_level_wave_lds() { return sizeof(double) * (3 * M * M + M + 2 * M * (2 * M + 1)); }
@@ -1729,9 +1787,11 @@ int gn_prepare(pba_engine* e) {
   const int ngp = (int)pfirst.size();
   G.n_gn_points = ngp;
   // Schur chunks
+  G.schur_lds = 0;
   std::vector<int4> sdesc;
-  std::vector<int2> saux;
+  std::vector<int4> saux;
   std::vector<uchar2> spairs;
+  std::vector<std::vector<char>> schur_used_flag;
   std::vector<uint8_t> blv(nb, 0);
   std::vector<std::vector<int>> schur_poses;
   std::vector<std::vector<std::pair<int, int>>> schur_used;
@@ -1764,16 +1824,26 @@ int gn_prepare(pba_engine* e) {
       for (int x : lv)
         for (int y : lv) used[std::min(x, y) * nv + std::max(x, y)] = 1;
     }
+    // pair slots: the used pairs, or every pair (a ≤ b) in canonical order when the chunk takes the matrix-core path
+    // of schur_kernel (≤ 5 local poses; unused pairs are zero blocks no contribution list references)
+    const bool canon = nv * 6 + 1 <= 32;
     std::vector<std::pair<int, int>> up;
+    std::vector<char> upu;
     for (int x = 0; x < nv; ++x)
       for (int y = x; y < nv; ++y)
-        if (used[x * nv + y]) up.emplace_back(x, y);
-    saux.push_back(make_int2((int)spairs.size(), (int)up.size()));
+        if (canon || used[x * nv + y]) {
+          up.emplace_back(x, y);
+          upu.push_back(used[x * nv + y]);
+        }
+    const int fb0 = pfirst[p], nbc = pfirst[q - 1] + pnblk[q - 1] - fb0;
+    saux.push_back(make_int4((int)spairs.size(), (int)up.size(), fb0, nbc));
     for (auto& pr : up) spairs.push_back(make_uchar2((unsigned char)pr.first, (unsigned char)pr.second));
     sdesc.push_back(make_int4(p, q - p, nv, (int)soff));
+    G.schur_lds = std::max<size_t>(G.schur_lds, sizeof(float) * 6 * (size_t)(q - p) * nv);
     soff += 36 * up.size() + 6 * nv;
     schur_poses.push_back(poses);
     schur_used.push_back(up);
+    schur_used_flag.push_back(upu);
     p = q;
   }
   G.schur_doubles = soff;
@@ -1803,6 +1873,7 @@ int gn_prepare(pba_engine* e) {
     const auto& poses = schur_poses[s];
     const int o = sdesc[s].w;
     for (size_t u = 0; u < schur_used[s].size(); ++u) {
+      if (!schur_used_flag[s][u]) continue;
       const int fa = poses[schur_used[s][u].first], fb = poses[schur_used[s][u].second];
       add(fa, fb, o + 36 * (int)u, C_SCHUR);
     }
@@ -2121,13 +2192,21 @@ int band_solve(pba_engine* e) {
   return PBA_OK;
 }
 
+// Dynamic LDS above the default 64 KiB limit (the attribute is per device: set on every launch, cheap).
+void schur_lds_limit(const GnData& G) {
+  if (G.schur_lds > 65536)
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&schur_kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)G.schur_lds);
+}
+
 // Schur complement for λ, assembly and reduced-system solve into G.x (enqueued only).
 int enqueue_solve(pba_engine* e, double lambda) {
   GnData& G = e->gn;
   const int nf = e->n_frames;
   SchurArgs sa{G.schur_desc.p, G.schur_aux.p, G.schur_pairs.p, G.pt_first.p, G.pt_nblk.p, G.blk_lv.p,
                G.blk_schur.p, G.part_schur.p, G.pt_data.p, G.n_schur};
-  schur_kernel<<<G.n_schur, kBlockThreads, 0, e->stream>>>(sa, lambda);
+  schur_lds_limit(G);
+  schur_kernel<<<G.n_schur, kBlockThreads, G.schur_lds, e->stream>>>(sa, lambda);
   AsmArgs aa{G.part_lin.p, G.part_schur.p, G.sky_cptr.p, G.sky_contrib.p, G.g_cptr.p, G.g_contrib.p,
              G.sky_blk_i.p, G.sky_blk_j.p, G.fixed.p, G.S.p, G.g.p, G.g_dir.p, G.Ddiag.p,
              G.band_kernel ? G.Sband.p : nullptr, G.band_kernel, G.n_sky, nf};
@@ -2245,7 +2324,8 @@ int step_export(pba_engine* e, double lambda, int band, double* X) {
   const int nf = e->n_frames;
   SchurArgs sa{G.schur_desc.p, G.schur_aux.p, G.schur_pairs.p, G.pt_first.p, G.pt_nblk.p, G.blk_lv.p,
                G.blk_schur.p, G.part_schur.p, G.pt_data.p, G.n_schur};
-  if (G.n_schur > 0) schur_kernel<<<G.n_schur, kBlockThreads, 0, e->stream>>>(sa, lambda);
+  schur_lds_limit(G);
+  if (G.n_schur > 0) schur_kernel<<<G.n_schur, kBlockThreads, G.schur_lds, e->stream>>>(sa, lambda);
   PBA_HIP(hipMemsetAsync(X, 0, sizeof(double) * (size_t)nf * ex_row(K), e->stream));
   AsmArgs aa{G.part_lin.p, G.part_schur.p, G.sky_cptr.p, G.sky_contrib.p, G.g_cptr.p, G.g_contrib.p,
              G.sky_blk_i.p, G.sky_blk_j.p, G.fixed.p, G.S.p, G.g.p, G.g_dir.p, G.Ddiag.p, nullptr, K, G.n_sky, nf};

@@ -454,7 +454,7 @@ struct GnData {
   std::vector<CrLevelHost> cr_levels;  // block-cyclic-reduction level layout (offsets into cr_buf)
   DevBuf<double> cr_buf;
   bool force_skyline = false;
-  size_t lin_floats = 0, schur_doubles = 0;
+  size_t lin_floats = 0, schur_doubles = 0, schur_lds = 0;
   DevBuf<int> lin_block;         // linearise order (GN order regrouped by target within each host) → block
   DevBuf<int> lin_gpos;          // linearise order → GN position
   DevBuf<int4> chunk_desc;       // linearise chunk: first linearise position, count, n_targets, partial offset
@@ -463,7 +463,7 @@ struct GnData {
   DevBuf<float> part_lin;        // linearise chunk partials (fp32)
   DevBuf<int> pt_first, pt_nblk, pt_orig;  // GN point → first GN block, block count, original point
   DevBuf<int4> schur_desc;       // Schur chunk: first GN point, n points, n local poses, partial offset
-  DevBuf<int2> schur_aux;        // Schur chunk: used-pair list offset, n used pairs
+  DevBuf<int4> schur_aux;        // Schur chunk: pair list offset, n pairs, first GN block, n blocks
   DevBuf<uchar2> schur_pairs;    // used local pose pairs (a ≤ b) of every Schur chunk
   DevBuf<int> pt_host, gn_target;  // GN point → host frame; GN block → target frame
   DevBuf<double> drho;           // last step's δρ (original point order)
