@@ -151,11 +151,18 @@ __global__ __launch_bounds__(kBlockThreads) void photometric_block_kernel(const 
   // per-block validity (ballot over the wave: the block's LPB lanes are an aligned bit field) and ‖r‖²
   const int ok = group_all<LPB>(act ? row.ok : 1);
   const float s = group_sum<LPB>(act ? row.r * row.r : 0.0f);
+  const float bc = ok ? huber_cost(s, a.huber) : 0.0f;
   if (live && k == 0) {
     a.valid[blk] = (uint8_t)ok;
-    a.cost[blk] = ok ? huber_cost(s, a.huber) : 0.0f;
+    a.cost[blk] = bc;
   }
-  if (MODE == 2) return;
+  if (MODE == 2) {
+    if (a.wg_red) {
+      const bool one = live && k == 0;
+      wg_reduce2(one ? (double)bc : 0.0, one && ok ? 1.0 : 0.0, a.wg_red + 2 * logical_tile());
+    }
+    return;
+  }
   if (!JAC) {
     if (act) out[(long long)blk * rec_f + k] = (T)(ok ? row.r : 0.0f);
     return;
@@ -249,11 +256,18 @@ __global__ __launch_bounds__((kMultiThreads<PPL, T>)) void photometric_block_ker
   // per-block validity (ballot over the wave: the block's LPB lanes are an aligned bit field) and ‖r‖²
   const int ok = group_all<LPB>(okl);
   s = group_sum<LPB>(s);
+  const float bc = ok ? huber_cost(s, a.huber) : 0.0f;
   if (live && k == 0) {
     a.valid[blk] = (uint8_t)ok;
-    a.cost[blk] = ok ? huber_cost(s, a.huber) : 0.0f;
+    a.cost[blk] = bc;
   }
-  if (MODE == 2) return;
+  if (MODE == 2) {
+    if (a.wg_red) {
+      const bool one = live && k == 0;
+      wg_reduce2(one ? (double)bc : 0.0, one && ok ? 1.0 : 0.0, a.wg_red + 2 * logical_tile());
+    }
+    return;
+  }
   if (!JAC) {
 #pragma unroll
     for (int j = 0; j < PPL; ++j) {
@@ -283,8 +297,10 @@ __global__ __launch_bounds__((kMultiThreads<PPL, T>)) void photometric_block_ker
 // ------------------------------------------------------------------------------------------------
 template <int MODEL, bool JAC>
 __global__ __launch_bounds__(kBlockThreads) void geometric_block_kernel(const KernelArgs a) {
-  const int blk = logical_tile() * kBlockThreads + threadIdx.x;
-  if (blk >= a.n_blocks) return;
+  const int blk_ = logical_tile() * kBlockThreads + threadIdx.x;
+  const bool live = blk_ < a.n_blocks;
+  if (!live && !a.wg_red) return;  // (with wg_red every thread reaches the workgroup reduction)
+  const int blk = live ? blk_ : a.n_blocks - 1;
   const int pt = a.block_point[blk];
   const PairRec& pp = a.pairs[a.block_pair[blk]];
   const double* khd = a.intr_d + kCamD * pp.host_cam;
@@ -328,8 +344,13 @@ __global__ __launch_bounds__(kBlockThreads) void geometric_block_kernel(const Ke
 #pragma unroll
     for (int i = 2; i < 28; ++i) ok = ok && isfinite(J[i]);
   }
+  const float bc = ok ? huber_cost(r0 * r0 + r1 * r1, a.huber) : 0.0f;
+  if (a.wg_red) {
+    wg_reduce2(live ? (double)bc : 0.0, live && ok ? 1.0 : 0.0, a.wg_red + 2 * logical_tile());
+    if (!live) return;
+  }
   a.valid[blk] = (uint8_t)ok;
-  a.cost[blk] = ok ? huber_cost(r0 * r0 + r1 * r1, a.huber) : 0.0f;
+  a.cost[blk] = bc;
   if (!ok) {
 #pragma unroll
     for (int i = 0; i < 28; ++i) J[i] = 0.0f;
@@ -346,6 +367,7 @@ __global__ __launch_bounds__(kBlockThreads) void geometric_block_kernel(const Ke
 template <int MODEL>
 void launch_geometric(pba_engine* e, const KernelArgs& ka, int mode) {
   const int grid = (e->n_blocks + kBlockThreads - 1) / kBlockThreads;
+  e->last_grid = grid;
   if (mode == 1) geometric_block_kernel<MODEL, true><<<grid, kBlockThreads, 0, e->stream>>>(ka);
   else geometric_block_kernel<MODEL, false><<<grid, kBlockThreads, 0, e->stream>>>(ka);
 }
@@ -356,6 +378,7 @@ void launch_photometric(pba_engine* e, const KernelArgs& ka, int mode) {
   const bool h = e->record_format == PBA_RECORD_F16;
   if (e->P <= 8) {
     const int grid = (int)(((long long)e->n_blocks * 8 + kBlockThreads - 1) / kBlockThreads);
+    e->last_grid = grid;
     if (mode == 1 && h) photometric_block_kernel<PM, 8, 1, _Float16><<<grid, kBlockThreads, 0, e->stream>>>(ka);
     else if (mode == 1) photometric_block_kernel<PM, 8, 1, float><<<grid, kBlockThreads, 0, e->stream>>>(ka);
     else if (mode == 0 && h) photometric_block_kernel<PM, 8, 0, _Float16><<<grid, kBlockThreads, 0, e->stream>>>(ka);
@@ -368,6 +391,7 @@ void launch_photometric(pba_engine* e, const KernelArgs& ka, int mode) {
   {                                                                                                     \
     constexpr int nth = kMultiThreads<PPL, TT>;                                                         \
     const int grid = (int)(((long long)e->n_blocks * 8 + nth - 1) / nth);                              \
+    e->last_grid = grid;                                                                                \
     const size_t lds = (M == 1 ? multi_stage_bytes(nth / 8, e->P, (int)sizeof(TT)) : 0) +              \
                        (size_t)(nth / 8) * sizeof(TileBlock);                                           \
     photometric_block_kernel_multi<PM, M, TT, PPL><<<grid, nth, lds, e->stream>>>(ka);                  \
@@ -448,9 +472,11 @@ void launch_pairs(pba_engine* e, const double* poses, PairRec* pairs) {
                                                                e->frame_cam.p, e->intr_d.p, pairs, e->n_pairs);
 }
 
-int launch_cost_only(pba_engine* e, const PairRec* pairs, const double* rho) {
-  const KernelArgs ka = make_kernel_args(e, pairs, rho);
+int launch_cost_only(pba_engine* e, const PairRec* pairs, const double* rho, double* wg_red, int* n_slots) {
+  KernelArgs ka = make_kernel_args(e, pairs, rho);
+  ka.wg_red = wg_red;
   launch_mode(e, ka, 2);
+  if (n_slots) *n_slots = e->last_grid;
   PBA_HIP(hipGetLastError());
   return PBA_OK;
 }

@@ -1450,22 +1450,6 @@ __device__ void se3_exp_mul(const double* T, const double* d, double* out) {
   out[6] = T[6] + tz + aw * u2 + (ax * u1 - ay * u0);
 }
 
-__device__ __forceinline__ void block_reduce2(double a, double b, double* out) {
-  __shared__ double sa[kBlockThreads / 64], sb[kBlockThreads / 64];
-  for (int m = 32; m >= 1; m >>= 1) {
-    a += __shfl_xor(a, m, 64);
-    b += __shfl_xor(b, m, 64);
-  }
-  const int w = threadIdx.x / 64, l = threadIdx.x % 64;
-  if (l == 0) { sa[w] = a; sb[w] = b; }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    double x = 0, y = 0;
-    for (int i = 0; i < (int)(blockDim.x / 64); ++i) { x += sa[i]; y += sb[i]; }
-    out[0] = x;
-    out[1] = y;
-  }
-}
 
 struct PoseUpdateArgs {
   const double* poses;
@@ -1499,7 +1483,7 @@ __device__ __forceinline__ void pose_update_block(const PoseUpdateArgs& a, int b
       }
     }
   }
-  block_reduce2(dg, dD, a.red + 2 * blk);
+  wg_reduce2(dg, dD, a.red + 2 * blk);
 }
 
 struct PointUpdateArgs {
@@ -1543,7 +1527,7 @@ __device__ __forceinline__ void point_update_block(const PointUpdateArgs& a, dou
     dg = dr * gl;
     dD = dr * dr * D;
   }
-  block_reduce2(dg, dD, a.red + 2 * slot);
+  wg_reduce2(dg, dD, a.red + 2 * slot);
 }
 
 struct PairUpdateArgs {
@@ -1589,7 +1573,7 @@ __global__ __launch_bounds__(kBlockThreads) void cost_reduce_kernel(const float*
     c += cost[i];
     v += valid[i];
   }
-  block_reduce2(c, v, red + 2 * blockIdx.x);
+  wg_reduce2(c, v, red + 2 * blockIdx.x);
 }
 
 // The LM trial's decision on the device (trust_region_minimizer.cc semantics, the same sums and order as the host
@@ -1600,22 +1584,36 @@ __global__ __launch_bounds__(kBlockThreads) void cost_reduce_kernel(const float*
 // The record is also published to page-locked, host-coherent memory (host_rec: the kLmFields values, then the trial's
 // sequence number after a system-scope fence), so the host learns the decision by polling instead of through a copy
 // and a stream event (each of which left the GPU idle ~6 µs).
-__global__ __launch_bounds__(256) void lm_decide_kernel(const double* __restrict__ red, int gp, int gq, int gc,
+constexpr int kDecideThreads = 1024;
+__global__ __launch_bounds__(kDecideThreads) void lm_decide_kernel(const double* __restrict__ red, int gp, int gq, int gc,
                                                         const int* __restrict__ status, double lambda, double min_rel,
                                                         double ftol, double* __restrict__ lm,
                                                         volatile double* __restrict__ host_rec, double seq) {
-  __shared__ double part[5][256];
+  constexpr int N = kDecideThreads, U = 4;
+  __shared__ double part[5][N];
   double v[5] = {0, 0, 0, 0, 0};  // dg, dD, qg, qD, c
-  for (int i = threadIdx.x; i < gp + gq + gc; i += 256) {
-    const double a = red[2 * i], b = red[2 * i + 1];
-    if (i < gp) { v[0] += a; v[1] += b; }
-    else if (i < gp + gq) { v[2] += a; v[3] += b; }
-    else v[4] += a;
-  }
+  // strided sums of each slot range, U independent loads in flight per thread (the candidate cost alone has one slot
+  // per evaluation workgroup: 12.5k at C4)
+  auto range = [&](int beg, int end, double& x, double& y) {
+    for (int i0 = beg + (int)threadIdx.x; i0 < end; i0 += U * N) {
+      double2 r[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int i = i0 + u * N;
+        r[u] = i < end ? reinterpret_cast<const double2*>(red)[i] : make_double2(0.0, 0.0);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) { x += r[u].x; y += r[u].y; }
+    }
+  };
+  double unused = 0.0;
+  range(0, gp, v[0], v[1]);
+  range(gp, gp + gq, v[2], v[3]);
+  range(gp + gq, gp + gq + gc, v[4], unused);
 #pragma unroll
   for (int q = 0; q < 5; ++q) part[q][threadIdx.x] = v[q];
   __syncthreads();
-  for (int w = 128; w > 0; w >>= 1) {
+  for (int w = N / 2; w > 0; w >>= 1) {
     if ((int)threadIdx.x < w)
 #pragma unroll
       for (int q = 0; q < 5; ++q) part[q][threadIdx.x] += part[q][threadIdx.x + w];
@@ -1981,7 +1979,8 @@ int gn_prepare(pba_engine* e) {
   PBA_HIP(G.status.resize(1));
   const int red_pose = (nf + kBlockThreads - 1) / kBlockThreads;
   const int red_pt = (ngp + kBlockThreads - 1) / kBlockThreads;
-  G.red_slots = red_pose + red_pt + 1024;  // update partials, then (step_and_candidate_cost) the cost partials
+  // update partials, then the candidate cost's workgroup partials (≤ one per 16 blocks: launch_cost_only's grids)
+  G.red_slots = red_pose + red_pt + std::max(1024, nb / 16 + 2);
   PBA_HIP(G.red.resize((size_t)2 * G.red_slots));
   PBA_HIP(G.red_h.resize(2 * G.red_slots));
   PBA_HIP(G.lm.resize(kLmFields));
@@ -2279,10 +2278,10 @@ int lm_trial(pba_engine* e, double lambda, double min_rel, double ftol, double s
   int gp = 0, gq = 0;
   enqueue_updates(e, lambda, G.fixed.p, &gp, &gq);
   if (ev) PBA_HIP(hipEventRecord(ev[1], e->stream));
-  if (int rc = launch_cost_only(e, G.pairs_new.p, G.rho_new.p)) return rc;  // pairs_new from update_kernel
-  const int gc = std::min(1024, (e->n_blocks + kBlockThreads - 1) / kBlockThreads);
-  cost_reduce_kernel<<<gc, kBlockThreads, 0, e->stream>>>(e->cost.p, e->valid.p, e->n_blocks, G.red.p + 2 * (gp + gq));
-  lm_decide_kernel<<<1, 256, 0, e->stream>>>(G.red.p, gp, gq, gc, G.status.p, lambda, min_rel, ftol, G.lm.p,
+  // candidate cost: the residual-only launch also writes one (Σ cost, Σ valid) slot per workgroup (no reduction launch)
+  int gc = 0;
+  if (int rc = launch_cost_only(e, G.pairs_new.p, G.rho_new.p, G.red.p + 2 * (gp + gq), &gc)) return rc;
+  lm_decide_kernel<<<1, kDecideThreads, 0, e->stream>>>(G.red.p, gp, gq, gc, G.status.p, lambda, min_rel, ftol, G.lm.p,
                                              G.lm_host_d, seq);
   PBA_HIP(hipGetLastError());
   if (ev) PBA_HIP(hipEventRecord(ev[2], e->stream));

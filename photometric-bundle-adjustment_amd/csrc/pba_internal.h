@@ -135,6 +135,7 @@ struct KernelArgs {
   int n_blocks;
   int P;
   float huber;
+  double* wg_red;  // residual-only launches of the LM loop: per-workgroup (Σ cost, Σ valid) at slot logical_tile()
   float pattern[2 * PBA_MAX_PATTERN];
 };
 
@@ -145,6 +146,25 @@ __device__ __forceinline__ int logical_tile() {
   const int xcd = b & 7, slot = b >> 3;
   const int q = n >> 3, rem = n & 7;
   return xcd * q + min(xcd, rem) + slot;
+}
+
+// Σ over the workgroup of two per-lane values in a fixed order (xor butterflies in each wave, then the waves in
+// order): bitwise reproducible.  Every thread of the workgroup must call it; thread 0 writes out[0..1].
+__device__ __forceinline__ void wg_reduce2(double a, double b, double* out) {
+  __shared__ double sa[16], sb[16];
+  for (int m = 32; m >= 1; m >>= 1) {
+    a += __shfl_xor(a, m, 64);
+    b += __shfl_xor(b, m, 64);
+  }
+  const int w = threadIdx.x / 64, l = threadIdx.x % 64;
+  if (l == 0) { sa[w] = a; sb[w] = b; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double x = 0, y = 0;
+    for (int i = 0; i < (int)(blockDim.x / 64); ++i) { x += sa[i]; y += sb[i]; }
+    out[0] = x;
+    out[1] = y;
+  }
 }
 
 // Huber loss (loss_function.cc:48-62): cost = ½ρ(s); Corrector weight ρ'(s) (corrector.cc:42-110 — ρ'' ≤ 0
@@ -538,6 +558,7 @@ struct pba_engine {
   bool pairs_fresh = false;          // pairs hold T_th of the current poses (pba_set_state_device forms them)
   bool evaluated = false;
   bool timing = false;
+  int last_grid = 0;                 // workgroups of the last evaluation launch (launch_mode)
   std::vector<hipEvent_t> ev_pool;   // start/stop pairs, reused
   int level = 0;                     // active pyramid level (its buffers are swapped into the fields above)
   std::vector<std::unique_ptr<pba::detail::LevelData>> pyr;  // [1, n_levels); [0] unused
@@ -562,7 +583,9 @@ KernelArgs make_kernel_args(pba_engine* e, const PairRec* pairs, const double* r
 void launch_pairs(pba_engine* e, const double* poses, PairRec* pairs);
 
 // Residual-only evaluation writing only per-block costs/validity (state given by pairs/rho).
-int launch_cost_only(pba_engine* e, const PairRec* pairs, const double* rho);
+// wg_red (optional): each workgroup also writes its (Σ cost, Σ valid) there; *n_slots = the launch's workgroups.
+int launch_cost_only(pba_engine* e, const PairRec* pairs, const double* rho, double* wg_red = nullptr,
+                     int* n_slots = nullptr);
 
 // Pyramid (pba_pyramid.hip): back to level 0 and drop the levels; I_h,k sampled from the active level's host images.
 void reset_pyramid(pba_engine* e);
