@@ -85,17 +85,34 @@ static_assert(pa(57) == 6 && pb(57) == 6 && pa(77) == 11 && pb(77) == 11, "table
 static_assert(pa(21) == 0 && pb(21) == 6 && pa(56) == 5 && pb(56) == 11, "table");
 
 // LM decision record kept on the device by the single-GPU loop (lm_decide_kernel).
-enum : int { kLmCost = 0, kLmCostNew = 1, kLmModel = 2, kLmRel = 3, kLmAccept = 4, kLmStatus = 5, kLmConverged = 6, kLmFields = 7 };
+// The trial's outcome, then the trust-region state the next trial runs with (λ = 1/radius, read by the kernels), the
+// done flag (1 converged, 2 radius underflow: every later kernel of the solve returns at once) and the index of the
+// linearisation buffer set holding the current state's normal-equation pieces (flipped on acceptance).
+enum : int {
+  kLmCost = 0, kLmCostNew = 1, kLmModel = 2, kLmRel = 3, kLmAccept = 4, kLmStatus = 5, kLmConverged = 6,
+  kLmLambda = 7, kLmRadius = 8, kLmFactor = 9, kLmDone = 10, kLmSet = 11, kLmFields = 12
+};
+// device LM record helpers (lm == nullptr: host-driven step, λ passed as an argument, buffer set 0)
+__device__ __forceinline__ bool lm_done(const double* lm) { return lm && lm[kLmDone] != 0.0; }
+__device__ __forceinline__ double lm_lambda(const double* lm, double lambda) { return lm ? lm[kLmLambda] : lambda; }
+template <class T>
+__device__ __forceinline__ T* lm_set(const double* lm, T* s0, T* s1, bool spare = false) {
+  if (!lm) return s0;
+  return ((lm[kLmSet] != 0.0) != spare) ? s1 : s0;
+}
 
 struct LinArgs {
   const int* lin_block;     // linearise order → block (GN order regrouped by target within each host)
+  float* blk_schur1;        // the second buffer set (device LM loop: the candidate's linearisation goes to the spare)
+  float* part_lin1;
+  double* wg_red;           // per-chunk (Σ cost, Σ valid) slots, or nullptr
   const int* lin_gpos;      // linearise order → GN position (blk_schur index)
   const int4* chunk_desc;   // first linearise position, count, n_targets, partial offset (floats)
   const uint8_t* blk_lt;    // linearise order → local target slot in its chunk
   float* blk_schur;
   float* part_lin;
   int n_chunks;
-  const double* gate;       // LM decision record (lm_decide_kernel): run only if it accepted; nullptr = always
+  const double* lm;         // device LM record: skip when the solve is done, write the spare set; nullptr: set 0
 };
 
 // ------------------------------------------------------------------------------------------------
@@ -149,7 +166,9 @@ void linearize_kernel(const KernelArgs a, const LinArgs g) {
   __shared__ int s_wlo[NW], s_wn[NW];
   const int chunk = logical_tile();
   if (chunk >= g.n_chunks) return;
-  if (g.gate && g.gate[kLmAccept] == 0.0) return;  // speculative linearisation of a rejected step: nothing to do
+  if (lm_done(g.lm)) return;
+  float* const blk_schur = lm_set(g.lm, g.blk_schur, g.blk_schur1, true);
+  float* const part_lin = lm_set(g.lm, g.part_lin, g.part_lin1, true);
   const int4 d = g.chunk_desc[chunk];
   const int first = d.x, count = d.y, n_t = d.z, poff = d.w;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -177,9 +196,10 @@ void linearize_kernel(const KernelArgs a, const LinArgs g) {
   const int ok = group_all<LPB>(act ? row.ok : 1);
   const float s = group_sum<LPB>(act && ok ? row.r * row.r : 0.0f);
   const float w = ok ? huber_weight(s, a.huber) : 0.0f;
+  const float bcost = ok ? huber_cost(s, a.huber) : 0.0f;
   if (live && k == 0) {
     a.valid[blk] = (uint8_t)ok;
-    a.cost[blk] = ok ? huber_cost(s, a.huber) : 0.0f;
+    a.cost[blk] = bcost;
   }
   // weighted row x̃ = √w · x  → products carry w (Ceres Corrector with ρ'' ≤ 0: J̃ = √ρ' J, r̃ = √ρ' r)
   const float sw = (act && ok) ? sqrtf(w) : 0.0f;  // rows outside the domain / of dead lanes are all zero
@@ -229,7 +249,7 @@ void linearize_kernel(const KernelArgs a, const LinArgs g) {
         for (int st = 0; st < SPB; ++st)
           acc = __builtin_amdgcn_mfma_f32_16x16x4f32(op[b * SPB + st], op[b * SPB + st], acc, 0, 0, 0);
         const int gpb = __builtin_amdgcn_readlane(gpos, b * LPB);
-        if (pc >= 0) g.blk_schur[(long long)gpb * 16 + pq] = acc[0];
+        if (pc >= 0) blk_schur[(long long)gpb * 16 + pq] = acc[0];
         const int ltb = __builtin_amdgcn_readlane(lt, b * LPB);
         if (ltb != cur) {
           flush(tacc, cur - lo);
@@ -274,8 +294,9 @@ void linearize_kernel(const KernelArgs a, const LinArgs g) {
         acc += sset(w, j - wl, v);
       }
     }
-    g.part_lin[(long long)poff + o] = acc;
+    part_lin[(long long)poff + o] = acc;
   }
+  if (g.wg_red) wg_reduce2(live && k == 0 ? (double)bcost : 0.0, live && k == 0 && ok ? 1.0 : 0.0, g.wg_red + 2 * chunk);
 }
 
 struct SchurArgs {
@@ -286,9 +307,11 @@ struct SchurArgs {
   const int* pt_nblk;
   const uint8_t* blk_lv;
   const float* blk_schur;
+  const float* blk_schur1;  // buffer set 1 (device LM loop)
   double* part_schur;
   double* pt_data;        // per GN point [H_ρρ, g_ρ, W_h(6)] (undamped)
   int n_chunks;
+  const double* lm;       // device LM record (λ, done, set), or nullptr
 };
 
 // ------------------------------------------------------------------------------------------------
@@ -298,7 +321,9 @@ __global__ __launch_bounds__(kBlockThreads) void schur_kernel(const SchurArgs g,
   extern __shared__ __attribute__((aligned(16))) float W_dyn[];  // W [points × local poses][6] (gn_prepare: schur_lds)
   __shared__ double s_inv[SCHUR_PTS], s_gl[SCHUR_PTS];
   const int c = blockIdx.x;
-  if (c >= g.n_chunks) return;
+  if (c >= g.n_chunks || lm_done(g.lm)) return;
+  lambda = lm_lambda(g.lm, lambda);
+  const float* const blk_schur = lm_set(g.lm, g.blk_schur, g.blk_schur1);
   const int4 d = g.desc[c];
   const int first = d.x, npt = d.y, nv = d.z, poff = d.w;
   const int4 ax = g.aux[c];
@@ -321,7 +346,7 @@ __global__ __launch_bounds__(kBlockThreads) void schur_kernel(const SchurArgs g,
 #pragma unroll
         for (int u = 0; u < kBatch; ++u) {
           const int b = min(b0 + u, fb + nb - 1);
-          v[u] = reinterpret_cast<const float4*>(g.blk_schur + (long long)b * 16)[q];
+          v[u] = reinterpret_cast<const float4*>(blk_schur + (long long)b * 16)[q];
           lv[u] = q < 2 ? 0 : g.blk_lv[b];
         }
 #pragma unroll
@@ -404,6 +429,8 @@ __global__ __launch_bounds__(kBlockThreads) void schur_kernel(const SchurArgs g,
 
 struct AsmArgs {
   const float* part_lin;
+  const float* part_lin1;  // buffer set 1 (device LM loop)
+  const double* lm;        // device LM record (λ, done, set), or nullptr
   const double* part_schur;
   const int* sky_cptr;
   const int2* sky_contrib;
@@ -456,7 +483,10 @@ __device__ __forceinline__ void contrib_sums(const AsmArgs& a, const int2* __res
 // ------------------------------------------------------------------------------------------------
 // assemble_kernel: S (skyline, lower blocks) and g from the partial slots
 // ------------------------------------------------------------------------------------------------
-__global__ void assemble_kernel(const AsmArgs a, double lambda) {
+__global__ void assemble_kernel(AsmArgs a, double lambda) {
+  if (lm_done(a.lm)) return;
+  lambda = lm_lambda(a.lm, lambda);
+  a.part_lin = lm_set(a.lm, a.part_lin, a.part_lin1);
   const int tid = blockIdx.x * blockDim.x + threadIdx.x;
   const int nS = a.n_sky * 36;
   if (tid < nS) {
@@ -607,6 +637,7 @@ struct SolveArgs {
   double* x;
   int* status;
   int N;
+  const double* gate;
 };
 
 __device__ __forceinline__ long long sky_off(const SolveArgs& a, int i, int j) {  // block (i, j), j ≥ first(i)
@@ -614,6 +645,7 @@ __device__ __forceinline__ long long sky_off(const SolveArgs& a, int i, int j) {
 }
 
 __global__ __launch_bounds__(256) void skyline_solve_kernel(const SolveArgs a) {
+  if (lm_done(a.gate)) return;
   __shared__ double sA[36], sL[36], sLi[36];
   __shared__ int s_fail;
   const int tid = threadIdx.x;
@@ -736,6 +768,7 @@ struct BandArgs {
   double* x;            // the step δ_poses
   int* status;
   int N;
+  const double* gate;
 };
 
 // rsqrt_nr (pba_device.h): hardware v_rsq_f64 seed + two Newton steps — the pivot is on the solver's
@@ -767,6 +800,7 @@ __device__ inline bool chol6_rcp(double* A, double* invd) {  // in place, lower;
 
 template <int B>
 __global__ __launch_bounds__(256) void band_solve_kernel(const BandArgs a) {
+  if (lm_done(a.gate)) return;
   constexpr int W = B + 1;
   constexpr int ROWF = W * 36;
   constexpr int ROWG = ROWF + 6;
@@ -983,6 +1017,7 @@ struct CrLevel {
   double* X;   // ⌊n/2⌋ × m × (2m+1)
   double* x;   // n × m
   int n;
+  const double* gate;  // device LM record: nothing to do once the solve is done (nullptr: always run)
 };
 
 template <int M>
@@ -990,6 +1025,7 @@ __global__ __launch_bounds__(256) void cr_build_kernel(const double* __restrict_
                                                        int* __restrict__ status) {
   // one thread per element of D_I, U_I and b_I of level 0 (rows ≥ N are identity padding); the solve's failure flag
   // is cleared here (the levels only ever set it), which saves a memset launch per solve
+  if (lm_done(L0.gate)) return;
   const long long tid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (tid == 0) *status = 0;
   const long long nD = (long long)L0.n * M * M;
@@ -1087,6 +1123,7 @@ constexpr size_t cr_level_lds() { return sizeof(double) * (2 * M * M + 2 * M * (
 
 template <int M>
 __global__ __launch_bounds__(2 * kCrOddThreads<M>) void cr_level_kernel(CrLevel L, CrLevel Ln, int* status) {
+  if (lm_done(L.gate)) return;
   constexpr int NC = 2 * M + 1, W = M + NC, T = kCrOddThreads<M>;
   __shared__ __attribute__((aligned(16))) double colk[2][2][2][M];
   extern __shared__ double smem[];
@@ -1231,6 +1268,7 @@ constexpr size_t cr_level_wave_lds() { return sizeof(double) * (3 * M * M + M + 
 template <int M>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void cr_level_wave_kernel(
     CrLevel L, CrLevel Ln, int* status) {
+  if (lm_done(L.gate)) return;
   static_assert(2 * M + 1 <= 64, "one wave per elimination");
   constexpr int NC = 2 * M + 1;
   __shared__ __attribute__((aligned(16))) double piv[3][M * kCrPivot];
@@ -1329,6 +1367,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 // The root super-row on one wave (lane 2M carries b; the coupling lanes are empty).
 template <int M>
 __global__ __launch_bounds__(64) void cr_root_wave_kernel(CrLevel L, int* status) {
+  if (lm_done(L.gate)) return;
   __shared__ __attribute__((aligned(16))) double piv[M * kCrPivot];
   double a[M];
   const int lane = threadIdx.x;
@@ -1345,6 +1384,7 @@ __global__ __launch_bounds__(64) void cr_root_wave_kernel(CrLevel L, int* status
 // The root super-row (the last level): x = D⁻¹ b.
 template <int M>
 __global__ __launch_bounds__(kCrOddThreads<M>) void cr_root_kernel(CrLevel L, int* status) {
+  if (lm_done(L.gate)) return;
   constexpr int W = 3 * M + 1;
   __shared__ __attribute__((aligned(16))) double colk[2][2][M];
   double a[M];
@@ -1394,6 +1434,7 @@ __device__ __forceinline__ void cr_back_row(const CrLevel& L, const double* __re
 // one (large) level, one lane per output
 template <int M>
 __global__ void cr_back_kernel(CrLevel L, const double* __restrict__ xn, double* __restrict__ out, int lim) {
+  if (lm_done(L.gate)) return;
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t < lim) cr_back_row<M>(L, xn, out, t);
 }
@@ -1402,6 +1443,7 @@ __global__ void cr_back_kernel(CrLevel L, const double* __restrict__ xn, double*
 template <int M>
 __global__ __launch_bounds__(1024) void cr_back_tail_kernel(const CrLevels C, int hi, int lo, double* __restrict__ step,
                                                             int N) {
+  if (lm_done(C.lv[0].gate)) return;
   for (int l = hi; l >= lo; --l) {
     const CrLevel& L = C.lv[l];
     double* out = l == 0 ? step : L.x;
@@ -1494,6 +1536,7 @@ struct PointUpdateArgs {
   const int* pt_host;
   const int* gn_target;
   const float* blk_schur;
+  const float* blk_schur1;  // buffer set 1 (device LM loop)
   const double* x;
   const uint8_t* fixed;
   const double* rho;
@@ -1515,10 +1558,24 @@ __device__ __forceinline__ void point_update_block(const PointUpdateArgs& a, dou
     const int h = a.pt_host[p];
     double s = gl;
     for (int i = 0; i < 6; ++i) s += pd[2 + i] * a.x[6 * h + i];
-    for (int b = a.pt_first[p]; b < a.pt_first[p] + a.pt_nblk[p]; ++b) {
-      const int t = a.gn_target[b];
-      const float* q = a.blk_schur + (long long)b * 16;
-      for (int i = 0; i < 6; ++i) s += (double)q[8 + i] * a.x[6 * t + i];
+    const int fb = a.pt_first[p], nb = a.pt_nblk[p];
+    constexpr int kBatch = 4;  // a batch's loads issued together, then summed in block order
+    for (int b0 = fb; b0 < fb + nb; b0 += kBatch) {
+      float w[kBatch][6];
+      int t[kBatch];
+#pragma unroll
+      for (int u = 0; u < kBatch; ++u) {
+        const int b = min(b0 + u, fb + nb - 1);
+        t[u] = a.gn_target[b];
+        const float* q = a.blk_schur + (long long)b * 16 + 8;
+#pragma unroll
+        for (int i = 0; i < 6; ++i) w[u][i] = q[i];
+      }
+#pragma unroll
+      for (int u = 0; u < kBatch; ++u) {
+        if (b0 + u >= fb + nb) break;
+        for (int i = 0; i < 6; ++i) s += (double)w[u][i] * a.x[6 * t[u] + i];
+      }
     }
     const double dr = Hd > 0.0 ? -s / Hd : 0.0;
     const int o = a.pt_orig[p];
@@ -1544,8 +1601,12 @@ struct PairUpdateArgs {
 // in the same fixed order as two separate launches), and the rest form the candidate pair table straight from
 // T_h·exp(δ_h), T_t·exp(δ_t) — candidate_pose, the same arithmetic as the pose workgroups, so the pairs equal
 // form_pair(poses_new) bit for bit — which saves the separate pair launch before the candidate cost.
-__global__ __launch_bounds__(kBlockThreads) void update_kernel(const PoseUpdateArgs pa, const PointUpdateArgs qa,
-                                                               const PairUpdateArgs ra, int gp, int gq, double lambda) {
+__global__ __launch_bounds__(kBlockThreads) void update_kernel(const PoseUpdateArgs pa, PointUpdateArgs qa,
+                                                               const PairUpdateArgs ra, int gp, int gq, double lambda,
+                                                               const double* __restrict__ lm) {
+  if (lm_done(lm)) return;
+  lambda = lm_lambda(lm, lambda);
+  qa.blk_schur = lm_set(lm, qa.blk_schur, qa.blk_schur1);
   const int b = blockIdx.x;
   if (b < gp) {
     pose_update_block(pa, b);
@@ -1586,9 +1647,11 @@ __global__ __launch_bounds__(kBlockThreads) void cost_reduce_kernel(const float*
 // and a stream event (each of which left the GPU idle ~6 µs).
 constexpr int kDecideThreads = 1024;
 __global__ __launch_bounds__(kDecideThreads) void lm_decide_kernel(const double* __restrict__ red, int gp, int gq, int gc,
-                                                        const int* __restrict__ status, double lambda, double min_rel,
+                                                        const int* __restrict__ status, double min_rel,
                                                         double ftol, double* __restrict__ lm,
                                                         volatile double* __restrict__ host_rec, double seq) {
+  if (lm_done(lm)) return;  // a trial enqueued ahead of the one that ended the solve
+  const double lambda = lm[kLmLambda];
   constexpr int N = kDecideThreads, U = 4;
   __shared__ double part[5][N];
   double v[5] = {0, 0, 0, 0, 0};  // dg, dD, qg, qD, c
@@ -1636,15 +1699,30 @@ __global__ __launch_bounds__(kDecideThreads) void lm_decide_kernel(const double*
   lm[kLmRel] = rel;
   lm[kLmAccept] = accept ? 1.0 : 0.0;
   lm[kLmStatus] = (double)st;
-  if (accept) lm[kLmCost] = c;
+  if (accept) {
+    lm[kLmCost] = c;
+    lm[kLmSet] = 1.0 - lm[kLmSet];  // the candidate's linearisation (the spare set) is now the current one
+  }
+  // trust region for the next trial (levenberg_marquardt_strategy.cc:125-150, trust_region_minimizer.cc):
+  // failure: radius /= factor, factor *= 2; success: radius /= max(1/3, 1 − (2ρ − 1)³), factor = 2
+  double radius = lm[kLmRadius], factor = lm[kLmFactor], done = 0.0;
+  if (converged) {
+    done = 1.0;
+  } else if (!accept) {
+    radius /= factor;
+    factor *= 2.0;
+    if (radius < 1e-32) done = 2.0;
+  } else {
+    const double q = 2.0 * rel - 1.0;
+    radius = radius / fmax(1.0 / 3.0, 1.0 - q * q * q);
+    factor = 2.0;
+  }
+  lm[kLmRadius] = radius;
+  lm[kLmFactor] = factor;
+  lm[kLmLambda] = 1.0 / radius;
+  lm[kLmDone] = done;
   if (host_rec) {
-    host_rec[kLmCost] = accept ? c : cost;
-    host_rec[kLmCostNew] = c;
-    host_rec[kLmModel] = model;
-    host_rec[kLmRel] = rel;
-    host_rec[kLmAccept] = accept ? 1.0 : 0.0;
-    host_rec[kLmStatus] = (double)st;
-    host_rec[kLmConverged] = converged ? 1.0 : 0.0;
+    for (int i = 0; i < kLmFields; ++i) host_rec[i] = lm[i];
     __threadfence_system();
     host_rec[kLmFields] = seq;
   }
@@ -1656,7 +1734,7 @@ __global__ __launch_bounds__(kDecideThreads) void lm_decide_kernel(const double*
 __global__ void lm_accept_kernel(const double* __restrict__ lm, const double* __restrict__ poses_new,
                                  const double* __restrict__ rho_new, const int* __restrict__ pt_orig,
                                  double* __restrict__ poses, double* __restrict__ rho, int n_pose_d, int n_gn_points) {
-  if (lm && lm[kLmAccept] == 0.0) return;
+  if (lm && (lm[kLmAccept] == 0.0 || lm[kLmDone] != 0.0)) return;
   const int n = max(n_pose_d, n_gn_points);
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
     if (i < n_pose_d) poses[i] = poses_new[i];
@@ -1928,6 +2006,8 @@ int gn_prepare(pba_engine* e) {
   PBA_HIP(G.blk_lt.upload(blt, st));
   PBA_HIP(G.blk_schur.resize((size_t)nb * 16));
   PBA_HIP(G.part_lin.resize(std::max<size_t>(G.lin_floats, 1)));
+  PBA_HIP(G.blk_schur1.resize((size_t)nb * 16));  // the device LM loop's second linearisation set
+  PBA_HIP(G.part_lin1.resize(std::max<size_t>(G.lin_floats, 1)));
   PBA_HIP(G.pt_first.upload(pfirst, st));
   PBA_HIP(G.pt_nblk.upload(pnblk, st));
   PBA_HIP(G.pt_orig.upload(porig, st));
@@ -1980,7 +2060,7 @@ int gn_prepare(pba_engine* e) {
   const int red_pose = (nf + kBlockThreads - 1) / kBlockThreads;
   const int red_pt = (ngp + kBlockThreads - 1) / kBlockThreads;
   // update partials, then the candidate cost's workgroup partials (≤ one per 16 blocks: launch_cost_only's grids)
-  G.red_slots = red_pose + red_pt + std::max(1024, nb / 16 + 2);
+  G.red_slots = red_pose + red_pt + std::max({1024, nb / 16 + 2, G.n_chunks});
   PBA_HIP(G.red.resize((size_t)2 * G.red_slots));
   PBA_HIP(G.red_h.resize(2 * G.red_slots));
   PBA_HIP(G.lm.resize(kLmFields));
@@ -2066,16 +2146,19 @@ int total_cost(pba_engine* e, double* cost, int* n_valid) {
   return PBA_OK;
 }
 
-// gate: the device LM decision record — the kernels then run only if it accepted (speculatively enqueued).
-// pairs: the relative poses of the state to linearise at (nullptr: formed here from the engine's poses).
-int linearize(pba_engine* e, double* cost, const double* gate = nullptr, const PairRec* pairs = nullptr) {
+// Linearisation at the engine's state (pairs == nullptr: formed here), or — the device LM loop — at the candidate:
+// lm = the device LM record (the pieces go to the spare buffer set, nothing runs once the solve is done), pairs / rho
+// the candidate's, and wg_red the slots of the per-chunk cost partials the decision sums.
+int linearize(pba_engine* e, double* cost, const double* lm = nullptr, const PairRec* pairs = nullptr,
+              const double* rho = nullptr, double* wg_red = nullptr) {
   GnData& G = e->gn;
   if (!pairs) {
     launch_pairs(e, e->poses.p, e->pairs.p);
     pairs = e->pairs.p;
   }
-  const KernelArgs ka = make_kernel_args(e, pairs, e->rho.p);
-  LinArgs la{G.lin_block.p, G.lin_gpos.p, G.chunk_desc.p, G.blk_lt.p, G.blk_schur.p, G.part_lin.p, G.n_chunks, gate};
+  const KernelArgs ka = make_kernel_args(e, pairs, rho ? rho : e->rho.p);
+  LinArgs la{G.lin_block.p, G.blk_schur1.p, G.part_lin1.p, wg_red, G.lin_gpos.p, G.chunk_desc.p, G.blk_lt.p,
+             G.blk_schur.p, G.part_lin.p, G.n_chunks, lm};
   if (e->opt.residual_kind == PBA_RESIDUAL_PHOTOMETRIC) launch_linearize_photometric(e, ka, la);
   else launch_linearize_geometric(e, ka, la);
   PBA_HIP(hipGetLastError());
@@ -2084,14 +2167,14 @@ int linearize(pba_engine* e, double* cost, const double* gate = nullptr, const P
   return PBA_OK;
 }
 
-CrLevel cr_level(GnData& G, int l) {
+CrLevel cr_level(GnData& G, int l, const double* lm = nullptr) {
   const CrLevelHost& h = G.cr_levels[l];
   double* base = G.cr_buf.p;
-  return CrLevel{base + h.D, base + h.U, base + h.b, base + h.X, base + h.x, h.n};
+  return CrLevel{base + h.D, base + h.U, base + h.b, base + h.X, base + h.x, h.n, lm};
 }
 
 template <int M>
-void cr_solve(pba_engine* e) {
+void cr_solve(pba_engine* e, const double* lm) {
   GnData& G = e->gn;
   if (cr_level_lds<M>() > 65536) {  // above the default dynamic-LDS limit (gfx950 has 160 KiB per CU)
     // the attribute is per device: set it on every solve (cheap) rather than once per process
@@ -2099,26 +2182,26 @@ void cr_solve(pba_engine* e) {
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)cr_level_lds<M>());
   }
   const int nl = (int)G.cr_levels.size();
-  CrLevel L0 = cr_level(G, 0);
+  CrLevel L0 = cr_level(G, 0, lm);
   const long long nthreads = (long long)L0.n * M * M + (long long)L0.n * M;
   cr_build_kernel<M><<<(unsigned)((nthreads + 255) / 256), 256, 0, e->stream>>>(G.Sband.p, L0, e->n_frames, G.band_kernel,
                                                                                 G.status.p);
   for (int l = 0; l + 1 < nl; ++l) {  // one fused launch per level (odd eliminations + even rebuild)
-    CrLevel L = cr_level(G, l), Ln = cr_level(G, l + 1);
+    CrLevel L = cr_level(G, l, lm), Ln = cr_level(G, l + 1, lm);
     if constexpr (2 * M + 1 <= 64)
       cr_level_wave_kernel<M><<<(L.n + 1) / 2, 256, cr_level_wave_lds<M>(), e->stream>>>(L, Ln, G.status.p);
     else
       cr_level_kernel<M><<<(L.n + 1) / 2, 2 * kCrOddThreads<M>, cr_level_lds<M>(), e->stream>>>(L, Ln, G.status.p);
   }
-  if constexpr (2 * M + 1 <= 64) cr_root_wave_kernel<M><<<1, 64, 0, e->stream>>>(cr_level(G, nl - 1), G.status.p);
-  else cr_root_kernel<M><<<1, kCrOddThreads<M>, 0, e->stream>>>(cr_level(G, nl - 1), G.status.p);
+  if constexpr (2 * M + 1 <= 64) cr_root_wave_kernel<M><<<1, 64, 0, e->stream>>>(cr_level(G, nl - 1, lm), G.status.p);
+  else cr_root_kernel<M><<<1, kCrOddThreads<M>, 0, e->stream>>>(cr_level(G, nl - 1, lm), G.status.p);
   if (nl == 1) {  // a single super-row: the root's x is the step
     (void)hipMemcpyAsync(G.x.p, L0.x, sizeof(double) * 6 * e->n_frames, hipMemcpyDeviceToDevice, e->stream);
     return;
   }
   CrLevels C{};
   C.nl = nl;
-  for (int l = 0; l < nl; ++l) C.lv[l] = cr_level(G, l);
+  for (int l = 0; l < nl; ++l) C.lv[l] = cr_level(G, l, lm);
   int lo = nl - 2;  // the tail: levels with at most kCrTailRows super-rows
   while (lo > 0 && C.lv[lo - 1].n <= kCrTailRows) --lo;
   cr_back_tail_kernel<M><<<1, 1024, 0, e->stream>>>(C, nl - 2, lo, G.x.p, e->n_frames);
@@ -2131,7 +2214,8 @@ void cr_solve(pba_engine* e) {
 // After a solve into G.x: solver status, candidate poses/points, and the two parts of the LM model decrease
 // L(0) − L(δ) = −gᵀδ − ½δᵀHδ = ½(λ δᵀDδ − gᵀδ)  (since (H + λD)δ = −g): pose part and point part.
 // Candidate poses/points and the model-decrease partials into reduction slots [0, gp + gq) of G.red.
-void enqueue_updates(pba_engine* e, double lambda, const uint8_t* fixed, int* gp_out, int* gq_out) {
+void enqueue_updates(pba_engine* e, double lambda, const uint8_t* fixed, int* gp_out, int* gq_out,
+                     const double* lm = nullptr) {
   GnData& G = e->gn;
   const int nf = e->n_frames;
   const int gp = (nf + kBlockThreads - 1) / kBlockThreads;
@@ -2140,9 +2224,10 @@ void enqueue_updates(pba_engine* e, double lambda, const uint8_t* fixed, int* gp
   PoseUpdateArgs pa{e->poses.p, G.x.p, G.g_dir.p, G.Ddiag.p, fixed, G.poses_new.p, G.red.p, nf};
   // point workgroup q writes reduction slot gp + q, as the separate launches did
   PointUpdateArgs qa{G.pt_data.p, G.pt_first.p, G.pt_nblk.p, G.pt_orig.p, G.pt_host.p, G.gn_target.p,
-                     G.blk_schur.p, G.x.p, fixed, e->rho.p, G.rho_new.p, G.drho.p, G.red.p, G.n_gn_points};
+                     G.blk_schur.p, G.blk_schur1.p, G.x.p, fixed, e->rho.p, G.rho_new.p, G.drho.p, G.red.p,
+                     G.n_gn_points};
   PairUpdateArgs ra{e->pair_host.p, e->pair_target.p, e->frame_cam.p, e->intr_d.p, G.pairs_new.p, e->n_pairs};
-  update_kernel<<<gp + gq + gr, kBlockThreads, 0, e->stream>>>(pa, qa, ra, gp, gq, lambda);
+  update_kernel<<<gp + gq + gr, kBlockThreads, 0, e->stream>>>(pa, qa, ra, gp, gq, lambda, lm);
   G.pairs_new_fresh = true;
   *gp_out = gp;
   *gq_out = gq;
@@ -2175,14 +2260,14 @@ int finish_step(pba_engine* e, double lambda, const uint8_t* fixed, double* mode
 }
 
 // Band solvers on G.Sband (block cyclic reduction for K ≤ 8, LDS-window band Cholesky for K = 16).
-int band_solve(pba_engine* e) {
+int band_solve(pba_engine* e, const double* lm = nullptr) {
   GnData& G = e->gn;
   const int nf = e->n_frames;
   if (G.solver == SOLVER_CR) {
-    if (G.band_kernel == 4) cr_solve<24>(e);
-    else cr_solve<48>(e);
+    if (G.band_kernel == 4) cr_solve<24>(e, lm);
+    else cr_solve<48>(e, lm);
   } else {
-    BandArgs ba{G.Sband.p, G.Lband.p, G.x.p, G.status.p, nf};
+    BandArgs ba{G.Sband.p, G.Lband.p, G.x.p, G.status.p, nf, lm};
     if (G.band_kernel == 4) band_solve_kernel<4><<<1, 256, 0, e->stream>>>(ba);
     else if (G.band_kernel == 8) band_solve_kernel<8><<<1, 256, 0, e->stream>>>(ba);
     else band_solve_kernel<16><<<1, 256, 0, e->stream>>>(ba);
@@ -2199,15 +2284,16 @@ void schur_lds_limit(const GnData& G) {
 }
 
 // Schur complement for λ, assembly and reduced-system solve into G.x (enqueued only).
-int enqueue_solve(pba_engine* e, double lambda) {
+// lm: the device LM record (λ, buffer set, done flag read on the device; lambda unused) or nullptr.
+int enqueue_solve(pba_engine* e, double lambda, const double* lm = nullptr) {
   GnData& G = e->gn;
   const int nf = e->n_frames;
   SchurArgs sa{G.schur_desc.p, G.schur_aux.p, G.schur_pairs.p, G.pt_first.p, G.pt_nblk.p, G.blk_lv.p,
-               G.blk_schur.p, G.part_schur.p, G.pt_data.p, G.n_schur};
+               G.blk_schur.p, G.blk_schur1.p, G.part_schur.p, G.pt_data.p, G.n_schur, lm};
   schur_lds_limit(G);
   schur_kernel<<<G.n_schur, kBlockThreads, G.schur_lds, e->stream>>>(sa, lambda);
-  AsmArgs aa{G.part_lin.p, G.part_schur.p, G.sky_cptr.p, G.sky_contrib.p, G.g_cptr.p, G.g_contrib.p,
-             G.sky_blk_i.p, G.sky_blk_j.p, G.fixed.p, G.S.p, G.g.p, G.g_dir.p, G.Ddiag.p,
+  AsmArgs aa{G.part_lin.p, G.part_lin1.p, lm, G.part_schur.p, G.sky_cptr.p, G.sky_contrib.p, G.g_cptr.p,
+             G.g_contrib.p, G.sky_blk_i.p, G.sky_blk_j.p, G.fixed.p, G.S.p, G.g.p, G.g_dir.p, G.Ddiag.p,
              G.band_kernel ? G.Sband.p : nullptr, G.band_kernel, G.n_sky, nf};
   if (G.sband_dirty && G.band_kernel) {  // a distributed import filled the whole band: clear the off-profile part
     PBA_HIP(hipMemsetAsync(G.Sband.p, 0, sizeof(double) * (size_t)nf * ((G.band_kernel + 1) * 36 + 6), e->stream));
@@ -2216,10 +2302,10 @@ int enqueue_solve(pba_engine* e, double lambda) {
   const int nthreads = G.n_sky * 36 + 6 * nf;
   assemble_kernel<<<(nthreads + 255) / 256, 256, 0, e->stream>>>(aa, lambda);
   if (G.band_kernel) {
-    if (int rc = band_solve(e)) return rc;
+    if (int rc = band_solve(e, lm)) return rc;
   } else {
     PBA_HIP(hipMemcpyAsync(G.L.p, G.S.p, sizeof(double) * 36 * (size_t)G.n_sky, hipMemcpyDeviceToDevice, e->stream));
-    SolveArgs so{G.L.p, G.sky_first.p, G.sky_row.p, G.sky_last.p, G.g.p, G.Linv.p, G.x.p, G.status.p, nf};
+    SolveArgs so{G.L.p, G.sky_first.p, G.sky_row.p, G.sky_last.p, G.g.p, G.Linv.p, G.x.p, G.status.p, nf, lm};
     skyline_solve_kernel<<<1, 256, 0, e->stream>>>(so);
   }
   PBA_HIP(hipGetLastError());
@@ -2263,34 +2349,30 @@ int wait_decision(pba_engine* e, double seq, double* d) {
   return PBA_OK;
 }
 
-// One LM trial on a single GPU, enqueued whole: solve → candidate state, candidate pairs and model-decrease partials →
-// candidate cost → the accept/reject decision on the device (lm_decide_kernel, which also publishes it to the host)
-// → gated accept → gated (speculative) linearisation at the new state, on the candidate's pair table.  The host waits
-// only for the published decision, so an accepted step's linearisation runs while the host computes the next λ.  The
-// candidate is evaluated even when the solve failed (its numbers are then discarded): a garbage state is memory-safe in
-// every evaluation kernel (non-finite or out-of-image projections are clamped / out of domain).  ev (phase timing
-// only, else nullptr): step begin | candidate cost begin | decision end | linearisation begin | end.  d receives the
-// decision record (kLm*).
-int lm_trial(pba_engine* e, double lambda, double min_rel, double ftol, double seq, const hipEvent_t* ev, double* d) {
+// One LM trial on a single GPU, enqueued whole and steered by the device LM record G.lm (λ, buffer set, done):
+// Schur complement + reduced solve → candidate state (poses, ρ, pair table) and model-decrease partials →
+// linearisation AT the candidate into the spare buffer set, whose per-chunk cost partials are the candidate cost →
+// the decision on the device (accept, the next trust radius, done; published to the host) → gated accept.  An accepted
+// step's linearisation is then already done (a rejected one cost a linearisation instead of a residual-only pass), and
+// since every kernel returns at once when the solve is done, the host enqueues the next trial before it has seen this
+// one's decision: no host round trip between trials.  The candidate is evaluated even when the solve failed (its
+// numbers are then discarded): a garbage state is memory-safe in every evaluation kernel.  ev (phase timing only,
+// else nullptr): begin | candidate state | candidate linearisation | decision + accept.
+int lm_trial(pba_engine* e, double min_rel, double ftol, double seq, const hipEvent_t* ev) {
   GnData& G = e->gn;
   if (ev) PBA_HIP(hipEventRecord(ev[0], e->stream));
-  if (int rc = enqueue_solve(e, lambda)) return rc;
+  if (int rc = enqueue_solve(e, 0.0, G.lm.p)) return rc;
   int gp = 0, gq = 0;
-  enqueue_updates(e, lambda, G.fixed.p, &gp, &gq);
+  enqueue_updates(e, 0.0, G.fixed.p, &gp, &gq, G.lm.p);
   if (ev) PBA_HIP(hipEventRecord(ev[1], e->stream));
-  // candidate cost: the residual-only launch also writes one (Σ cost, Σ valid) slot per workgroup (no reduction launch)
-  int gc = 0;
-  if (int rc = launch_cost_only(e, G.pairs_new.p, G.rho_new.p, G.red.p + 2 * (gp + gq), &gc)) return rc;
-  lm_decide_kernel<<<1, kDecideThreads, 0, e->stream>>>(G.red.p, gp, gq, gc, G.status.p, lambda, min_rel, ftol, G.lm.p,
-                                             G.lm_host_d, seq);
-  PBA_HIP(hipGetLastError());
+  if (int rc = linearize(e, nullptr, G.lm.p, G.pairs_new.p, G.rho_new.p, G.red.p + 2 * (gp + gq))) return rc;
   if (ev) PBA_HIP(hipEventRecord(ev[2], e->stream));
+  lm_decide_kernel<<<1, kDecideThreads, 0, e->stream>>>(G.red.p, gp, gq, G.n_chunks, G.status.p, min_rel, ftol, G.lm.p,
+                                                        G.lm_host_d, seq);
+  PBA_HIP(hipGetLastError());
   launch_accept(e, G.lm.p);
   if (ev) PBA_HIP(hipEventRecord(ev[3], e->stream));
-  // an accepted candidate's relative poses are pairs_new (update_kernel): no pair launch at the new state
-  if (int rc = linearize(e, nullptr, G.lm.p, G.pairs_new.p)) return rc;
-  if (ev) PBA_HIP(hipEventRecord(ev[4], e->stream));
-  return wait_decision(e, seq, d);
+  return PBA_OK;
 }
 
 int candidate_cost(pba_engine* e, double* cost) {
@@ -2322,12 +2404,13 @@ int step_export(pba_engine* e, double lambda, int band, double* X) {
   if (int rc = exchange_K(e, band, &K)) return rc;
   const int nf = e->n_frames;
   SchurArgs sa{G.schur_desc.p, G.schur_aux.p, G.schur_pairs.p, G.pt_first.p, G.pt_nblk.p, G.blk_lv.p,
-               G.blk_schur.p, G.part_schur.p, G.pt_data.p, G.n_schur};
+               G.blk_schur.p, G.blk_schur1.p, G.part_schur.p, G.pt_data.p, G.n_schur, nullptr};
   schur_lds_limit(G);
   if (G.n_schur > 0) schur_kernel<<<G.n_schur, kBlockThreads, G.schur_lds, e->stream>>>(sa, lambda);
   PBA_HIP(hipMemsetAsync(X, 0, sizeof(double) * (size_t)nf * ex_row(K), e->stream));
-  AsmArgs aa{G.part_lin.p, G.part_schur.p, G.sky_cptr.p, G.sky_contrib.p, G.g_cptr.p, G.g_contrib.p,
-             G.sky_blk_i.p, G.sky_blk_j.p, G.fixed.p, G.S.p, G.g.p, G.g_dir.p, G.Ddiag.p, nullptr, K, G.n_sky, nf};
+  AsmArgs aa{G.part_lin.p, G.part_lin1.p, nullptr, G.part_schur.p, G.sky_cptr.p, G.sky_contrib.p, G.g_cptr.p,
+             G.g_contrib.p, G.sky_blk_i.p, G.sky_blk_j.p, G.fixed.p, G.S.p, G.g.p, G.g_dir.p, G.Ddiag.p, nullptr, K,
+             G.n_sky, nf};
   const int nthreads = G.n_sky * 36 + 6 * nf;
   export_kernel<<<(nthreads + 255) / 256, 256, 0, e->stream>>>(aa, G.observed.p, X, K);
   PBA_HIP(hipGetLastError());
@@ -2527,48 +2610,53 @@ int lm_loop_single(pba_engine* e, const pba_solver_options* o, pba_solver_summar
   GnData& G = e->gn;
   const pba_solver_options opt = lm_options(o);
   pba_solver_summary s{};
-  struct Events {  // phase timing (pba_set_solver_timing): step | candidate cost | decision; two linearisation pairs
-    hipEvent_t ev[7] = {};
+  struct Events {  // phase timing (pba_set_solver_timing): two sets of 4 (a trial is enqueued ahead)
+    hipEvent_t ev[8] = {};
     ~Events() {
       for (hipEvent_t x : ev)
         if (x) (void)hipEventDestroy(x);
     }
   } events;
   const bool timed = G.phase_timing;
-  hipEvent_t* ev = events.ev;
   if (timed)
-    for (int i = 0; i < 7; ++i) PBA_HIP(hipEventCreate(&ev[i]));
+    for (int i = 0; i < 8; ++i) PBA_HIP(hipEventCreate(&events.ev[i]));
   const double t0 = now_ms();
   double cost = 0.0;
-  if (int rc = linearize(e, &cost)) return rc;
+  if (int rc = linearize(e, &cost)) return rc;  // the initial state's pieces, buffer set 0
   s.linearize_ms += now_ms() - t0;
   s.initial_cost = cost;
-  G.lm_h[kLmCost] = cost;  // the device's current cost
-  G.lm_h[kLmFields] = 0.0;  // no trial published yet
-  PBA_HIP(hipMemcpyAsync(G.lm.p, G.lm_h.data(), sizeof(double), hipMemcpyHostToDevice, e->stream));
-  double radius = opt.initial_trust_region_radius, factor = 2.0;
-  int iter = 0, pending = -1;  // pending: event pair of an accepted step's linearisation not yet timed
+  // the device record: current cost, trust region, nothing done, set 0; no trial published yet
+  for (int i = 0; i <= kLmFields; ++i) G.lm_h[i] = 0.0;
+  G.lm_h[kLmCost] = cost;
+  G.lm_h[kLmRadius] = opt.initial_trust_region_radius;
+  G.lm_h[kLmFactor] = 2.0;
+  G.lm_h[kLmLambda] = 1.0 / opt.initial_trust_region_radius;
+  PBA_HIP(hipMemcpyAsync(G.lm.p, G.lm_h.data(), sizeof(double) * kLmFields, hipMemcpyHostToDevice, e->stream));
+  const int n = std::max(0, opt.max_iterations);
+  auto enqueue = [&](int i) {
+    return lm_trial(e, opt.min_relative_decrease, opt.function_tolerance, (double)(i + 1),
+                    timed ? events.ev + 4 * (i & 1) : nullptr);
+  };
+  if (n > 0)
+    if (int rc = enqueue(0)) return rc;
+  int iter = 0, set = 0;
   s.termination = PBA_TERMINATION_MAX_ITERATIONS;
-  hipEvent_t tev[5] = {};
-  for (; iter < opt.max_iterations; ++iter) {
-    const double lambda = 1.0 / radius;
-    const int lin = 3 + 2 * (iter & 1);
-    if (timed) tev[0] = ev[0], tev[1] = ev[1], tev[2] = ev[2], tev[3] = ev[lin], tev[4] = ev[lin + 1];
+  for (; iter < n; ++iter) {
+    if (iter + 1 < n)
+      if (int rc = enqueue(iter + 1)) return rc;  // ahead of this trial's decision
     double d[kLmFields];
-    if (int rc = lm_trial(e, lambda, opt.min_relative_decrease, opt.function_tolerance, (double)(iter + 1),
-                          timed ? tev : nullptr, d)) return rc;
+    if (int rc = wait_decision(e, (double)(iter + 1), d)) return rc;
+    set = (int)d[kLmSet];
     if (timed) {
+      const hipEvent_t* ev = events.ev + 4 * (iter & 1);
       float ms = 0.0f;
-      PBA_HIP(hipEventSynchronize(ev[2]));
+      PBA_HIP(hipEventSynchronize(ev[3]));
       PBA_HIP(hipEventElapsedTime(&ms, ev[0], ev[1]));
       s.solve_ms += ms;
       PBA_HIP(hipEventElapsedTime(&ms, ev[1], ev[2]));
+      s.linearize_ms += ms;
+      PBA_HIP(hipEventElapsedTime(&ms, ev[2], ev[3]));
       s.cost_ms += ms;
-      if (pending >= 0) {  // the previous accepted step's linearisation ran before this trial's events
-        PBA_HIP(hipEventElapsedTime(&ms, ev[pending], ev[pending + 1]));
-        s.linearize_ms += ms;
-        pending = -1;
-      }
     }
     if (d[kLmConverged] != 0.0) {  // |Δcost| ≤ function_tolerance · cost: stop at the current state
       s.termination = PBA_TERMINATION_CONVERGENCE;
@@ -2577,23 +2665,18 @@ int lm_loop_single(pba_engine* e, const pba_solver_options* o, pba_solver_summar
     }
     if (d[kLmAccept] == 0.0) {  // failed solve, no predicted decrease, or too little actual decrease
       ++s.unsuccessful_steps;
-      radius /= factor;
-      factor *= 2.0;
-      if (radius < 1e-32) { s.termination = PBA_TERMINATION_FAILURE; break; }
+      if (d[kLmDone] != 0.0) { s.termination = PBA_TERMINATION_FAILURE; break; }  // trust radius < 1e-32
       continue;
     }
-    const double rel = d[kLmRel];
     ++s.successful_steps;
-    radius = radius / std::max(1.0 / 3.0, 1.0 - std::pow(2.0 * rel - 1.0, 3));
-    factor = 2.0;
     cost = d[kLmCostNew];
-    pending = lin;
   }
-  PBA_HIP(hipStreamSynchronize(e->stream));  // the last trial's accept / linearisation
-  if (timed && pending >= 0) {
-    float ms = 0.0f;
-    PBA_HIP(hipEventElapsedTime(&ms, ev[pending], ev[pending + 1]));
-    s.linearize_ms += ms;
+  PBA_HIP(hipStreamSynchronize(e->stream));  // the last trial's accept, and the gated trial enqueued after the end
+  if (set == 1) {  // the current state's pieces are in set 1: make it set 0 for the host-driven entry points
+    std::swap(G.blk_schur.p, G.blk_schur1.p);
+    std::swap(G.blk_schur.n, G.blk_schur1.n);
+    std::swap(G.part_lin.p, G.part_lin1.p);
+    std::swap(G.part_lin.n, G.part_lin1.n);
   }
   s.iterations = iter;
   s.final_cost = cost;

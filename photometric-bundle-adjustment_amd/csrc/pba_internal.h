@@ -481,6 +481,7 @@ struct GnData {
   DevBuf<uint8_t> blk_lt;        // linearise position → local target slot in its chunk
   DevBuf<float> blk_schur;       // GN block → 16 floats [Hll gl Wh(6) Wt(6) 0 0]
   DevBuf<float> part_lin;        // linearise chunk partials (fp32)
+  DevBuf<float> blk_schur1, part_lin1;  // second set: the device LM loop linearises each candidate into the spare
   DevBuf<int> pt_first, pt_nblk, pt_orig;  // GN point → first GN block, block count, original point
   DevBuf<int4> schur_desc;       // Schur chunk: first GN point, n points, n local poses, partial offset
   DevBuf<int4> schur_aux;        // Schur chunk: pair list offset, n pairs, first GN block, n blocks
