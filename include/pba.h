@@ -197,8 +197,7 @@ typedef struct pba_solver_summary {
   /* total_ms: host wall clock of the whole solve.  The parts: pba_solve — device time between stream events, only
    * with pba_set_solver_timing(engine, 1) (the events cost the GPU a few µs of idle time each, so they are off by
    * default and the parts are then 0): solve_ms = Schur complement + reduced solve + candidate state, linearize_ms =
-   * the linearisation at each candidate (which is also its cost; plus the initial one), cost_ms = the decision and
-   * the accept; pba_solve_distributed — host wall clock of each phase, collectives included. */
+   * the linearisation at each candidate (which is also its cost; plus the initial one), cost_ms = the decision; pba_solve_distributed — host wall clock of each phase, collectives included. */
   double total_ms, linearize_ms, solve_ms, cost_ms;
 } pba_solver_summary;
 /* per-phase device timing of pba_solve (linearize_ms / solve_ms / cost_ms of the summary); default off */

@@ -32,6 +32,7 @@
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
+#include <limits>
 #include <map>
 #include <numeric>
 #include <string>
@@ -92,14 +93,16 @@ enum : int {
   kLmCost = 0, kLmCostNew = 1, kLmModel = 2, kLmRel = 3, kLmAccept = 4, kLmStatus = 5, kLmConverged = 6,
   kLmLambda = 7, kLmRadius = 8, kLmFactor = 9, kLmDone = 10, kLmSet = 11, kLmFields = 12
 };
-// device LM record helpers (lm == nullptr: host-driven step, λ passed as an argument, buffer set 0)
-__device__ __forceinline__ bool lm_done(const double* lm) { return lm && lm[kLmDone] != 0.0; }
-__device__ __forceinline__ double lm_lambda(const double* lm, double lambda) { return lm ? lm[kLmLambda] : lambda; }
-template <class T>
-__device__ __forceinline__ T* lm_set(const double* lm, T* s0, T* s1, bool spare = false) {
-  if (!lm) return s0;
-  return ((lm[kLmSet] != 0.0) != spare) ? s1 : s0;
+// The kernels always get a record: the device loop's, or — host-driven steps — GnData::lm_idle (not done, set 0, λ NaN
+// = use the kernel's λ argument).  They read it with their first loads, never behind a branch of its own (a gate
+// read before anything else cost the linearisation ~8 µs of serialised scalar round trips).
+struct LmView {
+  double done, set, lambda, accept;
+};
+__device__ __forceinline__ LmView lm_view(const double* lm) {
+  return LmView{lm[kLmDone], lm[kLmSet], lm[kLmLambda], lm[kLmAccept]};
 }
+__device__ __forceinline__ double lm_lambda(const LmView& v, double lambda) { return isnan(v.lambda) ? lambda : v.lambda; }
 
 struct LinArgs {
   const int* lin_block;     // linearise order → block (GN order regrouped by target within each host)
@@ -112,7 +115,8 @@ struct LinArgs {
   float* blk_schur;
   float* part_lin;
   int n_chunks;
-  const double* lm;         // device LM record: skip when the solve is done, write the spare set; nullptr: set 0
+  const double* lm;         // LM record: skip when the solve is done; spare: write the set the record does not hold
+  bool spare;
 };
 
 // ------------------------------------------------------------------------------------------------
@@ -164,12 +168,15 @@ void linearize_kernel(const KernelArgs a, const LinArgs g) {
   __shared__ __attribute__((aligned(16))) unsigned char arena[NW][kArena];
   __shared__ float2 s_pat[LPB];
   __shared__ int s_wlo[NW], s_wn[NW];
+  __shared__ float s_bc[kBlockThreads / LPB];  // block costs (0: invalid or dead), for the chunk's cost partial
   const int chunk = logical_tile();
   if (chunk >= g.n_chunks) return;
-  if (lm_done(g.lm)) return;
-  float* const blk_schur = lm_set(g.lm, g.blk_schur, g.blk_schur1, true);
-  float* const part_lin = lm_set(g.lm, g.part_lin, g.part_lin1, true);
   const int4 d = g.chunk_desc[chunk];
+  const LmView lv = lm_view(g.lm);
+  if (lv.done != 0.0) return;
+  const bool s1 = (lv.set != 0.0) != g.spare;
+  float* const blk_schur = s1 ? g.blk_schur1 : g.blk_schur;
+  float* const part_lin = s1 ? g.part_lin1 : g.part_lin;
   const int first = d.x, count = d.y, n_t = d.z, poff = d.w;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int lb = threadIdx.x / LPB, k = threadIdx.x % LPB, wb = lb % BW;
@@ -201,6 +208,7 @@ void linearize_kernel(const KernelArgs a, const LinArgs g) {
     a.valid[blk] = (uint8_t)ok;
     a.cost[blk] = bcost;
   }
+  if (k == 0) s_bc[lb] = live && ok ? bcost : -1.0f;  // read after the barrier below
   // weighted row x̃ = √w · x  → products carry w (Ceres Corrector with ρ'' ≤ 0: J̃ = √ρ' J, r̃ = √ρ' r)
   const float sw = (act && ok) ? sqrtf(w) : 0.0f;  // rows outside the domain / of dead lanes are all zero
   const float x[14] = {sw * row.hv.x, sw * row.hv.y, sw * row.hv.z, sw * row.hw.x, sw * row.hw.y, sw * row.hw.z,
@@ -296,7 +304,19 @@ void linearize_kernel(const KernelArgs a, const LinArgs g) {
     }
     part_lin[(long long)poff + o] = acc;
   }
-  if (g.wg_red) wg_reduce2(live && k == 0 ? (double)bcost : 0.0, live && k == 0 && ok ? 1.0 : 0.0, g.wg_red + 2 * chunk);
+  if (g.wg_red && wave == 0) {  // the chunk's (Σ cost, Σ valid): lane b takes block b, xor butterflies (fixed order)
+    static_assert(kBlockThreads / LPB <= 64, "one lane per block of the chunk");
+    const float x = lane < count ? s_bc[lane] : -1.0f;
+    double c = x >= 0.0f ? (double)x : 0.0, v = x >= 0.0f ? 1.0 : 0.0;
+    for (int m = 32; m >= 1; m >>= 1) {
+      c += __shfl_xor(c, m, 64);
+      v += __shfl_xor(v, m, 64);
+    }
+    if (lane == 0) {
+      g.wg_red[2 * chunk] = c;
+      g.wg_red[2 * chunk + 1] = v;
+    }
+  }
 }
 
 struct SchurArgs {
@@ -311,7 +331,15 @@ struct SchurArgs {
   double* part_schur;
   double* pt_data;        // per GN point [H_ρρ, g_ρ, W_h(6)] (undamped)
   int n_chunks;
-  const double* lm;       // device LM record (λ, done, set), or nullptr
+  const double* lm;       // LM record (λ, set; the loop's or GnData::lm_idle)
+  // device LM loop: the previous trial's accept (state ← candidate when the record says accepted), done here by the
+  // workgroups before their chunks instead of by a launch of its own; poses == nullptr: nothing to apply
+  double* poses;
+  const double* poses_new;
+  double* rho;
+  const double* rho_new;
+  const int* pt_orig;
+  int n_pose_d, n_gn_points;
 };
 
 // ------------------------------------------------------------------------------------------------
@@ -321,9 +349,20 @@ __global__ __launch_bounds__(kBlockThreads) void schur_kernel(const SchurArgs g,
   extern __shared__ __attribute__((aligned(16))) float W_dyn[];  // W [points × local poses][6] (gn_prepare: schur_lds)
   __shared__ double s_inv[SCHUR_PTS], s_gl[SCHUR_PTS];
   const int c = blockIdx.x;
-  if (c >= g.n_chunks || lm_done(g.lm)) return;
-  lambda = lm_lambda(g.lm, lambda);
-  const float* const blk_schur = lm_set(g.lm, g.blk_schur, g.blk_schur1);
+  if (c >= g.n_chunks) return;  // (not gated by the record's done flag: a trial after the end only wastes time here)
+  const LmView lv = lm_view(g.lm);
+  if (g.poses && lv.accept != 0.0) {  // the last trial's accept (same copies as lm_accept_kernel)
+    const int n = max(g.n_pose_d, g.n_gn_points);
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+      if (i < g.n_pose_d) g.poses[i] = g.poses_new[i];
+      if (i < g.n_gn_points) {
+        const int o = g.pt_orig[i];
+        g.rho[o] = g.rho_new[o];
+      }
+    }
+  }
+  lambda = lm_lambda(lv, lambda);
+  const float* const blk_schur = lv.set != 0.0 ? g.blk_schur1 : g.blk_schur;
   const int4 d = g.desc[c];
   const int first = d.x, npt = d.y, nv = d.z, poff = d.w;
   const int4 ax = g.aux[c];
@@ -430,7 +469,7 @@ __global__ __launch_bounds__(kBlockThreads) void schur_kernel(const SchurArgs g,
 struct AsmArgs {
   const float* part_lin;
   const float* part_lin1;  // buffer set 1 (device LM loop)
-  const double* lm;        // device LM record (λ, done, set), or nullptr
+  const double* lm;        // LM record (λ, set; the loop's or GnData::lm_idle)
   const double* part_schur;
   const int* sky_cptr;
   const int2* sky_contrib;
@@ -447,6 +486,14 @@ struct AsmArgs {
   int band;
   int n_sky;
   int n_frames;
+  // optional: level 0 of the block cyclic reduction written directly (super-rows of crB keyframes: D, U, b = −g; the
+  // positions outside the profile and the identity padding set once by configure_solver), which replaces cr_build's
+  // pass over Sband; status (the solve's failure flag) is then cleared here
+  double* crD;
+  double* crU;
+  double* crb;
+  int crB;
+  int* status;
 };
 
 // Fixed-order sums over a contribution list (total, and the part that is not a Schur term — the undamped
@@ -484,9 +531,9 @@ __device__ __forceinline__ void contrib_sums(const AsmArgs& a, const int2* __res
 // assemble_kernel: S (skyline, lower blocks) and g from the partial slots
 // ------------------------------------------------------------------------------------------------
 __global__ void assemble_kernel(AsmArgs a, double lambda) {
-  if (lm_done(a.lm)) return;
-  lambda = lm_lambda(a.lm, lambda);
-  a.part_lin = lm_set(a.lm, a.part_lin, a.part_lin1);
+  const LmView lv = lm_view(a.lm);  // (no done gate: see schur_kernel)
+  lambda = lm_lambda(lv, lambda);
+  if (lv.set != 0.0) a.part_lin = a.part_lin1;
   const int tid = blockIdx.x * blockDim.x + threadIdx.x;
   const int nS = a.n_sky * 36;
   if (tid < nS) {
@@ -504,6 +551,17 @@ __global__ void assemble_kernel(AsmArgs a, double lambda) {
     }
     a.S[tid] = val;
     if (a.Sband) a.Sband[(long long)i * ((a.band + 1) * 36 + 6) + (j - i + a.band) * 36 + e] = val;
+    if (a.crD) {
+      const int B = a.crB, M = 6 * B, I = i / B, J = j / B;
+      const int Ri = (i % B) * 6 + r, Cj = (j % B) * 6 + cc;  // row of i's entry / column of j's in their super-rows
+      if (I == J) {
+        double* D = a.crD + (long long)I * M * M;
+        D[Ri * M + Cj] = val;
+        D[Cj * M + Ri] = val;
+      } else {  // I == J + 1 (bandwidth ≤ B): U_J[row of j][column of i] = S[6j+cc][6i+r]
+        a.crU[(long long)J * M * M + Cj * M + Ri] = val;
+      }
+    }
     return;
   }
   const int t = tid - nS;
@@ -513,6 +571,10 @@ __global__ void assemble_kernel(AsmArgs a, double lambda) {
   contrib_sums(a, a.g_contrib, a.g_cptr[i], a.g_cptr[i + 1], r, r, sum, dsum);
   a.g[t] = a.fixed[i] ? 0.0 : sum;
   if (a.Sband) a.Sband[(long long)i * ((a.band + 1) * 36 + 6) + (a.band + 1) * 36 + r] = a.fixed[i] ? 0.0 : sum;
+  if (a.crD) {
+    a.crb[t] = a.fixed[i] ? 0.0 : -sum;  // super-row i / B, row (i % B)·6 + r: t itself (M = 6B, rows padded after N)
+    if (t == 0) *a.status = 0;
+  }
   a.g_dir[t] = a.fixed[i] ? 0.0 : dsum;
   if (a.fixed[i]) a.Ddiag[t] = 0.0;
 }
@@ -637,7 +699,6 @@ struct SolveArgs {
   double* x;
   int* status;
   int N;
-  const double* gate;
 };
 
 __device__ __forceinline__ long long sky_off(const SolveArgs& a, int i, int j) {  // block (i, j), j ≥ first(i)
@@ -645,7 +706,6 @@ __device__ __forceinline__ long long sky_off(const SolveArgs& a, int i, int j) {
 }
 
 __global__ __launch_bounds__(256) void skyline_solve_kernel(const SolveArgs a) {
-  if (lm_done(a.gate)) return;
   __shared__ double sA[36], sL[36], sLi[36];
   __shared__ int s_fail;
   const int tid = threadIdx.x;
@@ -768,7 +828,6 @@ struct BandArgs {
   double* x;            // the step δ_poses
   int* status;
   int N;
-  const double* gate;
 };
 
 // rsqrt_nr (pba_device.h): hardware v_rsq_f64 seed + two Newton steps — the pivot is on the solver's
@@ -800,7 +859,6 @@ __device__ inline bool chol6_rcp(double* A, double* invd) {  // in place, lower;
 
 template <int B>
 __global__ __launch_bounds__(256) void band_solve_kernel(const BandArgs a) {
-  if (lm_done(a.gate)) return;
   constexpr int W = B + 1;
   constexpr int ROWF = W * 36;
   constexpr int ROWG = ROWF + 6;
@@ -1017,7 +1075,6 @@ struct CrLevel {
   double* X;   // ⌊n/2⌋ × m × (2m+1)
   double* x;   // n × m
   int n;
-  const double* gate;  // device LM record: nothing to do once the solve is done (nullptr: always run)
 };
 
 template <int M>
@@ -1025,7 +1082,6 @@ __global__ __launch_bounds__(256) void cr_build_kernel(const double* __restrict_
                                                        int* __restrict__ status) {
   // one thread per element of D_I, U_I and b_I of level 0 (rows ≥ N are identity padding); the solve's failure flag
   // is cleared here (the levels only ever set it), which saves a memset launch per solve
-  if (lm_done(L0.gate)) return;
   const long long tid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (tid == 0) *status = 0;
   const long long nD = (long long)L0.n * M * M;
@@ -1123,7 +1179,6 @@ constexpr size_t cr_level_lds() { return sizeof(double) * (2 * M * M + 2 * M * (
 
 template <int M>
 __global__ __launch_bounds__(2 * kCrOddThreads<M>) void cr_level_kernel(CrLevel L, CrLevel Ln, int* status) {
-  if (lm_done(L.gate)) return;
   constexpr int NC = 2 * M + 1, W = M + NC, T = kCrOddThreads<M>;
   __shared__ __attribute__((aligned(16))) double colk[2][2][2][M];
   extern __shared__ double smem[];
@@ -1268,7 +1323,6 @@ constexpr size_t cr_level_wave_lds() { return sizeof(double) * (3 * M * M + M + 
 template <int M>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void cr_level_wave_kernel(
     CrLevel L, CrLevel Ln, int* status) {
-  if (lm_done(L.gate)) return;
   static_assert(2 * M + 1 <= 64, "one wave per elimination");
   constexpr int NC = 2 * M + 1;
   __shared__ __attribute__((aligned(16))) double piv[3][M * kCrPivot];
@@ -1367,7 +1421,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 // The root super-row on one wave (lane 2M carries b; the coupling lanes are empty).
 template <int M>
 __global__ __launch_bounds__(64) void cr_root_wave_kernel(CrLevel L, int* status) {
-  if (lm_done(L.gate)) return;
   __shared__ __attribute__((aligned(16))) double piv[M * kCrPivot];
   double a[M];
   const int lane = threadIdx.x;
@@ -1384,7 +1437,6 @@ __global__ __launch_bounds__(64) void cr_root_wave_kernel(CrLevel L, int* status
 // The root super-row (the last level): x = D⁻¹ b.
 template <int M>
 __global__ __launch_bounds__(kCrOddThreads<M>) void cr_root_kernel(CrLevel L, int* status) {
-  if (lm_done(L.gate)) return;
   constexpr int W = 3 * M + 1;
   __shared__ __attribute__((aligned(16))) double colk[2][2][M];
   double a[M];
@@ -1434,7 +1486,6 @@ __device__ __forceinline__ void cr_back_row(const CrLevel& L, const double* __re
 // one (large) level, one lane per output
 template <int M>
 __global__ void cr_back_kernel(CrLevel L, const double* __restrict__ xn, double* __restrict__ out, int lim) {
-  if (lm_done(L.gate)) return;
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t < lim) cr_back_row<M>(L, xn, out, t);
 }
@@ -1443,7 +1494,6 @@ __global__ void cr_back_kernel(CrLevel L, const double* __restrict__ xn, double*
 template <int M>
 __global__ __launch_bounds__(1024) void cr_back_tail_kernel(const CrLevels C, int hi, int lo, double* __restrict__ step,
                                                             int N) {
-  if (lm_done(C.lv[0].gate)) return;
   for (int l = hi; l >= lo; --l) {
     const CrLevel& L = C.lv[l];
     double* out = l == 0 ? step : L.x;
@@ -1604,9 +1654,10 @@ struct PairUpdateArgs {
 __global__ __launch_bounds__(kBlockThreads) void update_kernel(const PoseUpdateArgs pa, PointUpdateArgs qa,
                                                                const PairUpdateArgs ra, int gp, int gq, double lambda,
                                                                const double* __restrict__ lm) {
-  if (lm_done(lm)) return;
-  lambda = lm_lambda(lm, lambda);
-  qa.blk_schur = lm_set(lm, qa.blk_schur, qa.blk_schur1);
+  const LmView lv = lm_view(lm);
+  if (lv.done != 0.0) return;  // gated: a trial after the end must not touch the last step (pba_gn_get_step)
+  lambda = lm_lambda(lv, lambda);
+  if (lv.set != 0.0) qa.blk_schur = qa.blk_schur1;
   const int b = blockIdx.x;
   if (b < gp) {
     pose_update_block(pa, b);
@@ -1650,13 +1701,13 @@ __global__ __launch_bounds__(kDecideThreads) void lm_decide_kernel(const double*
                                                         const int* __restrict__ status, double min_rel,
                                                         double ftol, double* __restrict__ lm,
                                                         volatile double* __restrict__ host_rec, double seq) {
-  if (lm_done(lm)) return;  // a trial enqueued ahead of the one that ended the solve
+  if (lm[kLmDone] != 0.0) return;  // a trial enqueued ahead of the one that ended the solve
   const double lambda = lm[kLmLambda];
-  constexpr int N = kDecideThreads, U = 4;
-  __shared__ double part[5][N];
+  constexpr int N = kDecideThreads, U = 8;
+  __shared__ double part[5][N / 64];
   double v[5] = {0, 0, 0, 0, 0};  // dg, dD, qg, qD, c
-  // strided sums of each slot range, U independent loads in flight per thread (the candidate cost alone has one slot
-  // per evaluation workgroup: 12.5k at C4)
+  // strided sums of each slot range, U independent 16-B loads in flight per thread (the candidate cost alone has one
+  // slot per linearisation chunk: 12.5k at C4), then xor butterflies per wave and the waves in order (deterministic)
   auto range = [&](int beg, int end, double& x, double& y) {
     for (int i0 = beg + (int)threadIdx.x; i0 < end; i0 += U * N) {
       double2 r[U];
@@ -1674,15 +1725,21 @@ __global__ __launch_bounds__(kDecideThreads) void lm_decide_kernel(const double*
   range(gp, gp + gq, v[2], v[3]);
   range(gp + gq, gp + gq + gc, v[4], unused);
 #pragma unroll
-  for (int q = 0; q < 5; ++q) part[q][threadIdx.x] = v[q];
-  __syncthreads();
-  for (int w = N / 2; w > 0; w >>= 1) {
-    if ((int)threadIdx.x < w)
+  for (int q = 0; q < 5; ++q)
+    for (int m = 32; m >= 1; m >>= 1) v[q] += __shfl_xor(v[q], m, 64);
+  if ((threadIdx.x & 63) == 0)
 #pragma unroll
-      for (int q = 0; q < 5; ++q) part[q][threadIdx.x] += part[q][threadIdx.x + w];
-    __syncthreads();
-  }
-  if (threadIdx.x != 0) return;
+    for (int q = 0; q < 5; ++q) part[q][threadIdx.x >> 6] = v[q];
+  __syncthreads();
+  if (threadIdx.x == 0)
+    for (int q = 0; q < 5; ++q) {
+      double t = 0.0;
+      for (int w = 0; w < N / 64; ++w) t += part[q][w];
+      part[q][0] = t;
+    }
+  if (threadIdx.x >= 64) return;  // wave 0 publishes; lane 0 decides
+  __shared__ double s_rec[kLmFields];
+  if (threadIdx.x == 0) {
   const double dg = part[0][0], dD = part[1][0], qg = part[2][0], qD = part[3][0], c = part[4][0];
   const int st = *status;
   const double model = __dadd_rn(__dmul_rn(0.5, __dsub_rn(__dmul_rn(lambda, dD), dg)),
@@ -1721,11 +1778,19 @@ __global__ __launch_bounds__(kDecideThreads) void lm_decide_kernel(const double*
   lm[kLmFactor] = factor;
   lm[kLmLambda] = 1.0 / radius;
   lm[kLmDone] = done;
-  if (host_rec) {
-    for (int i = 0; i < kLmFields; ++i) host_rec[i] = lm[i];
-    __threadfence_system();
-    host_rec[kLmFields] = seq;
+  for (int i = 0; i < kLmFields; ++i) s_rec[i] = lm[i];
   }
+  if (!host_rec) return;
+  // publish: lane i stores field i (one system-scope store instruction, fine-grained host memory, completion awaited
+  // once), then lane 0 the sequence number the host polls for — no L2 write-back fence, no per-field wait
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  const int l = threadIdx.x;
+  if (l < kLmFields) host_rec[l] = s_rec[l];
+  __builtin_amdgcn_s_waitcnt(0);  // vmcnt(0) & lgkmcnt(0): every lane's field store has completed
+  __builtin_amdgcn_wave_barrier();
+  if (l == 0) host_rec[kLmFields] = seq;
 }
 
 // The accepted candidate becomes the state (device-side accept, gated by the decision record; lm == nullptr: always).
@@ -1789,6 +1854,7 @@ int configure_solver(pba_engine* e, int K, int solver) {
       L.X = off; off += (size_t)(n / 2) * M * (2 * M + 1);
       G.cr_levels.push_back(L);
     }
+    G.cr0_dirty = true;  // level 0 is set up for assemble_kernel's direct writes on first use
   }
   return PBA_OK;
 }
@@ -2064,6 +2130,11 @@ int gn_prepare(pba_engine* e) {
   PBA_HIP(G.red.resize((size_t)2 * G.red_slots));
   PBA_HIP(G.red_h.resize(2 * G.red_slots));
   PBA_HIP(G.lm.resize(kLmFields));
+  {  // the record of host-driven steps: not done, buffer set 0, λ NaN (the kernels then use their λ argument)
+    std::vector<double> idle(kLmFields, 0.0);
+    idle[kLmLambda] = std::numeric_limits<double>::quiet_NaN();
+    PBA_HIP(G.lm_idle.upload(idle, st));
+  }
   // decision record + sequence number, written by lm_decide_kernel over the bus (fine-grained host memory)
   PBA_HIP(G.lm_h.resize(kLmFields + 1, hipHostMallocCoherent | hipHostMallocMapped));
   PBA_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&G.lm_host_d), G.lm_h.p, 0));
@@ -2158,7 +2229,7 @@ int linearize(pba_engine* e, double* cost, const double* lm = nullptr, const Pai
   }
   const KernelArgs ka = make_kernel_args(e, pairs, rho ? rho : e->rho.p);
   LinArgs la{G.lin_block.p, G.blk_schur1.p, G.part_lin1.p, wg_red, G.lin_gpos.p, G.chunk_desc.p, G.blk_lt.p,
-             G.blk_schur.p, G.part_lin.p, G.n_chunks, lm};
+             G.blk_schur.p, G.part_lin.p, G.n_chunks, lm ? lm : G.lm_idle.p, lm != nullptr};
   if (e->opt.residual_kind == PBA_RESIDUAL_PHOTOMETRIC) launch_linearize_photometric(e, ka, la);
   else launch_linearize_geometric(e, ka, la);
   PBA_HIP(hipGetLastError());
@@ -2167,14 +2238,32 @@ int linearize(pba_engine* e, double* cost, const double* lm = nullptr, const Pai
   return PBA_OK;
 }
 
-CrLevel cr_level(GnData& G, int l, const double* lm = nullptr) {
+CrLevel cr_level(GnData& G, int l) {
   const CrLevelHost& h = G.cr_levels[l];
   double* base = G.cr_buf.p;
-  return CrLevel{base + h.D, base + h.U, base + h.b, base + h.X, base + h.x, h.n, lm};
+  return CrLevel{base + h.D, base + h.U, base + h.b, base + h.X, base + h.x, h.n};
 }
 
+// Level 0 of the cyclic reduction as assemble_kernel expects it: zeros (positions outside the reduced system's profile
+// are never written), identity diagonal on the padding rows past the last keyframe.
+int init_cr_level0(pba_engine* e) {
+  GnData& G = e->gn;
+  if (G.cr_levels.empty()) return PBA_OK;
+  const int B = G.band_kernel, M = 6 * B, N = e->n_frames;
+  const CrLevelHost& h = G.cr_levels[0];
+  std::vector<double> z((size_t)h.n * M * M * 2 + (size_t)h.n * M, 0.0);  // D | U | b (contiguous: configure_solver)
+  for (int I = 0; I < h.n; ++I)
+    for (int R = 0; R < M; ++R)
+      if (I * B + R / 6 >= N) z[(size_t)I * M * M + (size_t)R * M + R] = 1.0;
+  PBA_HIP(hipMemcpyAsync(G.cr_buf.p + h.D, z.data(), z.size() * sizeof(double), hipMemcpyHostToDevice, e->stream));
+  PBA_HIP(hipStreamSynchronize(e->stream));  // z is pageable and goes out of scope
+  G.cr0_dirty = false;
+  return PBA_OK;
+}
+
+// build: level 0 from Sband (cr_build_kernel); false when assemble_kernel wrote it directly
 template <int M>
-void cr_solve(pba_engine* e, const double* lm) {
+void cr_solve(pba_engine* e, bool build) {
   GnData& G = e->gn;
   if (cr_level_lds<M>() > 65536) {  // above the default dynamic-LDS limit (gfx950 has 160 KiB per CU)
     // the attribute is per device: set it on every solve (cheap) rather than once per process
@@ -2182,26 +2271,27 @@ void cr_solve(pba_engine* e, const double* lm) {
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)cr_level_lds<M>());
   }
   const int nl = (int)G.cr_levels.size();
-  CrLevel L0 = cr_level(G, 0, lm);
+  CrLevel L0 = cr_level(G, 0);
   const long long nthreads = (long long)L0.n * M * M + (long long)L0.n * M;
-  cr_build_kernel<M><<<(unsigned)((nthreads + 255) / 256), 256, 0, e->stream>>>(G.Sband.p, L0, e->n_frames, G.band_kernel,
-                                                                                G.status.p);
+  if (build)
+    cr_build_kernel<M><<<(unsigned)((nthreads + 255) / 256), 256, 0, e->stream>>>(G.Sband.p, L0, e->n_frames,
+                                                                                  G.band_kernel, G.status.p);
   for (int l = 0; l + 1 < nl; ++l) {  // one fused launch per level (odd eliminations + even rebuild)
-    CrLevel L = cr_level(G, l, lm), Ln = cr_level(G, l + 1, lm);
+    CrLevel L = cr_level(G, l), Ln = cr_level(G, l + 1);
     if constexpr (2 * M + 1 <= 64)
       cr_level_wave_kernel<M><<<(L.n + 1) / 2, 256, cr_level_wave_lds<M>(), e->stream>>>(L, Ln, G.status.p);
     else
       cr_level_kernel<M><<<(L.n + 1) / 2, 2 * kCrOddThreads<M>, cr_level_lds<M>(), e->stream>>>(L, Ln, G.status.p);
   }
-  if constexpr (2 * M + 1 <= 64) cr_root_wave_kernel<M><<<1, 64, 0, e->stream>>>(cr_level(G, nl - 1, lm), G.status.p);
-  else cr_root_kernel<M><<<1, kCrOddThreads<M>, 0, e->stream>>>(cr_level(G, nl - 1, lm), G.status.p);
+  if constexpr (2 * M + 1 <= 64) cr_root_wave_kernel<M><<<1, 64, 0, e->stream>>>(cr_level(G, nl - 1), G.status.p);
+  else cr_root_kernel<M><<<1, kCrOddThreads<M>, 0, e->stream>>>(cr_level(G, nl - 1), G.status.p);
   if (nl == 1) {  // a single super-row: the root's x is the step
     (void)hipMemcpyAsync(G.x.p, L0.x, sizeof(double) * 6 * e->n_frames, hipMemcpyDeviceToDevice, e->stream);
     return;
   }
   CrLevels C{};
   C.nl = nl;
-  for (int l = 0; l < nl; ++l) C.lv[l] = cr_level(G, l, lm);
+  for (int l = 0; l < nl; ++l) C.lv[l] = cr_level(G, l);
   int lo = nl - 2;  // the tail: levels with at most kCrTailRows super-rows
   while (lo > 0 && C.lv[lo - 1].n <= kCrTailRows) --lo;
   cr_back_tail_kernel<M><<<1, 1024, 0, e->stream>>>(C, nl - 2, lo, G.x.p, e->n_frames);
@@ -2227,7 +2317,7 @@ void enqueue_updates(pba_engine* e, double lambda, const uint8_t* fixed, int* gp
                      G.blk_schur.p, G.blk_schur1.p, G.x.p, fixed, e->rho.p, G.rho_new.p, G.drho.p, G.red.p,
                      G.n_gn_points};
   PairUpdateArgs ra{e->pair_host.p, e->pair_target.p, e->frame_cam.p, e->intr_d.p, G.pairs_new.p, e->n_pairs};
-  update_kernel<<<gp + gq + gr, kBlockThreads, 0, e->stream>>>(pa, qa, ra, gp, gq, lambda, lm);
+  update_kernel<<<gp + gq + gr, kBlockThreads, 0, e->stream>>>(pa, qa, ra, gp, gq, lambda, lm ? lm : G.lm_idle.p);
   G.pairs_new_fresh = true;
   *gp_out = gp;
   *gq_out = gq;
@@ -2260,14 +2350,14 @@ int finish_step(pba_engine* e, double lambda, const uint8_t* fixed, double* mode
 }
 
 // Band solvers on G.Sband (block cyclic reduction for K ≤ 8, LDS-window band Cholesky for K = 16).
-int band_solve(pba_engine* e, const double* lm = nullptr) {
+int band_solve(pba_engine* e, bool build = true) {
   GnData& G = e->gn;
   const int nf = e->n_frames;
   if (G.solver == SOLVER_CR) {
-    if (G.band_kernel == 4) cr_solve<24>(e, lm);
-    else cr_solve<48>(e, lm);
+    if (G.band_kernel == 4) cr_solve<24>(e, build);
+    else cr_solve<48>(e, build);
   } else {
-    BandArgs ba{G.Sband.p, G.Lband.p, G.x.p, G.status.p, nf, lm};
+    BandArgs ba{G.Sband.p, G.Lband.p, G.x.p, G.status.p, nf};
     if (G.band_kernel == 4) band_solve_kernel<4><<<1, 256, 0, e->stream>>>(ba);
     else if (G.band_kernel == 8) band_solve_kernel<8><<<1, 256, 0, e->stream>>>(ba);
     else band_solve_kernel<16><<<1, 256, 0, e->stream>>>(ba);
@@ -2289,23 +2379,30 @@ int enqueue_solve(pba_engine* e, double lambda, const double* lm = nullptr) {
   GnData& G = e->gn;
   const int nf = e->n_frames;
   SchurArgs sa{G.schur_desc.p, G.schur_aux.p, G.schur_pairs.p, G.pt_first.p, G.pt_nblk.p, G.blk_lv.p,
-               G.blk_schur.p, G.blk_schur1.p, G.part_schur.p, G.pt_data.p, G.n_schur, lm};
+               G.blk_schur.p, G.blk_schur1.p, G.part_schur.p, G.pt_data.p, G.n_schur, lm ? lm : G.lm_idle.p,
+               lm ? e->poses.p : nullptr, G.poses_new.p, e->rho.p, G.rho_new.p, G.pt_orig.p, 7 * nf, G.n_gn_points};
   schur_lds_limit(G);
   schur_kernel<<<G.n_schur, kBlockThreads, G.schur_lds, e->stream>>>(sa, lambda);
-  AsmArgs aa{G.part_lin.p, G.part_lin1.p, lm, G.part_schur.p, G.sky_cptr.p, G.sky_contrib.p, G.g_cptr.p,
+  // block cyclic reduction: assemble writes its level 0 directly (no Sband, no cr_build pass)
+  const bool direct = G.band_kernel && G.solver == SOLVER_CR;
+  if (direct && G.cr0_dirty)  // a distributed solve rebuilt level 0 over the whole band: back to zeros + padding
+    if (int rc = init_cr_level0(e)) return rc;
+  CrLevel L0 = direct ? cr_level(G, 0) : CrLevel{};
+  AsmArgs aa{G.part_lin.p, G.part_lin1.p, lm ? lm : G.lm_idle.p, G.part_schur.p, G.sky_cptr.p, G.sky_contrib.p, G.g_cptr.p,
              G.g_contrib.p, G.sky_blk_i.p, G.sky_blk_j.p, G.fixed.p, G.S.p, G.g.p, G.g_dir.p, G.Ddiag.p,
-             G.band_kernel ? G.Sband.p : nullptr, G.band_kernel, G.n_sky, nf};
-  if (G.sband_dirty && G.band_kernel) {  // a distributed import filled the whole band: clear the off-profile part
+             G.band_kernel && !direct ? G.Sband.p : nullptr, G.band_kernel, G.n_sky, nf,
+             direct ? L0.D : nullptr, L0.U, L0.b, G.band_kernel, G.status.p};
+  if (G.sband_dirty && G.band_kernel && !direct) {  // a distributed import filled the whole band: clear the off-profile part
     PBA_HIP(hipMemsetAsync(G.Sband.p, 0, sizeof(double) * (size_t)nf * ((G.band_kernel + 1) * 36 + 6), e->stream));
     G.sband_dirty = false;
   }
   const int nthreads = G.n_sky * 36 + 6 * nf;
   assemble_kernel<<<(nthreads + 255) / 256, 256, 0, e->stream>>>(aa, lambda);
   if (G.band_kernel) {
-    if (int rc = band_solve(e, lm)) return rc;
+    if (int rc = band_solve(e, !direct)) return rc;
   } else {
     PBA_HIP(hipMemcpyAsync(G.L.p, G.S.p, sizeof(double) * 36 * (size_t)G.n_sky, hipMemcpyDeviceToDevice, e->stream));
-    SolveArgs so{G.L.p, G.sky_first.p, G.sky_row.p, G.sky_last.p, G.g.p, G.Linv.p, G.x.p, G.status.p, nf, lm};
+    SolveArgs so{G.L.p, G.sky_first.p, G.sky_row.p, G.sky_last.p, G.g.p, G.Linv.p, G.x.p, G.status.p, nf};
     skyline_solve_kernel<<<1, 256, 0, e->stream>>>(so);
   }
   PBA_HIP(hipGetLastError());
@@ -2352,12 +2449,13 @@ int wait_decision(pba_engine* e, double seq, double* d) {
 // One LM trial on a single GPU, enqueued whole and steered by the device LM record G.lm (λ, buffer set, done):
 // Schur complement + reduced solve → candidate state (poses, ρ, pair table) and model-decrease partials →
 // linearisation AT the candidate into the spare buffer set, whose per-chunk cost partials are the candidate cost →
-// the decision on the device (accept, the next trust radius, done; published to the host) → gated accept.  An accepted
+// the decision on the device (accept, the next trust radius, done; published to the host); the accept itself is applied
+// by the next trial's first kernel.  An accepted
 // step's linearisation is then already done (a rejected one cost a linearisation instead of a residual-only pass), and
 // since every kernel returns at once when the solve is done, the host enqueues the next trial before it has seen this
 // one's decision: no host round trip between trials.  The candidate is evaluated even when the solve failed (its
 // numbers are then discarded): a garbage state is memory-safe in every evaluation kernel.  ev (phase timing only,
-// else nullptr): begin | candidate state | candidate linearisation | decision + accept.
+// else nullptr): begin | candidate state | candidate linearisation | decision.
 int lm_trial(pba_engine* e, double min_rel, double ftol, double seq, const hipEvent_t* ev) {
   GnData& G = e->gn;
   if (ev) PBA_HIP(hipEventRecord(ev[0], e->stream));
@@ -2370,9 +2468,8 @@ int lm_trial(pba_engine* e, double min_rel, double ftol, double seq, const hipEv
   lm_decide_kernel<<<1, kDecideThreads, 0, e->stream>>>(G.red.p, gp, gq, G.n_chunks, G.status.p, min_rel, ftol, G.lm.p,
                                                         G.lm_host_d, seq);
   PBA_HIP(hipGetLastError());
-  launch_accept(e, G.lm.p);
   if (ev) PBA_HIP(hipEventRecord(ev[3], e->stream));
-  return PBA_OK;
+  return PBA_OK;  // an accepted candidate becomes the state in the next trial's schur_kernel (or after the loop)
 }
 
 int candidate_cost(pba_engine* e, double* cost) {
@@ -2404,13 +2501,14 @@ int step_export(pba_engine* e, double lambda, int band, double* X) {
   if (int rc = exchange_K(e, band, &K)) return rc;
   const int nf = e->n_frames;
   SchurArgs sa{G.schur_desc.p, G.schur_aux.p, G.schur_pairs.p, G.pt_first.p, G.pt_nblk.p, G.blk_lv.p,
-               G.blk_schur.p, G.blk_schur1.p, G.part_schur.p, G.pt_data.p, G.n_schur, nullptr};
+               G.blk_schur.p, G.blk_schur1.p, G.part_schur.p, G.pt_data.p, G.n_schur, G.lm_idle.p,
+               nullptr, nullptr, nullptr, nullptr, nullptr, 0, 0};
   schur_lds_limit(G);
   if (G.n_schur > 0) schur_kernel<<<G.n_schur, kBlockThreads, G.schur_lds, e->stream>>>(sa, lambda);
   PBA_HIP(hipMemsetAsync(X, 0, sizeof(double) * (size_t)nf * ex_row(K), e->stream));
-  AsmArgs aa{G.part_lin.p, G.part_lin1.p, nullptr, G.part_schur.p, G.sky_cptr.p, G.sky_contrib.p, G.g_cptr.p,
+  AsmArgs aa{G.part_lin.p, G.part_lin1.p, G.lm_idle.p, G.part_schur.p, G.sky_cptr.p, G.sky_contrib.p, G.g_cptr.p,
              G.g_contrib.p, G.sky_blk_i.p, G.sky_blk_j.p, G.fixed.p, G.S.p, G.g.p, G.g_dir.p, G.Ddiag.p, nullptr, K,
-             G.n_sky, nf};
+             G.n_sky, nf, nullptr, nullptr, nullptr, 0, nullptr};
   const int nthreads = G.n_sky * 36 + 6 * nf;
   export_kernel<<<(nthreads + 255) / 256, 256, 0, e->stream>>>(aa, G.observed.p, X, K);
   PBA_HIP(hipGetLastError());
@@ -2433,6 +2531,7 @@ int step_import(pba_engine* e, double lambda, int band, const double* X, double*
   import_kernel<<<(unsigned)((n + 255) / 256), 256, 0, e->stream>>>(ia, lambda);
   PBA_HIP(hipGetLastError());
   G.sband_dirty = true;
+  G.cr0_dirty = true;  // cr_build writes level 0 over the whole band
   if (int rc = band_solve(e)) return rc;
   return finish_step(e, lambda, G.fixed_dist.p, model_pose, model_points, solver_status);
 }
@@ -2671,7 +2770,8 @@ int lm_loop_single(pba_engine* e, const pba_solver_options* o, pba_solver_summar
     ++s.successful_steps;
     cost = d[kLmCostNew];
   }
-  PBA_HIP(hipStreamSynchronize(e->stream));  // the last trial's accept, and the gated trial enqueued after the end
+  launch_accept(e, G.lm.p);  // the last trial's accept (no trial after it to apply it)
+  PBA_HIP(hipStreamSynchronize(e->stream));
   if (set == 1) {  // the current state's pieces are in set 1: make it set 0 for the host-driven entry points
     std::swap(G.blk_schur.p, G.blk_schur1.p);
     std::swap(G.blk_schur.n, G.blk_schur1.n);

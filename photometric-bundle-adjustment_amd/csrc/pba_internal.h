@@ -500,6 +500,7 @@ struct GnData {
   DevBuf<uint8_t> fixed;
   DevBuf<uint8_t> observed, fixed_req, fixed_dist;  // multi-GPU: local observation flags, requested / effective constants
   bool sband_dirty = false;                         // Sband fully written by a distributed import
+  bool cr0_dirty = true;                            // CR level 0 not (re)initialised for assemble's direct writes
   std::vector<uint8_t> fixed_h;
   DevBuf<double> poses_new, rho_new, red;
   DevBuf<int> status;
@@ -507,6 +508,7 @@ struct GnData {
   bool pairs_new_fresh = false;  // pairs_new formed by the last update_kernel (its candidate state)
   PinnedBuf<double> red_h;
   DevBuf<double> lm;         // LM decision record of the single-GPU loop (pba_gn.hip: kLm*)
+  DevBuf<double> lm_idle;    // the record host-driven steps pass to the kernels (not done, set 0, λ from the argument)
   PinnedBuf<double> lm_h;    // its host copy (+ sequence number), host-coherent, written by lm_decide_kernel
   double* lm_host_d = nullptr;  // lm_h's device address
   bool phase_timing = false;    // pba_set_solver_timing: stream events around the LM phases

@@ -21,6 +21,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--texture", default="noise")
+    ap.add_argument("--solve", action="store_true", help="time pba_solve (the device-steered LM loop) instead")
     args = ap.parse_args()
     import numpy as np
     import torch
@@ -31,6 +32,13 @@ def main():
     eng.set_fixed_frames(np.array([0, 1], np.int32))
     eng.set_state(pb.poses, pb.rho)
     eng.gn_linearize()
+    if args.solve:
+        eng.solve(max_iterations=2, function_tolerance=0.0)
+        eng.set_state(pb.poses, pb.rho)
+        s = eng.solve(max_iterations=args.iters, function_tolerance=0.0)
+        print(f"{s['total_ms'] / max(s['iterations'], 1):.3f} ms per LM iteration (pba_solve), {s['successful_steps']} accepted")
+        eng.close()
+        return
     t0 = time.perf_counter()
     for _ in range(args.iters):
         eng.gn_linearize()

@@ -1,0 +1,22 @@
+#!/usr/bin/env python3
+"""Per-iteration kernel timeline of a pba_solve kernel trace (rocprofv3 --kernel-trace CSV): the kernels of one LM
+trial in launch order with their durations and the idle gaps before them.  Diagnostic.
+    python tools/gn_trace.py gpurun_out/<dir>/run_kernel_trace.csv"""
+import csv
+import sys
+
+rows = sorted(csv.DictReader(open(sys.argv[1])), key=lambda r: int(r["Start_Timestamp"]))
+idx = [i for i, r in enumerate(rows) if "schur_kernel" in r["Kernel_Name"]]
+if len(idx) < 4:
+    sys.exit("fewer than 4 trials in the trace")
+a, b = idx[-3], idx[-2]
+prev = int(rows[a - 1]["End_Timestamp"])
+tot_k = tot_g = 0.0
+for r in rows[a:b]:
+    s, e = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
+    gap, dur = (s - prev) / 1e3, (e - s) / 1e3
+    prev = e
+    tot_k += dur
+    tot_g += gap
+    print(f"{r['Kernel_Name'][:70]:70s} gap {gap:7.2f}  dur {dur:7.2f}")
+print(f"kernels {tot_k:.1f} us + gaps {tot_g:.1f} us = {tot_k + tot_g:.1f} us per trial")
