@@ -143,7 +143,14 @@ __global__ __launch_bounds__(kBlockThreads) void photometric_block_kernel(const 
 
   if ((int)threadIdx.x < P) s_pat[threadIdx.x] = make_float2(a.pattern[2 * threadIdx.x], a.pattern[2 * threadIdx.x + 1]);
   adopt_state(a);
-  const int pt = stage_tile<LPB>(a, s_tb, lb, k, blk, live);
+  int pt;
+  if (LPB == 8 && a.poses) {  // fused state: the workgroup-cooperative prologue (BPW = 32)
+    static_assert(kBlockThreads == 256, "stage_tile_wg: 4 waves, 32 blocks");
+    pt = a.block_rec[live ? blk : a.n_blocks - 1].x;
+    stage_tile_wg(a, s_tb, blk0);
+  } else {
+    pt = stage_tile<LPB>(a, s_tb, lb, k, blk, live);
+  }
   const float Ih = act ? a.host_int[(long long)pt * P + k] : 0.0f;
   __syncthreads();
   Row row;

@@ -1317,12 +1317,19 @@ __device__ __forceinline__ bool gj_wave(const double* __restrict__ D, const doub
 template <int M>
 constexpr size_t cr_level_wave_lds() { return sizeof(double) * (3 * M * M + M + 2 * M * (2 * M + 1)); }
 
-// One level, 4 waves per even super-row i: wave 0 eliminates row i−1 on [D | U_{i−1} | b] (X^U, X^b), waves 1 and 2
-// row i+1 on [D | U_iᵀ | b] (X^L, X^b) and [D | U_{i+1}] (X^U) — D's columns replicated per wave — while wave 3
-// parks U_{i−1}, U_i, D_i and b_i in LDS for the rebuild of row i.
-template <int M>
+// One level, 4 waves per rebuilt super-row i: wave 0 eliminates its left neighbour l on [D | U_l | b] (X^U, X^b),
+// waves 1 and 2 its right neighbour r on [D | U_iᵀ | b] (X^L, X^b) and [D | U_r] (X^U) — D's columns replicated per
+// wave — while wave 3 parks U_l, U_i, D_i and b_i in LDS for the rebuild of row i.
+//   CR  (PCR = false): i = 2·blockIdx (the even rows), l = i − 1, r = i + 1, rebuilt row i/2 of the next level; X_r
+//       is stored for the back-substitution.
+//   PCR (PCR = true, stride s): i = blockIdx (EVERY row), l = i − s, r = i + s, rebuilt row i of the next level
+//       (couplings now at stride 2s).  Every row stays in the system, so after ⌈log2 n⌉ levels all couplings are
+//       gone and x_i = D_i⁻¹ b_i (pcr_solve_kernel): no back-substitution.  A PCR level runs twice the workgroups of a
+//       CR level at the same per-workgroup latency, so it is used while the rows fit one workgroup per CU.
+// The D_i' are Schur complements of SPD principal submatrices ({l, i, r}), so every pivot block stays SPD.
+template <int M, bool PCR>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void cr_level_wave_kernel(
-    CrLevel L, CrLevel Ln, int* status) {
+    CrLevel L, CrLevel Ln, int s, int* status) {
   static_assert(2 * M + 1 <= 64, "one wave per elimination");
   constexpr int NC = 2 * M + 1;
   __shared__ __attribute__((aligned(16))) double piv[3][M * kCrPivot];
@@ -1332,36 +1339,38 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   double* sD = sUi + M * M;
   double* sb = sD + M * M;
   double* sX[2] = {sb + M, sb + M + M * NC};
-  const int i = 2 * blockIdx.x, in = blockIdx.x;
-  const bool left = i - 1 >= 0, right = i + 1 < L.n;
+  const int i = PCR ? (int)blockIdx.x : 2 * (int)blockIdx.x, in = blockIdx.x;
+  if (!PCR) s = 1;
+  const int il = i - s, ir = i + s;
+  const bool left = il >= 0, right = ir < L.n;
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   if (w == 3) {
     for (int e = lane; e < 3 * M * M + M; e += 64) {
       const double* src = nullptr;
-      if (e < M * M) src = left ? L.U + (long long)(i - 1) * M * M + e : nullptr;
-      else if (e < 2 * M * M) src = L.U + (long long)i * M * M + (e - M * M);
+      if (e < M * M) src = left ? L.U + (long long)il * M * M + e : nullptr;
+      else if (e < 2 * M * M) src = right ? L.U + (long long)i * M * M + (e - M * M) : nullptr;
       else if (e < 3 * M * M) src = L.D + (long long)i * M * M + (e - 2 * M * M);
       else src = L.b + (long long)i * M + (e - 3 * M * M);
       smem[e] = src ? *src : 0.0;
     }
   } else {
-    const int j = w == 0 ? i - 1 : i + 1;
-    const bool has = j >= 0 && j < L.n;
-    const int jj = has ? j : 1;  // a missing neighbour eliminates a real row and contributes zeros
+    const int j = w == 0 ? il : ir;
+    const bool has = w == 0 ? left : right;
+    const int jj = has ? j : i;  // a missing neighbour eliminates a real row and contributes zeros
     const double* D = L.D + (long long)jj * M * M;
     const double* bj = L.b + (long long)jj * M;
     double a[M];
     bool ok;
     if (w == 0) ok = gj_wave<M>(D, L.U + (long long)jj * M * M, false, bj, M + 1, lane, piv[0], a);
-    else if (w == 1) ok = gj_wave<M>(D, L.U + (long long)(jj - 1) * M * M, true, bj, M + 1, lane, piv[1], a);
-    else ok = gj_wave<M>(D, jj + 1 < L.n ? L.U + (long long)jj * M * M : nullptr, false, nullptr, M, lane, piv[2], a);
+    else if (w == 1) ok = gj_wave<M>(D, L.U + (long long)i * M * M, true, bj, M + 1, lane, piv[1], a);
+    else ok = gj_wave<M>(D, jj + s < L.n ? L.U + (long long)jj * M * M : nullptr, false, nullptr, M, lane, piv[2], a);
     if (!ok && has && lane == 0) atomicOr(status, 1);
     if (lane >= M && lane < 2 * M + (w == 2 ? 0 : 1)) {
       const int col = lane < 2 * M ? (w == 1 ? lane - M : lane) : 2 * M;
       double* x = sX[w == 0 ? 0 : 1] + col;
 #pragma unroll
       for (int r = 0; r < M; ++r) x[r * NC] = has ? a[r] : 0.0;
-      if (w != 0 && has) {  // X_{i+1} for the back-substitution
+      if (!PCR && w != 0 && has) {  // X_{i+1} for the back-substitution
         double* X = L.X + (long long)(j / 2) * M * NC + col;
 #pragma unroll
         for (int r = 0; r < M; ++r) X[r * NC] = a[r];
@@ -1412,7 +1421,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       const int r = 16 * rt + (lane >> 4) + 4 * v, c = bcol[h];
       if (r < M) {
         if (c < M) Ln.D[(long long)in * M * M + r * M + c] = acc[h][v];
-        else if (c < 2 * M) Ln.U[(long long)in * M * M + r * M + (c - M)] = right ? acc[h][v] : 0.0;
+        else if (c < 2 * M) Ln.U[(long long)in * M * M + r * M + (c - M)] = (PCR ? i + 2 * s < L.n : right) ? acc[h][v] : 0.0;
         else if (c == 2 * M) Ln.b[(long long)in * M + r] = acc[h][v];
       }
     }
@@ -1432,6 +1441,24 @@ __global__ __launch_bounds__(64) void cr_root_wave_kernel(CrLevel L, int* status
   if (lane == 2 * M)
 #pragma unroll
     for (int r = 0; r < M; ++r) L.x[r] = a[r];
+}
+
+// The last PCR level's decoupled rows: x_i = D_i⁻¹ b_i, one wave per row; x in the level-0 layout is the step itself
+// (out = the step vector, lim = 6N), else the x of the CR level the PCR levels took over from.
+template <int M>
+__global__ __launch_bounds__(64) void pcr_solve_kernel(CrLevel L, double* __restrict__ out, int lim, int* status) {
+  __shared__ __attribute__((aligned(16))) double piv[M * kCrPivot];
+  double a[M];
+  const int lane = threadIdx.x, i = blockIdx.x;
+  const bool ok = gj_wave<M>(L.D + (long long)i * M * M, nullptr, false, L.b + (long long)i * M, M + 1, lane, piv, a);
+  if (!ok) {
+    if (lane == 0) atomicOr(status, 1);
+    return;
+  }
+  if (lane == 2 * M)
+#pragma unroll
+    for (int r = 0; r < M; ++r)
+      if (i * M + r < lim) out[(long long)i * M + r] = a[r];
 }
 
 // The root super-row (the last level): x = D⁻¹ b.
@@ -1836,11 +1863,23 @@ int configure_solver(pba_engine* e, int K, int solver) {
     PBA_HIP(hipMemsetAsync(G.Sband.p, 0, nb_ * sizeof(double), st));  // positions outside the profile stay 0
   }
   G.cr_levels.clear();
+  G.cr_pcr = -1;
   if (solver == SOLVER_CR) {
     const int M = 6 * K;
+    // Parallel cyclic reduction takes over (wave kernel, M = 24) once the rows fit one workgroup per CU:
+    // PBA_PCR_CAP overrides the row limit (0: cyclic reduction only) — the tests force the hybrid with small caps
+    int cap = 0;
+    if (M == 24) {
+      int cus = 0;
+      if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, e->opt.device) != hipSuccess) cus = 0;
+      cap = cus;
+      if (const char* v = std::getenv("PBA_PCR_CAP")) cap = std::atoi(v);
+    }
     std::vector<int> ns{(nf + K - 1) / K};
-    while (ns.back() > 1) ns.push_back((ns.back() + 1) / 2);
-    size_t total = 0;
+    while (ns.back() > (cap > 0 ? cap : 1)) ns.push_back((ns.back() + 1) / 2);
+    if (cap > 0) G.cr_pcr = (int)ns.size() - 1;
+    const int np = cap > 0 ? ns.back() : 0;
+    size_t total = 2 * ((size_t)np * M * M * 2 + (size_t)np * M);
     for (int n : ns) total += (size_t)n * M * M * 2 + (size_t)n * M * 2 + (size_t)(n / 2) * M * (2 * M + 1);
     PBA_HIP(G.cr_buf.resize(total));
     size_t off = 0;
@@ -1853,6 +1892,12 @@ int configure_solver(pba_engine* e, int K, int solver) {
       L.x = off; off += (size_t)n * M;
       L.X = off; off += (size_t)(n / 2) * M * (2 * M + 1);
       G.cr_levels.push_back(L);
+    }
+    for (CrLevelHost& P : G.pcr_bufs) {
+      P.n = np;
+      P.D = off; off += (size_t)np * M * M;
+      P.U = off; off += (size_t)np * M * M;
+      P.b = off; off += (size_t)np * M;
     }
     G.cr0_dirty = true;  // level 0 is set up for assemble_kernel's direct writes on first use
   }
@@ -2243,6 +2288,11 @@ CrLevel cr_level(GnData& G, int l) {
   double* base = G.cr_buf.p;
   return CrLevel{base + h.D, base + h.U, base + h.b, base + h.X, base + h.x, h.n};
 }
+CrLevel pcr_level(GnData& G, int i) {  // PCR ping-pong buffer i (D, U, b of the rows of level G.cr_pcr)
+  const CrLevelHost& h = G.pcr_bufs[i];
+  double* base = G.cr_buf.p;
+  return CrLevel{base + h.D, base + h.U, base + h.b, nullptr, nullptr, h.n};
+}
 
 // Level 0 of the cyclic reduction as assemble_kernel expects it: zeros (positions outside the reduced system's profile
 // are never written), identity diagonal on the padding rows past the last keyframe.
@@ -2276,25 +2326,47 @@ void cr_solve(pba_engine* e, bool build) {
   if (build)
     cr_build_kernel<M><<<(unsigned)((nthreads + 255) / 256), 256, 0, e->stream>>>(G.Sband.p, L0, e->n_frames,
                                                                                   G.band_kernel, G.status.p);
-  for (int l = 0; l + 1 < nl; ++l) {  // one fused launch per level (odd eliminations + even rebuild)
+  // CR levels 0 … c−1 (one fused launch each: odd eliminations + even rebuild); level c is solved either by PCR
+  // levels (G.cr_pcr = c) or, as the last CR level of one row, by the root kernel
+  const int c = G.cr_pcr >= 0 ? G.cr_pcr : nl - 1;
+  for (int l = 0; l < c; ++l) {
     CrLevel L = cr_level(G, l), Ln = cr_level(G, l + 1);
     if constexpr (2 * M + 1 <= 64)
-      cr_level_wave_kernel<M><<<(L.n + 1) / 2, 256, cr_level_wave_lds<M>(), e->stream>>>(L, Ln, G.status.p);
+      cr_level_wave_kernel<M, false><<<(L.n + 1) / 2, 256, cr_level_wave_lds<M>(), e->stream>>>(L, Ln, 1, G.status.p);
     else
       cr_level_kernel<M><<<(L.n + 1) / 2, 2 * kCrOddThreads<M>, cr_level_lds<M>(), e->stream>>>(L, Ln, G.status.p);
   }
-  if constexpr (2 * M + 1 <= 64) cr_root_wave_kernel<M><<<1, 64, 0, e->stream>>>(cr_level(G, nl - 1), G.status.p);
-  else cr_root_kernel<M><<<1, kCrOddThreads<M>, 0, e->stream>>>(cr_level(G, nl - 1), G.status.p);
-  if (nl == 1) {  // a single super-row: the root's x is the step
+  bool solved = false;  // the step vector already written (level c = 0 solved in place)
+  if constexpr (2 * M + 1 <= 64) {
+    if (G.cr_pcr >= 0) {
+      CrLevel src = cr_level(G, c);
+      const int n = src.n;
+      int pi = 0;
+      for (int s = 1; s < n; s *= 2, pi ^= 1) {
+        CrLevel dst = pcr_level(G, pi);
+        cr_level_wave_kernel<M, true><<<n, 256, cr_level_wave_lds<M>(), e->stream>>>(src, dst, s, G.status.p);
+        src = dst;
+      }
+      solved = c == 0;
+      pcr_solve_kernel<M><<<n, 64, 0, e->stream>>>(src, solved ? G.x.p : cr_level(G, c).x,
+                                                   solved ? 6 * e->n_frames : n * M, G.status.p);
+    } else {
+      cr_root_wave_kernel<M><<<1, 64, 0, e->stream>>>(cr_level(G, nl - 1), G.status.p);
+    }
+  } else {
+    cr_root_kernel<M><<<1, kCrOddThreads<M>, 0, e->stream>>>(cr_level(G, nl - 1), G.status.p);
+  }
+  if (solved) return;
+  if (c == 0) {  // a single super-row: the root's x is the step
     (void)hipMemcpyAsync(G.x.p, L0.x, sizeof(double) * 6 * e->n_frames, hipMemcpyDeviceToDevice, e->stream);
     return;
   }
   CrLevels C{};
   C.nl = nl;
   for (int l = 0; l < nl; ++l) C.lv[l] = cr_level(G, l);
-  int lo = nl - 2;  // the tail: levels with at most kCrTailRows super-rows
+  int lo = c;  // the tail: levels c−1 … lo with at most kCrTailRows super-rows, in one workgroup
   while (lo > 0 && C.lv[lo - 1].n <= kCrTailRows) --lo;
-  cr_back_tail_kernel<M><<<1, 1024, 0, e->stream>>>(C, nl - 2, lo, G.x.p, e->n_frames);
+  if (lo <= c - 1) cr_back_tail_kernel<M><<<1, 1024, 0, e->stream>>>(C, c - 1, lo, G.x.p, e->n_frames);
   for (int l = lo - 1; l >= 0; --l) {
     const int lim = l == 0 ? 6 * e->n_frames : C.lv[l].n * M;
     cr_back_kernel<M><<<(lim + 255) / 256, 256, 0, e->stream>>>(C.lv[l], C.lv[l + 1].x, l == 0 ? G.x.p : C.lv[l].x, lim);

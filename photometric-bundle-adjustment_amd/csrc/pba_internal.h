@@ -28,7 +28,7 @@ struct alignas(16) PairRec {
   double hk[kCamK];            // host camera, unprojection layout [cx cy 1/fx 1/fy p1 p2 p3 p4]
   double tk[kCamK];            // target camera, projection layout [fx fy cx cy p1 p2 p3 p4]
   float Rf[9], tf[3];          // fp32 R_th, t_th (Jacobian chain)
-  float pad[8];
+  float kf[8];                 // target camera, fp32 [fx fy 0 0 p1 p2 p3 p4] (projection Jacobian)
 };
 static_assert(sizeof(PairRec) == 320, "PairRec layout");
 static_assert(offsetof(PairRec, hk) % 16 == 0 && offsetof(PairRec, tk) == offsetof(PairRec, hk) + 8 * kCamK,
@@ -74,8 +74,22 @@ __device__ __forceinline__ void pair_translation(const double* __restrict__ H, c
     r.t[j] = tt[j];
     r.tf[j] = (float)tt[j];
   }
+}
+// fp32 projection constants of the Jacobian chain from the fp64 projection layout (cx, cy unused there)
+__device__ __forceinline__ void camera_kf(const double* __restrict__ tk, float* kf) {
+  kf[0] = (float)tk[0];
+  kf[1] = (float)tk[1];
+  kf[2] = 0.0f;
+  kf[3] = 0.0f;
 #pragma unroll
-  for (int j = 0; j < 8; ++j) r.pad[j] = 0.0f;
+  for (int j = 4; j < 8; ++j) kf[j] = (float)tk[j];
+}
+// the same from the 16-B part q ∈ [0, 4) of tk (tk[2q], tk[2q+1]) as one lane holds it in a tile prologue
+__device__ __forceinline__ void camera_kf_part(const uint4& part, int q, float* kf) {
+  const float2 v = q == 1 ? make_float2(0.0f, 0.0f)
+                          : make_float2((float)__hiloint2double((int)part.y, (int)part.x),
+                                        (float)__hiloint2double((int)part.w, (int)part.z));
+  reinterpret_cast<float2*>(kf)[q] = v;
 }
 __device__ __forceinline__ void pair_cameras(const double* __restrict__ cams, int h, int t, int hc, int tc,
                                              PairRec& r) {
@@ -90,6 +104,7 @@ __device__ __forceinline__ void pair_cameras(const double* __restrict__ cams, in
     r.hk[j] = hk[j];
     r.tk[j] = tk[j];
   }
+  camera_kf(tk, r.kf);
 }
 __device__ __forceinline__ void form_pair(const double* __restrict__ poses, const int* __restrict__ frame_cam,
                                           const double* __restrict__ cams, int h, int t, PairRec& r) {
@@ -254,6 +269,7 @@ __device__ __forceinline__ int stage_tile(const KernelArgs& a, TileBlock* s_tb, 
     for (int j = 0; j < 7; ++j) asm volatile("" ::"v"(h[j]), "v"(t[j]));
     PairRec& pr = s_tb[lb].pr;
     if (k < 8) dst[(int)(offsetof(PairRec, hk) / 16) + k] = cam;
+    if (k >= 4 && k < 8) camera_kf_part(cam, k - 4, pr.kf);
     if (k == 0) {
       pair_rotation(h, t, pr);
     } else if (k == 1) {
@@ -285,6 +301,68 @@ __device__ __forceinline__ int stage_tile(const KernelArgs& a, TileBlock* s_tb, 
     dst[part] = v;
   }
   return pp.x;
+}
+
+// Fused state, workgroup-cooperative form for 256-thread workgroups of 32 blocks: the four waves split the 32
+// blocks' prologue by part instead of each wave staging its own 8 blocks — wave 0 forms R_th of all 32 (lane b < 32),
+// wave 1 t_th and the ids, wave 2 copies the cameras' constants (lanes 0-31 the host part, 32-63 the target part
+// with its fp32 copy), wave 3 the point data (lanes 0-31 u_ref, 32-63 ρ).  The fp64 relative-pose arithmetic is then
+// issued once per workgroup instead of once per wave (SIMT: a wave pays for every branch any of its lanes takes, so
+// the rotation and translation branches of stage_tile cost each of the four waves both).  The caller barriers.
+__device__ __forceinline__ void stage_tile_wg(const KernelArgs& a, TileBlock* s_tb, int blk0) {
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, b = lane & 31;
+  const int4 br = a.block_rec[min(blk0 + b, a.n_blocks - 1)];  // a dead block stages the last block
+  PairRec& pr = s_tb[b].pr;
+  uint4* dst = reinterpret_cast<uint4*>(s_tb + b);
+  if (w == 0) {
+    if (lane < 32) {
+      const double* H = a.poses + 7 * br.y;
+      const double* T = a.poses + 7 * br.z;
+      double h[4], t[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        h[j] = H[j];
+        t[j] = T[j];
+      }
+      pair_rotation(h, t, pr);
+    }
+  } else if (w == 1) {
+    if (lane < 32) {
+      const double* H = a.poses + 7 * br.y;
+      const double* T = a.poses + 7 * br.z;
+      double h[7], t[7];
+#pragma unroll
+      for (int j = 0; j < 7; ++j) {
+        h[j] = H[j];
+        t[j] = T[j];
+      }
+      pair_translation(h, t, pr);
+      pr.host_cam = br.w >> 16;
+      pr.target_cam = br.w & 0xffff;
+      pr.target = br.z;
+      pr.host = br.y;
+    }
+  } else if (w == 2) {
+    const bool tgt = lane >= 32;
+    const uint4* src = reinterpret_cast<const uint4*>(a.intr_d + (tgt ? kCamD * (br.w & 0xffff) : kCamD * (br.w >> 16) + kCamHk));
+    uint4 c[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) c[q] = src[q];
+    uint4* d = dst + (int)(offsetof(PairRec, hk) / 16) + (tgt ? 4 : 0);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) d[q] = c[q];
+    if (tgt) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) camera_kf_part(c[q], q, pr.kf);
+    }
+  } else {
+    if (lane < 32) {
+      dst[kPairParts] = reinterpret_cast<const uint4*>(a.u_ref)[br.x];
+    } else {
+      const double rho = a.rho[br.x];
+      dst[kPairParts + 1] = make_uint4(__double2loint(rho), __double2hiint(rho), (unsigned)br.x, 0u);
+    }
+  }
 }
 
 // The launch that evaluates at a caller's state also adopts it: one element per lane (grid ≥ frames·7, points).
@@ -326,10 +404,8 @@ __device__ __forceinline__ Row photometric_row(const KernelArgs& a, const TileBl
   if (JAC && dom) {
     // q = ∇I · ∂π/∂p̃ (1×3)
     const Vec3 pf = to_f(p), bf = to_f(b);
-    const float kf[8] = {(float)pp.tk[0], (float)pp.tk[1], 0.0f, 0.0f,
-                         (float)pp.tk[4], (float)pp.tk[5], (float)pp.tk[6], (float)pp.tk[7]};
     Vec3 du, dv;
-    project_jac<MODEL>(kf, pf, (float)iden, du, dv);
+    project_jac<MODEL>(pp.kf, pf, (float)iden, du, dv);
     const Vec3 q = {gx * du.x + gy * dv.x, gx * du.y + gy * dv.y, gx * du.z + gy * dv.z};
     const Vec3 qR = row_mul(q, pp.Rf);
     const float rf = (float)rho;
@@ -472,6 +548,8 @@ struct GnData {
   int lpb = 8, bpw = 32;
   int n_chunks = 0, n_schur = 0, n_gn_points = 0, n_sky = 0, band = 0, band_kernel = 0, solver = 0;
   std::vector<CrLevelHost> cr_levels;  // block-cyclic-reduction level layout (offsets into cr_buf)
+  int cr_pcr = -1;                     // the CR level whose rows parallel cyclic reduction solves (-1: root kernel)
+  CrLevelHost pcr_bufs[2];             // PCR ping-pong buffers (D, U, b) for that level's rows
   DevBuf<double> cr_buf;
   bool force_skyline = false;
   size_t lin_floats = 0, schur_doubles = 0, schur_lds = 0;
