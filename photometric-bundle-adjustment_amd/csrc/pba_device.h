@@ -256,10 +256,10 @@ struct Taps {
   double fu, fv;       // cell fractions u − ⌊u⌋, v − ⌊v⌋ (fp64: the gradient needs them exactly)
   float I00, I10, I01, I11;
 };
-__device__ __forceinline__ Taps bilinear_taps(const uint8_t* __restrict__ img, int W, int H, int tiles_x, double u,
-                                              double v) {
-  u = fmin(fmax(u, -2.0), (double)W + 1.0);  // NaN positions clamp to −2 (maxNum): always an in-bounds read
-  v = fmin(fmax(v, -2.0), (double)H + 1.0);
+__device__ __forceinline__ Taps bilinear_taps(const uint8_t* __restrict__ img, double umax, double vmax, int tiles_x,
+                                              double u, double v) {
+  u = fmin(fmax(u, -2.0), umax);  // NaN positions clamp to −2 (maxNum): always an in-bounds read
+  v = fmin(fmax(v, -2.0), vmax);
   const double xf = floor(u), yf = floor(v);
   const int xp = (int)xf + kImgPad, yp = (int)yf + kImgPad;  // ∈ [2, W+5] × [2, H+5]
   const unsigned i00 = texel_index(xp, yp, tiles_x);
@@ -285,9 +285,9 @@ __device__ __forceinline__ void bilinear_eval(const Taps& t, float& I, float& gx
   gx = (float)fma(t.fv, (double)((t.I11 - t.I01) - (t.I10 - t.I00)), (double)(t.I10 - t.I00));
   gy = (float)fma(t.fu, (double)((t.I11 - t.I10) - (t.I01 - t.I00)), (double)(t.I01 - t.I00));
 }
-__device__ __forceinline__ void bilinear(const uint8_t* __restrict__ img, int W, int H, int tiles_x, double u,
-                                         double v, float& I, float& gx, float& gy) {
-  bilinear_eval(bilinear_taps(img, W, H, tiles_x, u, v), I, gx, gy);
+__device__ __forceinline__ void bilinear(const uint8_t* __restrict__ img, double umax, double vmax, int tiles_x,
+                                         double u, double v, float& I, float& gx, float& gy) {
+  bilinear_eval(bilinear_taps(img, umax, vmax, tiles_x, u, v), I, gx, gy);
 }
 
 // Ceres' BiCubicInterpolator over Grid2D<uint8_t, 1> (cubic_interpolation.h:252-344, the interpolator of
@@ -304,10 +304,10 @@ __device__ __forceinline__ void hermite(double p0, double p1, double p2, double 
   f = d + x * (c + x * (b + x * a));
   df = c + x * (2.0 * b + 3.0 * a * x);
 }
-__device__ __forceinline__ void bicubic(const uint8_t* __restrict__ img, int W, int H, int tiles_x, double u, double v,
-                                        float& I, float& gx, float& gy) {
-  u = fmin(fmax(u, -2.0), (double)W + 1.0);
-  v = fmin(fmax(v, -2.0), (double)H + 1.0);
+__device__ __forceinline__ void bicubic(const uint8_t* __restrict__ img, double umax, double vmax, int tiles_x, double u,
+                                        double v, float& I, float& gx, float& gy) {
+  u = fmin(fmax(u, -2.0), umax);
+  v = fmin(fmax(v, -2.0), vmax);
   const double xf = floor(u), yf = floor(v);
   const int xp = (int)xf + kImgPad, yp = (int)yf + kImgPad;  // taps xp−1 … xp+2 ∈ [1, W+7]: inside the apron
   const double x = u - xf, y = v - yf;
@@ -333,11 +333,12 @@ enum : int { INTERP_BILINEAR = 0, INTERP_BICUBIC = 1 };
 __host__ __device__ constexpr int cam_of(int pm) { return pm & 3; }
 __host__ __device__ constexpr int interp_of(int pm) { return pm >> 2; }
 
+// umax, vmax = W + 1, H + 1: the interpolation clamp [−2, W+1] × [−2, H+1] (kernel arguments, not per-lane work)
 template <int INTERP>
-__device__ __forceinline__ void interpolate(const uint8_t* __restrict__ img, int W, int H, int tiles_x, double u, double v,
-                                            float& I, float& gx, float& gy) {
-  if (INTERP == INTERP_BICUBIC) bicubic(img, W, H, tiles_x, u, v, I, gx, gy);
-  else bilinear(img, W, H, tiles_x, u, v, I, gx, gy);
+__device__ __forceinline__ void interpolate(const uint8_t* __restrict__ img, double umax, double vmax, int tiles_x,
+                                            double u, double v, float& I, float& gx, float& gy) {
+  if (INTERP == INTERP_BICUBIC) bicubic(img, umax, vmax, tiles_x, u, v, I, gx, gy);
+  else bilinear(img, umax, vmax, tiles_x, u, v, I, gx, gy);
 }
 
 }  // namespace pba

@@ -231,7 +231,13 @@ __global__ __launch_bounds__((kMultiThreads<PPL, T>)) void photometric_block_ker
 
   if ((int)threadIdx.x < P) s_pat[threadIdx.x] = make_float2(a.pattern[2 * threadIdx.x], a.pattern[2 * threadIdx.x + 1]);
   adopt_state(a);
-  const int pt = stage_tile<LPB>(a, s_tb, lb, k, blk, live);
+  int pt;
+  if (NTH == 256 && a.poses) {  // fused state: the workgroup-cooperative prologue (BPW = 32)
+    pt = a.block_rec[live ? blk : a.n_blocks - 1].x;
+    stage_tile_wg(a, s_tb, blk0);
+  } else {
+    pt = stage_tile<LPB>(a, s_tb, lb, k, blk, live);
+  }
   float Ih[PPL];
 #pragma unroll
   for (int j = 0; j < PPL; ++j) {
@@ -451,6 +457,8 @@ KernelArgs make_kernel_args(pba_engine* e, const PairRec* pairs, const double* r
   ka.height = e->height;
   ka.tiles_x = tiles_x_of(e->width);
   ka.frame_stride = tiled_frame_bytes(e->width, e->height);
+  ka.umax = e->width + 1.0;
+  ka.vmax = e->height + 1.0;
   ka.intr = e->intr.p;
   ka.intr_d = e->intr_d.p;
   ka.block_point = e->block_point.p;

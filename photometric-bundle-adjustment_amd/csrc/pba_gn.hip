@@ -1255,14 +1255,30 @@ template <int M, int PB = kCrPivot>
 __device__ __forceinline__ bool gj_wave(const double* __restrict__ D, const double* __restrict__ R1, bool r1_trans,
                                         const double* __restrict__ b, int ncol, int c, double* piv, double* a) {
   static_assert(M % PB == 0, "pivot blocks tile the system");
-#pragma unroll
-  for (int r = 0; r < M; ++r) {
-    const double* src = nullptr;
-    if (c < M) src = D + r * M + c;
-    else if (c < 2 * M) src = R1 ? (r1_trans ? R1 + (c - M) * M + r : R1 + r * M + (c - M)) : nullptr;
-    else if (c < M + ncol) src = b ? b + r : nullptr;
-    a[r] = src ? *src : 0.0;
+  // column c of [D | R1 | b] as base + r·stride: one address choice per lane, then M unconditional loads in flight
+  // together (a lane without a column reads D's and keeps zeros)
+  const double* base = D + min(c, M - 1);
+  int stride = M;
+  bool zero = c >= M + ncol;
+  if (c >= M && c < 2 * M) {
+    if (R1) {
+      base = r1_trans ? R1 + (c - M) * M : R1 + (c - M);
+      stride = r1_trans ? 1 : M;
+    } else {
+      zero = true;
+    }
+  } else if (c >= 2 * M && c < M + ncol) {
+    if (b) {
+      base = b;
+      stride = 1;
+    } else {
+      zero = true;
+    }
   }
+#pragma unroll
+  for (int r = 0; r < M; ++r) a[r] = base[r * stride];
+#pragma unroll
+  for (int r = 0; r < M; ++r) a[r] = zero ? 0.0 : a[r];
   bool bad = false;
 #pragma unroll
   for (int k = 0; k < M; k += PB) {
@@ -1344,14 +1360,29 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   const int il = i - s, ir = i + s;
   const bool left = il >= 0, right = ir < L.n;
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+#ifdef PBA_CR_STAMPS
+  long long t0 = wall_clock64(), t1 = 0, t2 = 0;
+#endif
   if (w == 3) {
-    for (int e = lane; e < 3 * M * M + M; e += 64) {
-      const double* src = nullptr;
-      if (e < M * M) src = left ? L.U + (long long)il * M * M + e : nullptr;
-      else if (e < 2 * M * M) src = right ? L.U + (long long)i * M * M + (e - M * M) : nullptr;
+    // U_l, U_i, D_i, b_i → LDS: every load in flight at once (a loop of load → LDS store pays one memory round trip
+    // per element, serially: measured ~10 µs of a 12.4-µs level); missing neighbours read U_i and store zeros
+    constexpr int NE = 3 * M * M + M, NQ = (NE + 63) / 64;
+    double v[NQ];
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      const int e = lane + 64 * q;
+      const double* src = L.b + (long long)i * M;
+      if (e < M * M) src = L.U + (long long)(left ? il : i) * M * M + e;
+      else if (e < 2 * M * M) src = L.U + (long long)i * M * M + (e - M * M);
       else if (e < 3 * M * M) src = L.D + (long long)i * M * M + (e - 2 * M * M);
-      else src = L.b + (long long)i * M + (e - 3 * M * M);
-      smem[e] = src ? *src : 0.0;
+      else if (e < NE) src = L.b + (long long)i * M + (e - 3 * M * M);
+      v[q] = *src;
+    }
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      const int e = lane + 64 * q;
+      const bool zero = (e < M * M && !left) || (e >= M * M && e < 2 * M * M && !right);
+      if (e < NE) smem[e] = zero ? 0.0 : v[q];
     }
   } else {
     const int j = w == 0 ? il : ir;
@@ -1377,7 +1408,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       }
     }
   }
+#ifdef PBA_CR_STAMPS
+  t1 = wall_clock64();
+#endif
   __syncthreads();
+#ifdef PBA_CR_STAMPS
+  t2 = wall_clock64();
+#endif
   // Rebuild of row i on the matrix cores: [D' | U' | b'] = [D | 0 | b] − U_{i−1}ᵀ·[X^U_{i−1} | 0 | X^b_{i−1}]
   // − U_i·X_{i+1}, as 2 × 4 output tiles of v_mfma_f64_16x16x4f64 (rows padded to 32, columns to 64).  Wave w takes
   // row tile w & 1 and column tiles 2(w >> 1) + {0, 1}: the two tiles share the A operands and run as two
@@ -1425,6 +1462,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         else if (c == 2 * M) Ln.b[(long long)in * M + r] = acc[h][v];
       }
     }
+#ifdef PBA_CR_STAMPS
+  __syncthreads();
+  const long long t3 = wall_clock64();
+  if (blockIdx.x == 5 && lane == 0)
+    printf("crstamp s=%d w=%d phase_end_us %.2f barrier_us %.2f rebuild_us %.2f\n", s, w, (t1 - t0) * 0.01,
+           (t2 - t0) * 0.01, (t3 - t0) * 0.01);
+#endif
 }
 
 // The root super-row on one wave (lane 2M carries b; the coupling lanes are empty).

@@ -118,7 +118,7 @@ struct alignas(16) TileBlock {
   PairRec pr;
   double2 ur;                  // u_ref (host pixel)
   double rho;                  // inverse distance (state)
-  int point, pad;
+  long long img;               // byte offset of the target's tiled image (target · frame_stride)
 };
 static_assert(sizeof(TileBlock) == 352, "TileBlock layout");
 constexpr int kPairParts = sizeof(PairRec) / 16;     // 20 × 16 B
@@ -128,6 +128,7 @@ struct KernelArgs {
   const uint8_t* images;
   int width, height, tiles_x;
   long long frame_stride;        // bytes per tiled frame
+  double umax, vmax;             // interpolation clamp bounds W + 1, H + 1
   const float* intr;             // 8 floats per camera (Jacobian chain)
   const double* intr_d;          // kCamD doubles per camera (warp / projection; pba_device.h)
   const int* block_point;
@@ -281,7 +282,8 @@ __device__ __forceinline__ int stage_tile(const KernelArgs& a, TileBlock* s_tb, 
     } else if (k == 2) {
       dst[kPairParts] = ur;
     } else if (k == 3) {
-      dst[kPairParts + 1] = make_uint4(__double2loint(rho), __double2hiint(rho), (unsigned)br.x, 0u);
+      const long long img = (long long)br.z * a.frame_stride;
+      dst[kPairParts + 1] = make_uint4(__double2loint(rho), __double2hiint(rho), (unsigned)img, (unsigned)(img >> 32));
     }
     return br.x;
   }
@@ -296,7 +298,8 @@ __device__ __forceinline__ int stage_tile(const KernelArgs& a, TileBlock* s_tb, 
       v = reinterpret_cast<const uint4*>(a.u_ref)[pp.x];
     } else {
       const double r = a.rho[pp.x];
-      v = make_uint4(__double2loint(r), __double2hiint(r), (unsigned)pp.x, 0u);
+      const long long img = (long long)a.pairs[pp.y].target * a.frame_stride;
+      v = make_uint4(__double2loint(r), __double2hiint(r), (unsigned)img, (unsigned)(img >> 32));
     }
     dst[part] = v;
   }
@@ -360,7 +363,8 @@ __device__ __forceinline__ void stage_tile_wg(const KernelArgs& a, TileBlock* s_
       dst[kPairParts] = reinterpret_cast<const uint4*>(a.u_ref)[br.x];
     } else {
       const double rho = a.rho[br.x];
-      dst[kPairParts + 1] = make_uint4(__double2loint(rho), __double2hiint(rho), (unsigned)br.x, 0u);
+      const long long img = (long long)br.z * a.frame_stride;
+      dst[kPairParts + 1] = make_uint4(__double2loint(rho), __double2hiint(rho), (unsigned)img, (unsigned)(img >> 32));
     }
   }
 }
@@ -396,7 +400,7 @@ __device__ __forceinline__ Row photometric_row(const KernelArgs& a, const TileBl
   if (dom) {
     double u, v;
     iden = project<MODEL>(pp.tk, p, u, v);
-    interpolate<interp_of(PM)>(a.images + (long long)pp.target * a.frame_stride, a.width, a.height, a.tiles_x, u, v,
+    interpolate<interp_of(PM)>(a.images + tb.img, a.umax, a.vmax, a.tiles_x, u, v,
                                I, gx, gy);
   }
   o.r = I - Ih;  // photometric_error.h:179

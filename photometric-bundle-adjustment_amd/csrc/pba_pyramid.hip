@@ -60,7 +60,7 @@ __global__ void host_intensity_kernel(const uint8_t* __restrict__ images, long l
   const int pt = (int)(i / P), k = (int)(i - (long long)pt * P);
   const double2 u = u_ref[pt];
   float I, gx, gy;
-  interpolate<INTERP>(images + (long long)host[pt] * frame_stride, W, H, tiles_x_of(W), u.x + (double)pattern[2 * k],
+  interpolate<INTERP>(images + (long long)host[pt] * frame_stride, W + 1.0, H + 1.0, tiles_x_of(W), u.x + (double)pattern[2 * k],
                       u.y + (double)pattern[2 * k + 1], I, gx, gy);
   out[i] = I;
 }
@@ -72,7 +72,7 @@ __global__ void sample_image_kernel(const uint8_t* __restrict__ img, int W, int 
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   float I, gx, gy;
-  interpolate<INTERP>(img, W, H, tiles_x_of(W), uv[i].x, uv[i].y, I, gx, gy);
+  interpolate<INTERP>(img, W + 1.0, H + 1.0, tiles_x_of(W), uv[i].x, uv[i].y, I, gx, gy);
   out[3 * i] = I;
   out[3 * i + 1] = gx;
   out[3 * i + 2] = gy;
