@@ -428,12 +428,28 @@ __global__ __launch_bounds__(kBlockThreads) void schur_kernel(const SchurArgs g,
     const int ca = 16 * ti + (lane & 15), cb = 16 * tj + (lane & 15), kq = lane >> 4;
     const float* Wf = &W[0][0];
     v4f64 acc = {0.0, 0.0, 0.0, 0.0};
-    for (int p0 = 0; p0 < npt; p0 += 4) {
-      const int p = p0 + kq;
-      const bool pin = p < npt;
-      const double av = (pin && ca < nv6) ? (double)Wf[p * nv6 + ca] * s_inv[p] : 0.0;
-      const double bv = !pin ? 0.0 : (cb < nv6 ? (double)Wf[p * nv6 + cb] : (cb == nv6 ? s_gl[p] : 0.0));
-      acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
+    // four K steps per batch: the batch's LDS reads first, at clamped indices with unconditional reads, the padding
+    // zeroed by selects afterwards (conditional reads were issued and waited one step at a time)
+    constexpr int KB = 4;
+    const int cac = min(ca, nv6 - 1), cbc = min(cb, nv6 - 1);
+    for (int p0 = 0; p0 < npt; p0 += 4 * KB) {
+      float wa[KB], wb[KB];
+      double si[KB], sg[KB];
+#pragma unroll
+      for (int u = 0; u < KB; ++u) {
+        const int pc = min(p0 + 4 * u + kq, npt - 1);
+        wa[u] = Wf[pc * nv6 + cac];
+        wb[u] = Wf[pc * nv6 + cbc];
+        si[u] = s_inv[pc];
+        sg[u] = s_gl[pc];
+      }
+#pragma unroll
+      for (int u = 0; u < KB; ++u) {
+        const bool pin = p0 + 4 * u + kq < npt;
+        const double av = (pin && ca < nv6) ? (double)wa[u] * si[u] : 0.0;
+        const double bv = !pin ? 0.0 : (cb < nv6 ? (double)wb[u] : (cb == nv6 ? sg[u] : 0.0));
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
+      }
     }
 #pragma unroll
     for (int v = 0; v < 4; ++v) {
@@ -1289,11 +1305,21 @@ __device__ __forceinline__ bool gj_wave(const double* __restrict__ D, const doub
     }
     __builtin_amdgcn_wave_barrier();
     asm volatile("" ::: "memory");
+    // every pivot row of the step read at once (the pivot block's rows first): the 24·PB broadcast reads are in flight
+    // during the PB×PB solve instead of one or two at a time between the update FMAs (the update was LDS-latency
+    // bound: ~2200 cycles per step)
+    double pr[M][PB];
+#pragma unroll
+    for (int i = 0; i < M; ++i) {
+      const int r = (i + k) % M;
+#pragma unroll
+      for (int j = 0; j < PB; ++j) pr[r][j] = piv[PB * r + j];
+    }
     double P[PB][PB], t[PB];
 #pragma unroll
     for (int i = 0; i < PB; ++i) {
 #pragma unroll
-      for (int j = 0; j < PB; ++j) P[i][j] = piv[PB * (k + i) + j];
+      for (int j = 0; j < PB; ++j) P[i][j] = pr[k + i][j];
       t[i] = a[k + i];
     }
 #pragma unroll
@@ -1319,7 +1345,7 @@ __device__ __forceinline__ bool gj_wave(const double* __restrict__ D, const doub
       } else {
         double v = a[r];
 #pragma unroll
-        for (int j = 0; j < PB; ++j) v -= piv[PB * r + j] * t[j];
+        for (int j = 0; j < PB; ++j) v -= pr[r][j] * t[j];
         a[r] = v;
       }
     }
@@ -1426,27 +1452,54 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   const double* sXr = sX[1];
   const int rt = w & 1;
   const int arow = 16 * rt + (lane & 15), kq = lane >> 4;
+  // every operand of the six K steps read from LDS first, at clamped (in-range) indices and with unconditional reads,
+  // then the padding zeroed by selects: conditional reads were issued and waited one at a time (~2.9 µs per level)
+  constexpr int KS = M / 4;
+  const bool aok = arow < M;
+  const int ar = aok ? arow : 0;
   int bcol[2];
-  v4f64 acc[2];
+  double av2[KS], av1[KS], bv2[2][KS], bv1[2][KS], cv[2][4];
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
     bcol[h] = 16 * ((w >> 1) * 2 + h) + (lane & 15);
+    const int c = bcol[h];
 #pragma unroll
     for (int v = 0; v < 4; ++v) {
-      const int r = 16 * rt + (lane >> 4) + 4 * v, c = bcol[h];
-      acc[h][v] = (r < M) ? (c < M ? sD[r * M + c] : (c == 2 * M ? sb[r] : 0.0)) : 0.0;
+      const int r = 16 * rt + (lane >> 4) + 4 * v;
+      cv[h][v] = c < M ? sD[min(r, M - 1) * M + c] : sb[min(r, M - 1)];
     }
   }
 #pragma unroll
-  for (int s4 = 0; s4 < M / 4; ++s4) {
+  for (int s4 = 0; s4 < KS; ++s4) {
     const int q = 4 * s4 + kq;
-    const double a2 = arow < M ? -sUi[arow * M + q] : 0.0;
-    const double a1 = arow < M ? -sUl[q * M + arow] : 0.0;
+    av2[s4] = sUi[ar * M + q];
+    av1[s4] = sUl[q * M + ar];
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       const int c = bcol[h];
-      const double b2 = c < NC ? sXr[q * NC + c] : 0.0;
-      const double b1 = c < M ? sXl[q * NC + M + c] : (c == 2 * M ? sXl[q * NC + 2 * M] : 0.0);
+      bv2[h][s4] = sXr[q * NC + min(c, NC - 1)];
+      bv1[h][s4] = sXl[q * NC + (c < M ? M + c : 2 * M)];
+    }
+  }
+  v4f64 acc[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int c = bcol[h];
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      const int r = 16 * rt + (lane >> 4) + 4 * v;
+      acc[h][v] = (r < M && (c < M || c == 2 * M)) ? cv[h][v] : 0.0;
+    }
+  }
+#pragma unroll
+  for (int s4 = 0; s4 < KS; ++s4) {
+    const double a2 = aok ? -av2[s4] : 0.0;
+    const double a1 = aok ? -av1[s4] : 0.0;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int c = bcol[h];
+      const double b2 = c < NC ? bv2[h][s4] : 0.0;
+      const double b1 = (c < M || c == 2 * M) ? bv1[h][s4] : 0.0;
       acc[h] = __builtin_amdgcn_mfma_f64_16x16x4f64(a2, b2, acc[h], 0, 0, 0);
       acc[h] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1, acc[h], 0, 0, 0);
     }
