@@ -122,8 +122,9 @@ __device__ __forceinline__ void store_slab(const unsigned char* src, unsigned ch
   }
 }
 
-template <int PM, int LPB, int MODE, class T>  // PM = camera model + 4 · interpolator
-__global__ __launch_bounds__(kBlockThreads) void photometric_block_kernel(const KernelArgs a) {
+template <int PM, int LPB, int MODE, class T, int NTH = kBlockThreads>  // PM = camera model + 4 · interpolator
+__global__ __launch_bounds__(NTH) void photometric_block_kernel(const KernelArgs a) {
+  constexpr int kBlockThreads = NTH;
   constexpr int BPW = kBlockThreads / LPB;  // blocks per workgroup
   constexpr bool JAC = MODE == 1;
   constexpr int kStageBytes = JAC ? BPW * 14 * LPB * (int)sizeof(T) : 0;
@@ -145,9 +146,9 @@ __global__ __launch_bounds__(kBlockThreads) void photometric_block_kernel(const 
   adopt_state(a);
   int pt;
   if (LPB == 8 && a.poses) {  // fused state: the workgroup-cooperative prologue (BPW = 32)
-    static_assert(kBlockThreads == 256, "stage_tile_wg: 4 waves, 32 blocks");
+    static_assert(kBlockThreads == 256 || kBlockThreads == 128, "stage_tile_wg: 4 waves of 32 blocks or 2 of 16");
     pt = a.block_rec[live ? blk : a.n_blocks - 1].x;
-    stage_tile_wg(a, s_tb, blk0);
+    stage_tile_wg<kBlockThreads>(a, s_tb, blk0);
   } else {
     pt = stage_tile<LPB>(a, s_tb, lb, k, blk, live);
   }
@@ -195,7 +196,7 @@ __global__ __launch_bounds__(kBlockThreads) void photometric_block_kernel(const 
   __syncthreads();
   const int nblk = min(BPW, a.n_blocks - blk0);
   if (nblk <= 0) return;
-  store_slab<T>(lds, reinterpret_cast<unsigned char*>(out + (long long)blk0 * rec_f), nblk * rec_f * (int)sizeof(T));
+  store_slab<T, NTH>(lds, reinterpret_cast<unsigned char*>(out + (long long)blk0 * rec_f), nblk * rec_f * (int)sizeof(T));
 }
 
 // Patterns of 9…32 pixels (the 21-px pattern of config C5): still 8 lanes per block, each lane evaluating pixels
@@ -232,9 +233,9 @@ __global__ __launch_bounds__((kMultiThreads<PPL, T>)) void photometric_block_ker
   if ((int)threadIdx.x < P) s_pat[threadIdx.x] = make_float2(a.pattern[2 * threadIdx.x], a.pattern[2 * threadIdx.x + 1]);
   adopt_state(a);
   int pt;
-  if (NTH == 256 && a.poses) {  // fused state: the workgroup-cooperative prologue (BPW = 32)
+  if (a.poses) {  // fused state: the workgroup-cooperative prologue (BPW = 32 or 16)
     pt = a.block_rec[live ? blk : a.n_blocks - 1].x;
-    stage_tile_wg(a, s_tb, blk0);
+    stage_tile_wg<NTH>(a, s_tb, blk0);
   } else {
     pt = stage_tile<LPB>(a, s_tb, lb, k, blk, live);
   }
@@ -392,7 +393,13 @@ void launch_photometric(pba_engine* e, const KernelArgs& ka, int mode) {
   if (e->P <= 8) {
     const int grid = (int)(((long long)e->n_blocks * 8 + kBlockThreads - 1) / kBlockThreads);
     e->last_grid = grid;
-    if (mode == 1 && h) photometric_block_kernel<PM, 8, 1, _Float16><<<grid, kBlockThreads, 0, e->stream>>>(ka);
+    static const bool wg128 = getenv("PBA_BLOCK_WG128") != nullptr;  // A/B experiment
+    if (mode == 1 && !h && wg128) {
+      const int g2 = (int)(((long long)e->n_blocks * 8 + 127) / 128);
+      e->last_grid = g2;
+      photometric_block_kernel<PM, 8, 1, float, 128><<<g2, 128, 0, e->stream>>>(ka);
+    }
+    else if (mode == 1 && h) photometric_block_kernel<PM, 8, 1, _Float16><<<grid, kBlockThreads, 0, e->stream>>>(ka);
     else if (mode == 1) photometric_block_kernel<PM, 8, 1, float><<<grid, kBlockThreads, 0, e->stream>>>(ka);
     else if (mode == 0 && h) photometric_block_kernel<PM, 8, 0, _Float16><<<grid, kBlockThreads, 0, e->stream>>>(ka);
     else if (mode == 0) photometric_block_kernel<PM, 8, 0, float><<<grid, kBlockThreads, 0, e->stream>>>(ka);

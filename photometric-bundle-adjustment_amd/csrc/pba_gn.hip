@@ -105,13 +105,11 @@ __device__ __forceinline__ LmView lm_view(const double* lm) {
 __device__ __forceinline__ double lm_lambda(const LmView& v, double lambda) { return isnan(v.lambda) ? lambda : v.lambda; }
 
 struct LinArgs {
-  const int* lin_block;     // linearise order → block (GN order regrouped by target within each host)
+  const int4* lin_rec;      // chunk slot → {block, point, pair | local target slot << 24, GN position (blk_schur index)}
   float* blk_schur1;        // the second buffer set (device LM loop: the candidate's linearisation goes to the spare)
   float* part_lin1;
   double* wg_red;           // per-chunk (Σ cost, Σ valid) slots, or nullptr
-  const int* lin_gpos;      // linearise order → GN position (blk_schur index)
   const int4* chunk_desc;   // first linearise position, count, n_targets, partial offset (floats)
-  const uint8_t* blk_lt;    // linearise order → local target slot in its chunk
   float* blk_schur;
   float* part_lin;
   int n_chunks;
@@ -177,23 +175,21 @@ void linearize_kernel(const KernelArgs a, const LinArgs g) {
   const bool s1 = (lv.set != 0.0) != g.spare;
   float* const blk_schur = s1 ? g.blk_schur1 : g.blk_schur;
   float* const part_lin = s1 ? g.part_lin1 : g.part_lin;
-  const int first = d.x, count = d.y, n_t = d.z, poff = d.w;
+  const int count = d.y, n_t = d.z, poff = d.w;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int lb = threadIdx.x / LPB, k = threadIdx.x % LPB, wb = lb % BW;
   const bool live = lb < count;
   const int R = KIND == PBA_RESIDUAL_PHOTOMETRIC ? a.P : 2;
   const bool act = live && k < R;
-  int blk = 0, gpos = 0, lt = 0;
+  // the chunk's slots are padded to the workgroup's blocks (dead slots repeat slot 0), so the record is read with the
+  // chunk descriptor, not behind it, and carries the block's point and pair: the tile prologue's loads come next
+  const int4 lr = g.lin_rec[(long long)chunk * (kBlockThreads / LPB) + lb];
+  const int blk = lr.x, gpos = lr.w, lt = (int)((unsigned)lr.z >> 24);
   Row row;
-  if (live) {
-    blk = g.lin_block[first + lb];
-    gpos = g.lin_gpos[first + lb];
-    lt = g.blk_lt[first + lb];
-  }
   if constexpr (KIND == PBA_RESIDUAL_PHOTOMETRIC) {
     TileBlock* s_tb = reinterpret_cast<TileBlock*>(arena[wave]);
     if ((int)threadIdx.x < R) s_pat[threadIdx.x] = make_float2(a.pattern[2 * threadIdx.x], a.pattern[2 * threadIdx.x + 1]);
-    const int pt = stage_tile<LPB>(a, s_tb, wb, k, blk, live);
+    const int pt = stage_tile_pp<LPB>(a, s_tb, wb, k, make_int2(lr.y, lr.z & 0xffffff));
     const float Ih = act ? a.host_int[(long long)pt * R + k] : 0.0f;
     __syncthreads();
     if (act) row = photometric_row<MODEL, true>(a, s_tb[wb], s_pat[k], Ih);
@@ -2206,12 +2202,15 @@ int gn_prepare(pba_engine* e) {
   for (int i = 0; i < nf; ++i) fixed[i] = (i < (int)G.fixed_h.size() && G.fixed_h[i]) || !observed[i];
   // upload
   hipStream_t st = e->stream;
-  std::vector<int> lblk(nb);
-  for (int i = 0; i < nb; ++i) lblk[i] = order[lpos[i]];
-  PBA_HIP(G.lin_block.upload(lblk, st));
-  PBA_HIP(G.lin_gpos.upload(lpos, st));
+  if (e->n_pairs >= (1 << 24)) return fail(PBA_ERR_INVALID_ARGUMENT, "more than 2^24 (host, target) pairs");
+  std::vector<int4> lrec((size_t)G.n_chunks * G.bpw);
+  for (int c = 0; c < G.n_chunks; ++c)
+    for (int s = 0; s < G.bpw; ++s) {
+      const int i = cdesc[c].x + (s < cdesc[c].y ? s : 0), b = order[lpos[i]];
+      lrec[(size_t)c * G.bpw + s] = make_int4(b, e->block_point_h[b], e->pair_of_h[b] | ((int)blt[i] << 24), lpos[i]);
+    }
+  PBA_HIP(G.lin_rec.upload(lrec, st));
   PBA_HIP(G.chunk_desc.upload(cdesc, st));
-  PBA_HIP(G.blk_lt.upload(blt, st));
   PBA_HIP(G.blk_schur.resize((size_t)nb * 16));
   PBA_HIP(G.part_lin.resize(std::max<size_t>(G.lin_floats, 1)));
   PBA_HIP(G.blk_schur1.resize((size_t)nb * 16));  // the device LM loop's second linearisation set
@@ -2370,8 +2369,7 @@ int linearize(pba_engine* e, double* cost, const double* lm = nullptr, const Pai
     pairs = e->pairs.p;
   }
   const KernelArgs ka = make_kernel_args(e, pairs, rho ? rho : e->rho.p);
-  LinArgs la{G.lin_block.p, G.blk_schur1.p, G.part_lin1.p, wg_red, G.lin_gpos.p, G.chunk_desc.p, G.blk_lt.p,
-             G.blk_schur.p, G.part_lin.p, G.n_chunks, lm ? lm : G.lm_idle.p, lm != nullptr};
+  LinArgs la{G.lin_rec.p, G.blk_schur1.p, G.part_lin1.p, wg_red, G.chunk_desc.p, G.blk_schur.p, G.part_lin.p, G.n_chunks, lm ? lm : G.lm_idle.p, lm != nullptr};
   if (e->opt.residual_kind == PBA_RESIDUAL_PHOTOMETRIC) launch_linearize_photometric(e, ka, la);
   else launch_linearize_geometric(e, ka, la);
   PBA_HIP(hipGetLastError());

@@ -240,6 +240,8 @@ struct Row {
 // loading the record and the point data itself — or, with a.poses set, form the pair record from the state
 // (no pair-table launch before the evaluation).  Returns the block's point.  The caller barriers.
 template <int LPB>
+__device__ __forceinline__ int stage_tile_pp(const KernelArgs& a, TileBlock* s_tb, int lb, int k, int2 pp);
+template <int LPB>
 __device__ __forceinline__ int stage_tile(const KernelArgs& a, TileBlock* s_tb, int lb, int k, int blk, bool live) {
   // a dead block (past the end of the problem) stages the last block, so every lane evaluates valid data
   uint4* dst = reinterpret_cast<uint4*>(s_tb + lb);
@@ -287,7 +289,13 @@ __device__ __forceinline__ int stage_tile(const KernelArgs& a, TileBlock* s_tb, 
     }
     return br.x;
   }
-  const int2 pp = a.block_pp[live ? blk : a.n_blocks - 1];
+  return stage_tile_pp<LPB>(a, s_tb, lb, k, a.block_pp[live ? blk : a.n_blocks - 1]);
+}
+
+// Table path with the block's {point, pair} already in hand (linearize_kernel reads it with its linearise record).
+template <int LPB>
+__device__ __forceinline__ int stage_tile_pp(const KernelArgs& a, TileBlock* s_tb, int lb, int k, int2 pp) {
+  uint4* dst = reinterpret_cast<uint4*>(s_tb + lb);
   const uint4* src = reinterpret_cast<const uint4*>(a.pairs + pp.y);
 #pragma unroll
   for (int part = k; part < kTileParts; part += LPB) {
@@ -312,7 +320,69 @@ __device__ __forceinline__ int stage_tile(const KernelArgs& a, TileBlock* s_tb, 
 // with its fp32 copy), wave 3 the point data (lanes 0-31 u_ref, 32-63 ρ).  The fp64 relative-pose arithmetic is then
 // issued once per workgroup instead of once per wave (SIMT: a wave pays for every branch any of its lanes takes, so
 // the rotation and translation branches of stage_tile cost each of the four waves both).  The caller barriers.
-__device__ __forceinline__ void stage_tile_wg(const KernelArgs& a, TileBlock* s_tb, int blk0) {
+// 128-thread workgroups (16 blocks, two waves): wave 0 forms R_th (lanes 0-15) and copies the point data (u_ref on
+// lanes 16-31, ρ on 32-47), wave 1 forms t_th and the ids (lanes 0-15) and copies the cameras' constants (host part on
+// lanes 16-31, target part with its fp32 copy on 32-47): each wave pays one fp64 branch plus copies.
+template <int NTH>
+__device__ __forceinline__ void stage_tile_wg(const KernelArgs& a, TileBlock* s_tb, int blk0);
+template <>
+__device__ __forceinline__ void stage_tile_wg<128>(const KernelArgs& a, TileBlock* s_tb, int blk0) {
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, b = lane & 15, part = lane >> 4;
+  const int4 br = a.block_rec[min(blk0 + b, a.n_blocks - 1)];  // a dead block stages the last block
+  PairRec& pr = s_tb[b].pr;
+  uint4* dst = reinterpret_cast<uint4*>(s_tb + b);
+  if (part == 3) return;
+  if (w == 0) {
+    if (part == 0) {
+      const double* H = a.poses + 7 * br.y;
+      const double* T = a.poses + 7 * br.z;
+      double h[4], t[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        h[j] = H[j];
+        t[j] = T[j];
+      }
+      pair_rotation(h, t, pr);
+    } else if (part == 1) {
+      dst[kPairParts] = reinterpret_cast<const uint4*>(a.u_ref)[br.x];
+    } else {
+      const double rho = a.rho[br.x];
+      const long long img = (long long)br.z * a.frame_stride;
+      dst[kPairParts + 1] = make_uint4(__double2loint(rho), __double2hiint(rho), (unsigned)img, (unsigned)(img >> 32));
+    }
+  } else {
+    if (part == 0) {
+      const double* H = a.poses + 7 * br.y;
+      const double* T = a.poses + 7 * br.z;
+      double h[7], t[7];
+#pragma unroll
+      for (int j = 0; j < 7; ++j) {
+        h[j] = H[j];
+        t[j] = T[j];
+      }
+      pair_translation(h, t, pr);
+      pr.host_cam = br.w >> 16;
+      pr.target_cam = br.w & 0xffff;
+      pr.target = br.z;
+      pr.host = br.y;
+    } else {
+      const bool tgt = part == 2;
+      const uint4* src = reinterpret_cast<const uint4*>(a.intr_d + (tgt ? kCamD * (br.w & 0xffff) : kCamD * (br.w >> 16) + kCamHk));
+      uint4 c[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) c[q] = src[q];
+      uint4* d = dst + (int)(offsetof(PairRec, hk) / 16) + (tgt ? 4 : 0);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) d[q] = c[q];
+      if (tgt) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) camera_kf_part(c[q], q, pr.kf);
+      }
+    }
+  }
+}
+template <>
+__device__ __forceinline__ void stage_tile_wg<256>(const KernelArgs& a, TileBlock* s_tb, int blk0) {
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, b = lane & 31;
   const int4 br = a.block_rec[min(blk0 + b, a.n_blocks - 1)];  // a dead block stages the last block
   PairRec& pr = s_tb[b].pr;
@@ -557,10 +627,10 @@ struct GnData {
   DevBuf<double> cr_buf;
   bool force_skyline = false;
   size_t lin_floats = 0, schur_doubles = 0, schur_lds = 0;
-  DevBuf<int> lin_block;         // linearise order (GN order regrouped by target within each host) → block
-  DevBuf<int> lin_gpos;          // linearise order → GN position
+  // linearise order (GN order regrouped by target within each host), bpw slots per chunk (a chunk's dead slots
+  // repeat its first block): {block, point, pair | local target slot << 24, GN position}
+  DevBuf<int4> lin_rec;
   DevBuf<int4> chunk_desc;       // linearise chunk: first linearise position, count, n_targets, partial offset
-  DevBuf<uint8_t> blk_lt;        // linearise position → local target slot in its chunk
   DevBuf<float> blk_schur;       // GN block → 16 floats [Hll gl Wh(6) Wt(6) 0 0]
   DevBuf<float> part_lin;        // linearise chunk partials (fp32)
   DevBuf<float> blk_schur1, part_lin1;  // second set: the device LM loop linearises each candidate into the spare
