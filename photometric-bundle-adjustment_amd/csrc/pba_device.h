@@ -52,23 +52,21 @@ __device__ __forceinline__ V3<S> mat_mul(const T* R, const V3<S>& b) {
           (S)R[6] * b.x + (S)R[7] * b.y + (S)R[8] * b.z};
 }
 
-// Reciprocal / reciprocal square root to ~1 ulp in fp64: hardware v_rcp_f64 / v_rsq_f64 seed + two Newton
-// steps.  The IEEE division and sqrt() sequences the compiler emits otherwise (div_scale / div_fmas /
-// div_fixup, ldexp range scaling) were ~15% of the block kernel's VALU instructions.  Arguments here are
-// finite and far from the denormal range (focal lengths, depths inside the projection domain, |b|² ≈ 1).
+// Reciprocal / reciprocal square root to ~1 ulp in fp64: hardware v_rcp_f64 / v_rsq_f64 seed + ONE third-order
+// correction (relative seed error e ≲ 2⁻²² → e³ ≲ 2⁻⁶⁶): 1/x = y(1 + e + e²) with e = 1 − xy, 1/√x = y(1 + e/2 +
+// 3e²/8) with e = 1 − xy² — 2 and 4 fp64 operations after the seed instead of the 4 and 6 of two Newton steps.  The
+// IEEE division and sqrt() sequences the compiler emits otherwise (div_scale / div_fmas / div_fixup, ldexp range
+// scaling) were ~15% of the block kernel's VALU instructions.  Arguments here are finite and far from the denormal
+// range (focal lengths, depths inside the projection domain, |b|² ≈ 1, SPD pivots).
 __device__ __forceinline__ double rcp_nr(double x) {
-  double y = __builtin_amdgcn_rcp(x);
-  double e = fma(-x, y, 1.0);
-  y = fma(y, e, y);
-  e = fma(-x, y, 1.0);
-  return fma(y, e, y);
+  const double y = __builtin_amdgcn_rcp(x);
+  const double e = fma(-x, y, 1.0);
+  return fma(y, fma(e, e, e), y);
 }
 __device__ __forceinline__ double rsqrt_nr(double x) {
-  double y = __builtin_amdgcn_rsq(x);
-  double e = fma(-x * y, y, 1.0);
-  y = fma(0.5 * y, e, y);
-  e = fma(-x * y, y, 1.0);
-  return fma(0.5 * y, e, y);
+  const double y = __builtin_amdgcn_rsq(x);
+  const double e = fma(-x * y, y, 1.0);
+  return fma(y * e, fma(e, 0.375, 0.5), y);
 }
 __device__ __forceinline__ float rcp_s(float x) { return __builtin_amdgcn_rcpf(x); }  // 1 ulp (fp32 chain)
 __device__ __forceinline__ double rcp_s(double x) { return rcp_nr(x); }

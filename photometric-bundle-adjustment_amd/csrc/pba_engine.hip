@@ -130,7 +130,6 @@ __global__ __launch_bounds__(NTH) void photometric_block_kernel(const KernelArgs
   constexpr int kStageBytes = JAC ? BPW * 14 * LPB * (int)sizeof(T) : 0;
   constexpr int kTileBytes = BPW * (int)sizeof(TileBlock);
   __shared__ __attribute__((aligned(16))) unsigned char lds[kStageBytes > kTileBytes ? kStageBytes : kTileBytes];
-  __shared__ float2 s_pat[LPB];
   TileBlock* s_tb = reinterpret_cast<TileBlock*>(lds);
   const int P = a.P;
   const int rec_f = 14 * P;
@@ -142,20 +141,19 @@ __global__ __launch_bounds__(NTH) void photometric_block_kernel(const KernelArgs
   const bool act = live && k < P;
   T* out = reinterpret_cast<T*>(a.out);  // records in the engine's format (fp32, or fp16 for PBA_RECORD_F16)
 
-  if ((int)threadIdx.x < P) s_pat[threadIdx.x] = make_float2(a.pattern[2 * threadIdx.x], a.pattern[2 * threadIdx.x + 1]);
+  const float2 off = pattern_at<LPB>(a, k);
   adopt_state(a);
   int pt;
   if (LPB == 8 && a.poses) {  // fused state: the workgroup-cooperative prologue (BPW = 32)
-    static_assert(kBlockThreads == 256 || kBlockThreads == 128, "stage_tile_wg: 4 waves of 32 blocks or 2 of 16");
+    static_assert(kBlockThreads == 256, "stage_tile_wg: 4 waves, 32 blocks");
     pt = a.block_rec[live ? blk : a.n_blocks - 1].x;
-    stage_tile_wg<kBlockThreads>(a, s_tb, blk0);
+    stage_tile_wg(a, s_tb, blk0);
   } else {
     pt = stage_tile<LPB>(a, s_tb, lb, k, blk, live);
   }
   const float Ih = act ? a.host_int[(long long)pt * P + k] : 0.0f;
   __syncthreads();
-  Row row;
-  if (act) row = photometric_row<PM, JAC>(a, s_tb[lb], s_pat[k], Ih);
+  const Row row = photometric_row<PM, JAC>(a, s_tb[lb], off, Ih);  // dead lanes evaluate a staged block, masked by act
   // per-block validity (ballot over the wave: the block's LPB lanes are an aligned bit field) and ‖r‖²
   const int ok = group_all<LPB>(act ? row.ok : 1);
   const float s = group_sum<LPB>(act ? row.r * row.r : 0.0f);
@@ -230,12 +228,12 @@ __global__ __launch_bounds__((kMultiThreads<PPL, T>)) void photometric_block_ker
   const bool live = blk < a.n_blocks;  // a block's LPB lanes agree
   T* out = reinterpret_cast<T*>(a.out);
 
-  if ((int)threadIdx.x < P) s_pat[threadIdx.x] = make_float2(a.pattern[2 * threadIdx.x], a.pattern[2 * threadIdx.x + 1]);
+  if ((int)threadIdx.x < LPB * PPL) s_pat[threadIdx.x] = pattern_at<LPB * PPL>(a, threadIdx.x);
   adopt_state(a);
   int pt;
-  if (a.poses) {  // fused state: the workgroup-cooperative prologue (BPW = 32 or 16)
+  if (NTH == 256 && a.poses) {  // fused state: the workgroup-cooperative prologue (BPW = 32)
     pt = a.block_rec[live ? blk : a.n_blocks - 1].x;
-    stage_tile_wg<NTH>(a, s_tb, blk0);
+    stage_tile_wg(a, s_tb, blk0);
   } else {
     pt = stage_tile<LPB>(a, s_tb, lb, k, blk, live);
   }
@@ -253,8 +251,7 @@ __global__ __launch_bounds__((kMultiThreads<PPL, T>)) void photometric_block_ker
   for (int j = 0; j < PPL; ++j) {
     const int px = k + LPB * j;
     const bool act = live && px < P;
-    Row row;
-    if (act) row = photometric_row<PM, JAC>(a, s_tb[lb], s_pat[px], Ih[j]);
+    const Row row = photometric_row<PM, JAC>(a, s_tb[lb], s_pat[px < P ? px : 0], Ih[j]);  // masked by act
     okl &= act ? row.ok : 1;
     s += act ? row.r * row.r : 0.0f;
     rr[j] = row.r;
@@ -393,13 +390,7 @@ void launch_photometric(pba_engine* e, const KernelArgs& ka, int mode) {
   if (e->P <= 8) {
     const int grid = (int)(((long long)e->n_blocks * 8 + kBlockThreads - 1) / kBlockThreads);
     e->last_grid = grid;
-    static const bool wg128 = getenv("PBA_BLOCK_WG128") != nullptr;  // A/B experiment
-    if (mode == 1 && !h && wg128) {
-      const int g2 = (int)(((long long)e->n_blocks * 8 + 127) / 128);
-      e->last_grid = g2;
-      photometric_block_kernel<PM, 8, 1, float, 128><<<g2, 128, 0, e->stream>>>(ka);
-    }
-    else if (mode == 1 && h) photometric_block_kernel<PM, 8, 1, _Float16><<<grid, kBlockThreads, 0, e->stream>>>(ka);
+    if (mode == 1 && h) photometric_block_kernel<PM, 8, 1, _Float16><<<grid, kBlockThreads, 0, e->stream>>>(ka);
     else if (mode == 1) photometric_block_kernel<PM, 8, 1, float><<<grid, kBlockThreads, 0, e->stream>>>(ka);
     else if (mode == 0 && h) photometric_block_kernel<PM, 8, 0, _Float16><<<grid, kBlockThreads, 0, e->stream>>>(ka);
     else if (mode == 0) photometric_block_kernel<PM, 8, 0, float><<<grid, kBlockThreads, 0, e->stream>>>(ka);
@@ -494,8 +485,10 @@ void launch_pairs(pba_engine* e, const double* poses, PairRec* pairs) {
                                                                e->frame_cam.p, e->intr_d.p, pairs, e->n_pairs);
 }
 
-int launch_cost_only(pba_engine* e, const PairRec* pairs, const double* rho, double* wg_red, int* n_slots) {
+int launch_cost_only(pba_engine* e, const PairRec* pairs, const double* rho, double* wg_red, int* n_slots,
+                     const double* poses) {
   KernelArgs ka = make_kernel_args(e, pairs, rho);
+  ka.poses = poses;
   ka.wg_red = wg_red;
   launch_mode(e, ka, 2);
   if (n_slots) *n_slots = e->last_grid;

@@ -164,7 +164,6 @@ void linearize_kernel(const KernelArgs a, const LinArgs g) {
   // per-wave arena, used in turn by the wave's tile blocks, its weighted rows and its per-target products
   // (each phase only touches the wave's own blocks; LDS is in order within a wave)
   __shared__ __attribute__((aligned(16))) unsigned char arena[NW][kArena];
-  __shared__ float2 s_pat[LPB];
   __shared__ int s_wlo[NW], s_wn[NW];
   __shared__ float s_bc[kBlockThreads / LPB];  // block costs (0: invalid or dead), for the chunk's cost partial
   const int chunk = logical_tile();
@@ -184,15 +183,18 @@ void linearize_kernel(const KernelArgs a, const LinArgs g) {
   // the chunk's slots are padded to the workgroup's blocks (dead slots repeat slot 0), so the record is read with the
   // chunk descriptor, not behind it, and carries the block's point and pair: the tile prologue's loads come next
   const int4 lr = g.lin_rec[(long long)chunk * (kBlockThreads / LPB) + lb];
+  // the product slot table (a vector load): issued with the record, not behind the stores of the block costs (a
+  // load issued after a store waits for the store too)
+  const unsigned slots = kSlotTable.w[lane];
   const int blk = lr.x, gpos = lr.w, lt = (int)((unsigned)lr.z >> 24);
   Row row;
   if constexpr (KIND == PBA_RESIDUAL_PHOTOMETRIC) {
     TileBlock* s_tb = reinterpret_cast<TileBlock*>(arena[wave]);
-    if ((int)threadIdx.x < R) s_pat[threadIdx.x] = make_float2(a.pattern[2 * threadIdx.x], a.pattern[2 * threadIdx.x + 1]);
+    const float2 off = pattern_at<LPB>(a, k);
     const int pt = stage_tile_pp<LPB>(a, s_tb, wb, k, make_int2(lr.y, lr.z & 0xffffff));
     const float Ih = act ? a.host_int[(long long)pt * R + k] : 0.0f;
     __syncthreads();
-    if (act) row = photometric_row<MODEL, true>(a, s_tb[wb], s_pat[k], Ih);
+    row = photometric_row<MODEL, true>(a, s_tb[wb], off, Ih);  // dead lanes evaluate a staged block, masked below
   } else {
     if (act) row = geometric_row<MODEL, true>(a, blk, k);
   }
@@ -200,16 +202,15 @@ void linearize_kernel(const KernelArgs a, const LinArgs g) {
   const float s = group_sum<LPB>(act && ok ? row.r * row.r : 0.0f);
   const float w = ok ? huber_weight(s, a.huber) : 0.0f;
   const float bcost = ok ? huber_cost(s, a.huber) : 0.0f;
-  if (live && k == 0) {
-    a.valid[blk] = (uint8_t)ok;
-    a.cost[blk] = bcost;
-  }
   if (k == 0) s_bc[lb] = live && ok ? bcost : -1.0f;  // read after the barrier below
   // weighted row x̃ = √w · x  → products carry w (Ceres Corrector with ρ'' ≤ 0: J̃ = √ρ' J, r̃ = √ρ' r)
-  const float sw = (act && ok) ? sqrtf(w) : 0.0f;  // rows outside the domain / of dead lanes are all zero
-  const float x[14] = {sw * row.hv.x, sw * row.hv.y, sw * row.hv.z, sw * row.hw.x, sw * row.hw.y, sw * row.hw.z,
-                       sw * row.tv.x, sw * row.tv.y, sw * row.tv.z, sw * row.tw.x, sw * row.tw.y, sw * row.tw.z,
-                       sw * row.jr, sw * row.r};
+  // rows outside the domain / of dead lanes are all zero (selects, not a zero weight: such a row may hold inf / NaN)
+  const bool use = act && ok;
+  const float sw = use ? sqrtf(w) : 0.0f;
+  auto wx = [&](float v) { return use ? sw * v : 0.0f; };
+  const float x[14] = {wx(row.hv.x), wx(row.hv.y), wx(row.hv.z), wx(row.hw.x), wx(row.hw.y), wx(row.hw.z),
+                       wx(row.tv.x), wx(row.tv.y), wx(row.tv.z), wx(row.tw.x), wx(row.tw.y), wx(row.tw.z),
+                       wx(row.jr), wx(row.r)};
   float* sX = reinterpret_cast<float*>(arena[wave]);  // the wave's 64 rows × 16 floats (overwrites its tile blocks)
   {
     float4* xr = reinterpret_cast<float4*>(sX + lane * 16);
@@ -229,7 +230,6 @@ void linearize_kernel(const KernelArgs a, const LinArgs g) {
 #pragma unroll
     for (int st = 0; st < BW * SPB; ++st) op[st] = sX[(4 * st + kq) * 16 + ci];
     float* sP = reinterpret_cast<float*>(arena[wave]);
-    const unsigned slots = kSlotTable.w[lane];
     const int nbw = min(max(count - wave * BW, 0), BW);  // live blocks of this wave (wave-uniform)
     const int lo = __builtin_amdgcn_readfirstlane(lt);     // lane 0 holds the wave's first block
     auto flush = [&](const f32x4& acc, int slot) {
@@ -299,6 +299,12 @@ void linearize_kernel(const KernelArgs a, const LinArgs g) {
       }
     }
     part_lin[(long long)poff + o] = acc;
+  }
+  // the block costs last: a store issued before a load makes the wait for that load wait for the store too (GFX9
+  // counts loads and stores in one counter), so the stores go after every load of the kernel
+  if (live && k == 0) {
+    a.valid[blk] = (uint8_t)ok;
+    a.cost[blk] = bcost;
   }
   if (g.wg_red && wave == 0) {  // the chunk's (Σ cost, Σ valid): lane b takes block b, xor butterflies (fixed order)
     static_assert(kBlockThreads / LPB <= 64, "one lane per block of the chunk");
@@ -2641,6 +2647,12 @@ int lm_trial(pba_engine* e, double min_rel, double ftol, double seq, const hipEv
 
 int candidate_cost(pba_engine* e, double* cost) {
   GnData& G = e->gn;
+  if (e->opt.residual_kind == PBA_RESIDUAL_PHOTOMETRIC) {
+    // the candidate poses straight into the fused-state prologue: no pair-table launch (C4: 32.4 → 29.8 µs for the
+    // cost launch, and the 7.6-µs pair launch gone)
+    if (int rc = launch_cost_only(e, G.pairs_new.p, G.rho_new.p, nullptr, nullptr, G.poses_new.p)) return rc;
+    return total_cost(e, cost, nullptr);
+  }
   if (!G.pairs_new_fresh) launch_pairs(e, G.poses_new.p, G.pairs_new.p);
   if (int rc = launch_cost_only(e, G.pairs_new.p, G.rho_new.p)) return rc;
   return total_cost(e, cost, nullptr);

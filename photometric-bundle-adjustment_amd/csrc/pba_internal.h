@@ -295,21 +295,31 @@ __device__ __forceinline__ int stage_tile(const KernelArgs& a, TileBlock* s_tb, 
 // Table path with the block's {point, pair} already in hand (linearize_kernel reads it with its linearise record).
 template <int LPB>
 __device__ __forceinline__ int stage_tile_pp(const KernelArgs& a, TileBlock* s_tb, int lb, int k, int2 pp) {
+  // every load first, unconditionally and at in-range addresses (a lane past the last part re-reads part 0; the point's
+  // ρ and the target id are read by every lane, one request per block), then the selects: per-part branches around
+  // the loads made the compiler issue and wait for them one branch at a time (three memory round trips)
+  constexpr int NP = (kTileParts + LPB - 1) / LPB;
   uint4* dst = reinterpret_cast<uint4*>(s_tb + lb);
   const uint4* src = reinterpret_cast<const uint4*>(a.pairs + pp.y);
+  uint4 v[NP];
 #pragma unroll
-  for (int part = k; part < kTileParts; part += LPB) {
-    uint4 v;
-    if (part < kPairParts) {
-      v = src[part];
-    } else if (part == kPairParts) {
-      v = reinterpret_cast<const uint4*>(a.u_ref)[pp.x];
-    } else {
-      const double r = a.rho[pp.x];
-      const long long img = (long long)a.pairs[pp.y].target * a.frame_stride;
-      v = make_uint4(__double2loint(r), __double2hiint(r), (unsigned)img, (unsigned)(img >> 32));
+  for (int i = 0; i < NP; ++i) {
+    const int part = k + LPB * i;
+    v[i] = part == kPairParts ? reinterpret_cast<const uint4*>(a.u_ref)[pp.x] : src[part < kPairParts ? part : 0];
+  }
+  const double r = a.rho[pp.x];
+  const int tgt = a.pairs[pp.y].target;
+  asm volatile("" ::"v"(r), "v"(tgt));
+#pragma unroll
+  for (int i = 0; i < NP; ++i) asm volatile("" ::"v"(v[i].x), "v"(v[i].y), "v"(v[i].z), "v"(v[i].w));
+#pragma unroll
+  for (int i = 0; i < NP; ++i) {
+    const int part = k + LPB * i;
+    if (part == kPairParts + 1) {
+      const long long img = (long long)tgt * a.frame_stride;
+      v[i] = make_uint4(__double2loint(r), __double2hiint(r), (unsigned)img, (unsigned)(img >> 32));
     }
-    dst[part] = v;
+    if (part < kTileParts) dst[part] = v[i];
   }
   return pp.x;
 }
@@ -320,69 +330,7 @@ __device__ __forceinline__ int stage_tile_pp(const KernelArgs& a, TileBlock* s_t
 // with its fp32 copy), wave 3 the point data (lanes 0-31 u_ref, 32-63 ρ).  The fp64 relative-pose arithmetic is then
 // issued once per workgroup instead of once per wave (SIMT: a wave pays for every branch any of its lanes takes, so
 // the rotation and translation branches of stage_tile cost each of the four waves both).  The caller barriers.
-// 128-thread workgroups (16 blocks, two waves): wave 0 forms R_th (lanes 0-15) and copies the point data (u_ref on
-// lanes 16-31, ρ on 32-47), wave 1 forms t_th and the ids (lanes 0-15) and copies the cameras' constants (host part on
-// lanes 16-31, target part with its fp32 copy on 32-47): each wave pays one fp64 branch plus copies.
-template <int NTH>
-__device__ __forceinline__ void stage_tile_wg(const KernelArgs& a, TileBlock* s_tb, int blk0);
-template <>
-__device__ __forceinline__ void stage_tile_wg<128>(const KernelArgs& a, TileBlock* s_tb, int blk0) {
-  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, b = lane & 15, part = lane >> 4;
-  const int4 br = a.block_rec[min(blk0 + b, a.n_blocks - 1)];  // a dead block stages the last block
-  PairRec& pr = s_tb[b].pr;
-  uint4* dst = reinterpret_cast<uint4*>(s_tb + b);
-  if (part == 3) return;
-  if (w == 0) {
-    if (part == 0) {
-      const double* H = a.poses + 7 * br.y;
-      const double* T = a.poses + 7 * br.z;
-      double h[4], t[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        h[j] = H[j];
-        t[j] = T[j];
-      }
-      pair_rotation(h, t, pr);
-    } else if (part == 1) {
-      dst[kPairParts] = reinterpret_cast<const uint4*>(a.u_ref)[br.x];
-    } else {
-      const double rho = a.rho[br.x];
-      const long long img = (long long)br.z * a.frame_stride;
-      dst[kPairParts + 1] = make_uint4(__double2loint(rho), __double2hiint(rho), (unsigned)img, (unsigned)(img >> 32));
-    }
-  } else {
-    if (part == 0) {
-      const double* H = a.poses + 7 * br.y;
-      const double* T = a.poses + 7 * br.z;
-      double h[7], t[7];
-#pragma unroll
-      for (int j = 0; j < 7; ++j) {
-        h[j] = H[j];
-        t[j] = T[j];
-      }
-      pair_translation(h, t, pr);
-      pr.host_cam = br.w >> 16;
-      pr.target_cam = br.w & 0xffff;
-      pr.target = br.z;
-      pr.host = br.y;
-    } else {
-      const bool tgt = part == 2;
-      const uint4* src = reinterpret_cast<const uint4*>(a.intr_d + (tgt ? kCamD * (br.w & 0xffff) : kCamD * (br.w >> 16) + kCamHk));
-      uint4 c[4];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) c[q] = src[q];
-      uint4* d = dst + (int)(offsetof(PairRec, hk) / 16) + (tgt ? 4 : 0);
-#pragma unroll
-      for (int q = 0; q < 4; ++q) d[q] = c[q];
-      if (tgt) {
-#pragma unroll
-        for (int q = 0; q < 4; ++q) camera_kf_part(c[q], q, pr.kf);
-      }
-    }
-  }
-}
-template <>
-__device__ __forceinline__ void stage_tile_wg<256>(const KernelArgs& a, TileBlock* s_tb, int blk0) {
+__device__ __forceinline__ void stage_tile_wg(const KernelArgs& a, TileBlock* s_tb, int blk0) {
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, b = lane & 31;
   const int4 br = a.block_rec[min(blk0 + b, a.n_blocks - 1)];  // a dead block stages the last block
   PairRec& pr = s_tb[b].pr;
@@ -439,6 +387,18 @@ __device__ __forceinline__ void stage_tile_wg<256>(const KernelArgs& a, TileBloc
   }
 }
 
+// Pattern offset k (k < N) read from the kernel arguments with scalar loads at constant offsets and picked per lane
+// by selects.  A lane-indexed read of the argument block is a vector-memory load, and staging it through LDS made
+// every workgroup wait one memory round trip before it issued any other load.
+template <int N>
+__device__ __forceinline__ float2 pattern_at(const KernelArgs& a, int k) {
+  float2 o = make_float2(a.pattern[0], a.pattern[1]);
+#pragma unroll
+  for (int j = 1; j < N; ++j)
+    if (k == j) o = make_float2(a.pattern[2 * j], a.pattern[2 * j + 1]);
+  return o;
+}
+
 // The launch that evaluates at a caller's state also adopts it: one element per lane (grid ≥ frames·7, points).
 __device__ __forceinline__ void adopt_state(const KernelArgs& a) {
   if (!a.adopt_rho) return;
@@ -464,18 +424,17 @@ __device__ __forceinline__ Row photometric_row(const KernelArgs& a, const TileBl
   const Vec3d b = unproject<MODEL>(pp.hk, tb.ur.x + (double)off.x, tb.ur.y + (double)off.y);
   const Vec3d Rb = mat_mul(pp.R, b);
   const Vec3d p = {Rb.x + rho * pp.t[0], Rb.y + rho * pp.t[1], Rb.z + rho * pp.t[2]};
+  // Branch-free: the projection and the taps run whatever the domain test says (the interpolator clamps any
+  // position, NaN and ±inf included, to an in-bounds read), and the caller masks a block that is not ok.  A branch
+  // here costs every lane the zero-initialised Row and the exec bookkeeping, and no wave ever skips it.
   const bool dom = in_domain<MODEL>(pp.tk, p);
-  float I = 0.0f, gx = 0.0f, gy = 0.0f;
-  double iden = 0.0;
-  if (dom) {
-    double u, v;
-    iden = project<MODEL>(pp.tk, p, u, v);
-    interpolate<interp_of(PM)>(a.images + tb.img, a.umax, a.vmax, a.tiles_x, u, v,
-                               I, gx, gy);
-  }
+  float I, gx, gy;
+  double u, v;
+  const double iden = project<MODEL>(pp.tk, p, u, v);
+  interpolate<interp_of(PM)>(a.images + tb.img, a.umax, a.vmax, a.tiles_x, u, v, I, gx, gy);
   o.r = I - Ih;  // photometric_error.h:179
   o.ok = dom && isfinite(o.r);
-  if (JAC && dom) {
+  if (JAC) {
     // q = ∇I · ∂π/∂p̃ (1×3)
     const Vec3 pf = to_f(p), bf = to_f(b);
     Vec3 du, dv;
@@ -739,8 +698,9 @@ void launch_pairs(pba_engine* e, const double* poses, PairRec* pairs);
 
 // Residual-only evaluation writing only per-block costs/validity (state given by pairs/rho).
 // wg_red (optional): each workgroup also writes its (Σ cost, Σ valid) there; *n_slots = the launch's workgroups.
+// poses (optional): evaluate at these state poses with the fused-state prologue instead of the pair table.
 int launch_cost_only(pba_engine* e, const PairRec* pairs, const double* rho, double* wg_red = nullptr,
-                     int* n_slots = nullptr);
+                     int* n_slots = nullptr, const double* poses = nullptr);
 
 // Pyramid (pba_pyramid.hip): back to level 0 and drop the levels; I_h,k sampled from the active level's host images.
 void reset_pyramid(pba_engine* e);
