@@ -122,9 +122,8 @@ __device__ __forceinline__ void store_slab(const unsigned char* src, unsigned ch
   }
 }
 
-template <int PM, int LPB, int MODE, class T, int NTH = kBlockThreads>  // PM = camera model + 4 · interpolator
-__global__ __launch_bounds__(NTH) void photometric_block_kernel(const KernelArgs a) {
-  constexpr int kBlockThreads = NTH;
+template <int PM, int LPB, int MODE, class T>  // PM = camera model + 4 · interpolator
+__global__ __launch_bounds__(kBlockThreads) void photometric_block_kernel(const KernelArgs a) {
   constexpr int BPW = kBlockThreads / LPB;  // blocks per workgroup
   constexpr bool JAC = MODE == 1;
   constexpr int kStageBytes = JAC ? BPW * 14 * LPB * (int)sizeof(T) : 0;
@@ -194,7 +193,7 @@ __global__ __launch_bounds__(NTH) void photometric_block_kernel(const KernelArgs
   __syncthreads();
   const int nblk = min(BPW, a.n_blocks - blk0);
   if (nblk <= 0) return;
-  store_slab<T, NTH>(lds, reinterpret_cast<unsigned char*>(out + (long long)blk0 * rec_f), nblk * rec_f * (int)sizeof(T));
+  store_slab<T>(lds, reinterpret_cast<unsigned char*>(out + (long long)blk0 * rec_f), nblk * rec_f * (int)sizeof(T));
 }
 
 // Patterns of 9…32 pixels (the 21-px pattern of config C5): still 8 lanes per block, each lane evaluating pixels

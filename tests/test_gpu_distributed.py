@@ -131,6 +131,56 @@ def test_solve_distributed_matches_solve(kind, model, huber):
             e.close()
 
 
+@pytest.mark.parametrize("kind,huber", [(0, 9.0), (1, 1.0)])
+def test_two_process_gloo_solve_matches_solve(kind, huber):
+    """Two processes, one engine each (both on cuda:0), a world-size-2 gloo group: distributed.solve_distributed
+    (the engine's export → torch.distributed all-reduce → import, every scalar of the LM decision all-reduced) takes
+    the same LM trajectory as one engine on the whole problem — the bench's multi-GPU GN path with gloo standing in
+    for RCCL (two ranks cannot share a device under RCCL)."""
+    import socket
+
+    import torch.multiprocessing as mp
+
+    import dist_workers
+    case = dict(kind=kind, n_frames=16, n_points=400, seed=83, huber=huber, fixed=[0, 1], iters=10)
+    pb = synth.make_problem(kind=kind, n_frames=16, n_points=400, width=376, height=240, seed=83, border=12,
+                            obs_sigma=0.3)
+    pb.poses[:2] = pb.poses_gt[:2]
+    with engine_for(pb, huber, (0, 1)) as full:
+        ref = full.solve(max_iterations=10)
+        poses_ref, rho_ref = full.get_state()
+    sk = socket.socket()
+    sk.bind(("127.0.0.1", 0))
+    port = sk.getsockname()[1]
+    sk.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=dist_workers.solve_worker, args=(r, 2, port, case, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    try:
+        res = {}
+        for _ in range(2):
+            r, v = q.get(timeout=240)
+            res[r] = v
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+    rho = np.zeros(pb.n_points)
+    for r in range(2):
+        assert isinstance(res[r], dict), res[r]
+        s = res[r]["summary"]
+        assert s["iterations"] == ref["iterations"] and s["successful_steps"] == ref["successful_steps"], (s, ref)
+        assert abs(s["initial_cost"] - ref["initial_cost"]) <= 1e-8 * ref["initial_cost"]
+        assert abs(s["final_cost"] - ref["final_cost"]) <= 1e-6 * ref["final_cost"], (s, ref)
+        np.testing.assert_allclose(res[r]["poses"], poses_ref, atol=1e-6)
+        rho[res[r]["pids"]] = res[r]["rho"]
+    np.testing.assert_allclose(rho, rho_ref, rtol=1e-6)
+    assert ref["final_cost"] < ref["initial_cost"]
+
+
 def test_band_too_small_is_rejected():
     import torch
     pb = synth.make_problem(kind="geometric", n_frames=12, n_points=60, seed=5)

@@ -52,7 +52,7 @@ def main(tag, prefix):
     for (k, g), cs in pmc.items():
         # the timed bench kernel: MODE 1 (full residual + Jacobian records), not the cost-only MODE 2 launch
         if ("FETCH_SIZE" in cs and "WRITE_SIZE" in cs and "photometric_block_kernel" in k
-                and re.search(r"<0, 8, 1(, float)?>$", k)):  # pinhole, 8 lanes, MODE 1, fp32 records
+                and re.search(r"<0, 8, 1(, float)?(, 256)?>$", k)):  # pinhole, 8 lanes, MODE 1, fp32 records
             fetch, write = cs["FETCH_SIZE"][0] * 1024, cs["WRITE_SIZE"][0] * 1024
             out = {"kernel": k, "grid_size": int(g), "fetch_bytes_per_launch": fetch, "write_bytes_per_launch": write,
                    "hbm_bytes_per_launch": fetch + write, "profile": f"profiles/{prefix}_pmc.csv",
