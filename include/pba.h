@@ -119,7 +119,9 @@ int pba_synchronize(pba_engine* engine);
 int pba_record_floats(const pba_engine* engine);   /* 14·R (values per record, in the record format) */
 /* Record storage format (photometric engines): PBA_RECORD_F32 (default) or PBA_RECORD_F16 — IEEE half records,
  * half the HBM write traffic (config C5's "fp16 residuals"; evaluation stays fp64 warp + fp32 chain, rounding
- * only at the store: ≤ 2⁻¹¹ relative per value).  pba_get_records returns floats either way;
+ * only at the store: ≤ 2⁻¹¹ relative per value; values beyond the half range saturate at ±65504 — at full
+ * resolution a strong edge's rotation Jacobian can exceed it; the on-device GN path never reads records, it
+ * accumulates JᵀJ from fp32 rows).  pba_get_records returns floats either way;
  * pba_device_records' pointer then addresses 14·R halves per block. */
 #define PBA_RECORD_F32 0
 #define PBA_RECORD_F16 1

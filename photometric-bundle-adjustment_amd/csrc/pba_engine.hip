@@ -98,6 +98,16 @@ __global__ void tile_images_kernel(const uint8_t* __restrict__ src, uint8_t* __r
   reinterpret_cast<uint4*>(dst)[i] = row.v;
 }
 
+// A record value in the engine's format.  fp16 saturates at ±65504 (the half range) instead of rounding to ±inf: at
+// full resolution a strong edge's rotation Jacobian ∇I·∂π/∂p·[b]× reaches ~1e5 intensity units per radian (measured
+// up to 9.0e4 on the C5-style problem), so those entries are clamped (pba.h, PBA_RECORD_F16).
+template <class T>
+__device__ __forceinline__ T rec_val(float v) { return (T)v; }
+template <>
+__device__ __forceinline__ _Float16 rec_val<_Float16>(float v) {
+  return (_Float16)__builtin_amdgcn_fmed3f(v, -65504.0f, 65504.0f);
+}
+
 // Store a workgroup's contiguous record slab (LDS → global): 16-B non-temporal stores when the slab is 16-B
 // aligned, 4-B or 2-B stores otherwise (odd patterns in fp16).
 template <class T, int NTH = kBlockThreads>
@@ -169,7 +179,7 @@ __global__ __launch_bounds__(kBlockThreads) void photometric_block_kernel(const 
     return;
   }
   if (!JAC) {
-    if (act) out[(long long)blk * rec_f + k] = (T)(ok ? row.r : 0.0f);
+    if (act) out[(long long)blk * rec_f + k] = rec_val<T>(ok ? row.r : 0.0f);
     return;
   }
   __syncthreads();  // every lane has read its tile block: the record stage may overwrite it
@@ -180,10 +190,12 @@ __global__ __launch_bounds__(kBlockThreads) void photometric_block_kernel(const 
     T* h = s_rec + P + 6 * k;
     T* t = s_rec + 7 * P + 6 * k;
     if (ok) {
-      s_rec[k] = (T)row.r;
-      h[0] = (T)row.hv.x; h[1] = (T)row.hv.y; h[2] = (T)row.hv.z; h[3] = (T)row.hw.x; h[4] = (T)row.hw.y; h[5] = (T)row.hw.z;
-      t[0] = (T)row.tv.x; t[1] = (T)row.tv.y; t[2] = (T)row.tv.z; t[3] = (T)row.tw.x; t[4] = (T)row.tw.y; t[5] = (T)row.tw.z;
-      s_rec[13 * P + k] = (T)row.jr;
+      s_rec[k] = rec_val<T>(row.r);
+      h[0] = rec_val<T>(row.hv.x); h[1] = rec_val<T>(row.hv.y); h[2] = rec_val<T>(row.hv.z);
+      h[3] = rec_val<T>(row.hw.x); h[4] = rec_val<T>(row.hw.y); h[5] = rec_val<T>(row.hw.z);
+      t[0] = rec_val<T>(row.tv.x); t[1] = rec_val<T>(row.tv.y); t[2] = rec_val<T>(row.tv.z);
+      t[3] = rec_val<T>(row.tw.x); t[4] = rec_val<T>(row.tw.y); t[5] = rec_val<T>(row.tw.z);
+      s_rec[13 * P + k] = rec_val<T>(row.jr);
     } else {
       s_rec[k] = (T)0.0f;
       for (int j = 0; j < 6; ++j) h[j] = t[j] = (T)0.0f;
@@ -257,10 +269,12 @@ __global__ __launch_bounds__((kMultiThreads<PPL, T>)) void photometric_block_ker
     if (JAC && act) {  // record row px: r | J_host row | J_target row | J_rho
       T* h = s_rec + P + 6 * px;
       T* t = s_rec + 7 * P + 6 * px;
-      s_rec[px] = (T)row.r;
-      h[0] = (T)row.hv.x; h[1] = (T)row.hv.y; h[2] = (T)row.hv.z; h[3] = (T)row.hw.x; h[4] = (T)row.hw.y; h[5] = (T)row.hw.z;
-      t[0] = (T)row.tv.x; t[1] = (T)row.tv.y; t[2] = (T)row.tv.z; t[3] = (T)row.tw.x; t[4] = (T)row.tw.y; t[5] = (T)row.tw.z;
-      s_rec[13 * P + px] = (T)row.jr;
+      s_rec[px] = rec_val<T>(row.r);
+      h[0] = rec_val<T>(row.hv.x); h[1] = rec_val<T>(row.hv.y); h[2] = rec_val<T>(row.hv.z);
+      h[3] = rec_val<T>(row.hw.x); h[4] = rec_val<T>(row.hw.y); h[5] = rec_val<T>(row.hw.z);
+      t[0] = rec_val<T>(row.tv.x); t[1] = rec_val<T>(row.tv.y); t[2] = rec_val<T>(row.tv.z);
+      t[3] = rec_val<T>(row.tw.x); t[4] = rec_val<T>(row.tw.y); t[5] = rec_val<T>(row.tw.z);
+      s_rec[13 * P + px] = rec_val<T>(row.jr);
     }
   }
   // per-block validity (ballot over the wave: the block's LPB lanes are an aligned bit field) and ‖r‖²
@@ -282,7 +296,7 @@ __global__ __launch_bounds__((kMultiThreads<PPL, T>)) void photometric_block_ker
 #pragma unroll
     for (int j = 0; j < PPL; ++j) {
       const int px = k + LPB * j;
-      if (live && px < P) out[(long long)blk * rec_f + px] = (T)(ok ? rr[j] : 0.0f);
+      if (live && px < P) out[(long long)blk * rec_f + px] = rec_val<T>(ok ? rr[j] : 0.0f);
     }
     return;
   }

@@ -95,3 +95,21 @@ def compare_records(kind: int, R: int, got: np.ndarray, ref: np.ndarray, valid_g
         stats[name + "_rel"] = float(err.max()) if err.size else 0.0
         assert stats[name + "_rel"] <= j_rtol, (name, stats)
     return stats
+
+
+def fp16_violations(rec_h, rec_a, uv, P):
+    """Entries of fp16 records outside the bound against the fp32 records of the same evaluation.  The fp16 and fp32
+    launches are separate instantiations whose fp32 arithmetic may contract differently: a Jacobian entry formed by
+    cancellation (e.g. the ω columns, b × (qR) with |qR| ~ 1e4) carries ~1e-7 of the block's Jacobian scale of
+    evaluation noise either way.  Bound: fp16 rounding (2⁻¹¹ relative, 2⁻¹⁴ absolute) plus 1e-6 of the block's largest
+    |J| (the north star's parity bound is 1e-5); Jacobian columns of pixels within 2e-3 px of a bilinear cell edge,
+    where the last-ulp warp difference may pick the neighbouring cell, are excluded as in compare_records.  Values
+    beyond the half range saturate at ±65504 (pba.h PBA_RECORD_F16), never ±inf."""
+    n = rec_a.shape[0]
+    rec_a = np.clip(rec_a, -65504.0, 65504.0)
+    edge = near_cell_boundary(uv)                                                  # (n_blocks, P)
+    col_edge = np.concatenate([np.zeros_like(edge), np.repeat(edge, 6, 1), np.repeat(edge, 6, 1), edge], 1)
+    jscale = np.abs(rec_a[:, P:]).max(1, keepdims=True)
+    bound = 2.0 ** -11 * np.abs(rec_a) + 2.0 ** -14 + np.concatenate([np.zeros((n, P)),
+                                                                      np.repeat(1e-6 * jscale, 13 * P, 1)], 1)
+    return (~(np.abs(rec_h - rec_a) <= bound) & ~col_edge) | ~np.isfinite(rec_h)

@@ -6,6 +6,9 @@
 * C2 (configs[1]) — 50 keyframes of real EuRoC V1 image content, 8-px pattern, 20k blocks, double sphere: the Ceres
   drop-in against real Ceres on the CPU, iteration by iteration, with the evaluation-callback protocol checked on
   every call (evaluation_callback_test.cc:79-160).
+* C5 (configs[4]) — the EuRoC V1 sequence is not in the container, so the C5 pieces run at full C4 size on rendered
+  images: 21-px disk pattern, I_h,k sampled on the device, 3-level pyramid, fp16 records; sampled oracle parity at
+  levels 2 and 0, fp16 within 2⁻¹¹ of fp32, and a coarse-to-fine LM (pba_solve_pyramid) that lowers the cost.
 * C4 (configs[3]) — the headline problem, 1000 keyframes × 100k points × 8 px (400k blocks): sampled oracle parity
   over all hosts, full-size properties (validity, finiteness, cost = Σ½ρ(‖r‖²), the state-adopting launch
   bit-identical to set_state + evaluate, fp16 records within 2⁻¹¹), and one Gauss-Newton / LM iteration on rendered
@@ -27,7 +30,7 @@ import pytest
 import ceres_runner as CR
 import gn_reference as GR
 import oracle as O
-from helpers import compare_records, engine_module, near_cell_boundary, projected_uv, synth
+from helpers import compare_records, engine_module, fp16_violations, projected_uv, synth
 
 pytestmark = pytest.mark.gpu
 E = engine_module()
@@ -171,18 +174,8 @@ def test_c4_full_size_parity_and_properties(c4):
         eng.evaluate(True)
         rec_h, valid_h = eng.records()
     assert np.array_equal(valid_h, valid_a)
-    # The fp16 and fp32 launches are separate instantiations whose fp32 arithmetic may contract differently: a
-    # Jacobian entry formed by cancellation (e.g. the ω columns, b × (qR) with |qR| ~ 1e4) carries ~1e-7 of the
-    # block's Jacobian scale of evaluation noise either way.  Bound: fp16 rounding (2⁻¹¹ relative, 2⁻¹⁴ absolute) plus
-    # 1e-6 of the block's largest |J| (the north star's parity bound is 1e-5); pixels within 2e-3 px of a bilinear
-    # cell edge, where the last-ulp warp difference may pick the neighbouring cell, are excluded as in compare_records.
     at1 = synth.Problem(**{**pb.__dict__, "poses": states[1][2], "rho": states[1][3]})
-    edge = near_cell_boundary(projected_uv(at1))                              # (n_blocks, 8)
-    col_edge = np.concatenate([np.zeros_like(edge), np.repeat(edge, 6, 1), np.repeat(edge, 6, 1), edge], 1)
-    jscale = np.abs(rec_a[:, 8:]).max(1, keepdims=True)
-    bound = 2.0 ** -11 * np.abs(rec_a) + 2.0 ** -14 + np.concatenate([np.zeros((pb.n_blocks, 8)),
-                                                                      np.repeat(1e-6 * jscale, 104, 1)], 1)
-    bad = ~(np.abs(rec_h - rec_a) <= bound) & ~col_edge
+    bad = fp16_violations(rec_h, rec_a, projected_uv(at1), 8)
     if bad.any():
         i, j = np.argwhere(bad)[0]
         pytest.fail(f"fp16 records: {bad.sum()} values out of bound, max|fp32| {np.abs(rec_a).max():.4g}, "
@@ -228,3 +221,50 @@ def test_c4_gauss_newton_iteration_on_rendered_images(monkeypatch):
         assert c1 < c0, (solver, c0, c1)
     for a, b in zip(steps["cr"], steps["band"]):
         assert np.linalg.norm(a - b) <= 1e-7 * np.linalg.norm(b)
+
+
+# ---------------------------------------------------------------------------------------------------- C5
+DISK21 = np.array([(dx, dy) for dy in range(-2, 3) for dx in range(-2, 3) if dx * dx + dy * dy <= 5], np.float32)
+
+
+def test_c5_style_full_size_pyramid_fp16():
+    """C5's configuration on the C4 problem (1004 keyframes, 400k blocks, rendered plane): 21-px pattern with the host
+    intensities sampled on the device, a 3-level pyramid, fp16 records.  At levels 2 and 0: 4096 blocks over all hosts
+    against the oracle evaluating that level's problem (fp32 records), every block valid and finite, and the fp16
+    records within 2⁻¹¹ relative + 2⁻¹⁴ absolute of the fp32 ones; then the coarse-to-fine LM lowers the cost."""
+    import torch
+    pb, images = synth.c4_shard(torch.device("cuda", 0), texture="render")
+    pb5 = synth.Problem(**{**pb.__dict__, "pattern": DISK21, "host_intensity": None})
+    P = DISK21.shape[0]
+    sel = np.linspace(0, pb.n_blocks - 1, 4096).astype(np.int64)
+    imgs = images.cpu().numpy()
+    with E.Engine(0, 0, huber_width=9.0) as eng:
+        eng.set_problem(pb5, images_device_ptr=images.data_ptr())
+        eng.set_fixed_frames(np.array([0, 1], np.int32))
+        eng.set_state(pb.poses, pb.rho)
+        eng.build_pyramid(3)
+        for level in (2, 0):
+            eng.set_level(level)
+            eng.set_record_format(E.RECORD_F32)
+            eng.evaluate(True)
+            r32, v32 = eng.records()
+            hi = eng.host_intensities()
+            eng.set_record_format(E.RECORD_F16)
+            eng.evaluate(True)
+            r16, v16 = eng.records()
+            assert v32.all() and np.array_equal(v16, v32) and np.isfinite(r32).all(), level
+            full = synth.Problem(**{**pb5.__dict__, "images": imgs})
+            lp = synth.level_problem(full, level, host_intensity=hi)
+            bad = fp16_violations(r16, r32, projected_uv(lp), P)
+            if bad.any():
+                i, j = np.argwhere(bad)[0]
+                pytest.fail(f"level {level}: {bad.sum()} fp16 values out of bound, columns "
+                            f"{np.unique(np.nonzero(bad)[1])[:20]}, e.g. [{i},{j}] {r32[i, j]!r} -> {r16[i, j]!r}, "
+                            f"max|fp32| over them {np.abs(r32[bad]).max():.6g}, non-finite fp16 {(~np.isfinite(r16)).sum()}")
+            sub = synth.Problem(**{**lp.__dict__, "block_point": pb.block_point[sel], "block_target": pb.block_target[sel]})
+            ref, vref = O.evaluate(sub)
+            compare_records(0, P, r32[sel], ref, v32[sel], vref, projected_uv(sub))
+        eng.set_record_format(E.RECORD_F32)
+        s = eng.solve_pyramid(max_iterations=4)
+        assert eng.level()[0] == 0
+    assert s["final_cost"] < s["initial_cost"], s

@@ -5,13 +5,14 @@ Pyramid parity: at every level the engine's records equal the oracle's on the le
 engine's own level-l host intensities, which in turn match double-precision bilinear sampling of the host's
 level-l image (≤ 1e-3 intensity units: fp32 interpolation weights).  Record tolerances as tests/helpers.py.
 fp16 records: every value within 2⁻¹¹ relative of the fp32 record (IEEE half rounding of the same evaluation;
-absolute floor 2⁻¹⁴ for values near zero) and identical validity.
+absolute floor 2⁻¹⁴ for values near zero; Jacobian entries formed by cancellation may differ by 1e-6 of the block's
+Jacobian scale between the two instantiations — helpers.fp16_violations) and identical validity.
 """
 import numpy as np
 import pytest
 
 import oracle as O
-from helpers import compare_records, engine_module, projected_uv, synth
+from helpers import compare_records, engine_module, fp16_violations, projected_uv, synth
 
 pytestmark = pytest.mark.gpu
 E = engine_module()
@@ -118,6 +119,7 @@ def test_fp16_records(P):
         eng.evaluate(False)  # residual-only path in fp16 too
         ro, _ = eng.records()
     assert np.array_equal(v32, v16)
-    tol = 2.0 ** -11 * np.abs(r32) + 2.0 ** -14
-    assert (np.abs(r16 - r32) <= tol).all()
-    assert (np.abs(ro[:, :P] - r32[:, :P]) <= tol[:, :P]).all()
+    bad = fp16_violations(r16, r32, projected_uv(pb), P)
+    assert not bad.any(), (bad.sum(), np.unique(np.nonzero(bad)[1]))
+    tol = 2.0 ** -11 * np.abs(r32[:, :P]) + 2.0 ** -14  # residuals: no cancellation, plain half rounding
+    assert (np.abs(ro[:, :P] - r32[:, :P]) <= tol).all()
