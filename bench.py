@@ -140,7 +140,10 @@ def make_states(pb, torch, dev, seed):
 
 def time_evaluation(eng, states, steps, warmup, clock_warmup_s, torch, dist, dev):
     """W warmup steps (after a clock warm-up), then K timed steps bracketed by barrier + synchronize; returns
-    (max-over-ranks elapsed s, max-over-ranks average block-kernel µs, host diagnostics)."""
+    (max-over-ranks elapsed s, max-over-ranks average block-kernel µs, host diagnostics).  The kernel duration comes
+    from two HIP events on the engine's stream around the K timed launches (elapsed ÷ K: each launch plus the
+    dispatch gap to the next, so never below rocprof's kernel average); the launches themselves carry no events —
+    a pair of timing events per launch idles the GPU ~4 µs per step (`host` reports that instrumented run too)."""
     def step(i):  # one launch: pairs formed in the block prologue, state adopted by the same launch
         p, r = states[i & 1]
         eng.evaluate_state_device(p.data_ptr(), r.data_ptr(), True, sync=False)
@@ -157,31 +160,37 @@ def time_evaluation(eng, states, steps, warmup, clock_warmup_s, torch, dist, dev
     for i in range(warmup):
         step(i)
     eng.synchronize()
-    # diagnostic (not the metric): the same steps without the per-launch timing events, and the host's enqueue rate
+    # diagnostic (not the metric): the same steps with a timing-event pair around every launch (the engine's
+    # per-launch kernel timing: kernel-only durations)
+    eng.enable_kernel_timing(True)
+    eng.kernel_timing()  # reset
     t0 = time.perf_counter()
     for i in range(steps):
         step(i)
-    t_enq = time.perf_counter()
     eng.synchronize()
-    host_diag = {"us_per_step_without_events": 1e6 * (time.perf_counter() - t0) / steps,
-                 "enqueue_us_per_step_without_events": 1e6 * (t_enq - t0) / steps}
-    eng.enable_kernel_timing(True)
-    eng.kernel_timing()  # reset
+    t_ev = time.perf_counter() - t0
+    kern_only_ms, launches = eng.kernel_timing()
+    eng.enable_kernel_timing(False)
+    host_diag = {"us_per_step_with_per_launch_events": 1e6 * t_ev / steps,
+                 "kernel_only_us_per_launch_events": 1e3 * kern_only_ms / max(launches, 1)}
+    # the timed region
+    stream = torch.cuda.ExternalStream(eng.stream(), device=dev)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    e0.record(stream)
     for i in range(steps):
         step(i)
     host_diag["enqueue_us_per_step"] = 1e6 * (time.perf_counter() - t0) / steps
+    e1.record(stream)
     eng.synchronize()
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     if dist is not None:
         dist.barrier()
-    kern_ms, launches = eng.kernel_timing()
-    eng.enable_kernel_timing(False)
-    t = all_reduce_max(torch, dist, [t1 - t0, 1e3 * kern_ms / max(launches, 1)], dev)
+    t = all_reduce_max(torch, dist, [t1 - t0, 1e3 * e0.elapsed_time(e1) / steps], dev)
     return float(t[0]), float(t[1]), host_diag
 
 
