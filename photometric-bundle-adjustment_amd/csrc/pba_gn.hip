@@ -2604,11 +2604,18 @@ void launch_accept(pba_engine* e, const double* lm) {
 // Wait for trial `seq`'s decision record, published by lm_decide_kernel into host-coherent memory: a poll, not a
 // stream event (an event left the GPU idle ~6 µs each) — while the host polls, the GPU runs on into the gated accept
 // and linearisation.  The stream is queried now and then so a device error or a record that never comes ends the wait.
+double now_ms();
+
 int wait_decision(pba_engine* e, double seq, double* d) {
   volatile double* r = e->gn.lm_h.p;
+  // the stream is queried only after 2 ms without the record (a trial takes ~0.23 ms at C4), then every 2 ms: a
+  // hipStreamQuery every few hundred spins idled the GPU 5.7 µs before every trial's first kernel
+  // (profiles/r2_gn_trial_trace_v7.txt → v9)
+  double next_query = now_ms() + 2.0;
   for (unsigned spins = 1;; ++spins) {
     if (r[kLmFields] == seq) break;
-    if ((spins & 255u) == 0u) {
+    if ((spins & 255u) == 0u && now_ms() >= next_query) {
+      next_query = now_ms() + 2.0;
       const hipError_t q = hipStreamQuery(e->stream);
       if (q == hipSuccess && r[kLmFields] != seq) return fail(PBA_ERR_DEVICE, "LM decision record was not published");
       if (q != hipSuccess && q != hipErrorNotReady) return fail(PBA_ERR_DEVICE, std::string("HIP: ") + hipGetErrorString(q));
