@@ -141,6 +141,52 @@ def test_evaluate_state_device_adopts(kind, model, extra_points):
     compare_records(kind, pb.R, a, ref, va, vref, projected_uv(pb_gt))
 
 
+@pytest.mark.parametrize("kind", [0, 1])
+@pytest.mark.parametrize("n_blocks", [1, 31, 33])
+def test_ragged_block_counts(kind, n_blocks):
+    """Block counts that leave the last workgroup partly empty (32 blocks per photometric workgroup, 256 per geometric
+    one) and a single block: records, validity and costs against the oracle, fused-state launch included."""
+    import torch
+    pb = synth.make_problem(kind=kind, n_frames=6, n_points=40, width=376, height=240, seed=90 + n_blocks, border=12)
+    keep = np.arange(n_blocks)
+    pb = synth.Problem(**{**pb.__dict__, "block_point": pb.block_point[keep], "block_target": pb.block_target[keep],
+                          "u_obs": None if pb.u_obs is None else pb.u_obs[keep]})
+    rec, valid, costs = run_engine(pb, huber=9.0 if kind == 0 else 1.0)
+    assert rec.shape[0] == n_blocks
+    ref, vref = O.evaluate(pb)
+    compare_records(kind, pb.R, rec, ref, valid, vref, projected_uv(pb) if kind == 0 else None)
+    with E.Engine(pb.kind, pb.model, huber_width=9.0 if kind == 0 else 1.0) as eng:
+        eng.set_problem(pb)
+        eng.set_state(pb.poses, pb.rho)
+        dev = torch.device("cuda", 0)
+        poses_d, rho_d = torch.from_numpy(pb.poses).to(dev), torch.from_numpy(pb.rho).to(dev)  # alive for the launch
+        eng.evaluate_state_device(poses_d.data_ptr(), rho_d.data_ptr(), True)
+        a, va = eng.records()
+        np.testing.assert_array_equal(va, valid)
+        np.testing.assert_array_equal(a.view(np.uint32), rec.view(np.uint32))
+        np.testing.assert_array_equal(eng.block_costs(), costs)
+
+
+@pytest.mark.parametrize("kind", [0, 1])
+def test_non_finite_state_gives_invalid_blocks(kind):
+    """A NaN inverse distance or a NaN pose makes the blocks that use it invalid (validity 0, zero record, zero cost;
+    Ceres' Evaluate returning false) and leaves every other block exactly as at the finite state: the branch-free row
+    clamps any position to an in-bounds read."""
+    pb = synth.make_problem(kind=kind, n_frames=6, n_points=120, width=376, height=240, seed=95, border=12)
+    rec0, valid0, _ = run_engine(pb)
+    rho = pb.rho.copy()
+    rho[5] = np.nan
+    poses = pb.poses.copy()
+    poses[3, 4] = np.nan
+    rec, valid, costs = run_engine(pb, poses=poses, rho=rho)
+    hit = (pb.block_point == 5) | (pb.block_target == 3) | (pb.point_host[pb.block_point] == 3)
+    assert hit.any() and (~hit).any()
+    assert not valid[hit].any()
+    assert (rec[hit] == 0).all() and (costs[hit] == 0).all()
+    np.testing.assert_array_equal(valid[~hit], valid0[~hit])
+    np.testing.assert_array_equal(rec[~hit].view(np.uint32), rec0[~hit].view(np.uint32))
+
+
 def test_invalid_inputs_raise():
     pb = synth.make_problem(n_frames=6, n_points=20, width=64, height=48, seed=1, border=6)
     with E.Engine(0, 0) as eng:
