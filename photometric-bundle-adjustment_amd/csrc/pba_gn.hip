@@ -183,9 +183,6 @@ void linearize_kernel(const KernelArgs a, const LinArgs g) {
   // the chunk's slots are padded to the workgroup's blocks (dead slots repeat slot 0), so the record is read with the
   // chunk descriptor, not behind it, and carries the block's point and pair: the tile prologue's loads come next
   const int4 lr = g.lin_rec[(long long)chunk * (kBlockThreads / LPB) + lb];
-  // the product slot table (a vector load): issued with the record, not behind the stores of the block costs (a
-  // load issued after a store waits for the store too)
-  const unsigned slots = kSlotTable.w[lane];
   const int blk = lr.x, gpos = lr.w, lt = (int)((unsigned)lr.z >> 24);
   Row row;
   if constexpr (KIND == PBA_RESIDUAL_PHOTOMETRIC) {
@@ -204,6 +201,9 @@ void linearize_kernel(const KernelArgs a, const LinArgs g) {
   const float bcost = ok ? huber_cost(s, a.huber) : 0.0f;
   if (k == 0) s_bc[lb] = live && ok ? bcost : -1.0f;  // read after the barrier below
   // weighted row x̃ = √w · x  → products carry w (Ceres Corrector with ρ'' ≤ 0: J̃ = √ρ' J, r̃ = √ρ' r)
+  // the product slot table (a vector load): after the row (one register fewer across it: the row's peak pressure spilled
+  // at 8 waves/SIMD) and before any store of this kernel (a load issued after a store waits for the store too)
+  const unsigned slots = kSlotTable.w[lane];
   // rows outside the domain / of dead lanes are all zero (selects, not a zero weight: such a row may hold inf / NaN)
   const bool use = act && ok;
   const float sw = use ? sqrtf(w) : 0.0f;
