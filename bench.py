@@ -360,7 +360,12 @@ def main():
     gn = None
     if args.gn_iterations > 0:
         eng.set_state(pb.poses, pb.rho)
-        gn = gn_benchmark(eng, args.gn_iterations, torch, dd, dev, world)
+        try:
+            gn = gn_benchmark(eng, args.gn_iterations, torch, dd, dev, world)
+        except Exception as ex:  # a secondary leg: report it, keep the headline line (every rank raises alike)
+            if world == 1:
+                raise
+            gn = {"error": f"{type(ex).__name__}: {ex}"[:300]}
     eng.close()
 
     weak = None
