@@ -167,12 +167,12 @@ def test_ragged_block_counts(kind, n_blocks):
         np.testing.assert_array_equal(eng.block_costs(), costs)
 
 
-@pytest.mark.parametrize("kind", [0, 1])
-def test_non_finite_state_gives_invalid_blocks(kind):
+@pytest.mark.parametrize("kind,model", [(0, 0), (0, 1), (0, 2), (0, 3), (1, 0), (1, 3)])
+def test_non_finite_state_gives_invalid_blocks(kind, model):
     """A NaN inverse distance or a NaN pose makes the blocks that use it invalid (validity 0, zero record, zero cost;
     Ceres' Evaluate returning false) and leaves every other block exactly as at the finite state: the branch-free row
     clamps any position to an in-bounds read."""
-    pb = synth.make_problem(kind=kind, n_frames=6, n_points=120, width=376, height=240, seed=95, border=12)
+    pb = synth.make_problem(kind=kind, model=model, n_frames=6, n_points=120, width=376, height=240, seed=95, border=12)
     rec0, valid0, _ = run_engine(pb)
     rho = pb.rho.copy()
     rho[5] = np.nan
