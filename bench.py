@@ -77,6 +77,56 @@ def host_cores():
     return {"usable": usable, "nproc": n_all, "affinity": aff, "cgroup_quota_cpus": quota, "cpu_model": model}
 
 
+def c4_sample(pb, images_host, hosts: int = 250):
+    """The points hosted by the first `hosts` keyframes of the C4 problem with all their blocks (100k blocks)."""
+    sel_pts = np.nonzero(pb.point_host < hosts)[0]
+    remap = np.full(pb.n_points, -1, np.int64)
+    remap[sel_pts] = np.arange(len(sel_pts))
+    sel_blk = np.nonzero(remap[pb.block_point] >= 0)[0]
+    nfs = hosts + 4
+    return synth.Problem(kind=pb.kind, model=pb.model, width=pb.width, height=pb.height, intrinsics=pb.intrinsics,
+                         frame_cam=pb.frame_cam[:nfs], images=images_host[:nfs], pattern=pb.pattern,
+                         point_host=pb.point_host[sel_pts], u_ref=pb.u_ref[sel_pts],
+                         host_intensity=pb.host_intensity[sel_pts], block_point=remap[pb.block_point[sel_blk]].astype(np.int32),
+                         block_target=pb.block_target[sel_blk], u_obs=None, poses=pb.poses[:nfs], rho=pb.rho[sel_pts])
+
+
+def per_call(r):
+    """Ceres' own timers (Solver::Summary) per evaluation call."""
+    return {"jacobian_evaluation_ms": 1e3 * r["jacobian_evaluation_s"] / max(r["jacobian_evaluations"], 1),
+            "jacobian_evaluations": r["jacobian_evaluations"],
+            "residual_evaluation_ms": 1e3 * r["residual_evaluation_s"] / max(r["residual_evaluations"], 1),
+            "linear_solver_ms_per_iteration": 1e3 * r["linear_solver_s"] / max(len(r["costs"]) - 1, 1),
+            "minimizer_s": r["minimizer_s"], "successful_steps": r["successful_steps"],
+            "unsuccessful_steps": r["unsuccessful_steps"], "final_cost": r["final_cost"], "threads": r["threads"]}
+
+
+def c2_dropin(pb_c4, images_host, threads: int):
+    """BASELINE.json configs[1] (C2) — "Ceres LM + GPU EvaluationCallback": real Ceres 2.0.0 ceres::Solve (LM,
+    SPARSE_SCHUR, Huber, the reference's LocalParameterizationSE3) over include/pba_ceres.h (GpuEvaluator + per-block
+    CostFunctions, the engine's records read back in chunks that overlap Ceres' per-block work) against the same Solve
+    over AutoDiff on the CPU.  Ceres' "Jacobian & residual evaluation" time per call (program_evaluator.h:139-258, with
+    the Jacobian writer) is C2's metric; also on the 100k-block C4 sample of cpu_baseline."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import ceres_runner as CR
+    if not CR.available():
+        return None
+    pb = synth.c2_problem()
+    pb.poses[:2] = pb.poses_gt[:2]
+    out = {"config": f"C2: {pb.n_frames} keyframes of EuRoC V1 image content, {pb.n_blocks} blocks, 8-px pattern, "
+                     f"double sphere, Huber 9, 10 LM iterations"}
+    g = CR.run("gpu", pb, iters=10, huber=9.0, threads=threads)
+    c = CR.run("cpu", pb, iters=10, huber=9.0, threads=threads)
+    out["gpu_dropin"], out["cpu_autodiff"] = per_call(g), per_call(c)
+    out["blocks"] = pb.n_blocks
+    out["speedup_jacobian_evaluation"] = out["cpu_autodiff"]["jacobian_evaluation_ms"] / out["gpu_dropin"]["jacobian_evaluation_ms"]
+    out["same_trajectory"] = bool(len(g["costs"]) == len(c["costs"]) and np.array_equal(g["step_ok"], c["step_ok"]))
+    sample = c4_sample(pb_c4, images_host)
+    gs = CR.run("gpu", sample, iters=4, huber=9.0, threads=threads, ftol=0.0)
+    out["c4_sample"] = dict(per_call(gs), blocks=sample.n_blocks)
+    return out
+
+
 def cpu_baseline(pb, images_host, budget_s: float):
     """The reference's CPU path on a bounded sample of the same workload: real Ceres 2.0.0 (oracle/_ref, built from
     the reference's vendored sources) — ceres::Solve, LEVENBERG_MARQUARDT + SPARSE_SCHUR, one AutoDiffCostFunction per
@@ -89,16 +139,8 @@ def cpu_baseline(pb, images_host, budget_s: float):
     if not CR.available():
         return None
     hosts = 250
-    sel_pts = np.nonzero(pb.point_host < hosts)[0]
-    remap = np.full(pb.n_points, -1, np.int64)
-    remap[sel_pts] = np.arange(len(sel_pts))
-    sel_blk = np.nonzero(remap[pb.block_point] >= 0)[0]
     nfs = hosts + 4
-    sample = synth.Problem(kind=pb.kind, model=pb.model, width=pb.width, height=pb.height, intrinsics=pb.intrinsics,
-                           frame_cam=pb.frame_cam[:nfs], images=images_host[:nfs], pattern=pb.pattern,
-                           point_host=pb.point_host[sel_pts], u_ref=pb.u_ref[sel_pts],
-                           host_intensity=pb.host_intensity[sel_pts], block_point=remap[pb.block_point[sel_blk]].astype(np.int32),
-                           block_target=pb.block_target[sel_blk], u_obs=None, poses=pb.poses[:nfs], rho=pb.rho[sel_pts])
+    sample = c4_sample(pb, images_host, hosts)
     t0 = time.perf_counter()
     r = CR.run("cpu", sample, iters=2, huber=9.0, threads=cores["usable"], fixed=(0, 1), ftol=0.0)
     per_eval = r["jacobian_evaluation_s"] / max(r["jacobian_evaluations"], 1)
@@ -107,8 +149,16 @@ def cpu_baseline(pb, images_host, budget_s: float):
         r = CR.run("cpu", sample, iters=iters, huber=9.0, threads=cores["usable"], fixed=(0, 1), ftol=0.0)
     n_eval = r["jacobian_evaluations"]
     rate = sample.n_blocks * n_eval / r["jacobian_evaluation_s"]
-    return {"value": rate, "unit": "blocks/s", "cores": r["threads"], "kind": "reference",
-            "per_core": rate / max(r["threads"], 1), "host": cores,
+    return {"value": rate, "unit": "blocks/s", "cores": r["threads"],
+            "kind": "reference",
+            "kind_detail": "Ceres 2.0.0 evaluator (ProgramEvaluator + AutoDiff) over the restated photometric functor",
+            "per_core": rate / max(r["threads"], 1),
+            "reference_functor_per_core": {
+                "value": 43000.0, "unit": "blocks/s",
+                "note": "SURVEY.md §6: the reference's own BundleAdjustmentReprojectionCostFunctor inside Ceres' evaluator "
+                        "(per-call AbstractCamera::from_data heap allocation + string dispatch, camera_models.h:452-474) "
+                        "measured in the survey container; the restated functor above avoids that overhead"},
+            "host": cores,
             "sample": f"{sample.n_blocks} blocks (the points hosted by keyframes 0-{hosts - 1} of the same problem, "
                       f"{nfs} frames), {n_eval} Jacobian+residual evaluations timed by Ceres' Solver::Summary "
                       f"({r['jacobian_evaluation_s']:.1f} s of {time.perf_counter() - t0:.1f} s wall) in ceres::Solve "
@@ -205,11 +255,11 @@ def gn_benchmark(eng, iters, torch, dist, dev, world):
     opts = dict(max_iterations=iters, function_tolerance=0.0)
     if world > 1:
         band = D.global_band(eng, None, dev)
-        ar = D.TorchAllReduce(eng.gn_exchange_size(band), dev)
-        eng.solve_distributed(band, ar.ptr, ar, max_iterations=1)  # warm-up
+        # the RCCL communicator is set up by the warm-up (nccl backend: both sums of a trial on the engine stream)
+        D.solve_distributed(eng, device=dev, max_iterations=1)
         dist.barrier()
         torch.cuda.synchronize()
-        s = eng.solve_distributed(band, ar.ptr, ar, **opts)
+        s = D.solve_distributed(eng, device=dev, **opts)
         exchange_mb = 8.0 * eng.gn_exchange_size(band) / 1e6
     else:
         eng.solve(max_iterations=1)  # warm-up
@@ -228,8 +278,10 @@ def gn_benchmark(eng, iters, torch, dist, dev, world):
             "breakdown_ms_per_iteration": {"linearize_ms": float(t[1]) / n, "step_ms": float(t[2]) / n,
                                            "cost_ms": float(t[3]) / n},
             "exchange_mb_per_iteration": exchange_mb,
-            "note": "host wall clock of the engine's LM loop (pba_solve" + (f"_distributed, {dist.get_backend()} all-reduce "
-                    "(nccl = RCCL) of the banded reduced camera system + 3 scalars per iteration" if world > 1 else "") +
+            "note": "host wall clock of the engine's LM loop (pba_solve" + (
+                "_distributed_comm: the device-steered loop with two RCCL all-reduces per trial on the engine stream "
+                "(the banded reduced camera system, then 8 point-part scalars)" if world > 1 and dist.get_backend() == "nccl"
+                else f"_distributed: {dist.get_backend()} all-reduces through a host callback" if world > 1 else "") +
                     "); noise-textured images, so the steps are not expected to converge — timing only"}
 
 
@@ -318,6 +370,7 @@ def main():
     ap.add_argument("--no-c3", action="store_true", help="skip the C3 Gauss-Newton measurement (configs[2])")
     ap.add_argument("--no-c5", action="store_true", help="skip the C5-style 21-px / fp16 / pyramid measurement")
     ap.add_argument("--no-weak", action="store_true", help="N > 1: skip the weak-scaling leg")
+    ap.add_argument("--no-c2", action="store_true", help="skip the C2 Ceres drop-in measurement (configs[1])")
     args = ap.parse_args()
 
     import torch
@@ -404,8 +457,15 @@ def main():
             except Exception:
                 traffic = None
         cpu = None
+        c2 = None
         if world == 1 and not args.no_cpu_baseline:
-            cpu = cpu_baseline(full, images.cpu().numpy(), args.cpu_seconds)
+            images_host = images.cpu().numpy()
+            cpu = cpu_baseline(full, images_host, args.cpu_seconds)
+            if not args.no_c2:
+                try:
+                    c2 = c2_dropin(full, images_host, host_cores()["usable"])
+                except Exception as ex:  # a secondary leg: report it, keep the headline line
+                    c2 = {"error": f"{type(ex).__name__}: {ex}"[:300]}
         out = {
             "metric": "photometric residual+jacobian blocks/sec",
             "value": value,
@@ -441,6 +501,7 @@ def main():
                 "kernel_avg_us": kern_us_local,
             },
             "cpu_baseline": cpu,
+            "c2": c2,
             "gn": gn,
             "gn_c3": c3,
             "c5": c5,

@@ -91,7 +91,7 @@ int pba_set_frames_device(pba_engine* engine, int32_t n_frames, const int32_t* f
 int pba_set_pattern(pba_engine* engine, int32_t P, const float* offsets);
 /* points: host keyframe, u_ref (2 doubles, pixel in the host image), host_intensity (P floats,
  * photometric only — the I_h,k of photometric_error.h:179; NULL: sampled on the device from the host keyframe's
- * image at u_ref + pattern offset, with the engine's interpolator: call pba_set_interpolator first). */
+ * image at u_ref + pattern offset, with the engine's interpolator; a later pba_set_interpolator samples them again). */
 int pba_set_points(pba_engine* engine, int32_t n_points, const int32_t* host_frame, const double* u_ref,
                    const float* host_intensity);
 /* blocks: point index and target keyframe per block; u_obs (2 doubles per block) for geometric engines.
@@ -116,7 +116,7 @@ int pba_evaluate_state_device(pba_engine* engine, const double* d_poses, const d
 int pba_synchronize(pba_engine* engine);
 
 /* Results ---------------------------------------------------------------------------------------- */
-int pba_record_floats(const pba_engine* engine);   /* 14·R (values per record, in the record format) */
+int pba_record_floats(const pba_engine* engine);   /* 14·R (22·R with pba_set_optimize_intrinsics) values per record */
 /* Record storage format (photometric engines): PBA_RECORD_F32 (default) or PBA_RECORD_F16 — IEEE half records,
  * half the HBM write traffic (config C5's "fp16 residuals"; evaluation stays fp64 warp + fp32 chain, rounding
  * only at the store: ≤ 2⁻¹¹ relative per value; values beyond the half range saturate at ±65504 — at full
@@ -127,6 +127,15 @@ int pba_record_floats(const pba_engine* engine);   /* 14·R (values per record, 
 #define PBA_RECORD_F16 1
 int pba_set_record_format(pba_engine* engine, int32_t format);
 int pba_record_format(const pba_engine* engine);
+/* Target-intrinsics Jacobian (geometric engines; BundleAdjustmentOptions::optimize_intrinsics, map_utils.h:339-345):
+ * the reference functor takes the TARGET camera's intrinsics as its 4th parameter block (sIntr_c2, reprojection.h:83-86,
+ * :108) and unprojects the host pixel with the intrinsics captured at problem build (ref_intrinsics, :93-98; Ceres never
+ * writes user memory during a solve without an evaluation callback, so those stay at their initial values).  Enabled,
+ * every projection uses the intrinsics state (pba_set_intrinsics_state, 8·n_cams doubles; initially the cameras'),
+ * host unprojection keeps the pba_set_cameras values, and each record grows by J_intr (R×8, row-major) after J_rho:
+ * 22·R values.  The on-device Gauss-Newton entry points refuse such an engine (PBA_ERR_INVALID_ARGUMENT). */
+int pba_set_optimize_intrinsics(pba_engine* engine, int32_t enable);
+int pba_set_intrinsics_state(pba_engine* engine, const double* intrinsics);
 /* Image interpolator of the photometric residual (and of the device-sampled I_h,k): PBA_INTERP_BILINEAR (default,
  * the north star's) or PBA_INTERP_BICUBIC — Ceres' BiCubicInterpolator over Grid2D<uint8_t, 1>
  * (cubic_interpolation.h:252-344, edge clamp :403-414), the interpolator of PhotometricError<8>
@@ -150,6 +159,12 @@ int pba_get_records(pba_engine* engine, float* records, uint8_t* valid);
  * whole record — what a residual-only evaluation needs, trust_region_minimizer.cc:761-779); valid may be NULL.
  * Synchronises. */
 int pba_get_residuals(pba_engine* engine, float* residuals, uint8_t* valid);
+/* Asynchronous read-back in chunks (fp32 records): enqueues the copies of records and validity into caller-owned
+ * page-locked memory behind the evaluation, chunk_blocks blocks per copy, and returns at once; pba_wait_records returns
+ * once the chunk holding `block` has arrived.  Thread-safe for concurrent waiters (Ceres' evaluator threads), so the
+ * per-block CostFunction::Evaluate work overlaps the transfer of later chunks (program_evaluator.h:187-258). */
+int pba_get_records_async(pba_engine* engine, float* records, uint8_t* valid, int32_t chunk_blocks);
+int pba_wait_records(pba_engine* engine, int32_t block);
 /* page-locked host memory for the read-back buffers of an adapter (records / residuals then arrive by DMA at
  * full PCIe rate instead of being staged through a driver buffer) */
 int pba_host_alloc(size_t bytes, void** ptr);
@@ -178,29 +193,50 @@ int pba_get_kernel_timing(pba_engine* engine, double* total_ms, int32_t* launche
  * structure of schur_complement_solver.cc:138-146), and the reduced camera system is factorised on the
  * device (block-skyline Cholesky, fp64).  Damping follows levenberg_marquardt_strategy.cc: (H + λ·D)δ = −g
  * with D = diag(JᵀJ) clamped to [1e-6, 1e32], λ = 1/trust-region radius. */
-#define PBA_TERMINATION_CONVERGENCE 0     /* a valid step with |cost − candidate cost| ≤ function_tolerance · cost
-                                           * (trust_region_minimizer.cc:115-117, :729-750); that step is NOT applied.
-                                           * Ceres' parameter/gradient tolerances are not evaluated. */
+/* Termination as Ceres' TerminationType (types.h): CONVERGENCE on a tolerance or the minimum trust region radius,
+ * NO_CONVERGENCE (here MAX_ITERATIONS) after max_iterations, FAILURE after max_num_consecutive_invalid_steps invalid
+ * steps; stop_reason says which test ended the solve (trust_region_minimizer.cc, in its order of evaluation):
+ *   gradient tolerance   max |x − (x ⊞ −∇)| ≤ gradient_tolerance at an accepted state (or the initial one), :668-684
+ *   parameter tolerance  |x − x_candidate| ≤ parameter_tolerance (|x| + parameter_tolerance) for a valid step, with
+ *                        |x| = −1 until the first accepted step (x_norm_, :185 / :814), :706-726
+ *   function tolerance   |cost − candidate cost| ≤ function_tolerance · cost for a valid step, :729-748
+ *   (neither candidate is applied) — norms in the ambient parameter space of the non-constant parameter blocks
+ *   (poses as Sophus [q | t], inverse distances).  A candidate that leaves a block invalid which is valid at the current
+ *   state has infinite cost (Ceres' failed Evaluate, :771-778). */
+#define PBA_TERMINATION_CONVERGENCE 0
 #define PBA_TERMINATION_MAX_ITERATIONS 1
-#define PBA_TERMINATION_FAILURE 2         /* trust region collapsed */
+#define PBA_TERMINATION_FAILURE 2
+
+#define PBA_STOP_MAX_ITERATIONS 0
+#define PBA_STOP_FUNCTION_TOLERANCE 1
+#define PBA_STOP_PARAMETER_TOLERANCE 2
+#define PBA_STOP_GRADIENT_TOLERANCE 3
+#define PBA_STOP_MIN_TRUST_REGION_RADIUS 4
+#define PBA_STOP_INVALID_STEPS 5
 
 typedef struct pba_solver_options {
-  int32_t max_iterations;               /* BundleAdjustmentOptions::max_num_iterations (20, map_utils.h:318) */
-  int32_t pad_;
-  double initial_trust_region_radius;   /* Ceres default 1e4 */
-  double function_tolerance;            /* Ceres default 1e-6 */
-  double parameter_tolerance;           /* reserved (Ceres default 1e-8) */
-  double min_relative_decrease;         /* Ceres default 1e-3 */
+  int32_t max_iterations;                     /* BundleAdjustmentOptions::max_num_iterations (20, map_utils.h:318) */
+  int32_t max_num_consecutive_invalid_steps;  /* Ceres default 5 (<= 0: 5) */
+  double initial_trust_region_radius;         /* Ceres default 1e4 */
+  double function_tolerance;                  /* Ceres default 1e-6 */
+  double parameter_tolerance;                 /* Ceres default 1e-8 */
+  double min_relative_decrease;               /* Ceres default 1e-3 */
+  double gradient_tolerance;                  /* Ceres default 1e-10 */
+  double max_trust_region_radius;             /* Ceres default 1e16 */
+  double min_trust_region_radius;             /* Ceres default 1e-32 */
 } pba_solver_options;
 
 typedef struct pba_solver_summary {
-  int32_t iterations, successful_steps, unsuccessful_steps, termination;
+  int32_t iterations;                   /* trials, the one that met a function / parameter tolerance included */
+  int32_t successful_steps, unsuccessful_steps, termination;
   double initial_cost, final_cost;      /* Σ ½ρ(‖r‖²) */
   /* total_ms: host wall clock of the whole solve.  The parts: pba_solve — device time between stream events, only
    * with pba_set_solver_timing(engine, 1) (the events cost the GPU a few µs of idle time each, so they are off by
    * default and the parts are then 0): solve_ms = Schur complement + reduced solve + candidate state, linearize_ms =
    * the linearisation at each candidate (which is also its cost; plus the initial one), cost_ms = the decision; pba_solve_distributed — host wall clock of each phase, collectives included. */
   double total_ms, linearize_ms, solve_ms, cost_ms;
+  double gradient_max_norm;             /* at the last state whose gradient was evaluated */
+  int32_t stop_reason, pad_;            /* PBA_STOP_* */
 } pba_solver_summary;
 /* per-phase device timing of pba_solve (linearize_ms / solve_ms / cost_ms of the summary); default off */
 int pba_set_solver_timing(pba_engine* engine, int32_t enable);
@@ -242,13 +278,35 @@ int pba_gn_step_export(pba_engine* engine, double lambda, int32_t band, double* 
  * pose part of the LM model decrease (identical on every rank), model_points this rank's point part. */
 int pba_gn_step_import(pba_engine* engine, double lambda, int32_t band, const double* d_exchange,
                        double* model_pose, double* model_points, int32_t* solver_status);
-/* In-place sum over all ranks of count doubles at d_buf (device memory of this engine's GPU), complete when
- * it returns; e.g. ncclAllReduce(d_buf, d_buf, count, ncclDouble, ncclSum, comm, stream) + stream sync. */
+/* pba_solve over all ranks, steered by the device LM record as on one GPU: per trial, the banded partial systems
+ * (count = pba_gn_exchange_size − 8 doubles) and then 8 point-part scalars (model decrease, candidate cost and valid
+ * blocks, step and state norms, points above the gradient tolerance) are summed over the ranks, and every rank takes the
+ * same decision on the device.  Two collectives per trial (trial i + 1's damping, hence its point elimination, depends
+ * on trial i's decision).
+ *
+ * The collective is either a host callback — the in-place sum over all ranks of count doubles at d_buf (device memory
+ * of this engine's GPU), called after the engine's stream has drained and complete when it returns — or a pba_comm,
+ * whose sums are enqueued on the engine's stream (the host then enqueues trial i + 1 before trial i's decision is
+ * known, as pba_solve does). */
 typedef int (*pba_allreduce_fn)(void* user, double* d_buf, int64_t count);
-/* pba_solve over all ranks: the same LM decisions everywhere (costs, model decreases and the reduced
- * system are all-reduced through `allreduce`, which every rank must call collectively). */
 int pba_solve_distributed(pba_engine* engine, const pba_solver_options* options, int32_t band, double* d_exchange,
                           pba_allreduce_fn allreduce, void* user, pba_solver_summary* summary);
+/* Communicators.  RCCL (one process per GPU, over xGMI): rank 0 gets a 128-byte id from pba_comm_unique_id and shares
+ * it (e.g. with torch.distributed.broadcast); every rank calls pba_comm_init (collective).  librccl.so.1 is opened at
+ * run time.  In-process group (tests / one-GPU rehearsal): pba_comm_init_local(n, device, comms) fills comms[0..n) for n
+ * engines on one device driven by n host threads; sums in rank order through events.  pba_comm_allreduce enqueues the
+ * in-place sum of count doubles at d_buf on hip_stream (every rank, same order). */
+typedef struct pba_comm pba_comm;
+int pba_comm_unique_id(void* id128);
+int pba_comm_init(const void* id128, int32_t n_ranks, int32_t rank, int32_t device, pba_comm** out_comm);
+int pba_comm_init_local(int32_t n_ranks, int32_t device, pba_comm** out_comms);
+int pba_comm_destroy(pba_comm* comm);
+int pba_comm_rank(const pba_comm* comm);
+int pba_comm_size(const pba_comm* comm);
+int pba_comm_allreduce(pba_comm* comm, double* d_buf, int64_t count, void* hip_stream);
+/* pba_solve_distributed over a communicator, with an exchange buffer owned by the engine */
+int pba_solve_distributed_comm(pba_engine* engine, const pba_solver_options* options, int32_t band, pba_comm* comm,
+                               pba_solver_summary* summary);
 
 /* Image pyramid / coarse-to-fine ------------------------------------------
  * pba_build_pyramid builds levels 1 … n−1 on the device from the current frames, cameras and points (DSO

@@ -13,11 +13,19 @@
 //                          evaluator's record buffer (Ceres calls it from num_threads workers,
 //                          program_evaluator.h:187-229); returns false for invalid blocks like a functor
 //                          whose projection failed (residual_block.cc:113-131).
-//   * SE3TangentParameterization : ceres::LocalParameterization with the SAME Plus as the reference's
-//                          LocalParameterizationSE3 (T·exp(δ), local_parameterization_se3.hpp:43-50) and
-//                          Jacobian [I₆; 0].  The engine returns tangent-space Jacobians J6; the adapter
-//                          exposes the 7-wide global Jacobian [J6 | 0], so Ceres' J_global·P
-//                          (residual_block.cc:136-158) reproduces J6 exactly.
+//   * Pose Jacobians.  The engine returns tangent-space Jacobians J6 (∂r/∂δ with T ⊞ δ = T·exp(δ)).  Ceres multiplies
+//     the 7-wide global Jacobian a CostFunction returns by the LocalParameterization's 7×6 Jacobian P
+//     (residual_block.cc:136-158), so the adapter writes J7 = J6·P⁺ with P⁺ = (PᵀP)⁻¹Pᵀ and P the reference's own
+//     Sophus::test::LocalParameterizationSE3::ComputeJacobian = Dx_this_mul_exp_x_at_0 (local_parameterization_se3.hpp:
+//     56-63, se3.hpp:135-203) at the evaluation point: J7·P = J6 for any full-rank P, so the reference's
+//     bundle_adjustment() keeps its LocalParameterizationSE3 registered unchanged (map_utils.h:331-333).
+//     Alternatively (PoseJacobian::kTangent) the adapter writes [J6 | 0] for SE3TangentParameterization: the SAME
+//     Plus (T·exp(δ), local_parameterization_se3.hpp:43-50) with Jacobian [I₆; 0] — no per-frame P⁺ to form.
+//   * Intrinsics (geometric): given the cameras' intrinsics parameter blocks, the evaluator enables the engine's target-
+//     intrinsics Jacobian (pba_set_optimize_intrinsics) and uploads the blocks' current values before every
+//     evaluation, so Ceres may leave them free (BundleAdjustmentOptions::optimize_intrinsics, map_utils.h:339-345).
+//     Without them, a Jacobian request for an intrinsics block is refused: that Evaluate returns false and Ceres
+//     stops with FAILURE instead of optimising with a zero gradient.
 //
 // The loss function stays with Ceres (HuberLoss is applied after Evaluate, residual_block.cc:161-196).
 // Requires <ceres/ceres.h> (Ceres ≥ 2.0, which has EvaluationCallback) and include/pba.h on the include path.
@@ -25,6 +33,7 @@
 
 #include <ceres/ceres.h>
 
+#include <atomic>
 #include <cmath>
 #include <cstring>
 #include <stdexcept>
@@ -71,6 +80,56 @@ inline void se3_plus(const double* T, const double* d, double* out) {
   out[6] = T[6] + tz + aw * u2 + (ax * u1 - ay * u0);
 }
 
+// Sophus SE3::Dx_this_mul_exp_x_at_0 (se3.hpp:135-203), 7×6 row-major: rows [q(4) | t(3)], columns [υ(3) | ω(3)];
+// the quaternion rows are ½·(q ⊗ ·) on ω, the translation rows R(q) on υ.
+inline void se3_plus_jacobian(const double* T, double* P) {
+  const double x = T[0], y = T[1], z = T[2], w = T[3];
+  for (int i = 0; i < 42; ++i) P[i] = 0.0;
+  const double hx = 0.5 * x, hy = 0.5 * y, hz = 0.5 * z, hw = 0.5 * w;
+  P[0 * 6 + 3] = hw;  P[0 * 6 + 4] = -hz; P[0 * 6 + 5] = hy;
+  P[1 * 6 + 3] = hz;  P[1 * 6 + 4] = hw;  P[1 * 6 + 5] = -hx;
+  P[2 * 6 + 3] = -hy; P[2 * 6 + 4] = hx;  P[2 * 6 + 5] = hw;
+  P[3 * 6 + 3] = -hx; P[3 * 6 + 4] = -hy; P[3 * 6 + 5] = -hz;
+  const double ww = w * w, xx = x * x, yy = y * y, zz = z * z;
+  P[4 * 6 + 0] = ww + xx - yy - zz;     P[4 * 6 + 1] = 2 * (x * y - w * z); P[4 * 6 + 2] = 2 * (w * y + x * z);
+  P[5 * 6 + 0] = 2 * (w * z + x * y);   P[5 * 6 + 1] = ww - xx + yy - zz;   P[5 * 6 + 2] = 2 * (y * z - w * x);
+  P[6 * 6 + 0] = 2 * (x * z - w * y);   P[6 * 6 + 1] = 2 * (w * x + y * z); P[6 * 6 + 2] = ww - xx - yy + zz;
+}
+
+// M = (PᵀP)⁻¹Pᵀ (6×7 row-major), the left inverse of P above: MP = I₆.  PᵀP is block diagonal (the υ columns only touch
+// the translation rows, the ω columns only the quaternion rows), so its inverse is two 3×3 inverses.
+inline void se3_plus_jacobian_pinv(const double* T, double* M) {
+  double P[42];
+  se3_plus_jacobian(T, P);
+  for (int i = 0; i < 42; ++i) M[i] = 0.0;
+  for (int blk = 0; blk < 2; ++blk) {
+    const int c0 = 3 * blk, r0 = blk == 0 ? 4 : 0, nr = blk == 0 ? 3 : 4;
+    double A[9];  // PᵀP block
+    for (int i = 0; i < 3; ++i)
+      for (int j = 0; j < 3; ++j) {
+        double a = 0.0;
+        for (int r = r0; r < r0 + nr; ++r) a += P[r * 6 + c0 + i] * P[r * 6 + c0 + j];
+        A[3 * i + j] = a;
+      }
+    const double c00 = A[4] * A[8] - A[5] * A[7], c01 = A[5] * A[6] - A[3] * A[8], c02 = A[3] * A[7] - A[4] * A[6];
+    const double det = A[0] * c00 + A[1] * c01 + A[2] * c02, id = 1.0 / det;
+    const double Ai[9] = {c00 * id, (A[2] * A[7] - A[1] * A[8]) * id, (A[1] * A[5] - A[2] * A[4]) * id,
+                          c01 * id, (A[0] * A[8] - A[2] * A[6]) * id, (A[2] * A[3] - A[0] * A[5]) * id,
+                          c02 * id, (A[1] * A[6] - A[0] * A[7]) * id, (A[0] * A[4] - A[1] * A[3]) * id};
+    for (int i = 0; i < 3; ++i)
+      for (int r = r0; r < r0 + nr; ++r) {
+        double m = 0.0;
+        for (int j = 0; j < 3; ++j) m += Ai[3 * i + j] * P[r * 6 + c0 + j];
+        M[(c0 + i) * 7 + r] = m;
+      }
+  }
+}
+
+enum class PoseJacobian {
+  kReferenceSE3,  // J7 = J6·P⁺ for the reference's Sophus::test::LocalParameterizationSE3 (default)
+  kTangent        // [J6 | 0] for SE3TangentParameterization
+};
+
 class SE3TangentParameterization : public ceres::LocalParameterization {
  public:
   bool Plus(const double* x, const double* delta, double* x_plus_delta) const override {
@@ -116,9 +175,16 @@ class PinnedArray {
 class GpuEvaluator : public ceres::EvaluationCallback {
  public:
   // poses[f] = T_w_c.data() of keyframe f (7 doubles, user memory Ceres optimises in place);
-  // inv_dist[p] = &landmark.inv_depth of point p.  The engine must already hold the problem structure.
-  GpuEvaluator(pba_engine* engine, std::vector<double*> poses, std::vector<double*> inv_dist)
-      : engine_(engine), poses_(std::move(poses)), rho_(std::move(inv_dist)) {
+  // inv_dist[p] = &landmark.inv_depth of point p; intrinsics[c] = calib_cam.intrinsics[c]->data() (8 doubles) when the
+  // geometric problem's intrinsics blocks may be free (optimize_intrinsics), else empty.  The engine must already hold
+  // the problem structure.
+  GpuEvaluator(pba_engine* engine, std::vector<double*> poses, std::vector<double*> inv_dist,
+               std::vector<double*> intrinsics = {}, PoseJacobian pose_jacobian = PoseJacobian::kReferenceSE3)
+      : engine_(engine), poses_(std::move(poses)), rho_(std::move(inv_dist)), intr_(std::move(intrinsics)),
+        form_(pose_jacobian) {
+    if (pba_record_format(engine_) != PBA_RECORD_F32)
+      throw std::runtime_error("pba_ceres: fp16 records saturate at ±65504; the adapter needs PBA_RECORD_F32");
+    if (!intr_.empty()) check(pba_set_optimize_intrinsics(engine_, 1), "pba_set_optimize_intrinsics");
     R_ = pba_residuals_per_block(engine_);
     rec_ = pba_record_floats(engine_);
   }
@@ -135,17 +201,30 @@ class GpuEvaluator : public ceres::EvaluationCallback {
     for (size_t f = 0; f < poses_.size(); ++f) std::memcpy(&state_p_[7 * f], poses_[f], 7 * sizeof(double));
     for (size_t p = 0; p < rho_.size(); ++p) state_r_[p] = *rho_[p];
     check(pba_set_state(engine_, state_p_.data(), state_r_.data()), "pba_set_state");
+    if (!intr_.empty()) {
+      state_k_.resize(8 * intr_.size());
+      for (size_t c = 0; c < intr_.size(); ++c) std::memcpy(&state_k_[8 * c], intr_[c], 8 * sizeof(double));
+      check(pba_set_intrinsics_state(engine_, state_k_.data()), "pba_set_intrinsics_state");
+    }
+    if (evaluate_jacobians && form_ == PoseJacobian::kReferenceSE3) {  // P⁺ of every pose at this point (overlaps the launch)
+      pinv_.resize(42 * poses_.size());
+      for (size_t f = 0; f < poses_.size(); ++f) se3_plus_jacobian_pinv(&state_p_[7 * f], &pinv_[42 * f]);
+    }
     check(pba_evaluate(engine_, evaluate_jacobians ? 1 : 0), "pba_evaluate");
     const size_t nb = (size_t)pba_num_blocks(engine_);
     valid_.resize(nb);
     if (evaluate_jacobians) {
+      // chunked asynchronous read-back: each block's Evaluate waits only for its chunk (wait()), so Ceres' per-block
+      // work overlaps the rest of the transfer
       records_.resize(nb * rec_);
-      check(pba_get_records(engine_, records_.data(), valid_.data()), "pba_get_records");
+      check(pba_get_records_async(engine_, records_.data(), valid_.data(), kChunkBlocks), "pba_get_records_async");
+      async_ = true;
       res_ = records_.data();
       res_stride_ = rec_;
     } else {
       residuals_.resize(nb * R_);
       check(pba_get_residuals(engine_, residuals_.data(), valid_.data()), "pba_get_residuals");
+      async_ = false;
       res_ = residuals_.data();
       res_stride_ = R_;
     }
@@ -153,16 +232,31 @@ class GpuEvaluator : public ceres::EvaluationCallback {
     have_jac_ = evaluate_jacobians;
   }
 
+  // Block `block`'s record (and validity) has arrived in host memory; called by Evaluate on Ceres' worker threads.
+  void wait(int block) const {
+    if (async_) check(pba_wait_records(engine_, block), "pba_wait_records");
+  }
+  static constexpr int kChunkBlocks = 4096;
+
   int residuals_per_block() const { return R_; }
   const float* record(int block) const { return records_.data() + (size_t)block * rec_; }  // with has_jacobians()
   const float* residuals(int block) const { return res_ + (size_t)block * res_stride_; }
   bool valid(int block) const { return valid_[block] != 0; }
   bool has_jacobians() const { return have_jac_; }
+  bool has_intrinsics() const { return !intr_.empty(); }
+  PoseJacobian pose_jacobian() const { return form_; }
+  const double* pose_pinv(int frame) const { return &pinv_[42 * (size_t)frame]; }  // P⁺ (6×7) at the prepared point
+  // a Jacobian was requested for an intrinsics block the evaluator was not given (Evaluate returned false)
+  bool refused_intrinsics() const { return refused_.load(); }
+  void refuse_intrinsics() const { refused_.store(true); }
 
  private:
   pba_engine* engine_;
-  std::vector<double*> poses_, rho_;
-  std::vector<double> state_p_, state_r_;
+  std::vector<double*> poses_, rho_, intr_;
+  PoseJacobian form_;
+  bool async_ = false;
+  std::vector<double> state_p_, state_r_, state_k_, pinv_;
+  mutable std::atomic<bool> refused_{false};
   PinnedArray<float> records_, residuals_;
   PinnedArray<uint8_t> valid_;
   const float* res_ = nullptr;
@@ -171,29 +265,48 @@ class GpuEvaluator : public ceres::EvaluationCallback {
   bool have_point_ = false, have_jac_ = false;
 };
 
-// Copy one block's record into Ceres' buffers.  Parameter blocks: T_w_host[7], T_w_target[7], ρ[1], and —
-// for the geometric functor's signature (reprojection.h:83-86) — the target intrinsics[8] (constant in the
-// reference, map_utils.h:340-345; its Jacobian is reported as zero).
-inline bool copy_block(const GpuEvaluator& ev, int block, int R, double* residuals, double** jacobians, int n_intr) {
+// One pose block's global Jacobian (R×7 row-major) from the record's tangent rows J6 (stride 6).
+inline void pose_jacobian_7(const GpuEvaluator& ev, int frame, const float* j6, int R, double* out) {
+  if (ev.pose_jacobian() == PoseJacobian::kTangent) {
+    for (int k = 0; k < R; ++k) {
+      for (int c = 0; c < 6; ++c) out[k * 7 + c] = j6[6 * k + c];
+      out[k * 7 + 6] = 0.0;
+    }
+    return;
+  }
+  const double* M = ev.pose_pinv(frame);  // J7 = J6·P⁺
+  for (int k = 0; k < R; ++k) {
+    double row[6];
+    for (int c = 0; c < 6; ++c) row[c] = j6[6 * k + c];
+    for (int g = 0; g < 7; ++g) {
+      double v = 0.0;
+      for (int c = 0; c < 6; ++c) v += row[c] * M[c * 7 + g];
+      out[k * 7 + g] = v;
+    }
+  }
+}
+
+// Copy one block's record into Ceres' buffers.  Parameter blocks: T_w_host[7], T_w_target[7], ρ[1], and — for the
+// geometric functor's signature (reprojection.h:83-86) — the target intrinsics[8] (n_intr = 8).
+inline bool copy_block(const GpuEvaluator& ev, int block, int host, int target, int R, double* residuals,
+                       double** jacobians, int n_intr) {
+  ev.wait(block);
   if (!ev.valid(block)) return false;
   const float* res = ev.residuals(block);
   for (int k = 0; k < R; ++k) residuals[k] = res[k];
   if (!jacobians) return true;
   if (!ev.has_jacobians()) return false;  // Ceres asked for J at a point evaluated residual-only
-  const float* rec = ev.record(block);
-  for (int k = 0; k < R; ++k) {
-    if (jacobians[0]) {
-      for (int c = 0; c < 6; ++c) jacobians[0][k * 7 + c] = rec[R + 6 * k + c];
-      jacobians[0][k * 7 + 6] = 0.0;
-    }
-    if (jacobians[1]) {
-      for (int c = 0; c < 6; ++c) jacobians[1][k * 7 + c] = rec[7 * R + 6 * k + c];
-      jacobians[1][k * 7 + 6] = 0.0;
-    }
-    if (jacobians[2]) jacobians[2][k] = rec[13 * R + k];
-    if (n_intr && jacobians[3])
-      for (int c = 0; c < n_intr; ++c) jacobians[3][k * n_intr + c] = 0.0;
+  if (n_intr && jacobians[3] && !ev.has_intrinsics()) {  // a free intrinsics block the engine was not told about
+    ev.refuse_intrinsics();
+    return false;
   }
+  const float* rec = ev.record(block);
+  if (jacobians[0]) pose_jacobian_7(ev, host, rec + R, R, jacobians[0]);
+  if (jacobians[1]) pose_jacobian_7(ev, target, rec + 7 * R, R, jacobians[1]);
+  if (jacobians[2])
+    for (int k = 0; k < R; ++k) jacobians[2][k] = rec[13 * R + k];
+  if (n_intr && jacobians[3])  // ∂r/∂sIntr_c2, the record's tail (pba_set_optimize_intrinsics)
+    for (int i = 0; i < R * n_intr; ++i) jacobians[3][i] = rec[14 * R + i];
   return true;
 }
 
@@ -201,28 +314,30 @@ inline bool copy_block(const GpuEvaluator& ev, int block, int R, double* residua
 template <int P>
 class GpuPhotometricCost : public ceres::SizedCostFunction<P, 7, 7, 1> {
  public:
-  GpuPhotometricCost(const GpuEvaluator* ev, int block) : ev_(ev), block_(block) {}
+  GpuPhotometricCost(const GpuEvaluator* ev, int block, int host, int target)
+      : ev_(ev), block_(block), host_(host), target_(target) {}
   bool Evaluate(double const* const* /*parameters*/, double* residuals, double** jacobians) const override {
-    return copy_block(*ev_, block_, P, residuals, jacobians, 0);
+    return copy_block(*ev_, block_, host_, target_, P, residuals, jacobians, 0);
   }
 
  private:
   const GpuEvaluator* ev_;
-  int block_;
+  int block_, host_, target_;
 };
 
 // Geometric block: SizedCostFunction<2, 7, 7, 1, 8> — the reference's AutoDiffCostFunction signature
 // (map_utils.h:365-367) so AddResidualBlock(…, T_w_host, T_w_target, &inv_depth, intrinsics) is unchanged.
 class GpuReprojectionCost : public ceres::SizedCostFunction<2, 7, 7, 1, 8> {
  public:
-  GpuReprojectionCost(const GpuEvaluator* ev, int block) : ev_(ev), block_(block) {}
+  GpuReprojectionCost(const GpuEvaluator* ev, int block, int host, int target)
+      : ev_(ev), block_(block), host_(host), target_(target) {}
   bool Evaluate(double const* const* /*parameters*/, double* residuals, double** jacobians) const override {
-    return copy_block(*ev_, block_, 2, residuals, jacobians, 8);
+    return copy_block(*ev_, block_, host_, target_, 2, residuals, jacobians, 8);
   }
 
  private:
   const GpuEvaluator* ev_;
-  int block_;
+  int block_, host_, target_;
 };
 
 }  // namespace pba_ceres

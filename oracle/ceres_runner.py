@@ -23,7 +23,11 @@ def available() -> bool:
 
 
 def run(mode: str, pb, iters: int = 20, huber: float = 1.0, threads: int = 8, fixed=(0, 1), ftol: float = 1e-6,
-        timeout: float = 600.0) -> dict:
+        timeout: float = 600.0, ptol: float = 1e-8, gtol: float = 1e-10, optimize_intrinsics: bool = False,
+        pose_param: str = "ref") -> dict:
+    """pose_param: "ref" — the reference's LocalParameterizationSE3 in both modes (the GPU adapter then emits 7-wide
+    Jacobians J6·P⁺); "tangent" — the adapter's SE3TangentParameterization in gpu mode.  optimize_intrinsics: 0 constant
+    intrinsics blocks, 1 free (the GPU evaluator is given them), 2 free but not given to the evaluator (refusal)."""
     from make_golden import write_problem
     with tempfile.TemporaryDirectory() as td:
         fin, fout = os.path.join(td, "in.bin"), os.path.join(td, "out.json")
@@ -31,13 +35,17 @@ def run(mode: str, pb, iters: int = 20, huber: float = 1.0, threads: int = 8, fi
             write_problem(f, pb)
         fx = ",".join(str(int(i)) for i in fixed) if len(fixed) else "-"
         subprocess.run([DRIVER, mode, fin, fout, str(iters), repr(float(huber)), str(threads), fx, repr(float(ftol)),
-                        str(int(getattr(pb, "interp", 0)))], check=True, timeout=timeout)
+                        str(int(getattr(pb, "interp", 0))), repr(float(ptol)), repr(float(gtol)),
+                        str(int(optimize_intrinsics)), pose_param], check=True, timeout=timeout)
         with open(fout) as f:
             out = json.load(f)
     out["poses"] = np.asarray(out["poses"]).reshape(-1, 7)
     out["rho"] = np.asarray(out["rho"])
-    it = np.asarray(out["iterations"], np.float64).reshape(-1, 5)
+    it = np.asarray(out["iterations"], np.float64).reshape(-1, 7)
     out["costs"] = it[:, 1]
     out["step_ok"] = it[:, 2].astype(bool)
     out["relative_decrease"] = it[:, 3]
+    out["step_norm"] = it[:, 5]
+    out["gradient_max_norm"] = it[:, 6]
+    out["intrinsics"] = np.asarray(out["intrinsics"]).reshape(-1, 8)
     return out

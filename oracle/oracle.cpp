@@ -199,14 +199,14 @@ inline void se3_mul(const double* a, const double* b, double* out) {
 // ----------------------------------------------------------------------------------------------
 enum { CAM_PINHOLE = 0, CAM_DS = 1, CAM_EUCM = 2, CAM_KB4 = 3 };
 
-template <class T>
-inline void project(int model, const double* k, const T p[3], T uv[2]) {
-  const double fx = k[0], fy = k[1], cx = k[2], cy = k[3];
+template <class T, class K = double>
+inline void project(int model, const K* k, const T p[3], T uv[2]) {
+  const K fx = k[0], fy = k[1], cx = k[2], cy = k[3];
   if (model == CAM_PINHOLE) {  // camera_models.h:75-91
     uv[0] = fx * p[0] / p[2] + cx;
     uv[1] = fy * p[1] / p[2] + cy;
   } else if (model == CAM_DS) {  // camera_models.h:226-245
-    const double xi = k[4], alpha = k[5];
+    const K xi = k[4], alpha = k[5];
     const T d1 = sqrt(p[0] * p[0] + p[1] * p[1] + p[2] * p[2]);
     const T xi_d1_z = xi * d1 + p[2];
     const T d2 = sqrt(p[0] * p[0] + p[1] * p[1] + xi_d1_z * xi_d1_z);
@@ -214,12 +214,12 @@ inline void project(int model, const double* k, const T p[3], T uv[2]) {
     uv[0] = fx * p[0] / denom + cx;
     uv[1] = fy * p[1] / denom + cy;
   } else if (model == CAM_EUCM) {  // camera_models.h:140-160
-    const double alpha = k[4], beta = k[5];
+    const K alpha = k[4], beta = k[5];
     const T d = sqrt(beta * (p[0] * p[0] + p[1] * p[1]) + p[2] * p[2]);
     uv[0] = fx * p[0] / (alpha * d + (1.0 - alpha) * p[2]) + cx;
     uv[1] = fy * p[1] / (alpha * d + (1.0 - alpha) * p[2]) + cy;
   } else {  // Kannala-Brandt 4, camera_models.h:316-348
-    const double k1 = k[4], k2 = k[5], k3 = k[6], k4 = k[7];
+    const K k1 = k[4], k2 = k[5], k3 = k[6], k4 = k[7];
     const T r = sqrt(p[0] * p[0] + p[1] * p[1]);
     if (val(r) == 0.0) {
       uv[0] = T(cx);
@@ -395,12 +395,15 @@ inline void seed_pose(const double* p, int, Quat<double>& q, double t[3]) {
 }
 inline J15 seed_rho(double r) { return J15(r, 14); }
 
-// Geometric functor (reprojection.h:83-112).  Returns false if a result is non-finite.
+// Geometric functor (reprojection.h:83-112).  Returns false if a result is non-finite.  intr_state (optional): the
+// target intrinsics parameter blocks sIntr_c2 (8 per camera) when they differ from the ones the host unprojection
+// captured (ref_intrinsics, reprojection.h:93-98; optimize_intrinsics, map_utils.h:339-345).
 template <class T>
-bool geometric_block(const orc_problem& pb, const double* poses, const double* rho, int b, T res[2]) {
+bool geometric_block(const orc_problem& pb, const double* poses, const double* rho, int b, T res[2],
+                     const double* intr_state = nullptr) {
   const int pt = pb.block_point[b], tgt = pb.block_target[b], host = pb.point_host[pt];
   const double* kh = pb.intrinsics + 8 * pb.frame_cam[host];
-  const double* kt = pb.intrinsics + 8 * pb.frame_cam[tgt];
+  const double* kt = (intr_state ? intr_state : pb.intrinsics) + 8 * pb.frame_cam[tgt];
   Quat<T> qh, qt; T th[3], tt[3];
   seed_pose(poses + 7 * host, 0, qh, th);
   seed_pose(poses + 7 * tgt, 7, qt, tt);
@@ -421,6 +424,36 @@ bool geometric_block(const orc_problem& pb, const double* poses, const double* r
   res[0] = pb.u_obs[2 * b + 0] - uv[0];
   res[1] = pb.u_obs[2 * b + 1] - uv[1];
   return std::isfinite(val(res[0])) && std::isfinite(val(res[1]));
+}
+
+// ∂r/∂sIntr_c2 (2×8 row-major) of the geometric functor: the point in the target frame in double, then the projection
+// with dual-number intrinsics (AutoDiffCostFunction's 4th parameter block, reprojection.h:86,108).
+bool geometric_intr_jacobian(const orc_problem& pb, const double* poses, const double* rho, int b,
+                             const double* intr_state, double J[16]) {
+  using J8 = Jet<8>;
+  const int pt = pb.block_point[b], tgt = pb.block_target[b], host = pb.point_host[pt];
+  const double* kh = pb.intrinsics + 8 * pb.frame_cam[host];
+  const double* kt = intr_state + 8 * pb.frame_cam[tgt];
+  Quat<double> qh, qt; double th[3], tt[3];
+  seed_pose(poses + 7 * host, 0, qh, th);
+  seed_pose(poses + 7 * tgt, 7, qt, tt);
+  double bear[3];
+  unproject(pb.model, kh, pb.u_ref + 2 * pt, bear);
+  const double ph[3] = {bear[0] / rho[pt], bear[1] / rho[pt], bear[2] / rho[pt]};
+  double pw[3];
+  qrot(qh, ph, pw);
+  const double d[3] = {pw[0] + th[0] - tt[0], pw[1] + th[1] - tt[1], pw[2] + th[2] - tt[2]};
+  double p3[3];
+  qrot(qconj(qt), d, p3);
+  J8 k[8], p[3], uv[2];
+  for (int i = 0; i < 8; ++i) k[i] = J8(kt[i], i);
+  for (int i = 0; i < 3; ++i) p[i] = J8(p3[i]);
+  project(pb.model, k, p, uv);
+  for (int r = 0; r < 2; ++r)
+    for (int i = 0; i < 8; ++i) J[8 * r + i] = -uv[r].v[i];
+  for (int i = 0; i < 16; ++i)
+    if (!std::isfinite(J[i])) return false;
+  return true;
 }
 
 // Photometric functor (photometric_error.h:139-182, bilinear or bicubic interpolator, camera per frame).
@@ -465,9 +498,9 @@ int record_size(const orc_problem& pb) {
 }
 
 void eval_range(const orc_problem& pb, const double* poses, const double* rho, int want_jac, double* out,
-                uint8_t* valid, int b0, int b1) {
+                uint8_t* valid, int b0, int b1, const double* intr_state = nullptr) {
   const int R = pb.kind == 0 ? pb.P : 2;
-  const int rec = 14 * R;
+  const int rec = (intr_state ? 22 : 14) * R;
   std::vector<J15> rj(R);
   std::vector<double> rd(R);
   double Ph[42], Pt[42];
@@ -477,11 +510,12 @@ void eval_range(const orc_problem& pb, const double* poses, const double* rho, i
     bool ok;
     if (!want_jac) {
       ok = pb.kind == 0 ? photometric_block<double>(pb, poses, rho, b, rd.data())
-                        : geometric_block<double>(pb, poses, rho, b, rd.data());
+                        : geometric_block<double>(pb, poses, rho, b, rd.data(), intr_state);
       if (ok) for (int k = 0; k < R; ++k) o[k] = rd[k];
     } else {
       ok = pb.kind == 0 ? photometric_block<J15>(pb, poses, rho, b, rj.data())
-                        : geometric_block<J15>(pb, poses, rho, b, rj.data());
+                        : geometric_block<J15>(pb, poses, rho, b, rj.data(), intr_state);
+      if (ok && intr_state) ok = geometric_intr_jacobian(pb, poses, rho, b, intr_state, o + 14 * R);
       if (ok) {
         const int pt = pb.block_point[b];
         const int host = pb.point_host[pt], tgt = pb.block_target[b];
@@ -514,6 +548,15 @@ void eval_range(const orc_problem& pb, const double* poses, const double* rho, i
 extern "C" {
 
 int orc_record_size(const orc_problem* pb) { return record_size(*pb); }
+
+// Geometric blocks with the target intrinsics as parameters (optimize_intrinsics): records of 22·R values, the last 8·R
+// being ∂r/∂sIntr_c2 (R×8) evaluated at intr_state (8·n_cams); the host unprojection uses pb->intrinsics.
+int orc_evaluate_intrinsics(const orc_problem* pb, const double* poses, const double* rho, const double* intr_state,
+                            int want_jac, double* out, uint8_t* valid) {
+  if (!pb || !poses || !rho || !out || !intr_state || pb->kind != 1 || !pb->u_obs) return -1;
+  eval_range(*pb, poses, rho, want_jac, out, valid, 0, pb->n_blocks, intr_state);
+  return 0;
+}
 
 // Evaluate every residual block; `out` holds n_blocks records of record_size doubles.
 int orc_evaluate(const orc_problem* pb, const double* poses, const double* rho, int want_jac, double* out,

@@ -40,6 +40,9 @@ def lib():
         L = C.CDLL(path)
         L.orc_evaluate.argtypes = [C.POINTER(OrcProblem), C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_int]
         L.orc_evaluate.restype = C.c_int
+        L.orc_evaluate_intrinsics.argtypes = [C.POINTER(OrcProblem), C.c_void_p, C.c_void_p, C.c_void_p, C.c_int,
+                                              C.c_void_p, C.c_void_p]
+        L.orc_evaluate_intrinsics.restype = C.c_int
         L.orc_huber_block.argtypes = [C.c_void_p, C.c_int, C.c_double, C.POINTER(C.c_double)]
         L.orc_huber_block.restype = C.c_double
         for name, n in [("orc_se3_exp", 2), ("orc_se3_mul", 3), ("orc_se3_plus", 3), ("orc_se3_plus_jacobian", 2),
@@ -120,6 +123,25 @@ def evaluate(pb, poses=None, rho=None, want_jac: bool = True, n_threads: int = 1
     rc = L.orc_evaluate(C.byref(s), _ptr(poses), _ptr(rho), int(bool(want_jac)), _ptr(out), _ptr(valid), int(n_threads))
     if rc != 0:
         raise RuntimeError(f"orc_evaluate failed ({rc})")
+    return out, valid
+
+
+def evaluate_intrinsics(pb, intr_state, poses=None, rho=None, want_jac: bool = True):
+    """Geometric blocks with the target intrinsics as a parameter block (optimize_intrinsics): (records (n_blocks, 44)
+    float64 = [r | J_host | J_target | J_rho | J_intr (2×8)], valid).  Projection with intr_state (n_cams × 8), host
+    unprojection with pb.intrinsics."""
+    L = lib()
+    keep = _Keep()
+    s = make_problem_struct(pb, keep)
+    poses = keep(pb.poses if poses is None else poses, np.float64)
+    rho = keep(pb.rho if rho is None else rho, np.float64)
+    ks = keep(intr_state, np.float64)
+    out = np.zeros((pb.n_blocks, 44), np.float64)
+    valid = np.zeros(pb.n_blocks, np.uint8)
+    rc = L.orc_evaluate_intrinsics(C.byref(s), _ptr(poses), _ptr(rho), _ptr(ks), int(bool(want_jac)), _ptr(out),
+                                   _ptr(valid))
+    if rc != 0:
+        raise RuntimeError(f"orc_evaluate_intrinsics failed ({rc})")
     return out, valid
 
 

@@ -227,6 +227,59 @@ __device__ __forceinline__ void project_jac(const S* k, const V3<S>& p, S iden, 
   dv = {-fy * iden * my * dden.x, fy * iden * (one - my * dden.y), -fy * iden * my * dden.z};
 }
 
+// ∂π/∂k (rows du, dv; 8 columns) of the projection at p with respect to the intrinsics k = [fx fy cx cy p1 p2 p3 p4]
+// (tk layout), given iden from project() — the Jacobian the reference's functor takes for its sIntr_c2 parameter block
+// (reprojection.h:83-86, :108; AutoDiffCostFunction<…, 8>), free when BundleAdjustmentOptions::optimize_intrinsics is set
+// (map_utils.h:339-345).  fp64.  Pinhole (camera_models.h:75-91): u = fx x/z + cx.  DS (:226-245) and EUCM (:140-160):
+// u = fx x/den + cx with ∂den/∂(ξ, α) = (α kk d1/d2 + (1 − α) d1, d2 − kk) resp. ∂den/∂(α, β) = (ρ − z, α (x² + y²)/2ρ).
+// KB4 (:316-348): u = fx d(θ) x/r + cx with ∂d/∂k_i = θ^(2i+1).
+template <int MODEL>
+__device__ __forceinline__ void project_intr_jac(const double* k, const Vec3d& p, double iden, double* du, double* dv) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) du[j] = dv[j] = 0.0;
+  du[2] = 1.0;
+  dv[3] = 1.0;
+  if (MODEL == CAM_KB4) {
+    const double r = sqrt(p.x * p.x + p.y * p.y);
+    if (r == 0.0) return;  // u = cx, v = cy
+    const double c = p.x / r, s = p.y / r, th = atan2(r, p.z), t2 = th * th;
+    du[0] = iden * p.x;  // d(θ)·x/r (iden = d/r from project())
+    dv[1] = iden * p.y;
+    double t = t2 * th;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      du[4 + i] = k[0] * c * t;
+      dv[4 + i] = k[1] * s * t;
+      t *= t2;
+    }
+    return;
+  }
+  const double mx = p.x * iden, my = p.y * iden;
+  du[0] = mx;
+  dv[1] = my;
+  if (MODEL == CAM_PINHOLE) return;
+  double d4, d5;  // ∂den/∂p1, ∂den/∂p2
+  if (MODEL == CAM_DS) {
+    const double xi = k[4], al = k[5];
+    const double d1 = sqrt(p.x * p.x + p.y * p.y + p.z * p.z);
+    const double kk = xi * d1 + p.z;
+    const double d2 = sqrt(p.x * p.x + p.y * p.y + kk * kk);
+    d4 = al * kk * d1 / d2 + (1.0 - al) * d1;
+    d5 = d2 - kk;
+  } else {
+    const double al = k[4], be = k[5];
+    const double r2 = p.x * p.x + p.y * p.y;
+    const double rho = sqrt(be * r2 + p.z * p.z);
+    d4 = rho - p.z;
+    d5 = al * r2 / (2.0 * rho);
+  }
+  // ∂u/∂den = −fx x/den² = −fx mx iden
+  du[4] = -k[0] * mx * iden * d4;
+  du[5] = -k[0] * mx * iden * d5;
+  dv[4] = -k[1] * my * iden * d4;
+  dv[5] = -k[1] * my * iden * d5;
+}
+
 // Keyframe images live in HBM as 16×8-texel tiles of 128 B (one L2 line): tile (x>>4, y>>3) at
 // ((y>>3)·tiles_x + (x>>4))·128, texel (x&15) + 16·(y&7) inside.  A warped 8-pixel pattern plus its bilinear
 // taps covers ≈6×6 texels, which touches ≈2.1 tiles against ≈6.3 lines in row-major order (DESIGN.md

@@ -105,7 +105,8 @@ template <class T>
 __device__ __forceinline__ T rec_val(float v) { return (T)v; }
 template <>
 __device__ __forceinline__ _Float16 rec_val<_Float16>(float v) {
-  return (_Float16)__builtin_amdgcn_fmed3f(v, -65504.0f, 65504.0f);
+  // (fmed3 would map NaN to −65504: a NaN stays NaN)
+  return (_Float16)(isnan(v) ? v : __builtin_amdgcn_fmed3f(v, -65504.0f, 65504.0f));
 }
 
 // Store a workgroup's contiguous record slab (LDS → global): 16-B non-temporal stores when the slab is 16-B
@@ -258,14 +259,12 @@ __global__ __launch_bounds__((kMultiThreads<PPL, T>)) void photometric_block_ker
   T* s_rec = stage + lb * rec_f;
   int okl = 1;
   float s = 0.0f, rr[PPL];
-#pragma unroll
-  for (int j = 0; j < PPL; ++j) {
+  auto pixel = [&](int j, float ih) {
     const int px = k + LPB * j;
     const bool act = live && px < P;
-    const Row row = photometric_row<PM, JAC>(a, s_tb[lb], s_pat[px < P ? px : 0], Ih[j]);  // masked by act
+    const Row row = photometric_row<PM, JAC>(a, s_tb[lb], s_pat[px < P ? px : 0], ih);  // masked by act
     okl &= act ? row.ok : 1;
     s += act ? row.r * row.r : 0.0f;
-    rr[j] = row.r;
     if (JAC && act) {  // record row px: r | J_host row | J_target row | J_rho
       T* h = s_rec + P + 6 * px;
       T* t = s_rec + 7 * P + 6 * px;
@@ -276,6 +275,24 @@ __global__ __launch_bounds__((kMultiThreads<PPL, T>)) void photometric_block_ker
       t[3] = rec_val<T>(row.tw.x); t[4] = rec_val<T>(row.tw.y); t[5] = rec_val<T>(row.tw.z);
       s_rec[13 * P + px] = rec_val<T>(row.jr);
     }
+    return row.r;
+  };
+  if constexpr (JAC) {
+    // one pixel at a time (no unrolling: an unrolled loop interleaves the PPL rows' evaluations and needed 122 VGPRs,
+    // 4 waves per SIMD); the pixel's I_h,k selected from the registers by a compare chain
+#pragma unroll 1
+    for (int j = 0; j < PPL; ++j) {
+      float ih = Ih[0];
+#pragma unroll
+      for (int q = 1; q < PPL; ++q) ih = j == q ? Ih[q] : ih;
+      // the tile block (pair record, cameras, point: ~70 registers) is read from LDS again by every pixel instead of
+      // being hoisted out of the loop and kept live across it
+      asm volatile("" ::: "memory");
+      pixel(j, ih);
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < PPL; ++j) rr[j] = pixel(j, Ih[j]);
   }
   // per-block validity (ballot over the wave: the block's LPB lanes are an aligned bit field) and ‖r‖²
   const int ok = group_all<LPB>(okl);
@@ -317,18 +334,22 @@ __global__ __launch_bounds__((kMultiThreads<PPL, T>)) void photometric_block_ker
 }
 
 // ------------------------------------------------------------------------------------------------
-// Geometric block kernel (reprojection.h:105-108): lane = block, record 28 floats = 7 float4 stores
+// Geometric block kernel (reprojection.h:105-108): lane = block, record 28 floats = 7 float4 stores, or with the
+// target-intrinsics Jacobian (INTR, pba_set_optimize_intrinsics) 44 floats = 11 float4 stores
 // ------------------------------------------------------------------------------------------------
-template <int MODEL, bool JAC>
+template <int MODEL, bool JAC, bool INTR>
 __global__ __launch_bounds__(kBlockThreads) void geometric_block_kernel(const KernelArgs a) {
+  constexpr int NR = INTR ? 44 : 28;
   const int blk_ = logical_tile() * kBlockThreads + threadIdx.x;
   const bool live = blk_ < a.n_blocks;
   if (!live && !a.wg_red) return;  // (with wg_red every thread reaches the workgroup reduction)
   const int blk = live ? blk_ : a.n_blocks - 1;
   const int pt = a.block_point[blk];
   const PairRec& pp = a.pairs[a.block_pair[blk]];
+  // the host camera unprojects with the constant intrinsics (the functor's captured ref_intrinsics, reprojection.h:
+  // 93-98), the target camera projects with the intrinsics parameter block (sIntr_c2)
   const double* khd = a.intr_d + kCamD * pp.host_cam;
-  const double* ktd = a.intr_d + kCamD * pp.target_cam;
+  const double* ktd = a.intr_t_d + kCamD * pp.target_cam;
   const double2 ur = a.u_ref[pt];
   const double2 uo = a.u_obs[blk];
   const double rho = a.rho[pt];
@@ -341,8 +362,8 @@ __global__ __launch_bounds__(kBlockThreads) void geometric_block_kernel(const Ke
   double u, v;
   const double iden = project<MODEL>(ktd, p, u, v);
   const float r0 = (float)(uo.x - u), r1 = (float)(uo.y - v);
-  f32x4* rec = reinterpret_cast<f32x4*>(a.out + (long long)blk * 28);
-  float J[28];
+  f32x4* rec = reinterpret_cast<f32x4*>(a.out + (long long)blk * NR);
+  float J[NR];
   J[0] = r0;
   J[1] = r1;
   bool ok = isfinite(r0) && isfinite(r1);
@@ -351,7 +372,16 @@ __global__ __launch_bounds__(kBlockThreads) void geometric_block_kernel(const Ke
     const Vec3 tf = {(float)pp.t[0], (float)pp.t[1], (float)pp.t[2]};
     const float irf = (float)irho;
     Vec3 du, dv;
-    project_jac<MODEL>(a.intr + 8 * pp.target_cam, pf, (float)iden, du, dv);
+    project_jac<MODEL>(a.intr_t + 8 * pp.target_cam, pf, (float)iden, du, dv);
+    if (INTR) {  // ∂r/∂k = −∂π/∂k (2×8, row-major) after J_rho
+      double ku[8], kv[8];
+      project_intr_jac<MODEL>(ktd, p, iden, ku, kv);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        J[28 + j] = (float)-ku[j];
+        J[36 + j] = (float)-kv[j];
+      }
+    }
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const Vec3 d = i == 0 ? du : dv;
@@ -366,7 +396,7 @@ __global__ __launch_bounds__(kBlockThreads) void geometric_block_kernel(const Ke
       J[26 + i] = dot(g, tf) * irf;  // = ∂π/∂p·R b/ρ² without the cancellation (∂π/∂p·p = 0), pba_internal.h
     }
 #pragma unroll
-    for (int i = 2; i < 28; ++i) ok = ok && isfinite(J[i]);
+    for (int i = 2; i < NR; ++i) ok = ok && isfinite(J[i]);
   }
   const float bc = ok ? huber_cost(r0 * r0 + r1 * r1, a.huber) : 0.0f;
   if (a.wg_red) {
@@ -377,11 +407,11 @@ __global__ __launch_bounds__(kBlockThreads) void geometric_block_kernel(const Ke
   a.cost[blk] = bc;
   if (!ok) {
 #pragma unroll
-    for (int i = 0; i < 28; ++i) J[i] = 0.0f;
+    for (int i = 0; i < NR; ++i) J[i] = 0.0f;
   }
   if (JAC) {
 #pragma unroll
-    for (int i = 0; i < 7; ++i)
+    for (int i = 0; i < NR / 4; ++i)
       __builtin_nontemporal_store(f32x4{J[4 * i], J[4 * i + 1], J[4 * i + 2], J[4 * i + 3]}, rec + i);
   } else {
     reinterpret_cast<float2*>(rec)[0] = make_float2(J[0], J[1]);
@@ -392,8 +422,10 @@ template <int MODEL>
 void launch_geometric(pba_engine* e, const KernelArgs& ka, int mode) {
   const int grid = (e->n_blocks + kBlockThreads - 1) / kBlockThreads;
   e->last_grid = grid;
-  if (mode == 1) geometric_block_kernel<MODEL, true><<<grid, kBlockThreads, 0, e->stream>>>(ka);
-  else geometric_block_kernel<MODEL, false><<<grid, kBlockThreads, 0, e->stream>>>(ka);
+  if (mode == 1 && e->opt_intr) geometric_block_kernel<MODEL, true, true><<<grid, kBlockThreads, 0, e->stream>>>(ka);
+  else if (mode == 1) geometric_block_kernel<MODEL, true, false><<<grid, kBlockThreads, 0, e->stream>>>(ka);
+  else if (e->opt_intr) geometric_block_kernel<MODEL, false, true><<<grid, kBlockThreads, 0, e->stream>>>(ka);
+  else geometric_block_kernel<MODEL, false, false><<<grid, kBlockThreads, 0, e->stream>>>(ka);
 }
 
 // PM = camera model + 4 · interpolator (pba_device.h)
@@ -472,6 +504,8 @@ KernelArgs make_kernel_args(pba_engine* e, const PairRec* pairs, const double* r
   ka.vmax = e->height + 1.0;
   ka.intr = e->intr.p;
   ka.intr_d = e->intr_d.p;
+  ka.intr_t = e->opt_intr ? e->intr_state.p : e->intr.p;
+  ka.intr_t_d = e->opt_intr ? e->intr_state_d.p : e->intr_d.p;
   ka.block_point = e->block_point.p;
   ka.block_pair = e->block_pair.p;
   ka.block_pp = e->block_pp.p;
@@ -562,6 +596,7 @@ int pba_destroy(pba_engine* e) {
   e->pair_target.release(); e->block_rec.release(); e->pairs.release(); e->poses.release(); e->rho.release(); e->out.release();
   e->cost.release(); e->valid.release();
   for (hipEvent_t ev : e->ev_pool) (void)hipEventDestroy(ev);
+  for (hipEvent_t ev : e->chunk_ev) (void)hipEventDestroy(ev);
   if (e->own_stream) (void)hipStreamDestroy(e->own_stream);
   delete e;
   return PBA_OK;
@@ -579,30 +614,64 @@ int pba_get_stream(pba_engine* e, void** s) {
   return PBA_OK;
 }
 
-int pba_set_cameras(pba_engine* e, int32_t n_cams, const double* intrinsics) {
-  if (!e || n_cams <= 0 || n_cams > 32767 || !intrinsics) return fail(PBA_ERR_INVALID_ARGUMENT, "bad camera arguments");
-  if (int rc = check_device(e)) return rc;
-  reset_pyramid(e);
-  std::vector<float> f(8 * (size_t)n_cams);
-  for (size_t i = 0; i < f.size(); ++i) f[i] = (float)intrinsics[i];
+// Camera tables from 8·n intrinsics: fp32 [fx fy cx cy p1..p4] (Jacobian chain) and the fp64 records (kCamD doubles
+// each, pba_device.h) [fx fy cx cy p1..p4 | cx cy 1/fx 1/fy p1..p4], uploaded to f / d on the engine stream.
+static int upload_cameras(pba_engine* e, int n_cams, const double* intrinsics, DevBuf<float>& f, DevBuf<double>& d) {
+  std::vector<float> hf(8 * (size_t)n_cams);
+  for (size_t i = 0; i < hf.size(); ++i) hf[i] = (float)intrinsics[i];
   for (int c = 0; c < n_cams; ++c)
-    if (!(f[8 * c] != 0.0f && f[8 * c + 1] != 0.0f)) return fail(PBA_ERR_INVALID_ARGUMENT, "zero focal length");
-  // fp64 camera records (kCamD doubles each, pba_device.h): [fx fy cx cy p1..p4 | cx cy 1/fx 1/fy p1..p4]
-  std::vector<double> d((size_t)kCamD * n_cams, 0.0);
+    if (!(hf[8 * c] != 0.0f && hf[8 * c + 1] != 0.0f)) return fail(PBA_ERR_INVALID_ARGUMENT, "zero focal length");
+  std::vector<double> hd((size_t)kCamD * n_cams, 0.0);
   for (int c = 0; c < n_cams; ++c) {
     const double* k = intrinsics + 8 * c;
-    double* r = d.data() + (size_t)kCamD * c;
+    double* r = hd.data() + (size_t)kCamD * c;
     for (int j = 0; j < 8; ++j) r[j] = k[j];
     r[8] = k[2]; r[9] = k[3]; r[10] = 1.0 / k[0]; r[11] = 1.0 / k[1];
     for (int j = 4; j < 8; ++j) r[8 + j] = k[j];
   }
-  PBA_HIP(e->intr.resize(f.size()));
-  PBA_HIP(e->intr_d.resize(d.size()));
-  PBA_HIP(hipMemcpyAsync(e->intr.p, f.data(), f.size() * sizeof(float), hipMemcpyHostToDevice, e->stream));
-  PBA_HIP(hipMemcpyAsync(e->intr_d.p, d.data(), d.size() * sizeof(double), hipMemcpyHostToDevice, e->stream));
+  PBA_HIP(f.resize(hf.size()));
+  PBA_HIP(d.resize(hd.size()));
+  PBA_HIP(hipMemcpyAsync(f.p, hf.data(), hf.size() * sizeof(float), hipMemcpyHostToDevice, e->stream));
+  PBA_HIP(hipMemcpyAsync(d.p, hd.data(), hd.size() * sizeof(double), hipMemcpyHostToDevice, e->stream));
   PBA_HIP(hipStreamSynchronize(e->stream));
-  e->n_cams = n_cams;
   return PBA_OK;
+}
+
+int pba_set_cameras(pba_engine* e, int32_t n_cams, const double* intrinsics) {
+  if (!e || n_cams <= 0 || n_cams > 32767 || !intrinsics) return fail(PBA_ERR_INVALID_ARGUMENT, "bad camera arguments");
+  if (int rc = check_device(e)) return rc;
+  reset_pyramid(e);
+  if (int rc = upload_cameras(e, n_cams, intrinsics, e->intr, e->intr_d)) return rc;
+  e->n_cams = n_cams;
+  if (e->opt_intr) return upload_cameras(e, n_cams, intrinsics, e->intr_state, e->intr_state_d);
+  return PBA_OK;
+}
+
+int pba_set_optimize_intrinsics(pba_engine* e, int32_t enable) {
+  if (!e) return fail(PBA_ERR_INVALID_ARGUMENT, "null engine");
+  if (enable && e->opt.residual_kind != PBA_RESIDUAL_GEOMETRIC)
+    return fail(PBA_ERR_INVALID_ARGUMENT, "intrinsics optimisation is geometric only");
+  if (enable && e->n_cams <= 0) return fail(PBA_ERR_NOT_READY, "pba_set_cameras first");
+  if (int rc = check_device(e)) return rc;
+  const bool on = enable != 0;
+  if (on && !e->opt_intr) {  // the state starts at the cameras' intrinsics
+    std::vector<double> k((size_t)kCamD * e->n_cams), k8(8 * (size_t)e->n_cams);
+    PBA_HIP(hipMemcpy(k.data(), e->intr_d.p, sizeof(double) * k.size(), hipMemcpyDeviceToHost));
+    for (int c = 0; c < e->n_cams; ++c)
+      for (int j = 0; j < 8; ++j) k8[8 * c + j] = k[(size_t)kCamD * c + j];
+    if (int rc = upload_cameras(e, e->n_cams, k8.data(), e->intr_state, e->intr_state_d)) return rc;
+  }
+  e->opt_intr = on;
+  e->evaluated = false;
+  if (e->n_blocks > 0) PBA_HIP(e->out.resize((size_t)e->n_blocks * e->rec_floats()));
+  return PBA_OK;
+}
+
+int pba_set_intrinsics_state(pba_engine* e, const double* intrinsics) {
+  if (!e || !intrinsics) return fail(PBA_ERR_INVALID_ARGUMENT, "null argument");
+  if (!e->opt_intr) return fail(PBA_ERR_NOT_READY, "pba_set_optimize_intrinsics first");
+  if (int rc = check_device(e)) return rc;
+  return upload_cameras(e, e->n_cams, intrinsics, e->intr_state, e->intr_state_d);
 }
 
 // Per-block {point, host, target, host_cam << 16 | target_cam} for the fused-state prologue (pba_internal.h
@@ -718,6 +787,7 @@ int pba_set_points(pba_engine* e, int32_t n_points, const int32_t* host_frame, c
     } else if (int rc = sample_host_intensities(e, e->u_ref.p, e->host_int.p)) {  // I_h,k from the host image
       return rc;
     }
+    e->host_int_sampled = host_intensity == nullptr;
   }
   PBA_HIP(hipStreamSynchronize(e->stream));
   e->point_host_h.assign(host_frame, host_frame + n_points);
@@ -731,7 +801,7 @@ int pba_set_blocks(pba_engine* e, int32_t n_blocks, const int32_t* block_point, 
   if (e->n_points <= 0) return fail(PBA_ERR_NOT_READY, "pba_set_points first");
   const bool geometric = e->opt.residual_kind == PBA_RESIDUAL_GEOMETRIC;
   if (geometric && !u_obs) return fail(PBA_ERR_INVALID_ARGUMENT, "geometric blocks need u_obs");
-  const long long rec = 14LL * e->R();
+  const long long rec = e->rec_floats();
   if ((long long)n_blocks * rec >= (1LL << 40)) return fail(PBA_ERR_INVALID_ARGUMENT, "problem too large");
   // distinct (host, target) pairs, in first-seen order
   std::vector<int> pair_of(n_blocks), ph, pt;
@@ -922,7 +992,7 @@ int pba_synchronize(pba_engine* e) {
   return PBA_OK;
 }
 
-int pba_record_floats(const pba_engine* e) { return e ? 14 * e->R() : 0; }
+int pba_record_floats(const pba_engine* e) { return e ? e->rec_floats() : 0; }
 
 int pba_set_record_format(pba_engine* e, int32_t format) {
   if (!e) return fail(PBA_ERR_INVALID_ARGUMENT, "null engine");
@@ -944,7 +1014,7 @@ int pba_get_records(pba_engine* e, float* records, uint8_t* valid) {
   if (!e) return fail(PBA_ERR_INVALID_ARGUMENT, "null engine");
   if (!e->evaluated) return fail(PBA_ERR_NOT_READY, "pba_evaluate first");
   if (int rc = check_device(e)) return rc;
-  const size_t n = (size_t)e->n_blocks * 14 * e->R();
+  const size_t n = (size_t)e->n_blocks * e->rec_floats();
   std::vector<_Float16> half;
   if (records && e->record_format == PBA_RECORD_F16) {
     half.resize(n);
@@ -958,20 +1028,60 @@ int pba_get_records(pba_engine* e, float* records, uint8_t* valid) {
   return PBA_OK;
 }
 
+// Chunked asynchronous read-back for the Ceres adapter: the copies go out on the engine stream behind the evaluation,
+// an event after each chunk; a caller waiting for one block only waits for its chunk, so Ceres' per-block work
+// (CostFunction::Evaluate, the Jacobian writer) overlaps the PCIe transfer of the later chunks.
+int pba_get_records_async(pba_engine* e, float* records, uint8_t* valid, int32_t chunk_blocks) {
+  if (!e || !records || !valid || chunk_blocks <= 0) return fail(PBA_ERR_INVALID_ARGUMENT, "bad async read-back arguments");
+  if (!e->evaluated) return fail(PBA_ERR_NOT_READY, "pba_evaluate first");
+  if (e->record_format != PBA_RECORD_F32) return fail(PBA_ERR_INVALID_ARGUMENT, "asynchronous read-back: fp32 records only");
+  if (int rc = check_device(e)) return rc;
+  const long long nb = e->n_blocks, rf = e->rec_floats();
+  const int nc = (int)((nb + chunk_blocks - 1) / chunk_blocks);
+  while ((int)e->chunk_ev.size() < nc) {
+    hipEvent_t ev;
+    PBA_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    e->chunk_ev.push_back(ev);
+  }
+  e->chunk_blocks = chunk_blocks;
+  e->n_chunks_async = nc;
+  e->chunks_arrived.store(0);
+  for (int c = 0; c < nc; ++c) {
+    const long long b0 = (long long)c * chunk_blocks, n = std::min<long long>(chunk_blocks, nb - b0);
+    PBA_HIP(hipMemcpyAsync(records + b0 * rf, e->out.p + b0 * rf, sizeof(float) * (size_t)(n * rf), hipMemcpyDeviceToHost,
+                           e->stream));
+    PBA_HIP(hipMemcpyAsync(valid + b0, e->valid.p + b0, (size_t)n, hipMemcpyDeviceToHost, e->stream));
+    PBA_HIP(hipEventRecord(e->chunk_ev[c], e->stream));
+  }
+  return PBA_OK;
+}
+
+int pba_wait_records(pba_engine* e, int32_t block) {
+  if (!e || block < 0 || block >= e->n_blocks || e->chunk_blocks <= 0)
+    return fail(PBA_ERR_INVALID_ARGUMENT, "bad wait arguments");
+  const int c = block / e->chunk_blocks;
+  if (c < e->chunks_arrived.load(std::memory_order_acquire)) return PBA_OK;
+  PBA_HIP(hipEventSynchronize(e->chunk_ev[c]));  // chunks arrive in stream order: every chunk ≤ c is in
+  int seen = e->chunks_arrived.load(std::memory_order_relaxed);
+  while (seen < c + 1 && !e->chunks_arrived.compare_exchange_weak(seen, c + 1, std::memory_order_release)) {
+  }
+  return PBA_OK;
+}
+
 int pba_get_residuals(pba_engine* e, float* residuals, uint8_t* valid) {
   if (!e) return fail(PBA_ERR_INVALID_ARGUMENT, "null engine");
   if (!e->evaluated) return fail(PBA_ERR_NOT_READY, "pba_evaluate first");
   if (int rc = check_device(e)) return rc;
-  const size_t R = (size_t)e->R(), nb = (size_t)e->n_blocks;
+  const size_t R = (size_t)e->R(), nb = (size_t)e->n_blocks, RF = (size_t)e->rec_floats();
   std::vector<_Float16> half;
   if (residuals && nb) {
     // the first R values of every 14R-value record: one pitched device-to-host copy
     if (e->record_format == PBA_RECORD_F16) {
       half.resize(nb * R);
-      PBA_HIP(hipMemcpy2DAsync(half.data(), R * sizeof(_Float16), e->out.p, 14 * R * sizeof(_Float16),
+      PBA_HIP(hipMemcpy2DAsync(half.data(), R * sizeof(_Float16), e->out.p, RF * sizeof(_Float16),
                                R * sizeof(_Float16), nb, hipMemcpyDeviceToHost, e->stream));
     } else {
-      PBA_HIP(hipMemcpy2DAsync(residuals, R * sizeof(float), e->out.p, 14 * R * sizeof(float), R * sizeof(float), nb,
+      PBA_HIP(hipMemcpy2DAsync(residuals, R * sizeof(float), e->out.p, RF * sizeof(float), R * sizeof(float), nb,
                                hipMemcpyDeviceToHost, e->stream));
     }
   }

@@ -28,6 +28,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <cfloat>
 #include <chrono>
 #include <cmath>
 #include <cstdlib>
@@ -87,12 +88,17 @@ static_assert(pa(21) == 0 && pb(21) == 6 && pa(56) == 5 && pb(56) == 11, "table"
 
 // LM decision record kept on the device by the single-GPU loop (lm_decide_kernel).
 // The trial's outcome, then the trust-region state the next trial runs with (λ = 1/radius, read by the kernels), the
-// done flag (1 converged, 2 radius underflow: every later kernel of the solve returns at once) and the index of the
-// linearisation buffer set holding the current state's normal-equation pieces (flipped on acceptance).
+// done flag (every later kernel of the solve returns at once: 1 function tolerance, 2 consecutive invalid steps,
+// 3 parameter tolerance, 4 gradient tolerance, 5 minimum trust region radius; lm_decide), the index of the
+// linearisation buffer set holding the current state's normal-equation pieces (flipped on acceptance), and Ceres'
+// bookkeeping: the current state's valid blocks, x_norm (−1 until the first accepted step), consecutive invalid steps,
+// and the trial's step and gradient norms.
 enum : int {
   kLmCost = 0, kLmCostNew = 1, kLmModel = 2, kLmRel = 3, kLmAccept = 4, kLmStatus = 5, kLmConverged = 6,
-  kLmLambda = 7, kLmRadius = 8, kLmFactor = 9, kLmDone = 10, kLmSet = 11, kLmFields = 12
+  kLmLambda = 7, kLmRadius = 8, kLmFactor = 9, kLmDone = 10, kLmSet = 11, kLmValid = 12, kLmXNorm = 13,
+  kLmInvalid = 14, kLmStepNorm = 15, kLmGradNorm = 16, kLmFields = 17
 };
+enum : int { kDoneFunction = 1, kDoneInvalid = 2, kDoneParameter = 3, kDoneGradient = 4, kDoneRadius = 5 };
 // The kernels always get a record: the device loop's, or — host-driven steps — GnData::lm_idle (not done, set 0, λ NaN
 // = use the kernel's λ argument).  They read it with their first loads, never behind a branch of its own (a gate
 // read before anything else cost the linearisation ~8 µs of serialised scalar round trips).
@@ -606,7 +612,8 @@ __host__ __device__ constexpr long long ex_row(int K) { return (long long)(K + 1
 
 // One lane per element of the local skyline (same contribution lists as assemble_kernel, nothing damped or
 // fixed) and per pose-gradient element.  Positions outside the local profile stay zero (memset).
-__global__ void export_kernel(const AsmArgs a, const uint8_t* __restrict__ observed, double* __restrict__ X, int K) {
+__global__ void export_kernel(AsmArgs a, const uint8_t* __restrict__ observed, double* __restrict__ X, int K) {
+  if (lm_view(a.lm).set != 0.0) a.part_lin = a.part_lin1;  // (no done gate: see schur_kernel)
   const int tid = blockIdx.x * blockDim.x + threadIdx.x;
   const int nS = a.n_sky * 36;
   const long long RS = ex_row(K);
@@ -644,7 +651,8 @@ struct ImportArgs {
 
 // One lane per element of the band solver input: + λ·clamp(diag(A)) (levenberg_marquardt_strategy.cc),
 // identity rows/columns for constant frames — the same arithmetic as assemble_kernel on the summed system.
-__global__ void import_kernel(const ImportArgs a, double lambda) {
+__global__ void import_kernel(const ImportArgs a, double lambda, const double* __restrict__ lm) {
+  lambda = lm_lambda(lm_view(lm), lambda);  // the device LM record's λ (host-driven steps: the argument)
   const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   const int K = a.K;
   const long long SR = (long long)(K + 1) * 36 + 6, RS = ex_row(K);
@@ -1669,6 +1677,41 @@ __device__ void se3_exp_mul(const double* T, const double* d, double* out) {
 }
 
 
+// Σ over the workgroup of N per-lane values and the max of one more, in a fixed order (xor butterflies in each wave,
+// then the waves in order, as wg_reduce2): thread 0 writes out[0..N) and *out_max.  Every thread must call it.
+template <int N>
+__device__ __forceinline__ void wg_reduce_sum_max(double (&v)[N], double m, double* out, double* out_max) {
+  __shared__ double s[N + 1][16];
+  for (int o = 32; o >= 1; o >>= 1) {
+#pragma unroll
+    for (int q = 0; q < N; ++q) v[q] += __shfl_xor(v[q], o, 64);
+    m = fmax(m, __shfl_xor(m, o, 64));
+  }
+  const int w = threadIdx.x / 64, l = threadIdx.x % 64;
+  if (l == 0) {
+#pragma unroll
+    for (int q = 0; q < N; ++q) s[q][w] = v[q];
+    s[N][w] = m;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int nw = (int)(blockDim.x / 64);
+#pragma unroll
+    for (int q = 0; q < N; ++q) {
+      double x = 0.0;
+      for (int i = 0; i < nw; ++i) x += s[q][i];
+      out[q] = x;
+    }
+    double x = 0.0;
+    for (int i = 0; i < nw; ++i) x = fmax(x, s[N][i]);
+    *out_max = x;
+  }
+}
+
+// The update workgroups' partials besides the model decrease (slot layout of red): Σ|x − x_new|² and Σ|x_new|² in the
+// ambient parameter space (red2, two doubles per slot: Ceres' step_norm and x_norm, trust_region_minimizer.cc:706-726,
+// :813-814) and max |x − (x ⊞ −g)| at the current state (gmax, one double per slot: gradient_max_norm,
+// trust_region_minimizer.cc:287-299).  Constant frames and points without blocks are not parameters of the solve.
 struct PoseUpdateArgs {
   const double* poses;
   const double* x;
@@ -1677,6 +1720,8 @@ struct PoseUpdateArgs {
   const uint8_t* fixed;
   double* poses_new;
   double* red;
+  double* red2;
+  double* gmax;
   int n;
 };
 
@@ -1691,17 +1736,36 @@ __device__ __forceinline__ void candidate_pose(const PoseUpdateArgs& a, int i, d
 
 __device__ __forceinline__ void pose_update_block(const PoseUpdateArgs& a, int blk) {
   const int i = blk * blockDim.x + threadIdx.x;
-  double dg = 0.0, dD = 0.0;
+  double v[4] = {0.0, 0.0, 0.0, 0.0};  // x·g, x·D·x, |T − T_new|², |T_new|²
+  double gm = 0.0;
   if (i < a.n) {
-    candidate_pose(a, i, a.poses_new + 7 * i);
+    double* tn = a.poses_new + 7 * i;
+    candidate_pose(a, i, tn);
     if (!a.fixed[i]) {
+      const double* T = a.poses + 7 * i;
+      double ng[6], tg[7];
       for (int r = 0; r < 6; ++r) {
-        dg += a.x[6 * i + r] * a.g_dir[6 * i + r];
-        dD += a.x[6 * i + r] * a.x[6 * i + r] * a.Ddiag[6 * i + r];
+        v[0] += a.x[6 * i + r] * a.g_dir[6 * i + r];
+        v[1] += a.x[6 * i + r] * a.x[6 * i + r] * a.Ddiag[6 * i + r];
+        ng[r] = -a.g_dir[6 * i + r];
+      }
+      se3_exp_mul(T, ng, tg);  // Plus(x, −gradient)
+      for (int q = 0; q < 7; ++q) {
+        const double d = tn[q] - T[q];
+        v[2] += d * d;
+        v[3] += tn[q] * tn[q];
+        gm = fmax(gm, fabs(T[q] - tg[q]));
       }
     }
   }
-  wg_reduce2(dg, dD, a.red + 2 * blk);
+  double s[4];
+  wg_reduce_sum_max<4>(v, gm, s, a.gmax + blk);
+  if (threadIdx.x == 0) {
+    a.red[2 * blk] = s[0];
+    a.red[2 * blk + 1] = s[1];
+    a.red2[2 * blk] = s[2];
+    a.red2[2 * blk + 1] = s[3];
+  }
 }
 
 struct PointUpdateArgs {
@@ -1719,13 +1783,16 @@ struct PointUpdateArgs {
   double* rho_new;
   double* drho;
   double* red;
+  double* red2;
+  double* gmax;
   int n_points;
 };
 
 // blk: the point workgroup's index among the point workgroups; slot: its reduction slot
 __device__ __forceinline__ void point_update_block(const PointUpdateArgs& a, double lambda, int blk, int slot) {
   const int p = blk * blockDim.x + threadIdx.x;
-  double dg = 0.0, dD = 0.0;
+  double v[4] = {0.0, 0.0, 0.0, 0.0};  // δρ·g, δρ·D·δρ, δρ², ρ_new²
+  double gm = 0.0;
   if (p < a.n_points) {
     const double* pd = a.pt_data + (long long)p * 8;
     const double H = pd[0], gl = pd[1];
@@ -1755,12 +1822,23 @@ __device__ __forceinline__ void point_update_block(const PointUpdateArgs& a, dou
     }
     const double dr = Hd > 0.0 ? -s / Hd : 0.0;
     const int o = a.pt_orig[p];
-    a.rho_new[o] = a.rho[o] + dr;
+    const double rn = a.rho[o] + dr;
+    a.rho_new[o] = rn;
     a.drho[o] = dr;
-    dg = dr * gl;
-    dD = dr * dr * D;
+    v[0] = dr * gl;
+    v[1] = dr * dr * D;
+    v[2] = dr * dr;
+    v[3] = rn * rn;
+    gm = fabs(gl);  // ρ has no local parameterisation: |ρ − (ρ − g_ρ)|
   }
-  wg_reduce2(dg, dD, a.red + 2 * slot);
+  double s[4];
+  wg_reduce_sum_max<4>(v, gm, s, a.gmax + slot);
+  if (threadIdx.x == 0) {
+    a.red[2 * slot] = s[0];
+    a.red[2 * slot + 1] = s[1];
+    a.red2[2 * slot] = s[2];
+    a.red2[2 * slot + 1] = s[3];
+  }
 }
 
 struct PairUpdateArgs {
@@ -1823,92 +1901,148 @@ __global__ __launch_bounds__(kBlockThreads) void cost_reduce_kernel(const float*
 // sequence number after a system-scope fence), so the host learns the decision by polling instead of through a copy
 // and a stream event (each of which left the GPU idle ~6 µs).
 constexpr int kDecideThreads = 1024;
-__global__ __launch_bounds__(kDecideThreads) void lm_decide_kernel(const double* __restrict__ red, int gp, int gq, int gc,
-                                                        const int* __restrict__ status, double min_rel,
-                                                        double ftol, double* __restrict__ lm,
-                                                        volatile double* __restrict__ host_rec, double seq) {
-  if (lm[kLmDone] != 0.0) return;  // a trial enqueued ahead of the one that ended the solve
+
+// Ceres' termination options of the LM loop (solver.h:278-322; pba_solver_options)
+struct DecideOpts {
+  double min_rel, ftol, ptol, gtol, max_radius, min_radius;
+  int max_invalid;
+};
+
+// The trial's sums: the pose part (identical on every rank of a distributed solve: same summed system, same step) and
+// the point part with the candidate's cost and valid blocks (summed over the ranks).
+enum : int {
+  kTsPoseG = 0, kTsPoseD, kTsPoseStep2, kTsPoseXNorm2, kTsPoseGMax,
+  kTsPtG, kTsPtD, kTsCost, kTsValid, kTsPtStep2, kTsPtXNorm2, kTsPtGMax, kTsCount
+};
+
+// The trial's decision (one lane): trust_region_minimizer.cc:85-133 + levenberg_marquardt_strategy.cc:146-160 over the
+// summed trial quantities t[kTs*] and the record lm.  In Ceres' order:
+//   gradient tolerance at the current state (FinalizeIteration… :336-355, GradientToleranceReached :668-684): checked
+//     here, before the step, because this trial is the first to see the current state's gradient; the trial is void
+//     (done 4, not an iteration);
+//   invalid step — solver failure or no predicted decrease (:400-439) — HandleInvalidStep (:453-484): the 5th
+//     consecutive one ends the solve with FAILURE (done 2, not an iteration), earlier ones shrink the radius;
+//   candidate cost: infinite (DBL_MAX, :771-778) when a block valid at the current state is invalid at the candidate;
+//   parameter tolerance (:706-726, step_norm ≤ ptol (x_norm + ptol) with x_norm = −1 until the first accepted step,
+//     :185 / :814) → done 3;  function tolerance (:729-748) → done 1 (neither step applied);
+//   IsStepSuccessful (:781-803) → accept (radius = min(max_radius, radius / max(1/3, 1 − (2ρ − 1)³)), :146-153) or
+//     reject (radius /= factor, factor *= 2, :155-160);  MinTrustRegionRadiusReached (:687-703) → done 5.
+__device__ void lm_decide(const double* t, int st, const DecideOpts& o, double* lm) {
   const double lambda = lm[kLmLambda];
-  constexpr int N = kDecideThreads, U = 8;
-  __shared__ double part[5][N / 64];
-  double v[5] = {0, 0, 0, 0, 0};  // dg, dD, qg, qD, c
-  // strided sums of each slot range, U independent 16-B loads in flight per thread (the candidate cost alone has one
-  // slot per linearisation chunk: 12.5k at C4), then xor butterflies per wave and the waves in order (deterministic)
-  auto range = [&](int beg, int end, double& x, double& y) {
-    for (int i0 = beg + (int)threadIdx.x; i0 < end; i0 += U * N) {
-      double2 r[U];
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int i = i0 + u * N;
-        r[u] = i < end ? reinterpret_cast<const double2*>(red)[i] : make_double2(0.0, 0.0);
-      }
-#pragma unroll
-      for (int u = 0; u < U; ++u) { x += r[u].x; y += r[u].y; }
-    }
-  };
-  double unused = 0.0;
-  range(0, gp, v[0], v[1]);
-  range(gp, gp + gq, v[2], v[3]);
-  range(gp + gq, gp + gq + gc, v[4], unused);
-#pragma unroll
-  for (int q = 0; q < 5; ++q)
-    for (int m = 32; m >= 1; m >>= 1) v[q] += __shfl_xor(v[q], m, 64);
-  if ((threadIdx.x & 63) == 0)
-#pragma unroll
-    for (int q = 0; q < 5; ++q) part[q][threadIdx.x >> 6] = v[q];
-  __syncthreads();
-  if (threadIdx.x == 0)
-    for (int q = 0; q < 5; ++q) {
-      double t = 0.0;
-      for (int w = 0; w < N / 64; ++w) t += part[q][w];
-      part[q][0] = t;
-    }
-  if (threadIdx.x >= 64) return;  // wave 0 publishes; lane 0 decides
-  __shared__ double s_rec[kLmFields];
-  if (threadIdx.x == 0) {
-  const double dg = part[0][0], dD = part[1][0], qg = part[2][0], qD = part[3][0], c = part[4][0];
-  const int st = *status;
-  const double model = __dadd_rn(__dmul_rn(0.5, __dsub_rn(__dmul_rn(lambda, dD), dg)),
-                                 __dmul_rn(0.5, __dsub_rn(__dmul_rn(lambda, qD), qg)));
+  const double model = __dadd_rn(__dmul_rn(0.5, __dsub_rn(__dmul_rn(lambda, t[kTsPoseD]), t[kTsPoseG])),
+                                 __dmul_rn(0.5, __dsub_rn(__dmul_rn(lambda, t[kTsPtD]), t[kTsPtG])));
   const double cost = lm[kLmCost];
+  const double gnorm = fmax(t[kTsPoseGMax], t[kTsPtGMax]);
+  double radius = lm[kLmRadius], factor = lm[kLmFactor], done = 0.0, invalid = lm[kLmInvalid];
+  bool accept = false, converged = false;
+  const bool valid_step = st == 0 && model > 0.0;
+  const double c = t[kTsValid] < lm[kLmValid] ? DBL_MAX : t[kTsCost];
+  const double step = sqrt(t[kTsPoseStep2] + t[kTsPtStep2]);
   const double rel = (cost - c) / model;
-  // a valid step whose cost change is within the function tolerance ends the solve WITHOUT being applied
-  // (trust_region_minimizer.cc:115-117, FunctionToleranceReached :729-750, checked before IsStepSuccessful)
-  const bool converged = st == 0 && model > 0.0 && fabs(cost - c) <= ftol * cost;
-  const bool accept = st == 0 && model > 0.0 && rel > min_rel && isfinite(c) && !converged;
+  if (gnorm <= o.gtol) {
+    done = 4.0;
+  } else if (!valid_step) {
+    invalid += 1.0;
+    if (invalid >= (double)o.max_invalid) {
+      done = 2.0;
+    } else {
+      radius /= factor;  // StepIsInvalid = StepRejected(0)
+      factor *= 2.0;
+      if (radius <= o.min_radius) done = 5.0;
+    }
+  } else {
+    invalid = 0.0;
+    if (step <= o.ptol * (lm[kLmXNorm] + o.ptol)) {
+      done = 3.0;
+      converged = true;
+    } else if (fabs(cost - c) <= o.ftol * cost) {
+      done = 1.0;
+      converged = true;
+    } else if (rel > o.min_rel) {
+      accept = true;
+      const double q = 2.0 * rel - 1.0;
+      radius = fmin(o.max_radius, radius / fmax(1.0 / 3.0, 1.0 - q * q * q));
+      factor = 2.0;
+    } else {
+      radius /= factor;
+      factor *= 2.0;
+      if (radius <= o.min_radius) done = 5.0;
+    }
+  }
   lm[kLmConverged] = converged ? 1.0 : 0.0;
   lm[kLmCostNew] = c;
   lm[kLmModel] = model;
   lm[kLmRel] = rel;
   lm[kLmAccept] = accept ? 1.0 : 0.0;
   lm[kLmStatus] = (double)st;
+  lm[kLmStepNorm] = step;
+  lm[kLmGradNorm] = gnorm;
   if (accept) {
     lm[kLmCost] = c;
+    lm[kLmValid] = t[kTsValid];
+    lm[kLmXNorm] = sqrt(t[kTsPoseXNorm2] + t[kTsPtXNorm2]);
     lm[kLmSet] = 1.0 - lm[kLmSet];  // the candidate's linearisation (the spare set) is now the current one
   }
-  // trust region for the next trial (levenberg_marquardt_strategy.cc:125-150, trust_region_minimizer.cc):
-  // failure: radius /= factor, factor *= 2; success: radius /= max(1/3, 1 − (2ρ − 1)³), factor = 2
-  double radius = lm[kLmRadius], factor = lm[kLmFactor], done = 0.0;
-  if (converged) {
-    done = 1.0;
-  } else if (!accept) {
-    radius /= factor;
-    factor *= 2.0;
-    if (radius < 1e-32) done = 2.0;
-  } else {
-    const double q = 2.0 * rel - 1.0;
-    radius = radius / fmax(1.0 / 3.0, 1.0 - q * q * q);
-    factor = 2.0;
-  }
+  lm[kLmInvalid] = invalid;
   lm[kLmRadius] = radius;
   lm[kLmFactor] = factor;
   lm[kLmLambda] = 1.0 / radius;
   lm[kLmDone] = done;
-  for (int i = 0; i < kLmFields; ++i) s_rec[i] = lm[i];
+}
+
+// The trial's sums from the update and cost partials (one workgroup: strided per-thread sums with U independent 16-B
+// loads in flight — the candidate cost alone has one slot per linearisation chunk, 12.5k at C4 — then xor butterflies
+// per wave and the waves in order: deterministic).  Slots: red [0, gp) poses, [gp, gp + gq) points (model decrease
+// parts), [gp + gq, gp + gq + gc) the candidate's (cost, valid); red2 / gmax [0, gp + gq) (update_kernel).  Thread 0
+// gets the totals in t.
+__device__ void trial_sums(const double* __restrict__ red, const double* __restrict__ red2,
+                           const double* __restrict__ gmax, int gp, int gq, int gc, double* t) {
+  constexpr int N = kDecideThreads, U = 8;
+  __shared__ double part[kTsCount][N / 64];
+  double v[kTsCount] = {};
+  auto range = [&](const double* src, int beg, int end, double& x, double& y) {
+    for (int i0 = beg + (int)threadIdx.x; i0 < end; i0 += U * N) {
+      double2 r[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int i = i0 + u * N;
+        r[u] = i < end ? reinterpret_cast<const double2*>(src)[i] : make_double2(0.0, 0.0);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) { x += r[u].x; y += r[u].y; }
+    }
+  };
+  range(red, 0, gp, v[kTsPoseG], v[kTsPoseD]);
+  range(red, gp, gp + gq, v[kTsPtG], v[kTsPtD]);
+  range(red, gp + gq, gp + gq + gc, v[kTsCost], v[kTsValid]);
+  range(red2, 0, gp, v[kTsPoseStep2], v[kTsPoseXNorm2]);
+  range(red2, gp, gp + gq, v[kTsPtStep2], v[kTsPtXNorm2]);
+  for (int i = threadIdx.x; i < gp + gq; i += N) {
+    const int q = i < gp ? kTsPoseGMax : kTsPtGMax;
+    v[q] = fmax(v[q], gmax[i]);
   }
-  if (!host_rec) return;
-  // publish: lane i stores field i (one system-scope store instruction, fine-grained host memory, completion awaited
-  // once), then lane 0 the sequence number the host polls for — no L2 write-back fence, no per-field wait
+  auto is_max = [](int q) { return q == kTsPoseGMax || q == kTsPtGMax; };
+#pragma unroll
+  for (int q = 0; q < kTsCount; ++q)
+    for (int m = 32; m >= 1; m >>= 1) {
+      const double o = __shfl_xor(v[q], m, 64);
+      v[q] = is_max(q) ? fmax(v[q], o) : v[q] + o;
+    }
+  if ((threadIdx.x & 63) == 0)
+#pragma unroll
+    for (int q = 0; q < kTsCount; ++q) part[q][threadIdx.x >> 6] = v[q];
+  __syncthreads();
+  if (threadIdx.x == 0)
+    for (int q = 0; q < kTsCount; ++q) {
+      double s = 0.0;
+      for (int w = 0; w < N / 64; ++w) s = is_max(q) ? fmax(s, part[q][w]) : s + part[q][w];
+      t[q] = s;
+    }
+}
+
+// Publish the record to page-locked, host-coherent memory (wave 0): lane i stores field i, every store completes, then
+// lane 0 stores the sequence number the host polls for with a system-scope release.
+__device__ void publish_record(const double* s_rec, volatile double* host_rec, double seq) {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -1916,7 +2050,77 @@ __global__ __launch_bounds__(kDecideThreads) void lm_decide_kernel(const double*
   if (l < kLmFields) host_rec[l] = s_rec[l];
   __builtin_amdgcn_s_waitcnt(0);  // vmcnt(0) & lgkmcnt(0): every lane's field store has completed
   __builtin_amdgcn_wave_barrier();
-  if (l == 0) host_rec[kLmFields] = seq;
+  if (l == 0) __hip_atomic_store(const_cast<double*>(host_rec + kLmFields), seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__global__ __launch_bounds__(kDecideThreads) void lm_decide_kernel(const double* __restrict__ red,
+                                                                   const double* __restrict__ red2,
+                                                                   const double* __restrict__ gmax, int gp, int gq,
+                                                                   int gc, const int* __restrict__ status,
+                                                                   const DecideOpts o, double* __restrict__ lm,
+                                                                   volatile double* __restrict__ host_rec, double seq) {
+  if (lm[kLmDone] != 0.0) return;  // a trial enqueued ahead of the one that ended the solve
+  __shared__ double t[kTsCount];
+  trial_sums(red, red2, gmax, gp, gq, gc, t);
+  if (threadIdx.x >= 64) return;  // wave 0 publishes; lane 0 decides
+  __shared__ double s_rec[kLmFields];
+  if (threadIdx.x == 0) {
+    lm_decide(t, *status, o, lm);
+    for (int i = 0; i < kLmFields; ++i) s_rec[i] = lm[i];
+  }
+  if (host_rec) publish_record(s_rec, host_rec, seq);
+}
+
+// Multi-GPU trial, before the scalar all-reduce: this rank's sums split into the pose part, which every rank computes
+// bit for bit the same (same summed system, same step) and keeps in tpose, and the point part, written to the exchange
+// buffer's kExScalars scalar slots Y for the Σ over ranks:
+//   Y = [δρ·g, δρ·D·δρ, candidate cost, candidate valid blocks, Σδρ², Σρ_new², points above the gradient tolerance, 0]
+// (the gradient test needs only whether some rank's point gradient exceeds the tolerance: a count sums exactly).
+constexpr int kExScalars = 8;
+__global__ __launch_bounds__(kDecideThreads) void dist_sums_kernel(const double* __restrict__ red,
+                                                                   const double* __restrict__ red2,
+                                                                   const double* __restrict__ gmax, int gp, int gq, int gc,
+                                                                   double gtol, const double* __restrict__ lm,
+                                                                   double* __restrict__ tpose, double* __restrict__ Y) {
+  if (lm[kLmDone] != 0.0) return;
+  __shared__ double t[kTsCount];
+  trial_sums(red, red2, gmax, gp, gq, gc, t);
+  if (threadIdx.x != 0) return;
+  for (int q = 0; q < 5; ++q) tpose[q] = t[kTsPoseG + q];
+  tpose[5] = t[kTsPtGMax];
+  Y[0] = t[kTsPtG];
+  Y[1] = t[kTsPtD];
+  Y[2] = t[kTsCost];
+  Y[3] = t[kTsValid];
+  Y[4] = t[kTsPtStep2];
+  Y[5] = t[kTsPtXNorm2];
+  Y[6] = t[kTsPtGMax] > gtol ? 1.0 : 0.0;
+  Y[7] = 0.0;
+}
+
+// Multi-GPU decision from the summed Y and the local pose part: the same lm_decide on every rank (identical inputs), so
+// every rank takes the same decision; the reported gradient norm is this rank's view (pose part and its own points).
+__global__ __launch_bounds__(64) void dist_decide_kernel(const double* __restrict__ Y, const double* __restrict__ tpose,
+                                                         const int* __restrict__ status, const DecideOpts o,
+                                                         double* __restrict__ lm, volatile double* __restrict__ host_rec,
+                                                         double seq) {
+  if (lm[kLmDone] != 0.0) return;
+  __shared__ double s_rec[kLmFields];
+  if (threadIdx.x == 0) {
+    double t[kTsCount];
+    for (int q = 0; q < 5; ++q) t[kTsPoseG + q] = tpose[q];
+    t[kTsPtG] = Y[0];
+    t[kTsPtD] = Y[1];
+    t[kTsCost] = Y[2];
+    t[kTsValid] = Y[3];
+    t[kTsPtStep2] = Y[4];
+    t[kTsPtXNorm2] = Y[5];
+    t[kTsPtGMax] = Y[6] > 0.0 ? INFINITY : tpose[5];
+    lm_decide(t, *status, o, lm);
+    lm[kLmGradNorm] = fmax(tpose[4], tpose[5]);
+    for (int i = 0; i < kLmFields; ++i) s_rec[i] = lm[i];
+  }
+  if (host_rec) publish_record(s_rec, host_rec, seq);
 }
 
 // The accepted candidate becomes the state (device-side accept, gated by the decision record; lm == nullptr: always).
@@ -2275,8 +2479,11 @@ int gn_prepare(pba_engine* e) {
   // update partials, then the candidate cost's workgroup partials (≤ one per 16 blocks: launch_cost_only's grids)
   G.red_slots = red_pose + red_pt + std::max({1024, nb / 16 + 2, G.n_chunks});
   PBA_HIP(G.red.resize((size_t)2 * G.red_slots));
+  PBA_HIP(G.red2.resize((size_t)2 * (red_pose + red_pt)));
+  PBA_HIP(G.gmax.resize((size_t)(red_pose + red_pt)));
   PBA_HIP(G.red_h.resize(2 * G.red_slots));
   PBA_HIP(G.lm.resize(kLmFields));
+  PBA_HIP(G.tpose.resize(8));
   {  // the record of host-driven steps: not done, buffer set 0, λ NaN (the kernels then use their λ argument)
     std::vector<double> idle(kLmFields, 0.0);
     idle[kLmLambda] = std::numeric_limits<double>::quiet_NaN();
@@ -2332,6 +2539,8 @@ int ensure_prepared(pba_engine* e) {
   if (!e->state_set) return fail(PBA_ERR_NOT_READY, "pba_set_state first");
   if (e->opt.residual_kind == PBA_RESIDUAL_PHOTOMETRIC && (!e->have_images || e->P <= 0))
     return fail(PBA_ERR_NOT_READY, "images/pattern missing");
+  if (e->opt_intr)  // the reduced camera system has no intrinsics blocks
+    return fail(PBA_ERR_INVALID_ARGUMENT, "intrinsics optimisation runs through the Ceres adapter (pba_ceres.h) only");
   if (int rc = check_device(e)) return rc;
   if (!e->gn.prepared)
     if (int rc = gn_prepare(e)) return rc;
@@ -2368,7 +2577,7 @@ int total_cost(pba_engine* e, double* cost, int* n_valid) {
 // lm = the device LM record (the pieces go to the spare buffer set, nothing runs once the solve is done), pairs / rho
 // the candidate's, and wg_red the slots of the per-chunk cost partials the decision sums.
 int linearize(pba_engine* e, double* cost, const double* lm = nullptr, const PairRec* pairs = nullptr,
-              const double* rho = nullptr, double* wg_red = nullptr) {
+              const double* rho = nullptr, double* wg_red = nullptr, int* n_valid = nullptr) {
   GnData& G = e->gn;
   if (!pairs) {
     launch_pairs(e, e->poses.p, e->pairs.p);
@@ -2380,7 +2589,7 @@ int linearize(pba_engine* e, double* cost, const double* lm = nullptr, const Pai
   else launch_linearize_geometric(e, ka, la);
   PBA_HIP(hipGetLastError());
   e->evaluated = false;  // records are not written in GN mode
-  if (cost) return total_cost(e, cost, nullptr);
+  if (cost) return total_cost(e, cost, n_valid);
   return PBA_OK;
 }
 
@@ -2484,11 +2693,11 @@ void enqueue_updates(pba_engine* e, double lambda, const uint8_t* fixed, int* gp
   const int gp = (nf + kBlockThreads - 1) / kBlockThreads;
   const int gq = (G.n_gn_points + kBlockThreads - 1) / kBlockThreads;
   const int gr = (e->n_pairs + kBlockThreads - 1) / kBlockThreads;
-  PoseUpdateArgs pa{e->poses.p, G.x.p, G.g_dir.p, G.Ddiag.p, fixed, G.poses_new.p, G.red.p, nf};
+  PoseUpdateArgs pa{e->poses.p, G.x.p, G.g_dir.p, G.Ddiag.p, fixed, G.poses_new.p, G.red.p, G.red2.p, G.gmax.p, nf};
   // point workgroup q writes reduction slot gp + q, as the separate launches did
   PointUpdateArgs qa{G.pt_data.p, G.pt_first.p, G.pt_nblk.p, G.pt_orig.p, G.pt_host.p, G.gn_target.p,
                      G.blk_schur.p, G.blk_schur1.p, G.x.p, fixed, e->rho.p, G.rho_new.p, G.drho.p, G.red.p,
-                     G.n_gn_points};
+                     G.red2.p, G.gmax.p, G.n_gn_points};
   PairUpdateArgs ra{e->pair_host.p, e->pair_target.p, e->frame_cam.p, e->intr_d.p, G.pairs_new.p, e->n_pairs};
   update_kernel<<<gp + gq + gr, kBlockThreads, 0, e->stream>>>(pa, qa, ra, gp, gq, lambda, lm ? lm : G.lm_idle.p);
   G.pairs_new_fresh = true;
@@ -2605,13 +2814,16 @@ void launch_accept(pba_engine* e, const double* lm) {
 // stream event (an event left the GPU idle ~6 µs each) — while the host polls, the GPU runs on into the gated accept
 // and linearisation.  The stream is queried now and then so a device error or a record that never comes ends the wait.
 double now_ms();
+constexpr double kDecisionTimeoutMs = 60000.0;  // one trial takes ~0.25 ms at C4
 
 int wait_decision(pba_engine* e, double seq, double* d) {
   volatile double* r = e->gn.lm_h.p;
   // the stream is queried only after 2 ms without the record (a trial takes ~0.23 ms at C4), then every 2 ms: a
   // hipStreamQuery every few hundred spins idled the GPU 5.7 µs before every trial's first kernel
   // (profiles/r2_gn_trial_trace_v7.txt → v9)
-  double next_query = now_ms() + 2.0;
+  // A device that stops making progress ends the wait after kDecisionTimeoutMs with PBA_ERR_DEVICE.
+  const double t0 = now_ms();
+  double next_query = t0 + 2.0;
   for (unsigned spins = 1;; ++spins) {
     if (r[kLmFields] == seq) break;
     if ((spins & 255u) == 0u && now_ms() >= next_query) {
@@ -2619,6 +2831,8 @@ int wait_decision(pba_engine* e, double seq, double* d) {
       const hipError_t q = hipStreamQuery(e->stream);
       if (q == hipSuccess && r[kLmFields] != seq) return fail(PBA_ERR_DEVICE, "LM decision record was not published");
       if (q != hipSuccess && q != hipErrorNotReady) return fail(PBA_ERR_DEVICE, std::string("HIP: ") + hipGetErrorString(q));
+      if (next_query - t0 > kDecisionTimeoutMs)
+        return fail(PBA_ERR_DEVICE, "LM decision record not published within " + std::to_string(kDecisionTimeoutMs / 1000) + " s");
     }
   }
   std::atomic_thread_fence(std::memory_order_acquire);
@@ -2636,7 +2850,7 @@ int wait_decision(pba_engine* e, double seq, double* d) {
 // one's decision: no host round trip between trials.  The candidate is evaluated even when the solve failed (its
 // numbers are then discarded): a garbage state is memory-safe in every evaluation kernel.  ev (phase timing only,
 // else nullptr): begin | candidate state | candidate linearisation | decision.
-int lm_trial(pba_engine* e, double min_rel, double ftol, double seq, const hipEvent_t* ev) {
+int lm_trial(pba_engine* e, const DecideOpts& dopt, double seq, const hipEvent_t* ev) {
   GnData& G = e->gn;
   if (ev) PBA_HIP(hipEventRecord(ev[0], e->stream));
   if (int rc = enqueue_solve(e, 0.0, G.lm.p)) return rc;
@@ -2645,8 +2859,8 @@ int lm_trial(pba_engine* e, double min_rel, double ftol, double seq, const hipEv
   if (ev) PBA_HIP(hipEventRecord(ev[1], e->stream));
   if (int rc = linearize(e, nullptr, G.lm.p, G.pairs_new.p, G.rho_new.p, G.red.p + 2 * (gp + gq))) return rc;
   if (ev) PBA_HIP(hipEventRecord(ev[2], e->stream));
-  lm_decide_kernel<<<1, kDecideThreads, 0, e->stream>>>(G.red.p, gp, gq, G.n_chunks, G.status.p, min_rel, ftol, G.lm.p,
-                                                        G.lm_host_d, seq);
+  lm_decide_kernel<<<1, kDecideThreads, 0, e->stream>>>(G.red.p, G.red2.p, G.gmax.p, gp, gq, G.n_chunks, G.status.p,
+                                                        dopt, G.lm.p, G.lm_host_d, seq);
   PBA_HIP(hipGetLastError());
   if (ev) PBA_HIP(hipEventRecord(ev[3], e->stream));
   return PBA_OK;  // an accepted candidate becomes the state in the next trial's schur_kernel (or after the loop)
@@ -2679,7 +2893,7 @@ int exchange_K(pba_engine* e, int band, int* K) {
   return PBA_OK;
 }
 
-long long exchange_count(pba_engine* e, int K) { return (long long)e->n_frames * ex_row(K) + 8; }
+long long exchange_count(pba_engine* e, int K) { return (long long)e->n_frames * ex_row(K) + kExScalars; }
 
 int step_export(pba_engine* e, double lambda, int band, double* X) {
   GnData& G = e->gn;
@@ -2714,7 +2928,7 @@ int step_import(pba_engine* e, double lambda, int band, const double* X, double*
   const int nf = e->n_frames;
   ImportArgs ia{X, G.fixed_req.p, G.Sband.p, G.g.p, G.g_dir.p, G.Ddiag.p, G.fixed_dist.p, nf, K};
   const long long n = (long long)nf * ((K + 1) * 36 + 6);
-  import_kernel<<<(unsigned)((n + 255) / 256), 256, 0, e->stream>>>(ia, lambda);
+  import_kernel<<<(unsigned)((n + 255) / 256), 256, 0, e->stream>>>(ia, lambda, G.lm_idle.p);
   PBA_HIP(hipGetLastError());
   G.sband_dirty = true;
   G.cr0_dirty = true;  // cr_build writes level 0 over the whole band
@@ -2722,16 +2936,6 @@ int step_import(pba_engine* e, double lambda, int band, const double* X, double*
   return finish_step(e, lambda, G.fixed_dist.p, model_pose, model_points, solver_status);
 }
 
-// Collective helper: Σ over ranks of n ≤ 8 host scalars through the scalar slots of the exchange buffer.
-int allreduce_scalars(pba_engine* e, double* X, int K, pba_allreduce_fn fn, void* user, double* v, int n) {
-  double* slot = X + (long long)e->n_frames * ex_row(K);
-  PBA_HIP(hipMemcpyAsync(slot, v, sizeof(double) * n, hipMemcpyHostToDevice, e->stream));
-  PBA_HIP(hipStreamSynchronize(e->stream));
-  if (int rc = fn(user, slot, n)) return fail(PBA_ERR_DEVICE, "allreduce callback failed (" + std::to_string(rc) + ")");
-  PBA_HIP(hipMemcpyAsync(v, slot, sizeof(double) * n, hipMemcpyDeviceToHost, e->stream));
-  PBA_HIP(hipStreamSynchronize(e->stream));
-  return PBA_OK;
-}
 
 double now_ms() {
   return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
@@ -2866,11 +3070,18 @@ int pba_gn_step_import(pba_engine* e, double lambda, int32_t band, const double*
 
 namespace {
 
-struct Reducer {  // multi-GPU collective context of pba_solve_distributed (null: single GPU)
-  pba_allreduce_fn fn;
-  void* user;
-  double* X;
-  int band, K;
+// The collective of the multi-GPU loop: stream-ordered (a pba_comm: RCCL or an in-process group) or a host callback
+// that is called once the engine's stream has drained and is complete when it returns.
+struct Collective {
+  pba_allreduce_fn fn = nullptr;
+  void* user = nullptr;
+  pba_comm* comm = nullptr;
+  int allreduce(pba_engine* e, double* buf, long long n) const {
+    if (comm) return comm_allreduce(comm, buf, n, e->stream);
+    PBA_HIP(hipStreamSynchronize(e->stream));
+    if (int rc = fn(user, buf, n)) return fail(PBA_ERR_DEVICE, "allreduce callback failed (" + std::to_string(rc) + ")");
+    return PBA_OK;
+  }
 };
 
 // Levenberg-Marquardt (trust_region_minimizer.cc + levenberg_marquardt_strategy.cc semantics):
@@ -2879,14 +3090,37 @@ struct Reducer {  // multi-GPU collective context of pba_solve_distributed (null
 // With a Reducer every cost, model decrease and the reduced system are sums over ranks, so all ranks take
 // the same decisions and the same pose steps.
 pba_solver_options lm_options(const pba_solver_options* o) {
-  pba_solver_options opt{};
+  pba_solver_options opt{};  // Ceres' defaults (solver.h:278-322), max_num_iterations as map_utils.h:318
   opt.max_iterations = 20;
+  opt.max_num_consecutive_invalid_steps = 5;
   opt.initial_trust_region_radius = 1e4;
   opt.function_tolerance = 1e-6;
   opt.parameter_tolerance = 1e-8;
   opt.min_relative_decrease = 1e-3;
+  opt.gradient_tolerance = 1e-10;
+  opt.max_trust_region_radius = 1e16;
+  opt.min_trust_region_radius = 1e-32;
   if (o) opt = *o;
+  if (opt.max_num_consecutive_invalid_steps <= 0) opt.max_num_consecutive_invalid_steps = 5;
   return opt;
+}
+
+DecideOpts decide_opts(const pba_solver_options& o) {
+  return DecideOpts{o.min_relative_decrease, o.function_tolerance, o.parameter_tolerance, o.gradient_tolerance,
+                    o.max_trust_region_radius, o.min_trust_region_radius, o.max_num_consecutive_invalid_steps};
+}
+
+// The summary's outcome from a published decision record (done != 0).  Returns whether the trial counts as an
+// iteration (Ceres pushes no IterationSummary for a gradient-tolerance stop, which happens before the step, nor for the
+// consecutive-invalid-steps failure).
+bool finish_summary(double done, pba_solver_summary& s) {
+  switch ((int)done) {
+    case kDoneFunction: s.termination = PBA_TERMINATION_CONVERGENCE; s.stop_reason = PBA_STOP_FUNCTION_TOLERANCE; return true;
+    case kDoneParameter: s.termination = PBA_TERMINATION_CONVERGENCE; s.stop_reason = PBA_STOP_PARAMETER_TOLERANCE; return true;
+    case kDoneGradient: s.termination = PBA_TERMINATION_CONVERGENCE; s.stop_reason = PBA_STOP_GRADIENT_TOLERANCE; return false;
+    case kDoneRadius: s.termination = PBA_TERMINATION_CONVERGENCE; s.stop_reason = PBA_STOP_MIN_TRUST_REGION_RADIUS; return true;
+    default: s.termination = PBA_TERMINATION_FAILURE; s.stop_reason = PBA_STOP_INVALID_STEPS; return false;
+  }
 }
 
 // Single GPU: every trial is enqueued whole (lm_trial) and the accept/reject decision is taken on the device, so
@@ -2907,25 +3141,27 @@ int lm_loop_single(pba_engine* e, const pba_solver_options* o, pba_solver_summar
     for (int i = 0; i < 8; ++i) PBA_HIP(hipEventCreate(&events.ev[i]));
   const double t0 = now_ms();
   double cost = 0.0;
-  if (int rc = linearize(e, &cost)) return rc;  // the initial state's pieces, buffer set 0
+  int n_valid = 0;
+  if (int rc = linearize(e, &cost, nullptr, nullptr, nullptr, nullptr, &n_valid)) return rc;  // initial state, set 0
   s.linearize_ms += now_ms() - t0;
   s.initial_cost = cost;
-  // the device record: current cost, trust region, nothing done, set 0; no trial published yet
+  // the device record: current cost and valid blocks, trust region, nothing done, set 0, x_norm −1; no trial published
   for (int i = 0; i <= kLmFields; ++i) G.lm_h[i] = 0.0;
   G.lm_h[kLmCost] = cost;
+  G.lm_h[kLmValid] = n_valid;
+  G.lm_h[kLmXNorm] = -1.0;
   G.lm_h[kLmRadius] = opt.initial_trust_region_radius;
   G.lm_h[kLmFactor] = 2.0;
   G.lm_h[kLmLambda] = 1.0 / opt.initial_trust_region_radius;
   PBA_HIP(hipMemcpyAsync(G.lm.p, G.lm_h.data(), sizeof(double) * kLmFields, hipMemcpyHostToDevice, e->stream));
   const int n = std::max(0, opt.max_iterations);
-  auto enqueue = [&](int i) {
-    return lm_trial(e, opt.min_relative_decrease, opt.function_tolerance, (double)(i + 1),
-                    timed ? events.ev + 4 * (i & 1) : nullptr);
-  };
+  const DecideOpts dopt = decide_opts(opt);
+  auto enqueue = [&](int i) { return lm_trial(e, dopt, (double)(i + 1), timed ? events.ev + 4 * (i & 1) : nullptr); };
   if (n > 0)
     if (int rc = enqueue(0)) return rc;
   int iter = 0, set = 0;
   s.termination = PBA_TERMINATION_MAX_ITERATIONS;
+  s.stop_reason = PBA_STOP_MAX_ITERATIONS;
   for (; iter < n; ++iter) {
     if (iter + 1 < n)
       if (int rc = enqueue(iter + 1)) return rc;  // ahead of this trial's decision
@@ -2943,14 +3179,19 @@ int lm_loop_single(pba_engine* e, const pba_solver_options* o, pba_solver_summar
       PBA_HIP(hipEventElapsedTime(&ms, ev[2], ev[3]));
       s.cost_ms += ms;
     }
-    if (d[kLmConverged] != 0.0) {  // |Δcost| ≤ function_tolerance · cost: stop at the current state
-      s.termination = PBA_TERMINATION_CONVERGENCE;
-      ++iter;
+    s.gradient_max_norm = d[kLmGradNorm];
+    const double done = d[kLmDone];
+    if (done != 0.0 && done != kDoneRadius) {  // a tolerance (the step is not applied) or the invalid-step limit
+      if (finish_summary(done, s)) ++iter;
       break;
     }
-    if (d[kLmAccept] == 0.0) {  // failed solve, no predicted decrease, or too little actual decrease
+    if (d[kLmAccept] == 0.0) {  // invalid step (failed solve, no predicted decrease) or too little actual decrease
       ++s.unsuccessful_steps;
-      if (d[kLmDone] != 0.0) { s.termination = PBA_TERMINATION_FAILURE; break; }  // trust radius < 1e-32
+      if (done != 0.0) {  // the trust region collapsed
+        finish_summary(done, s);
+        ++iter;
+        break;
+      }
       continue;
     }
     ++s.successful_steps;
@@ -2971,71 +3212,129 @@ int lm_loop_single(pba_engine* e, const pba_solver_options* o, pba_solver_summar
   return PBA_OK;
 }
 
-// Multi-GPU: the reduced system and the costs are all-reduced through the caller's collective between the steps
-// (host-synchronised), so every rank takes the same decisions and the same pose steps.
-int lm_loop(pba_engine* e, const pba_solver_options* o, const Reducer* red, pba_solver_summary* sum) {
-  if (!red) return lm_loop_single(e, o, sum);
+// One multi-GPU LM trial, enqueued whole on the engine stream and steered by the device LM record like lm_trial:
+// point elimination for the record's λ (the previous trial's accept applied first) → this rank's banded partial system
+// into X → Σ over ranks → damping, constant frames (requested, or observed by no rank), solve → candidate state and the
+// update partials → candidate linearisation into the spare buffer set (its chunk partials are this rank's candidate
+// cost) → this rank's trial sums, the point part Σ over ranks (kExScalars doubles) → the decision, the same on every
+// rank, published to the host.  Two collectives per trial: λ of trial i + 1 depends on the decision of trial i, and the
+// point elimination (hence this rank's system) on λ.  With a stream-ordered collective the host enqueues the next trial
+// before this one's decision is known, as on one GPU; every rank enqueues the same trials (the decisions agree), so the
+// collectives match.
+int dist_trial(pba_engine* e, const Collective& coll, const DecideOpts& dopt, double* X, int K, double seq) {
+  GnData& G = e->gn;
+  const int nf = e->n_frames;
+  SchurArgs sa{G.schur_desc.p, G.schur_aux.p, G.schur_pairs.p, G.pt_first.p, G.pt_nblk.p, G.blk_lv.p,
+               G.blk_schur.p, G.blk_schur1.p, G.part_schur.p, G.pt_data.p, G.n_schur, G.lm.p,
+               e->poses.p, G.poses_new.p, e->rho.p, G.rho_new.p, G.pt_orig.p, 7 * nf, G.n_gn_points};
+  schur_lds_limit(G);
+  if (G.n_schur > 0) schur_kernel<<<G.n_schur, kBlockThreads, G.schur_lds, e->stream>>>(sa, 0.0);
+  else launch_accept(e, G.lm.p);  // no points on this rank: the accept alone
+  const long long nx = (long long)nf * ex_row(K);
+  PBA_HIP(hipMemsetAsync(X, 0, sizeof(double) * (size_t)nx, e->stream));
+  AsmArgs aa{G.part_lin.p, G.part_lin1.p, G.lm.p, G.part_schur.p, G.sky_cptr.p, G.sky_contrib.p, G.g_cptr.p,
+             G.g_contrib.p, G.sky_blk_i.p, G.sky_blk_j.p, G.fixed.p, G.S.p, G.g.p, G.g_dir.p, G.Ddiag.p, nullptr, K,
+             G.n_sky, nf, nullptr, nullptr, nullptr, 0, nullptr};
+  const int nthreads = G.n_sky * 36 + 6 * nf;
+  export_kernel<<<(nthreads + 255) / 256, 256, 0, e->stream>>>(aa, G.observed.p, X, K);
+  PBA_HIP(hipGetLastError());
+  if (int rc = coll.allreduce(e, X, nx)) return rc;
+  ImportArgs ia{X, G.fixed_req.p, G.Sband.p, G.g.p, G.g_dir.p, G.Ddiag.p, G.fixed_dist.p, nf, K};
+  const long long n = (long long)nf * ((K + 1) * 36 + 6);
+  import_kernel<<<(unsigned)((n + 255) / 256), 256, 0, e->stream>>>(ia, 0.0, G.lm.p);
+  PBA_HIP(hipGetLastError());
+  G.sband_dirty = true;
+  G.cr0_dirty = true;  // cr_build writes level 0 over the whole band
+  if (int rc = band_solve(e)) return rc;
+  int gp = 0, gq = 0;
+  enqueue_updates(e, 0.0, G.fixed_dist.p, &gp, &gq, G.lm.p);
+  if (G.n_chunks > 0)
+    if (int rc = linearize(e, nullptr, G.lm.p, G.pairs_new.p, G.rho_new.p, G.red.p + 2 * (gp + gq))) return rc;
+  double* Y = X + nx;
+  dist_sums_kernel<<<1, kDecideThreads, 0, e->stream>>>(G.red.p, G.red2.p, G.gmax.p, gp, gq, G.n_chunks, dopt.gtol,
+                                                         G.lm.p, G.tpose.p, Y);
+  PBA_HIP(hipGetLastError());
+  if (int rc = coll.allreduce(e, Y, kExScalars)) return rc;
+  dist_decide_kernel<<<1, 64, 0, e->stream>>>(Y, G.tpose.p, G.status.p, dopt, G.lm.p, G.lm_host_d, seq);
+  PBA_HIP(hipGetLastError());
+  return PBA_OK;
+}
+
+// The LM loop over one GPU (coll == nullptr) or all ranks: the host enqueues trial i + 1, then waits for the published
+// decision of trial i and builds Ceres' summary from it; after the loop the last accepted candidate becomes the state and
+// the current linearisation is moved to buffer set 0 for the host-driven entry points.
+int lm_loop(pba_engine* e, const pba_solver_options* o, const Collective* coll, double* X, int K, pba_solver_summary* sum) {
+  if (!coll) return lm_loop_single(e, o, sum);
+  GnData& G = e->gn;
   const pba_solver_options opt = lm_options(o);
   pba_solver_summary s{};
   const double t0 = now_ms();
+  if (G.band_kernel != K || G.solver == SOLVER_SKYLINE) {
+    const char* fs = getenv("PBA_SOLVER");
+    const int solver = (K <= 8 && !(fs && std::string(fs) == "band")) ? SOLVER_CR : SOLVER_BAND;
+    if (int rc = configure_solver(e, K, solver)) return rc;
+  }
   double cost = 0.0;
-  double t = now_ms();
-  if (int rc = linearize(e, &cost)) return rc;
-  if (int rc = allreduce_scalars(e, red->X, red->K, red->fn, red->user, &cost, 1)) return rc;
-  s.linearize_ms += now_ms() - t;
-  s.initial_cost = cost;
-  double radius = opt.initial_trust_region_radius, factor = 2.0;
-  int iter = 0;
-  s.termination = PBA_TERMINATION_MAX_ITERATIONS;
-  for (; iter < opt.max_iterations; ++iter) {
-    const double lambda = 1.0 / radius;
-    double model = 0.0, cost_new = 0.0;
-    int st = 0;
-    t = now_ms();
-    if (int rc = step_export(e, lambda, red->band, red->X)) return rc;
+  int n_valid = 0;
+  if (int rc = linearize(e, &cost, nullptr, nullptr, nullptr, nullptr, &n_valid)) return rc;
+  {  // Σ over ranks of the initial cost and valid blocks, through the scalar slots
+    double v[2] = {cost, (double)n_valid};
+    double* Y = X + (long long)e->n_frames * ex_row(K);
+    PBA_HIP(hipMemcpyAsync(Y, v, sizeof v, hipMemcpyHostToDevice, e->stream));
+    if (int rc = coll->allreduce(e, Y, 2)) return rc;
+    PBA_HIP(hipMemcpyAsync(v, Y, sizeof v, hipMemcpyDeviceToHost, e->stream));
     PBA_HIP(hipStreamSynchronize(e->stream));
-    if (int rc = red->fn(red->user, red->X, (long long)e->n_frames * ex_row(red->K)))
-      return fail(PBA_ERR_DEVICE, "allreduce callback failed (" + std::to_string(rc) + ")");
-    double mp = 0.0, mq = 0.0;
-    if (int rc = step_import(e, lambda, red->band, red->X, &mp, &mq, &st)) return rc;
-    s.solve_ms += now_ms() - t;
-    double v[2] = {mq, 0.0};
-    t = now_ms();
-    if (st == 0)  // st is identical on every rank (same summed system)
-      if (int rc = candidate_cost(e, &v[1])) return rc;
-    if (int rc = allreduce_scalars(e, red->X, red->K, red->fn, red->user, v, 2)) return rc;
-    s.cost_ms += now_ms() - t;
-    model = mp + v[0];
-    cost_new = v[1];
-    if (st != 0 || !(model > 0.0)) {  // non-positive-definite or no predicted decrease: shrink the region
-      radius /= factor;
-      factor *= 2.0;
-      ++s.unsuccessful_steps;
-      if (radius < 1e-32) { s.termination = PBA_TERMINATION_FAILURE; break; }
-      continue;
-    }
-    if (std::fabs(cost - cost_new) <= opt.function_tolerance * cost) {  // trust_region_minimizer.cc:115-117, :729
-      s.termination = PBA_TERMINATION_CONVERGENCE;                       // (the step is not applied)
-      ++iter;
+    cost = v[0];
+    n_valid = (int)v[1];
+  }
+  s.linearize_ms = now_ms() - t0;
+  s.initial_cost = cost;
+  for (int i = 0; i <= kLmFields; ++i) G.lm_h[i] = 0.0;
+  G.lm_h[kLmCost] = cost;
+  G.lm_h[kLmValid] = n_valid;
+  G.lm_h[kLmXNorm] = -1.0;
+  G.lm_h[kLmRadius] = opt.initial_trust_region_radius;
+  G.lm_h[kLmFactor] = 2.0;
+  G.lm_h[kLmLambda] = 1.0 / opt.initial_trust_region_radius;
+  PBA_HIP(hipMemcpyAsync(G.lm.p, G.lm_h.data(), sizeof(double) * kLmFields, hipMemcpyHostToDevice, e->stream));
+  const int n = std::max(0, opt.max_iterations);
+  const DecideOpts dopt = decide_opts(opt);
+  if (n > 0)
+    if (int rc = dist_trial(e, *coll, dopt, X, K, 1.0)) return rc;
+  int iter = 0, set = 0;
+  s.termination = PBA_TERMINATION_MAX_ITERATIONS;
+  s.stop_reason = PBA_STOP_MAX_ITERATIONS;
+  for (; iter < n; ++iter) {
+    if (iter + 1 < n)
+      if (int rc = dist_trial(e, *coll, dopt, X, K, (double)(iter + 2))) return rc;  // ahead of this trial's decision
+    double d[kLmFields];
+    if (int rc = wait_decision(e, (double)(iter + 1), d)) return rc;
+    set = (int)d[kLmSet];
+    s.gradient_max_norm = d[kLmGradNorm];
+    const double done = d[kLmDone];
+    if (done != 0.0 && done != kDoneRadius) {
+      if (finish_summary(done, s)) ++iter;
       break;
     }
-    const double rel = (cost - cost_new) / model;
-    if (rel > opt.min_relative_decrease && std::isfinite(cost_new)) {
-      if (int rc = accept(e)) return rc;
-      ++s.successful_steps;
-      radius = radius / std::max(1.0 / 3.0, 1.0 - std::pow(2.0 * rel - 1.0, 3));
-      factor = 2.0;
-      cost = cost_new;
-      t = now_ms();
-      if (int rc = linearize(e, nullptr)) return rc;
-      PBA_HIP(hipStreamSynchronize(e->stream));
-      s.linearize_ms += now_ms() - t;
-    } else {
+    if (d[kLmAccept] == 0.0) {
       ++s.unsuccessful_steps;
-      radius /= factor;
-      factor *= 2.0;
-      if (radius < 1e-32) { s.termination = PBA_TERMINATION_FAILURE; break; }
+      if (done != 0.0) {
+        finish_summary(done, s);
+        ++iter;
+        break;
+      }
+      continue;
     }
+    ++s.successful_steps;
+    cost = d[kLmCostNew];
+  }
+  launch_accept(e, G.lm.p);
+  PBA_HIP(hipStreamSynchronize(e->stream));
+  if (set == 1) {
+    std::swap(G.blk_schur.p, G.blk_schur1.p);
+    std::swap(G.blk_schur.n, G.blk_schur1.n);
+    std::swap(G.part_lin.p, G.part_lin1.p);
+    std::swap(G.part_lin.n, G.part_lin1.n);
   }
   s.iterations = iter;
   s.final_cost = cost;
@@ -3050,7 +3349,7 @@ extern "C" {
 
 int pba_solve(pba_engine* e, const pba_solver_options* o, pba_solver_summary* sum) {
   if (int rc = ensure_prepared(e)) return rc;
-  return lm_loop(e, o, nullptr, sum);
+  return lm_loop(e, o, nullptr, nullptr, 0, sum);
 }
 
 int pba_set_solver_timing(pba_engine* e, int32_t enable) {
@@ -3063,9 +3362,25 @@ int pba_solve_distributed(pba_engine* e, const pba_solver_options* o, int32_t ba
                           pba_allreduce_fn allreduce, void* user, pba_solver_summary* sum) {
   if (int rc = ensure_prepared(e)) return rc;
   if (!d_exchange || !allreduce) return fail(PBA_ERR_INVALID_ARGUMENT, "null exchange buffer or allreduce");
-  Reducer r{allreduce, user, d_exchange, band, 0};
-  if (int rc = exchange_K(e, band, &r.K)) return rc;
-  return lm_loop(e, o, &r, sum);
+  int K;
+  if (int rc = exchange_K(e, band, &K)) return rc;
+  Collective c;
+  c.fn = allreduce;
+  c.user = user;
+  return lm_loop(e, o, &c, d_exchange, K, sum);
+}
+
+int pba_solve_distributed_comm(pba_engine* e, const pba_solver_options* o, int32_t band, pba_comm* comm,
+                               pba_solver_summary* sum) {
+  if (int rc = ensure_prepared(e)) return rc;
+  if (!comm) return fail(PBA_ERR_INVALID_ARGUMENT, "null communicator");
+  int K;
+  if (int rc = exchange_K(e, band, &K)) return rc;
+  GnData& G = e->gn;
+  PBA_HIP(G.exchange.resize((size_t)exchange_count(e, K)));
+  Collective c;
+  c.comm = comm;
+  return lm_loop(e, o, &c, G.exchange.p, K, sum);
 }
 
 }  // extern "C"

@@ -131,6 +131,8 @@ struct KernelArgs {
   double umax, vmax;             // interpolation clamp bounds W + 1, H + 1
   const float* intr;             // 8 floats per camera (Jacobian chain)
   const double* intr_d;          // kCamD doubles per camera (warp / projection; pba_device.h)
+  const float* intr_t;           // the target cameras' projection constants (geometric kernels): intr, or the
+  const double* intr_t_d;        // intrinsics state of pba_set_optimize_intrinsics (host unprojection stays on intr_d)
   const int* block_point;
   const int* block_pair;
   const int2* block_pp;          // per block {point, pair}
@@ -614,6 +616,9 @@ struct GnData {
   bool cr0_dirty = true;                            // CR level 0 not (re)initialised for assemble's direct writes
   std::vector<uint8_t> fixed_h;
   DevBuf<double> poses_new, rho_new, red;
+  DevBuf<double> red2, gmax;  // update partials: (Σ step², Σ x_new²) and max gradient component per slot (lm_decide)
+  DevBuf<double> tpose;       // multi-GPU: the trial's pose-part sums (dist_sums_kernel)
+  DevBuf<double> exchange;    // multi-GPU exchange buffer of pba_solve_distributed_comm
   DevBuf<int> status;
   DevBuf<PairRec> pairs_new;
   bool pairs_new_fresh = false;  // pairs_new formed by the last update_kernel (its candidate state)
@@ -639,6 +644,7 @@ struct LevelData {
 }  // namespace detail
 }  // namespace pba
 
+#include <atomic>
 #include <memory>
 
 struct pba_engine {
@@ -668,6 +674,10 @@ struct pba_engine {
   pba::detail::DevBuf<uint8_t> valid;
   int record_format = PBA_RECORD_F32;
   int interp = PBA_INTERP_BILINEAR;  // pba_set_interpolator
+  bool host_int_sampled = false;     // I_h,k sampled on the device (pba_set_points without intensities)
+  bool opt_intr = false;             // pba_set_optimize_intrinsics: target intrinsics state + J_intr record tail
+  pba::detail::DevBuf<float> intr_state;     // its projection constants (8 floats per camera)
+  pba::detail::DevBuf<double> intr_state_d;  // and fp64 camera records (kCamD per camera)
   bool state_set = false;
   bool pairs_fresh = false;          // pairs hold T_th of the current poses (pba_set_state_device forms them)
   bool evaluated = false;
@@ -677,9 +687,15 @@ struct pba_engine {
   int level = 0;                     // active pyramid level (its buffers are swapped into the fields above)
   std::vector<std::unique_ptr<pba::detail::LevelData>> pyr;  // [1, n_levels); [0] unused
   size_t ev_used = 0;
+  // pba_get_records_async: one event per chunk of copied records, and how many chunks are known to have arrived
+  std::vector<hipEvent_t> chunk_ev;
+  int chunk_blocks = 0, n_chunks_async = 0;
+  std::atomic<int> chunks_arrived{0};
   pba::detail::GnData gn;
 
   int R() const { return opt.residual_kind == PBA_RESIDUAL_PHOTOMETRIC ? P : 2; }
+  // values per record: [r | J_host | J_target | J_rho] (14R), + J_intr (8R) with pba_set_optimize_intrinsics
+  int rec_floats() const { return (opt_intr ? 22 : 14) * R(); }
 };
 
 namespace pba {
@@ -701,6 +717,11 @@ void launch_pairs(pba_engine* e, const double* poses, PairRec* pairs);
 // poses (optional): evaluate at these state poses with the fused-state prologue instead of the pair table.
 int launch_cost_only(pba_engine* e, const PairRec* pairs, const double* rho, double* wg_red = nullptr,
                      int* n_slots = nullptr, const double* poses = nullptr);
+
+// Collectives of the multi-GPU loop (pba_comm.hip): Σ over the ranks in place, enqueued on stream.
+int comm_allreduce(pba_comm* c, double* buf, long long count, hipStream_t stream);
+int comm_rank(const pba_comm* c);
+int comm_size(const pba_comm* c);
 
 // Pyramid (pba_pyramid.hip): back to level 0 and drop the levels; I_h,k sampled from the active level's host images.
 void reset_pyramid(pba_engine* e);

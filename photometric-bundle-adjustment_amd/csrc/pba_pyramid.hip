@@ -132,9 +132,23 @@ int pba_set_interpolator(pba_engine* e, int32_t interpolator) {
   if (!e) return fail(PBA_ERR_INVALID_ARGUMENT, "null engine");
   if (interpolator != PBA_INTERP_BILINEAR && interpolator != PBA_INTERP_BICUBIC)
     return fail(PBA_ERR_INVALID_ARGUMENT, "unknown interpolator");
+  const bool resample = e->host_int_sampled && interpolator != e->interp;
   e->interp = interpolator;
   e->evaluated = false;
-  return PBA_OK;
+  if (!resample) return PBA_OK;
+  // I_h,k were sampled on the device with the previous interpolator: sample them again with this one, at every level
+  if (int rc = check_device(e)) return rc;
+  const int active = e->level;
+  if (int rc = pba_set_level(e, 0)) return rc;
+  if (int rc = sample_host_intensities(e, e->u_ref.p, e->host_int.p)) return rc;
+  for (size_t l = 1; l < e->pyr.size(); ++l) {
+    LevelData& L = *e->pyr[l];
+    swap_level(e, L);
+    const int rc = sample_host_intensities(e, e->u_ref.p, e->host_int.p);
+    swap_level(e, L);
+    if (rc) return rc;
+  }
+  return pba_set_level(e, active);
 }
 
 int pba_interpolator(const pba_engine* e) { return e ? e->interp : PBA_INTERP_BILINEAR; }
@@ -266,6 +280,8 @@ int pba_solve_pyramid(pba_engine* e, const pba_solver_options* options, pba_solv
     acc.successful_steps += s.successful_steps;
     acc.unsuccessful_steps += s.unsuccessful_steps;
     acc.termination = s.termination;
+    acc.stop_reason = s.stop_reason;
+    acc.gradient_max_norm = s.gradient_max_norm;
     acc.final_cost = s.final_cost;
     acc.total_ms += s.total_ms;
     acc.linearize_ms += s.linearize_ms;

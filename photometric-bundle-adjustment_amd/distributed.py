@@ -6,14 +6,16 @@ eliminator.  Both properties make the host keyframe the natural shard unit: a po
 live on the rank that owns the point's host keyframe, so
 
 * evaluation (the headline metric) needs no collective at all — each rank evaluates its own blocks;
-* Gauss-Newton needs exactly one exchange per LM iteration: the sum of the per-rank reduced camera systems
-  (banded, (K+1)·36 + 24 doubles per keyframe) plus three scalars (cost, candidate cost, point part of the
-  model decrease).  Every rank then solves the same system and back-substitutes its own points.
+* Gauss-Newton needs two sums per LM trial: the per-rank reduced camera systems (banded, (K+1)·36 + 24 doubles per
+  keyframe), then 8 point-part scalars of the trial (model decrease, candidate cost and valid blocks, step and state
+  norms, points above the gradient tolerance).  Every rank solves the same system, back-substitutes its own points and
+  takes the same LM decision on the device.
 
 Every rank holds all keyframe poses (7 doubles each) and the images of the keyframes its blocks target.
-The collective is `torch.distributed.all_reduce` (RCCL on ROCm for the "nccl" backend; "gloo" stages
-through the host) on a device buffer the engine writes into; `pba_solve_distributed` calls back into
-`TorchAllReduce` whenever it needs a sum.
+With the "nccl" backend (RCCL on ROCm) the engine gets its own RCCL communicator (`rccl_comm`: rank 0's id broadcast
+through the process group) and enqueues both sums on its stream (`pba_solve_distributed_comm`: the host never waits
+inside a trial).  Other backends ("gloo", CPU tests) go through `TorchAllReduce`, a host callback the engine calls once
+its stream has drained.
 """
 from __future__ import annotations
 
@@ -132,8 +134,34 @@ def global_band(engine, group=None, device=None) -> int:
     return int(t.item())
 
 
-def solve_distributed(engine, group=None, device=None, **options) -> dict:
-    """LM over all ranks of `group` (pba_solve_distributed): collective, every rank calls it."""
+_RCCL = {}
+
+
+def rccl_comm(group=None, device_index: int = 0):
+    """The engine's RCCL communicator over the ranks of `group` (collective on first use, then cached): rank 0's
+    ncclUniqueId is broadcast through the torch.distributed group, every rank calls pba_comm_init."""
+    import torch.distributed as dist
+    key = (id(group), device_index)
+    if key not in _RCCL:
+        import importlib
+        E = importlib.import_module(__package__ + ".engine")
+        rank, world = dist.get_rank(group), dist.get_world_size(group)
+        obj = [E.Comm.unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(obj, src=dist.get_global_rank(group, 0) if group is not None else 0, group=group)
+        _RCCL[key] = E.Comm.rccl(obj[0], world, rank, device_index)
+    return _RCCL[key]
+
+
+def solve_distributed(engine, group=None, device=None, comm=None, **options) -> dict:
+    """LM over all ranks of `group`: collective, every rank calls it.  comm (an engine.Comm) or, for the "nccl" backend
+    on a GPU, the cached RCCL communicator: stream-ordered pba_solve_distributed_comm; otherwise the TorchAllReduce
+    callback of pba_solve_distributed."""
+    import torch.distributed as dist
     band = global_band(engine, group, device)
+    if comm is None and device is not None and getattr(device, "type", str(device)) == "cuda" \
+            and dist.get_backend(group) == "nccl":
+        comm = rccl_comm(group, device.index or 0)
+    if comm is not None:
+        return engine.solve_distributed_comm(band, comm, **options)
     ar = TorchAllReduce(engine.gn_exchange_size(band), device if device is not None else "cpu", group)
     return engine.solve_distributed(band, ar.ptr, ar, **options)

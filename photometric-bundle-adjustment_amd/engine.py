@@ -45,19 +45,38 @@ class MapInfo(C.Structure):
 
 
 class SolverOptions(C.Structure):
-    _fields_ = [("max_iterations", C.c_int32), ("pad_", C.c_int32), ("initial_trust_region_radius", C.c_double),
-                ("function_tolerance", C.c_double), ("parameter_tolerance", C.c_double),
-                ("min_relative_decrease", C.c_double)]
+    """pba_solver_options (Ceres' Solver::Options defaults, solver.h:278-322)."""
+    _fields_ = [("max_iterations", C.c_int32), ("max_num_consecutive_invalid_steps", C.c_int32),
+                ("initial_trust_region_radius", C.c_double), ("function_tolerance", C.c_double),
+                ("parameter_tolerance", C.c_double), ("min_relative_decrease", C.c_double),
+                ("gradient_tolerance", C.c_double), ("max_trust_region_radius", C.c_double),
+                ("min_trust_region_radius", C.c_double)]
+
+
+def solver_options(max_iterations=20, initial_trust_region_radius=1e4, function_tolerance=1e-6,
+                   min_relative_decrease=1e-3, parameter_tolerance=1e-8, gradient_tolerance=1e-10,
+                   max_trust_region_radius=1e16, min_trust_region_radius=1e-32, max_num_consecutive_invalid_steps=5):
+    return SolverOptions(max_iterations, max_num_consecutive_invalid_steps, initial_trust_region_radius,
+                         function_tolerance, parameter_tolerance, min_relative_decrease, gradient_tolerance,
+                         max_trust_region_radius, min_trust_region_radius)
+
+
+TERMINATION_CONVERGENCE, TERMINATION_MAX_ITERATIONS, TERMINATION_FAILURE = 0, 1, 2
+STOP_REASONS = ("max_iterations", "function_tolerance", "parameter_tolerance", "gradient_tolerance",
+                "min_trust_region_radius", "invalid_steps")
 
 
 class SolverSummary(C.Structure):
     _fields_ = [("iterations", C.c_int32), ("successful_steps", C.c_int32), ("unsuccessful_steps", C.c_int32),
                 ("termination", C.c_int32), ("initial_cost", C.c_double), ("final_cost", C.c_double),
                 ("total_ms", C.c_double), ("linearize_ms", C.c_double), ("solve_ms", C.c_double),
-                ("cost_ms", C.c_double)]
+                ("cost_ms", C.c_double), ("gradient_max_norm", C.c_double), ("stop_reason_code", C.c_int32),
+                ("pad_", C.c_int32)]
 
     def as_dict(self):
-        return {f: getattr(self, f) for f, _ in self._fields_}
+        d = {f: getattr(self, f) for f, _ in self._fields_ if f != "pad_"}
+        d["stop_reason"] = STOP_REASONS[self.stop_reason_code]
+        return d
 
 
 # int (*pba_allreduce_fn)(void* user, double* d_buf, int64_t count)
@@ -146,6 +165,16 @@ def lib():
                                 C.POINTER(i32)], C.c_int),
         "pba_solve_distributed": ([vp, C.POINTER(SolverOptions), i32, vp, ALLREDUCE_FN, vp,
                                    C.POINTER(SolverSummary)], C.c_int),
+        "pba_solve_distributed_comm": ([vp, C.POINTER(SolverOptions), i32, vp, C.POINTER(SolverSummary)], C.c_int),
+        "pba_comm_unique_id": ([vp], C.c_int),
+        "pba_comm_init": ([vp, i32, i32, i32, C.POINTER(vp)], C.c_int),
+        "pba_comm_init_local": ([i32, i32, vp], C.c_int),
+        "pba_comm_destroy": ([vp], C.c_int),
+        "pba_comm_rank": ([vp], C.c_int),
+        "pba_comm_size": ([vp], C.c_int),
+        "pba_comm_allreduce": ([vp, vp, C.c_int64, vp], C.c_int),
+        "pba_set_optimize_intrinsics": ([vp, i32], C.c_int),
+        "pba_set_intrinsics_state": ([vp, vp], C.c_int),
         "pba_compute_projections": ([vp, i32, vp, vp, vp, vp, C.POINTER(OutlierThresholds), vp, vp, vp, vp], C.c_int),
         "pba_outlier_landmarks": ([i32, i32, vp, vp, vp, vp, vp, vp], C.c_int),
         "pba_set_record_format": ([vp, i32], C.c_int),
@@ -355,10 +384,9 @@ class Engine:
         """per-phase device timing of solve() (linearize_ms / solve_ms / cost_ms); off by default"""
         _check(self._L.pba_set_solver_timing(self._h, 1 if enable else 0), "pba_set_solver_timing")
 
-    def solve(self, max_iterations=20, initial_trust_region_radius=1e4, function_tolerance=1e-6,
-              min_relative_decrease=1e-3) -> dict:
-        o = SolverOptions(max_iterations, 0, initial_trust_region_radius, function_tolerance, 1e-8,
-                          min_relative_decrease)
+    def solve(self, **options) -> dict:
+        """pba_solve; options as solver_options() (Ceres' names and defaults, max_iterations 20)."""
+        o = solver_options(**options)
         s = SolverSummary()
         _check(self._L.pba_solve(self._h, C.byref(o), C.byref(s)), "pba_solve")
         return s.as_dict()
@@ -381,10 +409,8 @@ class Engine:
         _check(self._L.pba_get_host_intensities(self._h, _p(out)), "pba_get_host_intensities")
         return out
 
-    def solve_pyramid(self, max_iterations=20, initial_trust_region_radius=1e4, function_tolerance=1e-6,
-                      min_relative_decrease=1e-3) -> dict:
-        o = SolverOptions(max_iterations, 0, initial_trust_region_radius, function_tolerance, 1e-8,
-                          min_relative_decrease)
+    def solve_pyramid(self, **options) -> dict:
+        o = solver_options(**options)
         s = SolverSummary()
         _check(self._L.pba_solve_pyramid(self._h, C.byref(o), C.byref(s)), "pba_solve_pyramid")
         return s.as_dict()
@@ -410,8 +436,7 @@ class Engine:
                                           C.byref(st)), "pba_gn_step_import")
         return mp.value, mq.value, st.value
 
-    def solve_distributed(self, band: int, exchange_ptr: int, allreduce, max_iterations=20,
-                          initial_trust_region_radius=1e4, function_tolerance=1e-6, min_relative_decrease=1e-3) -> dict:
+    def solve_distributed(self, band: int, exchange_ptr: int, allreduce, **options) -> dict:
         """pba_solve_distributed; `allreduce(ptr, count) -> None` sums `count` doubles at device address `ptr`
         over all ranks in place (collective, complete on return)."""
         err = []
@@ -425,14 +450,31 @@ class Engine:
                 return 1
 
         fn = ALLREDUCE_FN(cb)
-        o = SolverOptions(max_iterations, 0, initial_trust_region_radius, function_tolerance, 1e-8,
-                          min_relative_decrease)
+        o = solver_options(**options)
         s = SolverSummary()
         rc = self._L.pba_solve_distributed(self._h, C.byref(o), band, C.c_void_p(exchange_ptr), fn, None, C.byref(s))
         if err:
             raise err[0]
         _check(rc, "pba_solve_distributed")
         return s.as_dict()
+
+    def solve_distributed_comm(self, band: int, comm: "Comm", **options) -> dict:
+        """pba_solve_distributed_comm: the collectives are enqueued on the engine stream (RCCL or an in-process
+        group), the exchange buffer is the engine's own."""
+        o = solver_options(**options)
+        s = SolverSummary()
+        _check(self._L.pba_solve_distributed_comm(self._h, C.byref(o), band, comm.handle, C.byref(s)),
+               "pba_solve_distributed_comm")
+        return s.as_dict()
+
+    # -- target intrinsics (geometric, optimize_intrinsics) -----------------------------------------
+    def set_optimize_intrinsics(self, enable: bool = True):
+        _check(self._L.pba_set_optimize_intrinsics(self._h, int(bool(enable))), "pba_set_optimize_intrinsics")
+        self.record = self._L.pba_record_floats(self._h)
+
+    def set_intrinsics_state(self, intrinsics: np.ndarray):
+        k = np.ascontiguousarray(intrinsics, np.float64)
+        _check(self._L.pba_set_intrinsics_state(self._h, _p(k)), "pba_set_intrinsics_state")
 
     def get_state(self):
         poses = np.empty((self.n_frames, 7), np.float64)
@@ -469,6 +511,54 @@ class Engine:
 
     def __exit__(self, *exc):
         self.close()
+
+
+class Comm:
+    """pba_comm: an RCCL communicator (one process per GPU) or one rank of an in-process group."""
+
+    def __init__(self, handle: C.c_void_p):
+        self.handle = handle
+
+    @staticmethod
+    def unique_id() -> bytes:
+        buf = (C.c_uint8 * 128)()
+        _check(lib().pba_comm_unique_id(buf), "pba_comm_unique_id")
+        return bytes(buf)
+
+    @classmethod
+    def rccl(cls, uid: bytes, n_ranks: int, rank: int, device: int = 0) -> "Comm":
+        buf = (C.c_uint8 * 128).from_buffer_copy(uid)
+        h = C.c_void_p()
+        _check(lib().pba_comm_init(buf, n_ranks, rank, device, C.byref(h)), "pba_comm_init")
+        return cls(h)
+
+    @classmethod
+    def local_group(cls, n_ranks: int, device: int = 0) -> list:
+        hs = (C.c_void_p * n_ranks)()
+        _check(lib().pba_comm_init_local(n_ranks, device, hs), "pba_comm_init_local")
+        return [cls(C.c_void_p(h)) for h in hs]
+
+    def allreduce(self, ptr: int, count: int, stream: int = 0):
+        _check(lib().pba_comm_allreduce(self.handle, C.c_void_p(ptr), count, C.c_void_p(stream)), "pba_comm_allreduce")
+
+    @property
+    def rank(self) -> int:
+        return lib().pba_comm_rank(self.handle)
+
+    @property
+    def size(self) -> int:
+        return lib().pba_comm_size(self.handle)
+
+    def close(self):
+        if self.handle:
+            lib().pba_comm_destroy(self.handle)
+            self.handle = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 def load_map(map_path: str, calib_path: str):

@@ -1,12 +1,16 @@
 // Drives include/pba_ceres.h the way Ceres' ProgramEvaluator/ResidualBlock would (program_evaluator.h:157-237,
 // residual_block.cc:69-158): PrepareForEvaluation, then per block CostFunction::Evaluate with the reference's
 // parameter pointers, then J_local = J_global · LocalParameterization::ComputeJacobian.  Writes the tangent
-// records for comparison with the oracle (tests/test_gpu_ceres_adapter.py).
-//   usage: adapter_driver <problem.bin> <out.bin>     (problem layout: tests/golden/make_golden.py)
+// records for comparison with the oracle (tests/test_ceres_adapter.py).
+//   pose_param "ref" (default): the 7-wide Jacobians are composed with Sophus' Dx_this_mul_exp_x_at_0 at each block's
+//   frames (se3_plus_jacobian, the product of the reference's LocalParameterizationSE3); "tangent": with the adapter's
+//   SE3TangentParameterization.  The 7×6 P of frame 0 is written too (the test pins it against Sophus' own).
+//   usage: adapter_driver <problem.bin> <out.bin> [ref|tangent]    (problem layout: tests/golden/make_golden.py)
 #include <array>
 #include <cstdio>
 #include <cstdlib>
 #include <memory>
+#include <string>
 #include <vector>
 
 #include "pba_ceres.h"
@@ -19,7 +23,8 @@ static std::vector<T> rd(FILE* f, size_t n) {
 }
 
 int main(int argc, char** argv) {
-  if (argc != 3) return 1;
+  if (argc < 3) return 1;
+  const bool tangent = argc > 3 && std::string(argv[3]) == "tangent";
   FILE* f = fopen(argv[1], "rb");
   if (!f) return 2;
   const auto hdr = rd<int32_t>(f, 9);
@@ -56,15 +61,20 @@ int main(int argc, char** argv) {
   for (int i = 0; i < nf; ++i) pose_ptr[i] = T[i].data();
   for (int p = 0; p < np; ++p) rho_ptr[p] = &rho[p];
   std::vector<double> intr_target(8);
-  pba_ceres::GpuEvaluator ev(e, pose_ptr, rho_ptr);
+  pba_ceres::GpuEvaluator ev(e, pose_ptr, rho_ptr, {},
+                             tangent ? pba_ceres::PoseJacobian::kTangent : pba_ceres::PoseJacobian::kReferenceSE3);
   std::vector<std::unique_ptr<ceres::CostFunction>> cfs;
   for (int b = 0; b < nb; ++b) {
-    if (kind == 0) cfs.emplace_back(new pba_ceres::GpuPhotometricCost<8>(&ev, b));
-    else cfs.emplace_back(new pba_ceres::GpuReprojectionCost(&ev, b));
+    const int h = point_host[block_point[b]], t = block_target[b];
+    if (kind == 0) cfs.emplace_back(new pba_ceres::GpuPhotometricCost<8>(&ev, b, h, t));
+    else cfs.emplace_back(new pba_ceres::GpuReprojectionCost(&ev, b, h, t));
   }
   pba_ceres::SE3TangentParameterization lp;
-  double Pj[42];
-  lp.ComputeJacobian(T[0].data(), Pj);
+  std::vector<double> Pf(42 * (size_t)nf);  // ComputeJacobian of every frame's parameterisation
+  for (int i = 0; i < nf; ++i) {
+    if (tangent) lp.ComputeJacobian(T[i].data(), &Pf[42 * i]);
+    else pba_ceres::se3_plus_jacobian(T[i].data(), &Pf[42 * i]);
+  }
 
   const int R = kind == 0 ? P : 2, rec = 14 * R;
   std::vector<double> out((size_t)nb * rec, 0.0), ronly((size_t)nb * R, 0.0);
@@ -75,17 +85,19 @@ int main(int argc, char** argv) {
   for (int b = 0; b < nb; ++b) {
     const int p = block_point[b], h = point_host[p], t = block_target[b];
     const double* params[4] = {T[h].data(), T[t].data(), &rho[p], intr_target.data()};
-    double* jac[4] = {J0.data(), J1.data(), J2.data(), J3.data()};
+    double* jac[4] = {J0.data(), J1.data(), J2.data(), nullptr};  // the intrinsics block is constant (map_utils.h:340-345)
     if (!cfs[b]->Evaluate(params, r.data(), jac)) continue;
     valid[b] = 1;
     double* o = &out[(size_t)b * rec];
+    const double* Ph = &Pf[42 * h];
+    const double* Pt = &Pf[42 * t];
     for (int k = 0; k < R; ++k) {
       o[k] = r[k];
       for (int c = 0; c < 6; ++c) {  // J_local = J_global · P   (residual_block.cc:136-158)
         double sh = 0, st = 0;
         for (int g = 0; g < 7; ++g) {
-          sh += J0[k * 7 + g] * Pj[g * 6 + c];
-          st += J1[k * 7 + g] * Pj[g * 6 + c];
+          sh += J0[k * 7 + g] * Ph[g * 6 + c];
+          st += J1[k * 7 + g] * Pt[g * 6 + c];
         }
         o[R + 6 * k + c] = sh;
         o[7 * R + 6 * k + c] = st;
@@ -112,6 +124,7 @@ int main(int argc, char** argv) {
   fwrite(ronly.data(), sizeof(double), ronly.size(), g);
   fwrite(valid_r.data(), 1, valid_r.size(), g);
   fwrite(plus, sizeof(double), 7, g);
+  fwrite(Pf.data(), sizeof(double), 42, g);  // frame 0's P
   fclose(g);
   pba_destroy(e);
   return 0;

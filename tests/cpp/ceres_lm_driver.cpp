@@ -4,8 +4,10 @@
 //   cpu  the reference's CPU path: one ceres::AutoDiffCostFunction per residual block over the restated functor
 //        (tests/cpp/ceres_functors.h), the reference's own LocalParameterizationSE3 (local_parameterization_se3.hpp).
 //   gpu  the drop-in: the same Problem with include/pba_ceres.h — GpuEvaluator as Problem::Options::
-//        evaluation_callback, GpuPhotometricCost / GpuReprojectionCost per block, SE3TangentParameterization —
-//        evaluated by the MI355X engine (libpba.so).  The evaluation-callback protocol of
+//        evaluation_callback, GpuPhotometricCost / GpuReprojectionCost per block, and the reference's own
+//        LocalParameterizationSE3 (pose_param "ref", the default: the adapter emits J7 = J6·P⁺) or the adapter's
+//        SE3TangentParameterization ("tangent") — evaluated by the MI355X engine (libpba.so).  The evaluation-callback
+//        protocol of
 //        evaluation_callback_test.cc:79-160 is checked on every call (Prepare/Evaluate pairing, new_evaluation_point
 //        semantics, Jacobians requested iff prepared with Jacobians, parameters equal to the prepared state).
 //
@@ -18,7 +20,12 @@
 // CPU mode, for an EUCM camera, runs the vendored ceres::PhotometricError<8> itself (photometric_error.h:79-189) —
 // the whole CPU side is then reference-held code.
 //
+// optimize_intrinsics = 1 (geometric): the intrinsics blocks are free (map_utils.h:339-345); the CPU functor keeps
+// unprojecting with the captured pointer (user memory, which Ceres does not write during a solve without a callback),
+// the GPU evaluator gets the blocks and enables the engine's target-intrinsics Jacobian.
+//
 //   usage: ceres_lm_driver <cpu|gpu> <problem.bin> <out.json> [iters] [huber] [threads] [fixed,frames] [ftol] [interp]
+//                          [ptol] [gtol] [optimize_intrinsics] [pose_param ref|tangent]
 //          (problem layout: tests/golden/make_golden.py write_problem)
 #include <atomic>
 #include <cstdint>
@@ -65,8 +72,9 @@ struct Protocol {
 // GpuEvaluator with the checks of evaluation_callback_test.cc:79-112 (Prepare side).
 class CheckedEvaluator : public pba_ceres::GpuEvaluator {
  public:
-  CheckedEvaluator(pba_engine* e, std::vector<double*> poses, std::vector<double*> rho, int n_blocks, Protocol* pr)
-      : GpuEvaluator(e, poses, rho), poses_(poses), rho_(rho), nb_(n_blocks), pr_(pr) {}
+  CheckedEvaluator(pba_engine* e, std::vector<double*> poses, std::vector<double*> rho, std::vector<double*> intr,
+                   pba_ceres::PoseJacobian form, int n_blocks, Protocol* pr)
+      : GpuEvaluator(e, poses, rho, intr, form), poses_(poses), rho_(rho), nb_(n_blocks), pr_(pr) {}
   void PrepareForEvaluation(bool evaluate_jacobians, bool new_evaluation_point) override {
     Protocol& p = *pr_;
     std::vector<double> st;
@@ -166,6 +174,13 @@ int main(int argc, char** argv) {
   }
   const double ftol = argc > 8 ? atof(argv[8]) : 1e-6;
   const int interp = argc > 9 ? atoi(argv[9]) : 0;
+  const double ptol = argc > 10 ? atof(argv[10]) : 1e-8;
+  const double gtol = argc > 11 ? atof(argv[11]) : 1e-10;
+  // 0: constant intrinsics blocks; 1: free, given to the GPU evaluator; 2: free but NOT given to it (the adapter must
+  // refuse the Jacobian request instead of reporting a zero gradient)
+  const int intr_mode = argc > 12 ? atoi(argv[12]) : 0;
+  const bool opt_intr = intr_mode != 0;
+  const bool tangent = argc > 13 && std::string(argv[13]) == "tangent";
 
   FILE* f = fopen(argv[2], "rb");
   if (!f) return 2;
@@ -212,17 +227,23 @@ int main(int argc, char** argv) {
                      "points");
     pba_ceres::check(pba_set_blocks(e, nb, block_point.data(), block_target.data(), kind == 1 ? u_obs.data() : nullptr),
                      "blocks");
-    ev.reset(new CheckedEvaluator(e, pose_ptr, rho_ptr, nb, &protocol));
+    std::vector<double*> intr_ptr;
+    if (intr_mode == 1)
+      for (int c = 0; c < nc; ++c) intr_ptr.push_back(&intr[8 * c]);
+    ev.reset(new CheckedEvaluator(e, pose_ptr, rho_ptr, intr_ptr,
+                                  tangent ? pba_ceres::PoseJacobian::kTangent : pba_ceres::PoseJacobian::kReferenceSE3,
+                                  nb, &protocol));
     popt.evaluation_callback = ev.get();  // problem.h:185 (not owned)
   }
   ceres::Problem problem(popt);
   for (int i = 0; i < nf; ++i) {  // map_utils.h:330-337
-    ceres::LocalParameterization* lp = gpu ? static_cast<ceres::LocalParameterization*>(new pba_ceres::SE3TangentParameterization)
-                                           : new Sophus::test::LocalParameterizationSE3;
+    ceres::LocalParameterization* lp =
+        gpu && tangent ? static_cast<ceres::LocalParameterization*>(new pba_ceres::SE3TangentParameterization)
+                       : new Sophus::test::LocalParameterizationSE3;  // the reference's own, in both modes
     problem.AddParameterBlock(T[i].data(), 7, lp);
   }
   for (int i : fixed) problem.SetParameterBlockConstant(T[i].data());
-  if (kind == 1)
+  if (kind == 1 && !opt_intr)
     for (int c = 0; c < nc; ++c) {  // :340-345
       problem.AddParameterBlock(&intr[8 * c], 8);
       problem.SetParameterBlockConstant(&intr[8 * c]);
@@ -263,8 +284,8 @@ int main(int argc, char** argv) {
     ceres::LossFunction* loss = huber > 0 ? new ceres::HuberLoss(huber) : nullptr;
     ceres::CostFunction* cf;
     if (gpu) {
-      ceres::CostFunction* inner = kind == 0 ? static_cast<ceres::CostFunction*>(new pba_ceres::GpuPhotometricCost<8>(ev.get(), b))
-                                             : new pba_ceres::GpuReprojectionCost(ev.get(), b);
+      ceres::CostFunction* inner = kind == 0 ? static_cast<ceres::CostFunction*>(new pba_ceres::GpuPhotometricCost<8>(ev.get(), b, h, t))
+                                             : new pba_ceres::GpuReprojectionCost(ev.get(), b, h, t);
       cf = new CheckedCost(inner, &protocol, h, t, p, nf);
     } else if (kind == 1) {
       cf = new ceres::AutoDiffCostFunction<pba_test::GeometricFunctor, 2, 7, 7, 1, 8>(new pba_test::GeometricFunctor(
@@ -289,6 +310,8 @@ int main(int argc, char** argv) {
   so.linear_solver_type = ceres::SPARSE_SCHUR;
   so.num_threads = threads;
   so.function_tolerance = ftol;
+  so.parameter_tolerance = ptol;
+  so.gradient_tolerance = gtol;
   ceres::Solver::Summary sum;
   ceres::Solve(so, &problem, &sum);
 
@@ -298,9 +321,10 @@ int main(int argc, char** argv) {
     << ",\"unsuccessful_steps\":" << sum.num_unsuccessful_steps << ",\"iterations\":[";
   for (size_t i = 0; i < sum.iterations.size(); ++i) {
     const auto& it = sum.iterations[i];
-    char buf[200];
-    snprintf(buf, sizeof buf, "%s[%d,%.17g,%d,%.17g,%.17g]", i ? "," : "", it.iteration, it.cost,
-             it.step_is_successful ? 1 : 0, it.relative_decrease, it.trust_region_radius);
+    char buf[300];
+    snprintf(buf, sizeof buf, "%s[%d,%.17g,%d,%.17g,%.17g,%.17g,%.17g]", i ? "," : "", it.iteration, it.cost,
+             it.step_is_successful ? 1 : 0, it.relative_decrease, it.trust_region_radius, it.step_norm,
+             it.gradient_max_norm);
     o << buf;
   }
   char buf[400];
@@ -321,6 +345,9 @@ int main(int argc, char** argv) {
   json_array(o, pf.data(), pf.size());
   o << ",\"rho\":";
   json_array(o, rho.data(), rho.size());
+  o << ",\"intrinsics\":";
+  json_array(o, intr.data(), intr.size());
+  o << ",\"refused_intrinsics\":" << (ev && ev->refused_intrinsics() ? 1 : 0);
   o << "}\n";
   FILE* g = fopen(argv[3], "w");
   if (!g) return 4;

@@ -39,8 +39,12 @@ def test_adapter_compiles_against_ceres_interface():
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("pose_param", ["ref", "tangent"])
 @pytest.mark.parametrize("kind,model", [(0, 0), (0, 1), (1, 0), (1, 1)])
-def test_adapter_records_match_oracle(kind, model):
+def test_adapter_records_match_oracle(kind, model, pose_param):
+    """pose_param "ref": the adapter's 7-wide Jacobians J6·P⁺ composed with the reference LocalParameterizationSE3's
+    Jacobian (Sophus Dx_this_mul_exp_x_at_0) give back the oracle's tangent records; "tangent": [J6 | 0] with
+    SE3TangentParameterization's [I₆; 0]."""
     sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
     from make_golden import write_problem
     pb = synth.make_problem(kind=kind, model=model, n_frames=8, n_points=100, width=376, height=240, seed=61,
@@ -50,7 +54,7 @@ def test_adapter_records_match_oracle(kind, model):
         fin, fout = os.path.join(td, "in.bin"), os.path.join(td, "out.bin")
         with open(fin, "wb") as f:
             write_problem(f, pb)
-        subprocess.run([exe, fin, fout], check=True)
+        subprocess.run([exe, fin, fout, pose_param], check=True)
         raw = np.fromfile(fout, np.uint8)
     R, nb = pb.R, pb.n_blocks
     o = 0
@@ -58,7 +62,10 @@ def test_adapter_records_match_oracle(kind, model):
     valid = raw[o:o + nb]; o += nb
     ronly = raw[o:o + 8 * nb * R].view(np.float64).reshape(nb, R); o += 8 * nb * R
     valid_r = raw[o:o + nb]; o += nb
-    plus = raw[o:o + 56].view(np.float64)
+    plus = raw[o:o + 56].view(np.float64); o += 56
+    P0 = raw[o:o + 8 * 42].view(np.float64).reshape(7, 6)
+    if pose_param == "ref":  # the adapter's restated Sophus plus-Jacobian against the oracle's (pinned by Sophus)
+        np.testing.assert_allclose(P0, O.se3_plus_jacobian(pb.poses[0]).reshape(7, 6), atol=1e-15)
     ref, vref = O.evaluate(pb)
     compare_records(kind, R, rec.astype(np.float32), ref, valid, vref, projected_uv(pb) if kind == 0 else None)
     assert np.array_equal(valid_r, vref)

@@ -88,14 +88,85 @@ def test_c1_engine_lm_matches_ceres_cpu(c1):
 
 
 @needs_ceres
-def test_c1_ceres_dropin_matches_ceres_cpu(c1):
-    """The north star's drop-in: the same ceres::Solve with the GPU EvaluationCallback + per-block CostFunctions."""
+@pytest.mark.parametrize("pose_param", ["ref", "tangent"])
+def test_c1_ceres_dropin_matches_ceres_cpu(c1, pose_param):
+    """The north star's drop-in: the same ceres::Solve with the GPU EvaluationCallback + per-block CostFunctions.
+    "ref": bundle_adjustment()'s own Sophus::test::LocalParameterizationSE3 stays registered (map_utils.h:331-333; the
+    adapter emits J7 = J6·P⁺); "tangent": the adapter's SE3TangentParameterization."""
     ref = CR.run("cpu", c1, iters=20, huber=1.0, threads=THREADS)
-    got = CR.run("gpu", c1, iters=20, huber=1.0, threads=THREADS)
+    got = CR.run("gpu", c1, iters=20, huber=1.0, threads=THREADS, pose_param=pose_param)
     assert got["protocol"]["violations"] == 0, got["protocol"]
     assert_same_trajectory(got, ref)
     np.testing.assert_allclose(got["poses"][:, 4:], ref["poses"][:, 4:], atol=1e-5)
     np.testing.assert_allclose(got["rho"], ref["rho"], rtol=1e-4, atol=1e-4 * np.abs(ref["rho"]).max())
+
+
+@needs_ceres
+def test_c1_ceres_dropin_optimize_intrinsics(c1):
+    """BundleAdjustmentOptions::optimize_intrinsics (map_utils.h:339-345): the cameras' intrinsics blocks are free, the
+    functor differentiates the TARGET camera's intrinsics (reprojection.h:83-86, :108) and unprojects the host pixel with
+    the intrinsics captured at problem build.  Real Ceres over the GPU adapter (target-intrinsics Jacobian from the
+    engine) takes the CPU AutoDiff run's accept/reject sequence, costs to 1e-5, and moves the intrinsics the same way."""
+    pb = synth.Problem(**{**c1.__dict__, "intrinsics": c1.intrinsics * np.array([1.002, 0.998, 1.0, 1.0, 1, 1, 1, 1])})
+    ref = CR.run("cpu", pb, iters=20, huber=1.0, threads=THREADS, optimize_intrinsics=1)
+    got = CR.run("gpu", pb, iters=20, huber=1.0, threads=THREADS, optimize_intrinsics=1)
+    assert got["protocol"]["violations"] == 0, got["protocol"]
+    assert_same_trajectory(got, ref)
+    moved = np.abs(ref["intrinsics"] - pb.intrinsics).max()
+    assert moved > 1e-3, moved  # the intrinsics are optimised, not held
+    np.testing.assert_allclose(got["intrinsics"], ref["intrinsics"], rtol=0, atol=1e-4 * moved + 1e-9)
+    np.testing.assert_allclose(got["poses"][:, 4:], ref["poses"][:, 4:], atol=1e-5)
+
+
+@needs_ceres
+def test_c1_free_intrinsics_without_engine_support_is_refused(c1):
+    """Free intrinsics blocks with an evaluator that was not given them: the adapter refuses the Jacobian request
+    (Evaluate returns false) and Ceres ends with FAILURE, instead of optimising with a zero intrinsics gradient."""
+    got = CR.run("gpu", c1, iters=5, huber=1.0, threads=THREADS, optimize_intrinsics=2)
+    assert got["refused_intrinsics"] == 1
+    assert got["termination"] == 2, got["message"]  # ceres::FAILURE
+    assert not (got["step_ok"][1:]).any()
+
+
+def _pick_threshold(values, earlier_ratio):
+    """first index k ≥ 1 whose value is below every earlier one by the given factor"""
+    for k in range(1, len(values)):
+        if np.isfinite(values[k]) and values[k] * earlier_ratio < np.min(values[:k]):
+            return k
+    return None
+
+
+@needs_ceres
+def test_c1_engine_lm_stops_like_ceres_on_parameter_and_gradient_tolerance(c1):
+    """pba_solve's ParameterToleranceReached / GradientToleranceReached (trust_region_minimizer.cc:668-728) against
+    real Ceres LM on the CPU path: tolerances chosen from Ceres' own per-iteration step and gradient norms (margin
+    ≥ 1.5×), then both solvers must stop by the same test with the same step counts and final cost."""
+    base = CR.run("cpu", c1, iters=20, huber=1.0, threads=THREADS, ptol=0.0, gtol=0.0, ftol=0.0)
+    x_norm = np.sqrt((base["poses"][2:] ** 2).sum() + (base["rho"] ** 2).sum())
+    ok = base["step_ok"]
+    # parameter tolerance: valid steps (accepted or not; step_norm > 0) after the first accepted one (x_norm is −1
+    # before it)
+    first = 1 + int(np.argmax(ok[1:]))
+    sn = base["step_norm"][first + 1:]
+    ratios = sn[sn > 0] / x_norm
+    k = _pick_threshold(ratios, 1.5)
+    assert k is not None, ratios
+    ptol = 1.2 * ratios[k]
+    gn = np.where(ok, base["gradient_max_norm"], np.inf)
+    kg = _pick_threshold(gn, 2.0)
+    assert kg is not None, gn
+    gtol = 1.4 * gn[kg]
+    for name, kw, reason in (("ptol", {"ptol": ptol}, "parameter_tolerance"),
+                             ("gtol", {"gtol": gtol}, "gradient_tolerance")):
+        ref = CR.run("cpu", c1, iters=20, huber=1.0, threads=THREADS, **kw)
+        assert ref["termination"] == 0 and reason.split("_")[0] in ref["message"].lower(), (name, ref["message"])
+        opts = {"parameter_tolerance": ptol} if name == "ptol" else {"gradient_tolerance": gtol}
+        with make_engine(c1, 1.0) as eng:
+            s = eng.solve(max_iterations=20, **opts)
+        assert s["stop_reason"] == reason, (name, s, ref["message"])
+        assert s["successful_steps"] == ref["successful_steps"] - 1, (name, s, ref["message"])
+        assert s["unsuccessful_steps"] == ref["unsuccessful_steps"], (name, s)
+        assert abs(s["final_cost"] - ref["final_cost"]) <= 1e-5 * ref["final_cost"], (name, s, ref["final_cost"])
 
 
 # ---------------------------------------------------------------------------------------------------- C2

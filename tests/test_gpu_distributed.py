@@ -131,6 +131,131 @@ def test_solve_distributed_matches_solve(kind, model, huber):
             e.close()
 
 
+def run_ranks(fn, world, timeout=600):
+    res, errs = [None] * world, []
+
+    def run(r):
+        try:
+            res[r] = fn(r)
+        except BaseException as ex:  # noqa: BLE001 (reported below)
+            errs.append(ex)
+
+    th = [threading.Thread(target=run, args=(r,)) for r in range(world)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout)
+    assert not any(t.is_alive() for t in th), "rank thread hung"
+    assert not errs, errs
+    return res
+
+
+def check_same_solve(pb, sh, res, ref, poses_ref, rho_ref, cost_rtol=1e-6, pose_atol=1e-6):
+    rho = np.zeros(pb.n_points)
+    for r, (e, pids) in enumerate(sh):
+        s = res[r]
+        for k in ("iterations", "successful_steps", "unsuccessful_steps", "termination", "stop_reason"):
+            assert s[k] == ref[k], (k, s, ref)
+        assert abs(s["initial_cost"] - ref["initial_cost"]) <= 1e-8 * ref["initial_cost"]
+        assert abs(s["final_cost"] - ref["final_cost"]) <= cost_rtol * ref["final_cost"], (s, ref)
+        poses, rr = e.get_state()
+        np.testing.assert_allclose(poses, poses_ref, atol=pose_atol)
+        rho[pids] = rr
+    np.testing.assert_allclose(rho, rho_ref, rtol=1e-6, atol=1e-9 * np.abs(rho_ref).max())
+
+
+@pytest.mark.parametrize("kind,model,huber", [(0, 0, 9.0), (1, 0, 1.0)])
+def test_solve_distributed_comm_local_group_matches_solve(kind, model, huber):
+    """The stream-ordered loop (pba_solve_distributed_comm): three shard engines in three threads over an in-process
+    pba_comm group — both sums of every trial enqueued on the engine streams, the next trial enqueued ahead of the
+    decision — take pba_solve's trajectory."""
+    pb = synth.make_problem(kind=kind, model=model, n_frames=16, n_points=400, width=376, height=240, seed=81,
+                            border=12, obs_sigma=0.3)
+    pb.poses[:2] = pb.poses_gt[:2]
+    fixed = (0, 1)
+    with engine_for(pb, huber, fixed) as full:
+        ref = full.solve(max_iterations=12)
+        poses_ref, rho_ref = full.get_state()
+    world = 3
+    sh = shards(pb, world, huber, fixed)
+    comms = E.Comm.local_group(world)
+    try:
+        band = max(e.gn_band() for e, _ in sh)
+        res = run_ranks(lambda r: sh[r][0].solve_distributed_comm(band, comms[r], max_iterations=12), world)
+        check_same_solve(pb, sh, res, ref, poses_ref, rho_ref)
+        assert ref["final_cost"] < ref["initial_cost"]
+    finally:
+        for c in comms:
+            c.close()
+        for e, _ in sh:
+            e.close()
+
+
+def test_solve_distributed_rccl_single_rank_matches_solve():
+    """RCCL itself (librccl through pba_comm_init, one rank on this GPU — two ranks cannot share a device under
+    RCCL): ncclAllReduce on the engine stream inside the device-steered loop gives pba_solve's trajectory."""
+    pb = synth.make_problem(kind=0, n_frames=16, n_points=400, width=376, height=240, seed=85, border=12)
+    pb.poses[:2] = pb.poses_gt[:2]
+    with engine_for(pb, 9.0, (0, 1)) as full:
+        ref = full.solve(max_iterations=10)
+        poses_ref, rho_ref = full.get_state()
+    comm = E.Comm.rccl(E.Comm.unique_id(), 1, 0, 0)
+    try:
+        assert comm.rank == 0 and comm.size == 1
+        with engine_for(pb, 9.0, (0, 1)) as e:
+            s = e.solve_distributed_comm(e.gn_band(), comm, max_iterations=10)
+            check_same_solve(pb, [(e, np.arange(pb.n_points))], [s], ref, poses_ref, rho_ref)
+    finally:
+        comm.close()
+
+
+def test_c4_eight_shard_rehearsal_matches_solve():
+    """The 8-GPU split of the C4 problem rehearsed on one GPU: the full 1000-keyframe × 100k-point problem (rendered
+    images) sharded by host keyframe over 8 engines, one thread each, summed through an in-process pba_comm group with
+    the stream-ordered device-steered loop.  Same LM trajectory as pba_solve on the whole problem."""
+    import time
+
+    import torch
+    pb, images = synth.c4_shard(torch.device("cuda", 0), texture="render")
+    fixed = (0, 1)
+    iters = 4
+
+    def engine_c4(p):
+        eng = E.Engine(0, 0, huber_width=9.0)
+        eng.set_problem(p, images_device_ptr=images.data_ptr())
+        eng.set_fixed_frames(np.array(fixed, np.int32))
+        eng.set_state(p.poses, p.rho)
+        return eng
+
+    with engine_c4(pb) as full:
+        full.solve(max_iterations=1)  # warm-up (prepare)
+        full.set_state(pb.poses, pb.rho)
+        ref = full.solve(max_iterations=iters)
+        poses_ref, rho_ref = full.get_state()
+    world = 8
+    sh = []
+    for r in range(world):
+        sub, pids, _ = D.shard_problem(pb, world, r)
+        sh.append((engine_c4(sub), pids))
+    comms = E.Comm.local_group(world)
+    try:
+        band = max(e.gn_band() for e, _ in sh)
+        run_ranks(lambda r: sh[r][0].solve_distributed_comm(band, comms[r], max_iterations=1), world)  # warm-up
+        for r, (e, pids) in enumerate(sh):
+            e.set_state(pb.poses, pb.rho[pids])
+        t0 = time.perf_counter()
+        res = run_ranks(lambda r: sh[r][0].solve_distributed_comm(band, comms[r], max_iterations=iters), world)
+        wall = time.perf_counter() - t0
+        check_same_solve(pb, sh, res, ref, poses_ref, rho_ref, cost_rtol=1e-6, pose_atol=1e-6)
+        print(f"\nC4 8-shard rehearsal on one GPU: {res[0]['iterations']} iterations, {1e3 * wall / iters:.3f} ms per "
+              f"iteration (one engine: {ref['total_ms'] / max(ref['iterations'], 1):.3f} ms)")
+    finally:
+        for c in comms:
+            c.close()
+        for e, _ in sh:
+            e.close()
+
+
 @pytest.mark.parametrize("kind,huber", [(0, 9.0), (1, 1.0)])
 def test_two_process_gloo_solve_matches_solve(kind, huber):
     """Two processes, one engine each (both on cuda:0), a world-size-2 gloo group: distributed.solve_distributed
@@ -190,7 +315,7 @@ def test_band_too_small_is_rejected():
         with pytest.raises(E.PbaError, match="band"):
             e.gn_exchange_size(b - 1)
         n = e.gn_exchange_size(b)
-        assert n == 12 * ((E_band(b) + 1) * 36 + 24) + 8
+        assert n == 12 * ((E_band(b) + 1) * 36 + 24) + 8  # banded rows + the 8 point-part scalars of a trial
 
 
 def E_band(b):
