@@ -363,8 +363,9 @@ def test_c3_reduced_system_and_step_against_fp64_reference(c3, lam):
     """At full C3 size: the device's reduced camera system S and right-hand side g_S (fp32 JᵀJ block products summed
     in fp64, point elimination and assembly in fp64) against the fp64 system built block-sparsely from the oracle's
     Jacobians (gn_reference.reduced_system_sparse, the schur_complement_solver.cc:138-146 quantities), and the step
-    against the dense fp64 solve of the reference system.  Measured at λ = 1e-4: S 1.3e-7, g 3.6e-8 of their scale,
-    step 6e-7 relative (profiles/r3_gpu_tests_*); bounds 1e-6 / 1e-6 / 1e-5."""
+    against the dense fp64 solve of the reference system.  Measured (MI355X): S 7.7e-8 and g 5.5e-8 of their scale at
+    both λ; the step 3.2e-5 relative at λ = 1e-4 (the weakly damped reduced system amplifies the fp32 products'
+    rounding) and 2.0e-7 at λ = 0.1; the cost 1.5e-8.  Bounds: 1e-6 (cost, S, g), 1e-4 (step)."""
     fixed = (0, 1)
     S_ref, g_ref, c_ref = GR.reduced_system_sparse(c3, c3.poses, c3.rho, 9.0, lam, fixed)
     dp_ref = np.linalg.solve(S_ref, -g_ref)
@@ -379,8 +380,8 @@ def test_c3_reduced_system_and_step_against_fp64_reference(c3, lam):
     ep = np.linalg.norm(dp.ravel() - dp_ref) / np.linalg.norm(dp_ref)
     print(f"\nC3 λ={lam}: cost {abs(c - c_ref) / c_ref:.2e}, S {eS:.2e}, g {eg:.2e}, step {ep:.2e}")
     assert abs(c - c_ref) <= 1e-6 * c_ref
-    assert eS <= 1e-5, eS
-    assert eg <= 1e-5, eg
+    assert eS <= 1e-6, eS
+    assert eg <= 1e-6, eg
     assert ep <= 1e-4, ep
 
 

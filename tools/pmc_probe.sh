@@ -12,7 +12,7 @@ while read -r GROUP; do
   [ -z "$GROUP" ] && continue
   i=$((i + 1))
   timeout -s KILL 90 rocprofv3 --pmc $GROUP --kernel-include-regex "${KREGEX:-photometric_block_kernel}" \
-      --output-format csv -d gpurun_out/pmc_${TAG}_$i -o run -- python bench.py $ARGS > gpurun_out/pmc_${TAG}_$i.log 2>&1
+      --output-format csv -d gpurun_out/pmc_${TAG}_$i -o run -- python ${SCRIPT:-bench.py} $ARGS > gpurun_out/pmc_${TAG}_$i.log 2>&1
   rc=$?; echo "pass $i ($GROUP) rc=$rc"; [ $rc -eq 0 ] || exit $rc
 done <<< "${GROUPS_LIST:-SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES
 SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_SCA SQ_WAIT_INST_ANY SQ_WAIT_ANY GRBM_GUI_ACTIVE GRBM_COUNT}"
