@@ -1272,12 +1272,25 @@ __global__ __launch_bounds__(2 * kCrOddThreads<M>) void cr_level_kernel(CrLevel 
 #endif
 constexpr int kCrPivot = PBA_CR_PIVOT;  // columns per Gauss-Jordan step of gj_wave (1, 2, 4 or 8; divides M)
 
+// Loads / stores of the rows handed between workgroups of pcr_fused_kernel (COH): `sc1` (L1-bypassing, write-through)
+// agent-scope accesses, the hand-off form of MI355X_MICROARCH.md's first table row; plain otherwise.
+template <bool COH>
+__device__ __forceinline__ double ld_row(const double* p) {
+  if constexpr (COH) return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else return *p;
+}
+template <bool COH>
+__device__ __forceinline__ void st_row(double* p, double v) {
+  if constexpr (COH) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else *p = v;
+}
+
 // Pivot blocks of PB columns: lanes k … k+PB−1 publish their columns to the wave's LDS buffer (row r: PB doubles),
 // every lane reads the PB×PB pivot block P and solves P t = a[k … k+PB−1] in registers (unpivoted Gauss-Jordan:
 // D is SPD, so is every pivot block; all of P's pivots must be positive), then updates its other rows
 // a[r] −= Σ_j piv[r][j] t_j.  The publish / read round trip is paid M/PB times instead of M/2 times; the updates are
 // the same FMAs.
-template <int M, int PB = kCrPivot>
+template <int M, bool COH = false, int PB = kCrPivot>
 __device__ __forceinline__ bool gj_wave(const double* __restrict__ D, const double* __restrict__ R1, bool r1_trans,
                                         const double* __restrict__ b, int ncol, int c, double* piv, double* a) {
   static_assert(M % PB == 0, "pivot blocks tile the system");
@@ -1302,7 +1315,7 @@ __device__ __forceinline__ bool gj_wave(const double* __restrict__ D, const doub
     }
   }
 #pragma unroll
-  for (int r = 0; r < M; ++r) a[r] = base[r * stride];
+  for (int r = 0; r < M; ++r) a[r] = ld_row<COH>(base + r * stride);
 #pragma unroll
   for (int r = 0; r < M; ++r) a[r] = zero ? 0.0 : a[r];
   bool bad = false;
@@ -1366,6 +1379,91 @@ __device__ __forceinline__ bool gj_wave(const double* __restrict__ D, const doub
 }
 
 
+// Rebuild of super-row i (next-level index in) from the two eliminations in LDS (sXl = X_{i−1}, sXr = X_{i+1}) and
+// U_{i−1}, U_i, D_i, b_i, on RB waves: 4 waves take two column tiles each, 8 waves one.  keep_u: the rebuilt row
+// still has a right coupling.  Waves w ≥ RB return at once.
+template <int M, int RB, bool COH = false>
+__device__ __forceinline__ void cr_rebuild(int w, int lane, const double* sUl, const double* sUi, const double* sD,
+                                           const double* sb, const double* sXl, const double* sXr, const CrLevel& Ln,
+                                           int in, bool keep_u) {
+  constexpr int NC = 2 * M + 1;
+  // Rebuild of row i on the matrix cores: [D' | U' | b'] = [D | 0 | b] − U_{i−1}ᵀ·[X^U_{i−1} | 0 | X^b_{i−1}]
+  // − U_i·X_{i+1}, as 2 × 4 output tiles of v_mfma_f64_16x16x4f64 (rows padded to 32, columns to 64).  Wave w takes
+  // row tile w & 1 and column tiles TPW·(w >> 1) + {0 … TPW−1}: a wave's tiles share the A operands and run as
+  // independent accumulator chains.  Layouts (tools/micro/mfma_f64_layout.hip): A lane l = (row l%16, k l/16),
+  // B lane l = (k l/16, column l%16), accumulator entry v of lane l = (row l/16 + 4v, column l%16).
+  // 3.9 → 2.7 µs per level against the scalar LDS products (tools/micro/cr_level_timing.hip, V5).
+  static_assert(M % 4 == 0 && M <= 32, "K steps of 4, two row tiles");
+  static_assert(RB == 4 || RB == 8, "2 × 4 tiles over the rebuild waves");
+  constexpr int TPW = 8 / RB;  // column tiles per wave
+  if (w >= RB) return;
+  const int rt = w & 1;
+  const int arow = 16 * rt + (lane & 15), kq = lane >> 4;
+  // every operand of the six K steps read from LDS first, at clamped (in-range) indices and with unconditional reads,
+  // then the padding zeroed by selects: conditional reads were issued and waited one at a time (~2.9 µs per level)
+  constexpr int KS = M / 4;
+  const bool aok = arow < M;
+  const int ar = aok ? arow : 0;
+  int bcol[TPW];
+  double av2[KS], av1[KS], bv2[TPW][KS], bv1[TPW][KS], cv[TPW][4];
+#pragma unroll
+  for (int h = 0; h < TPW; ++h) {
+    bcol[h] = 16 * ((w >> 1) * TPW + h) + (lane & 15);
+    const int c = bcol[h];
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      const int r = 16 * rt + (lane >> 4) + 4 * v;
+      cv[h][v] = c < M ? sD[min(r, M - 1) * M + c] : sb[min(r, M - 1)];
+    }
+  }
+#pragma unroll
+  for (int s4 = 0; s4 < KS; ++s4) {
+    const int q = 4 * s4 + kq;
+    av2[s4] = sUi[ar * M + q];
+    av1[s4] = sUl[q * M + ar];
+#pragma unroll
+    for (int h = 0; h < TPW; ++h) {
+      const int c = bcol[h];
+      bv2[h][s4] = sXr[q * NC + min(c, NC - 1)];
+      bv1[h][s4] = sXl[q * NC + (c < M ? M + c : 2 * M)];
+    }
+  }
+  v4f64 acc[TPW];
+#pragma unroll
+  for (int h = 0; h < TPW; ++h) {
+    const int c = bcol[h];
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      const int r = 16 * rt + (lane >> 4) + 4 * v;
+      acc[h][v] = (r < M && (c < M || c == 2 * M)) ? cv[h][v] : 0.0;
+    }
+  }
+#pragma unroll
+  for (int s4 = 0; s4 < KS; ++s4) {
+    const double a2 = aok ? -av2[s4] : 0.0;
+    const double a1 = aok ? -av1[s4] : 0.0;
+#pragma unroll
+    for (int h = 0; h < TPW; ++h) {
+      const int c = bcol[h];
+      const double b2 = c < NC ? bv2[h][s4] : 0.0;
+      const double b1 = (c < M || c == 2 * M) ? bv1[h][s4] : 0.0;
+      acc[h] = __builtin_amdgcn_mfma_f64_16x16x4f64(a2, b2, acc[h], 0, 0, 0);
+      acc[h] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1, acc[h], 0, 0, 0);
+    }
+  }
+#pragma unroll
+  for (int h = 0; h < TPW; ++h)
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      const int r = 16 * rt + (lane >> 4) + 4 * v, c = bcol[h];
+      if (r < M) {
+        if (c < M) st_row<COH>(Ln.D + (long long)in * M * M + r * M + c, acc[h][v]);
+        else if (c < 2 * M) st_row<COH>(Ln.U + (long long)in * M * M + r * M + (c - M), keep_u ? acc[h][v] : 0.0);
+        else if (c == 2 * M) st_row<COH>(Ln.b + (long long)in * M + r, acc[h][v]);
+      }
+    }
+}
+
 template <int M>
 constexpr size_t cr_level_wave_lds() { return sizeof(double) * (3 * M * M + M + 2 * M * (2 * M + 1)); }
 
@@ -1379,20 +1477,18 @@ constexpr size_t cr_level_wave_lds() { return sizeof(double) * (3 * M * M + M + 
 //       gone and x_i = D_i⁻¹ b_i (pcr_solve_kernel): no back-substitution.  A PCR level runs twice the workgroups of a
 //       CR level at the same per-workgroup latency, so it is used while the rows fit one workgroup per CU.
 // The D_i' are Schur complements of SPD principal submatrices ({l, i, r}), so every pivot block stays SPD.
-template <int M, bool PCR>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void cr_level_wave_kernel(
-    CrLevel L, CrLevel Ln, int s, int* status) {
+// The level's work for row i (rebuilt as row `in` of Ln) by a 4-wave workgroup: piv = 3 × M·kCrPivot doubles, smem =
+// cr_level_wave_lds<M>() bytes.  COH: rows read and written with the hand-off accesses of pcr_fused_kernel.
+template <int M, bool PCR, bool COH>
+__device__ __forceinline__ void cr_wave_level(const CrLevel& L, const CrLevel& Ln, int i, int in, int s, int* status,
+                                              double (*piv)[M * kCrPivot], double* smem) {
   static_assert(2 * M + 1 <= 64, "one wave per elimination");
   constexpr int NC = 2 * M + 1;
-  __shared__ __attribute__((aligned(16))) double piv[3][M * kCrPivot];
-  extern __shared__ double smem[];
   double* sUl = smem;
   double* sUi = sUl + M * M;
   double* sD = sUi + M * M;
   double* sb = sD + M * M;
   double* sX[2] = {sb + M, sb + M + M * NC};
-  const int i = PCR ? (int)blockIdx.x : 2 * (int)blockIdx.x, in = blockIdx.x;
-  if (!PCR) s = 1;
   const int il = i - s, ir = i + s;
   const bool left = il >= 0, right = ir < L.n;
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -1412,7 +1508,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       else if (e < 2 * M * M) src = L.U + (long long)i * M * M + (e - M * M);
       else if (e < 3 * M * M) src = L.D + (long long)i * M * M + (e - 2 * M * M);
       else if (e < NE) src = L.b + (long long)i * M + (e - 3 * M * M);
-      v[q] = *src;
+      v[q] = ld_row<COH>(src);
     }
 #pragma unroll
     for (int q = 0; q < NQ; ++q) {
@@ -1428,9 +1524,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     const double* bj = L.b + (long long)jj * M;
     double a[M];
     bool ok;
-    if (w == 0) ok = gj_wave<M>(D, L.U + (long long)jj * M * M, false, bj, M + 1, lane, piv[0], a);
-    else if (w == 1) ok = gj_wave<M>(D, L.U + (long long)i * M * M, true, bj, M + 1, lane, piv[1], a);
-    else ok = gj_wave<M>(D, jj + s < L.n ? L.U + (long long)jj * M * M : nullptr, false, nullptr, M, lane, piv[2], a);
+    if (w == 0) ok = gj_wave<M, COH>(D, L.U + (long long)jj * M * M, false, bj, M + 1, lane, piv[0], a);
+    else if (w == 1) ok = gj_wave<M, COH>(D, L.U + (long long)i * M * M, true, bj, M + 1, lane, piv[1], a);
+    else ok = gj_wave<M, COH>(D, jj + s < L.n ? L.U + (long long)jj * M * M : nullptr, false, nullptr, M, lane, piv[2], a);
     if (!ok && has && lane == 0) atomicOr(status, 1);
     if (lane >= M && lane < 2 * M + (w == 2 ? 0 : 1)) {
       const int col = lane < 2 * M ? (w == 1 ? lane - M : lane) : 2 * M;
@@ -1451,80 +1547,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 #ifdef PBA_CR_STAMPS
   t2 = wall_clock64();
 #endif
-  // Rebuild of row i on the matrix cores: [D' | U' | b'] = [D | 0 | b] − U_{i−1}ᵀ·[X^U_{i−1} | 0 | X^b_{i−1}]
-  // − U_i·X_{i+1}, as 2 × 4 output tiles of v_mfma_f64_16x16x4f64 (rows padded to 32, columns to 64).  Wave w takes
-  // row tile w & 1 and column tiles 2(w >> 1) + {0, 1}: the two tiles share the A operands and run as two
-  // independent accumulator chains.  Layouts (tools/micro/mfma_f64_layout.hip): A lane l = (row l%16, k l/16),
-  // B lane l = (k l/16, column l%16), accumulator entry v of lane l = (row l/16 + 4v, column l%16).
-  // 3.9 → 2.7 µs per level against the scalar LDS products (tools/micro/cr_level_timing.hip, V5).
-  static_assert(M % 4 == 0 && M <= 32, "K steps of 4, two row tiles");
-  const double* sXl = sX[0];
-  const double* sXr = sX[1];
-  const int rt = w & 1;
-  const int arow = 16 * rt + (lane & 15), kq = lane >> 4;
-  // every operand of the six K steps read from LDS first, at clamped (in-range) indices and with unconditional reads,
-  // then the padding zeroed by selects: conditional reads were issued and waited one at a time (~2.9 µs per level)
-  constexpr int KS = M / 4;
-  const bool aok = arow < M;
-  const int ar = aok ? arow : 0;
-  int bcol[2];
-  double av2[KS], av1[KS], bv2[2][KS], bv1[2][KS], cv[2][4];
-#pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    bcol[h] = 16 * ((w >> 1) * 2 + h) + (lane & 15);
-    const int c = bcol[h];
-#pragma unroll
-    for (int v = 0; v < 4; ++v) {
-      const int r = 16 * rt + (lane >> 4) + 4 * v;
-      cv[h][v] = c < M ? sD[min(r, M - 1) * M + c] : sb[min(r, M - 1)];
-    }
-  }
-#pragma unroll
-  for (int s4 = 0; s4 < KS; ++s4) {
-    const int q = 4 * s4 + kq;
-    av2[s4] = sUi[ar * M + q];
-    av1[s4] = sUl[q * M + ar];
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int c = bcol[h];
-      bv2[h][s4] = sXr[q * NC + min(c, NC - 1)];
-      bv1[h][s4] = sXl[q * NC + (c < M ? M + c : 2 * M)];
-    }
-  }
-  v4f64 acc[2];
-#pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    const int c = bcol[h];
-#pragma unroll
-    for (int v = 0; v < 4; ++v) {
-      const int r = 16 * rt + (lane >> 4) + 4 * v;
-      acc[h][v] = (r < M && (c < M || c == 2 * M)) ? cv[h][v] : 0.0;
-    }
-  }
-#pragma unroll
-  for (int s4 = 0; s4 < KS; ++s4) {
-    const double a2 = aok ? -av2[s4] : 0.0;
-    const double a1 = aok ? -av1[s4] : 0.0;
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int c = bcol[h];
-      const double b2 = c < NC ? bv2[h][s4] : 0.0;
-      const double b1 = (c < M || c == 2 * M) ? bv1[h][s4] : 0.0;
-      acc[h] = __builtin_amdgcn_mfma_f64_16x16x4f64(a2, b2, acc[h], 0, 0, 0);
-      acc[h] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1, acc[h], 0, 0, 0);
-    }
-  }
-#pragma unroll
-  for (int h = 0; h < 2; ++h)
-#pragma unroll
-    for (int v = 0; v < 4; ++v) {
-      const int r = 16 * rt + (lane >> 4) + 4 * v, c = bcol[h];
-      if (r < M) {
-        if (c < M) Ln.D[(long long)in * M * M + r * M + c] = acc[h][v];
-        else if (c < 2 * M) Ln.U[(long long)in * M * M + r * M + (c - M)] = (PCR ? i + 2 * s < L.n : right) ? acc[h][v] : 0.0;
-        else if (c == 2 * M) Ln.b[(long long)in * M + r] = acc[h][v];
-      }
-    }
+  cr_rebuild<M, 4, COH>(w, lane, sUl, sUi, sD, sb, sX[0], sX[1], Ln, in, PCR ? i + 2 * s < L.n : right);
 #ifdef PBA_CR_STAMPS
   __syncthreads();
   const long long t3 = wall_clock64();
@@ -1532,6 +1555,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     printf("crstamp s=%d w=%d phase_end_us %.2f barrier_us %.2f rebuild_us %.2f\n", s, w, (t1 - t0) * 0.01,
            (t2 - t0) * 0.01, (t3 - t0) * 0.01);
 #endif
+}
+
+template <int M, bool PCR>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void cr_level_wave_kernel(
+    CrLevel L, CrLevel Ln, int s, int* status) {
+  __shared__ __attribute__((aligned(16))) double piv[3][M * kCrPivot];
+  extern __shared__ double smem[];
+  const int i = PCR ? (int)blockIdx.x : 2 * (int)blockIdx.x;
+  cr_wave_level<M, PCR, false>(L, Ln, i, blockIdx.x, PCR ? s : 1, status, piv, smem);
 }
 
 // The root super-row on one wave (lane 2M carries b; the coupling lanes are empty).
@@ -1566,6 +1598,95 @@ __global__ __launch_bounds__(64) void pcr_solve_kernel(CrLevel L, double* __rest
 #pragma unroll
     for (int r = 0; r < M; ++r)
       if (i * M + r < lim) out[(long long)i * M + r] = a[r];
+}
+
+// ---- parallel cyclic reduction in one launch ---------------------------------------------------------------------
+// All PCR levels and the final x_i = D_i⁻¹ b_i as tasks (l, i) of ONE launch, synchronised by data flow instead of
+// launch boundaries: task (l, i) (l < n_levels, stride s = 2^l) waits for rows i − s, i, i + s of level l, runs
+// cr_wave_level into level l + 1 (each level its own buffer: a row is read by tasks that no later writer waits for)
+// and publishes row i of level l + 1 with a ready flag; task (n_levels, i) solves row i.  One workgroup per task,
+// each taking the next task number from a device counter when it starts, so a task only ever waits for tasks taken
+// earlier by workgroups already resident: no deadlock whatever the residency (another engine's kernels on the same
+// device, more tasks than CUs).  (A persistent loop over tasks spilled 200-400 B of registers per lane.)  Hand-off: rows stored `sc1` (write-through) by every wave, each storing wave's
+// vmcnt(0), a workgroup barrier, then ONE lane's `sc1` flag store; the consumer polls with `sc1` loads and its
+// waves read the rows with `sc1` loads after a workgroup barrier (MI355X_MICROARCH.md, the first row of the
+// hand-off table: hipMalloc memory, one workgroup per CU).  Flags hold the launch's epoch (no reset launch); the
+// counter runs on across launches (base = the tasks of the launches before).
+constexpr int kMaxPcrLevels = 16;
+struct PcrFusedArgs {
+  CrLevel lv0;                    // the level PCR starts from
+  double* lv;                     // level l ≥ 1 (after the stride-2^(l−1) level): D, U, b at lv + (l − 1)·(2nM² + nM)
+  int n_levels, n, lim, epoch;
+  double* out;
+  int* status;
+  int* flags;                     // (n_levels + 1) × n: row i of level l published in this launch ⇔ epoch
+  unsigned* counter;
+  unsigned base;
+};
+
+// Poll a ready flag (one lane).  A flag that never comes (a bug, a dead producer) ends the wait after 1 s with the
+// status flagged (the solve then reports a failed step), so the grid always drains.
+__device__ __forceinline__ void pcr_wait(const int* f, int epoch, int* status) {
+  const long long t0 = wall_clock64();
+  while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != epoch) {
+    __builtin_amdgcn_s_sleep(2);
+    if (wall_clock64() - t0 > 100000000ll) {  // 100 MHz constant clock
+      atomicOr(status, 2);
+      return;
+    }
+  }
+}
+
+template <int M>
+__device__ __forceinline__ CrLevel pcr_fused_level(const PcrFusedArgs& a, int l) {
+  if (l == 0) return a.lv0;
+  const long long nm2 = (long long)a.n * M * M;
+  double* base = a.lv + (long long)(l - 1) * (2 * nm2 + (long long)a.n * M);
+  return CrLevel{base, base + nm2, base + 2 * nm2, nullptr, nullptr, a.n};
+}
+
+template <int M>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void pcr_fused_kernel(const PcrFusedArgs a) {
+  __shared__ __attribute__((aligned(16))) double piv[3][M * kCrPivot];
+  extern __shared__ double smem[];
+  __shared__ unsigned s_task;
+  if (threadIdx.x == 0) s_task = atomicAdd(a.counter, 1u) - a.base;
+  __syncthreads();
+  const unsigned t = s_task;
+  if (t >= (unsigned)((a.n_levels + 1) * a.n)) return;  // (the grid is exactly the tasks)
+  const int l = (int)(t / (unsigned)a.n), i = (int)(t % (unsigned)a.n);
+  const int s = 1 << min(l, 30);
+  if (l < a.n_levels) {
+    if (l > 0 && threadIdx.x == 0) {
+      const int* f = a.flags + (long long)l * a.n;
+      pcr_wait(f + i, a.epoch, a.status);
+      if (i - s >= 0) pcr_wait(f + i - s, a.epoch, a.status);
+      if (i + s < a.n) pcr_wait(f + i + s, a.epoch, a.status);
+    }
+    __syncthreads();
+    cr_wave_level<M, true, true>(pcr_fused_level<M>(a, l), pcr_fused_level<M>(a, l + 1), i, i, s, a.status, piv, smem);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's row stores have completed
+    __syncthreads();
+    if (threadIdx.x == 0)
+      __hip_atomic_store(a.flags + (long long)(l + 1) * a.n + i, a.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return;
+  }
+  // the decoupled row: x_i = D_i⁻¹ b_i on wave 0 (lane 2M carries b)
+  if (threadIdx.x >= 64) return;
+  const int lane = threadIdx.x;
+  if (l > 0 && lane == 0) pcr_wait(a.flags + (long long)l * a.n + i, a.epoch, a.status);
+  __builtin_amdgcn_wave_barrier();
+  const CrLevel L = pcr_fused_level<M>(a, a.n_levels);
+  double x[M];
+  const bool ok = gj_wave<M, true>(L.D + (long long)i * M * M, nullptr, false, L.b + (long long)i * M, M + 1, lane, piv[0], x);
+  if (!ok) {
+    if (lane == 0) atomicOr(a.status, 1);
+    return;
+  }
+  if (lane == 2 * M)
+#pragma unroll
+    for (int r = 0; r < M; ++r)
+      if (i * M + r < a.lim) a.out[(long long)i * M + r] = x[r];
 }
 
 // The root super-row (the last level): x = D⁻¹ b.
@@ -1678,9 +1799,10 @@ __device__ void se3_exp_mul(const double* T, const double* d, double* out) {
 
 
 // Σ over the workgroup of N per-lane values and the max of one more, in a fixed order (xor butterflies in each wave,
-// then the waves in order, as wg_reduce2): thread 0 writes out[0..N) and *out_max.  Every thread must call it.
+// then the waves in order, as wg_reduce2): thread q < N stores sum q to *out[q], thread N the max to *out_max.  Every
+// thread must call it.
 template <int N>
-__device__ __forceinline__ void wg_reduce_sum_max(double (&v)[N], double m, double* out, double* out_max) {
+__device__ __forceinline__ void wg_reduce_sum_max(double (&v)[N], double m, double* const (&out)[N], double* out_max) {
   __shared__ double s[N + 1][16];
   for (int o = 32; o >= 1; o >>= 1) {
 #pragma unroll
@@ -1694,17 +1816,14 @@ __device__ __forceinline__ void wg_reduce_sum_max(double (&v)[N], double m, doub
     s[N][w] = m;
   }
   __syncthreads();
-  if (threadIdx.x == 0) {
-    const int nw = (int)(blockDim.x / 64);
-#pragma unroll
-    for (int q = 0; q < N; ++q) {
-      double x = 0.0;
-      for (int i = 0; i < nw; ++i) x += s[q][i];
-      out[q] = x;
-    }
+  if (threadIdx.x <= N) {  // one thread per sum, the waves in order
+    const int q = threadIdx.x, nw = (int)(blockDim.x / 64);
     double x = 0.0;
-    for (int i = 0; i < nw; ++i) x = fmax(x, s[N][i]);
-    *out_max = x;
+    for (int i = 0; i < nw; ++i) x = q < N ? x + s[q][i] : fmax(x, s[N][i]);
+    double* dst = out_max;
+#pragma unroll
+    for (int k = 0; k < N; ++k) dst = q == k ? out[k] : dst;
+    *dst = x;
   }
 }
 
@@ -1758,14 +1877,8 @@ __device__ __forceinline__ void pose_update_block(const PoseUpdateArgs& a, int b
       }
     }
   }
-  double s[4];
-  wg_reduce_sum_max<4>(v, gm, s, a.gmax + blk);
-  if (threadIdx.x == 0) {
-    a.red[2 * blk] = s[0];
-    a.red[2 * blk + 1] = s[1];
-    a.red2[2 * blk] = s[2];
-    a.red2[2 * blk + 1] = s[3];
-  }
+  double* const dst[4] = {a.red + 2 * blk, a.red + 2 * blk + 1, a.red2 + 2 * blk, a.red2 + 2 * blk + 1};
+  wg_reduce_sum_max<4>(v, gm, dst, a.gmax + blk);
 }
 
 struct PointUpdateArgs {
@@ -1831,14 +1944,8 @@ __device__ __forceinline__ void point_update_block(const PointUpdateArgs& a, dou
     v[3] = rn * rn;
     gm = fabs(gl);  // ρ has no local parameterisation: |ρ − (ρ − g_ρ)|
   }
-  double s[4];
-  wg_reduce_sum_max<4>(v, gm, s, a.gmax + slot);
-  if (threadIdx.x == 0) {
-    a.red[2 * slot] = s[0];
-    a.red[2 * slot + 1] = s[1];
-    a.red2[2 * slot] = s[2];
-    a.red2[2 * slot + 1] = s[3];
-  }
+  double* const dst[4] = {a.red + 2 * slot, a.red + 2 * slot + 1, a.red2 + 2 * slot, a.red2 + 2 * slot + 1};
+  wg_reduce_sum_max<4>(v, gm, dst, a.gmax + slot);
 }
 
 struct PairUpdateArgs {
@@ -1990,37 +2097,57 @@ __device__ void lm_decide(const double* t, int st, const DecideOpts& o, double* 
   lm[kLmDone] = done;
 }
 
-// The trial's sums from the update and cost partials (one workgroup: strided per-thread sums with U independent 16-B
-// loads in flight — the candidate cost alone has one slot per linearisation chunk, 12.5k at C4 — then xor butterflies
-// per wave and the waves in order: deterministic).  Slots: red [0, gp) poses, [gp, gp + gq) points (model decrease
-// parts), [gp + gq, gp + gq + gc) the candidate's (cost, valid); red2 / gmax [0, gp + gq) (update_kernel).  Thread 0
-// gets the totals in t.
+// The trial's sums from the update and cost partials (one workgroup; deterministic).  Slots: red [0, gp) poses,
+// [gp, gp + gq) points (model decrease parts), [gp + gq, gp + gq + gc) the candidate's (cost, valid) — one slot per
+// linearisation chunk, 12.5k at C4; red2 / gmax [0, gp + gq) (update_kernel).  The red2 / gmax slots one per
+// thread, then one strided pass over red with U slots per thread in flight, then xor butterflies per wave and the
+// waves in order (U loads of three arrays spilled 172 B per lane at 1024 threads: 16 µs per decision).  t: the
+// totals, in LDS.
 __device__ void trial_sums(const double* __restrict__ red, const double* __restrict__ red2,
                            const double* __restrict__ gmax, int gp, int gq, int gc, double* t) {
   constexpr int N = kDecideThreads, U = 8;
   __shared__ double part[kTsCount][N / 64];
   double v[kTsCount] = {};
-  auto range = [&](const double* src, int beg, int end, double& x, double& y) {
-    for (int i0 = beg + (int)threadIdx.x; i0 < end; i0 += U * N) {
-      double2 r[U];
+  const int S = gp + gq, E = S + gc;
+  const double2* r1 = reinterpret_cast<const double2*>(red);
+  const double2* r2 = reinterpret_cast<const double2*>(red2);
+  // the update slots' norms and gradient maxima: one slot per thread, loaded before the red pass so that both are
+  // in flight together (S ≤ N unless the problem has > 260k points: a tail loop then)
+  const int i_s = (int)threadIdx.x;
+  const double2 ys = i_s < S ? r2[i_s] : make_double2(0.0, 0.0);
+  const double ms = i_s < S ? gmax[i_s] : 0.0;
+  for (int i0 = (int)threadIdx.x; i0 < E; i0 += U * N) {
+    double2 x[U];
 #pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int i = i0 + u * N;
-        r[u] = i < end ? reinterpret_cast<const double2*>(src)[i] : make_double2(0.0, 0.0);
-      }
+    for (int u = 0; u < U; ++u) {
+      const int i = i0 + u * N;
+      x[u] = i < E ? r1[i] : make_double2(0.0, 0.0);
+    }
 #pragma unroll
-      for (int u = 0; u < U; ++u) { x += r[u].x; y += r[u].y; }
+    for (int u = 0; u < U; ++u) {  // selects, not a computed index (that put v in scratch memory)
+      const int i = i0 + u * N;
+      const bool p = i < gp, t = i >= gp && i < S;
+      v[kTsPoseG] += p ? x[u].x : 0.0;
+      v[kTsPoseD] += p ? x[u].y : 0.0;
+      v[kTsPtG] += t ? x[u].x : 0.0;
+      v[kTsPtD] += t ? x[u].y : 0.0;
+      v[kTsCost] += i >= S ? x[u].x : 0.0;  // (slots past E loaded as zeros)
+      v[kTsValid] += i >= S ? x[u].y : 0.0;
+    }
+  }
+  auto add_small = [&](int i, const double2& y, double m) {
+    if (i < gp) {
+      v[kTsPoseStep2] += y.x;
+      v[kTsPoseXNorm2] += y.y;
+      v[kTsPoseGMax] = fmax(v[kTsPoseGMax], m);
+    } else if (i < S) {
+      v[kTsPtStep2] += y.x;
+      v[kTsPtXNorm2] += y.y;
+      v[kTsPtGMax] = fmax(v[kTsPtGMax], m);
     }
   };
-  range(red, 0, gp, v[kTsPoseG], v[kTsPoseD]);
-  range(red, gp, gp + gq, v[kTsPtG], v[kTsPtD]);
-  range(red, gp + gq, gp + gq + gc, v[kTsCost], v[kTsValid]);
-  range(red2, 0, gp, v[kTsPoseStep2], v[kTsPoseXNorm2]);
-  range(red2, gp, gp + gq, v[kTsPtStep2], v[kTsPtXNorm2]);
-  for (int i = threadIdx.x; i < gp + gq; i += N) {
-    const int q = i < gp ? kTsPoseGMax : kTsPtGMax;
-    v[q] = fmax(v[q], gmax[i]);
-  }
+  add_small(i_s, ys, ms);
+  for (int i = i_s + N; i < S; i += N) add_small(i, r2[i], gmax[i]);
   auto is_max = [](int q) { return q == kTsPoseGMax || q == kTsPtGMax; };
 #pragma unroll
   for (int q = 0; q < kTsCount; ++q)
@@ -2032,25 +2159,35 @@ __device__ void trial_sums(const double* __restrict__ red, const double* __restr
 #pragma unroll
     for (int q = 0; q < kTsCount; ++q) part[q][threadIdx.x >> 6] = v[q];
   __syncthreads();
-  if (threadIdx.x == 0)
-    for (int q = 0; q < kTsCount; ++q) {
-      double s = 0.0;
-      for (int w = 0; w < N / 64; ++w) s = is_max(q) ? fmax(s, part[q][w]) : s + part[q][w];
-      t[q] = s;
-    }
+  // the waves in order, one thread per sum (one thread summing all twelve, 192 dependent LDS reads, was ~8 µs)
+  if (threadIdx.x < kTsCount) {
+    const int q = threadIdx.x;
+    double w16[N / 64];
+#pragma unroll
+    for (int w = 0; w < N / 64; ++w) w16[w] = part[q][w];
+    double s = 0.0;
+#pragma unroll
+    for (int w = 0; w < N / 64; ++w) s = is_max(q) ? fmax(s, w16[w]) : s + w16[w];
+    t[q] = s;
+  }
+  __syncthreads();
 }
 
 // Publish the record to page-locked, host-coherent memory (wave 0): lane i stores field i, every store completes, then
 // lane 0 stores the sequence number the host polls for with a system-scope release.
-__device__ void publish_record(const double* s_rec, volatile double* host_rec, double seq) {
+// Every store is a system-scope relaxed atomic (`sc0 sc1`: written through to memory, whatever the page's cache
+// policy), and the sequence number is stored only after every field store has completed (vmcnt(0)).  A release fence
+// at system scope instead (`buffer_wbl2`) wrote back every dirty line the candidate linearisation had left in L2: the
+// decision launch took 14.5-16.4 µs against 8.6 µs (profiles/r3_gn_trial_trace_*).
+__device__ void publish_record(const double* s_rec, double* host_rec, double seq) {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   const int l = threadIdx.x;
-  if (l < kLmFields) host_rec[l] = s_rec[l];
-  __builtin_amdgcn_s_waitcnt(0);  // vmcnt(0) & lgkmcnt(0): every lane's field store has completed
+  if (l < kLmFields) __hip_atomic_store(host_rec + l, s_rec[l], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every lane's field store has completed
   __builtin_amdgcn_wave_barrier();
-  if (l == 0) __hip_atomic_store(const_cast<double*>(host_rec + kLmFields), seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (l == 0) __hip_atomic_store(host_rec + kLmFields, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 __global__ __launch_bounds__(kDecideThreads) void lm_decide_kernel(const double* __restrict__ red,
@@ -2058,7 +2195,7 @@ __global__ __launch_bounds__(kDecideThreads) void lm_decide_kernel(const double*
                                                                    const double* __restrict__ gmax, int gp, int gq,
                                                                    int gc, const int* __restrict__ status,
                                                                    const DecideOpts o, double* __restrict__ lm,
-                                                                   volatile double* __restrict__ host_rec, double seq) {
+                                                                   double* __restrict__ host_rec, double seq) {
   if (lm[kLmDone] != 0.0) return;  // a trial enqueued ahead of the one that ended the solve
   __shared__ double t[kTsCount];
   trial_sums(red, red2, gmax, gp, gq, gc, t);
@@ -2102,7 +2239,7 @@ __global__ __launch_bounds__(kDecideThreads) void dist_sums_kernel(const double*
 // every rank takes the same decision; the reported gradient norm is this rank's view (pose part and its own points).
 __global__ __launch_bounds__(64) void dist_decide_kernel(const double* __restrict__ Y, const double* __restrict__ tpose,
                                                          const int* __restrict__ status, const DecideOpts o,
-                                                         double* __restrict__ lm, volatile double* __restrict__ host_rec,
+                                                         double* __restrict__ lm, double* __restrict__ host_rec,
                                                          double seq) {
   if (lm[kLmDone] != 0.0) return;
   __shared__ double s_rec[kLmFields];
@@ -2167,6 +2304,10 @@ int configure_solver(pba_engine* e, int K, int solver) {
   }
   G.cr_levels.clear();
   G.cr_pcr = -1;
+  if (const char* v = std::getenv("PBA_PCR_FUSED")) {  // A/B switch: 0 = a launch per level, 2 = two workgroups per CU
+    G.pcr_fused_opt = std::atoi(v) != 0;
+    G.pcr_fused_per_cu = std::atoi(v) == 2 ? 2 : 1;
+  }
   if (solver == SOLVER_CR) {
     const int M = 6 * K;
     // Parallel cyclic reduction takes over (wave kernel, M = 24) once the rows fit one workgroup per CU:
@@ -2203,6 +2344,19 @@ int configure_solver(pba_engine* e, int K, int solver) {
       P.b = off; off += (size_t)np * M;
     }
     G.cr0_dirty = true;  // level 0 is set up for assemble_kernel's direct writes on first use
+    // the one-launch PCR (pcr_fused_kernel): a buffer per stride level, ready flags, the task counter
+    G.pcr_levels = 0;
+    for (int st = 1; st < np; st *= 2) ++G.pcr_levels;
+    G.pcr_fused = G.pcr_fused_opt && M == 24 && np > 0 && G.pcr_levels <= kMaxPcrLevels;
+    if (G.pcr_fused) {
+      PBA_HIP(G.pcr_lv.resize((size_t)std::max(G.pcr_levels, 1) * ((size_t)np * M * M * 2 + (size_t)np * M)));
+      PBA_HIP(G.pcr_flags.resize((size_t)(G.pcr_levels + 1) * np));
+      PBA_HIP(G.pcr_counter.resize(1));
+      PBA_HIP(hipMemsetAsync(G.pcr_flags.p, 0, sizeof(int) * G.pcr_flags.n, st));
+      PBA_HIP(hipMemsetAsync(G.pcr_counter.p, 0, sizeof(unsigned), st));
+      G.pcr_base = 0;
+      G.pcr_epoch = 0;
+    }
   }
   return PBA_OK;
 }
@@ -2641,14 +2795,39 @@ void cr_solve(pba_engine* e, bool build) {
   const int c = G.cr_pcr >= 0 ? G.cr_pcr : nl - 1;
   for (int l = 0; l < c; ++l) {
     CrLevel L = cr_level(G, l), Ln = cr_level(G, l + 1);
-    if constexpr (2 * M + 1 <= 64)
+    if constexpr (2 * M + 1 <= 64) {
       cr_level_wave_kernel<M, false><<<(L.n + 1) / 2, 256, cr_level_wave_lds<M>(), e->stream>>>(L, Ln, 1, G.status.p);
-    else
+    } else
       cr_level_kernel<M><<<(L.n + 1) / 2, 2 * kCrOddThreads<M>, cr_level_lds<M>(), e->stream>>>(L, Ln, G.status.p);
   }
   bool solved = false;  // the step vector already written (level c = 0 solved in place)
   if constexpr (2 * M + 1 <= 64) {
-    if (G.cr_pcr >= 0) {
+    if (G.cr_pcr >= 0 && G.pcr_fused) {
+      PcrFusedArgs fa{};
+      fa.lv0 = cr_level(G, c);
+      const int n = fa.lv0.n;
+      fa.lv = G.pcr_lv.p;
+      fa.n_levels = G.pcr_levels;
+      fa.n = n;
+      solved = c == 0;
+      fa.out = solved ? G.x.p : cr_level(G, c).x;
+      fa.lim = solved ? 6 * e->n_frames : n * M;
+      fa.epoch = ++G.pcr_epoch;
+      fa.status = G.status.p;
+      fa.flags = G.pcr_flags.p;
+      fa.counter = G.pcr_counter.p;
+      fa.base = G.pcr_base;
+      const int grid = (G.pcr_levels + 1) * n;  // one workgroup per task
+      // dynamic LDS sized so that one workgroup fits a CU (160 KiB): the hand-off form is the one validated at one
+      // workgroup per CU
+      constexpr int kFusedLds = 81 * 1024;
+      static_assert(cr_level_wave_lds<24>() <= (size_t)kFusedLds, "the level's LDS");
+      const int lds = G.pcr_fused_per_cu == 1 ? kFusedLds : (int)cr_level_wave_lds<M>();
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&pcr_fused_kernel<M>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+      pcr_fused_kernel<M><<<grid, 256, lds, e->stream>>>(fa);
+      G.pcr_base += (unsigned)grid;
+    } else if (G.cr_pcr >= 0) {
       CrLevel src = cr_level(G, c);
       const int n = src.n;
       int pi = 0;
@@ -2658,8 +2837,9 @@ void cr_solve(pba_engine* e, bool build) {
         src = dst;
       }
       solved = c == 0;
-      pcr_solve_kernel<M><<<n, 64, 0, e->stream>>>(src, solved ? G.x.p : cr_level(G, c).x,
-                                                   solved ? 6 * e->n_frames : n * M, G.status.p);
+      double* out = solved ? G.x.p : cr_level(G, c).x;
+      const int lim = solved ? 6 * e->n_frames : n * M;
+      pcr_solve_kernel<M><<<n, 64, 0, e->stream>>>(src, out, lim, G.status.p);
     } else {
       cr_root_wave_kernel<M><<<1, 64, 0, e->stream>>>(cr_level(G, nl - 1), G.status.p);
     }

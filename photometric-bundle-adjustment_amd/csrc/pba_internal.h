@@ -585,6 +585,12 @@ struct GnData {
   std::vector<CrLevelHost> cr_levels;  // block-cyclic-reduction level layout (offsets into cr_buf)
   int cr_pcr = -1;                     // the CR level whose rows parallel cyclic reduction solves (-1: root kernel)
   CrLevelHost pcr_bufs[2];             // PCR ping-pong buffers (D, U, b) for that level's rows
+  bool pcr_fused_opt = false, pcr_fused = false;  // PCR levels + solve in one data-flow launch (PBA_PCR_FUSED=1)
+  int pcr_levels = 0, pcr_epoch = 0, pcr_fused_per_cu = 1;
+  unsigned pcr_base = 0;
+  DevBuf<double> pcr_lv;                 // the one-launch PCR's level buffers (D, U, b per stride level)
+  DevBuf<int> pcr_flags;
+  DevBuf<unsigned> pcr_counter;
   DevBuf<double> cr_buf;
   bool force_skyline = false;
   size_t lin_floats = 0, schur_doubles = 0, schur_lds = 0;

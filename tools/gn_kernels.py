@@ -36,7 +36,7 @@ def main():
         eng.solve(max_iterations=2, function_tolerance=0.0)
         eng.set_state(pb.poses, pb.rho)
         s = eng.solve(max_iterations=args.iters, function_tolerance=0.0)
-        print(f"{s['total_ms'] / max(s['iterations'], 1):.3f} ms per LM iteration (pba_solve), {s['successful_steps']} accepted")
+        print(f"{s['total_ms'] / max(s['iterations'], 1):.3f} ms per LM iteration (pba_solve), {s['successful_steps']} accepted, final cost {s['final_cost']!r}")
         eng.close()
         return
     t0 = time.perf_counter()

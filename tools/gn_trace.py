@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Per-iteration kernel timeline of a pba_solve kernel trace (rocprofv3 --kernel-trace CSV): the kernels of one LM
 trial in launch order with their durations and the idle gaps before them.  Diagnostic.
-    python tools/gn_trace.py gpurun_out/<dir>/run_kernel_trace.csv"""
+    python tools/gn_trace.py gpurun_out/<dir>/run_kernel_trace.csv [trial]
+(trial: the index of the trial's schur_kernel launch in the trace; default the second-to-last trial)"""
 import csv
 import sys
 
@@ -9,7 +10,8 @@ rows = sorted(csv.DictReader(open(sys.argv[1])), key=lambda r: int(r["Start_Time
 idx = [i for i, r in enumerate(rows) if "schur_kernel" in r["Kernel_Name"]]
 if len(idx) < 4:
     sys.exit("fewer than 4 trials in the trace")
-a, b = idx[-3], idx[-2]
+k = int(sys.argv[2]) if len(sys.argv) > 2 else len(idx) - 3
+a, b = idx[k], idx[k + 1]
 prev = int(rows[a - 1]["End_Timestamp"])
 tot_k = tot_g = 0.0
 for r in rows[a:b]:
