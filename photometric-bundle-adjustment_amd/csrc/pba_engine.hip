@@ -221,17 +221,23 @@ __host__ __device__ constexpr int multi_stage_bytes(int bpw, int P, int tsize) {
 template <int PPL, class T>
 constexpr int kMultiThreads = 32 * 14 * 8 * PPL * (int)sizeof(T) + 32 * (int)sizeof(TileBlock) > 60 * 1024 ? 128 : 256;
 
-template <int PM, int MODE, class T, int PPL>
+// CT: the camera-table form (fused state, ≤ kCamTab cameras, 256 threads): compact 192-B tile blocks plus one LDS
+// CamRec per camera instead of 352-B tile blocks carrying both cameras (the 21-px fp16 launch: 30.1 → 25.6 KB of LDS
+// per workgroup, 5 → 6 workgroups per CU, which its 78 VGPRs also allow).
+template <int PM, int MODE, class T, int PPL, bool CT = false>
 __global__ __launch_bounds__((kMultiThreads<PPL, T>)) void photometric_block_kernel_multi(const KernelArgs a) {
   constexpr int LPB = 8, NTH = kMultiThreads<PPL, T>, BPW = NTH / LPB;
   constexpr bool JAC = MODE == 1;
+  static_assert(!CT || NTH == 256, "camera table: the workgroup-cooperative prologue");
+  using TB = typename std::conditional<CT, TileBlockC, TileBlock>::type;
   // dynamic LDS sized for the actual P (multi_stage_bytes): the 21-px fp16 stage is 18.4 KB instead of 21 KB for
   // 24 px, which lets a fifth workgroup onto the CU (LDS is what bounds this kernel's occupancy)
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   __shared__ float2 s_pat[LPB * PPL];
+  __shared__ CamRec s_cam[CT ? kCamTab : 1];
   const int P = a.P;
   T* stage = reinterpret_cast<T*>(lds);
-  TileBlock* s_tb = reinterpret_cast<TileBlock*>(lds + (JAC ? multi_stage_bytes(BPW, P, (int)sizeof(T)) : 0));
+  TB* s_tb = reinterpret_cast<TB*>(lds + (JAC ? multi_stage_bytes(BPW, P, (int)sizeof(T)) : 0));
   const int rec_f = 14 * P;
   const int blk0 = logical_tile() * BPW;
   const int lb = threadIdx.x / LPB;
@@ -243,7 +249,10 @@ __global__ __launch_bounds__((kMultiThreads<PPL, T>)) void photometric_block_ker
   if ((int)threadIdx.x < LPB * PPL) s_pat[threadIdx.x] = pattern_at<LPB * PPL>(a, threadIdx.x);
   adopt_state(a);
   int pt;
-  if (NTH == 256 && a.poses) {  // fused state: the workgroup-cooperative prologue (BPW = 32)
+  if constexpr (CT) {
+    pt = a.block_rec[live ? blk : a.n_blocks - 1].x;
+    stage_tile_wg_ct(a, s_tb, s_cam, a.n_cams, blk0);
+  } else if (NTH == 256 && a.poses) {  // fused state: the workgroup-cooperative prologue (BPW = 32)
     pt = a.block_rec[live ? blk : a.n_blocks - 1].x;
     stage_tile_wg(a, s_tb, blk0);
   } else {
@@ -262,7 +271,7 @@ __global__ __launch_bounds__((kMultiThreads<PPL, T>)) void photometric_block_ker
   auto pixel = [&](int j, float ih) {
     const int px = k + LPB * j;
     const bool act = live && px < P;
-    const Row row = photometric_row<PM, JAC>(a, s_tb[lb], s_pat[px < P ? px : 0], ih);  // masked by act
+    const Row row = photometric_row<PM, JAC>(a, s_tb[lb], s_pat[px < P ? px : 0], ih, s_cam);  // masked by act
     okl &= act ? row.ok : 1;
     s += act ? row.r * row.r : 0.0f;
     if (JAC && act) {  // record row px: r | J_host row | J_target row | J_rho
@@ -443,14 +452,21 @@ void launch_photometric(pba_engine* e, const KernelArgs& ka, int mode) {
     return;
   }
   // 9…32 pixels: 8 lanes per block, ⌈P/8⌉ pixels per lane
+  // the camera-table form for record launches at a fused state with few cameras (the C5 configuration)
+  const bool ct = mode == 1 && ka.poses != nullptr && ka.n_cams <= kCamTab && !e->no_cam_table;
 #define PBA_LAUNCH_ONE(PPL, M, TT)                                                                      \
   {                                                                                                     \
     constexpr int nth = kMultiThreads<PPL, TT>;                                                         \
     const int grid = (int)(((long long)e->n_blocks * 8 + nth - 1) / nth);                              \
     e->last_grid = grid;                                                                                \
-    const size_t lds = (M == 1 ? multi_stage_bytes(nth / 8, e->P, (int)sizeof(TT)) : 0) +              \
-                       (size_t)(nth / 8) * sizeof(TileBlock);                                           \
-    photometric_block_kernel_multi<PM, M, TT, PPL><<<grid, nth, lds, e->stream>>>(ka);                  \
+    const size_t stage = M == 1 ? multi_stage_bytes(nth / 8, e->P, (int)sizeof(TT)) : 0;               \
+    if (M == 1 && nth == 256 && ct) {                                                                   \
+      photometric_block_kernel_multi<PM, M, TT, PPL, (M == 1 && nth == 256)>                            \
+          <<<grid, nth, stage + (size_t)(nth / 8) * sizeof(TileBlockC), e->stream>>>(ka);              \
+    } else {                                                                                            \
+      photometric_block_kernel_multi<PM, M, TT, PPL>                                                    \
+          <<<grid, nth, stage + (size_t)(nth / 8) * sizeof(TileBlock), e->stream>>>(ka);               \
+    }                                                                                                   \
   }
 #define PBA_LAUNCH_PPL(PPL)                                        \
   if (mode == 1 && h) PBA_LAUNCH_ONE(PPL, 1, _Float16)             \
@@ -521,6 +537,7 @@ KernelArgs make_kernel_args(pba_engine* e, const PairRec* pairs, const double* r
   ka.cost = e->cost.p;
   ka.valid = e->valid.p;
   ka.n_blocks = e->n_blocks;
+  ka.n_cams = e->n_cams;
   ka.P = e->opt.residual_kind == PBA_RESIDUAL_PHOTOMETRIC ? e->P : 2;
   ka.huber = e->opt.huber_width;
   for (size_t i = 0; i < e->pattern_h.size() && i < 2 * PBA_MAX_PATTERN; ++i) ka.pattern[i] = e->pattern_h[i];

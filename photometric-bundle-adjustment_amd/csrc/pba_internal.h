@@ -5,6 +5,8 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <cstdlib>
+#include <type_traits>
 #include <string>
 #include <vector>
 
@@ -38,7 +40,8 @@ static_assert(offsetof(PairRec, hk) % 16 == 0 && offsetof(PairRec, tk) == offset
 // 151-153; Hamilton product as so3.hpp:338-345, rotation as so3.hpp:367-370), with the camera constants.  The
 // three parts write their fields in place, so r may live in LDS (tile prologue: one lane per part, which keeps
 // the prologue's register peak below the row evaluation's) or in the pair table (pair_kernel: all three).
-__device__ __forceinline__ void pair_rotation(const double* __restrict__ H, const double* __restrict__ T, PairRec& r) {
+template <class Rec>  // PairRec or TileBlockC: fields R, Rf
+__device__ __forceinline__ void pair_rotation(const double* __restrict__ H, const double* __restrict__ T, Rec& r) {
   const double ax = -T[0], ay = -T[1], az = -T[2], aw = T[3];
   const double bx = H[0], by = H[1], bz = H[2], bw = H[3];
   const double qw = aw * bw - ax * bx - ay * by - az * bz;
@@ -59,8 +62,9 @@ __device__ __forceinline__ void pair_rotation(const double* __restrict__ H, cons
     r.Rf[j] = (float)R[j];
   }
 }
+template <class Rec>  // PairRec or TileBlockC: fields t, tf
 __device__ __forceinline__ void pair_translation(const double* __restrict__ H, const double* __restrict__ T,
-                                                 PairRec& r) {
+                                                 Rec& r) {
   const double ax = -T[0], ay = -T[1], az = -T[2], aw = T[3];
   const double d0 = H[4] - T[4], d1 = H[5] - T[5], d2 = H[6] - T[6];
   double u0 = ay * d2 - az * d1, u1 = az * d0 - ax * d2, u2 = ax * d1 - ay * d0;
@@ -124,6 +128,41 @@ static_assert(sizeof(TileBlock) == 352, "TileBlock layout");
 constexpr int kPairParts = sizeof(PairRec) / 16;     // 20 × 16 B
 constexpr int kTileParts = sizeof(TileBlock) / 16;   // 22 × 16 B
 
+// Compact tile block of the camera-table form (photometric_block_kernel_multi when the problem has ≤ kCamTab cameras):
+// the pair's pose part and the point, 192 B instead of 352 — the two cameras' constants (160 B per block) live once
+// per camera in a small LDS table (CamRec) — so the C5 kernel's 32-block tile shrinks by 5 KB and a sixth workgroup
+// fits a CU.
+struct alignas(16) TileBlockC {
+  double R[9];
+  double t[3];
+  int host_cam, target_cam, target, host;
+  float Rf[9], tf[3];
+  double2 ur;
+  double rho;
+  long long img;
+};
+static_assert(sizeof(TileBlockC) == 192, "TileBlockC layout");
+struct alignas(16) CamRec {
+  double hk[kCamK];            // unprojection layout (as PairRec::hk)
+  double tk[kCamK];            // projection layout (as PairRec::tk)
+  float kf[8];                 // fp32 projection constants (as PairRec::kf)
+};
+static_assert(sizeof(CamRec) == 160, "CamRec layout");
+constexpr int kCamTab = 4;     // cameras in the LDS table (mono, stereo and up to four-camera rigs)
+
+// The pose part and the camera constants a photometric row reads, from either tile form.
+struct CamView {
+  const double* hk;
+  const double* tk;
+  const float* kf;
+};
+__device__ __forceinline__ const PairRec& pose_of(const TileBlock& tb) { return tb.pr; }
+__device__ __forceinline__ const TileBlockC& pose_of(const TileBlockC& tb) { return tb; }
+__device__ __forceinline__ CamView cams_of(const TileBlock& tb, const CamRec*) { return {tb.pr.hk, tb.pr.tk, tb.pr.kf}; }
+__device__ __forceinline__ CamView cams_of(const TileBlockC& tb, const CamRec* tab) {
+  return {tab[tb.host_cam].hk, tab[tb.target_cam].tk, tab[tb.target_cam].kf};
+}
+
 struct KernelArgs {
   const uint8_t* images;
   int width, height, tiles_x;
@@ -152,6 +191,7 @@ struct KernelArgs {
   uint8_t* valid;                // per block
   int n_blocks;
   int P;
+  int n_cams;                    // cameras (photometric_block_kernel_multi's camera table: ≤ kCamTab)
   float huber;
   double* wg_red;  // residual-only launches of the LM loop: per-workgroup (Σ cost, Σ valid) at slot logical_tile()
   float pattern[2 * PBA_MAX_PATTERN];
@@ -389,6 +429,61 @@ __device__ __forceinline__ void stage_tile_wg(const KernelArgs& a, TileBlock* s_
   }
 }
 
+// The same for the compact tile (TileBlockC) and the LDS camera table of n_cams ≤ kCamTab cameras: waves 0, 1 and 3
+// as above; wave 2 copies the camera table instead of every block's two cameras (lane = 16-B part: per camera the four
+// parts of hk, the four of tk, and the fp32 kf from tk's).  The caller barriers.
+__device__ __forceinline__ void stage_tile_wg_ct(const KernelArgs& a, TileBlockC* s_tb, CamRec* s_cam, int n_cams,
+                                                 int blk0) {
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, b = lane & 31;
+  const int4 br = a.block_rec[min(blk0 + b, a.n_blocks - 1)];  // a dead block stages the last block
+  TileBlockC& tb = s_tb[b];
+  if (w == 0) {
+    if (lane < 32) {
+      const double* H = a.poses + 7 * br.y;
+      const double* T = a.poses + 7 * br.z;
+      double h[4], t[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        h[j] = H[j];
+        t[j] = T[j];
+      }
+      pair_rotation(h, t, tb);
+    }
+  } else if (w == 1) {
+    if (lane < 32) {
+      const double* H = a.poses + 7 * br.y;
+      const double* T = a.poses + 7 * br.z;
+      double h[7], t[7];
+#pragma unroll
+      for (int j = 0; j < 7; ++j) {
+        h[j] = H[j];
+        t[j] = T[j];
+      }
+      pair_translation(h, t, tb);
+      tb.host_cam = br.w >> 16;
+      tb.target_cam = br.w & 0xffff;
+      tb.target = br.z;
+      tb.host = br.y;
+    }
+  } else if (w == 2) {
+    // lane = camera c (lane >> 3) × part q (lane & 7): q < 4 → hk part q, q ≥ 4 → tk part q − 4 (+ its fp32 kf)
+    const int c = lane >> 3, q = lane & 7;
+    if (c < n_cams) {
+      const uint4 v = reinterpret_cast<const uint4*>(a.intr_d + (q < 4 ? kCamD * c + kCamHk : kCamD * c))[q & 3];
+      uint4* d = reinterpret_cast<uint4*>(s_cam + c);
+      d[q] = v;  // hk parts 0-3, tk parts 4-7 (CamRec: hk then tk, contiguous)
+      if (q >= 4) camera_kf_part(v, q - 4, s_cam[c].kf);
+    }
+  } else {
+    if (lane < 32) {
+      tb.ur = a.u_ref[br.x];
+    } else {
+      tb.rho = a.rho[br.x];
+      tb.img = (long long)br.z * a.frame_stride;
+    }
+  }
+}
+
 // Pattern offset k (k < N) read from the kernel arguments with scalar loads at constant offsets and picked per lane
 // by selects.  A lane-indexed read of the argument block is a vector-memory load, and staging it through LDS made
 // every workgroup wait one memory round trip before it issued any other load.
@@ -416,23 +511,26 @@ __device__ __forceinline__ void adopt_state(const KernelArgs& a) {
 // Jacobian chain of pba_device.h).  Warp and projection in fp64, chain in fp32.  off = pattern offset k,
 // Ih = host intensity I_h,k.
 // PM = camera model + 4 · interpolator (pba_device.h cam_of / interp_of).
-template <int PM, bool JAC>
-__device__ __forceinline__ Row photometric_row(const KernelArgs& a, const TileBlock& tb, float2 off, float Ih) {
+// TB = TileBlock (cameras in the block), or TileBlockC with the LDS camera table `tab`.
+template <int PM, bool JAC, class TB = TileBlock>
+__device__ __forceinline__ Row photometric_row(const KernelArgs& a, const TB& tb, float2 off, float Ih,
+                                               const CamRec* tab = nullptr) {
   constexpr int MODEL = cam_of(PM);
   Row o;
-  const PairRec& pp = tb.pr;
+  const auto& pp = pose_of(tb);
+  const CamView cv = cams_of(tb, tab);
   const double rho = tb.rho;
   // p̃ = R_th b_k + ρ t_th  (photometric_error.h:158-159)
-  const Vec3d b = unproject<MODEL>(pp.hk, tb.ur.x + (double)off.x, tb.ur.y + (double)off.y);
+  const Vec3d b = unproject<MODEL>(cv.hk, tb.ur.x + (double)off.x, tb.ur.y + (double)off.y);
   const Vec3d Rb = mat_mul(pp.R, b);
   const Vec3d p = {Rb.x + rho * pp.t[0], Rb.y + rho * pp.t[1], Rb.z + rho * pp.t[2]};
   // Branch-free: the projection and the taps run whatever the domain test says (the interpolator clamps any
   // position, NaN and ±inf included, to an in-bounds read), and the caller masks a block that is not ok.  A branch
   // here costs every lane the zero-initialised Row and the exec bookkeeping, and no wave ever skips it.
-  const bool dom = in_domain<MODEL>(pp.tk, p);
+  const bool dom = in_domain<MODEL>(cv.tk, p);
   float I, gx, gy;
   double u, v;
-  const double iden = project<MODEL>(pp.tk, p, u, v);
+  const double iden = project<MODEL>(cv.tk, p, u, v);
   interpolate<interp_of(PM)>(a.images + tb.img, a.umax, a.vmax, a.tiles_x, u, v, I, gx, gy);
   o.r = I - Ih;  // photometric_error.h:179
   o.ok = dom && isfinite(o.r);
@@ -440,7 +538,7 @@ __device__ __forceinline__ Row photometric_row(const KernelArgs& a, const TileBl
     // q = ∇I · ∂π/∂p̃ (1×3)
     const Vec3 pf = to_f(p), bf = to_f(b);
     Vec3 du, dv;
-    project_jac<MODEL>(pp.kf, pf, (float)iden, du, dv);
+    project_jac<MODEL>(cv.kf, pf, (float)iden, du, dv);
     const Vec3 q = {gx * du.x + gy * dv.x, gx * du.y + gy * dv.y, gx * du.z + gy * dv.z};
     const Vec3 qR = row_mul(q, pp.Rf);
     const float rf = (float)rho;
@@ -454,10 +552,10 @@ __device__ __forceinline__ Row photometric_row(const KernelArgs& a, const TileBl
       // ∂u/∂p̃·t = fx/z (t_x − m_x t_z), ∂v/∂p̃·t = fy/z (t_y − m_y t_z), m = p̃_xy / z (the projection's own
       // quotients): 7 fp64 operations instead of the general 2×3 Jacobian and two dot products
       const double ex = fma(-(p.x * iden), pp.t[2], pp.t[0]), ey = fma(-(p.y * iden), pp.t[2], pp.t[1]);
-      o.jr = (float)(iden * fma((double)gx * pp.tk[0], ex, (double)gy * pp.tk[1] * ey));
+      o.jr = (float)(iden * fma((double)gx * cv.tk[0], ex, (double)gy * cv.tk[1] * ey));
     } else {
       Vec3d dud, dvd;
-      project_jac<MODEL>(pp.tk, p, iden, dud, dvd);
+      project_jac<MODEL>(cv.tk, p, iden, dud, dvd);
       const Vec3d td = {pp.t[0], pp.t[1], pp.t[2]};
       o.jr = (float)((double)gx * dot(dud, td) + (double)gy * dot(dvd, td));
     }
@@ -688,6 +786,7 @@ struct pba_engine {
   bool pairs_fresh = false;          // pairs hold T_th of the current poses (pba_set_state_device forms them)
   bool evaluated = false;
   bool timing = false;
+  bool no_cam_table = std::getenv("PBA_NO_CAM_TABLE") != nullptr;  // A/B switch: the C5 kernel without its camera table
   int last_grid = 0;                 // workgroups of the last evaluation launch (launch_mode)
   std::vector<hipEvent_t> ev_pool;   // start/stop pairs, reused
   int level = 0;                     // active pyramid level (its buffers are swapped into the fields above)
