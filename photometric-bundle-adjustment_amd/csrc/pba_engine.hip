@@ -13,6 +13,8 @@
 // validity come from wave shuffles, and the workgroup's records leave as one contiguous slab.
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
@@ -225,7 +227,8 @@ constexpr int kMultiThreads = 32 * 14 * 8 * PPL * (int)sizeof(T) + 32 * (int)siz
 // CamRec per camera instead of 352-B tile blocks carrying both cameras (the 21-px fp16 launch: 30.1 → 25.6 KB of LDS
 // per workgroup, 5 → 6 workgroups per CU, which its 78 VGPRs also allow).
 template <int PM, int MODE, class T, int PPL, bool CT = false>
-__global__ __launch_bounds__((kMultiThreads<PPL, T>)) void photometric_block_kernel_multi(const KernelArgs a) {
+__global__ __launch_bounds__((kMultiThreads<PPL, T>)) __attribute__((amdgpu_waves_per_eu(CT ? 6 : 1, 8)))
+void photometric_block_kernel_multi(const KernelArgs a) {
   constexpr int LPB = 8, NTH = kMultiThreads<PPL, T>, BPW = NTH / LPB;
   constexpr bool JAC = MODE == 1;
   static_assert(!CT || NTH == 256, "camera table: the workgroup-cooperative prologue");
@@ -274,6 +277,38 @@ __global__ __launch_bounds__((kMultiThreads<PPL, T>)) void photometric_block_ker
     const Row row = photometric_row<PM, JAC>(a, s_tb[lb], s_pat[px < P ? px : 0], ih, s_cam);  // masked by act
     okl &= act ? row.ok : 1;
     s += act ? row.r * row.r : 0.0f;
+    if constexpr (JAC && std::is_same<T, _Float16>::value) {
+      // fp16 records: the 14 values in 7 packed round-to-nearest conversions (v_cvt_pk_f16_f32) instead of a
+      // NaN-preserving clamp + conversion each; a value beyond the half range rounds to ±inf there, which rec_val
+      // saturates to ±65504 — applied afterwards, only when some lane of the wave has one (a ballot)
+      typedef float f2 __attribute__((ext_vector_type(2)));
+      typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+      const float v[14] = {row.r, row.jr, row.hv.x, row.hv.y, row.hv.z, row.hw.x, row.hw.y, row.hw.z,
+                           row.tv.x, row.tv.y, row.tv.z, row.tw.x, row.tw.y, row.tw.z};
+      h2 c[7];
+      bool big = false;
+#pragma unroll
+      for (int q = 0; q < 7; ++q) {
+        c[q] = __builtin_convertvector((f2){v[2 * q], v[2 * q + 1]}, h2);
+        big |= __builtin_isinf(c[q].x) || __builtin_isinf(c[q].y);
+      }
+      if (__ballot(act && big) != 0) {
+        auto sat = [](_Float16 h) -> _Float16 {
+          return __builtin_isinf(h) ? (h > (_Float16)0 ? (_Float16)65504.0f : (_Float16)-65504.0f) : h;
+        };
+#pragma unroll
+        for (int q = 0; q < 7; ++q) c[q] = (h2){sat(c[q].x), sat(c[q].y)};
+      }
+      if (act) {
+        T* h = s_rec + P + 6 * px;
+        T* t = s_rec + 7 * P + 6 * px;
+        s_rec[px] = c[0].x;
+        s_rec[13 * P + px] = c[0].y;
+        h[0] = c[1].x; h[1] = c[1].y; h[2] = c[2].x; h[3] = c[2].y; h[4] = c[3].x; h[5] = c[3].y;
+        t[0] = c[4].x; t[1] = c[4].y; t[2] = c[5].x; t[3] = c[5].y; t[4] = c[6].x; t[5] = c[6].y;
+      }
+      return row.r;
+    }
     if (JAC && act) {  // record row px: r | J_host row | J_target row | J_rho
       T* h = s_rec + P + 6 * px;
       T* t = s_rec + 7 * P + 6 * px;

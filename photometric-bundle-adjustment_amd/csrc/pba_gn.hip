@@ -42,6 +42,7 @@
 
 #include "pba_internal.h"
 
+
 using namespace pba;
 using namespace pba::detail;
 
@@ -149,6 +150,23 @@ constexpr auto make_slot_table(std::integer_sequence<int, L...>) {
 }
 __constant__ const auto kSlotTable = make_slot_table(std::make_integer_sequence<int, 64>{});
 
+// Product index of chunk partial output o (linearize_kernel's partial slots): o < 42 → H_hh (6×6, both triangles from
+// the upper products) and g_h; o = 42 + q → H_ht (36), H_tt (6×6) and g_t of one target.
+__host__ __device__ constexpr int lin_out_v(int o) {
+  if (o < 36) { const int r = o / 6, c = o % 6; return upper_index(r < c ? r : c, r < c ? c : r); }
+  if (o < 42) return 78 + (o - 36);
+  const int q = o - 42;
+  if (q < 36) return 21 + q;
+  if (q < 72) { const int r = (q - 36) / 6, c = (q - 36) % 6; return 57 + upper_index(r < c ? r : c, r < c ? c : r); }
+  return 84 + (q - 72);
+}
+template <int... L>
+constexpr auto make_out_table(std::integer_sequence<int, L...>) {
+  struct T { unsigned char v[sizeof...(L)]; };
+  return T{{(unsigned char)lin_out_v(L)...}};
+}
+__constant__ const auto kLinOutV = make_out_table(std::make_integer_sequence<int, 42 + 78>{});
+
 // Normal-equation products by matrix cores: weighted rows X (R × 14, padded to LPB × 16 per block) give
 // XᵀX = Σ_k x_kᵀx_k as v_mfma_f32_16x16x4f32 steps (operand A = Xᵀ and B = X are the same register: lane l holds
 // X[4s + l/16][l%16]).  A chunk's blocks are ordered by target (gn_prepare), so the blocks of one target are
@@ -166,7 +184,8 @@ void linearize_kernel(const KernelArgs a, const LinArgs g) {
   constexpr int NVP = 108;                  // 104 products, padded
   constexpr int kTileW = KIND == PBA_RESIDUAL_PHOTOMETRIC ? BW * (int)sizeof(TileBlock) : 0;
   constexpr int kRowsW = 64 * 16 * 4, kProdW = BW * NVP * 4;
-  constexpr int kArena = (kTileW > kRowsW ? (kTileW > kProdW ? kTileW : kProdW) : (kRowsW > kProdW ? kRowsW : kProdW));
+  constexpr int kArena0 = (kTileW > kRowsW ? (kTileW > kProdW ? kTileW : kProdW) : (kRowsW > kProdW ? kRowsW : kProdW));
+  constexpr int kArena = kArena0 < kProdW + 256 ? kProdW + 256 : kArena0;  // (+ the flush's dummy words)
   // per-wave arena, used in turn by the wave's tile blocks, its weighted rows and its per-target products
   // (each phase only touches the wave's own blocks; LDS is in order within a wave)
   __shared__ __attribute__((aligned(16))) unsigned char arena[NW][kArena];
@@ -180,8 +199,11 @@ void linearize_kernel(const KernelArgs a, const LinArgs g) {
   const bool s1 = (lv.set != 0.0) != g.spare;
   float* const blk_schur = s1 ? g.blk_schur1 : g.blk_schur;
   float* const part_lin = s1 ? g.part_lin1 : g.part_lin;
-  const int count = d.y, n_t = d.z, poff = d.w;
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  // (a vector load of a uniform address: readfirstlane tells the compiler the values are wave-uniform, so the loops and
+  // branches over them below are scalar instead of exec-mask regions)
+  const int count = __builtin_amdgcn_readfirstlane(d.y), n_t = __builtin_amdgcn_readfirstlane(d.z),
+            poff = __builtin_amdgcn_readfirstlane(d.w);
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;  // (wave-uniform)
   const int lb = threadIdx.x / LPB, k = threadIdx.x % LPB, wb = lb % BW;
   const bool live = lb < count;
   const int R = KIND == PBA_RESIDUAL_PHOTOMETRIC ? a.P : 2;
@@ -238,11 +260,14 @@ void linearize_kernel(const KernelArgs a, const LinArgs g) {
     float* sP = reinterpret_cast<float*>(arena[wave]);
     const int nbw = min(max(count - wave * BW, 0), BW);  // live blocks of this wave (wave-uniform)
     const int lo = __builtin_amdgcn_readfirstlane(lt);     // lane 0 holds the wave's first block
+    // branch-free scatter: a lane's entries outside the 104 products go to its own dummy word past the wave's product
+    // sets (the arena's tail), so the four stores need no exec-mask regions
+    static_assert(kProdW + 64 * 4 <= kArena, "dummy words after the product sets");
     auto flush = [&](const f32x4& acc, int slot) {
 #pragma unroll
       for (int m = 0; m < 4; ++m) {
         const unsigned v = (slots >> (8 * m)) & 255u;
-        if (v < (unsigned)NV) sP[slot * NVP + v] = acc[m];
+        sP[v < (unsigned)NV ? slot * NVP + (int)v : BW * NVP + lane] = acc[m];
       }
     };
     // per block: its own chain (SPB steps); row 12 of the result, C[12][c] on lanes 48 + c, is the block's
@@ -251,15 +276,16 @@ void linearize_kernel(const KernelArgs a, const LinArgs g) {
     const int pc = lane - 48, pq = pc < 12 ? pc + 2 : (pc < 14 ? pc - 12 : pc);
     f32x4 tacc = {0.0f, 0.0f, 0.0f, 0.0f};
     int cur = lo;
+    float pdat[BW];  // the blocks' point-elimination data (lanes 48-63), stored after the loop in one exec region
 #pragma unroll
     for (int b = 0; b < BW; ++b) {
+      pdat[b] = 0.0f;
       if (b < nbw) {
         f32x4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
         for (int st = 0; st < SPB; ++st)
           acc = __builtin_amdgcn_mfma_f32_16x16x4f32(op[b * SPB + st], op[b * SPB + st], acc, 0, 0, 0);
-        const int gpb = __builtin_amdgcn_readlane(gpos, b * LPB);
-        if (pc >= 0) blk_schur[(long long)gpb * 16 + pq] = acc[0];
+        pdat[b] = acc[0];
         const int ltb = __builtin_amdgcn_readlane(lt, b * LPB);
         if (ltb != cur) {
           flush(tacc, cur - lo);
@@ -270,6 +296,11 @@ void linearize_kernel(const KernelArgs a, const LinArgs g) {
       }
     }
     if (nbw > 0) flush(tacc, cur - lo);
+    if (pc >= 0) {
+#pragma unroll
+      for (int b = 0; b < BW; ++b)
+        if (b < nbw) blk_schur[(long long)__builtin_amdgcn_readlane(gpos, b * LPB) * 16 + pq] = pdat[b];
+    }
     if (lane == 0) {
       s_wlo[wave] = lo;
       s_wn[wave] = nbw > 0 ? cur - lo + 1 : 0;
@@ -280,31 +311,26 @@ void linearize_kernel(const KernelArgs a, const LinArgs g) {
   // H_ht / H_tt / g_t of local target j from the ≤ NW sets of j (one per wave that holds j's blocks)
   auto sset = [&](int w, int i, int v) -> float { return reinterpret_cast<const float*>(arena[w])[i * NVP + v]; };
   const int nout = SLOT_LIN_BASE + SLOT_LIN_T * n_t;
+  // product index of each output from a table (kLinOutV), the waves' set ranges as scalars; every lane sums both the
+  // base sets and its target's sets with selects, no per-lane branches (same order as below: bitwise the same sums)
+  int wl[NW], wn[NW];
+#pragma unroll
+  for (int w = 0; w < NW; ++w) {
+    wl[w] = __builtin_amdgcn_readfirstlane(s_wlo[w]);
+    wn[w] = __builtin_amdgcn_readfirstlane(s_wn[w]);
+  }
   for (int o = threadIdx.x; o < nout; o += kBlockThreads) {
-    int v, j = -1;
-    if (o < 36) {
-      const int r = o / 6, c = o % 6;
-      v = upper_index(min(r, c), max(r, c));
-    } else if (o < 42) {
-      v = 78 + (o - 36);
-    } else {
-      j = (o - 42) / SLOT_LIN_T;
-      const int q = (o - 42) % SLOT_LIN_T;
-      if (q < 36) v = 21 + q;
-      else if (q < 72) { const int r = (q - 36) / 6, c = (q - 36) % 6; v = 57 + upper_index(min(r, c), max(r, c)); }
-      else v = 84 + (q - 72);
-    }
-    float acc = 0.0f;
+    const int j = o < SLOT_LIN_BASE ? -1 : (o - SLOT_LIN_BASE) / SLOT_LIN_T;
+    const int v = kLinOutV.v[o < SLOT_LIN_BASE ? o : SLOT_LIN_BASE + (o - SLOT_LIN_BASE) % SLOT_LIN_T];
+    float ab = 0.0f, at = 0.0f;
 #pragma unroll
     for (int w = 0; w < NW; ++w) {
-      const int wl = s_wlo[w], wn = s_wn[w];
-      if (j < 0) {
-        for (int i = 0; i < wn; ++i) acc += sset(w, i, v);
-      } else if (j >= wl && j < wl + wn) {
-        acc += sset(w, j - wl, v);
-      }
+      for (int i = 0; i < wn[w]; ++i) ab += sset(w, i, v);
+      const int jj = j - wl[w];
+      const float t = sset(w, min(max(jj, 0), BW - 1), v);
+      at += jj >= 0 && jj < wn[w] ? t : 0.0f;
     }
-    part_lin[(long long)poff + o] = acc;
+    part_lin[(long long)poff + o] = j < 0 ? ab : at;
   }
   // the block costs last: a store issued before a load makes the wait for that load wait for the store too (GFX9
   // counts loads and stores in one counter), so the stores go after every load of the kernel
@@ -1379,6 +1405,168 @@ __device__ __forceinline__ bool gj_wave(const double* __restrict__ D, const doub
 }
 
 
+#ifndef PBA_CR_MFMA
+#define PBA_CR_MFMA 0
+#endif
+
+#if PBA_CR_MFMA
+
+// ---- Gauss-Jordan on the fp64 matrix cores (M = 24) -----------------------------------------------------------------
+// The same elimination as gj_wave<24> — X = D⁻¹[R1 | b] by 4-column pivot blocks, no pivoting (D is SPD, so is every
+// pivot block) — with the augmented matrix [D | R1 | b | 0] (24 × 64, padded to 32 rows) held by one wave in the
+// v_mfma_f64_16x16x4f64 accumulator layout: tile (rt, ct) entry v of lane l = row 16rt + l/16 + 4v, column 16ct + l%16.
+// In that layout the four pivot rows k … k+3 are entry (k%16)/4 of every lane of row tile k/16, i.e. exactly the B
+// operand of a K = 4 step (lane l = (k l/16, column l%16)).  A step is then:
+//   P = the 4 × 4 pivot block (16 readlanes), P⁻¹ by 2 × 2 blocks (every lane the same; all leading minors positive
+//   ⇔ the pivots of gj_wave's in-register solve),
+//   T = P⁻¹·R on the matrix cores (one MFMA per column tile, rows 0-3 of the result = T in the B layout),
+//   C = the pivot columns of every row → A layout through a 1-KB LDS transpose,
+//   [D | R1 | b] −= C·T (one MFMA per tile), then the pivot rows ← T.
+// The serial chain per step is the readlanes, the 2 × 2-block inverse and two MFMA latencies, against gj_wave's LDS
+// publish / 96 broadcast reads / in-register 4 × 4 solve / 80 fp64 FMAs per lane.
+__device__ __forceinline__ double readlane_d(double x, int l) {
+  const int lo = __builtin_amdgcn_readlane(__double2loint(x), l), hi = __builtin_amdgcn_readlane(__double2hiint(x), l);
+  return __hiloint2double(hi, lo);
+}
+
+// 2 × 2 inverse (row-major a, b, c, d) → false when the leading minors are not both positive
+__device__ __forceinline__ bool inv2(double a, double b, double c, double d, double (&o)[4]) {
+  const double det = a * d - b * c;
+  const double r = rcp_nr(det);
+  o[0] = d * r; o[1] = -b * r; o[2] = -c * r; o[3] = a * r;
+  return a > 0.0 && det > 0.0;
+}
+
+// P⁻¹ of a 4 × 4 (row-major) by 2 × 2 blocks: P = [A B; C E], S = E − C A⁻¹ B,
+// P⁻¹ = [A⁻¹ + A⁻¹B S⁻¹ C A⁻¹, −A⁻¹B S⁻¹; −S⁻¹ C A⁻¹, S⁻¹].  Returns false when a leading minor of P is not positive.
+__device__ __forceinline__ bool inv4(const double (&P)[16], double (&Q)[16]) {
+  double Ai[4], Si[4];
+  bool ok = inv2(P[0], P[1], P[4], P[5], Ai);
+  const double B[4] = {P[2], P[3], P[6], P[7]}, C[4] = {P[8], P[9], P[12], P[13]};
+  // AB = A⁻¹B, CA = C A⁻¹
+  const double AB[4] = {Ai[0] * B[0] + Ai[1] * B[2], Ai[0] * B[1] + Ai[1] * B[3],
+                        Ai[2] * B[0] + Ai[3] * B[2], Ai[2] * B[1] + Ai[3] * B[3]};
+  const double CA[4] = {C[0] * Ai[0] + C[1] * Ai[2], C[0] * Ai[1] + C[1] * Ai[3],
+                        C[2] * Ai[0] + C[3] * Ai[2], C[2] * Ai[1] + C[3] * Ai[3]};
+  const double S0 = P[10] - (C[0] * AB[0] + C[1] * AB[2]), S1 = P[11] - (C[0] * AB[1] + C[1] * AB[3]);
+  const double S2 = P[14] - (C[2] * AB[0] + C[3] * AB[2]), S3 = P[15] - (C[2] * AB[1] + C[3] * AB[3]);
+  ok = inv2(S0, S1, S2, S3, Si) && ok;
+  // top-right −A⁻¹B S⁻¹, bottom-left −S⁻¹ C A⁻¹
+  const double TR[4] = {-(AB[0] * Si[0] + AB[1] * Si[2]), -(AB[0] * Si[1] + AB[1] * Si[3]),
+                        -(AB[2] * Si[0] + AB[3] * Si[2]), -(AB[2] * Si[1] + AB[3] * Si[3])};
+  const double BL[4] = {-(Si[0] * CA[0] + Si[1] * CA[2]), -(Si[0] * CA[1] + Si[1] * CA[3]),
+                        -(Si[2] * CA[0] + Si[3] * CA[2]), -(Si[2] * CA[1] + Si[3] * CA[3])};
+  // top-left A⁻¹ − A⁻¹B·BL
+  const double TL[4] = {Ai[0] - (AB[0] * BL[0] + AB[1] * BL[2]), Ai[1] - (AB[0] * BL[1] + AB[1] * BL[3]),
+                        Ai[2] - (AB[2] * BL[0] + AB[3] * BL[2]), Ai[3] - (AB[2] * BL[1] + AB[3] * BL[3])};
+  Q[0] = TL[0]; Q[1] = TL[1]; Q[2] = TR[0]; Q[3] = TR[1];
+  Q[4] = TL[2]; Q[5] = TL[3]; Q[6] = TR[2]; Q[7] = TR[3];
+  Q[8] = BL[0]; Q[9] = BL[1]; Q[10] = Si[0]; Q[11] = Si[1];
+  Q[12] = BL[2]; Q[13] = BL[3]; Q[14] = Si[2]; Q[15] = Si[3];
+  return ok;
+}
+
+// One wave: [D | R1 | b] (R1: M × M, row-major or transposed; b: M values, present when ncol > M) → A = [I | X].
+// cbuf: 2 × 16 × 4 doubles of LDS owned by the wave.
+template <bool COH>
+__device__ __forceinline__ bool gj_mfma(const double* __restrict__ D, const double* __restrict__ R1, bool r1_trans,
+                                        const double* __restrict__ b, int ncol, int lane, double* cbuf,
+                                        v4f64 (&A)[2][4]) {
+  constexpr int M = 24;
+  const int cl = lane & 15, rq = lane >> 4;
+  // column 16ct + cl as base + row·stride (one address choice per lane and tile, then unconditional loads)
+  const double* base[4];
+  int stride[4];
+  bool zero[4];
+#pragma unroll
+  for (int ct = 0; ct < 4; ++ct) {
+    const int c = 16 * ct + cl;
+    base[ct] = D + min(c, M - 1);
+    stride[ct] = M;
+    zero[ct] = c >= M + ncol;
+    if (c >= M && c < 2 * M) {
+      if (R1) {
+        base[ct] = r1_trans ? R1 + (c - M) * M : R1 + (c - M);
+        stride[ct] = r1_trans ? 1 : M;
+      } else {
+        zero[ct] = true;
+      }
+    } else if (c >= 2 * M && c < M + ncol) {
+      if (b) {
+        base[ct] = b;
+        stride[ct] = 1;
+      } else {
+        zero[ct] = true;
+      }
+    }
+  }
+  // rows 16rt + rq + 4v < 24: row tile 0 all four entries, row tile 1 entries 0 and 1 (entries 2-3 are padding)
+  double ld[4][6];
+#pragma unroll
+  for (int ct = 0; ct < 4; ++ct)
+#pragma unroll
+    for (int e = 0; e < 6; ++e) ld[ct][e] = ld_row<COH>(base[ct] + (rq + 4 * e) * stride[ct]);
+#pragma unroll
+  for (int ct = 0; ct < 4; ++ct) {
+#pragma unroll
+    for (int v = 0; v < 4; ++v) A[0][ct][v] = zero[ct] ? 0.0 : ld[ct][v];
+    A[1][ct][0] = zero[ct] ? 0.0 : ld[ct][4];
+    A[1][ct][1] = zero[ct] ? 0.0 : ld[ct][5];
+    A[1][ct][2] = 0.0;
+    A[1][ct][3] = 0.0;
+  }
+  bool ok = true;
+#pragma unroll
+  for (int k = 0; k < M; k += 4) {
+    const int rtk = k >> 4, vk = (k & 15) >> 2, ctk = k >> 4, c0 = k & 15;
+    // pivot block P[i][j] = row k+i, column k+j: lane 16i + c0 + j of entry vk, tile (rtk, ctk)
+    double P[16], Q[16];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) P[4 * i + j] = readlane_d(A[rtk][ctk][vk], 16 * i + c0 + j);
+    // the pivot columns of every row → A layout (lane l: row 16rt + l%16, column k + l/16), through LDS
+    if (cl >= c0 && cl < c0 + 4) {
+#pragma unroll
+      for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+        for (int v = 0; v < 4; ++v) cbuf[(rt * 16 + rq + 4 * v) * 4 + (cl - c0)] = A[rt][ctk][v];
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const double cop0 = -cbuf[cl * 4 + rq], cop1 = -cbuf[(16 + cl) * 4 + rq];
+    ok = inv4(P, Q) && ok;
+    // A operand of T = P⁻¹R: lane l = (row l%16, k l/16) → P⁻¹[cl][rq] for cl < 4
+    double qa = 0.0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) qa = (cl == i && rq == j) ? Q[4 * i + j] : qa;
+    // column tiles left of the pivot block's are finished (every column's update reads only its own pivot-row
+    // entries, and those of a finished column take no further part): skipped
+    v4f64 T[4];
+#pragma unroll
+    for (int ct = k >> 4; ct < 4; ++ct) {
+      const v4f64 z = {0.0, 0.0, 0.0, 0.0};
+      T[ct] = __builtin_amdgcn_mfma_f64_16x16x4f64(qa, A[rtk][ct][vk], z, 0, 0, 0);
+    }
+#pragma unroll
+    for (int ct = k >> 4; ct < 4; ++ct) {
+      A[0][ct] = __builtin_amdgcn_mfma_f64_16x16x4f64(cop0, T[ct][0], A[0][ct], 0, 0, 0);
+      A[1][ct] = __builtin_amdgcn_mfma_f64_16x16x4f64(cop1, T[ct][0], A[1][ct], 0, 0, 0);
+    }
+#pragma unroll
+    for (int ct = k >> 4; ct < 4; ++ct) A[rtk][ct][vk] = T[ct][0];
+    // the next step's transpose overwrites cbuf (LDS operations of one wave are processed in order)
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+  return ok;
+}
+#endif
+
 // Rebuild of super-row i (next-level index in) from the two eliminations in LDS (sXl = X_{i−1}, sXr = X_{i+1}) and
 // U_{i−1}, U_i, D_i, b_i, on RB waves: 4 waves take two column tiles each, 8 waves one.  keep_u: the rebuilt row
 // still has a right coupling.  Waves w ≥ RB return at once.
@@ -1464,6 +1652,10 @@ __device__ __forceinline__ void cr_rebuild(int w, int lane, const double* sUl, c
     }
 }
 
+// per-wave LDS of an elimination: gj_wave's pivot columns, or gj_mfma's pivot-column transpose (M = 24)
+template <int M>
+constexpr int kPivBuf = (PBA_CR_MFMA && M == 24) ? 128 : M * kCrPivot;
+
 template <int M>
 constexpr size_t cr_level_wave_lds() { return sizeof(double) * (3 * M * M + M + 2 * M * (2 * M + 1)); }
 
@@ -1481,7 +1673,7 @@ constexpr size_t cr_level_wave_lds() { return sizeof(double) * (3 * M * M + M + 
 // cr_level_wave_lds<M>() bytes.  COH: rows read and written with the hand-off accesses of pcr_fused_kernel.
 template <int M, bool PCR, bool COH>
 __device__ __forceinline__ void cr_wave_level(const CrLevel& L, const CrLevel& Ln, int i, int in, int s, int* status,
-                                              double (*piv)[M * kCrPivot], double* smem) {
+                                              double (*piv)[kPivBuf<M>], double* smem) {
   static_assert(2 * M + 1 <= 64, "one wave per elimination");
   constexpr int NC = 2 * M + 1;
   double* sUl = smem;
@@ -1522,6 +1714,34 @@ __device__ __forceinline__ void cr_wave_level(const CrLevel& L, const CrLevel& L
     const int jj = has ? j : i;  // a missing neighbour eliminates a real row and contributes zeros
     const double* D = L.D + (long long)jj * M * M;
     const double* bj = L.b + (long long)jj * M;
+#if PBA_CR_MFMA
+    if constexpr (M == 24) {
+      v4f64 A[2][4];
+      bool ok;
+      if (w == 0) ok = gj_mfma<COH>(D, L.U + (long long)jj * M * M, false, bj, M + 1, lane, piv[0], A);
+      else if (w == 1) ok = gj_mfma<COH>(D, L.U + (long long)i * M * M, true, bj, M + 1, lane, piv[1], A);
+      else ok = gj_mfma<COH>(D, jj + s < L.n ? L.U + (long long)jj * M * M : nullptr, false, nullptr, M, lane, piv[2], A);
+      if (!ok && has && lane == 0) atomicOr(status, 1);
+      // X columns (M … 2M of [D | R1 | b]) → the LDS operands of the rebuild, as the column-per-lane form below does
+      const int cl = lane & 15, rq = lane >> 4;
+      double* xd = sX[w == 0 ? 0 : 1];
+#pragma unroll
+      for (int ct = 1; ct < 4; ++ct) {
+        const int col = 16 * ct + cl;
+        const int dcol = col < M || col > 2 * M || (w == 2 && col == 2 * M) ? -1 : (w == 1 && col < 2 * M ? col - M : col);
+        if (dcol < 0) continue;
+#pragma unroll
+        for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+          for (int v = 0; v < (rt == 0 ? 4 : 2); ++v) {
+            const int row = 16 * rt + rq + 4 * v;
+            xd[row * NC + dcol] = has ? A[rt][ct][v] : 0.0;
+            if (!PCR && w != 0 && has) L.X[(long long)(j / 2) * M * NC + row * NC + dcol] = A[rt][ct][v];
+          }
+      }
+      goto eliminated;
+    }
+#endif
     double a[M];
     bool ok;
     if (w == 0) ok = gj_wave<M, COH>(D, L.U + (long long)jj * M * M, false, bj, M + 1, lane, piv[0], a);
@@ -1540,6 +1760,9 @@ __device__ __forceinline__ void cr_wave_level(const CrLevel& L, const CrLevel& L
       }
     }
   }
+#if PBA_CR_MFMA
+eliminated:
+#endif
 #ifdef PBA_CR_STAMPS
   t1 = wall_clock64();
 #endif
@@ -1560,7 +1783,7 @@ __device__ __forceinline__ void cr_wave_level(const CrLevel& L, const CrLevel& L
 template <int M, bool PCR>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void cr_level_wave_kernel(
     CrLevel L, CrLevel Ln, int s, int* status) {
-  __shared__ __attribute__((aligned(16))) double piv[3][M * kCrPivot];
+  __shared__ __attribute__((aligned(16))) double piv[3][kPivBuf<M>];
   extern __shared__ double smem[];
   const int i = PCR ? (int)blockIdx.x : 2 * (int)blockIdx.x;
   cr_wave_level<M, PCR, false>(L, Ln, i, blockIdx.x, PCR ? s : 1, status, piv, smem);
@@ -1569,7 +1792,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 // The root super-row on one wave (lane 2M carries b; the coupling lanes are empty).
 template <int M>
 __global__ __launch_bounds__(64) void cr_root_wave_kernel(CrLevel L, int* status) {
-  __shared__ __attribute__((aligned(16))) double piv[M * kCrPivot];
+  __shared__ __attribute__((aligned(16))) double piv[kPivBuf<M>];
   double a[M];
   const int lane = threadIdx.x;
   const bool ok = gj_wave<M>(L.D, nullptr, false, L.b, M + 1, lane, piv, a);
@@ -1586,9 +1809,27 @@ __global__ __launch_bounds__(64) void cr_root_wave_kernel(CrLevel L, int* status
 // (out = the step vector, lim = 6N), else the x of the CR level the PCR levels took over from.
 template <int M>
 __global__ __launch_bounds__(64) void pcr_solve_kernel(CrLevel L, double* __restrict__ out, int lim, int* status) {
-  __shared__ __attribute__((aligned(16))) double piv[M * kCrPivot];
-  double a[M];
+  __shared__ __attribute__((aligned(16))) double piv[kPivBuf<M>];
   const int lane = threadIdx.x, i = blockIdx.x;
+#if PBA_CR_MFMA
+  if constexpr (M == 24) {  // x = column 2M of [I | X]: lanes l % 16 = 0 of column tile 3
+    v4f64 A[2][4];
+    if (!gj_mfma<false>(L.D + (long long)i * M * M, nullptr, false, L.b + (long long)i * M, M + 1, lane, piv, A)) {
+      if (lane == 0) atomicOr(status, 1);
+      return;
+    }
+    if ((lane & 15) == 0)
+#pragma unroll
+      for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+        for (int v = 0; v < (rt == 0 ? 4 : 2); ++v) {
+          const int r = 16 * rt + (lane >> 4) + 4 * v;
+          if (i * M + r < lim) out[(long long)i * M + r] = A[rt][3][v];
+        }
+    return;
+  }
+#endif
+  double a[M];
   const bool ok = gj_wave<M>(L.D + (long long)i * M * M, nullptr, false, L.b + (long long)i * M, M + 1, lane, piv, a);
   if (!ok) {
     if (lane == 0) atomicOr(status, 1);
@@ -1647,7 +1888,7 @@ __device__ __forceinline__ CrLevel pcr_fused_level(const PcrFusedArgs& a, int l)
 
 template <int M>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void pcr_fused_kernel(const PcrFusedArgs a) {
-  __shared__ __attribute__((aligned(16))) double piv[3][M * kCrPivot];
+  __shared__ __attribute__((aligned(16))) double piv[3][kPivBuf<M>];
   extern __shared__ double smem[];
   __shared__ unsigned s_task;
   if (threadIdx.x == 0) s_task = atomicAdd(a.counter, 1u) - a.base;
@@ -1771,10 +2012,15 @@ __device__ void se3_exp_mul(const double* T, const double* d, double* out) {
     A = 0.5;
     B = 1.0 / 6.0;
   } else {
-    real = cos(0.5 * th);
-    imag = sin(0.5 * th) / th;
-    A = (1.0 - cos(th)) / th2;
-    B = (th - sin(th)) / (th2 * th);
+    // one sincos of θ/2 (sin θ = 2 sc, 1 − cos θ = 2 s², the latter without cancellation) and one reciprocal of θ
+    // instead of two sincos and three IEEE divisions: the candidate poses' fp64 chain is the update kernel's latency
+    double sh, ch;
+    sincos(0.5 * th, &sh, &ch);
+    const double it = rcp_nr(th);
+    real = ch;
+    imag = sh * it;
+    A = 2.0 * imag * imag;
+    B = (th - 2.0 * sh * ch) * (it * it * it);
   }
   const double qx = imag * w0, qy = imag * w1, qz = imag * w2, qw = real;
   // V υ = υ + A ω×υ + B ω×(ω×υ)
@@ -1788,7 +2034,7 @@ __device__ void se3_exp_mul(const double* T, const double* d, double* out) {
   double rx = aw * qx + ax * qw + ay * qz - az * qy;
   double ry = aw * qy + ay * qw + az * qx - ax * qz;
   double rz = aw * qz + az * qw + ax * qy - ay * qx;
-  const double n = 1.0 / sqrt(rw * rw + rx * rx + ry * ry + rz * rz);
+  const double n = rsqrt_nr(rw * rw + rx * rx + ry * ry + rz * rz);  // (|q| ≈ 1: the seed + correction is ~1 ulp)
   double u0 = ay * tz - az * ty, u1 = az * tx - ax * tz, u2 = ax * ty - ay * tx;
   u0 += u0; u1 += u1; u2 += u2;
   out[0] = rx * n; out[1] = ry * n; out[2] = rz * n; out[3] = rw * n;
@@ -1853,10 +2099,25 @@ __device__ __forceinline__ void candidate_pose(const PoseUpdateArgs& a, int i, d
   }
 }
 
-__device__ __forceinline__ void pose_update_block(const PoseUpdateArgs& a, int blk) {
+__device__ __forceinline__ void pose_update_block(const PoseUpdateArgs& a, const LmView& lv, int blk) {
   const int i = blk * blockDim.x + threadIdx.x;
   double v[4] = {0.0, 0.0, 0.0, 0.0};  // x·g, x·D·x, |T − T_new|², |T_new|²
   double gm = 0.0;
+  {  // the frame's inputs in flight with the record's load, then the done test (uniform)
+    const int ic = min(i, a.n - 1);
+    double in[7 + 18];
+#pragma unroll
+    for (int q = 0; q < 7; ++q) in[q] = a.poses[7 * ic + q];
+#pragma unroll
+    for (int q = 0; q < 6; ++q) {
+      in[7 + q] = a.x[6 * ic + q];
+      in[13 + q] = a.g_dir[6 * ic + q];
+      in[19 + q] = a.Ddiag[6 * ic + q];
+    }
+#pragma unroll
+    for (int q = 0; q < 25; ++q) asm volatile("" ::"v"(in[q]));
+    if (lv.done != 0.0) return;
+  }
   if (i < a.n) {
     double* tn = a.poses_new + 7 * i;
     candidate_pose(a, i, tn);
@@ -1883,10 +2144,7 @@ __device__ __forceinline__ void pose_update_block(const PoseUpdateArgs& a, int b
 
 struct PointUpdateArgs {
   const double* pt_data;
-  const int* pt_first;
-  const int* pt_nblk;
-  const int* pt_orig;
-  const int* pt_host;
+  const int4* pt_rec;
   const int* gn_target;
   const float* blk_schur;
   const float* blk_schur1;  // buffer set 1 (device LM loop)
@@ -1902,19 +2160,33 @@ struct PointUpdateArgs {
 };
 
 // blk: the point workgroup's index among the point workgroups; slot: its reduction slot
-__device__ __forceinline__ void point_update_block(const PointUpdateArgs& a, double lambda, int blk, int slot) {
+// lm: the LM record (done → return before any store; read with the point's first loads, not ahead of them)
+__device__ __forceinline__ void point_update_block(const PointUpdateArgs& a, const double* lm, double lambda, int blk,
+                                                   int slot) {
   const int p = blk * blockDim.x + threadIdx.x;
   double v[4] = {0.0, 0.0, 0.0, 0.0};  // δρ·g, δρ·D·δρ, δρ², ρ_new²
   double gm = 0.0;
+  const LmView lv = lm_view(lm);
+  const int pc = min(p, a.n_points - 1);
+  const int4 pr = a.pt_rec[pc];  // first block, block count, host, original point
+  double pd[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) pd[i] = a.pt_data[(long long)pc * 8 + i];
+  if (lv.done != 0.0) return;  // (uniform: every thread of the workgroup returns)
+#ifdef PBA_UPD_STAMPS
+  long long ts[4];
+  ts[0] = wall_clock64();
+#endif
+  lambda = lm_lambda(lv, lambda);
+  const float* blk_schur = lv.set != 0.0 ? a.blk_schur1 : a.blk_schur;
   if (p < a.n_points) {
-    const double* pd = a.pt_data + (long long)p * 8;
     const double H = pd[0], gl = pd[1];
     const double D = fmin(fmax(H, 1e-6), 1e32);
     const double Hd = H + lambda * D;
-    const int h = a.pt_host[p];
+    const int h = pr.z;
     double s = gl;
     for (int i = 0; i < 6; ++i) s += pd[2 + i] * a.x[6 * h + i];
-    const int fb = a.pt_first[p], nb = a.pt_nblk[p];
+    const int fb = pr.x, nb = pr.y;
     constexpr int kBatch = 4;  // a batch's loads issued together, then summed in block order
     for (int b0 = fb; b0 < fb + nb; b0 += kBatch) {
       float w[kBatch][6];
@@ -1923,7 +2195,7 @@ __device__ __forceinline__ void point_update_block(const PointUpdateArgs& a, dou
       for (int u = 0; u < kBatch; ++u) {
         const int b = min(b0 + u, fb + nb - 1);
         t[u] = a.gn_target[b];
-        const float* q = a.blk_schur + (long long)b * 16 + 8;
+        const float* q = blk_schur + (long long)b * 16 + 8;
 #pragma unroll
         for (int i = 0; i < 6; ++i) w[u][i] = q[i];
       }
@@ -1933,8 +2205,11 @@ __device__ __forceinline__ void point_update_block(const PointUpdateArgs& a, dou
         for (int i = 0; i < 6; ++i) s += (double)w[u][i] * a.x[6 * t[u] + i];
       }
     }
+#ifdef PBA_UPD_STAMPS
+    ts[1] = wall_clock64();
+#endif
     const double dr = Hd > 0.0 ? -s / Hd : 0.0;
-    const int o = a.pt_orig[p];
+    const int o = pr.w;
     const double rn = a.rho[o] + dr;
     a.rho_new[o] = rn;
     a.drho[o] = dr;
@@ -1944,8 +2219,16 @@ __device__ __forceinline__ void point_update_block(const PointUpdateArgs& a, dou
     v[3] = rn * rn;
     gm = fabs(gl);  // ρ has no local parameterisation: |ρ − (ρ − g_ρ)|
   }
+#ifdef PBA_UPD_STAMPS
+  ts[2] = wall_clock64();
+#endif
   double* const dst[4] = {a.red + 2 * slot, a.red + 2 * slot + 1, a.red2 + 2 * slot, a.red2 + 2 * slot + 1};
   wg_reduce_sum_max<4>(v, gm, dst, a.gmax + slot);
+#ifdef PBA_UPD_STAMPS
+  ts[3] = wall_clock64();
+  if (threadIdx.x == 0 && (blk == 0 || blk == 196))
+    printf("updpoint blk=%d loads %lld loop %lld stores %lld reduce %lld\n", blk, ts[0], ts[1] - ts[0], ts[2] - ts[1], ts[3] - ts[2]);
+#endif
 }
 
 struct PairUpdateArgs {
@@ -1965,19 +2248,32 @@ struct PairUpdateArgs {
 __global__ __launch_bounds__(kBlockThreads) void update_kernel(const PoseUpdateArgs pa, PointUpdateArgs qa,
                                                                const PairUpdateArgs ra, int gp, int gq, double lambda,
                                                                const double* __restrict__ lm) {
-  const LmView lv = lm_view(lm);
-  if (lv.done != 0.0) return;  // gated: a trial after the end must not touch the last step (pba_gn_get_step)
-  lambda = lm_lambda(lv, lambda);
-  if (lv.set != 0.0) qa.blk_schur = qa.blk_schur1;
+  // gated: a trial after the end must not touch the last step (pba_gn_get_step).  Each part tests the record after
+  // its own first loads are issued (a test ahead of them cost a memory round trip of its own)
   const int b = blockIdx.x;
+#ifdef PBA_UPD_STAMPS  // timing dissection only: absolute 100-MHz stamps at the start and end of chosen workgroups
+  const long long t0 = wall_clock64();
+  struct Stamp {
+    long long t0;
+    int b;
+    __device__ ~Stamp() {
+      if (threadIdx.x == 0 && (b == 0 || b == 4 || b == 200 || b == 394 || b == 395 || b == 410))
+        printf("updstamp b=%d start %lld end %lld\n", b, t0, wall_clock64());
+    }
+  } stamp{t0, b};
+#endif
+  if (b >= gp && b < gp + gq) {
+    point_update_block(qa, lm, lambda, b - gp, b);
+    return;
+  }
+  const LmView lv = lm_view(lm);
   if (b < gp) {
-    pose_update_block(pa, b);
-  } else if (b < gp + gq) {
-    point_update_block(qa, lambda, b - gp, b);
+    pose_update_block(pa, lv, b);
   } else {
     const int i = (b - gp - gq) * blockDim.x + threadIdx.x;
-    if (i >= ra.n_pairs) return;
-    const int h = ra.pair_host[i], t = ra.pair_target[i];
+    const int ic = min(i, ra.n_pairs - 1);
+    const int h = ra.pair_host[ic], t = ra.pair_target[ic];
+    if (lv.done != 0.0 || i >= ra.n_pairs) return;
     double H[7], T[7];
     candidate_pose(pa, h, H);
     candidate_pose(pa, t, T);
@@ -2149,12 +2445,17 @@ __device__ void trial_sums(const double* __restrict__ red, const double* __restr
   add_small(i_s, ys, ms);
   for (int i = i_s + N; i < S; i += N) add_small(i, r2[i], gmax[i]);
   auto is_max = [](int q) { return q == kTsPoseGMax || q == kTsPtGMax; };
+  // a wave past the update slots holds only candidate-cost sums: its other ten are zeros, not butterflied (the same
+  // totals: only zeros are left out)
+  const bool upd = __builtin_amdgcn_readfirstlane((int)threadIdx.x & ~63) < S;
 #pragma unroll
-  for (int q = 0; q < kTsCount; ++q)
+  for (int q = 0; q < kTsCount; ++q) {
+    if (!upd && q != kTsCost && q != kTsValid) continue;
     for (int m = 32; m >= 1; m >>= 1) {
       const double o = __shfl_xor(v[q], m, 64);
       v[q] = is_max(q) ? fmax(v[q], o) : v[q] + o;
     }
+  }
   if ((threadIdx.x & 63) == 0)
 #pragma unroll
     for (int q = 0; q < kTsCount; ++q) part[q][threadIdx.x >> 6] = v[q];
@@ -2196,10 +2497,12 @@ __global__ __launch_bounds__(kDecideThreads) void lm_decide_kernel(const double*
                                                                    int gc, const int* __restrict__ status,
                                                                    const DecideOpts o, double* __restrict__ lm,
                                                                    double* __restrict__ host_rec, double seq) {
-  if (lm[kLmDone] != 0.0) return;  // a trial enqueued ahead of the one that ended the solve
+  // a trial enqueued ahead of the one that ended the solve returns — tested after the sums, so the record's load is in
+  // flight with the partials' instead of a round trip of its own before them (the partials are always readable)
+  const double done = lm[kLmDone];
   __shared__ double t[kTsCount];
   trial_sums(red, red2, gmax, gp, gq, gc, t);
-  if (threadIdx.x >= 64) return;  // wave 0 publishes; lane 0 decides
+  if (done != 0.0 || threadIdx.x >= 64) return;  // wave 0 publishes; lane 0 decides
   __shared__ double s_rec[kLmFields];
   if (threadIdx.x == 0) {
     lm_decide(t, *status, o, lm);
@@ -2219,10 +2522,10 @@ __global__ __launch_bounds__(kDecideThreads) void dist_sums_kernel(const double*
                                                                    const double* __restrict__ gmax, int gp, int gq, int gc,
                                                                    double gtol, const double* __restrict__ lm,
                                                                    double* __restrict__ tpose, double* __restrict__ Y) {
-  if (lm[kLmDone] != 0.0) return;
+  const double done = lm[kLmDone];  // (tested after the sums, as lm_decide_kernel)
   __shared__ double t[kTsCount];
   trial_sums(red, red2, gmax, gp, gq, gc, t);
-  if (threadIdx.x != 0) return;
+  if (done != 0.0 || threadIdx.x != 0) return;
   for (int q = 0; q < 5; ++q) tpose[q] = t[kTsPoseG + q];
   tpose[5] = t[kTsPtGMax];
   Y[0] = t[kTsPtG];
@@ -2583,6 +2886,11 @@ int gn_prepare(pba_engine* e) {
   PBA_HIP(G.pt_nblk.upload(pnblk, st));
   PBA_HIP(G.pt_orig.upload(porig, st));
   PBA_HIP(G.pt_host.upload(phost, st));
+  {
+    std::vector<int4> prec(ngp);
+    for (int q = 0; q < ngp; ++q) prec[q] = make_int4(pfirst[q], pnblk[q], phost[q], porig[q]);
+    PBA_HIP(G.pt_rec.upload(prec, st));
+  }
   PBA_HIP(G.gn_target.upload(gtgt, st));
   PBA_HIP(G.schur_desc.upload(sdesc, st));
   PBA_HIP(G.schur_aux.upload(saux, st));
@@ -2875,7 +3183,7 @@ void enqueue_updates(pba_engine* e, double lambda, const uint8_t* fixed, int* gp
   const int gr = (e->n_pairs + kBlockThreads - 1) / kBlockThreads;
   PoseUpdateArgs pa{e->poses.p, G.x.p, G.g_dir.p, G.Ddiag.p, fixed, G.poses_new.p, G.red.p, G.red2.p, G.gmax.p, nf};
   // point workgroup q writes reduction slot gp + q, as the separate launches did
-  PointUpdateArgs qa{G.pt_data.p, G.pt_first.p, G.pt_nblk.p, G.pt_orig.p, G.pt_host.p, G.gn_target.p,
+  PointUpdateArgs qa{G.pt_data.p, G.pt_rec.p, G.gn_target.p,
                      G.blk_schur.p, G.blk_schur1.p, G.x.p, fixed, e->rho.p, G.rho_new.p, G.drho.p, G.red.p,
                      G.red2.p, G.gmax.p, G.n_gn_points};
   PairUpdateArgs ra{e->pair_host.p, e->pair_target.p, e->frame_cam.p, e->intr_d.p, G.pairs_new.p, e->n_pairs};

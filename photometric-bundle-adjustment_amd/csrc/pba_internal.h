@@ -241,7 +241,7 @@ __device__ __forceinline__ float huber_weight(float s, float a) {
 // quads of an 8-lane group), row_mirror (the two halves of a 16-lane row), then a swizzle for 32.
 template <int CTRL>
 __device__ __forceinline__ float dpp(float v) {
-  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, true));
 }
 template <int LPB>
 __device__ __forceinline__ float group_sum(float v) {
@@ -700,6 +700,7 @@ struct GnData {
   DevBuf<float> part_lin;        // linearise chunk partials (fp32)
   DevBuf<float> blk_schur1, part_lin1;  // second set: the device LM loop linearises each candidate into the spare
   DevBuf<int> pt_first, pt_nblk, pt_orig;  // GN point → first GN block, block count, original point
+  DevBuf<int4> pt_rec;           // GN point → {first GN block, block count, host frame, original point} (one load)
   DevBuf<int4> schur_desc;       // Schur chunk: first GN point, n points, n local poses, partial offset
   DevBuf<int4> schur_aux;        // Schur chunk: pair list offset, n pairs, first GN block, n blocks
   DevBuf<uchar2> schur_pairs;    // used local pose pairs (a ≤ b) of every Schur chunk
