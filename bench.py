@@ -23,6 +23,7 @@ on-device Gauss-Newton (C4 here, C3 = configs[2] in "gn_c3"); and the C5-style 2
 from __future__ import annotations
 
 import argparse
+import glob
 import importlib
 import json
 import os
@@ -355,6 +356,68 @@ def c5_eval(pb, images, states, steps, warmup, clock_warmup_s, torch, dev_index,
             "pyramid_build_ms": pyr_ms}
 
 
+HEADLINE_KERNEL = "photometric_block_kernel<0, 8, 1, float>"
+
+
+def traffic_probe(args):
+    """--traffic-probe (a child of measure_traffic under rocprofv3 --pmc): the headline launch at 5 HBM-resident
+    states of the same C4 problem, nothing else."""
+    import torch
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(0)
+    pb, images = synth.c4_shard(dev, n_frames=args.frames, n_points=args.points, K=args.targets)
+    eng = engine_mod.Engine(synth.PHOTOMETRIC, synth.PINHOLE, device=0, huber_width=9.0)
+    eng.set_problem(pb, images_device_ptr=images.data_ptr())
+    states = make_states(pb, torch, dev, 7)
+    for i in range(5):
+        eng.evaluate_state_device(states[i % len(states)][0].data_ptr(), states[i % len(states)][1].data_ptr(), True)
+    eng.synchronize()
+    eng.close()
+    print(json.dumps({"probe": "ok", "n_blocks": pb.n_blocks}), flush=True)
+
+
+def measure_traffic(args, n_blocks, timeout_s=150):
+    """HBM bytes per headline launch, measured in this run: two rocprofv3 --pmc passes (FETCH_SIZE, then WRITE_SIZE —
+    separate passes, MI355X_MICROARCH.md: the two do not fit one pass) over a child process running --traffic-probe,
+    raw KB x 1024 (the guide's 2x FETCH correction is calibrated for 16-B streaming reads; these are byte gathers of
+    tiled image lines and the corrected total would exceed the chip's achievable 6.3 TB/s at the measured launch time,
+    DESIGN.md §5).  Returns (bytes, source) or (None, reason)."""
+    import csv
+    import shutil
+    import subprocess
+    import tempfile
+    prof = shutil.which("rocprofv3")
+    if not prof:
+        return None, "rocprofv3 not found"
+    vals = {}
+    env = dict(os.environ, TMPDIR="/tmp")
+    for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
+        with tempfile.TemporaryDirectory(dir="/tmp") as d:
+            cmd = [prof, "--pmc", ctr, "--kernel-include-regex", HEADLINE_KERNEL,
+                   "--output-format", "csv", "-d", d, "-o", "run", "--", sys.executable, os.path.abspath(__file__),
+                   "--traffic-probe", "--frames", str(args.frames), "--points", str(args.points),
+                   "--targets", str(args.targets)]
+            try:
+                r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=timeout_s)
+            except subprocess.TimeoutExpired:
+                return None, f"rocprofv3 --pmc {ctr} pass timed out"
+            if r.returncode != 0:
+                return None, f"rocprofv3 --pmc {ctr} pass failed (rc {r.returncode})"
+            rows = []
+            for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+                rows += [x for x in csv.DictReader(open(f)) if x["Counter_Name"] == ctr]
+            per = {}
+            for x in rows:
+                if HEADLINE_KERNEL in x["Kernel_Name"]:
+                    per[x["Dispatch_Id"]] = per.get(x["Dispatch_Id"], 0.0) + float(x["Counter_Value"])
+            if not per:
+                return None, f"no {ctr} samples for {HEADLINE_KERNEL}"
+            vals[ctr] = sum(per.values()) / len(per) * 1024.0
+    return vals["FETCH_SIZE"] + vals["WRITE_SIZE"], {
+        "source": "measured in this run: rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE passes (child processes), raw KB x 1024",
+        "fetch_bytes": vals["FETCH_SIZE"], "write_bytes": vals["WRITE_SIZE"]}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -371,7 +434,13 @@ def main():
     ap.add_argument("--no-c5", action="store_true", help="skip the C5-style 21-px / fp16 / pyramid measurement")
     ap.add_argument("--no-weak", action="store_true", help="N > 1: skip the weak-scaling leg")
     ap.add_argument("--no-c2", action="store_true", help="skip the C2 Ceres drop-in measurement (configs[1])")
+    ap.add_argument("--no-live-traffic", action="store_true",
+                    help="take roofline.traffic from the committed profiles/ file instead of two rocprofv3 --pmc passes")
+    ap.add_argument("--traffic-probe", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
+    if args.traffic_probe:
+        traffic_probe(args)
+        return
 
     import torch
     import torch.distributed as dist
@@ -447,15 +516,21 @@ def main():
         value = total_blocks * args.steps / elapsed
         bpb = algorithmic_bytes_per_block(pb.P, K, pb.n_frames, pb.n_points, pb.n_blocks)
         achieved = bpb * pb.n_blocks / (kern_us_local * 1e-6) / 1e9
-        traffic = None
-        tf = os.path.join(ROOT, "profiles", "traffic_photometric_block_kernel.json")
-        if os.path.exists(tf):
-            try:
-                tj = json.load(open(tf))
-                if tj.get("n_blocks") == pb.n_blocks and tj.get("P") == pb.P:
-                    traffic = tj.get("hbm_bytes_per_launch")
-            except Exception:
-                traffic = None
+        traffic, traffic_info = None, None
+        if world == 1 and not args.no_live_traffic:
+            traffic, traffic_info = measure_traffic(args, pb.n_blocks)
+        if traffic is None:  # fall back to the committed profile of the same workload
+            reason = traffic_info
+            tf = os.path.join(ROOT, "profiles", "traffic_photometric_block_kernel.json")
+            if os.path.exists(tf):
+                try:
+                    tj = json.load(open(tf))
+                    if tj.get("n_blocks") == pb.n_blocks and tj.get("P") == pb.P:
+                        traffic = tj.get("hbm_bytes_per_launch")
+                        traffic_info = {"source": "profiles/traffic_photometric_block_kernel.json (committed rocprofv3 passes)",
+                                        "live_measurement": reason}
+                except Exception:
+                    traffic = None
         cpu = None
         c2 = None
         if world == 1 and not args.no_cpu_baseline:
@@ -497,6 +572,7 @@ def main():
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS,
                 "traffic": traffic,
+                "traffic_detail": traffic_info,
                 "bytes_per_block_alg": bpb,
                 "kernel_avg_us": kern_us_local,
             },

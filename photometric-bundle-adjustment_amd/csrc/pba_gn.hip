@@ -122,6 +122,7 @@ struct LinArgs {
   int n_chunks;
   const double* lm;         // LM record: skip when the solve is done; spare: write the set the record does not hold
   bool spare;
+  int n_gn_blocks;          // the W_t plane of blk_schur starts at 8 · n_gn_blocks floats
 };
 
 // ------------------------------------------------------------------------------------------------
@@ -274,6 +275,9 @@ void linearize_kernel(const KernelArgs a, const LinArgs g) {
     // point-elimination data x̃_ρ·x̃_c → [H_ρρ, g_ρ, W_h(6), W_t(6), 0, 0] at its GN position (schur_kernel walks
     // them point by point); the block's products are then added to its target run's sum
     const int pc = lane - 48, pq = pc < 12 ? pc + 2 : (pc < 14 ? pc - 12 : pc);
+    // two planes (blk_schur layout): [H_ρρ, g_ρ, W_h] at 8·b, [W_t, 0, 0] at 8·(n + b) — the update kernel reads only
+    // the second, half the lines of the interleaved record
+    const long long pdst = pq < 8 ? pq : 8ll * g.n_gn_blocks + (pq - 8);
     f32x4 tacc = {0.0f, 0.0f, 0.0f, 0.0f};
     int cur = lo;
     float pdat[BW];  // the blocks' point-elimination data (lanes 48-63), stored after the loop in one exec region
@@ -299,7 +303,7 @@ void linearize_kernel(const KernelArgs a, const LinArgs g) {
     if (pc >= 0) {
 #pragma unroll
       for (int b = 0; b < BW; ++b)
-        if (b < nbw) blk_schur[(long long)__builtin_amdgcn_readlane(gpos, b * LPB) * 16 + pq] = pdat[b];
+        if (b < nbw) blk_schur[(long long)__builtin_amdgcn_readlane(gpos, b * LPB) * 8 + pdst] = pdat[b];
     }
     if (lane == 0) {
       s_wlo[wave] = lo;
@@ -357,12 +361,12 @@ struct SchurArgs {
   const int4* desc;       // first GN point, n points, n local poses, partial offset (doubles)
   const int4* aux;        // pair list offset, n pairs, first GN block, n blocks (the last two: diagnostics)
   const uchar2* pairs;    // (a, b) local pose pairs, a ≤ b
-  const int* pt_first;
-  const int* pt_nblk;
+  const int2* pt_fb;       // chunk c's point p → {first GN block, block count} at c · SCHUR_PTS + p (padded table)
   const uint8_t* blk_lv;
   const float* blk_schur;
   const float* blk_schur1;  // buffer set 1 (device LM loop)
   double* part_schur;
+  int n_gn_blocks;          // blk_schur's W_t plane offset / 8
   double* pt_data;        // per GN point [H_ρρ, g_ρ, W_h(6)] (undamped)
   int n_chunks;
   const double* lm;       // LM record (λ, set; the loop's or GnData::lm_idle)
@@ -384,22 +388,44 @@ __global__ __launch_bounds__(kBlockThreads) void schur_kernel(const SchurArgs g,
   __shared__ double s_inv[SCHUR_PTS], s_gl[SCHUR_PTS];
   const int c = blockIdx.x;
   if (c >= g.n_chunks) return;  // (not gated by the record's done flag: a trial after the end only wastes time here)
+  // Memory rounds (each dependent one is ~1.7 µs here): 1 — the record, the chunk descriptors, the chunk's point
+  // records (padded per-chunk table) and the accept copy's sources; 2 — the points' block data (and the copied ρ);
+  // the accept copy's stores come last, so no load of the chunk waits behind them (loads and stores share vmcnt).
   const LmView lv = lm_view(g.lm);
-  if (g.poses && lv.accept != 0.0) {  // the last trial's accept (same copies as lm_accept_kernel)
+  const int4 d = g.desc[c];
+  const int4 ax = g.aux[c];
+  constexpr int kPtIter = (SCHUR_PTS + kBlockThreads / 4 - 1) / (kBlockThreads / 4);
+  int2 prec[kPtIter];
+#pragma unroll
+  for (int it = 0; it < kPtIter; ++it)
+    prec[it] = g.pt_fb[(long long)c * SCHUR_PTS + it * (kBlockThreads / 4) + (threadIdx.x >> 2)];
+  // the last trial's accept (the copies of lm_accept_kernel): one element per thread (the grid covers them; a
+  // grid-stride tail otherwise)
+  const bool accepted = g.poses && lv.accept != 0.0;
+  const int ia = blockIdx.x * blockDim.x + threadIdx.x;
+  double pnew = 0.0, rnew = 0.0;
+  int oa = 0;
+  if (g.poses) {
+    pnew = g.poses_new[min(ia, g.n_pose_d - 1)];
+    oa = g.pt_orig[min(ia, g.n_gn_points - 1)];
+  }
+  lambda = lm_lambda(lv, lambda);
+  const float* const blk_schur = lv.set != 0.0 ? g.blk_schur1 : g.blk_schur;
+  if (g.poses) rnew = g.rho_new[oa];
+  auto finish_accept = [&]() {  // after the chunk's stores
+    if (!accepted) return;
+    if (ia < g.n_pose_d) g.poses[ia] = pnew;
+    if (ia < g.n_gn_points) g.rho[oa] = rnew;
     const int n = max(g.n_pose_d, g.n_gn_points);
-    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    for (int i = ia + gridDim.x * blockDim.x; i < n; i += gridDim.x * blockDim.x) {
       if (i < g.n_pose_d) g.poses[i] = g.poses_new[i];
       if (i < g.n_gn_points) {
         const int o = g.pt_orig[i];
         g.rho[o] = g.rho_new[o];
       }
     }
-  }
-  lambda = lm_lambda(lv, lambda);
-  const float* const blk_schur = lv.set != 0.0 ? g.blk_schur1 : g.blk_schur;
-  const int4 d = g.desc[c];
+  };
   const int first = d.x, npt = d.y, nv = d.z, poff = d.w;
-  const int4 ax = g.aux[c];
   float (*W)[6] = reinterpret_cast<float (*)[6]>(W_dyn);
   for (int i = threadIdx.x; i < npt * nv * 6; i += kBlockThreads) (&W[0][0])[i] = 0.0f;
   __syncthreads();
@@ -407,10 +433,12 @@ __global__ __launch_bounds__(kBlockThreads) void schur_kernel(const SchurArgs g,
   // q = 0: H_ρρ, g_ρ, W_h[0..1]   q = 1: W_h[2..5]   q = 2: W_t[0..3] → W[p][lv]   q = 3: W_t[4..5] → W[p][lv]
   // (staging the chunk's records in LDS block-parallel instead measured slower: 23 → 35 µs at C4, its LDS halves the
   // resident workgroups)
-  for (int p0 = 0; p0 < npt; p0 += kBlockThreads / 4) {
+#pragma unroll
+  for (int it = 0; it < kPtIter; ++it) {
+    const int p0 = it * (kBlockThreads / 4);
     const int p = p0 + (threadIdx.x >> 2), q = threadIdx.x & 3, gp = first + p;
     if (p < npt) {
-      const int fb = g.pt_first[gp], nb = g.pt_nblk[gp];
+      const int fb = prec[it].x, nb = prec[it].y;
       double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
       constexpr int kBatch = 8;  // every load of a batch issued before the first use: one memory round trip per batch
       for (int b0 = fb; b0 < fb + nb; b0 += kBatch) {
@@ -419,7 +447,7 @@ __global__ __launch_bounds__(kBlockThreads) void schur_kernel(const SchurArgs g,
 #pragma unroll
         for (int u = 0; u < kBatch; ++u) {
           const int b = min(b0 + u, fb + nb - 1);
-          v[u] = reinterpret_cast<const float4*>(blk_schur + (long long)b * 16)[q];
+          v[u] = *reinterpret_cast<const float4*>(blk_schur + (long long)((q >> 1) * g.n_gn_blocks + b) * 8 + 4 * (q & 1));
           lv[u] = q < 2 ? 0 : g.blk_lv[b];
         }
 #pragma unroll
@@ -498,6 +526,7 @@ __global__ __launch_bounds__(kBlockThreads) void schur_kernel(const SchurArgs g,
         g.part_schur[(long long)poff + ax.y * 36 + r] = acc[v];
       }
     }
+    finish_accept();
     return;
   }
   const int nout = ax.y * 36 + nv * 6;
@@ -514,6 +543,7 @@ __global__ __launch_bounds__(kBlockThreads) void schur_kernel(const SchurArgs g,
     }
     g.part_schur[(long long)poff + o] = acc;
   }
+  finish_accept();
 }
 
 struct AsmArgs {
@@ -548,7 +578,9 @@ struct AsmArgs {
 
 // Fixed-order sums over a contribution list (total, and the part that is not a Schur term — the undamped
 // JᵀJ diagonal / direct gradient).  The list entries and their values are gathered 8 at a time so eight
-// independent loads are in flight per lane instead of one dependent index → value chain per term.
+// independent loads are in flight per lane instead of one dependent index → value chain per term.  (16 at a time with
+// the next batch's entries loaded beside the current batch's values measured slower: 12.8 → 15.0 µs at C4, 128
+// VGPRs and twice the clamped loads of the short off-diagonal lists.)
 constexpr int GATHER = 8;
 __device__ __forceinline__ void contrib_sums(const AsmArgs& a, const int2* __restrict__ list, int beg, int end, int e,
                                              int et, double& sum, double& dsum) {
@@ -1780,13 +1812,32 @@ eliminated:
 #endif
 }
 
+// out != nullptr (the last PCR level): the workgroup then also solves its decoupled row, x_i = D'_i⁻¹ b'_i, from the
+// rows it has just written (read back with L1-bypassing loads after every wave's stores completed) — pcr_solve_kernel's
+// work without its launch boundary and its reload of the level (out / lim as pcr_solve_kernel).
 template <int M, bool PCR>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void cr_level_wave_kernel(
-    CrLevel L, CrLevel Ln, int s, int* status) {
+    CrLevel L, CrLevel Ln, int s, int* status, double* __restrict__ out, int lim) {
   __shared__ __attribute__((aligned(16))) double piv[3][kPivBuf<M>];
   extern __shared__ double smem[];
   const int i = PCR ? (int)blockIdx.x : 2 * (int)blockIdx.x;
   cr_wave_level<M, PCR, false>(L, Ln, i, blockIdx.x, PCR ? s : 1, status, piv, smem);
+  if (!PCR || !out) return;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's row stores have completed
+  __syncthreads();
+  if (threadIdx.x >= 64) return;
+  const int lane = threadIdx.x;
+  double a[M];
+  const bool ok = gj_wave<M, true>(Ln.D + (long long)i * M * M, nullptr, false, Ln.b + (long long)i * M, M + 1, lane,
+                                   piv[0], a);
+  if (!ok) {
+    if (lane == 0) atomicOr(status, 1);
+    return;
+  }
+  if (lane == 2 * M)
+#pragma unroll
+    for (int r = 0; r < M; ++r)
+      if (i * M + r < lim) out[(long long)i * M + r] = a[r];
 }
 
 // The root super-row on one wave (lane 2M carries b; the coupling lanes are empty).
@@ -2090,12 +2141,44 @@ struct PoseUpdateArgs {
   int n;
 };
 
-// candidate pose of frame i: T·exp(δ_i), or T for a constant frame
-__device__ __forceinline__ void candidate_pose(const PoseUpdateArgs& a, int i, double* out) {
-  if (a.fixed[i]) {
-    for (int q = 0; q < 7; ++q) out[q] = a.poses[7 * i + q];
+
+// Frame i's update inputs, all loaded in one memory round (every dependent round trip is ~1.7 µs in these kernels):
+// the pose, the step, the gradient direction, the LM diagonal and the constant flag.
+struct FrameIn {
+  double T[7], x[6], g[6], D[6];
+  bool fixed;
+};
+__device__ __forceinline__ FrameIn frame_in(const PoseUpdateArgs& a, int i, bool grad) {
+  FrameIn f;
+  const double* P = a.poses + 7 * i;
+#pragma unroll
+  for (int q = 0; q < 7; ++q) f.T[q] = P[q];
+  const double2* X = reinterpret_cast<const double2*>(a.x + 6 * i);
+  const double2* G = reinterpret_cast<const double2*>(a.g_dir + 6 * i);
+  const double2* Dd = reinterpret_cast<const double2*>(a.Ddiag + 6 * i);
+#pragma unroll
+  for (int q = 0; q < 3; ++q) {
+    const double2 xv = X[q];
+    f.x[2 * q] = xv.x;
+    f.x[2 * q + 1] = xv.y;
+    if (grad) {
+      const double2 gv = G[q], dv = Dd[q];
+      f.g[2 * q] = gv.x;
+      f.g[2 * q + 1] = gv.y;
+      f.D[2 * q] = dv.x;
+      f.D[2 * q + 1] = dv.y;
+    }
+  }
+  f.fixed = a.fixed[i] != 0;
+  return f;
+}
+// candidate pose T·exp(δ), or T for a constant frame
+__device__ __forceinline__ void candidate_pose(const FrameIn& f, double* out) {
+  if (f.fixed) {
+#pragma unroll
+    for (int q = 0; q < 7; ++q) out[q] = f.T[q];
   } else {
-    se3_exp_mul(a.poses + 7 * i, a.x + 6 * i, out);
+    se3_exp_mul(f.T, f.x, out);
   }
 }
 
@@ -2103,38 +2186,29 @@ __device__ __forceinline__ void pose_update_block(const PoseUpdateArgs& a, const
   const int i = blk * blockDim.x + threadIdx.x;
   double v[4] = {0.0, 0.0, 0.0, 0.0};  // x·g, x·D·x, |T − T_new|², |T_new|²
   double gm = 0.0;
-  {  // the frame's inputs in flight with the record's load, then the done test (uniform)
-    const int ic = min(i, a.n - 1);
-    double in[7 + 18];
-#pragma unroll
-    for (int q = 0; q < 7; ++q) in[q] = a.poses[7 * ic + q];
-#pragma unroll
-    for (int q = 0; q < 6; ++q) {
-      in[7 + q] = a.x[6 * ic + q];
-      in[13 + q] = a.g_dir[6 * ic + q];
-      in[19 + q] = a.Ddiag[6 * ic + q];
-    }
-#pragma unroll
-    for (int q = 0; q < 25; ++q) asm volatile("" ::"v"(in[q]));
-    if (lv.done != 0.0) return;
-  }
+  const FrameIn f = frame_in(a, min(i, a.n - 1), true);  // in flight with the record's load; then the done test
+  if (lv.done != 0.0) return;  // (uniform)
   if (i < a.n) {
-    double* tn = a.poses_new + 7 * i;
-    candidate_pose(a, i, tn);
-    if (!a.fixed[i]) {
-      const double* T = a.poses + 7 * i;
+    double tn[7];
+    candidate_pose(f, tn);
+    double* out = a.poses_new + 7 * i;
+#pragma unroll
+    for (int q = 0; q < 7; ++q) out[q] = tn[q];
+    if (!f.fixed) {
       double ng[6], tg[7];
+#pragma unroll
       for (int r = 0; r < 6; ++r) {
-        v[0] += a.x[6 * i + r] * a.g_dir[6 * i + r];
-        v[1] += a.x[6 * i + r] * a.x[6 * i + r] * a.Ddiag[6 * i + r];
-        ng[r] = -a.g_dir[6 * i + r];
+        v[0] += f.x[r] * f.g[r];
+        v[1] += f.x[r] * f.x[r] * f.D[r];
+        ng[r] = -f.g[r];
       }
-      se3_exp_mul(T, ng, tg);  // Plus(x, −gradient)
+      se3_exp_mul(f.T, ng, tg);  // Plus(x, −gradient)
+#pragma unroll
       for (int q = 0; q < 7; ++q) {
-        const double d = tn[q] - T[q];
+        const double d = tn[q] - f.T[q];
         v[2] += d * d;
         v[3] += tn[q] * tn[q];
-        gm = fmax(gm, fabs(T[q] - tg[q]));
+        gm = fmax(gm, fabs(f.T[q] - tg[q]));
       }
     }
   }
@@ -2145,9 +2219,11 @@ __device__ __forceinline__ void pose_update_block(const PoseUpdateArgs& a, const
 struct PointUpdateArgs {
   const double* pt_data;
   const int4* pt_rec;
+  const int4* pt_tgt;
   const int* gn_target;
   const float* blk_schur;
   const float* blk_schur1;  // buffer set 1 (device LM loop)
+  int n_gn_blocks;          // blk_schur's W_t plane offset / 8
   const double* x;
   const uint8_t* fixed;
   const double* rho;
@@ -2169,9 +2245,14 @@ __device__ __forceinline__ void point_update_block(const PointUpdateArgs& a, con
   const LmView lv = lm_view(lm);
   const int pc = min(p, a.n_points - 1);
   const int4 pr = a.pt_rec[pc];  // first block, block count, host, original point
+  const int4 pt4 = a.pt_tgt[pc];  // the targets of its first four blocks
   double pd[8];
 #pragma unroll
-  for (int i = 0; i < 8; ++i) pd[i] = a.pt_data[(long long)pc * 8 + i];
+  for (int i = 0; i < 4; ++i) {
+    const double2 d2 = reinterpret_cast<const double2*>(a.pt_data + (long long)pc * 8)[i];
+    pd[2 * i] = d2.x;
+    pd[2 * i + 1] = d2.y;
+  }
   if (lv.done != 0.0) return;  // (uniform: every thread of the workgroup returns)
 #ifdef PBA_UPD_STAMPS
   long long ts[4];
@@ -2184,26 +2265,44 @@ __device__ __forceinline__ void point_update_block(const PointUpdateArgs& a, con
     const double D = fmin(fmax(H, 1e-6), 1e32);
     const double Hd = H + lambda * D;
     const int h = pr.z;
+    // vector loads (16 B) and every load of a batch in flight before the first use: the target steps' loads used to sit
+    // behind a data-dependent break (one memory round trip per block) and 4-B / 8-B scalar loads of scattered rows
+    auto x6 = [&](int f, double* o) {
+      const double2* q = reinterpret_cast<const double2*>(a.x + 6 * f);
+#pragma unroll
+      for (int i = 0; i < 3; ++i) {
+        const double2 d2 = q[i];
+        o[2 * i] = d2.x;
+        o[2 * i + 1] = d2.y;
+      }
+    };
+    double xh[6];
+    x6(h, xh);
     double s = gl;
-    for (int i = 0; i < 6; ++i) s += pd[2 + i] * a.x[6 * h + i];
+    for (int i = 0; i < 6; ++i) s += pd[2 + i] * xh[i];
     const int fb = pr.x, nb = pr.y;
     constexpr int kBatch = 4;  // a batch's loads issued together, then summed in block order
     for (int b0 = fb; b0 < fb + nb; b0 += kBatch) {
       float w[kBatch][6];
       int t[kBatch];
+      const bool first = b0 == fb;  // the first batch's targets came with the point record
 #pragma unroll
       for (int u = 0; u < kBatch; ++u) {
         const int b = min(b0 + u, fb + nb - 1);
-        t[u] = a.gn_target[b];
-        const float* q = blk_schur + (long long)b * 16 + 8;
-#pragma unroll
-        for (int i = 0; i < 6; ++i) w[u][i] = q[i];
+        t[u] = first ? (u == 0 ? pt4.x : u == 1 ? pt4.y : u == 2 ? pt4.z : pt4.w) : a.gn_target[b];
+        const float* wt = blk_schur + (long long)(a.n_gn_blocks + b) * 8;  // the W_t plane
+        const float4 q4 = *reinterpret_cast<const float4*>(wt);
+        const float2 q2 = *reinterpret_cast<const float2*>(wt + 4);
+        w[u][0] = q4.x; w[u][1] = q4.y; w[u][2] = q4.z; w[u][3] = q4.w; w[u][4] = q2.x; w[u][5] = q2.y;
       }
+      double xt[kBatch][6];
 #pragma unroll
-      for (int u = 0; u < kBatch; ++u) {
-        if (b0 + u >= fb + nb) break;
-        for (int i = 0; i < 6; ++i) s += (double)w[u][i] * a.x[6 * t[u] + i];
-      }
+      for (int u = 0; u < kBatch; ++u) x6(t[u], xt[u]);
+#pragma unroll
+      for (int u = 0; u < kBatch; ++u)
+        if (b0 + u < fb + nb)
+#pragma unroll
+          for (int i = 0; i < 6; ++i) s += (double)w[u][i] * xt[u][i];
     }
 #ifdef PBA_UPD_STAMPS
     ts[1] = wall_clock64();
@@ -2232,9 +2331,7 @@ __device__ __forceinline__ void point_update_block(const PointUpdateArgs& a, con
 }
 
 struct PairUpdateArgs {
-  const int* pair_host;
-  const int* pair_target;
-  const int* frame_cam;
+  const int4* pair_rec;  // {host, target, host camera, target camera}
   const double* cams;
   PairRec* pairs_new;  // nullptr: no candidate pair table (geometric engines form theirs in the cost path too)
   int n_pairs;
@@ -2270,17 +2367,33 @@ __global__ __launch_bounds__(kBlockThreads) void update_kernel(const PoseUpdateA
   if (b < gp) {
     pose_update_block(pa, lv, b);
   } else {
+    // two memory rounds: the pair record, then both frames' inputs and both cameras' constants together
     const int i = (b - gp - gq) * blockDim.x + threadIdx.x;
-    const int ic = min(i, ra.n_pairs - 1);
-    const int h = ra.pair_host[ic], t = ra.pair_target[ic];
+    const int4 pr = ra.pair_rec[min(i, ra.n_pairs - 1)];
+    const FrameIn fh = frame_in(pa, pr.x, false), ft = frame_in(pa, pr.y, false);
+    double hk[kCamK], tk[kCamK];
+#pragma unroll
+    for (int j = 0; j < kCamK; ++j) {
+      hk[j] = ra.cams[kCamD * pr.z + kCamHk + j];
+      tk[j] = ra.cams[kCamD * pr.w + j];
+    }
     if (lv.done != 0.0 || i >= ra.n_pairs) return;
     double H[7], T[7];
-    candidate_pose(pa, h, H);
-    candidate_pose(pa, t, T);
+    candidate_pose(fh, H);
+    candidate_pose(ft, T);
     PairRec r;
     pair_rotation(H, T, r);
     pair_translation(H, T, r);
-    pair_cameras(ra.cams, h, t, ra.frame_cam[h], ra.frame_cam[t], r);
+    r.host_cam = pr.z;
+    r.target_cam = pr.w;
+    r.target = pr.y;
+    r.host = pr.x;
+#pragma unroll
+    for (int j = 0; j < kCamK; ++j) {
+      r.hk[j] = hk[j];
+      r.tk[j] = tk[j];
+    }
+    camera_kf(tk, r.kf);
     ra.pairs_new[i] = r;
   }
 }
@@ -2795,6 +2908,12 @@ int gn_prepare(pba_engine* e) {
   }
   G.schur_doubles = soff;
   G.n_schur = (int)sdesc.size();
+  {  // chunk c's point p → {first GN block, block count} at c · SCHUR_PTS + p (schur_kernel reads it with its descriptor)
+    std::vector<int2> fbt((size_t)G.n_schur * SCHUR_PTS, make_int2(0, 0));
+    for (int c = 0; c < G.n_schur; ++c)
+      for (int q = 0; q < sdesc[c].y; ++q) fbt[(size_t)c * SCHUR_PTS + q] = make_int2(pfirst[sdesc[c].x + q], pnblk[sdesc[c].x + q]);
+    PBA_HIP(G.pt_fb.upload(fbt, e->stream));
+  }
   // reduced camera system structure: lower blocks (i ≥ j)
   std::map<std::pair<int, int>, std::vector<int2>> contrib;
   std::vector<std::vector<int2>> gcon(nf);
@@ -2887,9 +3006,21 @@ int gn_prepare(pba_engine* e) {
   PBA_HIP(G.pt_orig.upload(porig, st));
   PBA_HIP(G.pt_host.upload(phost, st));
   {
-    std::vector<int4> prec(ngp);
-    for (int q = 0; q < ngp; ++q) prec[q] = make_int4(pfirst[q], pnblk[q], phost[q], porig[q]);
+    std::vector<int4> prec(ngp), ptgt(ngp);
+    for (int q = 0; q < ngp; ++q) {
+      prec[q] = make_int4(pfirst[q], pnblk[q], phost[q], porig[q]);
+      int t4[4] = {0, 0, 0, 0};
+      for (int u = 0; u < 4 && u < pnblk[q]; ++u) t4[u] = gtgt[pfirst[q] + u];
+      ptgt[q] = make_int4(t4[0], t4[1], t4[2], t4[3]);
+    }
     PBA_HIP(G.pt_rec.upload(prec, st));
+    PBA_HIP(G.pt_tgt.upload(ptgt, st));
+    std::vector<int4> parec(std::max(e->n_pairs, 1), make_int4(0, 0, 0, 0));
+    for (int q = 0; q < e->n_pairs; ++q) {
+      const int h = e->pair_host_h[q], t = e->pair_target_h[q];
+      parec[q] = make_int4(h, t, e->frame_cam_h[h], e->frame_cam_h[t]);
+    }
+    PBA_HIP(G.pair_rec.upload(parec, st));
   }
   PBA_HIP(G.gn_target.upload(gtgt, st));
   PBA_HIP(G.schur_desc.upload(sdesc, st));
@@ -3046,7 +3177,7 @@ int linearize(pba_engine* e, double* cost, const double* lm = nullptr, const Pai
     pairs = e->pairs.p;
   }
   const KernelArgs ka = make_kernel_args(e, pairs, rho ? rho : e->rho.p);
-  LinArgs la{G.lin_rec.p, G.blk_schur1.p, G.part_lin1.p, wg_red, G.chunk_desc.p, G.blk_schur.p, G.part_lin.p, G.n_chunks, lm ? lm : G.lm_idle.p, lm != nullptr};
+  LinArgs la{G.lin_rec.p, G.blk_schur1.p, G.part_lin1.p, wg_red, G.chunk_desc.p, G.blk_schur.p, G.part_lin.p, G.n_chunks, lm ? lm : G.lm_idle.p, lm != nullptr, e->n_blocks};
   if (e->opt.residual_kind == PBA_RESIDUAL_PHOTOMETRIC) launch_linearize_photometric(e, ka, la);
   else launch_linearize_geometric(e, ka, la);
   PBA_HIP(hipGetLastError());
@@ -3104,7 +3235,8 @@ void cr_solve(pba_engine* e, bool build) {
   for (int l = 0; l < c; ++l) {
     CrLevel L = cr_level(G, l), Ln = cr_level(G, l + 1);
     if constexpr (2 * M + 1 <= 64) {
-      cr_level_wave_kernel<M, false><<<(L.n + 1) / 2, 256, cr_level_wave_lds<M>(), e->stream>>>(L, Ln, 1, G.status.p);
+      cr_level_wave_kernel<M, false><<<(L.n + 1) / 2, 256, cr_level_wave_lds<M>(), e->stream>>>(L, Ln, 1, G.status.p,
+                                                                                               nullptr, 0);
     } else
       cr_level_kernel<M><<<(L.n + 1) / 2, 2 * kCrOddThreads<M>, cr_level_lds<M>(), e->stream>>>(L, Ln, G.status.p);
   }
@@ -3138,16 +3270,18 @@ void cr_solve(pba_engine* e, bool build) {
     } else if (G.cr_pcr >= 0) {
       CrLevel src = cr_level(G, c);
       const int n = src.n;
-      int pi = 0;
-      for (int s = 1; s < n; s *= 2, pi ^= 1) {
-        CrLevel dst = pcr_level(G, pi);
-        cr_level_wave_kernel<M, true><<<n, 256, cr_level_wave_lds<M>(), e->stream>>>(src, dst, s, G.status.p);
-        src = dst;
-      }
       solved = c == 0;
       double* out = solved ? G.x.p : cr_level(G, c).x;
       const int lim = solved ? 6 * e->n_frames : n * M;
-      pcr_solve_kernel<M><<<n, 64, 0, e->stream>>>(src, out, lim, G.status.p);
+      int pi = 0;
+      for (int s = 1; s < n; s *= 2, pi ^= 1) {  // the last level also solves the decoupled rows
+        CrLevel dst = pcr_level(G, pi);
+        const bool last = 2 * s >= n;
+        cr_level_wave_kernel<M, true><<<n, 256, cr_level_wave_lds<M>(), e->stream>>>(src, dst, s, G.status.p,
+                                                                                     last ? out : nullptr, lim);
+        src = dst;
+      }
+      if (n <= 1) pcr_solve_kernel<M><<<n, 64, 0, e->stream>>>(src, out, lim, G.status.p);
     } else {
       cr_root_wave_kernel<M><<<1, 64, 0, e->stream>>>(cr_level(G, nl - 1), G.status.p);
     }
@@ -3183,10 +3317,10 @@ void enqueue_updates(pba_engine* e, double lambda, const uint8_t* fixed, int* gp
   const int gr = (e->n_pairs + kBlockThreads - 1) / kBlockThreads;
   PoseUpdateArgs pa{e->poses.p, G.x.p, G.g_dir.p, G.Ddiag.p, fixed, G.poses_new.p, G.red.p, G.red2.p, G.gmax.p, nf};
   // point workgroup q writes reduction slot gp + q, as the separate launches did
-  PointUpdateArgs qa{G.pt_data.p, G.pt_rec.p, G.gn_target.p,
-                     G.blk_schur.p, G.blk_schur1.p, G.x.p, fixed, e->rho.p, G.rho_new.p, G.drho.p, G.red.p,
+  PointUpdateArgs qa{G.pt_data.p, G.pt_rec.p, G.pt_tgt.p, G.gn_target.p,
+                     G.blk_schur.p, G.blk_schur1.p, e->n_blocks, G.x.p, fixed, e->rho.p, G.rho_new.p, G.drho.p, G.red.p,
                      G.red2.p, G.gmax.p, G.n_gn_points};
-  PairUpdateArgs ra{e->pair_host.p, e->pair_target.p, e->frame_cam.p, e->intr_d.p, G.pairs_new.p, e->n_pairs};
+  PairUpdateArgs ra{G.pair_rec.p, e->intr_d.p, G.pairs_new.p, e->n_pairs};
   update_kernel<<<gp + gq + gr, kBlockThreads, 0, e->stream>>>(pa, qa, ra, gp, gq, lambda, lm ? lm : G.lm_idle.p);
   G.pairs_new_fresh = true;
   *gp_out = gp;
@@ -3248,8 +3382,8 @@ void schur_lds_limit(const GnData& G) {
 int enqueue_solve(pba_engine* e, double lambda, const double* lm = nullptr) {
   GnData& G = e->gn;
   const int nf = e->n_frames;
-  SchurArgs sa{G.schur_desc.p, G.schur_aux.p, G.schur_pairs.p, G.pt_first.p, G.pt_nblk.p, G.blk_lv.p,
-               G.blk_schur.p, G.blk_schur1.p, G.part_schur.p, G.pt_data.p, G.n_schur, lm ? lm : G.lm_idle.p,
+  SchurArgs sa{G.schur_desc.p, G.schur_aux.p, G.schur_pairs.p, G.pt_fb.p, G.blk_lv.p,
+               G.blk_schur.p, G.blk_schur1.p, G.part_schur.p, e->n_blocks, G.pt_data.p, G.n_schur, lm ? lm : G.lm_idle.p,
                lm ? e->poses.p : nullptr, G.poses_new.p, e->rho.p, G.rho_new.p, G.pt_orig.p, 7 * nf, G.n_gn_points};
   schur_lds_limit(G);
   schur_kernel<<<G.n_schur, kBlockThreads, G.schur_lds, e->stream>>>(sa, lambda);
@@ -3388,8 +3522,8 @@ int step_export(pba_engine* e, double lambda, int band, double* X) {
   int K;
   if (int rc = exchange_K(e, band, &K)) return rc;
   const int nf = e->n_frames;
-  SchurArgs sa{G.schur_desc.p, G.schur_aux.p, G.schur_pairs.p, G.pt_first.p, G.pt_nblk.p, G.blk_lv.p,
-               G.blk_schur.p, G.blk_schur1.p, G.part_schur.p, G.pt_data.p, G.n_schur, G.lm_idle.p,
+  SchurArgs sa{G.schur_desc.p, G.schur_aux.p, G.schur_pairs.p, G.pt_fb.p, G.blk_lv.p,
+               G.blk_schur.p, G.blk_schur1.p, G.part_schur.p, e->n_blocks, G.pt_data.p, G.n_schur, G.lm_idle.p,
                nullptr, nullptr, nullptr, nullptr, nullptr, 0, 0};
   schur_lds_limit(G);
   if (G.n_schur > 0) schur_kernel<<<G.n_schur, kBlockThreads, G.schur_lds, e->stream>>>(sa, lambda);
@@ -3712,8 +3846,8 @@ int lm_loop_single(pba_engine* e, const pba_solver_options* o, pba_solver_summar
 int dist_trial(pba_engine* e, const Collective& coll, const DecideOpts& dopt, double* X, int K, double seq) {
   GnData& G = e->gn;
   const int nf = e->n_frames;
-  SchurArgs sa{G.schur_desc.p, G.schur_aux.p, G.schur_pairs.p, G.pt_first.p, G.pt_nblk.p, G.blk_lv.p,
-               G.blk_schur.p, G.blk_schur1.p, G.part_schur.p, G.pt_data.p, G.n_schur, G.lm.p,
+  SchurArgs sa{G.schur_desc.p, G.schur_aux.p, G.schur_pairs.p, G.pt_fb.p, G.blk_lv.p,
+               G.blk_schur.p, G.blk_schur1.p, G.part_schur.p, e->n_blocks, G.pt_data.p, G.n_schur, G.lm.p,
                e->poses.p, G.poses_new.p, e->rho.p, G.rho_new.p, G.pt_orig.p, 7 * nf, G.n_gn_points};
   schur_lds_limit(G);
   if (G.n_schur > 0) schur_kernel<<<G.n_schur, kBlockThreads, G.schur_lds, e->stream>>>(sa, 0.0);

@@ -696,11 +696,14 @@ struct GnData {
   // repeat its first block): {block, point, pair | local target slot << 24, GN position}
   DevBuf<int4> lin_rec;
   DevBuf<int4> chunk_desc;       // linearise chunk: first linearise position, count, n_targets, partial offset
-  DevBuf<float> blk_schur;       // GN block → 16 floats [Hll gl Wh(6) Wt(6) 0 0]
+  DevBuf<float> blk_schur;       // GN block b → [Hll gl Wh(6)] at 8b and [Wt(6) 0 0] at 8(n_blocks + b) (two planes)
   DevBuf<float> part_lin;        // linearise chunk partials (fp32)
   DevBuf<float> blk_schur1, part_lin1;  // second set: the device LM loop linearises each candidate into the spare
   DevBuf<int> pt_first, pt_nblk, pt_orig;  // GN point → first GN block, block count, original point
   DevBuf<int4> pt_rec;           // GN point → {first GN block, block count, host frame, original point} (one load)
+  DevBuf<int4> pt_tgt;           // GN point → the targets of its first four GN blocks (the update's x_t loads in round 2)
+  DevBuf<int4> pair_rec;         // pair → {host, target, host camera, target camera}
+  DevBuf<int2> pt_fb;            // Schur chunk c's point p → {first GN block, block count} at c · SCHUR_PTS + p
   DevBuf<int4> schur_desc;       // Schur chunk: first GN point, n points, n local poses, partial offset
   DevBuf<int4> schur_aux;        // Schur chunk: pair list offset, n pairs, first GN block, n blocks
   DevBuf<uchar2> schur_pairs;    // used local pose pairs (a ≤ b) of every Schur chunk

@@ -27,11 +27,11 @@ if [ -n "${EXTRA:-}" ]; then
 fi
 if [ "${PROFILE:-1}" = "1" ]; then
   timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_${TAG}_kt -o run -- \
-      python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-c3 > gpurun_out/prof_${TAG}_kt.log 2>&1; rc=$?
+      python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-c3 --no-live-traffic > gpurun_out/prof_${TAG}_kt.log 2>&1; rc=$?
   echo "rocprof kt rc=$rc"; [ $rc -eq 0 ] || exit $rc
   for C in FETCH_SIZE WRITE_SIZE; do
     timeout -k 10 600 rocprofv3 --pmc $C --output-format csv -d gpurun_out/prof_${TAG}_$C -o run -- \
-        python bench.py --steps 5 --warmup 2 --clock-warmup-s 0 --gn-iterations 2 --no-c3 --no-c5 --no-cpu-baseline > gpurun_out/prof_${TAG}_$C.log 2>&1; rc=$?
+        python bench.py --steps 5 --warmup 2 --clock-warmup-s 0 --gn-iterations 2 --no-c3 --no-c5 --no-cpu-baseline --no-live-traffic > gpurun_out/prof_${TAG}_$C.log 2>&1; rc=$?
     echo "rocprof $C rc=$rc"; [ $rc -eq 0 ] || exit $rc
   done
 fi

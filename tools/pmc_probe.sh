@@ -6,7 +6,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 TAG=${TAG:-probe}
-ARGS=${ARGS:---steps 5 --warmup 2 --no-cpu-baseline --gn-iterations 0 --no-c5}
+ARGS=${ARGS:---steps 5 --warmup 2 --no-cpu-baseline --gn-iterations 0 --no-c5 --no-live-traffic}
 i=0
 while read -r GROUP; do
   [ -z "$GROUP" ] && continue

@@ -11,7 +11,7 @@ $SQ2
 $SQ3
 FETCH_SIZE
 WRITE_SIZE"
-TAG=c5 KREGEX=photometric_block_kernel_multi ARGS="--steps 5 --warmup 2 --no-cpu-baseline --gn-iterations 0" \
+TAG=c5 KREGEX=photometric_block_kernel_multi ARGS="--steps 5 --warmup 2 --no-cpu-baseline --gn-iterations 0 --no-live-traffic" \
   GROUPS_LIST="$ALL" tools/pmc_probe.sh || exit $?
 TAG=lin KREGEX=linearize_kernel SCRIPT=tools/gn_kernels.py ARGS="--iters 5" GROUPS_LIST="$ALL" tools/pmc_probe.sh || exit $?
 TAG=blk KREGEX="photometric_block_kernel<" GROUPS_LIST="$SQ1
