@@ -376,6 +376,16 @@ def traffic_probe(args):
     print(json.dumps({"probe": "ok", "n_blocks": pb.n_blocks}), flush=True)
 
 
+def counter_bytes_per_launch(rows, ctr, kernel):
+    """Mean bytes per dispatch of `kernel` from rocprofv3 counter_collection rows of counter `ctr` (KB): the rows of
+    one dispatch (one per XCD / instance dimension) are summed, the dispatches averaged, KB x 1024.  None: no sample."""
+    per = {}
+    for x in rows:
+        if x["Counter_Name"] == ctr and kernel in x["Kernel_Name"]:
+            per[x["Dispatch_Id"]] = per.get(x["Dispatch_Id"], 0.0) + float(x["Counter_Value"])
+    return sum(per.values()) / len(per) * 1024.0 if per else None
+
+
 def measure_traffic(args, n_blocks, timeout_s=150):
     """HBM bytes per headline launch, measured in this run: two rocprofv3 --pmc passes (FETCH_SIZE, then WRITE_SIZE —
     separate passes, MI355X_MICROARCH.md: the two do not fit one pass) over a child process running --traffic-probe,
@@ -405,14 +415,11 @@ def measure_traffic(args, n_blocks, timeout_s=150):
                 return None, f"rocprofv3 --pmc {ctr} pass failed (rc {r.returncode})"
             rows = []
             for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
-                rows += [x for x in csv.DictReader(open(f)) if x["Counter_Name"] == ctr]
-            per = {}
-            for x in rows:
-                if HEADLINE_KERNEL in x["Kernel_Name"]:
-                    per[x["Dispatch_Id"]] = per.get(x["Dispatch_Id"], 0.0) + float(x["Counter_Value"])
-            if not per:
+                rows += list(csv.DictReader(open(f)))
+            v = counter_bytes_per_launch(rows, ctr, HEADLINE_KERNEL)
+            if v is None:
                 return None, f"no {ctr} samples for {HEADLINE_KERNEL}"
-            vals[ctr] = sum(per.values()) / len(per) * 1024.0
+            vals[ctr] = v
     return vals["FETCH_SIZE"] + vals["WRITE_SIZE"], {
         "source": "measured in this run: rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE passes (child processes), raw KB x 1024",
         "fetch_bytes": vals["FETCH_SIZE"], "write_bytes": vals["WRITE_SIZE"]}

@@ -300,12 +300,23 @@ void photometric_block_kernel_multi(const KernelArgs a) {
         for (int q = 0; q < 7; ++q) c[q] = (h2){sat(c[q].x), sat(c[q].y)};
       }
       if (act) {
+        // the 6-value rows as 4-byte LDS writes where they are 4-byte aligned (LDS issue is what this kernel waits on:
+        // SQ_WAIT_INST_LDS ≈ 0.26 of wave time): 3 per row for even P, 1 + 2 + 1 for odd P (the inner pairs re-packed)
         T* h = s_rec + P + 6 * px;
         T* t = s_rec + 7 * P + 6 * px;
         s_rec[px] = c[0].x;
         s_rec[13 * P + px] = c[0].y;
-        h[0] = c[1].x; h[1] = c[1].y; h[2] = c[2].x; h[3] = c[2].y; h[4] = c[3].x; h[5] = c[3].y;
-        t[0] = c[4].x; t[1] = c[4].y; t[2] = c[5].x; t[3] = c[5].y; t[4] = c[6].x; t[5] = c[6].y;
+        if ((P & 1) == 0) {
+          h2* h4 = reinterpret_cast<h2*>(h);
+          h2* t4 = reinterpret_cast<h2*>(t);
+          h4[0] = c[1]; h4[1] = c[2]; h4[2] = c[3];
+          t4[0] = c[4]; t4[1] = c[5]; t4[2] = c[6];
+        } else {
+          h2* h4 = reinterpret_cast<h2*>(h + 1);
+          h2* t4 = reinterpret_cast<h2*>(t + 1);
+          h[0] = c[1].x; h4[0] = (h2){c[1].y, c[2].x}; h4[1] = (h2){c[2].y, c[3].x}; h[5] = c[3].y;
+          t[0] = c[4].x; t4[0] = (h2){c[4].y, c[5].x}; t4[1] = (h2){c[5].y, c[6].x}; t[5] = c[6].y;
+        }
       }
       return row.r;
     }
@@ -789,6 +800,7 @@ static int set_frames_impl(pba_engine* e, int32_t n_frames, const int32_t* frame
   PBA_HIP(hipStreamSynchronize(e->stream));
   e->frame_cam_h.assign(frame_cam, frame_cam + n_frames);
   e->pairs_fresh = false;
+  e->gn.prepared = false;  // the GN structure (frame count, the pairs' camera records) is re-analysed on next use
   e->n_frames = n_frames;
   e->width = width;
   e->height = height;
