@@ -43,6 +43,7 @@
 #include "pba_internal.h"
 
 
+
 using namespace pba;
 using namespace pba::detail;
 
@@ -122,7 +123,6 @@ struct LinArgs {
   int n_chunks;
   const double* lm;         // LM record: skip when the solve is done; spare: write the set the record does not hold
   bool spare;
-  int n_gn_blocks;          // the W_t plane of blk_schur starts at 8 · n_gn_blocks floats
 };
 
 // ------------------------------------------------------------------------------------------------
@@ -151,22 +151,6 @@ constexpr auto make_slot_table(std::integer_sequence<int, L...>) {
 }
 __constant__ const auto kSlotTable = make_slot_table(std::make_integer_sequence<int, 64>{});
 
-// Product index of chunk partial output o (linearize_kernel's partial slots): o < 42 → H_hh (6×6, both triangles from
-// the upper products) and g_h; o = 42 + q → H_ht (36), H_tt (6×6) and g_t of one target.
-__host__ __device__ constexpr int lin_out_v(int o) {
-  if (o < 36) { const int r = o / 6, c = o % 6; return upper_index(r < c ? r : c, r < c ? c : r); }
-  if (o < 42) return 78 + (o - 36);
-  const int q = o - 42;
-  if (q < 36) return 21 + q;
-  if (q < 72) { const int r = (q - 36) / 6, c = (q - 36) % 6; return 57 + upper_index(r < c ? r : c, r < c ? c : r); }
-  return 84 + (q - 72);
-}
-template <int... L>
-constexpr auto make_out_table(std::integer_sequence<int, L...>) {
-  struct T { unsigned char v[sizeof...(L)]; };
-  return T{{(unsigned char)lin_out_v(L)...}};
-}
-__constant__ const auto kLinOutV = make_out_table(std::make_integer_sequence<int, 42 + 78>{});
 
 // Normal-equation products by matrix cores: weighted rows X (R × 14, padded to LPB × 16 per block) give
 // XᵀX = Σ_k x_kᵀx_k as v_mfma_f32_16x16x4f32 steps (operand A = Xᵀ and B = X are the same register: lane l holds
@@ -185,8 +169,7 @@ void linearize_kernel(const KernelArgs a, const LinArgs g) {
   constexpr int NVP = 108;                  // 104 products, padded
   constexpr int kTileW = KIND == PBA_RESIDUAL_PHOTOMETRIC ? BW * (int)sizeof(TileBlock) : 0;
   constexpr int kRowsW = 64 * 16 * 4, kProdW = BW * NVP * 4;
-  constexpr int kArena0 = (kTileW > kRowsW ? (kTileW > kProdW ? kTileW : kProdW) : (kRowsW > kProdW ? kRowsW : kProdW));
-  constexpr int kArena = kArena0 < kProdW + 256 ? kProdW + 256 : kArena0;  // (+ the flush's dummy words)
+  constexpr int kArena = (kTileW > kRowsW ? (kTileW > kProdW ? kTileW : kProdW) : (kRowsW > kProdW ? kRowsW : kProdW));
   // per-wave arena, used in turn by the wave's tile blocks, its weighted rows and its per-target products
   // (each phase only touches the wave's own blocks; LDS is in order within a wave)
   __shared__ __attribute__((aligned(16))) unsigned char arena[NW][kArena];
@@ -200,11 +183,8 @@ void linearize_kernel(const KernelArgs a, const LinArgs g) {
   const bool s1 = (lv.set != 0.0) != g.spare;
   float* const blk_schur = s1 ? g.blk_schur1 : g.blk_schur;
   float* const part_lin = s1 ? g.part_lin1 : g.part_lin;
-  // (a vector load of a uniform address: readfirstlane tells the compiler the values are wave-uniform, so the loops and
-  // branches over them below are scalar instead of exec-mask regions)
-  const int count = __builtin_amdgcn_readfirstlane(d.y), n_t = __builtin_amdgcn_readfirstlane(d.z),
-            poff = __builtin_amdgcn_readfirstlane(d.w);
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;  // (wave-uniform)
+  const int count = d.y, n_t = d.z, poff = d.w;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int lb = threadIdx.x / LPB, k = threadIdx.x % LPB, wb = lb % BW;
   const bool live = lb < count;
   const int R = KIND == PBA_RESIDUAL_PHOTOMETRIC ? a.P : 2;
@@ -261,35 +241,28 @@ void linearize_kernel(const KernelArgs a, const LinArgs g) {
     float* sP = reinterpret_cast<float*>(arena[wave]);
     const int nbw = min(max(count - wave * BW, 0), BW);  // live blocks of this wave (wave-uniform)
     const int lo = __builtin_amdgcn_readfirstlane(lt);     // lane 0 holds the wave's first block
-    // branch-free scatter: a lane's entries outside the 104 products go to its own dummy word past the wave's product
-    // sets (the arena's tail), so the four stores need no exec-mask regions
-    static_assert(kProdW + 64 * 4 <= kArena, "dummy words after the product sets");
     auto flush = [&](const f32x4& acc, int slot) {
 #pragma unroll
       for (int m = 0; m < 4; ++m) {
         const unsigned v = (slots >> (8 * m)) & 255u;
-        sP[v < (unsigned)NV ? slot * NVP + (int)v : BW * NVP + lane] = acc[m];
+        if (v < (unsigned)NV) sP[slot * NVP + v] = acc[m];
       }
     };
     // per block: its own chain (SPB steps); row 12 of the result, C[12][c] on lanes 48 + c, is the block's
     // point-elimination data x̃_ρ·x̃_c → [H_ρρ, g_ρ, W_h(6), W_t(6), 0, 0] at its GN position (schur_kernel walks
     // them point by point); the block's products are then added to its target run's sum
     const int pc = lane - 48, pq = pc < 12 ? pc + 2 : (pc < 14 ? pc - 12 : pc);
-    // two planes (blk_schur layout): [H_ρρ, g_ρ, W_h] at 8·b, [W_t, 0, 0] at 8·(n + b) — the update kernel reads only
-    // the second, half the lines of the interleaved record
-    const long long pdst = pq < 8 ? pq : 8ll * g.n_gn_blocks + (pq - 8);
     f32x4 tacc = {0.0f, 0.0f, 0.0f, 0.0f};
     int cur = lo;
-    float pdat[BW];  // the blocks' point-elimination data (lanes 48-63), stored after the loop in one exec region
 #pragma unroll
     for (int b = 0; b < BW; ++b) {
-      pdat[b] = 0.0f;
       if (b < nbw) {
         f32x4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
         for (int st = 0; st < SPB; ++st)
           acc = __builtin_amdgcn_mfma_f32_16x16x4f32(op[b * SPB + st], op[b * SPB + st], acc, 0, 0, 0);
-        pdat[b] = acc[0];
+        const int gpb = __builtin_amdgcn_readlane(gpos, b * LPB);
+        if (pc >= 0) blk_schur[(long long)gpb * 16 + pq] = acc[0];
         const int ltb = __builtin_amdgcn_readlane(lt, b * LPB);
         if (ltb != cur) {
           flush(tacc, cur - lo);
@@ -300,11 +273,6 @@ void linearize_kernel(const KernelArgs a, const LinArgs g) {
       }
     }
     if (nbw > 0) flush(tacc, cur - lo);
-    if (pc >= 0) {
-#pragma unroll
-      for (int b = 0; b < BW; ++b)
-        if (b < nbw) blk_schur[(long long)__builtin_amdgcn_readlane(gpos, b * LPB) * 8 + pdst] = pdat[b];
-    }
     if (lane == 0) {
       s_wlo[wave] = lo;
       s_wn[wave] = nbw > 0 ? cur - lo + 1 : 0;
@@ -315,26 +283,31 @@ void linearize_kernel(const KernelArgs a, const LinArgs g) {
   // H_ht / H_tt / g_t of local target j from the ≤ NW sets of j (one per wave that holds j's blocks)
   auto sset = [&](int w, int i, int v) -> float { return reinterpret_cast<const float*>(arena[w])[i * NVP + v]; };
   const int nout = SLOT_LIN_BASE + SLOT_LIN_T * n_t;
-  // product index of each output from a table (kLinOutV), the waves' set ranges as scalars; every lane sums both the
-  // base sets and its target's sets with selects, no per-lane branches (same order as below: bitwise the same sums)
-  int wl[NW], wn[NW];
-#pragma unroll
-  for (int w = 0; w < NW; ++w) {
-    wl[w] = __builtin_amdgcn_readfirstlane(s_wlo[w]);
-    wn[w] = __builtin_amdgcn_readfirstlane(s_wn[w]);
-  }
   for (int o = threadIdx.x; o < nout; o += kBlockThreads) {
-    const int j = o < SLOT_LIN_BASE ? -1 : (o - SLOT_LIN_BASE) / SLOT_LIN_T;
-    const int v = kLinOutV.v[o < SLOT_LIN_BASE ? o : SLOT_LIN_BASE + (o - SLOT_LIN_BASE) % SLOT_LIN_T];
-    float ab = 0.0f, at = 0.0f;
+    int v, j = -1;
+    if (o < 36) {
+      const int r = o / 6, c = o % 6;
+      v = upper_index(min(r, c), max(r, c));
+    } else if (o < 42) {
+      v = 78 + (o - 36);
+    } else {
+      j = (o - 42) / SLOT_LIN_T;
+      const int q = (o - 42) % SLOT_LIN_T;
+      if (q < 36) v = 21 + q;
+      else if (q < 72) { const int r = (q - 36) / 6, c = (q - 36) % 6; v = 57 + upper_index(min(r, c), max(r, c)); }
+      else v = 84 + (q - 72);
+    }
+    float acc = 0.0f;
 #pragma unroll
     for (int w = 0; w < NW; ++w) {
-      for (int i = 0; i < wn[w]; ++i) ab += sset(w, i, v);
-      const int jj = j - wl[w];
-      const float t = sset(w, min(max(jj, 0), BW - 1), v);
-      at += jj >= 0 && jj < wn[w] ? t : 0.0f;
+      const int wl = s_wlo[w], wn = s_wn[w];
+      if (j < 0) {
+        for (int i = 0; i < wn; ++i) acc += sset(w, i, v);
+      } else if (j >= wl && j < wl + wn) {
+        acc += sset(w, j - wl, v);
+      }
     }
-    part_lin[(long long)poff + o] = j < 0 ? ab : at;
+    part_lin[(long long)poff + o] = acc;
   }
   // the block costs last: a store issued before a load makes the wait for that load wait for the store too (GFX9
   // counts loads and stores in one counter), so the stores go after every load of the kernel
@@ -366,7 +339,6 @@ struct SchurArgs {
   const float* blk_schur;
   const float* blk_schur1;  // buffer set 1 (device LM loop)
   double* part_schur;
-  int n_gn_blocks;          // blk_schur's W_t plane offset / 8
   double* pt_data;        // per GN point [H_ρρ, g_ρ, W_h(6)] (undamped)
   int n_chunks;
   const double* lm;       // LM record (λ, set; the loop's or GnData::lm_idle)
@@ -447,7 +419,7 @@ __global__ __launch_bounds__(kBlockThreads) void schur_kernel(const SchurArgs g,
 #pragma unroll
         for (int u = 0; u < kBatch; ++u) {
           const int b = min(b0 + u, fb + nb - 1);
-          v[u] = *reinterpret_cast<const float4*>(blk_schur + (long long)((q >> 1) * g.n_gn_blocks + b) * 8 + 4 * (q & 1));
+          v[u] = reinterpret_cast<const float4*>(blk_schur + (long long)b * 16)[q];
           lv[u] = q < 2 ? 0 : g.blk_lv[b];
         }
 #pragma unroll
@@ -2223,7 +2195,6 @@ struct PointUpdateArgs {
   const int* gn_target;
   const float* blk_schur;
   const float* blk_schur1;  // buffer set 1 (device LM loop)
-  int n_gn_blocks;          // blk_schur's W_t plane offset / 8
   const double* x;
   const uint8_t* fixed;
   const double* rho;
@@ -2290,7 +2261,7 @@ __device__ __forceinline__ void point_update_block(const PointUpdateArgs& a, con
       for (int u = 0; u < kBatch; ++u) {
         const int b = min(b0 + u, fb + nb - 1);
         t[u] = first ? (u == 0 ? pt4.x : u == 1 ? pt4.y : u == 2 ? pt4.z : pt4.w) : a.gn_target[b];
-        const float* wt = blk_schur + (long long)(a.n_gn_blocks + b) * 8;  // the W_t plane
+        const float* wt = blk_schur + (long long)b * 16 + 8;  // W_t
         const float4 q4 = *reinterpret_cast<const float4*>(wt);
         const float2 q2 = *reinterpret_cast<const float2*>(wt + 4);
         w[u][0] = q4.x; w[u][1] = q4.y; w[u][2] = q4.z; w[u][3] = q4.w; w[u][4] = q2.x; w[u][5] = q2.y;
@@ -3177,7 +3148,7 @@ int linearize(pba_engine* e, double* cost, const double* lm = nullptr, const Pai
     pairs = e->pairs.p;
   }
   const KernelArgs ka = make_kernel_args(e, pairs, rho ? rho : e->rho.p);
-  LinArgs la{G.lin_rec.p, G.blk_schur1.p, G.part_lin1.p, wg_red, G.chunk_desc.p, G.blk_schur.p, G.part_lin.p, G.n_chunks, lm ? lm : G.lm_idle.p, lm != nullptr, e->n_blocks};
+  LinArgs la{G.lin_rec.p, G.blk_schur1.p, G.part_lin1.p, wg_red, G.chunk_desc.p, G.blk_schur.p, G.part_lin.p, G.n_chunks, lm ? lm : G.lm_idle.p, lm != nullptr};
   if (e->opt.residual_kind == PBA_RESIDUAL_PHOTOMETRIC) launch_linearize_photometric(e, ka, la);
   else launch_linearize_geometric(e, ka, la);
   PBA_HIP(hipGetLastError());
@@ -3318,7 +3289,7 @@ void enqueue_updates(pba_engine* e, double lambda, const uint8_t* fixed, int* gp
   PoseUpdateArgs pa{e->poses.p, G.x.p, G.g_dir.p, G.Ddiag.p, fixed, G.poses_new.p, G.red.p, G.red2.p, G.gmax.p, nf};
   // point workgroup q writes reduction slot gp + q, as the separate launches did
   PointUpdateArgs qa{G.pt_data.p, G.pt_rec.p, G.pt_tgt.p, G.gn_target.p,
-                     G.blk_schur.p, G.blk_schur1.p, e->n_blocks, G.x.p, fixed, e->rho.p, G.rho_new.p, G.drho.p, G.red.p,
+                     G.blk_schur.p, G.blk_schur1.p, G.x.p, fixed, e->rho.p, G.rho_new.p, G.drho.p, G.red.p,
                      G.red2.p, G.gmax.p, G.n_gn_points};
   PairUpdateArgs ra{G.pair_rec.p, e->intr_d.p, G.pairs_new.p, e->n_pairs};
   update_kernel<<<gp + gq + gr, kBlockThreads, 0, e->stream>>>(pa, qa, ra, gp, gq, lambda, lm ? lm : G.lm_idle.p);
@@ -3383,7 +3354,7 @@ int enqueue_solve(pba_engine* e, double lambda, const double* lm = nullptr) {
   GnData& G = e->gn;
   const int nf = e->n_frames;
   SchurArgs sa{G.schur_desc.p, G.schur_aux.p, G.schur_pairs.p, G.pt_fb.p, G.blk_lv.p,
-               G.blk_schur.p, G.blk_schur1.p, G.part_schur.p, e->n_blocks, G.pt_data.p, G.n_schur, lm ? lm : G.lm_idle.p,
+               G.blk_schur.p, G.blk_schur1.p, G.part_schur.p, G.pt_data.p, G.n_schur, lm ? lm : G.lm_idle.p,
                lm ? e->poses.p : nullptr, G.poses_new.p, e->rho.p, G.rho_new.p, G.pt_orig.p, 7 * nf, G.n_gn_points};
   schur_lds_limit(G);
   schur_kernel<<<G.n_schur, kBlockThreads, G.schur_lds, e->stream>>>(sa, lambda);
@@ -3523,7 +3494,7 @@ int step_export(pba_engine* e, double lambda, int band, double* X) {
   if (int rc = exchange_K(e, band, &K)) return rc;
   const int nf = e->n_frames;
   SchurArgs sa{G.schur_desc.p, G.schur_aux.p, G.schur_pairs.p, G.pt_fb.p, G.blk_lv.p,
-               G.blk_schur.p, G.blk_schur1.p, G.part_schur.p, e->n_blocks, G.pt_data.p, G.n_schur, G.lm_idle.p,
+               G.blk_schur.p, G.blk_schur1.p, G.part_schur.p, G.pt_data.p, G.n_schur, G.lm_idle.p,
                nullptr, nullptr, nullptr, nullptr, nullptr, 0, 0};
   schur_lds_limit(G);
   if (G.n_schur > 0) schur_kernel<<<G.n_schur, kBlockThreads, G.schur_lds, e->stream>>>(sa, lambda);
@@ -3847,7 +3818,7 @@ int dist_trial(pba_engine* e, const Collective& coll, const DecideOpts& dopt, do
   GnData& G = e->gn;
   const int nf = e->n_frames;
   SchurArgs sa{G.schur_desc.p, G.schur_aux.p, G.schur_pairs.p, G.pt_fb.p, G.blk_lv.p,
-               G.blk_schur.p, G.blk_schur1.p, G.part_schur.p, e->n_blocks, G.pt_data.p, G.n_schur, G.lm.p,
+               G.blk_schur.p, G.blk_schur1.p, G.part_schur.p, G.pt_data.p, G.n_schur, G.lm.p,
                e->poses.p, G.poses_new.p, e->rho.p, G.rho_new.p, G.pt_orig.p, 7 * nf, G.n_gn_points};
   schur_lds_limit(G);
   if (G.n_schur > 0) schur_kernel<<<G.n_schur, kBlockThreads, G.schur_lds, e->stream>>>(sa, 0.0);

@@ -696,7 +696,7 @@ struct GnData {
   // repeat its first block): {block, point, pair | local target slot << 24, GN position}
   DevBuf<int4> lin_rec;
   DevBuf<int4> chunk_desc;       // linearise chunk: first linearise position, count, n_targets, partial offset
-  DevBuf<float> blk_schur;       // GN block b → [Hll gl Wh(6)] at 8b and [Wt(6) 0 0] at 8(n_blocks + b) (two planes)
+  DevBuf<float> blk_schur;       // GN block → 16 floats [Hll gl Wh(6) Wt(6) 0 0]
   DevBuf<float> part_lin;        // linearise chunk partials (fp32)
   DevBuf<float> blk_schur1, part_lin1;  // second set: the device LM loop linearises each candidate into the spare
   DevBuf<int> pt_first, pt_nblk, pt_orig;  // GN point → first GN block, block count, original point
