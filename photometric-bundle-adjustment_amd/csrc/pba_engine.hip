@@ -226,7 +226,9 @@ constexpr int kMultiThreads = 32 * 14 * 8 * PPL * (int)sizeof(T) + 32 * (int)siz
 // CT: the camera-table form (fused state, ≤ kCamTab cameras, 256 threads): compact 192-B tile blocks plus one LDS
 // CamRec per camera instead of 352-B tile blocks carrying both cameras (the 21-px fp16 launch: 30.1 → 25.6 KB of LDS
 // per workgroup, 5 → 6 workgroups per CU, which its 78 VGPRs also allow).
-template <int PM, int MODE, class T, int PPL, bool CT = false>
+// C1 (with CT, one camera): the rows take the camera constants from scalar loads of the engine's camera record instead
+// of the LDS table (no per-row LDS reads of them, no VGPRs).
+template <int PM, int MODE, class T, int PPL, bool CT = false, bool C1 = false>
 __global__ __launch_bounds__((kMultiThreads<PPL, T>)) __attribute__((amdgpu_waves_per_eu(CT ? 6 : 1, 8)))
 void photometric_block_kernel_multi(const KernelArgs a) {
   constexpr int LPB = 8, NTH = kMultiThreads<PPL, T>, BPW = NTH / LPB;
@@ -274,7 +276,7 @@ void photometric_block_kernel_multi(const KernelArgs a) {
   auto pixel = [&](int j, float ih) {
     const int px = k + LPB * j;
     const bool act = live && px < P;
-    const Row row = photometric_row<PM, JAC>(a, s_tb[lb], s_pat[px < P ? px : 0], ih, s_cam);  // masked by act
+    const Row row = photometric_row<PM, JAC, TB, C1>(a, s_tb[lb], s_pat[px < P ? px : 0], ih, s_cam);  // masked by act
     okl &= act ? row.ok : 1;
     s += act ? row.r * row.r : 0.0f;
     if constexpr (JAC && std::is_same<T, _Float16>::value) {
@@ -506,7 +508,10 @@ void launch_photometric(pba_engine* e, const KernelArgs& ka, int mode) {
     const int grid = (int)(((long long)e->n_blocks * 8 + nth - 1) / nth);                              \
     e->last_grid = grid;                                                                                \
     const size_t stage = M == 1 ? multi_stage_bytes(nth / 8, e->P, (int)sizeof(TT)) : 0;               \
-    if (M == 1 && nth == 256 && ct) {                                                                   \
+    if (M == 1 && nth == 256 && ct && ka.n_cams == 1) {                                                 \
+      photometric_block_kernel_multi<PM, M, TT, PPL, (M == 1 && nth == 256), (M == 1 && nth == 256)>    \
+          <<<grid, nth, stage + (size_t)(nth / 8) * sizeof(TileBlockC), e->stream>>>(ka);              \
+    } else if (M == 1 && nth == 256 && ct) {                                                            \
       photometric_block_kernel_multi<PM, M, TT, PPL, (M == 1 && nth == 256)>                            \
           <<<grid, nth, stage + (size_t)(nth / 8) * sizeof(TileBlockC), e->stream>>>(ka);              \
     } else {                                                                                            \

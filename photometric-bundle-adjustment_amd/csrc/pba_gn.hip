@@ -609,9 +609,14 @@ __global__ void assemble_kernel(AsmArgs a, double lambda) {
       const int B = a.crB, M = 6 * B, I = i / B, J = j / B;
       const int Ri = (i % B) * 6 + r, Cj = (j % B) * 6 + cc;  // row of i's entry / column of j's in their super-rows
       if (I == J) {
+        // a diagonal block's (r, cc) and (cc, r) are two lanes whose sums may differ in the last bit (the Schur
+        // terms' products round differently): only the lower one writes both, so D is symmetric and the solve
+        // reproducible (both lanes writing both positions left whichever stored last)
         double* D = a.crD + (long long)I * M * M;
-        D[Ri * M + Cj] = val;
-        D[Cj * M + Ri] = val;
+        if (i != j || r >= cc) {
+          D[Ri * M + Cj] = val;
+          D[Cj * M + Ri] = val;
+        }
       } else {  // I == J + 1 (bandwidth ≤ B): U_J[row of j][column of i] = S[6j+cc][6i+r]
         a.crU[(long long)J * M * M + Cj * M + Ri] = val;
       }

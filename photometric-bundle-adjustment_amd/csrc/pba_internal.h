@@ -197,6 +197,15 @@ struct KernelArgs {
   float pattern[2 * PBA_MAX_PATTERN];
 };
 
+// Camera 0's constants read through the constant address space: uniform scalar loads (photometric rows of a
+// one-camera problem; the same values the tile prologues copy).
+__device__ __forceinline__ CamView single_camera(const KernelArgs& a) {
+  typedef const __attribute__((address_space(4))) double cdouble;
+  typedef const __attribute__((address_space(4))) float cfloat;
+  return {(const double*)(cdouble*)(a.intr_d + kCamHk), (const double*)(cdouble*)a.intr_d,
+          (const float*)(cfloat*)a.intr};
+}
+
 // XCD-aware tile order: consecutive logical tiles (→ neighbouring host keyframes → shared target images)
 // land on the same XCD's L2 (blocks are dealt round-robin over the 8 XCDs; speed only, never correctness).
 __device__ __forceinline__ int logical_tile() {
@@ -512,13 +521,13 @@ __device__ __forceinline__ void adopt_state(const KernelArgs& a) {
 // Ih = host intensity I_h,k.
 // PM = camera model + 4 · interpolator (pba_device.h cam_of / interp_of).
 // TB = TileBlock (cameras in the block), or TileBlockC with the LDS camera table `tab`.
-template <int PM, bool JAC, class TB = TileBlock>
+template <int PM, bool JAC, class TB = TileBlock, bool C1 = false>
 __device__ __forceinline__ Row photometric_row(const KernelArgs& a, const TB& tb, float2 off, float Ih,
                                                const CamRec* tab = nullptr) {
   constexpr int MODEL = cam_of(PM);
   Row o;
   const auto& pp = pose_of(tb);
-  const CamView cv = cams_of(tb, tab);
+  const CamView cv = C1 ? single_camera(a) : cams_of(tb, tab);
   const double rho = tb.rho;
   // p̃ = R_th b_k + ρ t_th  (photometric_error.h:158-159)
   const Vec3d b = unproject<MODEL>(cv.hk, tb.ur.x + (double)off.x, tb.ur.y + (double)off.y);

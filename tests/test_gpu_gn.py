@@ -279,6 +279,32 @@ def test_c3_sized_gn_iteration_runs():
     assert np.isfinite(c_new)
 
 
+@pytest.mark.parametrize("solver", ["cr", "band"])
+def test_gn_step_and_solve_are_reproducible(solver, monkeypatch):
+    """C3 size: the same linearisation gives the same step bit for bit, twice in one engine and in a second engine
+    (fresh buffers), and pba_solve the same final state — every device sum has a fixed order and nothing races.
+    (Cyclic reduction's level 0 had each diagonal block entry written by two lanes whose sums can differ in the last
+    bit, so the step varied from run to run.)"""
+    monkeypatch.setenv("PBA_SOLVER", solver)
+    pb = synth.make_problem(n_frames=200, n_points=20000, texture="noise", seed=42, pose_sigma=5e-4, rho_sigma=5e-3)
+    runs = []
+    for _ in range(2):
+        with make_engine(pb, 9.0, (0, 1)) as eng:
+            for _ in range(2):
+                eng.set_state(pb.poses, pb.rho)
+                eng.gn_linearize()
+                _, st = eng.gn_step(1e-3)
+                assert st == 0
+                dp, dl = eng.gn_last_step()
+                eng.set_state(pb.poses, pb.rho)
+                s = eng.solve(max_iterations=4, function_tolerance=0.0)
+                poses, rho = eng.get_state()
+                runs.append((dp, dl, np.float64(s["final_cost"]), poses, rho))
+    for r in runs[1:]:
+        for a, b in zip(runs[0], r):
+            assert np.array_equal(a, b)
+
+
 @pytest.mark.parametrize("solver", ["cr", "band", "skyline"])
 @pytest.mark.parametrize("n_frames", [12, 13, 6, 37])
 def test_reduced_solvers_agree(solver, n_frames, monkeypatch):
