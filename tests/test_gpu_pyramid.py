@@ -123,3 +123,40 @@ def test_fp16_records(P):
     assert not bad.any(), (bad.sum(), np.unique(np.nonzero(bad)[1]))
     tol = 2.0 ** -11 * np.abs(r32[:, :P]) + 2.0 ** -14  # residuals: no cancellation, plain half rounding
     assert (np.abs(ro[:, :P] - r32[:, :P]) <= tol).all()
+
+
+@pytest.mark.parametrize("n_cams", [1, 2])
+@pytest.mark.parametrize("P", [21, 30])
+def test_multi_pixel_kernel_forms_agree_bitwise(P, n_cams, monkeypatch):
+    """The 9-32 px kernel at a device state takes its camera constants three ways: once per lane from the camera
+    record (one-camera problems), from the LDS camera table (≤ 4 cameras), or from each block's tile
+    (PBA_NO_CAM_TABLE=1).  The same values in the same arithmetic: fp32 and fp16 records must be bit-identical."""
+    import torch
+    rng = np.random.default_rng(P + n_cams)
+    pat = rng.integers(-3, 4, (P, 2)).astype(np.float32)
+    intr = None
+    if n_cams == 2:
+        intr = np.array([synth.DEFAULT_INTRINSICS[synth.PINHOLE], synth.DEFAULT_INTRINSICS[synth.PINHOLE]], np.float64)
+        intr[:, :4] *= 320 / 752.0  # (explicit intrinsics are quoted for the image size)
+        intr[1, :4] *= [1.01, 0.99, 1.0, 1.0]
+    pb = synth.make_problem(n_frames=9, n_points=400, width=320, height=200, pattern=pat, seed=80 + P, border=16,
+                            intrinsics=intr, frame_cam=None if n_cams == 1 else np.arange(9) % 2)
+    poses = torch.from_numpy(np.ascontiguousarray(pb.poses)).cuda()
+    rho = torch.from_numpy(np.ascontiguousarray(pb.rho)).cuda()
+    out = {}
+    for form in ("default", "per-block"):
+        if form == "per-block":
+            monkeypatch.setenv("PBA_NO_CAM_TABLE", "1")
+        with E.Engine(pb.kind, pb.model) as eng:
+            eng.set_problem(pb)
+            eng.evaluate_state_device(poses.data_ptr(), rho.data_ptr(), True)
+            r32, v32 = eng.records()
+            eng.set_record_format(E.RECORD_F16)
+            eng.evaluate_state_device(poses.data_ptr(), rho.data_ptr(), True)
+            r16, v16 = eng.records()
+        out[form] = (r32.copy(), v32.copy(), r16.copy(), v16.copy())
+    a, b = out["default"], out["per-block"]
+    assert a[1].sum() > 0.8 * pb.n_blocks
+    assert np.array_equal(a[1], b[1]) and np.array_equal(a[3], b[3])
+    assert np.array_equal(a[0].view(np.uint32), b[0].view(np.uint32))
+    assert np.array_equal(a[2].view(np.uint16), b[2].view(np.uint16))
