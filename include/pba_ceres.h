@@ -196,19 +196,21 @@ class GpuEvaluator : public ceres::EvaluationCallback {
   // when the point was already evaluated with Jacobians nothing is recomputed.
   void PrepareForEvaluation(bool evaluate_jacobians, bool new_evaluation_point) override {
     if (!new_evaluation_point && have_point_ && (have_jac_ || !evaluate_jacobians)) return;
-    state_p_.resize(7 * poses_.size());
-    state_r_.resize(rho_.size());
-    for (size_t f = 0; f < poses_.size(); ++f) std::memcpy(&state_p_[7 * f], poses_[f], 7 * sizeof(double));
-    for (size_t p = 0; p < rho_.size(); ++p) state_r_[p] = *rho_[p];
-    check(pba_set_state(engine_, state_p_.data(), state_r_.data()), "pba_set_state");
+    // the state is gathered into page-locked memory, so pba_set_state's uploads are DMA copies that do not stage
+    // through a driver buffer; the launch is enqueued right behind them
+    const size_t nf = poses_.size(), np = rho_.size();
+    if (async_) check(pba_synchronize(engine_), "pba_synchronize");  // the last upload from these buffers is done
+    state_p_.resize(7 * nf);
+    state_r_.resize(np);
+    double* sp = state_p_.data();
+    double* sr = state_r_.data();
+    for (size_t f = 0; f < nf; ++f) std::memcpy(sp + 7 * f, poses_[f], 7 * sizeof(double));
+    for (size_t p = 0; p < np; ++p) sr[p] = *rho_[p];
+    check(pba_set_state(engine_, sp, sr), "pba_set_state");
     if (!intr_.empty()) {
       state_k_.resize(8 * intr_.size());
       for (size_t c = 0; c < intr_.size(); ++c) std::memcpy(&state_k_[8 * c], intr_[c], 8 * sizeof(double));
       check(pba_set_intrinsics_state(engine_, state_k_.data()), "pba_set_intrinsics_state");
-    }
-    if (evaluate_jacobians && form_ == PoseJacobian::kReferenceSE3) {  // P⁺ of every pose at this point (overlaps the launch)
-      pinv_.resize(42 * poses_.size());
-      for (size_t f = 0; f < poses_.size(); ++f) se3_plus_jacobian_pinv(&state_p_[7 * f], &pinv_[42 * f]);
     }
     check(pba_evaluate(engine_, evaluate_jacobians ? 1 : 0), "pba_evaluate");
     const size_t nb = (size_t)pba_num_blocks(engine_);
@@ -221,7 +223,13 @@ class GpuEvaluator : public ceres::EvaluationCallback {
       async_ = true;
       res_ = records_.data();
       res_stride_ = rec_;
+      if (form_ == PoseJacobian::kReferenceSE3) {  // P⁺ of every pose at this point, while the launch and copies run
+        pinv_.resize(42 * nf);
+        for (size_t f = 0; f < nf; ++f) se3_plus_jacobian_pinv(sp + 7 * f, &pinv_[42 * f]);
+      }
     } else {
+      // residual-only: the launch also writes the residuals contiguously, so this is one plain D2H copy of 4R bytes per
+      // block (not a pitched copy out of the records)
       residuals_.resize(nb * R_);
       check(pba_get_residuals(engine_, residuals_.data(), valid_.data()), "pba_get_residuals");
       async_ = false;
@@ -255,7 +263,8 @@ class GpuEvaluator : public ceres::EvaluationCallback {
   std::vector<double*> poses_, rho_, intr_;
   PoseJacobian form_;
   bool async_ = false;
-  std::vector<double> state_p_, state_r_, state_k_, pinv_;
+  std::vector<double> state_k_, pinv_;
+  PinnedArray<double> state_p_, state_r_;
   mutable std::atomic<bool> refused_{false};
   PinnedArray<float> records_, residuals_;
   PinnedArray<uint8_t> valid_;

@@ -24,8 +24,10 @@ def available() -> bool:
 
 def run(mode: str, pb, iters: int = 20, huber: float = 1.0, threads: int = 8, fixed=(0, 1), ftol: float = 1e-6,
         timeout: float = 600.0, ptol: float = 1e-8, gtol: float = 1e-10, optimize_intrinsics: bool = False,
-        pose_param: str = "ref") -> dict:
-    """pose_param: "ref" — the reference's LocalParameterizationSE3 in both modes (the GPU adapter then emits 7-wide
+        pose_param: str = "ref", check: bool = True) -> dict:
+    """mode: "cpu" (AutoDiff), "gpu" (the drop-in) or "floor" (constant cost functions: Ceres' own per-evaluation work).
+    check: gpu mode with the evaluation-callback protocol checks (tests) or the plain adapter (timing).
+    pose_param: "ref" — the reference's LocalParameterizationSE3 in both modes (the GPU adapter then emits 7-wide
     Jacobians J6·P⁺); "tangent" — the adapter's SE3TangentParameterization in gpu mode.  optimize_intrinsics: 0 constant
     intrinsics blocks, 1 free (the GPU evaluator is given them), 2 free but not given to the evaluator (refusal)."""
     from make_golden import write_problem
@@ -36,7 +38,7 @@ def run(mode: str, pb, iters: int = 20, huber: float = 1.0, threads: int = 8, fi
         fx = ",".join(str(int(i)) for i in fixed) if len(fixed) else "-"
         subprocess.run([DRIVER, mode, fin, fout, str(iters), repr(float(huber)), str(threads), fx, repr(float(ftol)),
                         str(int(getattr(pb, "interp", 0))), repr(float(ptol)), repr(float(gtol)),
-                        str(int(optimize_intrinsics)), pose_param], check=True, timeout=timeout)
+                        str(int(optimize_intrinsics)), pose_param, "1" if check else "0"], check=True, timeout=timeout)
         with open(fout) as f:
             out = json.load(f)
     out["poses"] = np.asarray(out["poses"]).reshape(-1, 7)

@@ -182,7 +182,10 @@ __global__ __launch_bounds__(kBlockThreads) void photometric_block_kernel(const 
     return;
   }
   if (!JAC) {
-    if (act) out[(long long)blk * rec_f + k] = rec_val<T>(ok ? row.r : 0.0f);
+    if (act) {
+      out[(long long)blk * rec_f + k] = rec_val<T>(ok ? row.r : 0.0f);
+      if (a.res_out) a.res_out[(long long)blk * P + k] = ok ? row.r : 0.0f;  // contiguous: one D2H copy for Ceres
+    }
     return;
   }
   __syncthreads();  // every lane has read its tile block: the record stage may overwrite it
@@ -370,7 +373,10 @@ void photometric_block_kernel_multi(const KernelArgs a) {
 #pragma unroll
     for (int j = 0; j < PPL; ++j) {
       const int px = k + LPB * j;
-      if (live && px < P) out[(long long)blk * rec_f + px] = rec_val<T>(ok ? rr[j] : 0.0f);
+      if (live && px < P) {
+        out[(long long)blk * rec_f + px] = rec_val<T>(ok ? rr[j] : 0.0f);
+        if (a.res_out) a.res_out[(long long)blk * P + px] = ok ? rr[j] : 0.0f;
+      }
     }
     return;
   }
@@ -472,6 +478,7 @@ __global__ __launch_bounds__(kBlockThreads) void geometric_block_kernel(const Ke
       __builtin_nontemporal_store(f32x4{J[4 * i], J[4 * i + 1], J[4 * i + 2], J[4 * i + 3]}, rec + i);
   } else {
     reinterpret_cast<float2*>(rec)[0] = make_float2(J[0], J[1]);
+    if (a.res_out) reinterpret_cast<float2*>(a.res_out)[blk] = make_float2(J[0], J[1]);
   }
 }
 
@@ -920,6 +927,10 @@ int pba_set_blocks(pba_engine* e, int32_t n_blocks, const int32_t* block_point, 
   e->n_blocks = n_blocks;
   e->n_pairs = np;
   e->evaluated = false;
+  e->res_fresh = false;
+  e->chunk_blocks = 0;
+  e->n_chunks_async = 0;
+  e->chunks_arrived.store(0);
   e->pairs_fresh = false;
   e->block_point_h.assign(block_point, block_point + n_blocks);
   e->block_target_h.assign(block_target, block_target + n_blocks);
@@ -1010,10 +1021,19 @@ int evaluate_at(pba_engine* e, const double* poses, const double* rho, bool adop
     ev_stop = e->ev_pool[e->ev_used + 1];
     e->ev_used += 2;
   }
+  if (!jac) {
+    PBA_HIP(e->res.resize((size_t)e->n_blocks * e->R()));
+    ka.res_out = e->res.p;
+  }
   launch_mode(e, ka, jac ? 1 : 0);
   PBA_HIP(hipGetLastError());
   if (ev_stop) PBA_HIP(hipEventRecord(ev_stop, e->stream));
   e->evaluated = true;
+  e->res_fresh = !jac;
+  // a new evaluation invalidates an earlier asynchronous read-back (pba_wait_records then fails instead of returning)
+  e->chunk_blocks = 0;
+  e->n_chunks_async = 0;
+  e->chunks_arrived.store(0);
   return PBA_OK;
 }
 
@@ -1126,9 +1146,12 @@ int pba_get_records_async(pba_engine* e, float* records, uint8_t* valid, int32_t
 }
 
 int pba_wait_records(pba_engine* e, int32_t block) {
-  if (!e || block < 0 || block >= e->n_blocks || e->chunk_blocks <= 0)
-    return fail(PBA_ERR_INVALID_ARGUMENT, "bad wait arguments");
+  if (!e || block < 0 || block >= e->n_blocks) return fail(PBA_ERR_INVALID_ARGUMENT, "bad wait arguments");
+  // no read-back in flight for the current evaluation (pba_evaluate / pba_set_blocks reset it), or one that does not
+  // cover this block: fail rather than report stale records as arrived
+  if (e->chunk_blocks <= 0) return fail(PBA_ERR_NOT_READY, "pba_get_records_async first");
   const int c = block / e->chunk_blocks;
+  if (c >= e->n_chunks_async || c >= (int)e->chunk_ev.size()) return fail(PBA_ERR_NOT_READY, "block not in the read-back");
   if (c < e->chunks_arrived.load(std::memory_order_acquire)) return PBA_OK;
   PBA_HIP(hipEventSynchronize(e->chunk_ev[c]));  // chunks arrive in stream order: every chunk ≤ c is in
   int seen = e->chunks_arrived.load(std::memory_order_relaxed);
@@ -1143,7 +1166,10 @@ int pba_get_residuals(pba_engine* e, float* residuals, uint8_t* valid) {
   if (int rc = check_device(e)) return rc;
   const size_t R = (size_t)e->R(), nb = (size_t)e->n_blocks, RF = (size_t)e->rec_floats();
   std::vector<_Float16> half;
-  if (residuals && nb) {
+  if (residuals && nb && e->res_fresh) {
+    // a residual-only evaluation also wrote its residuals contiguously: one plain device-to-host copy
+    PBA_HIP(hipMemcpyAsync(residuals, e->res.p, nb * R * sizeof(float), hipMemcpyDeviceToHost, e->stream));
+  } else if (residuals && nb) {
     // the first R values of every 14R-value record: one pitched device-to-host copy
     if (e->record_format == PBA_RECORD_F16) {
       half.resize(nb * R);

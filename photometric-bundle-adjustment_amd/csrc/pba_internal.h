@@ -187,6 +187,7 @@ struct KernelArgs {
   const double* rho;             // per point (state)
   const double2* u_obs;          // per block (geometric)
   float* out;                    // records
+  float* res_out;                // residual-only launches: R contiguous fp32 residuals per block (pba_get_residuals)
   float* cost;                   // per block
   uint8_t* valid;                // per block
   int n_blocks;
@@ -788,6 +789,8 @@ struct pba_engine {
   pba::detail::DevBuf<pba::detail::PairRec> pairs;
   pba::detail::DevBuf<double> poses, rho;
   pba::detail::DevBuf<float> out, cost;
+  pba::detail::DevBuf<float> res;    // contiguous residuals of the last residual-only evaluation (R per block)
+  bool res_fresh = false;            // res holds the last evaluation's residuals (it was residual-only)
   pba::detail::DevBuf<uint8_t> valid;
   int record_format = PBA_RECORD_F32;
   int interp = PBA_INTERP_BILINEAR;  // pba_set_interpolator

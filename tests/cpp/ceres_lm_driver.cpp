@@ -24,13 +24,20 @@
 // unprojecting with the captured pointer (user memory, which Ceres does not write during a solve without a callback),
 // the GPU evaluator gets the blocks and enables the engine's target-intrinsics Jacobian.
 //
-//   usage: ceres_lm_driver <cpu|gpu> <problem.bin> <out.json> [iters] [huber] [threads] [fixed,frames] [ftol] [interp]
-//                          [ptol] [gtol] [optimize_intrinsics] [pose_param ref|tangent]
+// floor: Ceres' own per-evaluation floor — the same Problem (parameter blocks, local parameterisations, Huber, sizes)
+//        with a SizedCostFunction per block that writes constants, so "Jacobian & residual evaluation" is Ceres'
+//        bookkeeping alone (ProgramEvaluator, the Jacobian writer, the LocalParameterization products, the loss).
+// check = 0 (gpu mode): the plain adapter, without the protocol checks (the bench's C2 timing: the checks hash the whole
+//        state per Prepare and count every Evaluate with an atomic shared by Ceres' threads).
+//
+//   usage: ceres_lm_driver <cpu|gpu|floor> <problem.bin> <out.json> [iters] [huber] [threads] [fixed,frames] [ftol]
+//                          [interp] [ptol] [gtol] [optimize_intrinsics] [pose_param ref|tangent] [check 1|0]
 //          (problem layout: tests/golden/make_golden.py write_problem)
 #include <atomic>
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
+#include <cmath>
 #include <cstring>
 #include <memory>
 #include <sstream>
@@ -130,6 +137,33 @@ class CheckedCost : public ceres::CostFunction {
   int host_, target_, point_, nf_;
 };
 
+// Ceres' floor (mode floor): a residual that costs next to nothing to evaluate but is a genuine nonlinear least-squares
+// term in (T_h, T_t, ρ) with its exact global Jacobians, so LM takes accepted steps (and Jacobian evaluations) as in the
+// real solve: r_k = c_k (ρ − 0.05) + 1e-3 sin(x_h[4] + c_k x_t[5]), c_k = k + 1.
+template <int R, int... N>
+class FloorCost : public ceres::SizedCostFunction<R, N...> {
+ public:
+  bool Evaluate(double const* const* x, double* residuals, double** jacobians) const override {
+    double s[R], c[R];
+    for (int k = 0; k < R; ++k) {
+      const double ck = k + 1.0, a = x[0][4] + ck * x[1][5];
+      s[k] = std::sin(a);
+      c[k] = std::cos(a);
+      residuals[k] = 1e-2 * ck * (x[2][0] - 0.05) + 1e-3 * s[k];
+    }
+    if (!jacobians) return true;
+    const int sizes[] = {N...};
+    for (size_t i = 0; i < sizeof(sizes) / sizeof(int); ++i)
+      if (jacobians[i]) std::memset(jacobians[i], 0, sizeof(double) * R * sizes[i]);
+    for (int k = 0; k < R; ++k) {
+      if (jacobians[0]) jacobians[0][7 * k + 4] = 1e-3 * c[k];
+      if (jacobians[1]) jacobians[1][7 * k + 5] = 1e-3 * (k + 1.0) * c[k];
+      if (jacobians[2]) jacobians[2][k] = 1e-2 * (k + 1.0);
+    }
+    return true;
+  }
+};
+
 // ceres::PhotometricError<8> throws outside the EUCM domain (photometric_error.h:165-171); inside a solve that is an
 // invalid evaluation (residual_block.cc:113-131): return false instead.
 struct CeresPhotometric {
@@ -163,6 +197,7 @@ int main(int argc, char** argv) {
     return 1;
   }
   const bool gpu = std::string(argv[1]) == "gpu";
+  const bool floor_mode = std::string(argv[1]) == "floor";
   const int iters = argc > 4 ? atoi(argv[4]) : 20;
   const double huber = argc > 5 ? atof(argv[5]) : 1.0;
   const int threads = argc > 6 ? atoi(argv[6]) : 8;
@@ -181,6 +216,7 @@ int main(int argc, char** argv) {
   const int intr_mode = argc > 12 ? atoi(argv[12]) : 0;
   const bool opt_intr = intr_mode != 0;
   const bool tangent = argc > 13 && std::string(argv[13]) == "tangent";
+  const bool checked = !(argc > 14 && atoi(argv[14]) == 0);
 
   FILE* f = fopen(argv[2], "rb");
   if (!f) return 2;
@@ -214,7 +250,7 @@ int main(int argc, char** argv) {
 
   Protocol protocol;
   pba_engine* e = nullptr;
-  std::unique_ptr<CheckedEvaluator> ev;
+  std::unique_ptr<pba_ceres::GpuEvaluator> ev;
   ceres::Problem::Options popt;
   if (gpu) {
     pba_options opt{0, kind, model, 0.0f};
@@ -230,9 +266,11 @@ int main(int argc, char** argv) {
     std::vector<double*> intr_ptr;
     if (intr_mode == 1)
       for (int c = 0; c < nc; ++c) intr_ptr.push_back(&intr[8 * c]);
-    ev.reset(new CheckedEvaluator(e, pose_ptr, rho_ptr, intr_ptr,
-                                  tangent ? pba_ceres::PoseJacobian::kTangent : pba_ceres::PoseJacobian::kReferenceSE3,
-                                  nb, &protocol));
+    const auto form = tangent ? pba_ceres::PoseJacobian::kTangent : pba_ceres::PoseJacobian::kReferenceSE3;
+    if (checked)
+      ev.reset(new CheckedEvaluator(e, pose_ptr, rho_ptr, intr_ptr, form, nb, &protocol));
+    else
+      ev.reset(new pba_ceres::GpuEvaluator(e, pose_ptr, rho_ptr, intr_ptr, form));
     popt.evaluation_callback = ev.get();  // problem.h:185 (not owned)
   }
   ceres::Problem problem(popt);
@@ -251,7 +289,7 @@ int main(int argc, char** argv) {
   // CPU photometric: one interpolator per keyframe image, host bearings per point
   using PE = ceres::PhotometricError<8>;
   const bool ceres_pe = !gpu && kind == 0 && interp == 1 && model == pba_test::CAM_EUCM;
-  if (!gpu && kind == 0 && interp == 1 && !ceres_pe) {
+  if (!gpu && !floor_mode && kind == 0 && interp == 1 && !ceres_pe) {
     fprintf(stderr, "cpu mode: bicubic is the vendored PhotometricError<8>, EUCM cameras only\n");
     return 3;
   }
@@ -263,7 +301,7 @@ int main(int argc, char** argv) {
   std::vector<PE::Intrinsics, Eigen::aligned_allocator<PE::Intrinsics>> K6(nc);
   for (int c = 0; c < nc; ++c) K6[c] << intr[8 * c], intr[8 * c + 1], intr[8 * c + 2], intr[8 * c + 3], intr[8 * c + 4], intr[8 * c + 5];
   std::vector<double> host_int_d;
-  if (!gpu && kind == 0) {
+  if (!gpu && !floor_mode && kind == 0) {
     for (int i = 0; i < nf; ++i) {
       bilin.emplace_back(new pba_test::BilinearInterpolator(&images[(size_t)i * W * H], H, W));
       grids.emplace_back(new pba_test::Grid(&images[(size_t)i * W * H], 0, H, 0, W));
@@ -286,7 +324,9 @@ int main(int argc, char** argv) {
     if (gpu) {
       ceres::CostFunction* inner = kind == 0 ? static_cast<ceres::CostFunction*>(new pba_ceres::GpuPhotometricCost<8>(ev.get(), b, h, t))
                                              : new pba_ceres::GpuReprojectionCost(ev.get(), b, h, t);
-      cf = new CheckedCost(inner, &protocol, h, t, p, nf);
+      cf = checked ? new CheckedCost(inner, &protocol, h, t, p, nf) : inner;
+    } else if (floor_mode) {
+      cf = kind == 0 ? static_cast<ceres::CostFunction*>(new FloorCost<8, 7, 7, 1>) : new FloorCost<2, 7, 7, 1, 8>;
     } else if (kind == 1) {
       cf = new ceres::AutoDiffCostFunction<pba_test::GeometricFunctor, 2, 7, 7, 1, 8>(new pba_test::GeometricFunctor(
           Eigen::Vector2d(u_obs[2 * b], u_obs[2 * b + 1]), Eigen::Vector2d(u_ref[2 * p], u_ref[2 * p + 1]),
@@ -316,7 +356,7 @@ int main(int argc, char** argv) {
   ceres::Solve(so, &problem, &sum);
 
   std::ostringstream o;
-  o << "{\"mode\":\"" << (gpu ? "gpu" : "cpu") << "\",\"termination\":" << (int)sum.termination_type
+  o << "{\"mode\":\"" << argv[1] << "\",\"checked\":" << (gpu && checked ? 1 : 0) << ",\"termination\":" << (int)sum.termination_type
     << ",\"message\":\"" << sum.message << "\",\"successful_steps\":" << sum.num_successful_steps
     << ",\"unsuccessful_steps\":" << sum.num_unsuccessful_steps << ",\"iterations\":[";
   for (size_t i = 0; i < sum.iterations.size(); ++i) {
