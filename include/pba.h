@@ -269,7 +269,7 @@ int pba_gn_get_step(pba_engine* engine, double* d_poses, double* d_inv_dist);
  *
  * The exchange buffer is a DEVICE array of pba_gn_exchange_size doubles, banded with K ∈ {4, 8, 16} block
  * rows, K ≥ max over ranks of pba_gn_band: per frame i, (K+1) 6×6 blocks (block c = column i−K+c, row
- * major) followed by 24 doubles [g(6) | g_direct(6) | diag(A)(6) | observed | 0…]; then 8 scalar slots. */
+ * major) followed by 24 doubles [g(6) | g_direct(6) | diag(A)(6) | observed | 0…]; then 16 scalar slots. */
 int pba_gn_band(pba_engine* engine, int32_t* band);   /* local reduced-system bandwidth (block rows) */
 int pba_gn_exchange_size(pba_engine* engine, int32_t band, int64_t* count);
 /* after pba_gn_linearize: point elimination for lambda + this rank's partial system into d_exchange */
@@ -279,9 +279,10 @@ int pba_gn_step_export(pba_engine* engine, double lambda, int32_t band, double* 
 int pba_gn_step_import(pba_engine* engine, double lambda, int32_t band, const double* d_exchange,
                        double* model_pose, double* model_points, int32_t* solver_status);
 /* pba_solve over all ranks, steered by the device LM record as on one GPU: per trial, the banded partial systems
- * (count = pba_gn_exchange_size − 8 doubles) and then 8 point-part scalars (model decrease, candidate cost and valid
- * blocks, step and state norms, points above the gradient tolerance) are summed over the ranks, and every rank takes the
- * same decision on the device.  Two collectives per trial (trial i + 1's damping, hence its point elimination, depends
+ * (count = pba_gn_exchange_size − 16 doubles) and then 16 scalars are summed over the ranks: the point part (model
+ * decrease, candidate cost and valid blocks, step and state norms, points above the gradient tolerance) from every
+ * rank, and — with a pba_comm — the pose part and the reduced solve's status from rank 0 alone, so every rank takes the
+ * same decision on the device from bit-identical inputs.  Two collectives per trial (trial i + 1's damping, hence its point elimination, depends
  * on trial i's decision).
  *
  * The collective is either a host callback — the in-place sum over all ranks of count doubles at d_buf (device memory

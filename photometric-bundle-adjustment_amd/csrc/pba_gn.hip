@@ -2600,16 +2600,23 @@ __global__ __launch_bounds__(kDecideThreads) void lm_decide_kernel(const double*
   if (host_rec) publish_record(s_rec, host_rec, seq);
 }
 
-// Multi-GPU trial, before the scalar all-reduce: this rank's sums split into the pose part, which every rank computes
-// bit for bit the same (same summed system, same step) and keeps in tpose, and the point part, written to the exchange
-// buffer's kExScalars scalar slots Y for the Σ over ranks:
-//   Y = [δρ·g, δρ·D·δρ, candidate cost, candidate valid blocks, Σδρ², Σρ_new², points above the gradient tolerance, 0]
-// (the gradient test needs only whether some rank's point gradient exceeds the tolerance: a count sums exactly).
-constexpr int kExScalars = 8;
+// Multi-GPU trial, before the scalar all-reduce: this rank's sums, written to the exchange buffer's kExScalars scalar
+// slots Y for the Σ over ranks:
+//   Y[0..7]  the point part: [δρ·g, δρ·D·δρ, candidate cost, candidate valid blocks, Σδρ², Σρ_new², points above the
+//            gradient tolerance, 0] (the gradient test needs only whether some rank's point gradient exceeds the
+//            tolerance: a count sums exactly);
+//   Y[8..14] the pose part [g·δ, δ·D·δ, Σδ², Σx_new², max|g|] and the reduced solve's status, from rank 0 only (0 on the
+//            other ranks).  Every rank computes them from the same summed system with the same kernels, so they agree
+//            bit for bit anyway; summing rank 0's copy makes the decision inputs identical on every rank by construction
+//            (a decision that differed between ranks would leave their collective sequences mismatched: a hang).
+// rank0 = −1 (a host-callback collective, which does not know the ranks): Y[8..14] stay 0 and the decision reads the
+// rank's own pose part from tpose.  tpose: [pose part (5) | this rank's point gradient max-norm | solve status].
+constexpr int kExScalars = 16;
 __global__ __launch_bounds__(kDecideThreads) void dist_sums_kernel(const double* __restrict__ red,
                                                                    const double* __restrict__ red2,
                                                                    const double* __restrict__ gmax, int gp, int gq, int gc,
                                                                    double gtol, const double* __restrict__ lm,
+                                                                   const int* __restrict__ status, int rank0,
                                                                    double* __restrict__ tpose, double* __restrict__ Y) {
   const double done = lm[kLmDone];  // (tested after the sums, as lm_decide_kernel)
   __shared__ double t[kTsCount];
@@ -2617,6 +2624,7 @@ __global__ __launch_bounds__(kDecideThreads) void dist_sums_kernel(const double*
   if (done != 0.0 || threadIdx.x != 0) return;
   for (int q = 0; q < 5; ++q) tpose[q] = t[kTsPoseG + q];
   tpose[5] = t[kTsPtGMax];
+  tpose[6] = (double)*status;
   Y[0] = t[kTsPtG];
   Y[1] = t[kTsPtD];
   Y[2] = t[kTsCost];
@@ -2625,28 +2633,32 @@ __global__ __launch_bounds__(kDecideThreads) void dist_sums_kernel(const double*
   Y[5] = t[kTsPtXNorm2];
   Y[6] = t[kTsPtGMax] > gtol ? 1.0 : 0.0;
   Y[7] = 0.0;
+  for (int q = 0; q < 5; ++q) Y[8 + q] = rank0 == 1 ? t[kTsPoseG + q] : 0.0;
+  Y[13] = rank0 == 1 ? (double)*status : 0.0;
+  Y[14] = Y[15] = 0.0;
 }
 
-// Multi-GPU decision from the summed Y and the local pose part: the same lm_decide on every rank (identical inputs), so
-// every rank takes the same decision; the reported gradient norm is this rank's view (pose part and its own points).
+// Multi-GPU decision from the summed Y: the same lm_decide on every rank (identical inputs), so every rank takes the
+// same decision; the reported gradient norm is this rank's view (the pose part and its own points).
 __global__ __launch_bounds__(64) void dist_decide_kernel(const double* __restrict__ Y, const double* __restrict__ tpose,
-                                                         const int* __restrict__ status, const DecideOpts o,
-                                                         double* __restrict__ lm, double* __restrict__ host_rec,
-                                                         double seq) {
+                                                         int local, const DecideOpts o, double* __restrict__ lm,
+                                                         double* __restrict__ host_rec, double seq) {
   if (lm[kLmDone] != 0.0) return;
   __shared__ double s_rec[kLmFields];
   if (threadIdx.x == 0) {
+    const double* pose = local ? tpose : Y + 8;  // [pose part (5) | …, status at 6 resp. 5]
     double t[kTsCount];
-    for (int q = 0; q < 5; ++q) t[kTsPoseG + q] = tpose[q];
+    for (int q = 0; q < 5; ++q) t[kTsPoseG + q] = pose[q];
     t[kTsPtG] = Y[0];
     t[kTsPtD] = Y[1];
     t[kTsCost] = Y[2];
     t[kTsValid] = Y[3];
     t[kTsPtStep2] = Y[4];
     t[kTsPtXNorm2] = Y[5];
-    t[kTsPtGMax] = Y[6] > 0.0 ? INFINITY : tpose[5];
-    lm_decide(t, *status, o, lm);
-    lm[kLmGradNorm] = fmax(tpose[4], tpose[5]);
+    // no rank's point gradient above the tolerance: the test then depends on the pose part alone (identical)
+    t[kTsPtGMax] = Y[6] > 0.0 ? INFINITY : 0.0;
+    lm_decide(t, (int)(local ? tpose[6] : Y[13]), o, lm);
+    lm[kLmGradNorm] = fmax(pose[4], tpose[5]);
     for (int i = 0; i < kLmFields; ++i) s_rec[i] = lm[i];
   }
   if (host_rec) publish_record(s_rec, host_rec, seq);
@@ -3052,7 +3064,7 @@ int gn_prepare(pba_engine* e) {
   PBA_HIP(G.gmax.resize((size_t)(red_pose + red_pt)));
   PBA_HIP(G.red_h.resize(2 * G.red_slots));
   PBA_HIP(G.lm.resize(kLmFields));
-  PBA_HIP(G.tpose.resize(8));
+  PBA_HIP(G.tpose.resize(8));  // pose part (5), point gradient max-norm, solve status
   {  // the record of host-driven steps: not done, buffer set 0, λ NaN (the kernels then use their λ argument)
     std::vector<double> idle(kLmFields, 0.0);
     idle[kLmLambda] = std::numeric_limits<double>::quiet_NaN();
@@ -3680,6 +3692,8 @@ struct Collective {
     if (int rc = fn(user, buf, n)) return fail(PBA_ERR_DEVICE, "allreduce callback failed (" + std::to_string(rc) + ")");
     return PBA_OK;
   }
+  // dist_sums_kernel's rank flag: 1 rank 0 of a communicator, 0 another rank, −1 a host callback (ranks unknown)
+  int rank0() const { return comm ? (comm_rank(comm) == 0 ? 1 : 0) : -1; }
 };
 
 // Levenberg-Marquardt (trust_region_minimizer.cc + levenberg_marquardt_strategy.cc semantics):
@@ -3850,10 +3864,10 @@ int dist_trial(pba_engine* e, const Collective& coll, const DecideOpts& dopt, do
     if (int rc = linearize(e, nullptr, G.lm.p, G.pairs_new.p, G.rho_new.p, G.red.p + 2 * (gp + gq))) return rc;
   double* Y = X + nx;
   dist_sums_kernel<<<1, kDecideThreads, 0, e->stream>>>(G.red.p, G.red2.p, G.gmax.p, gp, gq, G.n_chunks, dopt.gtol,
-                                                         G.lm.p, G.tpose.p, Y);
+                                                         G.lm.p, G.status.p, coll.rank0(), G.tpose.p, Y);
   PBA_HIP(hipGetLastError());
   if (int rc = coll.allreduce(e, Y, kExScalars)) return rc;
-  dist_decide_kernel<<<1, 64, 0, e->stream>>>(Y, G.tpose.p, G.status.p, dopt, G.lm.p, G.lm_host_d, seq);
+  dist_decide_kernel<<<1, 64, 0, e->stream>>>(Y, G.tpose.p, coll.comm ? 0 : 1, dopt, G.lm.p, G.lm_host_d, seq);
   PBA_HIP(hipGetLastError());
   return PBA_OK;
 }

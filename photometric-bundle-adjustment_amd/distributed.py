@@ -157,10 +157,12 @@ def solve_distributed(engine, group=None, device=None, comm=None, **options) -> 
     on a GPU, the cached RCCL communicator: stream-ordered pba_solve_distributed_comm; otherwise the TorchAllReduce
     callback of pba_solve_distributed."""
     import torch.distributed as dist
+    import torch
+    if device is not None:
+        device = torch.device(device)  # "cuda", "cuda:1", torch.device(...) alike
     band = global_band(engine, group, device)
-    if comm is None and device is not None and getattr(device, "type", str(device)) == "cuda" \
-            and dist.get_backend(group) == "nccl":
-        comm = rccl_comm(group, device.index or 0)
+    if comm is None and device is not None and device.type == "cuda" and dist.get_backend(group) == "nccl":
+        comm = rccl_comm(group, device.index if device.index is not None else torch.cuda.current_device())
     if comm is not None:
         return engine.solve_distributed_comm(band, comm, **options)
     ar = TorchAllReduce(engine.gn_exchange_size(band), device if device is not None else "cpu", group)

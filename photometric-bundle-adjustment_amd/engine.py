@@ -319,7 +319,8 @@ class Engine:
         return out
 
     def residuals(self):
-        """Residuals only (the first R values of every record, one pitched copy) and the validity flags."""
+        """Residuals only (after a residual-only evaluation one contiguous copy, else the first R values of every record)
+        and the validity flags."""
         r = np.empty((self.n_blocks, self.R), np.float32)
         valid = np.empty(self.n_blocks, np.uint8)
         _check(self._L.pba_get_residuals(self._h, _p(r), _p(valid)), "pba_get_residuals")

@@ -61,6 +61,41 @@ def test_residual_only_mode(kind):
     np.testing.assert_allclose(c1, c2, rtol=1e-4, atol=1e-3)
 
 
+@pytest.mark.parametrize("kind,P", [(0, 8), (0, 21), (1, 2)])
+def test_residual_read_back_paths(kind, P):
+    """pba_get_residuals after a residual-only evaluation (the contiguous copy the Ceres adapter's LM candidates use) is
+    bit-identical to the residual part of that evaluation's records; after a Jacobian evaluation it reads the records
+    (pitched copy).  An asynchronous read-back of an earlier evaluation is not reported as arrived after a new one."""
+    import ctypes as C
+    pb = synth.make_problem(n_frames=8, n_points=200, width=376, height=240, kind=kind, seed=7, border=10)
+    if kind == 0 and P != 8:
+        disk = np.array([(dx, dy) for dy in range(-2, 3) for dx in range(-2, 3) if dx * dx + dy * dy <= 5], np.float32)
+        pb = synth.Problem(**{**pb.__dict__, "pattern": disk, "host_intensity": None})
+    with E.Engine(pb.kind, pb.model) as eng:
+        eng.set_problem(pb)
+        eng.set_state(pb.poses, pb.rho)
+        for jac in (False, True):
+            eng.evaluate(jac)
+            rec, v_rec = eng.records()
+            res, v_res = eng.residuals()
+            assert np.array_equal(v_rec, v_res)
+            assert np.array_equal(rec[:, :pb.R].view(np.uint32), res.reshape(pb.n_blocks, pb.R).view(np.uint32)), jac
+        L, h = eng._L, eng._h
+        L.pba_get_records_async.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32]
+        L.pba_wait_records.argtypes = [C.c_void_p, C.c_int32]
+        buf = C.c_void_p()
+        assert L.pba_host_alloc(C.c_size_t(rec.nbytes + pb.n_blocks), C.byref(buf)) == 0
+        try:
+            assert L.pba_get_records_async(h, buf, C.c_void_p(buf.value + rec.nbytes), 64) == 0
+            assert L.pba_wait_records(h, pb.n_blocks - 1) == 0
+            got = np.frombuffer((C.c_float * rec.size).from_address(buf.value), np.float32).reshape(rec.shape)
+            assert np.array_equal(got.view(np.uint32), rec.view(np.uint32))
+            eng.evaluate(True)  # a new evaluation: the earlier read-back no longer describes the records
+            assert L.pba_wait_records(h, 0) == -4  # PBA_ERR_NOT_READY
+        finally:
+            L.pba_host_free(buf)
+
+
 @pytest.mark.parametrize("kind,huber", [(0, 0.0), (0, 9.0), (1, 1.0)])
 def test_block_costs_match_oracle_huber(kind, huber):
     pb = synth.make_problem(n_frames=8, n_points=200, width=376, height=240, kind=kind, seed=8, border=10)
