@@ -133,9 +133,15 @@ int pba_record_format(const pba_engine* engine);
  * writes user memory during a solve without an evaluation callback, so those stay at their initial values).  Enabled,
  * every projection uses the intrinsics state (pba_set_intrinsics_state, 8·n_cams doubles; initially the cameras'),
  * host unprojection keeps the pba_set_cameras values, and each record grows by J_intr (R×8, row-major) after J_rho:
- * 22·R values.  The on-device Gauss-Newton entry points refuse such an engine (PBA_ERR_INVALID_ARGUMENT). */
+ * 22·R values.  The on-device Gauss-Newton (pba_gn_*, pba_solve) then optimises the intrinsics too: each camera's 8
+ * intrinsics are 12 unknowns of the reduced camera system after the keyframes' (two 6-dim blocks, the last four pads
+ * with identity rows), a dense border of the skyline system (SPARSE_SCHUR keeps the intrinsics blocks among the f-blocks,
+ * schur_complement_solver.cc:138-146); k ← k + δk, Ceres' LM diagonal over them too.  Single GPU only (the multi-GPU
+ * entry points refuse such an engine). */
 int pba_set_optimize_intrinsics(pba_engine* engine, int32_t enable);
 int pba_set_intrinsics_state(pba_engine* engine, const double* intrinsics);
+/* the intrinsics state (8·n_cams doubles: the free intrinsics with pba_set_optimize_intrinsics, else the cameras') */
+int pba_get_intrinsics(pba_engine* engine, double* intrinsics);
 /* Image interpolator of the photometric residual (and of the device-sampled I_h,k): PBA_INTERP_BILINEAR (default,
  * the north star's) or PBA_INTERP_BICUBIC — Ceres' BiCubicInterpolator over Grid2D<uint8_t, 1>
  * (cubic_interpolation.h:252-344, edge clamp :403-414), the interpolator of PhotometricError<8>
@@ -254,8 +260,10 @@ int pba_gn_accept(pba_engine* engine);   /* state ← candidate */
 int pba_solve(pba_engine* engine, const pba_solver_options* options, pba_solver_summary* summary);
 /* read back the state (7·n_frames poses, n_points inverse distances) */
 int pba_get_state(pba_engine* engine, double* poses, double* inv_dist);
-/* testing/inspection: reduced camera system as a dense (6·n_frames)² matrix and its right-hand side g
- * (the solve is S δ = −g), and the last step (δ poses 6·n_frames, δρ n_points) */
+/* testing/inspection: reduced camera system as a dense n² matrix, n = pba_gn_system_size (6·n_frames, + 12 per camera
+ * with free intrinsics), and its right-hand side g (the solve is S δ = −g), and the last step (δ poses 6·n_frames, δρ
+ * n_points) */
+int pba_gn_system_size(pba_engine* engine, int32_t* n);
 int pba_gn_get_reduced_system(pba_engine* engine, double* S_dense, double* g);
 int pba_gn_get_step(pba_engine* engine, double* d_poses, double* d_inv_dist);
 

@@ -608,9 +608,11 @@ void launch_pairs(pba_engine* e, const double* poses, PairRec* pairs) {
 }
 
 int launch_cost_only(pba_engine* e, const PairRec* pairs, const double* rho, double* wg_red, int* n_slots,
-                     const double* poses) {
+                     const double* poses, const float* intr_t, const double* intr_t_d) {
   KernelArgs ka = make_kernel_args(e, pairs, rho);
   ka.poses = poses;
+  if (intr_t) ka.intr_t = intr_t;
+  if (intr_t_d) ka.intr_t_d = intr_t_d;
   ka.wg_red = wg_red;
   launch_mode(e, ka, 2);
   if (n_slots) *n_slots = e->last_grid;
@@ -738,7 +740,21 @@ int pba_set_optimize_intrinsics(pba_engine* e, int32_t enable) {
   }
   e->opt_intr = on;
   e->evaluated = false;
+  e->gn.prepared = false;  // the reduced camera system gains / loses its intrinsics border
   if (e->n_blocks > 0) PBA_HIP(e->out.resize((size_t)e->n_blocks * e->rec_floats()));
+  return PBA_OK;
+}
+
+int pba_get_intrinsics(pba_engine* e, double* intrinsics) {
+  if (!e || !intrinsics) return fail(PBA_ERR_INVALID_ARGUMENT, "null argument");
+  if (e->n_cams <= 0) return fail(PBA_ERR_NOT_READY, "pba_set_cameras first");
+  if (int rc = check_device(e)) return rc;
+  std::vector<double> k((size_t)kCamD * e->n_cams);
+  PBA_HIP(hipMemcpyAsync(k.data(), e->opt_intr ? e->intr_state_d.p : e->intr_d.p, sizeof(double) * k.size(),
+                         hipMemcpyDeviceToHost, e->stream));
+  PBA_HIP(hipStreamSynchronize(e->stream));
+  for (int c = 0; c < e->n_cams; ++c)
+    for (int j = 0; j < 8; ++j) intrinsics[8 * c + j] = k[(size_t)kCamD * c + j];
   return PBA_OK;
 }
 

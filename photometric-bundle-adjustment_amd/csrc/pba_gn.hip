@@ -2101,6 +2101,11 @@ __device__ __forceinline__ void wg_reduce_sum_max(double (&v)[N], double m, doub
   }
 }
 
+// ib_data per GN block (free intrinsics, intr_rows_kernel): weighted fp64 rows J_i (2×8) | J_h (2×6) | J_t (2×6) | J_ρ (2) |
+// r (2), and W_i = J_iᵀJ_ρ (8)
+constexpr int kIbStride = 52;
+constexpr int kIbJi = 0, kIbJh = 16, kIbJt = 28, kIbJr = 40, kIbR = 42, kIbWi = 44;
+
 // The update workgroups' partials besides the model decrease (slot layout of red): Σ|x − x_new|² and Σ|x_new|² in the
 // ambient parameter space (red2, two doubles per slot: Ceres' step_norm and x_norm, trust_region_minimizer.cc:706-726,
 // :813-814) and max |x − (x ⊞ −g)| at the current state (gmax, one double per slot: gradient_max_norm,
@@ -2115,7 +2120,11 @@ struct PoseUpdateArgs {
   double* red;
   double* red2;
   double* gmax;
-  int n;
+  int n;                 // system frames: the keyframes, then two per camera with free intrinsics
+  int nf;                // keyframes
+  const double* kcur;    // free intrinsics: the state's camera records (projection part) …
+  double* knew_d;        // … the candidate's (camera records) …
+  float* knew_f;         // … and their fp32 copy (8 per camera)
 };
 
 
@@ -2159,13 +2168,37 @@ __device__ __forceinline__ void candidate_pose(const FrameIn& f, double* out) {
   }
 }
 
+// A free camera's intrinsics (system frames nf + 2c, nf + 2c + 1: dims 6h … 6h + 5 of the 8, the rest pads): k ← k + δ
+// (a plain parameter block, no local parameterisation), with the same model-decrease, norm and gradient partials.
+__device__ __forceinline__ void intr_update_frame(const PoseUpdateArgs& a, int i, double* v, double& gm) {
+  const int c = (i - a.nf) >> 1, h = (i - a.nf) & 1;
+  const bool fx = a.fixed[i] != 0;
+#pragma unroll
+  for (int r = 0; r < 6; ++r) {
+    const int d = 6 * h + r;
+    if (d >= 8) break;
+    const double xk = a.x[6 * i + r], gk = a.g_dir[6 * i + r], Dk = a.Ddiag[6 * i + r];
+    const double k = a.kcur[kCamD * c + d], kn = fx ? k : k + xk;
+    a.knew_d[kCamD * c + d] = kn;
+    a.knew_f[8 * c + d] = (float)kn;
+    if (fx) continue;
+    v[0] += xk * gk;
+    v[1] += xk * xk * Dk;
+    v[2] += (kn - k) * (kn - k);
+    v[3] += kn * kn;
+    gm = fmax(gm, fabs(gk));  // |k − (k − g)|
+  }
+}
+
 __device__ __forceinline__ void pose_update_block(const PoseUpdateArgs& a, const LmView& lv, int blk) {
   const int i = blk * blockDim.x + threadIdx.x;
   double v[4] = {0.0, 0.0, 0.0, 0.0};  // x·g, x·D·x, |T − T_new|², |T_new|²
   double gm = 0.0;
-  const FrameIn f = frame_in(a, min(i, a.n - 1), true);  // in flight with the record's load; then the done test
+  const FrameIn f = frame_in(a, min(i, a.nf - 1), true);  // in flight with the record's load; then the done test
   if (lv.done != 0.0) return;  // (uniform)
-  if (i < a.n) {
+  if (i >= a.nf && i < a.n) {
+    intr_update_frame(a, i, v, gm);
+  } else if (i < a.n) {
     double tn[7];
     candidate_pose(f, tn);
     double* out = a.poses_new + 7 * i;
@@ -2209,6 +2242,9 @@ struct PointUpdateArgs {
   double* red2;
   double* gmax;
   int n_points;
+  const double* ib;      // free intrinsics: per GN block W_i (ib_data), its target's camera, and the keyframe count
+  const int* ib_cam;     // (the intrinsics steps start at x[6·nf], 12 per camera)
+  int nf;
 };
 
 // blk: the point workgroup's index among the point workgroups; slot: its reduction slot
@@ -2279,6 +2315,14 @@ __device__ __forceinline__ void point_update_block(const PointUpdateArgs& a, con
         if (b0 + u < fb + nb)
 #pragma unroll
           for (int i = 0; i < 6; ++i) s += (double)w[u][i] * xt[u][i];
+    }
+    if (a.ib) {  // + Σ_b W_i(b)·δk(camera of b's target)
+      for (int b = fb; b < fb + nb; ++b) {
+        const double* wi = a.ib + (long long)b * kIbStride + kIbWi;
+        const double* xk = a.x + 6 * a.nf + 12 * a.ib_cam[b];
+#pragma unroll
+        for (int d = 0; d < 8; ++d) s += wi[d] * xk[d];
+      }
     }
 #ifdef PBA_UPD_STAMPS
     ts[1] = wall_clock64();
@@ -2372,6 +2416,219 @@ __global__ __launch_bounds__(kBlockThreads) void update_kernel(const PoseUpdateA
     camera_kf(tk, r.kf);
     ra.pairs_new[i] = r;
   }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Free intrinsics in the reduced camera system (pba_set_optimize_intrinsics; geometric engines)
+// ------------------------------------------------------------------------------------------------
+// bundle_adjustment() with BundleAdjustmentOptions::optimize_intrinsics leaves the cameras' 8-vector intrinsics blocks
+// free (map_utils.h:339-345); the functor differentiates the TARGET camera's intrinsics (reprojection.h:83-86, :108) and
+// SPARSE_SCHUR keeps those blocks among the f-blocks of the reduced camera system (schur_complement_solver.cc:138-146).
+// Here camera c's intrinsics are the system frames nf + 2c (dims 0-5) and nf + 2c + 1 (dims 6-7, then four identity
+// pads): a dense border of the skyline system (their profile starts at frame 0).  The keyframe part is linearised,
+// eliminated and assembled as without intrinsics; the border — the blocks' direct terms J_iᵀJ_x and the points' Schur
+// terms −W_i,c W_xᵀ / H'_ρρ — is formed in fp64 by intr_border_kernel, one lane per element, in a fixed order (the CSR lists
+// of gn_prepare), from weighted fp64 rows (intr_rows_kernel) and schur_kernel's undamped H_ρρ.
+struct IntrRowsArgs {
+  const int4* rec;       // GN block → {block, point, host, target}
+  const double* poses;
+  const double* rho;
+  const double2* u_ref;
+  const double2* u_obs;
+  const int* frame_cam;
+  const double* cams;    // host unprojection: the cameras (the functor's captured intrinsics, reprojection.h:93-98)
+  const double* kt;      // target projection: the intrinsics state (camera records)
+  double huber;
+  double* out;           // ib_data
+  int n;
+  const double* lm;      // LM record: nothing to do once the solve is done
+};
+struct PoseT {  // a relative pose for pair_rotation / pair_translation
+  double R[9], t[3];
+  float Rf[9], tf[3];
+};
+
+// One lane per GN block at the current state: r = u_obs − π_t(T_th b/ρ) and its Jacobians (the geometric_row chain, in
+// fp64), J_i = −∂π/∂k (project_intr_jac), Ceres' Corrector weighting √ρ' (corrector.cc, ρ'' ≤ 0 for Huber), W_i = J_iᵀJ_ρ.
+template <int MODEL>
+__global__ __launch_bounds__(256) void intr_rows_kernel(const IntrRowsArgs a) {
+  const int gb = blockIdx.x * blockDim.x + threadIdx.x;
+  if (gb >= a.n || lm_view(a.lm).done != 0.0) return;
+  const int4 br = a.rec[gb];
+  PoseT T;
+  pair_rotation(a.poses + 7 * br.z, a.poses + 7 * br.w, T);
+  pair_translation(a.poses + 7 * br.z, a.poses + 7 * br.w, T);
+  const int hc = a.frame_cam[br.z], tc = a.frame_cam[br.w];
+  const double* kt = a.kt + kCamD * tc;
+  const double2 ur = a.u_ref[br.y], uo = a.u_obs[br.x];
+  const double irho = 1.0 / a.rho[br.y];
+  const Vec3d b = unproject<MODEL>(a.cams + kCamD * hc + kCamHk, ur.x, ur.y);
+  const Vec3d ph = {b.x * irho, b.y * irho, b.z * irho};
+  const Vec3d Rp = mat_mul(T.R, ph);
+  const Vec3d p = {Rp.x + T.t[0], Rp.y + T.t[1], Rp.z + T.t[2]};
+  double u, v;
+  const double iden = project<MODEL>(kt, p, u, v);
+  double J[kIbStride];
+  J[kIbR] = uo.x - u;
+  J[kIbR + 1] = uo.y - v;
+  Vec3d du, dv;
+  project_jac<MODEL>(kt, p, iden, du, dv);
+  double ku[8], kv[8];
+  project_intr_jac<MODEL>(kt, p, iden, ku, kv);
+  const Vec3d td = {T.t[0], T.t[1], T.t[2]};
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const Vec3d d = i == 0 ? du : dv;
+    const Vec3d g = {-d.x, -d.y, -d.z};  // ∂r/∂p = −∂π/∂p
+    const Vec3d gR = row_mul(g, T.R);
+    const Vec3d wh = cross(ph, gR);
+    const Vec3d wt = cross(g, p);
+    double* jh = J + kIbJh + 6 * i;
+    double* jt = J + kIbJt + 6 * i;
+    jh[0] = gR.x; jh[1] = gR.y; jh[2] = gR.z; jh[3] = wh.x; jh[4] = wh.y; jh[5] = wh.z;
+    jt[0] = -g.x; jt[1] = -g.y; jt[2] = -g.z; jt[3] = wt.x; jt[4] = wt.y; jt[5] = wt.z;
+    J[kIbJr + i] = dot(g, td) * irho;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) J[kIbJi + 8 * i + j] = -(i == 0 ? ku[j] : kv[j]);
+  }
+  bool ok = true;
+#pragma unroll
+  for (int q = 0; q < kIbWi; ++q) ok = ok && isfinite(J[q]);
+  const double s2 = J[kIbR] * J[kIbR] + J[kIbR + 1] * J[kIbR + 1], hb = a.huber;
+  const double w = (hb <= 0.0 || s2 <= hb * hb) ? 1.0 : hb / sqrt(s2);
+  const double sw = ok ? sqrt(w) : 0.0;
+#pragma unroll
+  for (int q = 0; q < kIbWi; ++q) J[q] = ok ? sw * J[q] : 0.0;
+#pragma unroll
+  for (int d = 0; d < 8; ++d) J[kIbWi + d] = J[kIbJi + d] * J[kIbJr] + J[kIbJi + 8 + d] * J[kIbJr + 1];
+  double* o = a.out + (long long)gb * kIbStride;
+#pragma unroll
+  for (int q = 0; q < kIbStride; q += 2) *reinterpret_cast<double2*>(o + q) = make_double2(J[q], J[q + 1]);
+}
+
+struct IntrBorderArgs {
+  const double* ib;        // ib_data
+  const int4* ib_rec;      // GN block → {block, point, host, target}
+  const int* ib_cam;       // GN block → its target's camera
+  const int4* pt_rec;      // GN point → {first GN block, block count, host, point}
+  const double* pt_data;   // GN point → [H_ρρ (undamped), g_ρ, …] (schur_kernel of this solve)
+  const int* bptr;         // border unit pair (c, u) = c·(nf + nc) + u → direct-term GN blocks …
+  const int* blist;
+  const int* pptr;         // … and Schur-term GN points
+  const int* plist;
+  const int* sky_first;
+  const int* sky_row;
+  const uint8_t* fixed;    // system frames
+  const double* lm;
+  double* S;
+  double* g;
+  double* g_dir;
+  double* Ddiag;
+  int nf, nc;
+};
+
+// Σ_b [h_b = x] J_h(b)ᵀJ_ρ(b) + [t_b = x] J_t(b)ᵀJ_ρ(b), column j (a point's W for keyframe x), or, for a camera
+// column (x < 0: camera −x − 1), Σ_b [camera of t_b = c] W_i(b)[j]: over the point's GN blocks in order.
+__device__ __forceinline__ double point_w(const IntrBorderArgs& a, int4 pr, int x, int j) {
+  double w = 0.0;
+  for (int b = pr.x; b < pr.x + pr.y; ++b) {
+    const double* B = a.ib + (long long)b * kIbStride;
+    if (x < 0) {
+      if (a.ib_cam[b] == -x - 1) w += B[kIbWi + j];
+    } else {
+      const int4 r = a.ib_rec[b];
+      if (r.z == x) w += B[kIbJh + j] * B[kIbJr] + B[kIbJh + 6 + j] * B[kIbJr + 1];
+      if (r.w == x) w += B[kIbJt + j] * B[kIbJr] + B[kIbJt + 6 + j] * B[kIbJr + 1];
+    }
+  }
+  return w;
+}
+
+// Grid (x: the row's elements, y: border row 0 … 2nc − 1): lane t < (P + 1)·36 → element (r, cc) of block (P, y = t / 36)
+// of the skyline system (P = nf + row); lanes nfs·36 … nfs·36 + 5 → g of P.  The keyframe blocks (P, x < nf) and the
+// camera blocks (P, y ≥ nf) get direct − Schur terms, + λ·clamp(diag) on the diagonal (the direct part is Ceres' LM
+// diagonal), identity pads, and — constant frames / unobserved cameras — identity rows and columns, as assemble_kernel.
+__global__ __launch_bounds__(256) void intr_border_kernel(const IntrBorderArgs a, double lambda) {
+  const LmView lv = lm_view(a.lm);
+  lambda = lm_lambda(lv, lambda);
+  const int row = blockIdx.y, P = a.nf + row, nfs = a.nf + 2 * a.nc, nu = a.nf + a.nc;
+  const int c = row >> 1, h = row & 1;
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  auto inv_of = [&](int gp) {
+    const double H = a.pt_data[(long long)gp * 8];
+    const double Hd = H + lambda * fmin(fmax(H, 1e-6), 1e32);
+    return Hd > 0.0 ? 1.0 / Hd : 0.0;
+  };
+  if (t >= nfs * 36) {  // the gradient of P
+    const int r = t - nfs * 36, d = 6 * h + r;
+    if (r >= 6) return;
+    double dir = 0.0, sch = 0.0;
+    if (d < 8) {
+      const int L = c * nu + a.nf + c;
+      for (int q = a.bptr[L]; q < a.bptr[L + 1]; ++q) {
+        const double* B = a.ib + (long long)a.blist[q] * kIbStride;
+        dir += B[kIbJi + d] * B[kIbR] + B[kIbJi + 8 + d] * B[kIbR + 1];
+      }
+      for (int q = a.pptr[L]; q < a.pptr[L + 1]; ++q) {
+        const int gp = a.plist[q];
+        sch += inv_of(gp) * point_w(a, a.pt_rec[gp], -c - 1, d) * a.pt_data[(long long)gp * 8 + 1];
+      }
+    }
+    const bool fx = a.fixed[P] != 0;
+    a.g[6 * P + r] = fx ? 0.0 : dir - sch;
+    a.g_dir[6 * P + r] = fx ? 0.0 : dir;
+    if (fx) a.Ddiag[6 * P + r] = 0.0;
+    return;
+  }
+  if (t >= (P + 1) * 36) return;
+  const int y = t / 36, e = t % 36, r = e / 6, cc = e % 6, d = 6 * h + r;
+  const bool cam = y >= a.nf;
+  const int c2 = cam ? (y - a.nf) >> 1 : 0, d2 = cam ? 6 * ((y - a.nf) & 1) + cc : cc;
+  double dir = 0.0, sch = 0.0;
+  if (d < 8 && d2 < 8) {
+    const int L = c * nu + (cam ? a.nf + c2 : y);
+    for (int q = a.bptr[L]; q < a.bptr[L + 1]; ++q) {
+      const int b = a.blist[q];
+      const double* B = a.ib + (long long)b * kIbStride;
+      double c0, c1;  // column d2 / cc of the block's Jacobian for y
+      if (cam) {
+        c0 = B[kIbJi + d2];
+        c1 = B[kIbJi + 8 + d2];
+      } else {
+        const int4 rr = a.ib_rec[b];
+        c0 = rr.z == y ? B[kIbJh + cc] : B[kIbJt + cc];
+        c1 = rr.z == y ? B[kIbJh + 6 + cc] : B[kIbJt + 6 + cc];
+      }
+      dir += B[kIbJi + d] * c0 + B[kIbJi + 8 + d] * c1;
+    }
+    for (int q = a.pptr[L]; q < a.pptr[L + 1]; ++q) {
+      const int gp = a.plist[q];
+      const int4 pr = a.pt_rec[gp];
+      sch += inv_of(gp) * point_w(a, pr, -c - 1, d) * point_w(a, pr, cam ? -c2 - 1 : y, d2);
+    }
+  } else if (y == P && r == cc) {
+    dir = 1.0;  // pad
+  }
+  double val = dir - sch;
+  if (a.fixed[P] || a.fixed[y]) {
+    val = (y == P && r == cc) ? 1.0 : 0.0;
+  } else if (y == P && r == cc) {
+    const double D = fmin(fmax(dir, 1e-6), 1e32);  // levenberg_marquardt_strategy.cc: the undamped JᵀJ diagonal
+    a.Ddiag[6 * P + r] = D;
+    val += lambda * D;
+  }
+  a.S[((long long)a.sky_row[P] + (y - a.sky_first[P])) * 36 + e] = val;
+}
+
+// The candidate intrinsics become the state (after an accepted trial; lm == nullptr: always), fp64 records and fp32 copy.
+__global__ void intr_accept_kernel(const double* __restrict__ lm, const double* __restrict__ knew_d,
+                                   const float* __restrict__ knew_f, double* __restrict__ k_d, float* __restrict__ k_f,
+                                   int nc) {
+  if (lm && (lm[kLmAccept] == 0.0 || lm[kLmDone] != 0.0)) return;
+  const int i = threadIdx.x, c = i >> 3, d = i & 7;
+  if (c >= nc) return;
+  k_d[kCamD * c + d] = knew_d[kCamD * c + d];
+  k_f[8 * c + d] = knew_f[8 * c + d];
 }
 
 __global__ __launch_bounds__(kBlockThreads) void cost_reduce_kernel(const float* cost, const uint8_t* valid, int n,
@@ -2934,21 +3191,26 @@ int gn_prepare(pba_engine* e) {
     for (size_t a = 0; a < poses.size(); ++a)
       gcon[poses[a]].push_back(make_int2(o + 36 * (int)schur_used[s].size() + 6 * (int)a, C_SCHUR));
   }
-  for (int i = 0; i < nf; ++i) contrib[{i, i}];  // every diagonal block exists
-  std::vector<int> first(nf), rowp(nf + 1), last(nf);
-  for (int i = 0; i < nf; ++i) first[i] = i;
+  // free intrinsics (geometric): two system frames per camera after the keyframes, a dense border (profile from 0)
+  const int nc = (e->opt_intr && e->opt.residual_kind == PBA_RESIDUAL_GEOMETRIC) ? e->n_cams : 0;
+  const int nfs = nf + 2 * nc;
+  G.nc_sys = nc;
+  G.nfs = nfs;
+  for (int i = 0; i < nfs; ++i) contrib[{i, i}];  // every diagonal block exists
+  std::vector<int> first(nfs), rowp(nfs + 1), last(nfs);
+  for (int i = 0; i < nfs; ++i) first[i] = i < nf ? i : 0;
   for (auto& kv : contrib) first[kv.first.first] = std::min(first[kv.first.first], kv.first.second);
   rowp[0] = 0;
-  for (int i = 0; i < nf; ++i) rowp[i + 1] = rowp[i] + (i - first[i] + 1);
-  G.n_sky = rowp[nf];
+  for (int i = 0; i < nfs; ++i) rowp[i + 1] = rowp[i] + (i - first[i] + 1);
+  G.n_sky = rowp[nfs];
   G.band = 0;
-  for (int i = 0; i < nf; ++i) G.band = std::max(G.band, i - first[i]);
-  for (int k = 0; k < nf; ++k) last[k] = k;
-  for (int i = 0; i < nf; ++i)
+  for (int i = 0; i < nfs; ++i) G.band = std::max(G.band, i - first[i]);
+  for (int k = 0; k < nfs; ++k) last[k] = k;
+  for (int i = 0; i < nfs; ++i)
     for (int k = first[i]; k < i; ++k) last[k] = std::max(last[k], i);
   std::vector<int> cptr(G.n_sky + 1, 0), bi(G.n_sky), bj(G.n_sky);
   std::vector<std::vector<int2>> per(G.n_sky);
-  for (int i = 0; i < nf; ++i)
+  for (int i = 0; i < nfs; ++i)
     for (int j = first[i]; j <= i; ++j) {
       const int s = rowp[i] + (j - first[i]);
       bi[s] = i;
@@ -2964,16 +3226,68 @@ int gn_prepare(pba_engine* e) {
     flat.insert(flat.end(), per[s].begin(), per[s].end());
   }
   cptr[G.n_sky] = (int)flat.size();
-  std::vector<int> gptr(nf + 1);
+  std::vector<int> gptr(nfs + 1);
   std::vector<int2> gflat;
-  for (int i = 0; i < nf; ++i) {
+  for (int i = 0; i < nfs; ++i) {
     gptr[i] = (int)gflat.size();
-    gflat.insert(gflat.end(), gcon[i].begin(), gcon[i].end());
+    if (i < nf) gflat.insert(gflat.end(), gcon[i].begin(), gcon[i].end());
   }
-  gptr[nf] = (int)gflat.size();
-  // constant frames: requested + never observed
-  std::vector<uint8_t> fixed(nf, 0);
+  gptr[nfs] = (int)gflat.size();
+  // constant frames: requested + never observed; a camera whose intrinsics no block projects with is constant too
+  std::vector<uint8_t> fixed(nfs, 0);
   for (int i = 0; i < nf; ++i) fixed[i] = (i < (int)G.fixed_h.size() && G.fixed_h[i]) || !observed[i];
+  if (nc) {
+    // the border's CSR lists: unit pair (camera c, unit u), u < nf keyframe u, u ≥ nf camera u − nf; direct terms from
+    // the blocks whose target camera is c and that touch u (host or target u; u = c: every block of camera c), Schur
+    // terms from the points with a block of camera c that touch u (a block of keyframe u / of camera u − nf)
+    const int nu = nf + nc;
+    std::vector<std::vector<int>> bl((size_t)nc * nu), pl((size_t)nc * nu);
+    std::vector<int> bcam(nb);
+    std::vector<int4> ibrec(nb);
+    std::vector<char> cam_seen(nc, 0);
+    for (int gb = 0; gb < nb; ++gb) {
+      const int b = order[gb], pt = e->block_point_h[b], h = ph[pt], t = e->block_target_h[b], c = e->frame_cam_h[t];
+      bcam[gb] = c;
+      ibrec[gb] = make_int4(b, pt, h, t);
+      cam_seen[c] = 1;
+      bl[(size_t)c * nu + h].push_back(gb);
+      bl[(size_t)c * nu + t].push_back(gb);
+      bl[(size_t)c * nu + nf + c].push_back(gb);
+    }
+    for (int q = 0; q < ngp; ++q) {
+      std::vector<int> cams, units{phost[q]};
+      for (int gb = pfirst[q]; gb < pfirst[q] + pnblk[q]; ++gb) {
+        if (std::find(cams.begin(), cams.end(), bcam[gb]) == cams.end()) cams.push_back(bcam[gb]);
+        if (std::find(units.begin(), units.end(), gtgt[gb]) == units.end()) units.push_back(gtgt[gb]);
+      }
+      for (int c : cams) units.push_back(nf + c);
+      for (int c : cams)
+        for (int u : units) pl[(size_t)c * nu + u].push_back(q);
+    }
+    std::vector<int> bp(1, 0), bflat, pp(1, 0), pflat;
+    for (size_t L = 0; L < bl.size(); ++L) {
+      bflat.insert(bflat.end(), bl[L].begin(), bl[L].end());
+      bp.push_back((int)bflat.size());
+      pflat.insert(pflat.end(), pl[L].begin(), pl[L].end());
+      pp.push_back((int)pflat.size());
+    }
+    if (bflat.empty()) bflat.push_back(0);
+    if (pflat.empty()) pflat.push_back(0);
+    for (int c = 0; c < nc; ++c) fixed[nf + 2 * c] = fixed[nf + 2 * c + 1] = !cam_seen[c];
+    hipStream_t st0 = e->stream;
+    PBA_HIP(G.ib_rec.upload(ibrec, st0));
+    PBA_HIP(G.ib_cam.upload(bcam, st0));
+    PBA_HIP(G.ib_bptr.upload(bp, st0));
+    PBA_HIP(G.ib_blist.upload(bflat, st0));
+    PBA_HIP(G.ib_pptr.upload(pp, st0));
+    PBA_HIP(G.ib_plist.upload(pflat, st0));
+    PBA_HIP(G.ib_data.resize((size_t)nb * kIbStride));
+    PBA_HIP(G.intr_new_d.resize((size_t)kCamD * nc));
+    PBA_HIP(G.intr_new_f.resize((size_t)8 * nc));
+    // the candidate records start as the state's (their unprojection half is never read: hosts unproject with the cameras)
+    PBA_HIP(hipMemcpyAsync(G.intr_new_d.p, e->intr_state_d.p, sizeof(double) * kCamD * nc, hipMemcpyDeviceToDevice, st0));
+    PBA_HIP(hipMemcpyAsync(G.intr_new_f.p, e->intr_state.p, sizeof(float) * 8 * nc, hipMemcpyDeviceToDevice, st0));
+  }
   // upload
   hipStream_t st = e->stream;
   if (e->n_pairs >= (1 << 24)) return fail(PBA_ERR_INVALID_ARGUMENT, "more than 2^24 (host, target) pairs");
@@ -3031,7 +3345,7 @@ int gn_prepare(pba_engine* e) {
   PBA_HIP(G.L.resize((size_t)G.n_sky * 36));
   // solver choice: block cyclic reduction (bandwidth ≤ 8), LDS-window band Cholesky (≤ 16), skyline (any).
   // PBA_SOLVER=cr|band|skyline forces one (test hook; cr/band fall back when the bandwidth does not allow).
-  const int K = band_kernel_for(G.band);
+  const int K = nc ? 0 : band_kernel_for(G.band);  // the intrinsics border: skyline
   int solver = K && K <= 8 ? SOLVER_CR : (K ? SOLVER_BAND : SOLVER_SKYLINE);
   if (const char* fs = getenv("PBA_SOLVER")) {
     const std::string f(fs);
@@ -3045,17 +3359,17 @@ int gn_prepare(pba_engine* e) {
   for (int i = 0; i < nf && i < (int)G.fixed_h.size(); ++i) req[i] = G.fixed_h[i];
   PBA_HIP(G.fixed_req.upload(req, st));
   PBA_HIP(G.fixed_dist.resize(nf));
-  PBA_HIP(G.g.resize((size_t)nf * 6));
-  PBA_HIP(G.g_dir.resize((size_t)nf * 6));
-  PBA_HIP(G.Ddiag.resize((size_t)nf * 6));
-  PBA_HIP(G.Linv.resize((size_t)nf * 36));
-  PBA_HIP(G.x.resize((size_t)nf * 6));
+  PBA_HIP(G.g.resize((size_t)nfs * 6));
+  PBA_HIP(G.g_dir.resize((size_t)nfs * 6));
+  PBA_HIP(G.Ddiag.resize((size_t)nfs * 6));
+  PBA_HIP(G.Linv.resize((size_t)nfs * 36));
+  PBA_HIP(G.x.resize((size_t)nfs * 6));
   PBA_HIP(G.poses_new.resize((size_t)nf * 7));
   PBA_HIP(G.rho_new.resize((size_t)e->n_points));
   PBA_HIP(G.drho.resize((size_t)e->n_points));
   PBA_HIP(G.pairs_new.resize((size_t)e->n_pairs));
   PBA_HIP(G.status.resize(1));
-  const int red_pose = (nf + kBlockThreads - 1) / kBlockThreads;
+  const int red_pose = (nfs + kBlockThreads - 1) / kBlockThreads;
   const int red_pt = (ngp + kBlockThreads - 1) / kBlockThreads;
   // update partials, then the candidate cost's workgroup partials (≤ one per 16 blocks: launch_cost_only's grids)
   G.red_slots = red_pose + red_pt + std::max({1024, nb / 16 + 2, G.n_chunks});
@@ -3120,8 +3434,6 @@ int ensure_prepared(pba_engine* e) {
   if (!e->state_set) return fail(PBA_ERR_NOT_READY, "pba_set_state first");
   if (e->opt.residual_kind == PBA_RESIDUAL_PHOTOMETRIC && (!e->have_images || e->P <= 0))
     return fail(PBA_ERR_NOT_READY, "images/pattern missing");
-  if (e->opt_intr)  // the reduced camera system has no intrinsics blocks
-    return fail(PBA_ERR_INVALID_ARGUMENT, "intrinsics optimisation runs through the Ceres adapter (pba_ceres.h) only");
   if (int rc = check_device(e)) return rc;
   if (!e->gn.prepared)
     if (int rc = gn_prepare(e)) return rc;
@@ -3157,14 +3469,19 @@ int total_cost(pba_engine* e, double* cost, int* n_valid) {
 // Linearisation at the engine's state (pairs == nullptr: formed here), or — the device LM loop — at the candidate:
 // lm = the device LM record (the pieces go to the spare buffer set, nothing runs once the solve is done), pairs / rho
 // the candidate's, and wg_red the slots of the per-chunk cost partials the decision sums.
+// cand_intr: with free intrinsics, project with the candidate's (G.intr_new_*) instead of the state's.
 int linearize(pba_engine* e, double* cost, const double* lm = nullptr, const PairRec* pairs = nullptr,
-              const double* rho = nullptr, double* wg_red = nullptr, int* n_valid = nullptr) {
+              const double* rho = nullptr, double* wg_red = nullptr, int* n_valid = nullptr, bool cand_intr = false) {
   GnData& G = e->gn;
   if (!pairs) {
     launch_pairs(e, e->poses.p, e->pairs.p);
     pairs = e->pairs.p;
   }
-  const KernelArgs ka = make_kernel_args(e, pairs, rho ? rho : e->rho.p);
+  KernelArgs ka = make_kernel_args(e, pairs, rho ? rho : e->rho.p);
+  if (cand_intr && G.nc_sys) {
+    ka.intr_t = G.intr_new_f.p;
+    ka.intr_t_d = G.intr_new_d.p;
+  }
   LinArgs la{G.lin_rec.p, G.blk_schur1.p, G.part_lin1.p, wg_red, G.chunk_desc.p, G.blk_schur.p, G.part_lin.p, G.n_chunks, lm ? lm : G.lm_idle.p, lm != nullptr};
   if (e->opt.residual_kind == PBA_RESIDUAL_PHOTOMETRIC) launch_linearize_photometric(e, ka, la);
   else launch_linearize_geometric(e, ka, la);
@@ -3299,15 +3616,17 @@ void cr_solve(pba_engine* e, bool build) {
 void enqueue_updates(pba_engine* e, double lambda, const uint8_t* fixed, int* gp_out, int* gq_out,
                      const double* lm = nullptr) {
   GnData& G = e->gn;
-  const int nf = e->n_frames;
-  const int gp = (nf + kBlockThreads - 1) / kBlockThreads;
+  const int nf = e->n_frames, nfs = G.nc_sys ? G.nfs : nf;
+  const int gp = (nfs + kBlockThreads - 1) / kBlockThreads;
   const int gq = (G.n_gn_points + kBlockThreads - 1) / kBlockThreads;
   const int gr = (e->n_pairs + kBlockThreads - 1) / kBlockThreads;
-  PoseUpdateArgs pa{e->poses.p, G.x.p, G.g_dir.p, G.Ddiag.p, fixed, G.poses_new.p, G.red.p, G.red2.p, G.gmax.p, nf};
+  const bool ki = G.nc_sys > 0;
+  PoseUpdateArgs pa{e->poses.p, G.x.p, G.g_dir.p, G.Ddiag.p, fixed, G.poses_new.p, G.red.p, G.red2.p, G.gmax.p, nfs, nf,
+                    ki ? e->intr_state_d.p : nullptr, ki ? G.intr_new_d.p : nullptr, ki ? G.intr_new_f.p : nullptr};
   // point workgroup q writes reduction slot gp + q, as the separate launches did
   PointUpdateArgs qa{G.pt_data.p, G.pt_rec.p, G.pt_tgt.p, G.gn_target.p,
                      G.blk_schur.p, G.blk_schur1.p, G.x.p, fixed, e->rho.p, G.rho_new.p, G.drho.p, G.red.p,
-                     G.red2.p, G.gmax.p, G.n_gn_points};
+                     G.red2.p, G.gmax.p, G.n_gn_points, ki ? G.ib_data.p : nullptr, G.ib_cam.p, nf};
   PairUpdateArgs ra{G.pair_rec.p, e->intr_d.p, G.pairs_new.p, e->n_pairs};
   update_kernel<<<gp + gq + gr, kBlockThreads, 0, e->stream>>>(pa, qa, ra, gp, gq, lambda, lm ? lm : G.lm_idle.p);
   G.pairs_new_fresh = true;
@@ -3369,12 +3688,25 @@ void schur_lds_limit(const GnData& G) {
 // lm: the device LM record (λ, buffer set, done flag read on the device; lambda unused) or nullptr.
 int enqueue_solve(pba_engine* e, double lambda, const double* lm = nullptr) {
   GnData& G = e->gn;
-  const int nf = e->n_frames;
+  const int nf = e->n_frames, nfs = G.nc_sys ? G.nfs : nf;
   SchurArgs sa{G.schur_desc.p, G.schur_aux.p, G.schur_pairs.p, G.pt_fb.p, G.blk_lv.p,
                G.blk_schur.p, G.blk_schur1.p, G.part_schur.p, G.pt_data.p, G.n_schur, lm ? lm : G.lm_idle.p,
                lm ? e->poses.p : nullptr, G.poses_new.p, e->rho.p, G.rho_new.p, G.pt_orig.p, 7 * nf, G.n_gn_points};
   schur_lds_limit(G);
   schur_kernel<<<G.n_schur, kBlockThreads, G.schur_lds, e->stream>>>(sa, lambda);
+  if (G.nc_sys) {  // free intrinsics: the last trial's accept, then the weighted fp64 rows at the state
+    if (lm) intr_accept_kernel<<<1, 256, 0, e->stream>>>(lm, G.intr_new_d.p, G.intr_new_f.p, e->intr_state_d.p,
+                                                         e->intr_state.p, G.nc_sys);
+    IntrRowsArgs ra{G.ib_rec.p, e->poses.p, e->rho.p, e->u_ref.p, e->u_obs.p, e->frame_cam.p, e->intr_d.p,
+                    e->intr_state_d.p, (double)e->opt.huber_width, G.ib_data.p, e->n_blocks, lm ? lm : G.lm_idle.p};
+    const int grid = (e->n_blocks + 255) / 256;
+    switch (e->opt.camera_model) {
+      case PBA_CAMERA_PINHOLE: intr_rows_kernel<CAM_PINHOLE><<<grid, 256, 0, e->stream>>>(ra); break;
+      case PBA_CAMERA_DOUBLE_SPHERE: intr_rows_kernel<CAM_DS><<<grid, 256, 0, e->stream>>>(ra); break;
+      case PBA_CAMERA_EUCM: intr_rows_kernel<CAM_EUCM><<<grid, 256, 0, e->stream>>>(ra); break;
+      default: intr_rows_kernel<CAM_KB4><<<grid, 256, 0, e->stream>>>(ra); break;
+    }
+  }
   // block cyclic reduction: assemble writes its level 0 directly (no Sband, no cr_build pass)
   const bool direct = G.band_kernel && G.solver == SOLVER_CR;
   if (direct && G.cr0_dirty)  // a distributed solve rebuilt level 0 over the whole band: back to zeros + padding
@@ -3382,19 +3714,25 @@ int enqueue_solve(pba_engine* e, double lambda, const double* lm = nullptr) {
   CrLevel L0 = direct ? cr_level(G, 0) : CrLevel{};
   AsmArgs aa{G.part_lin.p, G.part_lin1.p, lm ? lm : G.lm_idle.p, G.part_schur.p, G.sky_cptr.p, G.sky_contrib.p, G.g_cptr.p,
              G.g_contrib.p, G.sky_blk_i.p, G.sky_blk_j.p, G.fixed.p, G.S.p, G.g.p, G.g_dir.p, G.Ddiag.p,
-             G.band_kernel && !direct ? G.Sband.p : nullptr, G.band_kernel, G.n_sky, nf,
+             G.band_kernel && !direct ? G.Sband.p : nullptr, G.band_kernel, G.n_sky, nfs,
              direct ? L0.D : nullptr, L0.U, L0.b, G.band_kernel, G.status.p};
   if (G.sband_dirty && G.band_kernel && !direct) {  // a distributed import filled the whole band: clear the off-profile part
     PBA_HIP(hipMemsetAsync(G.Sband.p, 0, sizeof(double) * (size_t)nf * ((G.band_kernel + 1) * 36 + 6), e->stream));
     G.sband_dirty = false;
   }
-  const int nthreads = G.n_sky * 36 + 6 * nf;
+  const int nthreads = G.n_sky * 36 + 6 * nfs;
   assemble_kernel<<<(nthreads + 255) / 256, 256, 0, e->stream>>>(aa, lambda);
+  if (G.nc_sys) {  // the intrinsics rows of the skyline system (over assemble's zeros there)
+    IntrBorderArgs ba{G.ib_data.p, G.ib_rec.p, G.ib_cam.p, G.pt_rec.p, G.pt_data.p, G.ib_bptr.p, G.ib_blist.p,
+                      G.ib_pptr.p, G.ib_plist.p, G.sky_first.p, G.sky_row.p, G.fixed.p, lm ? lm : G.lm_idle.p, G.S.p,
+                      G.g.p, G.g_dir.p, G.Ddiag.p, nf, G.nc_sys};
+    intr_border_kernel<<<dim3((nfs * 36 + 6 + 255) / 256, 2 * G.nc_sys), 256, 0, e->stream>>>(ba, lambda);
+  }
   if (G.band_kernel) {
     if (int rc = band_solve(e, !direct)) return rc;
   } else {
     PBA_HIP(hipMemcpyAsync(G.L.p, G.S.p, sizeof(double) * 36 * (size_t)G.n_sky, hipMemcpyDeviceToDevice, e->stream));
-    SolveArgs so{G.L.p, G.sky_first.p, G.sky_row.p, G.sky_last.p, G.g.p, G.Linv.p, G.x.p, G.status.p, nf};
+    SolveArgs so{G.L.p, G.sky_first.p, G.sky_row.p, G.sky_last.p, G.g.p, G.Linv.p, G.x.p, G.status.p, nfs};
     skyline_solve_kernel<<<1, 256, 0, e->stream>>>(so);
   }
   PBA_HIP(hipGetLastError());
@@ -3417,6 +3755,9 @@ void launch_accept(pba_engine* e, const double* lm) {
   const int na = std::max(npd, G.n_gn_points);
   lm_accept_kernel<<<std::min(1024, (na + 255) / 256), 256, 0, e->stream>>>(lm, G.poses_new.p, G.rho_new.p, G.pt_orig.p,
                                                                              e->poses.p, e->rho.p, npd, G.n_gn_points);
+  if (G.nc_sys)
+    intr_accept_kernel<<<1, 256, 0, e->stream>>>(lm, G.intr_new_d.p, G.intr_new_f.p, e->intr_state_d.p, e->intr_state.p,
+                                                 G.nc_sys);
   e->pairs_fresh = false;
 }
 
@@ -3467,7 +3808,7 @@ int lm_trial(pba_engine* e, const DecideOpts& dopt, double seq, const hipEvent_t
   int gp = 0, gq = 0;
   enqueue_updates(e, 0.0, G.fixed.p, &gp, &gq, G.lm.p);
   if (ev) PBA_HIP(hipEventRecord(ev[1], e->stream));
-  if (int rc = linearize(e, nullptr, G.lm.p, G.pairs_new.p, G.rho_new.p, G.red.p + 2 * (gp + gq))) return rc;
+  if (int rc = linearize(e, nullptr, G.lm.p, G.pairs_new.p, G.rho_new.p, G.red.p + 2 * (gp + gq), nullptr, true)) return rc;
   if (ev) PBA_HIP(hipEventRecord(ev[2], e->stream));
   lm_decide_kernel<<<1, kDecideThreads, 0, e->stream>>>(G.red.p, G.red2.p, G.gmax.p, gp, gq, G.n_chunks, G.status.p,
                                                         dopt, G.lm.p, G.lm_host_d, seq);
@@ -3485,7 +3826,9 @@ int candidate_cost(pba_engine* e, double* cost) {
     return total_cost(e, cost, nullptr);
   }
   if (!G.pairs_new_fresh) launch_pairs(e, G.poses_new.p, G.pairs_new.p);
-  if (int rc = launch_cost_only(e, G.pairs_new.p, G.rho_new.p)) return rc;
+  if (int rc = launch_cost_only(e, G.pairs_new.p, G.rho_new.p, nullptr, nullptr, nullptr,
+                                G.nc_sys ? G.intr_new_f.p : nullptr, G.nc_sys ? G.intr_new_d.p : nullptr))
+    return rc;
   return total_cost(e, cost, nullptr);
 }
 
@@ -3497,6 +3840,7 @@ int accept(pba_engine* e) {
 
 // ---- multi-GPU step (include/pba.h) ------------------------------------------------------------
 int exchange_K(pba_engine* e, int band, int* K) {
+  if (e->gn.nc_sys) return fail(PBA_ERR_INVALID_ARGUMENT, "free intrinsics: the single-GPU solve (pba_solve) only");
   *K = band_kernel_for(std::max(band, e->gn.band));
   if (band < e->gn.band) return fail(PBA_ERR_INVALID_ARGUMENT, "band below this rank's reduced-system bandwidth");
   if (*K == 0) return fail(PBA_ERR_INVALID_ARGUMENT, "distributed solve needs a reduced-system bandwidth <= 16");
@@ -3606,7 +3950,7 @@ int pba_get_state(pba_engine* e, double* poses, double* inv_dist) {
 int pba_gn_get_reduced_system(pba_engine* e, double* S_dense, double* g) {
   if (int rc = ensure_prepared(e)) return rc;
   GnData& G = e->gn;
-  const int nf = e->n_frames;
+  const int nf = G.nc_sys ? G.nfs : e->n_frames;  // system frames (pba_gn_system_size)
   std::vector<int> first(nf), row(nf + 1);
   PBA_HIP(hipMemcpy(first.data(), G.sky_first.p, sizeof(int) * nf, hipMemcpyDeviceToHost));
   PBA_HIP(hipMemcpy(row.data(), G.sky_row.p, sizeof(int) * (nf + 1), hipMemcpyDeviceToHost));
@@ -3634,6 +3978,13 @@ int pba_gn_get_step(pba_engine* e, double* dposes, double* drho) {
   GnData& G = e->gn;
   if (dposes) PBA_HIP(hipMemcpy(dposes, G.x.p, sizeof(double) * 6 * e->n_frames, hipMemcpyDeviceToHost));
   if (drho) PBA_HIP(hipMemcpy(drho, G.drho.p, sizeof(double) * e->n_points, hipMemcpyDeviceToHost));
+  return PBA_OK;
+}
+
+int pba_gn_system_size(pba_engine* e, int32_t* n) {
+  if (int rc = ensure_prepared(e)) return rc;
+  if (!n) return fail(PBA_ERR_INVALID_ARGUMENT, "null size");
+  *n = 6 * (e->gn.nc_sys ? e->gn.nfs : e->n_frames);
   return PBA_OK;
 }
 

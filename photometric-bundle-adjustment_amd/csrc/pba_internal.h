@@ -587,13 +587,15 @@ __device__ __forceinline__ Row geometric_row(const KernelArgs& a, int blk, int k
   const Vec3d Rp = mat_mul(pp.R, ph);
   const Vec3d p = {Rp.x + pp.t[0], Rp.y + pp.t[1], Rp.z + pp.t[2]};
   double u, v;
-  const double iden = project<MODEL>(a.intr_d + kCamD * pp.target_cam, p, u, v);
+  // the target camera projects with the intrinsics state (intr_t: the cameras, or the free intrinsics of
+  // pba_set_optimize_intrinsics / a candidate's), the host unprojects with the cameras (reprojection.h:93-98)
+  const double iden = project<MODEL>(a.intr_t_d + kCamD * pp.target_cam, p, u, v);
   o.r = (float)(k == 0 ? uo.x - u : uo.y - v);
   o.ok = isfinite(o.r);
   if (JAC) {
     const Vec3 pf = to_f(p), phf = to_f(ph);
     Vec3 du, dv;
-    project_jac<MODEL>(a.intr + 8 * pp.target_cam, pf, (float)iden, du, dv);
+    project_jac<MODEL>(a.intr_t + 8 * pp.target_cam, pf, (float)iden, du, dv);
     const Vec3 d = k == 0 ? du : dv;
     const Vec3 g = {-d.x, -d.y, -d.z};  // ∂r/∂p = −∂π/∂p
     const Vec3 gR = row_mul(g, pp.R);
@@ -744,6 +746,17 @@ struct GnData {
   DevBuf<double> lm;         // LM decision record of the single-GPU loop (pba_gn.hip: kLm*)
   DevBuf<double> lm_idle;    // the record host-driven steps pass to the kernels (not done, set 0, λ from the argument)
   PinnedBuf<double> lm_h;    // its host copy (+ sequence number), host-coherent, written by lm_decide_kernel
+  // Intrinsics in the reduced camera system (pba_set_optimize_intrinsics, geometric engines; pba_gn.hip "intrinsics"):
+  // camera c's 8 intrinsics are the system frames nf + 2c (dims 0-5) and nf + 2c + 1 (dims 6-7, four identity pads), a
+  // dense border of the skyline system.  nc_sys = 0 without intrinsics; nfs = nf + 2·nc_sys system frames.
+  int nc_sys = 0, nfs = 0;
+  DevBuf<int4> ib_rec;          // GN block → {block, point, host, target}
+  DevBuf<double> ib_data;       // GN block → weighted fp64 rows [J_i (2×8) | J_h (2×6) | J_t (2×6) | J_ρ (2) | r (2) | W_i (8)]
+  DevBuf<int> ib_bptr, ib_blist;  // border unit pair (camera c, unit u) → GN blocks of its direct terms (CSR)
+  DevBuf<int> ib_pptr, ib_plist;  // … → GN points of its Schur terms (CSR); unit u < nf: frame u, else camera u − nf
+  DevBuf<int> ib_cam;           // GN block → its target's camera
+  DevBuf<double> intr_new_d;    // candidate intrinsics: camera records (kCamD doubles, projection part) …
+  DevBuf<float> intr_new_f;     // … and their fp32 copy (8 per camera)
   double* lm_host_d = nullptr;  // lm_h's device address
   bool phase_timing = false;    // pba_set_solver_timing: stream events around the LM phases
   int red_slots = 0;
@@ -836,8 +849,10 @@ void launch_pairs(pba_engine* e, const double* poses, PairRec* pairs);
 // Residual-only evaluation writing only per-block costs/validity (state given by pairs/rho).
 // wg_red (optional): each workgroup also writes its (Σ cost, Σ valid) there; *n_slots = the launch's workgroups.
 // poses (optional): evaluate at these state poses with the fused-state prologue instead of the pair table.
+// intr_t / intr_t_d (optional): the target projection's intrinsics (a candidate's free intrinsics).
 int launch_cost_only(pba_engine* e, const PairRec* pairs, const double* rho, double* wg_red = nullptr,
-                     int* n_slots = nullptr, const double* poses = nullptr);
+                     int* n_slots = nullptr, const double* poses = nullptr, const float* intr_t = nullptr,
+                     const double* intr_t_d = nullptr);
 
 // Collectives of the multi-GPU loop (pba_comm.hip): Σ over the ranks in place, enqueued on stream.
 int comm_allreduce(pba_comm* c, double* buf, long long count, hipStream_t stream);

@@ -175,6 +175,8 @@ def lib():
         "pba_comm_allreduce": ([vp, vp, C.c_int64, vp], C.c_int),
         "pba_set_optimize_intrinsics": ([vp, i32], C.c_int),
         "pba_set_intrinsics_state": ([vp, vp], C.c_int),
+        "pba_get_intrinsics": ([vp, vp], C.c_int),
+        "pba_gn_system_size": ([vp, C.POINTER(i32)], C.c_int),
         "pba_compute_projections": ([vp, i32, vp, vp, vp, vp, C.POINTER(OutlierThresholds), vp, vp, vp, vp], C.c_int),
         "pba_outlier_landmarks": ([i32, i32, vp, vp, vp, vp, vp, vp], C.c_int),
         "pba_set_record_format": ([vp, i32], C.c_int),
@@ -226,7 +228,7 @@ class Engine:
         opt = Options(device, kind, model, huber_width)
         _check(L.pba_create(C.byref(opt), C.byref(self._h)), "pba_create")
         self.kind, self.model = kind, model
-        self.n_blocks = self.n_points = self.n_frames = 0
+        self.n_blocks = self.n_points = self.n_frames = self._n_cams = 0
         self._keep = []
 
     # -- problem -------------------------------------------------------------------------------
@@ -234,6 +236,7 @@ class Engine:
         L, h = self._L, self._h
         intr = np.ascontiguousarray(pb.intrinsics, np.float64)
         _check(L.pba_set_cameras(h, intr.shape[0], _p(intr)), "pba_set_cameras")
+        self._n_cams = intr.shape[0]
         fc = np.ascontiguousarray(pb.frame_cam, np.int32)
         if images_device_ptr is not None:
             _check(L.pba_set_frames_device(h, fc.shape[0], _p(fc), pb.width, pb.height, C.c_void_p(images_device_ptr)),
@@ -483,8 +486,21 @@ class Engine:
         _check(self._L.pba_get_state(self._h, _p(poses), _p(rho)), "pba_get_state")
         return poses, rho
 
+    def get_intrinsics(self) -> np.ndarray:
+        """the intrinsics state (n_cams × 8): the free intrinsics with set_optimize_intrinsics, else the cameras'"""
+        k = np.empty((self._n_cams, 8), np.float64)
+        _check(self._L.pba_get_intrinsics(self._h, _p(k)), "pba_get_intrinsics")
+        return k
+
+    def gn_system_size(self) -> int:
+        n = C.c_int32()
+        _check(self._L.pba_gn_system_size(self._h, C.byref(n)), "pba_gn_system_size")
+        return n.value
+
     def gn_reduced_system(self):
-        n = 6 * self.n_frames
+        """(S, g) of the reduced camera system over pba_gn_system_size unknowns: 6 per keyframe, then — free intrinsics —
+        12 per camera (its 8 intrinsics and 4 identity pads)."""
+        n = self.gn_system_size()
         S = np.empty((n, n), np.float64)
         g = np.empty(n, np.float64)
         _check(self._L.pba_gn_get_reduced_system(self._h, _p(S), _p(g)), "pba_gn_get_reduced_system")

@@ -318,3 +318,84 @@ def reduced_system_sparse(pb, poses, rho, a, lam, fixed=(), n_threads=16):
     gp[fxe] = 0.0
     cost = float(np.where(valid == 1, cost_b, 0.0).sum())
     return S, gp, cost
+
+
+def linearize_intrinsics(pb, poses, rho, intr, a, fixed=()):
+    """Geometric blocks with the TARGET camera's intrinsics free (optimize_intrinsics, map_utils.h:339-345; the functor's
+    sIntr_c2 block, reprojection.h:83-86): H (N×N), g, cost with N = 6·n_frames + 8·n_cams + n_points (unknowns in that
+    order), from the oracle's 44-value records (orc_evaluate_intrinsics: projection with `intr`, host unprojection with
+    pb.intrinsics); fixed frames' columns zeroed."""
+    rec, valid = O.evaluate_intrinsics(pb, intr, poses=poses, rho=rho)
+    r, Jh, Jt, Jr = O.split_record(rec[:, :28], 2)
+    Ji = rec[:, 28:44].reshape(-1, 2, 8)
+    s = (r ** 2).sum(1)
+    cost_b, w = huber(s, a)
+    w = np.where(valid == 1, w, 0.0)
+    cost = float(np.where(valid == 1, cost_b, 0.0).sum())
+    nf, nc, npt = pb.n_frames, pb.intrinsics.shape[0], pb.n_points
+    K0 = 6 * nf
+    N = K0 + 8 * nc + npt
+    fixed = set(int(f) for f in fixed)
+    H = np.zeros((N, N))
+    g = np.zeros(N)
+    for b in range(pb.n_blocks):
+        if w[b] == 0:
+            continue
+        p = pb.block_point[b]
+        h, t = pb.point_host[p], pb.block_target[b]
+        c = pb.frame_cam[t]
+        J = np.zeros((2, N))
+        if h not in fixed:
+            J[:, 6 * h:6 * h + 6] = Jh[b]
+        if t not in fixed:
+            J[:, 6 * t:6 * t + 6] = Jt[b]
+        J[:, K0 + 8 * c:K0 + 8 * c + 8] = Ji[b]
+        J[:, K0 + 8 * nc + p] = Jr[b]
+        H += w[b] * J.T @ J
+        g += w[b] * J.T @ r[b]
+    return H, g, cost
+
+
+def schur_step_intrinsics(H, g, nf, nc, lam, fixed=()):
+    """schur_step over the f-blocks (poses, then the cameras' intrinsics): (S, gS, δ_f, δ_points, model_decrease) of
+    (H + λD)δ = −g with the points eliminated; constant frames and never-observed frames / cameras get identity rows."""
+    P = 6 * nf + 8 * nc
+    D = np.clip(np.diag(H), 1e-6, 1e32)
+    fx = np.zeros(P, bool)
+    for f in fixed:
+        fx[6 * f:6 * f + 6] = True
+    for i in range(nf):
+        if not np.any(H[6 * i:6 * i + 6, :]):
+            fx[6 * i:6 * i + 6] = True
+    for c in range(nc):
+        sl = slice(6 * nf + 8 * c, 6 * nf + 8 * c + 8)
+        if not np.any(H[sl, :]):
+            fx[sl] = True
+    Ha = H + lam * np.diag(D)
+    A, B, C = Ha[:P, :P].copy(), Ha[:P, P:].copy(), np.diag(Ha[P:, P:]).copy()
+    gp, gl = g[:P].copy(), g[P:].copy()
+    A[fx, :] = 0
+    A[:, fx] = 0
+    A[fx, fx] = 1.0
+    B[fx, :] = 0
+    gp[fx] = 0
+    Ci = np.where(C > 0, 1.0 / np.where(C > 0, C, 1.0), 0.0)
+    S = A - (B * Ci) @ B.T
+    gS = gp - B @ (Ci * gl)
+    S[fx, :] = 0
+    S[:, fx] = 0
+    S[fx, fx] = 1.0
+    gS[fx] = 0
+    df = np.linalg.solve(S, -gS)
+    dl = -(gl + B.T @ df) * Ci
+    delta = np.concatenate([df, dl])
+    Dm = D.copy()
+    Dm[:P][fx] = 0
+    model = 0.5 * (lam * float(delta @ (Dm * delta)) - float(np.concatenate([gp, gl]) @ delta))
+    return S, gS, df, dl, model
+
+
+def intrinsics_system_index(nf, nc):
+    """Indices of the 6·nf + 8·nc f-block unknowns in the engine's reduced camera system (pba_gn_system_size: 6 per
+    keyframe, then 12 per camera of which the first 8 are its intrinsics)."""
+    return np.concatenate([np.arange(6 * nf)] + [6 * nf + 12 * c + np.arange(8) for c in range(nc)])

@@ -121,6 +121,32 @@ def test_c1_ceres_dropin_optimize_intrinsics(c1):
 
 
 @needs_ceres
+def test_c1_engine_lm_optimize_intrinsics_matches_ceres_cpu(c1):
+    """The engine's own LM (pba_solve, on-device Schur GN) with free intrinsics (optimize_intrinsics, map_utils.h:339-345:
+    the cameras' intrinsics blocks free, the functor's target-camera Jacobian, reprojection.h:83-86, :108) against real
+    Ceres 2.0.0 on the CPU (AutoDiff, SPARSE_SCHUR with the intrinsics among the f-blocks): the same successful /
+    unsuccessful step counts, the final cost to 1e-5, the intrinsics to 2e-6 relative (1e-6 absolute for the distortion
+    parameter near 0), as test_c1_ceres_dropin_optimize_intrinsics holds the drop-in."""
+    pb = synth.Problem(**{**c1.__dict__, "intrinsics": c1.intrinsics * np.array([1.002, 0.998, 1.0, 1.0, 1, 1, 1, 1])})
+    ref = CR.run("cpu", pb, iters=20, huber=1.0, threads=THREADS, optimize_intrinsics=1)
+    with make_engine(pb, 1.0) as eng:
+        eng.set_optimize_intrinsics(True)
+        s = eng.solve(max_iterations=20)
+        k = eng.get_intrinsics()
+        poses, _ = eng.get_state()
+    print(f"\nC1 free intrinsics: engine {s['successful_steps']}/{s['unsuccessful_steps']} final {s['final_cost']:.10g}; "
+          f"Ceres {ref['successful_steps'] - 1}/{ref['unsuccessful_steps']} final {ref['final_cost']:.10g} "
+          f"({ref['message']}); intrinsics max rel {np.abs(k - ref['intrinsics']).max() / np.abs(ref['intrinsics']).max():.2e}")
+    assert np.abs(ref["intrinsics"] - pb.intrinsics).max() > 1e-3  # Ceres moved them
+    assert s["successful_steps"] == ref["successful_steps"] - 1, (s, ref["message"])
+    assert s["unsuccessful_steps"] == ref["unsuccessful_steps"], (s, ref["message"])
+    assert abs(s["initial_cost"] - ref["costs"][0]) <= 1e-6 * ref["costs"][0]
+    assert abs(s["final_cost"] - ref["final_cost"]) <= 1e-5 * ref["final_cost"], (s["final_cost"], ref["final_cost"])
+    np.testing.assert_allclose(k, ref["intrinsics"], rtol=2e-6, atol=1e-6)
+    np.testing.assert_allclose(poses[:, 4:], ref["poses"][:, 4:], atol=1e-4)
+
+
+@needs_ceres
 def test_c1_free_intrinsics_without_engine_support_is_refused(c1):
     """Free intrinsics blocks with an evaluator that was not given them: the adapter refuses the Jacobian request
     (Evaluate returns false) and Ceres ends with FAILURE, instead of optimising with a zero intrinsics gradient."""

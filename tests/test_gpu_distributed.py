@@ -325,7 +325,19 @@ def test_band_too_small_is_rejected():
         with pytest.raises(E.PbaError, match="band"):
             e.gn_exchange_size(b - 1)
         n = e.gn_exchange_size(b)
-        assert n == 12 * ((E_band(b) + 1) * 36 + 24) + 8  # banded rows + the 8 point-part scalars of a trial
+        # banded rows + the 16 scalars of a trial (point part from every rank, pose part + solve status from rank 0)
+        assert n == 12 * ((E_band(b) + 1) * 36 + 24) + 16
+
+
+def test_free_intrinsics_are_single_gpu():
+    """Free intrinsics put a dense border into the reduced camera system (skyline solve): the banded multi-GPU exchange
+    refuses such an engine instead of dropping the intrinsics."""
+    pb = synth.make_problem(kind="geometric", n_frames=12, n_points=60, seed=5)
+    with engine_for(pb, 1.0, (0,)) as e:
+        e.set_optimize_intrinsics(True)
+        e.gn_linearize()
+        with pytest.raises(E.PbaError, match="intrinsics"):
+            e.gn_exchange_size(e.gn_band())
 
 
 def E_band(b):

@@ -464,3 +464,52 @@ def test_set_frames_after_gn_reanalyses_the_problem():
     for a, b, o in zip(d1, d2, d0):
         assert np.allclose(a, b, rtol=1e-9, atol=1e-12 * np.abs(b).max())
         assert np.abs(o - b).max() > 1e-3 * np.abs(b).max()
+
+
+@pytest.mark.parametrize("model", [0, 1, 3])
+@pytest.mark.parametrize("lam", [1e-4, 1e-1])
+def test_free_intrinsics_reduced_system_and_step(model, lam):
+    """Free intrinsics (pba_set_optimize_intrinsics; optimize_intrinsics, map_utils.h:339-345) in the on-device Schur GN:
+    two cameras (a stereo rig) whose intrinsics state differs from the cameras the hosts unproject with
+    (reprojection.h:93-98).  The device's reduced camera system over the keyframes AND the 8 intrinsics of each camera
+    (the dense border of the skyline system) and its right-hand side against the dense fp64 reference built from the
+    oracle's 44-value records (gn_reference.linearize_intrinsics / schur_step_intrinsics), the pose and inverse-distance
+    step, the candidate intrinsics k + δk and the LM model decrease."""
+    pb0 = synth.make_problem(kind=1, model=model, n_frames=10, n_points=120, width=376, height=240, seed=13, border=12)
+    k1 = pb0.intrinsics[0].copy()
+    k1[:4] *= np.array([1.01, 0.99, 1.0, 1.0])
+    intr = np.stack([pb0.intrinsics[0], k1])
+    pb = synth.make_problem(kind=1, model=model, n_frames=10, n_points=120, width=376, height=240, seed=13, border=12,
+                            intrinsics=intr, frame_cam=np.arange(10, dtype=np.int32) % 2)
+    state = intr * np.array([1.003, 0.998, 1.0005, 0.9995, 1, 1, 1, 1])
+    fixed = (0, 1)
+    nf, nc = pb.n_frames, 2
+    H, g, c_ref = GR.linearize_intrinsics(pb, pb.poses, pb.rho, state, 1.0, fixed)
+    S_ref, gS_ref, df_ref, dl_ref, m_ref = GR.schur_step_intrinsics(H, g, nf, nc, lam, fixed)
+    with make_engine(pb, 1.0, fixed) as eng:
+        eng.set_optimize_intrinsics(True)
+        eng.set_intrinsics_state(state)
+        c = eng.gn_linearize()
+        m, st = eng.gn_step(lam)
+        assert st == 0
+        assert eng.gn_system_size() == 6 * nf + 12 * nc
+        S, gs = eng.gn_reduced_system()
+        dp, dr = eng.gn_last_step()
+        eng.gn_accept()
+        k_new = eng.get_intrinsics()
+    idx = GR.intrinsics_system_index(nf, nc)
+    Ss, gss = S[np.ix_(idx, idx)], gs[idx]
+    eS = np.abs(Ss - S_ref).max() / np.abs(S_ref).max()
+    eg = np.abs(gss - gS_ref).max() / np.abs(gS_ref).max()
+    dk = (k_new - state).ravel()
+    ep = np.linalg.norm(np.concatenate([dp.ravel(), dk]) - df_ref) / np.linalg.norm(df_ref)
+    el = np.linalg.norm(dr - dl_ref) / np.linalg.norm(dl_ref)
+    print(f"\nintrinsics model {model} λ={lam}: cost {abs(c - c_ref) / c_ref:.2e} S {eS:.2e} g {eg:.2e} "
+          f"step {ep:.2e} δρ {el:.2e} model {abs(m - m_ref) / abs(m_ref):.2e}")
+    # the pads: identity rows, zero gradient
+    pad = np.concatenate([6 * nf + 12 * c + np.arange(8, 12) for c in range(nc)])
+    assert np.allclose(S[np.ix_(pad, pad)], np.eye(len(pad)) * (1 + lam)) and not gs[pad].any()
+    assert abs(c - c_ref) <= 1e-6 * c_ref
+    assert eS <= 1e-5 and eg <= 1e-5, (eS, eg)
+    assert ep <= 1e-3 and el <= 1e-3, (ep, el)
+    assert abs(m - m_ref) <= 1e-3 * abs(m_ref)

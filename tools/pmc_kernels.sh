@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round-3 counter passes (diagnostic): the C5 21-px kernel (camera-table form), the GN linearisation and, for
+# Counter passes (diagnostic): the C5 21-px kernel (camera-table form), the GN linearisation and, for
 # comparison, the headline block kernel; one rocprofv3 --pmc pass per counter group (tools/pmc_probe.sh).
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
