@@ -8,11 +8,12 @@ block's residuals and tangent Jacobians (Ceres-mode records, include/pba.h) at a
 ONE launch (pba_evaluate_state_device — the blocks form their relative poses in the prologue and the launch adopts
 the state).
 
-Multi-GPU (torch.distributed.run, one rank per GPU): the one problem's residual blocks are sharded by host keyframe
-(distributed.shard_problem: contiguous host ranges balanced by block count); every rank evaluates its shard with no
-data-path collective (the evaluation has no exchange step) → `scaling: "strong"`, value = 400k blocks
-÷ the max-over-ranks time.  The weak-scaling figure (every rank its own full 1000-keyframe problem) is reported under
-"weak" when N > 1.  Timing: a clock warm-up, W warmup steps, then exactly K steps bracketed by barrier + synchronize.
+Multi-GPU (torch.distributed.run, one rank per GPU): the evaluation partitions by host keyframe with no exchange step
+(SURVEY.md §8e), so the headline scales weakly — rank r evaluates host keyframes [r·1000, (r+1)·1000) of one
+N·1000-keyframe trajectory, a full C4-size shard (400k blocks) per GPU, with no data-path collective → `scaling: "weak"`,
+value = N × 400k blocks ÷ the max-over-ranks time.  The one C4 problem itself split N ways (strong scaling) is reported
+under "strong", and at N = 1 the step of a 1/8 shard under "shard8" (the strong-scaling ceiling at N = 8).  Timing: a
+clock warm-up, W warmup steps, then exactly K steps bracketed by barrier + synchronize.
 
 Also reported: the block kernel's roofline position (algorithmic bytes ÷ HIP-event-timed kernel duration on the engine
 stream); the CPU baseline — the reference's CPU path, real Ceres 2.0.0 (built from the reference's vendored sources
@@ -371,7 +372,8 @@ def traffic_probe(args):
     import torch
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(0)
-    pb, images = synth.c4_shard(dev, n_frames=args.frames, n_points=args.points, K=args.targets)
+    pb, images = synth.c4_shard(dev, n_frames=args.frames, n_points=args.points, K=args.targets,
+                                block_order=args.block_order)
     eng = engine_mod.Engine(synth.PHOTOMETRIC, synth.PINHOLE, device=0, huber_width=9.0)
     eng.set_problem(pb, images_device_ptr=images.data_ptr())
     states = make_states(pb, torch, dev, 7)
@@ -445,11 +447,12 @@ def main():
     ap.add_argument("--gn-iterations", type=int, default=10)
     ap.add_argument("--no-c3", action="store_true", help="skip the C3 Gauss-Newton measurement (configs[2])")
     ap.add_argument("--no-c5", action="store_true", help="skip the C5-style 21-px / fp16 / pyramid measurement")
-    ap.add_argument("--no-weak", action="store_true", help="N > 1: skip the weak-scaling leg")
+    ap.add_argument("--no-shard-leg", action="store_true", help="N = 1: skip the 1/8-shard step leg")
     ap.add_argument("--no-c2", action="store_true", help="skip the C2 Ceres drop-in measurement (configs[1])")
     ap.add_argument("--no-live-traffic", action="store_true",
                     help="take roofline.traffic from the committed profiles/ file instead of two rocprofv3 --pmc passes")
     ap.add_argument("--traffic-probe", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--block-order", default="point", help=argparse.SUPPRESS)  # traffic probe: "point" | "morton"
     args = ap.parse_args()
     if args.traffic_probe:
         traffic_probe(args)
@@ -476,45 +479,70 @@ def main():
             dist.init_process_group(backend)
         dd = dist
 
-    # ---- the one C4 problem, sharded by host keyframe (strong scaling) ----------------------------------------
+    # ---- the headline: the C4 problem on one GPU; N > 1 — weak scaling, every rank a full C4-size shard -------------
+    # (the evaluation partitions by host keyframe with no exchange step, SURVEY.md §8e: rank r holds host keyframes
+    # [r·F, (r+1)·F) of one N·F-keyframe trajectory with their 100k points and 400k blocks; per-GPU work fixed)
     K, F, Np = args.targets, args.frames, args.points
-    full, images = synth.c4_shard(dev, n_frames=F, n_points=Np, K=K)  # identical on every rank (same seeds)
     if world > 1:
-        pb, _, _ = D.shard_problem(full, world, rank)
+        pb, images_w = synth.c4_shard(dev, rank=rank, world=world, n_frames=F, n_points=Np, K=K)
     else:
-        pb = full
+        pb, images_w = synth.c4_shard(dev, n_frames=F, n_points=Np, K=K)
     eng = engine_mod.Engine(synth.PHOTOMETRIC, synth.PINHOLE, device=dev_index, huber_width=9.0)
-    eng.set_problem(pb, images_device_ptr=images.data_ptr())
-    states = make_states(pb, torch, dev, 7)
+    eng.set_problem(pb, images_device_ptr=images_w.data_ptr())
+    states = make_states(pb, torch, dev, 7 + rank)
     eng.set_state_device(states[0][0].data_ptr(), states[0][1].data_ptr())
     eng.evaluate(True)
     _, valid = eng.records()
     elapsed, kern_us, host_diag = time_evaluation(eng, states, args.steps, args.warmup, args.clock_warmup_s, torch, dd, dev)
     kern_us_local = kern_us
+    eng.close()
+    if world > 1:
+        del images_w
+
+    # ---- the one C4 problem itself (1004 keyframes), sharded by host keyframe: strong scaling (N > 1), the GN leg ----
+    if world > 1:
+        full, images = synth.c4_shard(dev, n_frames=F, n_points=Np, K=K)  # identical on every rank (same seeds)
+    else:
+        full, images = pb, images_w
+    strong = None
+    if world > 1:
+        pbs, _, _ = D.shard_problem(full, world, rank)
+        engs = engine_mod.Engine(synth.PHOTOMETRIC, synth.PINHOLE, device=dev_index, huber_width=9.0)
+        engs.set_problem(pbs, images_device_ptr=images.data_ptr())
+        sts = make_states(pbs, torch, dev, 7)
+        el_s, kern_s, _ = time_evaluation(engs, sts, args.steps, args.warmup, args.clock_warmup_s, torch, dd, dev)
+        engs.close()
+        strong = {"value": full.n_blocks * args.steps / el_s, "unit": "blocks/s", "ms_per_step": 1e3 * el_s / args.steps,
+                  "blocks_total": full.n_blocks, "blocks_rank0": pbs.n_blocks, "kernel_avg_us": kern_s,
+                  "note": f"the one C4 problem ({full.n_frames} keyframes, {full.n_blocks} blocks) split by host keyframe "
+                          f"over {world} GPUs (distributed.shard_problem), no data-path collective"}
+    else:
+        pbs = full
+    shard8 = None
+    if world == 1 and not args.no_shard_leg:  # one rank's step of the C4 problem split 8 ways, on this GPU
+        p8, _, _ = D.shard_problem(full, 8, 0)
+        e8 = engine_mod.Engine(synth.PHOTOMETRIC, synth.PINHOLE, device=dev_index, huber_width=9.0)
+        e8.set_problem(p8, images_device_ptr=images.data_ptr())
+        st8 = make_states(p8, torch, dev, 7)
+        el8, k8, _ = time_evaluation(e8, st8, args.steps, args.warmup, args.clock_warmup_s, torch, None, dev)
+        e8.close()
+        shard8 = {"blocks": p8.n_blocks, "ms_per_step": 1e3 * el8 / args.steps, "kernel_avg_us": k8,
+                  "strong_scaling_ceiling_n8": (elapsed / args.steps) / (el8 / args.steps),
+                  "note": "a 1/8 host-keyframe shard of the C4 problem (rank 0's share at N = 8) timed on one GPU: the "
+                          "strong-scaling ceiling at N = 8 is the full problem's step over this step"}
 
     gn = None
     if args.gn_iterations > 0:
-        eng.set_state(pb.poses, pb.rho)
+        eng = engine_mod.Engine(synth.PHOTOMETRIC, synth.PINHOLE, device=dev_index, huber_width=9.0)
+        eng.set_problem(pbs, images_device_ptr=images.data_ptr())
+        eng.set_state(pbs.poses, pbs.rho)
         try:
             gn = gn_benchmark(eng, args.gn_iterations, torch, dd, dev, world)
         except Exception as ex:  # a secondary leg: report it, keep the headline line (every rank raises alike)
             if world == 1:
                 raise
             gn = {"error": f"{type(ex).__name__}: {ex}"[:300]}
-    eng.close()
-
-    weak = None
-    if world > 1 and not args.no_weak:  # every rank its own full-size problem (global keyframe indices)
-        pbw, imw = synth.c4_shard(dev, rank=rank, world=world, n_frames=F, n_points=Np, K=K)
-        engw = engine_mod.Engine(synth.PHOTOMETRIC, synth.PINHOLE, device=dev_index, huber_width=9.0)
-        engw.set_problem(pbw, images_device_ptr=imw.data_ptr())
-        stw = make_states(pbw, torch, dev, 7 + rank)
-        el_w, kern_w, _ = time_evaluation(engw, stw, args.steps, args.warmup, args.clock_warmup_s, torch, dd, dev)
-        engw.close()
-        del imw
-        weak = {"value": pbw.n_blocks * world * args.steps / el_w, "unit": "blocks/s", "ms_per_step": 1e3 * el_w / args.steps,
-                "blocks_per_gpu": pbw.n_blocks, "kernel_avg_us": kern_w,
-                "note": "every rank evaluates its own 1000-host-keyframe x 100k-point problem (per-GPU work fixed)"}
+        eng.close()
 
     c3 = None
     if world == 1 and not args.no_c3 and args.gn_iterations > 0:
@@ -524,7 +552,7 @@ def main():
         c5 = c5_eval(full, images, states, args.steps, args.warmup, args.clock_warmup_s, torch, dev_index, dev)
 
     if rank == 0:
-        total_blocks = full.n_blocks
+        total_blocks = pb.n_blocks * world
         ms_per_step = 1e3 * elapsed / args.steps
         value = total_blocks * args.steps / elapsed
         bpb = algorithmic_bytes_per_block(pb.P, K, pb.n_frames, pb.n_points, pb.n_blocks)
@@ -563,16 +591,19 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": ms_per_step,
             "higher_is_better": True,
-            "scaling": "strong",
+            "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic",
             "config": {
-                "workload": f"C4: one synthetic problem of {F} host keyframes x {Np} points x {pb.P}-px patch x {K} "
-                            f"targets = {total_blocks} residual blocks, {full.width}x{full.height} u8 images, pinhole; one "
-                            f"step = full r + tangent-J evaluation (Ceres-mode records) at a new HBM-resident state"
-                            + (f", sharded by host keyframe over {world} GPUs" if world > 1 else ""),
-                "keyframes": F, "keyframes_global": full.n_frames, "points": Np, "patch": pb.P, "targets_per_point": K,
+                "workload": (f"C4: one synthetic problem of {F} host keyframes x {Np} points x {pb.P}-px patch x {K} "
+                             f"targets = {pb.n_blocks} residual blocks, {full.width}x{full.height} u8 images, pinhole"
+                             if world == 1 else
+                             f"C4 per GPU: host keyframes [r*{F}, (r+1)*{F}) of one {world * F + K}-keyframe trajectory "
+                             f"on rank r, each with {Np} points x {pb.P}-px patch x {K} targets = {pb.n_blocks} blocks "
+                             f"({total_blocks} in all), {full.width}x{full.height} u8 images, pinhole") +
+                            "; one step = full r + tangent-J evaluation (Ceres-mode records) at a new HBM-resident state",
+                "keyframes": F, "points": Np, "patch": pb.P, "targets_per_point": K,
                 "blocks_total": total_blocks, "blocks_rank0": pb.n_blocks, "valid_blocks_rank0": int(valid.sum()),
                 "parallelism": f"host-keyframe shards x{world} (evaluation: no data-path collective; "
                                f"GN: RCCL all-reduce of the reduced camera system)",
@@ -594,7 +625,8 @@ def main():
             "gn": gn,
             "gn_c3": c3,
             "c5": c5,
-            "weak": weak,
+            "strong": strong,
+            "shard8": shard8,
             "host": {k: round(v, 2) for k, v in host_diag.items()},
         }
         print(json.dumps(out), flush=True)

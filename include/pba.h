@@ -298,6 +298,10 @@ int pba_gn_step_import(pba_engine* engine, double lambda, int32_t band, const do
  * whose sums are enqueued on the engine's stream (the host then enqueues trial i + 1 before trial i's decision is
  * known, as pba_solve does). */
 typedef int (*pba_allreduce_fn)(void* user, double* d_buf, int64_t count);
+/* This engine's rank in the host-callback collective of pba_solve_distributed (a pba_comm knows its own): rank 0 then
+ * contributes the pose part and the solve status to the scalar sum as with a pba_comm; −1 (the default) leaves every
+ * rank deciding from its own, bit-identical, copy. */
+int pba_gn_set_rank(pba_engine* engine, int32_t rank);
 int pba_solve_distributed(pba_engine* engine, const pba_solver_options* options, int32_t band, double* d_exchange,
                           pba_allreduce_fn allreduce, void* user, pba_solver_summary* summary);
 /* Communicators.  RCCL (one process per GPU, over xGMI): rank 0 gets a 128-byte id from pba_comm_unique_id and shares

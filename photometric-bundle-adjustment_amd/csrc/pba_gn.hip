@@ -672,6 +672,43 @@ __global__ void export_kernel(AsmArgs a, const uint8_t* __restrict__ observed, d
   if (r == 0) tail[18] = observed[i] ? 1.0 : 0.0;
 }
 
+// The same over every element of the exchange buffer: positions outside the local profile get their zero here, so the
+// buffer needs no fill launch before it (round 3: a 5-µs hipMemsetAsync of the whole band per trial).
+__global__ void export_band_kernel(AsmArgs a, const uint8_t* __restrict__ observed, const int* __restrict__ sky_first,
+                                   const int* __restrict__ sky_row, double* __restrict__ X, int K) {
+  if (lm_view(a.lm).set != 0.0) a.part_lin = a.part_lin1;  // (no done gate: see schur_kernel)
+  // lanes [0, nf·(K+1)·36): the band elements; then 24 per frame for the tails, in waves of their own (the gradient lists
+  // are long: interleaved with the band's short lists they made every wave wait for them, 12 → 21 µs at C4)
+  const long long RS = ex_row(K), t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const int QB = (K + 1) * 36;
+  const long long nB = (long long)a.n_frames * QB;
+  if (t < nB) {
+    const int i = (int)(t / QB), q = (int)(t - (long long)i * QB);
+    const int c = q / 36, e = q % 36, r = e / 6, cc = e % 6, j = i - K + c;
+    double sum = 0.0, dsum = 0.0;
+    if (j >= 0 && j >= sky_first[i]) {
+      const int s = sky_row[i] + (j - sky_first[i]);
+      contrib_sums(a, a.sky_contrib, a.sky_cptr[s], a.sky_cptr[s + 1], r * 6 + cc, cc * 6 + r, sum, dsum);
+    }
+    double* row = X + (long long)i * RS;
+    row[q] = sum;
+    if (i == j && r == cc) row[QB + 12 + r] = dsum;  // diag(A)
+    return;
+  }
+  const long long u = t - nB;
+  if (u >= (long long)a.n_frames * EX_TAIL) return;
+  const int i = (int)(u / EX_TAIL), r = (int)(u % EX_TAIL);
+  double* tail = X + (long long)i * RS + QB;
+  if (r < 6) {  // g and the direct gradient from one list walk
+    double sum, dsum;
+    contrib_sums(a, a.g_contrib, a.g_cptr[i], a.g_cptr[i + 1], r, r, sum, dsum);
+    tail[r] = sum;
+    tail[6 + r] = dsum;
+  } else if (r >= 18) {
+    tail[r] = r == 18 && observed[i] ? 1.0 : 0.0;
+  }
+}
+
 struct ImportArgs {
   const double* X;         // summed exchange buffer
   const uint8_t* fixed_req;
@@ -682,6 +719,11 @@ struct ImportArgs {
   uint8_t* fixed;          // effective constant frames: requested, or observed by no rank
   int n_frames;
   int K;
+  // block cyclic reduction: level 0 written directly (super-rows of K keyframes; as assemble_kernel), else Sband
+  double* crD;
+  double* crU;
+  double* crb;
+  int* status;
 };
 
 // One lane per element of the band solver input: + λ·clamp(diag(A)) (levenberg_marquardt_strategy.cc),
@@ -708,11 +750,26 @@ __global__ void import_kernel(const ImportArgs a, double lambda, const double* _
         val += lambda * fmin(fmax(tail[12 + r], 1e-6), 1e32);
       }
     }
-    a.Sband[t] = val;
+    if (!a.crD) {
+      a.Sband[t] = val;
+    } else if (j >= 0) {  // the (i, j) entry into level 0 (I = i / K, J = j / K, I − J ≤ 1), as assemble_kernel
+      const int M = 6 * K, I = i / K, J = j / K, Ri = (i % K) * 6 + r, Cj = (j % K) * 6 + cc;
+      if (I == J) {
+        if (i != j || r >= cc) {  // the lower lane writes both positions (a symmetric D, reproducible)
+          double* D = a.crD + (long long)I * M * M;
+          D[Ri * M + Cj] = val;
+          D[Cj * M + Ri] = val;
+        }
+      } else {
+        a.crU[(long long)J * M * M + Cj * M + Ri] = val;
+      }
+    }
     return;
   }
   const int r = q - (K + 1) * 36;
-  a.Sband[t] = fi ? 0.0 : tail[r];
+  if (!a.crD) a.Sband[t] = fi ? 0.0 : tail[r];
+  else a.crb[6 * i + r] = fi ? 0.0 : -tail[r];
+  if (a.crD && t == (K + 1) * 36) *a.status = 0;  // the solve's failure flag (cr_build_kernel clears it otherwise)
   a.g[6 * i + r] = fi ? 0.0 : tail[r];
   a.g_dir[6 * i + r] = fi ? 0.0 : tail[6 + r];
   a.Ddiag[6 * i + r] = fi ? 0.0 : fmin(fmax(tail[12 + r], 1e-6), 1e32);
@@ -3005,6 +3062,7 @@ int configure_solver(pba_engine* e, int K, int solver) {
       P.b = off; off += (size_t)np * M;
     }
     G.cr0_dirty = true;  // level 0 is set up for assemble_kernel's direct writes on first use
+    G.cr0_inited = false;
     // the one-launch PCR (pcr_fused_kernel): a buffer per stride level, ready flags, the task counter
     G.pcr_levels = 0;
     for (int st = 1; st < np; st *= 2) ++G.pcr_levels;
@@ -3516,6 +3574,7 @@ int init_cr_level0(pba_engine* e) {
   PBA_HIP(hipMemcpyAsync(G.cr_buf.p + h.D, z.data(), z.size() * sizeof(double), hipMemcpyHostToDevice, e->stream));
   PBA_HIP(hipStreamSynchronize(e->stream));  // z is pageable and goes out of scope
   G.cr0_dirty = false;
+  G.cr0_inited = true;
   return PBA_OK;
 }
 
@@ -3849,6 +3908,39 @@ int exchange_K(pba_engine* e, int band, int* K) {
 
 long long exchange_count(pba_engine* e, int K) { return (long long)e->n_frames * ex_row(K) + kExScalars; }
 
+// This rank's partial system into the exchange buffer X (every element written: no fill launch).
+int enqueue_export(pba_engine* e, const double* lm, double* X, int K) {
+  GnData& G = e->gn;
+  const int nf = e->n_frames;
+  AsmArgs aa{G.part_lin.p, G.part_lin1.p, lm, G.part_schur.p, G.sky_cptr.p, G.sky_contrib.p, G.g_cptr.p,
+             G.g_contrib.p, G.sky_blk_i.p, G.sky_blk_j.p, G.fixed.p, G.S.p, G.g.p, G.g_dir.p, G.Ddiag.p, nullptr, K,
+             G.n_sky, nf, nullptr, nullptr, nullptr, 0, nullptr};
+  const long long n = (long long)nf * ex_row(K);  // (K+1)·36 band + EX_TAIL tail lanes per frame
+  export_band_kernel<<<(unsigned)((n + 255) / 256), 256, 0, e->stream>>>(aa, G.observed.p, G.sky_first.p, G.sky_row.p,
+                                                                        X, K);
+  PBA_HIP(hipGetLastError());
+  return PBA_OK;
+}
+
+// The summed exchange → damping, constant frames and the band solver's input — for block cyclic reduction its level 0
+// directly (no Sband, no cr_build pass), as assemble_kernel does on one GPU — then the reduced solve into G.x.
+int enqueue_import(pba_engine* e, double lambda, const double* lm, const double* X, int K) {
+  GnData& G = e->gn;
+  const int nf = e->n_frames;
+  const bool direct = G.solver == SOLVER_CR;
+  if (direct && !G.cr0_inited)  // zeros outside the band, identity padding rows
+    if (int rc = init_cr_level0(e)) return rc;
+  CrLevel L0 = direct ? cr_level(G, 0) : CrLevel{};
+  ImportArgs ia{X, G.fixed_req.p, G.Sband.p, G.g.p, G.g_dir.p, G.Ddiag.p, G.fixed_dist.p, nf, K,
+                direct ? L0.D : nullptr, L0.U, L0.b, G.status.p};
+  const long long n = (long long)nf * ((K + 1) * 36 + 6);
+  import_kernel<<<(unsigned)((n + 255) / 256), 256, 0, e->stream>>>(ia, lambda, lm);
+  PBA_HIP(hipGetLastError());
+  G.sband_dirty = !direct;
+  G.cr0_dirty = true;  // level 0 holds the whole band now: a single-GPU assembly re-initialises it first
+  return band_solve(e, !direct);
+}
+
 int step_export(pba_engine* e, double lambda, int band, double* X) {
   GnData& G = e->gn;
   int K;
@@ -3859,14 +3951,8 @@ int step_export(pba_engine* e, double lambda, int band, double* X) {
                nullptr, nullptr, nullptr, nullptr, nullptr, 0, 0};
   schur_lds_limit(G);
   if (G.n_schur > 0) schur_kernel<<<G.n_schur, kBlockThreads, G.schur_lds, e->stream>>>(sa, lambda);
-  PBA_HIP(hipMemsetAsync(X, 0, sizeof(double) * (size_t)nf * ex_row(K), e->stream));
-  AsmArgs aa{G.part_lin.p, G.part_lin1.p, G.lm_idle.p, G.part_schur.p, G.sky_cptr.p, G.sky_contrib.p, G.g_cptr.p,
-             G.g_contrib.p, G.sky_blk_i.p, G.sky_blk_j.p, G.fixed.p, G.S.p, G.g.p, G.g_dir.p, G.Ddiag.p, nullptr, K,
-             G.n_sky, nf, nullptr, nullptr, nullptr, 0, nullptr};
-  const int nthreads = G.n_sky * 36 + 6 * nf;
-  export_kernel<<<(nthreads + 255) / 256, 256, 0, e->stream>>>(aa, G.observed.p, X, K);
-  PBA_HIP(hipGetLastError());
-  return PBA_OK;
+  (void)nf;
+  return enqueue_export(e, G.lm_idle.p, X, K);
 }
 
 int step_import(pba_engine* e, double lambda, int band, const double* X, double* model_pose, double* model_points,
@@ -3879,14 +3965,7 @@ int step_import(pba_engine* e, double lambda, int band, const double* X, double*
     const int solver = (K <= 8 && !(fs && std::string(fs) == "band")) ? SOLVER_CR : SOLVER_BAND;
     if (int rc = configure_solver(e, K, solver)) return rc;
   }
-  const int nf = e->n_frames;
-  ImportArgs ia{X, G.fixed_req.p, G.Sband.p, G.g.p, G.g_dir.p, G.Ddiag.p, G.fixed_dist.p, nf, K};
-  const long long n = (long long)nf * ((K + 1) * 36 + 6);
-  import_kernel<<<(unsigned)((n + 255) / 256), 256, 0, e->stream>>>(ia, lambda, G.lm_idle.p);
-  PBA_HIP(hipGetLastError());
-  G.sband_dirty = true;
-  G.cr0_dirty = true;  // cr_build writes level 0 over the whole band
-  if (int rc = band_solve(e)) return rc;
+  if (int rc = enqueue_import(e, lambda, G.lm_idle.p, X, K)) return rc;
   return finish_step(e, lambda, G.fixed_dist.p, model_pose, model_points, solver_status);
 }
 
@@ -3981,6 +4060,12 @@ int pba_gn_get_step(pba_engine* e, double* dposes, double* drho) {
   return PBA_OK;
 }
 
+int pba_gn_set_rank(pba_engine* e, int32_t rank) {
+  if (!e) return fail(PBA_ERR_INVALID_ARGUMENT, "null engine");
+  e->gn.dist_rank = rank < 0 ? -1 : rank;
+  return PBA_OK;
+}
+
 int pba_gn_system_size(pba_engine* e, int32_t* n) {
   if (int rc = ensure_prepared(e)) return rc;
   if (!n) return fail(PBA_ERR_INVALID_ARGUMENT, "null size");
@@ -4043,8 +4128,11 @@ struct Collective {
     if (int rc = fn(user, buf, n)) return fail(PBA_ERR_DEVICE, "allreduce callback failed (" + std::to_string(rc) + ")");
     return PBA_OK;
   }
-  // dist_sums_kernel's rank flag: 1 rank 0 of a communicator, 0 another rank, −1 a host callback (ranks unknown)
-  int rank0() const { return comm ? (comm_rank(comm) == 0 ? 1 : 0) : -1; }
+  // dist_sums_kernel's rank flag: 1 rank 0, 0 another rank, −1 unknown (a host callback without pba_gn_set_rank)
+  int rank0(const pba_engine* e) const {
+    const int r = comm ? comm_rank(comm) : e->gn.dist_rank;
+    return r < 0 ? -1 : (r == 0 ? 1 : 0);
+  }
 };
 
 // Levenberg-Marquardt (trust_region_minimizer.cc + levenberg_marquardt_strategy.cc semantics):
@@ -4194,31 +4282,19 @@ int dist_trial(pba_engine* e, const Collective& coll, const DecideOpts& dopt, do
   if (G.n_schur > 0) schur_kernel<<<G.n_schur, kBlockThreads, G.schur_lds, e->stream>>>(sa, 0.0);
   else launch_accept(e, G.lm.p);  // no points on this rank: the accept alone
   const long long nx = (long long)nf * ex_row(K);
-  PBA_HIP(hipMemsetAsync(X, 0, sizeof(double) * (size_t)nx, e->stream));
-  AsmArgs aa{G.part_lin.p, G.part_lin1.p, G.lm.p, G.part_schur.p, G.sky_cptr.p, G.sky_contrib.p, G.g_cptr.p,
-             G.g_contrib.p, G.sky_blk_i.p, G.sky_blk_j.p, G.fixed.p, G.S.p, G.g.p, G.g_dir.p, G.Ddiag.p, nullptr, K,
-             G.n_sky, nf, nullptr, nullptr, nullptr, 0, nullptr};
-  const int nthreads = G.n_sky * 36 + 6 * nf;
-  export_kernel<<<(nthreads + 255) / 256, 256, 0, e->stream>>>(aa, G.observed.p, X, K);
-  PBA_HIP(hipGetLastError());
+  if (int rc = enqueue_export(e, G.lm.p, X, K)) return rc;
   if (int rc = coll.allreduce(e, X, nx)) return rc;
-  ImportArgs ia{X, G.fixed_req.p, G.Sband.p, G.g.p, G.g_dir.p, G.Ddiag.p, G.fixed_dist.p, nf, K};
-  const long long n = (long long)nf * ((K + 1) * 36 + 6);
-  import_kernel<<<(unsigned)((n + 255) / 256), 256, 0, e->stream>>>(ia, 0.0, G.lm.p);
-  PBA_HIP(hipGetLastError());
-  G.sband_dirty = true;
-  G.cr0_dirty = true;  // cr_build writes level 0 over the whole band
-  if (int rc = band_solve(e)) return rc;
+  if (int rc = enqueue_import(e, 0.0, G.lm.p, X, K)) return rc;
   int gp = 0, gq = 0;
   enqueue_updates(e, 0.0, G.fixed_dist.p, &gp, &gq, G.lm.p);
   if (G.n_chunks > 0)
     if (int rc = linearize(e, nullptr, G.lm.p, G.pairs_new.p, G.rho_new.p, G.red.p + 2 * (gp + gq))) return rc;
   double* Y = X + nx;
   dist_sums_kernel<<<1, kDecideThreads, 0, e->stream>>>(G.red.p, G.red2.p, G.gmax.p, gp, gq, G.n_chunks, dopt.gtol,
-                                                         G.lm.p, G.status.p, coll.rank0(), G.tpose.p, Y);
+                                                         G.lm.p, G.status.p, coll.rank0(e), G.tpose.p, Y);
   PBA_HIP(hipGetLastError());
   if (int rc = coll.allreduce(e, Y, kExScalars)) return rc;
-  dist_decide_kernel<<<1, 64, 0, e->stream>>>(Y, G.tpose.p, coll.comm ? 0 : 1, dopt, G.lm.p, G.lm_host_d, seq);
+  dist_decide_kernel<<<1, 64, 0, e->stream>>>(Y, G.tpose.p, coll.rank0(e) < 0 ? 1 : 0, dopt, G.lm.p, G.lm_host_d, seq);
   PBA_HIP(hipGetLastError());
   return PBA_OK;
 }

@@ -734,6 +734,7 @@ struct GnData {
   DevBuf<uint8_t> observed, fixed_req, fixed_dist;  // multi-GPU: local observation flags, requested / effective constants
   bool sband_dirty = false;                         // Sband fully written by a distributed import
   bool cr0_dirty = true;                            // CR level 0 not (re)initialised for assemble's direct writes
+  bool cr0_inited = false;                          // CR level 0 has its zeros and padding (init_cr_level0)
   std::vector<uint8_t> fixed_h;
   DevBuf<double> poses_new, rho_new, red;
   DevBuf<double> red2, gmax;  // update partials: (Σ step², Σ x_new²) and max gradient component per slot (lm_decide)
@@ -750,6 +751,7 @@ struct GnData {
   // camera c's 8 intrinsics are the system frames nf + 2c (dims 0-5) and nf + 2c + 1 (dims 6-7, four identity pads), a
   // dense border of the skyline system.  nc_sys = 0 without intrinsics; nfs = nf + 2·nc_sys system frames.
   int nc_sys = 0, nfs = 0;
+  int dist_rank = -1;           // rank in a host-callback collective (pba_gn_set_rank); −1 unknown
   DevBuf<int4> ib_rec;          // GN block → {block, point, host, target}
   DevBuf<double> ib_data;       // GN block → weighted fp64 rows [J_i (2×8) | J_h (2×6) | J_t (2×6) | J_ρ (2) | r (2) | W_i (8)]
   DevBuf<int> ib_bptr, ib_blist;  // border unit pair (camera c, unit u) → GN blocks of its direct terms (CSR)

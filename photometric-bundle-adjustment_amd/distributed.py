@@ -166,4 +166,5 @@ def solve_distributed(engine, group=None, device=None, comm=None, **options) -> 
     if comm is not None:
         return engine.solve_distributed_comm(band, comm, **options)
     ar = TorchAllReduce(engine.gn_exchange_size(band), device if device is not None else "cpu", group)
+    engine.set_rank(dist.get_rank(group))  # rank 0's pose part decides on every rank (pba_gn_set_rank)
     return engine.solve_distributed(band, ar.ptr, ar, **options)

@@ -177,6 +177,7 @@ def lib():
         "pba_set_intrinsics_state": ([vp, vp], C.c_int),
         "pba_get_intrinsics": ([vp, vp], C.c_int),
         "pba_gn_system_size": ([vp, C.POINTER(i32)], C.c_int),
+        "pba_gn_set_rank": ([vp, i32], C.c_int),
         "pba_compute_projections": ([vp, i32, vp, vp, vp, vp, C.POINTER(OutlierThresholds), vp, vp, vp, vp], C.c_int),
         "pba_outlier_landmarks": ([i32, i32, vp, vp, vp, vp, vp, vp], C.c_int),
         "pba_set_record_format": ([vp, i32], C.c_int),
@@ -439,6 +440,10 @@ class Engine:
         _check(self._L.pba_gn_step_import(self._h, lam, band, C.c_void_p(exchange_ptr), C.byref(mp), C.byref(mq),
                                           C.byref(st)), "pba_gn_step_import")
         return mp.value, mq.value, st.value
+
+    def set_rank(self, rank: int):
+        """this engine's rank in solve_distributed's host-callback collective (pba_gn_set_rank)"""
+        _check(self._L.pba_gn_set_rank(self._h, int(rank)), "pba_gn_set_rank")
 
     def solve_distributed(self, band: int, exchange_ptr: int, allreduce, **options) -> dict:
         """pba_solve_distributed; `allreduce(ptr, count) -> None` sums `count` doubles at device address `ptr`

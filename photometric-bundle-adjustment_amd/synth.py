@@ -521,12 +521,14 @@ def render_torch(tex: PlaneTexture, K: np.ndarray, poses: np.ndarray, W: int, H:
 
 
 def c4_shard(device, rank: int = 0, world: int = 1, n_frames: int = 1000, n_points: int = 100000, K: int = 4,
-             width: int = 752, height: int = 480, texture: str = "noise", seed: int = 42):
+             width: int = 752, height: int = 480, texture: str = "noise", seed: int = 42, block_order: str = "point"):
     """configs[3] (C4) shard of `rank`: hosts [rank·F, (rank+1)·F) of a world·F + K keyframe trajectory, n_points
     points each seen by the K keyframes after its host (n_blocks = K·n_points), pinhole 752×480, 8-px pattern.
     Images are built on the GPU (torch): "noise" (independent smooth textures; throughput) or "render" (one
     textured plane seen by every keyframe, so the residual at the true state is ~0 and LM converges).  Returns
-    (problem with images=None and host intensities filled, images as a device tensor of all world·F + K frames)."""
+    (problem with images=None and host intensities filled, images as a device tensor of all world·F + K frames).
+    block_order: "point" (each point's K blocks together, hosts in order) or "morton" (within each host by target, then
+    by the Morton code of u_ref — the image-locality order of the round-4 FETCH A/B)."""
     import torch
     import torch.nn.functional as F_
     F = n_frames
@@ -565,4 +567,16 @@ def c4_shard(device, rank: int = 0, world: int = 1, n_frames: int = 1000, n_poin
         torch.from_numpy(pb.pattern[:, 1].astype(np.int64)).to(device)
     # integer u_ref and integer pattern → the bilinear host sample is exactly the pixel value
     pb.host_intensity = images[host[:, None], vv, uu].float().cpu().numpy()
+    if block_order == "morton":
+        def spread(x):  # 16-bit interleave for the Morton code
+            x = x.astype(np.uint64) & np.uint64(0xFFFF)
+            x = (x | (x << np.uint64(8))) & np.uint64(0x00FF00FF)
+            x = (x | (x << np.uint64(4))) & np.uint64(0x0F0F0F0F)
+            x = (x | (x << np.uint64(2))) & np.uint64(0x33333333)
+            return (x | (x << np.uint64(1))) & np.uint64(0x55555555)
+        ur = pb.u_ref[pb.block_point].astype(np.int64)
+        code = spread(ur[:, 0]) | (spread(ur[:, 1]) << np.uint64(1))
+        order = np.lexsort((code, pb.block_target, pb.point_host[pb.block_point]))
+        pb.block_point = np.ascontiguousarray(pb.block_point[order])
+        pb.block_target = np.ascontiguousarray(pb.block_target[order])
     return pb, images
