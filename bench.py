@@ -119,10 +119,16 @@ def c2_dropin(pb_c4, images_host, threads: int):
                      f"double sphere, Huber 9, 10 LM iterations"}
     # the plain adapter (no protocol checks: the tests run those), Ceres' own floor (constant CostFunctions in the same
     # Problem), and the CPU AutoDiff path — same Solve options
-    g = CR.run("gpu", pb, iters=10, huber=9.0, threads=threads, check=False)
-    c = CR.run("cpu", pb, iters=10, huber=9.0, threads=threads)
-    fl = CR.run("floor", pb, iters=10, huber=9.0, threads=threads)
+    # each mode twice, interleaved, the faster run of each reported (the box's host is shared: a 16-CPU cgroup quota)
+    runs = {m: [] for m in ("gpu", "cpu", "floor")}
+    for _ in range(2):
+        runs["gpu"].append(CR.run("gpu", pb, iters=10, huber=9.0, threads=threads, check=False))
+        runs["cpu"].append(CR.run("cpu", pb, iters=10, huber=9.0, threads=threads))
+        runs["floor"].append(CR.run("floor", pb, iters=10, huber=9.0, threads=threads))
+    best = {m: min(v, key=lambda r: r["jacobian_evaluation_s"] + r["residual_evaluation_s"]) for m, v in runs.items()}
+    g, c, fl = best["gpu"], best["cpu"], best["floor"]
     out["gpu_dropin"], out["cpu_autodiff"], out["ceres_floor"] = per_call(g), per_call(c), per_call(fl)
+    out["runs_per_mode"] = 2
     out["blocks"] = pb.n_blocks
     out["speedup_jacobian_evaluation"] = out["cpu_autodiff"]["jacobian_evaluation_ms"] / out["gpu_dropin"]["jacobian_evaluation_ms"]
     out["speedup_residual_evaluation"] = out["cpu_autodiff"]["residual_evaluation_ms"] / out["gpu_dropin"]["residual_evaluation_ms"]

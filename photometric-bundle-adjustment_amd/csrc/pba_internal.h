@@ -825,6 +825,7 @@ struct pba_engine {
   size_t ev_used = 0;
   // pba_get_records_async: one event per chunk of copied records, and how many chunks are known to have arrived
   std::vector<hipEvent_t> chunk_ev;
+  hipEvent_t res_ev = nullptr;       // pba_get_residuals: the copies' completion (polled, not a blocking wait)
   int chunk_blocks = 0, n_chunks_async = 0;
   std::atomic<int> chunks_arrived{0};
   pba::detail::GnData gn;
