@@ -100,7 +100,8 @@ def per_call(r):
             "residual_evaluation_ms": 1e3 * r["residual_evaluation_s"] / max(r["residual_evaluations"], 1),
             "linear_solver_ms_per_iteration": 1e3 * r["linear_solver_s"] / max(len(r["costs"]) - 1, 1),
             "minimizer_s": r["minimizer_s"], "successful_steps": r["successful_steps"],
-            "unsuccessful_steps": r["unsuccessful_steps"], "final_cost": r["final_cost"], "threads": r["threads"]}
+            "unsuccessful_steps": r["unsuccessful_steps"], "final_cost": r["final_cost"], "threads": r["threads"],
+            **({"prepare_breakdown": r["prepare"]} if "prepare" in r else {})}
 
 
 def c2_dropin(pb_c4, images_host, threads: int):
@@ -450,7 +451,8 @@ def main():
     ap.add_argument("--targets", type=int, default=4)
     ap.add_argument("--cpu-seconds", type=float, default=8.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--gn-iterations", type=int, default=10)
+    # a bundle adjustment of the reference runs 20 LM iterations (sfm.cpp:1910, map_utils.h:318)
+    ap.add_argument("--gn-iterations", type=int, default=20)
     ap.add_argument("--no-c3", action="store_true", help="skip the C3 Gauss-Newton measurement (configs[2])")
     ap.add_argument("--no-c5", action="store_true", help="skip the C5-style 21-px / fp16 / pyramid measurement")
     ap.add_argument("--no-shard-leg", action="store_true", help="N = 1: skip the 1/8-shard step leg")

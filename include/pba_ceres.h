@@ -34,7 +34,9 @@
 #include <ceres/ceres.h>
 
 #include <atomic>
+#include <chrono>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <stdexcept>
 #include <string>
@@ -187,6 +189,14 @@ class GpuEvaluator : public ceres::EvaluationCallback {
     if (!intr_.empty()) check(pba_set_optimize_intrinsics(engine_, 1), "pba_set_optimize_intrinsics");
     R_ = pba_residuals_per_block(engine_);
     rec_ = pba_record_floats(engine_);
+    // the page-locked read-back and state buffers are allocated (and mapped for the device) here, with the problem,
+    // rather than inside the first evaluation Ceres times
+    const size_t nb = (size_t)pba_num_blocks(engine_);
+    records_.resize(nb * rec_);
+    residuals_.resize(nb * R_);
+    valid_.resize(nb);
+    state_p_.resize(7 * poses_.size());
+    state_r_.resize(rho_.size());
   }
 
   // Called on the solver thread after Ceres has written the evaluation point into the user's parameter memory
@@ -194,8 +204,24 @@ class GpuEvaluator : public ceres::EvaluationCallback {
   // LM candidate, trust_region_minimizer.cc:761-779) only the residuals, R of every 14R record values.  The
   // evaluation after an accepted step comes with new_evaluation_point = false (trust_region_minimizer.cc:805-822):
   // when the point was already evaluated with Jacobians nothing is recomputed.
+  // Where PrepareForEvaluation's time goes (seconds, summed over calls; [0] residual-only, [1] with Jacobians):
+  // gather = the state into page-locked memory (+ the previous read-back's stream drain), launch = uploads + launch +
+  // enqueued read-back, wait = the residual-only read-back's wait (Jacobian read-backs are waited for per chunk by
+  // Evaluate on Ceres' threads: wait_s, summed over those threads).  Ceres times all of it inside "Residual only
+  // evaluation" / "Jacobian & residual evaluation" (program_evaluator.h:145-162).
+  struct PrepareTimes {
+    double gather_s[2] = {0, 0}, launch_s[2] = {0, 0}, readback_wait_s[2] = {0, 0}, post_s[2] = {0, 0};
+    double evaluate_call_s[2] = {0, 0};  // the pba_evaluate call alone (part of launch_s)
+    long calls[2] = {0, 0};
+  };
+  const PrepareTimes& prepare_times() const { return times_; }
+  double evaluate_wait_s() const { return 1e-9 * (double)wait_ns_.load(); }
+
   void PrepareForEvaluation(bool evaluate_jacobians, bool new_evaluation_point) override {
     if (!new_evaluation_point && have_point_ && (have_jac_ || !evaluate_jacobians)) return;
+    using clk = std::chrono::steady_clock;
+    const int m = evaluate_jacobians ? 1 : 0;
+    const auto t0 = clk::now();
     // the state is gathered into page-locked memory, so pba_set_state's uploads are DMA copies that do not stage
     // through a driver buffer; the launch is enqueued right behind them
     const size_t nf = poses_.size(), np = rho_.size();
@@ -212,22 +238,27 @@ class GpuEvaluator : public ceres::EvaluationCallback {
       for (size_t c = 0; c < intr_.size(); ++c) std::memcpy(&state_k_[8 * c], intr_[c], 8 * sizeof(double));
       check(pba_set_intrinsics_state(engine_, state_k_.data()), "pba_set_intrinsics_state");
     }
+    const auto t1 = clk::now();
     check(pba_evaluate(engine_, evaluate_jacobians ? 1 : 0), "pba_evaluate");
+    times_.evaluate_call_s[m] += std::chrono::duration<double>(clk::now() - t1).count();
     const size_t nb = (size_t)pba_num_blocks(engine_);
+    auto t2 = clk::now(), t3 = t2;
     valid_.resize(nb);
     if (evaluate_jacobians) {
       // chunked asynchronous read-back: each block's Evaluate waits only for its chunk (wait()), so Ceres' per-block
       // work overlaps the rest of the transfer
       records_.resize(nb * rec_);
-      check(pba_get_records_async(engine_, records_.data(), valid_.data(), kChunkBlocks), "pba_get_records_async");
+      check(pba_get_records_async(engine_, records_.data(), valid_.data(), chunk_blocks_), "pba_get_records_async");
       async_ = true;
       res_ = records_.data();
       res_stride_ = rec_;
+      t2 = t3 = clk::now();
       if (form_ == PoseJacobian::kReferenceSE3) {  // P⁺ of every pose at this point, while the launch and copies run
         pinv_.resize(42 * nf);
         for (size_t f = 0; f < nf; ++f) se3_plus_jacobian_pinv(sp + 7 * f, &pinv_[42 * f]);
       }
     } else {
+      t2 = clk::now();
       // residual-only: the launch also writes the residuals contiguously, so this is one plain D2H copy of 4R bytes per
       // block (not a pitched copy out of the records)
       residuals_.resize(nb * R_);
@@ -235,16 +266,30 @@ class GpuEvaluator : public ceres::EvaluationCallback {
       async_ = false;
       res_ = residuals_.data();
       res_stride_ = R_;
+      t3 = clk::now();
     }
+    const auto t4 = clk::now();
+    auto sec = [](clk::duration d) { return std::chrono::duration<double>(d).count(); };
+    times_.gather_s[m] += sec(t1 - t0);
+    times_.launch_s[m] += sec(t2 - t1);
+    times_.readback_wait_s[m] += sec(t3 - t2);
+    times_.post_s[m] += sec(t4 - t3);
+    times_.calls[m]++;
     have_point_ = true;
     have_jac_ = evaluate_jacobians;
   }
 
   // Block `block`'s record (and validity) has arrived in host memory; called by Evaluate on Ceres' worker threads.
   void wait(int block) const {
-    if (async_) check(pba_wait_records(engine_, block), "pba_wait_records");
+    if (!async_) return;
+    const auto t0 = std::chrono::steady_clock::now();
+    check(pba_wait_records(engine_, block), "pba_wait_records");
+    const long long ns = std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
+    if (ns > 1000) wait_ns_.fetch_add(ns, std::memory_order_relaxed);  // (an arrived chunk returns in ~100 ns)
   }
   static constexpr int kChunkBlocks = 4096;
+  // blocks per read-back chunk (PBA_CERES_CHUNK_BLOCKS overrides kChunkBlocks: diagnostic)
+  int chunk_blocks_ = std::getenv("PBA_CERES_CHUNK_BLOCKS") ? std::atoi(std::getenv("PBA_CERES_CHUNK_BLOCKS")) : kChunkBlocks;
 
   int residuals_per_block() const { return R_; }
   const float* record(int block) const { return records_.data() + (size_t)block * rec_; }  // with has_jacobians()
@@ -266,6 +311,8 @@ class GpuEvaluator : public ceres::EvaluationCallback {
   std::vector<double> state_k_, pinv_;
   PinnedArray<double> state_p_, state_r_;
   mutable std::atomic<bool> refused_{false};
+  mutable std::atomic<long long> wait_ns_{0};
+  PrepareTimes times_;
   PinnedArray<float> records_, residuals_;
   PinnedArray<uint8_t> valid_;
   const float* res_ = nullptr;

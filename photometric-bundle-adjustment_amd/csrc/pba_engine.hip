@@ -76,6 +76,24 @@ __global__ void state_kernel(const double* __restrict__ src_poses, const double*
 // Image relayout: row-major u8 frames → 16×8 tiles with the edge-replicating apron (pba_device.h).  One lane per
 // 16-texel tile row of the padded frame; texels beyond the padded frame are zero and never read.
 // ------------------------------------------------------------------------------------------------
+// Device → page-locked host copy by a kernel (the host buffer is mapped into the device's address space): 16-B
+// stores over the bus when both ends are 16-B aligned, bytes otherwise.  Enqueued like any launch, so the host never
+// waits inside the call — hipMemcpyAsync into the same buffers returned only when the data had arrived (C4 sample:
+// 2.4 ms per Jacobian read-back spent inside the enqueue, tools/probe/c2_probe.py).
+__global__ void host_copy_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst, long long bytes) {
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  const long long i0 = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if ((((uintptr_t)src | (uintptr_t)dst) & 15) == 0) {
+    const long long n16 = bytes >> 4;
+    const uint4* s4 = reinterpret_cast<const uint4*>(src);
+    uint4* d4 = reinterpret_cast<uint4*>(dst);
+    for (long long i = i0; i < n16; i += stride) d4[i] = s4[i];
+    for (long long i = (n16 << 4) + i0; i < bytes; i += stride) dst[i] = src[i];
+  } else {
+    for (long long i = i0; i < bytes; i += stride) dst[i] = src[i];
+  }
+}
+
 __global__ void tile_images_kernel(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst, int W, int H,
                                    int tiles_x, int tiles_y, long long n_rows) {
   const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -291,12 +309,15 @@ void photometric_block_kernel_multi(const KernelArgs a) {
       const float v[14] = {row.r, row.jr, row.hv.x, row.hv.y, row.hv.z, row.hw.x, row.hw.y, row.hw.z,
                            row.tv.x, row.tv.y, row.tv.z, row.tw.x, row.tw.y, row.tw.z};
       h2 c[7];
-      bool big = false;
+      // a value rounds to ±inf in half precision iff |v| ≥ 65520: one max over the 14 magnitudes (v_max3 with abs
+      // modifiers; a NaN drops out of the max and stays NaN) instead of a class test per converted half
+      float m = 0.0f;
 #pragma unroll
       for (int q = 0; q < 7; ++q) {
         c[q] = __builtin_convertvector((f2){v[2 * q], v[2 * q + 1]}, h2);
-        big |= __builtin_isinf(c[q].x) || __builtin_isinf(c[q].y);
+        m = fmaxf(m, fmaxf(fabsf(v[2 * q]), fabsf(v[2 * q + 1])));
       }
+      const bool big = m >= 65520.0f;
       if (__ballot(act && big) != 0) {
         auto sat = [](_Float16 h) -> _Float16 {
           return __builtin_isinf(h) ? (h > (_Float16)0 ? (_Float16)65504.0f : (_Float16)-65504.0f) : h;
@@ -1147,6 +1168,34 @@ static hipError_t wait_event(hipEvent_t ev) {
   return hipEventSynchronize(ev);
 }
 
+// Enqueue a device → host copy: by host_copy_kernel when the destination is page-locked memory mapped for the device
+// (pba_host_alloc), else hipMemcpyAsync.
+// The device address of a page-locked host buffer (the base of its allocation: an interior pointer is not found), or
+// nullptr for other memory.
+static void* mapped_device_ptr(void* host) {
+  void* dd = nullptr;
+  if (hipHostGetDevicePointer(&dd, host, 0) != hipSuccess) {
+    (void)hipGetLastError();  // (not a mapped host allocation: clear the query's error)
+    return nullptr;
+  }
+  return dd;
+}
+
+// dd: dst's device address (mapped_device_ptr of its allocation, plus the offset), or nullptr.
+static int enqueue_to_host(pba_engine* e, void* dst, void* dd, const void* src, size_t bytes) {
+  if (!bytes) return PBA_OK;
+  if (dd) {
+    const long long n16 = (long long)((bytes + 15) >> 4);
+    const int grid = (int)std::min<long long>(1024, std::max<long long>(1, (n16 + 255) / 256));
+    host_copy_kernel<<<grid, 256, 0, e->stream>>>(static_cast<const uint8_t*>(src), static_cast<uint8_t*>(dd),
+                                                  (long long)bytes);
+    PBA_HIP(hipGetLastError());
+    return PBA_OK;
+  }
+  PBA_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, e->stream));
+  return PBA_OK;
+}
+
 // Chunked asynchronous read-back for the Ceres adapter: the copies go out on the engine stream behind the evaluation,
 // an event after each chunk; a caller waiting for one block only waits for its chunk, so Ceres' per-block work
 // (CostFunction::Evaluate, the Jacobian writer) overlaps the PCIe transfer of the later chunks.
@@ -1165,11 +1214,16 @@ int pba_get_records_async(pba_engine* e, float* records, uint8_t* valid, int32_t
   e->chunk_blocks = chunk_blocks;
   e->n_chunks_async = nc;
   e->chunks_arrived.store(0);
+  // the validity flags of every block in one copy ahead of the record chunks (a copy per chunk of chunk_blocks bytes was
+  // small enough for the runtime to complete it on the host, which made every chunk's enqueue wait for the transfers
+  // before it: the whole read-back then ran inside this call, 2.5 ms of the C4 sample's evaluation)
+  float* rd = static_cast<float*>(mapped_device_ptr(records));
+  if (int rc = enqueue_to_host(e, valid, mapped_device_ptr(valid), e->valid.p, (size_t)nb)) return rc;
   for (int c = 0; c < nc; ++c) {
     const long long b0 = (long long)c * chunk_blocks, n = std::min<long long>(chunk_blocks, nb - b0);
-    PBA_HIP(hipMemcpyAsync(records + b0 * rf, e->out.p + b0 * rf, sizeof(float) * (size_t)(n * rf), hipMemcpyDeviceToHost,
-                           e->stream));
-    PBA_HIP(hipMemcpyAsync(valid + b0, e->valid.p + b0, (size_t)n, hipMemcpyDeviceToHost, e->stream));
+    if (int rc = enqueue_to_host(e, records + b0 * rf, rd ? rd + b0 * rf : nullptr, e->out.p + b0 * rf,
+                                 sizeof(float) * (size_t)(n * rf)))
+      return rc;
     PBA_HIP(hipEventRecord(e->chunk_ev[c], e->stream));
   }
   return PBA_OK;
@@ -1198,7 +1252,7 @@ int pba_get_residuals(pba_engine* e, float* residuals, uint8_t* valid) {
   std::vector<_Float16> half;
   if (residuals && nb && e->res_fresh) {
     // a residual-only evaluation also wrote its residuals contiguously: one plain device-to-host copy
-    PBA_HIP(hipMemcpyAsync(residuals, e->res.p, nb * R * sizeof(float), hipMemcpyDeviceToHost, e->stream));
+    if (int rc = enqueue_to_host(e, residuals, mapped_device_ptr(residuals), e->res.p, nb * R * sizeof(float))) return rc;
   } else if (residuals && nb) {
     // the first R values of every 14R-value record: one pitched device-to-host copy
     if (e->record_format == PBA_RECORD_F16) {
@@ -1210,7 +1264,8 @@ int pba_get_residuals(pba_engine* e, float* residuals, uint8_t* valid) {
                                hipMemcpyDeviceToHost, e->stream));
     }
   }
-  if (valid) PBA_HIP(hipMemcpyAsync(valid, e->valid.p, nb, hipMemcpyDeviceToHost, e->stream));
+  if (valid)
+    if (int rc = enqueue_to_host(e, valid, mapped_device_ptr(valid), e->valid.p, nb)) return rc;
   if (!e->res_ev) PBA_HIP(hipEventCreateWithFlags(&e->res_ev, hipEventDisableTiming));
   PBA_HIP(hipEventRecord(e->res_ev, e->stream));
   PBA_HIP(wait_event(e->res_ev));
@@ -1221,7 +1276,18 @@ int pba_get_residuals(pba_engine* e, float* residuals, uint8_t* valid) {
 int pba_host_alloc(size_t bytes, void** ptr) {
   if (!ptr) return fail(PBA_ERR_INVALID_ARGUMENT, "null argument");
   *ptr = nullptr;
-  PBA_HIP(hipHostMalloc(ptr, bytes ? bytes : 1, hipHostMallocDefault));
+  // mapped into the device's address space: the read-backs into it are copy kernels (enqueue_to_host), not
+  // hipMemcpyAsync, which returned only once a device-to-host copy had arrived
+  PBA_HIP(hipHostMalloc(ptr, bytes ? bytes : 1, hipHostMallocMapped | hipHostMallocPortable));
+  // touch every page from the device now: the first device access to fresh page-locked memory maps it into the GPU's
+  // page tables (tools/micro/d2h_enqueue: 18.5 ms for 45 MB, against 0.9 ms per later 45-MB read-back) — setup work that
+  // otherwise lands inside the first evaluation Ceres times
+  void* dd = nullptr;
+  if (bytes && hipHostGetDevicePointer(&dd, *ptr, 0) == hipSuccess && dd) {
+    PBA_HIP(hipMemsetAsync(dd, 0, bytes, nullptr));
+    PBA_HIP(hipStreamSynchronize(nullptr));
+  }
+  (void)hipGetLastError();
   return PBA_OK;
 }
 

@@ -2914,6 +2914,26 @@ __global__ __launch_bounds__(kDecideThreads) void lm_decide_kernel(const double*
   if (host_rec) publish_record(s_rec, host_rec, seq);
 }
 
+// The LM record of a new solve, on the device: the initial cost and valid blocks summed from the initial linearisation's
+// chunk partials (slots [0, gc) of red — the same partials, in the same order, as a trial's candidate cost), the trust
+// region, nothing done, buffer set 0, x_norm −1.  The host enqueues the first trials behind it instead of reading the cost
+// back first (a host round trip with the GPU idle, once per solve); init[0..1] = the initial cost and valid blocks.
+__global__ __launch_bounds__(kDecideThreads) void lm_init_kernel(const double* __restrict__ red, int gc, double radius,
+                                                                 double* __restrict__ lm, double* __restrict__ init) {
+  __shared__ double t[kTsCount];
+  trial_sums(red, red, red, 0, 0, gc, t);
+  if (threadIdx.x != 0) return;
+  for (int i = 0; i < kLmFields; ++i) lm[i] = 0.0;
+  lm[kLmCost] = t[kTsCost];
+  lm[kLmValid] = t[kTsValid];
+  lm[kLmXNorm] = -1.0;
+  lm[kLmRadius] = radius;
+  lm[kLmFactor] = 2.0;
+  lm[kLmLambda] = 1.0 / radius;
+  init[0] = t[kTsCost];
+  init[1] = t[kTsValid];
+}
+
 // Multi-GPU trial, before the scalar all-reduce: this rank's sums, written to the exchange buffer's kExScalars scalar
 // slots Y for the Σ over ranks:
 //   Y[0..7]  the point part: [δρ·g, δρ·D·δρ, candidate cost, candidate valid blocks, Σδρ², Σρ_new², points above the
@@ -4192,19 +4212,14 @@ int lm_loop_single(pba_engine* e, const pba_solver_options* o, pba_solver_summar
     for (int i = 0; i < 8; ++i) PBA_HIP(hipEventCreate(&events.ev[i]));
   const double t0 = now_ms();
   double cost = 0.0;
-  int n_valid = 0;
-  if (int rc = linearize(e, &cost, nullptr, nullptr, nullptr, nullptr, &n_valid)) return rc;  // initial state, set 0
-  s.linearize_ms += now_ms() - t0;
-  s.initial_cost = cost;
-  // the device record: current cost and valid blocks, trust region, nothing done, set 0, x_norm −1; no trial published
-  for (int i = 0; i <= kLmFields; ++i) G.lm_h[i] = 0.0;
-  G.lm_h[kLmCost] = cost;
-  G.lm_h[kLmValid] = n_valid;
-  G.lm_h[kLmXNorm] = -1.0;
-  G.lm_h[kLmRadius] = opt.initial_trust_region_radius;
-  G.lm_h[kLmFactor] = 2.0;
-  G.lm_h[kLmLambda] = 1.0 / opt.initial_trust_region_radius;
-  PBA_HIP(hipMemcpyAsync(G.lm.p, G.lm_h.data(), sizeof(double) * kLmFields, hipMemcpyHostToDevice, e->stream));
+  // the initial linearisation (set 0) with its chunk cost partials in red, and the device record formed from them
+  // (lm_init_kernel): no host round trip before the first trial
+  if (int rc = linearize(e, nullptr, nullptr, nullptr, nullptr, G.red.p)) return rc;
+  if (G.lm_init.n < 2) PBA_HIP(G.lm_init.resize(2));
+  lm_init_kernel<<<1, kDecideThreads, 0, e->stream>>>(G.red.p, G.n_chunks, opt.initial_trust_region_radius, G.lm.p,
+                                                       G.lm_init.p);
+  PBA_HIP(hipGetLastError());
+  G.lm_h[kLmFields] = 0.0;  // no trial published yet
   const int n = std::max(0, opt.max_iterations);
   const DecideOpts dopt = decide_opts(opt);
   auto enqueue = [&](int i) { return lm_trial(e, dopt, (double)(i + 1), timed ? events.ev + 4 * (i & 1) : nullptr); };
@@ -4249,7 +4264,11 @@ int lm_loop_single(pba_engine* e, const pba_solver_options* o, pba_solver_summar
     cost = d[kLmCostNew];
   }
   launch_accept(e, G.lm.p);  // the last trial's accept (no trial after it to apply it)
+  double init[2] = {0.0, 0.0};
+  PBA_HIP(hipMemcpyAsync(init, G.lm_init.p, sizeof init, hipMemcpyDeviceToHost, e->stream));
   PBA_HIP(hipStreamSynchronize(e->stream));
+  s.initial_cost = init[0];
+  if (s.successful_steps == 0) cost = init[0];
   if (set == 1) {  // the current state's pieces are in set 1: make it set 0 for the host-driven entry points
     std::swap(G.blk_schur.p, G.blk_schur1.p);
     std::swap(G.blk_schur.n, G.blk_schur1.n);

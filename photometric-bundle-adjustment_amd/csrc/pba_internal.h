@@ -745,6 +745,7 @@ struct GnData {
   bool pairs_new_fresh = false;  // pairs_new formed by the last update_kernel (its candidate state)
   PinnedBuf<double> red_h;
   DevBuf<double> lm;         // LM decision record of the single-GPU loop (pba_gn.hip: kLm*)
+  DevBuf<double> lm_init;    // the solve's initial cost and valid blocks (lm_init_kernel)
   DevBuf<double> lm_idle;    // the record host-driven steps pass to the kernels (not done, set 0, λ from the argument)
   PinnedBuf<double> lm_h;    // its host copy (+ sequence number), host-coherent, written by lm_decide_kernel
   // Intrinsics in the reduced camera system (pba_set_optimize_intrinsics, geometric engines; pba_gn.hip "intrinsics"):

@@ -388,6 +388,17 @@ int main(int argc, char** argv) {
   o << ",\"intrinsics\":";
   json_array(o, intr.data(), intr.size());
   o << ",\"refused_intrinsics\":" << (ev && ev->refused_intrinsics() ? 1 : 0);
+  if (ev) {  // the adapter's own breakdown of PrepareForEvaluation ([residual-only, with Jacobians], seconds)
+    const auto& t = ev->prepare_times();
+    snprintf(buf, sizeof buf,
+             ",\"prepare\":{\"calls\":[%ld,%ld],\"gather_s\":[%.6g,%.6g],\"launch_s\":[%.6g,%.6g],"
+             "\"readback_wait_s\":[%.6g,%.6g],\"post_s\":[%.6g,%.6g],\"evaluate_wait_s\":%.6g,"
+             "\"evaluate_call_s\":[%.6g,%.6g]}",
+             t.calls[0], t.calls[1], t.gather_s[0], t.gather_s[1], t.launch_s[0], t.launch_s[1], t.readback_wait_s[0],
+             t.readback_wait_s[1], t.post_s[0], t.post_s[1], ev->evaluate_wait_s(), t.evaluate_call_s[0],
+             t.evaluate_call_s[1]);
+    o << buf;
+  }
   o << "}\n";
   FILE* g = fopen(argv[3], "w");
   if (!g) return 4;
