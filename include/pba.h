@@ -256,7 +256,11 @@ int pba_gn_linearize(pba_engine* engine, double* cost);
 int pba_gn_step(pba_engine* engine, double lambda, double* model_decrease, int32_t* solver_status);
 int pba_gn_candidate_cost(pba_engine* engine, double* cost);
 int pba_gn_accept(pba_engine* engine);   /* state ← candidate */
-/* full LM loop (trust_region_minimizer.cc semantics); options may be NULL (Ceres defaults, 20 iterations) */
+/* full LM loop (trust_region_minimizer.cc semantics); options may be NULL (Ceres defaults, 20 iterations).
+ * A candidate counts as a failed evaluation (cost DBL_MAX, trust_region_minimizer.cc:771-778) when it has fewer valid
+ * blocks than the current state — exactly Ceres' rule when every block is valid at the current state (the normal case:
+ * an invalid block has no residual for Ceres either); from a state that already has invalid blocks, a block turning
+ * valid can mask another turning invalid. */
 int pba_solve(pba_engine* engine, const pba_solver_options* options, pba_solver_summary* summary);
 /* read back the state (7·n_frames poses, n_points inverse distances) */
 int pba_get_state(pba_engine* engine, double* poses, double* inv_dist);
