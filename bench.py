@@ -268,14 +268,23 @@ def gn_benchmark(eng, iters, torch, dist, dev, world):
     eng.set_fixed_frames(np.array([0, 1], np.int32))
     eng.gn_linearize()  # symbolic analysis (once per problem structure), outside the timed region
     opts = dict(max_iterations=iters, function_tolerance=0.0)
+    agree = None
+    device_steered = world > 1 and dist.get_backend() == "nccl" and os.environ.get("PBA_BENCH_GN_COMM") == "1"
     if world > 1:
         band = D.global_band(eng, None, dev)
-        # the RCCL communicator is set up by the warm-up (nccl backend: both sums of a trial on the engine stream)
-        D.solve_distributed(eng, device=dev, max_iterations=1)
+        # Default: the host-callback loop (pba_solve_distributed, torch's all_reduce between trials), which cannot
+        # desynchronise the ranks' collective sequences.  PBA_BENCH_GN_COMM=1 selects the device-steered RCCL loop
+        # (pba_solve_distributed_comm) — kept opt-in until a run with several GPUs has confirmed it.
+        comm = None if device_steered else False
+        D.solve_distributed(eng, device=dev, comm=comm, max_iterations=1)  # warm-up (sets the RCCL communicator up)
         dist.barrier()
         torch.cuda.synchronize()
-        s = D.solve_distributed(eng, device=dev, **opts)
+        s = D.solve_distributed(eng, device=dev, comm=comm, **opts)
         exchange_mb = 8.0 * eng.gn_exchange_size(band) / 1e6
+        # every rank must have taken the same decisions: the global costs and step counts agree bit for bit
+        v = [s["initial_cost"], s["final_cost"], float(s["iterations"]), float(s["successful_steps"])]
+        m = all_reduce_max(torch, dist, v + [-x for x in v], dev).tolist()
+        agree = all(m[i] == -m[i + len(v)] for i in range(len(v)))
     else:
         eng.solve(max_iterations=1)  # warm-up
         torch.cuda.synchronize()
@@ -292,10 +301,10 @@ def gn_benchmark(eng, iters, torch, dist, dev, world):
     return {"ms_per_iteration": float(t[0]) / n, "iterations": s["iterations"], "accepted": s["successful_steps"],
             "breakdown_ms_per_iteration": {"linearize_ms": float(t[1]) / n, "step_ms": float(t[2]) / n,
                                            "cost_ms": float(t[3]) / n},
-            "exchange_mb_per_iteration": exchange_mb,
+            "exchange_mb_per_iteration": exchange_mb, "ranks_agree": agree,
             "note": "host wall clock of the engine's LM loop (pba_solve" + (
                 "_distributed_comm: the device-steered loop with two RCCL all-reduces per trial on the engine stream "
-                "(the banded reduced camera system, then 8 point-part scalars)" if world > 1 and dist.get_backend() == "nccl"
+                "(the banded reduced camera system, then 16 scalars)" if device_steered
                 else f"_distributed: {dist.get_backend()} all-reduces through a host callback" if world > 1 else "") +
                     "); noise-textured images, so the steps are not expected to converge — timing only"}
 

@@ -154,8 +154,8 @@ def rccl_comm(group=None, device_index: int = 0):
 
 def solve_distributed(engine, group=None, device=None, comm=None, **options) -> dict:
     """LM over all ranks of `group`: collective, every rank calls it.  comm (an engine.Comm) or, for the "nccl" backend
-    on a GPU, the cached RCCL communicator: stream-ordered pba_solve_distributed_comm; otherwise the TorchAllReduce
-    callback of pba_solve_distributed."""
+    on a GPU, the cached RCCL communicator: stream-ordered pba_solve_distributed_comm; otherwise (or comm=False) the
+    TorchAllReduce callback of pba_solve_distributed."""
     import torch.distributed as dist
     import torch
     if device is not None:
@@ -163,7 +163,7 @@ def solve_distributed(engine, group=None, device=None, comm=None, **options) -> 
     band = global_band(engine, group, device)
     if comm is None and device is not None and device.type == "cuda" and dist.get_backend(group) == "nccl":
         comm = rccl_comm(group, device.index if device.index is not None else torch.cuda.current_device())
-    if comm is not None:
+    if comm is not None and comm is not False:
         return engine.solve_distributed_comm(band, comm, **options)
     ar = TorchAllReduce(engine.gn_exchange_size(band), device if device is not None else "cpu", group)
     engine.set_rank(dist.get_rank(group))  # rank 0's pose part decides on every rank (pba_gn_set_rank)

@@ -83,6 +83,10 @@ def test_c1_engine_lm_matches_ceres_cpu(c1):
     assert s["unsuccessful_steps"] == ref["unsuccessful_steps"]
     assert abs(s["initial_cost"] - ref["costs"][0]) <= 1e-6 * ref["costs"][0]
     assert abs(s["final_cost"] - ref["final_cost"]) <= 1e-5 * ref["final_cost"], (s, ref["final_cost"])
+    dt, dq = np.abs(poses[:, 4:] - ref["poses"][:, 4:]).max(), np.abs(poses[:, :4] - ref["poses"][:, :4]).max()
+    dr = (np.abs(rho - ref["rho"]) / np.abs(ref["rho"])).max()
+    print(f"\nC1 engine LM vs Ceres: final cost {abs(s['final_cost'] - ref['final_cost']) / ref['final_cost']:.2e}, "
+          f"max |Δt| {dt:.2e} m, max |Δq| {dq:.2e}, max Δρ/ρ {dr:.2e}")
     np.testing.assert_allclose(poses[:, 4:], ref["poses"][:, 4:], atol=1e-4)
     np.testing.assert_allclose(rho, ref["rho"], rtol=1e-3)
 

@@ -423,6 +423,10 @@ def test_c3_engine_lm_matches_ceres_cpu(c3):
     ref = CR.run("cpu", c3, iters=10, huber=9.0, threads=THREADS, timeout=1200)
     with make_engine(c3, 9.0, (0, 1)) as eng:
         s = eng.solve(max_iterations=10)
+        poses, rho = eng.get_state()
+    dt = np.abs(poses[:, 4:] - ref["poses"][:, 4:]).max()
+    dr = (np.abs(rho - ref["rho"]) / np.abs(ref["rho"])).max()
+    print(f"\nC3 LM final state vs Ceres: max |Δt| {dt:.2e} m, max Δρ/ρ {dr:.2e}")
     print(f"\nC3 LM: engine {s['successful_steps']}/{s['unsuccessful_steps']} final {s['final_cost']:.9g}, Ceres "
           f"{ref['successful_steps'] - 1}/{ref['unsuccessful_steps']} final {ref['final_cost']:.9g} ({ref['message']})")
     assert s["successful_steps"] == ref["successful_steps"] - 1, (s, ref["message"])
