@@ -193,6 +193,12 @@ def all_reduce_max(torch, dist, values, dev):
     return t.cpu()
 
 
+def ranks_agree(torch, dist, values, dev):
+    """True when every rank holds bit-identical `values` (one MAX all-reduce of v and -v)."""
+    m = all_reduce_max(torch, dist, list(values) + [-x for x in values], dev).tolist()
+    return all(m[i] == -m[i + len(values)] for i in range(len(values)))
+
+
 def make_states(pb, torch, dev, seed):
     rng = np.random.default_rng(seed)
     states = []
@@ -282,9 +288,8 @@ def gn_benchmark(eng, iters, torch, dist, dev, world):
         s = D.solve_distributed(eng, device=dev, comm=comm, **opts)
         exchange_mb = 8.0 * eng.gn_exchange_size(band) / 1e6
         # every rank must have taken the same decisions: the global costs and step counts agree bit for bit
-        v = [s["initial_cost"], s["final_cost"], float(s["iterations"]), float(s["successful_steps"])]
-        m = all_reduce_max(torch, dist, v + [-x for x in v], dev).tolist()
-        agree = all(m[i] == -m[i + len(v)] for i in range(len(v)))
+        agree = ranks_agree(torch, dist, [s["initial_cost"], s["final_cost"], float(s["iterations"]),
+                                          float(s["successful_steps"])], dev)
     else:
         eng.solve(max_iterations=1)  # warm-up
         torch.cuda.synchronize()

@@ -94,3 +94,17 @@ def solve_worker(rank: int, world: int, port: int, case: dict, out):
     except BaseException:
         out.put((rank, traceback.format_exc()))
         raise
+
+
+def agree_worker(rank: int, world: int, port: int, values_by_rank: list, out):
+    """Rank body of bench.ranks_agree over gloo: each rank contributes its own values."""
+    try:
+        import torch
+        import torch.distributed as dist
+        bench = importlib.import_module("bench")
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        out.put((rank, bench.ranks_agree(torch, dist, values_by_rank[rank], "cpu")))
+        dist.destroy_process_group()
+    except BaseException:
+        out.put((rank, traceback.format_exc()))

@@ -77,3 +77,23 @@ def test_gloo_exchange_equals_single_process_schur(case):
         assert e["S"] <= 1e-9 and e["g"] <= 1e-9 and e["dp"] <= 1e-7 and e["cost"] <= 1e-12, e
     assert res[0]["n_points"] + res[1]["n_points"] == case["n_points"]
     assert res[0]["n_points"] > 0 and res[1]["n_points"] > 0
+
+
+@pytest.mark.parametrize("values,expect", [
+    ([[3.25, 1.0e-3, 20.0, 7.0], [3.25, 1.0e-3, 20.0, 7.0]], True),
+    ([[3.25, 1.0e-3, 20.0, 7.0], [3.25, 1.0e-3 * (1 + 2 ** -52), 20.0, 7.0]], False),  # one ulp apart
+    ([[3.25, 1.0e-3, 20.0, 7.0], [3.25, 1.0e-3, 20.0, 6.0]], False),
+])
+def test_bench_ranks_agree(values, expect):
+    """bench.py's multi-GPU GN leg reports ranks_agree: every rank's global costs and step counts bit-identical."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=dist_workers.agree_worker, args=(r, world, port, values, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=240) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+    assert res[0] is expect and res[1] is expect, res
