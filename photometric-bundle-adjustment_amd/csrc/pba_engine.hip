@@ -422,156 +422,6 @@ void photometric_block_kernel_multi(const KernelArgs a) {
   store_slab<T, NTH>(lds, reinterpret_cast<unsigned char*>(out + (long long)blk0 * rec_f), nblk * rec_f * (int)sizeof(T));
 }
 
-// The records of a 9…32-px pattern at a fused state with the LDS camera table (the C5 configuration), its (block, pixel)
-// rows dealt to a wave's lanes flat: row i of the wave is pixel i mod P of its block i / P, PPL rows per lane, so a wave
-// carries bw = ⌊64·PPL / P⌋ blocks (P = 21: 9 blocks in 189 of its 192 lane slots, against 8 blocks in 168 with 8 lanes per
-// block, photometric_block_kernel_multi).  The rows are the same arithmetic (photometric_row, stage_row), so the records
-// are bit-identical to the other forms; per-block ‖r‖² and validity come from an LDS row table summed in pixel order.
-// LDS: the record stage and compact tiles of 4·bw blocks, the row table, the camera table.
-__host__ __device__ constexpr int flat_blocks_per_wave(int P, int ppl) { return 64 * ppl / P; }
-// (P = 21, fp16: 21168 + 36·(192 + 84) = 31104 B, with the static s_pat / s_cam 31.9 KB: five workgroups per CU)
-__host__ __device__ constexpr int flat_lds_bytes(int P, int ppl, int tsize) {
-  return multi_stage_bytes(4 * flat_blocks_per_wave(P, ppl), P, tsize) + 4 * flat_blocks_per_wave(P, ppl) *
-         ((int)sizeof(TileBlockC) + 4 * P);
-}
-
-// The prologue of stage_tile_wg_ct for nb ≤ 64 tile blocks: lane b of waves 0 / 1 / 3 stages block b's rotation /
-// translation and ids / point, wave 2 the camera table.  Tile blocks past the problem's end stage its last block (every
-// row then reads valid data: a dead row's image offset must be in bounds).  The caller barriers.
-__device__ __forceinline__ void stage_tile_wg_ct_n(const KernelArgs& a, TileBlockC* s_tb, CamRec* s_cam, int n_cams,
-                                                   int blk0, int nb) {
-  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, b = lane;
-  const int4 br = a.block_rec[min(blk0 + b, a.n_blocks - 1)];  // a dead block stages the last block
-  TileBlockC& tb = s_tb[b < nb ? b : 0];
-  if (w == 2) {
-    const int c = lane >> 3, q = lane & 7;
-    if (c < n_cams) {
-      const uint4 v = reinterpret_cast<const uint4*>(a.intr_d + (q < 4 ? kCamD * c + kCamHk : kCamD * c))[q & 3];
-      reinterpret_cast<uint4*>(s_cam + c)[q] = v;
-      if (q >= 4) camera_kf_part(v, q - 4, s_cam[c].kf);
-    }
-    return;
-  }
-  if (b >= nb) return;
-  if (w == 0) {
-    const double* H = a.poses + 7 * br.y;
-    const double* T = a.poses + 7 * br.z;
-    double h[4], t[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      h[j] = H[j];
-      t[j] = T[j];
-    }
-    pair_rotation(h, t, tb);
-  } else if (w == 1) {
-    const double* H = a.poses + 7 * br.y;
-    const double* T = a.poses + 7 * br.z;
-    double h[7], t[7];
-#pragma unroll
-    for (int j = 0; j < 7; ++j) {
-      h[j] = H[j];
-      t[j] = T[j];
-    }
-    pair_translation(h, t, tb);
-    tb.host_cam = br.w >> 16;
-    tb.target_cam = br.w & 0xffff;
-    tb.target = br.z;
-    tb.host = br.y;
-  } else {
-    const double2 ur = a.u_ref[br.x];
-    const double rho = a.rho[br.x];
-    tb.ur = ur;
-    tb.rho = rho;
-    tb.img = (long long)br.z * a.frame_stride;
-  }
-}
-
-template <int PM, class T, int PPL, bool C1>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5, 8)))
-void photometric_block_kernel_flat(const KernelArgs a) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
-  __shared__ float2 s_pat[8 * PPL];
-  __shared__ CamRec s_cam[kCamTab];
-  const int P = a.P, bw = flat_blocks_per_wave(P, PPL), BPW = 4 * bw, rec_f = 14 * P;
-  T* stage = reinterpret_cast<T*>(lds);
-  TileBlockC* s_tb = reinterpret_cast<TileBlockC*>(lds + multi_stage_bytes(BPW, P, (int)sizeof(T)));
-  // [block][pixel]: r² of a valid row, −1 for an invalid one; after the sums, [block][0] holds the block's validity
-  float* s_r2 = reinterpret_cast<float*>(s_tb + BPW);
-  const int blk0 = logical_tile() * BPW;
-  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63, wb0 = w * bw;
-  T* out = reinterpret_cast<T*>(a.out);
-  if ((int)threadIdx.x < P) s_pat[threadIdx.x] = pattern_at<8 * PPL>(a, threadIdx.x);
-  adopt_state(a);
-  // this lane's rows: block wb0 + bj[j] of the workgroup, pixel pj[j]; their I_h,k loaded before the prologue's barrier
-  int bj[PPL], pj[PPL];
-  bool lj[PPL];
-  float Ih[PPL];
-#pragma unroll
-  for (int j = 0; j < PPL; ++j) {
-    const int i = j * 64 + lane, b = i / P;
-    bj[j] = min(b, bw - 1);
-    pj[j] = i - b * P;
-    lj[j] = b < bw && blk0 + wb0 + b < a.n_blocks;
-    const int pt = a.block_rec[min(blk0 + wb0 + bj[j], a.n_blocks - 1)].x;
-    Ih[j] = lj[j] ? a.host_int[(long long)pt * P + pj[j]] : 0.0f;
-  }
-  stage_tile_wg_ct_n(a, s_tb, s_cam, a.n_cams, blk0, BPW);
-  __syncthreads();
-#pragma unroll 1
-  for (int j = 0; j < PPL; ++j) {
-    int b = bj[0], px = pj[0];
-    bool act = lj[0];
-    float ih = Ih[0];
-#pragma unroll
-    for (int q = 1; q < PPL; ++q)
-      if (j == q) {
-        b = bj[q];
-        px = pj[q];
-        act = lj[q];
-        ih = Ih[q];
-      }
-    asm volatile("" ::: "memory");  // the tile is read from LDS per row (see photometric_block_kernel_multi)
-    const Row row = photometric_row<PM, true, TileBlockC, C1>(a, s_tb[wb0 + b], s_pat[act ? px : 0], ih, s_cam);
-    stage_row<T>(stage + (wb0 + b) * rec_f, P, px, row, act);
-    if (act) s_r2[(wb0 + b) * P + px] = row.ok ? row.r * row.r : -1.0f;
-  }
-  // the wave's blocks: lane l sums block wb0 + l's rows in pixel order (LDS operations of a wave stay in order)
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  if (lane < bw) {
-    const int B = wb0 + lane, blk = blk0 + B;
-    if (blk < a.n_blocks) {
-      float sum = 0.0f;
-      int ok = 1;
-      for (int px = 0; px < P; ++px) {
-        const float v = s_r2[B * P + px];
-        ok &= v >= 0.0f;
-        sum += v >= 0.0f ? v : 0.0f;
-      }
-      s_r2[B * P] = ok ? 1.0f : 0.0f;
-      a.valid[blk] = (uint8_t)ok;
-      a.cost[blk] = ok ? huber_cost(sum, a.huber) : 0.0f;
-    }
-  }
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-#pragma unroll
-  for (int j = 0; j < PPL; ++j) {  // an invalid block leaves a zero record (Ceres' Evaluate returning false)
-    if (!lj[j] || s_r2[(wb0 + bj[j]) * P] != 0.0f) continue;
-    T* r = stage + (wb0 + bj[j]) * rec_f;
-    const int px = pj[j];
-    r[px] = (T)0.0f;
-    r[13 * P + px] = (T)0.0f;
-    for (int q = 0; q < 6; ++q) r[P + 6 * px + q] = r[7 * P + 6 * px + q] = (T)0.0f;
-  }
-  __syncthreads();
-  const int nblk = min(BPW, a.n_blocks - blk0);
-  if (nblk <= 0) return;
-  store_slab<T, 256>(lds, reinterpret_cast<unsigned char*>(out + (long long)blk0 * rec_f), nblk * rec_f * (int)sizeof(T));
-}
-
 // ------------------------------------------------------------------------------------------------
 // Geometric block kernel (reprojection.h:105-108): lane = block, record 28 floats = 7 float4 stores, or with the
 // target-intrinsics Jacobian (INTR, pba_set_optimize_intrinsics) 44 floats = 11 float4 stores
@@ -685,24 +535,13 @@ void launch_photometric(pba_engine* e, const KernelArgs& ka, int mode) {
   // 9…32 pixels: 8 lanes per block, ⌈P/8⌉ pixels per lane
   // the camera-table form for record launches at a fused state with few cameras (the C5 configuration)
   const bool ct = mode == 1 && ka.poses != nullptr && ka.n_cams <= kCamTab && !e->no_cam_table;
-  // the flat row layout for those launches (PBA_FLAT_ROWS=0: 8 lanes per block, photometric_block_kernel_multi)
-  const bool flat = !e->no_flat_rows;
 #define PBA_LAUNCH_ONE(PPL, M, TT)                                                                      \
   {                                                                                                     \
     constexpr int nth = kMultiThreads<PPL, TT>;                                                         \
     const int grid = (int)(((long long)e->n_blocks * 8 + nth - 1) / nth);                              \
     e->last_grid = grid;                                                                                \
     const size_t stage = M == 1 ? multi_stage_bytes(nth / 8, e->P, (int)sizeof(TT)) : 0;               \
-    if (M == 1 && ct && flat && flat_lds_bytes(e->P, PPL, (int)sizeof(TT)) <= 60 * 1024) {              \
-      const int bpw_ = 4 * flat_blocks_per_wave(e->P, PPL);                                             \
-      const int grid_ = (e->n_blocks + bpw_ - 1) / bpw_;                                                \
-      e->last_grid = grid_;                                                                             \
-      const size_t lds_ = (size_t)flat_lds_bytes(e->P, PPL, (int)sizeof(TT));                          \
-      if (ka.n_cams == 1)                                                                               \
-        photometric_block_kernel_flat<PM, TT, PPL, true><<<grid_, 256, lds_, e->stream>>>(ka);          \
-      else                                                                                              \
-        photometric_block_kernel_flat<PM, TT, PPL, false><<<grid_, 256, lds_, e->stream>>>(ka);         \
-    } else if (M == 1 && nth == 256 && ct && ka.n_cams == 1) {                                          \
+    if (M == 1 && nth == 256 && ct && ka.n_cams == 1) {                                                 \
       photometric_block_kernel_multi<PM, M, TT, PPL, (M == 1 && nth == 256), (M == 1 && nth == 256)>    \
           <<<grid, nth, stage + (size_t)(nth / 8) * sizeof(TileBlockC), e->stream>>>(ka);              \
     } else if (M == 1 && nth == 256 && ct) {                                                            \
@@ -1187,9 +1026,8 @@ int evaluate_at(pba_engine* e, const double* poses, const double* rho, bool adop
   if (int rc = check_device(e)) return rc;
   KernelArgs ka;
   if (photometric) {
-    // every photometric launch runs ≥ 4 lanes per block (8: photometric_block_kernel / _multi; 256 per ≤ 64 blocks:
-    // photometric_block_kernel_flat)
-    const long long lanes = (long long)e->n_blocks * 4;
+    // every photometric launch runs 8 lanes per block (photometric_block_kernel / _multi, launch_blocks)
+    const long long lanes = (long long)e->n_blocks * 8;
     if (adopt && lanes < std::max<long long>(7LL * e->n_frames, e->n_points)) {
       if (int rc = pba_set_state_device(e, poses, rho)) return rc;  // more state than lanes: copy first
       poses = e->poses.p;

@@ -819,7 +819,6 @@ struct pba_engine {
   bool evaluated = false;
   bool timing = false;
   bool no_cam_table = std::getenv("PBA_NO_CAM_TABLE") != nullptr;  // A/B switch: the C5 kernel without its camera table
-  bool no_flat_rows = std::getenv("PBA_FLAT_ROWS") && std::string(std::getenv("PBA_FLAT_ROWS")) == "0";  // A/B: 8 lanes per block
   int last_grid = 0;                 // workgroups of the last evaluation launch (launch_mode)
   std::vector<hipEvent_t> ev_pool;   // start/stop pairs, reused
   int level = 0;                     // active pyramid level (its buffers are swapped into the fields above)

@@ -87,8 +87,10 @@ def test_c1_engine_lm_matches_ceres_cpu(c1):
     dr = (np.abs(rho - ref["rho"]) / np.abs(ref["rho"])).max()
     print(f"\nC1 engine LM vs Ceres: final cost {abs(s['final_cost'] - ref['final_cost']) / ref['final_cost']:.2e}, "
           f"max |Δt| {dt:.2e} m, max |Δq| {dq:.2e}, max Δρ/ρ {dr:.2e}")
+    # measured (round 4): final cost 9.9e-9, |Δt| 2.7e-5 m, |Δq| 2.7e-8, Δρ/ρ 1.2e-5 — bounds ~4-40× above
     np.testing.assert_allclose(poses[:, 4:], ref["poses"][:, 4:], atol=1e-4)
-    np.testing.assert_allclose(rho, ref["rho"], rtol=1e-3)
+    np.testing.assert_allclose(poses[:, :4], ref["poses"][:, :4], atol=1e-6)
+    np.testing.assert_allclose(rho, ref["rho"], rtol=1e-4)
 
 
 @needs_ceres

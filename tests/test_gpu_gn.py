@@ -417,7 +417,9 @@ def test_c3_reduced_system_and_step_against_fp64_reference(c3, lam):
 def test_c3_engine_lm_matches_ceres_cpu(c3):
     """pba_solve at full C3 size against real Ceres 2.0.0 LM (SPARSE_SCHUR, AutoDiff over the restated photometric
     functor, the reference's LocalParameterizationSE3): the same successful / unsuccessful step counts and the final
-    cost to 1e-5."""
+    cost to 1e-5.  The state after 10 iterations (not converged: Ceres stops at the iteration limit) measured |Δt| ≤
+    6.3e-4 m and Δρ/ρ ≤ 3.6e-2 at the worst point (the 99th percentile is printed): weakly observed inverse distances
+    move along their null direction with the order of the fp64 sums; bounded at ~3× those."""
     if not CR.available():
         pytest.skip("oracle/_ref/ceres_lm_driver not built")
     ref = CR.run("cpu", c3, iters=10, huber=9.0, threads=THREADS, timeout=1200)
@@ -426,13 +428,15 @@ def test_c3_engine_lm_matches_ceres_cpu(c3):
         poses, rho = eng.get_state()
     dt = np.abs(poses[:, 4:] - ref["poses"][:, 4:]).max()
     dr = (np.abs(rho - ref["rho"]) / np.abs(ref["rho"])).max()
-    print(f"\nC3 LM final state vs Ceres: max |Δt| {dt:.2e} m, max Δρ/ρ {dr:.2e}")
+    dr99 = np.percentile(np.abs(rho - ref["rho"]) / np.abs(ref["rho"]), 99)
+    print(f"\nC3 LM final state vs Ceres: max |Δt| {dt:.2e} m, max Δρ/ρ {dr:.2e} (99th percentile {dr99:.2e})")
     print(f"\nC3 LM: engine {s['successful_steps']}/{s['unsuccessful_steps']} final {s['final_cost']:.9g}, Ceres "
           f"{ref['successful_steps'] - 1}/{ref['unsuccessful_steps']} final {ref['final_cost']:.9g} ({ref['message']})")
     assert s["successful_steps"] == ref["successful_steps"] - 1, (s, ref["message"])
     assert s["unsuccessful_steps"] == ref["unsuccessful_steps"], (s, ref["message"])
     assert abs(s["initial_cost"] - ref["costs"][0]) <= 1e-6 * ref["costs"][0]
     assert abs(s["final_cost"] - ref["final_cost"]) <= 1e-5 * ref["final_cost"], (s["final_cost"], ref["final_cost"])
+    assert dt <= 2e-3 and dr <= 0.1, (dt, dr)
 
 
 def test_set_frames_after_gn_reanalyses_the_problem():
