@@ -24,7 +24,11 @@ def exchange_worker(rank: int, world: int, port: int, case: dict, out):
         synth = importlib.import_module("photometric-bundle-adjustment_amd.synth")
         D = importlib.import_module("photometric-bundle-adjustment_amd.distributed")
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-        dist.init_process_group("gloo", rank=rank, world_size=world)
+        if case.get("backend", "gloo") == "nccl":  # RCCL: one rank per device
+            torch.cuda.set_device(0)
+            dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", 0))
+        else:
+            dist.init_process_group("gloo", rank=rank, world_size=world)
         pb = synth.make_problem(kind=case["kind"], n_frames=case["n_frames"], n_points=case["n_points"],
                                 width=376, height=240, seed=case["seed"], border=12, obs_sigma=0.3)
         lam, huber, fixed = case["lam"], case["huber"], tuple(case["fixed"])
@@ -74,7 +78,11 @@ def solve_worker(rank: int, world: int, port: int, case: dict, out):
         E = importlib.import_module("photometric-bundle-adjustment_amd.engine")
         D = importlib.import_module("photometric-bundle-adjustment_amd.distributed")
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-        dist.init_process_group("gloo", rank=rank, world_size=world)
+        if case.get("backend", "gloo") == "nccl":  # RCCL: one rank per device
+            torch.cuda.set_device(0)
+            dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", 0))
+        else:
+            dist.init_process_group("gloo", rank=rank, world_size=world)
         pb = synth.make_problem(kind=case["kind"], n_frames=case["n_frames"], n_points=case["n_points"],
                                 width=376, height=240, seed=case["seed"], border=12, obs_sigma=0.3)
         pb.poses[:2] = pb.poses_gt[:2]
@@ -84,7 +92,9 @@ def solve_worker(rank: int, world: int, port: int, case: dict, out):
             eng.set_problem(sub)
             eng.set_fixed_frames(np.array(case["fixed"], np.int32))
             eng.set_state(sub.poses, sub.rho)
-            s = D.solve_distributed(eng, device=torch.device("cuda", 0), max_iterations=case["iters"])
+            # comm False: the host-callback loop (TorchAllReduce); None: the RCCL communicator for an nccl group
+            s = D.solve_distributed(eng, device=torch.device("cuda", 0), comm=case.get("comm"),
+                                    max_iterations=case["iters"])
             poses, rho = eng.get_state()
         finally:
             eng.close()

@@ -316,6 +316,47 @@ def test_two_process_gloo_solve_matches_solve(kind, huber):
     assert ref["final_cost"] < ref["initial_cost"]
 
 
+@pytest.mark.parametrize("comm", ["callback", "rccl"])
+def test_one_rank_nccl_group_solve_matches_solve(comm):
+    """bench.py's multi-GPU GN leg under an "nccl" (RCCL) torch.distributed group, with the one rank a single GPU allows:
+    the default host-callback loop (TorchAllReduce: torch's all_reduce on the exchange buffer between trials) and the
+    opt-in device-steered loop (the RCCL communicator distributed.rccl_comm sets up from the group) both take
+    pba_solve's trajectory."""
+    import socket
+
+    import torch.multiprocessing as mp
+
+    import dist_workers
+    case = dict(kind=0, n_frames=16, n_points=400, seed=83, huber=9.0, fixed=[0, 1], iters=10, backend="nccl",
+                comm=False if comm == "callback" else None)
+    pb = synth.make_problem(kind=0, n_frames=16, n_points=400, width=376, height=240, seed=83, border=12,
+                            obs_sigma=0.3)
+    pb.poses[:2] = pb.poses_gt[:2]
+    with engine_for(pb, 9.0, (0, 1)) as full:
+        ref = full.solve(max_iterations=10)
+        poses_ref, rho_ref = full.get_state()
+    sk = socket.socket()
+    sk.bind(("127.0.0.1", 0))
+    port = sk.getsockname()[1]
+    sk.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=dist_workers.solve_worker, args=(0, 1, port, case, q))
+    p.start()
+    try:
+        r, v = q.get(timeout=240)
+    finally:
+        p.join(timeout=60)
+        if p.is_alive():
+            p.kill()
+    assert isinstance(v, dict), v
+    s = v["summary"]
+    assert s["iterations"] == ref["iterations"] and s["successful_steps"] == ref["successful_steps"], (s, ref)
+    assert abs(s["final_cost"] - ref["final_cost"]) <= 1e-6 * ref["final_cost"], (s, ref)
+    np.testing.assert_allclose(v["poses"], poses_ref, atol=1e-6)
+    np.testing.assert_allclose(v["rho"], rho_ref, rtol=1e-6)
+
+
 def test_band_too_small_is_rejected():
     import torch
     pb = synth.make_problem(kind="geometric", n_frames=12, n_points=60, seed=5)
