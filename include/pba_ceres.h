@@ -321,8 +321,12 @@ class GpuEvaluator : public ceres::EvaluationCallback {
   bool have_point_ = false, have_jac_ = false;
 };
 
-// One pose block's global Jacobian (R×7 row-major) from the record's tangent rows J6 (stride 6).
-inline void pose_jacobian_7(const GpuEvaluator& ev, int frame, const float* j6, int R, double* out) {
+// One pose block's global Jacobian (R×7 row-major) from the record's tangent rows J6 (stride 6).  P⁺ (6×7) has two
+// non-zero blocks — the υ rows touch only the translation columns, the ω rows only the quaternion columns
+// (se3_plus_jacobian_pinv) — so J7 = J6·P⁺ is a 3×4 and a 3×3 product per row: the same sums as the full 6×7 product,
+// whose other terms are exact zeros, in half the multiply-adds.
+template <int R>
+inline void pose_jacobian_7(const GpuEvaluator& ev, int frame, const float* j6, double* out) {
   if (ev.pose_jacobian() == PoseJacobian::kTangent) {
     for (int k = 0; k < R; ++k) {
       for (int c = 0; c < 6; ++c) out[k * 7 + c] = j6[6 * k + c];
@@ -330,22 +334,26 @@ inline void pose_jacobian_7(const GpuEvaluator& ev, int frame, const float* j6, 
     }
     return;
   }
-  const double* M = ev.pose_pinv(frame);  // J7 = J6·P⁺
+  const double* M = ev.pose_pinv(frame);
+  double mq[12], mt[9];  // ω rows × q columns, υ rows × t columns
+  for (int c = 0; c < 3; ++c) {
+    for (int g = 0; g < 4; ++g) mq[4 * c + g] = M[(3 + c) * 7 + g];
+    for (int g = 0; g < 3; ++g) mt[3 * c + g] = M[c * 7 + 4 + g];
+  }
   for (int k = 0; k < R; ++k) {
-    double row[6];
-    for (int c = 0; c < 6; ++c) row[c] = j6[6 * k + c];
-    for (int g = 0; g < 7; ++g) {
-      double v = 0.0;
-      for (int c = 0; c < 6; ++c) v += row[c] * M[c * 7 + g];
-      out[k * 7 + g] = v;
-    }
+    const float* a = j6 + 6 * k;
+    const double a0 = a[0], a1 = a[1], a2 = a[2], a3 = a[3], a4 = a[4], a5 = a[5];
+    double* o = out + 7 * k;
+    for (int g = 0; g < 4; ++g) o[g] = a3 * mq[g] + a4 * mq[4 + g] + a5 * mq[8 + g];
+    for (int g = 0; g < 3; ++g) o[4 + g] = a0 * mt[g] + a1 * mt[3 + g] + a2 * mt[6 + g];
   }
 }
 
 // Copy one block's record into Ceres' buffers.  Parameter blocks: T_w_host[7], T_w_target[7], ρ[1], and — for the
 // geometric functor's signature (reprojection.h:83-86) — the target intrinsics[8] (n_intr = 8).
-inline bool copy_block(const GpuEvaluator& ev, int block, int host, int target, int R, double* residuals,
-                       double** jacobians, int n_intr) {
+template <int R>
+inline bool copy_block(const GpuEvaluator& ev, int block, int host, int target, double* residuals, double** jacobians,
+                       int n_intr) {
   ev.wait(block);
   if (!ev.valid(block)) return false;
   const float* res = ev.residuals(block);
@@ -357,8 +365,8 @@ inline bool copy_block(const GpuEvaluator& ev, int block, int host, int target, 
     return false;
   }
   const float* rec = ev.record(block);
-  if (jacobians[0]) pose_jacobian_7(ev, host, rec + R, R, jacobians[0]);
-  if (jacobians[1]) pose_jacobian_7(ev, target, rec + 7 * R, R, jacobians[1]);
+  if (jacobians[0]) pose_jacobian_7<R>(ev, host, rec + R, jacobians[0]);
+  if (jacobians[1]) pose_jacobian_7<R>(ev, target, rec + 7 * R, jacobians[1]);
   if (jacobians[2])
     for (int k = 0; k < R; ++k) jacobians[2][k] = rec[13 * R + k];
   if (n_intr && jacobians[3])  // ∂r/∂sIntr_c2, the record's tail (pba_set_optimize_intrinsics)
@@ -373,7 +381,7 @@ class GpuPhotometricCost : public ceres::SizedCostFunction<P, 7, 7, 1> {
   GpuPhotometricCost(const GpuEvaluator* ev, int block, int host, int target)
       : ev_(ev), block_(block), host_(host), target_(target) {}
   bool Evaluate(double const* const* /*parameters*/, double* residuals, double** jacobians) const override {
-    return copy_block(*ev_, block_, host_, target_, P, residuals, jacobians, 0);
+    return copy_block<P>(*ev_, block_, host_, target_, residuals, jacobians, 0);
   }
 
  private:
@@ -388,7 +396,7 @@ class GpuReprojectionCost : public ceres::SizedCostFunction<2, 7, 7, 1, 8> {
   GpuReprojectionCost(const GpuEvaluator* ev, int block, int host, int target)
       : ev_(ev), block_(block), host_(host), target_(target) {}
   bool Evaluate(double const* const* /*parameters*/, double* residuals, double** jacobians) const override {
-    return copy_block(*ev_, block_, host_, target_, 2, residuals, jacobians, 8);
+    return copy_block<2>(*ev_, block_, host_, target_, residuals, jacobians, 8);
   }
 
  private:
