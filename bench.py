@@ -628,7 +628,8 @@ def main():
                 "keyframes": F, "points": Np, "patch": pb.P, "targets_per_point": K,
                 "blocks_total": total_blocks, "blocks_rank0": pb.n_blocks, "valid_blocks_rank0": int(valid.sum()),
                 "parallelism": f"host-keyframe shards x{world} (evaluation: no data-path collective; "
-                               f"GN: RCCL all-reduce of the reduced camera system)",
+                               f"GN: all-reduce of the reduced camera system, "
+                               f"{'device-steered RCCL loop' if os.environ.get('PBA_BENCH_GN_COMM') == '1' else 'torch.distributed between trials'})",
             },
             "roofline": {
                 "bound": "hbm",
