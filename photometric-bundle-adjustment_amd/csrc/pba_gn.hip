@@ -52,7 +52,10 @@ namespace {
 typedef double v4f64 __attribute__((ext_vector_type(4)));
 
 constexpr int NV = 104;          // normal-equation products per residual row
-constexpr int SCHUR_PTS = 128;   // points per Schur chunk
+#ifndef PBA_SCHUR_PTS
+#define PBA_SCHUR_PTS 128
+#endif
+constexpr int SCHUR_PTS = PBA_SCHUR_PTS;   // points per Schur chunk (-DPBA_SCHUR_PTS: A/B builds)
 constexpr int SCHUR_W = 2048;    // points × local poses per Schur chunk (LDS budget: dynamic, 24 B each)
 constexpr int SLOT_LIN_BASE = 42;  // H_hh(36) + g_h(6)
 constexpr int SLOT_LIN_T = 78;     // H_ht(36) + H_tt(36) + g_t(6)
