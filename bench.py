@@ -42,14 +42,14 @@ D = importlib.import_module("photometric-bundle-adjustment_amd.distributed")
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 
 
-def algorithmic_bytes_per_block(P: int, K: int, n_frames: int, n_points: int, n_blocks: int) -> float:
+def algorithmic_bytes_per_block(P: int, K: int, n_frames: int, n_points: int, n_blocks: int, value_bytes: int = 4) -> float:
     """SURVEY.md §8d, Ceres mode, fp32 records, fused state (pba_evaluate_state_device): inputs + taps + outputs
     per block (formula in DESIGN.md §3)."""
     idx = 16.0                                 # block record {point, host, target, cameras} (int32 × 4)
     point = (16.0 + 8.0 + 4.0 * P) / K         # u_ref (2×f64) + ρ (f64) + I_h (P×f32), shared by the point's K blocks
     state = (56.0 * 2 * n_frames + 8.0 * n_points) / n_blocks  # pose reads (L2-shared) + adopted state written
     taps = 4.0 * P                             # 4 u8 bilinear taps per pixel (gradient from the same taps)
-    out = 4.0 * 14 * P + 4.0 + 1.0             # record [r | J_h | J_t | J_ρ] + cost + valid
+    out = value_bytes * 14.0 * P + 4.0 + 1.0   # record [r | J_h | J_t | J_ρ] (fp32, or fp16 for C5) + cost + valid
     return idx + point + state + taps + out
 
 
@@ -378,8 +378,11 @@ def c5_eval(pb, images, states, steps, warmup, clock_warmup_s, torch, dev_index,
     finally:
         eng.close()
     P = DISK21.shape[0]
+    bpb = algorithmic_bytes_per_block(P, pb.n_blocks // max(pb.n_points, 1), pb.n_frames, pb.n_points, pb.n_blocks, 2)
+    gbs = bpb * pb.n_blocks / (kern_us * 1e-6) / 1e9
     return {"config": f"C5-style: the C4 problem with a {P}-px pattern, fp16 records, 3-level pyramid (synthetic images)",
             "blocks_per_s": pb.n_blocks * steps / el, "ms_per_step": 1e3 * el / steps, "kernel_avg_us": kern_us,
+            "bytes_per_block_alg": bpb, "achieved_gbs": gbs, "hbm_frac": gbs / HBM_PEAK_GBS,
             "record_format": "f16", "P": P, "record_bytes_per_block": 2 * 14 * P, "pyramid_levels": 3,
             "pyramid_build_ms": pyr_ms}
 
