@@ -37,6 +37,7 @@
 #include <map>
 #include <numeric>
 #include <string>
+#include <thread>
 #include <utility>
 #include <vector>
 
@@ -104,6 +105,15 @@ enum : int {
   kLmInvalid = 14, kLmStepNorm = 15, kLmGradNorm = 16, kLmFields = 17
 };
 enum : int { kDoneFunction = 1, kDoneInvalid = 2, kDoneParameter = 3, kDoneGradient = 4, kDoneRadius = 5 };
+// The published copies of the record (host-coherent page-locked memory): a ring of kRecRing slots of kLmFields fields
+// + the trial's sequence number, trial `seq` in slot seq mod kRecRing.  The host enqueues one trial ahead of the record
+// it waits for, so two records can be in flight; with a single slot, a host thread descheduled for longer than a trial
+// (~0.23 ms at C4) would find the next trial's record over the one it waits for and fail the solve.
+#ifndef PBA_REC_RING
+#define PBA_REC_RING 4
+#endif
+constexpr int kRecRing = PBA_REC_RING, kRecStride = kLmFields + 1;  // (-DPBA_REC_RING=1: the one-slot record, tests)
+__host__ __device__ inline long long rec_slot(double seq) { return ((long long)seq % kRecRing) * kRecStride; }
 // The kernels always get a record: the device loop's, or — host-driven steps — GnData::lm_idle (not done, set 0, λ NaN
 // = use the kernel's λ argument).  They read it with their first loads, never behind a branch of its own (a gate
 // read before anything else cost the linearisation ~8 µs of serialised scalar round trips).
@@ -3466,7 +3476,7 @@ int gn_prepare(pba_engine* e) {
     PBA_HIP(G.lm_idle.upload(idle, st));
   }
   // decision record + sequence number, written by lm_decide_kernel over the bus (fine-grained host memory)
-  PBA_HIP(G.lm_h.resize(kLmFields + 1, hipHostMallocCoherent | hipHostMallocMapped));
+  PBA_HIP(G.lm_h.resize(kRecRing * kRecStride, hipHostMallocCoherent | hipHostMallocMapped));
   PBA_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&G.lm_host_d), G.lm_h.p, 0));
   PBA_HIP(hipMemsetAsync(G.drho.p, 0, sizeof(double) * e->n_points, st));
   PBA_HIP(hipStreamSynchronize(st));
@@ -3850,7 +3860,7 @@ double now_ms();
 constexpr double kDecisionTimeoutMs = 60000.0;  // one trial takes ~0.25 ms at C4
 
 int wait_decision(pba_engine* e, double seq, double* d) {
-  volatile double* r = e->gn.lm_h.p;
+  volatile double* r = e->gn.lm_h.p + rec_slot(seq);
   // the stream is queried only after 2 ms without the record (a trial takes ~0.23 ms at C4), then every 2 ms: a
   // hipStreamQuery every few hundred spins idled the GPU 5.7 µs before every trial's first kernel
   // (profiles/r2_gn_trial_trace_v7.txt → v9)
@@ -3893,7 +3903,7 @@ int lm_trial(pba_engine* e, const DecideOpts& dopt, double seq, const hipEvent_t
   if (int rc = linearize(e, nullptr, G.lm.p, G.pairs_new.p, G.rho_new.p, G.red.p + 2 * (gp + gq), nullptr, true)) return rc;
   if (ev) PBA_HIP(hipEventRecord(ev[2], e->stream));
   lm_decide_kernel<<<1, kDecideThreads, 0, e->stream>>>(G.red.p, G.red2.p, G.gmax.p, gp, gq, G.n_chunks, G.status.p,
-                                                        dopt, G.lm.p, G.lm_host_d, seq);
+                                                        dopt, G.lm.p, G.lm_host_d + rec_slot(seq), seq);
   PBA_HIP(hipGetLastError());
   if (ev) PBA_HIP(hipEventRecord(ev[3], e->stream));
   return PBA_OK;  // an accepted candidate becomes the state in the next trial's schur_kernel (or after the loop)
@@ -4222,7 +4232,10 @@ int lm_loop_single(pba_engine* e, const pba_solver_options* o, pba_solver_summar
   lm_init_kernel<<<1, kDecideThreads, 0, e->stream>>>(G.red.p, G.n_chunks, opt.initial_trust_region_radius, G.lm.p,
                                                        G.lm_init.p);
   PBA_HIP(hipGetLastError());
-  G.lm_h[kLmFields] = 0.0;  // no trial published yet
+  for (int r = 0; r < kRecRing; ++r) G.lm_h[r * kRecStride + kLmFields] = 0.0;  // no trial published yet
+  // PBA_LM_HOST_DELAY_US (tests): the host thread sleeps this long before each wait, as a descheduled thread would
+  const char* dly = std::getenv("PBA_LM_HOST_DELAY_US");
+  const int delay_us = dly ? std::atoi(dly) : 0;
   const int n = std::max(0, opt.max_iterations);
   const DecideOpts dopt = decide_opts(opt);
   auto enqueue = [&](int i) { return lm_trial(e, dopt, (double)(i + 1), timed ? events.ev + 4 * (i & 1) : nullptr); };
@@ -4234,6 +4247,7 @@ int lm_loop_single(pba_engine* e, const pba_solver_options* o, pba_solver_summar
   for (; iter < n; ++iter) {
     if (iter + 1 < n)
       if (int rc = enqueue(iter + 1)) return rc;  // ahead of this trial's decision
+    if (delay_us > 0) std::this_thread::sleep_for(std::chrono::microseconds(delay_us));
     double d[kLmFields];
     if (int rc = wait_decision(e, (double)(iter + 1), d)) return rc;
     set = (int)d[kLmSet];
@@ -4316,7 +4330,8 @@ int dist_trial(pba_engine* e, const Collective& coll, const DecideOpts& dopt, do
                                                          G.lm.p, G.status.p, coll.rank0(e), G.tpose.p, Y);
   PBA_HIP(hipGetLastError());
   if (int rc = coll.allreduce(e, Y, kExScalars)) return rc;
-  dist_decide_kernel<<<1, 64, 0, e->stream>>>(Y, G.tpose.p, coll.rank0(e) < 0 ? 1 : 0, dopt, G.lm.p, G.lm_host_d, seq);
+  dist_decide_kernel<<<1, 64, 0, e->stream>>>(Y, G.tpose.p, coll.rank0(e) < 0 ? 1 : 0, dopt, G.lm.p,
+                                              G.lm_host_d + rec_slot(seq), seq);
   PBA_HIP(hipGetLastError());
   return PBA_OK;
 }
@@ -4350,7 +4365,7 @@ int lm_loop(pba_engine* e, const pba_solver_options* o, const Collective* coll, 
   }
   s.linearize_ms = now_ms() - t0;
   s.initial_cost = cost;
-  for (int i = 0; i <= kLmFields; ++i) G.lm_h[i] = 0.0;
+  for (int i = 0; i < kRecRing * kRecStride; ++i) G.lm_h[i] = 0.0;  // (slot 0 stages the initial record below)
   G.lm_h[kLmCost] = cost;
   G.lm_h[kLmValid] = n_valid;
   G.lm_h[kLmXNorm] = -1.0;

@@ -305,6 +305,24 @@ def test_gn_step_and_solve_are_reproducible(solver, monkeypatch):
             assert np.array_equal(a, b)
 
 
+def test_solve_survives_a_slow_host_thread(monkeypatch):
+    """The device-steered LM loop publishes each trial's decision record while the host already has the next trial
+    enqueued.  A host thread that sleeps longer than a trial before each wait (PBA_LM_HOST_DELAY_US, as a descheduled
+    thread would) must still read every trial's own record — the records go to a ring of slots by sequence number; with
+    one slot the next trial's record overwrote the awaited one and the solve failed.  Same trajectory as without."""
+    pb = synth.make_problem(n_frames=40, n_points=2000, texture="noise", seed=44, pose_sigma=5e-4, rho_sigma=5e-3)
+    with make_engine(pb, 9.0, (0, 1)) as eng:
+        ref = eng.solve(max_iterations=6, function_tolerance=0.0)
+        ref_state = eng.get_state()
+    monkeypatch.setenv("PBA_LM_HOST_DELAY_US", "3000")  # ≫ one trial at this size
+    with make_engine(pb, 9.0, (0, 1)) as eng:
+        s = eng.solve(max_iterations=6, function_tolerance=0.0)
+        state = eng.get_state()
+    for k in ("iterations", "successful_steps", "unsuccessful_steps", "final_cost"):
+        assert s[k] == ref[k], (k, s, ref)
+    assert all(np.array_equal(a, b) for a, b in zip(state, ref_state))
+
+
 @pytest.mark.parametrize("solver", ["cr", "band", "skyline"])
 @pytest.mark.parametrize("n_frames", [12, 13, 6, 37])
 def test_reduced_solvers_agree(solver, n_frames, monkeypatch):
