@@ -353,7 +353,7 @@ def gn_c3(iters, torch, dev_index, dev):
 DISK21 = np.array([(dx, dy) for dy in range(-2, 3) for dx in range(-2, 3) if dx * dx + dy * dy <= 5], np.float32)
 
 
-def c5_eval(pb, images, states, steps, warmup, clock_warmup_s, torch, dev_index, dev):
+def c5_eval(pb, images, states, steps, warmup, clock_warmup_s, torch, dev_index, dev, gn_iterations=0):
     """BASELINE.json configs[4] (C5) on the C4 problem: 21-pixel pattern (the radius-√5 disk), records stored as
     fp16 (PBA_RECORD_F16), and a 3-level image pyramid built on the device.  Same one-launch step and the same clock
     warm-up / warmup count as the headline; the full EuRoC sequence is not in the container, so the images are the
@@ -375,6 +375,18 @@ def c5_eval(pb, images, states, steps, warmup, clock_warmup_s, torch, dev_index,
         eng.synchronize()
         pyr_ms = 1e3 * (time.perf_counter() - t0)
         el, kern_us, _ = time_evaluation(eng, states, steps, warmup, clock_warmup_s, torch, None, dev)
+        gn = None
+        if gn_iterations > 0:
+            # on-device GN at the 21-px pattern (the finest level; BASELINE C5's "fp32 jacobian accumulate": the rows go
+            # through the fp32 matrix cores into JᵀJ, nothing is stored): the LM loop as in the C4 GN leg
+            eng.set_fixed_frames(np.array([0, 1], np.int32))
+            eng.set_state(pb5.poses, pb5.rho)
+            eng.gn_linearize()
+            eng.solve(max_iterations=1)  # warm-up
+            torch.cuda.synchronize()
+            sg = eng.solve(max_iterations=gn_iterations, function_tolerance=0.0)
+            gn = {"ms_per_iteration": sg["total_ms"] / max(sg["iterations"], 1), "iterations": sg["iterations"],
+                  "accepted": sg["successful_steps"]}
     finally:
         eng.close()
     P = DISK21.shape[0]
@@ -384,7 +396,7 @@ def c5_eval(pb, images, states, steps, warmup, clock_warmup_s, torch, dev_index,
             "blocks_per_s": pb.n_blocks * steps / el, "ms_per_step": 1e3 * el / steps, "kernel_avg_us": kern_us,
             "bytes_per_block_alg": bpb, "achieved_gbs": gbs, "hbm_frac": gbs / HBM_PEAK_GBS,
             "record_format": "f16", "P": P, "record_bytes_per_block": 2 * 14 * P, "pyramid_levels": 3,
-            "pyramid_build_ms": pyr_ms}
+            "pyramid_build_ms": pyr_ms, "gn": gn}
 
 
 HEADLINE_KERNEL = "photometric_block_kernel<0, 8, 1, float>"
@@ -574,7 +586,8 @@ def main():
         c3 = gn_c3(args.gn_iterations, torch, dev_index, dev)
     c5 = None
     if world == 1 and not args.no_c5:
-        c5 = c5_eval(full, images, states, args.steps, args.warmup, args.clock_warmup_s, torch, dev_index, dev)
+        c5 = c5_eval(full, images, states, args.steps, args.warmup, args.clock_warmup_s, torch, dev_index, dev,
+                     args.gn_iterations)
 
     if rank == 0:
         total_blocks = pb.n_blocks * world

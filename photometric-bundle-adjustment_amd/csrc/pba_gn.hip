@@ -343,6 +343,183 @@ void linearize_kernel(const KernelArgs a, const LinArgs g) {
   }
 }
 
+// Patterns of 9…32 pixels (C5: 21 px): 8 lanes per block as in the evaluation kernel (photometric_block_kernel_multi),
+// lane k evaluating pixels k, k+8, … (PPL rows, one pass each), so a chunk holds 32 blocks as at 8 px — the same chunk
+// partials — instead of 8 blocks of 32 lanes (at 21 px a third of those lanes idle, and four times the chunks for the
+// assembly and the decision to sum).  The block's Huber weight needs all of its rows, so each pass's rows go through
+// the matrix cores unweighted into per-block accumulators (x̃ᵀx̃ = w·xᵀx) and the weight scales them once known; rows
+// that are not active or not ok are zero (an invalid block's products then scale by 0).  LDS per wave: the tile blocks
+// and the pass's 64 rows side by side (the rows no longer overwrite the tile), then the product sets over both.
+#ifndef PBA_LINROWS_WAVES
+#define PBA_LINROWS_WAVES 5  // 96 VGPRs (a few spilled): 150 against 161 µs at 4 waves (C5 pattern, C4 problem)
+#endif
+template <int MODEL, int PPL>
+__global__ __launch_bounds__(kBlockThreads) __attribute__((amdgpu_waves_per_eu(PBA_LINROWS_WAVES, 8)))
+void linearize_rows_kernel(const KernelArgs a, const LinArgs g) {
+  constexpr int LPB = 8, BW = 64 / LPB, NW = kBlockThreads / 64, SPB = LPB / 4, NVP = 108;
+  constexpr int kTileW = BW * (int)sizeof(TileBlock), kRowsW = 64 * 16 * 4, kProdW = BW * NVP * 4;
+  constexpr int kArena = kTileW + kRowsW;
+  static_assert(kProdW <= kArena, "product sets fit the arena");
+  __shared__ __attribute__((aligned(16))) unsigned char arena[NW][kArena];
+  __shared__ int s_wlo[NW], s_wn[NW];
+  __shared__ float s_bc[kBlockThreads / LPB];
+  __shared__ float2 s_pat[LPB * PPL];
+  const int chunk = logical_tile();
+  if (chunk >= g.n_chunks) return;
+  const int4 d = g.chunk_desc[chunk];
+  const LmView lv = lm_view(g.lm);
+  if (lv.done != 0.0) return;
+  const bool s1 = (lv.set != 0.0) != g.spare;
+  float* const blk_schur = s1 ? g.blk_schur1 : g.blk_schur;
+  float* const part_lin = s1 ? g.part_lin1 : g.part_lin;
+  const int count = d.y, n_t = d.z, poff = d.w;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int lb = threadIdx.x / LPB, k = threadIdx.x % LPB, wb = lb % BW;
+  const bool live = lb < count;
+  const int R = a.P;
+  if ((int)threadIdx.x < LPB * PPL) s_pat[threadIdx.x] = pattern_at<LPB * PPL>(a, threadIdx.x);
+  const int4 lr = g.lin_rec[(long long)chunk * (kBlockThreads / LPB) + lb];
+  const int blk = lr.x, gpos = lr.w, lt = (int)((unsigned)lr.z >> 24);
+  TileBlock* s_tb = reinterpret_cast<TileBlock*>(arena[wave]);
+  const int pt = stage_tile_pp<LPB>(a, s_tb, wb, k, make_int2(lr.y, lr.z & 0xffffff));
+  float Ih[PPL];
+#pragma unroll
+  for (int j = 0; j < PPL; ++j) {
+    const int px = k + LPB * j;
+    Ih[j] = live && px < R ? a.host_int[(long long)pt * R + px] : 0.0f;
+  }
+  __syncthreads();
+  float* sX = reinterpret_cast<float*>(arena[wave] + kTileW);  // the pass's 64 rows × 16 floats
+  const int ci = lane & 15, kq = lane >> 4;
+  f32x4 accb[BW];
+#pragma unroll
+  for (int b = 0; b < BW; ++b) accb[b] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+  int okl = 1;
+  float s = 0.0f;
+#pragma unroll 1
+  for (int j = 0; j < PPL; ++j) {
+    const int px = k + LPB * j;
+    const bool act = live && px < R;
+    float ih = Ih[0];
+#pragma unroll
+    for (int q = 1; q < PPL; ++q) ih = j == q ? Ih[q] : ih;
+    asm volatile("" ::: "memory");  // the tile is read from LDS per pass (see photometric_block_kernel_multi)
+    const Row row = photometric_row<MODEL, true>(a, s_tb[wb], s_pat[act ? px : 0], ih);
+    const bool use = act && row.ok;
+    okl &= act ? row.ok : 1;
+    s += use ? row.r * row.r : 0.0f;
+    auto xv = [&](float v) { return use ? v : 0.0f; };  // selects: a row that is not ok may hold inf / NaN
+    float4* xr = reinterpret_cast<float4*>(sX + lane * 16);
+    xr[0] = make_float4(xv(row.hv.x), xv(row.hv.y), xv(row.hv.z), xv(row.hw.x));
+    xr[1] = make_float4(xv(row.hw.y), xv(row.hw.z), xv(row.tv.x), xv(row.tv.y));
+    xr[2] = make_float4(xv(row.tv.z), xv(row.tw.x), xv(row.tw.y), xv(row.tw.z));
+    xr[3] = make_float4(xv(row.jr), xv(row.r), 0.0f, 0.0f);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    float op[BW * SPB];
+#pragma unroll
+    for (int st = 0; st < BW * SPB; ++st) op[st] = sX[(4 * st + kq) * 16 + ci];
+#pragma unroll
+    for (int b = 0; b < BW; ++b)
+#pragma unroll
+      for (int st = 0; st < SPB; ++st)
+        accb[b] = __builtin_amdgcn_mfma_f32_16x16x4f32(op[b * SPB + st], op[b * SPB + st], accb[b], 0, 0, 0);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // this pass's reads before the next pass's row stores
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+  const int ok = group_all<LPB>(okl);
+  s = group_sum<LPB>(s);
+  const float w = ok ? huber_weight(s, a.huber) : 0.0f;
+  const float bcost = ok ? huber_cost(s, a.huber) : 0.0f;
+  if (k == 0) s_bc[lb] = live && ok ? bcost : -1.0f;  // read after the barrier below
+  const unsigned slots = kSlotTable.w[lane];
+  {
+    // as linearize_kernel: per block its (now weighted) products — row 12 the point-elimination data at its GN
+    // position — added to its target run's sum, each run's 16×16 result scattered once as the 104 products
+    float* sP = reinterpret_cast<float*>(arena[wave]);  // over the tile and the rows (both consumed)
+    const int nbw = min(max(count - wave * BW, 0), BW);
+    const int lo = __builtin_amdgcn_readfirstlane(lt);
+    auto flush = [&](const f32x4& acc, int slot) {
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+        const unsigned v = (slots >> (8 * m)) & 255u;
+        if (v < (unsigned)NV) sP[slot * NVP + v] = acc[m];
+      }
+    };
+    const int pc = lane - 48, pq = pc < 12 ? pc + 2 : (pc < 14 ? pc - 12 : pc);
+    f32x4 tacc = {0.0f, 0.0f, 0.0f, 0.0f};
+    int cur = lo;
+#pragma unroll
+    for (int b = 0; b < BW; ++b) {
+      if (b < nbw) {
+        const float wb_ = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(w), b * LPB));
+        const f32x4 acc = accb[b] * wb_;
+        const int gpb = __builtin_amdgcn_readlane(gpos, b * LPB);
+        if (pc >= 0) blk_schur[(long long)gpb * 16 + pq] = acc[0];
+        const int ltb = __builtin_amdgcn_readlane(lt, b * LPB);
+        if (ltb != cur) {
+          flush(tacc, cur - lo);
+          tacc = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+          cur = ltb;
+        }
+        tacc += acc;
+      }
+    }
+    if (nbw > 0) flush(tacc, cur - lo);
+    if (lane == 0) {
+      s_wlo[wave] = lo;
+      s_wn[wave] = nbw > 0 ? cur - lo + 1 : 0;
+    }
+  }
+  __syncthreads();
+  auto sset = [&](int w_, int i, int v) -> float { return reinterpret_cast<const float*>(arena[w_])[i * NVP + v]; };
+  const int nout = SLOT_LIN_BASE + SLOT_LIN_T * n_t;
+  for (int o = threadIdx.x; o < nout; o += kBlockThreads) {
+    int v, jt = -1;
+    if (o < 36) {
+      const int r = o / 6, c = o % 6;
+      v = upper_index(min(r, c), max(r, c));
+    } else if (o < 42) {
+      v = 78 + (o - 36);
+    } else {
+      jt = (o - 42) / SLOT_LIN_T;
+      const int q = (o - 42) % SLOT_LIN_T;
+      if (q < 36) v = 21 + q;
+      else if (q < 72) { const int r = (q - 36) / 6, c = (q - 36) % 6; v = 57 + upper_index(min(r, c), max(r, c)); }
+      else v = 84 + (q - 72);
+    }
+    float acc = 0.0f;
+#pragma unroll
+    for (int w_ = 0; w_ < NW; ++w_) {
+      const int wl = s_wlo[w_], wn = s_wn[w_];
+      if (jt < 0) {
+        for (int i = 0; i < wn; ++i) acc += sset(w_, i, v);
+      } else if (jt >= wl && jt < wl + wn) {
+        acc += sset(w_, jt - wl, v);
+      }
+    }
+    part_lin[(long long)poff + o] = acc;
+  }
+  if (live && k == 0) {
+    a.valid[blk] = (uint8_t)ok;
+    a.cost[blk] = bcost;
+  }
+  if (g.wg_red && wave == 0) {
+    const float x = lane < count ? s_bc[lane] : -1.0f;
+    double c = x >= 0.0f ? (double)x : 0.0, vv = x >= 0.0f ? 1.0 : 0.0;
+    for (int m = 32; m >= 1; m >>= 1) {
+      c += __shfl_xor(c, m, 64);
+      vv += __shfl_xor(vv, m, 64);
+    }
+    if (lane == 0) {
+      g.wg_red[2 * chunk] = c;
+      g.wg_red[2 * chunk + 1] = vv;
+    }
+  }
+}
+
 struct SchurArgs {
   const int4* desc;       // first GN point, n points, n local poses, partial offset (doubles)
   const int4* aux;        // pair list offset, n pairs, first GN block, n blocks (the last two: diagnostics)
@@ -3031,10 +3208,9 @@ __global__ void lm_accept_kernel(const double* __restrict__ lm, const double* __
 // ------------------------------------------------------------------------------------------------
 // host side
 // ------------------------------------------------------------------------------------------------
-int gn_lpb(const pba_engine* e) {
-  if (e->opt.residual_kind == PBA_RESIDUAL_GEOMETRIC) return 4;
-  return e->P <= 8 ? 8 : (e->P <= 16 ? 16 : 32);
-}
+int gn_lpb(const pba_engine* e) { return e->opt.residual_kind == PBA_RESIDUAL_GEOMETRIC ? 4 : 8; }
+// rows per lane of the linearisation: 1 up to 8 px (one lane per row), ⌈P/8⌉ above (linearize_rows_kernel)
+int gn_ppl(const pba_engine* e) { return e->opt.residual_kind == PBA_RESIDUAL_GEOMETRIC ? 1 : (e->P + 7) / 8; }
 
 int band_kernel_for(int band) { return band <= 4 ? 4 : (band <= 8 ? 8 : (band <= 16 ? 16 : 0)); }
 
@@ -3119,6 +3295,7 @@ int gn_prepare(pba_engine* e) {
   const int nb = e->n_blocks, nf = e->n_frames;
   if (nb <= 0) return fail(PBA_ERR_NOT_READY, "pba_set_blocks first");
   G.lpb = gn_lpb(e);
+  G.ppl = gn_ppl(e);
   G.bpw = kBlockThreads / G.lpb;
   const std::vector<int>& ph = e->point_host_h;
   // GN order: (host, point, target)
@@ -3489,11 +3666,16 @@ int gn_prepare(pba_engine* e) {
 template <int KIND, int MODEL>  // photometric: MODEL = camera model + 4 · interpolator
 void launch_linearize(pba_engine* e, const KernelArgs& ka, const LinArgs& la) {
   const int grid = la.n_chunks;
-  switch (e->gn.lpb) {
-    case 4: linearize_kernel<KIND, MODEL, 4><<<grid, kBlockThreads, 0, e->stream>>>(ka, la); break;
-    case 8: linearize_kernel<KIND, MODEL, 8><<<grid, kBlockThreads, 0, e->stream>>>(ka, la); break;
-    case 16: linearize_kernel<KIND, MODEL, 16><<<grid, kBlockThreads, 0, e->stream>>>(ka, la); break;
-    default: linearize_kernel<KIND, MODEL, 32><<<grid, kBlockThreads, 0, e->stream>>>(ka, la); break;
+  if constexpr (KIND == PBA_RESIDUAL_PHOTOMETRIC) {
+    switch (e->gn.ppl) {  // 9…32 px: 8 lanes per block, ⌈P/8⌉ rows per lane
+      case 1: break;
+      case 2: linearize_rows_kernel<MODEL, 2><<<grid, kBlockThreads, 0, e->stream>>>(ka, la); return;
+      case 3: linearize_rows_kernel<MODEL, 3><<<grid, kBlockThreads, 0, e->stream>>>(ka, la); return;
+      default: linearize_rows_kernel<MODEL, 4><<<grid, kBlockThreads, 0, e->stream>>>(ka, la); return;
+    }
+    linearize_kernel<KIND, MODEL, 8><<<grid, kBlockThreads, 0, e->stream>>>(ka, la);
+  } else {
+    linearize_kernel<KIND, MODEL, 4><<<grid, kBlockThreads, 0, e->stream>>>(ka, la);
   }
 }
 

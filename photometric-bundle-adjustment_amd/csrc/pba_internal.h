@@ -690,7 +690,7 @@ struct CrLevelHost {
 // the device buffers of one linearisation / Schur complement / solve.  See pba_gn.hip for the layouts.
 struct GnData {
   bool prepared = false;
-  int lpb = 8, bpw = 32;
+  int lpb = 8, bpw = 32, ppl = 1;  // linearisation: lanes per block, blocks per chunk, rows per lane
   int n_chunks = 0, n_schur = 0, n_gn_points = 0, n_sky = 0, band = 0, band_kernel = 0, solver = 0;
   std::vector<CrLevelHost> cr_levels;  // block-cyclic-reduction level layout (offsets into cr_buf)
   int cr_pcr = -1;                     // the CR level whose rows parallel cyclic reduction solves (-1: root kernel)

@@ -9,7 +9,7 @@ i=0
 for v in "$@"; do
   i=$((i + 1))
   PBA_LIBRARY=$PWD/variants/libpba_$v.so timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv \
-      -d gpurun_out/abs_${v}_$i -o run -- python tools/gn_kernels.py --solve --iters 10 > gpurun_out/abs_${v}_$i.log 2>&1 \
+      -d gpurun_out/abs_${v}_$i -o run -- python tools/gn_kernels.py --solve --iters 10 ${GN_ARGS:-} > gpurun_out/abs_${v}_$i.log 2>&1 \
       || { echo "variant $v failed"; tail -5 gpurun_out/abs_${v}_$i.log; exit 1; }
   echo "== $v ($i): $(grep 'ms per' gpurun_out/abs_${v}_$i.log)"
   python3 tools/gn_trace.py gpurun_out/abs_${v}_$i/run_kernel_trace.csv | grep -v cr_level || exit 1

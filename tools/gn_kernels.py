@@ -22,11 +22,19 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--texture", default="noise")
     ap.add_argument("--solve", action="store_true", help="time pba_solve (the device-steered LM loop) instead")
+    ap.add_argument("--p21", action="store_true", help="the C5 pattern: the 21-px disk of radius √5 (bench.py DISK21)")
     args = ap.parse_args()
     import numpy as np
     import torch
     dev = torch.device("cuda", 0)
     pb, images = synth.c4_shard(dev, texture=args.texture)
+    if args.p21:
+        disk = np.array([(dx, dy) for dy in range(-2, 3) for dx in range(-2, 3) if dx * dx + dy * dy <= 5], np.float32)
+        host = torch.from_numpy(pb.point_host.astype(np.int64)).to(dev)[:, None]
+        uu = torch.from_numpy((pb.u_ref[:, 0][:, None] + disk[None, :, 0]).astype(np.int64)).to(dev)
+        vv = torch.from_numpy((pb.u_ref[:, 1][:, None] + disk[None, :, 1]).astype(np.int64)).to(dev)
+        pb.pattern = disk
+        pb.host_intensity = images[host, vv, uu].float().cpu().numpy()
     eng = E.Engine(synth.PHOTOMETRIC, synth.PINHOLE, device=0, huber_width=9.0)
     eng.set_problem(pb, images_device_ptr=images.data_ptr())
     eng.set_fixed_frames(np.array([0, 1], np.int32))
