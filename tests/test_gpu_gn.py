@@ -55,12 +55,16 @@ def test_reduced_system_and_step(kind, model, huber, lam):
     assert abs(model_dec - model_ref) <= 1e-3 * abs(model_ref) + 1e-9
 
 
-@pytest.mark.parametrize("P", [12, 21, 32])
-def test_reduced_system_large_patterns(P):
-    """Patterns beyond 8 px (the 16/32-lane linearisation and the multi-pixel candidate-cost kernel): reduced
+@pytest.mark.parametrize("P,pm", [(12, 0), (21, 0), (32, 0), (21, 1), (17, 2), (21, 3), (21, 6), (30, 5)])
+def test_reduced_system_large_patterns(P, pm):
+    """Patterns beyond 8 px (linearize_rows_kernel: 8 lanes per block, 2-4 rows per lane; the multi-pixel
+    candidate-cost kernel) for every camera model and both interpolators (pm = model + 4 · interpolator): reduced
     system, step and candidate cost against the dense reference, same tolerances as above."""
     pat = np.random.default_rng(P).integers(-3, 4, (P, 2)).astype(np.float32)
-    pb = synth.make_problem(n_frames=8, n_points=60, width=376, height=240, pattern=pat, seed=40 + P, border=12)
+    interp, model = pm >> 2, pm & 3
+    pb = synth.make_problem(model=model, n_frames=8, n_points=60, width=376, height=240, pattern=pat, seed=40 + P + pm,
+                            border=12)
+    pb.interp = interp
     fixed = (0,)
     lam = 1e-3
     H, g, cost = GR.linearize(pb, pb.poses, pb.rho, 9.0, fixed)
