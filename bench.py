@@ -8,18 +8,20 @@ block's residuals and tangent Jacobians (Ceres-mode records, include/pba.h) at a
 ONE launch (pba_evaluate_state_device — the blocks form their relative poses in the prologue and the launch adopts
 the state).
 
-Multi-GPU (torch.distributed.run, one rank per GPU): the evaluation partitions by host keyframe with no exchange step
-(SURVEY.md §8e), so the headline scales weakly — rank r evaluates host keyframes [r·1000, (r+1)·1000) of one
-N·1000-keyframe trajectory, a full C4-size shard (400k blocks) per GPU, with no data-path collective → `scaling: "weak"`,
-value = N × 400k blocks ÷ the max-over-ranks time.  The one C4 problem itself split N ways (strong scaling) is reported
-under "strong", and at N = 1 the step of a 1/8 shard under "shard8" (the strong-scaling ceiling at N = 8).  Timing: a
-clock warm-up, W warmup steps, then exactly K steps bracketed by barrier + synchronize.
+Multi-GPU (torch.distributed.run, one rank per GPU): BASELINE.json configs[3] is ONE 1000-keyframe problem sharded by
+host keyframe across the GPUs, so the headline scales strongly — rank r evaluates its host-keyframe shard of the one C4
+problem (distributed.shard_problem: contiguous host ranges balanced by block count), with no data-path collective (the
+evaluation has no exchange step) → `scaling: "strong"`, value = 400k blocks ÷ the max-over-ranks time of a
+step.  The weak form (every rank a full C4-size shard of an N·1000-keyframe trajectory) is reported under "weak", and at
+N = 1 the step of a 1/8 shard under "shard8" (the strong-scaling ceiling at N = 8).  Timing: a clock warm-up, W warmup
+steps, then exactly K steps bracketed by barrier + synchronize.
 
 Also reported: the block kernel's roofline position (algorithmic bytes ÷ HIP-event-timed kernel duration on the engine
 stream); the CPU baseline — the reference's CPU path, real Ceres 2.0.0 (built from the reference's vendored sources
 by oracle/ceres.mk) evaluating AutoDiff cost functions with its ProgramEvaluator on this host's cores, timed by its
 own "Jacobian & residual evaluation" timer on a bounded sample of the same workload; ms per LM iteration of the
-on-device Gauss-Newton (C4 here, C3 = configs[2] in "gn_c3"); and the C5-style 21-px / fp16 / pyramid leg.
+on-device Gauss-Newton (C4 on rendered images — the solve the GPU tests pin against real Ceres, whose trajectory on the
+same problem is reported beside it — and C3 = configs[2] in "gn_c3"); and the C5-style 21-px / fp16 / pyramid leg.
 """
 from __future__ import annotations
 
@@ -118,8 +120,9 @@ def c2_dropin(pb_c4, images_host, threads: int):
     pb.poses[:2] = pb.poses_gt[:2]
     out = {"config": f"C2: {pb.n_frames} keyframes of EuRoC V1 image content, {pb.n_blocks} blocks, 8-px pattern, "
                      f"double sphere, Huber 9, 10 LM iterations"}
-    # the plain adapter (no protocol checks: the tests run those), Ceres' own floor (constant CostFunctions in the same
-    # Problem), and the CPU AutoDiff path — same Solve options
+    # the plain adapter (no protocol checks: the tests run those), its floor (the same Solve replayed over the drop-in's
+    # recorded read-backs: Ceres' own work plus the adapter's per-block copy on the drop-in's own trajectory, i.e.
+    # everything but the device's part), and the CPU AutoDiff path — same Solve options
     # each mode twice, interleaved, the faster run of each reported (the box's host is shared: a 16-CPU cgroup quota)
     runs = {m: [] for m in ("gpu", "cpu", "floor")}
     for _ in range(2):
@@ -134,11 +137,21 @@ def c2_dropin(pb_c4, images_host, threads: int):
     out["speedup_jacobian_evaluation"] = out["cpu_autodiff"]["jacobian_evaluation_ms"] / out["gpu_dropin"]["jacobian_evaluation_ms"]
     out["speedup_residual_evaluation"] = out["cpu_autodiff"]["residual_evaluation_ms"] / out["gpu_dropin"]["residual_evaluation_ms"]
     out["jacobian_evaluation_vs_floor"] = out["gpu_dropin"]["jacobian_evaluation_ms"] / out["ceres_floor"]["jacobian_evaluation_ms"]
+    out["residual_evaluation_vs_floor"] = out["gpu_dropin"]["residual_evaluation_ms"] / out["ceres_floor"]["residual_evaluation_ms"]
     out["same_trajectory"] = bool(len(g["costs"]) == len(c["costs"]) and np.array_equal(g["step_ok"], c["step_ok"]))
+    out["floor_replay_ok"] = bool(all(r["replay_ok"] == 1 for r in runs["floor"]))
+    out["floor_same_evaluations"] = bool(fl["jacobian_evaluations"] == g["jacobian_evaluations"] and
+                                         fl["residual_evaluations"] == g["residual_evaluations"])
+    out["floor_note"] = ("ceres_floor: the same Solve over the same per-block CostFunctions, replaying the drop-in's "
+                         "recorded read-backs (records / residuals, validity, P+) — the drop-in's trajectory and evaluation "
+                         "counts with the device's part (state upload, launch, read-back) removed")
     sample = c4_sample(pb_c4, images_host)
     gs = CR.run("gpu", sample, iters=4, huber=9.0, threads=threads, ftol=0.0, check=False)
     fs = CR.run("floor", sample, iters=4, huber=9.0, threads=threads, ftol=0.0)
-    out["c4_sample"] = dict(per_call(gs), blocks=sample.n_blocks, ceres_floor=per_call(fs))
+    out["c4_sample"] = dict(per_call(gs), blocks=sample.n_blocks, ceres_floor=per_call(fs),
+                            jacobian_evaluation_vs_floor=(gs["jacobian_evaluation_s"] / max(gs["jacobian_evaluations"], 1)) /
+                            (fs["jacobian_evaluation_s"] / max(fs["jacobian_evaluations"], 1)),
+                            floor_replay_ok=bool(fs["replay_ok"] == 1))
     return out
 
 
@@ -265,16 +278,19 @@ def time_evaluation(eng, states, steps, warmup, clock_warmup_s, torch, dist, dev
     return float(t[0]), float(t[1]), host_diag
 
 
-def gn_benchmark(eng, iters, torch, dist, dev, world):
-    """ms per Levenberg-Marquardt iteration (BASELINE.json metric, part 2) on the same problem, through the
-    engine's own LM loop (pba_solve; pba_solve_distributed with an RCCL all-reduce of the banded reduced
-    system for N>1).  An iteration = Schur complement + reduced-system solve + candidate cost, plus the
-    next linearisation (r, J, Huber, JᵀJ/Jᵀr partials) after an accepted step; function_tolerance = 0 so
-    exactly `iters` iterations run.  Two keyframes are held constant (the reference's fixed cameras)."""
+def gn_benchmark(eng, pb, iters, torch, dist, dev, world, ceres_problem=None, threads=1):
+    """ms per Levenberg-Marquardt iteration (BASELINE.json metric, part 2) on the C4 problem with rendered images (the
+    problem test_c4_engine_lm_matches_ceres_cpu pins against real Ceres), through the engine's own LM loop (pba_solve;
+    pba_solve_distributed with an all-reduce of the banded reduced system for N>1).  An iteration = Schur complement +
+    reduced-system solve + candidate linearisation (its cost) + the decision; function_tolerance = 0 so exactly `iters`
+    iterations run.  Two keyframes are held constant (the reference's fixed cameras).  ceres_problem (N = 1): the same
+    problem with host images — real Ceres 2.0.0 LM over the AutoDiff functor runs the same 20 iterations on the CPU and its
+    trajectory is reported beside the engine's."""
     eng.set_fixed_frames(np.array([0, 1], np.int32))
     eng.gn_linearize()  # symbolic analysis (once per problem structure), outside the timed region
     opts = dict(max_iterations=iters, function_tolerance=0.0)
     agree = None
+    traj = None
     device_steered = world > 1 and dist.get_backend() == "nccl" and os.environ.get("PBA_BENCH_GN_COMM") == "1"
     if world > 1:
         band = D.global_band(eng, None, dev)
@@ -283,6 +299,7 @@ def gn_benchmark(eng, iters, torch, dist, dev, world):
         # (pba_solve_distributed_comm) — kept opt-in until a run with several GPUs has confirmed it.
         comm = None if device_steered else False
         D.solve_distributed(eng, device=dev, comm=comm, max_iterations=1)  # warm-up (sets the RCCL communicator up)
+        eng.set_state(pb.poses, pb.rho)
         dist.barrier()
         torch.cuda.synchronize()
         s = D.solve_distributed(eng, device=dev, comm=comm, **opts)
@@ -292,26 +309,52 @@ def gn_benchmark(eng, iters, torch, dist, dev, world):
                                           float(s["successful_steps"])], dev)
     else:
         eng.solve(max_iterations=1)  # warm-up
+        eng.set_state(pb.poses, pb.rho)
         torch.cuda.synchronize()
         s = eng.solve(**opts)
+        traj = eng.solver_iterations()
         exchange_mb = None
         # the per-phase breakdown comes from a second, event-instrumented solve (events idle the GPU a few µs each,
-        # so the timed solve above runs without them); same state sequence, so the same work per iteration
+        # so the timed solve above runs without them) from the same initial state: the same work per iteration
+        eng.set_state(pb.poses, pb.rho)
         eng.set_solver_timing(True)
         sb = eng.solve(**opts)
         eng.set_solver_timing(False)
         s = dict(s, linearize_ms=sb["linearize_ms"], solve_ms=sb["solve_ms"], cost_ms=sb["cost_ms"])
     t = all_reduce_max(torch, dist, [s["total_ms"], s["linearize_ms"], s["solve_ms"], s["cost_ms"]], dev)
     n = max(s["iterations"], 1)
-    return {"ms_per_iteration": float(t[0]) / n, "iterations": s["iterations"], "accepted": s["successful_steps"],
-            "breakdown_ms_per_iteration": {"linearize_ms": float(t[1]) / n, "step_ms": float(t[2]) / n,
-                                           "cost_ms": float(t[3]) / n},
-            "exchange_mb_per_iteration": exchange_mb, "ranks_agree": agree,
-            "note": "host wall clock of the engine's LM loop (pba_solve" + (
-                "_distributed_comm: the device-steered loop with two RCCL all-reduces per trial on the engine stream "
-                "(the banded reduced camera system, then 16 scalars)" if device_steered
-                else f"_distributed: {dist.get_backend()} all-reduces through a host callback" if world > 1 else "") +
-                    "); noise-textured images, so the steps are not expected to converge — timing only"}
+    out = {"ms_per_iteration": float(t[0]) / n, "iterations": s["iterations"], "accepted": s["successful_steps"],
+           "initial_cost": s["initial_cost"], "final_cost": s["final_cost"],
+           "breakdown_ms_per_iteration": {"linearize_ms": float(t[1]) / n, "step_ms": float(t[2]) / n,
+                                          "cost_ms": float(t[3]) / n},
+           "exchange_mb_per_iteration": exchange_mb, "ranks_agree": agree,
+           "note": "host wall clock of the engine's LM loop (pba_solve" + (
+               "_distributed_comm: the device-steered loop with two RCCL all-reduces per trial on the engine stream "
+               "(the banded reduced camera system, then 16 scalars)" if device_steered
+               else f"_distributed: {dist.get_backend()} all-reduces through a host callback" if world > 1 else "") +
+                   ") on the C4 problem with rendered images (one textured plane seen by every keyframe), from its "
+                   "perturbed initial state"}
+    if ceres_problem is not None and traj is not None:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import ceres_runner as CR
+        if CR.available():
+            t0 = time.perf_counter()
+            ref = CR.run("cpu", ceres_problem, iters=iters, huber=9.0, threads=threads, ftol=0.0, timeout=900)
+            m = min(len(traj["cost"]), len(ref["costs"]))
+            rel = np.abs(traj["cost"][:m] - ref["costs"][:m]) / np.abs(ref["costs"][:m])
+            out["ceres"] = {
+                "final_cost": ref["final_cost"], "successful_steps": ref["successful_steps"] - 1,
+                "unsuccessful_steps": ref["unsuccessful_steps"], "message": ref["message"],
+                "same_steps": bool(len(traj["cost"]) == len(ref["costs"]) and
+                                   np.array_equal(traj["step_is_successful"].astype(bool), ref["step_ok"])),
+                "max_rel_cost_difference_per_iteration": float(rel.max()),
+                "final_cost_rel_difference": abs(s["final_cost"] - ref["final_cost"]) / abs(ref["final_cost"]),
+                "minimizer_s": ref["minimizer_s"], "linear_solver_s_per_iteration": ref["linear_solver_s"] / max(m - 1, 1),
+                "threads": ref["threads"], "wall_s": time.perf_counter() - t0,
+                "note": "real Ceres 2.0.0 LM (SPARSE_SCHUR, AutoDiff over the restated photometric functor, the reference's "
+                        "LocalParameterizationSE3, the same options) on the same problem on this host's cores: the "
+                        "trajectory the engine's timed solve is compared with, iteration by iteration"}
+    return out
 
 
 def gn_c3(iters, torch, dev_index, dev):
@@ -516,45 +559,36 @@ def main():
             dist.init_process_group(backend)
         dd = dist
 
-    # ---- the headline: the C4 problem on one GPU; N > 1 — weak scaling, every rank a full C4-size shard -------------
-    # (the evaluation partitions by host keyframe with no exchange step, SURVEY.md §8e: rank r holds host keyframes
-    # [r·F, (r+1)·F) of one N·F-keyframe trajectory with their 100k points and 400k blocks; per-GPU work fixed)
+    # ---- the headline: the one C4 problem (BASELINE.json configs[3]); N > 1 — split by host keyframe, strong scaling ------
+    # (the evaluation partitions by host keyframe with no exchange step, SURVEY.md §8e: rank r evaluates the points
+    # hosted by its contiguous range of host keyframes, with all their blocks; every rank holds all poses and images)
     K, F, Np = args.targets, args.frames, args.points
-    if world > 1:
-        pb, images_w = synth.c4_shard(dev, rank=rank, world=world, n_frames=F, n_points=Np, K=K)
-    else:
-        pb, images_w = synth.c4_shard(dev, n_frames=F, n_points=Np, K=K)
+    full, images = synth.c4_shard(dev, n_frames=F, n_points=Np, K=K)  # identical on every rank (same seeds)
+    pb = D.shard_problem(full, world, rank)[0] if world > 1 else full
     eng = engine_mod.Engine(synth.PHOTOMETRIC, synth.PINHOLE, device=dev_index, huber_width=9.0)
-    eng.set_problem(pb, images_device_ptr=images_w.data_ptr())
-    states = make_states(pb, torch, dev, 7 + rank)
+    eng.set_problem(pb, images_device_ptr=images.data_ptr())
+    states = make_states(pb, torch, dev, 7)
     eng.set_state_device(states[0][0].data_ptr(), states[0][1].data_ptr())
     eng.evaluate(True)
     _, valid = eng.records()
     elapsed, kern_us, host_diag = time_evaluation(eng, states, args.steps, args.warmup, args.clock_warmup_s, torch, dd, dev)
-    kern_us_local = kern_us
     eng.close()
-    if world > 1:
-        del images_w
+    kern_us_max = float(all_reduce_max(torch, dd, [kern_us], dev)[0])
 
-    # ---- the one C4 problem itself (1004 keyframes), sharded by host keyframe: strong scaling (N > 1), the GN leg ----
+    # ---- N > 1: the weak form beside it — every rank a full C4-size shard of one N·F-keyframe trajectory ---------------
+    weak = None
     if world > 1:
-        full, images = synth.c4_shard(dev, n_frames=F, n_points=Np, K=K)  # identical on every rank (same seeds)
-    else:
-        full, images = pb, images_w
-    strong = None
-    if world > 1:
-        pbs, _, _ = D.shard_problem(full, world, rank)
-        engs = engine_mod.Engine(synth.PHOTOMETRIC, synth.PINHOLE, device=dev_index, huber_width=9.0)
-        engs.set_problem(pbs, images_device_ptr=images.data_ptr())
-        sts = make_states(pbs, torch, dev, 7)
-        el_s, kern_s, _ = time_evaluation(engs, sts, args.steps, args.warmup, args.clock_warmup_s, torch, dd, dev)
-        engs.close()
-        strong = {"value": full.n_blocks * args.steps / el_s, "unit": "blocks/s", "ms_per_step": 1e3 * el_s / args.steps,
-                  "blocks_total": full.n_blocks, "blocks_rank0": pbs.n_blocks, "kernel_avg_us": kern_s,
-                  "note": f"the one C4 problem ({full.n_frames} keyframes, {full.n_blocks} blocks) split by host keyframe "
-                          f"over {world} GPUs (distributed.shard_problem), no data-path collective"}
-    else:
-        pbs = full
+        pw, images_w = synth.c4_shard(dev, rank=rank, world=world, n_frames=F, n_points=Np, K=K)
+        ew = engine_mod.Engine(synth.PHOTOMETRIC, synth.PINHOLE, device=dev_index, huber_width=9.0)
+        ew.set_problem(pw, images_device_ptr=images_w.data_ptr())
+        sw = make_states(pw, torch, dev, 7 + rank)
+        el_w, kern_w, _ = time_evaluation(ew, sw, args.steps, args.warmup, args.clock_warmup_s, torch, dd, dev)
+        ew.close()
+        del images_w
+        weak = {"value": world * pw.n_blocks * args.steps / el_w, "unit": "blocks/s", "ms_per_step": 1e3 * el_w / args.steps,
+                "blocks_per_rank": pw.n_blocks, "kernel_avg_us_rank0": kern_w,
+                "note": f"weak scaling: rank r evaluates host keyframes [r*{F}, (r+1)*{F}) of one {world * F + K}-keyframe "
+                        f"trajectory ({pw.n_blocks} blocks per GPU), no data-path collective"}
     shard8 = None
     if world == 1 and not args.no_shard_leg:  # one rank's step of the C4 problem split 8 ways, on this GPU
         p8, _, _ = D.shard_problem(full, 8, 0)
@@ -563,23 +597,32 @@ def main():
         st8 = make_states(p8, torch, dev, 7)
         el8, k8, _ = time_evaluation(e8, st8, args.steps, args.warmup, args.clock_warmup_s, torch, None, dev)
         e8.close()
+        bpb8 = algorithmic_bytes_per_block(p8.P, K, p8.n_frames, p8.n_points, p8.n_blocks)
         shard8 = {"blocks": p8.n_blocks, "ms_per_step": 1e3 * el8 / args.steps, "kernel_avg_us": k8,
+                  "hbm_frac": bpb8 * p8.n_blocks / (k8 * 1e-6) / 1e9 / HBM_PEAK_GBS,
                   "strong_scaling_ceiling_n8": (elapsed / args.steps) / (el8 / args.steps),
                   "note": "a 1/8 host-keyframe shard of the C4 problem (rank 0's share at N = 8) timed on one GPU: the "
                           "strong-scaling ceiling at N = 8 is the full problem's step over this step"}
 
+    # ---- the Gauss-Newton leg: the C4 problem with rendered images (the solve the GPU tests pin against real Ceres) ----
     gn = None
     if args.gn_iterations > 0:
+        gfull, gimages = synth.c4_shard(dev, n_frames=F, n_points=Np, K=K, texture="render")
+        gpb = D.shard_problem(gfull, world, rank)[0] if world > 1 else gfull
         eng = engine_mod.Engine(synth.PHOTOMETRIC, synth.PINHOLE, device=dev_index, huber_width=9.0)
-        eng.set_problem(pbs, images_device_ptr=images.data_ptr())
-        eng.set_state(pbs.poses, pbs.rho)
+        eng.set_problem(gpb, images_device_ptr=gimages.data_ptr())
+        eng.set_state(gpb.poses, gpb.rho)
+        cp = None
+        if world == 1 and not args.no_cpu_baseline:
+            cp = synth.Problem(**{**gfull.__dict__, "images": gimages.cpu().numpy()})
         try:
-            gn = gn_benchmark(eng, args.gn_iterations, torch, dd, dev, world)
+            gn = gn_benchmark(eng, gpb, args.gn_iterations, torch, dd, dev, world, cp, host_cores()["usable"])
         except Exception as ex:  # a secondary leg: report it, keep the headline line (every rank raises alike)
             if world == 1:
                 raise
             gn = {"error": f"{type(ex).__name__}: {ex}"[:300]}
         eng.close()
+        del gimages
 
     c3 = None
     if world == 1 and not args.no_c3 and args.gn_iterations > 0:
@@ -590,11 +633,11 @@ def main():
                      args.gn_iterations)
 
     if rank == 0:
-        total_blocks = pb.n_blocks * world
+        total_blocks = full.n_blocks
         ms_per_step = 1e3 * elapsed / args.steps
         value = total_blocks * args.steps / elapsed
         bpb = algorithmic_bytes_per_block(pb.P, K, pb.n_frames, pb.n_points, pb.n_blocks)
-        achieved = bpb * pb.n_blocks / (kern_us_local * 1e-6) / 1e9
+        achieved = bpb * pb.n_blocks / (kern_us * 1e-6) / 1e9
         traffic, traffic_info = None, None
         if world == 1 and not args.no_live_traffic:
             traffic, traffic_info = measure_traffic(args, pb.n_blocks)
@@ -629,17 +672,14 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": ms_per_step,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong",
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic",
             "config": {
-                "workload": (f"C4: one synthetic problem of {F} host keyframes x {Np} points x {pb.P}-px patch x {K} "
-                             f"targets = {pb.n_blocks} residual blocks, {full.width}x{full.height} u8 images, pinhole"
-                             if world == 1 else
-                             f"C4 per GPU: host keyframes [r*{F}, (r+1)*{F}) of one {world * F + K}-keyframe trajectory "
-                             f"on rank r, each with {Np} points x {pb.P}-px patch x {K} targets = {pb.n_blocks} blocks "
-                             f"({total_blocks} in all), {full.width}x{full.height} u8 images, pinhole") +
+                "workload": f"C4: one synthetic problem of {F} host keyframes x {Np} points x {pb.P}-px patch x {K} "
+                            f"targets = {total_blocks} residual blocks, {full.width}x{full.height} u8 images, pinhole" +
+                            (f", split by host keyframe over {world} GPUs (rank 0: {pb.n_blocks} blocks)" if world > 1 else "") +
                             "; one step = full r + tangent-J evaluation (Ceres-mode records) at a new HBM-resident state",
                 "keyframes": F, "points": Np, "patch": pb.P, "targets_per_point": K,
                 "blocks_total": total_blocks, "blocks_rank0": pb.n_blocks, "valid_blocks_rank0": int(valid.sum()),
@@ -657,14 +697,16 @@ def main():
                 "traffic": traffic,
                 "traffic_detail": traffic_info,
                 "bytes_per_block_alg": bpb,
-                "kernel_avg_us": kern_us_local,
+                "kernel_avg_us": kern_us,
+                "kernel_avg_us_max_over_ranks": kern_us_max,
+                **({"note": "rank 0's shard: its algorithmic bytes over its launch duration"} if world > 1 else {}),
             },
             "cpu_baseline": cpu,
             "c2": c2,
             "gn": gn,
             "gn_c3": c3,
             "c5": c5,
-            "strong": strong,
+            "weak": weak,
             "shard8": shard8,
             "host": {k: round(v, 2) for k, v in host_diag.items()},
         }

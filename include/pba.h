@@ -247,6 +247,21 @@ typedef struct pba_solver_summary {
 /* per-phase device timing of pba_solve (linearize_ms / solve_ms / cost_ms of the summary); default off */
 int pba_set_solver_timing(pba_engine* engine, int32_t enable);
 
+/* One entry of the last solve's trajectory — Ceres' Solver::Summary::iterations (IterationSummary, iteration_callback.h;
+ * filled as trust_region_minimizer.cc does): entry 0 is the initial state (successful, cost = the initial cost, radius =
+ * the initial radius); then one entry per trial Ceres would push — accepted, rejected, invalid (:476-483) or ending on the
+ * minimum trust-region radius — but not the trial that met the parameter / function tolerance or the invalid-step limit
+ * (Minimize returns before FinalizeIteration, :110-115, :453-466).  cost: accepted — the new state's; rejected — the
+ * candidate's (:124); invalid — the current state's.  trust_region_radius: after this iteration's update (:327).
+ * gradient_max_norm: at the state the iteration ended in (a rejected step keeps the previous one, :130). */
+typedef struct pba_iteration_summary {
+  int32_t iteration, step_is_successful, step_is_valid, pad_;
+  double cost, cost_change, relative_decrease, trust_region_radius, step_norm, gradient_max_norm;
+} pba_iteration_summary;
+/* copies min(capacity, entries) entries of the last pba_solve / pba_solve_distributed(_comm) into out (may be NULL with
+ * capacity 0) and the number of entries into count; replaces reading Solver::Summary::iterations (map_utils.h:384-392) */
+int pba_solver_iterations(const pba_engine* engine, int32_t capacity, pba_iteration_summary* out, int32_t* count);
+
 /* constant parameter blocks (Problem::SetParameterBlockConstant, map_utils.h:334-336) */
 int pba_set_fixed_frames(pba_engine* engine, int32_t n, const int32_t* frames);
 /* Jacobian evaluation at the current state + normal-equation pieces; cost may be NULL */

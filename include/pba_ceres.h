@@ -250,12 +250,13 @@ class GpuEvaluator : public ceres::EvaluationCallback {
       records_.resize(nb * rec_);
       check(pba_get_records_async(engine_, records_.data(), valid_.data(), chunk_blocks_), "pba_get_records_async");
       async_ = true;
-      res_ = records_.data();
+      rec_src_ = res_ = records_.data();
       res_stride_ = rec_;
       t2 = t3 = clk::now();
       if (form_ == PoseJacobian::kReferenceSE3) {  // P⁺ of every pose at this point, while the launch and copies run
         pinv_.resize(42 * nf);
         for (size_t f = 0; f < nf; ++f) se3_plus_jacobian_pinv(sp + 7 * f, &pinv_[42 * f]);
+        pinv_src_ = pinv_.data();
       }
     } else {
       t2 = clk::now();
@@ -264,10 +265,12 @@ class GpuEvaluator : public ceres::EvaluationCallback {
       residuals_.resize(nb * R_);
       check(pba_get_residuals(engine_, residuals_.data(), valid_.data()), "pba_get_residuals");
       async_ = false;
+      rec_src_ = nullptr;
       res_ = residuals_.data();
       res_stride_ = R_;
       t3 = clk::now();
     }
+    valid_src_ = valid_.data();
     const auto t4 = clk::now();
     auto sec = [](clk::duration d) { return std::chrono::duration<double>(d).count(); };
     times_.gather_s[m] += sec(t1 - t0);
@@ -292,18 +295,24 @@ class GpuEvaluator : public ceres::EvaluationCallback {
   int chunk_blocks_ = std::getenv("PBA_CERES_CHUNK_BLOCKS") ? std::atoi(std::getenv("PBA_CERES_CHUNK_BLOCKS")) : kChunkBlocks;
 
   int residuals_per_block() const { return R_; }
-  const float* record(int block) const { return records_.data() + (size_t)block * rec_; }  // with has_jacobians()
+  const float* record(int block) const { return rec_src_ + (size_t)block * rec_; }  // with has_jacobians()
   const float* residuals(int block) const { return res_ + (size_t)block * res_stride_; }
-  bool valid(int block) const { return valid_[block] != 0; }
+  bool valid(int block) const { return valid_src_[block] != 0; }
   bool has_jacobians() const { return have_jac_; }
   bool has_intrinsics() const { return !intr_.empty(); }
   PoseJacobian pose_jacobian() const { return form_; }
-  const double* pose_pinv(int frame) const { return &pinv_[42 * (size_t)frame]; }  // P⁺ (6×7) at the prepared point
+  const double* pose_pinv(int frame) const { return pinv_src_ + 42 * (size_t)frame; }  // P⁺ (6×7) at the prepared point
   // a Jacobian was requested for an intrinsics block the evaluator was not given (Evaluate returned false)
   bool refused_intrinsics() const { return refused_.load(); }
   void refuse_intrinsics() const { refused_.store(true); }
 
- private:
+ protected:
+  // What Evaluate reads (record / residuals / valid / pose_pinv): the read-back buffers below after a
+  // PrepareForEvaluation; a derived evaluator may point them at host arrays of its own (tests/cpp/ceres_lm_driver.cpp's
+  // replay floor: the same per-block copy with the device's work removed).
+  const float* rec_src_ = nullptr;
+  const uint8_t* valid_src_ = nullptr;
+  const double* pinv_src_ = nullptr;
   pba_engine* engine_;
   std::vector<double*> poses_, rho_, intr_;
   PoseJacobian form_;

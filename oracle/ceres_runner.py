@@ -47,6 +47,7 @@ def run(mode: str, pb, iters: int = 20, huber: float = 1.0, threads: int = 8, fi
     out["costs"] = it[:, 1]
     out["step_ok"] = it[:, 2].astype(bool)
     out["relative_decrease"] = it[:, 3]
+    out["radius"] = it[:, 4]
     out["step_norm"] = it[:, 5]
     out["gradient_max_norm"] = it[:, 6]
     out["intrinsics"] = np.asarray(out["intrinsics"]).reshape(-1, 8)

@@ -16,6 +16,7 @@
 #include <type_traits>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -534,7 +535,7 @@ void launch_photometric(pba_engine* e, const KernelArgs& ka, int mode) {
   }
   // 9…32 pixels: 8 lanes per block, ⌈P/8⌉ pixels per lane
   // the camera-table form for record launches at a fused state with few cameras (the C5 configuration)
-  const bool ct = mode == 1 && ka.poses != nullptr && ka.n_cams <= kCamTab && !e->no_cam_table;
+  const bool ct = mode == 1 && ka.poses != nullptr && ka.n_cams <= kCamTab;
 #define PBA_LAUNCH_ONE(PPL, M, TT)                                                                      \
   {                                                                                                     \
     constexpr int nth = kMultiThreads<PPL, TT>;                                                         \
@@ -877,6 +878,8 @@ int pba_set_pattern(pba_engine* e, int32_t P, const float* offsets) {
   reset_pyramid(e);
   e->pattern_h.assign(offsets, offsets + 2 * P);
   e->P = P;
+  e->evaluated = false;  // the records and contiguous residuals of the last evaluation were sized for the old P
+  e->res_fresh = false;
   return PBA_OK;
 }
 
@@ -1133,6 +1136,7 @@ int pba_set_record_format(pba_engine* e, int32_t format) {
     return fail(PBA_ERR_INVALID_ARGUMENT, "fp16 records are photometric only");
   e->record_format = format;
   e->evaluated = false;
+  e->res_fresh = false;
   return PBA_OK;
 }
 
@@ -1163,12 +1167,19 @@ int pba_get_records(pba_engine* e, float* records, uint8_t* valid) {
 // Wait for an event by polling it (its completion signal lives in host memory) before falling back to a blocking
 // wait: the read-backs of the Ceres adapter sit inside Ceres' evaluation timer, and a blocking wait's wake-up came late
 // when the process's cgroup CPU quota was saturated by Ceres' own threads (C2 residual-only evaluations measured
-// 0.7-1.8 ms box to box for the same work).
+// 0.7-1.8 ms box to box for the same work).  The poll is bounded in time (kEventSpinUs; a C2 read-back chunk arrives
+// within ~0.1 ms), so a long wait — or several of Ceres' threads waiting at once — blocks instead of spinning on the
+// quota Ceres' own threads need.
+constexpr double kEventSpinUs = 200.0;
 static hipError_t wait_event(hipEvent_t ev) {
-  for (int i = 0; i < (1 << 20); ++i) {
+  const auto t0 = std::chrono::steady_clock::now();
+  for (unsigned i = 0;; ++i) {
     const hipError_t q = hipEventQuery(ev);
     if (q != hipErrorNotReady) return q;
     __builtin_ia32_pause();
+    if ((i & 63u) == 63u &&
+        std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count() > kEventSpinUs)
+      break;
   }
   return hipEventSynchronize(ev);
 }
@@ -1255,7 +1266,7 @@ int pba_get_residuals(pba_engine* e, float* residuals, uint8_t* valid) {
   if (int rc = check_device(e)) return rc;
   const size_t R = (size_t)e->R(), nb = (size_t)e->n_blocks, RF = (size_t)e->rec_floats();
   std::vector<_Float16> half;
-  if (residuals && nb && e->res_fresh) {
+  if (residuals && nb && e->res_fresh && e->res.n >= nb * R) {
     // a residual-only evaluation also wrote its residuals contiguously: one plain device-to-host copy
     if (int rc = enqueue_to_host(e, residuals, mapped_device_ptr(residuals), e->res.p, nb * R * sizeof(float))) return rc;
   } else if (residuals && nb) {

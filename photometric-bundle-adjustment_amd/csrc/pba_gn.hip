@@ -835,34 +835,8 @@ __global__ void assemble_kernel(AsmArgs a, double lambda) {
 constexpr int EX_TAIL = 24;  // g(6) | g_direct(6) | diag(A)(6) | observed | pad
 __host__ __device__ constexpr long long ex_row(int K) { return (long long)(K + 1) * 36 + EX_TAIL; }
 
-// One lane per element of the local skyline (same contribution lists as assemble_kernel, nothing damped or
-// fixed) and per pose-gradient element.  Positions outside the local profile stay zero (memset).
-__global__ void export_kernel(AsmArgs a, const uint8_t* __restrict__ observed, double* __restrict__ X, int K) {
-  if (lm_view(a.lm).set != 0.0) a.part_lin = a.part_lin1;  // (no done gate: see schur_kernel)
-  const int tid = blockIdx.x * blockDim.x + threadIdx.x;
-  const int nS = a.n_sky * 36;
-  const long long RS = ex_row(K);
-  if (tid < nS) {
-    const int s = tid / 36, e = tid % 36, r = e / 6, cc = e % 6;
-    const int i = a.blk_i[s], j = a.blk_j[s];
-    double sum, dsum;
-    contrib_sums(a, a.sky_contrib, a.sky_cptr[s], a.sky_cptr[s + 1], r * 6 + cc, cc * 6 + r, sum, dsum);
-    X[(long long)i * RS + (j - i + K) * 36 + e] = sum;
-    if (i == j && r == cc) X[(long long)i * RS + (K + 1) * 36 + 12 + r] = dsum;
-    return;
-  }
-  const int t = tid - nS;
-  if (t >= 6 * a.n_frames) return;
-  const int i = t / 6, r = t % 6;
-  double sum, dsum;
-  contrib_sums(a, a.g_contrib, a.g_cptr[i], a.g_cptr[i + 1], r, r, sum, dsum);
-  double* tail = X + (long long)i * RS + (K + 1) * 36;
-  tail[r] = sum;
-  tail[6 + r] = dsum;
-  if (r == 0) tail[18] = observed[i] ? 1.0 : 0.0;
-}
-
-// The same over every element of the exchange buffer: positions outside the local profile get their zero here, so the
+// One lane per element of the exchange buffer (the local skyline's elements by the contribution lists of
+// assemble_kernel, nothing damped or fixed; the pose gradients): positions outside the local profile get their zero here, so the
 // buffer needs no fill launch before it (round 3: a 5-µs hipMemsetAsync of the whole band per trial).
 __global__ void export_band_kernel(AsmArgs a, const uint8_t* __restrict__ observed, const int* __restrict__ sky_first,
                                    const int* __restrict__ sky_row, double* __restrict__ X, int K) {
@@ -1554,17 +1528,12 @@ __global__ __launch_bounds__(2 * kCrOddThreads<M>) void cr_level_kernel(CrLevel 
 #endif
 constexpr int kCrPivot = PBA_CR_PIVOT;  // columns per Gauss-Jordan step of gj_wave (1, 2, 4 or 8; divides M)
 
-// Loads / stores of the rows handed between workgroups of pcr_fused_kernel (COH): `sc1` (L1-bypassing, write-through)
-// agent-scope accesses, the hand-off form of MI355X_MICROARCH.md's first table row; plain otherwise.
+// Loads of the rows a launch wrote itself (COH: the last PCR level's solve reads the rows its own workgroup has just
+// stored, cr_level_wave_kernel): `sc1` (L1-bypassing) agent-scope loads; plain otherwise.
 template <bool COH>
 __device__ __forceinline__ double ld_row(const double* p) {
   if constexpr (COH) return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   else return *p;
-}
-template <bool COH>
-__device__ __forceinline__ void st_row(double* p, double v) {
-  if constexpr (COH) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  else *p = v;
 }
 
 // Pivot blocks of PB columns: lanes k … k+PB−1 publish their columns to the wave's LDS buffer (row r: PB doubles),
@@ -1661,172 +1630,10 @@ __device__ __forceinline__ bool gj_wave(const double* __restrict__ D, const doub
 }
 
 
-#ifndef PBA_CR_MFMA
-#define PBA_CR_MFMA 0
-#endif
-
-#if PBA_CR_MFMA
-
-// ---- Gauss-Jordan on the fp64 matrix cores (M = 24) -----------------------------------------------------------------
-// The same elimination as gj_wave<24> — X = D⁻¹[R1 | b] by 4-column pivot blocks, no pivoting (D is SPD, so is every
-// pivot block) — with the augmented matrix [D | R1 | b | 0] (24 × 64, padded to 32 rows) held by one wave in the
-// v_mfma_f64_16x16x4f64 accumulator layout: tile (rt, ct) entry v of lane l = row 16rt + l/16 + 4v, column 16ct + l%16.
-// In that layout the four pivot rows k … k+3 are entry (k%16)/4 of every lane of row tile k/16, i.e. exactly the B
-// operand of a K = 4 step (lane l = (k l/16, column l%16)).  A step is then:
-//   P = the 4 × 4 pivot block (16 readlanes), P⁻¹ by 2 × 2 blocks (every lane the same; all leading minors positive
-//   ⇔ the pivots of gj_wave's in-register solve),
-//   T = P⁻¹·R on the matrix cores (one MFMA per column tile, rows 0-3 of the result = T in the B layout),
-//   C = the pivot columns of every row → A layout through a 1-KB LDS transpose,
-//   [D | R1 | b] −= C·T (one MFMA per tile), then the pivot rows ← T.
-// The serial chain per step is the readlanes, the 2 × 2-block inverse and two MFMA latencies, against gj_wave's LDS
-// publish / 96 broadcast reads / in-register 4 × 4 solve / 80 fp64 FMAs per lane.
-__device__ __forceinline__ double readlane_d(double x, int l) {
-  const int lo = __builtin_amdgcn_readlane(__double2loint(x), l), hi = __builtin_amdgcn_readlane(__double2hiint(x), l);
-  return __hiloint2double(hi, lo);
-}
-
-// 2 × 2 inverse (row-major a, b, c, d) → false when the leading minors are not both positive
-__device__ __forceinline__ bool inv2(double a, double b, double c, double d, double (&o)[4]) {
-  const double det = a * d - b * c;
-  const double r = rcp_nr(det);
-  o[0] = d * r; o[1] = -b * r; o[2] = -c * r; o[3] = a * r;
-  return a > 0.0 && det > 0.0;
-}
-
-// P⁻¹ of a 4 × 4 (row-major) by 2 × 2 blocks: P = [A B; C E], S = E − C A⁻¹ B,
-// P⁻¹ = [A⁻¹ + A⁻¹B S⁻¹ C A⁻¹, −A⁻¹B S⁻¹; −S⁻¹ C A⁻¹, S⁻¹].  Returns false when a leading minor of P is not positive.
-__device__ __forceinline__ bool inv4(const double (&P)[16], double (&Q)[16]) {
-  double Ai[4], Si[4];
-  bool ok = inv2(P[0], P[1], P[4], P[5], Ai);
-  const double B[4] = {P[2], P[3], P[6], P[7]}, C[4] = {P[8], P[9], P[12], P[13]};
-  // AB = A⁻¹B, CA = C A⁻¹
-  const double AB[4] = {Ai[0] * B[0] + Ai[1] * B[2], Ai[0] * B[1] + Ai[1] * B[3],
-                        Ai[2] * B[0] + Ai[3] * B[2], Ai[2] * B[1] + Ai[3] * B[3]};
-  const double CA[4] = {C[0] * Ai[0] + C[1] * Ai[2], C[0] * Ai[1] + C[1] * Ai[3],
-                        C[2] * Ai[0] + C[3] * Ai[2], C[2] * Ai[1] + C[3] * Ai[3]};
-  const double S0 = P[10] - (C[0] * AB[0] + C[1] * AB[2]), S1 = P[11] - (C[0] * AB[1] + C[1] * AB[3]);
-  const double S2 = P[14] - (C[2] * AB[0] + C[3] * AB[2]), S3 = P[15] - (C[2] * AB[1] + C[3] * AB[3]);
-  ok = inv2(S0, S1, S2, S3, Si) && ok;
-  // top-right −A⁻¹B S⁻¹, bottom-left −S⁻¹ C A⁻¹
-  const double TR[4] = {-(AB[0] * Si[0] + AB[1] * Si[2]), -(AB[0] * Si[1] + AB[1] * Si[3]),
-                        -(AB[2] * Si[0] + AB[3] * Si[2]), -(AB[2] * Si[1] + AB[3] * Si[3])};
-  const double BL[4] = {-(Si[0] * CA[0] + Si[1] * CA[2]), -(Si[0] * CA[1] + Si[1] * CA[3]),
-                        -(Si[2] * CA[0] + Si[3] * CA[2]), -(Si[2] * CA[1] + Si[3] * CA[3])};
-  // top-left A⁻¹ − A⁻¹B·BL
-  const double TL[4] = {Ai[0] - (AB[0] * BL[0] + AB[1] * BL[2]), Ai[1] - (AB[0] * BL[1] + AB[1] * BL[3]),
-                        Ai[2] - (AB[2] * BL[0] + AB[3] * BL[2]), Ai[3] - (AB[2] * BL[1] + AB[3] * BL[3])};
-  Q[0] = TL[0]; Q[1] = TL[1]; Q[2] = TR[0]; Q[3] = TR[1];
-  Q[4] = TL[2]; Q[5] = TL[3]; Q[6] = TR[2]; Q[7] = TR[3];
-  Q[8] = BL[0]; Q[9] = BL[1]; Q[10] = Si[0]; Q[11] = Si[1];
-  Q[12] = BL[2]; Q[13] = BL[3]; Q[14] = Si[2]; Q[15] = Si[3];
-  return ok;
-}
-
-// One wave: [D | R1 | b] (R1: M × M, row-major or transposed; b: M values, present when ncol > M) → A = [I | X].
-// cbuf: 2 × 16 × 4 doubles of LDS owned by the wave.
-template <bool COH>
-__device__ __forceinline__ bool gj_mfma(const double* __restrict__ D, const double* __restrict__ R1, bool r1_trans,
-                                        const double* __restrict__ b, int ncol, int lane, double* cbuf,
-                                        v4f64 (&A)[2][4]) {
-  constexpr int M = 24;
-  const int cl = lane & 15, rq = lane >> 4;
-  // column 16ct + cl as base + row·stride (one address choice per lane and tile, then unconditional loads)
-  const double* base[4];
-  int stride[4];
-  bool zero[4];
-#pragma unroll
-  for (int ct = 0; ct < 4; ++ct) {
-    const int c = 16 * ct + cl;
-    base[ct] = D + min(c, M - 1);
-    stride[ct] = M;
-    zero[ct] = c >= M + ncol;
-    if (c >= M && c < 2 * M) {
-      if (R1) {
-        base[ct] = r1_trans ? R1 + (c - M) * M : R1 + (c - M);
-        stride[ct] = r1_trans ? 1 : M;
-      } else {
-        zero[ct] = true;
-      }
-    } else if (c >= 2 * M && c < M + ncol) {
-      if (b) {
-        base[ct] = b;
-        stride[ct] = 1;
-      } else {
-        zero[ct] = true;
-      }
-    }
-  }
-  // rows 16rt + rq + 4v < 24: row tile 0 all four entries, row tile 1 entries 0 and 1 (entries 2-3 are padding)
-  double ld[4][6];
-#pragma unroll
-  for (int ct = 0; ct < 4; ++ct)
-#pragma unroll
-    for (int e = 0; e < 6; ++e) ld[ct][e] = ld_row<COH>(base[ct] + (rq + 4 * e) * stride[ct]);
-#pragma unroll
-  for (int ct = 0; ct < 4; ++ct) {
-#pragma unroll
-    for (int v = 0; v < 4; ++v) A[0][ct][v] = zero[ct] ? 0.0 : ld[ct][v];
-    A[1][ct][0] = zero[ct] ? 0.0 : ld[ct][4];
-    A[1][ct][1] = zero[ct] ? 0.0 : ld[ct][5];
-    A[1][ct][2] = 0.0;
-    A[1][ct][3] = 0.0;
-  }
-  bool ok = true;
-#pragma unroll
-  for (int k = 0; k < M; k += 4) {
-    const int rtk = k >> 4, vk = (k & 15) >> 2, ctk = k >> 4, c0 = k & 15;
-    // pivot block P[i][j] = row k+i, column k+j: lane 16i + c0 + j of entry vk, tile (rtk, ctk)
-    double P[16], Q[16];
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) P[4 * i + j] = readlane_d(A[rtk][ctk][vk], 16 * i + c0 + j);
-    // the pivot columns of every row → A layout (lane l: row 16rt + l%16, column k + l/16), through LDS
-    if (cl >= c0 && cl < c0 + 4) {
-#pragma unroll
-      for (int rt = 0; rt < 2; ++rt)
-#pragma unroll
-        for (int v = 0; v < 4; ++v) cbuf[(rt * 16 + rq + 4 * v) * 4 + (cl - c0)] = A[rt][ctk][v];
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    const double cop0 = -cbuf[cl * 4 + rq], cop1 = -cbuf[(16 + cl) * 4 + rq];
-    ok = inv4(P, Q) && ok;
-    // A operand of T = P⁻¹R: lane l = (row l%16, k l/16) → P⁻¹[cl][rq] for cl < 4
-    double qa = 0.0;
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) qa = (cl == i && rq == j) ? Q[4 * i + j] : qa;
-    // column tiles left of the pivot block's are finished (every column's update reads only its own pivot-row
-    // entries, and those of a finished column take no further part): skipped
-    v4f64 T[4];
-#pragma unroll
-    for (int ct = k >> 4; ct < 4; ++ct) {
-      const v4f64 z = {0.0, 0.0, 0.0, 0.0};
-      T[ct] = __builtin_amdgcn_mfma_f64_16x16x4f64(qa, A[rtk][ct][vk], z, 0, 0, 0);
-    }
-#pragma unroll
-    for (int ct = k >> 4; ct < 4; ++ct) {
-      A[0][ct] = __builtin_amdgcn_mfma_f64_16x16x4f64(cop0, T[ct][0], A[0][ct], 0, 0, 0);
-      A[1][ct] = __builtin_amdgcn_mfma_f64_16x16x4f64(cop1, T[ct][0], A[1][ct], 0, 0, 0);
-    }
-#pragma unroll
-    for (int ct = k >> 4; ct < 4; ++ct) A[rtk][ct][vk] = T[ct][0];
-    // the next step's transpose overwrites cbuf (LDS operations of one wave are processed in order)
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  }
-  return ok;
-}
-#endif
-
 // Rebuild of super-row i (next-level index in) from the two eliminations in LDS (sXl = X_{i−1}, sXr = X_{i+1}) and
 // U_{i−1}, U_i, D_i, b_i, on RB waves: 4 waves take two column tiles each, 8 waves one.  keep_u: the rebuilt row
 // still has a right coupling.  Waves w ≥ RB return at once.
-template <int M, int RB, bool COH = false>
+template <int M, int RB>
 __device__ __forceinline__ void cr_rebuild(int w, int lane, const double* sUl, const double* sUi, const double* sD,
                                            const double* sb, const double* sXl, const double* sXr, const CrLevel& Ln,
                                            int in, bool keep_u) {
@@ -1901,16 +1708,16 @@ __device__ __forceinline__ void cr_rebuild(int w, int lane, const double* sUl, c
     for (int v = 0; v < 4; ++v) {
       const int r = 16 * rt + (lane >> 4) + 4 * v, c = bcol[h];
       if (r < M) {
-        if (c < M) st_row<COH>(Ln.D + (long long)in * M * M + r * M + c, acc[h][v]);
-        else if (c < 2 * M) st_row<COH>(Ln.U + (long long)in * M * M + r * M + (c - M), keep_u ? acc[h][v] : 0.0);
-        else if (c == 2 * M) st_row<COH>(Ln.b + (long long)in * M + r, acc[h][v]);
+        if (c < M) Ln.D[(long long)in * M * M + r * M + c] = acc[h][v];
+        else if (c < 2 * M) Ln.U[(long long)in * M * M + r * M + (c - M)] = keep_u ? acc[h][v] : 0.0;
+        else if (c == 2 * M) Ln.b[(long long)in * M + r] = acc[h][v];
       }
     }
 }
 
-// per-wave LDS of an elimination: gj_wave's pivot columns, or gj_mfma's pivot-column transpose (M = 24)
+// per-wave LDS of an elimination: gj_wave's pivot columns
 template <int M>
-constexpr int kPivBuf = (PBA_CR_MFMA && M == 24) ? 128 : M * kCrPivot;
+constexpr int kPivBuf = M * kCrPivot;
 
 template <int M>
 constexpr size_t cr_level_wave_lds() { return sizeof(double) * (3 * M * M + M + 2 * M * (2 * M + 1)); }
@@ -1926,8 +1733,8 @@ constexpr size_t cr_level_wave_lds() { return sizeof(double) * (3 * M * M + M + 
 //       CR level at the same per-workgroup latency, so it is used while the rows fit one workgroup per CU.
 // The D_i' are Schur complements of SPD principal submatrices ({l, i, r}), so every pivot block stays SPD.
 // The level's work for row i (rebuilt as row `in` of Ln) by a 4-wave workgroup: piv = 3 × M·kCrPivot doubles, smem =
-// cr_level_wave_lds<M>() bytes.  COH: rows read and written with the hand-off accesses of pcr_fused_kernel.
-template <int M, bool PCR, bool COH>
+// cr_level_wave_lds<M>() bytes.
+template <int M, bool PCR>
 __device__ __forceinline__ void cr_wave_level(const CrLevel& L, const CrLevel& Ln, int i, int in, int s, int* status,
                                               double (*piv)[kPivBuf<M>], double* smem) {
   static_assert(2 * M + 1 <= 64, "one wave per elimination");
@@ -1956,7 +1763,7 @@ __device__ __forceinline__ void cr_wave_level(const CrLevel& L, const CrLevel& L
       else if (e < 2 * M * M) src = L.U + (long long)i * M * M + (e - M * M);
       else if (e < 3 * M * M) src = L.D + (long long)i * M * M + (e - 2 * M * M);
       else if (e < NE) src = L.b + (long long)i * M + (e - 3 * M * M);
-      v[q] = ld_row<COH>(src);
+      v[q] = *src;
     }
 #pragma unroll
     for (int q = 0; q < NQ; ++q) {
@@ -1970,39 +1777,11 @@ __device__ __forceinline__ void cr_wave_level(const CrLevel& L, const CrLevel& L
     const int jj = has ? j : i;  // a missing neighbour eliminates a real row and contributes zeros
     const double* D = L.D + (long long)jj * M * M;
     const double* bj = L.b + (long long)jj * M;
-#if PBA_CR_MFMA
-    if constexpr (M == 24) {
-      v4f64 A[2][4];
-      bool ok;
-      if (w == 0) ok = gj_mfma<COH>(D, L.U + (long long)jj * M * M, false, bj, M + 1, lane, piv[0], A);
-      else if (w == 1) ok = gj_mfma<COH>(D, L.U + (long long)i * M * M, true, bj, M + 1, lane, piv[1], A);
-      else ok = gj_mfma<COH>(D, jj + s < L.n ? L.U + (long long)jj * M * M : nullptr, false, nullptr, M, lane, piv[2], A);
-      if (!ok && has && lane == 0) atomicOr(status, 1);
-      // X columns (M … 2M of [D | R1 | b]) → the LDS operands of the rebuild, as the column-per-lane form below does
-      const int cl = lane & 15, rq = lane >> 4;
-      double* xd = sX[w == 0 ? 0 : 1];
-#pragma unroll
-      for (int ct = 1; ct < 4; ++ct) {
-        const int col = 16 * ct + cl;
-        const int dcol = col < M || col > 2 * M || (w == 2 && col == 2 * M) ? -1 : (w == 1 && col < 2 * M ? col - M : col);
-        if (dcol < 0) continue;
-#pragma unroll
-        for (int rt = 0; rt < 2; ++rt)
-#pragma unroll
-          for (int v = 0; v < (rt == 0 ? 4 : 2); ++v) {
-            const int row = 16 * rt + rq + 4 * v;
-            xd[row * NC + dcol] = has ? A[rt][ct][v] : 0.0;
-            if (!PCR && w != 0 && has) L.X[(long long)(j / 2) * M * NC + row * NC + dcol] = A[rt][ct][v];
-          }
-      }
-      goto eliminated;
-    }
-#endif
     double a[M];
     bool ok;
-    if (w == 0) ok = gj_wave<M, COH>(D, L.U + (long long)jj * M * M, false, bj, M + 1, lane, piv[0], a);
-    else if (w == 1) ok = gj_wave<M, COH>(D, L.U + (long long)i * M * M, true, bj, M + 1, lane, piv[1], a);
-    else ok = gj_wave<M, COH>(D, jj + s < L.n ? L.U + (long long)jj * M * M : nullptr, false, nullptr, M, lane, piv[2], a);
+    if (w == 0) ok = gj_wave<M>(D, L.U + (long long)jj * M * M, false, bj, M + 1, lane, piv[0], a);
+    else if (w == 1) ok = gj_wave<M>(D, L.U + (long long)i * M * M, true, bj, M + 1, lane, piv[1], a);
+    else ok = gj_wave<M>(D, jj + s < L.n ? L.U + (long long)jj * M * M : nullptr, false, nullptr, M, lane, piv[2], a);
     if (!ok && has && lane == 0) atomicOr(status, 1);
     if (lane >= M && lane < 2 * M + (w == 2 ? 0 : 1)) {
       const int col = lane < 2 * M ? (w == 1 ? lane - M : lane) : 2 * M;
@@ -2016,9 +1795,6 @@ __device__ __forceinline__ void cr_wave_level(const CrLevel& L, const CrLevel& L
       }
     }
   }
-#if PBA_CR_MFMA
-eliminated:
-#endif
 #ifdef PBA_CR_STAMPS
   t1 = wall_clock64();
 #endif
@@ -2026,7 +1802,7 @@ eliminated:
 #ifdef PBA_CR_STAMPS
   t2 = wall_clock64();
 #endif
-  cr_rebuild<M, 4, COH>(w, lane, sUl, sUi, sD, sb, sX[0], sX[1], Ln, in, PCR ? i + 2 * s < L.n : right);
+  cr_rebuild<M, 4>(w, lane, sUl, sUi, sD, sb, sX[0], sX[1], Ln, in, PCR ? i + 2 * s < L.n : right);
 #ifdef PBA_CR_STAMPS
   __syncthreads();
   const long long t3 = wall_clock64();
@@ -2045,7 +1821,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   __shared__ __attribute__((aligned(16))) double piv[3][kPivBuf<M>];
   extern __shared__ double smem[];
   const int i = PCR ? (int)blockIdx.x : 2 * (int)blockIdx.x;
-  cr_wave_level<M, PCR, false>(L, Ln, i, blockIdx.x, PCR ? s : 1, status, piv, smem);
+  cr_wave_level<M, PCR>(L, Ln, i, blockIdx.x, PCR ? s : 1, status, piv, smem);
   if (!PCR || !out) return;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's row stores have completed
   __syncthreads();
@@ -2086,24 +1862,6 @@ template <int M>
 __global__ __launch_bounds__(64) void pcr_solve_kernel(CrLevel L, double* __restrict__ out, int lim, int* status) {
   __shared__ __attribute__((aligned(16))) double piv[kPivBuf<M>];
   const int lane = threadIdx.x, i = blockIdx.x;
-#if PBA_CR_MFMA
-  if constexpr (M == 24) {  // x = column 2M of [I | X]: lanes l % 16 = 0 of column tile 3
-    v4f64 A[2][4];
-    if (!gj_mfma<false>(L.D + (long long)i * M * M, nullptr, false, L.b + (long long)i * M, M + 1, lane, piv, A)) {
-      if (lane == 0) atomicOr(status, 1);
-      return;
-    }
-    if ((lane & 15) == 0)
-#pragma unroll
-      for (int rt = 0; rt < 2; ++rt)
-#pragma unroll
-        for (int v = 0; v < (rt == 0 ? 4 : 2); ++v) {
-          const int r = 16 * rt + (lane >> 4) + 4 * v;
-          if (i * M + r < lim) out[(long long)i * M + r] = A[rt][3][v];
-        }
-    return;
-  }
-#endif
   double a[M];
   const bool ok = gj_wave<M>(L.D + (long long)i * M * M, nullptr, false, L.b + (long long)i * M, M + 1, lane, piv, a);
   if (!ok) {
@@ -2114,95 +1872,6 @@ __global__ __launch_bounds__(64) void pcr_solve_kernel(CrLevel L, double* __rest
 #pragma unroll
     for (int r = 0; r < M; ++r)
       if (i * M + r < lim) out[(long long)i * M + r] = a[r];
-}
-
-// ---- parallel cyclic reduction in one launch ---------------------------------------------------------------------
-// All PCR levels and the final x_i = D_i⁻¹ b_i as tasks (l, i) of ONE launch, synchronised by data flow instead of
-// launch boundaries: task (l, i) (l < n_levels, stride s = 2^l) waits for rows i − s, i, i + s of level l, runs
-// cr_wave_level into level l + 1 (each level its own buffer: a row is read by tasks that no later writer waits for)
-// and publishes row i of level l + 1 with a ready flag; task (n_levels, i) solves row i.  One workgroup per task,
-// each taking the next task number from a device counter when it starts, so a task only ever waits for tasks taken
-// earlier by workgroups already resident: no deadlock whatever the residency (another engine's kernels on the same
-// device, more tasks than CUs).  (A persistent loop over tasks spilled 200-400 B of registers per lane.)  Hand-off: rows stored `sc1` (write-through) by every wave, each storing wave's
-// vmcnt(0), a workgroup barrier, then ONE lane's `sc1` flag store; the consumer polls with `sc1` loads and its
-// waves read the rows with `sc1` loads after a workgroup barrier (MI355X_MICROARCH.md, the first row of the
-// hand-off table: hipMalloc memory, one workgroup per CU).  Flags hold the launch's epoch (no reset launch); the
-// counter runs on across launches (base = the tasks of the launches before).
-constexpr int kMaxPcrLevels = 16;
-struct PcrFusedArgs {
-  CrLevel lv0;                    // the level PCR starts from
-  double* lv;                     // level l ≥ 1 (after the stride-2^(l−1) level): D, U, b at lv + (l − 1)·(2nM² + nM)
-  int n_levels, n, lim, epoch;
-  double* out;
-  int* status;
-  int* flags;                     // (n_levels + 1) × n: row i of level l published in this launch ⇔ epoch
-  unsigned* counter;
-  unsigned base;
-};
-
-// Poll a ready flag (one lane).  A flag that never comes (a bug, a dead producer) ends the wait after 1 s with the
-// status flagged (the solve then reports a failed step), so the grid always drains.
-__device__ __forceinline__ void pcr_wait(const int* f, int epoch, int* status) {
-  const long long t0 = wall_clock64();
-  while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != epoch) {
-    __builtin_amdgcn_s_sleep(2);
-    if (wall_clock64() - t0 > 100000000ll) {  // 100 MHz constant clock
-      atomicOr(status, 2);
-      return;
-    }
-  }
-}
-
-template <int M>
-__device__ __forceinline__ CrLevel pcr_fused_level(const PcrFusedArgs& a, int l) {
-  if (l == 0) return a.lv0;
-  const long long nm2 = (long long)a.n * M * M;
-  double* base = a.lv + (long long)(l - 1) * (2 * nm2 + (long long)a.n * M);
-  return CrLevel{base, base + nm2, base + 2 * nm2, nullptr, nullptr, a.n};
-}
-
-template <int M>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void pcr_fused_kernel(const PcrFusedArgs a) {
-  __shared__ __attribute__((aligned(16))) double piv[3][kPivBuf<M>];
-  extern __shared__ double smem[];
-  __shared__ unsigned s_task;
-  if (threadIdx.x == 0) s_task = atomicAdd(a.counter, 1u) - a.base;
-  __syncthreads();
-  const unsigned t = s_task;
-  if (t >= (unsigned)((a.n_levels + 1) * a.n)) return;  // (the grid is exactly the tasks)
-  const int l = (int)(t / (unsigned)a.n), i = (int)(t % (unsigned)a.n);
-  const int s = 1 << min(l, 30);
-  if (l < a.n_levels) {
-    if (l > 0 && threadIdx.x == 0) {
-      const int* f = a.flags + (long long)l * a.n;
-      pcr_wait(f + i, a.epoch, a.status);
-      if (i - s >= 0) pcr_wait(f + i - s, a.epoch, a.status);
-      if (i + s < a.n) pcr_wait(f + i + s, a.epoch, a.status);
-    }
-    __syncthreads();
-    cr_wave_level<M, true, true>(pcr_fused_level<M>(a, l), pcr_fused_level<M>(a, l + 1), i, i, s, a.status, piv, smem);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's row stores have completed
-    __syncthreads();
-    if (threadIdx.x == 0)
-      __hip_atomic_store(a.flags + (long long)(l + 1) * a.n + i, a.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return;
-  }
-  // the decoupled row: x_i = D_i⁻¹ b_i on wave 0 (lane 2M carries b)
-  if (threadIdx.x >= 64) return;
-  const int lane = threadIdx.x;
-  if (l > 0 && lane == 0) pcr_wait(a.flags + (long long)l * a.n + i, a.epoch, a.status);
-  __builtin_amdgcn_wave_barrier();
-  const CrLevel L = pcr_fused_level<M>(a, a.n_levels);
-  double x[M];
-  const bool ok = gj_wave<M, true>(L.D + (long long)i * M * M, nullptr, false, L.b + (long long)i * M, M + 1, lane, piv[0], x);
-  if (!ok) {
-    if (lane == 0) atomicOr(a.status, 1);
-    return;
-  }
-  if (lane == 2 * M)
-#pragma unroll
-    for (int r = 0; r < M; ++r)
-      if (i * M + r < a.lim) a.out[(long long)i * M + r] = x[r];
 }
 
 // The root super-row (the last level): x = D⁻¹ b.
@@ -3231,10 +2900,6 @@ int configure_solver(pba_engine* e, int K, int solver) {
   }
   G.cr_levels.clear();
   G.cr_pcr = -1;
-  if (const char* v = std::getenv("PBA_PCR_FUSED")) {  // A/B switch: 0 = a launch per level, 2 = two workgroups per CU
-    G.pcr_fused_opt = std::atoi(v) != 0;
-    G.pcr_fused_per_cu = std::atoi(v) == 2 ? 2 : 1;
-  }
   if (solver == SOLVER_CR) {
     const int M = 6 * K;
     // Parallel cyclic reduction takes over (wave kernel, M = 24) once the rows fit one workgroup per CU:
@@ -3272,19 +2937,6 @@ int configure_solver(pba_engine* e, int K, int solver) {
     }
     G.cr0_dirty = true;  // level 0 is set up for assemble_kernel's direct writes on first use
     G.cr0_inited = false;
-    // the one-launch PCR (pcr_fused_kernel): a buffer per stride level, ready flags, the task counter
-    G.pcr_levels = 0;
-    for (int st = 1; st < np; st *= 2) ++G.pcr_levels;
-    G.pcr_fused = G.pcr_fused_opt && M == 24 && np > 0 && G.pcr_levels <= kMaxPcrLevels;
-    if (G.pcr_fused) {
-      PBA_HIP(G.pcr_lv.resize((size_t)std::max(G.pcr_levels, 1) * ((size_t)np * M * M * 2 + (size_t)np * M)));
-      PBA_HIP(G.pcr_flags.resize((size_t)(G.pcr_levels + 1) * np));
-      PBA_HIP(G.pcr_counter.resize(1));
-      PBA_HIP(hipMemsetAsync(G.pcr_flags.p, 0, sizeof(int) * G.pcr_flags.n, st));
-      PBA_HIP(hipMemsetAsync(G.pcr_counter.p, 0, sizeof(unsigned), st));
-      G.pcr_base = 0;
-      G.pcr_epoch = 0;
-    }
   }
   return PBA_OK;
 }
@@ -3821,32 +3473,7 @@ void cr_solve(pba_engine* e, bool build) {
   }
   bool solved = false;  // the step vector already written (level c = 0 solved in place)
   if constexpr (2 * M + 1 <= 64) {
-    if (G.cr_pcr >= 0 && G.pcr_fused) {
-      PcrFusedArgs fa{};
-      fa.lv0 = cr_level(G, c);
-      const int n = fa.lv0.n;
-      fa.lv = G.pcr_lv.p;
-      fa.n_levels = G.pcr_levels;
-      fa.n = n;
-      solved = c == 0;
-      fa.out = solved ? G.x.p : cr_level(G, c).x;
-      fa.lim = solved ? 6 * e->n_frames : n * M;
-      fa.epoch = ++G.pcr_epoch;
-      fa.status = G.status.p;
-      fa.flags = G.pcr_flags.p;
-      fa.counter = G.pcr_counter.p;
-      fa.base = G.pcr_base;
-      const int grid = (G.pcr_levels + 1) * n;  // one workgroup per task
-      // dynamic LDS sized so that one workgroup fits a CU (160 KiB): the hand-off form is the one validated at one
-      // workgroup per CU
-      constexpr int kFusedLds = 81 * 1024;
-      static_assert(cr_level_wave_lds<24>() <= (size_t)kFusedLds, "the level's LDS");
-      const int lds = G.pcr_fused_per_cu == 1 ? kFusedLds : (int)cr_level_wave_lds<M>();
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&pcr_fused_kernel<M>),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-      pcr_fused_kernel<M><<<grid, 256, lds, e->stream>>>(fa);
-      G.pcr_base += (unsigned)grid;
-    } else if (G.cr_pcr >= 0) {
+    if (G.cr_pcr >= 0) {
       CrLevel src = cr_level(G, c);
       const int n = src.n;
       solved = c == 0;
@@ -4389,6 +4016,52 @@ bool finish_summary(double done, pba_solver_summary& s) {
   }
 }
 
+// The trajectory of a solve, as Ceres' Solver::Summary::iterations (pba.h, pba_iteration_summary): entry 0 the initial
+// state, then one entry per trial Ceres pushes.  Filled from the published decision records as the host reads them; the
+// costs and cost changes are completed by finish() once the initial cost is known (pba_solve reads it after the loop).
+struct Trajectory {
+  std::vector<pba_iteration_summary>& it;
+  explicit Trajectory(std::vector<pba_iteration_summary>& v, double radius) : it(v) {
+    it.clear();
+    pba_iteration_summary z{};
+    z.step_is_successful = z.step_is_valid = 1;
+    z.trust_region_radius = radius;
+    z.gradient_max_norm = NAN;
+    it.push_back(z);
+  }
+  // trial record d (kLm* fields): its gradient is the one at the state the trial started from, i.e. the state the last
+  // entry ended in, if that entry has none yet (the initial state, an accepted step)
+  void trial(const double* d) {
+    if (std::isnan(it.back().gradient_max_norm)) it.back().gradient_max_norm = d[kLmGradNorm];
+    const double done = d[kLmDone];
+    if (done != 0.0 && done != kDoneRadius) return;  // a tolerance or the invalid-step limit: Minimize returns first
+    pba_iteration_summary x{};
+    x.iteration = (int)it.size();
+    x.step_is_valid = d[kLmStatus] == 0.0 && d[kLmModel] > 0.0;
+    x.step_is_successful = d[kLmAccept] != 0.0;
+    x.cost = d[kLmCostNew];  // (the candidate's; finish() puts the current cost on invalid steps)
+    x.relative_decrease = x.step_is_valid ? d[kLmRel] : 0.0;
+    x.trust_region_radius = d[kLmRadius];
+    x.step_norm = x.step_is_valid ? d[kLmStepNorm] : 0.0;
+    x.gradient_max_norm = x.step_is_successful ? NAN : it.back().gradient_max_norm;
+    it.push_back(x);
+  }
+  void finish(double initial_cost) {
+    double cur = initial_cost;
+    it[0].cost = initial_cost;
+    for (size_t k = 1; k < it.size(); ++k) {
+      pba_iteration_summary& x = it[k];
+      if (!x.step_is_valid) {
+        x.cost = cur;
+        x.cost_change = 0.0;
+        continue;
+      }
+      x.cost_change = cur - x.cost;
+      if (x.step_is_successful) cur = x.cost;
+    }
+  }
+};
+
 // Single GPU: every trial is enqueued whole (lm_trial) and the accept/reject decision is taken on the device, so
 // the host only reads the decision record back; the breakdown is device time between stream events.
 int lm_loop_single(pba_engine* e, const pba_solver_options* o, pba_solver_summary* sum) {
@@ -4421,6 +4094,7 @@ int lm_loop_single(pba_engine* e, const pba_solver_options* o, pba_solver_summar
   const int n = std::max(0, opt.max_iterations);
   const DecideOpts dopt = decide_opts(opt);
   auto enqueue = [&](int i) { return lm_trial(e, dopt, (double)(i + 1), timed ? events.ev + 4 * (i & 1) : nullptr); };
+  Trajectory traj(G.history, opt.initial_trust_region_radius);
   if (n > 0)
     if (int rc = enqueue(0)) return rc;
   int iter = 0, set = 0;
@@ -4433,6 +4107,7 @@ int lm_loop_single(pba_engine* e, const pba_solver_options* o, pba_solver_summar
     double d[kLmFields];
     if (int rc = wait_decision(e, (double)(iter + 1), d)) return rc;
     set = (int)d[kLmSet];
+    traj.trial(d);
     if (timed) {
       const hipEvent_t* ev = events.ev + 4 * (iter & 1);
       float ms = 0.0f;
@@ -4467,6 +4142,7 @@ int lm_loop_single(pba_engine* e, const pba_solver_options* o, pba_solver_summar
   PBA_HIP(hipMemcpyAsync(init, G.lm_init.p, sizeof init, hipMemcpyDeviceToHost, e->stream));
   PBA_HIP(hipStreamSynchronize(e->stream));
   s.initial_cost = init[0];
+  traj.finish(init[0]);
   if (s.successful_steps == 0) cost = init[0];
   if (set == 1) {  // the current state's pieces are in set 1: make it set 0 for the host-driven entry points
     std::swap(G.blk_schur.p, G.blk_schur1.p);
@@ -4557,6 +4233,7 @@ int lm_loop(pba_engine* e, const pba_solver_options* o, const Collective* coll, 
   PBA_HIP(hipMemcpyAsync(G.lm.p, G.lm_h.data(), sizeof(double) * kLmFields, hipMemcpyHostToDevice, e->stream));
   const int n = std::max(0, opt.max_iterations);
   const DecideOpts dopt = decide_opts(opt);
+  Trajectory traj(G.history, opt.initial_trust_region_radius);
   if (n > 0)
     if (int rc = dist_trial(e, *coll, dopt, X, K, 1.0)) return rc;
   int iter = 0, set = 0;
@@ -4568,6 +4245,7 @@ int lm_loop(pba_engine* e, const pba_solver_options* o, const Collective* coll, 
     double d[kLmFields];
     if (int rc = wait_decision(e, (double)(iter + 1), d)) return rc;
     set = (int)d[kLmSet];
+    traj.trial(d);
     s.gradient_max_norm = d[kLmGradNorm];
     const double done = d[kLmDone];
     if (done != 0.0 && done != kDoneRadius) {
@@ -4588,6 +4266,7 @@ int lm_loop(pba_engine* e, const pba_solver_options* o, const Collective* coll, 
   }
   launch_accept(e, G.lm.p);
   PBA_HIP(hipStreamSynchronize(e->stream));
+  traj.finish(s.initial_cost);
   if (set == 1) {
     std::swap(G.blk_schur.p, G.blk_schur1.p);
     std::swap(G.blk_schur.n, G.blk_schur1.n);
@@ -4608,6 +4287,15 @@ extern "C" {
 int pba_solve(pba_engine* e, const pba_solver_options* o, pba_solver_summary* sum) {
   if (int rc = ensure_prepared(e)) return rc;
   return lm_loop(e, o, nullptr, nullptr, 0, sum);
+}
+
+int pba_solver_iterations(const pba_engine* e, int32_t capacity, pba_iteration_summary* out, int32_t* count) {
+  if (!e || !count || capacity < 0 || (capacity > 0 && !out)) return fail(PBA_ERR_INVALID_ARGUMENT, "bad arguments");
+  const std::vector<pba_iteration_summary>& h = e->gn.history;
+  const int n = std::min<int>(capacity, (int)h.size());
+  for (int i = 0; i < n; ++i) out[i] = h[i];
+  *count = (int)h.size();
+  return PBA_OK;
 }
 
 int pba_set_solver_timing(pba_engine* e, int32_t enable) {

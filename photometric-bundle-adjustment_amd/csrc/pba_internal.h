@@ -695,12 +695,6 @@ struct GnData {
   std::vector<CrLevelHost> cr_levels;  // block-cyclic-reduction level layout (offsets into cr_buf)
   int cr_pcr = -1;                     // the CR level whose rows parallel cyclic reduction solves (-1: root kernel)
   CrLevelHost pcr_bufs[2];             // PCR ping-pong buffers (D, U, b) for that level's rows
-  bool pcr_fused_opt = false, pcr_fused = false;  // PCR levels + solve in one data-flow launch (PBA_PCR_FUSED=1)
-  int pcr_levels = 0, pcr_epoch = 0, pcr_fused_per_cu = 1;
-  unsigned pcr_base = 0;
-  DevBuf<double> pcr_lv;                 // the one-launch PCR's level buffers (D, U, b per stride level)
-  DevBuf<int> pcr_flags;
-  DevBuf<unsigned> pcr_counter;
   DevBuf<double> cr_buf;
   bool force_skyline = false;
   size_t lin_floats = 0, schur_doubles = 0, schur_lds = 0;
@@ -762,6 +756,7 @@ struct GnData {
   DevBuf<float> intr_new_f;     // … and their fp32 copy (8 per camera)
   double* lm_host_d = nullptr;  // lm_h's device address
   bool phase_timing = false;    // pba_set_solver_timing: stream events around the LM phases
+  std::vector<pba_iteration_summary> history;  // the last LM solve's trajectory (pba_solver_iterations)
   int red_slots = 0;
 };
 
@@ -818,7 +813,6 @@ struct pba_engine {
   bool pairs_fresh = false;          // pairs hold T_th of the current poses (pba_set_state_device forms them)
   bool evaluated = false;
   bool timing = false;
-  bool no_cam_table = std::getenv("PBA_NO_CAM_TABLE") != nullptr;  // A/B switch: the C5 kernel without its camera table
   int last_grid = 0;                 // workgroups of the last evaluation launch (launch_mode)
   std::vector<hipEvent_t> ev_pool;   // start/stop pairs, reused
   int level = 0;                     // active pyramid level (its buffers are swapped into the fields above)

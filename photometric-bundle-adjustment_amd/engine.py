@@ -79,13 +79,21 @@ class SolverSummary(C.Structure):
         return d
 
 
+class IterationSummary(C.Structure):
+    """pba_iteration_summary (Ceres' IterationSummary fields, iteration_callback.h)."""
+    _fields_ = [("iteration", C.c_int32), ("step_is_successful", C.c_int32), ("step_is_valid", C.c_int32),
+                ("pad_", C.c_int32), ("cost", C.c_double), ("cost_change", C.c_double),
+                ("relative_decrease", C.c_double), ("trust_region_radius", C.c_double), ("step_norm", C.c_double),
+                ("gradient_max_norm", C.c_double)]
+
+
 # int (*pba_allreduce_fn)(void* user, double* d_buf, int64_t count)
 ALLREDUCE_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_int64)
 
 
 def build(force: bool = False) -> str:
     """Compile csrc/libpba.so for gfx950 with hipcc (in-tree)."""
-    args = ["make", "-s", "-C", CSRC]
+    args = ["make", "-s", "-j", str(min(8, os.cpu_count() or 1)), "-C", CSRC]
     if force:
         args.append("-B")
     subprocess.run(args + ["libpba.so"], check=True)
@@ -141,6 +149,7 @@ def lib():
         "pba_host_free": ([vp], C.c_int),
         "pba_set_interpolator": ([vp, i32], C.c_int),
         "pba_set_solver_timing": ([vp, i32], C.c_int),
+        "pba_solver_iterations": ([vp, i32, vp, C.POINTER(i32)], C.c_int),
         "pba_interpolator": ([vp], C.c_int),
         "pba_sample_image": ([vp, i32, i32, vp, vp], C.c_int),
         "pba_get_cost": ([vp, C.POINTER(C.c_double), C.POINTER(i32)], C.c_int),
@@ -388,6 +397,17 @@ class Engine:
     def set_solver_timing(self, enable: bool):
         """per-phase device timing of solve() (linearize_ms / solve_ms / cost_ms); off by default"""
         _check(self._L.pba_set_solver_timing(self._h, 1 if enable else 0), "pba_set_solver_timing")
+
+    def solver_iterations(self) -> dict:
+        """The last solve's trajectory (pba_solver_iterations: Ceres' Solver::Summary::iterations) as arrays."""
+        n = C.c_int32()
+        _check(self._L.pba_solver_iterations(self._h, 0, None, C.byref(n)), "pba_solver_iterations")
+        arr = (IterationSummary * max(n.value, 1))()
+        _check(self._L.pba_solver_iterations(self._h, n.value, arr, C.byref(n)), "pba_solver_iterations")
+        rows = arr[:n.value]
+        return {f: np.array([getattr(r, f) for r in rows], np.float64 if f not in (
+            "iteration", "step_is_successful", "step_is_valid") else np.int64) for f, _ in IterationSummary._fields_
+                if f != "pad_"}
 
     def solve(self, **options) -> dict:
         """pba_solve; options as solver_options() (Ceres' names and defaults, max_iterations 20)."""

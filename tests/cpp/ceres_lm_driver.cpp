@@ -24,9 +24,15 @@
 // unprojecting with the captured pointer (user memory, which Ceres does not write during a solve without a callback),
 // the GPU evaluator gets the blocks and enables the engine's target-intrinsics Jacobian.
 //
-// floor: Ceres' own per-evaluation floor — the same Problem (parameter blocks, local parameterisations, Huber, sizes)
-//        with a SizedCostFunction per block that writes constants, so "Jacobian & residual evaluation" is Ceres'
-//        bookkeeping alone (ProgramEvaluator, the Jacobian writer, the LocalParameterization products, the loss).
+// floor: the drop-in's floor on the drop-in's own trajectory — the gpu-mode Solve is run once while every evaluation's
+//        read-back (records or residuals, validity, the poses' P⁺) is recorded, then the SAME Solve (same Problem, the
+//        same GpuPhotometricCost / GpuReprojectionCost per block, the reference's LocalParameterizationSE3, Huber) is
+//        run again from the same initial state with an evaluator that only points the adapter at the recorded arrays:
+//        the same values give Ceres the same decisions, so both runs make the same evaluations, and "Jacobian &
+//        residual evaluation" of the second run is Ceres' own work (ProgramEvaluator, the Jacobian writer, the
+//        LocalParameterization products, the loss) plus the adapter's per-block copy — everything but the device's part
+//        (state upload, launch, read-back).  The summary is the second run's, with "replay_ok" saying whether it took
+//        exactly the recorded evaluations.
 // check = 0 (gpu mode): the plain adapter, without the protocol checks (the bench's C2 timing: the checks hash the whole
 //        state per Prepare and count every Evaluate with an atomic shared by Ceres' threads).
 //
@@ -137,31 +143,72 @@ class CheckedCost : public ceres::CostFunction {
   int host_, target_, point_, nf_;
 };
 
-// Ceres' floor (mode floor): a residual that costs next to nothing to evaluate but is a genuine nonlinear least-squares
-// term in (T_h, T_t, ρ) with its exact global Jacobians, so LM takes accepted steps (and Jacobian evaluations) as in the
-// real solve: r_k = c_k (ρ − 0.05) + 1e-3 sin(x_h[4] + c_k x_t[5]), c_k = k + 1.
-template <int R, int... N>
-class FloorCost : public ceres::SizedCostFunction<R, N...> {
+// The floor (mode floor): what one PrepareForEvaluation left for Evaluate to read — nothing when the adapter kept the
+// previous point (same point, no new work).
+struct Snapshot {
+  bool kept = false, jac = false;
+  std::vector<float> rec;      // records (jac) or residuals
+  std::vector<uint8_t> valid;
+  std::vector<double> pinv;    // the poses' P⁺ (jac, reference parameterisation)
+};
+
+// Pass 1: the drop-in, recording every evaluation's read-back (waits for the whole read-back: untimed pass).
+class RecordingEvaluator : public pba_ceres::GpuEvaluator {
  public:
-  bool Evaluate(double const* const* x, double* residuals, double** jacobians) const override {
-    double s[R], c[R];
-    for (int k = 0; k < R; ++k) {
-      const double ck = k + 1.0, a = x[0][4] + ck * x[1][5];
-      s[k] = std::sin(a);
-      c[k] = std::cos(a);
-      residuals[k] = 1e-2 * ck * (x[2][0] - 0.05) + 1e-3 * s[k];
+  RecordingEvaluator(pba_engine* e, std::vector<double*> poses, std::vector<double*> rho, std::vector<double*> intr,
+                     pba_ceres::PoseJacobian form, int n_blocks, int n_frames, std::vector<Snapshot>* out)
+      : GpuEvaluator(e, poses, rho, intr, form), nb_(n_blocks), nf_(n_frames), out_(out) {}
+  void PrepareForEvaluation(bool evaluate_jacobians, bool new_evaluation_point) override {
+    const long before = prepare_times().calls[0] + prepare_times().calls[1];
+    GpuEvaluator::PrepareForEvaluation(evaluate_jacobians, new_evaluation_point);
+    Snapshot s;
+    s.kept = prepare_times().calls[0] + prepare_times().calls[1] == before;
+    if (!s.kept) {
+      s.jac = has_jacobians();
+      for (int b = 0; b < nb_; b += chunk_blocks_) wait(b);
+      const int R = residuals_per_block(), rf = pba_record_floats(engine_);
+      if (s.jac) s.rec.assign(record(0), record(0) + (size_t)nb_ * rf);
+      else s.rec.assign(residuals(0), residuals(0) + (size_t)nb_ * R);
+      s.valid.assign(valid_src_, valid_src_ + nb_);
+      if (s.jac && pose_jacobian() == pba_ceres::PoseJacobian::kReferenceSE3) s.pinv.assign(pinv_src_, pinv_src_ + 42 * nf_);
     }
-    if (!jacobians) return true;
-    const int sizes[] = {N...};
-    for (size_t i = 0; i < sizeof(sizes) / sizeof(int); ++i)
-      if (jacobians[i]) std::memset(jacobians[i], 0, sizeof(double) * R * sizes[i]);
-    for (int k = 0; k < R; ++k) {
-      if (jacobians[0]) jacobians[0][7 * k + 4] = 1e-3 * c[k];
-      if (jacobians[1]) jacobians[1][7 * k + 5] = 1e-3 * (k + 1.0) * c[k];
-      if (jacobians[2]) jacobians[2][k] = 1e-2 * (k + 1.0);
-    }
-    return true;
+    out_->push_back(std::move(s));
   }
+
+ private:
+  int nb_, nf_;
+  std::vector<Snapshot>* out_;
+};
+
+// Pass 2: the same adapter reading the recorded arrays — the device's part (gather, upload, launch, read-back) removed.
+class ReplayEvaluator : public pba_ceres::GpuEvaluator {
+ public:
+  ReplayEvaluator(pba_engine* e, std::vector<double*> poses, std::vector<double*> rho, std::vector<double*> intr,
+                  pba_ceres::PoseJacobian form, const std::vector<Snapshot>* snaps)
+      : GpuEvaluator(e, poses, rho, intr, form), snaps_(snaps) {}
+  void PrepareForEvaluation(bool evaluate_jacobians, bool /*new_evaluation_point*/) override {
+    if (next_ >= snaps_->size()) {
+      ok_ = false;
+      return;
+    }
+    const Snapshot& s = (*snaps_)[next_++];
+    if (s.kept) return;
+    if (s.jac != evaluate_jacobians) ok_ = false;
+    async_ = false;
+    rec_src_ = s.jac ? s.rec.data() : nullptr;
+    res_ = s.rec.data();
+    res_stride_ = s.jac ? rec_ : R_;
+    valid_src_ = s.valid.data();
+    pinv_src_ = s.pinv.empty() ? nullptr : s.pinv.data();
+    have_point_ = true;
+    have_jac_ = s.jac;
+  }
+  bool replay_ok() const { return ok_ && next_ == snaps_->size(); }
+
+ private:
+  const std::vector<Snapshot>* snaps_;
+  size_t next_ = 0;
+  bool ok_ = true;
 };
 
 // ceres::PhotometricError<8> throws outside the EUCM domain (photometric_error.h:165-171); inside a solve that is an
@@ -251,8 +298,10 @@ int main(int argc, char** argv) {
   Protocol protocol;
   pba_engine* e = nullptr;
   std::unique_ptr<pba_ceres::GpuEvaluator> ev;
-  ceres::Problem::Options popt;
-  if (gpu) {
+  const bool engine = gpu || floor_mode;
+  std::vector<double*> intr_ptr;
+  const auto form = tangent ? pba_ceres::PoseJacobian::kTangent : pba_ceres::PoseJacobian::kReferenceSE3;
+  if (engine) {
     pba_options opt{0, kind, model, 0.0f};
     pba_ceres::check(pba_create(&opt, &e), "pba_create");
     pba_ceres::check(pba_set_cameras(e, nc, intr.data()), "cameras");
@@ -263,33 +312,13 @@ int main(int argc, char** argv) {
                      "points");
     pba_ceres::check(pba_set_blocks(e, nb, block_point.data(), block_target.data(), kind == 1 ? u_obs.data() : nullptr),
                      "blocks");
-    std::vector<double*> intr_ptr;
     if (intr_mode == 1)
       for (int c = 0; c < nc; ++c) intr_ptr.push_back(&intr[8 * c]);
-    const auto form = tangent ? pba_ceres::PoseJacobian::kTangent : pba_ceres::PoseJacobian::kReferenceSE3;
-    if (checked)
-      ev.reset(new CheckedEvaluator(e, pose_ptr, rho_ptr, intr_ptr, form, nb, &protocol));
-    else
-      ev.reset(new pba_ceres::GpuEvaluator(e, pose_ptr, rho_ptr, intr_ptr, form));
-    popt.evaluation_callback = ev.get();  // problem.h:185 (not owned)
   }
-  ceres::Problem problem(popt);
-  for (int i = 0; i < nf; ++i) {  // map_utils.h:330-337
-    ceres::LocalParameterization* lp =
-        gpu && tangent ? static_cast<ceres::LocalParameterization*>(new pba_ceres::SE3TangentParameterization)
-                       : new Sophus::test::LocalParameterizationSE3;  // the reference's own, in both modes
-    problem.AddParameterBlock(T[i].data(), 7, lp);
-  }
-  for (int i : fixed) problem.SetParameterBlockConstant(T[i].data());
-  if (kind == 1 && !opt_intr)
-    for (int c = 0; c < nc; ++c) {  // :340-345
-      problem.AddParameterBlock(&intr[8 * c], 8);
-      problem.SetParameterBlockConstant(&intr[8 * c]);
-    }
   // CPU photometric: one interpolator per keyframe image, host bearings per point
   using PE = ceres::PhotometricError<8>;
-  const bool ceres_pe = !gpu && kind == 0 && interp == 1 && model == pba_test::CAM_EUCM;
-  if (!gpu && !floor_mode && kind == 0 && interp == 1 && !ceres_pe) {
+  const bool ceres_pe = !engine && kind == 0 && interp == 1 && model == pba_test::CAM_EUCM;
+  if (!engine && kind == 0 && interp == 1 && !ceres_pe) {
     fprintf(stderr, "cpu mode: bicubic is the vendored PhotometricError<8>, EUCM cameras only\n");
     return 3;
   }
@@ -301,7 +330,7 @@ int main(int argc, char** argv) {
   std::vector<PE::Intrinsics, Eigen::aligned_allocator<PE::Intrinsics>> K6(nc);
   for (int c = 0; c < nc; ++c) K6[c] << intr[8 * c], intr[8 * c + 1], intr[8 * c + 2], intr[8 * c + 3], intr[8 * c + 4], intr[8 * c + 5];
   std::vector<double> host_int_d;
-  if (!gpu && !floor_mode && kind == 0) {
+  if (!engine && kind == 0) {
     for (int i = 0; i < nf; ++i) {
       bilin.emplace_back(new pba_test::BilinearInterpolator(&images[(size_t)i * W * H], H, W));
       grids.emplace_back(new pba_test::Grid(&images[(size_t)i * W * H], 0, H, 0, W));
@@ -317,33 +346,6 @@ int main(int argc, char** argv) {
         patches[p][k] = host_int[(size_t)8 * p + k];
       }
   }
-  for (int b = 0; b < nb; ++b) {  // :347-375
-    const int p = block_point[b], h = point_host[p], t = block_target[b];
-    ceres::LossFunction* loss = huber > 0 ? new ceres::HuberLoss(huber) : nullptr;
-    ceres::CostFunction* cf;
-    if (gpu) {
-      ceres::CostFunction* inner = kind == 0 ? static_cast<ceres::CostFunction*>(new pba_ceres::GpuPhotometricCost<8>(ev.get(), b, h, t))
-                                             : new pba_ceres::GpuReprojectionCost(ev.get(), b, h, t);
-      cf = checked ? new CheckedCost(inner, &protocol, h, t, p, nf) : inner;
-    } else if (floor_mode) {
-      cf = kind == 0 ? static_cast<ceres::CostFunction*>(new FloorCost<8, 7, 7, 1>) : new FloorCost<2, 7, 7, 1, 8>;
-    } else if (kind == 1) {
-      cf = new ceres::AutoDiffCostFunction<pba_test::GeometricFunctor, 2, 7, 7, 1, 8>(new pba_test::GeometricFunctor(
-          Eigen::Vector2d(u_obs[2 * b], u_obs[2 * b + 1]), Eigen::Vector2d(u_ref[2 * p], u_ref[2 * p + 1]),
-          &intr[8 * frame_cam[h]], model));
-    } else if (ceres_pe) {  // the vendored functor itself (it keeps references to the patch, bearings, image, K)
-      cf = new ceres::AutoDiffCostFunction<CeresPhotometric, 8, 7, 7, 1>(
-          new CeresPhotometric(new PE(patches[p], bearings[p], *bicub[t], K6[frame_cam[t]])));
-    } else {
-      using F = pba_test::PhotometricFunctor<8, pba_test::BilinearInterpolator>;
-      cf = new ceres::AutoDiffCostFunction<F, 8, 7, 7, 1>(
-          new F(&host_int_d[(size_t)8 * p], bearings[p], *bilin[t], &intr[8 * frame_cam[t]], model));
-    }
-    if (kind == 1)
-      problem.AddResidualBlock(cf, loss, T[h].data(), T[t].data(), &rho[p], &intr[8 * frame_cam[t]]);
-    else
-      problem.AddResidualBlock(cf, loss, T[h].data(), T[t].data(), &rho[p]);
-  }
 
   ceres::Solver::Options so;  // map_utils.h:376-381
   so.max_num_iterations = iters;
@@ -353,7 +355,77 @@ int main(int argc, char** argv) {
   so.parameter_tolerance = ptol;
   so.gradient_tolerance = gtol;
   ceres::Solver::Summary sum;
-  ceres::Solve(so, &problem, &sum);
+  // bundle_adjustment()'s problem build (map_utils.h:322-375) over the evaluator ev (nullptr: AutoDiff on the CPU),
+  // then ceres::Solve (:376-383)
+  auto solve = [&](pba_ceres::GpuEvaluator* evaluator, bool checked_costs) {
+    ceres::Problem::Options popt;
+    popt.evaluation_callback = evaluator;  // problem.h:185 (not owned)
+    ceres::Problem problem(popt);
+    for (int i = 0; i < nf; ++i) {  // map_utils.h:330-337
+      ceres::LocalParameterization* lp =
+          evaluator && tangent ? static_cast<ceres::LocalParameterization*>(new pba_ceres::SE3TangentParameterization)
+                               : new Sophus::test::LocalParameterizationSE3;  // the reference's own, in both modes
+      problem.AddParameterBlock(T[i].data(), 7, lp);
+    }
+    for (int i : fixed) problem.SetParameterBlockConstant(T[i].data());
+    if (kind == 1 && !opt_intr)
+      for (int c = 0; c < nc; ++c) {  // :340-345
+        problem.AddParameterBlock(&intr[8 * c], 8);
+        problem.SetParameterBlockConstant(&intr[8 * c]);
+      }
+    for (int b = 0; b < nb; ++b) {  // :347-375
+      const int p = block_point[b], h = point_host[p], t = block_target[b];
+      ceres::LossFunction* loss = huber > 0 ? new ceres::HuberLoss(huber) : nullptr;
+      ceres::CostFunction* cf;
+      if (evaluator) {
+        ceres::CostFunction* inner = kind == 0 ? static_cast<ceres::CostFunction*>(new pba_ceres::GpuPhotometricCost<8>(evaluator, b, h, t))
+                                               : new pba_ceres::GpuReprojectionCost(evaluator, b, h, t);
+        cf = checked_costs ? new CheckedCost(inner, &protocol, h, t, p, nf) : inner;
+      } else if (kind == 1) {
+        cf = new ceres::AutoDiffCostFunction<pba_test::GeometricFunctor, 2, 7, 7, 1, 8>(new pba_test::GeometricFunctor(
+            Eigen::Vector2d(u_obs[2 * b], u_obs[2 * b + 1]), Eigen::Vector2d(u_ref[2 * p], u_ref[2 * p + 1]),
+            &intr[8 * frame_cam[h]], model));
+      } else if (ceres_pe) {  // the vendored functor itself (it keeps references to the patch, bearings, image, K)
+        cf = new ceres::AutoDiffCostFunction<CeresPhotometric, 8, 7, 7, 1>(
+            new CeresPhotometric(new PE(patches[p], bearings[p], *bicub[t], K6[frame_cam[t]])));
+      } else {
+        using F = pba_test::PhotometricFunctor<8, pba_test::BilinearInterpolator>;
+        cf = new ceres::AutoDiffCostFunction<F, 8, 7, 7, 1>(
+            new F(&host_int_d[(size_t)8 * p], bearings[p], *bilin[t], &intr[8 * frame_cam[t]], model));
+      }
+      if (kind == 1)
+        problem.AddResidualBlock(cf, loss, T[h].data(), T[t].data(), &rho[p], &intr[8 * frame_cam[t]]);
+      else
+        problem.AddResidualBlock(cf, loss, T[h].data(), T[t].data(), &rho[p]);
+    }
+    ceres::Solve(so, &problem, &sum);
+  };
+
+  int replay_ok = -1;
+  if (floor_mode) {
+    // pass 1: the drop-in, recording its read-backs; then the same Solve from the same initial state over the recording
+    std::vector<Snapshot> snaps;
+    const std::vector<double> rho0 = rho, intr0 = intr;
+    {
+      RecordingEvaluator rec(e, pose_ptr, rho_ptr, intr_ptr, form, nb, nf, &snaps);
+      solve(&rec, false);
+    }
+    for (int i = 0; i < nf; ++i) std::memcpy(T[i].data(), &poses_in[7 * i], 7 * sizeof(double));
+    rho = rho0;
+    intr = intr0;
+    std::unique_ptr<ReplayEvaluator> rep(new ReplayEvaluator(e, pose_ptr, rho_ptr, intr_ptr, form, &snaps));
+    solve(rep.get(), false);
+    replay_ok = rep->replay_ok() ? 1 : 0;
+    ev = std::move(rep);
+  } else if (gpu) {
+    if (checked)
+      ev.reset(new CheckedEvaluator(e, pose_ptr, rho_ptr, intr_ptr, form, nb, &protocol));
+    else
+      ev.reset(new pba_ceres::GpuEvaluator(e, pose_ptr, rho_ptr, intr_ptr, form));
+    solve(ev.get(), checked);
+  } else {
+    solve(nullptr, false);
+  }
 
   std::ostringstream o;
   o << "{\"mode\":\"" << argv[1] << "\",\"checked\":" << (gpu && checked ? 1 : 0) << ",\"termination\":" << (int)sum.termination_type
@@ -387,7 +459,7 @@ int main(int argc, char** argv) {
   json_array(o, rho.data(), rho.size());
   o << ",\"intrinsics\":";
   json_array(o, intr.data(), intr.size());
-  o << ",\"refused_intrinsics\":" << (ev && ev->refused_intrinsics() ? 1 : 0);
+  o << ",\"refused_intrinsics\":" << (ev && ev->refused_intrinsics() ? 1 : 0) << ",\"replay_ok\":" << replay_ok;
   if (ev) {  // the adapter's own breakdown of PrepareForEvaluation ([residual-only, with Jacobians], seconds)
     const auto& t = ev->prepare_times();
     snprintf(buf, sizeof buf,

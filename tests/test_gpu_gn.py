@@ -348,20 +348,17 @@ def test_reduced_solvers_agree(solver, n_frames, monkeypatch):
     assert np.linalg.norm(dl - dl_ref) <= 1e-3 * np.linalg.norm(dl_ref)
 
 
-@pytest.mark.parametrize("fused", ["1", "0"])
 @pytest.mark.parametrize("pcr_cap", ["0", "1", "4", "16", "1000"])
 @pytest.mark.parametrize("n_frames", [37, 150, 300])
-def test_cyclic_reduction_large_levels(n_frames, pcr_cap, fused, monkeypatch):
+def test_cyclic_reduction_large_levels(n_frames, pcr_cap, monkeypatch):
     """Problems whose top cyclic-reduction levels exceed the single-workgroup tail (> 32 super-rows) take the
     per-level back-substitution launches; parallel cyclic reduction takes over once a level has at most
     PBA_PCR_CAP rows (0: cyclic reduction down to the root; 1000: PCR from level 0, no back-substitution; 4 / 16:
     CR levels, PCR, then back-substitution through the tail and the large levels).  The step must equal the band
-    Cholesky's, with the PCR levels and the final solve in one data-flow launch (pcr_fused_kernel, the default) and
-    as a launch per level."""
+    Cholesky's (the PCR levels a launch each, the last one also solving its decoupled rows)."""
     pb = synth.make_problem(n_frames=n_frames, n_points=20 * n_frames, width=376, height=240, seed=7 + n_frames,
                             border=12)
     monkeypatch.setenv("PBA_PCR_CAP", pcr_cap)
-    monkeypatch.setenv("PBA_PCR_FUSED", fused)
     steps = {}
     for solver in ("cr", "band"):
         monkeypatch.setenv("PBA_SOLVER", solver)
@@ -496,7 +493,7 @@ def test_set_frames_after_gn_reanalyses_the_problem():
         assert np.abs(o - b).max() > 1e-3 * np.abs(b).max()
 
 
-@pytest.mark.parametrize("model", [0, 1, 3])
+@pytest.mark.parametrize("model", [0, 1, 2, 3])
 @pytest.mark.parametrize("lam", [1e-4, 1e-1])
 def test_free_intrinsics_reduced_system_and_step(model, lam):
     """Free intrinsics (pba_set_optimize_intrinsics; optimize_intrinsics, map_utils.h:339-345) in the on-device Schur GN:

@@ -127,28 +127,27 @@ def test_fp16_records(P):
 
 @pytest.mark.parametrize("n_cams", [1, 2])
 @pytest.mark.parametrize("P", [21, 30])
-def test_multi_pixel_kernel_forms_agree_bitwise(P, n_cams, monkeypatch):
+def test_multi_pixel_kernel_forms_agree_bitwise(P, n_cams):
     """The 9-32 px kernel at a device state takes its camera constants three ways: once per lane from the camera
-    record (one-camera problems), from the LDS camera table (≤ 4 cameras), or from each block's tile
-    (PBA_NO_CAM_TABLE=1).  The same values in the same arithmetic: fp32 and fp16 records must be bit-identical."""
+    record (one-camera problems), from the LDS camera table (≤ 4 cameras), or from each block's tile (more cameras).
+    The per-block form is reached by the same problem registered with 6 cameras, the extra ones copies that no frame
+    uses: the same values in the same arithmetic, so fp32 and fp16 records must be bit-identical."""
     import torch
     rng = np.random.default_rng(P + n_cams)
     pat = rng.integers(-3, 4, (P, 2)).astype(np.float32)
-    intr = None
+    intr = np.array([synth.DEFAULT_INTRINSICS[synth.PINHOLE]] * n_cams, np.float64)
+    intr[:, :4] *= 320 / 752.0  # (explicit intrinsics are quoted for the image size)
     if n_cams == 2:
-        intr = np.array([synth.DEFAULT_INTRINSICS[synth.PINHOLE], synth.DEFAULT_INTRINSICS[synth.PINHOLE]], np.float64)
-        intr[:, :4] *= 320 / 752.0  # (explicit intrinsics are quoted for the image size)
         intr[1, :4] *= [1.01, 0.99, 1.0, 1.0]
     pb = synth.make_problem(n_frames=9, n_points=400, width=320, height=200, pattern=pat, seed=80 + P, border=16,
                             intrinsics=intr, frame_cam=None if n_cams == 1 else np.arange(9) % 2)
+    pb6 = synth.Problem(**{**pb.__dict__, "intrinsics": np.concatenate([intr, np.repeat(intr[:1], 6 - n_cams, 0)])})
     poses = torch.from_numpy(np.ascontiguousarray(pb.poses)).cuda()
     rho = torch.from_numpy(np.ascontiguousarray(pb.rho)).cuda()
     out = {}
-    for form in ("default", "per-block"):
-        if form == "per-block":
-            monkeypatch.setenv("PBA_NO_CAM_TABLE", "1")
+    for form, prob in (("default", pb), ("per-block", pb6)):
         with E.Engine(pb.kind, pb.model) as eng:
-            eng.set_problem(pb)
+            eng.set_problem(prob)
             eng.evaluate_state_device(poses.data_ptr(), rho.data_ptr(), True)
             r32, v32 = eng.records()
             c32 = eng.block_costs().copy()
