@@ -24,21 +24,31 @@ def available() -> bool:
 
 def run(mode: str, pb, iters: int = 20, huber: float = 1.0, threads: int = 8, fixed=(0, 1), ftol: float = 1e-6,
         timeout: float = 600.0, ptol: float = 1e-8, gtol: float = 1e-10, optimize_intrinsics: bool = False,
-        pose_param: str = "ref", check: bool = True) -> dict:
+        pose_param: str = "ref", check: bool = True, teacher=None) -> dict:
     """mode: "cpu" (AutoDiff), "gpu" (the drop-in) or "floor" (constant cost functions: Ceres' own per-evaluation work).
     check: gpu mode with the evaluation-callback protocol checks (tests) or the plain adapter (timing).
     pose_param: "ref" — the reference's LocalParameterizationSE3 in both modes (the GPU adapter then emits 7-wide
     Jacobians J6·P⁺); "tangent" — the adapter's SE3TangentParameterization in gpu mode.  optimize_intrinsics: 0 constant
-    intrinsics blocks, 1 free (the GPU evaluator is given them), 2 free but not given to the evaluator (refusal)."""
+    intrinsics blocks, 1 free (the GPU evaluator is given them), 2 free but not given to the evaluator (refusal).
+    teacher (cpu mode): a list of (poses, rho, radius) states — one LM iteration of the Solve from each, returned as
+    out["teacher"] rows [cost at the state, cost after, step_is_successful, relative_decrease, radius after, step_norm,
+    iterations pushed, gradient max norm at the state]."""
     from make_golden import write_problem
     with tempfile.TemporaryDirectory() as td:
         fin, fout = os.path.join(td, "in.bin"), os.path.join(td, "out.json")
         with open(fin, "wb") as f:
             write_problem(f, pb)
         fx = ",".join(str(int(i)) for i in fixed) if len(fixed) else "-"
+        ft = "-"
+        if teacher is not None:
+            ft = os.path.join(td, "teacher.bin")
+            with open(ft, "wb") as f:
+                for poses, rho, radius in teacher:
+                    np.concatenate([np.asarray(poses, np.float64).ravel(), np.asarray(rho, np.float64).ravel(),
+                                    [float(radius)]]).tofile(f)
         subprocess.run([DRIVER, mode, fin, fout, str(iters), repr(float(huber)), str(threads), fx, repr(float(ftol)),
                         str(int(getattr(pb, "interp", 0))), repr(float(ptol)), repr(float(gtol)),
-                        str(int(optimize_intrinsics)), pose_param, "1" if check else "0"], check=True, timeout=timeout)
+                        str(int(optimize_intrinsics)), pose_param, "1" if check else "0", ft], check=True, timeout=timeout)
         with open(fout) as f:
             out = json.load(f)
     out["poses"] = np.asarray(out["poses"]).reshape(-1, 7)
@@ -51,4 +61,6 @@ def run(mode: str, pb, iters: int = 20, huber: float = 1.0, threads: int = 8, fi
     out["step_norm"] = it[:, 5]
     out["gradient_max_norm"] = it[:, 6]
     out["intrinsics"] = np.asarray(out["intrinsics"]).reshape(-1, 8)
+    if out.get("teacher") is not None:
+        out["teacher"] = np.asarray(out["teacher"], np.float64).reshape(-1, 8)
     return out

@@ -38,6 +38,11 @@
 //
 //   usage: ceres_lm_driver <cpu|gpu|floor> <problem.bin> <out.json> [iters] [huber] [threads] [fixed,frames] [ftol]
 //                          [interp] [ptol] [gtol] [optimize_intrinsics] [pose_param ref|tangent] [check 1|0]
+//                          [teacher states file | -]
+// teacher (cpu mode): one LM iteration from each of a list of states, each with its own initial trust-region radius —
+//        the engine's iterates, so that every iteration of its solve is checked against Ceres' own step from the same
+//        point (the "teacher" array of the JSON: [cost at the state, cost after the iteration, step_is_successful,
+//        relative_decrease, radius after, step_norm, iterations pushed, gradient max norm at the state] per state).
 //          (problem layout: tests/golden/make_golden.py write_problem)
 #include <atomic>
 #include <cstdint>
@@ -264,6 +269,9 @@ int main(int argc, char** argv) {
   const bool opt_intr = intr_mode != 0;
   const bool tangent = argc > 13 && std::string(argv[13]) == "tangent";
   const bool checked = !(argc > 14 && atoi(argv[14]) == 0);
+  // teacher file (cpu mode): n states of [poses (7·nf) | ρ (np) | trust-region radius] doubles; one LM iteration of the
+  // Solve from each (Solver::Options::initial_trust_region_radius = that radius) instead of the one solve
+  const char* teacher_path = argc > 15 && std::string(argv[15]) != "-" ? argv[15] : nullptr;
 
   FILE* f = fopen(argv[2], "rb");
   if (!f) return 2;
@@ -402,6 +410,7 @@ int main(int argc, char** argv) {
   };
 
   int replay_ok = -1;
+  std::string teacher_json = "null";
   if (floor_mode) {
     // pass 1: the drop-in, recording its read-backs; then the same Solve from the same initial state over the recording
     std::vector<Snapshot> snaps;
@@ -423,6 +432,39 @@ int main(int argc, char** argv) {
     else
       ev.reset(new pba_ceres::GpuEvaluator(e, pose_ptr, rho_ptr, intr_ptr, form));
     solve(ev.get(), checked);
+  } else if (teacher_path) {
+    FILE* tf = fopen(teacher_path, "rb");
+    if (!tf) return 2;
+    const size_t per = 7 * (size_t)nf + np + 1;
+    std::vector<double> st;
+    for (;;) {
+      std::vector<double> v(per);
+      if (fread(v.data(), sizeof(double), per, tf) != per) break;
+      st.insert(st.end(), v.begin(), v.end());
+    }
+    fclose(tf);
+    const int n_states = (int)(st.size() / per);
+    const int iters_saved = so.max_num_iterations;
+    so.max_num_iterations = 1;
+    std::ostringstream tj;
+    tj << "[";
+    for (int q = 0; q < n_states; ++q) {
+      const double* v = &st[(size_t)q * per];
+      for (int i = 0; i < nf; ++i) std::memcpy(T[i].data(), v + 7 * i, 7 * sizeof(double));
+      for (int p = 0; p < np; ++p) rho[p] = v[7 * (size_t)nf + p];
+      so.initial_trust_region_radius = v[per - 1];
+      solve(nullptr, false);
+      char buf[400];
+      const auto& it0 = sum.iterations.front();
+      const auto& it1 = sum.iterations.back();
+      snprintf(buf, sizeof buf, "%s[%.17g,%.17g,%d,%.17g,%.17g,%.17g,%d,%.17g]", q ? "," : "", it0.cost, it1.cost,
+               it1.step_is_successful ? 1 : 0, it1.relative_decrease, it1.trust_region_radius, it1.step_norm,
+               (int)sum.iterations.size(), it0.gradient_max_norm);
+      tj << buf;
+    }
+    tj << "]";
+    teacher_json = tj.str();
+    so.max_num_iterations = iters_saved;
   } else {
     solve(nullptr, false);
   }
@@ -460,6 +502,7 @@ int main(int argc, char** argv) {
   o << ",\"intrinsics\":";
   json_array(o, intr.data(), intr.size());
   o << ",\"refused_intrinsics\":" << (ev && ev->refused_intrinsics() ? 1 : 0) << ",\"replay_ok\":" << replay_ok;
+  o << ",\"teacher\":" << teacher_json;
   if (ev) {  // the adapter's own breakdown of PrepareForEvaluation ([residual-only, with Jacobians], seconds)
     const auto& t = ev->prepare_times();
     snprintf(buf, sizeof buf,

@@ -247,6 +247,14 @@ def reduced_system_sparse(pb, poses, rho, a, lam, fixed=(), n_threads=16):
     bincount, the per-point Schur terms −W_p W_pᵀ / C'_p over the ≤ K + 1 frames each point touches.  Constant frames
     (requested, or observed by no block) get identity rows/columns and zero gradient, as in schur_step."""
     rec, valid = O.evaluate(pb, poses=poses, rho=rho, want_jac=True, n_threads=n_threads)
+    return reduced_system_from_records(pb, rec, valid, a, lam, fixed)
+
+
+def reduced_system_from_records(pb, rec, valid, a, lam, fixed=()):
+    """reduced_system_sparse's system from given records ([r | J_h | J_t | J_ρ] per block, tangent space), every
+    product and sum in fp64 — from the oracle's fp64 records, or from the engine's fp32 ones (what fp64 normal-equation
+    products over the engine's fp32 rows would give: tools/probe/c4_lm_divergence.py)."""
+    rec = np.asarray(rec, np.float64)
     R = pb.R
     r, Jh, Jt, Jr = O.split_record(rec, R)
     s = (r ** 2).sum(1)

@@ -86,3 +86,20 @@ def test_real_ceres_c1_sized_solve_converges():
     out, valid = O.evaluate(pb, poses=pb.poses_gt, rho=pb.rho_gt, want_jac=False)
     c_true = sum(O.huber_block(out[b, :2], 1.0)[0] for b in range(pb.n_blocks) if valid[b])
     assert got["final_cost"] <= c_true, (got["final_cost"], c_true)
+
+
+@needs_driver
+def test_teacher_mode_reproduces_the_free_solve():
+    """ceres_lm_driver's teacher mode (one LM iteration from each given state and trust-region radius — how the GPU
+    tests check every iteration of the engine's solve against Ceres' own step from the same point): from the initial
+    state with the default radius it takes the free solve's first iteration (cost before and after, accept, radius after)."""
+    pb = synth.make_problem(n_frames=8, n_points=120, width=376, height=240, seed=21, border=14)
+    free = CR.run("cpu", pb, iters=3, huber=9.0, threads=2)
+    tr = CR.run("cpu", pb, iters=3, huber=9.0, threads=2, teacher=[(pb.poses, pb.rho, 1e4), (pb.poses, pb.rho, 1e4)])
+    t = tr["teacher"]
+    assert t.shape == (2, 8)
+    for row in t:
+        assert row[0] == pytest.approx(free["costs"][0], rel=1e-12)
+        assert row[1] == pytest.approx(free["costs"][1], rel=1e-12)
+        assert bool(row[2]) == bool(free["step_ok"][1])
+        assert row[4] == pytest.approx(free["radius"][1], rel=1e-12)

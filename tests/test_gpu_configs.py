@@ -261,7 +261,7 @@ def test_c2_floor_replays_the_dropin_trajectory(c2):
     assert fl["jacobian_evaluations"] == got["jacobian_evaluations"]
     assert fl["residual_evaluations"] == got["residual_evaluations"]
     assert np.array_equal(fl["step_ok"], got["step_ok"])
-    np.testing.assert_allclose(fl["costs"], got["costs"], rtol=1e-12)
+    np.testing.assert_allclose(fl["costs"], got["costs"], rtol=1e-7)  # (two runs: Ceres' threaded sums differ ~1e-9)
     print(f"\nC2 floor: J evaluation {1e3 * fl['jacobian_evaluation_s'] / fl['jacobian_evaluations']:.3f} ms vs drop-in "
           f"{1e3 * got['jacobian_evaluation_s'] / got['jacobian_evaluations']:.3f} ms")
 
@@ -401,36 +401,85 @@ def test_c4_reduced_system_and_step_against_fp64_reference(c4_render, lam):
     assert ep <= (1e-4 if lam < 1e-2 else 1e-6), ep
 
 
-@needs_ceres
-def test_c4_engine_lm_matches_ceres_cpu(c4_render):
-    """The reference's whole bundle-adjustment solve at full C4 size: pba_solve against real Ceres 2.0.0 LM (SPARSE_SCHUR,
-    AutoDiff over the restated photometric functor, the reference's LocalParameterizationSE3, 2 constant keyframes) with
-    BundleAdjustmentOptions' max_num_iterations = 20 (map_utils.h:318, sfm.cpp:1910) and Ceres' default tolerances, both
-    trajectories taken from ONE solve each (pba_solver_iterations against Solver::Summary::iterations): the same number of
-    iterations, the same accept/reject sequence, the same termination, and every iteration's cost (the new state's on an
-    accepted step, the candidate's on a rejected one, trust_region_minimizer.cc:124) within the north star's 1e-5
-    relative.  The initial cost is the fp32 residuals' sum against Ceres' fp64 one: 3e-8 (measured 1.5e-8, round 4)."""
+@pytest.fixture(scope="module")
+def c4_lm(c4_render):
+    """The reference's whole bundle-adjustment solve at full C4 size, both ways, each trajectory from ONE solve:
+    pba_solve (pba_solver_iterations) and real Ceres 2.0.0 LM (SPARSE_SCHUR, AutoDiff over the restated photometric
+    functor, the reference's LocalParameterizationSE3, 2 constant keyframes; Solver::Summary::iterations), with
+    BundleAdjustmentOptions' max_num_iterations = 20 (map_utils.h:318, sfm.cpp:1910) and Ceres' default tolerances.
+    Plus the engine's iterates: the state after k = 0 … 19 iterations (pba_solve of k iterations from the same initial
+    state — bit-reproducible, so the prefix of the 20-iteration solve) with the trust-region radius it carries."""
     pbh, images = c4_render
     iters = 20
     ref = CR.run("cpu", pbh, iters=iters, huber=9.0, threads=THREADS, timeout=1500)
+    states = []
     with c4_engine(pbh, images) as eng:
         summ = eng.solve(max_iterations=iters)
         traj = eng.solver_iterations()
+        for k in range(iters):
+            eng.set_state(pbh.poses, pbh.rho)
+            sk = eng.solve(max_iterations=k)
+            tk = eng.solver_iterations()
+            # the prefix of the 20-iteration solve, bit for bit
+            assert np.array_equal(tk["cost"], traj["cost"][:k + 1]), k
+            poses, rho = eng.get_state()
+            states.append((poses, rho, traj["trust_region_radius"][k]))
+    return pbh, ref, summ, traj, states
+
+
+@needs_ceres
+def test_c4_engine_lm_matches_ceres_cpu_free_running(c4_lm):
+    """The two 20-iteration solves side by side.  Both take the same steps and the same costs (1e-5 relative, the north
+    star's bound) until the trajectories part: this problem amplifies any difference in the iterates by ~×10 per
+    iteration once the trust region has grown (radius 6.6e7 at iteration 8: λ = 1.5e-8, an almost undamped step on
+    weakly observed inverse distances) — real Ceres against itself with 8 and 1 threads (fp64, only the summation order
+    differs) goes 1e-14 → 1e-9 over the 20 iterations.  Measured (round 5): costs 1.5e-8 … 4.6e-6 relative
+    through iteration 7, 5.7e-5 at iteration 8, the first rejected step at 12 in both.  Asserted: iterations 0-7 within
+    1e-5 with identical accept flags, the initial cost within 3e-8 (fp32 residuals; measured 1.5e-8).  Every one of the 20
+    iterations is pinned from the engine's own iterates in the next test."""
+    pbh, ref, summ, traj, _ = c4_lm
     n = min(len(traj["cost"]), len(ref["costs"]))
     rel = np.abs(traj["cost"][:n] - ref["costs"][:n]) / np.abs(ref["costs"][:n])
     rows = [f"{k:2d} {'+' if traj['step_is_successful'][k] else '-'}{'+' if ref['step_ok'][k] else '-'} "
-            f"{traj['cost'][k]:.10e} {ref['costs'][k]:.10e} {rel[k]:.2e} radius {traj['trust_region_radius'][k]:.3e} "
-            f"step {traj['step_norm'][k]:.3e} / {ref['step_norm'][k]:.3e}" for k in range(n)]
+            f"{traj['cost'][k]:.10e} {ref['costs'][k]:.10e} {rel[k]:.2e} radius {traj['trust_region_radius'][k]:.3e} / "
+            f"{ref['radius'][k]:.3e} step {traj['step_norm'][k]:.3e} / {ref['step_norm'][k]:.3e}" for k in range(n)]
     print(f"\nC4 LM, 20 iterations: engine {summ['successful_steps']}/{summ['unsuccessful_steps']} "
           f"({summ['stop_reason']}), Ceres {ref['successful_steps'] - 1}/{ref['unsuccessful_steps']} ({ref['message']})\n"
           "it ok(engine,Ceres) engine cost / Ceres cost / relative difference\n" + "\n".join(rows))
-    assert len(traj["cost"]) == len(ref["costs"]), (len(traj["cost"]), len(ref["costs"]))
-    assert np.array_equal(traj["step_is_successful"].astype(bool), ref["step_ok"])
-    assert summ["successful_steps"] == ref["successful_steps"] - 1, (summ, ref["message"])
-    assert summ["unsuccessful_steps"] == ref["unsuccessful_steps"], (summ, ref["message"])
-    assert summ["iterations"] == len(ref["costs"]) - 1 or summ["stop_reason"] in ("function_tolerance", "parameter_tolerance")
+    assert len(traj["cost"]) == 21 and len(ref["costs"]) == 21
     assert rel[0] <= 3e-8, rel[0]
-    assert rel.max() <= 1e-5, rel
+    assert np.array_equal(traj["step_is_successful"][:8].astype(bool), ref["step_ok"][:8])
+    assert rel[:8].max() <= 1e-5, rel[:8]
+
+
+@needs_ceres
+@pytest.mark.timeout(1500)
+def test_c4_every_engine_iteration_matches_a_ceres_iteration(c4_lm):
+    """Every one of the engine's 20 LM iterations against Ceres' own iteration from the same point: from the engine's
+    iterate k (state and trust-region radius), real Ceres runs ONE LM iteration (ceres_lm_driver teacher mode:
+    Solver::Options::initial_trust_region_radius = the engine's radius) and must take the engine's decision at iteration
+    k + 1 — accept or reject — with the cost at the iterate within 3e-8 (fp32 residuals) and the cost after the iteration
+    (the new state's, or the rejected candidate's) within the north star's 1e-5 relative."""
+    pbh, ref, summ, traj, states = c4_lm
+    t = CR.run("cpu", pbh, iters=1, huber=9.0, threads=THREADS, timeout=2400, teacher=states)["teacher"]
+    assert t.shape[0] == len(states)
+    cur = traj["cost"][0]
+    rows, bad = [], []
+    for k in range(len(states)):
+        e_ok = bool(traj["step_is_successful"][k + 1])
+        c_ok = bool(t[k, 2]) and t[k, 6] == 2
+        e_before, e_after = cur, traj["cost"][k + 1]
+        r0 = abs(e_before - t[k, 0]) / t[k, 0]
+        r1 = abs(e_after - t[k, 1]) / abs(t[k, 1])
+        rows.append(f"{k + 1:2d} {'+' if e_ok else '-'}{'+' if c_ok else '-'} at {r0:.1e} after {r1:.2e} "
+                    f"(engine {e_after:.10e}, Ceres {t[k, 1]:.10e}) radius {states[k][2]:.3e} λ {1 / states[k][2]:.2e} "
+                    f"step {traj['step_norm'][k + 1]:.4e} / {t[k, 5]:.4e}")
+        if e_ok != c_ok or r0 > 3e-8 or r1 > 1e-5:
+            bad.append(k + 1)
+        if e_ok:
+            cur = e_after
+    print("\nC4 LM, each engine iteration against one Ceres iteration from the engine's iterate:\n" + "\n".join(rows))
+    assert not bad, bad
 
 
 # ---------------------------------------------------------------------------------------------------- C5
@@ -478,3 +527,52 @@ def test_c5_style_full_size_pyramid_fp16():
         s = eng.solve_pyramid(max_iterations=4)
         assert eng.level()[0] == 0
     assert s["final_cost"] < s["initial_cost"], s
+
+
+@needs_ceres
+@pytest.mark.timeout(1500)
+def test_c4_lm_step_sensitivity_and_fp64_products(c4_lm, c4_render):
+    """Why the free-running C4 trajectories part after iteration 7, measured at the engine's iterates k (its state and
+    λ = 1/radius):
+      * the device step (fp32 rows, fp32 JᵀJ block products on the matrix cores, fp64 sums) — step_dev;
+      * the same engine's fp32 records with every product and sum in fp64 — step_f64p: what fp64 matrix-core products
+        (v_mfma_f64_16x16x4f64) in linearize_kernel would give, since its rows are these fp32 rows;
+      * the oracle's fp64 records in fp64 — step_ref (the reference's arithmetic).
+    If |step_f64p − step_ref| ≈ |step_dev − step_ref| the fp32 JᵀJ products are not what separates the engine from the
+    fp64 reference: the fp32 rows are (the north star's fp32 evaluation), amplified by the weakly damped system.  The
+    reference itself is that sensitive: real Ceres against itself with THREADS and 3 threads (fp64, only the summation
+    order differs) is printed beside it.  Asserted: fp64 products would not bring the step more than 2× closer to the
+    fp64 reference at any iterate."""
+    pbh, images = c4_render
+    _, ref, _, traj, states = c4_lm
+    rows, ratios = [], []
+    with c4_engine(pbh, images) as eng:
+        for k in (0, 4, 8, 11, 16):
+            poses, rho, radius = states[k]
+            lam = 1.0 / radius
+            eng.set_state(poses, rho)
+            eng.gn_linearize()
+            _, st = eng.gn_step(lam)
+            assert st == 0
+            dp_dev = eng.gn_last_step()[0].ravel()
+            eng.set_state(poses, rho)
+            eng.evaluate(True)
+            rec32, v32 = eng.records()
+            at = synth.Problem(**{**pbh.__dict__, "poses": poses, "rho": rho})
+            S_a, g_a, _ = GR.reduced_system_from_records(at, rec32, v32, 9.0, lam, (0, 1))
+            S_r, g_r, _ = GR.reduced_system_sparse(at, poses, rho, 9.0, lam, (0, 1))
+            dp_a = np.linalg.solve(S_a, -g_a)
+            dp_r = np.linalg.solve(S_r, -g_r)
+            nr = np.linalg.norm(dp_r)
+            e_dev, e_a, e_da = (np.linalg.norm(dp_dev - dp_r) / nr, np.linalg.norm(dp_a - dp_r) / nr,
+                                np.linalg.norm(dp_dev - dp_a) / nr)
+            ratios.append(e_dev / max(e_a, 1e-300))
+            rows.append(f"iterate {k:2d} λ {lam:.2e} |step| {nr:.3e}: dev−ref {e_dev:.2e}, fp64-products−ref {e_a:.2e}, "
+                        f"dev−fp64-products {e_da:.2e}")
+    other = CR.run("cpu", pbh, iters=20, huber=9.0, threads=3, timeout=2400)
+    m = min(len(other["costs"]), len(ref["costs"]))
+    rc = np.abs(other["costs"][:m] - ref["costs"][:m]) / np.abs(ref["costs"][:m])
+    print("\nC4 step sensitivity (pose steps, relative to the fp64 reference step):\n" + "\n".join(rows) +
+          f"\nCeres {THREADS} vs 3 threads, per-iteration cost: " + " ".join(f"{x:.1e}" for x in rc) +
+          f"\n  accept flags equal: {np.array_equal(other['step_ok'][:m], ref['step_ok'][:m])}")
+    assert max(ratios) <= 2.0, ratios
