@@ -123,16 +123,20 @@ def c2_dropin(pb_c4, images_host, threads: int):
     # the plain adapter (no protocol checks: the tests run those), its floor (the same Solve replayed over the drop-in's
     # recorded read-backs: Ceres' own work plus the adapter's per-block copy on the drop-in's own trajectory, i.e.
     # everything but the device's part), and the CPU AutoDiff path — same Solve options
-    # each mode twice, interleaved, the faster run of each reported (the box's host is shared: a 16-CPU cgroup quota)
+    # each mode three times, interleaved, the median run of each reported (the box's host is shared: a 16-CPU cgroup quota;
+    # single runs of these ~3-ms evaluations vary by ±10 %)
     runs = {m: [] for m in ("gpu", "cpu", "floor")}
-    for _ in range(2):
+    for _ in range(3):
         runs["gpu"].append(CR.run("gpu", pb, iters=10, huber=9.0, threads=threads, check=False))
         runs["cpu"].append(CR.run("cpu", pb, iters=10, huber=9.0, threads=threads))
         runs["floor"].append(CR.run("floor", pb, iters=10, huber=9.0, threads=threads))
-    best = {m: min(v, key=lambda r: r["jacobian_evaluation_s"] + r["residual_evaluation_s"]) for m, v in runs.items()}
+    best = {m: sorted(v, key=lambda r: r["jacobian_evaluation_s"] + r["residual_evaluation_s"])[len(v) // 2]
+            for m, v in runs.items()}
     g, c, fl = best["gpu"], best["cpu"], best["floor"]
     out["gpu_dropin"], out["cpu_autodiff"], out["ceres_floor"] = per_call(g), per_call(c), per_call(fl)
-    out["runs_per_mode"] = 2
+    out["runs_per_mode"] = 3
+    out["jacobian_evaluation_ms_runs"] = {m: [1e3 * r["jacobian_evaluation_s"] / max(r["jacobian_evaluations"], 1)
+                                              for r in v] for m, v in runs.items()}
     out["blocks"] = pb.n_blocks
     out["speedup_jacobian_evaluation"] = out["cpu_autodiff"]["jacobian_evaluation_ms"] / out["gpu_dropin"]["jacobian_evaluation_ms"]
     out["speedup_residual_evaluation"] = out["cpu_autodiff"]["residual_evaluation_ms"] / out["gpu_dropin"]["residual_evaluation_ms"]

@@ -57,7 +57,7 @@ constexpr int NV = 104;          // normal-equation products per residual row
 #define PBA_SCHUR_PTS 128
 #endif
 constexpr int SCHUR_PTS = PBA_SCHUR_PTS;   // points per Schur chunk (-DPBA_SCHUR_PTS: A/B builds)
-constexpr int SCHUR_W = 2048;    // points × local poses per Schur chunk (LDS budget: dynamic, 24 B each)
+constexpr int SCHUR_W = 2048;    // points × local poses per Schur chunk (LDS budget: dynamic, 48 B each)
 constexpr int SLOT_LIN_BASE = 42;  // H_hh(36) + g_h(6)
 constexpr int SLOT_LIN_T = 78;     // H_ht(36) + H_tt(36) + g_t(6)
 
@@ -127,12 +127,12 @@ __device__ __forceinline__ double lm_lambda(const LmView& v, double lambda) { re
 
 struct LinArgs {
   const int4* lin_rec;      // chunk slot → {block, point, pair | local target slot << 24, GN position (blk_schur index)}
-  float* blk_schur1;        // the second buffer set (device LM loop: the candidate's linearisation goes to the spare)
-  float* part_lin1;
+  double* blk_schur1;       // the second buffer set (device LM loop: the candidate's linearisation goes to the spare)
+  double* part_lin1;
   double* wg_red;           // per-chunk (Σ cost, Σ valid) slots, or nullptr
-  const int4* chunk_desc;   // first linearise position, count, n_targets, partial offset (floats)
-  float* blk_schur;
-  float* part_lin;
+  const int4* chunk_desc;   // first linearise position, count, n_targets, partial offset (slots)
+  double* blk_schur;
+  double* part_lin;
   int n_chunks;
   const double* lm;         // LM record: skip when the solve is done; spare: write the set the record does not hold
   bool spare;
@@ -147,29 +147,36 @@ __host__ __device__ constexpr int slot_of(int r, int c) {
     if (pa(v) == r && pb(v) == c) return v;
   return 255;
 }
-// MFMA 16×16 output held by lane l: C[4(l/16) + m][l%16], m = 0..3 → the four slots of lane l (upper triangle
-// only, so each product is written once), packed as bytes.
-__host__ __device__ constexpr unsigned slot_word(int lane) {
+// MFMA 16×16 output held by lane l, entry m = 0..3: v_mfma_f32_16x16x4f32 C[4(l/16) + m][l%16], v_mfma_f64_16x16x4f64
+// C[l/16 + 4m][l%16] (cdna_hip_programming.md: the f64 form has a layout of its own) → the four slots of lane l (upper
+// triangle only, so each product is written once), packed as bytes.
+__host__ __device__ constexpr unsigned slot_word(int lane, bool f64) {
   unsigned w = 0;
   for (int m = 0; m < 4; ++m) {
-    const int r = 4 * (lane >> 4) + m, c = lane & 15;
+    const int r = f64 ? (lane >> 4) + 4 * m : 4 * (lane >> 4) + m, c = lane & 15;
     w |= (unsigned)(r <= c ? slot_of(r, c) : 255) << (8 * m);
   }
   return w;
 }
 template <int... L>
-constexpr auto make_slot_table(std::integer_sequence<int, L...>) {
+constexpr auto make_slot_table(bool f64, std::integer_sequence<int, L...>) {
   struct T { unsigned w[64]; };
-  return T{{slot_word(L)...}};
+  return T{{slot_word(L, f64)...}};
 }
-__constant__ const auto kSlotTable = make_slot_table(std::make_integer_sequence<int, 64>{});
+__constant__ const auto kSlotTable = make_slot_table(false, std::make_integer_sequence<int, 64>{});
+__constant__ const auto kSlotTable64 = make_slot_table(true, std::make_integer_sequence<int, 64>{});
+
+// At most this many targets per linearise chunk (gn_prepare cuts chunks there): a wave's blocks then hold ≤ 4 target
+// runs, so its per-run product sets (fp64) fit the LDS the fp32 ones took for 8.
+constexpr int kChunkTargets = 4;
 
 
-// Normal-equation products by matrix cores: weighted rows X (R × 14, padded to LPB × 16 per block) give
-// XᵀX = Σ_k x_kᵀx_k as v_mfma_f32_16x16x4f32 steps (operand A = Xᵀ and B = X are the same register: lane l holds
-// X[4s + l/16][l%16]).  A chunk's blocks are ordered by target (gn_prepare), so the blocks of one target are
-// consecutive in a wave and their rows form ONE accumulation chain: a wave issues 16 MFMAs whatever its targets, and
-// stores one product set per distinct target instead of one per block.
+// Normal-equation products by matrix cores: weighted rows X (R × 14, padded to LPB × 16 per block; fp32) give
+// XᵀX = Σ_k x_kᵀx_k as v_mfma_f64_16x16x4f64 steps (operand A = Xᵀ and B = X are the same register: lane l holds
+// X[4s + l/16][l%16], converted to fp64) — the products of fp32 rows are exact in fp64, so the system is the Gram
+// matrix of the rows to fp64 rounding.  A chunk's blocks are ordered by target (gn_prepare), so the blocks of one
+// target are consecutive in a wave: each block's product set is added to its target run's sum, and a wave stores one
+// product set per distinct target (≤ kChunkTargets) instead of one per block.
 template <int KIND, int MODEL, int LPB>
 constexpr int kLinWaves = KIND == PBA_RESIDUAL_PHOTOMETRIC && MODEL == CAM_PINHOLE + 4 * INTERP_BILINEAR && LPB == 8 ? 8 : 1;
 
@@ -181,7 +188,7 @@ void linearize_kernel(const KernelArgs a, const LinArgs g) {
   constexpr int SPB = LPB / 4;              // MFMA steps per block
   constexpr int NVP = 108;                  // 104 products, padded
   constexpr int kTileW = KIND == PBA_RESIDUAL_PHOTOMETRIC ? BW * (int)sizeof(TileBlock) : 0;
-  constexpr int kRowsW = 64 * 16 * 4, kProdW = BW * NVP * 4;
+  constexpr int kRowsW = 64 * 16 * 4, kProdW = kChunkTargets * NVP * 8;
   constexpr int kArena = (kTileW > kRowsW ? (kTileW > kProdW ? kTileW : kProdW) : (kRowsW > kProdW ? kRowsW : kProdW));
   // per-wave arena, used in turn by the wave's tile blocks, its weighted rows and its per-target products
   // (each phase only touches the wave's own blocks; LDS is in order within a wave)
@@ -194,8 +201,8 @@ void linearize_kernel(const KernelArgs a, const LinArgs g) {
   const LmView lv = lm_view(g.lm);
   if (lv.done != 0.0) return;
   const bool s1 = (lv.set != 0.0) != g.spare;
-  float* const blk_schur = s1 ? g.blk_schur1 : g.blk_schur;
-  float* const part_lin = s1 ? g.part_lin1 : g.part_lin;
+  double* const blk_schur = s1 ? g.blk_schur1 : g.blk_schur;
+  double* const part_lin = s1 ? g.part_lin1 : g.part_lin;
   const int count = d.y, n_t = d.z, poff = d.w;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int lb = threadIdx.x / LPB, k = threadIdx.x % LPB, wb = lb % BW;
@@ -225,7 +232,7 @@ void linearize_kernel(const KernelArgs a, const LinArgs g) {
   // weighted row x̃ = √w · x  → products carry w (Ceres Corrector with ρ'' ≤ 0: J̃ = √ρ' J, r̃ = √ρ' r)
   // the product slot table (a vector load): after the row (one register fewer across it: the row's peak pressure spilled
   // at 8 waves/SIMD) and before any store of this kernel (a load issued after a store waits for the store too)
-  const unsigned slots = kSlotTable.w[lane];
+  const unsigned slots = kSlotTable64.w[lane];
   // rows outside the domain / of dead lanes are all zero (selects, not a zero weight: such a row may hold inf / NaN)
   const bool use = act && ok;
   const float sw = use ? sqrtf(w) : 0.0f;
@@ -251,35 +258,37 @@ void linearize_kernel(const KernelArgs a, const LinArgs g) {
     float op[BW * SPB];
 #pragma unroll
     for (int st = 0; st < BW * SPB; ++st) op[st] = sX[(4 * st + kq) * 16 + ci];
-    float* sP = reinterpret_cast<float*>(arena[wave]);
+    double* sP = reinterpret_cast<double*>(arena[wave]);
     const int nbw = min(max(count - wave * BW, 0), BW);  // live blocks of this wave (wave-uniform)
     const int lo = __builtin_amdgcn_readfirstlane(lt);     // lane 0 holds the wave's first block
-    auto flush = [&](const f32x4& acc, int slot) {
+    auto flush = [&](const v4f64& acc, int slot) {
 #pragma unroll
       for (int m = 0; m < 4; ++m) {
         const unsigned v = (slots >> (8 * m)) & 255u;
         if (v < (unsigned)NV) sP[slot * NVP + v] = acc[m];
       }
     };
-    // per block: its own chain (SPB steps); row 12 of the result, C[12][c] on lanes 48 + c, is the block's
+    // per block: its own chain (SPB steps); row 12 of the result, C[12][c] in entry 3 of lanes c < 16, is the block's
     // point-elimination data x̃_ρ·x̃_c → [H_ρρ, g_ρ, W_h(6), W_t(6), 0, 0] at its GN position (schur_kernel walks
     // them point by point); the block's products are then added to its target run's sum
-    const int pc = lane - 48, pq = pc < 12 ? pc + 2 : (pc < 14 ? pc - 12 : pc);
-    f32x4 tacc = {0.0f, 0.0f, 0.0f, 0.0f};
+    const int pc = lane < 16 ? lane : -1, pq = pc < 12 ? pc + 2 : (pc < 14 ? pc - 12 : pc);
+    v4f64 tacc = {0.0, 0.0, 0.0, 0.0};
     int cur = lo;
 #pragma unroll
     for (int b = 0; b < BW; ++b) {
       if (b < nbw) {
-        f32x4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
+        v4f64 acc = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-        for (int st = 0; st < SPB; ++st)
-          acc = __builtin_amdgcn_mfma_f32_16x16x4f32(op[b * SPB + st], op[b * SPB + st], acc, 0, 0, 0);
+        for (int st = 0; st < SPB; ++st) {
+          const double o = (double)op[b * SPB + st];
+          acc = __builtin_amdgcn_mfma_f64_16x16x4f64(o, o, acc, 0, 0, 0);
+        }
         const int gpb = __builtin_amdgcn_readlane(gpos, b * LPB);
-        if (pc >= 0) blk_schur[(long long)gpb * 16 + pq] = acc[0];
+        if (pc >= 0) blk_schur[(long long)gpb * 16 + pq] = acc[3];
         const int ltb = __builtin_amdgcn_readlane(lt, b * LPB);
         if (ltb != cur) {
           flush(tacc, cur - lo);
-          tacc = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+          tacc = v4f64{0.0, 0.0, 0.0, 0.0};
           cur = ltb;
         }
         tacc += acc;
@@ -294,7 +303,7 @@ void linearize_kernel(const KernelArgs a, const LinArgs g) {
   __syncthreads();
   // chunk partial slots, fixed summation order (wave, then slot): H_hh / g_h over every product set of the chunk,
   // H_ht / H_tt / g_t of local target j from the ≤ NW sets of j (one per wave that holds j's blocks)
-  auto sset = [&](int w, int i, int v) -> float { return reinterpret_cast<const float*>(arena[w])[i * NVP + v]; };
+  auto sset = [&](int w, int i, int v) -> double { return reinterpret_cast<const double*>(arena[w])[i * NVP + v]; };
   const int nout = SLOT_LIN_BASE + SLOT_LIN_T * n_t;
   for (int o = threadIdx.x; o < nout; o += kBlockThreads) {
     int v, j = -1;
@@ -310,7 +319,7 @@ void linearize_kernel(const KernelArgs a, const LinArgs g) {
       else if (q < 72) { const int r = (q - 36) / 6, c = (q - 36) % 6; v = 57 + upper_index(min(r, c), max(r, c)); }
       else v = 84 + (q - 72);
     }
-    float acc = 0.0f;
+    double acc = 0.0;
 #pragma unroll
     for (int w = 0; w < NW; ++w) {
       const int wl = s_wlo[w], wn = s_wn[w];
@@ -357,7 +366,7 @@ template <int MODEL, int PPL>
 __global__ __launch_bounds__(kBlockThreads) __attribute__((amdgpu_waves_per_eu(PBA_LINROWS_WAVES, 8)))
 void linearize_rows_kernel(const KernelArgs a, const LinArgs g) {
   constexpr int LPB = 8, BW = 64 / LPB, NW = kBlockThreads / 64, SPB = LPB / 4, NVP = 108;
-  constexpr int kTileW = BW * (int)sizeof(TileBlock), kRowsW = 64 * 16 * 4, kProdW = BW * NVP * 4;
+  constexpr int kTileW = BW * (int)sizeof(TileBlock), kRowsW = 64 * 16 * 4, kProdW = kChunkTargets * NVP * 8;
   constexpr int kArena = kTileW + kRowsW;
   static_assert(kProdW <= kArena, "product sets fit the arena");
   __shared__ __attribute__((aligned(16))) unsigned char arena[NW][kArena];
@@ -370,8 +379,8 @@ void linearize_rows_kernel(const KernelArgs a, const LinArgs g) {
   const LmView lv = lm_view(g.lm);
   if (lv.done != 0.0) return;
   const bool s1 = (lv.set != 0.0) != g.spare;
-  float* const blk_schur = s1 ? g.blk_schur1 : g.blk_schur;
-  float* const part_lin = s1 ? g.part_lin1 : g.part_lin;
+  double* const blk_schur = s1 ? g.blk_schur1 : g.blk_schur;
+  double* const part_lin = s1 ? g.part_lin1 : g.part_lin;
   const int count = d.y, n_t = d.z, poff = d.w;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int lb = threadIdx.x / LPB, k = threadIdx.x % LPB, wb = lb % BW;
@@ -438,30 +447,32 @@ void linearize_rows_kernel(const KernelArgs a, const LinArgs g) {
   {
     // as linearize_kernel: per block its (now weighted) products — row 12 the point-elimination data at its GN
     // position — added to its target run's sum, each run's 16×16 result scattered once as the 104 products
-    float* sP = reinterpret_cast<float*>(arena[wave]);  // over the tile and the rows (both consumed)
+    double* sP = reinterpret_cast<double*>(arena[wave]);  // over the tile and the rows (both consumed)
     const int nbw = min(max(count - wave * BW, 0), BW);
     const int lo = __builtin_amdgcn_readfirstlane(lt);
-    auto flush = [&](const f32x4& acc, int slot) {
+    auto flush = [&](const v4f64& acc, int slot) {
 #pragma unroll
       for (int m = 0; m < 4; ++m) {
         const unsigned v = (slots >> (8 * m)) & 255u;
         if (v < (unsigned)NV) sP[slot * NVP + v] = acc[m];
       }
     };
+    // (this kernel's block products are fp32 matrix-core chains over the block's ⌈P/8⌉ passes; the weighting, the
+    // point data and every sum after them are fp64)
     const int pc = lane - 48, pq = pc < 12 ? pc + 2 : (pc < 14 ? pc - 12 : pc);
-    f32x4 tacc = {0.0f, 0.0f, 0.0f, 0.0f};
+    v4f64 tacc = {0.0, 0.0, 0.0, 0.0};
     int cur = lo;
 #pragma unroll
     for (int b = 0; b < BW; ++b) {
       if (b < nbw) {
-        const float wb_ = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(w), b * LPB));
-        const f32x4 acc = accb[b] * wb_;
+        const double wb_ = (double)__int_as_float(__builtin_amdgcn_readlane(__float_as_int(w), b * LPB));
+        const v4f64 acc = {accb[b][0] * wb_, accb[b][1] * wb_, accb[b][2] * wb_, accb[b][3] * wb_};
         const int gpb = __builtin_amdgcn_readlane(gpos, b * LPB);
         if (pc >= 0) blk_schur[(long long)gpb * 16 + pq] = acc[0];
         const int ltb = __builtin_amdgcn_readlane(lt, b * LPB);
         if (ltb != cur) {
           flush(tacc, cur - lo);
-          tacc = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+          tacc = v4f64{0.0, 0.0, 0.0, 0.0};
           cur = ltb;
         }
         tacc += acc;
@@ -474,7 +485,7 @@ void linearize_rows_kernel(const KernelArgs a, const LinArgs g) {
     }
   }
   __syncthreads();
-  auto sset = [&](int w_, int i, int v) -> float { return reinterpret_cast<const float*>(arena[w_])[i * NVP + v]; };
+  auto sset = [&](int w_, int i, int v) -> double { return reinterpret_cast<const double*>(arena[w_])[i * NVP + v]; };
   const int nout = SLOT_LIN_BASE + SLOT_LIN_T * n_t;
   for (int o = threadIdx.x; o < nout; o += kBlockThreads) {
     int v, jt = -1;
@@ -490,7 +501,7 @@ void linearize_rows_kernel(const KernelArgs a, const LinArgs g) {
       else if (q < 72) { const int r = (q - 36) / 6, c = (q - 36) % 6; v = 57 + upper_index(min(r, c), max(r, c)); }
       else v = 84 + (q - 72);
     }
-    float acc = 0.0f;
+    double acc = 0.0;
 #pragma unroll
     for (int w_ = 0; w_ < NW; ++w_) {
       const int wl = s_wlo[w_], wn = s_wn[w_];
@@ -526,8 +537,8 @@ struct SchurArgs {
   const uchar2* pairs;    // (a, b) local pose pairs, a ≤ b
   const int2* pt_fb;       // chunk c's point p → {first GN block, block count} at c · SCHUR_PTS + p (padded table)
   const uint8_t* blk_lv;
-  const float* blk_schur;
-  const float* blk_schur1;  // buffer set 1 (device LM loop)
+  const double* blk_schur;
+  const double* blk_schur1;  // buffer set 1 (device LM loop)
   double* part_schur;
   double* pt_data;        // per GN point [H_ρρ, g_ρ, W_h(6)] (undamped)
   int n_chunks;
@@ -546,7 +557,7 @@ struct SchurArgs {
 // schur_kernel: point elimination for damping λ
 // ------------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(kBlockThreads) void schur_kernel(const SchurArgs g, double lambda) {
-  extern __shared__ __attribute__((aligned(16))) float W_dyn[];  // W [points × local poses][6] (gn_prepare: schur_lds)
+  extern __shared__ __attribute__((aligned(16))) double W_dyn[];  // W [points × local poses][6] (gn_prepare: schur_lds)
   __shared__ double s_inv[SCHUR_PTS], s_gl[SCHUR_PTS];
   const int c = blockIdx.x;
   if (c >= g.n_chunks) return;  // (not gated by the record's done flag: a trial after the end only wastes time here)
@@ -572,7 +583,7 @@ __global__ __launch_bounds__(kBlockThreads) void schur_kernel(const SchurArgs g,
     oa = g.pt_orig[min(ia, g.n_gn_points - 1)];
   }
   lambda = lm_lambda(lv, lambda);
-  const float* const blk_schur = lv.set != 0.0 ? g.blk_schur1 : g.blk_schur;
+  const double* const blk_schur = lv.set != 0.0 ? g.blk_schur1 : g.blk_schur;
   if (g.poses) rnew = g.rho_new[oa];
   auto finish_accept = [&]() {  // after the chunk's stores
     if (!accepted) return;
@@ -588,11 +599,11 @@ __global__ __launch_bounds__(kBlockThreads) void schur_kernel(const SchurArgs g,
     }
   };
   const int first = d.x, npt = d.y, nv = d.z, poff = d.w;
-  float (*W)[6] = reinterpret_cast<float (*)[6]>(W_dyn);
-  for (int i = threadIdx.x; i < npt * nv * 6; i += kBlockThreads) (&W[0][0])[i] = 0.0f;
+  double (*W)[6] = reinterpret_cast<double (*)[6]>(W_dyn);
+  for (int i = threadIdx.x; i < npt * nv * 6; i += kBlockThreads) (&W[0][0])[i] = 0.0;
   __syncthreads();
-  // four lanes per point, each summing one float4 of the point's blocks' 16-float records in block order:
-  // q = 0: H_ρρ, g_ρ, W_h[0..1]   q = 1: W_h[2..5]   q = 2: W_t[0..3] → W[p][lv]   q = 3: W_t[4..5] → W[p][lv]
+  // four lanes per point, each summing four doubles (two 16-B loads) of the point's blocks' 16-value records in block
+  // order: q = 0: H_ρρ, g_ρ, W_h[0..1]   q = 1: W_h[2..5]   q = 2: W_t[0..3] → W[p][lv]   q = 3: W_t[4..5] → W[p][lv]
   // (staging the chunk's records in LDS block-parallel instead measured slower: 23 → 35 µs at C4, its LDS halves the
   // resident workgroups)
 #pragma unroll
@@ -604,37 +615,39 @@ __global__ __launch_bounds__(kBlockThreads) void schur_kernel(const SchurArgs g,
       double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
       constexpr int kBatch = 8;  // every load of a batch issued before the first use: one memory round trip per batch
       for (int b0 = fb; b0 < fb + nb; b0 += kBatch) {
-        float4 v[kBatch];
+        double2 v[kBatch][2];
         int lv[kBatch];
 #pragma unroll
         for (int u = 0; u < kBatch; ++u) {
           const int b = min(b0 + u, fb + nb - 1);
-          v[u] = reinterpret_cast<const float4*>(blk_schur + (long long)b * 16)[q];
+          const double2* r2 = reinterpret_cast<const double2*>(blk_schur + (long long)b * 16) + 2 * q;
+          v[u][0] = r2[0];
+          v[u][1] = r2[1];
           lv[u] = q < 2 ? 0 : g.blk_lv[b];
         }
 #pragma unroll
         for (int u = 0; u < kBatch; ++u) {
           if (b0 + u >= fb + nb) break;
           if (q < 2) {
-            s0 += v[u].x; s1 += v[u].y; s2 += v[u].z; s3 += v[u].w;
+            s0 += v[u][0].x; s1 += v[u][0].y; s2 += v[u][1].x; s3 += v[u][1].y;
           } else {
-            float* wt = W[p * nv + lv[u]];
-            if (q == 2) { wt[0] += v[u].x; wt[1] += v[u].y; wt[2] += v[u].z; wt[3] += v[u].w; }
-            else { wt[4] += v[u].x; wt[5] += v[u].y; }
+            double* wt = W[p * nv + lv[u]];
+            if (q == 2) { wt[0] += v[u][0].x; wt[1] += v[u][0].y; wt[2] += v[u][1].x; wt[3] += v[u][1].y; }
+            else { wt[4] += v[u][0].x; wt[5] += v[u][0].y; }
           }
         }
       }
       double* pd = g.pt_data + (long long)gp * 8;
       if (q == 0) {
-        W[p * nv][0] = (float)s2;
-        W[p * nv][1] = (float)s3;
+        W[p * nv][0] = s2;
+        W[p * nv][1] = s3;
         const double D = fmin(fmax(s0, 1e-6), 1e32);
         const double Hd = s0 + lambda * D;
         s_inv[p] = Hd > 0.0 ? 1.0 / Hd : 0.0;
         s_gl[p] = s1;
         pd[0] = s0; pd[1] = s1; pd[2] = s2; pd[3] = s3;
       } else if (q == 1) {
-        W[p * nv][2] = (float)s0; W[p * nv][3] = (float)s1; W[p * nv][4] = (float)s2; W[p * nv][5] = (float)s3;
+        W[p * nv][2] = s0; W[p * nv][3] = s1; W[p * nv][4] = s2; W[p * nv][5] = s3;
         pd[4] = s0; pd[5] = s1; pd[6] = s2; pd[7] = s3;
       }
     }
@@ -650,15 +663,14 @@ __global__ __launch_bounds__(kBlockThreads) void schur_kernel(const SchurArgs g,
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int ti = wv & 1, tj = wv >> 1;
     const int ca = 16 * ti + (lane & 15), cb = 16 * tj + (lane & 15), kq = lane >> 4;
-    const float* Wf = &W[0][0];
+    const double* Wf = &W[0][0];
     v4f64 acc = {0.0, 0.0, 0.0, 0.0};
     // four K steps per batch: the batch's LDS reads first, at clamped indices with unconditional reads, the padding
     // zeroed by selects afterwards (conditional reads were issued and waited one step at a time)
     constexpr int KB = 4;
     const int cac = min(ca, nv6 - 1), cbc = min(cb, nv6 - 1);
     for (int p0 = 0; p0 < npt; p0 += 4 * KB) {
-      float wa[KB], wb[KB];
-      double si[KB], sg[KB];
+      double wa[KB], wb[KB], si[KB], sg[KB];
 #pragma unroll
       for (int u = 0; u < KB; ++u) {
         const int pc = min(p0 + 4 * u + kq, npt - 1);
@@ -670,8 +682,8 @@ __global__ __launch_bounds__(kBlockThreads) void schur_kernel(const SchurArgs g,
 #pragma unroll
       for (int u = 0; u < KB; ++u) {
         const bool pin = p0 + 4 * u + kq < npt;
-        const double av = (pin && ca < nv6) ? (double)wa[u] * si[u] : 0.0;
-        const double bv = !pin ? 0.0 : (cb < nv6 ? (double)wb[u] : (cb == nv6 ? sg[u] : 0.0));
+        const double av = (pin && ca < nv6) ? wa[u] * si[u] : 0.0;
+        const double bv = !pin ? 0.0 : (cb < nv6 ? wb[u] : (cb == nv6 ? sg[u] : 0.0));
         acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
       }
     }
@@ -698,10 +710,10 @@ __global__ __launch_bounds__(kBlockThreads) void schur_kernel(const SchurArgs g,
       const uchar2 ab = g.pairs[ax.x + o / 36];
       const int r = (o % 36) / 6, cc = o % 6;
       for (int p = 0; p < npt; ++p)
-        acc += (double)W[p * nv + ab.x][r] * (double)W[p * nv + ab.y][cc] * s_inv[p];
+        acc += W[p * nv + ab.x][r] * W[p * nv + ab.y][cc] * s_inv[p];
     } else {
       const int q = o - ax.y * 36, a = q / 6, r = q % 6;
-      for (int p = 0; p < npt; ++p) acc += (double)W[p * nv + a][r] * s_gl[p] * s_inv[p];
+      for (int p = 0; p < npt; ++p) acc += W[p * nv + a][r] * s_gl[p] * s_inv[p];
     }
     g.part_schur[(long long)poff + o] = acc;
   }
@@ -709,8 +721,8 @@ __global__ __launch_bounds__(kBlockThreads) void schur_kernel(const SchurArgs g,
 }
 
 struct AsmArgs {
-  const float* part_lin;
-  const float* part_lin1;  // buffer set 1 (device LM loop)
+  const double* part_lin;
+  const double* part_lin1;  // buffer set 1 (device LM loop)
   const double* lm;        // LM record (λ, set; the loop's or GnData::lm_idle)
   const double* part_schur;
   const int* sky_cptr;
@@ -758,8 +770,8 @@ __device__ __forceinline__ void contrib_sums(const AsmArgs& a, const int2* __res
       const int off = c[u].x + ((c[u].y & C_TRANSPOSE) ? et : e);
       const bool sc = (c[u].y & C_SCHUR) != 0;
       const double vs = a.part_schur[sc ? off : 0];
-      const float vl = a.part_lin[sc ? 0 : off];
-      v[u] = sc ? -vs : (double)vl;
+      const double vl = a.part_lin[sc ? 0 : off];
+      v[u] = sc ? -vs : vl;
     }
 #pragma unroll
     for (int u = 0; u < GATHER; ++u) {
@@ -2147,8 +2159,8 @@ struct PointUpdateArgs {
   const int4* pt_rec;
   const int4* pt_tgt;
   const int* gn_target;
-  const float* blk_schur;
-  const float* blk_schur1;  // buffer set 1 (device LM loop)
+  const double* blk_schur;
+  const double* blk_schur1;  // buffer set 1 (device LM loop)
   const double* x;
   const uint8_t* fixed;
   const double* rho;
@@ -2187,7 +2199,7 @@ __device__ __forceinline__ void point_update_block(const PointUpdateArgs& a, con
   ts[0] = wall_clock64();
 #endif
   lambda = lm_lambda(lv, lambda);
-  const float* blk_schur = lv.set != 0.0 ? a.blk_schur1 : a.blk_schur;
+  const double* blk_schur = lv.set != 0.0 ? a.blk_schur1 : a.blk_schur;
   if (p < a.n_points) {
     const double H = pd[0], gl = pd[1];
     const double D = fmin(fmax(H, 1e-6), 1e32);
@@ -2211,17 +2223,20 @@ __device__ __forceinline__ void point_update_block(const PointUpdateArgs& a, con
     const int fb = pr.x, nb = pr.y;
     constexpr int kBatch = 4;  // a batch's loads issued together, then summed in block order
     for (int b0 = fb; b0 < fb + nb; b0 += kBatch) {
-      float w[kBatch][6];
+      double w[kBatch][6];
       int t[kBatch];
       const bool first = b0 == fb;  // the first batch's targets came with the point record
 #pragma unroll
       for (int u = 0; u < kBatch; ++u) {
         const int b = min(b0 + u, fb + nb - 1);
         t[u] = first ? (u == 0 ? pt4.x : u == 1 ? pt4.y : u == 2 ? pt4.z : pt4.w) : a.gn_target[b];
-        const float* wt = blk_schur + (long long)b * 16 + 8;  // W_t
-        const float4 q4 = *reinterpret_cast<const float4*>(wt);
-        const float2 q2 = *reinterpret_cast<const float2*>(wt + 4);
-        w[u][0] = q4.x; w[u][1] = q4.y; w[u][2] = q4.z; w[u][3] = q4.w; w[u][4] = q2.x; w[u][5] = q2.y;
+        const double2* wt = reinterpret_cast<const double2*>(blk_schur + (long long)b * 16 + 8);  // W_t
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+          const double2 q2 = wt[i];
+          w[u][2 * i] = q2.x;
+          w[u][2 * i + 1] = q2.y;
+        }
       }
       double xt[kBatch][6];
 #pragma unroll
@@ -2230,7 +2245,7 @@ __device__ __forceinline__ void point_update_block(const PointUpdateArgs& a, con
       for (int u = 0; u < kBatch; ++u)
         if (b0 + u < fb + nb)
 #pragma unroll
-          for (int i = 0; i < 6; ++i) s += (double)w[u][i] * xt[u][i];
+          for (int i = 0; i < 6; ++i) s += w[u][i] * xt[u][i];
     }
     if (a.ib) {  // + Σ_b W_i(b)·δk(camera of b's target)
       for (int b = fb; b < fb + nb; ++b) {
@@ -2985,6 +3000,7 @@ int gn_prepare(pba_engine* e) {
     while (j < nb && j - i < G.bpw && ph[e->block_point_h[order[lpos[j]]]] == h) {
       const int t = gtgt[lpos[j]];
       auto it = std::find(tg.begin(), tg.end(), t);
+      if (it == tg.end() && (int)tg.size() == kChunkTargets) break;  // a chunk spans ≤ kChunkTargets targets
       blt[j] = (uint8_t)(it - tg.begin());
       if (it == tg.end()) tg.push_back(t);
       ++j;
@@ -2995,7 +3011,7 @@ int gn_prepare(pba_engine* e) {
     chunk_host.push_back(h);
     i = j;
   }
-  G.lin_floats = off;
+  G.lin_slots = off;
   G.n_chunks = (int)cdesc.size();
   // GN points
   std::vector<int> pfirst, pnblk, porig, phost;
@@ -3064,7 +3080,7 @@ int gn_prepare(pba_engine* e) {
     saux.push_back(make_int4((int)spairs.size(), (int)up.size(), fb0, nbc));
     for (auto& pr : up) spairs.push_back(make_uchar2((unsigned char)pr.first, (unsigned char)pr.second));
     sdesc.push_back(make_int4(p, q - p, nv, (int)soff));
-    G.schur_lds = std::max<size_t>(G.schur_lds, sizeof(float) * 6 * (size_t)(q - p) * nv);
+    G.schur_lds = std::max<size_t>(G.schur_lds, sizeof(double) * 6 * (size_t)(q - p) * nv);
     soff += 36 * up.size() + 6 * nv;
     schur_poses.push_back(poses);
     schur_used.push_back(up);
@@ -3220,9 +3236,9 @@ int gn_prepare(pba_engine* e) {
   PBA_HIP(G.lin_rec.upload(lrec, st));
   PBA_HIP(G.chunk_desc.upload(cdesc, st));
   PBA_HIP(G.blk_schur.resize((size_t)nb * 16));
-  PBA_HIP(G.part_lin.resize(std::max<size_t>(G.lin_floats, 1)));
+  PBA_HIP(G.part_lin.resize(std::max<size_t>(G.lin_slots, 1)));
   PBA_HIP(G.blk_schur1.resize((size_t)nb * 16));  // the device LM loop's second linearisation set
-  PBA_HIP(G.part_lin1.resize(std::max<size_t>(G.lin_floats, 1)));
+  PBA_HIP(G.part_lin1.resize(std::max<size_t>(G.lin_slots, 1)));
   PBA_HIP(G.pt_first.upload(pfirst, st));
   PBA_HIP(G.pt_nblk.upload(pnblk, st));
   PBA_HIP(G.pt_orig.upload(porig, st));

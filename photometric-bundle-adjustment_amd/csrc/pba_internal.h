@@ -697,14 +697,18 @@ struct GnData {
   CrLevelHost pcr_bufs[2];             // PCR ping-pong buffers (D, U, b) for that level's rows
   DevBuf<double> cr_buf;
   bool force_skyline = false;
-  size_t lin_floats = 0, schur_doubles = 0, schur_lds = 0;
+  size_t lin_slots = 0, schur_doubles = 0, schur_lds = 0;
   // linearise order (GN order regrouped by target within each host), bpw slots per chunk (a chunk's dead slots
   // repeat its first block): {block, point, pair | local target slot << 24, GN position}
   DevBuf<int4> lin_rec;
   DevBuf<int4> chunk_desc;       // linearise chunk: first linearise position, count, n_targets, partial offset
-  DevBuf<float> blk_schur;       // GN block → 16 floats [Hll gl Wh(6) Wt(6) 0 0]
-  DevBuf<float> part_lin;        // linearise chunk partials (fp32)
-  DevBuf<float> blk_schur1, part_lin1;  // second set: the device LM loop linearises each candidate into the spare
+  // The normal-equation pieces are fp64: the block products of the fp32 rows are formed on the fp64 matrix cores, so
+  // JᵀJ is the exact Gram matrix of the rows and stays consistent with the point elimination's W W / H (fp32 products
+  // and sums gave the reduced system errors of ~1e-7 of its scale that its condition number, ~1e11 at C4, turned into
+  // wrong steps once the trust region had grown: DESIGN.md §4, tests/test_gpu_configs.py).
+  DevBuf<double> blk_schur;      // GN block → 16 doubles [Hll gl Wh(6) Wt(6) 0 0]
+  DevBuf<double> part_lin;       // linearise chunk partials
+  DevBuf<double> blk_schur1, part_lin1;  // second set: the device LM loop linearises each candidate into the spare
   DevBuf<int> pt_first, pt_nblk, pt_orig;  // GN point → first GN block, block count, original point
   DevBuf<int4> pt_rec;           // GN point → {first GN block, block count, host frame, original point} (one load)
   DevBuf<int4> pt_tgt;           // GN point → the targets of its first four GN blocks (the update's x_t loads in round 2)

@@ -150,10 +150,11 @@ class CheckedCost : public ceres::CostFunction {
 
 // The floor (mode floor): what one PrepareForEvaluation left for Evaluate to read — nothing when the adapter kept the
 // previous point (same point, no new work).
+// The arrays are page-locked host memory from the engine library, as the drop-in's own read-back buffers.
 struct Snapshot {
   bool kept = false, jac = false;
-  std::vector<float> rec;      // records (jac) or residuals
-  std::vector<uint8_t> valid;
+  std::unique_ptr<pba_ceres::PinnedArray<float>> rec;     // records (jac) or residuals
+  std::unique_ptr<pba_ceres::PinnedArray<uint8_t>> valid;
   std::vector<double> pinv;    // the poses' P⁺ (jac, reference parameterisation)
 };
 
@@ -172,9 +173,13 @@ class RecordingEvaluator : public pba_ceres::GpuEvaluator {
       s.jac = has_jacobians();
       for (int b = 0; b < nb_; b += chunk_blocks_) wait(b);
       const int R = residuals_per_block(), rf = pba_record_floats(engine_);
-      if (s.jac) s.rec.assign(record(0), record(0) + (size_t)nb_ * rf);
-      else s.rec.assign(residuals(0), residuals(0) + (size_t)nb_ * R);
-      s.valid.assign(valid_src_, valid_src_ + nb_);
+      const size_t n = (size_t)nb_ * (s.jac ? rf : R);
+      s.rec.reset(new pba_ceres::PinnedArray<float>);
+      s.rec->resize(n);
+      std::memcpy(s.rec->data(), s.jac ? record(0) : residuals(0), n * sizeof(float));
+      s.valid.reset(new pba_ceres::PinnedArray<uint8_t>);
+      s.valid->resize(nb_);
+      std::memcpy(s.valid->data(), valid_src_, nb_);
       if (s.jac && pose_jacobian() == pba_ceres::PoseJacobian::kReferenceSE3) s.pinv.assign(pinv_src_, pinv_src_ + 42 * nf_);
     }
     out_->push_back(std::move(s));
@@ -200,10 +205,10 @@ class ReplayEvaluator : public pba_ceres::GpuEvaluator {
     if (s.kept) return;
     if (s.jac != evaluate_jacobians) ok_ = false;
     async_ = false;
-    rec_src_ = s.jac ? s.rec.data() : nullptr;
-    res_ = s.rec.data();
+    rec_src_ = s.jac ? s.rec->data() : nullptr;
+    res_ = s.rec->data();
     res_stride_ = s.jac ? rec_ : R_;
-    valid_src_ = s.valid.data();
+    valid_src_ = s.valid->data();
     pinv_src_ = s.pinv.empty() ? nullptr : s.pinv.data();
     have_point_ = true;
     have_jac_ = s.jac;
