@@ -30,8 +30,9 @@
 //        run again from the same initial state with an evaluator that only points the adapter at the recorded arrays:
 //        the same values give Ceres the same decisions, so both runs make the same evaluations, and "Jacobian &
 //        residual evaluation" of the second run is Ceres' own work (ProgramEvaluator, the Jacobian writer, the
-//        LocalParameterization products, the loss) plus the adapter's per-block copy — everything but the device's part
-//        (state upload, launch, read-back).  The summary is the second run's, with "replay_ok" saying whether it took
+//        LocalParameterization products, the loss) plus the adapter's per-block copy out of its own read-back buffers
+//        (staged with the recorded values between iterations, outside Ceres' timers) and its P⁺ — everything but the
+//        device's part (state gather and upload, launch, read-back).  The summary is the second run's, with "replay_ok" saying whether it took
 //        exactly the recorded evaluations.
 // check = 0 (gpu mode): the plain adapter, without the protocol checks (the bench's C2 timing: the checks hash the whole
 //        state per Prepare and count every Evaluate with an atomic shared by Ceres' threads).
@@ -190,34 +191,83 @@ class RecordingEvaluator : public pba_ceres::GpuEvaluator {
   std::vector<Snapshot>* out_;
 };
 
-// Pass 2: the same adapter reading the recorded arrays — the device's part (gather, upload, launch, read-back) removed.
-class ReplayEvaluator : public pba_ceres::GpuEvaluator {
+// Pass 2: the same adapter with the device's part (state gather, upload, launch, read-back) removed.  Its Evaluate reads
+// the adapter's own page-locked read-back buffers, as the drop-in does, which hold the recorded values of the
+// evaluation Ceres is about to make: they are staged outside Ceres' evaluation timers — before the Solve and in an
+// IterationCallback after each iteration (an iteration makes at most one residual-only and one Jacobian evaluation, into
+// two different buffers).  P⁺ is formed from the state in PrepareForEvaluation, as the drop-in forms it.
+class ReplayEvaluator : public pba_ceres::GpuEvaluator, public ceres::IterationCallback {
  public:
   ReplayEvaluator(pba_engine* e, std::vector<double*> poses, std::vector<double*> rho, std::vector<double*> intr,
                   pba_ceres::PoseJacobian form, const std::vector<Snapshot>* snaps)
-      : GpuEvaluator(e, poses, rho, intr, form), snaps_(snaps) {}
+      : GpuEvaluator(e, poses, rho, intr, form), snaps_(snaps) {
+    valid_r_.resize((size_t)pba_num_blocks(e));
+    stage();
+  }
+  ceres::CallbackReturnType operator()(const ceres::IterationSummary&) override {
+    stage();
+    return ceres::SOLVER_CONTINUE;
+  }
   void PrepareForEvaluation(bool evaluate_jacobians, bool /*new_evaluation_point*/) override {
     if (next_ >= snaps_->size()) {
       ok_ = false;
       return;
     }
-    const Snapshot& s = (*snaps_)[next_++];
+    const size_t i = next_++;
+    const Snapshot& s = (*snaps_)[i];
     if (s.kept) return;
     if (s.jac != evaluate_jacobians) ok_ = false;
     async_ = false;
-    rec_src_ = s.jac ? s.rec->data() : nullptr;
-    res_ = s.rec->data();
-    res_stride_ = s.jac ? rec_ : R_;
-    valid_src_ = s.valid->data();
-    pinv_src_ = s.pinv.empty() ? nullptr : s.pinv.data();
+    if (s.jac) {
+      if (staged_j_ != i) ok_ = false;
+      rec_src_ = res_ = records_.data();
+      res_stride_ = rec_;
+      valid_src_ = valid_.data();
+      if (form_ == pba_ceres::PoseJacobian::kReferenceSE3) {
+        pinv_.resize(42 * poses_.size());
+        for (size_t f = 0; f < poses_.size(); ++f) pba_ceres::se3_plus_jacobian_pinv(poses_[f], &pinv_[42 * f]);
+        pinv_src_ = pinv_.data();
+      }
+    } else {
+      if (staged_r_ != i) ok_ = false;
+      rec_src_ = nullptr;
+      res_ = residuals_.data();
+      res_stride_ = R_;
+      valid_src_ = valid_r_.data();
+    }
     have_point_ = true;
     have_jac_ = s.jac;
   }
   bool replay_ok() const { return ok_ && next_ == snaps_->size(); }
 
  private:
+  // the next residual-only and the next Jacobian evaluation from next_ on, into the read-back buffers
+  void stage() {
+    bool r = false, j = false;
+    for (size_t i = next_; i < snaps_->size() && !(r && j); ++i) {
+      const Snapshot& s = (*snaps_)[i];
+      if (s.kept) continue;
+      const size_t nb = (size_t)pba_num_blocks(engine_);
+      if (s.jac && !j) {
+        if (staged_j_ != i) {
+          std::memcpy(records_.data(), s.rec->data(), nb * rec_ * sizeof(float));
+          std::memcpy(valid_.data(), s.valid->data(), nb);
+          staged_j_ = i;
+        }
+        j = true;
+      } else if (!s.jac && !r) {
+        if (staged_r_ != i) {
+          std::memcpy(residuals_.data(), s.rec->data(), nb * R_ * sizeof(float));
+          std::memcpy(valid_r_.data(), s.valid->data(), nb);
+          staged_r_ = i;
+        }
+        r = true;
+      }
+    }
+  }
   const std::vector<Snapshot>* snaps_;
-  size_t next_ = 0;
+  pba_ceres::PinnedArray<uint8_t> valid_r_;
+  size_t next_ = 0, staged_r_ = (size_t)-1, staged_j_ = (size_t)-1;
   bool ok_ = true;
 };
 
@@ -370,7 +420,7 @@ int main(int argc, char** argv) {
   ceres::Solver::Summary sum;
   // bundle_adjustment()'s problem build (map_utils.h:322-375) over the evaluator ev (nullptr: AutoDiff on the CPU),
   // then ceres::Solve (:376-383)
-  auto solve = [&](pba_ceres::GpuEvaluator* evaluator, bool checked_costs) {
+  auto solve = [&](pba_ceres::GpuEvaluator* evaluator, bool checked_costs, ceres::IterationCallback* cb = nullptr) {
     ceres::Problem::Options popt;
     popt.evaluation_callback = evaluator;  // problem.h:185 (not owned)
     ceres::Problem problem(popt);
@@ -411,7 +461,9 @@ int main(int argc, char** argv) {
       else
         problem.AddResidualBlock(cf, loss, T[h].data(), T[t].data(), &rho[p]);
     }
-    ceres::Solve(so, &problem, &sum);
+    ceres::Solver::Options o = so;
+    if (cb) o.callbacks.push_back(cb);
+    ceres::Solve(o, &problem, &sum);
   };
 
   int replay_ok = -1;
@@ -428,7 +480,7 @@ int main(int argc, char** argv) {
     rho = rho0;
     intr = intr0;
     std::unique_ptr<ReplayEvaluator> rep(new ReplayEvaluator(e, pose_ptr, rho_ptr, intr_ptr, form, &snaps));
-    solve(rep.get(), false);
+    solve(rep.get(), false, rep.get());
     replay_ok = rep->replay_ok() ? 1 : 0;
     ev = std::move(rep);
   } else if (gpu) {
