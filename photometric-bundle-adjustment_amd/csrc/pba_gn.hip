@@ -136,6 +136,8 @@ struct LinArgs {
   int n_chunks;
   const double* lm;         // LM record: skip when the solve is done; spare: write the set the record does not hold
   bool spare;
+  int* lin_set;             // or nullptr: the set written (workgroup 0 stores it, and clears degen[set])
+  int* degen;
 };
 
 // ------------------------------------------------------------------------------------------------
@@ -203,6 +205,10 @@ void linearize_kernel(const KernelArgs a, const LinArgs g) {
   const bool s1 = (lv.set != 0.0) != g.spare;
   double* const blk_schur = s1 ? g.blk_schur1 : g.blk_schur;
   double* const part_lin = s1 ? g.part_lin1 : g.part_lin;
+  if (g.lin_set && chunk == 0 && threadIdx.x == 0) {  // (the λ-free elimination after this launch reads them)
+    *g.lin_set = s1 ? 1 : 0;
+    g.degen[s1 ? 1 : 0] = 0;
+  }
   const int count = d.y, n_t = d.z, poff = d.w;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int lb = threadIdx.x / LPB, k = threadIdx.x % LPB, wb = lb % BW;
@@ -381,6 +387,10 @@ void linearize_rows_kernel(const KernelArgs a, const LinArgs g) {
   const bool s1 = (lv.set != 0.0) != g.spare;
   double* const blk_schur = s1 ? g.blk_schur1 : g.blk_schur;
   double* const part_lin = s1 ? g.part_lin1 : g.part_lin;
+  if (g.lin_set && chunk == 0 && threadIdx.x == 0) {  // (the λ-free elimination after this launch reads them)
+    *g.lin_set = s1 ? 1 : 0;
+    g.degen[s1 ? 1 : 0] = 0;
+  }
   const int count = d.y, n_t = d.z, poff = d.w;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int lb = threadIdx.x / LPB, k = threadIdx.x % LPB, wb = lb % BW;
@@ -556,15 +566,14 @@ struct SchurArgs {
 // ------------------------------------------------------------------------------------------------
 // schur_kernel: point elimination for damping λ
 // ------------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(kBlockThreads) void schur_kernel(const SchurArgs g, double lambda) {
-  extern __shared__ __attribute__((aligned(16))) double W_dyn[];  // W [points × local poses][6] (gn_prepare: schur_lds)
-  __shared__ double s_inv[SCHUR_PTS], s_gl[SCHUR_PTS];
-  const int c = blockIdx.x;
-  if (c >= g.n_chunks) return;  // (not gated by the record's done flag: a trial after the end only wastes time here)
-  // Memory rounds (each dependent one is ~1.7 µs here): 1 — the record, the chunk descriptors, the chunk's point
-  // records (padded per-chunk table) and the accept copy's sources; 2 — the points' block data (and the copied ρ);
-  // the accept copy's stores come last, so no load of the chunk waits behind them (loads and stores share vmcnt).
-  const LmView lv = lm_view(g.lm);
+// One Schur chunk c for damping λ: the points' H_ρρ, g_ρ, W sums from the block data of the linearisation set blk_schur,
+// their point data into pt_out (nullptr: not stored), and the chunk's partial slots into part_out.  degen != nullptr (the
+// λ-free pass of the device LM loop, λ = 0): set to 1 when a point's H_ρρ lies outside the LM diagonal's clamp [1e-6, 1e32]
+// (H = 0 excepted: such a point has W = 0) — only inside it is H + λ·clamp(H) = (1 + λ)·H, the identity the λ-free pass
+// relies on (schur_free_decide_kernel).
+__device__ __forceinline__ void schur_chunk(const SchurArgs& g, int c, double lambda, const double* __restrict__ blk_schur,
+                                            double* __restrict__ part_out, double* __restrict__ pt_out, int* degen,
+                                            double* W_dyn, double* s_inv, double* s_gl) {
   const int4 d = g.desc[c];
   const int4 ax = g.aux[c];
   constexpr int kPtIter = (SCHUR_PTS + kBlockThreads / 4 - 1) / (kBlockThreads / 4);
@@ -572,32 +581,6 @@ __global__ __launch_bounds__(kBlockThreads) void schur_kernel(const SchurArgs g,
 #pragma unroll
   for (int it = 0; it < kPtIter; ++it)
     prec[it] = g.pt_fb[(long long)c * SCHUR_PTS + it * (kBlockThreads / 4) + (threadIdx.x >> 2)];
-  // the last trial's accept (the copies of lm_accept_kernel): one element per thread (the grid covers them; a
-  // grid-stride tail otherwise)
-  const bool accepted = g.poses && lv.accept != 0.0;
-  const int ia = blockIdx.x * blockDim.x + threadIdx.x;
-  double pnew = 0.0, rnew = 0.0;
-  int oa = 0;
-  if (g.poses) {
-    pnew = g.poses_new[min(ia, g.n_pose_d - 1)];
-    oa = g.pt_orig[min(ia, g.n_gn_points - 1)];
-  }
-  lambda = lm_lambda(lv, lambda);
-  const double* const blk_schur = lv.set != 0.0 ? g.blk_schur1 : g.blk_schur;
-  if (g.poses) rnew = g.rho_new[oa];
-  auto finish_accept = [&]() {  // after the chunk's stores
-    if (!accepted) return;
-    if (ia < g.n_pose_d) g.poses[ia] = pnew;
-    if (ia < g.n_gn_points) g.rho[oa] = rnew;
-    const int n = max(g.n_pose_d, g.n_gn_points);
-    for (int i = ia + gridDim.x * blockDim.x; i < n; i += gridDim.x * blockDim.x) {
-      if (i < g.n_pose_d) g.poses[i] = g.poses_new[i];
-      if (i < g.n_gn_points) {
-        const int o = g.pt_orig[i];
-        g.rho[o] = g.rho_new[o];
-      }
-    }
-  };
   const int first = d.x, npt = d.y, nv = d.z, poff = d.w;
   double (*W)[6] = reinterpret_cast<double (*)[6]>(W_dyn);
   for (int i = threadIdx.x; i < npt * nv * 6; i += kBlockThreads) (&W[0][0])[i] = 0.0;
@@ -606,6 +589,7 @@ __global__ __launch_bounds__(kBlockThreads) void schur_kernel(const SchurArgs g,
   // order: q = 0: H_ρρ, g_ρ, W_h[0..1]   q = 1: W_h[2..5]   q = 2: W_t[0..3] → W[p][lv]   q = 3: W_t[4..5] → W[p][lv]
   // (staging the chunk's records in LDS block-parallel instead measured slower: 23 → 35 µs at C4, its LDS halves the
   // resident workgroups)
+  bool bad = false;
 #pragma unroll
   for (int it = 0; it < kPtIter; ++it) {
     const int p0 = it * (kBlockThreads / 4);
@@ -637,7 +621,7 @@ __global__ __launch_bounds__(kBlockThreads) void schur_kernel(const SchurArgs g,
           }
         }
       }
-      double* pd = g.pt_data + (long long)gp * 8;
+      double* pd = pt_out ? pt_out + (long long)gp * 8 : nullptr;
       if (q == 0) {
         W[p * nv][0] = s2;
         W[p * nv][1] = s3;
@@ -645,13 +629,15 @@ __global__ __launch_bounds__(kBlockThreads) void schur_kernel(const SchurArgs g,
         const double Hd = s0 + lambda * D;
         s_inv[p] = Hd > 0.0 ? 1.0 / Hd : 0.0;
         s_gl[p] = s1;
-        pd[0] = s0; pd[1] = s1; pd[2] = s2; pd[3] = s3;
+        bad = s0 != 0.0 && !(s0 >= 1e-6 && s0 <= 1e32);
+        if (pd) { pd[0] = s0; pd[1] = s1; pd[2] = s2; pd[3] = s3; }
       } else if (q == 1) {
         W[p * nv][2] = s0; W[p * nv][3] = s1; W[p * nv][4] = s2; W[p * nv][5] = s3;
-        pd[4] = s0; pd[5] = s1; pd[6] = s2; pd[7] = s3;
+        if (pd) { pd[4] = s0; pd[5] = s1; pd[6] = s2; pd[7] = s3; }
       }
     }
   }
+  if (degen && __syncthreads_or(bad) && threadIdx.x == 0) atomicOr(degen, 1);
   __syncthreads();
   if (nv * 6 + 1 <= 32) {
     // ≤ 5 local poses (a temporal window): the chunk's sums are one small GEMM on the matrix cores,
@@ -695,12 +681,11 @@ __global__ __launch_bounds__(kBlockThreads) void schur_kernel(const SchurArgs g,
         // canonical pair order (gn_prepare): (0,0) (0,1) … (0,nv−1) (1,1) …; blocks of unused pairs are zero
         const int pa_ = r / 6, pb_ = cb / 6;
         const int u = pa_ * nv - pa_ * (pa_ - 1) / 2 + (pb_ - pa_);
-        if (pa_ <= pb_) g.part_schur[(long long)poff + u * 36 + (r % 6) * 6 + cb % 6] = acc[v];
+        if (pa_ <= pb_) part_out[(long long)poff + u * 36 + (r % 6) * 6 + cb % 6] = acc[v];
       } else if (cb == nv6) {
-        g.part_schur[(long long)poff + ax.y * 36 + r] = acc[v];
+        part_out[(long long)poff + ax.y * 36 + r] = acc[v];
       }
     }
-    finish_accept();
     return;
   }
   const int nout = ax.y * 36 + nv * 6;
@@ -715,9 +700,58 @@ __global__ __launch_bounds__(kBlockThreads) void schur_kernel(const SchurArgs g,
       const int q = o - ax.y * 36, a = q / 6, r = q % 6;
       for (int p = 0; p < npt; ++p) acc += W[p * nv + a][r] * s_gl[p] * s_inv[p];
     }
-    g.part_schur[(long long)poff + o] = acc;
+    part_out[(long long)poff + o] = acc;
   }
-  finish_accept();
+}
+
+// The accept of the device LM loop's previous trial (state ← candidate when the record says accepted; the copies of
+// lm_accept_kernel): one element per thread, a grid-stride tail beyond the grid.  Loads first (with the kernel's first
+// loads), stores after the kernel's own stores (loads and stores share vmcnt).
+struct AcceptCopy {
+  bool accepted = false;
+  int ia = 0, oa = 0;
+  double pnew = 0.0, rnew = 0.0;
+  __device__ __forceinline__ void load(const SchurArgs& g, const LmView& lv) {
+    accepted = g.poses && lv.accept != 0.0 && lv.done == 0.0;
+    ia = blockIdx.x * blockDim.x + threadIdx.x;
+    if (g.poses) {
+      pnew = g.poses_new[min(ia, g.n_pose_d - 1)];
+      oa = g.pt_orig[min(ia, g.n_gn_points - 1)];
+      rnew = g.rho_new[oa];
+    }
+  }
+  __device__ __forceinline__ void store(const SchurArgs& g) const {
+    if (!accepted) return;
+    if (ia < g.n_pose_d) g.poses[ia] = pnew;
+    if (ia < g.n_gn_points) g.rho[oa] = rnew;
+    const int n = max(g.n_pose_d, g.n_gn_points);
+    for (int i = ia + gridDim.x * blockDim.x; i < n; i += gridDim.x * blockDim.x) {
+      if (i < g.n_pose_d) g.poses[i] = g.poses_new[i];
+      if (i < g.n_gn_points) {
+        const int o = g.pt_orig[i];
+        g.rho[o] = g.rho_new[o];
+      }
+    }
+  }
+};
+
+// Point elimination for damping λ (host-driven steps, the multi-GPU loop, free intrinsics): one chunk per workgroup, the
+// linearisation set of the record, plus the previous trial's accept when g.poses is set.
+__global__ __launch_bounds__(kBlockThreads) void schur_kernel(const SchurArgs g, double lambda) {
+  extern __shared__ __attribute__((aligned(16))) double W_dyn[];  // W [points × local poses][6] (gn_prepare: schur_lds)
+  __shared__ double s_inv[SCHUR_PTS], s_gl[SCHUR_PTS];
+  const int c = blockIdx.x;
+  if (c >= g.n_chunks) return;  // (not gated by the record's done flag: a trial after the end only wastes time here)
+  // Memory rounds (each dependent one is ~1.7 µs here): 1 — the record, the chunk descriptors, the chunk's point
+  // records (padded per-chunk table) and the accept copy's sources; 2 — the points' block data (and the copied ρ);
+  // the accept copy's stores come last, so no load of the chunk waits behind them (loads and stores share vmcnt).
+  const LmView lv = lm_view(g.lm);
+  AcceptCopy ac;
+  ac.load(g, lv);
+  lambda = lm_lambda(lv, lambda);
+  const double* const blk_schur = lv.set != 0.0 ? g.blk_schur1 : g.blk_schur;
+  schur_chunk(g, c, lambda, blk_schur, g.part_schur, g.pt_data, nullptr, W_dyn, s_inv, s_gl);
+  ac.store(g);
 }
 
 struct AsmArgs {
@@ -748,6 +782,11 @@ struct AsmArgs {
   double* crb;
   int crB;
   int* status;
+  // the single-GPU LM loop: the current set's λ-free Schur partials (scaled by 1/(1 + λ)) unless the set is flagged
+  // degen (schur_free_decide_kernel); nullptr: part_schur as it is
+  const double* part_free0;
+  const double* part_free1;
+  const int* degen;
 };
 
 // Fixed-order sums over a contribution list (total, and the part that is not a Schur term — the undamped
@@ -757,7 +796,7 @@ struct AsmArgs {
 // VGPRs and twice the clamped loads of the short off-diagonal lists.)
 constexpr int GATHER = 8;
 __device__ __forceinline__ void contrib_sums(const AsmArgs& a, const int2* __restrict__ list, int beg, int end, int e,
-                                             int et, double& sum, double& dsum) {
+                                             int et, double& sum, double& dsum, double pscale = 1.0) {
   sum = dsum = 0.0;
   for (int q0 = beg; q0 < end; q0 += GATHER) {
     int2 c[GATHER];
@@ -771,7 +810,7 @@ __device__ __forceinline__ void contrib_sums(const AsmArgs& a, const int2* __res
       const bool sc = (c[u].y & C_SCHUR) != 0;
       const double vs = a.part_schur[sc ? off : 0];
       const double vl = a.part_lin[sc ? 0 : off];
-      v[u] = sc ? -vs : vl;
+      v[u] = sc ? -pscale * vs : vl;
     }
 #pragma unroll
     for (int u = 0; u < GATHER; ++u) {
@@ -788,15 +827,21 @@ __device__ __forceinline__ void contrib_sums(const AsmArgs& a, const int2* __res
 // ------------------------------------------------------------------------------------------------
 __global__ void assemble_kernel(AsmArgs a, double lambda) {
   const LmView lv = lm_view(a.lm);  // (no done gate: see schur_kernel)
+  const int dg0 = a.degen ? a.degen[0] : 1, dg1 = a.degen ? a.degen[1] : 1;
   lambda = lm_lambda(lv, lambda);
   if (lv.set != 0.0) a.part_lin = a.part_lin1;
+  double pscale = 1.0;  // the λ-free partials of the current set: P / (1 + λ)
+  if (a.degen && (lv.set != 0.0 ? dg1 : dg0) == 0) {
+    a.part_schur = lv.set != 0.0 ? a.part_free1 : a.part_free0;
+    pscale = 1.0 / (1.0 + lambda);
+  }
   const int tid = blockIdx.x * blockDim.x + threadIdx.x;
   const int nS = a.n_sky * 36;
   if (tid < nS) {
     const int s = tid / 36, e = tid % 36, r = e / 6, cc = e % 6;
     const int i = a.blk_i[s], j = a.blk_j[s];
     double sum, dsum;
-    contrib_sums(a, a.sky_contrib, a.sky_cptr[s], a.sky_cptr[s + 1], r * 6 + cc, cc * 6 + r, sum, dsum);
+    contrib_sums(a, a.sky_contrib, a.sky_cptr[s], a.sky_cptr[s + 1], r * 6 + cc, cc * 6 + r, sum, dsum, pscale);
     double val = sum;
     if (a.fixed[i] || a.fixed[j]) {
       val = (i == j && r == cc) ? 1.0 : 0.0;
@@ -829,7 +874,7 @@ __global__ void assemble_kernel(AsmArgs a, double lambda) {
   if (t >= 6 * a.n_frames) return;
   const int i = t / 6, r = t % 6;
   double sum, dsum;
-  contrib_sums(a, a.g_contrib, a.g_cptr[i], a.g_cptr[i + 1], r, r, sum, dsum);
+  contrib_sums(a, a.g_contrib, a.g_cptr[i], a.g_cptr[i + 1], r, r, sum, dsum, pscale);
   a.g[t] = a.fixed[i] ? 0.0 : sum;
   if (a.Sband) a.Sband[(long long)i * ((a.band + 1) * 36 + 6) + (a.band + 1) * 36 + r] = a.fixed[i] ? 0.0 : sum;
   if (a.crD) {
@@ -2156,6 +2201,7 @@ __device__ __forceinline__ void pose_update_block(const PoseUpdateArgs& a, const
 
 struct PointUpdateArgs {
   const double* pt_data;
+  const double* pt_data1;  // the single-GPU LM loop: set 1's point data (schur_free_decide_kernel), else pt_data
   const int4* pt_rec;
   const int4* pt_tgt;
   const int* gn_target;
@@ -2186,13 +2232,20 @@ __device__ __forceinline__ void point_update_block(const PointUpdateArgs& a, con
   const int pc = min(p, a.n_points - 1);
   const int4 pr = a.pt_rec[pc];  // first block, block count, host, original point
   const int4 pt4 = a.pt_tgt[pc];  // the targets of its first four blocks
-  double pd[8];
+  // both sets' point data with the record (which of them is current is the record's): no dependent round for the choice
+  double pd[8], pd1[8];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const double2 d2 = reinterpret_cast<const double2*>(a.pt_data + (long long)pc * 8)[i];
+    const double2 e2 = reinterpret_cast<const double2*>(a.pt_data1 + (long long)pc * 8)[i];
     pd[2 * i] = d2.x;
     pd[2 * i + 1] = d2.y;
+    pd1[2 * i] = e2.x;
+    pd1[2 * i + 1] = e2.y;
   }
+  if (lv.set != 0.0)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) pd[i] = pd1[i];
   if (lv.done != 0.0) return;  // (uniform: every thread of the workgroup returns)
 #ifdef PBA_UPD_STAMPS
   long long ts[4];
@@ -2676,9 +2729,10 @@ __device__ void lm_decide(const double* t, int st, const DecideOpts& o, double* 
 // thread, then one strided pass over red with U slots per thread in flight, then xor butterflies per wave and the
 // waves in order (U loads of three arrays spilled 172 B per lane at 1024 threads: 16 µs per decision).  t: the
 // totals, in LDS.
+template <int N>
 __device__ void trial_sums(const double* __restrict__ red, const double* __restrict__ red2,
                            const double* __restrict__ gmax, int gp, int gq, int gc, double* t) {
-  constexpr int N = kDecideThreads, U = 8;
+  constexpr int U = 8;
   __shared__ double part[kTsCount][N / 64];
   double v[kTsCount] = {};
   const int S = gp + gq, E = S + gc;
@@ -2778,7 +2832,7 @@ __global__ __launch_bounds__(kDecideThreads) void lm_decide_kernel(const double*
   // flight with the partials' instead of a round trip of its own before them (the partials are always readable)
   const double done = lm[kLmDone];
   __shared__ double t[kTsCount];
-  trial_sums(red, red2, gmax, gp, gq, gc, t);
+  trial_sums<kDecideThreads>(red, red2, gmax, gp, gq, gc, t);
   if (done != 0.0 || threadIdx.x >= 64) return;  // wave 0 publishes; lane 0 decides
   __shared__ double s_rec[kLmFields];
   if (threadIdx.x == 0) {
@@ -2795,7 +2849,7 @@ __global__ __launch_bounds__(kDecideThreads) void lm_decide_kernel(const double*
 __global__ __launch_bounds__(kDecideThreads) void lm_init_kernel(const double* __restrict__ red, int gc, double radius,
                                                                  double* __restrict__ lm, double* __restrict__ init) {
   __shared__ double t[kTsCount];
-  trial_sums(red, red, red, 0, 0, gc, t);
+  trial_sums<kDecideThreads>(red, red, red, 0, 0, gc, t);
   if (threadIdx.x != 0) return;
   for (int i = 0; i < kLmFields; ++i) lm[i] = 0.0;
   lm[kLmCost] = t[kTsCost];
@@ -2806,6 +2860,101 @@ __global__ __launch_bounds__(kDecideThreads) void lm_init_kernel(const double* _
   lm[kLmLambda] = 1.0 / radius;
   init[0] = t[kTsCost];
   init[1] = t[kTsValid];
+}
+
+// ---- the single-GPU LM loop's λ-free point elimination ---------------------------------------------------------------
+// For a point whose H_ρρ lies inside the LM diagonal's clamp [1e-6, 1e32] (levenberg_marquardt_strategy.cc), the damped
+// H' = H + λ·clamp(H) = (1 + λ)·H, so its Schur terms W Wᵀ / H' and W g / H' are (1 + λ)⁻¹ times the λ-free W Wᵀ / H and
+// W g / H.  A linearisation set's λ-free partials P are therefore formed once, right after the set is linearised, and every
+// trial on that set (an accepted candidate's first, or the retries after rejections) assembles A + λD − P / (1 + λ):
+// no per-trial point elimination.  A set with a point outside the clamp (H ≠ 0: a point with H = 0 has W = 0) is flagged
+// (degen[set]) and its trials form the λ-specific partials in schur_gate_kernel, exactly as schur_kernel does.
+//
+// The kernel after the candidate linearisation: workgroup 0 takes the trial's decision (lm_decide_kernel's sums and
+// decision, 256 threads) — or, init, forms the record of a new solve (lm_init_kernel's) — while workgroups 1 … n_schur
+// form the λ-free partials and point data of the set linearize_kernel has just written (lin_set); the two parts share no
+// data, so the decision costs no launch and runs beside the elimination.  The elimination never reads the record's set
+// (the decision may flip it meanwhile); only its done flag (a workgroup that sees the solve ended skips its chunk: nothing
+// reads it then).
+struct DecideArgs {
+  const double* red;
+  const double* red2;
+  const double* gmax;
+  int gp, gq, gc;
+  const int* status;
+  DecideOpts o;
+  double* lm;
+  double* host_rec;   // the published record slot, or nullptr
+  double seq;
+  int init;           // 1: a new solve's record (lm_init_kernel), 0: the trial's decision
+  double radius;      // init: the initial trust-region radius
+  double* init_out;   // init: [initial cost, valid blocks]
+};
+struct FreeSets {
+  double* part[2];    // λ-free Schur partials per linearisation set
+  double* pt[2];      // point data per set ([H, g, W_h(6)] per GN point, undamped)
+  int* degen;         // [2]: a point of the set outside the clamp
+  const int* lin_set; // the set the last linearisation wrote
+};
+
+__global__ __launch_bounds__(kBlockThreads) void schur_free_decide_kernel(const SchurArgs g, const DecideArgs da,
+                                                                        const FreeSets fs) {
+  extern __shared__ __attribute__((aligned(16))) double W_dyn[];
+  __shared__ double s_inv[SCHUR_PTS], s_gl[SCHUR_PTS];
+  if (blockIdx.x == 0) {
+    __shared__ double t[kTsCount];
+    if (da.init) {
+      trial_sums<kBlockThreads>(da.red, da.red, da.red, 0, 0, da.gc, t);
+      if (threadIdx.x != 0) return;
+      double* lm = da.lm;
+      for (int i = 0; i < kLmFields; ++i) lm[i] = 0.0;
+      lm[kLmCost] = t[kTsCost];
+      lm[kLmValid] = t[kTsValid];
+      lm[kLmXNorm] = -1.0;
+      lm[kLmRadius] = da.radius;
+      lm[kLmFactor] = 2.0;
+      lm[kLmLambda] = 1.0 / da.radius;
+      da.init_out[0] = t[kTsCost];
+      da.init_out[1] = t[kTsValid];
+      return;
+    }
+    const double done = da.lm[kLmDone];  // (tested after the sums, as lm_decide_kernel)
+    trial_sums<kBlockThreads>(da.red, da.red2, da.gmax, da.gp, da.gq, da.gc, t);
+    if (done != 0.0 || threadIdx.x >= 64) return;
+    __shared__ double s_rec[kLmFields];
+    if (threadIdx.x == 0) {
+      lm_decide(t, *da.status, da.o, da.lm);
+      for (int i = 0; i < kLmFields; ++i) s_rec[i] = da.lm[i];
+    }
+    if (da.host_rec) publish_record(s_rec, da.host_rec, da.seq);
+    return;
+  }
+  const int c = blockIdx.x - 1;
+  if (c >= g.n_chunks) return;
+  if (!da.init && da.lm[kLmDone] != 0.0) return;
+  const int set = *fs.lin_set != 0;
+  schur_chunk(g, c, 0.0, set ? g.blk_schur1 : g.blk_schur, fs.part[set], fs.pt[set], fs.degen + set, W_dyn, s_inv, s_gl);
+}
+
+// The single-GPU LM trial's first kernel: the previous trial's accept, and — only for a set flagged degen — the
+// λ-specific point elimination of the current set into part_schur (every chunk, grid-stride), which the assembly then
+// takes instead of the λ-free partials.
+__global__ __launch_bounds__(kBlockThreads) void schur_gate_kernel(const SchurArgs g, const int* __restrict__ degen) {
+  extern __shared__ __attribute__((aligned(16))) double W_dyn[];
+  __shared__ double s_inv[SCHUR_PTS], s_gl[SCHUR_PTS];
+  const LmView lv = lm_view(g.lm);
+  const int dg0 = degen[0], dg1 = degen[1];
+  AcceptCopy ac;
+  ac.load(g, lv);
+  const int set = lv.set != 0.0;
+  if ((set ? dg1 : dg0) != 0 && lv.done == 0.0) {
+    const double* blk_schur = set ? g.blk_schur1 : g.blk_schur;
+    for (int c = blockIdx.x; c < g.n_chunks; c += gridDim.x) {
+      schur_chunk(g, c, lv.lambda, blk_schur, g.part_schur, nullptr, nullptr, W_dyn, s_inv, s_gl);
+      __syncthreads();
+    }
+  }
+  ac.store(g);
 }
 
 // Multi-GPU trial, before the scalar all-reduce: this rank's sums, written to the exchange buffer's kExScalars scalar
@@ -2828,7 +2977,7 @@ __global__ __launch_bounds__(kDecideThreads) void dist_sums_kernel(const double*
                                                                    double* __restrict__ tpose, double* __restrict__ Y) {
   const double done = lm[kLmDone];  // (tested after the sums, as lm_decide_kernel)
   __shared__ double t[kTsCount];
-  trial_sums(red, red2, gmax, gp, gq, gc, t);
+  trial_sums<kDecideThreads>(red, red2, gmax, gp, gq, gc, t);
   if (done != 0.0 || threadIdx.x != 0) return;
   for (int q = 0; q < 5; ++q) tpose[q] = t[kTsPoseG + q];
   tpose[5] = t[kTsPtGMax];
@@ -3267,6 +3416,12 @@ int gn_prepare(pba_engine* e) {
   PBA_HIP(G.blk_lv.upload(blv, st));
   PBA_HIP(G.part_schur.resize(std::max<size_t>(G.schur_doubles, 1)));
   PBA_HIP(G.pt_data.resize((size_t)ngp * 8));
+  PBA_HIP(G.pt_data1.resize((size_t)ngp * 8));
+  PBA_HIP(G.part_free0.resize(std::max<size_t>(G.schur_doubles, 1)));
+  PBA_HIP(G.part_free1.resize(std::max<size_t>(G.schur_doubles, 1)));
+  PBA_HIP(G.degen.resize(2));
+  PBA_HIP(G.lin_set.resize(1));
+  PBA_HIP(hipMemsetAsync(G.degen.p, 0, 2 * sizeof(int), st));
   PBA_HIP(G.sky_first.upload(first, st));
   PBA_HIP(G.sky_row.upload(rowp, st));
   PBA_HIP(G.sky_last.upload(last, st));
@@ -3411,8 +3566,10 @@ int total_cost(pba_engine* e, double* cost, int* n_valid) {
 // lm = the device LM record (the pieces go to the spare buffer set, nothing runs once the solve is done), pairs / rho
 // the candidate's, and wg_red the slots of the per-chunk cost partials the decision sums.
 // cand_intr: with free intrinsics, project with the candidate's (G.intr_new_*) instead of the state's.
+// mark_set: record the set written (and clear its degen flag) for the λ-free elimination that follows.
 int linearize(pba_engine* e, double* cost, const double* lm = nullptr, const PairRec* pairs = nullptr,
-              const double* rho = nullptr, double* wg_red = nullptr, int* n_valid = nullptr, bool cand_intr = false) {
+              const double* rho = nullptr, double* wg_red = nullptr, int* n_valid = nullptr, bool cand_intr = false,
+              bool mark_set = false) {
   GnData& G = e->gn;
   if (!pairs) {
     launch_pairs(e, e->poses.p, e->pairs.p);
@@ -3423,7 +3580,8 @@ int linearize(pba_engine* e, double* cost, const double* lm = nullptr, const Pai
     ka.intr_t = G.intr_new_f.p;
     ka.intr_t_d = G.intr_new_d.p;
   }
-  LinArgs la{G.lin_rec.p, G.blk_schur1.p, G.part_lin1.p, wg_red, G.chunk_desc.p, G.blk_schur.p, G.part_lin.p, G.n_chunks, lm ? lm : G.lm_idle.p, lm != nullptr};
+  LinArgs la{G.lin_rec.p, G.blk_schur1.p, G.part_lin1.p, wg_red, G.chunk_desc.p, G.blk_schur.p, G.part_lin.p, G.n_chunks,
+             lm ? lm : G.lm_idle.p, lm != nullptr, mark_set ? G.lin_set.p : nullptr, mark_set ? G.degen.p : nullptr};
   if (e->opt.residual_kind == PBA_RESIDUAL_PHOTOMETRIC) launch_linearize_photometric(e, ka, la);
   else launch_linearize_geometric(e, ka, la);
   PBA_HIP(hipGetLastError());
@@ -3530,8 +3688,9 @@ void cr_solve(pba_engine* e, bool build) {
 // After a solve into G.x: solver status, candidate poses/points, and the two parts of the LM model decrease
 // L(0) − L(δ) = −gᵀδ − ½δᵀHδ = ½(λ δᵀDδ − gᵀδ)  (since (H + λD)δ = −g): pose part and point part.
 // Candidate poses/points and the model-decrease partials into reduction slots [0, gp + gq) of G.red.
+// free_sets: the single-GPU LM loop's per-set point data (the record says which set is current), else G.pt_data.
 void enqueue_updates(pba_engine* e, double lambda, const uint8_t* fixed, int* gp_out, int* gq_out,
-                     const double* lm = nullptr) {
+                     const double* lm = nullptr, bool free_sets = false) {
   GnData& G = e->gn;
   const int nf = e->n_frames, nfs = G.nc_sys ? G.nfs : nf;
   const int gp = (nfs + kBlockThreads - 1) / kBlockThreads;
@@ -3541,7 +3700,7 @@ void enqueue_updates(pba_engine* e, double lambda, const uint8_t* fixed, int* gp
   PoseUpdateArgs pa{e->poses.p, G.x.p, G.g_dir.p, G.Ddiag.p, fixed, G.poses_new.p, G.red.p, G.red2.p, G.gmax.p, nfs, nf,
                     ki ? e->intr_state_d.p : nullptr, ki ? G.intr_new_d.p : nullptr, ki ? G.intr_new_f.p : nullptr};
   // point workgroup q writes reduction slot gp + q, as the separate launches did
-  PointUpdateArgs qa{G.pt_data.p, G.pt_rec.p, G.pt_tgt.p, G.gn_target.p,
+  PointUpdateArgs qa{G.pt_data.p, free_sets ? G.pt_data1.p : G.pt_data.p, G.pt_rec.p, G.pt_tgt.p, G.gn_target.p,
                      G.blk_schur.p, G.blk_schur1.p, G.x.p, fixed, e->rho.p, G.rho_new.p, G.drho.p, G.red.p,
                      G.red2.p, G.gmax.p, G.n_gn_points, ki ? G.ib_data.p : nullptr, G.ib_cam.p, nf};
   PairUpdateArgs ra{G.pair_rec.p, e->intr_d.p, G.pairs_new.p, e->n_pairs};
@@ -3597,20 +3756,26 @@ int band_solve(pba_engine* e, bool build = true) {
 // Dynamic LDS above the default 64 KiB limit (the attribute is per device: set on every launch, cheap).
 void schur_lds_limit(const GnData& G) {
   if (G.schur_lds > 65536)
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&schur_kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)G.schur_lds);
+    for (const void* f : {reinterpret_cast<const void*>(&schur_kernel), reinterpret_cast<const void*>(&schur_gate_kernel),
+                          reinterpret_cast<const void*>(&schur_free_decide_kernel)})
+      (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)G.schur_lds);
 }
 
 // Schur complement for λ, assembly and reduced-system solve into G.x (enqueued only).
 // lm: the device LM record (λ, buffer set, done flag read on the device; lambda unused) or nullptr.
-int enqueue_solve(pba_engine* e, double lambda, const double* lm = nullptr) {
+// free_sets (the single-GPU LM loop without free intrinsics): the current set's λ-free partials, scaled in the assembly,
+// and schur_gate_kernel (the accept, the λ-specific elimination only for a degen set) instead of schur_kernel.
+int enqueue_solve(pba_engine* e, double lambda, const double* lm = nullptr, bool free_sets = false) {
   GnData& G = e->gn;
   const int nf = e->n_frames, nfs = G.nc_sys ? G.nfs : nf;
   SchurArgs sa{G.schur_desc.p, G.schur_aux.p, G.schur_pairs.p, G.pt_fb.p, G.blk_lv.p,
                G.blk_schur.p, G.blk_schur1.p, G.part_schur.p, G.pt_data.p, G.n_schur, lm ? lm : G.lm_idle.p,
                lm ? e->poses.p : nullptr, G.poses_new.p, e->rho.p, G.rho_new.p, G.pt_orig.p, 7 * nf, G.n_gn_points};
   schur_lds_limit(G);
-  schur_kernel<<<G.n_schur, kBlockThreads, G.schur_lds, e->stream>>>(sa, lambda);
+  if (free_sets)
+    schur_gate_kernel<<<std::max(1, std::min(G.n_schur, 512)), kBlockThreads, G.schur_lds, e->stream>>>(sa, G.degen.p);
+  else
+    schur_kernel<<<G.n_schur, kBlockThreads, G.schur_lds, e->stream>>>(sa, lambda);
   if (G.nc_sys) {  // free intrinsics: the last trial's accept, then the weighted fp64 rows at the state
     if (lm) intr_accept_kernel<<<1, 256, 0, e->stream>>>(lm, G.intr_new_d.p, G.intr_new_f.p, e->intr_state_d.p,
                                                          e->intr_state.p, G.nc_sys);
@@ -3632,7 +3797,8 @@ int enqueue_solve(pba_engine* e, double lambda, const double* lm = nullptr) {
   AsmArgs aa{G.part_lin.p, G.part_lin1.p, lm ? lm : G.lm_idle.p, G.part_schur.p, G.sky_cptr.p, G.sky_contrib.p, G.g_cptr.p,
              G.g_contrib.p, G.sky_blk_i.p, G.sky_blk_j.p, G.fixed.p, G.S.p, G.g.p, G.g_dir.p, G.Ddiag.p,
              G.band_kernel && !direct ? G.Sband.p : nullptr, G.band_kernel, G.n_sky, nfs,
-             direct ? L0.D : nullptr, L0.U, L0.b, G.band_kernel, G.status.p};
+             direct ? L0.D : nullptr, L0.U, L0.b, G.band_kernel, G.status.p, free_sets ? G.part_free0.p : nullptr,
+             free_sets ? G.part_free1.p : nullptr, free_sets ? G.degen.p : nullptr};
   if (G.sband_dirty && G.band_kernel && !direct) {  // a distributed import filled the whole band: clear the off-profile part
     PBA_HIP(hipMemsetAsync(G.Sband.p, 0, sizeof(double) * (size_t)nf * ((G.band_kernel + 1) * 36 + 6), e->stream));
     G.sband_dirty = false;
@@ -3718,20 +3884,45 @@ int wait_decision(pba_engine* e, double seq, double* d) {
 // one's decision: no host round trip between trials.  The candidate is evaluated even when the solve failed (its
 // numbers are then discarded): a garbage state is memory-safe in every evaluation kernel.  ev (phase timing only,
 // else nullptr): begin | candidate state | candidate linearisation | decision.
+// The λ-free point elimination's launch after a linearisation (schur_free_decide_kernel): workgroup 0 the decision of
+// trial seq (init: the record of a new solve), the others the set's partials.
+void launch_free_decide(pba_engine* e, const DecideOpts& dopt, double seq, int gp, int gq, bool init, double radius) {
+  GnData& G = e->gn;
+  const int nf = e->n_frames;
+  SchurArgs sa{G.schur_desc.p, G.schur_aux.p, G.schur_pairs.p, G.pt_fb.p, G.blk_lv.p,
+               G.blk_schur.p, G.blk_schur1.p, G.part_schur.p, G.pt_data.p, G.n_schur, G.lm.p,
+               nullptr, nullptr, nullptr, nullptr, nullptr, 7 * nf, G.n_gn_points};
+  DecideArgs da{G.red.p, G.red2.p, G.gmax.p, gp, gq, G.n_chunks, G.status.p, dopt, G.lm.p,
+                init ? nullptr : G.lm_host_d + rec_slot(seq), seq, init ? 1 : 0, radius, G.lm_init.p};
+  FreeSets fs{{G.part_free0.p, G.part_free1.p}, {G.pt_data.p, G.pt_data1.p}, G.degen.p, G.lin_set.p};
+  schur_lds_limit(G);
+  schur_free_decide_kernel<<<1 + G.n_schur, kBlockThreads, G.schur_lds, e->stream>>>(sa, da, fs);
+  // tests: every set flagged, so every trial takes the λ-specific elimination (the degenerate-point path)
+  if (G.force_degen) (void)hipMemsetAsync(G.degen.p, 0x01, 2 * sizeof(int), e->stream);
+}
+
+// free intrinsics keep the per-trial elimination (their border kernels read its point data at the trial's λ)
+bool lm_free_sets(const pba_engine* e) { return e->gn.nc_sys == 0 && e->gn.n_schur > 0; }
+
 int lm_trial(pba_engine* e, const DecideOpts& dopt, double seq, const hipEvent_t* ev) {
   GnData& G = e->gn;
+  const bool fs = lm_free_sets(e);
   if (ev) PBA_HIP(hipEventRecord(ev[0], e->stream));
-  if (int rc = enqueue_solve(e, 0.0, G.lm.p)) return rc;
+  if (int rc = enqueue_solve(e, 0.0, G.lm.p, fs)) return rc;
   int gp = 0, gq = 0;
-  enqueue_updates(e, 0.0, G.fixed.p, &gp, &gq, G.lm.p);
+  enqueue_updates(e, 0.0, G.fixed.p, &gp, &gq, G.lm.p, fs);
   if (ev) PBA_HIP(hipEventRecord(ev[1], e->stream));
-  if (int rc = linearize(e, nullptr, G.lm.p, G.pairs_new.p, G.rho_new.p, G.red.p + 2 * (gp + gq), nullptr, true)) return rc;
+  if (int rc = linearize(e, nullptr, G.lm.p, G.pairs_new.p, G.rho_new.p, G.red.p + 2 * (gp + gq), nullptr, true, fs))
+    return rc;
   if (ev) PBA_HIP(hipEventRecord(ev[2], e->stream));
-  lm_decide_kernel<<<1, kDecideThreads, 0, e->stream>>>(G.red.p, G.red2.p, G.gmax.p, gp, gq, G.n_chunks, G.status.p,
-                                                        dopt, G.lm.p, G.lm_host_d + rec_slot(seq), seq);
+  if (fs)
+    launch_free_decide(e, dopt, seq, gp, gq, false, 0.0);
+  else
+    lm_decide_kernel<<<1, kDecideThreads, 0, e->stream>>>(G.red.p, G.red2.p, G.gmax.p, gp, gq, G.n_chunks, G.status.p,
+                                                          dopt, G.lm.p, G.lm_host_d + rec_slot(seq), seq);
   PBA_HIP(hipGetLastError());
   if (ev) PBA_HIP(hipEventRecord(ev[3], e->stream));
-  return PBA_OK;  // an accepted candidate becomes the state in the next trial's schur_kernel (or after the loop)
+  return PBA_OK;  // an accepted candidate becomes the state in the next trial's first kernel (or after the loop)
 }
 
 int candidate_cost(pba_engine* e, double* cost) {
@@ -3772,7 +3963,7 @@ int enqueue_export(pba_engine* e, const double* lm, double* X, int K) {
   const int nf = e->n_frames;
   AsmArgs aa{G.part_lin.p, G.part_lin1.p, lm, G.part_schur.p, G.sky_cptr.p, G.sky_contrib.p, G.g_cptr.p,
              G.g_contrib.p, G.sky_blk_i.p, G.sky_blk_j.p, G.fixed.p, G.S.p, G.g.p, G.g_dir.p, G.Ddiag.p, nullptr, K,
-             G.n_sky, nf, nullptr, nullptr, nullptr, 0, nullptr};
+             G.n_sky, nf, nullptr, nullptr, nullptr, 0, nullptr, nullptr, nullptr, nullptr};
   const long long n = (long long)nf * ex_row(K);  // (K+1)·36 band + EX_TAIL tail lanes per frame
   export_band_kernel<<<(unsigned)((n + 255) / 256), 256, 0, e->stream>>>(aa, G.observed.p, G.sky_first.p, G.sky_row.p,
                                                                         X, K);
@@ -4098,10 +4289,14 @@ int lm_loop_single(pba_engine* e, const pba_solver_options* o, pba_solver_summar
   double cost = 0.0;
   // the initial linearisation (set 0) with its chunk cost partials in red, and the device record formed from them
   // (lm_init_kernel): no host round trip before the first trial
-  if (int rc = linearize(e, nullptr, nullptr, nullptr, nullptr, G.red.p)) return rc;
+  const bool fs = lm_free_sets(e);
+  if (int rc = linearize(e, nullptr, nullptr, nullptr, nullptr, G.red.p, nullptr, false, fs)) return rc;
   if (G.lm_init.n < 2) PBA_HIP(G.lm_init.resize(2));
-  lm_init_kernel<<<1, kDecideThreads, 0, e->stream>>>(G.red.p, G.n_chunks, opt.initial_trust_region_radius, G.lm.p,
-                                                       G.lm_init.p);
+  if (fs)  // the record and set 0's λ-free partials in one launch
+    launch_free_decide(e, decide_opts(opt), 0.0, 0, 0, true, opt.initial_trust_region_radius);
+  else
+    lm_init_kernel<<<1, kDecideThreads, 0, e->stream>>>(G.red.p, G.n_chunks, opt.initial_trust_region_radius, G.lm.p,
+                                                         G.lm_init.p);
   PBA_HIP(hipGetLastError());
   for (int r = 0; r < kRecRing; ++r) G.lm_h[r * kRecStride + kLmFields] = 0.0;  // no trial published yet
   // PBA_LM_HOST_DELAY_US (tests): the host thread sleeps this long before each wait, as a descheduled thread would

@@ -722,7 +722,12 @@ struct GnData {
   std::vector<uint8_t> fixed_eff;  // constant frames actually used (requested + unobserved)
   DevBuf<uint8_t> blk_lv;        // GN block → local pose index of its target in its Schur chunk
   DevBuf<double> part_schur;     // Schur chunk partials (fp64)
-  DevBuf<double> pt_data;        // GN point → [H'll, gl, Wh(6)] of the last Schur pass (fp64)
+  DevBuf<double> pt_data;        // GN point → [H'll, gl, Wh(6)] of the last Schur pass (fp64); set 0 of the LM loop
+  // the single-GPU LM loop's λ-free point elimination (schur_free_decide_kernel): per linearisation set the partials
+  // Σ W Wᵀ/H, Σ W g/H and the point data, a flag for a point outside the LM clamp, the set the last linearisation wrote
+  DevBuf<double> part_free0, part_free1, pt_data1;
+  DevBuf<int> degen, lin_set;
+  bool force_degen = std::getenv("PBA_TEST_FORCE_DEGEN") != nullptr;  // tests: the λ-specific path on every trial
   DevBuf<int> sky_first, sky_row, sky_last;  // skyline profile of the reduced camera system
   DevBuf<int> sky_cptr, g_cptr;  // contribution lists (CSR) per skyline block / per pose
   DevBuf<int2> sky_contrib, g_contrib;

@@ -540,3 +540,33 @@ def test_free_intrinsics_reduced_system_and_step(model, lam):
     assert eS <= 1e-5 and eg <= 1e-5, (eS, eg)
     assert ep <= 1e-3 and el <= 1e-3, (ep, el)
     assert abs(m - m_ref) <= 1e-3 * abs(m_ref)
+
+
+@pytest.mark.parametrize("force_degen", [False, True])
+@pytest.mark.parametrize("kind,model,huber,ps,rs,min_rel,iters", [LM_CASES[0], LM_CASES[2], LM_CASES[4]])
+def test_lm_point_elimination_paths_agree(kind, model, huber, ps, rs, min_rel, iters, force_degen, monkeypatch):
+    """The single-GPU LM loop eliminates the points once per linearisation, λ-free (P = Σ W Wᵀ/H, scaled by 1/(1 + λ)
+    in the assembly: exact for every point whose H_ρρ lies inside the LM diagonal's clamp [1e-6, 1e32]), and falls back
+    to the per-trial λ-specific elimination of schur_kernel for a set with a point outside it.  PBA_TEST_FORCE_DEGEN
+    flags every set, so every trial takes the fallback: both paths take the reference LM's decisions, and their final
+    costs agree to 1e-9 (the two orders of the same sums)."""
+    if force_degen:
+        monkeypatch.setenv("PBA_TEST_FORCE_DEGEN", "1")
+    pb = synth.make_problem(kind=kind, model=model, n_frames=8, n_points=120, width=376, height=240, seed=31,
+                            border=12, obs_sigma=0.3, pose_sigma=ps, rho_sigma=rs)
+    pb.poses[:2] = pb.poses_gt[:2]
+    ref = GR.lm(pb, huber, (0, 1), max_iterations=iters, min_relative_decrease=min_rel, summary=True)
+    with make_engine(pb, huber, (0, 1)) as eng:
+        summ = eng.solve(max_iterations=iters, min_relative_decrease=min_rel)
+        poses, rho = eng.get_state()
+        traj = eng.solver_iterations()
+    _same_lm(summ, poses, rho, ref)
+    assert len(traj["cost"]) >= 2 and traj["cost"][0] == summ["initial_cost"]
+    key = (kind, model, min_rel)
+    _ELIM_RESULTS.setdefault(key, {})[force_degen] = summ["final_cost"]
+    if len(_ELIM_RESULTS[key]) == 2:
+        a, b = _ELIM_RESULTS[key][False], _ELIM_RESULTS[key][True]
+        assert abs(a - b) <= 1e-9 * abs(a), (a, b)
+
+
+_ELIM_RESULTS = {}
