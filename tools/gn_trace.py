@@ -7,7 +7,8 @@ import csv
 import sys
 
 rows = sorted(csv.DictReader(open(sys.argv[1])), key=lambda r: int(r["Start_Timestamp"]))
-idx = [i for i, r in enumerate(rows) if "schur_kernel" in r["Kernel_Name"]]
+first = "schur_gate_kernel" if any("schur_gate_kernel" in r["Kernel_Name"] for r in rows) else "schur_kernel"
+idx = [i for i, r in enumerate(rows) if first in r["Kernel_Name"]]
 if len(idx) < 4:
     sys.exit("fewer than 4 trials in the trace")
 k = int(sys.argv[2]) if len(sys.argv) > 2 else len(idx) - 3
