@@ -295,12 +295,14 @@ def gn_benchmark(eng, pb, iters, torch, dist, dev, world, ceres_problem=None, th
     opts = dict(max_iterations=iters, function_tolerance=0.0)
     agree = None
     traj = None
-    device_steered = world > 1 and dist.get_backend() == "nccl" and os.environ.get("PBA_BENCH_GN_COMM") == "1"
+    device_steered = world > 1 and dist.get_backend() == "nccl" and os.environ.get("PBA_BENCH_GN_COMM", "1") != "0"
     if world > 1:
         band = D.global_band(eng, None, dev)
-        # Default: the host-callback loop (pba_solve_distributed, torch's all_reduce between trials), which cannot
-        # desynchronise the ranks' collective sequences.  PBA_BENCH_GN_COMM=1 selects the device-steered RCCL loop
-        # (pba_solve_distributed_comm) — kept opt-in until a run with several GPUs has confirmed it.
+        # Default under RCCL: the device-steered loop (pba_solve_distributed_comm: both all-reduces of every trial on
+        # the engine stream, the next trial enqueued ahead of the decision).  Every trial's scalar all-reduce also checks
+        # that the ranks took the same previous decision, and a final all-reduce checks the last one: ranks that
+        # disagree end the solve with an error instead of hanging on mismatched collectives.  PBA_BENCH_GN_COMM=0
+        # selects the host-callback loop (pba_solve_distributed, torch's all_reduce between trials).
         comm = None if device_steered else False
         D.solve_distributed(eng, device=dev, comm=comm, max_iterations=1)  # warm-up (sets the RCCL communicator up)
         eng.set_state(pb.poses, pb.rho)

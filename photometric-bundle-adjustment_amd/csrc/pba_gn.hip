@@ -102,9 +102,21 @@ static_assert(pa(21) == 0 && pb(21) == 6 && pa(56) == 5 && pb(56) == 11, "table"
 enum : int {
   kLmCost = 0, kLmCostNew = 1, kLmModel = 2, kLmRel = 3, kLmAccept = 4, kLmStatus = 5, kLmConverged = 6,
   kLmLambda = 7, kLmRadius = 8, kLmFactor = 9, kLmDone = 10, kLmSet = 11, kLmValid = 12, kLmXNorm = 13,
-  kLmInvalid = 14, kLmStepNorm = 15, kLmGradNorm = 16, kLmFields = 17
+  kLmInvalid = 14, kLmStepNorm = 15, kLmGradNorm = 16, kLmDesync = 17, kLmFields = 18
 };
-enum : int { kDoneFunction = 1, kDoneInvalid = 2, kDoneParameter = 3, kDoneGradient = 4, kDoneRadius = 5 };
+// kDoneDesync (multi-GPU): the ranks' decisions of the previous trial differed (kLmDesync = 1 + the number of ranks whose
+// record said done then); every rank ends the solve with an error
+enum : int { kDoneFunction = 1, kDoneInvalid = 2, kDoneParameter = 3, kDoneGradient = 4, kDoneRadius = 5, kDoneDesync = 6 };
+
+// A record's decision as a small integer, identical on ranks with identical records: accept, done != 0 and 10 bits of
+// the trust-region state (λ's bits folded) — summed with its square over the ranks in the next trial's scalar all-reduce
+// (N·Σw² = (Σw)² ⇔ every w equal; exact in fp64 for w < 2^12)
+__device__ inline double decision_word(const double* lm) {
+  const unsigned long long b = (unsigned long long)__double_as_longlong(lm[kLmLambda]);
+  unsigned h = (unsigned)(b ^ (b >> 20) ^ (b >> 40) ^ (b >> 60));
+  h = (h ^ (h >> 10) ^ (h >> 20)) & 1023u;
+  return (double)((h << 2) | (lm[kLmDone] != 0.0 ? 2u : 0u) | (lm[kLmAccept] != 0.0 ? 1u : 0u));
+}
 // The published copies of the record (host-coherent page-locked memory): a ring of kRecRing slots of kLmFields fields
 // + the trial's sequence number, trial `seq` in slot seq mod kRecRing.  The host enqueues one trial ahead of the record
 // it waits for, so two records can be in flight; with a single slot, a host thread descheduled for longer than a trial
@@ -280,15 +292,24 @@ void linearize_kernel(const KernelArgs a, const LinArgs g) {
     const int pc = lane < 16 ? lane : -1, pq = pc < 12 ? pc + 2 : (pc < 14 ? pc - 12 : pc);
     v4f64 tacc = {0.0, 0.0, 0.0, 0.0};
     int cur = lo;
+    // block b's chain (SPB dependent steps); a dead block's rows are zeros, so its chain is issued unconditionally
+    auto chain = [&](int b) {
+      v4f64 acc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int st = 0; st < SPB; ++st) {
+        const double o = (double)op[b * SPB + st];
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(o, o, acc, 0, 0, 0);
+      }
+      return acc;
+    };
+    // two blocks in flight: block b + 1's matrix-core steps are issued before block b's result is consumed (each
+    // dependent fp64 step waited out its latency before the point-data store and the run sum otherwise)
+    v4f64 nxt = chain(0);
 #pragma unroll
     for (int b = 0; b < BW; ++b) {
+      const v4f64 acc = nxt;
+      if (b + 1 < BW) nxt = chain(b + 1);
       if (b < nbw) {
-        v4f64 acc = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-        for (int st = 0; st < SPB; ++st) {
-          const double o = (double)op[b * SPB + st];
-          acc = __builtin_amdgcn_mfma_f64_16x16x4f64(o, o, acc, 0, 0, 0);
-        }
         const int gpb = __builtin_amdgcn_readlane(gpos, b * LPB);
         if (pc >= 0) blk_schur[(long long)gpb * 16 + pq] = acc[3];
         const int ltb = __builtin_amdgcn_readlane(lt, b * LPB);
@@ -2978,7 +2999,17 @@ __global__ __launch_bounds__(kDecideThreads) void dist_sums_kernel(const double*
   const double done = lm[kLmDone];  // (tested after the sums, as lm_decide_kernel)
   __shared__ double t[kTsCount];
   trial_sums<kDecideThreads>(red, red2, gmax, gp, gq, gc, t);
-  if (done != 0.0 || threadIdx.x != 0) return;
+  if (threadIdx.x != 0) return;
+  // the previous decision's word, with its square, and whether it ended the solve on this rank: every rank, done or not
+  const double w = decision_word(lm);
+  Y[7] = done != 0.0 ? 1.0 : 0.0;
+  Y[14] = w;
+  Y[15] = w * w;
+  if (done != 0.0) {  // (the sums are not used; zeros keep them finite)
+    for (int q = 0; q < 7; ++q) Y[q] = 0.0;
+    for (int q = 8; q < 14; ++q) Y[q] = 0.0;
+    return;
+  }
   for (int q = 0; q < 5; ++q) tpose[q] = t[kTsPoseG + q];
   tpose[5] = t[kTsPtGMax];
   tpose[6] = (double)*status;
@@ -2989,36 +3020,61 @@ __global__ __launch_bounds__(kDecideThreads) void dist_sums_kernel(const double*
   Y[4] = t[kTsPtStep2];
   Y[5] = t[kTsPtXNorm2];
   Y[6] = t[kTsPtGMax] > gtol ? 1.0 : 0.0;
-  Y[7] = 0.0;
   for (int q = 0; q < 5; ++q) Y[8 + q] = rank0 == 1 ? t[kTsPoseG + q] : 0.0;
   Y[13] = rank0 == 1 ? (double)*status : 0.0;
-  Y[14] = Y[15] = 0.0;
 }
 
 // Multi-GPU decision from the summed Y: the same lm_decide on every rank (identical inputs), so every rank takes the
-// same decision; the reported gradient norm is this rank's view (the pose part and its own points).
+// same decision; the reported gradient norm is this rank's view (the pose part and its own points).  First the check of
+// the previous decision (decision_word over the ranks, n_ranks of them): if the ranks' records differed, every rank
+// ends the solve here (done = kDoneDesync, kLmDesync = 1 + the number of ranks that had stopped) — the host loops then
+// match their remaining collectives (lm_loop) and report the error instead of hanging.  The record is published even
+// when the solve was already done, so a host that stopped can read this check.  perturb_seq (tests,
+// PBA_TEST_PERTURB_DECISION): this rank's decision of that trial is overridden (mode 1 flips accept, 2 ends the solve).
 __global__ __launch_bounds__(64) void dist_decide_kernel(const double* __restrict__ Y, const double* __restrict__ tpose,
                                                          int local, const DecideOpts o, double* __restrict__ lm,
-                                                         double* __restrict__ host_rec, double seq) {
-  if (lm[kLmDone] != 0.0) return;
+                                                         double* __restrict__ host_rec, double seq, int n_ranks,
+                                                         double perturb_seq, int perturb_mode, int verify_only) {
   __shared__ double s_rec[kLmFields];
   if (threadIdx.x == 0) {
-    const double* pose = local ? tpose : Y + 8;  // [pose part (5) | …, status at 6 resp. 5]
-    double t[kTsCount];
-    for (int q = 0; q < 5; ++q) t[kTsPoseG + q] = pose[q];
-    t[kTsPtG] = Y[0];
-    t[kTsPtD] = Y[1];
-    t[kTsCost] = Y[2];
-    t[kTsValid] = Y[3];
-    t[kTsPtStep2] = Y[4];
-    t[kTsPtXNorm2] = Y[5];
-    // no rank's point gradient above the tolerance: the test then depends on the pose part alone (identical)
-    t[kTsPtGMax] = Y[6] > 0.0 ? INFINITY : 0.0;
-    lm_decide(t, (int)(local ? tpose[6] : Y[13]), o, lm);
-    lm[kLmGradNorm] = fmax(pose[4], tpose[5]);
+    const bool desync = (double)n_ranks * Y[15] != Y[14] * Y[14];
+    if (desync) {
+      lm[kLmDone] = kDoneDesync;
+      lm[kLmDesync] = Y[7] + 1.0;
+      lm[kLmAccept] = 0.0;
+    } else if (lm[kLmDone] == 0.0 && !verify_only) {
+      const double* pose = local ? tpose : Y + 8;  // [pose part (5) | …, status at 6 resp. 5]
+      double t[kTsCount];
+      for (int q = 0; q < 5; ++q) t[kTsPoseG + q] = pose[q];
+      t[kTsPtG] = Y[0];
+      t[kTsPtD] = Y[1];
+      t[kTsCost] = Y[2];
+      t[kTsValid] = Y[3];
+      t[kTsPtStep2] = Y[4];
+      t[kTsPtXNorm2] = Y[5];
+      // no rank's point gradient above the tolerance: the test then depends on the pose part alone (identical)
+      t[kTsPtGMax] = Y[6] > 0.0 ? INFINITY : 0.0;
+      lm_decide(t, (int)(local ? tpose[6] : Y[13]), o, lm);
+      lm[kLmGradNorm] = fmax(pose[4], tpose[5]);
+      if (seq == perturb_seq) {
+        if (perturb_mode == 1) lm[kLmAccept] = 1.0 - lm[kLmAccept];
+        else lm[kLmDone] = kDoneFunction;
+      }
+    }
     for (int i = 0; i < kLmFields; ++i) s_rec[i] = lm[i];
   }
   if (host_rec) publish_record(s_rec, host_rec, seq);
+}
+
+// The check of the last decision of a multi-GPU solve (no trial follows it): the decision word into Y as dist_sums_kernel
+// writes it, every other slot zero.
+__global__ void dist_verify_kernel(const double* __restrict__ lm, double* __restrict__ Y) {
+  if (threadIdx.x != 0) return;
+  const double w = decision_word(lm);
+  for (int q = 0; q < kExScalars; ++q) Y[q] = 0.0;
+  Y[7] = lm[kLmDone] != 0.0 ? 1.0 : 0.0;
+  Y[14] = w;
+  Y[15] = w * w;
 }
 
 // The accepted candidate becomes the state (device-side accept, gated by the decision record; lm == nullptr: always).
@@ -4377,7 +4433,16 @@ int lm_loop_single(pba_engine* e, const pba_solver_options* o, pba_solver_summar
 // point elimination (hence this rank's system) on λ.  With a stream-ordered collective the host enqueues the next trial
 // before this one's decision is known, as on one GPU; every rank enqueues the same trials (the decisions agree), so the
 // collectives match.
-int dist_trial(pba_engine* e, const Collective& coll, const DecideOpts& dopt, double* X, int K, double seq) {
+// PBA_TEST_PERTURB_DECISION = "rank:trial:mode" (tests): that rank's decision of that trial is overridden (mode 1: the
+// accept flag flipped, 2: the solve ended) — the ranks' records then differ, which the next trial's check must catch.
+struct DistCheck {
+  int n_ranks = 1;
+  double perturb_seq = -1.0;
+  int perturb_mode = 0;
+};
+
+int dist_trial(pba_engine* e, const Collective& coll, const DecideOpts& dopt, double* X, int K, double seq,
+               const DistCheck& chk) {
   GnData& G = e->gn;
   const int nf = e->n_frames;
   SchurArgs sa{G.schur_desc.p, G.schur_aux.p, G.schur_pairs.p, G.pt_fb.p, G.blk_lv.p,
@@ -4400,7 +4465,8 @@ int dist_trial(pba_engine* e, const Collective& coll, const DecideOpts& dopt, do
   PBA_HIP(hipGetLastError());
   if (int rc = coll.allreduce(e, Y, kExScalars)) return rc;
   dist_decide_kernel<<<1, 64, 0, e->stream>>>(Y, G.tpose.p, coll.rank0(e) < 0 ? 1 : 0, dopt, G.lm.p,
-                                              G.lm_host_d + rec_slot(seq), seq);
+                                              G.lm_host_d + rec_slot(seq), seq, chk.n_ranks, chk.perturb_seq,
+                                              chk.perturb_mode, 0);
   PBA_HIP(hipGetLastError());
   return PBA_OK;
 }
@@ -4422,15 +4488,24 @@ int lm_loop(pba_engine* e, const pba_solver_options* o, const Collective* coll, 
   double cost = 0.0;
   int n_valid = 0;
   if (int rc = linearize(e, &cost, nullptr, nullptr, nullptr, nullptr, &n_valid)) return rc;
-  {  // Σ over ranks of the initial cost and valid blocks, through the scalar slots
-    double v[2] = {cost, (double)n_valid};
+  DistCheck chk;
+  {  // Σ over ranks of the initial cost and valid blocks — and of 1: the number of ranks — through the scalar slots
+    double v[3] = {cost, (double)n_valid, 1.0};
     double* Y = X + (long long)e->n_frames * ex_row(K);
     PBA_HIP(hipMemcpyAsync(Y, v, sizeof v, hipMemcpyHostToDevice, e->stream));
-    if (int rc = coll->allreduce(e, Y, 2)) return rc;
+    if (int rc = coll->allreduce(e, Y, 3)) return rc;
     PBA_HIP(hipMemcpyAsync(v, Y, sizeof v, hipMemcpyDeviceToHost, e->stream));
     PBA_HIP(hipStreamSynchronize(e->stream));
     cost = v[0];
     n_valid = (int)v[1];
+    chk.n_ranks = (int)v[2];
+  }
+  if (const char* pv = std::getenv("PBA_TEST_PERTURB_DECISION")) {  // tests: "rank:trial:mode"
+    int pr = -1, pt = -1, pm = 1;
+    if (std::sscanf(pv, "%d:%d:%d", &pr, &pt, &pm) >= 2 && pr == (coll->comm ? comm_rank(coll->comm) : G.dist_rank)) {
+      chk.perturb_seq = pt;
+      chk.perturb_mode = pm;
+    }
   }
   s.linearize_ms = now_ms() - t0;
   s.initial_cost = cost;
@@ -4445,27 +4520,42 @@ int lm_loop(pba_engine* e, const pba_solver_options* o, const Collective* coll, 
   const int n = std::max(0, opt.max_iterations);
   const DecideOpts dopt = decide_opts(opt);
   Trajectory traj(G.history, opt.initial_trust_region_radius);
-  if (n > 0)
-    if (int rc = dist_trial(e, *coll, dopt, X, K, 1.0)) return rc;
-  int iter = 0, set = 0;
+  int last_enq = 0;  // the last trial enqueued (collectives included)
+  if (n > 0) {
+    if (int rc = dist_trial(e, *coll, dopt, X, K, 1.0, chk)) return rc;
+    last_enq = 1;
+  }
+  int iter = 0, set = 0, stop_seq = 0;  // stop_seq: the trial whose record ended the loop
+  double stop_done = 0.0;
   s.termination = PBA_TERMINATION_MAX_ITERATIONS;
   s.stop_reason = PBA_STOP_MAX_ITERATIONS;
   for (; iter < n; ++iter) {
-    if (iter + 1 < n)
-      if (int rc = dist_trial(e, *coll, dopt, X, K, (double)(iter + 2))) return rc;  // ahead of this trial's decision
+    if (iter + 1 < n) {
+      if (int rc = dist_trial(e, *coll, dopt, X, K, (double)(iter + 2), chk)) return rc;  // ahead of this decision
+      last_enq = iter + 2;
+    }
     double d[kLmFields];
     if (int rc = wait_decision(e, (double)(iter + 1), d)) return rc;
     set = (int)d[kLmSet];
-    traj.trial(d);
     s.gradient_max_norm = d[kLmGradNorm];
     const double done = d[kLmDone];
+    if (done == kDoneDesync) {
+      stop_seq = iter + 1;
+      stop_done = done;
+      break;
+    }
+    traj.trial(d);
     if (done != 0.0 && done != kDoneRadius) {
+      stop_seq = iter + 1;
+      stop_done = done;
       if (finish_summary(done, s)) ++iter;
       break;
     }
     if (d[kLmAccept] == 0.0) {
       ++s.unsuccessful_steps;
       if (done != 0.0) {
+        stop_seq = iter + 1;
+        stop_done = done;
         finish_summary(done, s);
         ++iter;
         break;
@@ -4475,8 +4565,47 @@ int lm_loop(pba_engine* e, const pba_solver_options* o, const Collective* coll, 
     ++s.successful_steps;
     cost = d[kLmCostNew];
   }
+  // Every rank must leave with the same collectives issued.  Ranks whose records agree stop on the same trial; if they
+  // differed at trial k, the next trial's check ends the solve everywhere (kDoneDesync), but a rank whose record k said
+  // done has enqueued one trial fewer than a rank that went on (which enqueued k + 2 ahead): it reads record k + 1 (always
+  // published) and, when ranks went on, issues trial k + 2 too.  Then the last decision is checked by one more scalar
+  // all-reduce on every rank.
+  bool desync = stop_done == kDoneDesync;
+  int desync_at = desync ? stop_seq - 1 : 0;
+  if (!desync && stop_seq > 0 && last_enq > stop_seq) {
+    double d2[kLmFields];
+    if (int rc = wait_decision(e, (double)(stop_seq + 1), d2)) return rc;
+    if (d2[kLmDone] == kDoneDesync) {
+      desync = true;
+      desync_at = stop_seq;
+      const int stopped = (int)d2[kLmDesync] - 1;  // ranks whose record stop_seq ended the solve
+      if (stopped < chk.n_ranks && stop_seq + 2 <= n) {
+        if (int rc = dist_trial(e, *coll, dopt, X, K, (double)(stop_seq + 2), chk)) return rc;
+        last_enq = stop_seq + 2;
+      }
+    }
+  }
+  {
+    double* Y = X + (long long)e->n_frames * ex_row(K);
+    dist_verify_kernel<<<1, 64, 0, e->stream>>>(G.lm.p, Y);
+    PBA_HIP(hipGetLastError());
+    if (int rc = coll->allreduce(e, Y, kExScalars)) return rc;
+    const double vseq = (double)(last_enq + 1);
+    dist_decide_kernel<<<1, 64, 0, e->stream>>>(Y, G.tpose.p, 1, dopt, G.lm.p, G.lm_host_d + rec_slot(vseq), vseq,
+                                                chk.n_ranks, -1.0, 0, 1);
+    PBA_HIP(hipGetLastError());
+    double d3[kLmFields];
+    if (int rc = wait_decision(e, vseq, d3)) return rc;
+    if (!desync && d3[kLmDone] == kDoneDesync) {
+      desync = true;
+      desync_at = last_enq;
+    }
+  }
   launch_accept(e, G.lm.p);
   PBA_HIP(hipStreamSynchronize(e->stream));
+  if (desync)
+    return fail(PBA_ERR_DEVICE, "multi-GPU solve: the ranks' LM decisions differed at trial " + std::to_string(desync_at) +
+                                    " (decision-word check); every rank ended the solve");
   traj.finish(s.initial_cost);
   if (set == 1) {
     std::swap(G.blk_schur.p, G.blk_schur1.p);

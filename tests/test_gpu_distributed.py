@@ -191,6 +191,47 @@ def test_solve_distributed_comm_local_group_matches_solve(kind, model, huber):
             e.close()
 
 
+@pytest.mark.parametrize("mode,trial", [(1, 3), (2, 3), (1, 6), (2, 6)])
+def test_solve_distributed_comm_desync_fails_loudly(monkeypatch, mode, trial):
+    """The decision-word check of the device-steered loop: every trial's scalar all-reduce also sums each rank's
+    previous decision word and its square (N·Σw² = (Σw)² iff the words agree).  PBA_TEST_PERTURB_DECISION overrides
+    one rank's decision of one trial (mode 1 flips accept, mode 2 ends that rank's solve): every rank must then return
+    an error naming the trial — not hang on mismatched collectives — including a perturbed last trial, which only the
+    final verification all-reduce sees."""
+    pb = synth.make_problem(kind=0, model=0, n_frames=16, n_points=400, width=376, height=240, seed=81,
+                            border=12, obs_sigma=0.3)
+    pb.poses[:2] = pb.poses_gt[:2]
+    world, iters = 3, 6
+    sh = shards(pb, world, 9.0, (0, 1))
+    comms = E.Comm.local_group(world)
+    try:
+        band = max(e.gn_band() for e, _ in sh)
+        res = run_ranks(lambda r: sh[r][0].solve_distributed_comm(band, comms[r], max_iterations=iters), world,
+                        timeout=120)
+        assert all(s["iterations"] == iters for s in res), res  # unperturbed: the loop runs its iterations
+        for e, pids in sh:
+            e.set_state(pb.poses, pb.rho[pids])
+        monkeypatch.setenv("PBA_TEST_PERTURB_DECISION", f"1:{trial}:{mode}")
+        errs = [None] * world
+
+        def run(r):
+            try:
+                sh[r][0].solve_distributed_comm(band, comms[r], max_iterations=iters)
+            except RuntimeError as ex:
+                errs[r] = str(ex)
+            return 0
+
+        run_ranks(run, world, timeout=120)
+        for r in range(world):
+            assert errs[r] is not None and f"differed at trial {trial} " in errs[r], (r, errs)
+        print("\n" + errs[0])
+    finally:
+        for c in comms:
+            c.close()
+        for e, _ in sh:
+            e.close()
+
+
 def test_solve_distributed_rccl_single_rank_matches_solve():
     """RCCL itself (librccl through pba_comm_init, one rank on this GPU — two ranks cannot share a device under
     RCCL): ncclAllReduce on the engine stream inside the device-steered loop gives pba_solve's trajectory."""
