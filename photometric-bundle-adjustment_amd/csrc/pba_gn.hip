@@ -209,11 +209,21 @@ void linearize_kernel(const KernelArgs a, const LinArgs g) {
   __shared__ __attribute__((aligned(16))) unsigned char arena[NW][kArena];
   __shared__ int s_wlo[NW], s_wn[NW];
   __shared__ float s_bc[kBlockThreads / LPB];  // block costs (0: invalid or dead), for the chunk's cost partial
+  __shared__ unsigned s_slots[NW][64];          // the product slot table (kSlotTable64), each lane's word parked in LDS
   const int chunk = logical_tile();
-  if (chunk >= g.n_chunks) return;
-  const int4 d = g.chunk_desc[chunk];
+  const int lb = threadIdx.x / LPB;
+  // one memory round: the record, the chunk descriptor, the block's linearise record and the slot table are all issued
+  // before either exit (at a clamped chunk), and the exits test them together — the compiler otherwise issued the record
+  // behind the chunk test, the descriptor behind the record's done test and the linearise record behind both (three
+  // dependent rounds before the tile's loads)
+  const int cc = min(chunk, g.n_chunks - 1);
+  const int4 d = g.chunk_desc[cc];
+  const int4 lr = g.lin_rec[(long long)cc * (kBlockThreads / LPB) + lb];
+  const unsigned slot_w = kSlotTable64.w[threadIdx.x & 63];
   const LmView lv = lm_view(g.lm);
-  if (lv.done != 0.0) return;
+  asm volatile("" ::"v"(lr.x), "v"(lr.y), "v"(lr.z), "v"(lr.w), "v"(slot_w), "s"(d.x), "s"(d.y), "s"(d.z), "s"(d.w));
+  s_slots[threadIdx.x >> 6][threadIdx.x & 63] = slot_w;  // (read back by the same lane: no barrier)
+  if (chunk >= g.n_chunks || lv.done != 0.0) return;
   const bool s1 = (lv.set != 0.0) != g.spare;
   double* const blk_schur = s1 ? g.blk_schur1 : g.blk_schur;
   double* const part_lin = s1 ? g.part_lin1 : g.part_lin;
@@ -223,22 +233,31 @@ void linearize_kernel(const KernelArgs a, const LinArgs g) {
   }
   const int count = d.y, n_t = d.z, poff = d.w;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int lb = threadIdx.x / LPB, k = threadIdx.x % LPB, wb = lb % BW;
+  const int k = threadIdx.x % LPB, wb = lb % BW;
   const bool live = lb < count;
   const int R = KIND == PBA_RESIDUAL_PHOTOMETRIC ? a.P : 2;
   const bool act = live && k < R;
   // the chunk's slots are padded to the workgroup's blocks (dead slots repeat slot 0), so the record is read with the
   // chunk descriptor, not behind it, and carries the block's point and pair: the tile prologue's loads come next
-  const int4 lr = g.lin_rec[(long long)chunk * (kBlockThreads / LPB) + lb];
   const int blk = lr.x, gpos = lr.w, lt = (int)((unsigned)lr.z >> 24);
   Row row;
   if constexpr (KIND == PBA_RESIDUAL_PHOTOMETRIC) {
     TileBlock* s_tb = reinterpret_cast<TileBlock*>(arena[wave]);
     const float2 off = pattern_at<LPB>(a, k);
-    const int pt = stage_tile_pp<LPB>(a, s_tb, wb, k, make_int2(lr.y, lr.z & 0xffffff));
-    const float Ih = act ? a.host_int[(long long)pt * R + k] : 0.0f;
+    // the host intensity in the tile's memory round (its point is in the linearise record): issued behind the tile's
+    // loads it cost a round of its own at the barrier
+    const float Ih = act ? a.host_int[(long long)lr.y * R + k] : 0.0f;
+    stage_tile_pp<LPB>(a, s_tb, wb, k, make_int2(lr.y, lr.z & 0xffffff));
+    asm volatile("" ::"v"(Ih));
     __syncthreads();
+#ifdef PBA_ABL_NOROW  // ablation builds (tools/build_variant.sh): timing of the parts, results are garbage
+    row.r = Ih + s_tb[wb].pr.Rf[k & 7] + off.x;
+    row.jr = row.hv.x = row.hv.y = row.hv.z = row.hw.x = row.hw.y = row.hw.z = row.r;
+    row.tv = row.hv;
+    row.tw = row.hw;
+#else
     row = photometric_row<MODEL, true>(a, s_tb[wb], off, Ih);  // dead lanes evaluate a staged block, masked below
+#endif
   } else {
     if (act) row = geometric_row<MODEL, true>(a, blk, k);
   }
@@ -248,9 +267,9 @@ void linearize_kernel(const KernelArgs a, const LinArgs g) {
   const float bcost = ok ? huber_cost(s, a.huber) : 0.0f;
   if (k == 0) s_bc[lb] = live && ok ? bcost : -1.0f;  // read after the barrier below
   // weighted row x̃ = √w · x  → products carry w (Ceres Corrector with ρ'' ≤ 0: J̃ = √ρ' J, r̃ = √ρ' r)
-  // the product slot table (a vector load): after the row (one register fewer across it: the row's peak pressure spilled
-  // at 8 waves/SIMD) and before any store of this kernel (a load issued after a store waits for the store too)
-  const unsigned slots = kSlotTable64.w[lane];
+  // the product slot table, loaded in the first memory round and parked in LDS across the row (one register fewer
+  // there: the row's peak pressure spilled at 8 waves/SIMD)
+  const unsigned slots = s_slots[wave][lane];
   // rows outside the domain / of dead lanes are all zero (selects, not a zero weight: such a row may hold inf / NaN)
   const bool use = act && ok;
   const float sw = use ? sqrtf(w) : 0.0f;
@@ -293,6 +312,7 @@ void linearize_kernel(const KernelArgs a, const LinArgs g) {
     v4f64 tacc = {0.0, 0.0, 0.0, 0.0};
     int cur = lo;
     // block b's chain (SPB dependent steps); a dead block's rows are zeros, so its chain is issued unconditionally
+#ifndef PBA_ABL_NOMFMA
     auto chain = [&](int b) {
       v4f64 acc = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
@@ -302,16 +322,36 @@ void linearize_kernel(const KernelArgs a, const LinArgs g) {
       }
       return acc;
     };
+#endif
     // two blocks in flight: block b + 1's matrix-core steps are issued before block b's result is consumed (each
     // dependent fp64 step waited out its latency before the point-data store and the run sum otherwise)
+#ifdef PBA_ABL_NOMFMA
+    auto chain = [&](int b) {
+      const double o = (double)op[b * SPB];
+      return v4f64{o, o, o, o};
+    };
+#endif
     v4f64 nxt = chain(0);
 #pragma unroll
     for (int b = 0; b < BW; ++b) {
       const v4f64 acc = nxt;
       if (b + 1 < BW) nxt = chain(b + 1);
+#ifdef PBA_ABL_NOBLK
+      if (b == 0) {
+        tacc = acc;
+        cur = lo;
+      }
+      if (false) {
+#else
       if (b < nbw) {
+#endif
         const int gpb = __builtin_amdgcn_readlane(gpos, b * LPB);
+#ifndef PBA_ABL_NOPTSTORE
         if (pc >= 0) blk_schur[(long long)gpb * 16 + pq] = acc[3];
+#else
+        if (pc >= 0 && gpb < 0) blk_schur[(long long)gpb * 16 + pq] = acc[3];
+#endif
+#ifndef PBA_ABL_NORUN
         const int ltb = __builtin_amdgcn_readlane(lt, b * LPB);
         if (ltb != cur) {
           flush(tacc, cur - lo);
@@ -319,6 +359,7 @@ void linearize_kernel(const KernelArgs a, const LinArgs g) {
           cur = ltb;
         }
         tacc += acc;
+#endif
       }
     }
     if (nbw > 0) flush(tacc, cur - lo);
@@ -331,7 +372,11 @@ void linearize_kernel(const KernelArgs a, const LinArgs g) {
   // chunk partial slots, fixed summation order (wave, then slot): H_hh / g_h over every product set of the chunk,
   // H_ht / H_tt / g_t of local target j from the ≤ NW sets of j (one per wave that holds j's blocks)
   auto sset = [&](int w, int i, int v) -> double { return reinterpret_cast<const double*>(arena[w])[i * NVP + v]; };
+#ifdef PBA_ABL_NOPART
+  const int nout = 0;
+#else
   const int nout = SLOT_LIN_BASE + SLOT_LIN_T * n_t;
+#endif
   for (int o = threadIdx.x; o < nout; o += kBlockThreads) {
     int v, j = -1;
     if (o < 36) {
@@ -375,6 +420,260 @@ void linearize_kernel(const KernelArgs a, const LinArgs g) {
     if (lane == 0) {
       g.wg_red[2 * chunk] = c;
       g.wg_red[2 * chunk + 1] = v;
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// linearize_adj_kernel: the photometric linearisation of ≤ 8-px patterns through the pair's adjoint
+// ------------------------------------------------------------------------------------------------
+// A photometric row's host Jacobian is its target Jacobian through the relative pose: with p̃ = R b + ρ t (R = R_th,
+// t = t_th) the rows of photometric_row satisfy [hv hw] = −[tv tw]·Ad, Ad = [[R, [t]×R], [0, R]] — the SE(3) adjoint of
+// T_th (exact algebra: hv = ρ qR = −tv R, hw = b × qR = −tw R − tv [t]× R).  Ceres differentiates both poses through
+// the functor (photometric_error.h:146-186); the normal equations only need their products, and those follow from the
+// target's: J_hᵀJ_h = Adᵀ(J_tᵀJ_t)Ad, J_hᵀJ_t = −Adᵀ(J_tᵀJ_t), J_hᵀr = −Adᵀ(J_tᵀr), J_ρᵀJ_h = −(J_ρᵀJ_t)Ad — linear in
+// the per-target sums, so applied once per (chunk, target) and once per block for the point data.  The matrix cores
+// then form only the 8-column products of x = √w [tv tw jr r] (36 in the upper triangle, against 104 of the 14-column
+// rows): per block the three 4×4 tiles (0,0), (0,1), (1,1) of xᵀx, K = 8 rows in two steps of v_mfma_f64_4x4x4_4b_f64
+// (16 cycles each, against two 64-cycle v_mfma_f64_16x16x4f64).  Same chunk partials and point data as
+// linearize_kernel (the 14-column kernel, kept for the geometric rows and as PBA_LIN_LEGACY's A/B reference).
+// MFMA layout (tools/micro/mfma_f64_4x4_layout.hip, measured): lane l works in 4×4 block β = (l >> 2) & 3; A holds
+// A_β[l & 3][l >> 4], B holds B_β[l >> 4][l & 3], the accumulator C_β[l >> 4][l & 3].
+__host__ __device__ constexpr int upper8(int r, int c) { return r * 8 - r * (r - 1) / 2 + (c - r); }  // r ≤ c < 8
+
+template <int MODEL>
+__global__ __launch_bounds__(kBlockThreads) __attribute__((amdgpu_waves_per_eu(8, 8)))
+void linearize_adj_kernel(const KernelArgs a, const LinArgs g) {
+  constexpr int LPB = 8, BW = 64 / LPB, NW = kBlockThreads / 64;
+  constexpr int kRowS = 12;                  // floats per staged row (8 used): 8-lane groups of b128 stores hit 32 banks
+  constexpr int NQ = 36;                     // products per run set (the 8 × 8 upper triangle)
+  constexpr int kTileW = BW * (int)sizeof(TileBlock), kRowsW = 64 * kRowS * 4, kProdW = kChunkTargets * NQ * 8;
+  constexpr int kRegW = kTileW > kRowsW ? kTileW : kRowsW;
+  constexpr int kArena = kRegW + kProdW;
+  constexpr int kWt = BW * 6 * 8;            // a wave's W_t (after its block loop, over block 0's rows)
+  static_assert(kWt + kChunkTargets * 64 * 8 <= kRowsW && kWt + kChunkTargets * 36 * 8 <= kRowsW, "phase data fits");
+  static_assert(kBlockThreads == 64 * kChunkTargets, "one thread per entry of the targets' 8 × 8 sums");
+  // per wave: [tile blocks, then the weighted rows over them | the run product sets]
+  __shared__ __attribute__((aligned(16))) unsigned char arena[NW][kArena];
+  __shared__ double s_rt[kChunkTargets][12];  // R_th, t_th of each local target (the host is the chunk's)
+  __shared__ double s_ad[kChunkTargets][36];  // Ad of each local target
+  __shared__ int s_wlo[NW], s_wn[NW];
+  __shared__ float s_bc[kBlockThreads / LPB];
+  const int chunk = logical_tile();
+  const int lb = threadIdx.x / LPB;
+  // one memory round: record, chunk descriptor and linearise record before either exit (see linearize_kernel)
+  const int cc = min(chunk, g.n_chunks - 1);
+  const int4 d = g.chunk_desc[cc];
+  const int4 lr = g.lin_rec[(long long)cc * (kBlockThreads / LPB) + lb];
+  const LmView lv = lm_view(g.lm);
+  asm volatile("" ::"v"(lr.x), "v"(lr.y), "v"(lr.z), "v"(lr.w), "s"(d.x), "s"(d.y), "s"(d.z), "s"(d.w));
+  if (chunk >= g.n_chunks || lv.done != 0.0) return;
+  const bool s1 = (lv.set != 0.0) != g.spare;
+  double* const blk_schur = s1 ? g.blk_schur1 : g.blk_schur;
+  double* const part_lin = s1 ? g.part_lin1 : g.part_lin;
+  if (g.lin_set && chunk == 0 && threadIdx.x == 0) {  // (the λ-free elimination after this launch reads them)
+    *g.lin_set = s1 ? 1 : 0;
+    g.degen[s1 ? 1 : 0] = 0;
+  }
+  const int count = d.y, n_t = d.z, poff = d.w;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int k = threadIdx.x % LPB, wb = lb % BW;
+  const bool live = lb < count;
+  const int R = a.P;
+  const bool act = live && k < R;
+  const int blk = lr.x, gpos = lr.w, lt = (int)((unsigned)lr.z >> 24);
+  TileBlock* s_tb = reinterpret_cast<TileBlock*>(arena[wave]);
+  const float2 off = pattern_at<LPB>(a, k);
+  const float Ih = act ? a.host_int[(long long)lr.y * R + k] : 0.0f;
+  stage_tile_pp<LPB>(a, s_tb, wb, k, make_int2(lr.y, lr.z & 0xffffff));
+  asm volatile("" ::"v"(Ih));
+  __syncthreads();
+  const Row row = photometric_row<MODEL, true>(a, s_tb[wb], off, Ih);  // (hv, hw unused: not formed)
+  {  // R_th, t_th of the block's target, from the first block of each target in the wave (same values if repeated)
+    const int prev = __shfl(lt, (lane - LPB) & 63, 64);
+    if (live && (wb == 0 || prev != lt)) {
+      const PairRec& pr = s_tb[wb].pr;
+      s_rt[lt][k] = pr.R[k];
+      if (k < 4) s_rt[lt][8 + k] = k == 0 ? pr.R[8] : pr.t[k - 1];
+    }
+  }
+  const int ok = group_all<LPB>(act ? row.ok : 1);
+  const float s = group_sum<LPB>(act && ok ? row.r * row.r : 0.0f);
+  const float w = ok ? huber_weight(s, a.huber) : 0.0f;
+  const float bcost = ok ? huber_cost(s, a.huber) : 0.0f;
+  if (k == 0) s_bc[lb] = live && ok ? bcost : -1.0f;  // read after the barrier below
+  const bool use = act && ok;
+  const float sw = use ? sqrtf(w) : 0.0f;
+  auto wx = [&](float v) { return use ? sw * v : 0.0f; };
+  float* sX = reinterpret_cast<float*>(arena[wave]);  // the wave's 64 rows (over its tile blocks)
+  {
+    float4* xr = reinterpret_cast<float4*>(sX + lane * kRowS);
+    xr[0] = make_float4(wx(row.tv.x), wx(row.tv.y), wx(row.tv.z), wx(row.tw.x));
+    xr[1] = make_float4(wx(row.tw.y), wx(row.tw.z), wx(row.jr), wx(row.r));
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  double* const sWt = reinterpret_cast<double*>(arena[wave]);  // W_t of the wave's blocks, over block 0's rows
+  const int nbw = min(max(count - wave * BW, 0), BW);
+  {
+    // lane l: 4×4 block β — tiles (0,0), (0,1), (1,1) of xᵀx, and β = 3 repeating (0,1) unused — operand columns
+    // ca / cb, product (pr_, pc_)
+    const int beta = (lane >> 2) & 3, i4 = lane & 3, kq = lane >> 4;
+    const int I = beta == 2 ? 1 : 0, J = beta == 0 ? 0 : 1;
+    const int ca = 4 * I + i4, cb = 4 * J + i4;
+    const int pr_ = 4 * I + kq, pc_ = 4 * J + i4;
+    const int pslot = beta < 3 && pr_ <= pc_ ? upper8(pr_, pc_) : -1;
+    // the point data: column 6 (jr) of tiles (0,1) and (1,1) — W_t[0..3] and W_t[4..5], H_ρρ, g_ρ — at its blk_schur
+    // position [H_ρρ, g_ρ, W_h(6), W_t(6), 0, 0] (the zeros from two lanes of β = 3)
+    const int ppos = beta == 3 ? (kq == 0 && i4 < 2 ? 14 + i4 : -1)
+                               : (i4 != 2 || beta == 0 ? -1 : (beta == 1 ? 8 + kq : (kq < 2 ? 12 + kq : kq - 2)));
+    double* sP = reinterpret_cast<double*>(arena[wave] + kRegW);
+    const int lo = __builtin_amdgcn_readfirstlane(lt);
+    auto ops = [&](int b, float* o) {  // block b's operands: A, B of K steps 0 and 1
+#pragma unroll
+      for (int st = 0; st < 2; ++st) {
+        const float* xr = sX + (8 * b + 4 * st + kq) * kRowS;
+        o[2 * st] = xr[ca];
+        o[2 * st + 1] = xr[cb];
+      }
+    };
+    double tacc = 0.0;
+    int cur = lo;
+    float o_n[4];
+    ops(0, o_n);
+#pragma unroll
+    for (int b = 0; b < BW; ++b) {
+      float o[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) o[q] = o_n[q];
+      if (b + 1 < BW) ops(b + 1, o_n);  // the next block's LDS reads in flight over this block's matrix-core steps
+      double acc = 0.0;
+#pragma unroll
+      for (int st = 0; st < 2; ++st)
+        acc = __builtin_amdgcn_mfma_f64_4x4x4f64((double)o[2 * st], (double)o[2 * st + 1], acc, 0, 0, 0);
+      if (b < nbw) {
+        const int gpb = __builtin_amdgcn_readlane(gpos, b * LPB);
+        if (ppos >= 0) {
+          blk_schur[(long long)gpb * 16 + ppos] = ppos < 14 ? acc : 0.0;
+          if (ppos >= 8 && ppos < 14) sWt[b * 6 + ppos - 8] = acc;
+        }
+        const int ltb = __builtin_amdgcn_readlane(lt, b * LPB);
+        if (ltb != cur) {
+          if (pslot >= 0) sP[(cur - lo) * NQ + pslot] = tacc;
+          tacc = 0.0;
+          cur = ltb;
+        }
+        tacc += acc;
+      }
+    }
+    if (nbw > 0 && pslot >= 0) sP[(cur - lo) * NQ + pslot] = tacc;
+    if (lane == 0) {
+      s_wlo[wave] = lo;
+      s_wn[wave] = nbw > 0 ? cur - lo + 1 : 0;
+    }
+  }
+  __syncthreads();
+  // Phase A: the chunk's product sums per local target j, as full 8 × 8 matrices (one thread per entry; the sets of j
+  // over the waves in order), and Ad_j from R_th, t_th.  Over wave 0's rows, after its W_t.
+  double* sT = reinterpret_cast<double*>(arena[0] + kWt);  // [j][8][8]
+  double* sN = reinterpret_cast<double*>(arena[1] + kWt);  // [j][6][6]: H_tt,j·Ad_j
+  {
+    const int t = threadIdx.x, j = t >> 6, r = (t >> 3) & 7, c = t & 7;
+    if (j < n_t) {
+      const int u = upper8(min(r, c), max(r, c));
+      double acc = 0.0;
+#pragma unroll
+      for (int w_ = 0; w_ < NW; ++w_) {
+        const int wl = s_wlo[w_], wn = s_wn[w_];
+        if (j >= wl && j < wl + wn) acc += reinterpret_cast<const double*>(arena[w_] + kRegW)[(j - wl) * NQ + u];
+      }
+      sT[t] = acc;
+    }
+    if (t < 36 * n_t) {  // Ad = [[R, [t]×R], [0, R]]; ([t]×R)[q][c] = t[q+1] R[q+2][c] − t[q+2] R[q+1][c] (indices mod 3)
+      const int jj = t / 36, e = t - 36 * jj, q = e / 6, p = e - 6 * q;
+      const double* rt = s_rt[jj];
+      double v = 0.0;
+      if (q < 3 && p < 3) {
+        v = rt[3 * q + p];
+      } else if (q >= 3 && p >= 3) {
+        v = rt[3 * (q - 3) + (p - 3)];
+      } else if (q < 3) {
+        const int c = p - 3, q1 = q == 2 ? 0 : q + 1, q2 = q == 0 ? 2 : q - 1;
+        v = rt[9 + q1] * rt[3 * q2 + c] - rt[9 + q2] * rt[3 * q1 + c];
+      }
+      s_ad[jj][e] = v;
+    }
+  }
+  __syncthreads();
+  // Phase B: per block W_h = −W_t·Ad (lane 6b + c of each wave); N_j = H_tt,j·Ad_j; the target outputs — H_ht = −AdᵀH_tt,
+  // H_tt, g_t — and g_h = −Σ_j Ad_jᵀ g_t,j
+  {
+    const int bb = lane / 6, c = lane - 6 * bb;
+    const int gpb = __shfl(gpos, (bb * LPB) & 63, 64), ltb = __shfl(lt, (bb * LPB) & 63, 64);
+    if (bb < nbw) {
+      double v = 0.0;
+#pragma unroll
+      for (int m = 0; m < 6; ++m) v += sWt[bb * 6 + m] * s_ad[ltb][6 * m + c];
+      blk_schur[(long long)gpb * 16 + 2 + c] = -v;
+    }
+  }
+  const int nout = SLOT_LIN_BASE + SLOT_LIN_T * n_t;
+  for (int o = threadIdx.x; o < nout; o += kBlockThreads) {
+    if (o < 36) {
+      const int r = o / 6, c = o - 6 * (o / 6);
+      for (int j = 0; j < n_t; ++j) {
+        double v = 0.0;
+#pragma unroll
+        for (int p = 0; p < 6; ++p) v += sT[64 * j + 8 * r + p] * s_ad[j][6 * p + c];
+        sN[36 * j + o] = v;
+      }
+      continue;
+    }
+    double v = 0.0;
+    if (o < 42) {
+      const int r = o - 36;
+      for (int j = 0; j < n_t; ++j)
+#pragma unroll
+        for (int q = 0; q < 6; ++q) v -= s_ad[j][6 * q + r] * sT[64 * j + 8 * q + 7];
+    } else {
+      const int j = (o - 42) / SLOT_LIN_T, q = (o - 42) - SLOT_LIN_T * j;
+      if (q < 36) {
+        const int r = q / 6, c = q - 6 * (q / 6);
+#pragma unroll
+        for (int p = 0; p < 6; ++p) v -= s_ad[j][6 * p + r] * sT[64 * j + 8 * p + c];
+      } else if (q < 72) {
+        const int r = (q - 36) / 6, c = (q - 36) % 6;
+        v = sT[64 * j + 8 * r + c];
+      } else {
+        v = sT[64 * j + 8 * (q - 72) + 7];
+      }
+    }
+    part_lin[(long long)poff + o] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x < 36) {  // Phase C: H_hh[r][c] = Σ_j Σ_q Ad_j[q][r] N_j[q][c], (r, c) and (c, r) from one sum
+    const int o = threadIdx.x, r0 = o / 6, c0 = o - 6 * (o / 6), r = min(r0, c0), c = max(r0, c0);
+    double v = 0.0;
+    for (int j = 0; j < n_t; ++j)
+#pragma unroll
+      for (int q = 0; q < 6; ++q) v += s_ad[j][6 * q + r] * sN[36 * j + 6 * q + c];
+    part_lin[(long long)poff + o] = v;
+  }
+  if (live && k == 0) {
+    a.valid[blk] = (uint8_t)ok;
+    a.cost[blk] = bcost;
+  }
+  if (g.wg_red && wave == 0) {  // the chunk's (Σ cost, Σ valid): lane b takes block b, xor butterflies (fixed order)
+    const float x = lane < count ? s_bc[lane] : -1.0f;
+    double cs = x >= 0.0f ? (double)x : 0.0, vs = x >= 0.0f ? 1.0 : 0.0;
+    for (int m = 32; m >= 1; m >>= 1) {
+      cs += __shfl_xor(cs, m, 64);
+      vs += __shfl_xor(vs, m, 64);
+    }
+    if (lane == 0) {
+      g.wg_red[2 * chunk] = cs;
+      g.wg_red[2 * chunk + 1] = vs;
     }
   }
 }
@@ -592,16 +891,29 @@ struct SchurArgs {
 // λ-free pass of the device LM loop, λ = 0): set to 1 when a point's H_ρρ lies outside the LM diagonal's clamp [1e-6, 1e32]
 // (H = 0 excepted: such a point has W = 0) — only inside it is H + λ·clamp(H) = (1 + λ)·H, the identity the λ-free pass
 // relies on (schur_free_decide_kernel).
-__device__ __forceinline__ void schur_chunk(const SchurArgs& g, int c, double lambda, const double* __restrict__ blk_schur,
-                                            double* __restrict__ part_out, double* __restrict__ pt_out, int* degen,
-                                            double* W_dyn, double* s_inv, double* s_gl) {
-  const int4 d = g.desc[c];
-  const int4 ax = g.aux[c];
-  constexpr int kPtIter = (SCHUR_PTS + kBlockThreads / 4 - 1) / (kBlockThreads / 4);
+// A chunk's descriptors and point records: the first loads of its elimination (schur_head), separate so that a kernel
+// can issue them in one memory round with loads of its own (schur_free_decide_kernel: the record and the set).
+constexpr int kPtIter = (SCHUR_PTS + kBlockThreads / 4 - 1) / (kBlockThreads / 4);
+struct SchurHead {
+  int4 d, ax;
   int2 prec[kPtIter];
+};
+__device__ __forceinline__ SchurHead schur_head(const SchurArgs& g, int c) {
+  SchurHead h;
+  h.d = g.desc[c];
+  h.ax = g.aux[c];
 #pragma unroll
   for (int it = 0; it < kPtIter; ++it)
-    prec[it] = g.pt_fb[(long long)c * SCHUR_PTS + it * (kBlockThreads / 4) + (threadIdx.x >> 2)];
+    h.prec[it] = g.pt_fb[(long long)c * SCHUR_PTS + it * (kBlockThreads / 4) + (threadIdx.x >> 2)];
+  return h;
+}
+__device__ __forceinline__ void schur_chunk(const SchurArgs& g, const SchurHead& h, double lambda,
+                                            const double* __restrict__ blk_schur, double* __restrict__ part_out,
+                                            double* __restrict__ pt_out, int* degen, double* W_dyn, double* s_inv,
+                                            double* s_gl) {
+  const int4 d = h.d;
+  const int4 ax = h.ax;
+  const int2* prec = h.prec;
   const int first = d.x, npt = d.y, nv = d.z, poff = d.w;
   double (*W)[6] = reinterpret_cast<double (*)[6]>(W_dyn);
   for (int i = threadIdx.x; i < npt * nv * 6; i += kBlockThreads) (&W[0][0])[i] = 0.0;
@@ -771,7 +1083,7 @@ __global__ __launch_bounds__(kBlockThreads) void schur_kernel(const SchurArgs g,
   ac.load(g, lv);
   lambda = lm_lambda(lv, lambda);
   const double* const blk_schur = lv.set != 0.0 ? g.blk_schur1 : g.blk_schur;
-  schur_chunk(g, c, lambda, blk_schur, g.part_schur, g.pt_data, nullptr, W_dyn, s_inv, s_gl);
+  schur_chunk(g, schur_head(g, c), lambda, blk_schur, g.part_schur, g.pt_data, nullptr, W_dyn, s_inv, s_gl);
   ac.store(g);
 }
 
@@ -2952,9 +3264,17 @@ __global__ __launch_bounds__(kBlockThreads) void schur_free_decide_kernel(const 
   }
   const int c = blockIdx.x - 1;
   if (c >= g.n_chunks) return;
-  if (!da.init && da.lm[kLmDone] != 0.0) return;
-  const int set = *fs.lin_set != 0;
-  schur_chunk(g, c, 0.0, set ? g.blk_schur1 : g.blk_schur, fs.part[set], fs.pt[set], fs.degen + set, W_dyn, s_inv, s_gl);
+  // one memory round: the chunk's descriptors, the record's done flag and the set, all issued before the exit (the
+  // compiler otherwise waited for the flag, then for the set, then issued the descriptors)
+  const SchurHead h = schur_head(g, c);
+  const double done = da.lm[kLmDone];
+  const int lset = *fs.lin_set;
+  asm volatile("" ::"v"(done), "v"(lset), "v"(h.d.x), "v"(h.ax.x));
+#pragma unroll
+  for (int it = 0; it < kPtIter; ++it) asm volatile("" ::"v"(h.prec[it].x), "v"(h.prec[it].y));
+  if (!da.init && done != 0.0) return;
+  const int set = lset != 0;
+  schur_chunk(g, h, 0.0, set ? g.blk_schur1 : g.blk_schur, fs.part[set], fs.pt[set], fs.degen + set, W_dyn, s_inv, s_gl);
 }
 
 // The single-GPU LM trial's first kernel: the previous trial's accept, and — only for a set flagged degen — the
@@ -2971,7 +3291,7 @@ __global__ __launch_bounds__(kBlockThreads) void schur_gate_kernel(const SchurAr
   if ((set ? dg1 : dg0) != 0 && lv.done == 0.0) {
     const double* blk_schur = set ? g.blk_schur1 : g.blk_schur;
     for (int c = blockIdx.x; c < g.n_chunks; c += gridDim.x) {
-      schur_chunk(g, c, lv.lambda, blk_schur, g.part_schur, nullptr, nullptr, W_dyn, s_inv, s_gl);
+      schur_chunk(g, schur_head(g, c), lv.lambda, blk_schur, g.part_schur, nullptr, nullptr, W_dyn, s_inv, s_gl);
       __syncthreads();
     }
   }
@@ -3552,7 +3872,8 @@ void launch_linearize(pba_engine* e, const KernelArgs& ka, const LinArgs& la) {
       case 3: linearize_rows_kernel<MODEL, 3><<<grid, kBlockThreads, 0, e->stream>>>(ka, la); return;
       default: linearize_rows_kernel<MODEL, 4><<<grid, kBlockThreads, 0, e->stream>>>(ka, la); return;
     }
-    linearize_kernel<KIND, MODEL, 8><<<grid, kBlockThreads, 0, e->stream>>>(ka, la);
+    if (e->gn.lin_legacy) linearize_kernel<KIND, MODEL, 8><<<grid, kBlockThreads, 0, e->stream>>>(ka, la);
+    else linearize_adj_kernel<MODEL><<<grid, kBlockThreads, 0, e->stream>>>(ka, la);
   } else {
     linearize_kernel<KIND, MODEL, 4><<<grid, kBlockThreads, 0, e->stream>>>(ka, la);
   }

@@ -727,7 +727,9 @@ struct GnData {
   // Σ W Wᵀ/H, Σ W g/H and the point data, a flag for a point outside the LM clamp, the set the last linearisation wrote
   DevBuf<double> part_free0, part_free1, pt_data1;
   DevBuf<int> degen, lin_set;
-  bool force_degen = std::getenv("PBA_TEST_FORCE_DEGEN") != nullptr;  // tests: the λ-specific path on every trial
+  bool force_degen = std::getenv("PBA_TEST_FORCE_DEGEN") != nullptr;
+  // tests: the 14-column linearisation (linearize_kernel) for ≤ 8-px photometric patterns instead of the adjoint form
+  bool lin_legacy = std::getenv("PBA_LIN_LEGACY") != nullptr;  // tests: the λ-specific path on every trial
   DevBuf<int> sky_first, sky_row, sky_last;  // skyline profile of the reduced camera system
   DevBuf<int> sky_cptr, g_cptr;  // contribution lists (CSR) per skyline block / per pose
   DevBuf<int2> sky_contrib, g_contrib;

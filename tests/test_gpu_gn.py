@@ -86,6 +86,48 @@ def test_reduced_system_large_patterns(P, pm):
     assert abs(c_new - cost_new_ref) <= 1e-5 * cost_new_ref + 1e-6
 
 
+@pytest.mark.parametrize("pm", [0, 1, 2, 3, 6])
+def test_adjoint_linearisation_matches_fourteen_columns(pm, monkeypatch):
+    """≤ 8-px photometric patterns linearise through the pair's adjoint (linearize_adj_kernel: the matrix cores form
+    the 8-column target products, the host blocks follow as Adᵀ·H_tt·Ad, −Adᵀ·H_tt, −Adᵀ·g_t and W_h = −W_t·Ad) —
+    against the 14-column products of the same rows (linearize_kernel, PBA_LIN_LEGACY) on the same problem: same
+    cost, reduced system and step to the rounding of the fp32 host rows (both are fp64 sums of fp32 rows; the host
+    Jacobian's fp32 rounding differs), then the same LM run."""
+    interp, model = pm >> 2, pm & 3
+    pb = synth.make_problem(model=model, n_frames=10, n_points=200, width=376, height=240, seed=70 + pm, border=12,
+                            obs_sigma=0.3)
+    pb.interp = interp
+    pb.poses[:2] = pb.poses_gt[:2]
+    out = {}
+    for legacy in (True, False):
+        if legacy:
+            monkeypatch.setenv("PBA_LIN_LEGACY", "1")
+        else:
+            monkeypatch.delenv("PBA_LIN_LEGACY")
+        with make_engine(pb, 9.0, (0, 1)) as eng:
+            c = eng.gn_linearize()
+            _, st = eng.gn_step(1e-3)
+            assert st == 0
+            S, gS = eng.gn_reduced_system()
+            dp, dl = eng.gn_last_step()
+            eng.set_state(pb.poses, pb.rho)
+            summ = eng.solve(max_iterations=10)
+        out[legacy] = (c, S, gS, dp, dl, summ)
+    (c0, S0, g0, dp0, dl0, s0), (c1, S1, g1, dp1, dl1, s1) = out[True], out[False]
+    eS = np.abs(S1 - S0).max() / np.abs(S0).max()
+    eg = np.abs(g1 - g0).max() / np.abs(g0).max()
+    ep = np.linalg.norm(dp1 - dp0) / np.linalg.norm(dp0)
+    el = np.linalg.norm(dl1 - dl0) / np.linalg.norm(dl0)
+    print(f"\nmodel {pm}: S {eS:.1e}, g {eg:.1e}, pose step {ep:.1e}, ρ step {el:.1e}, final cost "
+          f"{s1['final_cost']:.10e} / {s0['final_cost']:.10e}")
+    assert c1 == c0  # the same rows and weights: the cost does not depend on the products
+    assert eS <= 1e-6 and eg <= 1e-6, (eS, eg)
+    assert ep <= 1e-5 and el <= 1e-5, (ep, el)
+    for key in ("iterations", "successful_steps", "unsuccessful_steps", "termination"):
+        assert s1[key] == s0[key], (key, s1, s0)
+    assert abs(s1["final_cost"] - s0["final_cost"]) <= 1e-6 * s0["final_cost"]
+
+
 def test_candidate_cost_and_accept():
     pb = synth.make_problem(n_frames=8, n_points=80, width=376, height=240, seed=21, border=12)
     with make_engine(pb, 9.0, (0,)) as eng:

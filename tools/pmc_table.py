@@ -9,20 +9,18 @@ import sys
 
 
 def load(tag):
-    vals = collections.defaultdict(list)
-    name = None
+    """{kernel name: {counter: mean per dispatch}} over the tag's passes (a pass may cover several kernels)"""
+    vals = collections.defaultdict(lambda: collections.defaultdict(list))
     for f in sorted(glob.glob(f"gpurun_out/pmc_{tag}_*/run_counter_collection.csv")):
-        per = collections.defaultdict(float)  # (dispatch, counter) -> summed over dimensions
+        per = collections.defaultdict(float)  # (kernel, dispatch, counter) -> summed over dimensions
         for r in csv.DictReader(open(f)):
-            name = r["Kernel_Name"]
-            per[(r["Dispatch_Id"], r["Counter_Name"])] += float(r["Counter_Value"])
-        for (d, c), v in per.items():
-            vals[c].append(v)
-    return name, {c: sum(v) / len(v) for c, v in vals.items()}
+            per[(r["Kernel_Name"], r["Dispatch_Id"], r["Counter_Name"])] += float(r["Counter_Value"])
+        for (k, d, c), v in per.items():
+            vals[k][c].append(v)
+    return {k: {c: sum(v) / len(v) for c, v in cs.items()} for k, cs in vals.items()}
 
 
-for tag in sys.argv[1:]:
-    name, m = load(tag)
+def show(tag, name, m):
     print(f"== {tag}: {name[:90] if name else '?'}")
     for c in sorted(m):
         print(f"   {c:24s} {m[c]:16.1f}")
@@ -38,3 +36,8 @@ for tag in sys.argv[1:]:
             print(f"   {c + ' / wave cyc':30s} {m[c] / m['SQ_WAVE_CYCLES']:10.3f}")
     if "FETCH_SIZE" in m:
         print(f"   FETCH MB {m['FETCH_SIZE'] * 1024 / 1e6:.1f}  WRITE MB {m.get('WRITE_SIZE', 0) * 1024 / 1e6:.1f}")
+
+
+for tag in sys.argv[1:]:
+    for name, m in sorted(load(tag).items()):
+        show(tag, name, m)
