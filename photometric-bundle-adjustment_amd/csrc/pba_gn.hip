@@ -58,6 +58,7 @@ constexpr int NV = 104;          // normal-equation products per residual row
 #endif
 constexpr int SCHUR_PTS = PBA_SCHUR_PTS;   // points per Schur chunk (-DPBA_SCHUR_PTS: A/B builds)
 constexpr int SCHUR_W = 2048;    // points × local poses per Schur chunk (LDS budget: dynamic, 48 B each)
+constexpr int kPd = 8;            // point data per GN block: [H_ρρ, g_ρ, W_t(6)] (blk_schur)
 constexpr int SLOT_LIN_BASE = 42;  // H_hh(36) + g_h(6)
 constexpr int SLOT_LIN_T = 78;     // H_ht(36) + H_tt(36) + g_t(6)
 
@@ -150,7 +151,20 @@ struct LinArgs {
   bool spare;
   int* lin_set;             // or nullptr: the set written (workgroup 0 stores it, and clears degen[set])
   int* degen;
+  double* pair_rt;          // per pair [R_th(9), t_th(3)] of the linearisation (set 0 / set 1): schur_chunk forms
+  double* pair_rt1;         // W_h = −W_t·Ad from them
 };
+
+// The linearisation's R_th, t_th of pair `pair` into pair_rt, by lanes k < 12 of the LPB lanes of the first block of
+// each target in the wave (the same values where a pair's blocks span waves or chunks)
+template <int LPB>
+__device__ __forceinline__ void store_pair_rt(double* pair_rt, const double* R, const double* t, int pair, int lt, int k,
+                                              bool live) {
+  const int lane = threadIdx.x & 63;
+  const int prev = __shfl(lt, (lane - LPB) & 63, 64);
+  if (live && ((lane & ~(LPB - 1)) == 0 || prev != lt))
+    for (int e = k; e < 12; e += LPB) pair_rt[(long long)pair * 12 + e] = e < 9 ? R[e] : t[e - 9];
+}
 
 // ------------------------------------------------------------------------------------------------
 // linearize_kernel
@@ -258,8 +272,11 @@ void linearize_kernel(const KernelArgs a, const LinArgs g) {
 #else
     row = photometric_row<MODEL, true>(a, s_tb[wb], off, Ih);  // dead lanes evaluate a staged block, masked below
 #endif
+    store_pair_rt<LPB>(s1 ? g.pair_rt1 : g.pair_rt, s_tb[wb].pr.R, s_tb[wb].pr.t, lr.z & 0xffffff, lt, k, live);
   } else {
     if (act) row = geometric_row<MODEL, true>(a, blk, k);
+    const PairRec& pr = a.pairs[lr.z & 0xffffff];
+    store_pair_rt<LPB>(s1 ? g.pair_rt1 : g.pair_rt, pr.R, pr.t, lr.z & 0xffffff, lt, k, live);
   }
   const int ok = group_all<LPB>(act ? row.ok : 1);
   const float s = group_sum<LPB>(act && ok ? row.r * row.r : 0.0f);
@@ -308,7 +325,8 @@ void linearize_kernel(const KernelArgs a, const LinArgs g) {
     // per block: its own chain (SPB steps); row 12 of the result, C[12][c] in entry 3 of lanes c < 16, is the block's
     // point-elimination data x̃_ρ·x̃_c → [H_ρρ, g_ρ, W_h(6), W_t(6), 0, 0] at its GN position (schur_kernel walks
     // them point by point); the block's products are then added to its target run's sum
-    const int pc = lane < 16 ? lane : -1, pq = pc < 12 ? pc + 2 : (pc < 14 ? pc - 12 : pc);
+    // (column c of row 12: W_h for c < 6 — not stored, schur_chunk forms it from W_t — W_t for 6 ≤ c < 12, H_ρρ, g_ρ)
+    const int pc = lane < 16 ? lane : -1, pq = pc >= 6 && pc < 12 ? pc - 4 : (pc == 12 ? 0 : (pc == 13 ? 1 : -1));
     v4f64 tacc = {0.0, 0.0, 0.0, 0.0};
     int cur = lo;
     // block b's chain (SPB dependent steps); a dead block's rows are zeros, so its chain is issued unconditionally
@@ -346,11 +364,7 @@ void linearize_kernel(const KernelArgs a, const LinArgs g) {
       if (b < nbw) {
 #endif
         const int gpb = __builtin_amdgcn_readlane(gpos, b * LPB);
-#ifndef PBA_ABL_NOPTSTORE
-        if (pc >= 0) blk_schur[(long long)gpb * 16 + pq] = acc[3];
-#else
-        if (pc >= 0 && gpb < 0) blk_schur[(long long)gpb * 16 + pq] = acc[3];
-#endif
+        if (pq >= 0) blk_schur[(long long)gpb * kPd + pq] = acc[3];
 #ifndef PBA_ABL_NORUN
         const int ltb = __builtin_amdgcn_readlane(lt, b * LPB);
         if (ltb != cur) {
@@ -441,24 +455,34 @@ void linearize_kernel(const KernelArgs a, const LinArgs g) {
 // A_β[l & 3][l >> 4], B holds B_β[l >> 4][l & 3], the accumulator C_β[l >> 4][l & 3].
 __host__ __device__ constexpr int upper8(int r, int c) { return r * 8 - r * (r - 1) / 2 + (c - r); }  // r ≤ c < 8
 
-template <int MODEL>
-__global__ __launch_bounds__(kBlockThreads) __attribute__((amdgpu_waves_per_eu(8, 8)))
+// PPL > 1 (9…32 px, C5's 21): lane k evaluates pixels k, k + 8, … in PPL passes, as linearize_rows_kernel; each pass's
+// unweighted rows go through the matrix cores into per-block fp64 accumulators (the chain runs on across the passes) and
+// the block's Huber weight, known after its last row, scales them (x̃ᵀx̃ = w·xᵀx).  LDS per wave: the tile blocks and a
+// pass's rows side by side, the run product sets over the tile once the passes are done.
+#ifndef PBA_LINADJ_WAVES
+#define PBA_LINADJ_WAVES 5
+#endif
+template <int MODEL, int PPL>
+__global__ __launch_bounds__(kBlockThreads) __attribute__((amdgpu_waves_per_eu(PPL == 1 ? 8 : PBA_LINADJ_WAVES, 8)))
 void linearize_adj_kernel(const KernelArgs a, const LinArgs g) {
   constexpr int LPB = 8, BW = 64 / LPB, NW = kBlockThreads / 64;
   constexpr int kRowS = 12;                  // floats per staged row (8 used): 8-lane groups of b128 stores hit 32 banks
   constexpr int NQ = 36;                     // products per run set (the 8 × 8 upper triangle)
   constexpr int kTileW = BW * (int)sizeof(TileBlock), kRowsW = 64 * kRowS * 4, kProdW = kChunkTargets * NQ * 8;
-  constexpr int kRegW = kTileW > kRowsW ? kTileW : kRowsW;
-  constexpr int kArena = kRegW + kProdW;
-  constexpr int kWt = BW * 6 * 8;            // a wave's W_t (after its block loop, over block 0's rows)
-  static_assert(kWt + kChunkTargets * 64 * 8 <= kRowsW && kWt + kChunkTargets * 36 * 8 <= kRowsW, "phase data fits");
+  // per wave — PPL = 1: [tile blocks, then the weighted rows over them | run product sets];
+  //            PPL > 1: [tile blocks, then the run product sets over them | a pass's rows]
+  constexpr int kRowsOff = PPL == 1 ? 0 : kTileW;
+  constexpr int kProdOff = PPL == 1 ? (kTileW > kRowsW ? kTileW : kRowsW) : 0;
+  constexpr int kArena = PPL == 1 ? kProdOff + kProdW : kTileW + kRowsW;
+  static_assert(kProdW <= kTileW && kRowsW <= kTileW + 512, "regions");
+  static_assert(kChunkTargets * 64 * 8 <= kRowsW, "phase data fits a rows region");
   static_assert(kBlockThreads == 64 * kChunkTargets, "one thread per entry of the targets' 8 × 8 sums");
-  // per wave: [tile blocks, then the weighted rows over them | the run product sets]
   __shared__ __attribute__((aligned(16))) unsigned char arena[NW][kArena];
   __shared__ double s_rt[kChunkTargets][12];  // R_th, t_th of each local target (the host is the chunk's)
   __shared__ double s_ad[kChunkTargets][36];  // Ad of each local target
   __shared__ int s_wlo[NW], s_wn[NW];
   __shared__ float s_bc[kBlockThreads / LPB];
+  __shared__ float2 s_pat[PPL == 1 ? 1 : LPB * PPL];
   const int chunk = logical_tile();
   const int lb = threadIdx.x / LPB;
   // one memory round: record, chunk descriptor and linearise record before either exit (see linearize_kernel)
@@ -480,84 +504,144 @@ void linearize_adj_kernel(const KernelArgs a, const LinArgs g) {
   const int k = threadIdx.x % LPB, wb = lb % BW;
   const bool live = lb < count;
   const int R = a.P;
-  const bool act = live && k < R;
   const int blk = lr.x, gpos = lr.w, lt = (int)((unsigned)lr.z >> 24);
   TileBlock* s_tb = reinterpret_cast<TileBlock*>(arena[wave]);
-  const float2 off = pattern_at<LPB>(a, k);
-  const float Ih = act ? a.host_int[(long long)lr.y * R + k] : 0.0f;
-  stage_tile_pp<LPB>(a, s_tb, wb, k, make_int2(lr.y, lr.z & 0xffffff));
-  asm volatile("" ::"v"(Ih));
-  __syncthreads();
-  const Row row = photometric_row<MODEL, true>(a, s_tb[wb], off, Ih);  // (hv, hw unused: not formed)
-  {  // R_th, t_th of the block's target, from the first block of each target in the wave (same values if repeated)
+  float* sX = reinterpret_cast<float*>(arena[wave] + kRowsOff);  // the wave's 64 rows
+  // lane l: 4×4 block β — tiles (0,0), (0,1), (1,1) of xᵀx, and β = 3 repeating (0,1) unused — operand columns
+  // ca / cb, product (pr_, pc_)
+  const int beta = (lane >> 2) & 3, i4 = lane & 3, kq = lane >> 4;
+  const int I = beta == 2 ? 1 : 0, J = beta == 0 ? 0 : 1;
+  const int ca = 4 * I + i4, cb = 4 * J + i4;
+  auto ops = [&](int b, float* o) {  // block b's operands from the staged rows: A, B of K steps 0 and 1
+#pragma unroll
+    for (int st = 0; st < 2; ++st) {
+      const float* xr = sX + (8 * b + 4 * st + kq) * kRowS;
+      o[2 * st] = xr[ca];
+      o[2 * st + 1] = xr[cb];
+    }
+  };
+  auto save_rt = [&]() {  // R_th, t_th of the block's target from the first block of each target in the wave, for
+                          // the phases below and (pair_rt) the point elimination's W_h
     const int prev = __shfl(lt, (lane - LPB) & 63, 64);
     if (live && (wb == 0 || prev != lt)) {
       const PairRec& pr = s_tb[wb].pr;
-      s_rt[lt][k] = pr.R[k];
-      if (k < 4) s_rt[lt][8 + k] = k == 0 ? pr.R[8] : pr.t[k - 1];
+      double* prt = (s1 ? g.pair_rt1 : g.pair_rt) + (long long)(lr.z & 0xffffff) * 12;
+      s_rt[lt][k] = prt[k] = pr.R[k];
+      if (k < 4) s_rt[lt][8 + k] = prt[8 + k] = k == 0 ? pr.R[8] : pr.t[k - 1];
     }
-  }
-  const int ok = group_all<LPB>(act ? row.ok : 1);
-  const float s = group_sum<LPB>(act && ok ? row.r * row.r : 0.0f);
-  const float w = ok ? huber_weight(s, a.huber) : 0.0f;
-  const float bcost = ok ? huber_cost(s, a.huber) : 0.0f;
-  if (k == 0) s_bc[lb] = live && ok ? bcost : -1.0f;  // read after the barrier below
-  const bool use = act && ok;
-  const float sw = use ? sqrtf(w) : 0.0f;
-  auto wx = [&](float v) { return use ? sw * v : 0.0f; };
-  float* sX = reinterpret_cast<float*>(arena[wave]);  // the wave's 64 rows (over its tile blocks)
-  {
-    float4* xr = reinterpret_cast<float4*>(sX + lane * kRowS);
+  };
+  int ok;
+  float bcost;
+  double accb[PPL == 1 ? 1 : BW];  // PPL > 1: the blocks' unweighted products, then weighted
+  if constexpr (PPL == 1) {
+    const bool act = live && k < R;
+    const float2 off = pattern_at<LPB>(a, k);
+    const float Ih = act ? a.host_int[(long long)lr.y * R + k] : 0.0f;
+    stage_tile_pp<LPB>(a, s_tb, wb, k, make_int2(lr.y, lr.z & 0xffffff));
+    asm volatile("" ::"v"(Ih));
+    __syncthreads();
+    const Row row = photometric_row<MODEL, true>(a, s_tb[wb], off, Ih);  // (hv, hw unused: not formed)
+    save_rt();
+    ok = group_all<LPB>(act ? row.ok : 1);
+    const float s = group_sum<LPB>(act && ok ? row.r * row.r : 0.0f);
+    const float w = ok ? huber_weight(s, a.huber) : 0.0f;
+    bcost = ok ? huber_cost(s, a.huber) : 0.0f;
+    const bool use = act && ok;
+    const float sw = use ? sqrtf(w) : 0.0f;
+    auto wx = [&](float v) { return use ? sw * v : 0.0f; };
+    float4* xr = reinterpret_cast<float4*>(sX + lane * kRowS);  // (over the wave's tile blocks, read above)
     xr[0] = make_float4(wx(row.tv.x), wx(row.tv.y), wx(row.tv.z), wx(row.tw.x));
     xr[1] = make_float4(wx(row.tw.y), wx(row.tw.z), wx(row.jr), wx(row.r));
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  } else {
+    if ((int)threadIdx.x < LPB * PPL) s_pat[threadIdx.x] = pattern_at<LPB * PPL>(a, threadIdx.x);
+    float Ih[PPL];
+#pragma unroll
+    for (int j = 0; j < PPL; ++j) {
+      const int px = k + LPB * j;
+      Ih[j] = live && px < R ? a.host_int[(long long)lr.y * R + px] : 0.0f;
+    }
+    stage_tile_pp<LPB>(a, s_tb, wb, k, make_int2(lr.y, lr.z & 0xffffff));
+#pragma unroll
+    for (int j = 0; j < PPL; ++j) asm volatile("" ::"v"(Ih[j]));
+    __syncthreads();
+    save_rt();
+#pragma unroll
+    for (int b = 0; b < BW; ++b) accb[b] = 0.0;
+    int okl = 1;
+    float s = 0.0f;
+#pragma unroll 1
+    for (int j = 0; j < PPL; ++j) {
+      const int px = k + LPB * j;
+      const bool act = live && px < R;
+      float ih = Ih[0];
+#pragma unroll
+      for (int q = 1; q < PPL; ++q) ih = j == q ? Ih[q] : ih;
+      asm volatile("" ::: "memory");  // the tile is read from LDS per pass (see photometric_block_kernel_multi)
+      const Row row = photometric_row<MODEL, true>(a, s_tb[wb], s_pat[act ? px : 0], ih);
+      const bool use = act && row.ok;
+      okl &= act ? row.ok : 1;
+      s += use ? row.r * row.r : 0.0f;
+      auto xv = [&](float v) { return use ? v : 0.0f; };  // selects: a row that is not ok may hold inf / NaN
+      float4* xr = reinterpret_cast<float4*>(sX + lane * kRowS);
+      xr[0] = make_float4(xv(row.tv.x), xv(row.tv.y), xv(row.tv.z), xv(row.tw.x));
+      xr[1] = make_float4(xv(row.tw.y), xv(row.tw.z), xv(row.jr), xv(row.r));
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+      for (int b = 0; b < BW; ++b) {
+        float o[4];
+        ops(b, o);
+#pragma unroll
+        for (int st = 0; st < 2; ++st)
+          accb[b] = __builtin_amdgcn_mfma_f64_4x4x4f64((double)o[2 * st], (double)o[2 * st + 1], accb[b], 0, 0, 0);
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // this pass's reads before the next pass's row stores
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+    ok = group_all<LPB>(okl);
+    s = group_sum<LPB>(s);
+    const float w = ok ? huber_weight(s, a.huber) : 0.0f;
+    bcost = ok ? huber_cost(s, a.huber) : 0.0f;
+#pragma unroll
+    for (int b = 0; b < BW; ++b)
+      accb[b] *= (double)__int_as_float(__builtin_amdgcn_readlane(__float_as_int(w), b * LPB));
   }
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  double* const sWt = reinterpret_cast<double*>(arena[wave]);  // W_t of the wave's blocks, over block 0's rows
+  if (k == 0) s_bc[lb] = live && ok ? bcost : -1.0f;  // read after the barrier below
   const int nbw = min(max(count - wave * BW, 0), BW);
   {
-    // lane l: 4×4 block β — tiles (0,0), (0,1), (1,1) of xᵀx, and β = 3 repeating (0,1) unused — operand columns
-    // ca / cb, product (pr_, pc_)
-    const int beta = (lane >> 2) & 3, i4 = lane & 3, kq = lane >> 4;
-    const int I = beta == 2 ? 1 : 0, J = beta == 0 ? 0 : 1;
-    const int ca = 4 * I + i4, cb = 4 * J + i4;
     const int pr_ = 4 * I + kq, pc_ = 4 * J + i4;
     const int pslot = beta < 3 && pr_ <= pc_ ? upper8(pr_, pc_) : -1;
     // the point data: column 6 (jr) of tiles (0,1) and (1,1) — W_t[0..3] and W_t[4..5], H_ρρ, g_ρ — at its blk_schur
-    // position [H_ρρ, g_ρ, W_h(6), W_t(6), 0, 0] (the zeros from two lanes of β = 3)
-    const int ppos = beta == 3 ? (kq == 0 && i4 < 2 ? 14 + i4 : -1)
-                               : (i4 != 2 || beta == 0 ? -1 : (beta == 1 ? 8 + kq : (kq < 2 ? 12 + kq : kq - 2)));
-    double* sP = reinterpret_cast<double*>(arena[wave] + kRegW);
+    // position [H_ρρ, g_ρ, W_t(6)]
+    const int ppos = i4 != 2 || beta == 0 || beta == 3 ? -1 : (beta == 1 ? 2 + kq : (kq < 2 ? 6 + kq : kq - 2));
+    double* sP = reinterpret_cast<double*>(arena[wave] + kProdOff);
     const int lo = __builtin_amdgcn_readfirstlane(lt);
-    auto ops = [&](int b, float* o) {  // block b's operands: A, B of K steps 0 and 1
-#pragma unroll
-      for (int st = 0; st < 2; ++st) {
-        const float* xr = sX + (8 * b + 4 * st + kq) * kRowS;
-        o[2 * st] = xr[ca];
-        o[2 * st + 1] = xr[cb];
-      }
-    };
     double tacc = 0.0;
     int cur = lo;
     float o_n[4];
-    ops(0, o_n);
+    if constexpr (PPL == 1) ops(0, o_n);
 #pragma unroll
     for (int b = 0; b < BW; ++b) {
-      float o[4];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) o[q] = o_n[q];
-      if (b + 1 < BW) ops(b + 1, o_n);  // the next block's LDS reads in flight over this block's matrix-core steps
       double acc = 0.0;
+      if constexpr (PPL == 1) {
+        float o[4];
 #pragma unroll
-      for (int st = 0; st < 2; ++st)
-        acc = __builtin_amdgcn_mfma_f64_4x4x4f64((double)o[2 * st], (double)o[2 * st + 1], acc, 0, 0, 0);
+        for (int q = 0; q < 4; ++q) o[q] = o_n[q];
+        if (b + 1 < BW) ops(b + 1, o_n);  // the next block's LDS reads in flight over this block's matrix-core steps
+#pragma unroll
+        for (int st = 0; st < 2; ++st)
+          acc = __builtin_amdgcn_mfma_f64_4x4x4f64((double)o[2 * st], (double)o[2 * st + 1], acc, 0, 0, 0);
+      } else {
+        acc = accb[b];
+      }
       if (b < nbw) {
         const int gpb = __builtin_amdgcn_readlane(gpos, b * LPB);
-        if (ppos >= 0) {
-          blk_schur[(long long)gpb * 16 + ppos] = ppos < 14 ? acc : 0.0;
-          if (ppos >= 8 && ppos < 14) sWt[b * 6 + ppos - 8] = acc;
-        }
+        if (ppos >= 0) blk_schur[(long long)gpb * kPd + ppos] = acc;
         const int ltb = __builtin_amdgcn_readlane(lt, b * LPB);
         if (ltb != cur) {
           if (pslot >= 0) sP[(cur - lo) * NQ + pslot] = tacc;
@@ -575,9 +659,9 @@ void linearize_adj_kernel(const KernelArgs a, const LinArgs g) {
   }
   __syncthreads();
   // Phase A: the chunk's product sums per local target j, as full 8 × 8 matrices (one thread per entry; the sets of j
-  // over the waves in order), and Ad_j from R_th, t_th.  Over wave 0's rows, after its W_t.
-  double* sT = reinterpret_cast<double*>(arena[0] + kWt);  // [j][8][8]
-  double* sN = reinterpret_cast<double*>(arena[1] + kWt);  // [j][6][6]: H_tt,j·Ad_j
+  // over the waves in order), and Ad_j from R_th, t_th.  Over wave 0's rows.
+  double* sT = reinterpret_cast<double*>(arena[0] + kRowsOff);  // [j][8][8]
+  double* sN = reinterpret_cast<double*>(arena[1] + kRowsOff);  // [j][6][6]: H_tt,j·Ad_j
   {
     const int t = threadIdx.x, j = t >> 6, r = (t >> 3) & 7, c = t & 7;
     if (j < n_t) {
@@ -586,7 +670,7 @@ void linearize_adj_kernel(const KernelArgs a, const LinArgs g) {
 #pragma unroll
       for (int w_ = 0; w_ < NW; ++w_) {
         const int wl = s_wlo[w_], wn = s_wn[w_];
-        if (j >= wl && j < wl + wn) acc += reinterpret_cast<const double*>(arena[w_] + kRegW)[(j - wl) * NQ + u];
+        if (j >= wl && j < wl + wn) acc += reinterpret_cast<const double*>(arena[w_] + kProdOff)[(j - wl) * NQ + u];
       }
       sT[t] = acc;
     }
@@ -606,18 +690,7 @@ void linearize_adj_kernel(const KernelArgs a, const LinArgs g) {
     }
   }
   __syncthreads();
-  // Phase B: per block W_h = −W_t·Ad (lane 6b + c of each wave); N_j = H_tt,j·Ad_j; the target outputs — H_ht = −AdᵀH_tt,
-  // H_tt, g_t — and g_h = −Σ_j Ad_jᵀ g_t,j
-  {
-    const int bb = lane / 6, c = lane - 6 * bb;
-    const int gpb = __shfl(gpos, (bb * LPB) & 63, 64), ltb = __shfl(lt, (bb * LPB) & 63, 64);
-    if (bb < nbw) {
-      double v = 0.0;
-#pragma unroll
-      for (int m = 0; m < 6; ++m) v += sWt[bb * 6 + m] * s_ad[ltb][6 * m + c];
-      blk_schur[(long long)gpb * 16 + 2 + c] = -v;
-    }
-  }
+  // Phase B: N_j = H_tt,j·Ad_j; the target outputs — H_ht = −AdᵀH_tt, H_tt, g_t — and g_h = −Σ_j Ad_jᵀ g_t,j
   const int nout = SLOT_LIN_BASE + SLOT_LIN_T * n_t;
   for (int o = threadIdx.x; o < nout; o += kBlockThreads) {
     if (o < 36) {
@@ -728,6 +801,7 @@ void linearize_rows_kernel(const KernelArgs a, const LinArgs g) {
     Ih[j] = live && px < R ? a.host_int[(long long)pt * R + px] : 0.0f;
   }
   __syncthreads();
+  store_pair_rt<LPB>(s1 ? g.pair_rt1 : g.pair_rt, s_tb[wb].pr.R, s_tb[wb].pr.t, lr.z & 0xffffff, lt, k, live);
   float* sX = reinterpret_cast<float*>(arena[wave] + kTileW);  // the pass's 64 rows × 16 floats
   const int ci = lane & 15, kq = lane >> 4;
   f32x4 accb[BW];
@@ -789,7 +863,7 @@ void linearize_rows_kernel(const KernelArgs a, const LinArgs g) {
     };
     // (this kernel's block products are fp32 matrix-core chains over the block's ⌈P/8⌉ passes; the weighting, the
     // point data and every sum after them are fp64)
-    const int pc = lane - 48, pq = pc < 12 ? pc + 2 : (pc < 14 ? pc - 12 : pc);
+    const int pc = lane - 48, pq = pc >= 6 && pc < 12 ? pc - 4 : (pc == 12 ? 0 : (pc == 13 ? 1 : -1));
     v4f64 tacc = {0.0, 0.0, 0.0, 0.0};
     int cur = lo;
 #pragma unroll
@@ -798,7 +872,7 @@ void linearize_rows_kernel(const KernelArgs a, const LinArgs g) {
         const double wb_ = (double)__int_as_float(__builtin_amdgcn_readlane(__float_as_int(w), b * LPB));
         const v4f64 acc = {accb[b][0] * wb_, accb[b][1] * wb_, accb[b][2] * wb_, accb[b][3] * wb_};
         const int gpb = __builtin_amdgcn_readlane(gpos, b * LPB);
-        if (pc >= 0) blk_schur[(long long)gpb * 16 + pq] = acc[0];
+        if (pc >= 0 && pq >= 0) blk_schur[(long long)gpb * kPd + pq] = acc[0];
         const int ltb = __builtin_amdgcn_readlane(lt, b * LPB);
         if (ltb != cur) {
           flush(tacc, cur - lo);
@@ -881,6 +955,11 @@ struct SchurArgs {
   const double* rho_new;
   const int* pt_orig;
   int n_pose_d, n_gn_points;
+  const double* pair_rt;   // per pair [R_th, t_th] of the linearisation in blk_schur / blk_schur1 (W_h = −W_t·Ad)
+  const double* pair_rt1;
+  const int4* lvp4;        // per chunk: the pairs of local targets 1 … 4
+  const int* lvp;          // all of them (from aux.z), for chunks of > 5 local poses
+  int rt_off;              // R, t at the start of the dynamic LDS (doubles); W after it
 };
 
 // ------------------------------------------------------------------------------------------------
@@ -895,83 +974,160 @@ struct SchurArgs {
 // can issue them in one memory round with loads of its own (schur_free_decide_kernel: the record and the set).
 constexpr int kPtIter = (SCHUR_PTS + kBlockThreads / 4 - 1) / (kBlockThreads / 4);
 struct SchurHead {
-  int4 d, ax;
+  int4 d, ax, lp4;
   int2 prec[kPtIter];
 };
 __device__ __forceinline__ SchurHead schur_head(const SchurArgs& g, int c) {
   SchurHead h;
   h.d = g.desc[c];
   h.ax = g.aux[c];
+  h.lp4 = g.lvp4[c];
 #pragma unroll
   for (int it = 0; it < kPtIter; ++it)
     h.prec[it] = g.pt_fb[(long long)c * SCHUR_PTS + it * (kBlockThreads / 4) + (threadIdx.x >> 2)];
   return h;
 }
+// The host block of W: a photometric (or geometric) row's host Jacobian is its target Jacobian through the pair's
+// adjoint, J_h = −J_t·Ad with Ad = [[R, [t]×R], [0, R]] (R = R_th, t = t_th; linearize_adj_kernel), so
+// W_h = J_ρᵀJ_h = −Σ_targets W_t·Ad = −Σ_lv [W_tv·R, (W_tv × t + W_tw)·R] over the point's per-target sums W[p][lv]: the
+// blocks carry W_t alone (8 doubles of point data instead of 16).  Component c of point p; rt: the local targets'
+// [R(9), t(3)] in LDS.
+__device__ __forceinline__ double host_w(const double (*W)[6], const double* rt, int p, int nv, int c) {
+  double v = 0.0;
+  for (int l = 1; l < nv; ++l) {
+    const double* w = W[p * nv + l];
+    const double* R = rt + 12 * (l - 1);
+    if (c < 3) {
+      v += w[0] * R[c] + w[1] * R[3 + c] + w[2] * R[6 + c];
+    } else {
+      const double* t = R + 9;
+      const int cc = c - 3;
+      const double u0 = w[1] * t[2] - w[2] * t[1] + w[3], u1 = w[2] * t[0] - w[0] * t[2] + w[4],
+                   u2 = w[0] * t[1] - w[1] * t[0] + w[5];
+      v += u0 * R[cc] + u1 * R[3 + cc] + u2 * R[6 + cc];
+    }
+  }
+  return -v;
+}
 __device__ __forceinline__ void schur_chunk(const SchurArgs& g, const SchurHead& h, double lambda,
-                                            const double* __restrict__ blk_schur, double* __restrict__ part_out,
-                                            double* __restrict__ pt_out, int* degen, double* W_dyn, double* s_inv,
-                                            double* s_gl) {
+                                            const double* __restrict__ blk_schur, const double* __restrict__ pair_rt,
+                                            double* __restrict__ part_out, double* __restrict__ pt_out, int* degen,
+                                            double* W_dyn, double* s_inv, double* s_gl) {
   const int4 d = h.d;
   const int4 ax = h.ax;
   const int2* prec = h.prec;
   const int first = d.x, npt = d.y, nv = d.z, poff = d.w;
-  double (*W)[6] = reinterpret_cast<double (*)[6]>(W_dyn);
+#ifdef PBA_FD_STAMPS
+  const long long ts0 = wall_clock64();
+  long long ts1 = 0, ts2 = 0;
+  auto stamp_out = [&](const char* tag) {
+    const int b = blockIdx.x;
+    if (threadIdx.x == 0 && (b == 17 || b == 300 || b == 600 || b == 1000))
+      printf("fdphase b=%d %s start %lld zero %lld loads %lld total %lld\n", b, tag, ts0, ts1 - ts0, ts2 - ts0,
+             wall_clock64() - ts0);
+  };
+#endif
+  double* const rt = W_dyn;  // the local targets' R_th, t_th (12 each)
+  double (*W)[6] = reinterpret_cast<double (*)[6]>(W_dyn + g.rt_off);
   for (int i = threadIdx.x; i < npt * nv * 6; i += kBlockThreads) (&W[0][0])[i] = 0.0;
   __syncthreads();
-  // four lanes per point, each summing four doubles (two 16-B loads) of the point's blocks' 16-value records in block
-  // order: q = 0: H_ρρ, g_ρ, W_h[0..1]   q = 1: W_h[2..5]   q = 2: W_t[0..3] → W[p][lv]   q = 3: W_t[4..5] → W[p][lv]
-  // (staging the chunk's records in LDS block-parallel instead measured slower: 23 → 35 µs at C4, its LDS halves the
-  // resident workgroups)
+#ifdef PBA_FD_STAMPS
+  ts1 = wall_clock64();
+#endif
+  // the targets' R, t: loaded beside the block data (the first four pairs came with the descriptors; a chunk of more
+  // local poses reads its pair list first), stored to LDS after the accumulation
+  double rtv[2];
+  int rti[2];
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int i = threadIdx.x + u * kBlockThreads, l = i / 12;
+    rti[u] = i < 12 * (nv - 1) ? i : -1;
+    int pr = 0;
+    if (rti[u] >= 0) pr = l < 4 ? (l == 0 ? h.lp4.x : l == 1 ? h.lp4.y : l == 2 ? h.lp4.z : h.lp4.w) : g.lvp[ax.z + l];
+    rtv[u] = rti[u] >= 0 ? pair_rt[(long long)pr * 12 + (i - 12 * l)] : 0.0;
+  }
+  // four lanes per point, each summing one 16-B load per block of the point's blocks' 8-value records in block order:
+  // q = 0: H_ρρ, g_ρ   q = 1, 2, 3: W_t[0..1], [2..3], [4..5] → W[p][lv] (staging the chunk's records in LDS
+  // block-parallel instead measured slower: 23 → 35 µs at C4, its LDS halves the resident workgroups)
   bool bad = false;
+  const int q = threadIdx.x & 3;
+  // the first kFirst blocks of both of the lane's points in ONE memory round (a point's block loop per point cost a
+  // round each), the rest of a point's blocks (more than kFirst observations) in batches after
+  constexpr int kFirst = 4, kBatch = 8;
+  double2 v0[kPtIter][kFirst];
+  int lv0[kPtIter][kFirst];
 #pragma unroll
   for (int it = 0; it < kPtIter; ++it) {
-    const int p0 = it * (kBlockThreads / 4);
-    const int p = p0 + (threadIdx.x >> 2), q = threadIdx.x & 3, gp = first + p;
+    const int fb = prec[it].x, nb = max(prec[it].y, 1);
+#pragma unroll
+    for (int u = 0; u < kFirst; ++u) {
+      const int b = fb + min(u, nb - 1);
+      v0[it][u] = reinterpret_cast<const double2*>(blk_schur + (long long)b * kPd)[q];
+      lv0[it][u] = q == 0 ? 0 : g.blk_lv[b];
+    }
+  }
+#pragma unroll
+  for (int it = 0; it < kPtIter; ++it) {
+    const int p = it * (kBlockThreads / 4) + (threadIdx.x >> 2), gp = first + p;
     if (p < npt) {
       const int fb = prec[it].x, nb = prec[it].y;
-      double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
-      constexpr int kBatch = 8;  // every load of a batch issued before the first use: one memory round trip per batch
-      for (int b0 = fb; b0 < fb + nb; b0 += kBatch) {
-        double2 v[kBatch][2];
+      double s0 = 0.0, s1 = 0.0;
+      auto add = [&](const double2& v, int lv) {
+        if (q == 0) {
+          s0 += v.x;
+          s1 += v.y;
+        } else {
+          double* wt = W[p * nv + lv] + 2 * (q - 1);
+          wt[0] += v.x;
+          wt[1] += v.y;
+        }
+      };
+#pragma unroll
+      for (int u = 0; u < kFirst; ++u)
+        if (u < nb) add(v0[it][u], lv0[it][u]);
+      for (int b0 = fb + kFirst; b0 < fb + nb; b0 += kBatch) {
+        double2 v[kBatch];
         int lv[kBatch];
 #pragma unroll
         for (int u = 0; u < kBatch; ++u) {
           const int b = min(b0 + u, fb + nb - 1);
-          const double2* r2 = reinterpret_cast<const double2*>(blk_schur + (long long)b * 16) + 2 * q;
-          v[u][0] = r2[0];
-          v[u][1] = r2[1];
-          lv[u] = q < 2 ? 0 : g.blk_lv[b];
+          v[u] = reinterpret_cast<const double2*>(blk_schur + (long long)b * kPd)[q];
+          lv[u] = q == 0 ? 0 : g.blk_lv[b];
         }
 #pragma unroll
-        for (int u = 0; u < kBatch; ++u) {
-          if (b0 + u >= fb + nb) break;
-          if (q < 2) {
-            s0 += v[u][0].x; s1 += v[u][0].y; s2 += v[u][1].x; s3 += v[u][1].y;
-          } else {
-            double* wt = W[p * nv + lv[u]];
-            if (q == 2) { wt[0] += v[u][0].x; wt[1] += v[u][0].y; wt[2] += v[u][1].x; wt[3] += v[u][1].y; }
-            else { wt[4] += v[u][0].x; wt[5] += v[u][0].y; }
-          }
-        }
+        for (int u = 0; u < kBatch; ++u)
+          if (b0 + u < fb + nb) add(v[u], lv[u]);
       }
-      double* pd = pt_out ? pt_out + (long long)gp * 8 : nullptr;
       if (q == 0) {
-        W[p * nv][0] = s2;
-        W[p * nv][1] = s3;
         const double D = fmin(fmax(s0, 1e-6), 1e32);
         const double Hd = s0 + lambda * D;
         s_inv[p] = Hd > 0.0 ? 1.0 / Hd : 0.0;
         s_gl[p] = s1;
         bad = s0 != 0.0 && !(s0 >= 1e-6 && s0 <= 1e32);
-        if (pd) { pd[0] = s0; pd[1] = s1; pd[2] = s2; pd[3] = s3; }
-      } else if (q == 1) {
-        W[p * nv][2] = s0; W[p * nv][3] = s1; W[p * nv][4] = s2; W[p * nv][5] = s3;
-        if (pd) { pd[4] = s0; pd[5] = s1; pd[6] = s2; pd[7] = s3; }
+        if (pt_out) {
+          pt_out[(long long)gp * 8] = s0;
+          pt_out[(long long)gp * 8 + 1] = s1;
+        }
       }
     }
   }
+#pragma unroll
+  for (int u = 0; u < 2; ++u)
+    if (rti[u] >= 0) rt[rti[u]] = rtv[u];
+  for (int i = threadIdx.x + 2 * kBlockThreads; i < 12 * (nv - 1); i += kBlockThreads)  // (> 43 local poses)
+    rt[i] = pair_rt[(long long)g.lvp[ax.z + i / 12] * 12 + i % 12];
   if (degen && __syncthreads_or(bad) && threadIdx.x == 0) atomicOr(degen, 1);
   __syncthreads();
+  for (int i = threadIdx.x; i < npt * 6; i += kBlockThreads) {  // W_h = W[p][0] from the targets' sums
+    const int p = i / 6, c = i - 6 * p;
+    const double v = host_w(W, rt, p, nv, c);
+    W[p * nv][c] = v;
+    if (pt_out) pt_out[(long long)(first + p) * 8 + 2 + c] = v;
+  }
+  __syncthreads();
+#ifdef PBA_FD_STAMPS
+  ts2 = wall_clock64();
+#endif
   if (nv * 6 + 1 <= 32) {
     // ≤ 5 local poses (a temporal window): the chunk's sums are one small GEMM on the matrix cores,
     // C = (W·diag(1/H'_ρρ))ᵀ [W | g_ρ] over its points (K = points, 4 per v_mfma_f64_16x16x4f64 step), 32 × 32 in
@@ -1019,6 +1175,9 @@ __device__ __forceinline__ void schur_chunk(const SchurArgs& g, const SchurHead&
         part_out[(long long)poff + ax.y * 36 + r] = acc[v];
       }
     }
+#ifdef PBA_FD_STAMPS
+    stamp_out("mfma");
+#endif
     return;
   }
   const int nout = ax.y * 36 + nv * 6;
@@ -1083,7 +1242,8 @@ __global__ __launch_bounds__(kBlockThreads) void schur_kernel(const SchurArgs g,
   ac.load(g, lv);
   lambda = lm_lambda(lv, lambda);
   const double* const blk_schur = lv.set != 0.0 ? g.blk_schur1 : g.blk_schur;
-  schur_chunk(g, schur_head(g, c), lambda, blk_schur, g.part_schur, g.pt_data, nullptr, W_dyn, s_inv, s_gl);
+  schur_chunk(g, schur_head(g, c), lambda, blk_schur, lv.set != 0.0 ? g.pair_rt1 : g.pair_rt, g.part_schur, g.pt_data,
+              nullptr, W_dyn, s_inv, s_gl);
   ac.store(g);
 }
 
@@ -2616,7 +2776,7 @@ __device__ __forceinline__ void point_update_block(const PointUpdateArgs& a, con
       for (int u = 0; u < kBatch; ++u) {
         const int b = min(b0 + u, fb + nb - 1);
         t[u] = first ? (u == 0 ? pt4.x : u == 1 ? pt4.y : u == 2 ? pt4.z : pt4.w) : a.gn_target[b];
-        const double2* wt = reinterpret_cast<const double2*>(blk_schur + (long long)b * 16 + 8);  // W_t
+        const double2* wt = reinterpret_cast<const double2*>(blk_schur + (long long)b * kPd + 2);  // W_t
 #pragma unroll
         for (int i = 0; i < 3; ++i) {
           const double2 q2 = wt[i];
@@ -3062,21 +3222,23 @@ __device__ void lm_decide(const double* t, int st, const DecideOpts& o, double* 
 // thread, then one strided pass over red with U slots per thread in flight, then xor butterflies per wave and the
 // waves in order (U loads of three arrays spilled 172 B per lane at 1024 threads: 16 µs per decision).  t: the
 // totals, in LDS.
+// lo, hi: only the slots [lo, hi) of both passes (a slice of the sums, schur_free_decide_kernel's decision workgroups).
 template <int N>
 __device__ void trial_sums(const double* __restrict__ red, const double* __restrict__ red2,
-                           const double* __restrict__ gmax, int gp, int gq, int gc, double* t) {
+                           const double* __restrict__ gmax, int gp, int gq, int gc, double* t, int lo = 0,
+                           int hi = 0x7fffffff) {
   constexpr int U = 8;
   __shared__ double part[kTsCount][N / 64];
   double v[kTsCount] = {};
-  const int S = gp + gq, E = S + gc;
+  const int S0 = gp + gq, S = min(S0, hi), E = min(S0 + gc, hi);
   const double2* r1 = reinterpret_cast<const double2*>(red);
   const double2* r2 = reinterpret_cast<const double2*>(red2);
   // the update slots' norms and gradient maxima: one slot per thread, loaded before the red pass so that both are
   // in flight together (S ≤ N unless the problem has > 260k points: a tail loop then)
-  const int i_s = (int)threadIdx.x;
+  const int i_s = lo + (int)threadIdx.x;
   const double2 ys = i_s < S ? r2[i_s] : make_double2(0.0, 0.0);
   const double ms = i_s < S ? gmax[i_s] : 0.0;
-  for (int i0 = (int)threadIdx.x; i0 < E; i0 += U * N) {
+  for (int i0 = lo + (int)threadIdx.x; i0 < E; i0 += U * N) {
     double2 x[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -3086,13 +3248,13 @@ __device__ void trial_sums(const double* __restrict__ red, const double* __restr
 #pragma unroll
     for (int u = 0; u < U; ++u) {  // selects, not a computed index (that put v in scratch memory)
       const int i = i0 + u * N;
-      const bool p = i < gp, t = i >= gp && i < S;
+      const bool p = i < gp, t = i >= gp && i < S0;
       v[kTsPoseG] += p ? x[u].x : 0.0;
       v[kTsPoseD] += p ? x[u].y : 0.0;
       v[kTsPtG] += t ? x[u].x : 0.0;
       v[kTsPtD] += t ? x[u].y : 0.0;
-      v[kTsCost] += i >= S ? x[u].x : 0.0;  // (slots past E loaded as zeros)
-      v[kTsValid] += i >= S ? x[u].y : 0.0;
+      v[kTsCost] += i >= S0 ? x[u].x : 0.0;  // (slots past E loaded as zeros)
+      v[kTsValid] += i >= S0 ? x[u].y : 0.0;
     }
   }
   auto add_small = [&](int i, const double2& y, double m) {
@@ -3111,7 +3273,7 @@ __device__ void trial_sums(const double* __restrict__ red, const double* __restr
   auto is_max = [](int q) { return q == kTsPoseGMax || q == kTsPtGMax; };
   // a wave past the update slots holds only candidate-cost sums: its other ten are zeros, not butterflied (the same
   // totals: only zeros are left out)
-  const bool upd = __builtin_amdgcn_readfirstlane((int)threadIdx.x & ~63) < S;
+  const bool upd = __builtin_amdgcn_readfirstlane(lo + ((int)threadIdx.x & ~63)) < S;
 #pragma unroll
   for (int q = 0; q < kTsCount; ++q) {
     if (!upd && q != kTsCost && q != kTsValid) continue;
@@ -3222,7 +3384,12 @@ struct DecideArgs {
   int init;           // 1: a new solve's record (lm_init_kernel), 0: the trial's decision
   double radius;      // init: the initial trust-region radius
   double* init_out;   // init: [initial cost, valid blocks]
+  double* ts_part;    // [kDecideWgs][kTsCount]: the decision workgroups' slices of the sums
+  int* ts_count;      // their arrivals (0 between launches)
 };
+// Workgroups of schur_free_decide_kernel that sum the trial's partial slots, a slice each: one workgroup alone took ~20 µs
+// for the 13.5k slots at C4 (seven dependent memory rounds), longer than the elimination beside it.
+constexpr int kDecideWgs = 16;
 struct FreeSets {
   double* part[2];    // λ-free Schur partials per linearisation set
   double* pt[2];      // point data per set ([H, g, W_h(6)] per GN point, undamped)
@@ -3230,14 +3397,65 @@ struct FreeSets {
   const int* lin_set; // the set the last linearisation wrote
 };
 
-__global__ __launch_bounds__(kBlockThreads) void schur_free_decide_kernel(const SchurArgs g, const DecideArgs da,
+__global__ __launch_bounds__(kBlockThreads) __attribute__((amdgpu_waves_per_eu(4, 8))) void schur_free_decide_kernel(const SchurArgs g, const DecideArgs da,
                                                                         const FreeSets fs) {
   extern __shared__ __attribute__((aligned(16))) double W_dyn[];
   __shared__ double s_inv[SCHUR_PTS], s_gl[SCHUR_PTS];
-  if (blockIdx.x == 0) {
+#ifdef PBA_FD_STAMPS  // timing dissection only: 100-MHz stamps at the start and end of chosen workgroups
+  struct Stamp {
+    long long t0 = wall_clock64();
+    __device__ ~Stamp() {
+      const int b = blockIdx.x;
+      if (threadIdx.x == 0 && (b == 0 || b == 1 || b == 300 || b == 600 || b == (int)gridDim.x - 1))
+        printf("fdstamp b=%d start %lld end %lld\n", b, t0, wall_clock64());
+    }
+  } stamp;
+#endif
+  if (blockIdx.x < kDecideWgs) {
+    // a slice of the sums per workgroup → sc1 stores → (every store completed, release) → arrival count; the last
+    // workgroup to arrive (acquire) adds the slices in workgroup order — the same totals whichever arrives last — and
+    // decides (or, init, writes the new solve's record)
     __shared__ double t[kTsCount];
+    __shared__ int s_last;
+    const double done = da.init ? 0.0 : da.lm[kLmDone];  // (tested after the sums, as lm_decide_kernel)
+    {
+      const int E = da.init ? da.gc : da.gp + da.gq + da.gc, per = (E + kDecideWgs - 1) / kDecideWgs;
+      const int lo = (int)blockIdx.x * per, hi = min(E, lo + per);
+      if (da.init) trial_sums<kBlockThreads>(da.red, da.red, da.red, 0, 0, da.gc, t, lo, hi);
+      else trial_sums<kBlockThreads>(da.red, da.red2, da.gmax, da.gp, da.gq, da.gc, t, lo, hi);
+      if (threadIdx.x < kTsCount)
+        __hip_atomic_store(da.ts_part + blockIdx.x * kTsCount + threadIdx.x, t[threadIdx.x], __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        s_last = __hip_atomic_fetch_add(da.ts_count, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == kDecideWgs - 1;
+        if (s_last) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      __syncthreads();
+      if (!s_last) return;
+      if (threadIdx.x < kTsCount) {
+        const int q = threadIdx.x;
+        const bool mx = q == kTsPoseGMax || q == kTsPtGMax;
+        double v = 0.0;
+#pragma unroll 1
+        for (int b0 = 0; b0 < kDecideWgs; b0 += 4) {  // (4 loads in flight: 16 held the elimination to 3 waves/SIMD)
+          double x[4];
+#pragma unroll
+          for (int b = 0; b < 4; ++b)
+            x[b] = __hip_atomic_load(da.ts_part + (b0 + b) * kTsCount + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+          for (int b = 0; b < 4; ++b) v = mx ? fmax(v, x[b]) : v + x[b];
+        }
+        t[q] = v;
+      }
+      if (threadIdx.x == 0) *da.ts_count = 0;  // for the next launch (ordered by the launch boundary)
+      __syncthreads();
+    }
     if (da.init) {
-      trial_sums<kBlockThreads>(da.red, da.red, da.red, 0, 0, da.gc, t);
       if (threadIdx.x != 0) return;
       double* lm = da.lm;
       for (int i = 0; i < kLmFields; ++i) lm[i] = 0.0;
@@ -3251,8 +3469,6 @@ __global__ __launch_bounds__(kBlockThreads) void schur_free_decide_kernel(const 
       da.init_out[1] = t[kTsValid];
       return;
     }
-    const double done = da.lm[kLmDone];  // (tested after the sums, as lm_decide_kernel)
-    trial_sums<kBlockThreads>(da.red, da.red2, da.gmax, da.gp, da.gq, da.gc, t);
     if (done != 0.0 || threadIdx.x >= 64) return;
     __shared__ double s_rec[kLmFields];
     if (threadIdx.x == 0) {
@@ -3262,19 +3478,20 @@ __global__ __launch_bounds__(kBlockThreads) void schur_free_decide_kernel(const 
     if (da.host_rec) publish_record(s_rec, da.host_rec, da.seq);
     return;
   }
-  const int c = blockIdx.x - 1;
+  const int c = blockIdx.x - kDecideWgs;
   if (c >= g.n_chunks) return;
   // one memory round: the chunk's descriptors, the record's done flag and the set, all issued before the exit (the
   // compiler otherwise waited for the flag, then for the set, then issued the descriptors)
   const SchurHead h = schur_head(g, c);
   const double done = da.lm[kLmDone];
   const int lset = *fs.lin_set;
-  asm volatile("" ::"v"(done), "v"(lset), "v"(h.d.x), "v"(h.ax.x));
+  asm volatile("" ::"v"(done), "v"(lset), "v"(h.d.x), "v"(h.ax.x), "v"(h.lp4.x));
 #pragma unroll
   for (int it = 0; it < kPtIter; ++it) asm volatile("" ::"v"(h.prec[it].x), "v"(h.prec[it].y));
   if (!da.init && done != 0.0) return;
   const int set = lset != 0;
-  schur_chunk(g, h, 0.0, set ? g.blk_schur1 : g.blk_schur, fs.part[set], fs.pt[set], fs.degen + set, W_dyn, s_inv, s_gl);
+  schur_chunk(g, h, 0.0, set ? g.blk_schur1 : g.blk_schur, set ? g.pair_rt1 : g.pair_rt, fs.part[set], fs.pt[set],
+              fs.degen + set, W_dyn, s_inv, s_gl);
 }
 
 // The single-GPU LM trial's first kernel: the previous trial's accept, and — only for a set flagged degen — the
@@ -3291,7 +3508,8 @@ __global__ __launch_bounds__(kBlockThreads) void schur_gate_kernel(const SchurAr
   if ((set ? dg1 : dg0) != 0 && lv.done == 0.0) {
     const double* blk_schur = set ? g.blk_schur1 : g.blk_schur;
     for (int c = blockIdx.x; c < g.n_chunks; c += gridDim.x) {
-      schur_chunk(g, schur_head(g, c), lv.lambda, blk_schur, g.part_schur, nullptr, nullptr, W_dyn, s_inv, s_gl);
+      schur_chunk(g, schur_head(g, c), lv.lambda, blk_schur, set ? g.pair_rt1 : g.pair_rt, g.part_schur, nullptr,
+                  nullptr, W_dyn, s_inv, s_gl);
       __syncthreads();
     }
   }
@@ -3557,6 +3775,8 @@ int gn_prepare(pba_engine* e) {
   std::vector<int4> sdesc;
   std::vector<int4> saux;
   std::vector<uchar2> spairs;
+  std::vector<int> lvp;
+  int max_nv = 1;
   std::vector<std::vector<char>> schur_used_flag;
   std::vector<uint8_t> blv(nb, 0);
   std::vector<std::vector<int>> schur_poses;
@@ -3580,11 +3800,13 @@ int gn_prepare(pba_engine* e) {
     }
     const int nv = (int)poses.size();
     std::vector<char> used(nv * nv, 0);
+    std::vector<int> lpair(nv, 0);  // the pair (host, poses[l]) of each local target
     for (int r = p; r < q; ++r) {
       std::vector<int> lv{0};
       for (int b = pfirst[r]; b < pfirst[r] + pnblk[r]; ++b) {
         const int l = (int)(std::find(poses.begin(), poses.end(), gtgt[b]) - poses.begin());
         blv[b] = (uint8_t)l;
+        lpair[l] = e->pair_of_h[order[b]];
         lv.push_back(l);
       }
       for (int x : lv)
@@ -3602,7 +3824,9 @@ int gn_prepare(pba_engine* e) {
           upu.push_back(used[x * nv + y]);
         }
     const int fb0 = pfirst[p], nbc = pfirst[q - 1] + pnblk[q - 1] - fb0;
-    saux.push_back(make_int4((int)spairs.size(), (int)up.size(), fb0, nbc));
+    saux.push_back(make_int4((int)spairs.size(), (int)up.size(), (int)lvp.size(), nbc));
+    lvp.insert(lvp.end(), lpair.begin() + 1, lpair.end());
+    max_nv = std::max(max_nv, nv);
     for (auto& pr : up) spairs.push_back(make_uchar2((unsigned char)pr.first, (unsigned char)pr.second));
     sdesc.push_back(make_int4(p, q - p, nv, (int)soff));
     G.schur_lds = std::max<size_t>(G.schur_lds, sizeof(double) * 6 * (size_t)(q - p) * nv);
@@ -3613,6 +3837,8 @@ int gn_prepare(pba_engine* e) {
     p = q;
   }
   G.schur_doubles = soff;
+  G.schur_rt_off = 12 * (max_nv - 1);  // the chunks' target poses, then W (schur_chunk)
+  G.schur_lds += sizeof(double) * G.schur_rt_off;
   G.n_schur = (int)sdesc.size();
   {  // chunk c's point p → {first GN block, block count} at c · SCHUR_PTS + p (schur_kernel reads it with its descriptor)
     std::vector<int2> fbt((size_t)G.n_schur * SCHUR_PTS, make_int2(0, 0));
@@ -3760,9 +3986,11 @@ int gn_prepare(pba_engine* e) {
     }
   PBA_HIP(G.lin_rec.upload(lrec, st));
   PBA_HIP(G.chunk_desc.upload(cdesc, st));
-  PBA_HIP(G.blk_schur.resize((size_t)nb * 16));
+  PBA_HIP(G.blk_schur.resize((size_t)nb * kPd));
   PBA_HIP(G.part_lin.resize(std::max<size_t>(G.lin_slots, 1)));
-  PBA_HIP(G.blk_schur1.resize((size_t)nb * 16));  // the device LM loop's second linearisation set
+  PBA_HIP(G.blk_schur1.resize((size_t)nb * kPd));  // the device LM loop's second linearisation set
+  PBA_HIP(G.pair_rt.resize((size_t)std::max(e->n_pairs, 1) * 12));
+  PBA_HIP(G.pair_rt1.resize((size_t)std::max(e->n_pairs, 1) * 12));
   PBA_HIP(G.part_lin1.resize(std::max<size_t>(G.lin_slots, 1)));
   PBA_HIP(G.pt_first.upload(pfirst, st));
   PBA_HIP(G.pt_nblk.upload(pnblk, st));
@@ -3790,6 +4018,18 @@ int gn_prepare(pba_engine* e) {
   PBA_HIP(G.schur_aux.upload(saux, st));
   PBA_HIP(G.schur_pairs.upload(spairs, st));
   PBA_HIP(G.blk_lv.upload(blv, st));
+  {
+    std::vector<int4> lvp4(sdesc.size(), make_int4(0, 0, 0, 0));
+    for (size_t c = 0; c < sdesc.size(); ++c) {
+      int l4[4] = {0, 0, 0, 0};
+      for (int l = 0; l < 4 && l < sdesc[c].z - 1; ++l) l4[l] = lvp[saux[c].z + l];
+      lvp4[c] = make_int4(l4[0], l4[1], l4[2], l4[3]);
+    }
+    if (lvp4.empty()) lvp4.push_back(make_int4(0, 0, 0, 0));
+    PBA_HIP(G.schur_lvp4.upload(lvp4, st));
+  }
+  if (lvp.empty()) lvp.push_back(0);
+  PBA_HIP(G.schur_lvp.upload(lvp, st));
   PBA_HIP(G.part_schur.resize(std::max<size_t>(G.schur_doubles, 1)));
   PBA_HIP(G.pt_data.resize((size_t)ngp * 8));
   PBA_HIP(G.pt_data1.resize((size_t)ngp * 8));
@@ -3798,6 +4038,9 @@ int gn_prepare(pba_engine* e) {
   PBA_HIP(G.degen.resize(2));
   PBA_HIP(G.lin_set.resize(1));
   PBA_HIP(hipMemsetAsync(G.degen.p, 0, 2 * sizeof(int), st));
+  PBA_HIP(G.ts_part.resize((size_t)kDecideWgs * kTsCount));
+  PBA_HIP(G.ts_count.resize(1));
+  PBA_HIP(hipMemsetAsync(G.ts_count.p, 0, sizeof(int), st));
   PBA_HIP(G.sky_first.upload(first, st));
   PBA_HIP(G.sky_row.upload(rowp, st));
   PBA_HIP(G.sky_last.upload(last, st));
@@ -3866,14 +4109,24 @@ template <int KIND, int MODEL>  // photometric: MODEL = camera model + 4 · inte
 void launch_linearize(pba_engine* e, const KernelArgs& ka, const LinArgs& la) {
   const int grid = la.n_chunks;
   if constexpr (KIND == PBA_RESIDUAL_PHOTOMETRIC) {
+    const bool leg = e->gn.lin_legacy;
     switch (e->gn.ppl) {  // 9…32 px: 8 lanes per block, ⌈P/8⌉ rows per lane
       case 1: break;
-      case 2: linearize_rows_kernel<MODEL, 2><<<grid, kBlockThreads, 0, e->stream>>>(ka, la); return;
-      case 3: linearize_rows_kernel<MODEL, 3><<<grid, kBlockThreads, 0, e->stream>>>(ka, la); return;
-      default: linearize_rows_kernel<MODEL, 4><<<grid, kBlockThreads, 0, e->stream>>>(ka, la); return;
+      case 2:
+        if (leg) linearize_rows_kernel<MODEL, 2><<<grid, kBlockThreads, 0, e->stream>>>(ka, la);
+        else linearize_adj_kernel<MODEL, 2><<<grid, kBlockThreads, 0, e->stream>>>(ka, la);
+        return;
+      case 3:
+        if (leg) linearize_rows_kernel<MODEL, 3><<<grid, kBlockThreads, 0, e->stream>>>(ka, la);
+        else linearize_adj_kernel<MODEL, 3><<<grid, kBlockThreads, 0, e->stream>>>(ka, la);
+        return;
+      default:
+        if (leg) linearize_rows_kernel<MODEL, 4><<<grid, kBlockThreads, 0, e->stream>>>(ka, la);
+        else linearize_adj_kernel<MODEL, 4><<<grid, kBlockThreads, 0, e->stream>>>(ka, la);
+        return;
     }
     if (e->gn.lin_legacy) linearize_kernel<KIND, MODEL, 8><<<grid, kBlockThreads, 0, e->stream>>>(ka, la);
-    else linearize_adj_kernel<MODEL><<<grid, kBlockThreads, 0, e->stream>>>(ka, la);
+    else linearize_adj_kernel<MODEL, 1><<<grid, kBlockThreads, 0, e->stream>>>(ka, la);
   } else {
     linearize_kernel<KIND, MODEL, 4><<<grid, kBlockThreads, 0, e->stream>>>(ka, la);
   }
@@ -3958,7 +4211,8 @@ int linearize(pba_engine* e, double* cost, const double* lm = nullptr, const Pai
     ka.intr_t_d = G.intr_new_d.p;
   }
   LinArgs la{G.lin_rec.p, G.blk_schur1.p, G.part_lin1.p, wg_red, G.chunk_desc.p, G.blk_schur.p, G.part_lin.p, G.n_chunks,
-             lm ? lm : G.lm_idle.p, lm != nullptr, mark_set ? G.lin_set.p : nullptr, mark_set ? G.degen.p : nullptr};
+             lm ? lm : G.lm_idle.p, lm != nullptr, mark_set ? G.lin_set.p : nullptr, mark_set ? G.degen.p : nullptr,
+             G.pair_rt.p, G.pair_rt1.p};
   if (e->opt.residual_kind == PBA_RESIDUAL_PHOTOMETRIC) launch_linearize_photometric(e, ka, la);
   else launch_linearize_geometric(e, ka, la);
   PBA_HIP(hipGetLastError());
@@ -4147,7 +4401,8 @@ int enqueue_solve(pba_engine* e, double lambda, const double* lm = nullptr, bool
   const int nf = e->n_frames, nfs = G.nc_sys ? G.nfs : nf;
   SchurArgs sa{G.schur_desc.p, G.schur_aux.p, G.schur_pairs.p, G.pt_fb.p, G.blk_lv.p,
                G.blk_schur.p, G.blk_schur1.p, G.part_schur.p, G.pt_data.p, G.n_schur, lm ? lm : G.lm_idle.p,
-               lm ? e->poses.p : nullptr, G.poses_new.p, e->rho.p, G.rho_new.p, G.pt_orig.p, 7 * nf, G.n_gn_points};
+               lm ? e->poses.p : nullptr, G.poses_new.p, e->rho.p, G.rho_new.p, G.pt_orig.p, 7 * nf, G.n_gn_points,
+               G.pair_rt.p, G.pair_rt1.p, G.schur_lvp4.p, G.schur_lvp.p, G.schur_rt_off};
   schur_lds_limit(G);
   if (free_sets)
     schur_gate_kernel<<<std::max(1, std::min(G.n_schur, 512)), kBlockThreads, G.schur_lds, e->stream>>>(sa, G.degen.p);
@@ -4268,12 +4523,14 @@ void launch_free_decide(pba_engine* e, const DecideOpts& dopt, double seq, int g
   const int nf = e->n_frames;
   SchurArgs sa{G.schur_desc.p, G.schur_aux.p, G.schur_pairs.p, G.pt_fb.p, G.blk_lv.p,
                G.blk_schur.p, G.blk_schur1.p, G.part_schur.p, G.pt_data.p, G.n_schur, G.lm.p,
-               nullptr, nullptr, nullptr, nullptr, nullptr, 7 * nf, G.n_gn_points};
+               nullptr, nullptr, nullptr, nullptr, nullptr, 7 * nf, G.n_gn_points,
+               G.pair_rt.p, G.pair_rt1.p, G.schur_lvp4.p, G.schur_lvp.p, G.schur_rt_off};
   DecideArgs da{G.red.p, G.red2.p, G.gmax.p, gp, gq, G.n_chunks, G.status.p, dopt, G.lm.p,
-                init ? nullptr : G.lm_host_d + rec_slot(seq), seq, init ? 1 : 0, radius, G.lm_init.p};
+                init ? nullptr : G.lm_host_d + rec_slot(seq), seq, init ? 1 : 0, radius, G.lm_init.p,
+                G.ts_part.p, G.ts_count.p};
   FreeSets fs{{G.part_free0.p, G.part_free1.p}, {G.pt_data.p, G.pt_data1.p}, G.degen.p, G.lin_set.p};
   schur_lds_limit(G);
-  schur_free_decide_kernel<<<1 + G.n_schur, kBlockThreads, G.schur_lds, e->stream>>>(sa, da, fs);
+  schur_free_decide_kernel<<<kDecideWgs + G.n_schur, kBlockThreads, G.schur_lds, e->stream>>>(sa, da, fs);
   // tests: every set flagged, so every trial takes the λ-specific elimination (the degenerate-point path)
   if (G.force_degen) (void)hipMemsetAsync(G.degen.p, 0x01, 2 * sizeof(int), e->stream);
 }
@@ -4374,7 +4631,8 @@ int step_export(pba_engine* e, double lambda, int band, double* X) {
   const int nf = e->n_frames;
   SchurArgs sa{G.schur_desc.p, G.schur_aux.p, G.schur_pairs.p, G.pt_fb.p, G.blk_lv.p,
                G.blk_schur.p, G.blk_schur1.p, G.part_schur.p, G.pt_data.p, G.n_schur, G.lm_idle.p,
-               nullptr, nullptr, nullptr, nullptr, nullptr, 0, 0};
+               nullptr, nullptr, nullptr, nullptr, nullptr, 0, 0,
+               G.pair_rt.p, G.pair_rt1.p, G.schur_lvp4.p, G.schur_lvp.p, G.schur_rt_off};
   schur_lds_limit(G);
   if (G.n_schur > 0) schur_kernel<<<G.n_schur, kBlockThreads, G.schur_lds, e->stream>>>(sa, lambda);
   (void)nf;
@@ -4735,6 +4993,8 @@ int lm_loop_single(pba_engine* e, const pba_solver_options* o, pba_solver_summar
   if (set == 1) {  // the current state's pieces are in set 1: make it set 0 for the host-driven entry points
     std::swap(G.blk_schur.p, G.blk_schur1.p);
     std::swap(G.blk_schur.n, G.blk_schur1.n);
+    std::swap(G.pair_rt.p, G.pair_rt1.p);
+    std::swap(G.pair_rt.n, G.pair_rt1.n);
     std::swap(G.part_lin.p, G.part_lin1.p);
     std::swap(G.part_lin.n, G.part_lin1.n);
   }
@@ -4768,7 +5028,8 @@ int dist_trial(pba_engine* e, const Collective& coll, const DecideOpts& dopt, do
   const int nf = e->n_frames;
   SchurArgs sa{G.schur_desc.p, G.schur_aux.p, G.schur_pairs.p, G.pt_fb.p, G.blk_lv.p,
                G.blk_schur.p, G.blk_schur1.p, G.part_schur.p, G.pt_data.p, G.n_schur, G.lm.p,
-               e->poses.p, G.poses_new.p, e->rho.p, G.rho_new.p, G.pt_orig.p, 7 * nf, G.n_gn_points};
+               e->poses.p, G.poses_new.p, e->rho.p, G.rho_new.p, G.pt_orig.p, 7 * nf, G.n_gn_points,
+               G.pair_rt.p, G.pair_rt1.p, G.schur_lvp4.p, G.schur_lvp.p, G.schur_rt_off};
   schur_lds_limit(G);
   if (G.n_schur > 0) schur_kernel<<<G.n_schur, kBlockThreads, G.schur_lds, e->stream>>>(sa, 0.0);
   else launch_accept(e, G.lm.p);  // no points on this rank: the accept alone
@@ -4931,6 +5192,8 @@ int lm_loop(pba_engine* e, const pba_solver_options* o, const Collective* coll, 
   if (set == 1) {
     std::swap(G.blk_schur.p, G.blk_schur1.p);
     std::swap(G.blk_schur.n, G.blk_schur1.n);
+    std::swap(G.pair_rt.p, G.pair_rt1.p);
+    std::swap(G.pair_rt.n, G.pair_rt1.n);
     std::swap(G.part_lin.p, G.part_lin1.p);
     std::swap(G.part_lin.n, G.part_lin1.n);
   }

@@ -706,8 +706,12 @@ struct GnData {
   // JᵀJ is the exact Gram matrix of the rows and stays consistent with the point elimination's W W / H (fp32 products
   // and sums gave the reduced system errors of ~1e-7 of its scale that its condition number, ~1e11 at C4, turned into
   // wrong steps once the trust region had grown: DESIGN.md §4, tests/test_gpu_configs.py).
-  DevBuf<double> blk_schur;      // GN block → 16 doubles [Hll gl Wh(6) Wt(6) 0 0]
+  DevBuf<double> blk_schur;      // GN block → 8 doubles [H_ρρ g_ρ W_t(6)] (W_h follows from W_t, pair_rt: schur_chunk)
   DevBuf<double> part_lin;       // linearise chunk partials
+  DevBuf<double> pair_rt, pair_rt1;  // per pair [R_th(9) t_th(3)] of the linearisation in blk_schur / blk_schur1
+  DevBuf<int> schur_lvp;         // per Schur chunk (offset aux.z): the pair of each local target lv = 1 … nv − 1 …
+  DevBuf<int4> schur_lvp4;       // … and its first four, read with the chunk's descriptors
+  int schur_rt_off = 0;          // doubles of R, t per Schur workgroup at the start of its dynamic LDS (12 per target)
   DevBuf<double> blk_schur1, part_lin1;  // second set: the device LM loop linearises each candidate into the spare
   DevBuf<int> pt_first, pt_nblk, pt_orig;  // GN point → first GN block, block count, original point
   DevBuf<int4> pt_rec;           // GN point → {first GN block, block count, host frame, original point} (one load)
@@ -727,6 +731,8 @@ struct GnData {
   // Σ W Wᵀ/H, Σ W g/H and the point data, a flag for a point outside the LM clamp, the set the last linearisation wrote
   DevBuf<double> part_free0, part_free1, pt_data1;
   DevBuf<int> degen, lin_set;
+  DevBuf<double> ts_part;  // the decision workgroups' slices of the trial sums (schur_free_decide_kernel) …
+  DevBuf<int> ts_count;    // … and their arrival count
   bool force_degen = std::getenv("PBA_TEST_FORCE_DEGEN") != nullptr;
   // tests: the 14-column linearisation (linearize_kernel) for ≤ 8-px photometric patterns instead of the adjoint form
   bool lin_legacy = std::getenv("PBA_LIN_LEGACY") != nullptr;  // tests: the λ-specific path on every trial

@@ -86,16 +86,18 @@ def test_reduced_system_large_patterns(P, pm):
     assert abs(c_new - cost_new_ref) <= 1e-5 * cost_new_ref + 1e-6
 
 
-@pytest.mark.parametrize("pm", [0, 1, 2, 3, 6])
-def test_adjoint_linearisation_matches_fourteen_columns(pm, monkeypatch):
-    """≤ 8-px photometric patterns linearise through the pair's adjoint (linearize_adj_kernel: the matrix cores form
-    the 8-column target products, the host blocks follow as Adᵀ·H_tt·Ad, −Adᵀ·H_tt, −Adᵀ·g_t and W_h = −W_t·Ad) —
-    against the 14-column products of the same rows (linearize_kernel, PBA_LIN_LEGACY) on the same problem: same
-    cost, reduced system and step to the rounding of the fp32 host rows (both are fp64 sums of fp32 rows; the host
-    Jacobian's fp32 rounding differs), then the same LM run."""
+@pytest.mark.parametrize("pm,P", [(0, 8), (1, 8), (2, 8), (3, 8), (6, 8), (0, 21), (1, 12), (2, 17), (5, 30)])
+def test_adjoint_linearisation_matches_fourteen_columns(pm, P, monkeypatch):
+    """Photometric patterns linearise through the pair's adjoint (linearize_adj_kernel: the matrix cores form the
+    8-column target products, the host blocks follow as Adᵀ·H_tt·Ad, −Adᵀ·H_tt, −Adᵀ·g_t and W_h = −W_t·Ad; 9…32 px
+    in ⌈P/8⌉ passes into fp64 per-block accumulators) — against the 14-column products of the same rows
+    (linearize_kernel / linearize_rows_kernel, PBA_LIN_LEGACY) on the same problem: same cost, reduced system and step
+    to the rounding of the fp32 host rows (the host Jacobian's fp32 rounding differs; beyond 8 px the legacy kernel's
+    block products are fp32), then the same LM run."""
     interp, model = pm >> 2, pm & 3
+    pat = None if P == 8 else np.random.default_rng(P).integers(-3, 4, (P, 2)).astype(np.float32)
     pb = synth.make_problem(model=model, n_frames=10, n_points=200, width=376, height=240, seed=70 + pm, border=12,
-                            obs_sigma=0.3)
+                            obs_sigma=0.3, pattern=pat)
     pb.interp = interp
     pb.poses[:2] = pb.poses_gt[:2]
     out = {}
@@ -121,8 +123,9 @@ def test_adjoint_linearisation_matches_fourteen_columns(pm, monkeypatch):
     print(f"\nmodel {pm}: S {eS:.1e}, g {eg:.1e}, pose step {ep:.1e}, ρ step {el:.1e}, final cost "
           f"{s1['final_cost']:.10e} / {s0['final_cost']:.10e}")
     assert c1 == c0  # the same rows and weights: the cost does not depend on the products
-    assert eS <= 1e-6 and eg <= 1e-6, (eS, eg)
-    assert ep <= 1e-5 and el <= 1e-5, (ep, el)
+    tol = 1e-6 if P == 8 else 1e-5  # (the legacy 9…32-px products are fp32 per block)
+    assert eS <= tol and eg <= tol, (eS, eg)
+    assert ep <= 10 * tol and el <= 10 * tol, (ep, el)
     for key in ("iterations", "successful_steps", "unsuccessful_steps", "termination"):
         assert s1[key] == s0[key], (key, s1, s0)
     assert abs(s1["final_cost"] - s0["final_cost"]) <= 1e-6 * s0["final_cost"]
