@@ -1280,6 +1280,9 @@ struct AsmArgs {
   const double* part_free0;
   const double* part_free1;
   const int* degen;
+  const int* sky_diag;  // assemble_kernel: the diagonal blocks (long contribution lists: kAsmSeg lanes per element) …
+  const int* sky_off;   // … and the off-diagonal ones (one lane)
+  int n_diag;
 };
 
 // Fixed-order sums over a contribution list (total, and the part that is not a Schur term — the undamped
@@ -1288,14 +1291,17 @@ struct AsmArgs {
 // the next batch's entries loaded beside the current batch's values measured slower: 12.8 → 15.0 µs at C4, 128
 // VGPRs and twice the clamped loads of the short off-diagonal lists.)
 constexpr int GATHER = 8;
+// seg / nseg: this lane's share of the list, entries beg + seg, beg + seg + nseg, … (the caller adds the nseg lanes'
+// sums in a fixed order).
 __device__ __forceinline__ void contrib_sums(const AsmArgs& a, const int2* __restrict__ list, int beg, int end, int e,
-                                             int et, double& sum, double& dsum, double pscale = 1.0) {
+                                             int et, double& sum, double& dsum, double pscale = 1.0, int seg = 0,
+                                             int nseg = 1) {
   sum = dsum = 0.0;
-  for (int q0 = beg; q0 < end; q0 += GATHER) {
+  for (int q0 = beg + seg; q0 < end; q0 += GATHER * nseg) {
     int2 c[GATHER];
     double v[GATHER];
 #pragma unroll
-    for (int u = 0; u < GATHER; ++u) c[u] = list[min(q0 + u, end - 1)];
+    for (int u = 0; u < GATHER; ++u) c[u] = list[min(q0 + u * nseg, end - 1)];
 #pragma unroll
     for (int u = 0; u < GATHER; ++u) {
       // both loads unconditional (the other one at a valid dummy offset): no divergent branch, no wait
@@ -1307,11 +1313,21 @@ __device__ __forceinline__ void contrib_sums(const AsmArgs& a, const int2* __res
     }
 #pragma unroll
     for (int u = 0; u < GATHER; ++u) {
-      if (q0 + u < end) {
+      if (q0 + u * nseg < end) {
         sum += v[u];
         if (!(c[u].y & C_SCHUR)) dsum += v[u];
       }
     }
+  }
+}
+// The kAsmSeg lanes of one element (aligned groups) add their list shares: lane 0 of the group gets the total, in a
+// fixed order.
+constexpr int kAsmSeg = 4;
+__device__ __forceinline__ void seg_total(double& sum, double& dsum) {
+#pragma unroll
+  for (int m = 1; m < kAsmSeg; m <<= 1) {
+    sum += __shfl_xor(sum, m, 64);
+    dsum += __shfl_xor(dsum, m, 64);
   }
 }
 
@@ -1328,13 +1344,24 @@ __global__ void assemble_kernel(AsmArgs a, double lambda) {
     a.part_schur = lv.set != 0.0 ? a.part_free1 : a.part_free0;
     pscale = 1.0 / (1.0 + lambda);
   }
+  // thread ranges: the diagonal blocks' elements, kAsmSeg lanes each (their lists are the long ones: every chunk hosted
+  // by or targeting the keyframe, ~30 partials at C4, four dependent memory rounds on one lane), then the off-diagonal
+  // blocks' elements one lane each, then the gradient rows kAsmSeg lanes each
   const int tid = blockIdx.x * blockDim.x + threadIdx.x;
-  const int nS = a.n_sky * 36;
+  const int nA = a.n_diag * 36 * kAsmSeg, nS = nA + (a.n_sky - a.n_diag) * 36;
   if (tid < nS) {
-    const int s = tid / 36, e = tid % 36, r = e / 6, cc = e % 6;
+    const bool dg = tid < nA;
+    const int w = dg ? tid / kAsmSeg : tid - nA, seg = dg ? tid % kAsmSeg : 0;
+    const int s = dg ? a.sky_diag[w / 36] : a.sky_off[w / 36], e = w % 36, r = e / 6, cc = e % 6;
     const int i = a.blk_i[s], j = a.blk_j[s];
     double sum, dsum;
-    contrib_sums(a, a.sky_contrib, a.sky_cptr[s], a.sky_cptr[s + 1], r * 6 + cc, cc * 6 + r, sum, dsum, pscale);
+    contrib_sums(a, a.sky_contrib, a.sky_cptr[s], a.sky_cptr[s + 1], r * 6 + cc, cc * 6 + r, sum, dsum, pscale, seg,
+                 dg ? kAsmSeg : 1);
+    if (dg) {
+      seg_total(sum, dsum);
+      if (seg != 0) return;
+    }
+    const int tid_s = s * 36 + e;  // the element's position in S
     double val = sum;
     if (a.fixed[i] || a.fixed[j]) {
       val = (i == j && r == cc) ? 1.0 : 0.0;
@@ -1343,7 +1370,7 @@ __global__ void assemble_kernel(AsmArgs a, double lambda) {
       a.Ddiag[6 * i + r] = D;
       val = sum + lambda * D;
     }
-    a.S[tid] = val;
+    a.S[tid_s] = val;
     if (a.Sband) a.Sband[(long long)i * ((a.band + 1) * 36 + 6) + (j - i + a.band) * 36 + e] = val;
     if (a.crD) {
       const int B = a.crB, M = 6 * B, I = i / B, J = j / B;
@@ -1363,11 +1390,13 @@ __global__ void assemble_kernel(AsmArgs a, double lambda) {
     }
     return;
   }
-  const int t = tid - nS;
+  const int tg = tid - nS, t = tg / kAsmSeg, seg = tg % kAsmSeg;
   if (t >= 6 * a.n_frames) return;
   const int i = t / 6, r = t % 6;
   double sum, dsum;
-  contrib_sums(a, a.g_contrib, a.g_cptr[i], a.g_cptr[i + 1], r, r, sum, dsum, pscale);
+  contrib_sums(a, a.g_contrib, a.g_cptr[i], a.g_cptr[i + 1], r, r, sum, dsum, pscale, seg, kAsmSeg);
+  seg_total(sum, dsum);
+  if (seg != 0) return;
   a.g[t] = a.fixed[i] ? 0.0 : sum;
   if (a.Sband) a.Sband[(long long)i * ((a.band + 1) * 36 + 6) + (a.band + 1) * 36 + r] = a.fixed[i] ? 0.0 : sum;
   if (a.crD) {
@@ -4050,6 +4079,15 @@ int gn_prepare(pba_engine* e) {
   PBA_HIP(G.g_contrib.upload(gflat.empty() ? std::vector<int2>{make_int2(0, 0)} : gflat, st));
   PBA_HIP(G.sky_blk_i.upload(bi, st));
   PBA_HIP(G.sky_blk_j.upload(bj, st));
+  {
+    std::vector<int> dg, od;
+    for (int q = 0; q < (int)bi.size(); ++q) (bi[q] == bj[q] ? dg : od).push_back(q);
+    G.n_sky_diag = (int)dg.size();
+    if (dg.empty()) dg.push_back(0);
+    if (od.empty()) od.push_back(0);
+    PBA_HIP(G.sky_diag.upload(dg, st));
+    PBA_HIP(G.sky_off.upload(od, st));
+  }
   PBA_HIP(G.fixed.upload(fixed, st));
   PBA_HIP(G.S.resize((size_t)G.n_sky * 36));
   PBA_HIP(G.L.resize((size_t)G.n_sky * 36));
@@ -4430,12 +4468,13 @@ int enqueue_solve(pba_engine* e, double lambda, const double* lm = nullptr, bool
              G.g_contrib.p, G.sky_blk_i.p, G.sky_blk_j.p, G.fixed.p, G.S.p, G.g.p, G.g_dir.p, G.Ddiag.p,
              G.band_kernel && !direct ? G.Sband.p : nullptr, G.band_kernel, G.n_sky, nfs,
              direct ? L0.D : nullptr, L0.U, L0.b, G.band_kernel, G.status.p, free_sets ? G.part_free0.p : nullptr,
-             free_sets ? G.part_free1.p : nullptr, free_sets ? G.degen.p : nullptr};
+             free_sets ? G.part_free1.p : nullptr, free_sets ? G.degen.p : nullptr, G.sky_diag.p, G.sky_off.p,
+             G.n_sky_diag};
   if (G.sband_dirty && G.band_kernel && !direct) {  // a distributed import filled the whole band: clear the off-profile part
     PBA_HIP(hipMemsetAsync(G.Sband.p, 0, sizeof(double) * (size_t)nf * ((G.band_kernel + 1) * 36 + 6), e->stream));
     G.sband_dirty = false;
   }
-  const int nthreads = G.n_sky * 36 + 6 * nfs;
+  const int nthreads = (G.n_sky + (kAsmSeg - 1) * G.n_sky_diag) * 36 + 6 * nfs * kAsmSeg;
   assemble_kernel<<<(nthreads + 255) / 256, 256, 0, e->stream>>>(aa, lambda);
   if (G.nc_sys) {  // the intrinsics rows of the skyline system (over assemble's zeros there)
     IntrBorderArgs ba{G.ib_data.p, G.ib_rec.p, G.ib_cam.p, G.pt_rec.p, G.pt_data.p, G.ib_bptr.p, G.ib_blist.p,

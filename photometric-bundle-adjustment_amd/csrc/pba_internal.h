@@ -740,6 +740,8 @@ struct GnData {
   DevBuf<int> sky_cptr, g_cptr;  // contribution lists (CSR) per skyline block / per pose
   DevBuf<int2> sky_contrib, g_contrib;
   DevBuf<int> sky_blk_i, sky_blk_j;  // skyline block → (row pose, column pose)
+  DevBuf<int> sky_diag, sky_off;     // the diagonal skyline blocks, the others (assemble_kernel's thread ranges)
+  int n_sky_diag = 0;
   DevBuf<double> S, L, Sband, Lband, g, g_dir, Ddiag, Linv, x;  // skyline system, its factor, rhs, direct gradient, LM diagonal, L_kk⁻¹, step
   DevBuf<uint8_t> fixed;
   DevBuf<uint8_t> observed, fixed_req, fixed_dist;  // multi-GPU: local observation flags, requested / effective constants
