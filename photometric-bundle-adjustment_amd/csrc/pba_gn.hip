@@ -532,7 +532,7 @@ void linearize_adj_kernel(const KernelArgs a, const LinArgs g) {
   };
   int ok;
   float bcost;
-  double accb[PPL == 1 ? 1 : BW];  // PPL > 1: the blocks' unweighted products, then weighted
+  double accb[BW];  // the blocks' products (PPL > 1: unweighted over the passes, then weighted)
   if constexpr (PPL == 1) {
     const bool act = live && k < R;
     const float2 off = pattern_at<LPB>(a, k);
@@ -540,7 +540,15 @@ void linearize_adj_kernel(const KernelArgs a, const LinArgs g) {
     stage_tile_pp<LPB>(a, s_tb, wb, k, make_int2(lr.y, lr.z & 0xffffff));
     asm volatile("" ::"v"(Ih));
     __syncthreads();
+#ifdef PBA_ABL_ROW  // ablation builds (tools/build_variant.sh): timing of the parts, results are garbage
+    Row row;
+    row.r = Ih + (float)s_tb[wb].pr.R[k] + off.x;
+    row.jr = row.r;
+    row.tv = Vec3{row.r, row.r, row.r};
+    row.tw = row.tv;
+#else
     const Row row = photometric_row<MODEL, true>(a, s_tb[wb], off, Ih);  // (hv, hw unused: not formed)
+#endif
     save_rt();
     ok = group_all<LPB>(act ? row.ok : 1);
     const float s = group_sum<LPB>(act && ok ? row.r * row.r : 0.0f);
@@ -621,34 +629,45 @@ void linearize_adj_kernel(const KernelArgs a, const LinArgs g) {
     const int ppos = i4 != 2 || beta == 0 || beta == 3 ? -1 : (beta == 1 ? 2 + kq : (kq < 2 ? 6 + kq : kq - 2));
     double* sP = reinterpret_cast<double*>(arena[wave] + kProdOff);
     const int lo = __builtin_amdgcn_readfirstlane(lt);
+    if constexpr (PPL == 1) {
+      // every block's products first — the two-step chains of four blocks at a time in flight together — then the
+      // stores: the matrix-core latency is paid once per four blocks, and the point-data and run-set stores each run
+      // under one exec mask instead of one per block
+#pragma unroll
+      for (int h = 0; h < BW; h += 4) {
+        float o[4][4];
+#pragma unroll
+        for (int b = 0; b < 4; ++b) ops(h + b, o[b]);
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+          double acc = 0.0;
+#pragma unroll
+          for (int st = 0; st < 2; ++st)
+            acc = __builtin_amdgcn_mfma_f64_4x4x4f64((double)o[b][2 * st], (double)o[b][2 * st + 1], acc, 0, 0, 0);
+          accb[h + b] = acc;
+        }
+      }
+    }
+    int gpb[BW];  // (read in uniform control flow: a readlane of a lane the exec mask excludes reads a dead register)
+#pragma unroll
+    for (int b = 0; b < BW; ++b) gpb[b] = __builtin_amdgcn_readlane(gpos, b * LPB);
+    if (ppos >= 0) {
+#pragma unroll
+      for (int b = 0; b < BW; ++b)
+        if (b < nbw) blk_schur[(long long)gpb[b] * kPd + ppos] = accb[b];
+    }
     double tacc = 0.0;
     int cur = lo;
-    float o_n[4];
-    if constexpr (PPL == 1) ops(0, o_n);
 #pragma unroll
     for (int b = 0; b < BW; ++b) {
-      double acc = 0.0;
-      if constexpr (PPL == 1) {
-        float o[4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) o[q] = o_n[q];
-        if (b + 1 < BW) ops(b + 1, o_n);  // the next block's LDS reads in flight over this block's matrix-core steps
-#pragma unroll
-        for (int st = 0; st < 2; ++st)
-          acc = __builtin_amdgcn_mfma_f64_4x4x4f64((double)o[2 * st], (double)o[2 * st + 1], acc, 0, 0, 0);
-      } else {
-        acc = accb[b];
-      }
       if (b < nbw) {
-        const int gpb = __builtin_amdgcn_readlane(gpos, b * LPB);
-        if (ppos >= 0) blk_schur[(long long)gpb * kPd + ppos] = acc;
         const int ltb = __builtin_amdgcn_readlane(lt, b * LPB);
         if (ltb != cur) {
           if (pslot >= 0) sP[(cur - lo) * NQ + pslot] = tacc;
           tacc = 0.0;
           cur = ltb;
         }
-        tacc += acc;
+        tacc += accb[b];
       }
     }
     if (nbw > 0 && pslot >= 0) sP[(cur - lo) * NQ + pslot] = tacc;
@@ -657,6 +676,9 @@ void linearize_adj_kernel(const KernelArgs a, const LinArgs g) {
       s_wn[wave] = nbw > 0 ? cur - lo + 1 : 0;
     }
   }
+#ifdef PBA_ABL_PHASE
+  if (n_t > 0) return;
+#endif
   __syncthreads();
   // Phase A: the chunk's product sums per local target j, as full 8 × 8 matrices (one thread per entry; the sets of j
   // over the waves in order), and Ad_j from R_th, t_th.  Over wave 0's rows.
@@ -990,24 +1012,37 @@ __device__ __forceinline__ SchurHead schur_head(const SchurArgs& g, int c) {
 // The host block of W: a photometric (or geometric) row's host Jacobian is its target Jacobian through the pair's
 // adjoint, J_h = −J_t·Ad with Ad = [[R, [t]×R], [0, R]] (R = R_th, t = t_th; linearize_adj_kernel), so
 // W_h = J_ρᵀJ_h = −Σ_targets W_t·Ad = −Σ_lv [W_tv·R, (W_tv × t + W_tw)·R] over the point's per-target sums W[p][lv]: the
-// blocks carry W_t alone (8 doubles of point data instead of 16).  Component c of point p; rt: the local targets'
-// [R(9), t(3)] in LDS.
-__device__ __forceinline__ double host_w(const double (*W)[6], const double* rt, int p, int nv, int c) {
-  double v = 0.0;
+// blocks carry W_t alone (8 doubles of point data instead of 16).  Point p, all six components (one thread per point:
+// per component, the reads of W and R, t were a third of the work); rt: the local targets' [R(9), t(3)] in LDS.
+__device__ __forceinline__ void host_w(const double (*W)[6], const double* rt, int p, int nv, double* out) {
+  double v[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
   for (int l = 1; l < nv; ++l) {
-    const double* w = W[p * nv + l];
-    const double* R = rt + 12 * (l - 1);
-    if (c < 3) {
-      v += w[0] * R[c] + w[1] * R[3 + c] + w[2] * R[6 + c];
-    } else {
-      const double* t = R + 9;
-      const int cc = c - 3;
-      const double u0 = w[1] * t[2] - w[2] * t[1] + w[3], u1 = w[2] * t[0] - w[0] * t[2] + w[4],
-                   u2 = w[0] * t[1] - w[1] * t[0] + w[5];
-      v += u0 * R[cc] + u1 * R[3 + cc] + u2 * R[6 + cc];
+    const double2* w2 = reinterpret_cast<const double2*>(W[p * nv + l]);
+    const double2* r2 = reinterpret_cast<const double2*>(rt + 12 * (l - 1));
+    double w[6], R[12];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      const double2 x = w2[i];
+      w[2 * i] = x.x;
+      w[2 * i + 1] = x.y;
+    }
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+      const double2 x = r2[i];
+      R[2 * i] = x.x;
+      R[2 * i + 1] = x.y;
+    }
+    const double* t = R + 9;
+    const double u0 = w[1] * t[2] - w[2] * t[1] + w[3], u1 = w[2] * t[0] - w[0] * t[2] + w[4],
+                 u2 = w[0] * t[1] - w[1] * t[0] + w[5];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      v[c] += w[0] * R[c] + w[1] * R[3 + c] + w[2] * R[6 + c];
+      v[3 + c] += u0 * R[c] + u1 * R[3 + c] + u2 * R[6 + c];
     }
   }
-  return -v;
+#pragma unroll
+  for (int c = 0; c < 6; ++c) out[c] = -v[c];
 }
 __device__ __forceinline__ void schur_chunk(const SchurArgs& g, const SchurHead& h, double lambda,
                                             const double* __restrict__ blk_schur, const double* __restrict__ pair_rt,
@@ -1019,12 +1054,12 @@ __device__ __forceinline__ void schur_chunk(const SchurArgs& g, const SchurHead&
   const int first = d.x, npt = d.y, nv = d.z, poff = d.w;
 #ifdef PBA_FD_STAMPS
   const long long ts0 = wall_clock64();
-  long long ts1 = 0, ts2 = 0;
+  long long ts1 = 0, ts2 = 0, tsa = 0, tsb = 0, tsc = 0;
   auto stamp_out = [&](const char* tag) {
     const int b = blockIdx.x;
     if (threadIdx.x == 0 && (b == 17 || b == 300 || b == 600 || b == 1000))
-      printf("fdphase b=%d %s start %lld zero %lld loads %lld total %lld\n", b, tag, ts0, ts1 - ts0, ts2 - ts0,
-             wall_clock64() - ts0);
+      printf("fdphase b=%d %s zero %lld acc %lld presync %lld sync %lld wh %lld total %lld\n", b, tag, ts1 - ts0,
+             tsa - ts0, tsb - ts0, tsc - ts0, ts2 - ts0, wall_clock64() - ts0);
   };
 #endif
   double* const rt = W_dyn;  // the local targets' R_th, t_th (12 each)
@@ -1066,6 +1101,10 @@ __device__ __forceinline__ void schur_chunk(const SchurArgs& g, const SchurHead&
       lv0[it][u] = q == 0 ? 0 : g.blk_lv[b];
     }
   }
+#ifdef PBA_FD_STAMPS
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  tsa = wall_clock64();
+#endif
 #pragma unroll
   for (int it = 0; it < kPtIter; ++it) {
     const int p = it * (kBlockThreads / 4) + (threadIdx.x >> 2), gp = first + p;
@@ -1116,13 +1155,22 @@ __device__ __forceinline__ void schur_chunk(const SchurArgs& g, const SchurHead&
     if (rti[u] >= 0) rt[rti[u]] = rtv[u];
   for (int i = threadIdx.x + 2 * kBlockThreads; i < 12 * (nv - 1); i += kBlockThreads)  // (> 43 local poses)
     rt[i] = pair_rt[(long long)g.lvp[ax.z + i / 12] * 12 + i % 12];
+#ifdef PBA_FD_STAMPS
+  tsb = wall_clock64();
+#endif
   if (degen && __syncthreads_or(bad) && threadIdx.x == 0) atomicOr(degen, 1);
   __syncthreads();
-  for (int i = threadIdx.x; i < npt * 6; i += kBlockThreads) {  // W_h = W[p][0] from the targets' sums
-    const int p = i / 6, c = i - 6 * p;
-    const double v = host_w(W, rt, p, nv, c);
-    W[p * nv][c] = v;
-    if (pt_out) pt_out[(long long)(first + p) * 8 + 2 + c] = v;
+#ifdef PBA_FD_STAMPS
+  tsc = wall_clock64();
+#endif
+  for (int p = threadIdx.x; p < npt; p += kBlockThreads) {  // W_h = W[p][0] from the targets' sums
+    double v[6];
+    host_w(W, rt, p, nv, v);
+#pragma unroll
+    for (int c = 0; c < 6; ++c) W[p * nv][c] = v[c];
+    if (pt_out)
+#pragma unroll
+      for (int c = 0; c < 6; ++c) pt_out[(long long)(first + p) * 8 + 2 + c] = v[c];
   }
   __syncthreads();
 #ifdef PBA_FD_STAMPS
