@@ -462,10 +462,13 @@ __host__ __device__ constexpr int upper8(int r, int c) { return r * 8 - r * (r -
 #ifndef PBA_LINADJ_WAVES
 #define PBA_LINADJ_WAVES 5
 #endif
-template <int MODEL, int PPL>
-__global__ __launch_bounds__(kBlockThreads) __attribute__((amdgpu_waves_per_eu(PPL == 1 ? 8 : PBA_LINADJ_WAVES, 8)))
+// NT: threads per workgroup (NT / 8 blocks per chunk).  Measured at 8 px: 512 threads (64-block chunks: the phases,
+// partial slots, assembly contributions and decision slots per chunk spread over twice the blocks) 71.1 → 76.6 µs for
+// the linearisation against 12.1 → 10.9 for the assembly — the 8-wave barriers cost more than the halved chunk work.
+template <int MODEL, int PPL, int NT>
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(PPL == 1 ? 8 : PBA_LINADJ_WAVES, 8)))
 void linearize_adj_kernel(const KernelArgs a, const LinArgs g) {
-  constexpr int LPB = 8, BW = 64 / LPB, NW = kBlockThreads / 64;
+  constexpr int LPB = 8, BW = 64 / LPB, NW = NT / 64;
   constexpr int kRowS = 12;                  // floats per staged row (8 used): 8-lane groups of b128 stores hit 32 banks
   constexpr int NQ = 36;                     // products per run set (the 8 × 8 upper triangle)
   constexpr int kTileW = BW * (int)sizeof(TileBlock), kRowsW = 64 * kRowS * 4, kProdW = kChunkTargets * NQ * 8;
@@ -476,19 +479,19 @@ void linearize_adj_kernel(const KernelArgs a, const LinArgs g) {
   constexpr int kArena = PPL == 1 ? kProdOff + kProdW : kTileW + kRowsW;
   static_assert(kProdW <= kTileW && kRowsW <= kTileW + 512, "regions");
   static_assert(kChunkTargets * 64 * 8 <= kRowsW, "phase data fits a rows region");
-  static_assert(kBlockThreads == 64 * kChunkTargets, "one thread per entry of the targets' 8 × 8 sums");
+  static_assert(NT >= 64 * kChunkTargets && NT / LPB <= 64, "one thread per entry of the targets' 8 × 8 sums");
   __shared__ __attribute__((aligned(16))) unsigned char arena[NW][kArena];
   __shared__ double s_rt[kChunkTargets][12];  // R_th, t_th of each local target (the host is the chunk's)
   __shared__ double s_ad[kChunkTargets][36];  // Ad of each local target
   __shared__ int s_wlo[NW], s_wn[NW];
-  __shared__ float s_bc[kBlockThreads / LPB];
+  __shared__ float s_bc[NT / LPB];
   __shared__ float2 s_pat[PPL == 1 ? 1 : LPB * PPL];
   const int chunk = logical_tile();
   const int lb = threadIdx.x / LPB;
   // one memory round: record, chunk descriptor and linearise record before either exit (see linearize_kernel)
   const int cc = min(chunk, g.n_chunks - 1);
   const int4 d = g.chunk_desc[cc];
-  const int4 lr = g.lin_rec[(long long)cc * (kBlockThreads / LPB) + lb];
+  const int4 lr = g.lin_rec[(long long)cc * (NT / LPB) + lb];
   const LmView lv = lm_view(g.lm);
   asm volatile("" ::"v"(lr.x), "v"(lr.y), "v"(lr.z), "v"(lr.w), "s"(d.x), "s"(d.y), "s"(d.z), "s"(d.w));
   if (chunk >= g.n_chunks || lv.done != 0.0) return;
@@ -686,7 +689,7 @@ void linearize_adj_kernel(const KernelArgs a, const LinArgs g) {
   double* sN = reinterpret_cast<double*>(arena[1] + kRowsOff);  // [j][6][6]: H_tt,j·Ad_j
   {
     const int t = threadIdx.x, j = t >> 6, r = (t >> 3) & 7, c = t & 7;
-    if (j < n_t) {
+    if (j < n_t && t < 64 * kChunkTargets) {
       const int u = upper8(min(r, c), max(r, c));
       double acc = 0.0;
 #pragma unroll
@@ -714,7 +717,7 @@ void linearize_adj_kernel(const KernelArgs a, const LinArgs g) {
   __syncthreads();
   // Phase B: N_j = H_tt,j·Ad_j; the target outputs — H_ht = −AdᵀH_tt, H_tt, g_t — and g_h = −Σ_j Ad_jᵀ g_t,j
   const int nout = SLOT_LIN_BASE + SLOT_LIN_T * n_t;
-  for (int o = threadIdx.x; o < nout; o += kBlockThreads) {
+  for (int o = threadIdx.x; o < nout; o += NT) {
     if (o < 36) {
       const int r = o / 6, c = o - 6 * (o / 6);
       for (int j = 0; j < n_t; ++j) {
@@ -4200,19 +4203,19 @@ void launch_linearize(pba_engine* e, const KernelArgs& ka, const LinArgs& la) {
       case 1: break;
       case 2:
         if (leg) linearize_rows_kernel<MODEL, 2><<<grid, kBlockThreads, 0, e->stream>>>(ka, la);
-        else linearize_adj_kernel<MODEL, 2><<<grid, kBlockThreads, 0, e->stream>>>(ka, la);
+        else linearize_adj_kernel<MODEL, 2, kBlockThreads><<<grid, kBlockThreads, 0, e->stream>>>(ka, la);
         return;
       case 3:
         if (leg) linearize_rows_kernel<MODEL, 3><<<grid, kBlockThreads, 0, e->stream>>>(ka, la);
-        else linearize_adj_kernel<MODEL, 3><<<grid, kBlockThreads, 0, e->stream>>>(ka, la);
+        else linearize_adj_kernel<MODEL, 3, kBlockThreads><<<grid, kBlockThreads, 0, e->stream>>>(ka, la);
         return;
       default:
         if (leg) linearize_rows_kernel<MODEL, 4><<<grid, kBlockThreads, 0, e->stream>>>(ka, la);
-        else linearize_adj_kernel<MODEL, 4><<<grid, kBlockThreads, 0, e->stream>>>(ka, la);
+        else linearize_adj_kernel<MODEL, 4, kBlockThreads><<<grid, kBlockThreads, 0, e->stream>>>(ka, la);
         return;
     }
     if (e->gn.lin_legacy) linearize_kernel<KIND, MODEL, 8><<<grid, kBlockThreads, 0, e->stream>>>(ka, la);
-    else linearize_adj_kernel<MODEL, 1><<<grid, kBlockThreads, 0, e->stream>>>(ka, la);
+    else linearize_adj_kernel<MODEL, 1, kBlockThreads><<<grid, kBlockThreads, 0, e->stream>>>(ka, la);
   } else {
     linearize_kernel<KIND, MODEL, 4><<<grid, kBlockThreads, 0, e->stream>>>(ka, la);
   }
