@@ -240,7 +240,8 @@ def make_states(pb, torch, dev, seed):
 
 
 def time_evaluation(eng, states, steps, warmup, clock_warmup_s, torch, dist, dev):
-    """W warmup steps (after a clock warm-up), then K timed steps bracketed by barrier + synchronize; returns
+    """W warmup steps (after a clock warm-up), then K timed steps bracketed by barrier + synchronize (enqueued by one
+    pba_evaluate_states_device call: K launches, one per step, each at a new HBM-resident state); returns
     (max-over-ranks elapsed s, max-over-ranks average block-kernel µs, host diagnostics).  The kernel duration comes
     from two HIP events on the engine's stream around the K timed launches (elapsed ÷ K: each launch plus the
     dispatch gap to the next, so never below rocprof's kernel average); the launches themselves carry no events —
@@ -277,13 +278,16 @@ def time_evaluation(eng, states, steps, warmup, clock_warmup_s, torch, dist, dev
     # the timed region
     stream = torch.cuda.ExternalStream(eng.stream(), device=dev)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    # the K steps enqueued by one ABI call (pba_evaluate_states_device: K launches, each at the next state and adopting
+    # it) — per-step foreign calls from Python cost ~5 µs of host time each, more than a 1/8 shard's 8-µs kernel
+    pp = [states[i & 1][0].data_ptr() for i in range(steps)]
+    rr = [states[i & 1][1].data_ptr() for i in range(steps)]
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     e0.record(stream)
-    for i in range(steps):
-        step(i)
+    eng.evaluate_states_device(pp, rr, True, sync=False)
     host_diag["enqueue_us_per_step"] = 1e6 * (time.perf_counter() - t0) / steps
     e1.record(stream)
     eng.synchronize()

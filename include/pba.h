@@ -113,6 +113,12 @@ int pba_evaluate(pba_engine* engine, int32_t want_jacobians);
  * launch precedes the evaluation.  d_poses / d_inv_dist must stay valid until the launch has run. */
 int pba_evaluate_state_device(pba_engine* engine, const double* d_poses, const double* d_inv_dist,
                               int32_t want_jacobians);
+/* n evaluations back to back — state i = (d_poses[i], d_inv_dist[i]), each as pba_evaluate_state_device (one launch
+ * that adopts it), enqueued by one call: a caller stepping through candidate states (a line search, a benchmark's
+ * steps) pays the host-side launch cost in C instead of per foreign-function call.  Replaces n calls of
+ * Evaluator::Evaluate (program_evaluator.h:139-258); the records hold the last state's evaluation. */
+int pba_evaluate_states_device(pba_engine* engine, int32_t n, const double* const* d_poses,
+                               const double* const* d_inv_dist, int32_t want_jacobians);
 int pba_synchronize(pba_engine* engine);
 
 /* Results ---------------------------------------------------------------------------------------- */

@@ -1098,6 +1098,17 @@ int pba_evaluate_state_device(pba_engine* e, const double* d_poses, const double
   return evaluate_at(e, d_poses, d_inv_dist, true, want_jacobians != 0);
 }
 
+int pba_evaluate_states_device(pba_engine* e, int32_t n, const double* const* d_poses, const double* const* d_inv_dist,
+                               int32_t want_jacobians) {
+  if (!e || n < 0 || (n > 0 && (!d_poses || !d_inv_dist))) return fail(PBA_ERR_INVALID_ARGUMENT, "null states");
+  if (e->n_blocks <= 0) return fail(PBA_ERR_NOT_READY, "pba_set_blocks first");
+  for (int i = 0; i < n; ++i) {
+    if (!d_poses[i] || !d_inv_dist[i]) return fail(PBA_ERR_INVALID_ARGUMENT, "null state");
+    if (int rc = evaluate_at(e, d_poses[i], d_inv_dist[i], true, want_jacobians != 0)) return rc;
+  }
+  return PBA_OK;
+}
+
 int pba_enable_kernel_timing(pba_engine* e, int32_t enable) {
   if (!e) return fail(PBA_ERR_INVALID_ARGUMENT, "null engine");
   e->timing = enable != 0;

@@ -136,6 +136,7 @@ def lib():
         "pba_set_state_device": ([vp, vp, vp], C.c_int),
         "pba_evaluate": ([vp, i32], C.c_int),
         "pba_evaluate_state_device": ([vp, vp, vp, i32], C.c_int),
+        "pba_evaluate_states_device": ([vp, i32, vp, vp, i32], C.c_int),
         "pba_synchronize": ([vp], C.c_int),
         "pba_record_floats": ([vp], C.c_int),
         "pba_residuals_per_block": ([vp], C.c_int),
@@ -291,6 +292,19 @@ class Engine:
         program_evaluator.h:139-258): one launch for photometric engines."""
         _check(self._L.pba_evaluate_state_device(self._h, C.c_void_p(poses_ptr), C.c_void_p(rho_ptr),
                                                  int(bool(want_jacobians))), "pba_evaluate_state_device")
+        if sync:
+            self.synchronize()
+
+    def evaluate_states_device(self, poses_ptrs, rho_ptrs, want_jacobians: bool = True, sync: bool = True):
+        """n evaluations back to back, one per (poses, ρ) device-pointer pair, enqueued by one ABI call
+        (pba_evaluate_states_device); each adopts its state, the records hold the last one's evaluation."""
+        n = len(poses_ptrs)
+        if len(rho_ptrs) != n:
+            raise ValueError("one ρ array per pose array")
+        pa = (C.c_void_p * max(n, 1))(*poses_ptrs)
+        ra = (C.c_void_p * max(n, 1))(*rho_ptrs)
+        _check(self._L.pba_evaluate_states_device(self._h, n, pa, ra, int(bool(want_jacobians))),
+               "pba_evaluate_states_device")
         if sync:
             self.synchronize()
 

@@ -131,6 +131,31 @@ def test_deterministic_and_state_update():
     compare_records(0, pb.R, c, ref, vc, vref, projected_uv(pb_gt))
 
 
+@pytest.mark.parametrize("kind", [0, 1])
+def test_evaluate_states_device_batch(kind):
+    """pba_evaluate_states_device: n evaluations enqueued by one call equal n pba_evaluate_state_device calls — the
+    engine ends at the last state, its records are that state's, and an empty batch is a no-op."""
+    import torch
+
+    pb = synth.make_problem(kind=kind, n_frames=8, n_points=300, width=376, height=240, seed=43, border=10)
+    dev = torch.device("cuda", 0)
+    states = [(torch.from_numpy(np.ascontiguousarray(p)).to(dev), torch.from_numpy(np.ascontiguousarray(r)).to(dev))
+              for p, r in ((pb.poses, pb.rho), (pb.poses_gt, pb.rho_gt), (pb.poses, pb.rho_gt))]
+    with E.Engine(kind, 0) as eng:
+        eng.set_problem(pb)
+        eng.set_state(pb.poses, pb.rho)
+        eng.evaluate_states_device([], [], True)
+        eng.evaluate_states_device([p.data_ptr() for p, _ in states], [r.data_ptr() for _, r in states], True)
+        a, va = eng.records()
+        poses, rho = eng.get_state()
+        np.testing.assert_array_equal(poses, pb.poses)
+        np.testing.assert_array_equal(rho, pb.rho_gt)
+        eng.evaluate_state_device(states[-1][0].data_ptr(), states[-1][1].data_ptr(), True)
+        b, vb = eng.records()
+    np.testing.assert_array_equal(a, b)
+    np.testing.assert_array_equal(va, vb)
+
+
 @pytest.mark.parametrize("kind,model,extra_points", [(0, 0, 0), (0, 3, 0), (1, 0, 0), (0, 0, 40000)])
 def test_evaluate_state_device_adopts(kind, model, extra_points):
     """pba_evaluate_state_device (one launch for photometric engines: pairs formed in the block prologue, state
