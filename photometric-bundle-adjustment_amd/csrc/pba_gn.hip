@@ -1573,28 +1573,39 @@ __global__ void import_kernel(const ImportArgs a, double lambda, const double* _
 // ------------------------------------------------------------------------------------------------
 // skyline_solve_kernel: S δ = −g, S = LLᵀ in place (block skyline, right-looking), one workgroup
 // ------------------------------------------------------------------------------------------------
-__device__ inline bool chol6(const double* A, double* L) {
+// chol6 / inv_lower6: the 6×6 diagonal block's Cholesky factor and its inverse, on register arrays (fully unrolled)
+__device__ __forceinline__ bool chol6_reg(const double (&A)[36], double (&L)[36]) {
+  bool ok = true;
+#pragma unroll
   for (int i = 0; i < 36; ++i) L[i] = 0.0;
+#pragma unroll
   for (int j = 0; j < 6; ++j) {
     double s = A[j * 6 + j];
+#pragma unroll
     for (int k = 0; k < j; ++k) s -= L[j * 6 + k] * L[j * 6 + k];
-    if (!(s > 0.0)) return false;
-    const double ljj = sqrt(s);
+    ok = ok && s > 0.0;
+    const double ljj = sqrt(fmax(s, 1e-300));
     L[j * 6 + j] = ljj;
+#pragma unroll
     for (int i = j + 1; i < 6; ++i) {
       double t = A[i * 6 + j];
+#pragma unroll
       for (int k = 0; k < j; ++k) t -= L[i * 6 + k] * L[j * 6 + k];
       L[i * 6 + j] = t / ljj;
     }
   }
-  return true;
+  return ok;
 }
-__device__ inline void inv_lower6(const double* L, double* Li) {
+__device__ __forceinline__ void inv_lower6_reg(const double (&L)[36], double (&Li)[36]) {
+#pragma unroll
   for (int i = 0; i < 36; ++i) Li[i] = 0.0;
+#pragma unroll
   for (int c = 0; c < 6; ++c) {
     Li[c * 6 + c] = 1.0 / L[c * 6 + c];
+#pragma unroll
     for (int r = c + 1; r < 6; ++r) {
       double s = 0.0;
+#pragma unroll
       for (int k = c; k < r; ++k) s += L[r * 6 + k] * Li[k * 6 + c];
       Li[r * 6 + c] = -s / L[r * 6 + r];
     }
@@ -1611,6 +1622,8 @@ struct SolveArgs {
   double* x;
   int* status;
   int N;
+  const int* cptr;   // column k's profile rows crows[cptr[k] … cptr[k+1]) (every i > k with first(i) ≤ k, in order)
+  const int* crows;
 };
 
 __device__ __forceinline__ long long sky_off(const SolveArgs& a, int i, int j) {  // block (i, j), j ≥ first(i)
@@ -1626,9 +1639,20 @@ __global__ __launch_bounds__(256) void skyline_solve_kernel(const SolveArgs a) {
     const long long okk = sky_off(a, k, k);
     if (tid < 36) sA[tid] = a.S[okk + tid];
     __syncthreads();
-    if (tid == 0) {
-      if (!chol6(sA, sL)) s_fail = k + 1;
-      else inv_lower6(sL, sLi);
+    if (tid == 0) {  // in registers: the LDS-pointer forms' dependent LDS round trips were most of a column's time
+      double A[36], L[36], Li[36];
+#pragma unroll
+      for (int q = 0; q < 36; ++q) A[q] = sA[q];
+      if (!chol6_reg(A, L)) {
+        s_fail = k + 1;
+      } else {
+        inv_lower6_reg(L, Li);
+#pragma unroll
+        for (int q = 0; q < 36; ++q) {
+          sL[q] = L[q];
+          sLi[q] = Li[q];
+        }
+      }
     }
     __syncthreads();
     if (s_fail) {
@@ -1639,15 +1663,18 @@ __global__ __launch_bounds__(256) void skyline_solve_kernel(const SolveArgs a) {
       a.S[okk + tid] = sL[tid];
       a.Linv[(long long)k * 36 + tid] = sLi[tid];
     }
-    const int lk = a.last[k];
+    // column k's profile rows: the band below the diagonal and, with free intrinsics, the dense border rows — walking
+    // (k, last(k)] instead enumerated every row pair up to the border, O(N²) per column (C3 with free intrinsics: 0.7 s
+    // per solve)
+    const int c0 = a.cptr[k], na = a.cptr[k + 1] - c0;
+    const int* rows = a.crows + c0;
     // column panel L_ik = A_ik · L_kk⁻ᵀ, 7 blocks per pass (read all, barrier, write)
-    for (int i0 = k + 1; i0 <= lk; i0 += 7) {
+    for (int i0 = 0; i0 < na; i0 += 7) {
       double val = 0.0;
       long long dst = -1;
-      const int idx = tid;
-      const int i = i0 + idx / 36;
-      if (idx < 252 && i <= lk && a.first[i] <= k) {
-        const int e = idx % 36, r = e / 6, c = e % 6;
+      const int li = i0 + tid / 36;
+      if (tid < 252 && li < na) {
+        const int i = rows[li], e = tid % 36, r = e / 6, c = e % 6;
         const long long o = sky_off(a, i, k);
         for (int m = 0; m <= c; ++m) val += a.S[o + r * 6 + m] * sLi[c * 6 + m];
         dst = o + e;
@@ -1657,16 +1684,14 @@ __global__ __launch_bounds__(256) void skyline_solve_kernel(const SolveArgs a) {
       __threadfence_block();
       __syncthreads();
     }
-    // trailing update A_ij −= L_ik L_jkᵀ for k < j ≤ i ≤ last(k)
-    const int nk = lk - k;
-    const int npairs = nk * (nk + 1) / 2;
+    // trailing update A_ij −= L_ik L_jkᵀ over the pairs of the column's rows (i ≥ j)
+    const int npairs = na * (na + 1) / 2;
     for (int idx = tid; idx < npairs * 36; idx += 256) {
       const int pidx = idx / 36, e = idx % 36, r = e / 6, c = e % 6;
       int ii = 0;  // decode lower-triangular pair index → (ii ≥ jj)
       while ((ii + 1) * (ii + 2) / 2 <= pidx) ++ii;
       const int jj = pidx - ii * (ii + 1) / 2;
-      const int i = k + 1 + ii, j = k + 1 + jj;
-      if (a.first[i] > k || a.first[j] > k) continue;
+      const int i = rows[ii], j = rows[jj];
       const long long oi = sky_off(a, i, k), oj = sky_off(a, j, k);
       double s = 0.0;
       for (int m = 0; m < 6; ++m) s += a.S[oi + r * 6 + m] * a.S[oj + c * 6 + m];
@@ -1688,10 +1713,9 @@ __global__ __launch_bounds__(256) void skyline_solve_kernel(const SolveArgs a) {
     }
     __syncthreads();
     if (tid < 6) a.x[6 * k + tid] = yk[tid];
-    const int lk = a.last[k];
-    for (int idx = tid; idx < (lk - k) * 6; idx += 256) {
-      const int i = k + 1 + idx / 6, r = idx % 6;
-      if (a.first[i] > k) continue;
+    const int c0 = a.cptr[k], na = a.cptr[k + 1] - c0;
+    for (int idx = tid; idx < na * 6; idx += 256) {
+      const int i = a.crows[c0 + idx / 6], r = idx % 6;
       const long long o = sky_off(a, i, k);
       double s = 0.0;
       for (int m = 0; m < 6; ++m) s += a.S[o + r * 6 + m] * yk[m];
@@ -1705,8 +1729,8 @@ __global__ __launch_bounds__(256) void skyline_solve_kernel(const SolveArgs a) {
     __shared__ double tk[6];
     if (tid < 6) {
       double s = a.x[6 * k + tid];
-      for (int i = k + 1; i <= a.last[k]; ++i) {
-        if (a.first[i] > k) continue;
+      for (int q = a.cptr[k]; q < a.cptr[k + 1]; ++q) {
+        const int i = a.crows[q];
         const long long o = sky_off(a, i, k);
         for (int m = 0; m < 6; ++m) s -= a.S[o + m * 6 + tid] * a.x[6 * i + m];
       }
@@ -3084,87 +3108,38 @@ struct IntrBorderArgs {
   int nf, nc;
 };
 
-// Σ_b [h_b = x] J_h(b)ᵀJ_ρ(b) + [t_b = x] J_t(b)ᵀJ_ρ(b), column j (a point's W for keyframe x), or, for a camera
-// column (x < 0: camera −x − 1), Σ_b [camera of t_b = c] W_i(b)[j]: over the point's GN blocks in order.
-__device__ __forceinline__ double point_w(const IntrBorderArgs& a, int4 pr, int x, int j) {
-  double w = 0.0;
-  for (int b = pr.x; b < pr.x + pr.y; ++b) {
-    const double* B = a.ib + (long long)b * kIbStride;
-    if (x < 0) {
-      if (a.ib_cam[b] == -x - 1) w += B[kIbWi + j];
-    } else {
-      const int4 r = a.ib_rec[b];
-      if (r.z == x) w += B[kIbJh + j] * B[kIbJr] + B[kIbJh + 6 + j] * B[kIbJr + 1];
-      if (r.w == x) w += B[kIbJt + j] * B[kIbJr] + B[kIbJt + 6 + j] * B[kIbJr + 1];
-    }
-  }
-  return w;
+// Element t of border row `row` (system frame P = nf + row): t < (P + 1)·36 → entry (r, cc) of block (P, y = t / 36) of
+// the skyline system; t = nfs·36 … nfs·36 + 5 → g of P.  The keyframe blocks (P, x < nf) and the camera blocks (P, y ≥ nf)
+// get direct − Schur terms, + λ·clamp(diag) on the diagonal (the direct part is Ceres' LM diagonal), identity pads, and
+// — constant frames / unobserved cameras — identity rows and columns, as assemble_kernel.  border_store writes element t
+// from its two totals (direct, Schur).
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m, 64);
+  return v;
 }
-
-// Grid (x: the row's elements, y: border row 0 … 2nc − 1): lane t < (P + 1)·36 → element (r, cc) of block (P, y = t / 36)
-// of the skyline system (P = nf + row); lanes nfs·36 … nfs·36 + 5 → g of P.  The keyframe blocks (P, x < nf) and the
-// camera blocks (P, y ≥ nf) get direct − Schur terms, + λ·clamp(diag) on the diagonal (the direct part is Ceres' LM
-// diagonal), identity pads, and — constant frames / unobserved cameras — identity rows and columns, as assemble_kernel.
-__global__ __launch_bounds__(256) void intr_border_kernel(const IntrBorderArgs a, double lambda) {
-  const LmView lv = lm_view(a.lm);
-  lambda = lm_lambda(lv, lambda);
-  const int row = blockIdx.y, P = a.nf + row, nfs = a.nf + 2 * a.nc, nu = a.nf + a.nc;
-  const int c = row >> 1, h = row & 1;
-  const int t = blockIdx.x * blockDim.x + threadIdx.x;
-  auto inv_of = [&](int gp) {
-    const double H = a.pt_data[(long long)gp * 8];
-    const double Hd = H + lambda * fmin(fmax(H, 1e-6), 1e32);
-    return Hd > 0.0 ? 1.0 / Hd : 0.0;
-  };
-  if (t >= nfs * 36) {  // the gradient of P
-    const int r = t - nfs * 36, d = 6 * h + r;
-    if (r >= 6) return;
-    double dir = 0.0, sch = 0.0;
-    if (d < 8) {
-      const int L = c * nu + a.nf + c;
-      for (int q = a.bptr[L]; q < a.bptr[L + 1]; ++q) {
-        const double* B = a.ib + (long long)a.blist[q] * kIbStride;
-        dir += B[kIbJi + d] * B[kIbR] + B[kIbJi + 8 + d] * B[kIbR + 1];
-      }
-      for (int q = a.pptr[L]; q < a.pptr[L + 1]; ++q) {
-        const int gp = a.plist[q];
-        sch += inv_of(gp) * point_w(a, a.pt_rec[gp], -c - 1, d) * a.pt_data[(long long)gp * 8 + 1];
-      }
-    }
+__device__ __forceinline__ double border_inv(const IntrBorderArgs& a, int gp, double lambda) {
+  const double H = a.pt_data[(long long)gp * 8];
+  const double Hd = H + lambda * fmin(fmax(H, 1e-6), 1e32);
+  return Hd > 0.0 ? 1.0 / Hd : 0.0;
+}
+__device__ __forceinline__ void border_store(const IntrBorderArgs& a, double lambda, int row, int t, double dir,
+                                             double sch) {
+  const int P = a.nf + row, nfs = a.nf + 2 * a.nc, h = row & 1;
+  if (t >= nfs * 36) {
+    const int r = t - nfs * 36;
     const bool fx = a.fixed[P] != 0;
     a.g[6 * P + r] = fx ? 0.0 : dir - sch;
     a.g_dir[6 * P + r] = fx ? 0.0 : dir;
     if (fx) a.Ddiag[6 * P + r] = 0.0;
     return;
   }
-  if (t >= (P + 1) * 36) return;
   const int y = t / 36, e = t % 36, r = e / 6, cc = e % 6, d = 6 * h + r;
   const bool cam = y >= a.nf;
-  const int c2 = cam ? (y - a.nf) >> 1 : 0, d2 = cam ? 6 * ((y - a.nf) & 1) + cc : cc;
-  double dir = 0.0, sch = 0.0;
-  if (d < 8 && d2 < 8) {
-    const int L = c * nu + (cam ? a.nf + c2 : y);
-    for (int q = a.bptr[L]; q < a.bptr[L + 1]; ++q) {
-      const int b = a.blist[q];
-      const double* B = a.ib + (long long)b * kIbStride;
-      double c0, c1;  // column d2 / cc of the block's Jacobian for y
-      if (cam) {
-        c0 = B[kIbJi + d2];
-        c1 = B[kIbJi + 8 + d2];
-      } else {
-        const int4 rr = a.ib_rec[b];
-        c0 = rr.z == y ? B[kIbJh + cc] : B[kIbJt + cc];
-        c1 = rr.z == y ? B[kIbJh + 6 + cc] : B[kIbJt + 6 + cc];
-      }
-      dir += B[kIbJi + d] * c0 + B[kIbJi + 8 + d] * c1;
-    }
-    for (int q = a.pptr[L]; q < a.pptr[L + 1]; ++q) {
-      const int gp = a.plist[q];
-      const int4 pr = a.pt_rec[gp];
-      sch += inv_of(gp) * point_w(a, pr, -c - 1, d) * point_w(a, pr, cam ? -c2 - 1 : y, d2);
-    }
-  } else if (y == P && r == cc) {
-    dir = 1.0;  // pad
+  const int d2 = cam ? 6 * ((y - a.nf) & 1) + cc : cc;
+  if (d >= 8 || d2 >= 8) {  // pad
+    dir = (y == P && r == cc) ? 1.0 : 0.0;
+    sch = 0.0;
   }
   double val = dir - sch;
   if (a.fixed[P] || a.fixed[y]) {
@@ -3175,6 +3150,189 @@ __global__ __launch_bounds__(256) void intr_border_kernel(const IntrBorderArgs a
     val += lambda * D;
   }
   a.S[((long long)a.sky_row[P] + (y - a.sky_first[P])) * 36 + e] = val;
+}
+
+// The keyframe blocks (P, y < nf): ONE WAVE per block (grid x: y, 4 per workgroup; y: camera c; NR = 6 → border row
+// 2c, NR = 2 → row 2c + 1, whose frame holds intrinsics 6, 7 and four pads), all 6·NR live entries at once — a lane
+// takes every 64th entry of the block's lists (the keyframe's blocks and points seen by the camera), the wave adds its
+// lanes' sums by xor butterflies (a fixed order) and lane e stores entry e.  (One wave per ENTRY re-walked each list 36
+// times: 0.5 ms per launch at C3.)
+template <int NR>
+__global__ __launch_bounds__(256) void intr_border_kernel(const IntrBorderArgs a, double lambda) {
+  lambda = lm_lambda(lm_view(a.lm), lambda);
+  const int c = blockIdx.y, row = 2 * c + (NR == 6 ? 0 : 1), h = row & 1, lane = threadIdx.x & 63;
+  const int y = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
+  if (y >= a.nf) return;
+  const int L = c * (a.nf + a.nc) + y;
+  double dir[NR][6], sch[NR][6];
+#pragma unroll
+  for (int r = 0; r < NR; ++r)
+#pragma unroll
+    for (int cc = 0; cc < 6; ++cc) dir[r][cc] = sch[r][cc] = 0.0;
+  for (int q = a.bptr[L] + lane; q < a.bptr[L + 1]; q += 64) {
+    const int b = a.blist[q];
+    const double* B = a.ib + (long long)b * kIbStride;
+    const double* Jc = B + (a.ib_rec[b].z == y ? kIbJh : kIbJt);
+    double c0[6], c1[6];
+#pragma unroll
+    for (int cc = 0; cc < 6; ++cc) {
+      c0[cc] = Jc[cc];
+      c1[cc] = Jc[6 + cc];
+    }
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+      const double j0 = B[kIbJi + 6 * h + r], j1 = B[kIbJi + 8 + 6 * h + r];
+#pragma unroll
+      for (int cc = 0; cc < 6; ++cc) dir[r][cc] += j0 * c0[cc] + j1 * c1[cc];
+    }
+  }
+  for (int q = a.pptr[L] + lane; q < a.pptr[L + 1]; q += 64) {
+    const int gp = a.plist[q];
+    const int4 pr = a.pt_rec[gp];
+    double wc[NR], wy[6];  // W of the point for the camera's columns 6h + r (Σ W_i over its blocks
+                           // seen by c) and for keyframe y (Σ J_h / J_t ᵀJ_ρ over its blocks hosted / targeted by y)
+#pragma unroll
+    for (int r = 0; r < NR; ++r) wc[r] = 0.0;
+#pragma unroll
+    for (int cc = 0; cc < 6; ++cc) wy[cc] = 0.0;
+    for (int b = pr.x; b < pr.x + pr.y; ++b) {
+      const double* B = a.ib + (long long)b * kIbStride;
+      if (a.ib_cam[b] == c) {
+#pragma unroll
+        for (int r = 0; r < NR; ++r) wc[r] += B[kIbWi + 6 * h + r];
+      }
+      const int4 rr = a.ib_rec[b];
+      if (rr.z == y) {
+#pragma unroll
+        for (int cc = 0; cc < 6; ++cc) wy[cc] += B[kIbJh + cc] * B[kIbJr] + B[kIbJh + 6 + cc] * B[kIbJr + 1];
+      }
+      if (rr.w == y) {
+#pragma unroll
+        for (int cc = 0; cc < 6; ++cc) wy[cc] += B[kIbJt + cc] * B[kIbJr] + B[kIbJt + 6 + cc] * B[kIbJr + 1];
+      }
+    }
+    const double inv = border_inv(a, gp, lambda);
+#pragma unroll
+    for (int r = 0; r < NR; ++r)
+#pragma unroll
+      for (int cc = 0; cc < 6; ++cc) sch[r][cc] += inv * wc[r] * wy[cc];
+  }
+  double vd = 0.0, vs = 0.0;
+#pragma unroll
+  for (int r = 0; r < NR; ++r)
+#pragma unroll
+    for (int cc = 0; cc < 6; ++cc) {
+      const double d = wave_sum(dir[r][cc]), sc = wave_sum(sch[r][cc]);
+      vd = lane == r * 6 + cc ? d : vd;
+      vs = lane == r * 6 + cc ? sc : vs;
+    }
+  if (lane < 36) border_store(a, lambda, row, y * 36 + lane, vd, vs);
+}
+
+// The camera blocks (P, y ≥ nf) and the gradient of P: their lists hold ALL of a camera's blocks and points (80k / 20k at
+// C3), so each block is split over kIbSplit workgroups (grid x: yb — camera block y = nf + yb for yb < 2nc, the gradient
+// for yb = 2nc; y: camera c, NR as intr_border_kernel; z: split s), thread k of split s taking list entries k + 256·s,
+// + 256·kIbSplit, …, all 6·NR entries at once; the workgroup's totals (wave butterflies, then its four waves in order)
+// go to part, and intr_border_fin_kernel adds the kIbSplit totals in order — a fixed order end to end.
+constexpr int kIbSplit = 32;
+template <int NR>
+__global__ __launch_bounds__(256) void intr_border_cam_kernel(const IntrBorderArgs a, double lambda, double2* part) {
+  __shared__ double2 s_w[4][36];
+  lambda = lm_lambda(lm_view(a.lm), lambda);
+  const int c = blockIdx.y, row = 2 * c + (NR == 6 ? 0 : 1), h = row & 1, yb = blockIdx.x, nb = 2 * a.nc + 1;
+  const bool grad = yb == 2 * a.nc;
+  const int y = a.nf + yb;
+  if (!grad && y > a.nf + row) return;  // above the diagonal: not stored (uniform per workgroup)
+  const int c2 = yb >> 1, L = c * (a.nf + a.nc) + a.nf + (grad ? c : c2), o2 = 6 * (yb & 1);
+  const int q0 = threadIdx.x + 256 * blockIdx.z, dq = 256 * kIbSplit;
+  double dir[NR][6], sch[NR][6];
+#pragma unroll
+  for (int r = 0; r < NR; ++r)
+#pragma unroll
+    for (int cc = 0; cc < 6; ++cc) dir[r][cc] = sch[r][cc] = 0.0;
+  for (int q = a.bptr[L] + q0; q < a.bptr[L + 1]; q += dq) {
+    const double* B = a.ib + (long long)a.blist[q] * kIbStride;
+    double c0[6], c1[6];  // the gradient: the residual; a camera block: intrinsics columns o2 … o2 + 5 (< 8 used)
+#pragma unroll
+    for (int cc = 0; cc < 6; ++cc) {
+      c0[cc] = grad ? B[kIbR] : B[kIbJi + min(o2 + cc, 7)];
+      c1[cc] = grad ? B[kIbR + 1] : B[kIbJi + 8 + min(o2 + cc, 7)];
+    }
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+      const double j0 = B[kIbJi + 6 * h + r], j1 = B[kIbJi + 8 + 6 * h + r];
+#pragma unroll
+      for (int cc = 0; cc < 6; ++cc) dir[r][cc] += j0 * c0[cc] + j1 * c1[cc];
+    }
+  }
+  for (int q = a.pptr[L] + q0; q < a.pptr[L + 1]; q += dq) {
+    const int gp = a.plist[q];
+    const int4 pr = a.pt_rec[gp];
+    double wc[NR], wy[6];  // W of the point for camera c's columns 6h + r and camera c2's o2 + cc
+#pragma unroll
+    for (int r = 0; r < NR; ++r) wc[r] = 0.0;
+#pragma unroll
+    for (int cc = 0; cc < 6; ++cc) wy[cc] = 0.0;
+    for (int b = pr.x; b < pr.x + pr.y; ++b) {
+      const double* B = a.ib + (long long)b * kIbStride;
+      const int cb = a.ib_cam[b];
+      if (cb == c) {
+#pragma unroll
+        for (int r = 0; r < NR; ++r) wc[r] += B[kIbWi + 6 * h + r];
+      }
+      if (!grad && cb == c2) {
+#pragma unroll
+        for (int cc = 0; cc < 6; ++cc) wy[cc] += B[kIbWi + min(o2 + cc, 7)];
+      }
+    }
+    const double inv = border_inv(a, gp, lambda);
+    if (grad) {
+      const double gr = a.pt_data[(long long)gp * 8 + 1];
+#pragma unroll
+      for (int cc = 0; cc < 6; ++cc) wy[cc] = gr;
+    }
+#pragma unroll
+    for (int r = 0; r < NR; ++r)
+#pragma unroll
+      for (int cc = 0; cc < 6; ++cc) sch[r][cc] += inv * wc[r] * wy[cc];
+  }
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  double vd = 0.0, vs = 0.0;
+#pragma unroll
+  for (int r = 0; r < NR; ++r)
+#pragma unroll
+    for (int cc = 0; cc < 6; ++cc) {
+      const double d = wave_sum(dir[r][cc]), sc = wave_sum(sch[r][cc]);
+      vd = lane == r * 6 + cc ? d : vd;
+      vs = lane == r * 6 + cc ? sc : vs;
+    }
+  if (lane < 36) s_w[w][lane] = make_double2(vd, vs);
+  __syncthreads();
+  if (threadIdx.x >= 36) return;
+  double2 t = s_w[0][threadIdx.x];
+  for (int k = 1; k < 4; ++k) {
+    t.x += s_w[k][threadIdx.x].x;
+    t.y += s_w[k][threadIdx.x].y;
+  }
+  part[(((long long)row * nb + yb) * kIbSplit + blockIdx.z) * 36 + threadIdx.x] = t;
+}
+// One thread per (border row, yb, entry e): the kIbSplit totals in order, then border_store (the gradient: e < 6 →
+// g[6P + e], column 0 of the entries).
+__global__ __launch_bounds__(256) void intr_border_fin_kernel(const IntrBorderArgs a, double lambda,
+                                                              const double2* part) {
+  lambda = lm_lambda(lm_view(a.lm), lambda);
+  const int nb = 2 * a.nc + 1, i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= 2 * a.nc * nb * 36) return;
+  const int e = i % 36, yb = (i / 36) % nb, row = i / (36 * nb);
+  const bool grad = yb == 2 * a.nc;
+  if (grad ? (e % 6 != 0) : (a.nf + yb > a.nf + row)) return;
+  const double2* pp = part + (((long long)row * nb + yb) * kIbSplit) * 36 + e;
+  double2 w = pp[0];
+  for (int k = 1; k < kIbSplit; ++k) {
+    w.x += pp[36 * k].x;
+    w.y += pp[36 * k].y;
+  }
+  border_store(a, lambda, row, grad ? (a.nf + 2 * a.nc) * 36 + e / 6 : (a.nf + yb) * 36 + e, w.x, w.y);
 }
 
 // The candidate intrinsics become the state (after an accepted trial; lm == nullptr: always), fp64 records and fp32 copy.
@@ -3975,6 +4133,17 @@ int gn_prepare(pba_engine* e) {
   for (int k = 0; k < nfs; ++k) last[k] = k;
   for (int i = 0; i < nfs; ++i)
     for (int k = first[i]; k < i; ++k) last[k] = std::max(last[k], i);
+  std::vector<int> ccptr(nfs + 1, 0), ccrows;  // the rows of each column's profile, in order
+  {
+    std::vector<std::vector<int>> col(nfs);
+    for (int i = 0; i < nfs; ++i)
+      for (int k = first[i]; k < i; ++k) col[k].push_back(i);
+    for (int k = 0; k < nfs; ++k) {
+      ccptr[k + 1] = ccptr[k] + (int)col[k].size();
+      ccrows.insert(ccrows.end(), col[k].begin(), col[k].end());
+    }
+    if (ccrows.empty()) ccrows.push_back(0);
+  }
   std::vector<int> cptr(G.n_sky + 1, 0), bi(G.n_sky), bj(G.n_sky);
   std::vector<std::vector<int2>> per(G.n_sky);
   for (int i = 0; i < nfs; ++i)
@@ -4049,6 +4218,7 @@ int gn_prepare(pba_engine* e) {
     PBA_HIP(G.ib_pptr.upload(pp, st0));
     PBA_HIP(G.ib_plist.upload(pflat, st0));
     PBA_HIP(G.ib_data.resize((size_t)nb * kIbStride));
+    PBA_HIP(G.ib_part.resize((size_t)2 * nc * (2 * nc + 1) * kIbSplit * 36));
     PBA_HIP(G.intr_new_d.resize((size_t)kCamD * nc));
     PBA_HIP(G.intr_new_f.resize((size_t)8 * nc));
     // the candidate records start as the state's (their unprojection half is never read: hosts unproject with the cameras)
@@ -4124,6 +4294,8 @@ int gn_prepare(pba_engine* e) {
   PBA_HIP(G.sky_first.upload(first, st));
   PBA_HIP(G.sky_row.upload(rowp, st));
   PBA_HIP(G.sky_last.upload(last, st));
+  PBA_HIP(G.sky_colptr.upload(ccptr, st));
+  PBA_HIP(G.sky_colrows.upload(ccrows, st));
   PBA_HIP(G.sky_cptr.upload(cptr, st));
   PBA_HIP(G.sky_contrib.upload(flat.empty() ? std::vector<int2>{make_int2(0, 0)} : flat, st));
   PBA_HIP(G.g_cptr.upload(gptr, st));
@@ -4531,13 +4703,19 @@ int enqueue_solve(pba_engine* e, double lambda, const double* lm = nullptr, bool
     IntrBorderArgs ba{G.ib_data.p, G.ib_rec.p, G.ib_cam.p, G.pt_rec.p, G.pt_data.p, G.ib_bptr.p, G.ib_blist.p,
                       G.ib_pptr.p, G.ib_plist.p, G.sky_first.p, G.sky_row.p, G.fixed.p, lm ? lm : G.lm_idle.p, G.S.p,
                       G.g.p, G.g_dir.p, G.Ddiag.p, nf, G.nc_sys};
-    intr_border_kernel<<<dim3((nfs * 36 + 6 + 255) / 256, 2 * G.nc_sys), 256, 0, e->stream>>>(ba, lambda);
+    const int nb = 2 * G.nc_sys + 1;
+    intr_border_kernel<6><<<dim3((nf + 3) / 4, G.nc_sys), 256, 0, e->stream>>>(ba, lambda);
+    intr_border_kernel<2><<<dim3((nf + 3) / 4, G.nc_sys), 256, 0, e->stream>>>(ba, lambda);
+    intr_border_cam_kernel<6><<<dim3(nb, G.nc_sys, kIbSplit), 256, 0, e->stream>>>(ba, lambda, G.ib_part.p);
+    intr_border_cam_kernel<2><<<dim3(nb, G.nc_sys, kIbSplit), 256, 0, e->stream>>>(ba, lambda, G.ib_part.p);
+    intr_border_fin_kernel<<<(2 * G.nc_sys * nb * 36 + 255) / 256, 256, 0, e->stream>>>(ba, lambda, G.ib_part.p);
   }
   if (G.band_kernel) {
     if (int rc = band_solve(e, !direct)) return rc;
   } else {
     PBA_HIP(hipMemcpyAsync(G.L.p, G.S.p, sizeof(double) * 36 * (size_t)G.n_sky, hipMemcpyDeviceToDevice, e->stream));
-    SolveArgs so{G.L.p, G.sky_first.p, G.sky_row.p, G.sky_last.p, G.g.p, G.Linv.p, G.x.p, G.status.p, nfs};
+    SolveArgs so{G.L.p, G.sky_first.p, G.sky_row.p, G.sky_last.p, G.g.p, G.Linv.p, G.x.p, G.status.p, nfs,
+                 G.sky_colptr.p, G.sky_colrows.p};
     skyline_solve_kernel<<<1, 256, 0, e->stream>>>(so);
   }
   PBA_HIP(hipGetLastError());

@@ -741,6 +741,7 @@ struct GnData {
   DevBuf<int2> sky_contrib, g_contrib;
   DevBuf<int> sky_blk_i, sky_blk_j;  // skyline block → (row pose, column pose)
   DevBuf<int> sky_diag, sky_off;     // the diagonal skyline blocks, the others (assemble_kernel's thread ranges)
+  DevBuf<int> sky_colptr, sky_colrows;  // per column k, the rows i > k of the profile (first(i) ≤ k): skyline solve
   int n_sky_diag = 0;
   DevBuf<double> S, L, Sband, Lband, g, g_dir, Ddiag, Linv, x;  // skyline system, its factor, rhs, direct gradient, LM diagonal, L_kk⁻¹, step
   DevBuf<uint8_t> fixed;
@@ -771,6 +772,7 @@ struct GnData {
   DevBuf<int> ib_bptr, ib_blist;  // border unit pair (camera c, unit u) → GN blocks of its direct terms (CSR)
   DevBuf<int> ib_pptr, ib_plist;  // … → GN points of its Schur terms (CSR); unit u < nf: frame u, else camera u − nf
   DevBuf<int> ib_cam;           // GN block → its target's camera
+  DevBuf<double2> ib_part;      // intr_border_cam_kernel's per-workgroup totals (dir, Schur) per camera element
   DevBuf<double> intr_new_d;    // candidate intrinsics: camera records (kCamD doubles, projection part) …
   DevBuf<float> intr_new_f;     // … and their fp32 copy (8 per camera)
   double* lm_host_d = nullptr;  // lm_h's device address
