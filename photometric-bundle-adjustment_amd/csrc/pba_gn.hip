@@ -1748,24 +1748,6 @@ __global__ __launch_bounds__(256) void skyline_solve_kernel(const SolveArgs a) {
   if (tid == 0) *a.status = 0;
 }
 
-// ------------------------------------------------------------------------------------------------
-// band_solve_kernel<B>: the same factorisation when every block row satisfies first(i) ≥ i − B (the
-// structure of windowed/sequential BA — C3/C4 have B = 4).  The assembly also writes S in dense band
-// layout (block c of row i = column i − B + c), so the next block row's address needs no indirection.
-// The active window of the factor (block rows k..k+B) lives in LDS as a ring; block row k+B+2 is
-// prefetched into registers two steps ahead.  Per step: one lane factors the 6×6 diagonal block
-// (reciprocal pivots, no inverse), B·6 lanes solve the column panel L_ik = A_ik L_kk⁻ᵀ row by row, the
-// trailing triangle is updated in parallel, and forward substitution is fused in.  Finished rows of L and
-// the reciprocal pivots go to global memory for the backward pass, which prefetches one step ahead.
-// ------------------------------------------------------------------------------------------------
-struct BandArgs {
-  const double* Sband;  // N rows × ((B+1)·36 + 6): blocks of columns i−B..i, then g_i
-  double* Lcol;         // N column records × (B·36 + 48): L_(k+q),k for q = 1..B | L_kk | 1/pivots | y_k
-  double* x;            // the step δ_poses
-  int* status;
-  int N;
-};
-
 // rsqrt_nr (pba_device.h): hardware v_rsq_f64 seed + two Newton steps — the pivot is on the solver's
 // serial critical path; this is ~3x shorter than sqrt() + division.
 __device__ inline bool chol6_rcp(double* A, double* invd) {  // in place, lower; returns reciprocal pivots
@@ -1792,6 +1774,311 @@ __device__ inline bool chol6_rcp(double* A, double* invd) {  // in place, lower;
     for (int j = i + 1; j < 6; ++j) A[i * 6 + j] = 0.0;
   return true;
 }
+
+// ------------------------------------------------------------------------------------------------
+// front_solve_kernel: the same factorisation and solve with the ACTIVE FRONT in LDS (one workgroup)
+// ------------------------------------------------------------------------------------------------
+// Right-looking block Cholesky touches, at column k, only the blocks among {k} ∪ rows(k), rows(k) = {i > k : first(i) ≤ k}
+// — the front.  It moves by one row per column: k leaves, the rows with first(i) = k + 1 enter with their blocks fresh
+// from S (no earlier column touched them).  gn_prepare gives every row a static LDS slot (a row admitted for column k + 1
+// never takes a slot in use at column k) and writes per column a record: the slots, row indices and factor-block
+// indices of rows(k), and the fresh blocks of the next column's admissions (source skyline block → front position
+// slot_hi·F + slot_lo).  skyline_solve_kernel walks the same factorisation through global memory, a dependent L2
+// round trip per phase (≈ 9 µs per column); here the front, the forward vector and the records live in LDS and the
+// next column's fresh blocks and record are loaded while this column is factored.  Free intrinsics make the profile a
+// band plus 2·nc dense border rows: F = K + 1 + 2nc slots (C3/C4: 7).
+// Every lane issues its share of the global loads of the record two columns ahead and of the next column's fresh
+// blocks (backward: its staged factor blocks) at a column's start and stores them to LDS at its end.  (A dedicated
+// loader wave measured slower: the compiler's conservative waits then stalled that wave at the barriers.)
+// Forward (3 barriers per column): one lane factors L_kk (reciprocal pivots) and y_k = L_kk⁻¹ v_k; 6·|rows(k)| lanes
+// form L_ik = A_ik L_kk⁻ᵀ row by row (to LDS, to L, v_i −= L_ik y_k); the trailing pairs A_ij −= L_ik L_jkᵀ.
+// Backward (2 barriers per column): 6·|rows(k)| lanes form the products L_ikᵀ x_i, one lane adds them in order and
+// solves x_k = L_kk⁻ᵀ (y_k − Σ_i L_ikᵀ x_i).
+constexpr int kFrontHdr = 3;
+struct FrontArgs {
+  const double* S;      // the assembled skyline system
+  const double* g;
+  double* L;            // the factor's off-diagonal blocks (skyline layout)
+  double* lrec;         // per column: L_kk | 1/pivots | y_k
+  const int* rec;       // per column: kFrontHdr + 3·fm + 2·mf ints
+  const int2* init;     // the rows of column 0's front: (source block, front position)
+  double* x;
+  int* status;
+  int N, F, fm, mf, R, n_init;
+};
+constexpr int kFrontPf = 4;  // doubles per lane per column: fresh blocks (mf·36) / staged blocks (fm·36 + 48)
+constexpr int kFrontPr = 1;  // record ints per lane (R ≤ 256)
+
+__global__ __launch_bounds__(256) void front_solve_kernel(const FrontArgs a) {
+  extern __shared__ double front_lds[];
+  const int tid = threadIdx.x, N = a.N, F = a.F, fm = a.fm, mf = a.mf, R = a.R;
+  const int SB = fm * 36 + 48, ld = tid;
+  double* fr = front_lds;                                // F·F blocks: block (i ≥ j) at slot_i·F + slot_j
+  double* ys = fr + (size_t)F * F * 36;                  // v → y → x, 6 per row
+  double* stg = ys + 6 * N;                              // backward: 2 × SB
+  int* recb = reinterpret_cast<int*>(stg + 2 * SB);      // 3 × R: records k, k + 1, k + 2 (backward: k, k − 1, k − 2)
+  int* pairs = recb + 3 * R;                             // lower-triangle pair p → (ii << 16) | jj
+  __shared__ double sL[36], sd[6], sy[6], sp[6 * 32];
+  __shared__ int s_fail;
+#ifdef PBA_FRONT_STAMPS  // timing variant: per-phase wall-clock sums of lanes 0 and 64, written over x[0 … 19]
+  unsigned long long fts[10] = {}, ft0 = 0;
+#define FRONT_STAMP(i) { const unsigned long long t_ = wall_clock64(); if ((i) > 0) fts[(i) - 1] += t_ - ft0; ft0 = t_; }
+#else
+#define FRONT_STAMP(i)
+#endif
+  // the prefetch loads: unconditional (clamped addresses; the stores are guarded) — under a branch, the compiler waited
+  // for every load in flight at the first use of any
+  auto load_rec = [&](int k, int (&regs)[kFrontPr]) {
+#pragma unroll
+    for (int q = 0; q < kFrontPr; ++q)
+      regs[q] = a.rec[(long long)min(max(k, 0), N - 1) * R + min(ld + 256 * q, R - 1)];
+  };
+  auto store_rec = [&](int k, const int (&regs)[kFrontPr]) {
+#pragma unroll
+    for (int q = 0; q < kFrontPr; ++q)
+      if (ld + 256 * q < R) recb[(k % 3) * R + ld + 256 * q] = regs[q];
+  };
+  auto load_fresh = [&](const int* rk, double (&regs)[kFrontPf]) {  // the blocks column k admits for column k + 1
+    const int nfr = rk[2];
+    const int* fsrc = rk + kFrontHdr + 3 * fm;
+#pragma unroll
+    for (int q = 0; q < kFrontPf; ++q) {
+      const int idx = min(ld + 256 * q, max(nfr * 36 - 1, 0));
+      regs[q] = a.S[(long long)(nfr ? fsrc[idx / 36] : 0) * 36 + idx % 36];
+    }
+  };
+  if (tid == 0) s_fail = 0;
+  for (int t = tid; t < 6 * N; t += 256) ys[t] = -a.g[t];
+  for (int t = tid; t < a.n_init * 36; t += 256) {
+    const int2 q = a.init[t / 36];
+    fr[(long long)q.y * 36 + t % 36] = a.S[(long long)q.x * 36 + t % 36];
+  }
+  for (int t = tid; t < 2 * R; t += 256)
+    if (t / R < N) recb[t] = a.rec[t];
+  for (int p = tid; p < fm * (fm + 1) / 2; p += 256) {
+    int ii = 0;
+    while ((ii + 1) * (ii + 2) / 2 <= p) ++ii;
+    pairs[p] = (ii << 16) | (p - ii * (ii + 1) / 2);
+  }
+  __syncthreads();
+
+  // one column; cur holds its admissions (loaded during the previous column), nxt receives the next column's — the
+  // loop runs two columns per pass with the arrays swapped (no register copies)
+  auto column = [&](int k, double (&cur)[kFrontPf], double (&nxt)[kFrontPf]) -> bool {
+    const int* rk = recb + (k % 3) * R;
+    const int sk = rk[0], na = rk[1], nfr = rk[2];
+    const int* slots = rk + kFrontHdr;
+    const int* rows = slots + fm;
+    const int* gbl = rows + fm;
+    const int* fdst = gbl + fm + mf;
+    FRONT_STAMP(0);
+    int pr[kFrontPr];
+    load_rec(k + 2, pr);  // before the fresh loads: waiting for it must not wait for them
+    if (k + 1 < N) load_fresh(recb + ((k + 1) % 3) * R, nxt);
+    if (tid == 0) {
+      const double* Dk = fr + (long long)(sk * F + sk) * 36;
+      double A[36], d[6];
+#pragma unroll
+      for (int e = 0; e < 36; ++e) A[e] = Dk[e];
+      if (!chol6_rcp(A, d)) {
+        s_fail = k + 1;
+      } else {
+        double b[6];
+#pragma unroll
+        for (int r = 0; r < 6; ++r) b[r] = ys[6 * k + r];
+#pragma unroll
+        for (int c = 0; c < 6; ++c) {  // y_k = L_kk⁻¹ v_k
+          double t = b[c];
+#pragma unroll
+          for (int m = 0; m < c; ++m) t -= A[c * 6 + m] * b[m];
+          b[c] = t * d[c];
+        }
+#pragma unroll
+        for (int e = 0; e < 36; ++e) sL[e] = A[e];
+#pragma unroll
+        for (int r = 0; r < 6; ++r) {
+          sd[r] = d[r];
+          sy[r] = b[r];
+          ys[6 * k + r] = b[r];
+        }
+      }
+    }
+    FRONT_STAMP(1);
+    __syncthreads();
+    FRONT_STAMP(2);
+    if (s_fail) {
+      if (tid == 0) *a.status = s_fail;
+      return false;
+    }
+    if (tid < na * 6) {  // panel row r of L_ik = A_ik L_kk⁻ᵀ; v_i −= L_ik y_k
+      const int li = tid / 6, r = tid % 6;
+      double* A = fr + (long long)(slots[li] * F + sk) * 36 + r * 6;
+      double X[6];
+#pragma unroll
+      for (int c = 0; c < 6; ++c) {
+        double t = A[c];
+#pragma unroll
+        for (int m = 0; m < c; ++m) t -= X[m] * sL[c * 6 + m];
+        X[c] = t * sd[c];
+      }
+      double* Lg = a.L + (long long)gbl[li] * 36 + r * 6;
+      double dv = 0.0;
+#pragma unroll
+      for (int c = 0; c < 6; ++c) {
+        A[c] = X[c];
+        Lg[c] = X[c];
+        dv += X[c] * sy[c];
+      }
+      ys[6 * rows[li] + r] -= dv;
+    } else if (tid >= 192 && tid < 240) {
+      const int e = tid - 192;
+      a.lrec[(long long)k * 48 + e] = e < 36 ? sL[e] : (e < 42 ? sd[e - 36] : sy[e - 42]);
+    }
+    FRONT_STAMP(3);
+    __syncthreads();
+    FRONT_STAMP(4);
+    const int np = na * (na + 1) / 2;  // trailing A_ij −= L_ik L_jkᵀ (i ≥ j in rows(k))
+    for (int idx = tid; idx < np * 36; idx += 256) {
+      const int pq = pairs[idx / 36], e = idx % 36, r = e / 6, c = e % 6;
+      const int si = slots[pq >> 16], sj = slots[pq & 0xffff];
+      const double* Li = fr + (long long)(si * F + sk) * 36 + r * 6;
+      const double* Lj = fr + (long long)(sj * F + sk) * 36 + c * 6;
+      double acc = 0.0;
+#pragma unroll
+      for (int m = 0; m < 6; ++m) acc += Li[m] * Lj[m];
+      fr[(long long)(si * F + sj) * 36 + e] -= acc;
+    }
+#pragma unroll
+    for (int q = 0; q < kFrontPf; ++q) {  // column k's admissions (slots unused at column k), the record of k + 2
+      const int idx = ld + 256 * q;
+      if (idx < nfr * 36) fr[(long long)fdst[idx / 36] * 36 + idx % 36] = cur[q];
+    }
+    if (k + 2 < N) store_rec(k + 2, pr);
+    FRONT_STAMP(5);
+    __syncthreads();
+    FRONT_STAMP(6);
+    return true;
+  };
+  double pf[kFrontPf], pfn[kFrontPf];
+  load_fresh(recb, pf);
+  for (int k = 0; k < N; k += 2) {
+    if (!column(k, pf, pfn)) return;
+    if (k + 1 < N && !column(k + 1, pfn, pf)) return;
+  }
+  __threadfence();
+  __syncthreads();
+
+  // backward: x_k = L_kk⁻ᵀ (y_k − Σ_i L_ikᵀ x_i); column k's blocks staged during column k + 1, loaded during k + 2
+  auto load_stage = [&](int k, const int* rk, double (&regs)[kFrontPf]) {
+    const int na = rk[1];
+    const int* gbl = rk + kFrontHdr + 2 * fm;
+#pragma unroll
+    for (int q = 0; q < kFrontPf; ++q) {  // unused stage entries hold any value
+      const int idx = ld + 256 * q;
+      const double* src = a.lrec;
+      if (k >= 0 && idx < na * 36) src = a.L + (long long)gbl[idx / 36] * 36 + idx % 36;
+      else if (k >= 0 && idx >= fm * 36 && idx < SB) src = a.lrec + (long long)k * 48 + idx - fm * 36;
+      regs[q] = *src;
+    }
+  };
+  auto store_stage = [&](int k, const double (&regs)[kFrontPf]) {
+#pragma unroll
+    for (int q = 0; q < kFrontPf; ++q)
+      if (ld + 256 * q < SB) stg[(k & 1) * SB + ld + 256 * q] = regs[q];
+  };
+  double pb[kFrontPf], pbn[kFrontPf];  // cur / nxt of bcolumn, swapped per column as the forward pass
+  for (int t = tid; t < 3 * R; t += 256) {
+    const int k = N - 1 - t / R;
+    if (k >= 0) recb[(k % 3) * R + t % R] = a.rec[(long long)k * R + t % R];
+  }
+  __syncthreads();
+  {
+    const int* rk = recb + ((N - 1) % 3) * R;
+    for (int t = tid; t < SB; t += 256) {
+      double v = 0.0;
+      if (t < rk[1] * 36) v = a.L[(long long)rk[kFrontHdr + 2 * fm + t / 36] * 36 + t % 36];
+      else if (t >= fm * 36) v = a.lrec[(long long)(N - 1) * 48 + t - fm * 36];
+      stg[((N - 1) & 1) * SB + t] = v;
+    }
+  }
+  load_stage(N - 2, recb + (((N - 2) % 3 + 3) % 3) * R, pb);
+  __syncthreads();
+  auto bcolumn = [&](int k, double (&cur)[kFrontPf], double (&nxt)[kFrontPf]) {
+    const int* rk = recb + (k % 3) * R;
+    const double* st = stg + (k & 1) * SB;
+    const int na = rk[1];
+    FRONT_STAMP(0);
+    int pr[kFrontPr];
+    load_rec(k - 3, pr);
+    load_stage(k - 2, recb + (((k - 2) % 3 + 3) % 3) * R, nxt);
+    if (tid < na * 6) {  // (L_ikᵀ x_i)_r
+      const int li = tid / 6, r = tid % 6;
+      const double* Lb = st + li * 36 + r;
+      const double* xi = ys + 6 * rk[kFrontHdr + fm + li];
+      double p = 0.0;
+#pragma unroll
+      for (int m = 0; m < 6; ++m) p += Lb[m * 6] * xi[m];
+      sp[tid] = p;
+    }
+    FRONT_STAMP(7);
+    __syncthreads();
+    FRONT_STAMP(8);
+    if (tid == 0) {
+      double t[6];
+#pragma unroll
+      for (int r = 0; r < 6; ++r) t[r] = st[fm * 36 + 42 + r];
+      for (int li = 0; li < na; ++li)
+#pragma unroll
+        for (int r = 0; r < 6; ++r) t[r] -= sp[li * 6 + r];
+#pragma unroll
+      for (int r = 5; r >= 0; --r) {  // L_kkᵀ x = t
+        double v = t[r];
+#pragma unroll
+        for (int m = r + 1; m < 6; ++m) v -= st[fm * 36 + m * 6 + r] * t[m];
+        t[r] = v * st[fm * 36 + 36 + r];
+      }
+#pragma unroll
+      for (int r = 0; r < 6; ++r) {
+        ys[6 * k + r] = t[r];
+        a.x[6 * k + r] = t[r];
+      }
+    }
+    if (k >= 1) store_stage(k - 1, cur);  // column k − 1's stage (not read at column k)
+    if (k >= 3) store_rec(k - 3, pr);     // the record of k − 3 (over record k)
+    FRONT_STAMP(9);
+    __syncthreads();
+    FRONT_STAMP(10);
+  };
+  for (int k = N - 1; k >= 0; k -= 2) {
+    bcolumn(k, pb, pbn);
+    if (k >= 1) bcolumn(k - 1, pbn, pb);
+  }
+  if (tid == 0) *a.status = 0;
+#ifdef PBA_FRONT_STAMPS
+  __syncthreads();
+  if (tid == 0 || tid == 64)
+    for (int i = 0; i < 10; ++i) a.x[(tid ? 10 : 0) + i] = (double)fts[i];
+#endif
+#undef FRONT_STAMP
+}
+
+// ------------------------------------------------------------------------------------------------
+// band_solve_kernel<B>: the same factorisation when every block row satisfies first(i) ≥ i − B (the
+// structure of windowed/sequential BA — C3/C4 have B = 4).  The assembly also writes S in dense band
+// layout (block c of row i = column i − B + c), so the next block row's address needs no indirection.
+// The active window of the factor (block rows k..k+B) lives in LDS as a ring; block row k+B+2 is
+// prefetched into registers two steps ahead.  Per step: one lane factors the 6×6 diagonal block
+// (reciprocal pivots, no inverse), B·6 lanes solve the column panel L_ik = A_ik L_kk⁻ᵀ row by row, the
+// trailing triangle is updated in parallel, and forward substitution is fused in.  Finished rows of L and
+// the reciprocal pivots go to global memory for the backward pass, which prefetches one step ahead.
+// ------------------------------------------------------------------------------------------------
+struct BandArgs {
+  const double* Sband;  // N rows × ((B+1)·36 + 6): blocks of columns i−B..i, then g_i
+  double* Lcol;         // N column records × (B·36 + 48): L_(k+q),k for q = 1..B | L_kk | 1/pivots | y_k
+  double* x;            // the step δ_poses
+  int* status;
+  int N;
+};
 
 template <int B>
 __global__ __launch_bounds__(256) void band_solve_kernel(const BandArgs a) {
@@ -4144,6 +4431,87 @@ int gn_prepare(pba_engine* e) {
     }
     if (ccrows.empty()) ccrows.push_back(0);
   }
+  {  // front_solve_kernel's plan: static slots, per-column records (see the kernel)
+    std::vector<std::vector<int>> adm(nfs);
+    for (int i = 0; i < nfs; ++i) adm[first[i]].push_back(i);
+    std::vector<int> slot(nfs, -1), freel;
+    int F = 0;
+    auto alloc = [&]() {
+      if (freel.empty()) return F++;
+      auto it = std::min_element(freel.begin(), freel.end());
+      const int v = *it;
+      freel.erase(it);
+      return v;
+    };
+    for (int i : adm[0]) slot[i] = alloc();
+    for (int k = 0; k < nfs; ++k) {
+      if (k + 1 < nfs)
+        for (int i : adm[k + 1]) slot[i] = alloc();
+      freel.push_back(slot[k]);
+    }
+    // active set after column k's admissions: (A_k \ {k}) ∪ adm(k+1), kept sorted
+    std::vector<std::vector<int2>> fresh(nfs);  // per column k: the blocks of the rows admitted for k + 1
+    std::vector<int2> init;
+    std::vector<int> act(adm[0].begin(), adm[0].end());
+    auto blk = [&](int hi, int lo) { return rowp[hi] + (lo - first[hi]); };
+    auto add_rows = [&](const std::vector<int>& newr, std::vector<int>& A, std::vector<int2>& out) {
+      for (int i : newr) A.push_back(i);
+      std::sort(A.begin(), A.end());
+      for (int i : newr)
+        for (int j : A) {
+          if (j > i && std::binary_search(newr.begin(), newr.end(), j)) continue;  // the pair once (from j)
+          const int hi = std::max(i, j), lo = std::min(i, j);
+          out.push_back(make_int2(blk(hi, lo), slot[hi] * F + slot[lo]));
+        }
+    };
+    {
+      std::vector<int> A0;
+      add_rows(adm[0], A0, init);
+      act = A0;
+    }
+    int fm = 1, mf = 1;
+    for (int k = 0; k < nfs; ++k) {
+      fm = std::max(fm, ccptr[k + 1] - ccptr[k]);
+      act.erase(std::remove(act.begin(), act.end(), k), act.end());
+      if (k + 1 < nfs) add_rows(adm[k + 1], act, fresh[k]);
+      mf = std::max(mf, (int)fresh[k].size());
+    }
+    const int R = kFrontHdr + 3 * fm + 2 * mf, SB = fm * 36 + 48;
+    const size_t lds = sizeof(double) * ((size_t)F * F * 36 + 6 * (size_t)nfs + 2 * SB) +
+                       sizeof(int) * (3 * (size_t)R + fm * (fm + 1) / 2);
+    G.front_lds = 0;
+    if (fm <= 32 && mf * 36 <= 256 * kFrontPf && SB <= 256 * kFrontPf && R <= 256 * kFrontPr && lds <= 150 * 1024 &&
+        !getenv("PBA_SKYLINE_GLOBAL")) {
+      std::vector<int> rec((size_t)nfs * R, 0);
+      for (int k = 0; k < nfs; ++k) {
+        int* r = rec.data() + (size_t)k * R;
+        const int na = ccptr[k + 1] - ccptr[k];
+        r[0] = slot[k];
+        r[1] = na;
+        r[2] = (int)fresh[k].size();
+        for (int li = 0; li < na; ++li) {
+          const int i = ccrows[ccptr[k] + li];
+          r[kFrontHdr + li] = slot[i];
+          r[kFrontHdr + fm + li] = i;
+          r[kFrontHdr + 2 * fm + li] = blk(i, k);
+        }
+        for (int q = 0; q < (int)fresh[k].size(); ++q) {
+          r[kFrontHdr + 3 * fm + q] = fresh[k][q].x;
+          r[kFrontHdr + 3 * fm + mf + q] = fresh[k][q].y;
+        }
+      }
+      PBA_HIP(G.front_rec.upload(rec, e->stream));
+      G.front_n_init = (int)init.size();
+      if (init.empty()) init.push_back(make_int2(0, 0));
+      PBA_HIP(G.front_init.upload(init, e->stream));
+      PBA_HIP(G.front_lrec.resize((size_t)nfs * 48));
+      G.front_F = F;
+      G.front_fm = fm;
+      G.front_mf = mf;
+      G.front_R = R;
+      G.front_lds = lds;
+    }
+  }
   std::vector<int> cptr(G.n_sky + 1, 0), bi(G.n_sky), bj(G.n_sky);
   std::vector<std::vector<int2>> per(G.n_sky);
   for (int i = 0; i < nfs; ++i)
@@ -4713,6 +5081,15 @@ int enqueue_solve(pba_engine* e, double lambda, const double* lm = nullptr, bool
   if (G.band_kernel) {
     if (int rc = band_solve(e, !direct)) return rc;
   } else {
+    if (G.front_lds) {
+      FrontArgs fa{G.S.p, G.g.p, G.L.p, G.front_lrec.p, G.front_rec.p, G.front_init.p, G.x.p, G.status.p, nfs,
+                   G.front_F, G.front_fm, G.front_mf, G.front_R, G.front_n_init};
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&front_solve_kernel),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)G.front_lds);  // may exceed 64 KB
+      front_solve_kernel<<<1, 256, G.front_lds, e->stream>>>(fa);
+      PBA_HIP(hipGetLastError());
+      return PBA_OK;
+    }
     PBA_HIP(hipMemcpyAsync(G.L.p, G.S.p, sizeof(double) * 36 * (size_t)G.n_sky, hipMemcpyDeviceToDevice, e->stream));
     SolveArgs so{G.L.p, G.sky_first.p, G.sky_row.p, G.sky_last.p, G.g.p, G.Linv.p, G.x.p, G.status.p, nfs,
                  G.sky_colptr.p, G.sky_colrows.p};

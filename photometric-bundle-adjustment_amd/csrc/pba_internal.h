@@ -743,6 +743,14 @@ struct GnData {
   DevBuf<int> sky_diag, sky_off;     // the diagonal skyline blocks, the others (assemble_kernel's thread ranges)
   DevBuf<int> sky_colptr, sky_colrows;  // per column k, the rows i > k of the profile (first(i) ≤ k): skyline solve
   int n_sky_diag = 0;
+  // front_solve_kernel's plan (gn_prepare): per column k one record of kFrontHdr + 3·fm + 2·mf ints — slot of k, the
+  // column's row count, the fresh-block count, then the rows' slots, indices and factor blocks, then the fresh blocks
+  // (source skyline block, front position) that the next column admits; the rows admitted at column 0 in front_init.
+  DevBuf<int> front_rec;
+  DevBuf<int2> front_init;
+  DevBuf<double> front_lrec;  // per column: L_kk (36) | reciprocal pivots (6) | y_k (6)
+  int front_F = 0, front_fm = 0, front_mf = 0, front_R = 0, front_n_init = 0;
+  size_t front_lds = 0;       // 0: the profile's front does not fit (skyline_solve_kernel)
   DevBuf<double> S, L, Sband, Lband, g, g_dir, Ddiag, Linv, x;  // skyline system, its factor, rhs, direct gradient, LM diagonal, L_kk⁻¹, step
   DevBuf<uint8_t> fixed;
   DevBuf<uint8_t> observed, fixed_req, fixed_dist;  // multi-GPU: local observation flags, requested / effective constants

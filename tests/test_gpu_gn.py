@@ -443,6 +443,56 @@ def test_loop_closure_structure_uses_skyline():
     assert np.linalg.norm(dl - dl_ref) <= 1e-3 * np.linalg.norm(dl_ref)
 
 
+def _intrinsics_problem(n_frames, n_points, seed):
+    pb0 = synth.make_problem(kind=1, n_frames=n_frames, n_points=n_points, width=376, height=240, seed=seed, border=12)
+    k1 = pb0.intrinsics[0].copy()
+    k1[:4] *= np.array([1.01, 0.99, 1.0, 1.0])
+    intr = np.stack([pb0.intrinsics[0], k1])
+    return synth.make_problem(kind=1, n_frames=n_frames, n_points=n_points, width=376, height=240, seed=seed,
+                              border=12, intrinsics=intr, frame_cam=np.arange(n_frames, dtype=np.int32) % 2)
+
+
+@pytest.mark.parametrize("case", ["band", "loop", "intrinsics"])
+def test_front_and_global_skyline_agree(case, monkeypatch):
+    """The skyline system's two solvers: front_solve_kernel (the active front — the rows of the current column's profile
+    — in LDS, statically slotted rows, fresh blocks prefetched a column ahead) and skyline_solve_kernel (the same
+    right-looking factorisation through global memory, PBA_SKYLINE_GLOBAL).  A band forced onto the skyline path, a
+    loop-closure profile (row n − 1 reaches column 0) and the free-intrinsics border (two cameras, 2·2 border rows) give
+    the same step to fp64 rounding (reciprocal pivots against divisions)."""
+    monkeypatch.setenv("PBA_SOLVER", "skyline")
+    if case == "band":
+        pb, huber = synth.make_problem(n_frames=37, n_points=370, width=376, height=240, seed=88, border=12), 9.0
+    elif case == "loop":
+        pb = synth.make_problem(kind="geometric", n_frames=24, n_points=150, seed=52, obs_sigma=0.2)
+        sel = np.nonzero(pb.point_host == 0)[0][:10]
+        Th, Tt = pb.poses_gt[0], pb.poses_gt[pb.n_frames - 1]
+        b = synth.unproject(pb.model, pb.intrinsics[0], pb.u_ref[sel])
+        pw = (synth.quat_to_rot(Th[:4]) @ (b / pb.rho_gt[sel, None]).T).T + Th[4:]
+        pt = (synth.quat_to_rot(Tt[:4]).T @ (pw - Tt[4:]).T).T
+        ok = pt[:, 2] > 0.5
+        pb = synth.Problem(**{**pb.__dict__,
+                              "block_point": np.concatenate([pb.block_point, sel[ok].astype(np.int32)]),
+                              "block_target": np.concatenate([pb.block_target,
+                                                              np.full(ok.sum(), pb.n_frames - 1, np.int32)]),
+                              "u_obs": np.concatenate([pb.u_obs, synth.project(pb.model, pb.intrinsics[0], pt)[ok]])})
+        huber = 1.0
+    else:
+        pb, huber = _intrinsics_problem(16, 200, 17), 1.0
+    steps = {}
+    for glob in (False, True):
+        if glob:
+            monkeypatch.setenv("PBA_SKYLINE_GLOBAL", "1")
+        with make_engine(pb, huber, (0, 1)) as eng:
+            if case == "intrinsics":
+                eng.set_optimize_intrinsics(True)
+            eng.gn_linearize()
+            m, st = eng.gn_step(1e-3)
+            assert st == 0
+            steps[glob] = (*eng.gn_last_step(), np.array([m]))
+    for a, b in zip(steps[False], steps[True]):
+        assert np.linalg.norm(a - b) <= 1e-9 * np.linalg.norm(b), (case, np.linalg.norm(a - b) / np.linalg.norm(b))
+
+
 @pytest.fixture(scope="module")
 def c3():
     """BASELINE configs[2] (C3): 200 keyframes × 20k points × 8 px × 4 targets = 80k blocks, rendered images."""
