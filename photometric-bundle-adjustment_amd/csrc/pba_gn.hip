@@ -591,7 +591,16 @@ void linearize_adj_kernel(const KernelArgs a, const LinArgs g) {
 #pragma unroll
       for (int q = 1; q < PPL; ++q) ih = j == q ? Ih[q] : ih;
       asm volatile("" ::: "memory");  // the tile is read from LDS per pass (see photometric_block_kernel_multi)
+#ifdef PBA_ABL_ROW
+      Row row;
+      row.ok = 1;
+      row.r = ih + (float)s_tb[wb].pr.R[k] + s_pat[act ? px : 0].x;
+      row.jr = row.r;
+      row.tv = Vec3{row.r, row.r, row.r};
+      row.tw = row.tv;
+#else
       const Row row = photometric_row<MODEL, true>(a, s_tb[wb], s_pat[act ? px : 0], ih);
+#endif
       const bool use = act && row.ok;
       okl &= act ? row.ok : 1;
       s += use ? row.r * row.r : 0.0f;
@@ -602,6 +611,7 @@ void linearize_adj_kernel(const KernelArgs a, const LinArgs g) {
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#ifndef PBA_ABL_MFMA
 #pragma unroll
       for (int b = 0; b < BW; ++b) {
         float o[4];
@@ -610,6 +620,7 @@ void linearize_adj_kernel(const KernelArgs a, const LinArgs g) {
         for (int st = 0; st < 2; ++st)
           accb[b] = __builtin_amdgcn_mfma_f64_4x4x4f64((double)o[2 * st], (double)o[2 * st + 1], accb[b], 0, 0, 0);
       }
+#endif
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // this pass's reads before the next pass's row stores
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
