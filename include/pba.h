@@ -142,8 +142,8 @@ int pba_record_format(const pba_engine* engine);
  * 22·R values.  The on-device Gauss-Newton (pba_gn_*, pba_solve) then optimises the intrinsics too: each camera's 8
  * intrinsics are 12 unknowns of the reduced camera system after the keyframes' (two 6-dim blocks, the last four pads
  * with identity rows), a dense border of the skyline system (SPARSE_SCHUR keeps the intrinsics blocks among the f-blocks,
- * schur_complement_solver.cc:138-146); k ← k + δk, Ceres' LM diagonal over them too.  Single GPU only (the multi-GPU
- * entry points refuse such an engine). */
+ * schur_complement_solver.cc:138-146); k ← k + δk, Ceres' LM diagonal over them too.  The multi-GPU entry points
+ * exchange the border rows too (pba_gn_exchange_size). */
 int pba_set_optimize_intrinsics(pba_engine* engine, int32_t enable);
 int pba_set_intrinsics_state(pba_engine* engine, const double* intrinsics);
 /* the intrinsics state (8·n_cams doubles: the free intrinsics with pba_set_optimize_intrinsics, else the cameras') */
@@ -302,7 +302,11 @@ int pba_gn_get_step(pba_engine* engine, double* d_poses, double* d_inv_dist);
  *
  * The exchange buffer is a DEVICE array of pba_gn_exchange_size doubles, banded with K ∈ {4, 8, 16} block
  * rows, K ≥ max over ranks of pba_gn_band: per frame i, (K+1) 6×6 blocks (block c = column i−K+c, row
- * major) followed by 24 doubles [g(6) | g_direct(6) | diag(A)(6) | observed | 0…]; then 16 scalar slots. */
+ * major) followed by 24 doubles [g(6) | g_direct(6) | diag(A)(6) | observed | 0…]; with free intrinsics
+ * (pba_set_optimize_intrinsics) then the 2·n_cams border rows of nfs = n_frames + 2·n_cams frames: per row, nfs 6×6
+ * blocks (block y = column y; those right of the diagonal unused) and the same 24-double tail (observed = a camera this
+ * rank observes) — the summed system is then solved as a skyline with its active front in LDS; then 16 scalar
+ * slots. */
 int pba_gn_band(pba_engine* engine, int32_t* band);   /* local reduced-system bandwidth (block rows) */
 int pba_gn_exchange_size(pba_engine* engine, int32_t band, int64_t* count);
 /* after pba_gn_linearize: point elimination for lambda + this rank's partial system into d_exchange */
@@ -312,7 +316,7 @@ int pba_gn_step_export(pba_engine* engine, double lambda, int32_t band, double* 
 int pba_gn_step_import(pba_engine* engine, double lambda, int32_t band, const double* d_exchange,
                        double* model_pose, double* model_points, int32_t* solver_status);
 /* pba_solve over all ranks, steered by the device LM record as on one GPU: per trial, the banded partial systems
- * (count = pba_gn_exchange_size − 16 doubles) and then 16 scalars are summed over the ranks: the point part (model
+ * (and border rows; count = pba_gn_exchange_size − 16 doubles) and then 16 scalars are summed over the ranks: the point part (model
  * decrease, candidate cost and valid blocks, step and state norms, points above the gradient tolerance) from every
  * rank, and — with a pba_comm — the pose part and the reduced solve's status from rank 0 alone, so every rank takes the
  * same decision on the device from bit-identical inputs.  Two collectives per trial (trial i + 1's damping, hence its point elimination, depends

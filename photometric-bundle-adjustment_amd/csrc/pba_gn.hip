@@ -1581,6 +1581,77 @@ __global__ void import_kernel(const ImportArgs a, double lambda, const double* _
   if (r == 0) a.fixed[i] = fi ? 1 : 0;
 }
 
+// Free intrinsics on several GPUs: the summed exchange — the keyframes' band rows and the 2·nc border rows (the
+// border region after the band, export by intr_border_kernel & co.) — into the skyline system of the summed profile
+// (keyframe i: columns max(0, i − K) … i; border rows: 0 … P; row offsets `row`), with the single-GPU arithmetic of
+// assemble_kernel and border_store: + λ·clamp(diag(A)), identity rows / columns for constant frames (requested, or
+// observed by no rank — cameras: seen by no rank), the intrinsics pads (1 + λ on the diagonal, LM diagonal 1).  One lane
+// per element, then six per frame for g, the direct gradient, the LM diagonal and the effective constant flag.
+struct ImportSkyArgs {
+  const double* X;          // summed exchange buffer: band rows
+  const double* Xb;         // … its border region
+  const uint8_t* fixed_req;
+  const int* row;           // skyline row offsets of the summed profile (nfs + 1)
+  double* S;
+  double* g;
+  double* g_dir;
+  double* Ddiag;
+  uint8_t* fixed;           // effective constant frames (nfs)
+  int nf, nc, K;
+  long long n_el;           // skyline elements (36 per block)
+};
+__device__ __forceinline__ bool import_fixed(const ImportSkyArgs& a, int i) {
+  const int nfs = a.nf + 2 * a.nc;
+  if (i < a.nf) return a.fixed_req[i] || a.X[(long long)i * ex_row(a.K) + (a.K + 1) * 36 + 18] == 0.0;
+  return a.Xb[(long long)(i - a.nf) * ((long long)nfs * 36 + EX_TAIL) + (long long)nfs * 36 + 18] == 0.0;
+}
+__global__ void import_sky_kernel(const ImportSkyArgs a, double lambda, const double* __restrict__ lm) {
+  lambda = lm_lambda(lm_view(lm), lambda);
+  const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const int nfs = a.nf + 2 * a.nc, K = a.K;
+  const long long RS = ex_row(K), BRS = (long long)nfs * 36 + EX_TAIL;
+  auto tail_of = [&](int i) {
+    return i < a.nf ? a.X + (long long)i * RS + (K + 1) * 36 : a.Xb + (long long)(i - a.nf) * BRS + (long long)nfs * 36;
+  };
+  if (t < a.n_el) {
+    const int blk = (int)(t / 36), e = (int)(t % 36), r = e / 6, cc = e % 6;
+    int lo = 0, hi = nfs;  // the row i with row[i] ≤ blk < row[i + 1]
+    while (hi - lo > 1) {
+      const int mid = (lo + hi) >> 1;
+      if (a.row[mid] <= blk) lo = mid;
+      else hi = mid;
+    }
+    const int i = lo, j = (i < a.nf ? max(0, i - K) : 0) + (blk - a.row[i]);
+    double val;
+    bool pad = false;
+    if (i < a.nf) {
+      val = a.X[(long long)i * RS + (j - i + K) * 36 + e];
+    } else {
+      const int p = i - a.nf, d = 6 * (p & 1) + r, d2 = j >= a.nf ? 6 * ((j - a.nf) & 1) + cc : cc;
+      pad = d >= 8 || d2 >= 8;
+      val = a.Xb[(long long)p * BRS + (long long)j * 36 + e];
+    }
+    if (import_fixed(a, i) || import_fixed(a, j)) {
+      val = (i == j && r == cc) ? 1.0 : 0.0;
+    } else if (pad) {
+      val = (i == j && r == cc) ? 1.0 + lambda : 0.0;  // border_store: direct 1, LM diagonal 1
+    } else if (i == j && r == cc) {
+      val += lambda * fmin(fmax(tail_of(i)[12 + r], 1e-6), 1e32);
+    }
+    a.S[t] = val;
+    return;
+  }
+  const long long u = t - a.n_el;
+  if (u >= 6LL * nfs) return;
+  const int i = (int)(u / 6), r = (int)(u % 6);
+  const double* tail = tail_of(i);
+  const bool fi = import_fixed(a, i), pad = i >= a.nf && ((i - a.nf) & 1) && r >= 2;
+  a.g[u] = fi || pad ? 0.0 : tail[r];
+  a.g_dir[u] = fi || pad ? 0.0 : tail[6 + r];
+  a.Ddiag[u] = fi ? 0.0 : (pad ? 1.0 : fmin(fmax(tail[12 + r], 1e-6), 1e32));
+  if (r == 0) a.fixed[i] = fi ? 1 : 0;
+}
+
 // ------------------------------------------------------------------------------------------------
 // skyline_solve_kernel: S δ = −g, S = LLᵀ in place (block skyline, right-looking), one workgroup
 // ------------------------------------------------------------------------------------------------
@@ -3404,6 +3475,8 @@ struct IntrBorderArgs {
   double* g_dir;
   double* Ddiag;
   int nf, nc;
+  double* X = nullptr;     // multi-GPU export (pba_gn_step_export): this rank's border rows, undamped, into the exchange
+  long long xs = 0;        // buffer's border region (row stride nfs·36 + EX_TAIL) instead of S
 };
 
 // Element t of border row `row` (system frame P = nf + row): t < (P + 1)·36 → entry (r, cc) of block (P, y = t / 36) of
@@ -3424,6 +3497,24 @@ __device__ __forceinline__ double border_inv(const IntrBorderArgs& a, int gp, do
 __device__ __forceinline__ void border_store(const IntrBorderArgs& a, double lambda, int row, int t, double dir,
                                              double sch) {
   const int P = a.nf + row, nfs = a.nf + 2 * a.nc, h = row & 1;
+  if (a.X) {  // export: direct − Schur, the direct diagonal, g, the direct gradient, observed (import_sky_kernel damps,
+              // pads and fixes the summed rows)
+    double* xr = a.X + (long long)row * a.xs;
+    double* tail = xr + (long long)nfs * 36;
+    if (t >= nfs * 36) {
+      const int r = t - nfs * 36;
+      tail[r] = dir - sch;
+      tail[6 + r] = dir;
+      if (r == 0) tail[18] = a.fixed[P] ? 0.0 : 1.0;  // a camera this rank observes
+      return;
+    }
+    const int y = t / 36, e = t % 36, r = e / 6, cc = e % 6, d = 6 * h + r;
+    const int d2 = y >= a.nf ? 6 * ((y - a.nf) & 1) + cc : cc;
+    const bool pad = d >= 8 || d2 >= 8;
+    xr[(long long)y * 36 + e] = pad ? 0.0 : dir - sch;
+    if (y == P && r == cc) tail[12 + r] = pad ? 0.0 : dir;
+    return;
+  }
   if (t >= nfs * 36) {
     const int r = t - nfs * 36;
     const bool fx = a.fixed[P] != 0;
@@ -4236,6 +4327,115 @@ int configure_solver(pba_engine* e, int K, int solver) {
 }
 
 // Symbolic analysis: GN block order, chunks, slot layouts, skyline profile and contribution lists.
+// The rows of each column's profile: column k → every i > k with first(i) ≤ k, in order (CSR).
+void profile_columns(const std::vector<int>& first, std::vector<int>& ccptr, std::vector<int>& ccrows) {
+  const int n = (int)first.size();
+  std::vector<std::vector<int>> col(n);
+  for (int i = 0; i < n; ++i)
+    for (int k = first[i]; k < i; ++k) col[k].push_back(i);
+  ccptr.assign(n + 1, 0);
+  ccrows.clear();
+  for (int k = 0; k < n; ++k) {
+    ccptr[k + 1] = ccptr[k] + (int)col[k].size();
+    ccrows.insert(ccrows.end(), col[k].begin(), col[k].end());
+  }
+  if (ccrows.empty()) ccrows.push_back(0);
+}
+
+// front_solve_kernel's plan for a skyline profile (first(i), row offsets rowp, column lists): static slots — a row
+// admitted for column k + 1 never takes a slot in use at column k — and the per-column records (see the kernel).
+// P.lds = 0 when the front does not fit (or use = false): the caller then takes skyline_solve_kernel.
+int build_front_plan(const std::vector<int>& first, const std::vector<int>& rowp, const std::vector<int>& ccptr,
+                     const std::vector<int>& ccrows, hipStream_t st, FrontPlan& P, bool use) {
+  const int nfs = (int)first.size();
+  std::vector<std::vector<int>> adm(nfs);
+  for (int i = 0; i < nfs; ++i) adm[first[i]].push_back(i);
+  std::vector<int> slot(nfs, -1), freel;
+  int F = 0;
+  auto alloc = [&]() {
+    if (freel.empty()) return F++;
+    auto it = std::min_element(freel.begin(), freel.end());
+    const int v = *it;
+    freel.erase(it);
+    return v;
+  };
+  for (int i : adm[0]) slot[i] = alloc();
+  for (int k = 0; k < nfs; ++k) {
+    if (k + 1 < nfs)
+      for (int i : adm[k + 1]) slot[i] = alloc();
+    freel.push_back(slot[k]);
+  }
+  // active set after column k's admissions: (A_k \ {k}) ∪ adm(k+1), kept sorted
+  std::vector<std::vector<int2>> fresh(nfs);  // per column k: the blocks of the rows admitted for k + 1
+  std::vector<int2> init;
+  std::vector<int> act;
+  auto blk = [&](int hi, int lo) { return rowp[hi] + (lo - first[hi]); };
+  auto add_rows = [&](const std::vector<int>& newr, std::vector<int>& A, std::vector<int2>& out) {
+    for (int i : newr) A.push_back(i);
+    std::sort(A.begin(), A.end());
+    for (int i : newr)
+      for (int j : A) {
+        if (j > i && std::binary_search(newr.begin(), newr.end(), j)) continue;  // the pair once (from j)
+        const int hi = std::max(i, j), lo = std::min(i, j);
+        out.push_back(make_int2(blk(hi, lo), slot[hi] * F + slot[lo]));
+      }
+  };
+  add_rows(adm[0], act, init);
+  int fm = 1, mf = 1;
+  for (int k = 0; k < nfs; ++k) {
+    fm = std::max(fm, ccptr[k + 1] - ccptr[k]);
+    act.erase(std::remove(act.begin(), act.end(), k), act.end());
+    if (k + 1 < nfs) add_rows(adm[k + 1], act, fresh[k]);
+    mf = std::max(mf, (int)fresh[k].size());
+  }
+  const int R = kFrontHdr + 3 * fm + 2 * mf, SB = fm * 36 + 48;
+  const size_t lds = sizeof(double) * ((size_t)F * F * 36 + 6 * (size_t)nfs + 2 * SB) +
+                     sizeof(int) * (3 * (size_t)R + fm * (fm + 1) / 2);
+  P.lds = 0;
+  if (!use || fm > 32 || mf * 36 > 256 * kFrontPf || SB > 256 * kFrontPf || R > 256 * kFrontPr || lds > 150 * 1024)
+    return PBA_OK;
+  std::vector<int> rec((size_t)nfs * R, 0);
+  for (int k = 0; k < nfs; ++k) {
+    int* r = rec.data() + (size_t)k * R;
+    const int na = ccptr[k + 1] - ccptr[k];
+    r[0] = slot[k];
+    r[1] = na;
+    r[2] = (int)fresh[k].size();
+    for (int li = 0; li < na; ++li) {
+      const int i = ccrows[ccptr[k] + li];
+      r[kFrontHdr + li] = slot[i];
+      r[kFrontHdr + fm + li] = i;
+      r[kFrontHdr + 2 * fm + li] = blk(i, k);
+    }
+    for (int q = 0; q < (int)fresh[k].size(); ++q) {
+      r[kFrontHdr + 3 * fm + q] = fresh[k][q].x;
+      r[kFrontHdr + 3 * fm + mf + q] = fresh[k][q].y;
+    }
+  }
+  PBA_HIP(P.rec.upload(rec, st));
+  P.n_init = (int)init.size();
+  if (init.empty()) init.push_back(make_int2(0, 0));
+  PBA_HIP(P.init.upload(init, st));
+  PBA_HIP(P.lrec.resize((size_t)nfs * 48));
+  P.F = F;
+  P.fm = fm;
+  P.mf = mf;
+  P.R = R;
+  P.lds = lds;
+  return PBA_OK;
+}
+
+// S δ = −g by front_solve_kernel with plan P (S: the profile's skyline blocks; L: room for its factor).
+int launch_front(pba_engine* e, FrontPlan& P, const double* S, double* L, int N) {
+  GnData& G = e->gn;
+  FrontArgs fa{S, G.g.p, L, P.lrec.p, P.rec.p, P.init.p, G.x.p, G.status.p, N, P.F, P.fm, P.mf, P.R, P.n_init};
+  (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&front_solve_kernel),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)P.lds);  // may exceed 64 KB
+  front_solve_kernel<<<1, 256, P.lds, e->stream>>>(fa);
+  PBA_HIP(hipGetLastError());
+  return PBA_OK;
+}
+
 int gn_prepare(pba_engine* e) {
   GnData& G = e->gn;
   const int nb = e->n_blocks, nf = e->n_frames;
@@ -4426,103 +4626,15 @@ int gn_prepare(pba_engine* e) {
   rowp[0] = 0;
   for (int i = 0; i < nfs; ++i) rowp[i + 1] = rowp[i] + (i - first[i] + 1);
   G.n_sky = rowp[nfs];
-  G.band = 0;
-  for (int i = 0; i < nfs; ++i) G.band = std::max(G.band, i - first[i]);
+  G.band = 0;  // over the keyframes (the free-intrinsics border rows start at frame 0)
+  for (int i = 0; i < nf; ++i) G.band = std::max(G.band, i - first[i]);
   for (int k = 0; k < nfs; ++k) last[k] = k;
   for (int i = 0; i < nfs; ++i)
     for (int k = first[i]; k < i; ++k) last[k] = std::max(last[k], i);
-  std::vector<int> ccptr(nfs + 1, 0), ccrows;  // the rows of each column's profile, in order
-  {
-    std::vector<std::vector<int>> col(nfs);
-    for (int i = 0; i < nfs; ++i)
-      for (int k = first[i]; k < i; ++k) col[k].push_back(i);
-    for (int k = 0; k < nfs; ++k) {
-      ccptr[k + 1] = ccptr[k] + (int)col[k].size();
-      ccrows.insert(ccrows.end(), col[k].begin(), col[k].end());
-    }
-    if (ccrows.empty()) ccrows.push_back(0);
-  }
-  {  // front_solve_kernel's plan: static slots, per-column records (see the kernel)
-    std::vector<std::vector<int>> adm(nfs);
-    for (int i = 0; i < nfs; ++i) adm[first[i]].push_back(i);
-    std::vector<int> slot(nfs, -1), freel;
-    int F = 0;
-    auto alloc = [&]() {
-      if (freel.empty()) return F++;
-      auto it = std::min_element(freel.begin(), freel.end());
-      const int v = *it;
-      freel.erase(it);
-      return v;
-    };
-    for (int i : adm[0]) slot[i] = alloc();
-    for (int k = 0; k < nfs; ++k) {
-      if (k + 1 < nfs)
-        for (int i : adm[k + 1]) slot[i] = alloc();
-      freel.push_back(slot[k]);
-    }
-    // active set after column k's admissions: (A_k \ {k}) ∪ adm(k+1), kept sorted
-    std::vector<std::vector<int2>> fresh(nfs);  // per column k: the blocks of the rows admitted for k + 1
-    std::vector<int2> init;
-    std::vector<int> act(adm[0].begin(), adm[0].end());
-    auto blk = [&](int hi, int lo) { return rowp[hi] + (lo - first[hi]); };
-    auto add_rows = [&](const std::vector<int>& newr, std::vector<int>& A, std::vector<int2>& out) {
-      for (int i : newr) A.push_back(i);
-      std::sort(A.begin(), A.end());
-      for (int i : newr)
-        for (int j : A) {
-          if (j > i && std::binary_search(newr.begin(), newr.end(), j)) continue;  // the pair once (from j)
-          const int hi = std::max(i, j), lo = std::min(i, j);
-          out.push_back(make_int2(blk(hi, lo), slot[hi] * F + slot[lo]));
-        }
-    };
-    {
-      std::vector<int> A0;
-      add_rows(adm[0], A0, init);
-      act = A0;
-    }
-    int fm = 1, mf = 1;
-    for (int k = 0; k < nfs; ++k) {
-      fm = std::max(fm, ccptr[k + 1] - ccptr[k]);
-      act.erase(std::remove(act.begin(), act.end(), k), act.end());
-      if (k + 1 < nfs) add_rows(adm[k + 1], act, fresh[k]);
-      mf = std::max(mf, (int)fresh[k].size());
-    }
-    const int R = kFrontHdr + 3 * fm + 2 * mf, SB = fm * 36 + 48;
-    const size_t lds = sizeof(double) * ((size_t)F * F * 36 + 6 * (size_t)nfs + 2 * SB) +
-                       sizeof(int) * (3 * (size_t)R + fm * (fm + 1) / 2);
-    G.front_lds = 0;
-    if (fm <= 32 && mf * 36 <= 256 * kFrontPf && SB <= 256 * kFrontPf && R <= 256 * kFrontPr && lds <= 150 * 1024 &&
-        !getenv("PBA_SKYLINE_GLOBAL")) {
-      std::vector<int> rec((size_t)nfs * R, 0);
-      for (int k = 0; k < nfs; ++k) {
-        int* r = rec.data() + (size_t)k * R;
-        const int na = ccptr[k + 1] - ccptr[k];
-        r[0] = slot[k];
-        r[1] = na;
-        r[2] = (int)fresh[k].size();
-        for (int li = 0; li < na; ++li) {
-          const int i = ccrows[ccptr[k] + li];
-          r[kFrontHdr + li] = slot[i];
-          r[kFrontHdr + fm + li] = i;
-          r[kFrontHdr + 2 * fm + li] = blk(i, k);
-        }
-        for (int q = 0; q < (int)fresh[k].size(); ++q) {
-          r[kFrontHdr + 3 * fm + q] = fresh[k][q].x;
-          r[kFrontHdr + 3 * fm + mf + q] = fresh[k][q].y;
-        }
-      }
-      PBA_HIP(G.front_rec.upload(rec, e->stream));
-      G.front_n_init = (int)init.size();
-      if (init.empty()) init.push_back(make_int2(0, 0));
-      PBA_HIP(G.front_init.upload(init, e->stream));
-      PBA_HIP(G.front_lrec.resize((size_t)nfs * 48));
-      G.front_F = F;
-      G.front_fm = fm;
-      G.front_mf = mf;
-      G.front_R = R;
-      G.front_lds = lds;
-    }
-  }
+  std::vector<int> ccptr, ccrows;  // the rows of each column's profile, in order
+  profile_columns(first, ccptr, ccrows);
+  if (int rc = build_front_plan(first, rowp, ccptr, ccrows, e->stream, G.front, getenv("PBA_SKYLINE_GLOBAL") == nullptr))
+    return rc;
   std::vector<int> cptr(G.n_sky + 1, 0), bi(G.n_sky), bj(G.n_sky);
   std::vector<std::vector<int2>> per(G.n_sky);
   for (int i = 0; i < nfs; ++i)
@@ -4708,7 +4820,7 @@ int gn_prepare(pba_engine* e) {
   std::vector<uint8_t> req(nf, 0);
   for (int i = 0; i < nf && i < (int)G.fixed_h.size(); ++i) req[i] = G.fixed_h[i];
   PBA_HIP(G.fixed_req.upload(req, st));
-  PBA_HIP(G.fixed_dist.resize(nf));
+  PBA_HIP(G.fixed_dist.resize(nfs));
   PBA_HIP(G.g.resize((size_t)nfs * 6));
   PBA_HIP(G.g_dir.resize((size_t)nfs * 6));
   PBA_HIP(G.Ddiag.resize((size_t)nfs * 6));
@@ -5032,6 +5144,38 @@ void schur_lds_limit(const GnData& G) {
       (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)G.schur_lds);
 }
 
+// Free intrinsics: the last trial's accept (lm: the LM record, else none), then the weighted fp64 rows at the state.
+void enqueue_intr_rows(pba_engine* e, const double* lm) {
+  GnData& G = e->gn;
+  if (lm) intr_accept_kernel<<<1, 256, 0, e->stream>>>(lm, G.intr_new_d.p, G.intr_new_f.p, e->intr_state_d.p,
+                                                       e->intr_state.p, G.nc_sys);
+  IntrRowsArgs ra{G.ib_rec.p, e->poses.p, e->rho.p, e->u_ref.p, e->u_obs.p, e->frame_cam.p, e->intr_d.p,
+                  e->intr_state_d.p, (double)e->opt.huber_width, G.ib_data.p, e->n_blocks, lm ? lm : G.lm_idle.p};
+  const int grid = (e->n_blocks + 255) / 256;
+  switch (e->opt.camera_model) {
+    case PBA_CAMERA_PINHOLE: intr_rows_kernel<CAM_PINHOLE><<<grid, 256, 0, e->stream>>>(ra); break;
+    case PBA_CAMERA_DOUBLE_SPHERE: intr_rows_kernel<CAM_DS><<<grid, 256, 0, e->stream>>>(ra); break;
+    case PBA_CAMERA_EUCM: intr_rows_kernel<CAM_EUCM><<<grid, 256, 0, e->stream>>>(ra); break;
+    default: intr_rows_kernel<CAM_KB4><<<grid, 256, 0, e->stream>>>(ra); break;
+  }
+}
+
+// The border rows of the reduced system (free intrinsics) into the skyline S — or, X ≠ nullptr, this rank's undamped
+// border into the exchange buffer's border region (X points at it).
+void enqueue_border(pba_engine* e, double lambda, const double* lm, double* X) {
+  GnData& G = e->gn;
+  const int nf = e->n_frames, nfs = G.nfs;
+  IntrBorderArgs ba{G.ib_data.p, G.ib_rec.p, G.ib_cam.p, G.pt_rec.p, G.pt_data.p, G.ib_bptr.p, G.ib_blist.p,
+                    G.ib_pptr.p, G.ib_plist.p, G.sky_first.p, G.sky_row.p, G.fixed.p, lm ? lm : G.lm_idle.p, G.S.p,
+                    G.g.p, G.g_dir.p, G.Ddiag.p, nf, G.nc_sys, X, (long long)nfs * 36 + EX_TAIL};
+  const int nb = 2 * G.nc_sys + 1;
+  intr_border_kernel<6><<<dim3((nf + 3) / 4, G.nc_sys), 256, 0, e->stream>>>(ba, lambda);
+  intr_border_kernel<2><<<dim3((nf + 3) / 4, G.nc_sys), 256, 0, e->stream>>>(ba, lambda);
+  intr_border_cam_kernel<6><<<dim3(nb, G.nc_sys, kIbSplit), 256, 0, e->stream>>>(ba, lambda, G.ib_part.p);
+  intr_border_cam_kernel<2><<<dim3(nb, G.nc_sys, kIbSplit), 256, 0, e->stream>>>(ba, lambda, G.ib_part.p);
+  intr_border_fin_kernel<<<(2 * G.nc_sys * nb * 36 + 255) / 256, 256, 0, e->stream>>>(ba, lambda, G.ib_part.p);
+}
+
 // Schur complement for λ, assembly and reduced-system solve into G.x (enqueued only).
 // lm: the device LM record (λ, buffer set, done flag read on the device; lambda unused) or nullptr.
 // free_sets (the single-GPU LM loop without free intrinsics): the current set's λ-free partials, scaled in the assembly,
@@ -5048,19 +5192,7 @@ int enqueue_solve(pba_engine* e, double lambda, const double* lm = nullptr, bool
     schur_gate_kernel<<<std::max(1, std::min(G.n_schur, 512)), kBlockThreads, G.schur_lds, e->stream>>>(sa, G.degen.p);
   else
     schur_kernel<<<G.n_schur, kBlockThreads, G.schur_lds, e->stream>>>(sa, lambda);
-  if (G.nc_sys) {  // free intrinsics: the last trial's accept, then the weighted fp64 rows at the state
-    if (lm) intr_accept_kernel<<<1, 256, 0, e->stream>>>(lm, G.intr_new_d.p, G.intr_new_f.p, e->intr_state_d.p,
-                                                         e->intr_state.p, G.nc_sys);
-    IntrRowsArgs ra{G.ib_rec.p, e->poses.p, e->rho.p, e->u_ref.p, e->u_obs.p, e->frame_cam.p, e->intr_d.p,
-                    e->intr_state_d.p, (double)e->opt.huber_width, G.ib_data.p, e->n_blocks, lm ? lm : G.lm_idle.p};
-    const int grid = (e->n_blocks + 255) / 256;
-    switch (e->opt.camera_model) {
-      case PBA_CAMERA_PINHOLE: intr_rows_kernel<CAM_PINHOLE><<<grid, 256, 0, e->stream>>>(ra); break;
-      case PBA_CAMERA_DOUBLE_SPHERE: intr_rows_kernel<CAM_DS><<<grid, 256, 0, e->stream>>>(ra); break;
-      case PBA_CAMERA_EUCM: intr_rows_kernel<CAM_EUCM><<<grid, 256, 0, e->stream>>>(ra); break;
-      default: intr_rows_kernel<CAM_KB4><<<grid, 256, 0, e->stream>>>(ra); break;
-    }
-  }
+  if (G.nc_sys) enqueue_intr_rows(e, lm);
   // block cyclic reduction: assemble writes its level 0 directly (no Sband, no cr_build pass)
   const bool direct = G.band_kernel && G.solver == SOLVER_CR;
   if (direct && G.cr0_dirty)  // a distributed solve rebuilt level 0 over the whole band: back to zeros + padding
@@ -5078,29 +5210,11 @@ int enqueue_solve(pba_engine* e, double lambda, const double* lm = nullptr, bool
   }
   const int nthreads = (G.n_sky + (kAsmSeg - 1) * G.n_sky_diag) * 36 + 6 * nfs * kAsmSeg;
   assemble_kernel<<<(nthreads + 255) / 256, 256, 0, e->stream>>>(aa, lambda);
-  if (G.nc_sys) {  // the intrinsics rows of the skyline system (over assemble's zeros there)
-    IntrBorderArgs ba{G.ib_data.p, G.ib_rec.p, G.ib_cam.p, G.pt_rec.p, G.pt_data.p, G.ib_bptr.p, G.ib_blist.p,
-                      G.ib_pptr.p, G.ib_plist.p, G.sky_first.p, G.sky_row.p, G.fixed.p, lm ? lm : G.lm_idle.p, G.S.p,
-                      G.g.p, G.g_dir.p, G.Ddiag.p, nf, G.nc_sys};
-    const int nb = 2 * G.nc_sys + 1;
-    intr_border_kernel<6><<<dim3((nf + 3) / 4, G.nc_sys), 256, 0, e->stream>>>(ba, lambda);
-    intr_border_kernel<2><<<dim3((nf + 3) / 4, G.nc_sys), 256, 0, e->stream>>>(ba, lambda);
-    intr_border_cam_kernel<6><<<dim3(nb, G.nc_sys, kIbSplit), 256, 0, e->stream>>>(ba, lambda, G.ib_part.p);
-    intr_border_cam_kernel<2><<<dim3(nb, G.nc_sys, kIbSplit), 256, 0, e->stream>>>(ba, lambda, G.ib_part.p);
-    intr_border_fin_kernel<<<(2 * G.nc_sys * nb * 36 + 255) / 256, 256, 0, e->stream>>>(ba, lambda, G.ib_part.p);
-  }
+  if (G.nc_sys) enqueue_border(e, lambda, lm, nullptr);  // the intrinsics rows of the skyline system (over assemble's zeros)
   if (G.band_kernel) {
     if (int rc = band_solve(e, !direct)) return rc;
   } else {
-    if (G.front_lds) {
-      FrontArgs fa{G.S.p, G.g.p, G.L.p, G.front_lrec.p, G.front_rec.p, G.front_init.p, G.x.p, G.status.p, nfs,
-                   G.front_F, G.front_fm, G.front_mf, G.front_R, G.front_n_init};
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&front_solve_kernel),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)G.front_lds);  // may exceed 64 KB
-      front_solve_kernel<<<1, 256, G.front_lds, e->stream>>>(fa);
-      PBA_HIP(hipGetLastError());
-      return PBA_OK;
-    }
+    if (G.front.lds) return launch_front(e, G.front, G.S.p, G.L.p, nfs);
     PBA_HIP(hipMemcpyAsync(G.L.p, G.S.p, sizeof(double) * 36 * (size_t)G.n_sky, hipMemcpyDeviceToDevice, e->stream));
     SolveArgs so{G.L.p, G.sky_first.p, G.sky_row.p, G.sky_last.p, G.g.p, G.Linv.p, G.x.p, G.status.p, nfs,
                  G.sky_colptr.p, G.sky_colrows.p};
@@ -5238,17 +5352,46 @@ int accept(pba_engine* e) {
 
 // ---- multi-GPU step (include/pba.h) ------------------------------------------------------------
 int exchange_K(pba_engine* e, int band, int* K) {
-  if (e->gn.nc_sys) return fail(PBA_ERR_INVALID_ARGUMENT, "free intrinsics: the single-GPU solve (pba_solve) only");
   *K = band_kernel_for(std::max(band, e->gn.band));
   if (band < e->gn.band) return fail(PBA_ERR_INVALID_ARGUMENT, "band below this rank's reduced-system bandwidth");
   if (*K == 0) return fail(PBA_ERR_INVALID_ARGUMENT, "distributed solve needs a reduced-system bandwidth <= 16");
   return PBA_OK;
 }
 
-long long exchange_count(pba_engine* e, int K) { return (long long)e->n_frames * ex_row(K) + kExScalars; }
+// The exchange buffer: the keyframes' band rows (nf × ex_row(K)), with free intrinsics the 2·nc border rows
+// (nfs·36 + EX_TAIL each), then the kExScalars scalar slots of the device-steered loop.
+long long ex_border(const pba_engine* e) {
+  const GnData& G = e->gn;
+  return G.nc_sys ? 2LL * G.nc_sys * ((long long)G.nfs * 36 + EX_TAIL) : 0;
+}
+long long ex_scalar_off(const pba_engine* e, int K) { return (long long)e->n_frames * ex_row(K) + ex_border(e); }
+long long exchange_count(pba_engine* e, int K) { return ex_scalar_off(e, K) + kExScalars; }
 
-// This rank's partial system into the exchange buffer X (every element written: no fill launch).
-int enqueue_export(pba_engine* e, const double* lm, double* X, int K) {
+// The summed profile of a multi-GPU free-intrinsics solve (band K over the keyframes, border rows from frame 0): its
+// skyline layout and front_solve_kernel plan, built once per K.
+int ensure_dist_sky(pba_engine* e, int K) {
+  GnData& G = e->gn;
+  if (G.dsky_K == K) return PBA_OK;
+  const int nf = e->n_frames, nfs = G.nfs;
+  std::vector<int> first(nfs), rowp(nfs + 1, 0), ccptr, ccrows;
+  for (int i = 0; i < nfs; ++i) first[i] = i < nf ? std::max(0, i - K) : 0;
+  for (int i = 0; i < nfs; ++i) rowp[i + 1] = rowp[i] + (i - first[i] + 1);
+  profile_columns(first, ccptr, ccrows);
+  if (int rc = build_front_plan(first, rowp, ccptr, ccrows, e->stream, G.dfront, true)) return rc;
+  if (!G.dfront.lds)
+    return fail(PBA_ERR_INVALID_ARGUMENT, "multi-GPU free intrinsics: the reduced system's active front exceeds LDS");
+  G.n_dsky = rowp[nfs];
+  PBA_HIP(G.dS.resize((size_t)G.n_dsky * 36));
+  PBA_HIP(G.dL.resize((size_t)G.n_dsky * 36));
+  PBA_HIP(G.dsky_row.upload(rowp, e->stream));
+  G.dsky_K = K;
+  return PBA_OK;
+}
+
+// This rank's partial system into the exchange buffer X (every element written: no fill launch); with free
+// intrinsics also the border rows (after this trial's accept and point elimination: the rows at the state, the Schur
+// terms at λ — the LM record's, or `lambda` for a host-driven step).
+int enqueue_export(pba_engine* e, double lambda, const double* lm, double* X, int K) {
   GnData& G = e->gn;
   const int nf = e->n_frames;
   AsmArgs aa{G.part_lin.p, G.part_lin1.p, lm, G.part_schur.p, G.sky_cptr.p, G.sky_contrib.p, G.g_cptr.p,
@@ -5257,6 +5400,10 @@ int enqueue_export(pba_engine* e, const double* lm, double* X, int K) {
   const long long n = (long long)nf * ex_row(K);  // (K+1)·36 band + EX_TAIL tail lanes per frame
   export_band_kernel<<<(unsigned)((n + 255) / 256), 256, 0, e->stream>>>(aa, G.observed.p, G.sky_first.p, G.sky_row.p,
                                                                         X, K);
+  if (G.nc_sys) {
+    enqueue_intr_rows(e, lm == G.lm_idle.p ? nullptr : lm);
+    enqueue_border(e, lambda, lm, X + n);
+  }
   PBA_HIP(hipGetLastError());
   return PBA_OK;
 }
@@ -5266,6 +5413,16 @@ int enqueue_export(pba_engine* e, const double* lm, double* X, int K) {
 int enqueue_import(pba_engine* e, double lambda, const double* lm, const double* X, int K) {
   GnData& G = e->gn;
   const int nf = e->n_frames;
+  if (G.nc_sys) {  // free intrinsics: the summed skyline system (band + border), solved with its active front in LDS
+    if (int rc = ensure_dist_sky(e, K)) return rc;
+    const int nfs = G.nfs;
+    ImportSkyArgs ia{X, X + (long long)nf * ex_row(K), G.fixed_req.p, G.dsky_row.p, G.dS.p, G.g.p, G.g_dir.p,
+                     G.Ddiag.p, G.fixed_dist.p, nf, G.nc_sys, K, (long long)G.n_dsky * 36};
+    const long long n = ia.n_el + 6LL * nfs;
+    import_sky_kernel<<<(unsigned)((n + 255) / 256), 256, 0, e->stream>>>(ia, lambda, lm);
+    PBA_HIP(hipGetLastError());
+    return launch_front(e, G.dfront, G.dS.p, G.dL.p, nfs);
+  }
   const bool direct = G.solver == SOLVER_CR;
   if (direct && !G.cr0_inited)  // zeros outside the band, identity padding rows
     if (int rc = init_cr_level0(e)) return rc;
@@ -5292,7 +5449,7 @@ int step_export(pba_engine* e, double lambda, int band, double* X) {
   schur_lds_limit(G);
   if (G.n_schur > 0) schur_kernel<<<G.n_schur, kBlockThreads, G.schur_lds, e->stream>>>(sa, lambda);
   (void)nf;
-  return enqueue_export(e, G.lm_idle.p, X, K);
+  return enqueue_export(e, lambda, G.lm_idle.p, X, K);
 }
 
 int step_import(pba_engine* e, double lambda, int band, const double* X, double* model_pose, double* model_points,
@@ -5300,7 +5457,7 @@ int step_import(pba_engine* e, double lambda, int band, const double* X, double*
   GnData& G = e->gn;
   int K;
   if (int rc = exchange_K(e, band, &K)) return rc;
-  if (G.band_kernel != K || G.solver == SOLVER_SKYLINE) {
+  if (!G.nc_sys && (G.band_kernel != K || G.solver == SOLVER_SKYLINE)) {
     const char* fs = getenv("PBA_SOLVER");
     const int solver = (K <= 8 && !(fs && std::string(fs) == "band")) ? SOLVER_CR : SOLVER_BAND;
     if (int rc = configure_solver(e, K, solver)) return rc;
@@ -5689,14 +5846,15 @@ int dist_trial(pba_engine* e, const Collective& coll, const DecideOpts& dopt, do
   schur_lds_limit(G);
   if (G.n_schur > 0) schur_kernel<<<G.n_schur, kBlockThreads, G.schur_lds, e->stream>>>(sa, 0.0);
   else launch_accept(e, G.lm.p);  // no points on this rank: the accept alone
-  const long long nx = (long long)nf * ex_row(K);
-  if (int rc = enqueue_export(e, G.lm.p, X, K)) return rc;
+  const long long nx = ex_scalar_off(e, K);  // the band rows and, with free intrinsics, the border rows
+  if (int rc = enqueue_export(e, 0.0, G.lm.p, X, K)) return rc;
   if (int rc = coll.allreduce(e, X, nx)) return rc;
   if (int rc = enqueue_import(e, 0.0, G.lm.p, X, K)) return rc;
   int gp = 0, gq = 0;
   enqueue_updates(e, 0.0, G.fixed_dist.p, &gp, &gq, G.lm.p);
   if (G.n_chunks > 0)
-    if (int rc = linearize(e, nullptr, G.lm.p, G.pairs_new.p, G.rho_new.p, G.red.p + 2 * (gp + gq))) return rc;
+    if (int rc = linearize(e, nullptr, G.lm.p, G.pairs_new.p, G.rho_new.p, G.red.p + 2 * (gp + gq), nullptr, true))
+      return rc;  // (at the candidate intrinsics too)
   double* Y = X + nx;
   dist_sums_kernel<<<1, kDecideThreads, 0, e->stream>>>(G.red.p, G.red2.p, G.gmax.p, gp, gq, G.n_chunks, dopt.gtol,
                                                          G.lm.p, G.status.p, coll.rank0(e), G.tpose.p, Y);
@@ -5718,7 +5876,7 @@ int lm_loop(pba_engine* e, const pba_solver_options* o, const Collective* coll, 
   const pba_solver_options opt = lm_options(o);
   pba_solver_summary s{};
   const double t0 = now_ms();
-  if (G.band_kernel != K || G.solver == SOLVER_SKYLINE) {
+  if (!G.nc_sys && (G.band_kernel != K || G.solver == SOLVER_SKYLINE)) {
     const char* fs = getenv("PBA_SOLVER");
     const int solver = (K <= 8 && !(fs && std::string(fs) == "band")) ? SOLVER_CR : SOLVER_BAND;
     if (int rc = configure_solver(e, K, solver)) return rc;
@@ -5729,7 +5887,7 @@ int lm_loop(pba_engine* e, const pba_solver_options* o, const Collective* coll, 
   DistCheck chk;
   {  // Σ over ranks of the initial cost and valid blocks — and of 1: the number of ranks — through the scalar slots
     double v[3] = {cost, (double)n_valid, 1.0};
-    double* Y = X + (long long)e->n_frames * ex_row(K);
+    double* Y = X + ex_scalar_off(e, K);
     PBA_HIP(hipMemcpyAsync(Y, v, sizeof v, hipMemcpyHostToDevice, e->stream));
     if (int rc = coll->allreduce(e, Y, 3)) return rc;
     PBA_HIP(hipMemcpyAsync(v, Y, sizeof v, hipMemcpyDeviceToHost, e->stream));
@@ -5824,7 +5982,7 @@ int lm_loop(pba_engine* e, const pba_solver_options* o, const Collective* coll, 
     }
   }
   {
-    double* Y = X + (long long)e->n_frames * ex_row(K);
+    double* Y = X + ex_scalar_off(e, K);
     dist_verify_kernel<<<1, 64, 0, e->stream>>>(G.lm.p, Y);
     PBA_HIP(hipGetLastError());
     if (int rc = coll->allreduce(e, Y, kExScalars)) return rc;

@@ -688,6 +688,17 @@ struct CrLevelHost {
 
 // Gauss-Newton state: the symbolic analysis of the normal equations (built once per problem structure) and
 // the device buffers of one linearisation / Schur complement / solve.  See pba_gn.hip for the layouts.
+// front_solve_kernel's plan (pba_gn.hip, build_front_plan): per column k one record of kFrontHdr + 3·fm + 2·mf ints — the
+// slot of k, the column's row count, the fresh-block count, then the rows' slots, indices and factor blocks, then the
+// fresh blocks (source skyline block, front position) that the next column admits; the rows admitted at column 0 in init.
+struct FrontPlan {
+  DevBuf<int> rec;
+  DevBuf<int2> init;
+  DevBuf<double> lrec;  // per column: L_kk (36) | reciprocal pivots (6) | y_k (6)
+  int F = 0, fm = 0, mf = 0, R = 0, n_init = 0;
+  size_t lds = 0;       // 0: the profile's front does not fit (skyline_solve_kernel)
+};
+
 struct GnData {
   bool prepared = false;
   int lpb = 8, bpw = 32, ppl = 1;  // linearisation: lanes per block, blocks per chunk, rows per lane
@@ -743,14 +754,13 @@ struct GnData {
   DevBuf<int> sky_diag, sky_off;     // the diagonal skyline blocks, the others (assemble_kernel's thread ranges)
   DevBuf<int> sky_colptr, sky_colrows;  // per column k, the rows i > k of the profile (first(i) ≤ k): skyline solve
   int n_sky_diag = 0;
-  // front_solve_kernel's plan (gn_prepare): per column k one record of kFrontHdr + 3·fm + 2·mf ints — slot of k, the
-  // column's row count, the fresh-block count, then the rows' slots, indices and factor blocks, then the fresh blocks
-  // (source skyline block, front position) that the next column admits; the rows admitted at column 0 in front_init.
-  DevBuf<int> front_rec;
-  DevBuf<int2> front_init;
-  DevBuf<double> front_lrec;  // per column: L_kk (36) | reciprocal pivots (6) | y_k (6)
-  int front_F = 0, front_fm = 0, front_mf = 0, front_R = 0, front_n_init = 0;
-  size_t front_lds = 0;       // 0: the profile's front does not fit (skyline_solve_kernel)
+  FrontPlan front;   // front_solve_kernel's plan for the local skyline profile (gn_prepare)
+  // multi-GPU with free intrinsics: the summed system's profile — the exchange band K over the keyframes, the border rows
+  // from frame 0 — its skyline system, factor blocks, row offsets and plan (ensure_dist_sky, for dsky_K)
+  FrontPlan dfront;
+  DevBuf<double> dS, dL;
+  DevBuf<int> dsky_row;
+  int dsky_K = -1, n_dsky = 0;
   DevBuf<double> S, L, Sband, Lband, g, g_dir, Ddiag, Linv, x;  // skyline system, its factor, rhs, direct gradient, LM diagonal, L_kk⁻¹, step
   DevBuf<uint8_t> fixed;
   DevBuf<uint8_t> observed, fixed_req, fixed_dist;  // multi-GPU: local observation flags, requested / effective constants

@@ -411,15 +411,116 @@ def test_band_too_small_is_rejected():
         assert n == 12 * ((E_band(b) + 1) * 36 + 24) + 16
 
 
-def test_free_intrinsics_are_single_gpu():
-    """Free intrinsics put a dense border into the reduced camera system (skyline solve): the banded multi-GPU exchange
-    refuses such an engine instead of dropping the intrinsics."""
-    pb = synth.make_problem(kind="geometric", n_frames=12, n_points=60, seed=5)
-    with engine_for(pb, 1.0, (0,)) as e:
-        e.set_optimize_intrinsics(True)
-        e.gn_linearize()
-        with pytest.raises(E.PbaError, match="intrinsics"):
-            e.gn_exchange_size(e.gn_band())
+def intrinsics_problem(n_frames, n_points, seed, model=0):
+    """A stereo rig (two cameras, alternate keyframes) whose intrinsics state differs from the cameras the hosts
+    unproject with (reprojection.h:93-98), as test_gpu_gn's free-intrinsics tests."""
+    pb0 = synth.make_problem(kind=1, model=model, n_frames=n_frames, n_points=n_points, width=376, height=240,
+                             seed=seed, border=12)
+    k1 = pb0.intrinsics[0].copy()
+    k1[:4] *= np.array([1.01, 0.99, 1.0, 1.0])
+    intr = np.stack([pb0.intrinsics[0], k1])
+    pb = synth.make_problem(kind=1, model=model, n_frames=n_frames, n_points=n_points, width=376, height=240,
+                            seed=seed, border=12, intrinsics=intr, frame_cam=np.arange(n_frames, dtype=np.int32) % 2,
+                            obs_sigma=0.3)
+    return pb, intr * np.array([1.003, 0.998, 1.0005, 0.9995, 1, 1, 1, 1])
+
+
+def intrinsics_engine(pb, state, fixed):
+    e = engine_for(pb, 1.0, fixed)
+    e.set_optimize_intrinsics(True)
+    e.set_intrinsics_state(state)
+    return e
+
+
+@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("lam", [1e-4, 1e-1])
+def test_free_intrinsics_exchange_matches_single_engine_step(world, lam):
+    """Free intrinsics on several GPUs (optimize_intrinsics, map_utils.h:339-345): each rank exports its keyframe band
+    AND its undamped border rows (the cameras' intrinsics against every keyframe and camera, direct − Schur terms at λ,
+    the direct diagonal, g, observed cameras) after the band; the importer builds the summed skyline system (band K +
+    border) and solves it with its active front in LDS.  Every rank's pose step, candidate intrinsics and point steps
+    equal the single engine's."""
+    import torch
+    pb, state = intrinsics_problem(14, 200, 23)
+    fixed = (0, 1)
+    with intrinsics_engine(pb, state, fixed) as full:
+        c_full = full.gn_linearize()
+        m_full, st_full = full.gn_step(lam)
+        dp_full, dr_full = full.gn_last_step()
+        full.gn_accept()
+        k_full = full.get_intrinsics()
+    assert st_full == 0
+    sh = [(intrinsics_engine(sub, state, fixed), pids)
+          for sub, pids, _ in (D.shard_problem(pb, world, r) for r in range(world))]
+    try:
+        costs = [e.gn_linearize() for e, _ in sh]
+        assert abs(sum(costs) - c_full) <= 1e-8 * c_full
+        band = max(e.gn_band() for e, _ in sh)
+        n = sh[0][0].gn_exchange_size(band)
+        nfs = pb.n_frames + 4
+        assert n == pb.n_frames * ((E_band(band) + 1) * 36 + 24) + 4 * (nfs * 36 + 24) + 16
+        bufs = [torch.zeros(n, dtype=torch.float64, device="cuda") for _ in sh]
+        for (e, _), b in zip(sh, bufs):
+            e.gn_step_export(lam, band, b.data_ptr())
+        tot = bufs[0].clone()
+        for b in bufs[1:]:
+            tot += b
+        torch.cuda.synchronize()
+        model_pts, dr, mps = 0.0, np.zeros(pb.n_points), []
+        for e, pids in sh:
+            mp, mq, st = e.gn_step_import(lam, band, tot.data_ptr())
+            assert st == 0
+            mps.append(mp)
+            model_pts += mq
+            dp, drs = e.gn_last_step()
+            assert np.linalg.norm(dp - dp_full) <= 1e-6 * np.linalg.norm(dp_full)
+            dr[pids] = drs
+            e.gn_accept()
+            np.testing.assert_allclose(e.get_intrinsics() - state, k_full - state,
+                                       rtol=1e-6, atol=1e-9 * np.abs(k_full - state).max())
+        assert max(mps) - min(mps) <= 1e-12 * abs(mps[0])  # identical pose (+ intrinsics) step on every rank
+        assert abs(mps[0] + model_pts - m_full) <= 1e-8 * abs(m_full)
+        np.testing.assert_allclose(dr, dr_full, rtol=1e-6, atol=1e-12 * np.abs(dr_full).max())
+    finally:
+        for e, _ in sh:
+            e.close()
+
+
+@pytest.mark.parametrize("loop", ["host", "comm"])
+def test_free_intrinsics_solve_distributed_matches_solve(loop):
+    """The multi-GPU LM loops with free intrinsics — host-callback sums (pba_solve_distributed) and the device-steered
+    loop over an in-process pba_comm group — take pba_solve's trajectory: the same steps, final cost, poses, inverse
+    distances and intrinsics."""
+    import torch
+    pb, state = intrinsics_problem(16, 300, 29)
+    fixed = (0, 1)
+    with intrinsics_engine(pb, state, fixed) as full:
+        ref = full.solve(max_iterations=8)
+        poses_ref, rho_ref = full.get_state()
+        k_ref = full.get_intrinsics()
+    world = 3
+    sh = [(intrinsics_engine(sub, state, fixed), pids)
+          for sub, pids, _ in (D.shard_problem(pb, world, r) for r in range(world))]
+    comms = E.Comm.local_group(world) if loop == "comm" else []
+    try:
+        band = max(e.gn_band() for e, _ in sh)
+        if loop == "comm":
+            res = run_ranks(lambda r: sh[r][0].solve_distributed_comm(band, comms[r], max_iterations=8), world)
+        else:
+            n = sh[0][0].gn_exchange_size(band)
+            bufs = [torch.zeros(n, dtype=torch.float64, device="cuda") for _ in sh]
+            ar = D.InProcessAllReduce(bufs, timeout=120)
+            res = run_ranks(lambda r: sh[r][0].solve_distributed(band, bufs[r].data_ptr(), ar.rank(r),
+                                                                 max_iterations=8), world)
+        check_same_solve(pb, sh, res, ref, poses_ref, rho_ref)
+        for e, _ in sh:
+            np.testing.assert_allclose(e.get_intrinsics(), k_ref, rtol=1e-7)
+        assert ref["final_cost"] < ref["initial_cost"]
+    finally:
+        for c in comms:
+            c.close()
+        for e, _ in sh:
+            e.close()
 
 
 def E_band(b):
