@@ -3377,8 +3377,9 @@ __global__ __launch_bounds__(kBlockThreads) void update_kernel(const PoseUpdateA
 // Here camera c's intrinsics are the system frames nf + 2c (dims 0-5) and nf + 2c + 1 (dims 6-7, then four identity
 // pads): a dense border of the skyline system (their profile starts at frame 0).  The keyframe part is linearised,
 // eliminated and assembled as without intrinsics; the border — the blocks' direct terms J_iᵀJ_x and the points' Schur
-// terms −W_i,c W_xᵀ / H'_ρρ — is formed in fp64 by intr_border_kernel, one lane per element, in a fixed order (the CSR lists
-// of gn_prepare), from weighted fp64 rows (intr_rows_kernel) and schur_kernel's undamped H_ρρ.
+// terms −W_i,c W_xᵀ / H'_ρρ — is formed in fp64 by the border kernels below (a wave per keyframe block, camera blocks
+// split over workgroups) in a fixed order (the CSR lists of gn_prepare), from weighted fp64 rows (intr_rows_kernel) and
+// schur_kernel's undamped H_ρρ; on several GPUs each rank exports its border rows undamped (import_sky_kernel sums them).
 struct IntrRowsArgs {
   const int4* rec;       // GN block → {block, point, host, target}
   const double* poses;
