@@ -5,25 +5,25 @@
 // Cholesky of SPARSE_SCHUR (schur_complement_solver.cc:138-146; Schur structure <2,1,6>), and the
 // Levenberg-Marquardt trust-region loop (trust_region_minimizer.cc, levenberg_marquardt_strategy.cc).
 //
-// Pipeline per LM iteration (all on the engine stream):
-//   linearize_kernel   lane = (block, residual row).  Row residual/Jacobian (pba_internal.h), Huber weight
-//                      per block (Ceres Corrector, first-order form), then the 104 normal-equation products
-//                      of the row are reduce-scattered over the block's lanes with wave shuffles, summed over
-//                      the workgroup's blocks in LDS in fixed order, and written as one partial slot set per
-//                      workgroup ("linearise chunk": ≤ 256/LPB blocks of one host keyframe):
-//                        H_hh, g_h, and per distinct target t: H_ht, H_tt, g_t   (fp32)
-//                      plus 16 floats per block for the point elimination: H_ρρ, g_ρ, W_h = J_hᵀJ_ρ, W_t = J_tᵀJ_ρ.
-//   schur_kernel       one workgroup per "Schur chunk" (≤ 64 points of one host): per point
-//                      H'_ρρ = H_ρρ + λ·clamp(H_ρρ), then −Σ_p W_a W_bᵀ / H'_ρρ and −Σ_p W_a g_ρ / H'_ρρ for every
-//                      co-observed pose pair (a, b) of the chunk, fp64, fixed order.
-//   assemble_kernel    one lane per element of the reduced camera system S (skyline storage, lower blocks)
-//                      and of g: fixed-order fp64 sums of the partial slots through precomputed contribution
-//                      lists, + λ·clamp(diag) (Ceres LM diagonal), identity rows for constant frames.
-//   skyline_solve_kernel  one workgroup: right-looking block-skyline Cholesky S = LLᵀ in fp64, then
-//                      forward/back substitution for δ_poses.
-//   update_kernel      T ← T·exp(δ) (Sophus SE3::exp, fp64), back-substitution
-//                      δρ = −(g_ρ + Σ W_aᵀ δ_a)/H'_ρρ, and the LM model decrease ½(λ δᵀDδ − gᵀδ).
-//   cost: pair_kernel + photometric/geometric kernel in cost-only mode + fixed-order reduction.
+// Pipeline of one single-GPU LM trial (all on the engine stream; DESIGN.md §3 has the measured times):
+//   schur_gate_kernel      the previous trial's accept; only for a buffer set flagged degenerate, the λ-specific point
+//                          elimination (schur_chunk) — else the λ-free partials below are used.
+//   assemble_kernel        one lane (four for the long lists) per element of the reduced camera system S and of g:
+//                          fixed-order fp64 sums of the partial slots, + λ·clamp(diag) (Ceres' LM diagonal), identity
+//                          rows for constant frames; writes cyclic reduction's level 0 directly.
+//   cr_level_wave_kernel   block (parallel) cyclic reduction, one launch per level (band ≤ 8); band_solve_kernel
+//                          (band ≤ 16); front_solve_kernel (any profile: loop closures, the free-intrinsics border —
+//                          the active front in LDS) or skyline_solve_kernel (global memory).
+//   update_kernel          T ← T·exp(δ) (Sophus SE3::exp, fp64), δρ = −(g_ρ + Σ W_aᵀ δ_a)/H'_ρρ, the LM model
+//                          decrease ½(λ δᵀDδ − gᵀδ) and the candidate pair table, in one launch.
+//   linearize_adj_kernel   at the candidate (photometric, ≤ 32 px): rows of 8 lanes per block, the target's 8-column
+//                          products on 4×4×4 fp64 matrix-core tiles, host blocks through the pair's adjoint, chunk
+//                          partial slots (fp64) and 8 doubles of point data per block; linearize_kernel: the
+//                          14-column form (geometric rows, PBA_LIN_LEGACY).
+//   schur_free_decide_kernel  the λ-free point elimination of the new linearisation (P/(1 + λ) in the assembly) and,
+//                          in 16 workgroups counted in by an atomic, the fixed-order trial sums and Ceres' decision.
+// Free intrinsics add intr_rows_kernel and the border kernels (intr_border_*) after the elimination; several GPUs
+// exchange the per-rank systems (export_band_kernel, import_kernel / import_sky_kernel, dist_* kernels).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
