@@ -1872,8 +1872,9 @@ __device__ inline bool chol6_rcp(double* A, double* invd) {  // in place, lower;
 // Every lane issues its share of the global loads of the record two columns ahead and of the next column's fresh
 // blocks (backward: its staged factor blocks) at a column's start and stores them to LDS at its end.  (A dedicated
 // loader wave measured slower: the compiler's conservative waits then stalled that wave at the barriers.)
-// Forward (3 barriers per column): one lane factors L_kk (reciprocal pivots) and y_k = L_kk⁻¹ v_k; 6·|rows(k)| lanes
-// form L_ik = A_ik L_kk⁻ᵀ row by row (to LDS, to L, v_i −= L_ik y_k); the trailing pairs A_ij −= L_ik L_jkᵀ.
+// Forward (2 barriers per column): 6·|rows(k)| lanes form L_ik = A_ik L_kk⁻ᵀ row by row (to LDS, to L, v_i −= L_ik y_k);
+// then the trailing pairs A_ij −= L_ik L_jkᵀ while one lane finishes and factors the next diagonal block (look-ahead:
+// L_kk, reciprocal pivots and y_k = L_kk⁻¹ v_k were formed during column k − 1).
 // Backward (2 barriers per column): 6·|rows(k)| lanes form the products L_ikᵀ x_i, one lane adds them in order and
 // solves x_k = L_kk⁻ᵀ (y_k − Σ_i L_ikᵀ x_i).
 constexpr int kFrontHdr = 3;
@@ -1900,9 +1901,10 @@ __global__ __launch_bounds__(256) void front_solve_kernel(const FrontArgs a) {
   double* stg = ys + 6 * N;                              // backward: 2 × SB
   int* recb = reinterpret_cast<int*>(stg + 2 * SB);      // 3 × R: records k, k + 1, k + 2 (backward: k, k − 1, k − 2)
   int* pairs = recb + 3 * R;                             // lower-triangle pair p → (ii << 16) | jj
-  __shared__ double sL[36], sd[6], sy[6], sp[6 * 32];
+  __shared__ double sL[2][36], sd[2][6], sy[2][6], sp[6 * 32];  // the diagonal factor of columns k, k + 1
+  __shared__ double sDn[36];                                       // column k + 1's diagonal block (look-ahead)
   __shared__ int s_fail;
-#ifdef PBA_FRONT_STAMPS  // timing variant: per-phase wall-clock sums of lanes 0 and 64, written over x[0 … 19]
+#ifdef PBA_FRONT_STAMPS  // timing variant: per-phase wall-clock sums of lanes 0, 64 and 192, written over x[0 … 29]
   unsigned long long fts[10] = {}, ft0 = 0;
 #define FRONT_STAMP(i) { const unsigned long long t_ = wall_clock64(); if ((i) > 0) fts[(i) - 1] += t_ - ft0; ft0 = t_; }
 #else
@@ -1944,11 +1946,55 @@ __global__ __launch_bounds__(256) void front_solve_kernel(const FrontArgs a) {
   }
   __syncthreads();
 
-  // one column; cur holds its admissions (loaded during the previous column), nxt receives the next column's — the
-  // loop runs two columns per pass with the arrays swapped (no register copies)
+  // the 6×6 factor of a diagonal block, y = L⁻¹ v, into buffer set q (one lane); false: not positive definite
+  auto factor = [&](const double (&D)[36], int col, int q) -> bool {
+    double A[36], d[6];
+#pragma unroll
+    for (int e = 0; e < 36; ++e) A[e] = D[e];
+    if (!chol6_rcp(A, d)) return false;
+    double b[6];
+#pragma unroll
+    for (int r = 0; r < 6; ++r) b[r] = ys[6 * col + r];
+#pragma unroll
+    for (int c = 0; c < 6; ++c) {  // y_col = L⁻¹ v_col
+      double t = b[c];
+#pragma unroll
+      for (int m = 0; m < c; ++m) t -= A[c * 6 + m] * b[m];
+      b[c] = t * d[c];
+    }
+#pragma unroll
+    for (int e = 0; e < 36; ++e) sL[q][e] = A[e];
+#pragma unroll
+    for (int r = 0; r < 6; ++r) {
+      sd[q][r] = d[r];
+      sy[q][r] = b[r];
+      ys[6 * col + r] = b[r];
+    }
+    return true;
+  };
+  auto factor_lds = [&](int col, int slot, int q) {  // column col's diagonal block as it stands in the front
+    double D[36];
+    const double* Dk = fr + (long long)(slot * F + slot) * 36;
+#pragma unroll
+    for (int e = 0; e < 36; ++e) D[e] = Dk[e];
+    if (!factor(D, col, q)) s_fail = col + 1;
+  };
+  if (N > 0 && tid == 0) factor_lds(0, recb[0], 0);
+  __syncthreads();
+  if (s_fail) {
+    if (tid == 0) *a.status = s_fail;
+    return;
+  }
+
+  // One column, LOOK-AHEAD: its diagonal block was factored during the previous column (buffer set k & 1).  Panel,
+  // then — while lanes 0-191 run the trailing update — lane 192 forms column k + 1's diagonal block (its last update,
+  // −L_{k+1,k} L_{k+1,k}ᵀ, when k + 1 is the column's first row) and factors it: the 6×6 factor's serial chain is off
+  // the critical path.  A column k + 1 outside rows(k) (admitted fresh at k + 1) is factored after the barrier.
+  // cur holds the column's admissions (loaded during the previous column), nxt receives the next column's — two
+  // columns per pass with the arrays swapped (no register copies).
   auto column = [&](int k, double (&cur)[kFrontPf], double (&nxt)[kFrontPf]) -> bool {
     const int* rk = recb + (k % 3) * R;
-    const int sk = rk[0], na = rk[1], nfr = rk[2];
+    const int sk = rk[0], na = rk[1], nfr = rk[2], q = k & 1;
     const int* slots = rk + kFrontHdr;
     const int* rows = slots + fm;
     const int* gbl = rows + fm;
@@ -1957,41 +2003,8 @@ __global__ __launch_bounds__(256) void front_solve_kernel(const FrontArgs a) {
     int pr[kFrontPr];
     load_rec(k + 2, pr);  // before the fresh loads: waiting for it must not wait for them
     if (k + 1 < N) load_fresh(recb + ((k + 1) % 3) * R, nxt);
-    if (tid == 0) {
-      const double* Dk = fr + (long long)(sk * F + sk) * 36;
-      double A[36], d[6];
-#pragma unroll
-      for (int e = 0; e < 36; ++e) A[e] = Dk[e];
-      if (!chol6_rcp(A, d)) {
-        s_fail = k + 1;
-      } else {
-        double b[6];
-#pragma unroll
-        for (int r = 0; r < 6; ++r) b[r] = ys[6 * k + r];
-#pragma unroll
-        for (int c = 0; c < 6; ++c) {  // y_k = L_kk⁻¹ v_k
-          double t = b[c];
-#pragma unroll
-          for (int m = 0; m < c; ++m) t -= A[c * 6 + m] * b[m];
-          b[c] = t * d[c];
-        }
-#pragma unroll
-        for (int e = 0; e < 36; ++e) sL[e] = A[e];
-#pragma unroll
-        for (int r = 0; r < 6; ++r) {
-          sd[r] = d[r];
-          sy[r] = b[r];
-          ys[6 * k + r] = b[r];
-        }
-      }
-    }
     FRONT_STAMP(1);
-    __syncthreads();
     FRONT_STAMP(2);
-    if (s_fail) {
-      if (tid == 0) *a.status = s_fail;
-      return false;
-    }
     if (tid < na * 6) {  // panel row r of L_ik = A_ik L_kk⁻ᵀ; v_i −= L_ik y_k
       const int li = tid / 6, r = tid % 6;
       double* A = fr + (long long)(slots[li] * F + sk) * 36 + r * 6;
@@ -2000,8 +2013,8 @@ __global__ __launch_bounds__(256) void front_solve_kernel(const FrontArgs a) {
       for (int c = 0; c < 6; ++c) {
         double t = A[c];
 #pragma unroll
-        for (int m = 0; m < c; ++m) t -= X[m] * sL[c * 6 + m];
-        X[c] = t * sd[c];
+        for (int m = 0; m < c; ++m) t -= X[m] * sL[q][c * 6 + m];
+        X[c] = t * sd[q][c];
       }
       double* Lg = a.L + (long long)gbl[li] * 36 + r * 6;
       double dv = 0.0;
@@ -2009,36 +2022,78 @@ __global__ __launch_bounds__(256) void front_solve_kernel(const FrontArgs a) {
       for (int c = 0; c < 6; ++c) {
         A[c] = X[c];
         Lg[c] = X[c];
-        dv += X[c] * sy[c];
+        dv += X[c] * sy[q][c];
       }
       ys[6 * rows[li] + r] -= dv;
     } else if (tid >= 192 && tid < 240) {
       const int e = tid - 192;
-      a.lrec[(long long)k * 48 + e] = e < 36 ? sL[e] : (e < 42 ? sd[e - 36] : sy[e - 42]);
+      a.lrec[(long long)k * 48 + e] = e < 36 ? sL[q][e] : (e < 42 ? sd[q][e - 36] : sy[q][e - 42]);
     }
     FRONT_STAMP(3);
     __syncthreads();
     FRONT_STAMP(4);
-    const int np = na * (na + 1) / 2;  // trailing A_ij −= L_ik L_jkᵀ (i ≥ j in rows(k))
-    for (int idx = tid; idx < np * 36; idx += 256) {
-      const int pq = pairs[idx / 36], e = idx % 36, r = e / 6, c = e % 6;
-      const int si = slots[pq >> 16], sj = slots[pq & 0xffff];
-      const double* Li = fr + (long long)(si * F + sk) * 36 + r * 6;
-      const double* Lj = fr + (long long)(sj * F + sk) * 36 + c * 6;
-      double acc = 0.0;
+    const bool ahead = k + 1 < N && na > 0 && rows[0] == k + 1;  // (uniform)
+    const int np = na * (na + 1) / 2;  // trailing A_ij −= L_ik L_jkᵀ (i ≥ j in rows(k)); pair 0 = (k+1, k+1) if ahead
+    if (tid < 192) {  // four items per lane in flight: their dependent LDS rounds (pair → slots → rows → element) overlap
+      constexpr int TR = 4;
+      const int i0 = ahead ? 36 : 0, ne = np * 36;
+      for (int base = i0 + tid; base < ne; base += 192 * TR) {
+        double acc[TR];
+        int dst[TR];
 #pragma unroll
-      for (int m = 0; m < 6; ++m) acc += Li[m] * Lj[m];
-      fr[(long long)(si * F + sj) * 36 + e] -= acc;
+        for (int u = 0; u < TR; ++u) {
+          const int idx = min(base + 192 * u, ne - 1);
+          const int pq = pairs[idx / 36], e = idx % 36, r = e / 6, c = e % 6;
+          const int si = slots[pq >> 16], sj = slots[pq & 0xffff];
+          const double* Li = fr + (si * F + sk) * 36 + r * 6;
+          const double* Lj = fr + (sj * F + sk) * 36 + c * 6;
+          double t = 0.0;
+#pragma unroll
+          for (int m = 0; m < 6; ++m) t += Li[m] * Lj[m];
+          acc[u] = t;
+          dst[u] = (si * F + sj) * 36 + e;
+        }
+#pragma unroll
+        for (int u = 0; u < TR; ++u)
+          if (base + 192 * u < ne) fr[dst[u]] -= acc[u];
+      }
+    } else if (ahead) {  // wave 3: column k + 1's diagonal block, final (lane e: entry e), then lane 192 factors it
+      const int s1 = slots[0], e = tid - 192;
+      if (e < 36) {
+        const double* Li = fr + (long long)(s1 * F + sk) * 36 + (e / 6) * 6;
+        const double* Lj = fr + (long long)(s1 * F + sk) * 36 + (e % 6) * 6;
+        double acc = 0.0;
+#pragma unroll
+        for (int m = 0; m < 6; ++m) acc += Li[m] * Lj[m];
+        sDn[e] = fr[(long long)(s1 * F + s1) * 36 + e] - acc;
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      if (e == 0) {
+        double D[36];
+#pragma unroll
+        for (int i = 0; i < 36; ++i) D[i] = sDn[i];
+        if (!factor(D, k + 1, q ^ 1)) s_fail = k + 2;
+      }
     }
 #pragma unroll
-    for (int q = 0; q < kFrontPf; ++q) {  // column k's admissions (slots unused at column k), the record of k + 2
-      const int idx = ld + 256 * q;
-      if (idx < nfr * 36) fr[(long long)fdst[idx / 36] * 36 + idx % 36] = cur[q];
+    for (int qq = 0; qq < kFrontPf; ++qq) {  // column k's admissions (slots unused at column k), the record of k + 2
+      const int idx = ld + 256 * qq;
+      if (idx < nfr * 36) fr[(long long)fdst[idx / 36] * 36 + idx % 36] = cur[qq];
     }
     if (k + 2 < N) store_rec(k + 2, pr);
     FRONT_STAMP(5);
     __syncthreads();
     FRONT_STAMP(6);
+    if (k + 1 < N && !ahead) {  // column k + 1 entered the front fresh: factor it now
+      if (tid == 0) factor_lds(k + 1, recb[((k + 1) % 3) * R], q ^ 1);
+      __syncthreads();
+    }
+    if (s_fail) {
+      if (tid == 0) *a.status = s_fail;
+      return false;
+    }
     return true;
   };
   double pf[kFrontPf], pfn[kFrontPf];
@@ -2138,8 +2193,8 @@ __global__ __launch_bounds__(256) void front_solve_kernel(const FrontArgs a) {
   if (tid == 0) *a.status = 0;
 #ifdef PBA_FRONT_STAMPS
   __syncthreads();
-  if (tid == 0 || tid == 64)
-    for (int i = 0; i < 10; ++i) a.x[(tid ? 10 : 0) + i] = (double)fts[i];
+  if (tid == 0 || tid == 64 || tid == 192)
+    for (int i = 0; i < 10; ++i) a.x[(tid == 0 ? 0 : (tid == 64 ? 10 : 20)) + i] = (double)fts[i];
 #endif
 #undef FRONT_STAMP
 }

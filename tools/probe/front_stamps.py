@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Diagnostic: per-phase wall-clock sums of front_solve_kernel (a PBA_FRONT_STAMPS variant writes them over x[0 … 19];
+"""Diagnostic: per-phase wall-clock sums of front_solve_kernel (a PBA_FRONT_STAMPS variant writes them over x[0 … 29];
 the step it returns is then meaningless).  C3-size free-intrinsics problem, one camera.
 
     PBA_LIBRARY=variants/libpba_fst.so python3 tools/probe/front_stamps.py
@@ -15,7 +15,7 @@ sys.path.insert(0, ROOT)
 synth = importlib.import_module("photometric-bundle-adjustment_amd.synth")
 E = importlib.import_module("photometric-bundle-adjustment_amd.engine")
 
-NAMES = ["chol", "bar A", "panel", "bar B", "trail+fresh", "bar C", "bwd dot", "bar 1", "bwd solve", "bar 2"]
+NAMES = ["loads", "-", "panel", "bar B", "trail|factor+fresh", "bar C", "bwd dot", "bar 1", "bwd solve", "bar 2"]
 
 if __name__ == "__main__":
     nf = int(sys.argv[1]) if len(sys.argv) > 1 else 200
@@ -30,7 +30,7 @@ if __name__ == "__main__":
         for _ in range(3):
             eng.gn_step(1e-3)
         dp, _ = eng.gn_last_step()
-    v = dp.ravel()[:20] * 10.0 / 1e3  # 100 MHz ticks → µs
+    v = dp.ravel()[:30] * 10.0 / 1e3  # 100 MHz ticks → µs
     ncol = nf + 2
-    for w, off in (("lane 0", 0), ("lane 64", 10)):
+    for w, off in (("lane 0", 0), ("lane 64", 10), ("lane 192", 20)):
         print(w, " ".join(f"{n}={v[off + i] / ncol:.3f}" for i, n in enumerate(NAMES)), "µs/column", flush=True)
