@@ -2160,13 +2160,16 @@ __global__ __launch_bounds__(256) void front_solve_kernel(const FrontArgs a) {
     FRONT_STAMP(7);
     __syncthreads();
     FRONT_STAMP(8);
-    if (tid == 0) {
+    if (tid < 64) {  // lanes 0-5 add the products of entry r in order, lane 0 solves
+      double tr = 0.0;
+      if (tid < 6) {
+        tr = st[fm * 36 + 42 + tid];
+        for (int li = 0; li < na; ++li) tr -= sp[li * 6 + tid];
+      }
       double t[6];
 #pragma unroll
-      for (int r = 0; r < 6; ++r) t[r] = st[fm * 36 + 42 + r];
-      for (int li = 0; li < na; ++li)
-#pragma unroll
-        for (int r = 0; r < 6; ++r) t[r] -= sp[li * 6 + r];
+      for (int r = 0; r < 6; ++r) t[r] = __shfl(tr, r, 64);
+      if (tid == 0) {
 #pragma unroll
       for (int r = 5; r >= 0; --r) {  // L_kkᵀ x = t
         double v = t[r];
@@ -2178,6 +2181,7 @@ __global__ __launch_bounds__(256) void front_solve_kernel(const FrontArgs a) {
       for (int r = 0; r < 6; ++r) {
         ys[6 * k + r] = t[r];
         a.x[6 * k + r] = t[r];
+      }
       }
     }
     if (k >= 1) store_stage(k - 1, cur);  // column k − 1's stage (not read at column k)
