@@ -4679,6 +4679,7 @@ int gn_prepare(pba_engine* e) {
   const int nfs = nf + 2 * nc;
   G.nc_sys = nc;
   G.nfs = nfs;
+  G.dsky_K = -1;  // the multi-GPU summed profile is rebuilt for this problem (ensure_dist_sky)
   for (int i = 0; i < nfs; ++i) contrib[{i, i}];  // every diagonal block exists
   std::vector<int> first(nfs), rowp(nfs + 1), last(nfs);
   for (int i = 0; i < nfs; ++i) first[i] = i < nf ? i : 0;
