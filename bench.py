@@ -543,6 +543,31 @@ def measure_traffic(args, n_blocks, timeout_s=150):
         "fetch_bytes": vals["FETCH_SIZE"], "write_bytes": vals["WRITE_SIZE"]}
 
 
+def stream_copy_peak(torch, dev, achieved):
+    """a measured streaming rate beside the 8 TB/s spec — a 1-GiB device-to-device tensor copy (read +
+    write = 2 GiB of HBM traffic per copy), the best of 5 timed by stream events after 3 untimed."""
+    try:
+        a = torch.empty(1 << 28, dtype=torch.float32, device=dev).fill_(1.0)
+        b = torch.empty_like(a)
+        for _ in range(3):
+            b.copy_(a)
+        best = None
+        for _ in range(5):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            b.copy_(a)
+            e1.record()
+            e1.synchronize()
+            ms = e0.elapsed_time(e1)
+            best = ms if best is None else min(best, ms)
+        gbs = 2.0 * a.numel() * 4 / (best * 1e-3) / 1e9
+        del a, b
+        return {"stream_copy_gbs": gbs, "frac_of_stream_copy": achieved / gbs,
+                "stream_copy_note": "torch device copy of 1 GiB (2 GiB read + write per copy), best of 5"}
+    except Exception as ex:  # diagnostic only
+        return {"stream_copy_error": f"{type(ex).__name__}: {ex}"[:200]}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -694,6 +719,10 @@ def main():
                     c2 = c2_dropin(full, images_host, host_cores()["usable"])
                 except Exception as ex:  # a secondary leg: report it, keep the headline line
                     c2 = {"error": f"{type(ex).__name__}: {ex}"[:300]}
+        stream_peak = stream_copy_peak(torch, dev, achieved)
+        # the GN leg's collective, as the leg chooses it (device-steered under RCCL unless PBA_BENCH_GN_COMM=0)
+        gn_comm = ("device-steered RCCL loop" if world > 1 and dist.get_backend() == "nccl"
+                   and os.environ.get("PBA_BENCH_GN_COMM", "1") != "0" else "torch.distributed between trials")
         out = {
             "metric": "photometric residual+jacobian blocks/sec",
             "value": value,
@@ -715,8 +744,8 @@ def main():
                 "keyframes": F, "points": Np, "patch": pb.P, "targets_per_point": K,
                 "blocks_total": total_blocks, "blocks_rank0": pb.n_blocks, "valid_blocks_rank0": int(valid.sum()),
                 "parallelism": f"host-keyframe shards x{world} (evaluation: no data-path collective; "
-                               f"GN: all-reduce of the reduced camera system, "
-                               f"{'device-steered RCCL loop' if os.environ.get('PBA_BENCH_GN_COMM') == '1' else 'torch.distributed between trials'})",
+                               + (f"GN: all-reduce of the reduced camera system — {gn_comm})" if world > 1
+                                  else "GN: one GPU)"),
             },
             "roofline": {
                 "bound": "hbm",
@@ -730,6 +759,7 @@ def main():
                 "bytes_per_block_alg": bpb,
                 "kernel_avg_us": kern_us,
                 "kernel_avg_us_max_over_ranks": kern_us_max,
+                **stream_peak,
                 **({"note": "rank 0's shard: its algorithmic bytes over its launch duration"} if world > 1 else {}),
             },
             "cpu_baseline": cpu,
