@@ -1865,7 +1865,8 @@ __device__ inline bool chol6_rcp(double* A, double* invd) {  // in place, lower;
 // from S (no earlier column touched them).  gn_prepare gives every row a static LDS slot (a row admitted for column k + 1
 // never takes a slot in use at column k) and writes per column a record: the slots, row indices and factor-block
 // indices of rows(k), and the fresh blocks of the next column's admissions (source skyline block → front position
-// slot_hi·F + slot_lo).  skyline_solve_kernel walks the same factorisation through global memory, a dependent L2
+// slot_hi·F + slot_lo) — build_front_plan; a multi-GPU free-intrinsics solve has a plan of its own for the summed
+// profile (ensure_dist_sky).  skyline_solve_kernel walks the same factorisation through global memory, a dependent L2
 // round trip per phase (≈ 9 µs per column); here the front, the forward vector and the records live in LDS and the
 // next column's fresh blocks and record are loaded while this column is factored.  Free intrinsics make the profile a
 // band plus 2·nc dense border rows: F = K + 1 + 2nc slots (C3/C4: 7).
@@ -1875,7 +1876,7 @@ __device__ inline bool chol6_rcp(double* A, double* invd) {  // in place, lower;
 // Forward (2 barriers per column): 6·|rows(k)| lanes form L_ik = A_ik L_kk⁻ᵀ row by row (to LDS, to L, v_i −= L_ik y_k);
 // then the trailing pairs A_ij −= L_ik L_jkᵀ while one lane finishes and factors the next diagonal block (look-ahead:
 // L_kk, reciprocal pivots and y_k = L_kk⁻¹ v_k were formed during column k − 1).
-// Backward (2 barriers per column): 6·|rows(k)| lanes form the products L_ikᵀ x_i, one lane adds them in order and
+// Backward (2 barriers per column): 6·|rows(k)| lanes form the products L_ikᵀ x_i, six lanes add them in order and one
 // solves x_k = L_kk⁻ᵀ (y_k − Σ_i L_ikᵀ x_i).
 constexpr int kFrontHdr = 3;
 struct FrontArgs {
