@@ -432,16 +432,16 @@ def intrinsics_engine(pb, state, fixed):
     return e
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world,model", [(2, 0), (3, 0), (2, 1), (2, 2), (2, 3)])
 @pytest.mark.parametrize("lam", [1e-4, 1e-1])
-def test_free_intrinsics_exchange_matches_single_engine_step(world, lam):
+def test_free_intrinsics_exchange_matches_single_engine_step(world, model, lam):
     """Free intrinsics on several GPUs (optimize_intrinsics, map_utils.h:339-345): each rank exports its keyframe band
     AND its undamped border rows (the cameras' intrinsics against every keyframe and camera, direct − Schur terms at λ,
     the direct diagonal, g, observed cameras) after the band; the importer builds the summed skyline system (band K +
     border) and solves it with its active front in LDS.  Every rank's pose step, candidate intrinsics and point steps
-    equal the single engine's."""
+    equal the single engine's (pinhole, double sphere, EUCM, KB4)."""
     import torch
-    pb, state = intrinsics_problem(14, 200, 23)
+    pb, state = intrinsics_problem(14, 200, 23, model)
     fixed = (0, 1)
     with intrinsics_engine(pb, state, fixed) as full:
         c_full = full.gn_linearize()
