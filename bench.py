@@ -290,7 +290,9 @@ def time_evaluation(eng, states, steps, warmup, clock_warmup_s, torch, dist, dev
     eng.evaluate_states_device(pp, rr, True, sync=False)
     host_diag["enqueue_us_per_step"] = 1e6 * (time.perf_counter() - t0) / steps
     e1.record(stream)
-    eng.synchronize()
+    # completion: ONE device-wide synchronize (it covers the engine's stream).  Round 5 synchronized the engine stream
+    # first and then the device: two wake-ups, ≈ 5 µs more per timed region (tools/probe/sync_probe.py,
+    # profiles/r6_sync_probe.txt: 17-20 µs of fixed cost per region against 23-25)
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     if dist is not None:
@@ -544,8 +546,28 @@ def measure_traffic(args, n_blocks, timeout_s=150):
 
 
 def stream_copy_peak(torch, dev, achieved):
-    """a measured streaming rate beside the 8 TB/s spec — a 1-GiB device-to-device tensor copy (read +
-    write = 2 GiB of HBM traffic per copy), the best of 5 timed by stream events after 3 untimed."""
+    """a measured streaming rate beside the 8 TB/s spec.  The reference point is a hand-written float4 copy
+    kernel (tools/micro/stream_copy.hip: 16-B loads, non-temporal 16-B stores, four moves per lane per iteration, 1 GiB,
+    the best of 5 launches at each of five grid sizes) — MI355X_MICROARCH.md's "float4 copy" measurement (6.29 TB/s
+    there), taken on this box; a torch device copy of the same size is reported beside it."""
+    import ctypes
+    out = {}
+    so = os.path.join(ROOT, "tools", "micro", "libstream_copy.so")
+    try:
+        lib = ctypes.CDLL(so)
+        lib.stream_copy_gbs.argtypes = [ctypes.c_size_t, ctypes.c_int, ctypes.POINTER(ctypes.c_double),
+                                        ctypes.POINTER(ctypes.c_int)]
+        g, grid = ctypes.c_double(0.0), ctypes.c_int(0)
+        torch.cuda.synchronize()
+        rc = lib.stream_copy_gbs(1 << 30, 5, ctypes.byref(g), ctypes.byref(grid))
+        if rc == 0 and g.value > 0:
+            out = {"stream_copy_gbs": g.value, "frac_of_stream_copy": achieved / g.value,
+                   "stream_copy_note": f"hand-written float4 copy kernel (16-B loads, non-temporal 16-B stores), 1 GiB "
+                                       f"(2 GiB of traffic per copy), best of 5 x 5 grid sizes ({grid.value} workgroups)"}
+        else:
+            out = {"stream_copy_error": f"stream_copy_gbs returned {rc}"}
+    except OSError as ex:
+        out = {"stream_copy_error": f"{so}: {ex}"[:200]}
     try:
         a = torch.empty(1 << 28, dtype=torch.float32, device=dev).fill_(1.0)
         b = torch.empty_like(a)
@@ -560,12 +582,11 @@ def stream_copy_peak(torch, dev, achieved):
             e1.synchronize()
             ms = e0.elapsed_time(e1)
             best = ms if best is None else min(best, ms)
-        gbs = 2.0 * a.numel() * 4 / (best * 1e-3) / 1e9
+        out["torch_copy_gbs"] = 2.0 * a.numel() * 4 / (best * 1e-3) / 1e9
         del a, b
-        return {"stream_copy_gbs": gbs, "frac_of_stream_copy": achieved / gbs,
-                "stream_copy_note": "torch device copy of 1 GiB (2 GiB read + write per copy), best of 5"}
     except Exception as ex:  # diagnostic only
-        return {"stream_copy_error": f"{type(ex).__name__}: {ex}"[:200]}
+        out["torch_copy_error"] = f"{type(ex).__name__}: {ex}"[:200]
+    return out
 
 
 def main():

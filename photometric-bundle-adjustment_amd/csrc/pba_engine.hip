@@ -132,15 +132,23 @@ __device__ __forceinline__ _Float16 rec_val<_Float16>(float v) {
 
 // Store a workgroup's contiguous record slab (LDS → global): 16-B non-temporal stores when the slab is 16-B
 // aligned, 4-B or 2-B stores otherwise (odd patterns in fp16).
+// wt (wave-uniform, KernelArgs::slab_wt): non-temporal write-through stores (`nt sc1`) — for launches of at most one
+// wave of workgroups (a 1/8 shard of C4: 8.29 → 8.07-8.15 µs, nothing left dirty in L2 for the kernel's end), never for
+// a full C4 launch (44.9 → 46.2 µs), DESIGN.md §3.
 template <class T, int NTH = kBlockThreads>
-__device__ __forceinline__ void store_slab(const unsigned char* src, unsigned char* dst, int bytes) {
+__device__ __forceinline__ void store_slab(const unsigned char* src, unsigned char* dst, int bytes, int wt = 0) {
   constexpr int kBlockThreads = NTH;  // the workgroup's threads share the slab
   if ((((uintptr_t)dst | (unsigned)bytes) & 15) == 0) {
     // non-temporal 16-B stores (write-through sc1 stores measured 49 → 71 µs for this kernel; per-lane stores
     // straight from registers, without the LDS slab, 49 → 104 µs: DESIGN.md §3)
     const f32x4* s4 = reinterpret_cast<const f32x4*>(src);
     f32x4* d4 = reinterpret_cast<f32x4*>(dst);
-    for (int i = threadIdx.x; i < (bytes >> 4); i += kBlockThreads) __builtin_nontemporal_store(s4[i], d4 + i);
+    if (wt) {
+      for (int i = threadIdx.x; i < (bytes >> 4); i += kBlockThreads)
+        asm volatile("global_store_dwordx4 %0, %1, off nt sc1" ::"v"(d4 + i), "v"(s4[i]) : "memory");
+    } else {
+      for (int i = threadIdx.x; i < (bytes >> 4); i += kBlockThreads) __builtin_nontemporal_store(s4[i], d4 + i);
+    }
   } else if (sizeof(T) == 4 || (((uintptr_t)dst | (unsigned)bytes) & 3) == 0) {
     const float* s1 = reinterpret_cast<const float*>(src);
     float* d1 = reinterpret_cast<float*>(dst);
@@ -230,7 +238,8 @@ __global__ __launch_bounds__(kBlockThreads) void photometric_block_kernel(const 
   __syncthreads();
   const int nblk = min(BPW, a.n_blocks - blk0);
   if (nblk <= 0) return;
-  store_slab<T>(lds, reinterpret_cast<unsigned char*>(out + (long long)blk0 * rec_f), nblk * rec_f * (int)sizeof(T));
+  store_slab<T>(lds, reinterpret_cast<unsigned char*>(out + (long long)blk0 * rec_f), nblk * rec_f * (int)sizeof(T),
+                a.slab_wt);
 }
 
 // Row px of a block's staged record (r | J_host row | J_target row | J_rho; T = float or _Float16), written by the lane
@@ -521,11 +530,12 @@ void launch_geometric(pba_engine* e, const KernelArgs& ka, int mode) {
 
 // PM = camera model + 4 · interpolator (pba_device.h)
 template <int PM>
-void launch_photometric(pba_engine* e, const KernelArgs& ka, int mode) {
+void launch_photometric(pba_engine* e, KernelArgs ka, int mode) {
   const bool h = e->record_format == PBA_RECORD_F16;
   if (e->P <= 8) {
     const int grid = (int)(((long long)e->n_blocks * 8 + kBlockThreads - 1) / kBlockThreads);
     e->last_grid = grid;
+    ka.slab_wt = grid <= kSlabWtGrid;  // one wave of workgroups: write-through record stores (store_slab)
     if (mode == 1 && h) photometric_block_kernel<PM, 8, 1, _Float16><<<grid, kBlockThreads, 0, e->stream>>>(ka);
     else if (mode == 1) photometric_block_kernel<PM, 8, 1, float><<<grid, kBlockThreads, 0, e->stream>>>(ka);
     else if (mode == 0 && h) photometric_block_kernel<PM, 8, 0, _Float16><<<grid, kBlockThreads, 0, e->stream>>>(ka);

@@ -163,6 +163,10 @@ __device__ __forceinline__ CamView cams_of(const TileBlockC& tb, const CamRec* t
   return {tab[tb.host_cam].hk, tab[tb.target_cam].tk, tab[tb.target_cam].kf};
 }
 
+// Workgroups of 256 threads in one full wave of the chip (256 CUs × 8 resident workgroups at the headline kernel's 60
+// VGPRs): launches up to this size store their record slabs write-through (store_slab).
+constexpr int kSlabWtGrid = 2048;
+
 struct KernelArgs {
   const uint8_t* images;
   int width, height, tiles_x;
@@ -195,6 +199,7 @@ struct KernelArgs {
   int n_cams;                    // cameras (photometric_block_kernel_multi's camera table: ≤ kCamTab)
   float huber;
   double* wg_red;  // residual-only launches of the LM loop: per-workgroup (Σ cost, Σ valid) at slot logical_tile()
+  int slab_wt;     // record slabs stored write-through (store_slab: grids of ≤ kSlabWtGrid workgroups)
   float pattern[2 * PBA_MAX_PATTERN];
 };
 
