@@ -2624,7 +2624,8 @@ __device__ __forceinline__ double ld_row(const double* p) {
 // D is SPD, so is every pivot block; all of P's pivots must be positive), then updates its other rows
 // a[r] −= Σ_j piv[r][j] t_j.  The publish / read round trip is paid M/PB times instead of M/2 times; the updates are
 // the same FMAs.
-template <int M, bool COH = false, int PB = kCrPivot>
+// b: NB right-hand-side columns, row-major (row r of column q at b[r·NB + q]); lanes 2M … M + ncol − 1 take them.
+template <int M, bool COH = false, int PB = kCrPivot, int NB = 1>
 __device__ __forceinline__ bool gj_wave(const double* __restrict__ D, const double* __restrict__ R1, bool r1_trans,
                                         const double* __restrict__ b, int ncol, int c, double* piv, double* a) {
   static_assert(M % PB == 0, "pivot blocks tile the system");
@@ -2642,8 +2643,8 @@ __device__ __forceinline__ bool gj_wave(const double* __restrict__ D, const doub
     }
   } else if (c >= 2 * M && c < M + ncol) {
     if (b) {
-      base = b;
-      stride = 1;
+      base = b + (c - 2 * M);
+      stride = NB;
     } else {
       zero = true;
     }
@@ -2716,11 +2717,12 @@ __device__ __forceinline__ bool gj_wave(const double* __restrict__ D, const doub
 // Rebuild of super-row i (next-level index in) from the two eliminations in LDS (sXl = X_{i−1}, sXr = X_{i+1}) and
 // U_{i−1}, U_i, D_i, b_i, on RB waves: 4 waves take two column tiles each, 8 waves one.  keep_u: the rebuilt row
 // still has a right coupling.  Waves w ≥ RB return at once.
-template <int M, int RB>
+template <int M, int RB, int NB = 1>
 __device__ __forceinline__ void cr_rebuild(int w, int lane, const double* sUl, const double* sUi, const double* sD,
                                            const double* sb, const double* sXl, const double* sXr, const CrLevel& Ln,
                                            int in, bool keep_u) {
-  constexpr int NC = 2 * M + 1;
+  constexpr int NC = 2 * M + NB;  // [D | U | b] columns: b's NB columns at 2M …
+  static_assert(NC <= 64, "four column tiles");
   // Rebuild of row i on the matrix cores: [D' | U' | b'] = [D | 0 | b] − U_{i−1}ᵀ·[X^U_{i−1} | 0 | X^b_{i−1}]
   // − U_i·X_{i+1}, as 2 × 4 output tiles of v_mfma_f64_16x16x4f64 (rows padded to 32, columns to 64).  Wave w takes
   // row tile w & 1 and column tiles TPW·(w >> 1) + {0 … TPW−1}: a wave's tiles share the A operands and run as
@@ -2747,7 +2749,7 @@ __device__ __forceinline__ void cr_rebuild(int w, int lane, const double* sUl, c
 #pragma unroll
     for (int v = 0; v < 4; ++v) {
       const int r = 16 * rt + (lane >> 4) + 4 * v;
-      cv[h][v] = c < M ? sD[min(r, M - 1) * M + c] : sb[min(r, M - 1)];
+      cv[h][v] = c < M ? sD[min(r, M - 1) * M + c] : sb[min(r, M - 1) * NB + min(max(c - 2 * M, 0), NB - 1)];
     }
   }
 #pragma unroll
@@ -2759,7 +2761,7 @@ __device__ __forceinline__ void cr_rebuild(int w, int lane, const double* sUl, c
     for (int h = 0; h < TPW; ++h) {
       const int c = bcol[h];
       bv2[h][s4] = sXr[q * NC + min(c, NC - 1)];
-      bv1[h][s4] = sXl[q * NC + (c < M ? M + c : 2 * M)];
+      bv1[h][s4] = sXl[q * NC + (c < M ? M + c : min(max(c, 2 * M), NC - 1))];
     }
   }
   v4f64 acc[TPW];
@@ -2769,7 +2771,7 @@ __device__ __forceinline__ void cr_rebuild(int w, int lane, const double* sUl, c
 #pragma unroll
     for (int v = 0; v < 4; ++v) {
       const int r = 16 * rt + (lane >> 4) + 4 * v;
-      acc[h][v] = (r < M && (c < M || c == 2 * M)) ? cv[h][v] : 0.0;
+      acc[h][v] = (r < M && (c < M || (c >= 2 * M && c < NC))) ? cv[h][v] : 0.0;
     }
   }
 #pragma unroll
@@ -2780,7 +2782,7 @@ __device__ __forceinline__ void cr_rebuild(int w, int lane, const double* sUl, c
     for (int h = 0; h < TPW; ++h) {
       const int c = bcol[h];
       const double b2 = c < NC ? bv2[h][s4] : 0.0;
-      const double b1 = (c < M || c == 2 * M) ? bv1[h][s4] : 0.0;
+      const double b1 = (c < M || (c >= 2 * M && c < NC)) ? bv1[h][s4] : 0.0;
       acc[h] = __builtin_amdgcn_mfma_f64_16x16x4f64(a2, b2, acc[h], 0, 0, 0);
       acc[h] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1, acc[h], 0, 0, 0);
     }
@@ -2793,7 +2795,7 @@ __device__ __forceinline__ void cr_rebuild(int w, int lane, const double* sUl, c
       if (r < M) {
         if (c < M) Ln.D[(long long)in * M * M + r * M + c] = acc[h][v];
         else if (c < 2 * M) Ln.U[(long long)in * M * M + r * M + (c - M)] = keep_u ? acc[h][v] : 0.0;
-        else if (c == 2 * M) Ln.b[(long long)in * M + r] = acc[h][v];
+        else if (c < NC) Ln.b[((long long)in * M + r) * NB + (c - 2 * M)] = acc[h][v];
       }
     }
 }
@@ -2802,8 +2804,8 @@ __device__ __forceinline__ void cr_rebuild(int w, int lane, const double* sUl, c
 template <int M>
 constexpr int kPivBuf = M * kCrPivot;
 
-template <int M>
-constexpr size_t cr_level_wave_lds() { return sizeof(double) * (3 * M * M + M + 2 * M * (2 * M + 1)); }
+template <int M, int NB = 1>
+constexpr size_t cr_level_wave_lds() { return sizeof(double) * (3 * M * M + M * NB + 2 * M * (2 * M + NB)); }
 
 // One level, 4 waves per rebuilt super-row i: wave 0 eliminates its left neighbour l on [D | U_l | b] (X^U, X^b),
 // waves 1 and 2 its right neighbour r on [D | U_iᵀ | b] (X^L, X^b) and [D | U_r] (X^U) — D's columns replicated per
@@ -2817,16 +2819,19 @@ constexpr size_t cr_level_wave_lds() { return sizeof(double) * (3 * M * M + M + 
 // The D_i' are Schur complements of SPD principal submatrices ({l, i, r}), so every pivot block stays SPD.
 // The level's work for row i (rebuilt as row `in` of Ln) by a 4-wave workgroup: piv = 3 × M·kCrPivot doubles, smem =
 // cr_level_wave_lds<M>() bytes.
-template <int M, bool PCR>
+// NB > 1 (PCR only): b holds NB right-hand-side columns (row-major, b[(i·M + r)·NB + q]) — the free-intrinsics
+// arrow solve's [−g | border columns] (arrow_solve).
+template <int M, bool PCR, int NB = 1>
 __device__ __forceinline__ void cr_wave_level(const CrLevel& L, const CrLevel& Ln, int i, int in, int s, int* status,
                                               double (*piv)[kPivBuf<M>], double* smem) {
-  static_assert(2 * M + 1 <= 64, "one wave per elimination");
-  constexpr int NC = 2 * M + 1;
+  static_assert(2 * M + NB <= 64, "one wave per elimination");
+  static_assert(PCR || NB == 1, "the back-substitution's X has one right-hand side");
+  constexpr int NC = 2 * M + NB;
   double* sUl = smem;
   double* sUi = sUl + M * M;
   double* sD = sUi + M * M;
   double* sb = sD + M * M;
-  double* sX[2] = {sb + M, sb + M + M * NC};
+  double* sX[2] = {sb + M * NB, sb + M * NB + M * NC};
   const int il = i - s, ir = i + s;
   const bool left = il >= 0, right = ir < L.n;
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -2836,16 +2841,16 @@ __device__ __forceinline__ void cr_wave_level(const CrLevel& L, const CrLevel& L
   if (w == 3) {
     // U_l, U_i, D_i, b_i → LDS: every load in flight at once (a loop of load → LDS store pays one memory round trip
     // per element, serially: measured ~10 µs of a 12.4-µs level); missing neighbours read U_i and store zeros
-    constexpr int NE = 3 * M * M + M, NQ = (NE + 63) / 64;
+    constexpr int NE = 3 * M * M + M * NB, NQ = (NE + 63) / 64;
     double v[NQ];
 #pragma unroll
     for (int q = 0; q < NQ; ++q) {
       const int e = lane + 64 * q;
-      const double* src = L.b + (long long)i * M;
+      const double* src = L.b + (long long)i * M * NB;
       if (e < M * M) src = L.U + (long long)(left ? il : i) * M * M + e;
       else if (e < 2 * M * M) src = L.U + (long long)i * M * M + (e - M * M);
       else if (e < 3 * M * M) src = L.D + (long long)i * M * M + (e - 2 * M * M);
-      else if (e < NE) src = L.b + (long long)i * M + (e - 3 * M * M);
+      else if (e < NE) src = L.b + (long long)i * M * NB + (e - 3 * M * M);
       v[q] = *src;
     }
 #pragma unroll
@@ -2859,15 +2864,15 @@ __device__ __forceinline__ void cr_wave_level(const CrLevel& L, const CrLevel& L
     const bool has = w == 0 ? left : right;
     const int jj = has ? j : i;  // a missing neighbour eliminates a real row and contributes zeros
     const double* D = L.D + (long long)jj * M * M;
-    const double* bj = L.b + (long long)jj * M;
+    const double* bj = L.b + (long long)jj * M * NB;
     double a[M];
     bool ok;
-    if (w == 0) ok = gj_wave<M>(D, L.U + (long long)jj * M * M, false, bj, M + 1, lane, piv[0], a);
-    else if (w == 1) ok = gj_wave<M>(D, L.U + (long long)i * M * M, true, bj, M + 1, lane, piv[1], a);
+    if (w == 0) ok = gj_wave<M, false, kCrPivot, NB>(D, L.U + (long long)jj * M * M, false, bj, M + NB, lane, piv[0], a);
+    else if (w == 1) ok = gj_wave<M, false, kCrPivot, NB>(D, L.U + (long long)i * M * M, true, bj, M + NB, lane, piv[1], a);
     else ok = gj_wave<M>(D, jj + s < L.n ? L.U + (long long)jj * M * M : nullptr, false, nullptr, M, lane, piv[2], a);
     if (!ok && has && lane == 0) atomicOr(status, 1);
-    if (lane >= M && lane < 2 * M + (w == 2 ? 0 : 1)) {
-      const int col = lane < 2 * M ? (w == 1 ? lane - M : lane) : 2 * M;
+    if (lane >= M && lane < 2 * M + (w == 2 ? 0 : NB)) {
+      const int col = lane < 2 * M ? (w == 1 ? lane - M : lane) : lane;  // (b's columns keep their lane index)
       double* x = sX[w == 0 ? 0 : 1] + col;
 #pragma unroll
       for (int r = 0; r < M; ++r) x[r * NC] = has ? a[r] : 0.0;
@@ -2885,7 +2890,7 @@ __device__ __forceinline__ void cr_wave_level(const CrLevel& L, const CrLevel& L
 #ifdef PBA_CR_STAMPS
   t2 = wall_clock64();
 #endif
-  cr_rebuild<M, 4>(w, lane, sUl, sUi, sD, sb, sX[0], sX[1], Ln, in, PCR ? i + 2 * s < L.n : right);
+  cr_rebuild<M, 4, NB>(w, lane, sUl, sUi, sD, sb, sX[0], sX[1], Ln, in, PCR ? i + 2 * s < L.n : right);
 #ifdef PBA_CR_STAMPS
   __syncthreads();
   const long long t3 = wall_clock64();
@@ -2898,29 +2903,30 @@ __device__ __forceinline__ void cr_wave_level(const CrLevel& L, const CrLevel& L
 // out != nullptr (the last PCR level): the workgroup then also solves its decoupled row, x_i = D'_i⁻¹ b'_i, from the
 // rows it has just written (read back with L1-bypassing loads after every wave's stores completed) — pcr_solve_kernel's
 // work without its launch boundary and its reload of the level (out / lim as pcr_solve_kernel).
-template <int M, bool PCR>
+// NB > 1: out row t = i·M + r holds the NB solution columns at out[t·ld + q].
+template <int M, bool PCR, int NB = 1>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void cr_level_wave_kernel(
-    CrLevel L, CrLevel Ln, int s, int* status, double* __restrict__ out, int lim) {
+    CrLevel L, CrLevel Ln, int s, int* status, double* __restrict__ out, int lim, int ld = 1) {
   __shared__ __attribute__((aligned(16))) double piv[3][kPivBuf<M>];
   extern __shared__ double smem[];
   const int i = PCR ? (int)blockIdx.x : 2 * (int)blockIdx.x;
-  cr_wave_level<M, PCR>(L, Ln, i, blockIdx.x, PCR ? s : 1, status, piv, smem);
+  cr_wave_level<M, PCR, NB>(L, Ln, i, blockIdx.x, PCR ? s : 1, status, piv, smem);
   if (!PCR || !out) return;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's row stores have completed
   __syncthreads();
   if (threadIdx.x >= 64) return;
   const int lane = threadIdx.x;
   double a[M];
-  const bool ok = gj_wave<M, true>(Ln.D + (long long)i * M * M, nullptr, false, Ln.b + (long long)i * M, M + 1, lane,
-                                   piv[0], a);
+  const bool ok = gj_wave<M, true, kCrPivot, NB>(Ln.D + (long long)i * M * M, nullptr, false, Ln.b + (long long)i * M * NB,
+                                                 M + NB, lane, piv[0], a);
   if (!ok) {
     if (lane == 0) atomicOr(status, 1);
     return;
   }
-  if (lane == 2 * M)
+  if (lane >= 2 * M && lane < 2 * M + NB)
 #pragma unroll
     for (int r = 0; r < M; ++r)
-      if (i * M + r < lim) out[(long long)i * M + r] = a[r];
+      if (i * M + r < lim) out[((long long)i * M + r) * ld + (lane - 2 * M)] = a[r];
 }
 
 // The root super-row on one wave (lane 2M carries b; the coupling lanes are empty).
@@ -2941,20 +2947,22 @@ __global__ __launch_bounds__(64) void cr_root_wave_kernel(CrLevel L, int* status
 
 // The last PCR level's decoupled rows: x_i = D_i⁻¹ b_i, one wave per row; x in the level-0 layout is the step itself
 // (out = the step vector, lim = 6N), else the x of the CR level the PCR levels took over from.
-template <int M>
-__global__ __launch_bounds__(64) void pcr_solve_kernel(CrLevel L, double* __restrict__ out, int lim, int* status) {
+template <int M, int NB = 1>
+__global__ __launch_bounds__(64) void pcr_solve_kernel(CrLevel L, double* __restrict__ out, int lim, int* status,
+                                                       int ld = 1) {
   __shared__ __attribute__((aligned(16))) double piv[kPivBuf<M>];
   const int lane = threadIdx.x, i = blockIdx.x;
   double a[M];
-  const bool ok = gj_wave<M>(L.D + (long long)i * M * M, nullptr, false, L.b + (long long)i * M, M + 1, lane, piv, a);
+  const bool ok = gj_wave<M, false, kCrPivot, NB>(L.D + (long long)i * M * M, nullptr, false, L.b + (long long)i * M * NB,
+                                                  M + NB, lane, piv, a);
   if (!ok) {
     if (lane == 0) atomicOr(status, 1);
     return;
   }
-  if (lane == 2 * M)
+  if (lane >= 2 * M && lane < 2 * M + NB)
 #pragma unroll
     for (int r = 0; r < M; ++r)
-      if (i * M + r < lim) out[(long long)i * M + r] = a[r];
+      if (i * M + r < lim) out[((long long)i * M + r) * ld + (lane - 2 * M)] = a[r];
 }
 
 // The root super-row (the last level): x = D⁻¹ b.
@@ -3024,6 +3032,179 @@ __global__ __launch_bounds__(1024) void cr_back_tail_kernel(const CrLevels C, in
     for (int t = threadIdx.x; t < lim; t += blockDim.x) cr_back_row<M>(L, C.lv[l + 1].x, out, t);
     __syncthreads();  // this level's x is read by the next (lower) level
   }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Free intrinsics as an arrow system (map_utils.h:339-345)
+// ------------------------------------------------------------------------------------------------
+// With free intrinsics the reduced camera system is S = [A B; Bᵀ C]: A the keyframes' band (bandwidth ≤ 4 keyframes), B
+// the 2·nc border frames' coupling to every keyframe (dense columns), C the border's own 12nc × 12nc block.  The skyline
+// factorisation (front_solve_kernel) walks the whole system column by column — one workgroup, ~3.5 µs per keyframe,
+// 3.64 ms at C4.  Eliminating the keyframes first is the same factorisation order (border last), so instead:
+//   X = A⁻¹ [−g_a | B]          parallel cyclic reduction over the band, the border's 12nc columns as extra right-hand
+//                               sides (cr_level_wave_kernel<24, true, kArrowNB>: [D | U | b] = 24 + 24 + 16 lanes),
+//                               in batches of kArrowNB columns;
+//   Sc = C − BᵀX_B,  rc = −g_c − BᵀX_0,  δc = Sc⁻¹ rc     (arrow_reduce_kernel: a workgroup per product;
+//                               arrow_cap_kernel: one workgroup, dense Cholesky of the ≤ 48 × 48 border system);
+//   δa = X_0 − X_B δc           (arrow_back_kernel).
+// The skyline S stays the assembled system (pba_gn_reduced_system, the multi-GPU export read it), g its gradient.
+constexpr int kArrowNB = 16;   // right-hand-side columns per cyclic-reduction run (2·24 + 16 = 64 lanes)
+constexpr int kArrowMaxNc = 4; // border of ≤ 48 unknowns (arrow_cap_kernel's LDS system)
+
+struct ArrowArgs {
+  const double* S;       // skyline system (lower blocks; block (i, j) at (row[i] + j − first[i])·36, element r·6 + c)
+  const int* first;
+  const int* row;
+  const double* g;       // gradient, 6 per system frame
+  const uint8_t* fixed;  // constant keyframes (their border coupling is dropped: identity rows of S)
+  CrLevel L0;            // level 0 of the band (D, U, b of kArrowNB columns)
+  double* X;             // 6·nf rows × ldx: A⁻¹[−g_a | B]
+  double* part;          // n_ent products (arrow_reduce_kernel)
+  double* dc;            // the border step (12nc)
+  double* x;             // the step, 6 per system frame
+  int* status;
+  int nf, nc, ldx, n_ent;
+};
+
+// Level 0 of the band (super-rows of 4 keyframes, identity padding past the last keyframe) and the batch's kArrowNB
+// right-hand-side columns: global column 0 = −g_a, 1 + q = column q of B (border frame nf + q/6, component q % 6),
+// B[6f + r][q] = S(border row, keyframe f)[q % 6][r].  du: also D and U (the first batch; later batches reuse them).
+__global__ __launch_bounds__(256) void arrow_build_kernel(const ArrowArgs a, int batch, int du) {
+  constexpr int M = 24, B = 4, NB = kArrowNB;
+  const long long tid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const int n = a.L0.n;
+  if (tid == 0 && batch == 0) *a.status = 0;
+  auto blk = [&](int i, int j, int r, int c) -> double {  // S[6i + r][6j + c], i ≥ j, 0 outside the profile
+    return j >= a.first[i] ? a.S[((long long)a.row[i] + (j - a.first[i])) * 36 + r * 6 + c] : 0.0;
+  };
+  const long long nDU = (long long)n * M * M;
+  if (tid < 2 * nDU) {
+    if (!du) return;
+    const bool isU = tid >= nDU;
+    const long long e0 = isU ? tid - nDU : tid;
+    const int I = (int)(e0 / (M * M)), e = (int)(e0 % (M * M)), R = e / M, C = e % M;
+    const int i = I * B + R / 6, r = R % 6, c = C % 6;
+    double v;
+    if (!isU) {
+      const int j = I * B + C / 6;
+      if (i >= a.nf || j >= a.nf) v = (i == j && r == c) ? 1.0 : 0.0;
+      else v = i >= j ? blk(i, j, r, c) : blk(j, i, c, r);
+      a.L0.D[e0] = v;
+    } else {
+      const int j = (I + 1) * B + C / 6;
+      a.L0.U[e0] = (I + 1 < n && i < a.nf && j < a.nf) ? blk(j, i, c, r) : 0.0;
+    }
+    return;
+  }
+  const long long t = tid - 2 * nDU;
+  if (t >= (long long)n * M * NB) return;
+  const int q = (int)(t % NB), R = (int)((t / NB) % M), I = (int)(t / ((long long)NB * M));
+  const int i = I * B + R / 6, r = R % 6, gq = NB * batch + q;
+  double v = 0.0;
+  if (i < a.nf && !a.fixed[i]) {
+    if (gq == 0) v = -a.g[6 * i + r];
+    else if (gq <= 12 * a.nc) v = blk(a.nf + (gq - 1) / 6, i, (gq - 1) % 6, r);
+  }
+  a.L0.b[t] = v;
+}
+
+// One workgroup per product: entry e < nb(nb+1)/2 — (q1 ≥ q2) of BᵀX_B — then e − that: q1 of BᵀX_0 (nb = 12nc), a dot
+// product over the T = 6nf keyframe rows (thread k takes rows k, k + 256, …; xor butterflies per wave, the four waves
+// in order: a fixed order).
+__global__ __launch_bounds__(256) void arrow_reduce_kernel(const ArrowArgs a) {
+  __shared__ double s_w[4];
+  const int nb = 12 * a.nc, nsym = nb * (nb + 1) / 2, T = 6 * a.nf, e = blockIdx.x;
+  int q1, xc;
+  if (e < nsym) {
+    q1 = (int)((sqrt(8.0 * e + 1.0) - 1.0) * 0.5);
+    while (q1 * (q1 + 1) / 2 > e) --q1;
+    while ((q1 + 1) * (q1 + 2) / 2 <= e) ++q1;
+    xc = 1 + (e - q1 * (q1 + 1) / 2);  // X column of q2
+  } else {
+    q1 = e - nsym;
+    xc = 0;
+  }
+  const int p = a.nf + q1 / 6, c = q1 % 6;
+  const double* Sp = a.S + (long long)a.row[p] * 36 + c * 6;  // border row p starts at frame 0
+  double acc = 0.0;
+  for (int tt = threadIdx.x; tt < T; tt += 256) acc += Sp[(long long)(tt / 6) * 36 + tt % 6] * a.X[(long long)tt * a.ldx + xc];
+  for (int m = 32; m >= 1; m >>= 1) acc += __shfl_xor(acc, m, 64);
+  if ((threadIdx.x & 63) == 0) s_w[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) a.part[e] = ((s_w[0] + s_w[1]) + s_w[2]) + s_w[3];
+}
+
+// The border system Sc = C − BᵀX_B, rc = −g_c − BᵀX_0 (partials added in workgroup order), its Cholesky in LDS and
+// δc = Sc⁻¹ rc (the border's part of the step); one workgroup.
+__global__ __launch_bounds__(256) void arrow_cap_kernel(const ArrowArgs a) {
+  constexpr int NBM = 12 * kArrowMaxNc;
+  __shared__ double sc[NBM][NBM + 1];
+  __shared__ double rc[NBM];
+  __shared__ int bad;
+  const int nb = 12 * a.nc, nsym = nb * (nb + 1) / 2, tid = threadIdx.x;
+  if (tid == 0) bad = 0;
+  for (int e = tid; e < a.n_ent; e += blockDim.x) {
+    const double acc = a.part[e];
+    if (e < nsym) {
+      int q1 = (int)((sqrt(8.0 * e + 1.0) - 1.0) * 0.5);
+      while (q1 * (q1 + 1) / 2 > e) --q1;
+      while ((q1 + 1) * (q1 + 2) / 2 <= e) ++q1;
+      const int q2 = e - q1 * (q1 + 1) / 2;
+      const int p1 = a.nf + q1 / 6, c1 = q1 % 6, p2 = a.nf + q2 / 6, c2 = q2 % 6;  // p1 ≥ p2
+      const double C = a.S[((long long)a.row[p1] + (p2 - a.first[p1])) * 36 + c1 * 6 + c2];
+      sc[q1][q2] = sc[q2][q1] = C - acc;
+    } else {
+      const int q1 = e - nsym;
+      rc[q1] = -a.g[6 * (a.nf + q1 / 6) + q1 % 6] - acc;
+    }
+  }
+  __syncthreads();
+  // right-looking Cholesky (lower), column by column
+  for (int k = 0; k < nb; ++k) {
+    if (tid == 0) {
+      const double d = sc[k][k];
+      if (!(d > 0.0)) bad = 1;
+      sc[k][k] = sqrt(fmax(d, 1e-300));
+    }
+    __syncthreads();
+    const double lkk = sc[k][k];
+    for (int i = k + 1 + tid; i < nb; i += blockDim.x) sc[i][k] /= lkk;
+    __syncthreads();
+    const int m = nb - k - 1;
+    for (int idx = tid; idx < m * m; idx += blockDim.x) {
+      const int i = k + 1 + idx / m, j = k + 1 + idx % m;
+      if (j <= i) sc[i][j] -= sc[i][k] * sc[j][k];
+    }
+    __syncthreads();
+  }
+  if (tid == 0) {  // L y = rc, Lᵀ δ = y
+    for (int i = 0; i < nb; ++i) {
+      double v = rc[i];
+      for (int j = 0; j < i; ++j) v -= sc[i][j] * rc[j];
+      rc[i] = v / sc[i][i];
+    }
+    for (int i = nb - 1; i >= 0; --i) {
+      double v = rc[i];
+      for (int j = i + 1; j < nb; ++j) v -= sc[j][i] * rc[j];
+      rc[i] = v / sc[i][i];
+    }
+    if (bad) atomicOr(a.status, 2);
+  }
+  __syncthreads();
+  for (int q = tid; q < nb; q += blockDim.x) {
+    a.dc[q] = rc[q];
+    a.x[6 * a.nf + q] = rc[q];
+  }
+}
+
+// δa = X_0 − X_B δc, one lane per keyframe unknown.
+__global__ __launch_bounds__(256) void arrow_back_kernel(const ArrowArgs a) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= 6 * a.nf) return;
+  const double* Xt = a.X + (long long)t * a.ldx;
+  double v = Xt[0];
+  for (int q = 0; q < 12 * a.nc; ++q) v -= Xt[1 + q] * a.dc[q];
+  a.x[t] = v;
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -3602,24 +3783,28 @@ __device__ __forceinline__ void border_store(const IntrBorderArgs& a, double lam
   a.S[((long long)a.sky_row[P] + (y - a.sky_first[P])) * 36 + e] = val;
 }
 
-// The keyframe blocks (P, y < nf): ONE WAVE per block (grid x: y, 4 per workgroup; y: camera c; NR = 6 → border row
-// 2c, NR = 2 → row 2c + 1, whose frame holds intrinsics 6, 7 and four pads), all 6·NR live entries at once — a lane
-// takes every 64th entry of the block's lists (the keyframe's blocks and points seen by the camera), the wave adds its
-// lanes' sums by xor butterflies (a fixed order) and lane e stores entry e.  (One wave per ENTRY re-walked each list 36
-// times: 0.5 ms per launch at C3.)
+// The keyframe blocks (P, y < nf): kpw WAVES per block (grid x: 4/kpw keyframes per workgroup; y: camera c; NR = 6 →
+// border row 2c, NR = 2 → row 2c + 1, whose frame holds intrinsics 6, 7 and four pads), all 6·NR live entries at once —
+// a lane takes every (64·kpw)th entry of the block's lists (the keyframe's blocks and points seen by the camera), each
+// wave adds its lanes' sums by xor butterflies and the kpw waves' sums are added in order (a fixed order), lane e stores
+// entry e.  kpw = 4 while the keyframe waves would not fill the SIMDs (C3, 200 keyframes: 95 → 40 µs per launch), else 1
+// (C4: 1004 waves; four per keyframe re-read the lists' data at 4× the waves, 133 → 160 µs).  (One wave per ENTRY
+// re-walked each list 36 times: 0.5 ms per launch at C3.)
 template <int NR>
-__global__ __launch_bounds__(256) void intr_border_kernel(const IntrBorderArgs a, double lambda) {
+__global__ __launch_bounds__(256) void intr_border_kernel(const IntrBorderArgs a, double lambda, int kpw) {
+  __shared__ double2 s_w[4][36];
   lambda = lm_lambda(lm_view(a.lm), lambda);
-  const int c = blockIdx.y, row = 2 * c + (NR == 6 ? 0 : 1), h = row & 1, lane = threadIdx.x & 63;
-  const int y = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
-  if (y >= a.nf) return;
+  const int c = blockIdx.y, row = 2 * c + (NR == 6 ? 0 : 1), h = row & 1, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int gw = blockIdx.x * 4 + w, y0 = gw / kpw, sub = gw % kpw;
+  const int y = min(y0, a.nf - 1);  // (a wave past the last keyframe walks nothing and stores nothing)
   const int L = c * (a.nf + a.nc) + y;
+  const int q0 = sub * 64 + lane, dq = y0 < a.nf ? 64 * kpw : 1 << 30;
   double dir[NR][6], sch[NR][6];
 #pragma unroll
   for (int r = 0; r < NR; ++r)
 #pragma unroll
     for (int cc = 0; cc < 6; ++cc) dir[r][cc] = sch[r][cc] = 0.0;
-  for (int q = a.bptr[L] + lane; q < a.bptr[L + 1]; q += 64) {
+  for (int q = a.bptr[L] + (y0 < a.nf ? q0 : 1 << 30); q < a.bptr[L + 1]; q += dq) {
     const int b = a.blist[q];
     const double* B = a.ib + (long long)b * kIbStride;
     const double* Jc = B + (a.ib_rec[b].z == y ? kIbJh : kIbJt);
@@ -3636,7 +3821,7 @@ __global__ __launch_bounds__(256) void intr_border_kernel(const IntrBorderArgs a
       for (int cc = 0; cc < 6; ++cc) dir[r][cc] += j0 * c0[cc] + j1 * c1[cc];
     }
   }
-  for (int q = a.pptr[L] + lane; q < a.pptr[L + 1]; q += 64) {
+  for (int q = a.pptr[L] + (y0 < a.nf ? q0 : 1 << 30); q < a.pptr[L + 1]; q += dq) {
     const int gp = a.plist[q];
     const int4 pr = a.pt_rec[gp];
     double wc[NR], wy[6];  // W of the point for the camera's columns 6h + r (Σ W_i over its blocks
@@ -3676,7 +3861,19 @@ __global__ __launch_bounds__(256) void intr_border_kernel(const IntrBorderArgs a
       vd = lane == r * 6 + cc ? d : vd;
       vs = lane == r * 6 + cc ? sc : vs;
     }
-  if (lane < 36) border_store(a, lambda, row, y * 36 + lane, vd, vs);
+  if (kpw == 1) {
+    if (lane < 36 && y0 < a.nf) border_store(a, lambda, row, y * 36 + lane, vd, vs);
+    return;
+  }
+  if (lane < 36) s_w[w][lane] = make_double2(vd, vs);
+  __syncthreads();
+  if (sub != 0 || lane >= 36 || y0 >= a.nf) return;
+  double2 t = s_w[w][lane];
+  for (int k = 1; k < kpw; ++k) {
+    t.x += s_w[w + k][lane].x;
+    t.y += s_w[w + k][lane].y;
+  }
+  border_store(a, lambda, row, y * 36 + lane, t.x, t.y);
 }
 
 // The camera blocks (P, y ≥ nf) and the gradient of P: their lists hold ALL of a camera's blocks and points (80k / 20k at
@@ -3684,7 +3881,7 @@ __global__ __launch_bounds__(256) void intr_border_kernel(const IntrBorderArgs a
 // for yb = 2nc; y: camera c, NR as intr_border_kernel; z: split s), thread k of split s taking list entries k + 256·s,
 // + 256·kIbSplit, …, all 6·NR entries at once; the workgroup's totals (wave butterflies, then its four waves in order)
 // go to part, and intr_border_fin_kernel adds the kIbSplit totals in order — a fixed order end to end.
-constexpr int kIbSplit = 32;
+constexpr int kIbSplit = 256;  // (32 until round 5: 96 workgroups for one camera, 195 µs per launch at C4)
 template <int NR>
 __global__ __launch_bounds__(256) void intr_border_cam_kernel(const IntrBorderArgs a, double lambda, double2* part) {
   __shared__ double2 s_w[4][36];
@@ -4329,6 +4526,8 @@ int gn_ppl(const pba_engine* e) { return e->opt.residual_kind == PBA_RESIDUAL_GE
 
 int band_kernel_for(int band) { return band <= 4 ? 4 : (band <= 8 ? 8 : (band <= 16 ? 16 : 0)); }
 
+int configure_arrow(pba_engine* e);  // (free intrinsics' arrow solve, below)
+
 // Reduced-system solver buffers for band K (0: skyline only): band input Sband (row stride (K+1)·36 + 6,
 // zero outside the profile), band-Cholesky column records, cyclic-reduction levels.
 int configure_solver(pba_engine* e, int K, int solver) {
@@ -4878,6 +5077,9 @@ int gn_prepare(pba_engine* e) {
     else if (f == "cr" && K && K <= 8) solver = SOLVER_CR;
   }
   if (int rc = configure_solver(e, solver == SOLVER_SKYLINE ? 0 : K, solver)) return rc;
+  G.ar_n = G.ar_batches = 0;  // free intrinsics: the arrow solve's buffers (arrow_for decides per solve)
+  if (nc > 0 && nc <= kArrowMaxNc)
+    if (int rc = configure_arrow(e)) return rc;
   PBA_HIP(G.observed.upload(std::vector<uint8_t>(observed.begin(), observed.end()), st));
   std::vector<uint8_t> req(nf, 0);
   for (int i = 0; i < nf && i < (int)G.fixed_h.size(); ++i) req[i] = G.fixed_h[i];
@@ -5130,6 +5332,69 @@ void cr_solve(pba_engine* e, bool build) {
   }
 }
 
+// Free intrinsics: the arrow solve's buffers (gn_prepare; nf keyframes, nc ≤ kArrowMaxNc cameras).
+int configure_arrow(pba_engine* e) {
+  GnData& G = e->gn;
+  constexpr int M = 24, NB = kArrowNB;
+  const int nf = e->n_frames, nc = G.nc_sys, nb = 12 * nc;
+  G.ar_n = (nf + 3) / 4;
+  G.ar_batches = (1 + nb + NB - 1) / NB;
+  const size_t lvl = (size_t)G.ar_n * M * M * 2 + (size_t)G.ar_n * M * NB;
+  PBA_HIP(G.ar_buf.resize(3 * lvl));
+  PBA_HIP(G.ar_X.resize((size_t)6 * nf * NB * G.ar_batches));
+  PBA_HIP(G.ar_part.resize((size_t)(nb * (nb + 1) / 2 + nb)));
+  PBA_HIP(G.ar_dc.resize((size_t)nb));
+  return PBA_OK;
+}
+
+// Whether a free-intrinsics system of keyframe bandwidth K is solved as an arrow (arrow_solve): K ≤ 4 (super-rows of 4
+// keyframes, M = 24), ≤ kArrowMaxNc cameras, and PBA_SOLVER does not force the skyline solvers ("skyline" / "front":
+// the A/B tests of the three solvers).
+bool arrow_for(const pba_engine* e, int K) {
+  const GnData& G = e->gn;
+  if (!G.nc_sys || G.nc_sys > kArrowMaxNc || K > 4 || !G.ar_n) return false;
+  const char* fs = getenv("PBA_SOLVER");
+  return !(fs && (std::string(fs) == "skyline" || std::string(fs) == "front"));
+}
+
+// X = A⁻¹[−g_a | B] by parallel cyclic reduction (batches of kArrowNB columns), the border system, the step into G.x
+// (the kernels above).  S, first, row: the skyline system and its profile; fixed: the constant frames.
+int arrow_solve(pba_engine* e, const double* S, const int* first, const int* row, const uint8_t* fixed) {
+  GnData& G = e->gn;
+  constexpr int M = 24, NB = kArrowNB;
+  const int nf = e->n_frames, nc = G.nc_sys, n = G.ar_n, nb = 12 * nc;
+  hipStream_t st = e->stream;
+  const size_t lvl = (size_t)n * M * M * 2 + (size_t)n * M * NB;
+  auto level = [&](int k) {
+    double* p = G.ar_buf.p + k * lvl;
+    return CrLevel{p, p + (size_t)n * M * M, p + (size_t)2 * n * M * M, nullptr, nullptr, n};
+  };
+  ArrowArgs aa{S, first, row, G.g.p, fixed, level(0), G.ar_X.p, G.ar_part.p, G.ar_dc.p, G.x.p, G.status.p,
+               nf, nc, NB * G.ar_batches, nb * (nb + 1) / 2 + nb};
+  constexpr size_t lds = cr_level_wave_lds<M, NB>();
+  static_assert(lds <= 65536, "default dynamic LDS limit");
+  const long long nth = 2LL * n * M * M + (long long)n * M * NB;
+  for (int bt = 0; bt < G.ar_batches; ++bt) {
+    arrow_build_kernel<<<(unsigned)((nth + 255) / 256), 256, 0, st>>>(aa, bt, bt == 0);
+    double* out = G.ar_X.p + NB * bt;
+    CrLevel src = level(0);
+    if (n <= 1) pcr_solve_kernel<M, NB><<<n, 64, 0, st>>>(src, out, 6 * nf, G.status.p, aa.ldx);
+    int pi = 1;
+    for (int s = 1; s < n; s *= 2, pi = 3 - pi) {  // the last level also solves the decoupled rows
+      const CrLevel dst = level(pi);
+      const bool last = 2 * s >= n;
+      cr_level_wave_kernel<M, true, NB><<<n, 256, lds, st>>>(src, dst, s, G.status.p, last ? out : nullptr, 6 * nf,
+                                                              aa.ldx);
+      src = dst;
+    }
+  }
+  arrow_reduce_kernel<<<aa.n_ent, 256, 0, st>>>(aa);
+  arrow_cap_kernel<<<1, 256, 0, st>>>(aa);
+  arrow_back_kernel<<<(6 * nf + 255) / 256, 256, 0, st>>>(aa);
+  PBA_HIP(hipGetLastError());
+  return PBA_OK;
+}
+
 // After a solve into G.x: solver status, candidate poses/points, and the two parts of the LM model decrease
 // L(0) − L(δ) = −gᵀδ − ½δᵀHδ = ½(λ δᵀDδ − gᵀδ)  (since (H + λD)δ = −g): pose part and point part.
 // Candidate poses/points and the model-decrease partials into reduction slots [0, gp + gq) of G.red.
@@ -5231,8 +5496,9 @@ void enqueue_border(pba_engine* e, double lambda, const double* lm, double* X) {
                     G.ib_pptr.p, G.ib_plist.p, G.sky_first.p, G.sky_row.p, G.fixed.p, lm ? lm : G.lm_idle.p, G.S.p,
                     G.g.p, G.g_dir.p, G.Ddiag.p, nf, G.nc_sys, X, (long long)nfs * 36 + EX_TAIL};
   const int nb = 2 * G.nc_sys + 1;
-  intr_border_kernel<6><<<dim3((nf + 3) / 4, G.nc_sys), 256, 0, e->stream>>>(ba, lambda);
-  intr_border_kernel<2><<<dim3((nf + 3) / 4, G.nc_sys), 256, 0, e->stream>>>(ba, lambda);
+  const int kpw = nf * G.nc_sys < 512 ? 4 : 1;  // waves per keyframe block (intr_border_kernel)
+  intr_border_kernel<6><<<dim3((nf * kpw + 3) / 4, G.nc_sys), 256, 0, e->stream>>>(ba, lambda, kpw);
+  intr_border_kernel<2><<<dim3((nf * kpw + 3) / 4, G.nc_sys), 256, 0, e->stream>>>(ba, lambda, kpw);
   intr_border_cam_kernel<6><<<dim3(nb, G.nc_sys, kIbSplit), 256, 0, e->stream>>>(ba, lambda, G.ib_part.p);
   intr_border_cam_kernel<2><<<dim3(nb, G.nc_sys, kIbSplit), 256, 0, e->stream>>>(ba, lambda, G.ib_part.p);
   intr_border_fin_kernel<<<(2 * G.nc_sys * nb * 36 + 255) / 256, 256, 0, e->stream>>>(ba, lambda, G.ib_part.p);
@@ -5276,6 +5542,7 @@ int enqueue_solve(pba_engine* e, double lambda, const double* lm = nullptr, bool
   if (G.band_kernel) {
     if (int rc = band_solve(e, !direct)) return rc;
   } else {
+    if (G.nc_sys && arrow_for(e, G.band)) return arrow_solve(e, G.S.p, G.sky_first.p, G.sky_row.p, G.fixed.p);
     if (G.front.lds) return launch_front(e, G.front, G.S.p, G.L.p, nfs);
     PBA_HIP(hipMemcpyAsync(G.L.p, G.S.p, sizeof(double) * 36 * (size_t)G.n_sky, hipMemcpyDeviceToDevice, e->stream));
     SolveArgs so{G.L.p, G.sky_first.p, G.sky_row.p, G.sky_last.p, G.g.p, G.Linv.p, G.x.p, G.status.p, nfs,
@@ -5440,12 +5707,19 @@ int ensure_dist_sky(pba_engine* e, int K) {
   for (int i = 0; i < nfs; ++i) rowp[i + 1] = rowp[i] + (i - first[i] + 1);
   profile_columns(first, ccptr, ccrows);
   if (int rc = build_front_plan(first, rowp, ccptr, ccrows, e->stream, G.dfront, true)) return rc;
-  if (!G.dfront.lds)
-    return fail(PBA_ERR_INVALID_ARGUMENT, "multi-GPU free intrinsics: the reduced system's active front exceeds LDS");
+  // (a front beyond LDS — many cameras or a wide band — is solved through global memory, skyline_solve_kernel)
+  std::vector<int> last(nfs);
+  for (int k = 0; k < nfs; ++k) last[k] = k;
+  for (int i = 0; i < nfs; ++i)
+    for (int k = first[i]; k < i; ++k) last[k] = std::max(last[k], i);
   G.n_dsky = rowp[nfs];
   PBA_HIP(G.dS.resize((size_t)G.n_dsky * 36));
   PBA_HIP(G.dL.resize((size_t)G.n_dsky * 36));
   PBA_HIP(G.dsky_row.upload(rowp, e->stream));
+  PBA_HIP(G.dsky_first.upload(first, e->stream));
+  PBA_HIP(G.dsky_last.upload(last, e->stream));
+  PBA_HIP(G.dsky_colptr.upload(ccptr, e->stream));
+  PBA_HIP(G.dsky_colrows.upload(ccrows.empty() ? std::vector<int>{0} : ccrows, e->stream));
   G.dsky_K = K;
   return PBA_OK;
 }
@@ -5475,7 +5749,7 @@ int enqueue_export(pba_engine* e, double lambda, const double* lm, double* X, in
 int enqueue_import(pba_engine* e, double lambda, const double* lm, const double* X, int K) {
   GnData& G = e->gn;
   const int nf = e->n_frames;
-  if (G.nc_sys) {  // free intrinsics: the summed skyline system (band + border), solved with its active front in LDS
+  if (G.nc_sys) {  // free intrinsics: the summed skyline system (band + border) — an arrow, or the skyline solvers
     if (int rc = ensure_dist_sky(e, K)) return rc;
     const int nfs = G.nfs;
     ImportSkyArgs ia{X, X + (long long)nf * ex_row(K), G.fixed_req.p, G.dsky_row.p, G.dS.p, G.g.p, G.g_dir.p,
@@ -5483,7 +5757,14 @@ int enqueue_import(pba_engine* e, double lambda, const double* lm, const double*
     const long long n = ia.n_el + 6LL * nfs;
     import_sky_kernel<<<(unsigned)((n + 255) / 256), 256, 0, e->stream>>>(ia, lambda, lm);
     PBA_HIP(hipGetLastError());
-    return launch_front(e, G.dfront, G.dS.p, G.dL.p, nfs);
+    if (arrow_for(e, K)) return arrow_solve(e, G.dS.p, G.dsky_first.p, G.dsky_row.p, G.fixed_dist.p);
+    if (G.dfront.lds) return launch_front(e, G.dfront, G.dS.p, G.dL.p, nfs);
+    PBA_HIP(hipMemcpyAsync(G.dL.p, G.dS.p, sizeof(double) * 36 * (size_t)G.n_dsky, hipMemcpyDeviceToDevice, e->stream));
+    SolveArgs so{G.dL.p, G.dsky_first.p, G.dsky_row.p, G.dsky_last.p, G.g.p, G.Linv.p, G.x.p, G.status.p, nfs,
+                 G.dsky_colptr.p, G.dsky_colrows.p};
+    skyline_solve_kernel<<<1, 256, 0, e->stream>>>(so);
+    PBA_HIP(hipGetLastError());
+    return PBA_OK;
   }
   const bool direct = G.solver == SOLVER_CR;
   if (direct && !G.cr0_inited)  // zeros outside the band, identity padding rows

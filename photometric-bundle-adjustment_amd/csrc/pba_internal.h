@@ -764,8 +764,15 @@ struct GnData {
   // from frame 0 — its skyline system, factor blocks, row offsets and plan (ensure_dist_sky, for dsky_K)
   FrontPlan dfront;
   DevBuf<double> dS, dL;
-  DevBuf<int> dsky_row;
+  DevBuf<int> dsky_row, dsky_first, dsky_last, dsky_colptr, dsky_colrows;
   int dsky_K = -1, n_dsky = 0;
+  // free intrinsics as an ARROW system (pba_gn.hip arrow_solve): the keyframe band by parallel cyclic reduction with
+  // the border's columns as extra right-hand sides, then the small dense border Schur complement.  ar_n super-rows of 4
+  // keyframes, ar_batches runs of kArrowNB columns; buffers: level 0 + two ping-pong levels (D, U, b of kArrowNB
+  // columns), the solutions X (6·nf rows × 16·ar_batches), the border reduction's partials, the border step.
+  bool arrow = false;           // the local (single-GPU) free-intrinsics system is solved as an arrow
+  int ar_n = 0, ar_batches = 0;
+  DevBuf<double> ar_buf, ar_X, ar_part, ar_dc;
   DevBuf<double> S, L, Sband, Lband, g, g_dir, Ddiag, Linv, x;  // skyline system, its factor, rhs, direct gradient, LM diagonal, L_kk⁻¹, step
   DevBuf<uint8_t> fixed;
   DevBuf<uint8_t> observed, fixed_req, fixed_dist;  // multi-GPU: local observation flags, requested / effective constants

@@ -486,6 +486,48 @@ def test_free_intrinsics_exchange_matches_single_engine_step(world, model, lam):
             e.close()
 
 
+@pytest.mark.parametrize("band", [4, 8, 16])
+def test_free_intrinsics_exchange_solver_paths(band):
+    """The summed free-intrinsics system of a multi-GPU step through each of its solvers, with a four-camera rig (8 border
+    frames): exchange band 4 — the arrow solve (band by cyclic reduction, 49 right-hand sides in 4 batches); 8 — the
+    skyline Cholesky with its active front in LDS (F = 8 + 1 + 8 slots); 16 — a front of 25 slots (≈ 180 KB) that does
+    not fit LDS, solved through global memory (skyline_solve_kernel) instead of failing.  Every path gives
+    the single engine's step."""
+    import torch
+    n_cams = 4
+    pb0 = synth.make_problem(kind=1, n_frames=20, n_points=260, width=376, height=240, seed=41, border=12)
+    intr = np.stack([pb0.intrinsics[0] * np.array([1 + 0.01 * c, 1 - 0.01 * c, 1, 1, 1, 1, 1, 1]) for c in range(n_cams)])
+    pb = synth.make_problem(kind=1, n_frames=20, n_points=260, width=376, height=240, seed=41, border=12, intrinsics=intr,
+                            frame_cam=(np.arange(20) % n_cams).astype(np.int32), obs_sigma=0.3)
+    state = intr * np.array([1.003, 0.998, 1.0005, 0.9995, 1, 1, 1, 1])
+    fixed, lam, world = (0, 1), 1e-3, 2
+    with intrinsics_engine(pb, state, fixed) as full:
+        full.gn_linearize()
+        m_full, st_full = full.gn_step(lam)
+        dp_full, dr_full = full.gn_last_step()
+    assert st_full == 0
+    sh = [(intrinsics_engine(sub, state, fixed), pids)
+          for sub, pids, _ in (D.shard_problem(pb, world, r) for r in range(world))]
+    try:
+        for e, _ in sh:
+            e.gn_linearize()
+        assert band >= max(e.gn_band() for e, _ in sh)
+        n = sh[0][0].gn_exchange_size(band)
+        bufs = [torch.zeros(n, dtype=torch.float64, device="cuda") for _ in sh]
+        for (e, _), b in zip(sh, bufs):
+            e.gn_step_export(lam, band, b.data_ptr())
+        tot = bufs[0] + bufs[1]
+        torch.cuda.synchronize()
+        for e, _ in sh:
+            mp, mq, st = e.gn_step_import(lam, band, tot.data_ptr())
+            assert st == 0
+            dp, _ = e.gn_last_step()
+            assert np.linalg.norm(dp - dp_full) <= 1e-6 * np.linalg.norm(dp_full), np.linalg.norm(dp - dp_full)
+    finally:
+        for e, _ in sh:
+            e.close()
+
+
 @pytest.mark.parametrize("loop", ["host", "comm"])
 def test_free_intrinsics_solve_distributed_matches_solve(loop):
     """The multi-GPU LM loops with free intrinsics — host-callback sums (pba_solve_distributed) and the device-steered

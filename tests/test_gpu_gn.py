@@ -493,6 +493,47 @@ def test_front_and_global_skyline_agree(case, monkeypatch):
         assert np.linalg.norm(a - b) <= 1e-9 * np.linalg.norm(b), (case, np.linalg.norm(a - b) / np.linalg.norm(b))
 
 
+def _intrinsics_rig(n_frames, n_points, seed, n_cams, model=0):
+    """A rig of n_cams cameras (keyframe f uses camera f % n_cams) whose intrinsics state differs from the cameras the
+    hosts unproject with (reprojection.h:93-98)."""
+    pb0 = synth.make_problem(kind=1, model=model, n_frames=n_frames, n_points=n_points, width=376, height=240,
+                             seed=seed, border=12)
+    intr = np.stack([pb0.intrinsics[0] * np.array([1 + 0.01 * c, 1 - 0.01 * c, 1, 1, 1, 1, 1, 1])
+                     for c in range(n_cams)])
+    pb = synth.make_problem(kind=1, model=model, n_frames=n_frames, n_points=n_points, width=376, height=240, seed=seed,
+                            border=12, intrinsics=intr, frame_cam=(np.arange(n_frames) % n_cams).astype(np.int32),
+                            obs_sigma=0.3)
+    return pb, intr * np.array([1.003, 0.998, 1.0005, 0.9995, 1, 1, 1, 1])
+
+
+@pytest.mark.parametrize("n_cams", [1, 2, 4])
+@pytest.mark.parametrize("lam", [1e-4, 1e-1])
+def test_arrow_and_front_solvers_agree(n_cams, lam, monkeypatch):
+    """Free intrinsics (map_utils.h:339-345): the reduced system is an arrow — the keyframes' band plus the 2·nc border
+    frames' dense rows.  arrow_solve (parallel cyclic reduction of the band with the border's 12·nc columns as extra
+    right-hand sides in batches of 16 — 1, 2 and 4 batches here — then the border's Schur complement) and
+    front_solve_kernel (the skyline Cholesky, border last: the same elimination order; PBA_SOLVER=front) give the same
+    pose, intrinsics and inverse-distance steps and model decrease to fp64 rounding."""
+    pb, state = _intrinsics_rig(23, 260, 31 + n_cams, n_cams)
+    out = {}
+    for solver in ("arrow", "front"):
+        if solver == "front":
+            monkeypatch.setenv("PBA_SOLVER", "front")
+        with make_engine(pb, 1.0, (0, 1)) as eng:
+            eng.set_optimize_intrinsics(True)
+            eng.set_intrinsics_state(state)
+            eng.gn_linearize()
+            m, st = eng.gn_step(lam)
+            assert st == 0, solver
+            dp, dr = eng.gn_last_step()
+            eng.gn_accept()
+            out[solver] = (dp, dr, eng.get_intrinsics() - state, np.array([m]))
+    for name, a, b in zip(("poses", "rho", "intrinsics", "model"), out["arrow"], out["front"]):
+        err = np.linalg.norm(a - b) / np.linalg.norm(b)
+        print(f"\nn_cams {n_cams} λ {lam}: {name} {err:.2e}")
+        assert err <= 1e-8, (name, err)
+
+
 @pytest.fixture(scope="module")
 def c3():
     """BASELINE configs[2] (C3): 200 keyframes × 20k points × 8 px × 4 targets = 80k blocks, rendered images."""
