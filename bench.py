@@ -106,7 +106,7 @@ def per_call(r):
             **({"prepare_breakdown": r["prepare"]} if "prepare" in r else {})}
 
 
-RUNS_PER_MODE = 5  # C2 / C4-sample Ceres runs per mode, interleaved; the median run of each is reported
+RUNS_PER_MODE = 7  # C2 / C4-sample Ceres runs per mode, interleaved; the median run of each is reported
 
 
 def c2_dropin(pb_c4, images_host, threads: int):
@@ -128,15 +128,23 @@ def c2_dropin(pb_c4, images_host, threads: int):
     # everything but the device's part), and the CPU AutoDiff path — same Solve options
     # each mode RUNS_PER_MODE times, interleaved, the median run of each reported (the box's host is shared: a 16-CPU
     # cgroup quota; single runs of these ~3-ms evaluations vary by ±10-30 %)
-    runs = {m: [] for m in ("gpu", "cpu", "floor")}
+    # floor_cold: the floor with its staged read-backs flushed from the CPU caches before each evaluation
+    # (PBA_FLOOR_COLD, tests/cpp/ceres_lm_driver.cpp) — the drop-in's records arrive by DMA into memory no core has cached
+    runs = {m: [] for m in ("gpu", "cpu", "floor", "floor_cold")}
     for _ in range(RUNS_PER_MODE):
         runs["gpu"].append(CR.run("gpu", pb, iters=10, huber=9.0, threads=threads, check=False))
         runs["cpu"].append(CR.run("cpu", pb, iters=10, huber=9.0, threads=threads))
         runs["floor"].append(CR.run("floor", pb, iters=10, huber=9.0, threads=threads))
+        os.environ["PBA_FLOOR_COLD"] = "1"
+        try:
+            runs["floor_cold"].append(CR.run("floor", pb, iters=10, huber=9.0, threads=threads))
+        finally:
+            os.environ.pop("PBA_FLOOR_COLD", None)
     best = {m: sorted(v, key=lambda r: r["jacobian_evaluation_s"] + r["residual_evaluation_s"])[len(v) // 2]
             for m, v in runs.items()}
     g, c, fl = best["gpu"], best["cpu"], best["floor"]
     out["gpu_dropin"], out["cpu_autodiff"], out["ceres_floor"] = per_call(g), per_call(c), per_call(fl)
+    out["ceres_floor_cold"] = per_call(best["floor_cold"])
     out["runs_per_mode"] = RUNS_PER_MODE
     out["jacobian_evaluation_ms_runs"] = {m: [1e3 * r["jacobian_evaluation_s"] / max(r["jacobian_evaluations"], 1)
                                               for r in v] for m, v in runs.items()}
@@ -146,6 +154,8 @@ def c2_dropin(pb_c4, images_host, threads: int):
     out["jacobian_evaluation_vs_floor"] = out["gpu_dropin"]["jacobian_evaluation_ms"] / out["ceres_floor"]["jacobian_evaluation_ms"]
     jr = out["jacobian_evaluation_ms_runs"]
     out["jacobian_evaluation_vs_floor_min"] = min(jr["gpu"]) / min(jr["floor"])  # (the fastest run of each mode)
+    out["jacobian_evaluation_vs_floor_cold"] = (out["gpu_dropin"]["jacobian_evaluation_ms"] /
+                                                out["ceres_floor_cold"]["jacobian_evaluation_ms"])
     out["residual_evaluation_vs_floor"] = out["gpu_dropin"]["residual_evaluation_ms"] / out["ceres_floor"]["residual_evaluation_ms"]
     out["same_trajectory"] = bool(len(g["costs"]) == len(c["costs"]) and np.array_equal(g["step_ok"], c["step_ok"]))
     out["floor_replay_ok"] = bool(all(r["replay_ok"] == 1 for r in runs["floor"]))
@@ -153,7 +163,9 @@ def c2_dropin(pb_c4, images_host, threads: int):
                                          fl["residual_evaluations"] == g["residual_evaluations"])
     out["floor_note"] = ("ceres_floor: the same Solve over the same per-block CostFunctions, replaying the drop-in's "
                          "recorded read-backs (records / residuals, validity, P+) — the drop-in's trajectory and evaluation "
-                         "counts with the device's part (state upload, launch, read-back) removed")
+                         "counts with the device's part (state upload, launch, read-back) removed; ceres_floor_cold: the "
+                         "same with the replayed records flushed from the CPU caches before each evaluation (the drop-in's "
+                         "arrive by DMA)")
     # the C4 sample the same way: interleaved runs per mode, the median of each (single runs moved the floor's
     # evaluations and even Ceres' own linear solver by +30-60 % between neighbouring processes on the shared host)
     sample = c4_sample(pb_c4, images_host)
@@ -546,9 +558,9 @@ def measure_traffic(args, n_blocks, timeout_s=150):
 
 
 def stream_copy_peak(torch, dev, achieved):
-    """a measured streaming rate beside the 8 TB/s spec.  The reference point is a hand-written float4 copy
-    kernel (tools/micro/stream_copy.hip: 16-B loads, non-temporal 16-B stores, four moves per lane per iteration, 1 GiB,
-    the best of 5 launches at each of five grid sizes) — MI355X_MICROARCH.md's "float4 copy" measurement (6.29 TB/s
+    """a measured streaming rate beside the 8 TB/s spec.  The reference point is hand-written float4 copy
+    kernels (tools/micro/stream_copy.hip: 16-B loads and stores, 1-4 moves per lane, default or non-temporal policies,
+    1 GiB, the best launch over forms and grid sizes) — MI355X_MICROARCH.md's "float4 copy" measurement (6.29 TB/s
     there), taken on this box; a torch device copy of the same size is reported beside it."""
     import ctypes
     out = {}
@@ -562,8 +574,10 @@ def stream_copy_peak(torch, dev, achieved):
         rc = lib.stream_copy_gbs(1 << 30, 5, ctypes.byref(g), ctypes.byref(grid))
         if rc == 0 and g.value > 0:
             out = {"stream_copy_gbs": g.value, "frac_of_stream_copy": achieved / g.value,
-                   "stream_copy_note": f"hand-written float4 copy kernel (16-B loads, non-temporal 16-B stores), 1 GiB "
-                                       f"(2 GiB of traffic per copy), best of 5 x 5 grid sizes ({grid.value} workgroups)"}
+                   "stream_copy_note": f"hand-written float4 copy kernels (16-B loads / stores, 1-4 moves per lane, "
+                                       f"default or non-temporal policies), 1 GiB (2 GiB of traffic per copy), best of "
+                                       f"5 launches x 7 forms x 4 grids (form {grid.value % 100}, "
+                                       f"{grid.value // 100} workgroups; tools/micro/stream_copy.hip)"}
         else:
             out = {"stream_copy_error": f"stream_copy_gbs returned {rc}"}
     except OSError as ex:

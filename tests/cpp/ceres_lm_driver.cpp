@@ -51,6 +51,7 @@
 #include <cstdlib>
 #include <cmath>
 #include <cstring>
+#include <immintrin.h>
 #include <memory>
 #include <sstream>
 #include <string>
@@ -242,7 +243,16 @@ class ReplayEvaluator : public pba_ceres::GpuEvaluator, public ceres::IterationC
 
  private:
   // the next residual-only and the next Jacobian evaluation from next_ on, into the read-back buffers
+  // PBA_FLOOR_COLD=1 (diagnostic): the staged arrays are flushed from the CPU caches after staging, as the drop-in's
+  // read-back arrives by DMA into memory no core has cached — the floor then differs from the drop-in by the device's
+  // part only, not also by where the records are read from.
+  static void evict(const void* p, size_t bytes) {
+    const char* c = static_cast<const char*>(p);
+    for (size_t o = 0; o < bytes; o += 64) _mm_clflush(c + o);
+    _mm_mfence();
+  }
   void stage() {
+    static const bool cold = std::getenv("PBA_FLOOR_COLD") != nullptr;
     bool r = false, j = false;
     for (size_t i = next_; i < snaps_->size() && !(r && j); ++i) {
       const Snapshot& s = (*snaps_)[i];
@@ -252,6 +262,10 @@ class ReplayEvaluator : public pba_ceres::GpuEvaluator, public ceres::IterationC
         if (staged_j_ != i) {
           std::memcpy(records_.data(), s.rec->data(), nb * rec_ * sizeof(float));
           std::memcpy(valid_.data(), s.valid->data(), nb);
+          if (cold) {
+            evict(records_.data(), nb * rec_ * sizeof(float));
+            evict(valid_.data(), nb);
+          }
           staged_j_ = i;
         }
         j = true;
@@ -259,6 +273,10 @@ class ReplayEvaluator : public pba_ceres::GpuEvaluator, public ceres::IterationC
         if (staged_r_ != i) {
           std::memcpy(residuals_.data(), s.rec->data(), nb * R_ * sizeof(float));
           std::memcpy(valid_r_.data(), s.valid->data(), nb);
+          if (cold) {
+            evict(residuals_.data(), nb * R_ * sizeof(float));
+            evict(valid_r_.data(), nb);
+          }
           staged_r_ = i;
         }
         r = true;
