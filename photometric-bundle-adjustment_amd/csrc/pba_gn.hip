@@ -191,7 +191,6 @@ constexpr auto make_slot_table(bool f64, std::integer_sequence<int, L...>) {
   struct T { unsigned w[64]; };
   return T{{slot_word(L, f64)...}};
 }
-__constant__ const auto kSlotTable = make_slot_table(false, std::make_integer_sequence<int, 64>{});
 __constant__ const auto kSlotTable64 = make_slot_table(true, std::make_integer_sequence<int, 64>{});
 
 // At most this many targets per linearise chunk (gn_prepare cuts chunks there): a wave's blocks then hold ≤ 4 target
@@ -455,7 +454,8 @@ void linearize_kernel(const KernelArgs a, const LinArgs g) {
 // A_β[l & 3][l >> 4], B holds B_β[l >> 4][l & 3], the accumulator C_β[l >> 4][l & 3].
 __host__ __device__ constexpr int upper8(int r, int c) { return r * 8 - r * (r - 1) / 2 + (c - r); }  // r ≤ c < 8
 
-// PPL > 1 (9…32 px, C5's 21): lane k evaluates pixels k, k + 8, … in PPL passes, as linearize_rows_kernel; each pass's
+// PPL > 1 (9…32 px, C5's 21): lane k evaluates pixels k, k + 8, … in PPL passes (8 lanes per block, as the evaluation's
+// photometric_block_kernel_multi: a chunk stays 32 blocks, the chunk partials those of 8 px); each pass's
 // unweighted rows go through the matrix cores into per-block fp64 accumulators (the chain runs on across the passes) and
 // the block's Huber weight, known after its last row, scales them (x̃ᵀx̃ = w·xᵀx).  LDS per wave: the tile blocks and a
 // pass's rows side by side, the run product sets over the tile once the passes are done.
@@ -787,189 +787,6 @@ void linearize_adj_kernel(const KernelArgs a, const LinArgs g) {
   }
 }
 
-// Patterns of 9…32 pixels (C5: 21 px): 8 lanes per block as in the evaluation kernel (photometric_block_kernel_multi),
-// lane k evaluating pixels k, k+8, … (PPL rows, one pass each), so a chunk holds 32 blocks as at 8 px — the same chunk
-// partials — instead of 8 blocks of 32 lanes (at 21 px a third of those lanes idle, and four times the chunks for the
-// assembly and the decision to sum).  The block's Huber weight needs all of its rows, so each pass's rows go through
-// the matrix cores unweighted into per-block accumulators (x̃ᵀx̃ = w·xᵀx) and the weight scales them once known; rows
-// that are not active or not ok are zero (an invalid block's products then scale by 0).  LDS per wave: the tile blocks
-// and the pass's 64 rows side by side (the rows no longer overwrite the tile), then the product sets over both.
-#ifndef PBA_LINROWS_WAVES
-#define PBA_LINROWS_WAVES 5  // 96 VGPRs (a few spilled): 150 against 161 µs at 4 waves (C5 pattern, C4 problem)
-#endif
-template <int MODEL, int PPL>
-__global__ __launch_bounds__(kBlockThreads) __attribute__((amdgpu_waves_per_eu(PBA_LINROWS_WAVES, 8)))
-void linearize_rows_kernel(const KernelArgs a, const LinArgs g) {
-  constexpr int LPB = 8, BW = 64 / LPB, NW = kBlockThreads / 64, SPB = LPB / 4, NVP = 108;
-  constexpr int kTileW = BW * (int)sizeof(TileBlock), kRowsW = 64 * 16 * 4, kProdW = kChunkTargets * NVP * 8;
-  constexpr int kArena = kTileW + kRowsW;
-  static_assert(kProdW <= kArena, "product sets fit the arena");
-  __shared__ __attribute__((aligned(16))) unsigned char arena[NW][kArena];
-  __shared__ int s_wlo[NW], s_wn[NW];
-  __shared__ float s_bc[kBlockThreads / LPB];
-  __shared__ float2 s_pat[LPB * PPL];
-  const int chunk = logical_tile();
-  if (chunk >= g.n_chunks) return;
-  const int4 d = g.chunk_desc[chunk];
-  const LmView lv = lm_view(g.lm);
-  if (lv.done != 0.0) return;
-  const bool s1 = (lv.set != 0.0) != g.spare;
-  double* const blk_schur = s1 ? g.blk_schur1 : g.blk_schur;
-  double* const part_lin = s1 ? g.part_lin1 : g.part_lin;
-  if (g.lin_set && chunk == 0 && threadIdx.x == 0) {  // (the λ-free elimination after this launch reads them)
-    *g.lin_set = s1 ? 1 : 0;
-    g.degen[s1 ? 1 : 0] = 0;
-  }
-  const int count = d.y, n_t = d.z, poff = d.w;
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int lb = threadIdx.x / LPB, k = threadIdx.x % LPB, wb = lb % BW;
-  const bool live = lb < count;
-  const int R = a.P;
-  if ((int)threadIdx.x < LPB * PPL) s_pat[threadIdx.x] = pattern_at<LPB * PPL>(a, threadIdx.x);
-  const int4 lr = g.lin_rec[(long long)chunk * (kBlockThreads / LPB) + lb];
-  const int blk = lr.x, gpos = lr.w, lt = (int)((unsigned)lr.z >> 24);
-  TileBlock* s_tb = reinterpret_cast<TileBlock*>(arena[wave]);
-  const int pt = stage_tile_pp<LPB>(a, s_tb, wb, k, make_int2(lr.y, lr.z & 0xffffff));
-  float Ih[PPL];
-#pragma unroll
-  for (int j = 0; j < PPL; ++j) {
-    const int px = k + LPB * j;
-    Ih[j] = live && px < R ? a.host_int[(long long)pt * R + px] : 0.0f;
-  }
-  __syncthreads();
-  store_pair_rt<LPB>(s1 ? g.pair_rt1 : g.pair_rt, s_tb[wb].pr.R, s_tb[wb].pr.t, lr.z & 0xffffff, lt, k, live);
-  float* sX = reinterpret_cast<float*>(arena[wave] + kTileW);  // the pass's 64 rows × 16 floats
-  const int ci = lane & 15, kq = lane >> 4;
-  f32x4 accb[BW];
-#pragma unroll
-  for (int b = 0; b < BW; ++b) accb[b] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-  int okl = 1;
-  float s = 0.0f;
-#pragma unroll 1
-  for (int j = 0; j < PPL; ++j) {
-    const int px = k + LPB * j;
-    const bool act = live && px < R;
-    float ih = Ih[0];
-#pragma unroll
-    for (int q = 1; q < PPL; ++q) ih = j == q ? Ih[q] : ih;
-    asm volatile("" ::: "memory");  // the tile is read from LDS per pass (see photometric_block_kernel_multi)
-    const Row row = photometric_row<MODEL, true>(a, s_tb[wb], s_pat[act ? px : 0], ih);
-    const bool use = act && row.ok;
-    okl &= act ? row.ok : 1;
-    s += use ? row.r * row.r : 0.0f;
-    auto xv = [&](float v) { return use ? v : 0.0f; };  // selects: a row that is not ok may hold inf / NaN
-    float4* xr = reinterpret_cast<float4*>(sX + lane * 16);
-    xr[0] = make_float4(xv(row.hv.x), xv(row.hv.y), xv(row.hv.z), xv(row.hw.x));
-    xr[1] = make_float4(xv(row.hw.y), xv(row.hw.z), xv(row.tv.x), xv(row.tv.y));
-    xr[2] = make_float4(xv(row.tv.z), xv(row.tw.x), xv(row.tw.y), xv(row.tw.z));
-    xr[3] = make_float4(xv(row.jr), xv(row.r), 0.0f, 0.0f);
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    float op[BW * SPB];
-#pragma unroll
-    for (int st = 0; st < BW * SPB; ++st) op[st] = sX[(4 * st + kq) * 16 + ci];
-#pragma unroll
-    for (int b = 0; b < BW; ++b)
-#pragma unroll
-      for (int st = 0; st < SPB; ++st)
-        accb[b] = __builtin_amdgcn_mfma_f32_16x16x4f32(op[b * SPB + st], op[b * SPB + st], accb[b], 0, 0, 0);
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // this pass's reads before the next pass's row stores
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  }
-  const int ok = group_all<LPB>(okl);
-  s = group_sum<LPB>(s);
-  const float w = ok ? huber_weight(s, a.huber) : 0.0f;
-  const float bcost = ok ? huber_cost(s, a.huber) : 0.0f;
-  if (k == 0) s_bc[lb] = live && ok ? bcost : -1.0f;  // read after the barrier below
-  const unsigned slots = kSlotTable.w[lane];
-  {
-    // as linearize_kernel: per block its (now weighted) products — row 12 the point-elimination data at its GN
-    // position — added to its target run's sum, each run's 16×16 result scattered once as the 104 products
-    double* sP = reinterpret_cast<double*>(arena[wave]);  // over the tile and the rows (both consumed)
-    const int nbw = min(max(count - wave * BW, 0), BW);
-    const int lo = __builtin_amdgcn_readfirstlane(lt);
-    auto flush = [&](const v4f64& acc, int slot) {
-#pragma unroll
-      for (int m = 0; m < 4; ++m) {
-        const unsigned v = (slots >> (8 * m)) & 255u;
-        if (v < (unsigned)NV) sP[slot * NVP + v] = acc[m];
-      }
-    };
-    // (this kernel's block products are fp32 matrix-core chains over the block's ⌈P/8⌉ passes; the weighting, the
-    // point data and every sum after them are fp64)
-    const int pc = lane - 48, pq = pc >= 6 && pc < 12 ? pc - 4 : (pc == 12 ? 0 : (pc == 13 ? 1 : -1));
-    v4f64 tacc = {0.0, 0.0, 0.0, 0.0};
-    int cur = lo;
-#pragma unroll
-    for (int b = 0; b < BW; ++b) {
-      if (b < nbw) {
-        const double wb_ = (double)__int_as_float(__builtin_amdgcn_readlane(__float_as_int(w), b * LPB));
-        const v4f64 acc = {accb[b][0] * wb_, accb[b][1] * wb_, accb[b][2] * wb_, accb[b][3] * wb_};
-        const int gpb = __builtin_amdgcn_readlane(gpos, b * LPB);
-        if (pc >= 0 && pq >= 0) blk_schur[(long long)gpb * kPd + pq] = acc[0];
-        const int ltb = __builtin_amdgcn_readlane(lt, b * LPB);
-        if (ltb != cur) {
-          flush(tacc, cur - lo);
-          tacc = v4f64{0.0, 0.0, 0.0, 0.0};
-          cur = ltb;
-        }
-        tacc += acc;
-      }
-    }
-    if (nbw > 0) flush(tacc, cur - lo);
-    if (lane == 0) {
-      s_wlo[wave] = lo;
-      s_wn[wave] = nbw > 0 ? cur - lo + 1 : 0;
-    }
-  }
-  __syncthreads();
-  auto sset = [&](int w_, int i, int v) -> double { return reinterpret_cast<const double*>(arena[w_])[i * NVP + v]; };
-  const int nout = SLOT_LIN_BASE + SLOT_LIN_T * n_t;
-  for (int o = threadIdx.x; o < nout; o += kBlockThreads) {
-    int v, jt = -1;
-    if (o < 36) {
-      const int r = o / 6, c = o % 6;
-      v = upper_index(min(r, c), max(r, c));
-    } else if (o < 42) {
-      v = 78 + (o - 36);
-    } else {
-      jt = (o - 42) / SLOT_LIN_T;
-      const int q = (o - 42) % SLOT_LIN_T;
-      if (q < 36) v = 21 + q;
-      else if (q < 72) { const int r = (q - 36) / 6, c = (q - 36) % 6; v = 57 + upper_index(min(r, c), max(r, c)); }
-      else v = 84 + (q - 72);
-    }
-    double acc = 0.0;
-#pragma unroll
-    for (int w_ = 0; w_ < NW; ++w_) {
-      const int wl = s_wlo[w_], wn = s_wn[w_];
-      if (jt < 0) {
-        for (int i = 0; i < wn; ++i) acc += sset(w_, i, v);
-      } else if (jt >= wl && jt < wl + wn) {
-        acc += sset(w_, jt - wl, v);
-      }
-    }
-    part_lin[(long long)poff + o] = acc;
-  }
-  if (live && k == 0) {
-    a.valid[blk] = (uint8_t)ok;
-    a.cost[blk] = bcost;
-  }
-  if (g.wg_red && wave == 0) {
-    const float x = lane < count ? s_bc[lane] : -1.0f;
-    double c = x >= 0.0f ? (double)x : 0.0, vv = x >= 0.0f ? 1.0 : 0.0;
-    for (int m = 32; m >= 1; m >>= 1) {
-      c += __shfl_xor(c, m, 64);
-      vv += __shfl_xor(vv, m, 64);
-    }
-    if (lane == 0) {
-      g.wg_red[2 * chunk] = c;
-      g.wg_red[2 * chunk + 1] = vv;
-    }
-  }
-}
 
 struct SchurArgs {
   const int4* desc;       // first GN point, n points, n local poses, partial offset (doubles)
@@ -4521,7 +4338,7 @@ __global__ void lm_accept_kernel(const double* __restrict__ lm, const double* __
 // host side
 // ------------------------------------------------------------------------------------------------
 int gn_lpb(const pba_engine* e) { return e->opt.residual_kind == PBA_RESIDUAL_GEOMETRIC ? 4 : 8; }
-// rows per lane of the linearisation: 1 up to 8 px (one lane per row), ⌈P/8⌉ above (linearize_rows_kernel)
+// rows per lane of the linearisation: 1 up to 8 px (one lane per row), ⌈P/8⌉ above (linearize_adj_kernel<·, PPL>)
 int gn_ppl(const pba_engine* e) { return e->opt.residual_kind == PBA_RESIDUAL_GEOMETRIC ? 1 : (e->P + 7) / 8; }
 
 int band_kernel_for(int band) { return band <= 4 ? 4 : (band <= 8 ? 8 : (band <= 16 ? 16 : 0)); }
@@ -5125,22 +4942,13 @@ template <int KIND, int MODEL>  // photometric: MODEL = camera model + 4 · inte
 void launch_linearize(pba_engine* e, const KernelArgs& ka, const LinArgs& la) {
   const int grid = la.n_chunks;
   if constexpr (KIND == PBA_RESIDUAL_PHOTOMETRIC) {
-    const bool leg = e->gn.lin_legacy;
     switch (e->gn.ppl) {  // 9…32 px: 8 lanes per block, ⌈P/8⌉ rows per lane
       case 1: break;
-      case 2:
-        if (leg) linearize_rows_kernel<MODEL, 2><<<grid, kBlockThreads, 0, e->stream>>>(ka, la);
-        else linearize_adj_kernel<MODEL, 2, kBlockThreads><<<grid, kBlockThreads, 0, e->stream>>>(ka, la);
-        return;
-      case 3:
-        if (leg) linearize_rows_kernel<MODEL, 3><<<grid, kBlockThreads, 0, e->stream>>>(ka, la);
-        else linearize_adj_kernel<MODEL, 3, kBlockThreads><<<grid, kBlockThreads, 0, e->stream>>>(ka, la);
-        return;
-      default:
-        if (leg) linearize_rows_kernel<MODEL, 4><<<grid, kBlockThreads, 0, e->stream>>>(ka, la);
-        else linearize_adj_kernel<MODEL, 4, kBlockThreads><<<grid, kBlockThreads, 0, e->stream>>>(ka, la);
-        return;
+      case 2: linearize_adj_kernel<MODEL, 2, kBlockThreads><<<grid, kBlockThreads, 0, e->stream>>>(ka, la); return;
+      case 3: linearize_adj_kernel<MODEL, 3, kBlockThreads><<<grid, kBlockThreads, 0, e->stream>>>(ka, la); return;
+      default: linearize_adj_kernel<MODEL, 4, kBlockThreads><<<grid, kBlockThreads, 0, e->stream>>>(ka, la); return;
     }
+    // the 14-column products of the same rows: the A/B reference of the test build (PBA_TEST_HOOKS, PBA_LIN_LEGACY)
     if (e->gn.lin_legacy) linearize_kernel<KIND, MODEL, 8><<<grid, kBlockThreads, 0, e->stream>>>(ka, la);
     else linearize_adj_kernel<MODEL, 1, kBlockThreads><<<grid, kBlockThreads, 0, e->stream>>>(ka, la);
   } else {
@@ -6090,9 +5898,9 @@ int lm_loop_single(pba_engine* e, const pba_solver_options* o, pba_solver_summar
                                                          G.lm_init.p);
   PBA_HIP(hipGetLastError());
   for (int r = 0; r < kRecRing; ++r) G.lm_h[r * kRecStride + kLmFields] = 0.0;  // no trial published yet
-  // PBA_LM_HOST_DELAY_US (tests): the host thread sleeps this long before each wait, as a descheduled thread would
-  const char* dly = std::getenv("PBA_LM_HOST_DELAY_US");
-  const int delay_us = dly ? std::atoi(dly) : 0;
+  // PBA_LM_HOST_DELAY_US (test build only, PBA_TEST_HOOKS): the host thread sleeps this long before each wait, as a
+  // descheduled thread would
+  const int delay_us = test_hook_int("PBA_LM_HOST_DELAY_US");
   const int n = std::max(0, opt.max_iterations);
   const DecideOpts dopt = decide_opts(opt);
   auto enqueue = [&](int i) { return lm_trial(e, dopt, (double)(i + 1), timed ? events.ev + 4 * (i & 1) : nullptr); };
@@ -6239,7 +6047,7 @@ int lm_loop(pba_engine* e, const pba_solver_options* o, const Collective* coll, 
     n_valid = (int)v[1];
     chk.n_ranks = (int)v[2];
   }
-  if (const char* pv = std::getenv("PBA_TEST_PERTURB_DECISION")) {  // tests: "rank:trial:mode"
+  if (const char* pv = test_hook("PBA_TEST_PERTURB_DECISION")) {  // test build: "rank:trial:mode"
     int pr = -1, pt = -1, pm = 1;
     if (std::sscanf(pv, "%d:%d:%d", &pr, &pt, &pm) >= 2 && pr == (coll->comm ? comm_rank(coll->comm) : G.dist_rank)) {
       chk.perturb_seq = pt;

@@ -17,6 +17,22 @@
 namespace pba {
 namespace detail {
 
+// Test hooks — environment variables some GPU tests set (a forced decision mismatch, a host delay, the λ-specific
+// elimination path, the 14-column A/B lineariser) — exist only in the library's test build (libpba_test.so, compiled
+// with PBA_TEST_HOOKS; tests/helpers.py loads it for those tests).  The product library ignores them.
+inline const char* test_hook(const char* name) {
+#ifdef PBA_TEST_HOOKS
+  return std::getenv(name);
+#else
+  (void)name;
+  return nullptr;
+#endif
+}
+inline int test_hook_int(const char* name) {
+  const char* v = test_hook(name);
+  return v ? std::atoi(v) : 0;
+}
+
 constexpr int kBlockThreads = 256;
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
@@ -749,9 +765,10 @@ struct GnData {
   DevBuf<int> degen, lin_set;
   DevBuf<double> ts_part;  // the decision workgroups' slices of the trial sums (schur_free_decide_kernel) …
   DevBuf<int> ts_count;    // … and their arrival count
-  bool force_degen = std::getenv("PBA_TEST_FORCE_DEGEN") != nullptr;
-  // tests: the 14-column linearisation (linearize_kernel) for ≤ 8-px photometric patterns instead of the adjoint form
-  bool lin_legacy = std::getenv("PBA_LIN_LEGACY") != nullptr;  // tests: the λ-specific path on every trial
+  // test build (PBA_TEST_HOOKS) only: the λ-specific point elimination on every trial (PBA_TEST_FORCE_DEGEN), the
+  // 14-column linearisation (linearize_kernel) for ≤ 8-px photometric patterns instead of the adjoint form (PBA_LIN_LEGACY)
+  bool force_degen = pba::detail::test_hook("PBA_TEST_FORCE_DEGEN") != nullptr;
+  bool lin_legacy = pba::detail::test_hook("PBA_LIN_LEGACY") != nullptr;
   DevBuf<int> sky_first, sky_row, sky_last;  // skyline profile of the reduced camera system
   DevBuf<int> sky_cptr, g_cptr;  // contribution lists (CSR) per skyline block / per pose
   DevBuf<int2> sky_contrib, g_contrib;

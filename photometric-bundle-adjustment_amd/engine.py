@@ -17,10 +17,13 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIB_PATH = os.environ.get("PBA_LIBRARY") or os.path.join(CSRC, "libpba.so")  # override: A/B builds (tools/)
+# the library's test build (PBA_TEST_HOOKS: forced decision mismatch, host delay, λ-specific path, 14-column A/B
+# lineariser — pba_internal.h test_hook); only the GPU tests that need those hooks load it (Engine(library=…))
+TEST_LIB_PATH = os.path.join(CSRC, "libpba_test.so")
 HEADER = os.path.join(os.path.dirname(HERE), "include", "pba.h")
 
 PBA_OK = 0
-_LIB = None
+_LIBS = {}
 
 
 class Options(C.Structure):
@@ -106,19 +109,20 @@ def header_functions() -> list[str]:
     return sorted(set(re.findall(r"^\s*(?:int|const char\*|void)\s+(pba_\w+)\s*\(", src, re.M)))
 
 
-def lib():
-    global _LIB
-    if _LIB is not None:
-        return _LIB
-    if not os.path.exists(LIB_PATH):
-        raise RuntimeError(f"HIP engine library missing: {LIB_PATH} (run __graft_entry__.build())")
+def lib(path: Optional[str] = None):
+    """The engine library at `path` (default LIB_PATH: csrc/libpba.so), loaded once per path."""
+    path = path or LIB_PATH
+    if path in _LIBS:
+        return _LIBS[path]
+    if not os.path.exists(path):
+        raise RuntimeError(f"HIP engine library missing: {path} (run __graft_entry__.build())")
     # torch bundles its own HIP runtime under the same soname: load it first so the engine binds to that one.
     # Loaded the other way round (engine first), torch's runtime later finds no devices in this process.
     try:
         import torch  # noqa: F401  (loads libraries only; no GPU initialisation)
     except ImportError:
         pass
-    L = C.CDLL(LIB_PATH)
+    L = C.CDLL(path)
     vp, i32 = C.c_void_p, C.c_int32
     sig = {
         "pba_create": ([C.POINTER(Options), C.POINTER(vp)], C.c_int),
@@ -211,7 +215,7 @@ def lib():
         f = getattr(L, name)
         f.argtypes = argt
         f.restype = rest
-    _LIB = L
+    _LIBS[path] = L
     return L
 
 
@@ -219,9 +223,9 @@ class PbaError(RuntimeError):
     pass
 
 
-def _check(rc: int, what: str):
+def _check(rc: int, what: str, L=None):
     if rc != PBA_OK:
-        L = lib()
+        L = L or lib()
         raise PbaError(f"{what}: {L.pba_status_string(rc).decode()} — {L.pba_last_error().decode()}")
 
 
@@ -232,41 +236,44 @@ def _p(a: Optional[np.ndarray]):
 class Engine:
     """One engine = one problem on one GPU (include/pba.h)."""
 
-    def __init__(self, kind: int, model: int, device: int = 0, huber_width: float = 0.0):
-        L = lib()
+    def __init__(self, kind: int, model: int, device: int = 0, huber_width: float = 0.0, library: Optional[str] = None):
+        L = lib(library)
         self._L = L
         self._h = C.c_void_p()
         opt = Options(device, kind, model, huber_width)
-        _check(L.pba_create(C.byref(opt), C.byref(self._h)), "pba_create")
+        _check(L.pba_create(C.byref(opt), C.byref(self._h)), "pba_create", L)
         self.kind, self.model = kind, model
         self.n_blocks = self.n_points = self.n_frames = self._n_cams = 0
         self._keep = []
+
+    def _ck(self, rc: int, what: str):
+        _check(rc, what, self._L)
 
     # -- problem -------------------------------------------------------------------------------
     def set_problem(self, pb, images_device_ptr: Optional[int] = None):
         L, h = self._L, self._h
         intr = np.ascontiguousarray(pb.intrinsics, np.float64)
-        _check(L.pba_set_cameras(h, intr.shape[0], _p(intr)), "pba_set_cameras")
+        _check(L.pba_set_cameras(h, intr.shape[0], _p(intr)), "pba_set_cameras", L)
         self._n_cams = intr.shape[0]
         fc = np.ascontiguousarray(pb.frame_cam, np.int32)
         if images_device_ptr is not None:
             _check(L.pba_set_frames_device(h, fc.shape[0], _p(fc), pb.width, pb.height, C.c_void_p(images_device_ptr)),
-                   "pba_set_frames_device")
+                   "pba_set_frames_device", L)
         else:
             imgs = None if pb.images is None else np.ascontiguousarray(pb.images, np.uint8)
-            _check(L.pba_set_frames(h, fc.shape[0], _p(fc), pb.width, pb.height, _p(imgs)), "pba_set_frames")
+            _check(L.pba_set_frames(h, fc.shape[0], _p(fc), pb.width, pb.height, _p(imgs)), "pba_set_frames", L)
         if pb.kind == 0:
             pat = np.ascontiguousarray(pb.pattern, np.float32)
-            _check(L.pba_set_pattern(h, pat.shape[0], _p(pat)), "pba_set_pattern")
-            _check(L.pba_set_interpolator(h, int(getattr(pb, "interp", 0))), "pba_set_interpolator")
+            _check(L.pba_set_pattern(h, pat.shape[0], _p(pat)), "pba_set_pattern", L)
+            _check(L.pba_set_interpolator(h, int(getattr(pb, "interp", 0))), "pba_set_interpolator", L)
         ph = np.ascontiguousarray(pb.point_host, np.int32)
         ur = np.ascontiguousarray(pb.u_ref, np.float64)
         hi = None if (pb.kind != 0 or pb.host_intensity is None) else np.ascontiguousarray(pb.host_intensity, np.float32)
-        _check(L.pba_set_points(h, ph.shape[0], _p(ph), _p(ur), _p(hi)), "pba_set_points")
+        _check(L.pba_set_points(h, ph.shape[0], _p(ph), _p(ur), _p(hi)), "pba_set_points", L)
         bp = np.ascontiguousarray(pb.block_point, np.int32)
         bt = np.ascontiguousarray(pb.block_target, np.int32)
         uo = None if pb.u_obs is None else np.ascontiguousarray(pb.u_obs, np.float64)
-        _check(L.pba_set_blocks(h, bp.shape[0], _p(bp), _p(bt), _p(uo)), "pba_set_blocks")
+        _check(L.pba_set_blocks(h, bp.shape[0], _p(bp), _p(bt), _p(uo)), "pba_set_blocks", L)
         self.n_blocks, self.n_points, self.n_frames = bp.shape[0], ph.shape[0], fc.shape[0]
         self.R = L.pba_residuals_per_block(h)
         self.record = L.pba_record_floats(h)
@@ -276,21 +283,21 @@ class Engine:
         rho = np.ascontiguousarray(rho, np.float64)
         if poses.size != 7 * self.n_frames or rho.size != self.n_points:
             raise ValueError("state shape mismatch")
-        _check(self._L.pba_set_state(self._h, _p(poses), _p(rho)), "pba_set_state")
+        self._ck(self._L.pba_set_state(self._h, _p(poses), _p(rho)), "pba_set_state")
 
     def set_state_device(self, poses_ptr: int, rho_ptr: int):
-        _check(self._L.pba_set_state_device(self._h, C.c_void_p(poses_ptr), C.c_void_p(rho_ptr)), "pba_set_state_device")
+        self._ck(self._L.pba_set_state_device(self._h, C.c_void_p(poses_ptr), C.c_void_p(rho_ptr)), "pba_set_state_device")
 
     # -- evaluation ------------------------------------------------------------------------------
     def evaluate(self, want_jacobians: bool = True, sync: bool = True):
-        _check(self._L.pba_evaluate(self._h, int(bool(want_jacobians))), "pba_evaluate")
+        self._ck(self._L.pba_evaluate(self._h, int(bool(want_jacobians))), "pba_evaluate")
         if sync:
             self.synchronize()
 
     def evaluate_state_device(self, poses_ptr: int, rho_ptr: int, want_jacobians: bool = True, sync: bool = True):
         """Evaluate at a device-resident state and adopt it (Ceres Evaluator::Evaluate(state, …),
         program_evaluator.h:139-258): one launch for photometric engines."""
-        _check(self._L.pba_evaluate_state_device(self._h, C.c_void_p(poses_ptr), C.c_void_p(rho_ptr),
+        self._ck(self._L.pba_evaluate_state_device(self._h, C.c_void_p(poses_ptr), C.c_void_p(rho_ptr),
                                                  int(bool(want_jacobians))), "pba_evaluate_state_device")
         if sync:
             self.synchronize()
@@ -303,13 +310,13 @@ class Engine:
             raise ValueError("one ρ array per pose array")
         pa = (C.c_void_p * max(n, 1))(*poses_ptrs)
         ra = (C.c_void_p * max(n, 1))(*rho_ptrs)
-        _check(self._L.pba_evaluate_states_device(self._h, n, pa, ra, int(bool(want_jacobians))),
+        self._ck(self._L.pba_evaluate_states_device(self._h, n, pa, ra, int(bool(want_jacobians))),
                "pba_evaluate_states_device")
         if sync:
             self.synchronize()
 
     def synchronize(self):
-        _check(self._L.pba_synchronize(self._h), "pba_synchronize")
+        self._ck(self._L.pba_synchronize(self._h), "pba_synchronize")
 
     # -- reprojections / outliers (src/sfm.cpp:1928-2008) --------------------------------------------
     def compute_projections(self, obs_point, obs_frame, obs_uv, obs_is_outlier=None, thresholds=None) -> dict:
@@ -323,26 +330,26 @@ class Engine:
         th = None if thresholds is None else C.byref(OutlierThresholds(*thresholds))
         out = {"reprojected": np.zeros((n, 2)), "point_c": np.zeros((n, 3)), "error": np.zeros(n),
                "flags": np.zeros(n, np.uint32)}
-        _check(self._L.pba_compute_projections(self._h, n, _p(op), _p(of), _p(uv), _p(oo), th, _p(out["reprojected"]),
+        self._ck(self._L.pba_compute_projections(self._h, n, _p(op), _p(of), _p(uv), _p(oo), th, _p(out["reprojected"]),
                                                _p(out["point_c"]), _p(out["error"]), _p(out["flags"])),
                "pba_compute_projections")
         return out
 
     def set_record_format(self, fmt: int):
         """RECORD_F32 (default) or RECORD_F16 (records stored as IEEE halves; records() still returns floats)."""
-        _check(self._L.pba_set_record_format(self._h, fmt), "pba_set_record_format")
+        self._ck(self._L.pba_set_record_format(self._h, fmt), "pba_set_record_format")
 
     def records(self):
         rec = np.empty((self.n_blocks, self.record), np.float32)
         valid = np.empty(self.n_blocks, np.uint8)
-        _check(self._L.pba_get_records(self._h, _p(rec), _p(valid)), "pba_get_records")
+        self._ck(self._L.pba_get_records(self._h, _p(rec), _p(valid)), "pba_get_records")
         return rec, valid
 
     def sample_image(self, frame: int, uv: np.ndarray) -> np.ndarray:
         """The engine's interpolator at (column, row) positions of one frame: (n, 3) float32 [I, ∂I/∂u, ∂I/∂v]."""
         uv = np.ascontiguousarray(uv, np.float64).reshape(-1, 2)
         out = np.empty((uv.shape[0], 3), np.float32)
-        _check(self._L.pba_sample_image(self._h, frame, uv.shape[0], _p(uv), _p(out)), "pba_sample_image")
+        self._ck(self._L.pba_sample_image(self._h, frame, uv.shape[0], _p(uv), _p(out)), "pba_sample_image")
         return out
 
     def residuals(self):
@@ -350,74 +357,74 @@ class Engine:
         and the validity flags."""
         r = np.empty((self.n_blocks, self.R), np.float32)
         valid = np.empty(self.n_blocks, np.uint8)
-        _check(self._L.pba_get_residuals(self._h, _p(r), _p(valid)), "pba_get_residuals")
+        self._ck(self._L.pba_get_residuals(self._h, _p(r), _p(valid)), "pba_get_residuals")
         return r, valid
 
     def block_costs(self):
         c = np.empty(self.n_blocks, np.float32)
-        _check(self._L.pba_get_block_costs(self._h, _p(c)), "pba_get_block_costs")
+        self._ck(self._L.pba_get_block_costs(self._h, _p(c)), "pba_get_block_costs")
         return c
 
     def cost(self):
         tot, nv = C.c_double(), C.c_int32()
-        _check(self._L.pba_get_cost(self._h, C.byref(tot), C.byref(nv)), "pba_get_cost")
+        self._ck(self._L.pba_get_cost(self._h, C.byref(tot), C.byref(nv)), "pba_get_cost")
         return tot.value, nv.value
 
     def stream(self) -> int:
         s = C.c_void_p()
-        _check(self._L.pba_get_stream(self._h, C.byref(s)), "pba_get_stream")
+        self._ck(self._L.pba_get_stream(self._h, C.byref(s)), "pba_get_stream")
         return s.value or 0
 
     def set_stream(self, stream_ptr: int):
-        _check(self._L.pba_set_stream(self._h, C.c_void_p(stream_ptr)), "pba_set_stream")
+        self._ck(self._L.pba_set_stream(self._h, C.c_void_p(stream_ptr)), "pba_set_stream")
 
     def device_records(self):
         r, v, c = C.c_void_p(), C.c_void_p(), C.c_void_p()
-        _check(self._L.pba_device_records(self._h, C.byref(r), C.byref(v), C.byref(c)), "pba_device_records")
+        self._ck(self._L.pba_device_records(self._h, C.byref(r), C.byref(v), C.byref(c)), "pba_device_records")
         return r.value, v.value, c.value
 
     def enable_kernel_timing(self, on: bool = True):
-        _check(self._L.pba_enable_kernel_timing(self._h, int(on)), "pba_enable_kernel_timing")
+        self._ck(self._L.pba_enable_kernel_timing(self._h, int(on)), "pba_enable_kernel_timing")
 
     def kernel_timing(self):
         """(summed block-kernel ms, launches) since the last call (HIP events on the engine stream)."""
         ms, n = C.c_double(), C.c_int32()
-        _check(self._L.pba_get_kernel_timing(self._h, C.byref(ms), C.byref(n)), "pba_get_kernel_timing")
+        self._ck(self._L.pba_get_kernel_timing(self._h, C.byref(ms), C.byref(n)), "pba_get_kernel_timing")
         return ms.value, n.value
 
     # -- on-device Gauss-Newton / LM ---------------------------------------------------------------
     def set_fixed_frames(self, frames):
         f = np.ascontiguousarray(frames, np.int32)
-        _check(self._L.pba_set_fixed_frames(self._h, f.shape[0], _p(f) if f.size else None), "pba_set_fixed_frames")
+        self._ck(self._L.pba_set_fixed_frames(self._h, f.shape[0], _p(f) if f.size else None), "pba_set_fixed_frames")
 
     def gn_linearize(self) -> float:
         c = C.c_double()
-        _check(self._L.pba_gn_linearize(self._h, C.byref(c)), "pba_gn_linearize")
+        self._ck(self._L.pba_gn_linearize(self._h, C.byref(c)), "pba_gn_linearize")
         return c.value
 
     def gn_step(self, lam: float):
         m, st = C.c_double(), C.c_int32()
-        _check(self._L.pba_gn_step(self._h, lam, C.byref(m), C.byref(st)), "pba_gn_step")
+        self._ck(self._L.pba_gn_step(self._h, lam, C.byref(m), C.byref(st)), "pba_gn_step")
         return m.value, st.value
 
     def gn_candidate_cost(self) -> float:
         c = C.c_double()
-        _check(self._L.pba_gn_candidate_cost(self._h, C.byref(c)), "pba_gn_candidate_cost")
+        self._ck(self._L.pba_gn_candidate_cost(self._h, C.byref(c)), "pba_gn_candidate_cost")
         return c.value
 
     def gn_accept(self):
-        _check(self._L.pba_gn_accept(self._h), "pba_gn_accept")
+        self._ck(self._L.pba_gn_accept(self._h), "pba_gn_accept")
 
     def set_solver_timing(self, enable: bool):
         """per-phase device timing of solve() (linearize_ms / solve_ms / cost_ms); off by default"""
-        _check(self._L.pba_set_solver_timing(self._h, 1 if enable else 0), "pba_set_solver_timing")
+        self._ck(self._L.pba_set_solver_timing(self._h, 1 if enable else 0), "pba_set_solver_timing")
 
     def solver_iterations(self) -> dict:
         """The last solve's trajectory (pba_solver_iterations: Ceres' Solver::Summary::iterations) as arrays."""
         n = C.c_int32()
-        _check(self._L.pba_solver_iterations(self._h, 0, None, C.byref(n)), "pba_solver_iterations")
+        self._ck(self._L.pba_solver_iterations(self._h, 0, None, C.byref(n)), "pba_solver_iterations")
         arr = (IterationSummary * max(n.value, 1))()
-        _check(self._L.pba_solver_iterations(self._h, n.value, arr, C.byref(n)), "pba_solver_iterations")
+        self._ck(self._L.pba_solver_iterations(self._h, n.value, arr, C.byref(n)), "pba_solver_iterations")
         rows = arr[:n.value]
         return {f: np.array([getattr(r, f) for r in rows], np.float64 if f not in (
             "iteration", "step_is_successful", "step_is_valid") else np.int64) for f, _ in IterationSummary._fields_
@@ -427,57 +434,57 @@ class Engine:
         """pba_solve; options as solver_options() (Ceres' names and defaults, max_iterations 20)."""
         o = solver_options(**options)
         s = SolverSummary()
-        _check(self._L.pba_solve(self._h, C.byref(o), C.byref(s)), "pba_solve")
+        self._ck(self._L.pba_solve(self._h, C.byref(o), C.byref(s)), "pba_solve")
         return s.as_dict()
 
     # -- image pyramid / coarse-to-fine (pba_pyramid.hip) ---------------------------------------------
     def build_pyramid(self, n_levels: int):
-        _check(self._L.pba_build_pyramid(self._h, n_levels), "pba_build_pyramid")
+        self._ck(self._L.pba_build_pyramid(self._h, n_levels), "pba_build_pyramid")
 
     def set_level(self, level: int):
-        _check(self._L.pba_set_level(self._h, level), "pba_set_level")
+        self._ck(self._L.pba_set_level(self._h, level), "pba_set_level")
 
     def level(self):
         """(active level, its width, its height)"""
         l, w, h = C.c_int32(), C.c_int32(), C.c_int32()
-        _check(self._L.pba_get_level(self._h, C.byref(l), C.byref(w), C.byref(h)), "pba_get_level")
+        self._ck(self._L.pba_get_level(self._h, C.byref(l), C.byref(w), C.byref(h)), "pba_get_level")
         return l.value, w.value, h.value
 
     def host_intensities(self) -> np.ndarray:
         out = np.zeros((self.n_points, self._L.pba_residuals_per_block(self._h)), np.float32)
-        _check(self._L.pba_get_host_intensities(self._h, _p(out)), "pba_get_host_intensities")
+        self._ck(self._L.pba_get_host_intensities(self._h, _p(out)), "pba_get_host_intensities")
         return out
 
     def solve_pyramid(self, **options) -> dict:
         o = solver_options(**options)
         s = SolverSummary()
-        _check(self._L.pba_solve_pyramid(self._h, C.byref(o), C.byref(s)), "pba_solve_pyramid")
+        self._ck(self._L.pba_solve_pyramid(self._h, C.byref(o), C.byref(s)), "pba_solve_pyramid")
         return s.as_dict()
 
     # -- multi-GPU Gauss-Newton (include/pba.h §8e; host driver in distributed.py) ------------------
     def gn_band(self) -> int:
         b = C.c_int32()
-        _check(self._L.pba_gn_band(self._h, C.byref(b)), "pba_gn_band")
+        self._ck(self._L.pba_gn_band(self._h, C.byref(b)), "pba_gn_band")
         return b.value
 
     def gn_exchange_size(self, band: int) -> int:
         n = C.c_int64()
-        _check(self._L.pba_gn_exchange_size(self._h, band, C.byref(n)), "pba_gn_exchange_size")
+        self._ck(self._L.pba_gn_exchange_size(self._h, band, C.byref(n)), "pba_gn_exchange_size")
         return n.value
 
     def gn_step_export(self, lam: float, band: int, exchange_ptr: int):
-        _check(self._L.pba_gn_step_export(self._h, lam, band, C.c_void_p(exchange_ptr)), "pba_gn_step_export")
+        self._ck(self._L.pba_gn_step_export(self._h, lam, band, C.c_void_p(exchange_ptr)), "pba_gn_step_export")
 
     def gn_step_import(self, lam: float, band: int, exchange_ptr: int):
         """(model decrease pose part, this rank's point part, solver status)"""
         mp, mq, st = C.c_double(), C.c_double(), C.c_int32()
-        _check(self._L.pba_gn_step_import(self._h, lam, band, C.c_void_p(exchange_ptr), C.byref(mp), C.byref(mq),
+        self._ck(self._L.pba_gn_step_import(self._h, lam, band, C.c_void_p(exchange_ptr), C.byref(mp), C.byref(mq),
                                           C.byref(st)), "pba_gn_step_import")
         return mp.value, mq.value, st.value
 
     def set_rank(self, rank: int):
         """this engine's rank in solve_distributed's host-callback collective (pba_gn_set_rank)"""
-        _check(self._L.pba_gn_set_rank(self._h, int(rank)), "pba_gn_set_rank")
+        self._ck(self._L.pba_gn_set_rank(self._h, int(rank)), "pba_gn_set_rank")
 
     def solve_distributed(self, band: int, exchange_ptr: int, allreduce, **options) -> dict:
         """pba_solve_distributed; `allreduce(ptr, count) -> None` sums `count` doubles at device address `ptr`
@@ -506,34 +513,34 @@ class Engine:
         group), the exchange buffer is the engine's own."""
         o = solver_options(**options)
         s = SolverSummary()
-        _check(self._L.pba_solve_distributed_comm(self._h, C.byref(o), band, comm.handle, C.byref(s)),
+        self._ck(self._L.pba_solve_distributed_comm(self._h, C.byref(o), band, comm.handle, C.byref(s)),
                "pba_solve_distributed_comm")
         return s.as_dict()
 
     # -- target intrinsics (geometric, optimize_intrinsics) -----------------------------------------
     def set_optimize_intrinsics(self, enable: bool = True):
-        _check(self._L.pba_set_optimize_intrinsics(self._h, int(bool(enable))), "pba_set_optimize_intrinsics")
+        self._ck(self._L.pba_set_optimize_intrinsics(self._h, int(bool(enable))), "pba_set_optimize_intrinsics")
         self.record = self._L.pba_record_floats(self._h)
 
     def set_intrinsics_state(self, intrinsics: np.ndarray):
         k = np.ascontiguousarray(intrinsics, np.float64)
-        _check(self._L.pba_set_intrinsics_state(self._h, _p(k)), "pba_set_intrinsics_state")
+        self._ck(self._L.pba_set_intrinsics_state(self._h, _p(k)), "pba_set_intrinsics_state")
 
     def get_state(self):
         poses = np.empty((self.n_frames, 7), np.float64)
         rho = np.empty(self.n_points, np.float64)
-        _check(self._L.pba_get_state(self._h, _p(poses), _p(rho)), "pba_get_state")
+        self._ck(self._L.pba_get_state(self._h, _p(poses), _p(rho)), "pba_get_state")
         return poses, rho
 
     def get_intrinsics(self) -> np.ndarray:
         """the intrinsics state (n_cams × 8): the free intrinsics with set_optimize_intrinsics, else the cameras'"""
         k = np.empty((self._n_cams, 8), np.float64)
-        _check(self._L.pba_get_intrinsics(self._h, _p(k)), "pba_get_intrinsics")
+        self._ck(self._L.pba_get_intrinsics(self._h, _p(k)), "pba_get_intrinsics")
         return k
 
     def gn_system_size(self) -> int:
         n = C.c_int32()
-        _check(self._L.pba_gn_system_size(self._h, C.byref(n)), "pba_gn_system_size")
+        self._ck(self._L.pba_gn_system_size(self._h, C.byref(n)), "pba_gn_system_size")
         return n.value
 
     def gn_reduced_system(self):
@@ -542,13 +549,13 @@ class Engine:
         n = self.gn_system_size()
         S = np.empty((n, n), np.float64)
         g = np.empty(n, np.float64)
-        _check(self._L.pba_gn_get_reduced_system(self._h, _p(S), _p(g)), "pba_gn_get_reduced_system")
+        self._ck(self._L.pba_gn_get_reduced_system(self._h, _p(S), _p(g)), "pba_gn_get_reduced_system")
         return S, g
 
     def gn_last_step(self):
         dp = np.empty((self.n_frames, 6), np.float64)
         dr = np.empty(self.n_points, np.float64)
-        _check(self._L.pba_gn_get_step(self._h, _p(dp), _p(dr)), "pba_gn_get_step")
+        self._ck(self._L.pba_gn_get_step(self._h, _p(dp), _p(dr)), "pba_gn_get_step")
         return dp, dr
 
     def close(self):
@@ -572,8 +579,9 @@ class Engine:
 class Comm:
     """pba_comm: an RCCL communicator (one process per GPU) or one rank of an in-process group."""
 
-    def __init__(self, handle: C.c_void_p):
+    def __init__(self, handle: C.c_void_p, library: Optional[str] = None):
         self.handle = handle
+        self.library = library
 
     @staticmethod
     def unique_id() -> bytes:
@@ -589,25 +597,28 @@ class Comm:
         return cls(h)
 
     @classmethod
-    def local_group(cls, n_ranks: int, device: int = 0) -> list:
+    def local_group(cls, n_ranks: int, device: int = 0, library: Optional[str] = None) -> list:
+        """An in-process group of n_ranks (library: the engines' library — a communicator is used by the library that
+        made it)."""
         hs = (C.c_void_p * n_ranks)()
-        _check(lib().pba_comm_init_local(n_ranks, device, hs), "pba_comm_init_local")
-        return [cls(C.c_void_p(h)) for h in hs]
+        _check(lib(library).pba_comm_init_local(n_ranks, device, hs), "pba_comm_init_local", lib(library))
+        return [cls(C.c_void_p(h), library) for h in hs]
 
     def allreduce(self, ptr: int, count: int, stream: int = 0):
-        _check(lib().pba_comm_allreduce(self.handle, C.c_void_p(ptr), count, C.c_void_p(stream)), "pba_comm_allreduce")
+        _check(lib(self.library).pba_comm_allreduce(self.handle, C.c_void_p(ptr), count, C.c_void_p(stream)),
+               "pba_comm_allreduce", lib(self.library))
 
     @property
     def rank(self) -> int:
-        return lib().pba_comm_rank(self.handle)
+        return lib(self.library).pba_comm_rank(self.handle)
 
     @property
     def size(self) -> int:
-        return lib().pba_comm_size(self.handle)
+        return lib(self.library).pba_comm_size(self.handle)
 
     def close(self):
         if self.handle:
-            lib().pba_comm_destroy(self.handle)
+            lib(self.library).pba_comm_destroy(self.handle)
             self.handle = C.c_void_p()
 
     def __del__(self):
@@ -623,21 +634,21 @@ def load_map(map_path: str, calib_path: str):
     synth = importlib.import_module(__package__ + ".synth")
     L = lib()
     h = C.c_void_p()
-    _check(L.pba_map_load(map_path.encode(), calib_path.encode(), C.byref(h)), "pba_map_load")
+    _check(L.pba_map_load(map_path.encode(), calib_path.encode(), C.byref(h)), "pba_map_load", L)
     try:
         info = MapInfo()
-        _check(L.pba_map_get_info(h, C.byref(info)), "pba_map_get_info")
+        _check(L.pba_map_get_info(h, C.byref(info)), "pba_map_get_info", L)
         nf, npt, nb, nc, no = info.n_frames, info.n_points, info.n_blocks, info.n_cams, info.n_outlier_obs
         intr, tic = np.zeros((nc, 8)), np.zeros((nc, 7))
         fid, fcam, poses = np.zeros(nf, np.int64), np.zeros(nf, np.int32), np.zeros((nf, 7))
         tid, host, uref, rho = np.zeros(npt, np.int64), np.zeros(npt, np.int32), np.zeros((npt, 2)), np.zeros(npt)
         bp, bt, uobs = np.zeros(nb, np.int32), np.zeros(nb, np.int32), np.zeros((nb, 2))
         op, of, ouv = np.zeros(no, np.int32), np.zeros(no, np.int32), np.zeros((no, 2))
-        _check(L.pba_map_get_cameras(h, _p(intr), _p(tic)), "pba_map_get_cameras")
-        _check(L.pba_map_get_frames(h, _p(fid), _p(fcam), _p(poses)), "pba_map_get_frames")
-        _check(L.pba_map_get_points(h, _p(tid), _p(host), _p(uref), _p(rho)), "pba_map_get_points")
-        _check(L.pba_map_get_blocks(h, _p(bp), _p(bt), _p(uobs)), "pba_map_get_blocks")
-        _check(L.pba_map_get_outlier_obs(h, _p(op), _p(of), _p(ouv)), "pba_map_get_outlier_obs")
+        _check(L.pba_map_get_cameras(h, _p(intr), _p(tic)), "pba_map_get_cameras", L)
+        _check(L.pba_map_get_frames(h, _p(fid), _p(fcam), _p(poses)), "pba_map_get_frames", L)
+        _check(L.pba_map_get_points(h, _p(tid), _p(host), _p(uref), _p(rho)), "pba_map_get_points", L)
+        _check(L.pba_map_get_blocks(h, _p(bp), _p(bt), _p(uobs)), "pba_map_get_blocks", L)
+        _check(L.pba_map_get_outlier_obs(h, _p(op), _p(of), _p(ouv)), "pba_map_get_outlier_obs", L)
     finally:
         L.pba_map_destroy(h)
     pb = synth.Problem(kind=synth.GEOMETRIC, model=info.camera_model, width=info.width, height=info.height,

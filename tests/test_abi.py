@@ -24,6 +24,19 @@ def test_every_header_function_is_exported():
     assert not missing, missing
 
 
+def test_test_build_exports_the_same_abi():
+    """libpba_test.so (PBA_TEST_HOOKS: the hooks some GPU tests set) is the same ABI; the product library carries no
+    hook names at all."""
+    assert os.path.exists(E.TEST_LIB_PATH), "run __graft_entry__.build() (make test-lib)"
+    L = ctypes.CDLL(E.TEST_LIB_PATH)
+    missing = [n for n in E.header_functions() if not hasattr(L, n)]
+    assert not missing, missing
+    hooks = (b"PBA_TEST_PERTURB_DECISION", b"PBA_LM_HOST_DELAY_US", b"PBA_TEST_FORCE_DEGEN", b"PBA_LIN_LEGACY")
+    test_blob, prod_blob = open(E.TEST_LIB_PATH, "rb").read(), open(E.LIB_PATH, "rb").read()
+    assert all(h in test_blob for h in hooks)
+    assert not any(h in prod_blob for h in hooks)
+
+
 def test_status_strings_and_version():
     L = E.lib()
     assert L.pba_version() >= 100

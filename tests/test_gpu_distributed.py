@@ -19,19 +19,19 @@ E = engine_module()
 D = importlib.import_module("photometric-bundle-adjustment_amd.distributed")
 
 
-def engine_for(pb, huber, fixed):
-    eng = E.Engine(pb.kind, pb.model, huber_width=huber)
+def engine_for(pb, huber, fixed, library=None):
+    eng = E.Engine(pb.kind, pb.model, huber_width=huber, library=library)
     eng.set_problem(pb)
     eng.set_fixed_frames(np.array(fixed, np.int32))
     eng.set_state(pb.poses, pb.rho)
     return eng
 
 
-def shards(pb, world, huber, fixed):
+def shards(pb, world, huber, fixed, library=None):
     out = []
     for r in range(world):
         sub, pids, bids = D.shard_problem(pb, world, r)
-        out.append((engine_for(sub, huber, fixed), pids))
+        out.append((engine_for(sub, huber, fixed, library), pids))
     return out
 
 
@@ -195,15 +195,16 @@ def test_solve_distributed_comm_local_group_matches_solve(kind, model, huber):
 def test_solve_distributed_comm_desync_fails_loudly(monkeypatch, mode, trial):
     """The decision-word check of the device-steered loop: every trial's scalar all-reduce also sums each rank's
     previous decision word and its square (N·Σw² = (Σw)² iff the words agree).  PBA_TEST_PERTURB_DECISION overrides
-    one rank's decision of one trial (mode 1 flips accept, mode 2 ends that rank's solve): every rank must then return
-    an error naming the trial — not hang on mismatched collectives — including a perturbed last trial, which only the
-    final verification all-reduce sees."""
+    one rank's decision of one trial (mode 1 flips accept, mode 2 ends that rank's solve) — a hook of the library's test
+    build (libpba_test.so, PBA_TEST_HOOKS), which this test loads: every rank must then return an error naming the
+    trial — not hang on mismatched collectives — including a perturbed last trial, which only the final verification
+    all-reduce sees."""
     pb = synth.make_problem(kind=0, model=0, n_frames=16, n_points=400, width=376, height=240, seed=81,
                             border=12, obs_sigma=0.3)
     pb.poses[:2] = pb.poses_gt[:2]
     world, iters = 3, 6
-    sh = shards(pb, world, 9.0, (0, 1))
-    comms = E.Comm.local_group(world)
+    sh = shards(pb, world, 9.0, (0, 1), E.TEST_LIB_PATH)
+    comms = E.Comm.local_group(world, library=E.TEST_LIB_PATH)
     try:
         band = max(e.gn_band() for e, _ in sh)
         res = run_ranks(lambda r: sh[r][0].solve_distributed_comm(band, comms[r], max_iterations=iters), world,
