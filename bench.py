@@ -326,14 +326,16 @@ def gn_benchmark(eng, pb, iters, torch, dist, dev, world, ceres_problem=None, th
     opts = dict(max_iterations=iters, function_tolerance=0.0)
     agree = None
     traj = None
-    device_steered = world > 1 and dist.get_backend() == "nccl" and os.environ.get("PBA_BENCH_GN_COMM", "1") != "0"
+    device_steered = world > 1 and dist.get_backend() == "nccl" and os.environ.get("PBA_BENCH_GN_COMM", "0") == "1"
     if world > 1:
         band = D.global_band(eng, None, dev)
-        # Default under RCCL: the device-steered loop (pba_solve_distributed_comm: both all-reduces of every trial on
-        # the engine stream, the next trial enqueued ahead of the decision).  Every trial's scalar all-reduce also checks
-        # that the ranks took the same previous decision, and a final all-reduce checks the last one: ranks that
-        # disagree end the solve with an error instead of hanging on mismatched collectives.  PBA_BENCH_GN_COMM=0
-        # selects the host-callback loop (pba_solve_distributed, torch's all_reduce between trials).
+        # Default: the host-callback loop (pba_solve_distributed: torch.distributed's all_reduce — RCCL under "nccl" —
+        # between trials, host decisions from the all-reduced sums).  PBA_BENCH_GN_COMM=1 selects the device-steered
+        # loop (pba_solve_distributed_comm: both all-reduces of every trial on the engine stream through the engine's
+        # own RCCL communicator, the next trial enqueued ahead of the decision, every trial's scalar all-reduce checking
+        # that the ranks took the same previous decision).  That loop has run with one RCCL rank and with in-process
+        # groups only (no multi-GPU box in the build pipeline), so the unattended N > 1 bench uses torch's collective,
+        # whose only failure mode is an error, not a hang on mismatched stream-ordered collectives.
         comm = None if device_steered else False
         D.solve_distributed(eng, device=dev, comm=comm, max_iterations=1)  # warm-up (sets the RCCL communicator up)
         eng.set_state(pb.poses, pb.rho)
@@ -755,9 +757,9 @@ def main():
                 except Exception as ex:  # a secondary leg: report it, keep the headline line
                     c2 = {"error": f"{type(ex).__name__}: {ex}"[:300]}
         stream_peak = stream_copy_peak(torch, dev, achieved)
-        # the GN leg's collective, as the leg chooses it (device-steered under RCCL unless PBA_BENCH_GN_COMM=0)
+        # the GN leg's collective, as the leg chooses it (torch.distributed between trials unless PBA_BENCH_GN_COMM=1)
         gn_comm = ("device-steered RCCL loop" if world > 1 and dist.get_backend() == "nccl"
-                   and os.environ.get("PBA_BENCH_GN_COMM", "1") != "0" else "torch.distributed between trials")
+                   and os.environ.get("PBA_BENCH_GN_COMM", "0") == "1" else "torch.distributed between trials")
         out = {
             "metric": "photometric residual+jacobian blocks/sec",
             "value": value,

@@ -247,7 +247,8 @@ typedef struct pba_solver_summary {
    * default and the parts are then 0): solve_ms = Schur complement + reduced solve + candidate state, linearize_ms =
    * the linearisation at each candidate (which is also its cost; plus the initial one), cost_ms = the decision; pba_solve_distributed — host wall clock of each phase, collectives included. */
   double total_ms, linearize_ms, solve_ms, cost_ms;
-  double gradient_max_norm;             /* at the last state whose gradient was evaluated */
+  double gradient_max_norm;             /* at the last state whose gradient was evaluated; pba_solve_distributed(_comm):
+                                         * rank-local — max(the global pose part, this rank's points) */
   int32_t stop_reason, pad_;            /* PBA_STOP_* */
 } pba_solver_summary;
 /* per-phase device timing of pba_solve (linearize_ms / solve_ms / cost_ms of the summary); default off */
@@ -259,7 +260,8 @@ int pba_set_solver_timing(pba_engine* engine, int32_t enable);
  * minimum trust-region radius — but not the trial that met the parameter / function tolerance or the invalid-step limit
  * (Minimize returns before FinalizeIteration, :110-115, :453-466).  cost: accepted — the new state's; rejected — the
  * candidate's (:124); invalid — the current state's.  trust_region_radius: after this iteration's update (:327).
- * gradient_max_norm: at the state the iteration ended in (a rejected step keeps the previous one, :130). */
+ * gradient_max_norm: at the state the iteration ended in (a rejected step keeps the previous one, :130); after a
+ * distributed solve it is rank-local (the global pose part, this rank's points), where Ceres reports the global value. */
 typedef struct pba_iteration_summary {
   int32_t iteration, step_is_successful, step_is_valid, pad_;
   double cost, cost_change, relative_decrease, trust_region_radius, step_norm, gradient_max_norm;
