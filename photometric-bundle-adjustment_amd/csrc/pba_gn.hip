@@ -2951,8 +2951,8 @@ __global__ __launch_bounds__(256) void arrow_reduce_kernel(const ArrowArgs a) {
   if (threadIdx.x == 0) a.part[e] = ((s_w[0] + s_w[1]) + s_w[2]) + s_w[3];
 }
 
-// The border system Sc = C − BᵀX_B, rc = −g_c − BᵀX_0 (partials added in workgroup order), its Cholesky in LDS and
-// δc = Sc⁻¹ rc (the border's part of the step); one workgroup.
+// The border system Sc = C − BᵀX_B, rc = −g_c − BᵀX_0, its Cholesky in LDS and δc = Sc⁻¹ rc (the border's part of the
+// step); one workgroup.  (A one-wave form without workgroup barriers measured no faster: 15.4 → 17.0 µs at C4.)
 __global__ __launch_bounds__(256) void arrow_cap_kernel(const ArrowArgs a) {
   constexpr int NBM = 12 * kArrowMaxNc;
   __shared__ double sc[NBM][NBM + 1];
@@ -3536,7 +3536,35 @@ struct IntrBorderArgs {
   int nf, nc;
   double* X = nullptr;     // multi-GPU export (pba_gn_step_export): this rank's border rows, undamped, into the exchange
   long long xs = 0;        // buffer's border region (row stride nfs·36 + EX_TAIL) instead of S
+  const double* pw = nullptr;  // GN point → its camera sums W_c (8 per camera) and W_h = Σ J_hᵀJ_ρ (6): intr_pw_kernel
 };
+
+// Per GN point, over its blocks in order: W_c = Σ_{b: camera(b) = c} W_i(b) for every camera c, and W_h = Σ_b J_h(b)ᵀJ_ρ(b)
+// (every block of a point has the point's host).  The border kernels' Schur terms read these 8·nc + 6 values instead of
+// walking the point's blocks (4-5 × 52 doubles) once per (point, list) — at C4 that walk re-read the blocks' rows five
+// times per kernel, ≈ 0.4 GB per launch.  The same sums in the same order: the border is unchanged bit for bit.
+__global__ __launch_bounds__(256) void intr_pw_kernel(const IntrBorderArgs a, int n_points) {
+  // 8 lanes per point: lane k sums component k of every camera's W_c and (k < 6) of W_h, over the blocks in order
+  const int t = blockIdx.x * blockDim.x + threadIdx.x, gp = t >> 3, k = t & 7;
+  if (gp >= n_points) return;
+  const int4 pr = a.pt_rec[gp];
+  const int st = 8 * a.nc + 6;
+  double* o = const_cast<double*>(a.pw) + (long long)gp * st;
+  double wh = 0.0;
+  for (int c0 = 0; c0 < a.nc; c0 += 4) {  // cameras in groups of four (one pass over the blocks per group)
+    double wc[4] = {0.0, 0.0, 0.0, 0.0};
+    for (int b = pr.x; b < pr.x + pr.y; ++b) {
+      const double* B = a.ib + (long long)b * kIbStride;
+      const int cb = a.ib_cam[b] - c0;
+      const double w = B[kIbWi + k];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) wc[c] += c == cb ? w : 0.0;
+      if (c0 == 0 && k < 6) wh += B[kIbJh + k] * B[kIbJr] + B[kIbJh + 6 + k] * B[kIbJr + 1];
+    }
+    for (int c = 0; c < 4 && c0 + c < a.nc; ++c) o[8 * (c0 + c) + k] = wc[c];
+  }
+  if (k < 6) o[8 * a.nc + k] = wh;
+}
 
 // Element t of border row `row` (system frame P = nf + row): t < (P + 1)·36 → entry (r, cc) of block (P, y = t / 36) of
 // the skyline system; t = nfs·36 … nfs·36 + 5 → g of P.  The keyframe blocks (P, x < nf) and the camera blocks (P, y ≥ nf)
@@ -3600,27 +3628,28 @@ __device__ __forceinline__ void border_store(const IntrBorderArgs& a, double lam
   a.S[((long long)a.sky_row[P] + (y - a.sky_first[P])) * 36 + e] = val;
 }
 
-// The keyframe blocks (P, y < nf): kpw WAVES per block (grid x: 4/kpw keyframes per workgroup; y: camera c; NR = 6 →
-// border row 2c, NR = 2 → row 2c + 1, whose frame holds intrinsics 6, 7 and four pads), all 6·NR live entries at once —
-// a lane takes every (64·kpw)th entry of the block's lists (the keyframe's blocks and points seen by the camera), each
-// wave adds its lanes' sums by xor butterflies and the kpw waves' sums are added in order (a fixed order), lane e stores
-// entry e.  kpw = 4 while the keyframe waves would not fill the SIMDs (C3, 200 keyframes: 95 → 40 µs per launch), else 1
-// (C4: 1004 waves; four per keyframe re-read the lists' data at 4× the waves, 133 → 160 µs).  (One wave per ENTRY
-// re-walked each list 36 times: 0.5 ms per launch at C3.)
-template <int NR>
+// The keyframe blocks (P, y < nf) of both border rows of a camera: kpw WAVES per keyframe y (grid x: 4/kpw keyframes per
+// workgroup; y: camera c) form the 8 × 6 live entries of (2c, y) and (2c + 1, y) — row 2c + 1's frame holds intrinsics 6,
+// 7 and four pads — at once: a lane takes every (64·kpw)th entry of the keyframe's lists (its blocks and points seen by
+// the camera), each wave adds its lanes' sums by xor butterflies and the kpw waves' sums are added in order (a fixed
+// order).  kpw = 4 while the keyframe waves would not fill the SIMDs (C3, 200 keyframes), else 1 (C4: 1004 waves).  Round 5
+// walked the lists twice (one kernel per border row: 133 + 117 µs at C4) and each point's blocks once per (point, list).
 __global__ __launch_bounds__(256) void intr_border_kernel(const IntrBorderArgs a, double lambda, int kpw) {
-  __shared__ double2 s_w[4][36];
+  __shared__ double2 s_w[4][48];
   lambda = lm_lambda(lm_view(a.lm), lambda);
-  const int c = blockIdx.y, row = 2 * c + (NR == 6 ? 0 : 1), h = row & 1, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int c = blockIdx.y, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int gw = blockIdx.x * 4 + w, y0 = gw / kpw, sub = gw % kpw;
   const int y = min(y0, a.nf - 1);  // (a wave past the last keyframe walks nothing and stores nothing)
   const int L = c * (a.nf + a.nc) + y;
   const int q0 = sub * 64 + lane, dq = y0 < a.nf ? 64 * kpw : 1 << 30;
-  double dir[NR][6], sch[NR][6];
+  // the 8 intrinsics rows d of camera c (border rows 2c: d = 0…5, 2c + 1: d = 6, 7) × the keyframe's 6 columns; the
+  // direct terms first, then the Schur terms in the same registers; lane v < 48 ends with value v = 6d + cc of each
+  double acc[8][6];
+  double vd = 0.0, vs = 0.0;
 #pragma unroll
-  for (int r = 0; r < NR; ++r)
+  for (int d = 0; d < 8; ++d)
 #pragma unroll
-    for (int cc = 0; cc < 6; ++cc) dir[r][cc] = sch[r][cc] = 0.0;
+    for (int cc = 0; cc < 6; ++cc) acc[d][cc] = 0.0;
   for (int q = a.bptr[L] + (y0 < a.nf ? q0 : 1 << 30); q < a.bptr[L + 1]; q += dq) {
     const int b = a.blist[q];
     const double* B = a.ib + (long long)b * kIbStride;
@@ -3632,171 +3661,194 @@ __global__ __launch_bounds__(256) void intr_border_kernel(const IntrBorderArgs a
       c1[cc] = Jc[6 + cc];
     }
 #pragma unroll
-    for (int r = 0; r < NR; ++r) {
-      const double j0 = B[kIbJi + 6 * h + r], j1 = B[kIbJi + 8 + 6 * h + r];
+    for (int d = 0; d < 8; ++d) {
+      const double j0 = B[kIbJi + d], j1 = B[kIbJi + 8 + d];
 #pragma unroll
-      for (int cc = 0; cc < 6; ++cc) dir[r][cc] += j0 * c0[cc] + j1 * c1[cc];
+      for (int cc = 0; cc < 6; ++cc) acc[d][cc] += j0 * c0[cc] + j1 * c1[cc];
     }
   }
+#pragma unroll
+  for (int d = 0; d < 8; ++d)
+#pragma unroll
+    for (int cc = 0; cc < 6; ++cc) {
+      const double t = wave_sum(acc[d][cc]);
+      vd = lane == d * 6 + cc ? t : vd;
+      acc[d][cc] = 0.0;
+    }
   for (int q = a.pptr[L] + (y0 < a.nf ? q0 : 1 << 30); q < a.pptr[L + 1]; q += dq) {
     const int gp = a.plist[q];
     const int4 pr = a.pt_rec[gp];
-    double wc[NR], wy[6];  // W of the point for the camera's columns 6h + r (Σ W_i over its blocks
-                           // seen by c) and for keyframe y (Σ J_h / J_t ᵀJ_ρ over its blocks hosted / targeted by y)
+    double wc[8], wy[6];  // W of the point for camera c (Σ W_i over its blocks seen by c, intr_pw_kernel) and for
+                          // keyframe y (Σ J_h / J_t ᵀJ_ρ over its blocks hosted / targeted by y)
+    const double* pw = a.pw + (long long)gp * (8 * a.nc + 6);
 #pragma unroll
-    for (int r = 0; r < NR; ++r) wc[r] = 0.0;
+    for (int d = 0; d < 8; ++d) wc[d] = pw[8 * c + d];
+    if (pr.z == y) {  // y hosts the point: every block's J_hᵀJ_ρ (intr_pw_kernel)
 #pragma unroll
-    for (int cc = 0; cc < 6; ++cc) wy[cc] = 0.0;
-    for (int b = pr.x; b < pr.x + pr.y; ++b) {
-      const double* B = a.ib + (long long)b * kIbStride;
-      if (a.ib_cam[b] == c) {
+      for (int cc = 0; cc < 6; ++cc) wy[cc] = pw[8 * a.nc + cc];
+    } else {          // y is a target: its block(s) of the point
 #pragma unroll
-        for (int r = 0; r < NR; ++r) wc[r] += B[kIbWi + 6 * h + r];
-      }
-      const int4 rr = a.ib_rec[b];
-      if (rr.z == y) {
-#pragma unroll
-        for (int cc = 0; cc < 6; ++cc) wy[cc] += B[kIbJh + cc] * B[kIbJr] + B[kIbJh + 6 + cc] * B[kIbJr + 1];
-      }
-      if (rr.w == y) {
+      for (int cc = 0; cc < 6; ++cc) wy[cc] = 0.0;
+      for (int b = pr.x; b < pr.x + pr.y; ++b) {
+        if (a.ib_rec[b].w != y) continue;
+        const double* B = a.ib + (long long)b * kIbStride;
 #pragma unroll
         for (int cc = 0; cc < 6; ++cc) wy[cc] += B[kIbJt + cc] * B[kIbJr] + B[kIbJt + 6 + cc] * B[kIbJr + 1];
       }
     }
     const double inv = border_inv(a, gp, lambda);
 #pragma unroll
-    for (int r = 0; r < NR; ++r)
+    for (int d = 0; d < 8; ++d)
 #pragma unroll
-      for (int cc = 0; cc < 6; ++cc) sch[r][cc] += inv * wc[r] * wy[cc];
+      for (int cc = 0; cc < 6; ++cc) acc[d][cc] += inv * wc[d] * wy[cc];
   }
-  double vd = 0.0, vs = 0.0;
 #pragma unroll
-  for (int r = 0; r < NR; ++r)
+  for (int d = 0; d < 8; ++d)
 #pragma unroll
     for (int cc = 0; cc < 6; ++cc) {
-      const double d = wave_sum(dir[r][cc]), sc = wave_sum(sch[r][cc]);
-      vd = lane == r * 6 + cc ? d : vd;
-      vs = lane == r * 6 + cc ? sc : vs;
+      const double t = wave_sum(acc[d][cc]);
+      vs = lane == d * 6 + cc ? t : vs;
     }
-  if (kpw == 1) {
-    if (lane < 36 && y0 < a.nf) border_store(a, lambda, row, y * 36 + lane, vd, vs);
-    return;
+  if (kpw > 1) {  // the keyframe's kpw waves, in order
+    if (lane < 48) s_w[w][lane] = make_double2(vd, vs);
+    __syncthreads();
+    if (sub == 0 && lane < 48) {
+      double2 t = s_w[w][lane];
+      for (int k = 1; k < kpw; ++k) {
+        t.x += s_w[w + k][lane].x;
+        t.y += s_w[w + k][lane].y;
+      }
+      vd = t.x;
+      vs = t.y;
+    }
+    if (sub != 0) return;  // (whole waves)
   }
-  if (lane < 36) s_w[w][lane] = make_double2(vd, vs);
-  __syncthreads();
-  if (sub != 0 || lane >= 36 || y0 >= a.nf) return;
-  double2 t = s_w[w][lane];
-  for (int k = 1; k < kpw; ++k) {
-    t.x += s_w[w + k][lane].x;
-    t.y += s_w[w + k][lane].y;
+  // row 2c + 1's live entries (d = 6, 7: values 36 … 47) to lanes 0 … 11; its other entries are pads (border_store)
+  const double xd = __shfl(vd, 36 + (lane % 12), 64), xs = __shfl(vs, 36 + (lane % 12), 64);
+  if (lane < 36 && y0 < a.nf) {
+    border_store(a, lambda, 2 * c, y * 36 + lane, vd, vs);
+    border_store(a, lambda, 2 * c + 1, y * 36 + lane, lane < 12 ? xd : 0.0, lane < 12 ? xs : 0.0);
   }
-  border_store(a, lambda, row, y * 36 + lane, t.x, t.y);
 }
 
-// The camera blocks (P, y ≥ nf) and the gradient of P: their lists hold ALL of a camera's blocks and points (80k / 20k at
-// C3), so each block is split over kIbSplit workgroups (grid x: yb — camera block y = nf + yb for yb < 2nc, the gradient
-// for yb = 2nc; y: camera c, NR as intr_border_kernel; z: split s), thread k of split s taking list entries k + 256·s,
-// + 256·kIbSplit, …, all 6·NR entries at once; the workgroup's totals (wave butterflies, then its four waves in order)
-// go to part, and intr_border_fin_kernel adds the kIbSplit totals in order — a fixed order end to end.
-constexpr int kIbSplit = 256;  // (32 until round 5: 96 workgroups for one camera, 195 µs per launch at C4)
-template <int NR>
-__global__ __launch_bounds__(256) void intr_border_cam_kernel(const IntrBorderArgs a, double lambda, double2* part) {
-  __shared__ double2 s_w[4][36];
-  lambda = lm_lambda(lm_view(a.lm), lambda);
-  const int c = blockIdx.y, row = 2 * c + (NR == 6 ? 0 : 1), h = row & 1, yb = blockIdx.x, nb = 2 * a.nc + 1;
-  const bool grad = yb == 2 * a.nc;
-  const int y = a.nf + yb;
-  if (!grad && y > a.nf + row) return;  // above the diagonal: not stored (uniform per workgroup)
-  const int c2 = yb >> 1, L = c * (a.nf + a.nc) + a.nf + (grad ? c : c2), o2 = 6 * (yb & 1);
-  const int q0 = threadIdx.x + 256 * blockIdx.z, dq = 256 * kIbSplit;
-  double dir[NR][6], sch[NR][6];
-#pragma unroll
-  for (int r = 0; r < NR; ++r)
-#pragma unroll
-    for (int cc = 0; cc < 6; ++cc) dir[r][cc] = sch[r][cc] = 0.0;
-  for (int q = a.bptr[L] + q0; q < a.bptr[L + 1]; q += dq) {
-    const double* B = a.ib + (long long)a.blist[q] * kIbStride;
-    double c0[6], c1[6];  // the gradient: the residual; a camera block: intrinsics columns o2 … o2 + 5 (< 8 used)
-#pragma unroll
-    for (int cc = 0; cc < 6; ++cc) {
-      c0[cc] = grad ? B[kIbR] : B[kIbJi + min(o2 + cc, 7)];
-      c1[cc] = grad ? B[kIbR + 1] : B[kIbJi + 8 + min(o2 + cc, 7)];
-    }
-#pragma unroll
-    for (int r = 0; r < NR; ++r) {
-      const double j0 = B[kIbJi + 6 * h + r], j1 = B[kIbJi + 8 + 6 * h + r];
-#pragma unroll
-      for (int cc = 0; cc < 6; ++cc) dir[r][cc] += j0 * c0[cc] + j1 * c1[cc];
-    }
-  }
-  for (int q = a.pptr[L] + q0; q < a.pptr[L + 1]; q += dq) {
-    const int gp = a.plist[q];
-    const int4 pr = a.pt_rec[gp];
-    double wc[NR], wy[6];  // W of the point for camera c's columns 6h + r and camera c2's o2 + cc
-#pragma unroll
-    for (int r = 0; r < NR; ++r) wc[r] = 0.0;
-#pragma unroll
-    for (int cc = 0; cc < 6; ++cc) wy[cc] = 0.0;
-    for (int b = pr.x; b < pr.x + pr.y; ++b) {
-      const double* B = a.ib + (long long)b * kIbStride;
-      const int cb = a.ib_cam[b];
-      if (cb == c) {
-#pragma unroll
-        for (int r = 0; r < NR; ++r) wc[r] += B[kIbWi + 6 * h + r];
-      }
-      if (!grad && cb == c2) {
-#pragma unroll
-        for (int cc = 0; cc < 6; ++cc) wy[cc] += B[kIbWi + min(o2 + cc, 7)];
-      }
-    }
-    const double inv = border_inv(a, gp, lambda);
-    if (grad) {
-      const double gr = a.pt_data[(long long)gp * 8 + 1];
-#pragma unroll
-      for (int cc = 0; cc < 6; ++cc) wy[cc] = gr;
-    }
-#pragma unroll
-    for (int r = 0; r < NR; ++r)
-#pragma unroll
-      for (int cc = 0; cc < 6; ++cc) sch[r][cc] += inv * wc[r] * wy[cc];
-  }
+// The camera blocks (P = nf + 2c + h, y = nf + 2c2 + h2 ≥ nf, c2 ≤ c) and the gradient rows of the border, as two
+// reductions over whole lists instead of one list walk per (border row, column block) — the list of a camera holds ALL
+// of its blocks (400k at C4) and points (100k), and round 5 walked it six times per trial (two row kernels × three column
+// blocks, 165 µs at C4 with the finishing kernel):
+//   intr_cam_dir_kernel — per camera c, over its blocks: Σ J_iᵀJ_i (the 8 × 8 upper triangle, 36) and Σ J_iᵀr (8): the
+//     direct terms (a block's intrinsics Jacobian is its target camera's, so the direct part couples a camera only with
+//     itself);
+//   intr_cam_sch_kernel — per camera pair (c, c2 ≤ c), over the points seen by both: Σ_p W_c W_c2ᵀ / H'_ρρ (8 × 8) and,
+//     for c2 = c, Σ_p W_c g_ρ / H'_ρρ (8): the Schur terms (W_c from intr_pw_kernel);
+// each over kCamSplit workgroups (a thread takes every (256·kCamSplit)th entry; wave butterflies, then the four waves in
+// order), and intr_cam_fin_kernel adds the kCamSplit totals in order per element and stores it (border_store) — a fixed
+// order end to end.
+constexpr int kCamSplit = 128;  // (512 measured no faster at C4, 2.7× slower for two cameras' Schur sums at C3)
+constexpr int kCamDir = 44, kCamSch = 72;  // accumulators per thread
+
+__device__ __forceinline__ int upper8i(int i, int j) { return i * 8 - i * (i - 1) / 2 + (j - i); }  // i ≤ j < 8
+
+// Σ over the workgroup of NV per-thread accumulators in a fixed order → out[0 … NV).  Every thread calls it.
+template <int NV>
+__device__ __forceinline__ void wg_sum_store(const double* acc, double* s_w, double* out) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  double vd = 0.0, vs = 0.0;
 #pragma unroll
-  for (int r = 0; r < NR; ++r)
-#pragma unroll
-    for (int cc = 0; cc < 6; ++cc) {
-      const double d = wave_sum(dir[r][cc]), sc = wave_sum(sch[r][cc]);
-      vd = lane == r * 6 + cc ? d : vd;
-      vs = lane == r * 6 + cc ? sc : vs;
-    }
-  if (lane < 36) s_w[w][lane] = make_double2(vd, vs);
-  __syncthreads();
-  if (threadIdx.x >= 36) return;
-  double2 t = s_w[0][threadIdx.x];
-  for (int k = 1; k < 4; ++k) {
-    t.x += s_w[k][threadIdx.x].x;
-    t.y += s_w[k][threadIdx.x].y;
+  for (int v = 0; v < NV; ++v) {
+    const double t = wave_sum(acc[v]);
+    if (lane == 0) s_w[w * NV + v] = t;
   }
-  part[(((long long)row * nb + yb) * kIbSplit + blockIdx.z) * 36 + threadIdx.x] = t;
+  __syncthreads();
+  for (int v = threadIdx.x; v < NV; v += blockDim.x) out[v] = ((s_w[v] + s_w[NV + v]) + s_w[2 * NV + v]) + s_w[3 * NV + v];
 }
-// One thread per (border row, yb, entry e): the kIbSplit totals in order, then border_store (the gradient: e < 6 →
-// g[6P + e], column 0 of the entries).
-__global__ __launch_bounds__(256) void intr_border_fin_kernel(const IntrBorderArgs a, double lambda,
-                                                              const double2* part) {
+
+__global__ __launch_bounds__(256) void intr_cam_dir_kernel(const IntrBorderArgs a, double* part) {
+  __shared__ double s_w[4 * kCamDir];
+  const int c = blockIdx.y, L = c * (a.nf + a.nc) + a.nf + c;  // (camera c, unit nf + c): every block of camera c
+  double acc[kCamDir];
+#pragma unroll
+  for (int v = 0; v < kCamDir; ++v) acc[v] = 0.0;
+  for (int q = a.bptr[L] + threadIdx.x + 256 * blockIdx.x; q < a.bptr[L + 1]; q += 256 * kCamSplit) {
+    const double* B = a.ib + (long long)a.blist[q] * kIbStride;
+    double j0[8], j1[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      j0[k] = B[kIbJi + k];
+      j1[k] = B[kIbJi + 8 + k];
+    }
+    const double r0 = B[kIbR], r1 = B[kIbR + 1];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+#pragma unroll
+      for (int j = i; j < 8; ++j) acc[upper8i(i, j)] += j0[i] * j0[j] + j1[i] * j1[j];
+      acc[36 + i] += j0[i] * r0 + j1[i] * r1;
+    }
+  }
+  wg_sum_store<kCamDir>(acc, s_w, part + ((long long)c * kCamSplit + blockIdx.x) * kCamDir);
+}
+
+__global__ __launch_bounds__(256) void intr_cam_sch_kernel(const IntrBorderArgs a, double lambda, double* part) {
+  __shared__ double s_w[4 * kCamSch];
   lambda = lm_lambda(lm_view(a.lm), lambda);
-  const int nb = 2 * a.nc + 1, i = blockIdx.x * blockDim.x + threadIdx.x;
+  const int pc = blockIdx.y;  // camera pair (c, c2 ≤ c), pc = c(c+1)/2 + c2
+  int c = 0;
+  while ((c + 1) * (c + 2) / 2 <= pc) ++c;
+  const int c2 = pc - c * (c + 1) / 2, L = c * (a.nf + a.nc) + a.nf + c2;  // points seen by c and c2
+  const int st = 8 * a.nc + 6;
+  double acc[kCamSch];
+#pragma unroll
+  for (int v = 0; v < kCamSch; ++v) acc[v] = 0.0;
+  for (int q = a.pptr[L] + threadIdx.x + 256 * blockIdx.x; q < a.pptr[L + 1]; q += 256 * kCamSplit) {
+    const int gp = a.plist[q];
+    const double* pw = a.pw + (long long)gp * st;
+    const double inv = border_inv(a, gp, lambda), gr = a.pt_data[(long long)gp * 8 + 1];
+    double wc[8], w2[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      wc[k] = pw[8 * c + k];
+      w2[k] = pw[8 * c2 + k];
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const double iw = inv * wc[i];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[8 * i + j] += iw * w2[j];
+      acc[64 + i] += iw * gr;
+    }
+  }
+  wg_sum_store<kCamSch>(acc, s_w, part + ((long long)pc * kCamSplit + blockIdx.x) * kCamSch);
+}
+
+// One WAVE per (border row, camera column block yb ≤ row, entry e) and per border gradient element: lane l adds totals l,
+// l + 64, … of the kCamSplit in order, the wave's lanes by xor butterflies (a fixed order); then border_store.
+__global__ __launch_bounds__(256) void intr_cam_fin_kernel(const IntrBorderArgs a, double lambda, const double* dpart,
+                                                          const double* spart) {
+  lambda = lm_lambda(lm_view(a.lm), lambda);
+  const int nb = 2 * a.nc + 1, i = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (i >= 2 * a.nc * nb * 36) return;
   const int e = i % 36, yb = (i / 36) % nb, row = i / (36 * nb);
   const bool grad = yb == 2 * a.nc;
-  if (grad ? (e % 6 != 0) : (a.nf + yb > a.nf + row)) return;
-  const double2* pp = part + (((long long)row * nb + yb) * kIbSplit) * 36 + e;
-  double2 w = pp[0];
-  for (int k = 1; k < kIbSplit; ++k) {
-    w.x += pp[36 * k].x;
-    w.y += pp[36 * k].y;
+  if (grad ? (e % 6 != 0) : (yb > row)) return;  // (the upper camera blocks are not stored; whole waves)
+  const int c = row >> 1, h = row & 1, r = e / 6, cc = e % 6, d = 6 * h + r;
+  auto sum = [&](const double* p, int stride, int idx) {
+    double v = 0.0;
+    for (int s = lane; s < kCamSplit; s += 64) v += p[(long long)s * stride + idx];
+    return wave_sum(v);
+  };
+  double dir = 0.0, sch = 0.0;
+  if (grad) {
+    if (d < 8) {
+      dir = sum(dpart + (long long)c * kCamSplit * kCamDir, kCamDir, 36 + d);
+      sch = sum(spart + (long long)(c * (c + 1) / 2 + c) * kCamSplit * kCamSch, kCamSch, 64 + d);
+    }
+    if (lane == 0) border_store(a, lambda, row, (a.nf + 2 * a.nc) * 36 + r, dir, sch);
+    return;
   }
-  border_store(a, lambda, row, grad ? (a.nf + 2 * a.nc) * 36 + e / 6 : (a.nf + yb) * 36 + e, w.x, w.y);
+  const int c2 = yb >> 1, d2 = 6 * (yb & 1) + cc;
+  if (d < 8 && d2 < 8) {  // (pads: border_store's identity rows)
+    if (c2 == c) dir = sum(dpart + (long long)c * kCamSplit * kCamDir, kCamDir, upper8i(min(d, d2), max(d, d2)));
+    sch = sum(spart + (long long)(c * (c + 1) / 2 + c2) * kCamSplit * kCamSch, kCamSch, 8 * d + d2);
+  }
+  if (lane == 0) border_store(a, lambda, row, (a.nf + yb) * 36 + e, dir, sch);
 }
 
 // The candidate intrinsics become the state (after an accepted trial; lm == nullptr: always), fp64 records and fp32 copy.
@@ -4787,7 +4839,8 @@ int gn_prepare(pba_engine* e) {
     PBA_HIP(G.ib_pptr.upload(pp, st0));
     PBA_HIP(G.ib_plist.upload(pflat, st0));
     PBA_HIP(G.ib_data.resize((size_t)nb * kIbStride));
-    PBA_HIP(G.ib_part.resize((size_t)2 * nc * (2 * nc + 1) * kIbSplit * 36));
+    PBA_HIP(G.ib_pw.resize((size_t)std::max(ngp, 1) * (8 * nc + 6)));
+    PBA_HIP(G.ib_part.resize((size_t)kCamSplit * (nc * kCamDir + nc * (nc + 1) / 2 * kCamSch)));
     PBA_HIP(G.intr_new_d.resize((size_t)kCamD * nc));
     PBA_HIP(G.intr_new_f.resize((size_t)8 * nc));
     // the candidate records start as the state's (their unprojection half is never read: hosts unproject with the cameras)
@@ -5302,14 +5355,16 @@ void enqueue_border(pba_engine* e, double lambda, const double* lm, double* X) {
   const int nf = e->n_frames, nfs = G.nfs;
   IntrBorderArgs ba{G.ib_data.p, G.ib_rec.p, G.ib_cam.p, G.pt_rec.p, G.pt_data.p, G.ib_bptr.p, G.ib_blist.p,
                     G.ib_pptr.p, G.ib_plist.p, G.sky_first.p, G.sky_row.p, G.fixed.p, lm ? lm : G.lm_idle.p, G.S.p,
-                    G.g.p, G.g_dir.p, G.Ddiag.p, nf, G.nc_sys, X, (long long)nfs * 36 + EX_TAIL};
+                    G.g.p, G.g_dir.p, G.Ddiag.p, nf, G.nc_sys, X, (long long)nfs * 36 + EX_TAIL, G.ib_pw.p};
   const int nb = 2 * G.nc_sys + 1;
+  intr_pw_kernel<<<(8 * G.n_gn_points + 255) / 256, 256, 0, e->stream>>>(ba, G.n_gn_points);
   const int kpw = nf * G.nc_sys < 512 ? 4 : 1;  // waves per keyframe block (intr_border_kernel)
-  intr_border_kernel<6><<<dim3((nf * kpw + 3) / 4, G.nc_sys), 256, 0, e->stream>>>(ba, lambda, kpw);
-  intr_border_kernel<2><<<dim3((nf * kpw + 3) / 4, G.nc_sys), 256, 0, e->stream>>>(ba, lambda, kpw);
-  intr_border_cam_kernel<6><<<dim3(nb, G.nc_sys, kIbSplit), 256, 0, e->stream>>>(ba, lambda, G.ib_part.p);
-  intr_border_cam_kernel<2><<<dim3(nb, G.nc_sys, kIbSplit), 256, 0, e->stream>>>(ba, lambda, G.ib_part.p);
-  intr_border_fin_kernel<<<(2 * G.nc_sys * nb * 36 + 255) / 256, 256, 0, e->stream>>>(ba, lambda, G.ib_part.p);
+  intr_border_kernel<<<dim3((nf * kpw + 3) / 4, G.nc_sys), 256, 0, e->stream>>>(ba, lambda, kpw);
+  double* dpart = G.ib_part.p;
+  double* spart = dpart + (size_t)G.nc_sys * kCamSplit * kCamDir;
+  intr_cam_dir_kernel<<<dim3(kCamSplit, G.nc_sys), 256, 0, e->stream>>>(ba, dpart);
+  intr_cam_sch_kernel<<<dim3(kCamSplit, G.nc_sys * (G.nc_sys + 1) / 2), 256, 0, e->stream>>>(ba, lambda, spart);
+  intr_cam_fin_kernel<<<(2 * G.nc_sys * nb * 36 + 3) / 4, 256, 0, e->stream>>>(ba, lambda, dpart, spart);
 }
 
 // Schur complement for λ, assembly and reduced-system solve into G.x (enqueued only).

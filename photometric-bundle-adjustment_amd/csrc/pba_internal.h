@@ -816,10 +816,11 @@ struct GnData {
   int dist_rank = -1;           // rank in a host-callback collective (pba_gn_set_rank); −1 unknown
   DevBuf<int4> ib_rec;          // GN block → {block, point, host, target}
   DevBuf<double> ib_data;       // GN block → weighted fp64 rows [J_i (2×8) | J_h (2×6) | J_t (2×6) | J_ρ (2) | r (2) | W_i (8)]
+  DevBuf<double> ib_pw;         // GN point → W_c (8 per camera), W_h (6): intr_pw_kernel
   DevBuf<int> ib_bptr, ib_blist;  // border unit pair (camera c, unit u) → GN blocks of its direct terms (CSR)
   DevBuf<int> ib_pptr, ib_plist;  // … → GN points of its Schur terms (CSR); unit u < nf: frame u, else camera u − nf
   DevBuf<int> ib_cam;           // GN block → its target's camera
-  DevBuf<double2> ib_part;      // intr_border_cam_kernel's per-workgroup totals (dir, Schur) per camera element
+  DevBuf<double> ib_part;       // the camera-block reductions' per-workgroup totals (intr_cam_dir / intr_cam_sch_kernel)
   DevBuf<double> intr_new_d;    // candidate intrinsics: camera records (kCamD doubles, projection part) …
   DevBuf<float> intr_new_f;     // … and their fp32 copy (8 per camera)
   double* lm_host_d = nullptr;  // lm_h's device address

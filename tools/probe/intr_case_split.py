@@ -1,3 +1,10 @@
+#!/usr/bin/env python3
+"""Per-case kernel breakdown of tools/probe/intr_probe.py's rocprofv3 kernel trace: the trace is split at every 12th
+intr_rows_kernel launch (each case runs 2 + 10 LM iterations) into C3 one camera, C3 two cameras and C4 one camera, and
+each kernel's time per LM iteration is printed.
+
+    python3 tools/probe/intr_case_split.py gpurun_out/<dir>/run_kernel_trace.csv
+"""
 import csv, collections, sys
 rows=list(csv.DictReader(open(sys.argv[1])))
 rows.sort(key=lambda r:int(r['Start_Timestamp']))
