@@ -2876,7 +2876,7 @@ struct ArrowArgs {
   const uint8_t* fixed;  // constant keyframes (their border coupling is dropped: identity rows of S)
   CrLevel L0;            // level 0 of the band (D, U, b of kArrowNB columns)
   double* X;             // 6·nf rows × ldx: A⁻¹[−g_a | B]
-  double* part;          // n_ent products (arrow_reduce_kernel)
+  double* part;          // kArrowSeg × n_ent partial products (arrow_reduce_kernel)
   double* dc;            // the border step (12nc)
   double* x;             // the step, 6 per system frame
   int* status;
@@ -2925,12 +2925,15 @@ __global__ __launch_bounds__(256) void arrow_build_kernel(const ArrowArgs a, int
   a.L0.b[t] = v;
 }
 
-// One workgroup per product: entry e < nb(nb+1)/2 — (q1 ≥ q2) of BᵀX_B — then e − that: q1 of BᵀX_0 (nb = 12nc), a dot
-// product over the T = 6nf keyframe rows (thread k takes rows k, k + 256, …; xor butterflies per wave, the four waves
-// in order: a fixed order).
+// kArrowSeg workgroups per product: entry e < nb(nb+1)/2 — (q1 ≥ q2) of BᵀX_B — then e − that: q1 of BᵀX_0 (nb = 12nc), a
+// dot product over the T = 6nf keyframe rows; workgroup (e, g) takes segment g of the rows (thread k: rows k, k + 256, …
+// of it; xor butterflies per wave, the four waves in order) → part[g·n_ent + e]; arrow_cap_kernel adds the kArrowSeg
+// segments in order (a fixed order).
+constexpr int kArrowSeg = 8;
 __global__ __launch_bounds__(256) void arrow_reduce_kernel(const ArrowArgs a) {
   __shared__ double s_w[4];
-  const int nb = 12 * a.nc, nsym = nb * (nb + 1) / 2, T = 6 * a.nf, e = blockIdx.x;
+  const int nb = 12 * a.nc, nsym = nb * (nb + 1) / 2, T = 6 * a.nf, e = blockIdx.x, g = blockIdx.y;
+  const int t0 = (int)((long long)g * T / kArrowSeg), t1 = (int)((long long)(g + 1) * T / kArrowSeg);
   int q1, xc;
   if (e < nsym) {
     q1 = (int)((sqrt(8.0 * e + 1.0) - 1.0) * 0.5);
@@ -2944,11 +2947,12 @@ __global__ __launch_bounds__(256) void arrow_reduce_kernel(const ArrowArgs a) {
   const int p = a.nf + q1 / 6, c = q1 % 6;
   const double* Sp = a.S + (long long)a.row[p] * 36 + c * 6;  // border row p starts at frame 0
   double acc = 0.0;
-  for (int tt = threadIdx.x; tt < T; tt += 256) acc += Sp[(long long)(tt / 6) * 36 + tt % 6] * a.X[(long long)tt * a.ldx + xc];
+  for (int tt = t0 + (int)threadIdx.x; tt < t1; tt += 256)
+    acc += Sp[(long long)(tt / 6) * 36 + tt % 6] * a.X[(long long)tt * a.ldx + xc];
   for (int m = 32; m >= 1; m >>= 1) acc += __shfl_xor(acc, m, 64);
   if ((threadIdx.x & 63) == 0) s_w[threadIdx.x >> 6] = acc;
   __syncthreads();
-  if (threadIdx.x == 0) a.part[e] = ((s_w[0] + s_w[1]) + s_w[2]) + s_w[3];
+  if (threadIdx.x == 0) a.part[(long long)g * a.n_ent + e] = ((s_w[0] + s_w[1]) + s_w[2]) + s_w[3];
 }
 
 // The border system Sc = C − BᵀX_B, rc = −g_c − BᵀX_0, its Cholesky in LDS and δc = Sc⁻¹ rc (the border's part of the
@@ -2961,7 +2965,8 @@ __global__ __launch_bounds__(256) void arrow_cap_kernel(const ArrowArgs a) {
   const int nb = 12 * a.nc, nsym = nb * (nb + 1) / 2, tid = threadIdx.x;
   if (tid == 0) bad = 0;
   for (int e = tid; e < a.n_ent; e += blockDim.x) {
-    const double acc = a.part[e];
+    double acc = a.part[e];
+    for (int g = 1; g < kArrowSeg; ++g) acc += a.part[(long long)g * a.n_ent + e];
     if (e < nsym) {
       int q1 = (int)((sqrt(8.0 * e + 1.0) - 1.0) * 0.5);
       while (q1 * (q1 + 1) / 2 > e) --q1;
@@ -2975,35 +2980,34 @@ __global__ __launch_bounds__(256) void arrow_cap_kernel(const ArrowArgs a) {
       rc[q1] = -a.g[6 * (a.nf + q1 / 6) + q1 % 6] - acc;
     }
   }
+  __shared__ double rdg[NBM];  // 1 / √ of the pivots
   __syncthreads();
-  // right-looking Cholesky (lower), column by column
+  // right-looking LDLᵀ-style elimination with one barrier per column: column k stays unscaled (A_ik after the earlier
+  // columns' updates), the trailing update is A_ij −= A_ik A_jk / A_kk, and L_ik = A_ik / √A_kk is applied in the solves
   for (int k = 0; k < nb; ++k) {
+    const double dkk = sc[k][k];
     if (tid == 0) {
-      const double d = sc[k][k];
-      if (!(d > 0.0)) bad = 1;
-      sc[k][k] = sqrt(fmax(d, 1e-300));
+      if (!(dkk > 0.0)) bad = 1;
+      rdg[k] = 1.0 / sqrt(fmax(dkk, 1e-300));
     }
-    __syncthreads();
-    const double lkk = sc[k][k];
-    for (int i = k + 1 + tid; i < nb; i += blockDim.x) sc[i][k] /= lkk;
-    __syncthreads();
+    const double idk = 1.0 / fmax(dkk, 1e-300);
     const int m = nb - k - 1;
     for (int idx = tid; idx < m * m; idx += blockDim.x) {
       const int i = k + 1 + idx / m, j = k + 1 + idx % m;
-      if (j <= i) sc[i][j] -= sc[i][k] * sc[j][k];
+      if (j <= i) sc[i][j] -= sc[i][k] * sc[j][k] * idk;
     }
     __syncthreads();
   }
-  if (tid == 0) {  // L y = rc, Lᵀ δ = y
+  if (tid == 0) {  // L y = rc, Lᵀ δ = y  (L_ij = A_ij·rdg_j, 1/L_ii = rdg_i): z_j = rdg_j·y_j in place of y
     for (int i = 0; i < nb; ++i) {
       double v = rc[i];
-      for (int j = 0; j < i; ++j) v -= sc[i][j] * rc[j];
-      rc[i] = v / sc[i][i];
+      for (int j = 0; j < i; ++j) v -= sc[i][j] * rc[j];  // A_ij·rdg_j·y_j = A_ij·z_j
+      rc[i] = v * rdg[i] * rdg[i];                         // z_i = rdg_i·y_i, y_i = v·rdg_i
     }
-    for (int i = nb - 1; i >= 0; --i) {
-      double v = rc[i];
-      for (int j = i + 1; j < nb; ++j) v -= sc[j][i] * rc[j];
-      rc[i] = v / sc[i][i];
+    for (int i = nb - 1; i >= 0; --i) {                    // x_i = rdg_i·(y_i − Σ_j A_ji·rdg_i·x_j) = z_i − rdg_i²·Σ A_ji x_j
+      double v = 0.0;
+      for (int j = i + 1; j < nb; ++j) v += sc[j][i] * rc[j];
+      rc[i] -= rdg[i] * rdg[i] * v;
     }
     if (bad) atomicOr(a.status, 2);
   }
@@ -5203,7 +5207,7 @@ int configure_arrow(pba_engine* e) {
   const size_t lvl = (size_t)G.ar_n * M * M * 2 + (size_t)G.ar_n * M * NB;
   PBA_HIP(G.ar_buf.resize(3 * lvl));
   PBA_HIP(G.ar_X.resize((size_t)6 * nf * NB * G.ar_batches));
-  PBA_HIP(G.ar_part.resize((size_t)(nb * (nb + 1) / 2 + nb)));
+  PBA_HIP(G.ar_part.resize((size_t)kArrowSeg * (nb * (nb + 1) / 2 + nb)));
   PBA_HIP(G.ar_dc.resize((size_t)nb));
   return PBA_OK;
 }
@@ -5249,7 +5253,7 @@ int arrow_solve(pba_engine* e, const double* S, const int* first, const int* row
       src = dst;
     }
   }
-  arrow_reduce_kernel<<<aa.n_ent, 256, 0, st>>>(aa);
+  arrow_reduce_kernel<<<dim3(aa.n_ent, kArrowSeg), 256, 0, st>>>(aa);
   arrow_cap_kernel<<<1, 256, 0, st>>>(aa);
   arrow_back_kernel<<<(6 * nf + 255) / 256, 256, 0, st>>>(aa);
   PBA_HIP(hipGetLastError());
