@@ -2721,11 +2721,25 @@ __device__ __forceinline__ void cr_wave_level(const CrLevel& L, const CrLevel& L
 // rows it has just written (read back with L1-bypassing loads after every wave's stores completed) — pcr_solve_kernel's
 // work without its launch boundary and its reload of the level (out / lim as pcr_solve_kernel).
 // NB > 1: out row t = i·M + r holds the NB solution columns at out[t·ld + q].
+// Several independent right-hand-side batches in one launch (the arrow solve, gridDim.y = batches): batch y reads L's
+// D, U at + y·bs_du and b at + y·bs_b, writes Ln at + y·bs_n and its solution columns at out + y·NB (its own CR run
+// over its own copies of the rows: the batches share only L when that is level 0).
 template <int M, bool PCR, int NB = 1>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void cr_level_wave_kernel(
-    CrLevel L, CrLevel Ln, int s, int* status, double* __restrict__ out, int lim, int ld = 1) {
+    CrLevel L, CrLevel Ln, int s, int* status, double* __restrict__ out, int lim, int ld = 1, long long bs_du = 0,
+    long long bs_b = 0, long long bs_n = 0) {
   __shared__ __attribute__((aligned(16))) double piv[3][kPivBuf<M>];
   extern __shared__ double smem[];
+  if (blockIdx.y) {
+    const long long y = blockIdx.y;
+    L.D += y * bs_du;
+    L.U += y * bs_du;
+    L.b += y * bs_b;
+    Ln.D += y * bs_n;
+    Ln.U += y * bs_n;
+    Ln.b += y * bs_n;
+    if (out) out += y * NB;
+  }
   const int i = PCR ? (int)blockIdx.x : 2 * (int)blockIdx.x;
   cr_wave_level<M, PCR, NB>(L, Ln, i, blockIdx.x, PCR ? s : 1, status, piv, smem);
   if (!PCR || !out) return;
@@ -2885,18 +2899,18 @@ struct ArrowArgs {
 
 // Level 0 of the band (super-rows of 4 keyframes, identity padding past the last keyframe) and the batch's kArrowNB
 // right-hand-side columns: global column 0 = −g_a, 1 + q = column q of B (border frame nf + q/6, component q % 6),
-// B[6f + r][q] = S(border row, keyframe f)[q % 6][r].  du: also D and U (the first batch; later batches reuse them).
-__global__ __launch_bounds__(256) void arrow_build_kernel(const ArrowArgs a, int batch, int du) {
+// B[6f + r][q] = S(border row, keyframe f)[q % 6][r].  Every batch's columns in one launch: batch bt's b at
+// L0.b + bt·n·M·kArrowNB (the batches share level 0's D and U).
+__global__ __launch_bounds__(256) void arrow_build_kernel(const ArrowArgs a, int batches) {
   constexpr int M = 24, B = 4, NB = kArrowNB;
   const long long tid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   const int n = a.L0.n;
-  if (tid == 0 && batch == 0) *a.status = 0;
+  if (tid == 0) *a.status = 0;
   auto blk = [&](int i, int j, int r, int c) -> double {  // S[6i + r][6j + c], i ≥ j, 0 outside the profile
     return j >= a.first[i] ? a.S[((long long)a.row[i] + (j - a.first[i])) * 36 + r * 6 + c] : 0.0;
   };
   const long long nDU = (long long)n * M * M;
   if (tid < 2 * nDU) {
-    if (!du) return;
     const bool isU = tid >= nDU;
     const long long e0 = isU ? tid - nDU : tid;
     const int I = (int)(e0 / (M * M)), e = (int)(e0 % (M * M)), R = e / M, C = e % M;
@@ -2914,8 +2928,9 @@ __global__ __launch_bounds__(256) void arrow_build_kernel(const ArrowArgs a, int
     return;
   }
   const long long t = tid - 2 * nDU;
-  if (t >= (long long)n * M * NB) return;
-  const int q = (int)(t % NB), R = (int)((t / NB) % M), I = (int)(t / ((long long)NB * M));
+  if (t >= (long long)batches * n * M * NB) return;
+  const int q = (int)(t % NB), R = (int)((t / NB) % M), I = (int)((t / ((long long)NB * M)) % n);
+  const int batch = (int)(t / ((long long)n * M * NB));
   const int i = I * B + R / 6, r = R % 6, gq = NB * batch + q;
   double v = 0.0;
   if (i < a.nf && !a.fixed[i]) {
@@ -2955,8 +2970,8 @@ __global__ __launch_bounds__(256) void arrow_reduce_kernel(const ArrowArgs a) {
   if (threadIdx.x == 0) a.part[(long long)g * a.n_ent + e] = ((s_w[0] + s_w[1]) + s_w[2]) + s_w[3];
 }
 
-// The border system Sc = C − BᵀX_B, rc = −g_c − BᵀX_0, its Cholesky in LDS and δc = Sc⁻¹ rc (the border's part of the
-// step); one workgroup.  (A one-wave form without workgroup barriers measured no faster: 15.4 → 17.0 µs at C4.)
+// The border system Sc = C − BᵀX_B, rc = −g_c − BᵀX_0, its elimination in LDS and δc = Sc⁻¹ rc (the border's part of
+// the step); one workgroup.  (A one-wave form without workgroup barriers measured no faster: 15.4 → 17.0 µs at C4.)
 __global__ __launch_bounds__(256) void arrow_cap_kernel(const ArrowArgs a) {
   constexpr int NBM = 12 * kArrowMaxNc;
   __shared__ double sc[NBM][NBM + 1];
@@ -2980,41 +2995,31 @@ __global__ __launch_bounds__(256) void arrow_cap_kernel(const ArrowArgs a) {
       rc[q1] = -a.g[6 * (a.nf + q1 / 6) + q1 % 6] - acc;
     }
   }
-  __shared__ double rdg[NBM];  // 1 / √ of the pivots
   __syncthreads();
-  // right-looking LDLᵀ-style elimination with one barrier per column: column k stays unscaled (A_ik after the earlier
-  // columns' updates), the trailing update is A_ij −= A_ik A_jk / A_kk, and L_ik = A_ik / √A_kk is applied in the solves
+  // Gauss-Jordan on [Sc | rc] with one barrier per column (no serial triangular solves: a one-lane substitution paid an
+  // LDS round trip per term, ~nb² of them — 30 µs at nb = 24): step k takes every row i ≠ k's columns j > k and rc,
+  // a_ij −= a_ik·a_kj / a_kk; column k and row k are only read in step k, so the step needs no second barrier.  The
+  // pivots are Gaussian elimination's (Sc is SPD: all positive), δc_i = rc_i / a_ii at the end.
   for (int k = 0; k < nb; ++k) {
     const double dkk = sc[k][k];
-    if (tid == 0) {
-      if (!(dkk > 0.0)) bad = 1;
-      rdg[k] = 1.0 / sqrt(fmax(dkk, 1e-300));
-    }
+    if (tid == 0 && !(dkk > 0.0)) bad = 1;
     const double idk = 1.0 / fmax(dkk, 1e-300);
-    const int m = nb - k - 1;
-    for (int idx = tid; idx < m * m; idx += blockDim.x) {
-      const int i = k + 1 + idx / m, j = k + 1 + idx % m;
-      if (j <= i) sc[i][j] -= sc[i][k] * sc[j][k] * idk;
+    const int m = nb - k;  // columns k + 1 … nb − 1, then rc
+    for (int idx = tid; idx < nb * m; idx += blockDim.x) {
+      const int i = idx / m, jj = idx - m * i;
+      if (i == k) continue;
+      const double f = sc[i][k] * idk;
+      if (jj < m - 1) sc[i][k + 1 + jj] -= f * sc[k][k + 1 + jj];
+      else rc[i] -= f * rc[k];
     }
     __syncthreads();
   }
-  if (tid == 0) {  // L y = rc, Lᵀ δ = y  (L_ij = A_ij·rdg_j, 1/L_ii = rdg_i): z_j = rdg_j·y_j in place of y
-    for (int i = 0; i < nb; ++i) {
-      double v = rc[i];
-      for (int j = 0; j < i; ++j) v -= sc[i][j] * rc[j];  // A_ij·rdg_j·y_j = A_ij·z_j
-      rc[i] = v * rdg[i] * rdg[i];                         // z_i = rdg_i·y_i, y_i = v·rdg_i
-    }
-    for (int i = nb - 1; i >= 0; --i) {                    // x_i = rdg_i·(y_i − Σ_j A_ji·rdg_i·x_j) = z_i − rdg_i²·Σ A_ji x_j
-      double v = 0.0;
-      for (int j = i + 1; j < nb; ++j) v += sc[j][i] * rc[j];
-      rc[i] -= rdg[i] * rdg[i] * v;
-    }
-    if (bad) atomicOr(a.status, 2);
-  }
+  if (tid == 0 && bad) atomicOr(a.status, 2);
   __syncthreads();
   for (int q = tid; q < nb; q += blockDim.x) {
-    a.dc[q] = rc[q];
-    a.x[6 * a.nf + q] = rc[q];
+    const double v = rc[q] / fmax(sc[q][q], 1e-300);
+    a.dc[q] = v;
+    a.x[6 * a.nf + q] = v;
   }
 }
 
@@ -5204,8 +5209,9 @@ int configure_arrow(pba_engine* e) {
   const int nf = e->n_frames, nc = G.nc_sys, nb = 12 * nc;
   G.ar_n = (nf + 3) / 4;
   G.ar_batches = (1 + nb + NB - 1) / NB;
+  // level 0: D, U (shared by the batches) and every batch's b; levels 1, 2 (ping-pong): per batch D, U, b
   const size_t lvl = (size_t)G.ar_n * M * M * 2 + (size_t)G.ar_n * M * NB;
-  PBA_HIP(G.ar_buf.resize(3 * lvl));
+  PBA_HIP(G.ar_buf.resize((size_t)G.ar_n * M * M * 2 + (size_t)G.ar_batches * (2 * lvl + (size_t)G.ar_n * M * NB)));
   PBA_HIP(G.ar_X.resize((size_t)6 * nf * NB * G.ar_batches));
   PBA_HIP(G.ar_part.resize((size_t)kArrowSeg * (nb * (nb + 1) / 2 + nb)));
   PBA_HIP(G.ar_dc.resize((size_t)nb));
@@ -5229,29 +5235,35 @@ int arrow_solve(pba_engine* e, const double* S, const int* first, const int* row
   constexpr int M = 24, NB = kArrowNB;
   const int nf = e->n_frames, nc = G.nc_sys, n = G.ar_n, nb = 12 * nc;
   hipStream_t st = e->stream;
-  const size_t lvl = (size_t)n * M * M * 2 + (size_t)n * M * NB;
-  auto level = [&](int k) {
-    double* p = G.ar_buf.p + k * lvl;
+  const int nbt = G.ar_batches;
+  const size_t lvl = (size_t)n * M * M * 2 + (size_t)n * M * NB, nbq = (size_t)n * M * NB;
+  auto level = [&](int k) {  // batch 0's rows of level k (configure_arrow's layout)
+    double* p = G.ar_buf.p + (k == 0 ? 0 : (size_t)n * M * M * 2 + nbt * nbq + (size_t)(k - 1) * nbt * lvl);
     return CrLevel{p, p + (size_t)n * M * M, p + (size_t)2 * n * M * M, nullptr, nullptr, n};
   };
   ArrowArgs aa{S, first, row, G.g.p, fixed, level(0), G.ar_X.p, G.ar_part.p, G.ar_dc.p, G.x.p, G.status.p,
                nf, nc, NB * G.ar_batches, nb * (nb + 1) / 2 + nb};
   constexpr size_t lds = cr_level_wave_lds<M, NB>();
   static_assert(lds <= 65536, "default dynamic LDS limit");
-  const long long nth = 2LL * n * M * M + (long long)n * M * NB;
-  for (int bt = 0; bt < G.ar_batches; ++bt) {
-    arrow_build_kernel<<<(unsigned)((nth + 255) / 256), 256, 0, st>>>(aa, bt, bt == 0);
-    double* out = G.ar_X.p + NB * bt;
-    CrLevel src = level(0);
-    if (n <= 1) pcr_solve_kernel<M, NB><<<n, 64, 0, st>>>(src, out, 6 * nf, G.status.p, aa.ldx);
-    int pi = 1;
-    for (int s = 1; s < n; s *= 2, pi = 3 - pi) {  // the last level also solves the decoupled rows
-      const CrLevel dst = level(pi);
-      const bool last = 2 * s >= n;
-      cr_level_wave_kernel<M, true, NB><<<n, 256, lds, st>>>(src, dst, s, G.status.p, last ? out : nullptr, 6 * nf,
-                                                              aa.ldx);
-      src = dst;
+  const long long nth = 2LL * n * M * M + (long long)nbt * n * M * NB;
+  arrow_build_kernel<<<(unsigned)((nth + 255) / 256), 256, 0, st>>>(aa, nbt);
+  // the batches' cyclic reductions side by side (gridDim.y): one launch per level whatever the number of cameras
+  CrLevel src = level(0);
+  if (n <= 1)
+    for (int bt = 0; bt < nbt; ++bt) {
+      CrLevel sb = src;
+      sb.b += bt * nbq;
+      pcr_solve_kernel<M, NB><<<n, 64, 0, st>>>(sb, G.ar_X.p + NB * bt, 6 * nf, G.status.p, aa.ldx);
     }
+  int pi = 1;
+  long long bs_du = 0, bs_b = (long long)nbq;  // level 0: shared D, U
+  for (int s = 1; s < n; s *= 2, pi = 3 - pi) {  // the last level also solves the decoupled rows
+    const CrLevel dst = level(pi);
+    const bool last = 2 * s >= n;
+    cr_level_wave_kernel<M, true, NB><<<dim3(n, nbt), 256, lds, st>>>(src, dst, s, G.status.p, last ? G.ar_X.p : nullptr,
+                                                                      6 * nf, aa.ldx, bs_du, bs_b, (long long)lvl);
+    src = dst;
+    bs_du = bs_b = (long long)lvl;
   }
   arrow_reduce_kernel<<<dim3(aa.n_ent, kArrowSeg), 256, 0, st>>>(aa);
   arrow_cap_kernel<<<1, 256, 0, st>>>(aa);

@@ -785,8 +785,9 @@ struct GnData {
   int dsky_K = -1, n_dsky = 0;
   // free intrinsics as an ARROW system (pba_gn.hip arrow_solve): the keyframe band by parallel cyclic reduction with
   // the border's columns as extra right-hand sides, then the small dense border Schur complement.  ar_n super-rows of 4
-  // keyframes, ar_batches runs of kArrowNB columns; buffers: level 0 + two ping-pong levels (D, U, b of kArrowNB
-  // columns), the solutions X (6·nf rows × 16·ar_batches), the border reduction's partials, the border step.
+  // keyframes, ar_batches runs of kArrowNB columns side by side; buffers: level 0 (D, U and every batch's b) + two
+  // ping-pong levels (per batch D, U, b of kArrowNB columns), the solutions X (6·nf rows × 16·ar_batches), the border
+  // reduction's partials, the border step.
   bool arrow = false;           // the local (single-GPU) free-intrinsics system is solved as an arrow
   int ar_n = 0, ar_batches = 0;
   DevBuf<double> ar_buf, ar_X, ar_part, ar_dc;
