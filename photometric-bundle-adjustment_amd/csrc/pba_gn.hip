@@ -3637,12 +3637,39 @@ __device__ __forceinline__ void border_store(const IntrBorderArgs& a, double lam
   a.S[((long long)a.sky_row[P] + (y - a.sky_first[P])) * 36 + e] = val;
 }
 
+// Σ over the wave of 48 per-lane values v[0 … 47] by recursive halving (a reduce-scatter: 24 + 12 + 6 + 3 + 6 shuffles
+// instead of 48 six-step butterflies): after the xor-32 / 16 / 8 / 4 steps lane l holds partial sums of the three values
+// base(l) … base(l) + 2, base = 24·b5 + 12·b4 + 6·b3 + 3·b2 of l's bits, completed over its quad by xor 2 and xor 1 (a + b
+// and b + a: the quad's lanes agree bit for bit).  Returns the total of value *vi = base(l) + (l & 3) for l & 3 < 3
+// (*vi = −1 and 0 otherwise).  A fixed order.
+__device__ __forceinline__ double wave_rs48(const double (&v)[48], int lane, int* vi) {
+  double a24[24], a12[12], a6[6], a3[3];
+  const bool h5 = lane & 32, h4 = lane & 16, h3 = lane & 8, h2 = lane & 4;
+#pragma unroll
+  for (int i = 0; i < 24; ++i) a24[i] = (h5 ? v[24 + i] : v[i]) + __shfl_xor(h5 ? v[i] : v[24 + i], 32, 64);
+#pragma unroll
+  for (int i = 0; i < 12; ++i) a12[i] = (h4 ? a24[12 + i] : a24[i]) + __shfl_xor(h4 ? a24[i] : a24[12 + i], 16, 64);
+#pragma unroll
+  for (int i = 0; i < 6; ++i) a6[i] = (h3 ? a12[6 + i] : a12[i]) + __shfl_xor(h3 ? a12[i] : a12[6 + i], 8, 64);
+#pragma unroll
+  for (int i = 0; i < 3; ++i) a3[i] = (h2 ? a6[3 + i] : a6[i]) + __shfl_xor(h2 ? a6[i] : a6[3 + i], 4, 64);
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    a3[i] += __shfl_xor(a3[i], 2, 64);
+    a3[i] += __shfl_xor(a3[i], 1, 64);
+  }
+  const int j = lane & 3;
+  *vi = j < 3 ? 24 * h5 + 12 * h4 + 6 * h3 + 3 * h2 + j : -1;
+  return j == 0 ? a3[0] : j == 1 ? a3[1] : j == 2 ? a3[2] : 0.0;
+}
+
 // The keyframe blocks (P, y < nf) of both border rows of a camera: kpw WAVES per keyframe y (grid x: 4/kpw keyframes per
 // workgroup; y: camera c) form the 8 × 6 live entries of (2c, y) and (2c + 1, y) — row 2c + 1's frame holds intrinsics 6,
 // 7 and four pads — at once: a lane takes every (64·kpw)th entry of the keyframe's lists (its blocks and points seen by
-// the camera), each wave adds its lanes' sums by xor butterflies and the kpw waves' sums are added in order (a fixed
-// order).  kpw = 4 while the keyframe waves would not fill the SIMDs (C3, 200 keyframes), else 1 (C4: 1004 waves).  Round 5
-// walked the lists twice (one kernel per border row: 133 + 117 µs at C4) and each point's blocks once per (point, list).
+// the camera), each wave adds its lanes' sums (wave_rs48) and the kpw waves' sums are added in order (a fixed order).
+// kpw = 4 while the keyframe waves would not fill the SIMDs (C3, 200 keyframes), else 2 (C4: 2008 waves; 1 and 4 measured
+// 80.5 and 82.4 against 76.5 µs).  Round 5 walked the lists twice (one kernel per border row: 133 + 117 µs at C4) and
+// each point's blocks once per (point, list).
 __global__ __launch_bounds__(256) void intr_border_kernel(const IntrBorderArgs a, double lambda, int kpw) {
   __shared__ double2 s_w[4][48];
   lambda = lm_lambda(lm_view(a.lm), lambda);
@@ -3651,10 +3678,9 @@ __global__ __launch_bounds__(256) void intr_border_kernel(const IntrBorderArgs a
   const int y = min(y0, a.nf - 1);  // (a wave past the last keyframe walks nothing and stores nothing)
   const int L = c * (a.nf + a.nc) + y;
   const int q0 = sub * 64 + lane, dq = y0 < a.nf ? 64 * kpw : 1 << 30;
-  // the 8 intrinsics rows d of camera c (border rows 2c: d = 0…5, 2c + 1: d = 6, 7) × the keyframe's 6 columns; the
-  // direct terms first, then the Schur terms in the same registers; lane v < 48 ends with value v = 6d + cc of each
+  // the 8 intrinsics rows d of camera c (border rows 2c: d = 0…5, 2c + 1: d = 6, 7) × the keyframe's 6 columns, value
+  // v = 6d + cc; the direct terms first, then the Schur terms in the same registers; lane l ends with value vi (wave_rs48)
   double acc[8][6];
-  double vd = 0.0, vs = 0.0;
 #pragma unroll
   for (int d = 0; d < 8; ++d)
 #pragma unroll
@@ -3676,14 +3702,12 @@ __global__ __launch_bounds__(256) void intr_border_kernel(const IntrBorderArgs a
       for (int cc = 0; cc < 6; ++cc) acc[d][cc] += j0 * c0[cc] + j1 * c1[cc];
     }
   }
+  int vi;
+  double vd = wave_rs48(reinterpret_cast<const double(&)[48]>(acc), lane, &vi);
 #pragma unroll
   for (int d = 0; d < 8; ++d)
 #pragma unroll
-    for (int cc = 0; cc < 6; ++cc) {
-      const double t = wave_sum(acc[d][cc]);
-      vd = lane == d * 6 + cc ? t : vd;
-      acc[d][cc] = 0.0;
-    }
+    for (int cc = 0; cc < 6; ++cc) acc[d][cc] = 0.0;
   for (int q = a.pptr[L] + (y0 < a.nf ? q0 : 1 << 30); q < a.pptr[L + 1]; q += dq) {
     const int gp = a.plist[q];
     const int4 pr = a.pt_rec[gp];
@@ -3711,32 +3735,26 @@ __global__ __launch_bounds__(256) void intr_border_kernel(const IntrBorderArgs a
 #pragma unroll
       for (int cc = 0; cc < 6; ++cc) acc[d][cc] += inv * wc[d] * wy[cc];
   }
-#pragma unroll
-  for (int d = 0; d < 8; ++d)
-#pragma unroll
-    for (int cc = 0; cc < 6; ++cc) {
-      const double t = wave_sum(acc[d][cc]);
-      vs = lane == d * 6 + cc ? t : vs;
-    }
+  double vs = wave_rs48(reinterpret_cast<const double(&)[48]>(acc), lane, &vi);
   if (kpw > 1) {  // the keyframe's kpw waves, in order
-    if (lane < 48) s_w[w][lane] = make_double2(vd, vs);
+    if (vi >= 0) s_w[w][vi] = make_double2(vd, vs);
     __syncthreads();
-    if (sub == 0 && lane < 48) {
-      double2 t = s_w[w][lane];
+    if (sub == 0 && vi >= 0) {
+      double2 t = s_w[w][vi];
       for (int k = 1; k < kpw; ++k) {
-        t.x += s_w[w + k][lane].x;
-        t.y += s_w[w + k][lane].y;
+        t.x += s_w[w + k][vi].x;
+        t.y += s_w[w + k][vi].y;
       }
       vd = t.x;
       vs = t.y;
     }
     if (sub != 0) return;  // (whole waves)
   }
-  // row 2c + 1's live entries (d = 6, 7: values 36 … 47) to lanes 0 … 11; its other entries are pads (border_store)
-  const double xd = __shfl(vd, 36 + (lane % 12), 64), xs = __shfl(vs, 36 + (lane % 12), 64);
-  if (lane < 36 && y0 < a.nf) {
-    border_store(a, lambda, 2 * c, y * 36 + lane, vd, vs);
-    border_store(a, lambda, 2 * c + 1, y * 36 + lane, lane < 12 ? xd : 0.0, lane < 12 ? xs : 0.0);
+  // row 2c: values 0 … 35 (element v); row 2c + 1: values 36 … 47 (d = 6, 7) as its elements 0 … 11, its elements
+  // 12 … 35 pads (border_store) from lanes 12 … 35
+  if (y0 < a.nf) {
+    if (vi >= 0) border_store(a, lambda, vi < 36 ? 2 * c : 2 * c + 1, y * 36 + (vi < 36 ? vi : vi - 36), vd, vs);
+    if (lane >= 12 && lane < 36) border_store(a, lambda, 2 * c + 1, y * 36 + lane, 0.0, 0.0);
   }
 }
 
@@ -3757,21 +3775,49 @@ constexpr int kCamDir = 44, kCamSch = 72;  // accumulators per thread
 
 __device__ __forceinline__ int upper8i(int i, int j) { return i * 8 - i * (i - 1) / 2 + (j - i); }  // i ≤ j < 8
 
-// Σ over the workgroup of NV per-thread accumulators in a fixed order → out[0 … NV).  Every thread calls it.
+// Σ over the wave of N per-lane values (N a multiple of 16) into dst[0 … N) by recursive halving, as wave_rs48: after the
+// xor-32 / 16 / 8 / 4 steps lane l holds partial sums of values base(l) … base(l) + N/16 − 1 (base = N/2·b5 + N/4·b4 +
+// N/8·b3 + N/16·b2), completed over its quad by xor 2 and xor 1; the quad's lanes store them.  A fixed order.
+template <int N>
+__device__ __forceinline__ void wave_rs_lds(const double (&v)[N], int lane, double* dst) {
+  static_assert(N % 16 == 0, "four halvings");
+  constexpr int H1 = N / 2, H2 = N / 4, H3 = N / 8, H4 = N / 16;
+  double a1[H1], a2[H2], a3[H3], a4[H4];
+  const bool h5 = lane & 32, h4 = lane & 16, h3 = lane & 8, h2 = lane & 4;
+#pragma unroll
+  for (int i = 0; i < H1; ++i) a1[i] = (h5 ? v[H1 + i] : v[i]) + __shfl_xor(h5 ? v[i] : v[H1 + i], 32, 64);
+#pragma unroll
+  for (int i = 0; i < H2; ++i) a2[i] = (h4 ? a1[H2 + i] : a1[i]) + __shfl_xor(h4 ? a1[i] : a1[H2 + i], 16, 64);
+#pragma unroll
+  for (int i = 0; i < H3; ++i) a3[i] = (h3 ? a2[H3 + i] : a2[i]) + __shfl_xor(h3 ? a2[i] : a2[H3 + i], 8, 64);
+#pragma unroll
+  for (int i = 0; i < H4; ++i) a4[i] = (h2 ? a3[H4 + i] : a3[i]) + __shfl_xor(h2 ? a3[i] : a3[H4 + i], 4, 64);
+  const int base = H1 * h5 + H2 * h4 + H3 * h3 + H4 * h2;
+#pragma unroll
+  for (int i = 0; i < H4; ++i) {
+    a4[i] += __shfl_xor(a4[i], 2, 64);
+    a4[i] += __shfl_xor(a4[i], 1, 64);
+    if ((i & 3) == (lane & 3)) dst[base + i] = a4[i];
+  }
+}
+constexpr int pad16(int n) { return (n + 15) / 16 * 16; }
+
+// Σ over the workgroup of NV per-thread accumulators in a fixed order → out[0 … NV): each wave's sums by wave_rs_lds
+// into s_w (4·pad16(NV) doubles), then the four waves in order.  Every thread calls it.
 template <int NV>
 __device__ __forceinline__ void wg_sum_store(const double* acc, double* s_w, double* out) {
+  constexpr int NP = pad16(NV);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  double v[NP];
 #pragma unroll
-  for (int v = 0; v < NV; ++v) {
-    const double t = wave_sum(acc[v]);
-    if (lane == 0) s_w[w * NV + v] = t;
-  }
+  for (int i = 0; i < NP; ++i) v[i] = i < NV ? acc[i] : 0.0;
+  wave_rs_lds<NP>(v, lane, s_w + w * NP);
   __syncthreads();
-  for (int v = threadIdx.x; v < NV; v += blockDim.x) out[v] = ((s_w[v] + s_w[NV + v]) + s_w[2 * NV + v]) + s_w[3 * NV + v];
+  for (int i = threadIdx.x; i < NV; i += blockDim.x) out[i] = ((s_w[i] + s_w[NP + i]) + s_w[2 * NP + i]) + s_w[3 * NP + i];
 }
 
 __global__ __launch_bounds__(256) void intr_cam_dir_kernel(const IntrBorderArgs a, double* part) {
-  __shared__ double s_w[4 * kCamDir];
+  __shared__ double s_w[4 * pad16(kCamDir)];
   const int c = blockIdx.y, L = c * (a.nf + a.nc) + a.nf + c;  // (camera c, unit nf + c): every block of camera c
   double acc[kCamDir];
 #pragma unroll
@@ -3796,7 +3842,7 @@ __global__ __launch_bounds__(256) void intr_cam_dir_kernel(const IntrBorderArgs 
 }
 
 __global__ __launch_bounds__(256) void intr_cam_sch_kernel(const IntrBorderArgs a, double lambda, double* part) {
-  __shared__ double s_w[4 * kCamSch];
+  __shared__ double s_w[4 * pad16(kCamSch)];
   lambda = lm_lambda(lm_view(a.lm), lambda);
   const int pc = blockIdx.y;  // camera pair (c, c2 ≤ c), pc = c(c+1)/2 + c2
   int c = 0;
@@ -5374,7 +5420,10 @@ void enqueue_border(pba_engine* e, double lambda, const double* lm, double* X) {
                     G.g.p, G.g_dir.p, G.Ddiag.p, nf, G.nc_sys, X, (long long)nfs * 36 + EX_TAIL, G.ib_pw.p};
   const int nb = 2 * G.nc_sys + 1;
   intr_pw_kernel<<<(8 * G.n_gn_points + 255) / 256, 256, 0, e->stream>>>(ba, G.n_gn_points);
-  const int kpw = nf * G.nc_sys < 512 ? 4 : 1;  // waves per keyframe block (intr_border_kernel)
+#ifndef PBA_INTR_KPW_BIG
+#define PBA_INTR_KPW_BIG 2
+#endif
+  const int kpw = nf * G.nc_sys < 512 ? 4 : PBA_INTR_KPW_BIG;  // waves per keyframe block (intr_border_kernel)
   intr_border_kernel<<<dim3((nf * kpw + 3) / 4, G.nc_sys), 256, 0, e->stream>>>(ba, lambda, kpw);
   double* dpart = G.ib_part.p;
   double* spart = dpart + (size_t)G.nc_sys * kCamSplit * kCamDir;
