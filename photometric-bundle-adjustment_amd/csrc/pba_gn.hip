@@ -813,6 +813,13 @@ struct SchurArgs {
   const int4* lvp4;        // per chunk: the pairs of local targets 1 … 4
   const int* lvp;          // all of them (from aux.z), for chunks of > 5 local poses
   int rt_off;              // R, t at the start of the dynamic LDS (doubles); W after it
+  // free intrinsics (single-GPU LM loop): the previous trial's accept also copies the candidate intrinsics (the copies of
+  // intr_accept_kernel, 8 per camera) — k_d == nullptr: not here
+  const double* knew_d = nullptr;
+  const float* knew_f = nullptr;
+  double* k_d = nullptr;
+  float* k_f = nullptr;
+  int n_intr = 0;
 };
 
 // ------------------------------------------------------------------------------------------------
@@ -1080,8 +1087,9 @@ __device__ __forceinline__ void schur_chunk(const SchurArgs& g, const SchurHead&
 // loads), stores after the kernel's own stores (loads and stores share vmcnt).
 struct AcceptCopy {
   bool accepted = false;
-  int ia = 0, oa = 0;
-  double pnew = 0.0, rnew = 0.0;
+  int ia = 0, oa = 0, ka = 0;
+  double pnew = 0.0, rnew = 0.0, kdnew = 0.0;
+  float kfnew = 0.0f;
   __device__ __forceinline__ void load(const SchurArgs& g, const LmView& lv) {
     accepted = g.poses && lv.accept != 0.0 && lv.done == 0.0;
     ia = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1090,11 +1098,20 @@ struct AcceptCopy {
       oa = g.pt_orig[min(ia, g.n_gn_points - 1)];
       rnew = g.rho_new[oa];
     }
+    if (g.k_d && ia < 8 * g.n_intr) {
+      ka = kCamD * (ia >> 3) + (ia & 7);
+      kdnew = g.knew_d[ka];
+      kfnew = g.knew_f[ia];
+    }
   }
   __device__ __forceinline__ void store(const SchurArgs& g) const {
     if (!accepted) return;
     if (ia < g.n_pose_d) g.poses[ia] = pnew;
     if (ia < g.n_gn_points) g.rho[oa] = rnew;
+    if (g.k_d && ia < 8 * g.n_intr) {
+      g.k_d[ka] = kdnew;
+      g.k_f[ia] = kfnew;
+    }
     const int n = max(g.n_pose_d, g.n_gn_points);
     for (int i = ia + gridDim.x * blockDim.x; i < n; i += gridDim.x * blockDim.x) {
       if (i < g.n_pose_d) g.poses[i] = g.poses_new[i];
@@ -2874,7 +2891,7 @@ __global__ __launch_bounds__(1024) void cr_back_tail_kernel(const CrLevels C, in
 // 3.64 ms at C4.  Eliminating the keyframes first is the same factorisation order (border last), so instead:
 //   X = A⁻¹ [−g_a | B]          parallel cyclic reduction over the band, the border's 12nc columns as extra right-hand
 //                               sides (cr_level_wave_kernel<24, true, kArrowNB>: [D | U | b] = 24 + 24 + 16 lanes),
-//                               in batches of kArrowNB columns;
+//                               in batches of kArrowNB columns run side by side (gridDim.y);
 //   Sc = C − BᵀX_B,  rc = −g_c − BᵀX_0,  δc = Sc⁻¹ rc     (arrow_reduce_kernel: a workgroup per product;
 //                               arrow_cap_kernel: one workgroup, dense Cholesky of the ≤ 48 × 48 border system);
 //   δa = X_0 − X_B δc           (arrow_back_kernel).
@@ -5394,10 +5411,11 @@ void schur_lds_limit(const GnData& G) {
       (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)G.schur_lds);
 }
 
-// Free intrinsics: the last trial's accept (lm: the LM record, else none), then the weighted fp64 rows at the state.
-void enqueue_intr_rows(pba_engine* e, const double* lm) {
+// Free intrinsics: the last trial's accept (lm: the LM record, else none; accept = false: the point elimination's
+// launch has applied it), then the weighted fp64 rows at the state.
+void enqueue_intr_rows(pba_engine* e, const double* lm, bool accept = true) {
   GnData& G = e->gn;
-  if (lm) intr_accept_kernel<<<1, 256, 0, e->stream>>>(lm, G.intr_new_d.p, G.intr_new_f.p, e->intr_state_d.p,
+  if (lm && accept) intr_accept_kernel<<<1, 256, 0, e->stream>>>(lm, G.intr_new_d.p, G.intr_new_f.p, e->intr_state_d.p,
                                                        e->intr_state.p, G.nc_sys);
   IntrRowsArgs ra{G.ib_rec.p, e->poses.p, e->rho.p, e->u_ref.p, e->u_obs.p, e->frame_cam.p, e->intr_d.p,
                   e->intr_state_d.p, (double)e->opt.huber_width, G.ib_data.p, e->n_blocks, lm ? lm : G.lm_idle.p};
@@ -5443,12 +5461,21 @@ int enqueue_solve(pba_engine* e, double lambda, const double* lm = nullptr, bool
                G.blk_schur.p, G.blk_schur1.p, G.part_schur.p, G.pt_data.p, G.n_schur, lm ? lm : G.lm_idle.p,
                lm ? e->poses.p : nullptr, G.poses_new.p, e->rho.p, G.rho_new.p, G.pt_orig.p, 7 * nf, G.n_gn_points,
                G.pair_rt.p, G.pair_rt1.p, G.schur_lvp4.p, G.schur_lvp.p, G.schur_rt_off};
+  // free intrinsics: the elimination's launch also applies the previous trial's intrinsics accept (no launch of its own)
+  const bool kacc = G.nc_sys && lm && !free_sets && G.n_schur > 0;
+  if (kacc) {
+    sa.knew_d = G.intr_new_d.p;
+    sa.knew_f = G.intr_new_f.p;
+    sa.k_d = e->intr_state_d.p;
+    sa.k_f = e->intr_state.p;
+    sa.n_intr = G.nc_sys;
+  }
   schur_lds_limit(G);
   if (free_sets)
     schur_gate_kernel<<<std::max(1, std::min(G.n_schur, 512)), kBlockThreads, G.schur_lds, e->stream>>>(sa, G.degen.p);
   else
     schur_kernel<<<G.n_schur, kBlockThreads, G.schur_lds, e->stream>>>(sa, lambda);
-  if (G.nc_sys) enqueue_intr_rows(e, lm);
+  if (G.nc_sys) enqueue_intr_rows(e, lm, !kacc);
   // block cyclic reduction: assemble writes its level 0 directly (no Sband, no cr_build pass)
   const bool direct = G.band_kernel && G.solver == SOLVER_CR;
   if (direct && G.cr0_dirty)  // a distributed solve rebuilt level 0 over the whole band: back to zeros + padding
