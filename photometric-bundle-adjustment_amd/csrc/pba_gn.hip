@@ -3485,10 +3485,22 @@ struct PoseT {  // a relative pose for pair_rotation / pair_translation
 
 // One lane per GN block at the current state: r = u_obs − π_t(T_th b/ρ) and its Jacobians (the geometric_row chain, in
 // fp64), J_i = −∂π/∂k (project_intr_jac), Ceres' Corrector weighting √ρ' (corrector.cc, ρ'' ≤ 0 for Huber), W_i = J_iᵀJ_ρ.
+// The rows leave through LDS (PBA_IB_DIRECT: straight from the lanes): a lane's 416-B row stored from registers is 26
+// 16-B stores 416 B apart per instruction — 64 partial lines each — so each wave stages its 64 rows in two halves of 26
+// doubles and stores every half as the 13 16-B chunks of each row, consecutive lanes on consecutive chunks.
+#ifndef PBA_IB_DIRECT
+constexpr int kIbStage = 27;  // doubles per staged half row (26 used; odd: 2-way LDS bank conflicts at most)
+#endif
 template <int MODEL>
 __global__ __launch_bounds__(256) void intr_rows_kernel(const IntrRowsArgs a) {
-  const int gb = blockIdx.x * blockDim.x + threadIdx.x;
-  if (gb >= a.n || lm_view(a.lm).done != 0.0) return;
+  const int gb0 = blockIdx.x * blockDim.x + threadIdx.x;
+#ifdef PBA_IB_DIRECT
+  if (gb0 >= a.n || lm_view(a.lm).done != 0.0) return;
+  const int gb = gb0;
+#else
+  if (lm_view(a.lm).done != 0.0) return;  // (uniform)
+  const int gb = min(gb0, a.n - 1);       // every lane of a wave takes part in its stores
+#endif
   const int4 br = a.rec[gb];
   PoseT T;
   pair_rotation(a.poses + 7 * br.z, a.poses + 7 * br.w, T);
@@ -3536,9 +3548,35 @@ __global__ __launch_bounds__(256) void intr_rows_kernel(const IntrRowsArgs a) {
   for (int q = 0; q < kIbWi; ++q) J[q] = ok ? sw * J[q] : 0.0;
 #pragma unroll
   for (int d = 0; d < 8; ++d) J[kIbWi + d] = J[kIbJi + d] * J[kIbJr] + J[kIbJi + 8 + d] * J[kIbJr + 1];
+#ifdef PBA_IB_DIRECT
   double* o = a.out + (long long)gb * kIbStride;
 #pragma unroll
   for (int q = 0; q < kIbStride; q += 2) *reinterpret_cast<double2*>(o + q) = make_double2(J[q], J[q + 1]);
+#else
+  constexpr int HALF = kIbStride / 2, CH = HALF / 2;  // 26 doubles, 13 chunks of 16 B per half row
+  __shared__ double stage[4][64 * kIbStage];
+  const int lane = threadIdx.x & 63;
+  const int row0 = gb0 - lane, nrow = min(64, a.n - row0);  // the wave's rows in ib_data
+  double* st = stage[threadIdx.x >> 6];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+#pragma unroll
+    for (int q = 0; q < HALF; ++q) st[lane * kIbStage + q] = J[HALF * h + q];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+    for (int c0 = 0; c0 < 64 * CH; c0 += 64) {
+      const int c = c0 + lane, r = c / CH, j = c - CH * r;
+      if (r < nrow)
+        *reinterpret_cast<double2*>(a.out + (long long)(row0 + r) * kIbStride + HALF * h + 2 * j) =
+            make_double2(st[r * kIbStage + 2 * j], st[r * kIbStage + 2 * j + 1]);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // this half's reads before the next half's writes
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+#endif
 }
 
 struct IntrBorderArgs {
