@@ -3586,7 +3586,7 @@ struct IntrBorderArgs {
   const int4* pt_rec;      // GN point → {first GN block, block count, host, point}
   const double* pt_data;   // GN point → [H_ρρ (undamped), g_ρ, …] (schur_kernel of this solve)
   const int* bptr;         // border unit pair (c, u) = c·(nf + nc) + u → direct-term GN blocks …
-  const int* blist;
+  const int* blist;        // (keyframe units: bit 31 set when the keyframe hosts the block)
   const int* pptr;         // … and Schur-term GN points
   const int* plist;
   const int* sky_first;
@@ -3601,6 +3601,8 @@ struct IntrBorderArgs {
   double* X = nullptr;     // multi-GPU export (pba_gn_step_export): this rank's border rows, undamped, into the exchange
   long long xs = 0;        // buffer's border region (row stride nfs·36 + EX_TAIL) instead of S
   const double* pw = nullptr;  // GN point → its camera sums W_c (8 per camera) and W_h = Σ J_hᵀJ_ρ (6): intr_pw_kernel
+  const int* pblk = nullptr;   // per plist entry of a keyframe unit: −1 the keyframe hosts the point, else the point's
+                               // one block targeting it (−2: several — walk the point's blocks)
 };
 
 // Per GN point, over its blocks in order: W_c = Σ_{b: camera(b) = c} W_i(b) for every camera c, and W_h = Σ_b J_h(b)ᵀJ_ρ(b)
@@ -3740,10 +3742,16 @@ __global__ __launch_bounds__(256) void intr_border_kernel(const IntrBorderArgs a
   for (int d = 0; d < 8; ++d)
 #pragma unroll
     for (int cc = 0; cc < 6; ++cc) acc[d][cc] = 0.0;
-  for (int q = a.bptr[L] + (y0 < a.nf ? q0 : 1 << 30); q < a.bptr[L + 1]; q += dq) {
-    const int b = a.blist[q];
-    const double* B = a.ib + (long long)b * kIbStride;
-    const double* Jc = B + (a.ib_rec[b].z == y ? kIbJh : kIbJt);
+  // the next entry's list index is loaded during this one (a list walk was two dependent memory rounds per entry: the
+  // index, then the row — and the host / target test on the block record before the row's Jacobian)
+  const int qb = a.bptr[L + 1];
+  int q = a.bptr[L] + (y0 < a.nf ? q0 : 1 << 30);
+  int bn = q < qb ? a.blist[q] : 0;
+  for (; q < qb; q += dq) {
+    const int bf = bn;
+    if (q + dq < qb) bn = a.blist[q + dq];
+    const double* B = a.ib + (long long)(bf & 0x7fffffff) * kIbStride;
+    const double* Jc = B + (bf < 0 ? kIbJh : kIbJt);
     double c0[6], c1[6];
 #pragma unroll
     for (int cc = 0; cc < 6; ++cc) {
@@ -3763,18 +3771,29 @@ __global__ __launch_bounds__(256) void intr_border_kernel(const IntrBorderArgs a
   for (int d = 0; d < 8; ++d)
 #pragma unroll
     for (int cc = 0; cc < 6; ++cc) acc[d][cc] = 0.0;
-  for (int q = a.pptr[L] + (y0 < a.nf ? q0 : 1 << 30); q < a.pptr[L + 1]; q += dq) {
-    const int gp = a.plist[q];
-    const int4 pr = a.pt_rec[gp];
+  const int qp = a.pptr[L + 1];
+  q = a.pptr[L] + (y0 < a.nf ? q0 : 1 << 30);
+  int gpn = q < qp ? a.plist[q] : 0, byn = q < qp ? a.pblk[q] : -1;
+  for (; q < qp; q += dq) {
+    const int gp = gpn, by = byn;
+    if (q + dq < qp) {
+      gpn = a.plist[q + dq];
+      byn = a.pblk[q + dq];
+    }
     double wc[8], wy[6];  // W of the point for camera c (Σ W_i over its blocks seen by c, intr_pw_kernel) and for
                           // keyframe y (Σ J_h / J_t ᵀJ_ρ over its blocks hosted / targeted by y)
     const double* pw = a.pw + (long long)gp * (8 * a.nc + 6);
 #pragma unroll
     for (int d = 0; d < 8; ++d) wc[d] = pw[8 * c + d];
-    if (pr.z == y) {  // y hosts the point: every block's J_hᵀJ_ρ (intr_pw_kernel)
+    if (by == -1) {  // y hosts the point: every block's J_hᵀJ_ρ (intr_pw_kernel)
 #pragma unroll
       for (int cc = 0; cc < 6; ++cc) wy[cc] = pw[8 * a.nc + cc];
-    } else {          // y is a target: its block(s) of the point
+    } else if (by >= 0) {  // y is a target: the point's block targeting it
+      const double* B = a.ib + (long long)by * kIbStride;
+#pragma unroll
+      for (int cc = 0; cc < 6; ++cc) wy[cc] = 0.0 + (B[kIbJt + cc] * B[kIbJr] + B[kIbJt + 6 + cc] * B[kIbJr + 1]);
+    } else {  // several blocks of the point target y: their sum, in block order
+      const int4 pr = a.pt_rec[gp];
 #pragma unroll
       for (int cc = 0; cc < 6; ++cc) wy[cc] = 0.0;
       for (int b = pr.x; b < pr.x + pr.y; ++b) {
@@ -3877,8 +3896,12 @@ __global__ __launch_bounds__(256) void intr_cam_dir_kernel(const IntrBorderArgs 
   double acc[kCamDir];
 #pragma unroll
   for (int v = 0; v < kCamDir; ++v) acc[v] = 0.0;
-  for (int q = a.bptr[L] + threadIdx.x + 256 * blockIdx.x; q < a.bptr[L + 1]; q += 256 * kCamSplit) {
-    const double* B = a.ib + (long long)a.blist[q] * kIbStride;
+  const int qe = a.bptr[L + 1];
+  int q = a.bptr[L] + threadIdx.x + 256 * blockIdx.x;
+  int bn = q < qe ? a.blist[q] : 0;  // (the next entry's index loaded during this one)
+  for (; q < qe; q += 256 * kCamSplit) {
+    const double* B = a.ib + (long long)bn * kIbStride;
+    if (q + 256 * kCamSplit < qe) bn = a.blist[q + 256 * kCamSplit];
     double j0[8], j1[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
@@ -4908,7 +4931,7 @@ int gn_prepare(pba_engine* e) {
     // the blocks whose target camera is c and that touch u (host or target u; u = c: every block of camera c), Schur
     // terms from the points with a block of camera c that touch u (a block of keyframe u / of camera u − nf)
     const int nu = nf + nc;
-    std::vector<std::vector<int>> bl((size_t)nc * nu), pl((size_t)nc * nu);
+    std::vector<std::vector<int>> bl((size_t)nc * nu), pl((size_t)nc * nu), pk((size_t)nc * nu);
     std::vector<int> bcam(nb);
     std::vector<int4> ibrec(nb);
     std::vector<char> cam_seen(nc, 0);
@@ -4917,7 +4940,7 @@ int gn_prepare(pba_engine* e) {
       bcam[gb] = c;
       ibrec[gb] = make_int4(b, pt, h, t);
       cam_seen[c] = 1;
-      bl[(size_t)c * nu + h].push_back(gb);
+      bl[(size_t)c * nu + h].push_back((int)((unsigned)gb | 0x80000000u));  // (bit 31: the unit hosts the block)
       bl[(size_t)c * nu + t].push_back(gb);
       bl[(size_t)c * nu + nf + c].push_back(gb);
     }
@@ -4929,17 +4952,33 @@ int gn_prepare(pba_engine* e) {
       }
       for (int c : cams) units.push_back(nf + c);
       for (int c : cams)
-        for (int u : units) pl[(size_t)c * nu + u].push_back(q);
+        for (int u : units) {
+          pl[(size_t)c * nu + u].push_back(q);
+          // the border kernel's Schur term for keyframe u: −1 u hosts the point, else its one block targeting u
+          int by = -1;
+          if (u < nf && u != phost[q]) {
+            int n_u = 0;
+            for (int gb = pfirst[q]; gb < pfirst[q] + pnblk[q]; ++gb)
+              if (gtgt[gb] == u) {
+                by = gb;
+                ++n_u;
+              }
+            if (n_u != 1) by = -2;
+          }
+          pk[(size_t)c * nu + u].push_back(by);
+        }
     }
-    std::vector<int> bp(1, 0), bflat, pp(1, 0), pflat;
+    std::vector<int> bp(1, 0), bflat, pp(1, 0), pflat, pkflat;
     for (size_t L = 0; L < bl.size(); ++L) {
       bflat.insert(bflat.end(), bl[L].begin(), bl[L].end());
       bp.push_back((int)bflat.size());
       pflat.insert(pflat.end(), pl[L].begin(), pl[L].end());
+      pkflat.insert(pkflat.end(), pk[L].begin(), pk[L].end());
       pp.push_back((int)pflat.size());
     }
     if (bflat.empty()) bflat.push_back(0);
     if (pflat.empty()) pflat.push_back(0);
+    if (pkflat.empty()) pkflat.push_back(-1);
     for (int c = 0; c < nc; ++c) fixed[nf + 2 * c] = fixed[nf + 2 * c + 1] = !cam_seen[c];
     hipStream_t st0 = e->stream;
     PBA_HIP(G.ib_rec.upload(ibrec, st0));
@@ -4948,6 +4987,7 @@ int gn_prepare(pba_engine* e) {
     PBA_HIP(G.ib_blist.upload(bflat, st0));
     PBA_HIP(G.ib_pptr.upload(pp, st0));
     PBA_HIP(G.ib_plist.upload(pflat, st0));
+    PBA_HIP(G.ib_pblk.upload(pkflat, st0));
     PBA_HIP(G.ib_data.resize((size_t)nb * kIbStride));
     PBA_HIP(G.ib_pw.resize((size_t)std::max(ngp, 1) * (8 * nc + 6)));
     PBA_HIP(G.ib_part.resize((size_t)kCamSplit * (nc * kCamDir + nc * (nc + 1) / 2 * kCamSch)));
@@ -5473,7 +5513,7 @@ void enqueue_border(pba_engine* e, double lambda, const double* lm, double* X) {
   const int nf = e->n_frames, nfs = G.nfs;
   IntrBorderArgs ba{G.ib_data.p, G.ib_rec.p, G.ib_cam.p, G.pt_rec.p, G.pt_data.p, G.ib_bptr.p, G.ib_blist.p,
                     G.ib_pptr.p, G.ib_plist.p, G.sky_first.p, G.sky_row.p, G.fixed.p, lm ? lm : G.lm_idle.p, G.S.p,
-                    G.g.p, G.g_dir.p, G.Ddiag.p, nf, G.nc_sys, X, (long long)nfs * 36 + EX_TAIL, G.ib_pw.p};
+                    G.g.p, G.g_dir.p, G.Ddiag.p, nf, G.nc_sys, X, (long long)nfs * 36 + EX_TAIL, G.ib_pw.p, G.ib_pblk.p};
   const int nb = 2 * G.nc_sys + 1;
   intr_pw_kernel<<<(8 * G.n_gn_points + 255) / 256, 256, 0, e->stream>>>(ba, G.n_gn_points);
 #ifndef PBA_INTR_KPW_BIG
