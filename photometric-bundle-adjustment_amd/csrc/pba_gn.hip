@@ -3477,6 +3477,12 @@ struct IntrRowsArgs {
   double* out;           // ib_data
   int n;
   const double* lm;      // LM record: nothing to do once the solve is done
+  // point-aligned waves (gn_prepare, every GN point ≤ 64 blocks): wave w takes GN blocks wave_tab[w].x … + .y − 1, whole
+  // points from GN point wave_tab[w].z on, and also writes their W sums into pw (intr_pw_kernel's work); else nullptr
+  const int4* wave_tab = nullptr;
+  int n_waves = 0;
+  double* pw = nullptr;
+  int nc = 0;
 };
 struct PoseT {  // a relative pose for pair_rotation / pair_translation
   double R[9], t[3];
@@ -3493,13 +3499,27 @@ constexpr int kIbStage = 27;  // doubles per staged half row (26 used; odd: 2-wa
 #endif
 template <int MODEL>
 __global__ __launch_bounds__(256) void intr_rows_kernel(const IntrRowsArgs a) {
-  const int gb0 = blockIdx.x * blockDim.x + threadIdx.x;
+  const int lane = threadIdx.x & 63;
 #ifdef PBA_IB_DIRECT
+  const int gb0 = blockIdx.x * blockDim.x + threadIdx.x;
   if (gb0 >= a.n || lm_view(a.lm).done != 0.0) return;
   const int gb = gb0;
 #else
-  if (lm_view(a.lm).done != 0.0) return;  // (uniform)
-  const int gb = min(gb0, a.n - 1);       // every lane of a wave takes part in its stores
+  // the wave's rows: 64 consecutive GN blocks, or (wave_tab) a point-aligned run of ≤ 64
+  int row0, nrow;
+  int4 wt = make_int4(0, 0, 0, 0);
+  if (a.wave_tab) {
+    const int w = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    if (w >= a.n_waves) return;  // (whole waves)
+    wt = a.wave_tab[w];
+    row0 = wt.x;
+    nrow = wt.y;
+  } else {
+    row0 = blockIdx.x * blockDim.x + (threadIdx.x & ~63);
+    nrow = min(64, a.n - row0);
+  }
+  if (lm_view(a.lm).done != 0.0) return;       // (uniform)
+  const int gb = row0 + max(min(lane, nrow - 1), 0);  // every lane of a wave takes part in its stores
 #endif
   const int4 br = a.rec[gb];
   PoseT T;
@@ -3555,8 +3575,6 @@ __global__ __launch_bounds__(256) void intr_rows_kernel(const IntrRowsArgs a) {
 #else
   constexpr int HALF = kIbStride / 2, CH = HALF / 2;  // 26 doubles, 13 chunks of 16 B per half row
   __shared__ double stage[4][64 * kIbStage];
-  const int lane = threadIdx.x & 63;
-  const int row0 = gb0 - lane, nrow = min(64, a.n - row0);  // the wave's rows in ib_data
   double* st = stage[threadIdx.x >> 6];
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
@@ -3576,6 +3594,53 @@ __global__ __launch_bounds__(256) void intr_rows_kernel(const IntrRowsArgs a) {
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   }
+  if (!a.wave_tab) return;
+  // the points' W sums (intr_pw_kernel's, in the same block order): each block's W_i, J_hᵀJ_ρ and camera through the
+  // stage, then the first block of every point adds its point's blocks
+  const int cam = a.frame_cam[br.w];
+#pragma unroll
+  for (int d = 0; d < 8; ++d) st[lane * kIbStage + d] = J[kIbWi + d];
+#pragma unroll
+  for (int k = 0; k < 6; ++k)
+    st[lane * kIbStage + 8 + k] = J[kIbJh + k] * J[kIbJr] + J[kIbJh + 6 + k] * J[kIbJr + 1];
+  st[lane * kIbStage + 14] = (double)cam;
+  const bool live = lane < nrow;
+  const int prev_pt = __shfl(br.y, (lane + 63) & 63, 64);
+  const unsigned long long firsts = __ballot(live && (lane == 0 || br.y != prev_pt));
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  if (!((firsts >> lane) & 1ull)) return;
+  const unsigned long long later = lane == 63 ? 0ull : firsts >> (lane + 1);
+  const int nb = later ? __builtin_ctzll(later) + 1 : nrow - lane;  // this point's blocks: lanes lane … lane + nb − 1
+  const int gp = wt.z + __popcll(firsts & ((1ull << lane) - 1ull));
+  double* o = a.pw + (long long)gp * (8 * a.nc + 6);
+  double wh[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+  for (int c0 = 0; c0 < a.nc; c0 += 4) {  // cameras in groups of four, as intr_pw_kernel
+    double wc[4][8];
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+      for (int d = 0; d < 8; ++d) wc[c][d] = 0.0;
+    for (int b = lane; b < lane + nb; ++b) {
+      const double* sb = st + b * kIbStage;
+      const int cb = (int)sb[14] - c0;
+#pragma unroll
+      for (int d = 0; d < 8; ++d) {
+        const double w = sb[d];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) wc[c][d] += c == cb ? w : 0.0;
+      }
+      if (c0 == 0)
+#pragma unroll
+        for (int k = 0; k < 6; ++k) wh[k] += sb[8 + k];
+    }
+    for (int c = 0; c < 4 && c0 + c < a.nc; ++c)
+#pragma unroll
+      for (int d = 0; d < 8; ++d) o[8 * (c0 + c) + d] = wc[c][d];
+  }
+#pragma unroll
+  for (int k = 0; k < 6; ++k) o[8 * a.nc + k] = wh[k];
 #endif
 }
 
@@ -4988,6 +5053,23 @@ int gn_prepare(pba_engine* e) {
     PBA_HIP(G.ib_pptr.upload(pp, st0));
     PBA_HIP(G.ib_plist.upload(pflat, st0));
     PBA_HIP(G.ib_pblk.upload(pkflat, st0));
+    // point-aligned waves for intr_rows_kernel (whole points of ≤ 64 blocks each; a longer point: consecutive waves and
+    // the separate point sums of intr_pw_kernel)
+    {
+      std::vector<int4> wt;
+      bool fits = true;
+      for (int q = 0; q < ngp && fits; ++q) {
+        if (pnblk[q] > 64) fits = false;
+        else if (wt.empty() || wt.back().y + pnblk[q] > 64) wt.push_back(make_int4(pfirst[q], pnblk[q], q, 0));
+        else wt.back().y += pnblk[q];
+      }
+      // (the GN points cover the GN blocks in order: pfirst[q + 1] = pfirst[q] + pnblk[q], checked here)
+      for (int q = 0; q + 1 < ngp && fits; ++q) fits = pfirst[q + 1] == pfirst[q] + pnblk[q];
+      fits = fits && ngp > 0 && pfirst[0] == 0 && pfirst[ngp - 1] + pnblk[ngp - 1] == nb;
+      if (test_hook("PBA_TEST_ROW_WAVES64")) fits = false;  // (tests: the 64-block waves + intr_pw_kernel path)
+      G.ir_waves = fits ? (int)wt.size() : 0;
+      if (fits) PBA_HIP(G.ir_wave.upload(wt, st0));
+    }
     PBA_HIP(G.ib_data.resize((size_t)nb * kIbStride));
     PBA_HIP(G.ib_pw.resize((size_t)std::max(ngp, 1) * (8 * nc + 6)));
     PBA_HIP(G.ib_part.resize((size_t)kCamSplit * (nc * kCamDir + nc * (nc + 1) / 2 * kCamSch)));
@@ -5497,7 +5579,14 @@ void enqueue_intr_rows(pba_engine* e, const double* lm, bool accept = true) {
                                                        e->intr_state.p, G.nc_sys);
   IntrRowsArgs ra{G.ib_rec.p, e->poses.p, e->rho.p, e->u_ref.p, e->u_obs.p, e->frame_cam.p, e->intr_d.p,
                   e->intr_state_d.p, (double)e->opt.huber_width, G.ib_data.p, e->n_blocks, lm ? lm : G.lm_idle.p};
-  const int grid = (e->n_blocks + 255) / 256;
+  int grid = (e->n_blocks + 255) / 256;
+  if (G.ir_waves > 0) {  // point-aligned waves: the points' W sums too (no intr_pw_kernel)
+    ra.wave_tab = G.ir_wave.p;
+    ra.n_waves = G.ir_waves;
+    ra.pw = G.ib_pw.p;
+    ra.nc = G.nc_sys;
+    grid = (G.ir_waves + 3) / 4;
+  }
   switch (e->opt.camera_model) {
     case PBA_CAMERA_PINHOLE: intr_rows_kernel<CAM_PINHOLE><<<grid, 256, 0, e->stream>>>(ra); break;
     case PBA_CAMERA_DOUBLE_SPHERE: intr_rows_kernel<CAM_DS><<<grid, 256, 0, e->stream>>>(ra); break;
@@ -5515,7 +5604,8 @@ void enqueue_border(pba_engine* e, double lambda, const double* lm, double* X) {
                     G.ib_pptr.p, G.ib_plist.p, G.sky_first.p, G.sky_row.p, G.fixed.p, lm ? lm : G.lm_idle.p, G.S.p,
                     G.g.p, G.g_dir.p, G.Ddiag.p, nf, G.nc_sys, X, (long long)nfs * 36 + EX_TAIL, G.ib_pw.p, G.ib_pblk.p};
   const int nb = 2 * G.nc_sys + 1;
-  intr_pw_kernel<<<(8 * G.n_gn_points + 255) / 256, 256, 0, e->stream>>>(ba, G.n_gn_points);
+  if (G.ir_waves == 0)  // (else intr_rows_kernel has formed them)
+    intr_pw_kernel<<<(8 * G.n_gn_points + 255) / 256, 256, 0, e->stream>>>(ba, G.n_gn_points);
 #ifndef PBA_INTR_KPW_BIG
 #define PBA_INTR_KPW_BIG 2
 #endif

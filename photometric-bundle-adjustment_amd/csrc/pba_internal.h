@@ -820,6 +820,8 @@ struct GnData {
   DevBuf<double> ib_pw;         // GN point → W_c (8 per camera), W_h (6): intr_pw_kernel
   DevBuf<int> ib_bptr, ib_blist;  // border unit pair (camera c, unit u) → GN blocks of its direct terms (CSR)
   DevBuf<int> ib_pptr, ib_plist;  // … → GN points of its Schur terms (CSR); unit u < nf: frame u, else camera u − nf
+  DevBuf<int4> ir_wave;           // intr_rows_kernel's point-aligned waves {first GN block, blocks, first GN point}
+  int ir_waves = 0;               // their number (0: 64-block waves + intr_pw_kernel)
   DevBuf<int> ib_pblk;            // per ib_plist entry: −1 (host / camera unit), the point's block targeting frame u, −2
   DevBuf<int> ib_cam;           // GN block → its target's camera
   DevBuf<double> ib_part;       // the camera-block reductions' per-workgroup totals (intr_cam_dir / intr_cam_sch_kernel)

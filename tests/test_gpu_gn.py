@@ -535,6 +535,32 @@ def test_arrow_and_front_solvers_agree(n_cams, lam, monkeypatch):
         assert err <= 1e-8, (name, err)
 
 
+@pytest.mark.parametrize("n_cams", [1, 2, 4])
+def test_point_sums_in_rows_match_separate_kernel(n_cams, monkeypatch):
+    """Free intrinsics: the points' W sums (per camera Σ W_i, and W_h) are formed by intr_rows_kernel itself when every
+    GN point fits one wave (point-aligned waves of ≤ 64 blocks), else by intr_pw_kernel after 64-block waves
+    (PBA_TEST_ROW_WAVES64 forces it; test build).  The same sums in the same block order: the two paths give the same
+    reduced-system step (measured: identical to the last bit or within 1e-15)."""
+    pb, state = _intrinsics_rig(23, 260, 41 + n_cams, n_cams)
+    out = {}
+    for path in ("fused", "separate"):
+        if path == "separate":
+            monkeypatch.setenv("PBA_TEST_ROW_WAVES64", "1")
+        with make_engine(pb, 1.0, (0, 1), E.TEST_LIB_PATH) as eng:
+            eng.set_optimize_intrinsics(True)
+            eng.set_intrinsics_state(state)
+            eng.gn_linearize()
+            m, st = eng.gn_step(1e-3)
+            assert st == 0, path
+            dp, dr = eng.gn_last_step()
+            eng.gn_accept()
+            out[path] = (dp, dr, eng.get_intrinsics() - state, np.array([m]))
+    for name, a, b in zip(("poses", "rho", "intrinsics", "model"), out["fused"], out["separate"]):
+        err = np.linalg.norm(a - b) / np.linalg.norm(b)
+        print(f"\nn_cams {n_cams}: {name} {err:.2e}")
+        assert err <= 1e-12, (name, err)
+
+
 @pytest.fixture(scope="module")
 def c3():
     """BASELINE configs[2] (C3): 200 keyframes × 20k points × 8 px × 4 targets = 80k blocks, rendered images."""
