@@ -2918,9 +2918,8 @@ struct ArrowArgs {
 // right-hand-side columns: global column 0 = −g_a, 1 + q = column q of B (border frame nf + q/6, component q % 6),
 // B[6f + r][q] = S(border row, keyframe f)[q % 6][r].  Every batch's columns in one launch: batch bt's b at
 // L0.b + bt·n·M·kArrowNB (the batches share level 0's D and U).
-__global__ __launch_bounds__(256) void arrow_build_kernel(const ArrowArgs a, int batches) {
+__device__ __forceinline__ void arrow_build(const ArrowArgs& a, int batches, long long tid) {
   constexpr int M = 24, B = 4, NB = kArrowNB;
-  const long long tid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   const int n = a.L0.n;
   if (tid == 0) *a.status = 0;
   auto blk = [&](int i, int j, int r, int c) -> double {  // S[6i + r][6j + c], i ≥ j, 0 outside the profile
@@ -2955,6 +2954,9 @@ __global__ __launch_bounds__(256) void arrow_build_kernel(const ArrowArgs a, int
     else if (gq <= 12 * a.nc) v = blk(a.nf + (gq - 1) / 6, i, (gq - 1) % 6, r);
   }
   a.L0.b[t] = v;
+}
+__global__ __launch_bounds__(256) void arrow_build_kernel(const ArrowArgs a, int batches) {
+  arrow_build(a, batches, (long long)blockIdx.x * blockDim.x + threadIdx.x);
 }
 
 // kArrowSeg workgroups per product: entry e < nb(nb+1)/2 — (q1 ≥ q2) of BᵀX_B — then e − that: q1 of BᵀX_0 (nb = 12nc), a
@@ -4018,10 +4020,10 @@ __global__ __launch_bounds__(256) void intr_cam_sch_kernel(const IntrBorderArgs 
 
 // One WAVE per (border row, camera column block yb ≤ row, entry e) and per border gradient element: lane l adds totals l,
 // l + 64, … of the kCamSplit in order, the wave's lanes by xor butterflies (a fixed order); then border_store.
-__global__ __launch_bounds__(256) void intr_cam_fin_kernel(const IntrBorderArgs a, double lambda, const double* dpart,
-                                                          const double* spart) {
+__device__ __forceinline__ void cam_fin(const IntrBorderArgs& a, double lambda, const double* dpart, const double* spart,
+                                        int blk) {
   lambda = lm_lambda(lm_view(a.lm), lambda);
-  const int nb = 2 * a.nc + 1, i = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int nb = 2 * a.nc + 1, i = blk * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (i >= 2 * a.nc * nb * 36) return;
   const int e = i % 36, yb = (i / 36) % nb, row = i / (36 * nb);
   const bool grad = yb == 2 * a.nc;
@@ -4047,6 +4049,19 @@ __global__ __launch_bounds__(256) void intr_cam_fin_kernel(const IntrBorderArgs 
     sch = sum(spart + (long long)(c * (c + 1) / 2 + c2) * kCamSplit * kCamSch, kCamSch, 8 * d + d2);
   }
   if (lane == 0) border_store(a, lambda, row, (a.nf + yb) * 36 + e, dir, sch);
+}
+__global__ __launch_bounds__(256) void intr_cam_fin_kernel(const IntrBorderArgs a, double lambda, const double* dpart,
+                                                          const double* spart) {
+  cam_fin(a, lambda, dpart, spart, blockIdx.x);
+}
+// The same, with the arrow solve's level 0 (arrow_build) in workgroups fin_blocks … of the same launch: it reads the
+// keyframe band and g (assemble_kernel) and the border rows' keyframe blocks (intr_border_kernel), nothing this launch
+// writes — one launch fewer per trial.
+__global__ __launch_bounds__(256) void intr_cam_fin_build_kernel(const IntrBorderArgs a, double lambda,
+                                                                const double* dpart, const double* spart,
+                                                                const ArrowArgs aa, int batches, int fin_blocks) {
+  if ((int)blockIdx.x < fin_blocks) cam_fin(a, lambda, dpart, spart, blockIdx.x);
+  else arrow_build(aa, batches, (long long)(blockIdx.x - fin_blocks) * blockDim.x + threadIdx.x);
 }
 
 // The candidate intrinsics become the state (after an accepted trial; lm == nullptr: always), fp64 records and fp32 copy.
@@ -5453,23 +5468,40 @@ bool arrow_for(const pba_engine* e, int K) {
 
 // X = A⁻¹[−g_a | B] by parallel cyclic reduction (batches of kArrowNB columns), the border system, the step into G.x
 // (the kernels above).  S, first, row: the skyline system and its profile; fixed: the constant frames.
-int arrow_solve(pba_engine* e, const double* S, const int* first, const int* row, const uint8_t* fixed) {
+// Batch 0's rows of arrow level k (configure_arrow's layout) and the arrow kernels' arguments.
+CrLevel arrow_level(const GnData& G, int k) {
+  constexpr int M = 24, NB = kArrowNB;
+  const int n = G.ar_n, nbt = G.ar_batches;
+  const size_t lvl = (size_t)n * M * M * 2 + (size_t)n * M * NB, nbq = (size_t)n * M * NB;
+  double* p = G.ar_buf.p + (k == 0 ? 0 : (size_t)n * M * M * 2 + nbt * nbq + (size_t)(k - 1) * nbt * lvl);
+  return CrLevel{p, p + (size_t)n * M * M, p + (size_t)2 * n * M * M, nullptr, nullptr, n};
+}
+ArrowArgs arrow_args(pba_engine* e, const double* S, const int* first, const int* row, const uint8_t* fixed) {
+  GnData& G = e->gn;
+  const int nb = 12 * G.nc_sys;
+  return ArrowArgs{S, first, row, G.g.p, fixed, arrow_level(G, 0), G.ar_X.p, G.ar_part.p, G.ar_dc.p, G.x.p, G.status.p,
+                   e->n_frames, G.nc_sys, kArrowNB * G.ar_batches, nb * (nb + 1) / 2 + nb};
+}
+// arrow_build's threads (level 0: D, U and every batch's right-hand sides)
+long long arrow_build_threads(const GnData& G) {
+  constexpr int M = 24;
+  return 2LL * G.ar_n * M * M + (long long)G.ar_batches * G.ar_n * M * kArrowNB;
+}
+
+// built: level 0 is already in place (intr_cam_fin_build_kernel of the same trial).
+int arrow_solve(pba_engine* e, const double* S, const int* first, const int* row, const uint8_t* fixed,
+                bool built = false) {
   GnData& G = e->gn;
   constexpr int M = 24, NB = kArrowNB;
-  const int nf = e->n_frames, nc = G.nc_sys, n = G.ar_n, nb = 12 * nc;
+  const int nf = e->n_frames, n = G.ar_n;
   hipStream_t st = e->stream;
   const int nbt = G.ar_batches;
   const size_t lvl = (size_t)n * M * M * 2 + (size_t)n * M * NB, nbq = (size_t)n * M * NB;
-  auto level = [&](int k) {  // batch 0's rows of level k (configure_arrow's layout)
-    double* p = G.ar_buf.p + (k == 0 ? 0 : (size_t)n * M * M * 2 + nbt * nbq + (size_t)(k - 1) * nbt * lvl);
-    return CrLevel{p, p + (size_t)n * M * M, p + (size_t)2 * n * M * M, nullptr, nullptr, n};
-  };
-  ArrowArgs aa{S, first, row, G.g.p, fixed, level(0), G.ar_X.p, G.ar_part.p, G.ar_dc.p, G.x.p, G.status.p,
-               nf, nc, NB * G.ar_batches, nb * (nb + 1) / 2 + nb};
+  auto level = [&](int k) { return arrow_level(G, k); };
+  const ArrowArgs aa = arrow_args(e, S, first, row, fixed);
   constexpr size_t lds = cr_level_wave_lds<M, NB>();
   static_assert(lds <= 65536, "default dynamic LDS limit");
-  const long long nth = 2LL * n * M * M + (long long)nbt * n * M * NB;
-  arrow_build_kernel<<<(unsigned)((nth + 255) / 256), 256, 0, st>>>(aa, nbt);
+  if (!built) arrow_build_kernel<<<(unsigned)((arrow_build_threads(G) + 255) / 256), 256, 0, st>>>(aa, nbt);
   // the batches' cyclic reductions side by side (gridDim.y): one launch per level whatever the number of cameras
   CrLevel src = level(0);
   if (n <= 1)
@@ -5597,7 +5629,9 @@ void enqueue_intr_rows(pba_engine* e, const double* lm, bool accept = true) {
 
 // The border rows of the reduced system (free intrinsics) into the skyline S — or, X ≠ nullptr, this rank's undamped
 // border into the exchange buffer's border region (X points at it).
-void enqueue_border(pba_engine* e, double lambda, const double* lm, double* X) {
+// arrow: the local solve is an arrow (arrow_solve follows with built = true): its level 0 is built in the same launch as
+// the camera blocks.
+void enqueue_border(pba_engine* e, double lambda, const double* lm, double* X, bool arrow = false) {
   GnData& G = e->gn;
   const int nf = e->n_frames, nfs = G.nfs;
   IntrBorderArgs ba{G.ib_data.p, G.ib_rec.p, G.ib_cam.p, G.pt_rec.p, G.pt_data.p, G.ib_bptr.p, G.ib_blist.p,
@@ -5615,7 +5649,15 @@ void enqueue_border(pba_engine* e, double lambda, const double* lm, double* X) {
   double* spart = dpart + (size_t)G.nc_sys * kCamSplit * kCamDir;
   intr_cam_dir_kernel<<<dim3(kCamSplit, G.nc_sys), 256, 0, e->stream>>>(ba, dpart);
   intr_cam_sch_kernel<<<dim3(kCamSplit, G.nc_sys * (G.nc_sys + 1) / 2), 256, 0, e->stream>>>(ba, lambda, spart);
-  intr_cam_fin_kernel<<<(2 * G.nc_sys * nb * 36 + 3) / 4, 256, 0, e->stream>>>(ba, lambda, dpart, spart);
+  const int fin_blocks = (2 * G.nc_sys * nb * 36 + 3) / 4;
+  if (arrow) {
+    const ArrowArgs aa = arrow_args(e, G.S.p, G.sky_first.p, G.sky_row.p, G.fixed.p);
+    const int build_blocks = (int)((arrow_build_threads(G) + 255) / 256);
+    intr_cam_fin_build_kernel<<<fin_blocks + build_blocks, 256, 0, e->stream>>>(ba, lambda, dpart, spart, aa,
+                                                                               G.ar_batches, fin_blocks);
+  } else {
+    intr_cam_fin_kernel<<<fin_blocks, 256, 0, e->stream>>>(ba, lambda, dpart, spart);
+  }
 }
 
 // Schur complement for λ, assembly and reduced-system solve into G.x (enqueued only).
@@ -5661,11 +5703,13 @@ int enqueue_solve(pba_engine* e, double lambda, const double* lm = nullptr, bool
   }
   const int nthreads = (G.n_sky + (kAsmSeg - 1) * G.n_sky_diag) * 36 + 6 * nfs * kAsmSeg;
   assemble_kernel<<<(nthreads + 255) / 256, 256, 0, e->stream>>>(aa, lambda);
-  if (G.nc_sys) enqueue_border(e, lambda, lm, nullptr);  // the intrinsics rows of the skyline system (over assemble's zeros)
+  // the intrinsics rows of the skyline system (over assemble's zeros); an arrow solve's level 0 in the same launch
+  const bool arrow = G.nc_sys && !G.band_kernel && arrow_for(e, G.band);
+  if (G.nc_sys) enqueue_border(e, lambda, lm, nullptr, arrow);
   if (G.band_kernel) {
     if (int rc = band_solve(e, !direct)) return rc;
   } else {
-    if (G.nc_sys && arrow_for(e, G.band)) return arrow_solve(e, G.S.p, G.sky_first.p, G.sky_row.p, G.fixed.p);
+    if (arrow) return arrow_solve(e, G.S.p, G.sky_first.p, G.sky_row.p, G.fixed.p, true);
     if (G.front.lds) return launch_front(e, G.front, G.S.p, G.L.p, nfs);
     PBA_HIP(hipMemcpyAsync(G.L.p, G.S.p, sizeof(double) * 36 * (size_t)G.n_sky, hipMemcpyDeviceToDevice, e->stream));
     SolveArgs so{G.L.p, G.sky_first.p, G.sky_row.p, G.sky_last.p, G.g.p, G.Linv.p, G.x.p, G.status.p, nfs,
