@@ -1416,7 +1416,7 @@ __global__ void import_kernel(const ImportArgs a, double lambda, const double* _
 }
 
 // Free intrinsics on several GPUs: the summed exchange — the keyframes' band rows and the 2·nc border rows (the
-// border region after the band, export by intr_border_kernel & co.) — into the skyline system of the summed profile
+// border region after the band, export by intr_border_all_kernel) — into the skyline system of the summed profile
 // (keyframe i: columns max(0, i − K) … i; border rows: 0 … P; row offsets `row`), with the single-GPU arithmetic of
 // assemble_kernel and border_store: + λ·clamp(diag(A)), identity rows / columns for constant frames (requested, or
 // observed by no rank — cameras: seen by no rank), the intrinsics pads (1 + λ on the diagonal, LM diagonal 1).  One lane
@@ -3794,11 +3794,11 @@ __device__ __forceinline__ double wave_rs48(const double (&v)[48], int lane, int
 // kpw = 4 while the keyframe waves would not fill the SIMDs (C3, 200 keyframes), else 2 (C4: 2008 waves; 1 and 4 measured
 // 80.5 and 82.4 against 76.5 µs).  Round 5 walked the lists twice (one kernel per border row: 133 + 117 µs at C4) and
 // each point's blocks once per (point, list).
-__global__ __launch_bounds__(256) void intr_border_kernel(const IntrBorderArgs a, double lambda, int kpw) {
+__device__ __forceinline__ void border_keyframes(const IntrBorderArgs& a, double lambda, int kpw, int bx, int by) {
   __shared__ double2 s_w[4][48];
   lambda = lm_lambda(lm_view(a.lm), lambda);
-  const int c = blockIdx.y, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int gw = blockIdx.x * 4 + w, y0 = gw / kpw, sub = gw % kpw;
+  const int c = by, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int gw = bx * 4 + w, y0 = gw / kpw, sub = gw % kpw;
   const int y = min(y0, a.nf - 1);  // (a wave past the last keyframe walks nothing and stores nothing)
   const int L = c * (a.nf + a.nc) + y;
   const int q0 = sub * 64 + lane, dq = y0 < a.nf ? 64 * kpw : 1 << 30;
@@ -3903,10 +3903,10 @@ __global__ __launch_bounds__(256) void intr_border_kernel(const IntrBorderArgs a
 // reductions over whole lists instead of one list walk per (border row, column block) — the list of a camera holds ALL
 // of its blocks (400k at C4) and points (100k), and round 5 walked it six times per trial (two row kernels × three column
 // blocks, 165 µs at C4 with the finishing kernel):
-//   intr_cam_dir_kernel — per camera c, over its blocks: Σ J_iᵀJ_i (the 8 × 8 upper triangle, 36) and Σ J_iᵀr (8): the
+//   cam_dir — per camera c, over its blocks: Σ J_iᵀJ_i (the 8 × 8 upper triangle, 36) and Σ J_iᵀr (8): the
 //     direct terms (a block's intrinsics Jacobian is its target camera's, so the direct part couples a camera only with
 //     itself);
-//   intr_cam_sch_kernel — per camera pair (c, c2 ≤ c), over the points seen by both: Σ_p W_c W_c2ᵀ / H'_ρρ (8 × 8) and,
+//   cam_sch — per camera pair (c, c2 ≤ c), over the points seen by both: Σ_p W_c W_c2ᵀ / H'_ρρ (8 × 8) and,
 //     for c2 = c, Σ_p W_c g_ρ / H'_ρρ (8): the Schur terms (W_c from intr_pw_kernel);
 // each over kCamSplit workgroups (a thread takes every (256·kCamSplit)th entry; wave butterflies, then the four waves in
 // order), and intr_cam_fin_kernel adds the kCamSplit totals in order per element and stores it (border_store) — a fixed
@@ -3957,14 +3957,14 @@ __device__ __forceinline__ void wg_sum_store(const double* acc, double* s_w, dou
   for (int i = threadIdx.x; i < NV; i += blockDim.x) out[i] = ((s_w[i] + s_w[NP + i]) + s_w[2 * NP + i]) + s_w[3 * NP + i];
 }
 
-__global__ __launch_bounds__(256) void intr_cam_dir_kernel(const IntrBorderArgs a, double* part) {
+__device__ __forceinline__ void cam_dir(const IntrBorderArgs& a, double* part, int bx, int by) {
   __shared__ double s_w[4 * pad16(kCamDir)];
-  const int c = blockIdx.y, L = c * (a.nf + a.nc) + a.nf + c;  // (camera c, unit nf + c): every block of camera c
+  const int c = by, L = c * (a.nf + a.nc) + a.nf + c;  // (camera c, unit nf + c): every block of camera c
   double acc[kCamDir];
 #pragma unroll
   for (int v = 0; v < kCamDir; ++v) acc[v] = 0.0;
   const int qe = a.bptr[L + 1];
-  int q = a.bptr[L] + threadIdx.x + 256 * blockIdx.x;
+  int q = a.bptr[L] + threadIdx.x + 256 * bx;
   int bn = q < qe ? a.blist[q] : 0;  // (the next entry's index loaded during this one)
   for (; q < qe; q += 256 * kCamSplit) {
     const double* B = a.ib + (long long)bn * kIbStride;
@@ -3983,13 +3983,13 @@ __global__ __launch_bounds__(256) void intr_cam_dir_kernel(const IntrBorderArgs 
       acc[36 + i] += j0[i] * r0 + j1[i] * r1;
     }
   }
-  wg_sum_store<kCamDir>(acc, s_w, part + ((long long)c * kCamSplit + blockIdx.x) * kCamDir);
+  wg_sum_store<kCamDir>(acc, s_w, part + ((long long)c * kCamSplit + bx) * kCamDir);
 }
 
-__global__ __launch_bounds__(256) void intr_cam_sch_kernel(const IntrBorderArgs a, double lambda, double* part) {
+__device__ __forceinline__ void cam_sch(const IntrBorderArgs& a, double lambda, double* part, int bx, int by) {
   __shared__ double s_w[4 * pad16(kCamSch)];
   lambda = lm_lambda(lm_view(a.lm), lambda);
-  const int pc = blockIdx.y;  // camera pair (c, c2 ≤ c), pc = c(c+1)/2 + c2
+  const int pc = by;  // camera pair (c, c2 ≤ c), pc = c(c+1)/2 + c2
   int c = 0;
   while ((c + 1) * (c + 2) / 2 <= pc) ++c;
   const int c2 = pc - c * (c + 1) / 2, L = c * (a.nf + a.nc) + a.nf + c2;  // points seen by c and c2
@@ -3997,7 +3997,7 @@ __global__ __launch_bounds__(256) void intr_cam_sch_kernel(const IntrBorderArgs 
   double acc[kCamSch];
 #pragma unroll
   for (int v = 0; v < kCamSch; ++v) acc[v] = 0.0;
-  for (int q = a.pptr[L] + threadIdx.x + 256 * blockIdx.x; q < a.pptr[L + 1]; q += 256 * kCamSplit) {
+  for (int q = a.pptr[L] + threadIdx.x + 256 * bx; q < a.pptr[L + 1]; q += 256 * kCamSplit) {
     const int gp = a.plist[q];
     const double* pw = a.pw + (long long)gp * st;
     const double inv = border_inv(a, gp, lambda), gr = a.pt_data[(long long)gp * 8 + 1];
@@ -4015,7 +4015,39 @@ __global__ __launch_bounds__(256) void intr_cam_sch_kernel(const IntrBorderArgs 
       acc[64 + i] += iw * gr;
     }
   }
-  wg_sum_store<kCamSch>(acc, s_w, part + ((long long)pc * kCamSplit + blockIdx.x) * kCamSch);
+  wg_sum_store<kCamSch>(acc, s_w, part + ((long long)pc * kCamSplit + bx) * kCamSch);
+}
+
+__global__ __launch_bounds__(256) void intr_border_kernel(const IntrBorderArgs a, double lambda, int kpw) {
+  border_keyframes(a, lambda, kpw, blockIdx.x, blockIdx.y);
+}
+__global__ __launch_bounds__(256) void intr_cam_dir_kernel(const IntrBorderArgs a, double* part) {
+  cam_dir(a, part, blockIdx.x, blockIdx.y);
+}
+__global__ __launch_bounds__(256) void intr_cam_sch_kernel(const IntrBorderArgs a, double lambda, double* part) {
+  cam_sch(a, lambda, part, blockIdx.x, blockIdx.y);
+}
+// The three border reductions are independent (they read the rows, the points' sums and the lists, and write
+// different outputs): while the keyframe part is small (nf·nc < 512 keyframe blocks, the 4-waves-per-keyframe regime:
+// C3), one launch runs them side by side — workgroups [0, nk) the keyframe blocks (nk_x per camera), then kCamSplit per
+// camera of direct sums, then kCamSplit per camera pair of Schur sums — instead of three launches in sequence, each a
+// fraction of the chip (C3: 35.3 → 24.6 µs, two cameras 41.3 → 31.1; at C4, where the keyframe part alone fills the
+// chip, side by side measured 108 against 102 µs in sequence).
+__global__ __launch_bounds__(256) void intr_border_all_kernel(const IntrBorderArgs a, double lambda, int kpw, int nk_x,
+                                                             double* dpart, double* spart) {
+  int b = blockIdx.x;
+  const int nk = nk_x * a.nc, nd = kCamSplit * a.nc;
+  if (b < nk) {
+    border_keyframes(a, lambda, kpw, b % nk_x, b / nk_x);
+    return;
+  }
+  b -= nk;
+  if (b < nd) {
+    cam_dir(a, dpart, b % kCamSplit, b / kCamSplit);
+    return;
+  }
+  b -= nd;
+  cam_sch(a, lambda, spart, b % kCamSplit, b / kCamSplit);
 }
 
 // One WAVE per (border row, camera column block yb ≤ row, entry e) and per border gradient element: lane l adds totals l,
@@ -4055,7 +4087,7 @@ __global__ __launch_bounds__(256) void intr_cam_fin_kernel(const IntrBorderArgs 
   cam_fin(a, lambda, dpart, spart, blockIdx.x);
 }
 // The same, with the arrow solve's level 0 (arrow_build) in workgroups fin_blocks … of the same launch: it reads the
-// keyframe band and g (assemble_kernel) and the border rows' keyframe blocks (intr_border_kernel), nothing this launch
+// keyframe band and g (assemble_kernel) and the border rows' keyframe blocks (border_keyframes), nothing this launch
 // writes — one launch fewer per trial.
 __global__ __launch_bounds__(256) void intr_cam_fin_build_kernel(const IntrBorderArgs a, double lambda,
                                                                 const double* dpart, const double* spart,
@@ -5643,12 +5675,18 @@ void enqueue_border(pba_engine* e, double lambda, const double* lm, double* X, b
 #ifndef PBA_INTR_KPW_BIG
 #define PBA_INTR_KPW_BIG 2
 #endif
-  const int kpw = nf * G.nc_sys < 512 ? 4 : PBA_INTR_KPW_BIG;  // waves per keyframe block (intr_border_kernel)
-  intr_border_kernel<<<dim3((nf * kpw + 3) / 4, G.nc_sys), 256, 0, e->stream>>>(ba, lambda, kpw);
+  const int kpw = nf * G.nc_sys < 512 ? 4 : PBA_INTR_KPW_BIG;  // waves per keyframe block (border_keyframes)
   double* dpart = G.ib_part.p;
   double* spart = dpart + (size_t)G.nc_sys * kCamSplit * kCamDir;
-  intr_cam_dir_kernel<<<dim3(kCamSplit, G.nc_sys), 256, 0, e->stream>>>(ba, dpart);
-  intr_cam_sch_kernel<<<dim3(kCamSplit, G.nc_sys * (G.nc_sys + 1) / 2), 256, 0, e->stream>>>(ba, lambda, spart);
+  const int nk_x = (nf * kpw + 3) / 4, ncp = G.nc_sys * (G.nc_sys + 1) / 2;
+  if (nf * G.nc_sys < 512) {
+    const int n_wg = nk_x * G.nc_sys + kCamSplit * (G.nc_sys + ncp);
+    intr_border_all_kernel<<<n_wg, 256, 0, e->stream>>>(ba, lambda, kpw, nk_x, dpart, spart);
+  } else {
+    intr_border_kernel<<<dim3(nk_x, G.nc_sys), 256, 0, e->stream>>>(ba, lambda, kpw);
+    intr_cam_dir_kernel<<<dim3(kCamSplit, G.nc_sys), 256, 0, e->stream>>>(ba, dpart);
+    intr_cam_sch_kernel<<<dim3(kCamSplit, ncp), 256, 0, e->stream>>>(ba, lambda, spart);
+  }
   const int fin_blocks = (2 * G.nc_sys * nb * 36 + 3) / 4;
   if (arrow) {
     const ArrowArgs aa = arrow_args(e, G.S.p, G.sky_first.p, G.sky_row.p, G.fixed.p);

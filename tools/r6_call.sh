@@ -1,5 +1,10 @@
 set -u
 cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out && export TMPDIR=/tmp && rm -f gpurun_out/steps.txt
-bash tools/gpu_steps.sh \
- 600 gpurun_out/r6_arrow_t23.log python3 -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_gn.py tests/test_gpu_distributed.py tests/test_gpu_configs.py -k "arrow or free_intrinsics or front_and_global or optimize_intrinsics or solver_paths or intrinsics or point_sums" @@ \
- 240 gpurun_out/r6_intr_probe23.log rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/intr6w -o run -- python3 tools/probe/intr_probe.py
+args=()
+for i in 1 2; do
+  for v in prev cur; do
+    args+=(240 gpurun_out/r6_ab27_${v}_$i.log env PBA_LIBRARY=$PWD/variants/libpba_$v.so rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/ab27_${v}_$i -o run -- python3 tools/probe/intr_probe.py @@)
+  done
+done
+unset 'args[${#args[@]}-1]'
+bash tools/gpu_steps.sh "${args[@]}"
