@@ -5044,6 +5044,7 @@ int gn_prepare(pba_engine* e) {
     // terms from the points with a block of camera c that touch u (a block of keyframe u / of camera u − nf)
     const int nu = nf + nc;
     std::vector<std::vector<int>> bl((size_t)nc * nu), pl((size_t)nc * nu), pk((size_t)nc * nu);
+    const bool walk = test_hook("PBA_TEST_PBLK_WALK") != nullptr;  // (tests: every target entry walks its point's blocks)
     std::vector<int> bcam(nb);
     std::vector<int4> ibrec(nb);
     std::vector<char> cam_seen(nc, 0);
@@ -5075,7 +5076,7 @@ int gn_prepare(pba_engine* e) {
                 by = gb;
                 ++n_u;
               }
-            if (n_u != 1) by = -2;
+            if (n_u != 1 || walk) by = -2;
           }
           pk[(size_t)c * nu + u].push_back(by);
         }

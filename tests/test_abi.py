@@ -32,7 +32,7 @@ def test_test_build_exports_the_same_abi():
     missing = [n for n in E.header_functions() if not hasattr(L, n)]
     assert not missing, missing
     hooks = (b"PBA_TEST_PERTURB_DECISION", b"PBA_LM_HOST_DELAY_US", b"PBA_TEST_FORCE_DEGEN", b"PBA_LIN_LEGACY",
-             b"PBA_TEST_ROW_WAVES64")
+             b"PBA_TEST_ROW_WAVES64", b"PBA_TEST_PBLK_WALK")
     test_blob, prod_blob = open(E.TEST_LIB_PATH, "rb").read(), open(E.LIB_PATH, "rb").read()
     assert all(h in test_blob for h in hooks)
     assert not any(h in prod_blob for h in hooks)

@@ -540,12 +540,17 @@ def test_point_sums_in_rows_match_separate_kernel(n_cams, monkeypatch):
     """Free intrinsics: the points' W sums (per camera Σ W_i, and W_h) are formed by intr_rows_kernel itself when every
     GN point fits one wave (point-aligned waves of ≤ 64 blocks), else by intr_pw_kernel after 64-block waves
     (PBA_TEST_ROW_WAVES64 forces it; test build).  The same sums in the same block order: the two paths give the same
-    reduced-system step (measured: identical to the last bit or within 1e-15)."""
+    reduced-system step (measured: bit-identical, all three paths).  Likewise the keyframe border kernel's
+    Schur terms from the point's one block targeting the keyframe (ib_pblk) and from a walk over the point's blocks (the
+    path of a point observed twice by one keyframe; PBA_TEST_PBLK_WALK forces it)."""
     pb, state = _intrinsics_rig(23, 260, 41 + n_cams, n_cams)
     out = {}
-    for path in ("fused", "separate"):
+    for path in ("fused", "separate", "walk"):
+        monkeypatch.delenv("PBA_TEST_ROW_WAVES64", raising=False)
         if path == "separate":
             monkeypatch.setenv("PBA_TEST_ROW_WAVES64", "1")
+        if path == "walk":
+            monkeypatch.setenv("PBA_TEST_PBLK_WALK", "1")
         with make_engine(pb, 1.0, (0, 1), E.TEST_LIB_PATH) as eng:
             eng.set_optimize_intrinsics(True)
             eng.set_intrinsics_state(state)
@@ -555,10 +560,11 @@ def test_point_sums_in_rows_match_separate_kernel(n_cams, monkeypatch):
             dp, dr = eng.gn_last_step()
             eng.gn_accept()
             out[path] = (dp, dr, eng.get_intrinsics() - state, np.array([m]))
-    for name, a, b in zip(("poses", "rho", "intrinsics", "model"), out["fused"], out["separate"]):
-        err = np.linalg.norm(a - b) / np.linalg.norm(b)
-        print(f"\nn_cams {n_cams}: {name} {err:.2e}")
-        assert err <= 1e-12, (name, err)
+    for other in ("separate", "walk"):
+        for name, a, b in zip(("poses", "rho", "intrinsics", "model"), out["fused"], out[other]):
+            err = np.linalg.norm(a - b) / np.linalg.norm(b)
+            print(f"\nn_cams {n_cams} {other}: {name} {err:.2e}")
+            assert err <= 1e-12, (other, name, err)
 
 
 @pytest.fixture(scope="module")
