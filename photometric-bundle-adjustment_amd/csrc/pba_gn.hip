@@ -3268,9 +3268,9 @@ struct PointUpdateArgs {
   double* red2;
   double* gmax;
   int n_points;
-  const double* ib;      // free intrinsics: per GN block W_i (ib_data), its target's camera, and the keyframe count
-  const int* ib_cam;     // (the intrinsics steps start at x[6·nf], 12 per camera)
-  int nf;
+  const double* pw;      // free intrinsics: per GN point its per-camera Σ W_i (ib_pw: intr_rows_kernel / intr_pw_kernel,
+  int nc;                // 8·nc + 6 per point), the cameras and the keyframe count (the intrinsics steps start at
+  int nf;                // x[6·nf], 12 per camera)
 };
 
 // blk: the point workgroup's index among the point workgroups; slot: its reduction slot
@@ -3352,12 +3352,13 @@ __device__ __forceinline__ void point_update_block(const PointUpdateArgs& a, con
 #pragma unroll
           for (int i = 0; i < 6; ++i) s += w[u][i] * xt[u][i];
     }
-    if (a.ib) {  // + Σ_b W_i(b)·δk(camera of b's target)
-      for (int b = fb; b < fb + nb; ++b) {
-        const double* wi = a.ib + (long long)b * kIbStride + kIbWi;
-        const double* xk = a.x + 6 * a.nf + 12 * a.ib_cam[b];
+    if (a.pw) {  // + Σ_b W_i(b)·δk(camera of b's target) = Σ_c W_c·δk_c from the point's camera sums (one load round,
+                 // not a camera index then its step per block)
+      const double* wc = a.pw + (long long)p * (8 * a.nc + 6);
+      for (int c = 0; c < a.nc; ++c) {
+        const double* xk = a.x + 6 * a.nf + 12 * c;
 #pragma unroll
-        for (int d = 0; d < 8; ++d) s += wi[d] * xk[d];
+        for (int d = 0; d < 8; ++d) s += wc[8 * c + d] * xk[d];
       }
     }
 #ifdef PBA_UPD_STAMPS
@@ -5577,7 +5578,7 @@ void enqueue_updates(pba_engine* e, double lambda, const uint8_t* fixed, int* gp
   // point workgroup q writes reduction slot gp + q, as the separate launches did
   PointUpdateArgs qa{G.pt_data.p, free_sets ? G.pt_data1.p : G.pt_data.p, G.pt_rec.p, G.pt_tgt.p, G.gn_target.p,
                      G.blk_schur.p, G.blk_schur1.p, G.x.p, fixed, e->rho.p, G.rho_new.p, G.drho.p, G.red.p,
-                     G.red2.p, G.gmax.p, G.n_gn_points, ki ? G.ib_data.p : nullptr, G.ib_cam.p, nf};
+                     G.red2.p, G.gmax.p, G.n_gn_points, ki ? G.ib_pw.p : nullptr, G.nc_sys, nf};
   PairUpdateArgs ra{G.pair_rec.p, e->intr_d.p, G.pairs_new.p, e->n_pairs};
   update_kernel<<<gp + gq + gr, kBlockThreads, 0, e->stream>>>(pa, qa, ra, gp, gq, lambda, lm ? lm : G.lm_idle.p);
   G.pairs_new_fresh = true;
